@@ -1,0 +1,177 @@
+#!/usr/bin/env python3
+"""Headline benchmark: GPT-2 345M Megatron-style pretraining throughput (tokens/s, whole job).
+
+Metric / config from BASELINE.json: "tokens/sec (whole node) GPT-2 345M pretrain at 1/2/4/8
+MI355X". Model: 24 layers, hidden 1024, 16 heads, seq 1024, vocab 50257 padded to 50304
+(Megatron `--make-vocab-size-divisible-by 128`), random init, synthetic CodeParrot-shaped
+tokens. Every timed step is a full training step: forward, backward, bucketed RCCL gradient
+reduction (DP), grad clipping and the fused Adam update.
+
+Baseline: the reference publishes no 345M number; its GPT-2-small run reaches ~41 model-TFLOP/s
+per A100 (derived from NB3:4718). ``vs_baseline`` compares our model-FLOPs/s per GPU
+against that 41 TFLOP/s/GPU, i.e. value / (41e12 * n_gpus / flops_per_token(345M)).
+
+Launch: ``python bench.py`` (1 GPU) or
+``python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N``.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+from smdt_amd.comm import init_distributed  # noqa: E402
+from smdt_amd.models.gpt import GPTModel, gpt_flops_per_token, pad_vocab_size  # noqa: E402
+from smdt_amd.models.transformer import TransformerConfig  # noqa: E402
+from smdt_amd.optim.optimizer import MixedPrecisionAdam  # noqa: E402
+from smdt_amd.optim.lr_scheduler import OptimizerParamScheduler  # noqa: E402
+from smdt_amd.parallel import state as ps  # noqa: E402
+from smdt_amd.parallel.distributed import DistributedDataParallel  # noqa: E402
+from smdt_amd.parallel.random import model_parallel_seed  # noqa: E402
+from smdt_amd.train.schedules import get_forward_backward_func  # noqa: E402
+
+REF_TFLOPS_PER_GPU = 41.0e12  # reference GPT-2-small on A100 (derived)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--tp", type=int, default=1)
+    p.add_argument("--pp", type=int, default=1)
+    p.add_argument("--micro-batch-size", type=int, default=16)
+    p.add_argument("--grad-accum", type=int, default=1, help="micro-batches per step per DP rank")
+    p.add_argument("--seq-length", type=int, default=1024)
+    p.add_argument("--num-layers", type=int, default=24)
+    p.add_argument("--hidden-size", type=int, default=1024)
+    p.add_argument("--num-attention-heads", type=int, default=16)
+    p.add_argument("--vocab-size", type=int, default=50257)
+    p.add_argument("--hidden-dropout", type=float, default=0.1)
+    p.add_argument("--attention-dropout", type=float, default=0.0)
+    p.add_argument("--zero", type=int, default=1, help="ZeRO-1/2 distributed optimizer when DP > 1")
+    p.add_argument("--bucket-size", type=int, default=40_000_000)
+    p.add_argument("--no-flash", action="store_true")
+    p.add_argument("--recompute", choices=["none", "full"], default="none")
+    p.add_argument("--profile-steps", type=int, default=0)
+    return p.parse_args()
+
+
+def main():
+    a = parse()
+    rank, local, world, backend = init_distributed("nccl")
+    if world != a.gpus and rank == 0:
+        print(f"[bench] note: --gpus {a.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
+    n = world
+    st = ps.initialize_model_parallel(a.tp, a.pp)
+    model_parallel_seed(1234)
+    dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
+    vocab = pad_vocab_size(a.vocab_size, 128, a.tp)
+    cfg = TransformerConfig(num_layers=a.num_layers, hidden_size=a.hidden_size,
+                            num_attention_heads=a.num_attention_heads, max_position_embeddings=a.seq_length,
+                            padded_vocab_size=vocab, hidden_dropout=a.hidden_dropout,
+                            attention_dropout=a.attention_dropout, params_dtype=torch.bfloat16,
+                            sequence_parallel=a.tp > 1, use_flash_attn=not a.no_flash,
+                            recompute_granularity="full" if a.recompute == "full" else None,
+                            recompute_method="uniform" if a.recompute == "full" else None)
+    model = GPTModel(cfg, pre_process=st.is_first_stage(), post_process=st.is_last_stage(), device=dev)
+    zero = bool(a.zero) and st.dp > 1
+    ddp = DistributedDataParallel(model, bucket_size=a.bucket_size, use_distributed_optimizer=zero)
+    opt = MixedPrecisionAdam(ddp, lr=1.5e-4, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.01, clip_grad=1.0)
+    sched = OptimizerParamScheduler(opt, max_lr=1.5e-4, min_lr=1e-5, lr_warmup_steps=10, lr_decay_steps=10000,
+                                    lr_decay_style="cosine")
+    mbs, S = a.micro_batch_size, a.seq_length
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(1000 + st.dp_rank)
+
+    def batches():
+        while True:
+            yield torch.randint(0, a.vocab_size, (mbs, S + 1), device=dev, generator=gen)
+
+    it = batches()
+    pos = torch.arange(S, device=dev).unsqueeze(0).expand(mbs, S)
+
+    def forward_step(data_iter, m):
+        toks = next(data_iter)
+        tokens, labels = toks[:, :-1], toks[:, 1:]
+        out = m(tokens, pos, None, labels=labels)
+
+        def loss_func(o):
+            loss = o.float().mean()
+            return loss, {"lm loss": loss.detach()}
+        return out, loss_func
+
+    fb = get_forward_backward_func()
+    shape = (S // a.tp if cfg.sequence_parallel else S, mbs, cfg.hidden_size)
+
+    def train_step():
+        ddp.zero_grad_buffer()
+        losses = fb(forward_step, it, ddp, a.grad_accum, tensor_shape=shape, dtype=torch.bfloat16)
+        ddp.finish_grad_sync()
+        lr = sched.step(1)
+        opt.step(lr)
+        return losses
+
+    for _ in range(a.warmup):
+        train_step()
+    if dist.is_initialized():
+        dist.barrier()
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    last = None
+    for _ in range(a.steps):
+        last = train_step()
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+    if dist.is_initialized():
+        dist.barrier()
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+    if dist.is_initialized():
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    elapsed = float(el.item())
+    global_batch = mbs * a.grad_accum * st.dp
+    tokens_per_step = global_batch * S
+    tps = tokens_per_step * a.steps / elapsed
+    fpt = gpt_flops_per_token(cfg, S, recompute=False)
+    ref_tps = REF_TFLOPS_PER_GPU * n / fpt
+    loss_val = None
+    if last:
+        loss_val = float(torch.stack([d["lm loss"] for d in last]).mean().item())
+    if rank == 0:
+        rec = {
+            "metric": "tokens/sec (whole node) GPT-2 345M pretrain",
+            "value": round(tps, 1),
+            "unit": "tokens/s",
+            "n_gpus": n,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(1000 * elapsed / a.steps, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": round(tps / ref_tps, 3),
+            "dtype": "bf16",
+            "data": "synthetic (random tokens, CodeParrot-shaped [mbs, 1025] int64; random-init weights)",
+            "config": {"model": "gpt2-345m (24L h1024 16A, vocab 50304)", "global_batch": global_batch,
+                       "seq_len": S, "micro_batch": mbs, "grad_accum": a.grad_accum,
+                       "parallelism": f"tp{a.tp}pp{a.pp}dp{st.dp}" + ("+zero" if zero else ""),
+                       "flash_attn": not a.no_flash, "hidden_dropout": a.hidden_dropout,
+                       "attention_dropout": a.attention_dropout, "recompute": a.recompute},
+            "model_tflops_per_gpu": round(tps * fpt / n / 1e12, 2),
+            "baseline": "41 model-TFLOP/s/GPU (reference GPT-2-small, 16xA100, BASELINE.md) at equal model FLOPs",
+            "final_loss": loss_val,
+        }
+        print(json.dumps(rec), flush=True)
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,404 @@
+// PyTorch bindings for the gfx950 kernel library (module `smdt_amd._C`).
+//
+// This is the only translation unit that sees ATen. Each binding validates shapes / dtypes /
+// contiguity on the host (a kernel is never launched on operands it does not expect), allocates
+// outputs through the caching allocator, and forwards raw pointers plus the current HIP stream
+// to the C launchers in kernels/launchers.h.
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <c10/hip/HIPGuard.h>
+
+#include "kernels/launchers.h"
+
+namespace {
+
+using torch::Tensor;
+using OptT = std::optional<Tensor>;
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+int dcode(const Tensor& t) {
+  switch (t.scalar_type()) {
+    case at::kFloat: return 0;
+    case at::kBFloat16: return 1;
+    case at::kHalf: return 2;
+    default: TORCH_CHECK(false, "smdt_amd: unsupported dtype ", t.scalar_type());
+  }
+}
+
+void check(hipError_t e, const char* what) {
+  TORCH_CHECK(e == hipSuccess, "smdt_amd kernel '", what, "' failed: ", hipGetErrorString(e));
+}
+
+void need_cuda(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), "smdt_amd: '", name, "' must be a GPU tensor");
+}
+
+void need_contig(const Tensor& t, const char* name) {
+  need_cuda(t, name);
+  TORCH_CHECK(t.is_contiguous(), "smdt_amd: '", name, "' must be contiguous");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, "smdt_amd: '", name,
+              "' must be 16-byte aligned");
+}
+
+const void* optr(const OptT& t) { return t.has_value() ? t->data_ptr() : nullptr; }
+
+// ------------------------------------------------------------------ LayerNorm / RMSNorm
+std::vector<Tensor> layernorm_fwd(Tensor x, OptT res, OptT bias, Tensor gamma, OptT beta,
+                                  double eps, double p_drop, int64_t seed, int64_t offset,
+                                  bool rms, bool want_s) {
+  need_contig(x, "x");
+  need_contig(gamma, "gamma");
+  const int64_t H = x.size(-1);
+  const int64_t rows = x.numel() / H;
+  TORCH_CHECK(gamma.numel() == H, "layernorm: gamma size mismatch");
+  if (res) { need_contig(*res, "residual"); TORCH_CHECK(res->sizes() == x.sizes() && res->dtype() == x.dtype(), "layernorm: residual mismatch"); }
+  if (bias) { need_contig(*bias, "bias"); TORCH_CHECK(bias->numel() == H && bias->dtype() == gamma.dtype(), "layernorm: bias mismatch"); }
+  if (beta) { need_contig(*beta, "beta"); TORCH_CHECK(beta->numel() == H && beta->dtype() == gamma.dtype(), "layernorm: beta mismatch"); }
+  auto y = torch::empty_like(x);
+  Tensor s;
+  const bool make_s = want_s || res.has_value() || bias.has_value() || p_drop > 0.0;
+  if (make_s) s = torch::empty_like(x);
+  auto f32 = x.options().dtype(at::kFloat);
+  auto mean = torch::empty({rows}, f32);
+  auto rstd = torch::empty({rows}, f32);
+  check(smdt_layernorm_fwd(dcode(x), dcode(gamma), x.data_ptr(), optr(res), optr(bias),
+                           gamma.data_ptr(), optr(beta), y.data_ptr(),
+                           make_s ? s.data_ptr() : nullptr, mean.data_ptr<float>(),
+                           rstd.data_ptr<float>(), rows, (int)H, (float)eps, (float)p_drop,
+                           (uint64_t)seed, (uint64_t)offset, rms ? 1 : 0, cur_stream()),
+        "layernorm_fwd");
+  return {y, make_s ? s : x, mean, rstd};
+}
+
+std::vector<Tensor> layernorm_bwd(Tensor dy, OptT ds_in, Tensor s, Tensor gamma, Tensor mean,
+                                  Tensor rstd, double p_drop, int64_t seed, int64_t offset,
+                                  bool rms, bool want_dx, bool want_dbias) {
+  need_contig(dy, "dy");
+  need_contig(s, "s");
+  need_contig(gamma, "gamma");
+  const int64_t H = s.size(-1);
+  const int64_t rows = s.numel() / H;
+  TORCH_CHECK(dy.sizes() == s.sizes() && dy.dtype() == s.dtype(), "layernorm_bwd: dy mismatch");
+  if (ds_in) { need_contig(*ds_in, "ds_in"); TORCH_CHECK(ds_in->sizes() == s.sizes() && ds_in->dtype() == s.dtype(), "layernorm_bwd: ds_in mismatch"); }
+  auto ds = torch::empty_like(s);
+  const bool sep = want_dx && p_drop > 0.0;
+  Tensor dx = sep ? torch::empty_like(s) : ds;
+  const int nb = smdt_ln_bwd_nblocks(rows, (int)H);
+  auto f32 = s.options().dtype(at::kFloat);
+  auto partials = torch::empty({nb, 3, H}, f32);
+  auto dgamma = torch::empty({H}, f32);
+  Tensor dbeta = rms ? Tensor() : torch::empty({H}, f32);
+  Tensor dbias = want_dbias ? torch::empty({H}, f32) : Tensor();
+  check(smdt_layernorm_bwd(dcode(s), dcode(gamma), dy.data_ptr(), optr(ds_in), s.data_ptr(),
+                           gamma.data_ptr(), rms ? nullptr : mean.data_ptr<float>(),
+                           rstd.data_ptr<float>(), ds.data_ptr(), dx.data_ptr(),
+                           partials.data_ptr<float>(), nb, dgamma.data_ptr<float>(),
+                           rms ? nullptr : dbeta.data_ptr<float>(),
+                           want_dbias ? dbias.data_ptr<float>() : nullptr, rows, (int)H,
+                           (float)p_drop, (uint64_t)seed, (uint64_t)offset, rms ? 1 : 0,
+                           cur_stream()),
+        "layernorm_bwd");
+  return {ds, dx, dgamma, rms ? dgamma.new_empty({0}) : dbeta,
+          want_dbias ? dbias : dgamma.new_empty({0})};
+}
+
+// ------------------------------------------------------------------ bias + activation
+Tensor bias_act_fwd(Tensor x, OptT bias, int64_t act) {
+  need_contig(x, "x");
+  const int64_t N = x.size(-1), rows = x.numel() / N;
+  if (bias) { need_contig(*bias, "bias"); TORCH_CHECK(bias->numel() == N && bias->dtype() == x.dtype(), "bias_act: bias mismatch"); }
+  auto y = torch::empty_like(x);
+  check(smdt_bias_act_fwd(dcode(x), (int)act, x.data_ptr(), optr(bias), y.data_ptr(), rows, (int)N,
+                          cur_stream()),
+        "bias_act_fwd");
+  return y;
+}
+
+std::vector<Tensor> bias_act_bwd(Tensor dy, Tensor x, OptT bias, int64_t act, bool want_dbias) {
+  need_contig(dy, "dy");
+  need_contig(x, "x");
+  TORCH_CHECK(dy.sizes() == x.sizes() && dy.dtype() == x.dtype(), "bias_act_bwd: shape mismatch");
+  const int64_t N = x.size(-1), rows = x.numel() / N;
+  auto dx = torch::empty_like(x);
+  Tensor part, dbias;
+  if (want_dbias) {
+    const int slices = smdt_bias_act_slices(rows, (int)N);
+    part = torch::empty({slices, N}, x.options().dtype(at::kFloat));
+    dbias = torch::empty({N}, x.options().dtype(at::kFloat));
+  }
+  check(smdt_bias_act_bwd(dcode(x), (int)act, dy.data_ptr(), x.data_ptr(), optr(bias),
+                          dx.data_ptr(), want_dbias ? part.data_ptr<float>() : nullptr,
+                          want_dbias ? dbias.data_ptr<float>() : nullptr, rows, (int)N,
+                          cur_stream()),
+        "bias_act_bwd");
+  return {dx, want_dbias ? dbias : dx.new_empty({0})};
+}
+
+Tensor swiglu_fwd(Tensor x) {
+  need_contig(x, "x");
+  const int64_t F2 = x.size(-1), rows = x.numel() / F2;
+  TORCH_CHECK(F2 % 2 == 0, "swiglu: last dim must be even");
+  auto sizes = x.sizes().vec();
+  sizes.back() = F2 / 2;
+  auto y = torch::empty(sizes, x.options());
+  check(smdt_swiglu_fwd(dcode(x), x.data_ptr(), y.data_ptr(), rows, (int)(F2 / 2), cur_stream()),
+        "swiglu_fwd");
+  return y;
+}
+
+Tensor swiglu_bwd(Tensor dy, Tensor x) {
+  need_contig(dy, "dy");
+  need_contig(x, "x");
+  const int64_t F2 = x.size(-1), rows = x.numel() / F2;
+  TORCH_CHECK(dy.numel() * 2 == x.numel(), "swiglu_bwd: shape mismatch");
+  auto dx = torch::empty_like(x);
+  check(smdt_swiglu_bwd(dcode(x), dy.data_ptr(), x.data_ptr(), dx.data_ptr(), rows, (int)(F2 / 2),
+                        cur_stream()),
+        "swiglu_bwd");
+  return dx;
+}
+
+// ------------------------------------------------------------------ masked softmax
+Tensor softmax_fwd(Tensor x, OptT mask, int64_t mode, double scale) {
+  need_contig(x, "x");
+  TORCH_CHECK(x.dim() == 4, "softmax: expects [b, np, sq, sk]");
+  const int64_t sk = x.size(3), sq = x.size(2), heads = x.size(1);
+  const int64_t rows = x.numel() / sk;
+  if (mode == 2) {
+    TORCH_CHECK(mask.has_value(), "softmax: mode 2 needs a mask");
+    need_contig(*mask, "mask");
+    TORCH_CHECK(mask->scalar_type() == at::kBool || mask->scalar_type() == at::kByte, "softmax: mask must be bool/uint8");
+    TORCH_CHECK(mask->numel() == x.size(0) * sq * sk, "softmax: mask must be [b, 1, sq, sk]");
+  }
+  auto y = torch::empty_like(x);
+  check(smdt_softmax_fwd(dcode(x), (int)mode, x.data_ptr(),
+                         mode == 2 ? (const uint8_t*)mask->data_ptr() : nullptr, y.data_ptr(), rows,
+                         (int)sq, (int)sk, (int)heads, (float)scale, cur_stream()),
+        "softmax_fwd");
+  return y;
+}
+
+Tensor softmax_bwd(Tensor dy, Tensor y, int64_t mode, double scale) {
+  need_contig(dy, "dy");
+  need_contig(y, "y");
+  TORCH_CHECK(dy.sizes() == y.sizes(), "softmax_bwd: shape mismatch");
+  const int64_t sk = y.size(3), sq = y.size(2), rows = y.numel() / sk;
+  auto dx = torch::empty_like(y);
+  check(smdt_softmax_bwd(dcode(y), (int)mode, dy.data_ptr(), y.data_ptr(), dx.data_ptr(), rows,
+                         (int)sq, (int)sk, (float)scale, cur_stream()),
+        "softmax_bwd");
+  return dx;
+}
+
+// ------------------------------------------------------------------ optimizer
+void adam(Tensor master, Tensor grad, Tensor m, Tensor v, OptT model_out, double lr, double beta1,
+          double beta2, double eps, double wd, int64_t step, bool adamw, OptT grad_mul,
+          OptT found_inf) {
+  for (auto* t : {&master, &grad, &m, &v}) {
+    need_contig(*t, "adam buffer");
+    TORCH_CHECK(t->scalar_type() == at::kFloat, "adam: fp32 buffers expected");
+    TORCH_CHECK(t->numel() == master.numel(), "adam: buffer size mismatch");
+  }
+  int mdt = 0;
+  if (model_out) {
+    need_contig(*model_out, "model_out");
+    TORCH_CHECK(model_out->numel() == master.numel(), "adam: model_out size mismatch");
+    mdt = dcode(*model_out);
+    TORCH_CHECK(mdt != 0, "adam: model_out must be bf16/fp16 (fp32 masters ARE the model)");
+  }
+  if (grad_mul) TORCH_CHECK(grad_mul->scalar_type() == at::kFloat && grad_mul->is_cuda(), "adam: grad_mul fp32 scalar");
+  if (found_inf) TORCH_CHECK(found_inf->scalar_type() == at::kInt && found_inf->is_cuda(), "adam: found_inf int32 scalar");
+  const double bc1 = 1.0 - std::pow(beta1, (double)step);
+  const double bc2 = 1.0 - std::pow(beta2, (double)step);
+  check(smdt_adam(master.data_ptr<float>(), grad.data_ptr<float>(), m.data_ptr<float>(),
+                  v.data_ptr<float>(), model_out ? model_out->data_ptr() : nullptr, mdt,
+                  master.numel(), (float)lr, (float)beta1, (float)beta2, (float)eps, (float)wd,
+                  (float)bc1, (float)bc2, adamw ? 1 : 0,
+                  grad_mul ? grad_mul->data_ptr<float>() : nullptr,
+                  found_inf ? found_inf->data_ptr<int>() : nullptr, cur_stream()),
+        "adam");
+}
+
+Tensor sumsq(Tensor x, OptT found_inf) {
+  need_contig(x, "x");
+  const int64_t n = x.numel();
+  const int nb = smdt_sumsq_nblocks(n);
+  auto f32 = x.options().dtype(at::kFloat);
+  auto partial = torch::empty({nb}, f32);
+  auto out = torch::empty({1}, f32);
+  if (found_inf) TORCH_CHECK(found_inf->scalar_type() == at::kInt && found_inf->is_cuda(), "sumsq: found_inf int32");
+  check(smdt_sumsq(dcode(x), x.data_ptr(), n, partial.data_ptr<float>(), nb, out.data_ptr<float>(),
+                   found_inf ? found_inf->data_ptr<int>() : nullptr, cur_stream()),
+        "sumsq");
+  return out;
+}
+
+std::vector<Tensor> clip_coef(Tensor sumsq_t, double max_norm, double inv_scale) {
+  TORCH_CHECK(sumsq_t.scalar_type() == at::kFloat && sumsq_t.is_cuda(), "clip_coef: fp32 scalar");
+  auto mul = torch::empty({1}, sumsq_t.options());
+  auto norm = torch::empty({1}, sumsq_t.options());
+  check(smdt_clip_coef(sumsq_t.data_ptr<float>(), (float)max_norm, (float)inv_scale,
+                       mul.data_ptr<float>(), norm.data_ptr<float>(), cur_stream()),
+        "clip_coef");
+  return {mul, norm};
+}
+
+void scale_(Tensor x, OptT mul, double cmul) {
+  need_contig(x, "x");
+  check(smdt_scale(dcode(x), x.data_ptr(), x.numel(), mul ? mul->data_ptr<float>() : nullptr,
+                   (float)cmul, cur_stream()),
+        "scale");
+}
+
+void cast_(Tensor x, Tensor y, bool accumulate) {
+  need_contig(x, "x");
+  need_contig(y, "y");
+  TORCH_CHECK(x.numel() == y.numel(), "cast: size mismatch");
+  check(smdt_cast(dcode(x), dcode(y), x.data_ptr(), y.data_ptr(), x.numel(), accumulate ? 1 : 0,
+                  cur_stream()),
+        "cast");
+}
+
+// ------------------------------------------------------------------ RoPE
+// x: [ntok, nh, d] strided view (last dim contiguous), rotary applied in place to the first
+// `rot` elements of each head.
+void rope_(Tensor x, Tensor cos_t, Tensor sin_t, int64_t rot, int64_t pos_div, int64_t pos_mod,
+           bool backward) {
+  need_cuda(x, "x");
+  TORCH_CHECK(x.dim() == 3 && x.stride(2) == 1, "rope: x must be [ntok, nh, d] with unit last stride");
+  need_contig(cos_t, "cos");
+  need_contig(sin_t, "sin");
+  TORCH_CHECK(cos_t.scalar_type() == at::kFloat && sin_t.scalar_type() == at::kFloat, "rope: fp32 tables");
+  TORCH_CHECK(rot <= x.size(2) && rot % 16 == 0 && cos_t.size(-1) == rot / 2, "rope: rotary dim mismatch");
+  TORCH_CHECK(x.stride(0) % 8 == 0 && x.stride(1) % 8 == 0, "rope: strides must keep 16-byte alignment");
+  check(smdt_rope(dcode(x), x.data_ptr(), x.size(0), (int)x.size(1), x.stride(0), x.stride(1),
+                  (int)rot, cos_t.data_ptr<float>(), sin_t.data_ptr<float>(), (int)pos_div,
+                  (int)pos_mod, backward ? 1 : 0, cur_stream()),
+        "rope");
+}
+
+// ------------------------------------------------------------------ cross entropy
+std::vector<Tensor> ce_stats(Tensor logits, Tensor target, int64_t vstart) {
+  need_contig(logits, "logits");
+  need_contig(target, "target");
+  TORCH_CHECK(target.scalar_type() == at::kLong, "ce: int64 targets");
+  const int64_t V = logits.size(-1), rows = logits.numel() / V;
+  TORCH_CHECK(target.numel() == rows, "ce: target size mismatch");
+  auto f32 = logits.options().dtype(at::kFloat);
+  auto mx = torch::empty({rows}, f32), se = torch::empty({rows}, f32), tg = torch::empty({rows}, f32);
+  check(smdt_ce_stats(dcode(logits), logits.data_ptr(), target.data_ptr<int64_t>(), rows, (int)V,
+                      vstart, mx.data_ptr<float>(), se.data_ptr<float>(), tg.data_ptr<float>(),
+                      cur_stream()),
+        "ce_stats");
+  return {mx, se, tg};
+}
+
+void ce_bwd(Tensor logits, Tensor target, Tensor gmax, Tensor gsum, Tensor dloss, Tensor out,
+            int64_t vstart, int64_t ignore_index) {
+  need_contig(logits, "logits");
+  need_contig(out, "dlogits");
+  TORCH_CHECK(out.sizes() == logits.sizes() && out.dtype() == logits.dtype(), "ce_bwd: out mismatch");
+  const int64_t V = logits.size(-1), rows = logits.numel() / V;
+  for (auto* t : {&gmax, &gsum, &dloss}) {
+    need_contig(*t, "ce row stat");
+    TORCH_CHECK(t->scalar_type() == at::kFloat && t->numel() == rows, "ce_bwd: fp32 [rows] stats");
+  }
+  check(smdt_ce_bwd(dcode(logits), logits.data_ptr(), target.data_ptr<int64_t>(),
+                    gmax.data_ptr<float>(), gsum.data_ptr<float>(), dloss.data_ptr<float>(),
+                    out.data_ptr(), rows, (int)V, vstart, ignore_index, cur_stream()),
+        "ce_bwd");
+}
+
+// ------------------------------------------------------------------ flash attention
+// q: [B, S, H, D], k/v: [B, S, Hkv, D] (unit last stride, any other strides).
+void fa_check(const Tensor& t, const char* n) {
+  need_cuda(t, n);
+  TORCH_CHECK(t.dim() == 4 && t.stride(3) == 1, "flash: '", n, "' must be [B, S, H, D] with unit last stride");
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16, "flash: bf16 only");
+  TORCH_CHECK(t.stride(0) % 8 == 0 && t.stride(1) % 8 == 0 && t.stride(2) % 8 == 0 &&
+                  reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0,
+              "flash: '", n, "' must keep 16-byte row alignment");
+}
+
+// `out` (optional) is a preallocated [B, S, H, D] view with any strides (e.g. the [s, b, h]
+// activation layout used by the transformer trunk).
+std::vector<Tensor> flash_fwd(Tensor q, Tensor k, Tensor v, double scale, bool causal, OptT out) {
+  fa_check(q, "q"); fa_check(k, "k"); fa_check(v, "v");
+  const int64_t B = q.size(0), S = q.size(1), H = q.size(2), D = q.size(3), Hkv = k.size(2);
+  TORCH_CHECK(k.size(0) == B && k.size(1) == S && k.size(3) == D && v.sizes() == k.sizes(), "flash: k/v shape mismatch");
+  TORCH_CHECK((D == 64 || D == 128) && S % 128 == 0 && H % Hkv == 0, "flash: needs D in {64,128}, S % 128 == 0, H % Hkv == 0");
+  Tensor o;
+  if (out) {
+    o = *out;
+    fa_check(o, "out");
+    TORCH_CHECK(o.sizes() == q.sizes(), "flash: out shape mismatch");
+  } else {
+    o = torch::empty({B, S, H, D}, q.options());
+  }
+  auto lse = torch::empty({B, H, S}, q.options().dtype(at::kFloat));
+  check(smdt_flash_fwd(1, q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr<float>(),
+                       (int)B, (int)H, (int)Hkv, (int)S, (int)D, q.stride(0), q.stride(1), q.stride(2),
+                       k.stride(0), k.stride(1), k.stride(2), v.stride(0), v.stride(1), v.stride(2),
+                       o.stride(0), o.stride(1), o.stride(2), (float)scale, causal ? 1 : 0, cur_stream()),
+        "flash_fwd");
+  return {o, lse};
+}
+
+// dq / dk / dv (optional) are preallocated [B, S, H(kv), D] views with any strides, typically
+// views into one fused d(QKV) buffer so the QKV projection backward needs no concatenation.
+std::vector<Tensor> flash_bwd(Tensor q, Tensor k, Tensor v, Tensor o, Tensor dout, Tensor lse,
+                              double scale, bool causal, OptT dq_out, OptT dk_out, OptT dv_out) {
+  fa_check(q, "q"); fa_check(k, "k"); fa_check(v, "v"); fa_check(o, "o");
+  const int64_t B = q.size(0), S = q.size(1), H = q.size(2), D = q.size(3), Hkv = k.size(2);
+  TORCH_CHECK((D == 64 || D == 128) && S % 128 == 0 && H % Hkv == 0, "flash_bwd: unsupported shape");
+  TORCH_CHECK(dout.sizes() == o.sizes(), "flash_bwd: dout shape mismatch");
+  if (dout.stride(3) != 1 || dout.stride(0) % 8 || dout.stride(1) % 8 || dout.stride(2) % 8) dout = dout.contiguous();
+  fa_check(dout, "dout");
+  TORCH_CHECK(lse.is_contiguous() && lse.numel() == B * H * S, "flash_bwd: lse mismatch");
+  auto mk = [&](const OptT& given, int64_t heads, const char* n) {
+    if (given) {
+      fa_check(*given, n);
+      TORCH_CHECK(given->size(0) == B && given->size(1) == S && given->size(2) == heads && given->size(3) == D,
+                  "flash_bwd: '", n, "' shape mismatch");
+      return *given;
+    }
+    return torch::empty({B, S, heads, D}, q.options());
+  };
+  Tensor dq = mk(dq_out, H, "dq"), dk = mk(dk_out, Hkv, "dk"), dv = mk(dv_out, Hkv, "dv");
+  auto delta = torch::empty({B, H, S}, q.options().dtype(at::kFloat));
+  int64_t st[24];
+  const Tensor* ts[8] = {&q, &k, &v, &o, &dout, &dq, &dk, &dv};
+  for (int i = 0; i < 8; ++i)
+    for (int j = 0; j < 3; ++j) st[3 * i + j] = ts[i]->stride(j);
+  check(smdt_flash_bwd(1, q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), dout.data_ptr(),
+                       lse.data_ptr<float>(), delta.data_ptr<float>(), dq.data_ptr(), dk.data_ptr(),
+                       dv.data_ptr(), (int)B, (int)H, (int)Hkv, (int)S, (int)D, st, (float)scale,
+                       causal ? 1 : 0, cur_stream()),
+        "flash_bwd");
+  return {dq, dk, dv};
+}
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "smdt_amd gfx950 (MI355X) HIP kernel library";
+  m.def("layernorm_fwd", &layernorm_fwd);
+  m.def("layernorm_bwd", &layernorm_bwd);
+  m.def("bias_act_fwd", &bias_act_fwd);
+  m.def("bias_act_bwd", &bias_act_bwd);
+  m.def("swiglu_fwd", &swiglu_fwd);
+  m.def("swiglu_bwd", &swiglu_bwd);
+  m.def("softmax_fwd", &softmax_fwd);
+  m.def("softmax_bwd", &softmax_bwd);
+  m.def("adam", &adam);
+  m.def("sumsq", &sumsq);
+  m.def("clip_coef", &clip_coef);
+  m.def("scale_", &scale_);
+  m.def("cast_", &cast_);
+  m.def("rope_", &rope_);
+  m.def("ce_stats", &ce_stats);
+  m.def("ce_bwd", &ce_bwd);
+  m.def("flash_fwd", &flash_fwd);
+  m.def("flash_bwd", &flash_bwd);
+}

@@ -1,0 +1,241 @@
+// Bias + activation (GeLU-tanh, exact-erf GeLU, SwiGLU) forward / backward for gfx950.
+//
+// Replaces Megatron's TorchScript `bias_gelu` fusion (flag `--no-bias-gelu-fusion`,
+// /root/reference/3_training_megatron-lm/megatron/arguments.py:819-821) and the SwiGLU
+// activation used by LLaMA-style blocks (`--swiglu`, arguments.py:254-260).
+//
+// Layout: x is [rows, N] row-major. A block of 256 threads covers 2048 columns (one 8-element
+// 16-byte chunk per thread) and a slice of rows (grid.y); a thread keeps the same columns for
+// every row of its slice, so d(bias) partial sums accumulate in registers and are written once
+// per block as an fp32 [grid.y, N] slab, reduced by `col_partials_reduce_kernel`.
+#include "common.h"
+#include "launchers.h"
+
+namespace smdt {
+
+__device__ __forceinline__ float gelu_tanh(float x) {
+  constexpr float k0 = 0.7978845608028654f;  // sqrt(2/pi)
+  constexpr float k1 = 0.044715f;
+  float u = k0 * (x + k1 * x * x * x);
+  return 0.5f * x * (1.f + tanhf(u));
+}
+__device__ __forceinline__ float gelu_tanh_grad(float x) {
+  constexpr float k0 = 0.7978845608028654f;
+  constexpr float k1 = 0.044715f;
+  float x2 = x * x;
+  float u = k0 * (x + k1 * x2 * x);
+  float t = tanhf(u);
+  return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k0 * (1.f + 3.f * k1 * x2);
+}
+__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.7071067811865476f)); }
+__device__ __forceinline__ float gelu_erf_grad(float x) {
+  float cdf = 0.5f * (1.f + erff(x * 0.7071067811865476f));
+  float pdf = 0.3989422804014327f * __expf(-0.5f * x * x);
+  return cdf + x * pdf;
+}
+__device__ __forceinline__ float silu(float x) { return x / (1.f + __expf(-x)); }
+
+// act: 0 = gelu_tanh, 1 = gelu_erf
+template <typename T, int ACT>
+__global__ __launch_bounds__(256) void bias_act_fwd_kernel(const T* __restrict__ x,
+                                                           const T* __restrict__ bias,
+                                                           T* __restrict__ y, int64_t rows, int N,
+                                                           int rows_per_slice) {
+  const int ch = blockIdx.x * 256 + threadIdx.x;
+  if (ch * 8 >= N) return;
+  float b[8];
+  if (bias) load_vec<T, 8>(bias + ch * 8, b);
+  else
+    for (int j = 0; j < 8; ++j) b[j] = 0.f;
+  int64_t r0 = (int64_t)blockIdx.y * rows_per_slice;
+  int64_t r1 = r0 + rows_per_slice < rows ? r0 + rows_per_slice : rows;
+  for (int64_t r = r0; r < r1; ++r) {
+    float v[8];
+    load_vec<T, 8>(x + r * N + ch * 8, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float z = v[j] + b[j];
+      v[j] = ACT == 0 ? gelu_tanh(z) : gelu_erf(z);
+    }
+    store_vec<T, 8>(y + r * N + ch * 8, v);
+  }
+}
+
+template <typename T, int ACT>
+__global__ __launch_bounds__(256) void bias_act_bwd_kernel(const T* __restrict__ dy,
+                                                           const T* __restrict__ x,
+                                                           const T* __restrict__ bias,
+                                                           T* __restrict__ dx,
+                                                           float* __restrict__ partials,
+                                                           int64_t rows, int N,
+                                                           int rows_per_slice) {
+  const int ch = blockIdx.x * 256 + threadIdx.x;
+  if (ch * 8 >= N) return;
+  float b[8], acc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+  if (bias) load_vec<T, 8>(bias + ch * 8, b);
+  else
+    for (int j = 0; j < 8; ++j) b[j] = 0.f;
+  int64_t r0 = (int64_t)blockIdx.y * rows_per_slice;
+  int64_t r1 = r0 + rows_per_slice < rows ? r0 + rows_per_slice : rows;
+  for (int64_t r = r0; r < r1; ++r) {
+    float v[8], g[8];
+    load_vec<T, 8>(x + r * N + ch * 8, v);
+    load_vec<T, 8>(dy + r * N + ch * 8, g);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float z = v[j] + b[j];
+      float d = g[j] * (ACT == 0 ? gelu_tanh_grad(z) : gelu_erf_grad(z));
+      v[j] = d;
+      acc[j] += to_f32(from_f32<T>(d));
+    }
+    store_vec<T, 8>(dx + r * N + ch * 8, v);
+  }
+  if (partials) store_vec<float, 8>(partials + (int64_t)blockIdx.y * N + ch * 8, acc);
+}
+
+// SwiGLU on a fused [rows, 2F] input laid out as [gate | up]: y = silu(gate) * up.
+template <typename T>
+__global__ __launch_bounds__(256) void swiglu_fwd_kernel(const T* __restrict__ x,
+                                                         T* __restrict__ y, int64_t rows, int F) {
+  const int64_t nchunks = rows * (F / 8);
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nchunks;
+       i += (int64_t)gridDim.x * 256) {
+    int64_t r = i / (F / 8);
+    int c = (int)(i % (F / 8)) * 8;
+    float g[8], u[8];
+    load_vec<T, 8>(x + r * 2 * F + c, g);
+    load_vec<T, 8>(x + r * 2 * F + F + c, u);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) g[j] = silu(g[j]) * u[j];
+    store_vec<T, 8>(y + r * F + c, g);
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void swiglu_bwd_kernel(const T* __restrict__ dy,
+                                                         const T* __restrict__ x,
+                                                         T* __restrict__ dx, int64_t rows, int F) {
+  const int64_t nchunks = rows * (F / 8);
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nchunks;
+       i += (int64_t)gridDim.x * 256) {
+    int64_t r = i / (F / 8);
+    int c = (int)(i % (F / 8)) * 8;
+    float g[8], u[8], d[8], dg[8], du[8];
+    load_vec<T, 8>(x + r * 2 * F + c, g);
+    load_vec<T, 8>(x + r * 2 * F + F + c, u);
+    load_vec<T, 8>(dy + r * F + c, d);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float s = 1.f / (1.f + __expf(-g[j]));
+      float sl = g[j] * s;
+      du[j] = d[j] * sl;
+      dg[j] = d[j] * u[j] * (s * (1.f + g[j] * (1.f - s)));
+    }
+    store_vec<T, 8>(dx + r * 2 * F + c, dg);
+    store_vec<T, 8>(dx + r * 2 * F + F + c, du);
+  }
+}
+
+__global__ __launch_bounds__(256) void col_partials_reduce_kernel(const float* __restrict__ part,
+                                                                 int nslices, int N,
+                                                                 float* __restrict__ out) {
+  int col = blockIdx.x * 256 + threadIdx.x;
+  if (col >= N) return;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  int s = 0;
+  for (; s + 3 < nslices; s += 4) {
+    a0 += part[(int64_t)s * N + col];
+    a1 += part[(int64_t)(s + 1) * N + col];
+    a2 += part[(int64_t)(s + 2) * N + col];
+    a3 += part[(int64_t)(s + 3) * N + col];
+  }
+  for (; s < nslices; ++s) a0 += part[(int64_t)s * N + col];
+  out[col] = (a0 + a1) + (a2 + a3);
+}
+
+// Rows per slice so that (column blocks) x (row slices) ~ 1024 blocks.
+static int act_slices(int64_t rows, int N, int* rows_per_slice) {
+  int colblocks = (N / 8 + 255) / 256;
+  int64_t want = 1024 / colblocks;
+  if (want < 1) want = 1;
+  if (want > rows) want = rows;
+  int64_t rps = (rows + want - 1) / want;
+  *rows_per_slice = (int)rps;
+  return (int)((rows + rps - 1) / rps);
+}
+
+}  // namespace smdt
+
+using namespace smdt;
+
+extern "C" int smdt_bias_act_slices(int64_t rows, int N) {
+  int rps;
+  return act_slices(rows, N, &rps);
+}
+
+extern "C" hipError_t smdt_bias_act_fwd(int dtype, int act, const void* x, const void* bias,
+                                        void* y, int64_t rows, int N, hipStream_t st) {
+  if (N % 8 != 0 || rows <= 0) return hipErrorInvalidValue;
+  int rps;
+  int slices = act_slices(rows, N, &rps);
+  dim3 grid((N / 8 + 255) / 256, slices);
+#define SMDT_BA_FWD(T, A)                                                                   \
+  hipLaunchKernelGGL((bias_act_fwd_kernel<T, A>), grid, dim3(256), 0, st, (const T*)x,      \
+                     (const T*)bias, (T*)y, rows, N, rps)
+  if (dtype == 1) { if (act == 0) SMDT_BA_FWD(bf16, 0); else SMDT_BA_FWD(bf16, 1); }
+  else if (dtype == 2) { if (act == 0) SMDT_BA_FWD(f16, 0); else SMDT_BA_FWD(f16, 1); }
+  else { if (act == 0) SMDT_BA_FWD(float, 0); else SMDT_BA_FWD(float, 1); }
+#undef SMDT_BA_FWD
+  return hipGetLastError();
+}
+
+extern "C" hipError_t smdt_bias_act_bwd(int dtype, int act, const void* dy, const void* x,
+                                        const void* bias, void* dx, float* partials,
+                                        float* dbias, int64_t rows, int N, hipStream_t st) {
+  if (N % 8 != 0 || rows <= 0) return hipErrorInvalidValue;
+  int rps;
+  int slices = act_slices(rows, N, &rps);
+  dim3 grid((N / 8 + 255) / 256, slices);
+  float* part = dbias ? partials : nullptr;
+#define SMDT_BA_BWD(T, A)                                                                   \
+  hipLaunchKernelGGL((bias_act_bwd_kernel<T, A>), grid, dim3(256), 0, st, (const T*)dy,     \
+                     (const T*)x, (const T*)bias, (T*)dx, part, rows, N, rps)
+  if (dtype == 1) { if (act == 0) SMDT_BA_BWD(bf16, 0); else SMDT_BA_BWD(bf16, 1); }
+  else if (dtype == 2) { if (act == 0) SMDT_BA_BWD(f16, 0); else SMDT_BA_BWD(f16, 1); }
+  else { if (act == 0) SMDT_BA_BWD(float, 0); else SMDT_BA_BWD(float, 1); }
+#undef SMDT_BA_BWD
+  if (dbias) {
+    hipLaunchKernelGGL(col_partials_reduce_kernel, dim3((N + 255) / 256), dim3(256), 0, st,
+                       partials, slices, N, dbias);
+  }
+  return hipGetLastError();
+}
+
+extern "C" hipError_t smdt_col_sum(const float* partials, int nslices, int N, float* out,
+                                   hipStream_t st) {
+  hipLaunchKernelGGL(col_partials_reduce_kernel, dim3((N + 255) / 256), dim3(256), 0, st,
+                     partials, nslices, N, out);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t smdt_swiglu_fwd(int dtype, const void* x, void* y, int64_t rows, int F,
+                                      hipStream_t st) {
+  if (F % 8 != 0) return hipErrorInvalidValue;
+  int grid = stream_grid(rows * (F / 8), 256);
+  if (dtype == 1) hipLaunchKernelGGL(swiglu_fwd_kernel<bf16>, dim3(grid), dim3(256), 0, st, (const bf16*)x, (bf16*)y, rows, F);
+  else if (dtype == 2) hipLaunchKernelGGL(swiglu_fwd_kernel<f16>, dim3(grid), dim3(256), 0, st, (const f16*)x, (f16*)y, rows, F);
+  else hipLaunchKernelGGL(swiglu_fwd_kernel<float>, dim3(grid), dim3(256), 0, st, (const float*)x, (float*)y, rows, F);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t smdt_swiglu_bwd(int dtype, const void* dy, const void* x, void* dx,
+                                      int64_t rows, int F, hipStream_t st) {
+  if (F % 8 != 0) return hipErrorInvalidValue;
+  int grid = stream_grid(rows * (F / 8), 256);
+  if (dtype == 1) hipLaunchKernelGGL(swiglu_bwd_kernel<bf16>, dim3(grid), dim3(256), 0, st, (const bf16*)dy, (const bf16*)x, (bf16*)dx, rows, F);
+  else if (dtype == 2) hipLaunchKernelGGL(swiglu_bwd_kernel<f16>, dim3(grid), dim3(256), 0, st, (const f16*)dy, (const f16*)x, (f16*)dx, rows, F);
+  else hipLaunchKernelGGL(swiglu_bwd_kernel<float>, dim3(grid), dim3(256), 0, st, (const float*)dy, (const float*)x, (float*)dx, rows, F);
+  return hipGetLastError();
+}

@@ -1,0 +1,140 @@
+// Fused (vocab-parallel) softmax cross-entropy for gfx950.
+//
+// Replaces Megatron's vocab-parallel cross entropy (`parallel_output=True` at
+// /root/reference/3_training_megatron-lm/pretrain_gpt.py:51-57, `--fp16-lm-cross-entropy` at
+// megatron/arguments.py:992-994).
+//
+// Forward is ONE pass over the logits: a block of 256 threads owns a row and keeps an online
+// (max, sum-exp) pair per thread over 16-byte vectors, merged across the block at the end, and
+// picks up the target logit when the target falls in this rank's vocab slice. The three
+// per-row statistics are what the tensor-parallel path all-reduces (MAX, then SUM, SUM).
+// Backward writes (softmax - onehot) * dloss straight into the gradient buffer, which may
+// alias the logits (in-place, no extra [tokens, V] allocation).
+#include "common.h"
+#include "launchers.h"
+
+namespace smdt {
+
+template <typename T>
+__global__ __launch_bounds__(256) void ce_stats_kernel(const T* __restrict__ logits,
+                                                       const int64_t* __restrict__ target,
+                                                       int64_t rows, int V, int64_t vstart,
+                                                       float* __restrict__ row_max,
+                                                       float* __restrict__ row_sumexp,
+                                                       float* __restrict__ row_tgt) {
+  __shared__ float sm[4], ss[4];
+  const int64_t row = blockIdx.x;
+  if (row >= rows) return;
+  const T* lr = logits + row * V;
+  float m = -INFINITY, s = 0.f;
+  constexpr int VE = 8;
+  const int nvec = V / VE;
+  for (int i = threadIdx.x; i < nvec; i += 256) {
+    float v[VE];
+    load_vec<T, VE>(lr + i * VE, v);
+    float lm = v[0];
+#pragma unroll
+    for (int j = 1; j < VE; ++j) lm = fmaxf(lm, v[j]);
+    float nm = fmaxf(m, lm);
+    float acc = 0.f;
+#pragma unroll
+    for (int j = 0; j < VE; ++j) acc += __expf(v[j] - nm);
+    s = s * __expf(m - nm) + acc;
+    m = nm;
+  }
+  for (int i = nvec * VE + threadIdx.x; i < V; i += 256) {
+    float v = to_f32(lr[i]);
+    float nm = fmaxf(m, v);
+    s = s * __expf(m - nm) + __expf(v - nm);
+    m = nm;
+  }
+  // Merge (m, s) pairs: wave level then block level.
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    float om = __shfl_xor(m, o, 64), os = __shfl_xor(s, o, 64);
+    float nm = fmaxf(m, om);
+    s = (m == -INFINITY ? 0.f : s * __expf(m - nm)) + (om == -INFINITY ? 0.f : os * __expf(om - nm));
+    m = nm;
+  }
+  if (lane == 0) {
+    sm[wid] = m;
+    ss[wid] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float M = sm[0], S = ss[0];
+    for (int w = 1; w < 4; ++w) {
+      float nm = fmaxf(M, sm[w]);
+      S = (M == -INFINITY ? 0.f : S * __expf(M - nm)) + (sm[w] == -INFINITY ? 0.f : ss[w] * __expf(sm[w] - nm));
+      M = nm;
+    }
+    row_max[row] = M;
+    row_sumexp[row] = S;
+    int64_t t = target[row] - vstart;
+    row_tgt[row] = (t >= 0 && t < V) ? to_f32(lr[t]) : 0.f;
+  }
+}
+
+// dlogits[r, j] = (exp(x - gmax) / gsum - [j == target]) * dloss[r]   (rows with ignore = 0)
+template <typename T>
+__global__ __launch_bounds__(256) void ce_bwd_kernel(const T* __restrict__ logits,
+                                                     const int64_t* __restrict__ target,
+                                                     const float* __restrict__ gmax,
+                                                     const float* __restrict__ gsum,
+                                                     const float* __restrict__ dloss,
+                                                     T* __restrict__ dlogits, int64_t rows, int V,
+                                                     int64_t vstart, int64_t ignore_index) {
+  const int64_t row = blockIdx.x;
+  if (row >= rows) return;
+  const T* lr = logits + row * V;
+  T* dr = dlogits + row * V;
+  const int64_t tg = target[row];
+  const float g = tg == ignore_index ? 0.f : dloss[row];
+  const float M = gmax[row];
+  const float inv = 1.f / gsum[row];
+  const int64_t t = tg - vstart;
+  constexpr int VE = 8;
+  const int nvec = V / VE;
+  for (int i = threadIdx.x; i < nvec; i += 256) {
+    float v[VE];
+    load_vec<T, VE>(lr + i * VE, v);
+#pragma unroll
+    for (int j = 0; j < VE; ++j) {
+      float p = __expf(v[j] - M) * inv;
+      if (i * VE + j == t) p -= 1.f;
+      v[j] = p * g;
+    }
+    store_vec<T, VE>(dr + i * VE, v);
+  }
+  for (int i = nvec * VE + threadIdx.x; i < V; i += 256) {
+    float p = __expf(to_f32(lr[i]) - M) * inv;
+    if (i == t) p -= 1.f;
+    dr[i] = from_f32<T>(p * g);
+  }
+}
+
+}  // namespace smdt
+
+using namespace smdt;
+
+extern "C" hipError_t smdt_ce_stats(int dtype, const void* logits, const int64_t* target,
+                                    int64_t rows, int V, int64_t vstart, float* row_max,
+                                    float* row_sumexp, float* row_tgt, hipStream_t st) {
+  if (V % 8 != 0) return hipErrorInvalidValue;
+  if (dtype == 1) hipLaunchKernelGGL(ce_stats_kernel<bf16>, dim3(rows), dim3(256), 0, st, (const bf16*)logits, target, rows, V, vstart, row_max, row_sumexp, row_tgt);
+  else if (dtype == 2) hipLaunchKernelGGL(ce_stats_kernel<f16>, dim3(rows), dim3(256), 0, st, (const f16*)logits, target, rows, V, vstart, row_max, row_sumexp, row_tgt);
+  else hipLaunchKernelGGL(ce_stats_kernel<float>, dim3(rows), dim3(256), 0, st, (const float*)logits, target, rows, V, vstart, row_max, row_sumexp, row_tgt);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t smdt_ce_bwd(int dtype, const void* logits, const int64_t* target,
+                                  const float* gmax, const float* gsum, const float* dloss,
+                                  void* dlogits, int64_t rows, int V, int64_t vstart,
+                                  int64_t ignore_index, hipStream_t st) {
+  if (V % 8 != 0) return hipErrorInvalidValue;
+  if (dtype == 1) hipLaunchKernelGGL(ce_bwd_kernel<bf16>, dim3(rows), dim3(256), 0, st, (const bf16*)logits, target, gmax, gsum, dloss, (bf16*)dlogits, rows, V, vstart, ignore_index);
+  else if (dtype == 2) hipLaunchKernelGGL(ce_bwd_kernel<f16>, dim3(rows), dim3(256), 0, st, (const f16*)logits, target, gmax, gsum, dloss, (f16*)dlogits, rows, V, vstart, ignore_index);
+  else hipLaunchKernelGGL(ce_bwd_kernel<float>, dim3(rows), dim3(256), 0, st, (const float*)logits, target, gmax, gsum, dloss, (float*)dlogits, rows, V, vstart, ignore_index);
+  return hipGetLastError();
+}

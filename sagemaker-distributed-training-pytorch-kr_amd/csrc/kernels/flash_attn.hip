@@ -1,0 +1,616 @@
+// Flash attention (causal / full, MHA / GQA) forward and backward on gfx950 MFMA.
+//
+// The fused-attention path behind Megatron's `--use-flash-attn` flag
+// (/root/reference/3_training_megatron-lm/megatron/arguments.py:825-827) and the
+// MI355X replacement for the materialised [b*np, sq, sk] scores + K1 fused softmax path.
+//
+// Everything is built on `v_mfma_f32_32x32x16_bf16` (wave64, 32x32 output tile, K = 16) and on
+// two gfx950 facts from the CDNA4 playbook (cdna_hip_programming.md §3, T10, T12):
+//   * an MFMA accumulator tile X (column on the lane, rows in registers) can be fed, after a
+//     bf16 pack, straight back as the B operand of a product that sums over X's ROW index
+//     ("A·X"), provided the A operand uses the matching permuted k order;
+//   * `ds_read_b64_tr_b16` delivers that permuted A operand (a column gather of 4 consecutive
+//     rows) from a plain row-major LDS tile, so no transpose copy is ever made.
+// Hence every kernel here computes the "swapped" products so the softmax row index sits on
+// the lane:
+//   forward  : S^T = K.Q^T  (query on lane)  -> online softmax in registers -> O^T += V^T.P^T
+//   dK/dV    : S   = Q.K^T  (key on lane)    -> dV^T += dO^T.P,  dK^T += Q^T.dS
+//   dQ       : S^T = K.Q^T  (query on lane)  -> dQ^T += K^T.dS^T
+// dK/dV and dQ run as two kernels (FA2 split) so there are no float atomics: deterministic
+// results and no atomic-rate floor (HIP guide Guideline 12).
+//
+// LDS tiles are 64 rows x D bf16 with an XOR swizzle of the 16-byte chunk index that makes
+// BOTH the row reads (ds_read_b128, 4x16-lane groups) and the transposed reads
+// (ds_read_b64_tr_b16, 2x32-lane groups) bank-conflict free for D = 64 and D = 128.
+//
+// Layout: q/k/v/o are [B, S, heads, D] with arbitrary batch / token / head strides (elements),
+// so the kernels read Q, K, V directly out of a fused QKV projection output. lse / delta are
+// fp32 [B, H, S]. Requirements (checked by the launcher): S % 128 == 0, D in {64, 128},
+// H % Hkv == 0, 16-byte aligned rows.
+#include "common.h"
+#include "launchers.h"
+
+namespace smdt {
+namespace fa {
+
+using s16x4 = __attribute__((ext_vector_type(4))) short;
+using s16x8 = __attribute__((ext_vector_type(8))) short;
+using lds_s16x4 = __attribute__((address_space(3))) s16x4;
+
+constexpr int kBlockRows = 128;  // rows owned by a workgroup (4 waves x 32)
+constexpr int kTile = 64;        // rows per streamed LDS tile
+constexpr float kLog2e = 1.4426950408889634f;
+
+__device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ f32x16 zero16() {
+  f32x16 z;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) z[i] = 0.f;
+  return z;
+}
+
+// Byte offset of 16-byte chunk c of row r inside a [64][D] bf16 LDS tile (see header).
+template <int D>
+__device__ __forceinline__ int toff(int r, int c) {
+  int f;
+  if constexpr (D == 128) {
+    f = ((r & 3) << 2) | ((r >> 2) & 3);
+  } else {
+    f = (((r >> 1) & 1) << 2) | ((r >> 2) & 3);
+  }
+  return r * (D * 2) + 16 * (c ^ f);
+}
+
+// Row operand fragment for k-step ks: lane holds row (rbase + lane&31), elements
+// [16 ks + 8 h, +8) with h = lane >> 5.
+template <int D>
+__device__ __forceinline__ bf16x8 row_frag(const char* lds, int rbase, int ks, int lane) {
+  const int r = rbase + (lane & 31);
+  const int c = 2 * ks + (lane >> 5);
+  return *reinterpret_cast<const bf16x8*>(lds + toff<D>(r, c));
+}
+
+// Transposed fragment: A[i = col dbase + (lane&31)][k] for k-step s over tile rows
+// rbase + 16 s + ..., in the permuted k order that matches an accumulator-derived B operand:
+// element j <-> row 16 s + 8 (j >> 2) + 4 h + (j & 3).
+template <int D>
+__device__ __forceinline__ bf16x8 tr_frag(const char* lds, int rbase, int s, int dbase,
+                                          int lane) {
+  const int q = (lane >> 2) & 3, p = lane & 3;
+  const int col = dbase + 16 * ((lane >> 4) & 1) + 4 * p;
+  const int c = col >> 3;
+  const int inb = 8 * (p & 1);
+  const int r0 = rbase + 16 * s + 4 * (lane >> 5) + q;
+  const lds_s16x4* a0 = (const lds_s16x4*)(lds + toff<D>(r0, c) + inb);
+  const lds_s16x4* a1 = (const lds_s16x4*)(lds + toff<D>(r0 + 8, c) + inb);
+  s16x4 x = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)a0);
+  s16x4 y = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)a1);
+  s16x8 z = __builtin_shufflevector(x, y, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8, z);
+}
+
+// Pack accumulator registers 8 s .. 8 s + 7 into a bf16 operand fragment.
+__device__ __forceinline__ bf16x8 pack8(const f32x16& x, int s) {
+  bf16x8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = (bf16)x[8 * s + j];
+  return r;
+}
+
+// Row of accumulator register i for lane half h (32x32 C/D map).
+__device__ __forceinline__ int acc_row(int i, int h) { return (i & 3) + 8 * (i >> 2) + 4 * h; }
+
+// Global -> register staging of a 64-row tile (CH = D/8 16-byte chunks per row; 256 threads).
+template <int D>
+struct Stage {
+  static constexpr int CH = D / 8;
+  static constexpr int N = kTile * CH / 256;  // chunks per thread
+  u16x8 v[N];
+  __device__ __forceinline__ void load(const bf16* base, int64_t row_stride, int row0, int nrows) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const int idx = threadIdx.x + 256 * i;
+      const int r = idx / CH, c = idx % CH;
+      if (row0 + r < nrows) {
+        v[i] = *reinterpret_cast<const u16x8*>(base + (int64_t)(row0 + r) * row_stride + c * 8);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[i][j] = 0;
+      }
+    }
+  }
+  __device__ __forceinline__ void store(char* lds) const {
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const int idx = threadIdx.x + 256 * i;
+      const int r = idx / CH, c = idx % CH;
+      *reinterpret_cast<u16x8*>(lds + toff<D>(r, c)) = v[i];
+    }
+  }
+};
+
+// Direct global load of a row-operand fragment (used for the operands that stay in registers
+// for a whole kernel): lane holds row (row0 + lane&31), elements [16 ks + 8 h, +8).
+template <int D>
+__device__ __forceinline__ void load_reg_frags(const bf16* base, int64_t row_stride, int row0,
+                                               int lane, bf16x8 (&f)[D / 16]) {
+  const bf16* p = base + (int64_t)(row0 + (lane & 31)) * row_stride + 8 * (lane >> 5);
+#pragma unroll
+  for (int ks = 0; ks < D / 16; ++ks) f[ks] = *reinterpret_cast<const bf16x8*>(p + 16 * ks);
+}
+
+struct Strides {
+  int64_t sb, ss, sh;
+};
+
+// ---------------------------------------------------------------------------------------
+// Forward. Workgroup = 4 waves = 128 query rows of one (b, h); K/V streamed in 64-key tiles.
+template <int D, bool CAUSAL>
+__global__ __launch_bounds__(256) void fwd_kernel(const bf16* __restrict__ Q,
+                                                  const bf16* __restrict__ K,
+                                                  const bf16* __restrict__ V, bf16* __restrict__ O,
+                                                  float* __restrict__ LSE, int B, int H, int Hkv,
+                                                  int S, Strides qs, Strides ks_, Strides vs,
+                                                  Strides os, float scale) {
+  __shared__ __attribute__((aligned(16))) char lds[2 * kTile * D * 2];
+  char* k_lds = lds;
+  char* v_lds = lds + kTile * D * 2;
+
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5;
+  const int nqb = S / kBlockRows;
+  // Heaviest (latest) causal blocks first: they have the most key tiles.
+  const int qb = CAUSAL ? (nqb - 1 - (int)(blockIdx.x % nqb)) : (int)(blockIdx.x % nqb);
+  const int bh = blockIdx.x / nqb;
+  const int b = bh / H, hq = bh % H, hk = hq / (H / Hkv);
+  const int q0 = qb * kBlockRows;
+  const int qw = q0 + 32 * w;  // this wave's first query row
+  const int my_q = qw + (lane & 31);
+
+  const bf16* Qb = Q + b * qs.sb + hq * qs.sh;
+  const bf16* Kb = K + b * ks_.sb + hk * ks_.sh;
+  const bf16* Vb = V + b * vs.sb + hk * vs.sh;
+
+  bf16x8 qf[D / 16];
+  load_reg_frags<D>(Qb, qs.ss, qw, lane, qf);
+
+  f32x16 o[D / 32];
+#pragma unroll
+  for (int t = 0; t < D / 32; ++t) o[t] = zero16();
+  float m = -INFINITY, l = 0.f;
+  const float c2 = scale * kLog2e;
+
+  const int kend = CAUSAL ? (q0 + kBlockRows) : S;
+  const int ntiles = kend / kTile;
+  Stage<D> sk, sv;
+  sk.load(Kb, ks_.ss, 0, S);
+  sv.load(Vb, vs.ss, 0, S);
+  sk.store(k_lds);
+  sv.store(v_lds);
+  __syncthreads();
+
+  for (int t = 0; t < ntiles; ++t) {
+    const int kb = t * kTile;
+    const bool more = t + 1 < ntiles;
+    if (more) {
+      sk.load(Kb, ks_.ss, kb + kTile, S);
+      sv.load(Vb, vs.ss, kb + kTile, S);
+    }
+    const bool active = !CAUSAL || kb <= qw + 31;
+    if (active) {
+      // S^T tiles: rows = keys (registers), column = this lane's query.
+      f32x16 st[2];
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt) {
+        st[tt] = zero16();
+#pragma unroll
+        for (int kk = 0; kk < D / 16; ++kk)
+          st[tt] = mfma(row_frag<D>(k_lds, 32 * tt, kk, lane), qf[kk], st[tt]);
+      }
+      float tmax = -INFINITY;
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          float sv2 = st[tt][i] * c2;
+          if (CAUSAL) {
+            const int key = kb + 32 * tt + acc_row(i, h);
+            if (key > my_q) sv2 = -INFINITY;
+          }
+          st[tt][i] = sv2;
+          tmax = fmaxf(tmax, sv2);
+        }
+      }
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+      const float mnew = fmaxf(m, tmax);
+      const float base = mnew == -INFINITY ? 0.f : mnew;
+      const float alpha = exp2f(m - base);
+      float rs = 0.f;
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          float p = exp2f(st[tt][i] - base);
+          st[tt][i] = p;
+          rs += p;
+        }
+      }
+      rs += __shfl_xor(rs, 32, 64);
+      l = l * alpha + rs;
+      m = mnew;
+#pragma unroll
+      for (int dt = 0; dt < D / 32; ++dt) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) o[dt][i] *= alpha;
+      }
+      // O^T[d, q] += V^T[d, keys] . P^T[keys, q]
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt) {
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const bf16x8 pb = pack8(st[tt], s);
+#pragma unroll
+          for (int dt = 0; dt < D / 32; ++dt)
+            o[dt] = mfma(tr_frag<D>(v_lds, 32 * tt, s, 32 * dt, lane), pb, o[dt]);
+        }
+      }
+    }
+    __syncthreads();
+    if (more) {
+      sk.store(k_lds);
+      sv.store(v_lds);
+    }
+    __syncthreads();
+  }
+
+  // Epilogue: O[q, d] = O^T / l ; lse = (m + log2 l) * ln 2.
+  const float inv = l > 0.f ? 1.f / l : 0.f;
+  bf16* Ob = O + b * os.sb + hq * os.sh + (int64_t)my_q * os.ss;
+#pragma unroll
+  for (int dt = 0; dt < D / 32; ++dt) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      using bf4 = __attribute__((ext_vector_type(4))) __bf16;
+      bf4 v4;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v4[j] = (bf16)(o[dt][4 * g + j] * inv);
+      *reinterpret_cast<bf4*>(Ob + 32 * dt + 8 * g + 4 * h) = v4;
+    }
+  }
+  if (h == 0) {
+    LSE[((int64_t)b * H + hq) * S + my_q] = (m + __log2f(l)) * 0.6931471805599453f;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// delta[b, h, q] = sum_d dO[q, d] * O[q, d]
+template <int D>
+__global__ __launch_bounds__(256) void delta_kernel(const bf16* __restrict__ O,
+                                                    const bf16* __restrict__ dO,
+                                                    float* __restrict__ delta, int B, int H,
+                                                    int S, Strides os, Strides dos) {
+  // 8 lanes per row, each lane D/8 contiguous elements.
+  const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t row = gid / 8;
+  const int part = (int)(gid % 8);
+  if (row >= (int64_t)B * H * S) return;
+  const int q = (int)(row % S);
+  const int64_t bh = row / S;
+  const int b = (int)(bh / H), hh = (int)(bh % H);
+  const bf16* o = O + b * os.sb + hh * os.sh + (int64_t)q * os.ss + part * (D / 8);
+  const bf16* g = dO + b * dos.sb + hh * dos.sh + (int64_t)q * dos.ss + part * (D / 8);
+  float acc = 0.f;
+#pragma unroll
+  for (int c = 0; c < D / 64; ++c) {
+    float a[8], bb[8];
+    load_vec<bf16, 8>(o + 8 * c, a);
+    load_vec<bf16, 8>(g + 8 * c, bb);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc += a[j] * bb[j];
+  }
+#pragma unroll
+  for (int off = 4; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 8);
+  if (part == 0) delta[row] = acc;
+}
+
+// ---------------------------------------------------------------------------------------
+// dK / dV. Workgroup = 4 waves = 128 keys of one (b, kv-head); each wave keeps K, V of its 32
+// keys and dK^T, dV^T in registers while the workgroup sweeps the query heads of the group and
+// their 64-row query tiles (Q, dO, lse, delta staged in LDS).
+template <int D, bool CAUSAL>
+__global__ __launch_bounds__(256) void bwd_dkdv_kernel(
+    const bf16* __restrict__ Q, const bf16* __restrict__ K, const bf16* __restrict__ V,
+    const bf16* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ DELTA,
+    bf16* __restrict__ dK, bf16* __restrict__ dV, int B, int H, int Hkv, int S, Strides qs,
+    Strides ks_, Strides vs, Strides dos, Strides dks, Strides dvs, float scale) {
+  __shared__ __attribute__((aligned(16))) char lds[2 * kTile * D * 2 + 2 * kTile * 4];
+  char* q_lds = lds;
+  char* do_lds = lds + kTile * D * 2;
+  float* lse_lds = reinterpret_cast<float*>(lds + 2 * kTile * D * 2);
+  float* del_lds = lse_lds + kTile;
+
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5;
+  const int nkb = S / kBlockRows;
+  const int kblk = CAUSAL ? (int)(blockIdx.x % nkb) : (int)(blockIdx.x % nkb);
+  const int bhk = blockIdx.x / nkb;
+  const int b = bhk / Hkv, hk = bhk % Hkv;
+  const int group = H / Hkv;
+  const int k0 = kblk * kBlockRows;
+  const int kw = k0 + 32 * w;
+  const int my_key = kw + (lane & 31);
+
+  bf16x8 kf[D / 16], vf[D / 16];
+  load_reg_frags<D>(K + b * ks_.sb + hk * ks_.sh, ks_.ss, kw, lane, kf);
+  load_reg_frags<D>(V + b * vs.sb + hk * vs.sh, vs.ss, kw, lane, vf);
+
+  f32x16 dk[D / 32], dv[D / 32];
+#pragma unroll
+  for (int t = 0; t < D / 32; ++t) dk[t] = dv[t] = zero16();
+  const float c2 = scale * kLog2e;
+
+  const int qstart = CAUSAL ? k0 : 0;
+  const int ntiles = (S - qstart) / kTile;
+  const int total = ntiles * group;
+
+  Stage<D> sq, sdo;
+  auto tile_coords = [&](int it, int& hq, int& qb) {
+    hq = hk * group + it / ntiles;
+    qb = qstart + (it % ntiles) * kTile;
+  };
+  {
+    int hq, qb;
+    tile_coords(0, hq, qb);
+    sq.load(Q + b * qs.sb + hq * qs.sh, qs.ss, qb, S);
+    sdo.load(dO + b * dos.sb + hq * dos.sh, dos.ss, qb, S);
+    sq.store(q_lds);
+    sdo.store(do_lds);
+    if (threadIdx.x < kTile) {
+      lse_lds[threadIdx.x] = LSE[((int64_t)b * H + hq) * S + qb + threadIdx.x] * kLog2e;
+      del_lds[threadIdx.x] = DELTA[((int64_t)b * H + hq) * S + qb + threadIdx.x];
+    }
+    __syncthreads();
+  }
+
+  for (int it = 0; it < total; ++it) {
+    int hq, qb;
+    tile_coords(it, hq, qb);
+    const bool more = it + 1 < total;
+    int nhq = 0, nqb = 0;
+    float nl = 0.f, nd = 0.f;
+    if (more) {
+      tile_coords(it + 1, nhq, nqb);
+      sq.load(Q + b * qs.sb + nhq * qs.sh, qs.ss, nqb, S);
+      sdo.load(dO + b * dos.sb + nhq * dos.sh, dos.ss, nqb, S);
+      if (threadIdx.x < kTile) {
+        nl = LSE[((int64_t)b * H + nhq) * S + nqb + threadIdx.x] * kLog2e;
+        nd = DELTA[((int64_t)b * H + nhq) * S + nqb + threadIdx.x];
+      }
+    }
+#pragma unroll
+    for (int qs2 = 0; qs2 < 2; ++qs2) {
+      const int qsub = qb + 32 * qs2;
+      if (CAUSAL && qsub + 31 < kw) continue;  // all queries precede all of this wave's keys
+      // S[q, key] = Q . K^T  (key on lane, query rows in registers)
+      f32x16 s = zero16(), dp = zero16();
+#pragma unroll
+      for (int kk = 0; kk < D / 16; ++kk) {
+        s = mfma(row_frag<D>(q_lds, 32 * qs2, kk, lane), kf[kk], s);
+        dp = mfma(row_frag<D>(do_lds, 32 * qs2, kk, lane), vf[kk], dp);
+      }
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int qr = 32 * qs2 + acc_row(i, h);
+        float p = exp2f(s[i] * c2 - lse_lds[qr]);
+        if (CAUSAL && my_key > qb + qr) p = 0.f;
+        s[i] = p;                            // P
+        dp[i] = p * (dp[i] - del_lds[qr]);   // dS
+      }
+      // dV^T[d, key] += dO^T[d, q] . P[q, key] ; dK^T[d, key] += Q^T[d, q] . dS[q, key]
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+        const bf16x8 pb = pack8(s, st);
+        const bf16x8 db = pack8(dp, st);
+#pragma unroll
+        for (int dt = 0; dt < D / 32; ++dt) {
+          dv[dt] = mfma(tr_frag<D>(do_lds, 32 * qs2, st, 32 * dt, lane), pb, dv[dt]);
+          dk[dt] = mfma(tr_frag<D>(q_lds, 32 * qs2, st, 32 * dt, lane), db, dk[dt]);
+        }
+      }
+    }
+    __syncthreads();
+    if (more) {
+      sq.store(q_lds);
+      sdo.store(do_lds);
+      if (threadIdx.x < kTile) {
+        lse_lds[threadIdx.x] = nl;
+        del_lds[threadIdx.x] = nd;
+      }
+    }
+    __syncthreads();
+  }
+
+  // dK[key, d] = scale * dK^T ; dV[key, d] = dV^T (key on lane, d in registers)
+  bf16* dKb = dK + b * dks.sb + hk * dks.sh + (int64_t)my_key * dks.ss;
+  bf16* dVb = dV + b * dvs.sb + hk * dvs.sh + (int64_t)my_key * dvs.ss;
+  using bf4 = __attribute__((ext_vector_type(4))) __bf16;
+#pragma unroll
+  for (int dt = 0; dt < D / 32; ++dt) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      bf4 a, c;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        a[j] = (bf16)(dk[dt][4 * g + j] * scale);
+        c[j] = (bf16)dv[dt][4 * g + j];
+      }
+      *reinterpret_cast<bf4*>(dKb + 32 * dt + 8 * g + 4 * h) = a;
+      *reinterpret_cast<bf4*>(dVb + 32 * dt + 8 * g + 4 * h) = c;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// dQ. Workgroup = 4 waves = 128 query rows of one (b, h); K/V streamed in 64-key tiles.
+template <int D, bool CAUSAL>
+__global__ __launch_bounds__(256) void bwd_dq_kernel(
+    const bf16* __restrict__ Q, const bf16* __restrict__ K, const bf16* __restrict__ V,
+    const bf16* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ DELTA,
+    bf16* __restrict__ dQ, int B, int H, int Hkv, int S, Strides qs, Strides ks_, Strides vs,
+    Strides dos, Strides dqs, float scale) {
+  __shared__ __attribute__((aligned(16))) char lds[2 * kTile * D * 2];
+  char* k_lds = lds;
+  char* v_lds = lds + kTile * D * 2;
+
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5;
+  const int nqb = S / kBlockRows;
+  const int qb = CAUSAL ? (nqb - 1 - (int)(blockIdx.x % nqb)) : (int)(blockIdx.x % nqb);
+  const int bh = blockIdx.x / nqb;
+  const int b = bh / H, hq = bh % H, hk = hq / (H / Hkv);
+  const int q0 = qb * kBlockRows;
+  const int qw = q0 + 32 * w;
+  const int my_q = qw + (lane & 31);
+
+  bf16x8 qf[D / 16], dof[D / 16];
+  load_reg_frags<D>(Q + b * qs.sb + hq * qs.sh, qs.ss, qw, lane, qf);
+  load_reg_frags<D>(dO + b * dos.sb + hq * dos.sh, dos.ss, qw, lane, dof);
+  const float lse2 = LSE[((int64_t)b * H + hq) * S + my_q] * kLog2e;
+  const float dl = DELTA[((int64_t)b * H + hq) * S + my_q];
+  const float c2 = scale * kLog2e;
+
+  const bf16* Kb = K + b * ks_.sb + hk * ks_.sh;
+  const bf16* Vb = V + b * vs.sb + hk * vs.sh;
+
+  f32x16 dq[D / 32];
+#pragma unroll
+  for (int t = 0; t < D / 32; ++t) dq[t] = zero16();
+
+  const int kend = CAUSAL ? (q0 + kBlockRows) : S;
+  const int ntiles = kend / kTile;
+  Stage<D> sk, sv;
+  sk.load(Kb, ks_.ss, 0, S);
+  sv.load(Vb, vs.ss, 0, S);
+  sk.store(k_lds);
+  sv.store(v_lds);
+  __syncthreads();
+
+  for (int t = 0; t < ntiles; ++t) {
+    const int kb = t * kTile;
+    const bool more = t + 1 < ntiles;
+    if (more) {
+      sk.load(Kb, ks_.ss, kb + kTile, S);
+      sv.load(Vb, vs.ss, kb + kTile, S);
+    }
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt) {
+      if (CAUSAL && kb + 32 * tt > qw + 31) continue;
+      f32x16 st = zero16(), dpt = zero16();
+#pragma unroll
+      for (int kk = 0; kk < D / 16; ++kk) {
+        st = mfma(row_frag<D>(k_lds, 32 * tt, kk, lane), qf[kk], st);
+        dpt = mfma(row_frag<D>(v_lds, 32 * tt, kk, lane), dof[kk], dpt);
+      }
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int key = kb + 32 * tt + acc_row(i, h);
+        float p = exp2f(st[i] * c2 - lse2);
+        if (CAUSAL && key > my_q) p = 0.f;
+        dpt[i] = p * (dpt[i] - dl);  // dS^T
+      }
+      // dQ^T[d, q] += K^T[d, keys] . dS^T[keys, q]
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const bf16x8 db = pack8(dpt, s);
+#pragma unroll
+        for (int dt = 0; dt < D / 32; ++dt)
+          dq[dt] = mfma(tr_frag<D>(k_lds, 32 * tt, s, 32 * dt, lane), db, dq[dt]);
+      }
+    }
+    __syncthreads();
+    if (more) {
+      sk.store(k_lds);
+      sv.store(v_lds);
+    }
+    __syncthreads();
+  }
+
+  bf16* dQb = dQ + b * dqs.sb + hq * dqs.sh + (int64_t)my_q * dqs.ss;
+  using bf4 = __attribute__((ext_vector_type(4))) __bf16;
+#pragma unroll
+  for (int dt = 0; dt < D / 32; ++dt) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      bf4 a;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) a[j] = (bf16)(dq[dt][4 * g + j] * scale);
+      *reinterpret_cast<bf4*>(dQb + 32 * dt + 8 * g + 4 * h) = a;
+    }
+  }
+}
+
+}  // namespace fa
+}  // namespace smdt
+
+using namespace smdt;
+using namespace smdt::fa;
+
+static bool fa_shape_ok(int dtype, int H, int Hkv, int S, int D) {
+  return dtype == 1 && (D == 64 || D == 128) && S % kBlockRows == 0 && S > 0 && Hkv > 0 &&
+         H % Hkv == 0;
+}
+
+extern "C" hipError_t smdt_flash_fwd(int dtype, const void* q, const void* k, const void* v,
+                                     void* o, float* lse, int B, int H, int Hkv, int S, int D,
+                                     int64_t q_sb, int64_t q_ss, int64_t q_sh, int64_t k_sb,
+                                     int64_t k_ss, int64_t k_sh, int64_t v_sb, int64_t v_ss,
+                                     int64_t v_sh, int64_t o_sb, int64_t o_ss, int64_t o_sh,
+                                     float scale, int causal, hipStream_t st) {
+  if (!fa_shape_ok(dtype, H, Hkv, S, D)) return hipErrorInvalidValue;
+  Strides qs{q_sb, q_ss, q_sh}, ks{k_sb, k_ss, k_sh}, vs{v_sb, v_ss, v_sh}, os{o_sb, o_ss, o_sh};
+  dim3 grid((unsigned)((int64_t)B * H * (S / kBlockRows)));
+#define SMDT_FA_FWD(DD, CC)                                                                     \
+  hipLaunchKernelGGL((fwd_kernel<DD, CC>), grid, dim3(256), 0, st, (const bf16*)q,             \
+                     (const bf16*)k, (const bf16*)v, (bf16*)o, lse, B, H, Hkv, S, qs, ks, vs, os, \
+                     scale)
+  if (D == 64) { if (causal) SMDT_FA_FWD(64, true); else SMDT_FA_FWD(64, false); }
+  else { if (causal) SMDT_FA_FWD(128, true); else SMDT_FA_FWD(128, false); }
+#undef SMDT_FA_FWD
+  return hipGetLastError();
+}
+
+extern "C" hipError_t smdt_flash_bwd(int dtype, const void* q, const void* k, const void* v,
+                                     const void* o, const void* dout, const float* lse,
+                                     float* delta, void* dq, void* dk, void* dv, int B, int H,
+                                     int Hkv, int S, int D, const int64_t* strides, float scale,
+                                     int causal, hipStream_t st) {
+  if (!fa_shape_ok(dtype, H, Hkv, S, D)) return hipErrorInvalidValue;
+  // strides: 8 x (batch, seq, head) element strides for q, k, v, o, dO, dQ, dK, dV.
+  Strides qs{strides[0], strides[1], strides[2]}, ks{strides[3], strides[4], strides[5]},
+      vs{strides[6], strides[7], strides[8]}, os{strides[9], strides[10], strides[11]},
+      dos{strides[12], strides[13], strides[14]}, dqs{strides[15], strides[16], strides[17]},
+      dks{strides[18], strides[19], strides[20]}, dvs{strides[21], strides[22], strides[23]};
+  {
+    int64_t rows = (int64_t)B * H * S;
+    dim3 grid((unsigned)((rows * 8 + 255) / 256));
+    if (D == 64)
+      hipLaunchKernelGGL((delta_kernel<64>), grid, dim3(256), 0, st, (const bf16*)o, (const bf16*)dout, delta, B, H, S, os, dos);
+    else
+      hipLaunchKernelGGL((delta_kernel<128>), grid, dim3(256), 0, st, (const bf16*)o, (const bf16*)dout, delta, B, H, S, os, dos);
+  }
+  dim3 gkv((unsigned)((int64_t)B * Hkv * (S / kBlockRows)));
+  dim3 gq((unsigned)((int64_t)B * H * (S / kBlockRows)));
+#define SMDT_FA_BWD(DD, CC)                                                                      \
+  do {                                                                                           \
+    hipLaunchKernelGGL((bwd_dkdv_kernel<DD, CC>), gkv, dim3(256), 0, st, (const bf16*)q,        \
+                       (const bf16*)k, (const bf16*)v, (const bf16*)dout, lse, delta, (bf16*)dk,  \
+                       (bf16*)dv, B, H, Hkv, S, qs, ks, vs, dos, dks, dvs, scale);                \
+    hipLaunchKernelGGL((bwd_dq_kernel<DD, CC>), gq, dim3(256), 0, st, (const bf16*)q,           \
+                       (const bf16*)k, (const bf16*)v, (const bf16*)dout, lse, delta, (bf16*)dq,  \
+                       B, H, Hkv, S, qs, ks, vs, dos, dqs, scale);                                \
+  } while (0)
+  if (D == 64) { if (causal) SMDT_FA_BWD(64, true); else SMDT_FA_BWD(64, false); }
+  else { if (causal) SMDT_FA_BWD(128, true); else SMDT_FA_BWD(128, false); }
+#undef SMDT_FA_BWD
+  return hipGetLastError();
+}

@@ -1,0 +1,85 @@
+// C ABI of the gfx950 kernel library. Kernel translation units (.hip) are compiled without any
+// PyTorch headers (fast, torch-independent builds); `bindings.cpp` is the only file that sees
+// ATen and forwards tensors + the current HIP stream to these launchers.
+//
+// dtype codes: 0 = fp32, 1 = bf16, 2 = fp16.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+extern "C" {
+
+// layernorm.hip
+int smdt_ln_bwd_nblocks(int64_t rows, int H);
+hipError_t smdt_layernorm_fwd(int dtype, int wdtype, const void* x, const void* res,
+                              const void* bias, const void* gamma, const void* beta, void* y,
+                              void* s_out, float* mean, float* rstd, int64_t rows, int H,
+                              float eps, float p_drop, uint64_t seed, uint64_t offset, int rms,
+                              hipStream_t st);
+hipError_t smdt_layernorm_bwd(int dtype, int wdtype, const void* dy, const void* ds_in,
+                              const void* s, const void* gamma, const float* mean,
+                              const float* rstd, void* ds_out, void* dx_out, float* partials,
+                              int nblocks, float* dgamma, float* dbeta, float* dbias,
+                              int64_t rows, int H, float p_drop, uint64_t seed, uint64_t offset,
+                              int rms, hipStream_t st);
+
+// bias_act.hip
+int smdt_bias_act_slices(int64_t rows, int N);
+hipError_t smdt_bias_act_fwd(int dtype, int act, const void* x, const void* bias, void* y,
+                             int64_t rows, int N, hipStream_t st);
+hipError_t smdt_bias_act_bwd(int dtype, int act, const void* dy, const void* x, const void* bias,
+                             void* dx, float* partials, float* dbias, int64_t rows, int N,
+                             hipStream_t st);
+hipError_t smdt_col_sum(const float* partials, int nslices, int N, float* out, hipStream_t st);
+hipError_t smdt_swiglu_fwd(int dtype, const void* x, void* y, int64_t rows, int F,
+                           hipStream_t st);
+hipError_t smdt_swiglu_bwd(int dtype, const void* dy, const void* x, void* dx, int64_t rows,
+                           int F, hipStream_t st);
+
+// softmax.hip
+hipError_t smdt_softmax_fwd(int dtype, int mode, const void* x, const uint8_t* mask, void* y,
+                            int64_t rows, int sq, int sk, int heads, float scale,
+                            hipStream_t st);
+hipError_t smdt_softmax_bwd(int dtype, int mode, const void* dy, const void* y, void* dx,
+                            int64_t rows, int sq, int sk, float scale, hipStream_t st);
+
+// optim.hip
+hipError_t smdt_adam(float* master, const float* grad, float* m, float* v, void* model_out,
+                     int model_dtype, int64_t n, float lr, float beta1, float beta2, float eps,
+                     float wd, float bc1, float bc2, int adamw, const float* grad_mul,
+                     const int* found_inf, hipStream_t st);
+int smdt_sumsq_nblocks(int64_t n);
+hipError_t smdt_sumsq(int dtype, const void* x, int64_t n, float* partial, int nblocks,
+                      float* out, int* found_inf, hipStream_t st);
+hipError_t smdt_clip_coef(const float* sumsq, float max_norm, float inv_scale, float* mul_out,
+                          float* norm_out, hipStream_t st);
+hipError_t smdt_scale(int dtype, void* x, int64_t n, const float* mul, float cmul,
+                      hipStream_t st);
+hipError_t smdt_cast(int in_dtype, int out_dtype, const void* x, void* y, int64_t n,
+                     int accumulate, hipStream_t st);
+
+// rope.hip
+hipError_t smdt_rope(int dtype, void* x, int64_t ntok, int nh, int64_t tok_stride,
+                     int64_t head_stride, int rot, const float* cos_t, const float* sin_t,
+                     int pos_div, int pos_mod, int backward, hipStream_t st);
+
+// cross_entropy.hip
+hipError_t smdt_ce_stats(int dtype, const void* logits, const int64_t* target, int64_t rows,
+                         int V, int64_t vstart, float* row_max, float* row_sumexp,
+                         float* row_tgt, hipStream_t st);
+hipError_t smdt_ce_bwd(int dtype, const void* logits, const int64_t* target, const float* gmax,
+                       const float* gsum, const float* dloss, void* dlogits, int64_t rows, int V,
+                       int64_t vstart, int64_t ignore_index, hipStream_t st);
+
+// flash_attn.hip
+hipError_t smdt_flash_fwd(int dtype, const void* q, const void* k, const void* v, void* o,
+                          float* lse, int B, int H, int Hkv, int S, int D, int64_t q_sb,
+                          int64_t q_ss, int64_t q_sh, int64_t k_sb, int64_t k_ss, int64_t k_sh,
+                          int64_t v_sb, int64_t v_ss, int64_t v_sh, int64_t o_sb, int64_t o_ss,
+                          int64_t o_sh, float scale, int causal, hipStream_t st);
+hipError_t smdt_flash_bwd(int dtype, const void* q, const void* k, const void* v, const void* o,
+                          const void* dout, const float* lse, float* delta, void* dq, void* dk,
+                          void* dv, int B, int H, int Hkv, int S, int D, const int64_t* strides,
+                          float scale, int causal, hipStream_t st);
+
+}  // extern "C"

@@ -1,0 +1,193 @@
+"""GPT model (Megatron ``GPTModel`` semantics) for pipeline / tensor / sequence parallelism.
+
+Reference behaviour: `model_provider` builds
+``GPTModel(config, num_tokentypes=0, parallel_output=True, pre_process, post_process)``
+(/root/reference/3_training_megatron-lm/pretrain_gpt.py:46-58); with labels the model returns the
+per-token LM loss [b, s] computed by the vocab-parallel cross entropy; vocab is padded to a
+multiple of ``make_vocab_size_divisible_by * tp`` (NB3:1212); word embeddings are tied to the
+output layer unless ``--untie-embeddings-and-output-weights``.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+
+from ..ops import functional as SF
+from ..parallel import state as ps
+from ..parallel import tensor_parallel as tp
+from .transformer import ParallelTransformer, TransformerConfig
+
+
+def pad_vocab_size(orig: int, divisible_by: int = 128, tp_size: int = 1) -> int:
+    """Megatron's ``_vocab_size_with_padding``."""
+    m = divisible_by * tp_size
+    return ((orig + m - 1) // m) * m
+
+
+def stage_layer_range(num_layers: int, pp: int, pp_rank: int, vpp: Optional[int] = None, vpp_rank: int = 0):
+    """(first_layer, count) for a (virtual) pipeline stage; layers split uniformly."""
+    if vpp is None:
+        assert num_layers % pp == 0, "num_layers must be divisible by the pipeline size"
+        n = num_layers // pp
+        return pp_rank * n, n
+    assert num_layers % (pp * vpp) == 0
+    n = num_layers // (pp * vpp)
+    return vpp_rank * (num_layers // vpp) + pp_rank * n, n
+
+
+class GPTModel(nn.Module):
+    def __init__(self, cfg: TransformerConfig, pre_process: bool = True, post_process: bool = True,
+                 parallel_output: bool = True, device=None, layer_range=None):
+        super().__init__()
+        st = ps.get_state()
+        self.cfg = cfg
+        self.pre_process, self.post_process = pre_process, post_process
+        self.parallel_output = parallel_output
+        self.sp = cfg.sequence_parallel and st.tp > 1
+        if layer_range is None:
+            layer_range = stage_layer_range(cfg.num_layers, st.pp, st.pp_rank, st.virtual_pp, st.virtual_pp_rank)
+        first, n = layer_range
+        self.first_layer, self.num_local_layers = first, n
+        std = cfg.init_method_std
+        if pre_process:
+            self.embedding = tp.VocabParallelEmbedding(cfg.padded_vocab_size, cfg.hidden_size, init_std=std,
+                                                       key="embedding.word", seed=cfg.seed,
+                                                       params_dtype=cfg.params_dtype, device=device)
+            if cfg.position_embedding_type == "learned_absolute":
+                w = tp.init_full_then_shard((cfg.max_position_embeddings, cfg.hidden_size), std,
+                                            "embedding.position.weight", cfg.seed, cfg.params_dtype, device, None, 0, 1)
+                self.position_embeddings = nn.Parameter(w)
+            else:
+                self.position_embeddings = None
+        self.decoder = ParallelTransformer(cfg, first, n, post_norm=post_process, device=device)
+        self.output_weight = None
+        if post_process:
+            if cfg.untie_embeddings_and_output_weights:
+                w = tp.init_full_then_shard((cfg.padded_vocab_size, cfg.hidden_size), std, "output_layer.weight",
+                                            cfg.seed, cfg.params_dtype, device, 0, st.tp_rank, st.tp)
+                self.output_weight = nn.Parameter(w)
+                self.output_weight.tensor_model_parallel = True
+            elif not pre_process:
+                # Tied embeddings across pipeline stages: the last stage keeps its own copy,
+                # initialised identically and kept in sync by an embedding-group all-reduce of
+                # the gradients (`allreduce_word_embedding_grads`).
+                w = tp.init_full_then_shard((cfg.padded_vocab_size, cfg.hidden_size), std, "embedding.word.weight",
+                                            cfg.seed, cfg.params_dtype, device, 0, st.tp_rank, st.tp)
+                self.output_weight = nn.Parameter(w)
+                self.output_weight.tensor_model_parallel = True
+                self.output_weight.shared_embedding = True
+        if pre_process and post_process is False and not cfg.untie_embeddings_and_output_weights and st.pp > 1:
+            self.embedding.weight.shared_embedding = True
+        self.input_tensor = None
+        if cfg.position_embedding_type == "rope":
+            rot = int(cfg.kv_channels * cfg.rotary_percent)
+            rot -= rot % 16
+            cos, sin = SF.rope_tables(cfg.max_position_embeddings, rot, cfg.rotary_base, device=device)
+            self.register_buffer("rope_cos", cos, persistent=False)
+            self.register_buffer("rope_sin", sin, persistent=False)
+            for layer in self.decoder.layers:
+                layer.attention.set_rope(self.rope_cos, self.rope_sin, rot)
+
+    # ---- pipeline plumbing
+    def set_input_tensor(self, t):
+        self.input_tensor = t
+
+    def word_embeddings_weight(self):
+        if self.pre_process:
+            return self.embedding.weight
+        return self.output_weight
+
+    def _embed(self, tokens, position_ids):
+        st = ps.get_state()
+        e = self.embedding(tokens, reduce=False)                  # [b, s, h] (TP-partial)
+        e = e.transpose(0, 1).contiguous()                        # [s, b, h]
+        if st.tp > 1:
+            if self.sp:
+                e = tp.reduce_scatter_to_sequence_parallel_region(e)
+            else:
+                e = tp.reduce_from_tensor_model_parallel_region(e)
+        if self.position_embeddings is not None:
+            pos = position_ids.transpose(0, 1)                   # [s, b]
+            pe = self.position_embeddings[pos]                   # [s, b, h]
+            if self.sp:
+                pe = tp.scatter_to_sequence_parallel_region(pe)
+            e = e + pe
+        return e
+
+    def lm_logits(self, h):
+        st = ps.get_state()
+        w = self.output_weight if self.output_weight is not None else self.embedding.weight
+        logits = tp.linear_with_grad_accumulation_and_async_allreduce(
+            h, w, None, sequence_parallel=self.sp, async_grad_allreduce=(st.tp > 1 and not self.sp))
+        if not self.parallel_output:
+            logits = tp.gather_from_tensor_model_parallel_region(logits)
+        return logits                                            # [s, b, V / tp]
+
+    def forward(self, tokens, position_ids=None, attention_mask=None, labels=None):
+        if self.pre_process:
+            if position_ids is None:
+                position_ids = torch.arange(tokens.shape[1], device=tokens.device).unsqueeze(0).expand_as(tokens)
+            x = self._embed(tokens, position_ids)
+        else:
+            x = self.input_tensor
+        out = self.decoder(x, None, None)
+        if not self.post_process:
+            px, pb, res = out
+            return SF.bias_dropout_add(px, pb, res, self.cfg.hidden_dropout, self.training)
+        logits = self.lm_logits(out)
+        if labels is None:
+            return logits.transpose(0, 1).contiguous()
+        st = ps.get_state()
+        vstart = st.tp_rank * (self.cfg.padded_vocab_size // st.tp) if self.parallel_output else 0
+        group = st.tp_group if (st.tp > 1 and self.parallel_output) else None
+        loss = SF.cross_entropy(logits, labels.transpose(0, 1), vstart, group, inplace_grad=True)
+        return loss.transpose(0, 1).contiguous()                 # [b, s]
+
+
+def allreduce_word_embedding_grads(model: GPTModel):
+    """Sum tied word-embedding grads between the first and last pipeline stage (Megatron's
+    embedding group)."""
+    st = ps.get_state()
+    if st.pp == 1 or model.cfg.untie_embeddings_and_output_weights or st.embd_group is None:
+        return
+    if not (st.is_first_stage(ignore_virtual=True) or st.is_last_stage(ignore_virtual=True)):
+        return
+    w = model.word_embeddings_weight()
+    g = getattr(w, "main_grad", None)
+    if g is None:
+        g = w.grad
+    if g is not None:
+        dist.all_reduce(g, group=st.embd_group)
+
+
+def gpt_flops_per_token(cfg: TransformerConfig, seq_len: int, recompute: bool = False) -> float:
+    """Model FLOPs per token, Megatron's formula 72 B s L h^2 (1 + s/6h + V/12Lh) / (B s)
+    (x 4/3 with full recompute); the reference's 41 TFLOP/s/GPU is derived with it."""
+    L, h, V = cfg.num_layers, cfg.hidden_size, cfg.padded_vocab_size
+    f = 72.0 * L * h * h * (1.0 + seq_len / (6.0 * h) + V / (12.0 * L * h))
+    if cfg.activation == "swiglu" or cfg.num_query_groups != cfg.num_attention_heads:
+        # exact count for non-GPT2 shapes: 6 * (params in matmuls) + attention
+        hd = cfg.kv_channels
+        qkv = h * (cfg.num_attention_heads + 2 * cfg.num_query_groups) * hd
+        proj = cfg.num_attention_heads * hd * h
+        ff = h * cfg.ffn_hidden_size * (3 if cfg.activation == "swiglu" else 2)
+        per_layer = 6 * (qkv + proj + ff) + 12 * seq_len * cfg.num_attention_heads * hd
+        f = L * per_layer + 6 * h * V
+    return f * (4.0 / 3.0 if recompute else 1.0)
+
+
+GPT_CONFIGS = {
+    # name: (layers, hidden, heads, seq)
+    "gpt2-small": dict(num_layers=12, hidden_size=768, num_attention_heads=12),
+    "gpt2-medium": dict(num_layers=24, hidden_size=1024, num_attention_heads=16),   # "345M"
+    "gpt2-345m": dict(num_layers=24, hidden_size=1024, num_attention_heads=16),
+    "gpt3-1.3b": dict(num_layers=24, hidden_size=2048, num_attention_heads=16),
+    "gpt3-6.7b": dict(num_layers=32, hidden_size=4096, num_attention_heads=32),
+    "llama-7b": dict(num_layers=32, hidden_size=4096, num_attention_heads=32, activation="swiglu",
+                     normalization="RMSNorm", position_embedding_type="rope", add_bias_linear=False,
+                     ffn_hidden_size=11008, layernorm_epsilon=1e-6, untie_embeddings_and_output_weights=True),
+}

@@ -1,0 +1,297 @@
+"""Megatron-compatible parallel transformer (GPT / LLaMA families) on the gfx950 kernel library.
+
+Covers the model side of the reference's Megatron recipe (`core_transformer_config_
+from_args`, /root/reference/3_training_megatron-lm/megatron/arguments.py:419-446, GPTModel at
+`pretrain_gpt.py:46-58`): pre-LN blocks, learned-absolute or RoPE positions, GeLU / SwiGLU /
+squared-ReLU MLPs, MHA or GQA, hidden/attention dropout, TP + SP + activation recompute.
+
+Activation layout is [s, b, h] (sequence-first, as Megatron) so sequence-parallel shards are
+contiguous chunks and the TP collectives move contiguous buffers.
+
+The residual stream is "deferred": a layer returns (branch_output, branch_bias) plus the
+residual, and the NEXT layer's first LayerNorm consumes them through ONE fused kernel
+(bias + dropout + residual-add + LayerNorm, K4+K6), so the residual stream is written once and
+read once per sub-block. Layer 0 folds the embedding dropout into the same kernel.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import Optional
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ..ops import functional as SF
+from ..parallel import state as ps
+from ..parallel import tensor_parallel as tp
+from ..parallel.random import checkpoint as rng_checkpoint, get_rng
+
+
+@dataclass
+class TransformerConfig:
+    num_layers: int = 24
+    hidden_size: int = 1024
+    num_attention_heads: int = 16
+    num_query_groups: Optional[int] = None       # GQA (None -> MHA)
+    ffn_hidden_size: Optional[int] = None        # default 4h (GeLU) / 8h/3 rounded (SwiGLU)
+    kv_channels: Optional[int] = None
+    hidden_dropout: float = 0.1
+    attention_dropout: float = 0.1
+    layernorm_epsilon: float = 1e-5
+    normalization: str = "LayerNorm"            # or "RMSNorm"
+    activation: str = "gelu"                     # gelu | swiglu | squared_relu | gelu_erf
+    add_bias_linear: bool = True
+    position_embedding_type: str = "learned_absolute"   # or "rope"
+    rotary_percent: float = 1.0
+    rotary_base: float = 10000.0
+    max_position_embeddings: int = 1024
+    padded_vocab_size: int = 50304
+    untie_embeddings_and_output_weights: bool = False
+    init_method_std: float = 0.02
+    params_dtype: torch.dtype = torch.bfloat16
+    seed: int = 1234
+    # parallelism
+    sequence_parallel: bool = False
+    async_tensor_model_parallel_allreduce: bool = True
+    # fusions (Megatron --no-*-fusion flags turn these off)
+    masked_softmax_fusion: bool = True
+    bias_gelu_fusion: bool = True
+    bias_dropout_fusion: bool = True
+    use_flash_attn: bool = True
+    apply_query_key_layer_scaling: bool = False
+    # recompute (P9)
+    recompute_granularity: Optional[str] = None  # "full" | "selective"
+    recompute_method: Optional[str] = None       # "uniform" | "block"
+    recompute_num_layers: Optional[int] = None
+
+    def __post_init__(self):
+        if self.num_query_groups is None:
+            self.num_query_groups = self.num_attention_heads
+        if self.kv_channels is None:
+            self.kv_channels = self.hidden_size // self.num_attention_heads
+        if self.ffn_hidden_size is None:
+            if self.activation == "swiglu":
+                f = int(8 * self.hidden_size / 3)
+                self.ffn_hidden_size = 256 * ((f + 255) // 256)
+            else:
+                self.ffn_hidden_size = 4 * self.hidden_size
+
+    @property
+    def rms(self) -> bool:
+        return self.normalization.lower() == "rmsnorm"
+
+
+class Norm(nn.Module):
+    """LayerNorm / RMSNorm parameters; the math runs in the fused BDA+norm kernel."""
+
+    def __init__(self, h, cfg: TransformerConfig, device=None):
+        super().__init__()
+        self.rms = cfg.rms
+        self.eps = cfg.layernorm_epsilon
+        # Sequence-parallel activations are sharded across TP: draw their dropout masks from the
+        # per-TP-rank stream; replicated activations use the TP-identical default stream.
+        self.rng_kind = "tp" if cfg.sequence_parallel and ps.get_state().tp > 1 else "default"
+        self.weight = nn.Parameter(torch.ones(h, dtype=cfg.params_dtype, device=device))
+        self.weight.sequence_parallel = cfg.sequence_parallel
+        if not self.rms:
+            self.bias = nn.Parameter(torch.zeros(h, dtype=cfg.params_dtype, device=device))
+            self.bias.sequence_parallel = cfg.sequence_parallel
+        else:
+            self.register_parameter("bias", None)
+
+    def fused(self, x, xbias, residual, p, training):
+        return SF.bias_dropout_add_norm(x, xbias, residual, self.weight, self.bias, p, training, self.eps, self.rms,
+                                        rng=get_rng(self.rng_kind))
+
+    def forward(self, x):
+        return self.fused(x, None, None, 0.0, False)[0]
+
+
+class ParallelAttention(nn.Module):
+    def __init__(self, cfg: TransformerConfig, layer_number: int, device=None):
+        super().__init__()
+        st = ps.get_state()
+        self.cfg = cfg
+        self.layer_number = layer_number
+        tpn = st.tp
+        assert cfg.num_attention_heads % tpn == 0 and cfg.num_query_groups % tpn == 0
+        self.nh = cfg.num_attention_heads // tpn
+        self.nkv = cfg.num_query_groups // tpn
+        self.hd = cfg.kv_channels
+        q_out = cfg.num_attention_heads * self.hd
+        kv_out = cfg.num_query_groups * self.hd
+        std = cfg.init_method_std
+        out_std = std / math.sqrt(2.0 * cfg.num_layers)
+        self.qkv = tp.ColumnParallelLinear(cfg.hidden_size, q_out + 2 * kv_out, bias=cfg.add_bias_linear,
+                                           init_std=std, key=f"layers.{layer_number}.qkv", seed=cfg.seed,
+                                           params_dtype=cfg.params_dtype, device=device,
+                                           sequence_parallel=cfg.sequence_parallel,
+                                           chunks=[q_out, kv_out, kv_out],
+                                           async_tensor_model_parallel_allreduce=cfg.async_tensor_model_parallel_allreduce)
+        self.proj = tp.RowParallelLinear(q_out, cfg.hidden_size, bias=cfg.add_bias_linear, init_std=out_std,
+                                         key=f"layers.{layer_number}.proj", seed=cfg.seed,
+                                         params_dtype=cfg.params_dtype, device=device,
+                                         sequence_parallel=cfg.sequence_parallel, skip_bias_add=True)
+        self.rope = None
+
+    def set_rope(self, cos, sin, rot):
+        self.rope = (cos, sin, rot)
+
+    def core_attention_unfused(self, qkv, training):
+        """Megatron's unfused path: baddbmm -> fused causal softmax (K1) -> dropout -> bmm."""
+        s, b = qkv.shape[0], qkv.shape[1]
+        q, k, v = SF._qkv_views(qkv, self.nh, self.nkv, self.hd, True)  # [b, s, h, d]
+        if self.nkv != self.nh:
+            rep = self.nh // self.nkv
+            k = k.repeat_interleave(rep, dim=2)
+            v = v.repeat_interleave(rep, dim=2)
+        qh = q.permute(0, 2, 1, 3).reshape(b * self.nh, s, self.hd)
+        kh = k.permute(0, 2, 3, 1).reshape(b * self.nh, self.hd, s)
+        vh = v.permute(0, 2, 1, 3).reshape(b * self.nh, s, self.hd)
+        scores = torch.bmm(qh, kh).view(b, self.nh, s, s)
+        probs = SF.scaled_masked_softmax(scores, None, 1.0 / math.sqrt(self.hd), causal=True)
+        if training and self.cfg.attention_dropout > 0:
+            probs = F.dropout(probs, p=self.cfg.attention_dropout, training=True)
+        ctx = torch.bmm(probs.view(b * self.nh, s, s), vh)          # [b*nh, s, d]
+        return ctx.view(b, self.nh, s, self.hd).permute(2, 0, 1, 3).reshape(s, b, self.nh * self.hd)
+
+    def forward(self, x, training=True):
+        qkv = self.qkv(x)                                        # [s, b, (nh + 2 nkv) d]
+        if self.rope is not None:
+            cos, sin, rot = self.rope
+            qkv = _RopeQKV.apply(qkv, cos, sin, rot, self.nh, self.nkv, self.hd)
+        use_flash = (self.cfg.use_flash_attn and (not training or self.cfg.attention_dropout == 0.0))
+        if use_flash:
+            ctx = SF.flash_attention_qkv(qkv, self.nh, self.nkv, self.hd, seq_first=True, causal=True)
+        else:
+            ctx = self.core_attention_unfused(qkv, training)
+        return self.proj(ctx)                                    # (out, bias)
+
+
+class _RopeQKV(torch.autograd.Function):
+    """RoPE on the q and k parts of a fused [s, b, W] QKV buffer (kernel: rope.hip)."""
+
+    @staticmethod
+    def forward(ctx, qkv, cos, sin, rot, nh, nkv, hd):
+        s, b, W = qkv.shape
+        out = qkv.contiguous().clone()
+        flat = out.view(s * b, W)
+        _apply_rope_parts(flat, cos, sin, rot, nh, nkv, hd, b, s, False)
+        ctx.save_for_backward(cos, sin)
+        ctx.cfg = (rot, nh, nkv, hd, b, s)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        cos, sin = ctx.saved_tensors
+        rot, nh, nkv, hd, b, s = ctx.cfg
+        d = g.contiguous().clone()
+        _apply_rope_parts(d.view(s * b, -1), cos, sin, rot, nh, nkv, hd, b, s, True)
+        return d, None, None, None, None, None, None
+
+
+def _apply_rope_parts(flat, cos, sin, rot, nh, nkv, hd, b, s, inverse):
+    q = flat[:, : nh * hd].view(s * b, nh, hd)
+    k = flat[:, nh * hd:(nh + nkv) * hd].view(s * b, nkv, hd)
+    from ..ops import _ext
+    if _ext.use_kernels(flat):
+        C = _ext.ext()
+        C.rope_(q, cos, sin, rot, b, s, inverse)
+        C.rope_(k, cos, sin, rot, b, s, inverse)
+    else:
+        pos = torch.arange(s * b, device=flat.device) // b
+        q.copy_(SF._rope_ref(q, cos.to(flat.device), sin.to(flat.device), rot, pos, inverse))
+        k.copy_(SF._rope_ref(k, cos.to(flat.device), sin.to(flat.device), rot, pos, inverse))
+
+
+class ParallelMLP(nn.Module):
+    def __init__(self, cfg: TransformerConfig, layer_number: int, device=None):
+        super().__init__()
+        self.cfg = cfg
+        f = cfg.ffn_hidden_size
+        std = cfg.init_method_std
+        out_std = std / math.sqrt(2.0 * cfg.num_layers)
+        self.gated = cfg.activation == "swiglu"
+        fc1_out = 2 * f if self.gated else f
+        self.fc1 = tp.ColumnParallelLinear(cfg.hidden_size, fc1_out, bias=cfg.add_bias_linear, init_std=std,
+                                           key=f"layers.{layer_number}.fc1", seed=cfg.seed,
+                                           params_dtype=cfg.params_dtype, device=device,
+                                           sequence_parallel=cfg.sequence_parallel, skip_bias_add=True,
+                                           chunks=[f, f] if self.gated else None,
+                                           async_tensor_model_parallel_allreduce=cfg.async_tensor_model_parallel_allreduce)
+        self.fc2 = tp.RowParallelLinear(f, cfg.hidden_size, bias=cfg.add_bias_linear, init_std=out_std,
+                                        key=f"layers.{layer_number}.fc2", seed=cfg.seed,
+                                        params_dtype=cfg.params_dtype, device=device,
+                                        sequence_parallel=cfg.sequence_parallel, skip_bias_add=True)
+
+    def forward(self, x):
+        h, b = self.fc1(x)
+        act = self.cfg.activation
+        if act in ("gelu", "gelu_erf"):
+            if self.cfg.bias_gelu_fusion:
+                h = SF.bias_gelu(h, b, "tanh" if act == "gelu" else "none")
+            else:
+                h = F.gelu(h + b if b is not None else h, approximate="tanh" if act == "gelu" else "none")
+        elif act == "swiglu":
+            if b is not None:
+                h = h + b
+            h = SF.swiglu(h)
+        elif act == "squared_relu":
+            h = F.relu(h + b if b is not None else h).pow(2)
+        else:
+            raise ValueError(f"unknown activation {act}")
+        return self.fc2(h)
+
+
+class ParallelTransformerLayer(nn.Module):
+    def __init__(self, cfg: TransformerConfig, layer_number: int, device=None):
+        super().__init__()
+        self.cfg = cfg
+        self.layer_number = layer_number
+        self.input_norm = Norm(cfg.hidden_size, cfg, device)
+        self.attention = ParallelAttention(cfg, layer_number, device)
+        self.post_attention_norm = Norm(cfg.hidden_size, cfg, device)
+        self.mlp = ParallelMLP(cfg, layer_number, device)
+
+    def forward(self, x, xbias, residual):
+        training = self.training
+        p = self.cfg.hidden_dropout
+        ln1, residual = self.input_norm.fused(x, xbias, residual, p, training)
+        a, ab = self.attention(ln1, training)
+        ln2, residual = self.post_attention_norm.fused(a, ab, residual, p, training)
+        m, mb = self.mlp(ln2)
+        return m, mb, residual
+
+
+class ParallelTransformer(nn.Module):
+    """A stack of layers [first, first + n) of the full model (pipeline stages own a slice)."""
+
+    def __init__(self, cfg: TransformerConfig, first_layer: int, num_layers: int, post_norm: bool, device=None):
+        super().__init__()
+        self.cfg = cfg
+        self.layers = nn.ModuleList([ParallelTransformerLayer(cfg, first_layer + i, device) for i in range(num_layers)])
+        self.final_norm = Norm(cfg.hidden_size, cfg, device) if post_norm else None
+
+    def _run(self, i, x, xb, res):
+        layer = self.layers[i]
+        cfg = self.cfg
+        if self.training and cfg.recompute_granularity == "full":
+            n = cfg.recompute_num_layers or len(self.layers)
+            if cfg.recompute_method == "block" and i >= n:
+                return layer(x, xb, res)
+            if xb is None:
+                return rng_checkpoint(lambda a, r: layer(a, None, r), x, res)
+            return rng_checkpoint(layer, x, xb, res)
+        return layer(x, xb, res)
+
+    def forward(self, x, xbias=None, residual=None):
+        """Returns (pending_x, pending_bias, residual) or, with ``final_norm``, the normalised
+        output (the pending branch folded into the residual first)."""
+        for i in range(len(self.layers)):
+            x, xbias, residual = self._run(i, x, xbias, residual)
+        if self.final_norm is not None:
+            y, _ = self.final_norm.fused(x, xbias, residual, self.cfg.hidden_dropout, self.training)
+            return y
+        return x, xbias, residual

@@ -1,0 +1,492 @@
+"""Autograd-aware fused ops backed by the gfx950 kernel library.
+
+Every op has two paths:
+  * GPU tensors -> the HIP kernels in ``smdt_amd/_C.so`` (no silent fallback: see ``_ext``);
+  * CPU tensors -> a plain PyTorch reference with identical semantics (tests, gloo runs).
+
+Reference-parity notes: these cover Megatron's fused kernels K1-K6, K12, K15,
+K16 (`megatron/arguments.py:814-854` in /root/reference/3_training_megatron-lm) with the same
+enable/disable flags wired up in ``smdt_amd.models.transformer``.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import torch
+import torch.nn.functional as F
+
+from . import _ext
+
+# --------------------------------------------------------------------------------------------
+# Dropout RNG: stateless Philox (seed, offset) pairs. The forward call records its pair in the
+# autograd context and the backward kernel regenerates the identical mask.
+
+
+class PhiloxState:
+    """Per-process (seed, offset) source for the fused dropout kernels.
+
+    ``offset`` advances by one per kernel call, so successive calls draw independent streams.
+    Tensor-parallel-aware seeding lives in ``smdt_amd.parallel.random``.
+    """
+
+    def __init__(self, seed: int = 1234):
+        self.seed = int(seed)
+        self.offset = 0
+
+    def next(self):
+        self.offset += 1
+        return self.seed, self.offset
+
+    def state_dict(self):
+        return {"seed": self.seed, "offset": self.offset}
+
+    def load_state_dict(self, d):
+        self.seed, self.offset = int(d["seed"]), int(d["offset"])
+
+
+_DEFAULT_RNG = PhiloxState()
+
+
+def default_rng() -> PhiloxState:
+    return _DEFAULT_RNG
+
+
+def _rng(rng: Optional[PhiloxState]) -> PhiloxState:
+    return rng if rng is not None else _DEFAULT_RNG
+
+
+# --------------------------------------------------------------------------------------------
+# Fused (bias + dropout + residual) -> LayerNorm / RMSNorm
+
+
+def _ln_ref(s, gamma, beta, eps, rms):
+    sf = s.float()
+    if rms:
+        y = sf * torch.rsqrt(sf.pow(2).mean(-1, keepdim=True) + eps) * gamma.float()
+    else:
+        y = F.layer_norm(sf, (s.shape[-1],), gamma.float(), None if beta is None else beta.float(), eps)
+    return y.to(s.dtype)
+
+
+class _BDALayerNorm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, bias, residual, gamma, beta, p, eps, rms, seed, offset):
+        C = _ext.ext()
+        y, s, mean, rstd = C.layernorm_fwd(x.contiguous(), None if residual is None else residual.contiguous(),
+                                           bias, gamma, beta, eps, p, seed, offset, rms, True)
+        ctx.save_for_backward(s, gamma, mean, rstd)
+        ctx.cfg = (p, seed, offset, rms, bias is not None, residual is not None, beta is not None,
+                   gamma.dtype, None if bias is None else bias.dtype)
+        return y, s
+
+    @staticmethod
+    def backward(ctx, dy, ds):
+        s, gamma, mean, rstd = ctx.saved_tensors
+        p, seed, offset, rms, has_bias, has_res, has_beta, gdt, bdt = ctx.cfg
+        C = _ext.ext()
+        dy = dy.contiguous()
+        ds = None if ds is None else ds.contiguous()
+        d_s, dx, dgamma, dbeta, dbias = C.layernorm_bwd(dy, ds, s, gamma, mean, rstd, p, seed, offset, rms,
+                                                        True, has_bias)
+        return (dx, dbias.to(bdt) if has_bias else None, d_s if has_res else None,
+                dgamma.to(gdt), dbeta.to(gdt) if has_beta else None, None, None, None, None, None)
+
+
+def bias_dropout_add_norm(x, bias, residual, gamma, beta, p: float, training: bool, eps: float = 1e-5,
+                          rms: bool = False, rng: Optional[PhiloxState] = None):
+    """Returns ``(norm(s), s)`` with ``s = residual + dropout(x + bias)``.
+
+    ``bias``, ``residual`` may be None; ``beta`` is ignored for RMSNorm. This is the
+    residual-stream step of a pre-LN transformer fused with the following LayerNorm.
+    """
+    p = float(p) if training else 0.0
+    if _ext.use_kernels(x):
+        seed, offset = _rng(rng).next() if p > 0 else (0, 0)
+        return _BDALayerNorm.apply(x, bias, residual, gamma, None if rms else beta, p, float(eps), bool(rms),
+                                   int(seed), int(offset))
+    h = x if bias is None else x + bias
+    if p > 0:
+        h = F.dropout(h, p=p, training=True)
+    s = h if residual is None else residual + h
+    if rms:
+        sf = s.float()
+        y = (sf * torch.rsqrt(sf.pow(2).mean(-1, keepdim=True) + eps) * gamma.float()).to(s.dtype)
+    else:
+        y = F.layer_norm(s.float(), (s.shape[-1],), gamma.float(), None if beta is None else beta.float(),
+                         eps).to(s.dtype)
+    return y, s
+
+
+def layer_norm(x, gamma, beta, eps: float = 1e-5):
+    return bias_dropout_add_norm(x, None, None, gamma, beta, 0.0, False, eps, False)[0]
+
+
+def rms_norm(x, gamma, eps: float = 1e-6):
+    return bias_dropout_add_norm(x, None, None, gamma, None, 0.0, False, eps, True)[0]
+
+
+def bias_dropout_add(x, bias, residual, p: float, training: bool):
+    """Unfused residual step (pipeline-stage boundaries only)."""
+    h = x if bias is None else x + bias
+    if training and p > 0:
+        h = F.dropout(h, p=p, training=True)
+    return h if residual is None else residual + h
+
+
+# --------------------------------------------------------------------------------------------
+# bias + GeLU / SwiGLU
+
+_ACT_CODES = {"gelu": 0, "gelu_tanh": 0, "gelu_erf": 1}
+
+
+class _BiasAct(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, bias, act):
+        C = _ext.ext()
+        x = x.contiguous()
+        y = C.bias_act_fwd(x, bias, act)
+        ctx.save_for_backward(x, bias)
+        ctx.act = act
+        ctx.has_bias = bias is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, bias = ctx.saved_tensors
+        C = _ext.ext()
+        dx, dbias = C.bias_act_bwd(dy.contiguous(), x, bias, ctx.act, ctx.has_bias)
+        return dx, (dbias.to(bias.dtype) if ctx.has_bias else None), None
+
+
+def bias_gelu(x, bias=None, approximate: str = "tanh"):
+    """GeLU(x + bias); ``approximate='tanh'`` is Megatron's bias_gelu, 'none' the erf form."""
+    act = 0 if approximate == "tanh" else 1
+    if _ext.use_kernels(x):
+        return _BiasAct.apply(x, bias, act)
+    h = x if bias is None else x + bias
+    return F.gelu(h.float(), approximate="tanh" if act == 0 else "none").to(x.dtype)
+
+
+class _SwiGLU(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        C = _ext.ext()
+        x = x.contiguous()
+        ctx.save_for_backward(x)
+        return C.swiglu_fwd(x)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        return _ext.ext().swiglu_bwd(dy.contiguous(), x)
+
+
+def swiglu(x):
+    """x = [gate | up] on the last dim -> silu(gate) * up."""
+    if _ext.use_kernels(x):
+        return _SwiGLU.apply(x)
+    g, u = x.chunk(2, dim=-1)
+    return (F.silu(g.float()) * u.float()).to(x.dtype)
+
+
+# --------------------------------------------------------------------------------------------
+# Scaled masked softmax (Megatron K1-K3)
+
+
+class _ScaledSoftmax(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, mask, mode, scale):
+        C = _ext.ext()
+        y = C.softmax_fwd(x.contiguous(), mask, mode, scale)
+        ctx.save_for_backward(y)
+        ctx.mode, ctx.scale = mode, scale
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (y,) = ctx.saved_tensors
+        return _ext.ext().softmax_bwd(dy.contiguous(), y, ctx.mode, ctx.scale), None, None, None
+
+
+def scaled_masked_softmax(x, mask=None, scale: float = 1.0, causal: bool = False):
+    """softmax(scale * x) over the last dim of [b, np, sq, sk].
+
+    ``causal`` masks key j > query i (Megatron's upper-triangular mask); otherwise ``mask``
+    ([b, 1, sq, sk] bool, True = masked) is applied if given.
+    """
+    mode = 1 if causal else (2 if mask is not None else 0)
+    if _ext.use_kernels(x) and x.shape[-1] <= 4096 and x.shape[-1] % 8 == 0:
+        m = None
+        if mode == 2:
+            m = mask.expand(x.shape[0], 1, x.shape[2], x.shape[3]).contiguous().to(torch.uint8)
+        return _ScaledSoftmax.apply(x, m, mode, float(scale))
+    xf = x.float() * scale
+    if mode == 1:
+        sq, sk = x.shape[-2], x.shape[-1]
+        cm = torch.ones(sq, sk, dtype=torch.bool, device=x.device).triu(1 + sk - sq)
+        xf = xf.masked_fill(cm, float("-inf"))
+    elif mode == 2:
+        xf = xf.masked_fill(mask, float("-inf"))
+    y = torch.softmax(xf, dim=-1)
+    y = torch.nan_to_num(y, nan=0.0)
+    return y.to(x.dtype)
+
+
+# --------------------------------------------------------------------------------------------
+# Flash attention
+
+
+def _qkv_views(qkv, nh, nkv, hd, seq_first):
+    """[S, B, W] (seq_first) or [B, S, W] fused projection output -> q, k, v as [B, S, H, D]
+    views with W = (nh + 2 nkv) hd laid out as [q heads | k heads | v heads]."""
+    if seq_first:
+        x = qkv.transpose(0, 1)
+    else:
+        x = qkv
+    q = x[..., : nh * hd].unflatten(-1, (nh, hd))
+    k = x[..., nh * hd:(nh + nkv) * hd].unflatten(-1, (nkv, hd))
+    v = x[..., (nh + nkv) * hd:].unflatten(-1, (nkv, hd))
+    return q, k, v
+
+
+class _FlashAttnQKV(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qkv, nh, nkv, hd, seq_first, scale, causal):
+        C = _ext.ext()
+        q, k, v = _qkv_views(qkv, nh, nkv, hd, seq_first)
+        if seq_first:
+            S, B = qkv.shape[0], qkv.shape[1]
+            out = qkv.new_empty(S, B, nh, hd)
+            ov = out.transpose(0, 1)
+        else:
+            B, S = qkv.shape[0], qkv.shape[1]
+            out = qkv.new_empty(B, S, nh, hd)
+            ov = out
+        _, lse = C.flash_fwd(q, k, v, scale, causal, ov)
+        ctx.save_for_backward(qkv, out, lse)
+        ctx.cfg = (nh, nkv, hd, seq_first, scale, causal)
+        return out.flatten(-2)
+
+    @staticmethod
+    def backward(ctx, dout):
+        qkv, out, lse = ctx.saved_tensors
+        nh, nkv, hd, seq_first, scale, causal = ctx.cfg
+        C = _ext.ext()
+        q, k, v = _qkv_views(qkv, nh, nkv, hd, seq_first)
+        dqkv = torch.empty_like(qkv)
+        dq, dk, dv = _qkv_views(dqkv, nh, nkv, hd, seq_first)
+        do = dout.unflatten(-1, (nh, hd))
+        o = out
+        if seq_first:
+            do = do.transpose(0, 1)
+            o = o.transpose(0, 1)
+        C.flash_bwd(q, k, v, o, do, lse, scale, causal, dq, dk, dv)
+        return dqkv, None, None, None, None, None, None
+
+
+class _FlashAttn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, q, k, v, scale, causal):
+        C = _ext.ext()
+        o, lse = C.flash_fwd(q, k, v, scale, causal, None)
+        ctx.save_for_backward(q, k, v, o, lse)
+        ctx.scale, ctx.causal = scale, causal
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        q, k, v, o, lse = ctx.saved_tensors
+        dq, dk, dv = _ext.ext().flash_bwd(q, k, v, o, do, lse, ctx.scale, ctx.causal, None, None, None)
+        return dq, dk, dv, None, None
+
+
+def attention_ref(q, k, v, scale, causal):
+    """Reference attention on [B, S, H, D] (GQA by head repetition), fp32 math."""
+    B, S, H, D = q.shape
+    Hkv = k.shape[2]
+    if Hkv != H:
+        k = k.repeat_interleave(H // Hkv, dim=2)
+        v = v.repeat_interleave(H // Hkv, dim=2)
+    qf, kf, vf = (t.float().transpose(1, 2) for t in (q, k, v))
+    s = torch.matmul(qf, kf.transpose(-1, -2)) * scale
+    if causal:
+        cm = torch.ones(S, S, dtype=torch.bool, device=q.device).triu(1)
+        s = s.masked_fill(cm, float("-inf"))
+    p = torch.softmax(s, dim=-1)
+    o = torch.matmul(p, vf).transpose(1, 2)
+    return o.to(q.dtype)
+
+
+def flash_supported(q, k) -> bool:
+    B, S, H, D = q.shape
+    return (q.dtype == torch.bfloat16 and D in (64, 128) and S % 128 == 0 and H % k.shape[2] == 0
+            and q.stride(-1) == 1 and k.stride(-1) == 1)
+
+
+def flash_attention(q, k, v, scale: Optional[float] = None, causal: bool = True):
+    """Attention over [B, S, H, D] tensors (any batch/seq/head strides, unit last stride);
+    ``k``/``v`` may have fewer heads (GQA)."""
+    if scale is None:
+        scale = 1.0 / math.sqrt(q.shape[-1])
+    if _ext.use_kernels(q) and flash_supported(q, k):
+        return _FlashAttn.apply(q, k, v, float(scale), bool(causal))
+    return attention_ref(q, k, v, scale, causal)
+
+
+def flash_attention_qkv(qkv, nh: int, nkv: int, hd: int, seq_first: bool = True, causal: bool = True,
+                        scale: Optional[float] = None):
+    """Attention straight off a fused QKV projection output.
+
+    ``qkv`` is [S, B, (nh + 2 nkv) hd] (``seq_first``) or [B, S, ...]; returns [S, B, nh hd]
+    (resp. [B, S, nh hd]). Backward produces ONE fused d(qkv) buffer.
+    """
+    if scale is None:
+        scale = 1.0 / math.sqrt(hd)
+    q, k, v = _qkv_views(qkv, nh, nkv, hd, seq_first)
+    if _ext.use_kernels(qkv) and qkv.is_contiguous() and flash_supported(q, k) and (nh + 2 * nkv) * hd % 8 == 0:
+        return _FlashAttnQKV.apply(qkv, nh, nkv, hd, bool(seq_first), float(scale), bool(causal))
+    o = attention_ref(q, k, v, scale, causal)  # [B, S, H, D]
+    if seq_first:
+        o = o.transpose(0, 1)
+    return o.flatten(-2).contiguous()
+# --------------------------------------------------------------------------------------------
+# Rotary embedding
+
+
+def rope_tables(max_pos: int, rot_dim: int, base: float = 10000.0, device=None):
+    inv = 1.0 / (base ** (torch.arange(0, rot_dim, 2, dtype=torch.float64) / rot_dim))
+    t = torch.arange(max_pos, dtype=torch.float64)
+    f = torch.outer(t, inv)
+    return f.cos().float().to(device), f.sin().float().to(device)
+
+
+def _rope_ref(x, cos, sin, rot, pos, inverse=False):
+    # x [ntok, nh, d]; pos [ntok]
+    xr = x[..., :rot].float()
+    x1, x2 = xr[..., : rot // 2], xr[..., rot // 2:]
+    c = cos[pos].unsqueeze(1)
+    s = sin[pos].unsqueeze(1)
+    if inverse:
+        s = -s
+    out = torch.cat([x1 * c - x2 * s, x2 * c + x1 * s], dim=-1).to(x.dtype)
+    return torch.cat([out, x[..., rot:]], dim=-1) if rot < x.shape[-1] else out
+
+
+class _Rope(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, cos, sin, rot, pos_div, pos_mod):
+        y = x.clone()
+        _ext.ext().rope_(y, cos, sin, rot, pos_div, pos_mod, False)
+        ctx.save_for_backward(cos, sin)
+        ctx.cfg = (rot, pos_div, pos_mod)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        cos, sin = ctx.saved_tensors
+        rot, pos_div, pos_mod = ctx.cfg
+        dx = dy.contiguous().clone()
+        _ext.ext().rope_(dx, cos, sin, rot, pos_div, pos_mod, True)
+        return dx, None, None, None, None, None
+
+
+def apply_rope(x, cos, sin, pos_div: int, pos_mod: int, rot: Optional[int] = None):
+    """Rotate-half RoPE on x [ntok, nh, d]; token t has position (t // pos_div) % pos_mod."""
+    rot = rot or x.shape[-1]
+    if _ext.use_kernels(x) and rot % 16 == 0:
+        xx = x if x.stride(-1) == 1 and x.stride(0) % 8 == 0 and x.stride(1) % 8 == 0 else x.contiguous()
+        return _Rope.apply(xx, cos, sin, rot, pos_div, pos_mod)
+    pos = (torch.arange(x.shape[0], device=x.device) // pos_div) % pos_mod
+    return _rope_ref(x, cos.to(x.device), sin.to(x.device), rot, pos)
+
+
+# --------------------------------------------------------------------------------------------
+# (Vocab-parallel) cross entropy
+
+
+class _FusedCE(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, target, vstart, group, ignore_index, inplace_grad):
+        C = _ext.ext()
+        lg = logits.contiguous()
+        t = target.contiguous().view(-1)
+        mx, se, tg = C.ce_stats(lg.view(-1, lg.shape[-1]), t, vstart)
+        if group is not None and torch.distributed.get_world_size(group) > 1:
+            gmax = mx.clone()
+            torch.distributed.all_reduce(gmax, op=torch.distributed.ReduceOp.MAX, group=group)
+            se = se * torch.exp(mx - gmax)
+            torch.distributed.all_reduce(se, group=group)
+            torch.distributed.all_reduce(tg, group=group)
+            mx = gmax
+        loss = torch.log(se) + mx - tg
+        loss = torch.where(t == ignore_index, torch.zeros_like(loss), loss)
+        ctx.save_for_backward(lg, t, mx, se)
+        ctx.cfg = (vstart, ignore_index, inplace_grad)
+        return loss.view(target.shape)
+
+    @staticmethod
+    def backward(ctx, dloss):
+        lg, t, mx, se = ctx.saved_tensors
+        vstart, ignore_index, inplace_grad = ctx.cfg
+        C = _ext.ext()
+        out = lg if inplace_grad else torch.empty_like(lg)
+        C.ce_bwd(lg.view(-1, lg.shape[-1]), t, mx, se, dloss.contiguous().view(-1).float(),
+                 out.view(-1, lg.shape[-1]), vstart, ignore_index)
+        return out, None, None, None, None, None
+
+
+def cross_entropy(logits, target, vocab_start: int = 0, group=None, ignore_index: int = -100,
+                  inplace_grad: bool = False):
+    """Per-token CE loss (fp32) for logits [..., V_local] holding vocab slice
+    [vocab_start, vocab_start + V_local). With ``group`` the logits are vocab-parallel and the
+    three per-row statistics are all-reduced (MAX, SUM, SUM) across it.
+
+    ``inplace_grad=True`` writes dlogits over the logits buffer (saves a [tokens, V] tensor);
+    only valid when nothing else reads the logits after the loss.
+    """
+    if _ext.use_kernels(logits) and logits.shape[-1] % 8 == 0:
+        return _FusedCE.apply(logits, target, int(vocab_start), group, int(ignore_index), bool(inplace_grad))
+    return _ce_ref(logits, target, vocab_start, group, ignore_index)
+
+
+class _CERef(torch.autograd.Function):
+    """Vocab-parallel CE in plain PyTorch (CPU path), same math as the fused kernel."""
+
+    @staticmethod
+    def forward(ctx, logits, target, vstart, group, ignore_index):
+        lf = logits.float()
+        V = lf.shape[-1]
+        mx = lf.max(-1).values
+        ws = 1
+        if group is not None:
+            ws = torch.distributed.get_world_size(group)
+        if ws > 1:
+            torch.distributed.all_reduce(mx, op=torch.distributed.ReduceOp.MAX, group=group)
+        ex = torch.exp(lf - mx.unsqueeze(-1))
+        se = ex.sum(-1)
+        local = target - vstart
+        inr = (local >= 0) & (local < V)
+        idx = local.clamp(0, V - 1)
+        tg = torch.gather(lf, -1, idx.unsqueeze(-1)).squeeze(-1) * inr
+        if ws > 1:
+            torch.distributed.all_reduce(se, group=group)
+            torch.distributed.all_reduce(tg, group=group)
+        loss = torch.log(se) + mx - tg
+        ign = target == ignore_index
+        loss = loss.masked_fill(ign, 0.0)
+        ctx.save_for_backward(ex, se, idx, inr, ign)
+        ctx.dtype = logits.dtype
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        ex, se, idx, inr, ign = ctx.saved_tensors
+        p = ex / se.unsqueeze(-1)
+        oh = torch.zeros_like(p).scatter_(-1, idx.unsqueeze(-1), inr.unsqueeze(-1).float())
+        d = (p - oh) * g.masked_fill(ign, 0.0).unsqueeze(-1)
+        return d.to(ctx.dtype), None, None, None, None
+
+
+def _ce_ref(logits, target, vocab_start, group, ignore_index):
+    return _CERef.apply(logits, target, int(vocab_start), group, int(ignore_index))

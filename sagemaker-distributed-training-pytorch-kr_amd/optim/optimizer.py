@@ -1,0 +1,245 @@
+"""Mixed-precision Adam/AdamW over the DDP flat buffers, with optional ZeRO sharding, grad
+clipping and (dynamic) loss scaling — no host synchronisation inside ``step``.
+
+Covers Megatron's ``Float16OptimizerWithFloat16Params`` + FusedAdam + clip + DynamicGradScaler
+(flags `--optimizer adam --adam-beta1/2 --adam-eps --weight-decay
+--clip-grad --loss-scale --initial-loss-scale --min-loss-scale --loss-scale-window --hysteresis`,
+/root/reference/3_training_megatron-lm/megatron/arguments.py:700-714, :968-979), the distributed
+optimizer (P7, `--use-distributed-optimizer`, :1059-1060) and DeepSpeed ZeRO-1/2 with FusedAdam
+(P8, K10; /root/reference/4_training_alpaca_deepspeed/configs/default_offload_opt_param.json).
+
+State layout: fp32 master weights, exp_avg, exp_avg_sq are flat buffers covering either the
+whole DDP buffer (plain) or only this DP rank's shard of every bucket (ZeRO). Each step runs:
+
+    sumsq (per region, HIP) -> [all-reduce over DP (ZeRO) / TP / PP] -> clip coefficient (device)
+    -> fused Adam per region / bucket shard (reads grad_mul + found_inf from device memory,
+       writes fp32 master AND the bf16 model copy) -> [ZeRO: all-gather bf16 params]
+
+With ZeRO the gradient buffer is reduce-scattered bucket by bucket during backward (stage 2
+style: only the owned shard of each bucket is needed after the collective).
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+from ..ops import _ext
+from ..parallel import state as ps
+from ..parallel.distributed import DistributedDataParallel
+
+
+class DynamicLossScaler:
+    """Megatron's DynamicGradScaler: halve on overflow after ``hysteresis`` hits, grow x2
+    every ``window`` clean steps; state lives on the device (no sync)."""
+
+    def __init__(self, initial_scale=2.0 ** 32, min_scale=1.0, growth_factor=2.0, backoff_factor=0.5,
+                 growth_interval=1000, hysteresis=2, device=None):
+        self.scale = torch.tensor([float(initial_scale)], dtype=torch.float32, device=device)
+        self.min_scale = float(min_scale)
+        self.growth_factor, self.backoff_factor = growth_factor, backoff_factor
+        self.growth_interval = int(growth_interval)
+        self.hysteresis = int(hysteresis)
+        self._hyst = torch.tensor([self.hysteresis], dtype=torch.int32, device=device)
+        self._growth = torch.tensor([0], dtype=torch.int32, device=device)
+
+    def update(self, found_inf):
+        inf = found_inf.bool()
+        self._hyst = torch.where(inf, self._hyst - 1, self._hyst)
+        shrink = inf & (self._hyst <= 0)
+        self.scale = torch.where(shrink, torch.clamp(self.scale * self.backoff_factor, min=self.min_scale), self.scale)
+        self._growth = torch.where(inf, torch.zeros_like(self._growth), self._growth + 1)
+        grow = self._growth >= self.growth_interval
+        self.scale = torch.where(grow, self.scale * self.growth_factor, self.scale)
+        self._growth = torch.where(grow, torch.zeros_like(self._growth), self._growth)
+        self._hyst = torch.where(grow, torch.full_like(self._hyst, self.hysteresis), self._hyst)
+
+    def state_dict(self):
+        return {"scale": self.scale.cpu(), "hyst": self._hyst.cpu(), "growth": self._growth.cpu()}
+
+    def load_state_dict(self, d):
+        dev = self.scale.device
+        self.scale = d["scale"].to(dev)
+        self._hyst = d["hyst"].to(dev)
+        self._growth = d["growth"].to(dev)
+
+
+class ConstantLossScaler:
+    def __init__(self, scale=1.0, device=None):
+        self.scale = torch.tensor([float(scale)], dtype=torch.float32, device=device)
+
+    def update(self, found_inf):
+        pass
+
+    def state_dict(self):
+        return {"scale": self.scale.cpu()}
+
+    def load_state_dict(self, d):
+        self.scale = d["scale"].to(self.scale.device)
+
+
+class MixedPrecisionAdam:
+    def __init__(self, ddp: DistributedDataParallel, lr: float = 1e-4, betas=(0.9, 0.999), eps: float = 1e-8,
+                 weight_decay: float = 0.0, adamw: bool = True, clip_grad: float = 0.0,
+                 loss_scaler=None, use_distributed_optimizer: Optional[bool] = None):
+        self.ddp = ddp
+        self.lr = lr
+        self.beta1, self.beta2 = betas
+        self.eps = eps
+        self.weight_decay = weight_decay
+        self.adamw = adamw
+        self.clip_grad = clip_grad
+        self.zero = ddp.zero if use_distributed_optimizer is None else use_distributed_optimizer
+        if self.zero and not ddp.zero:
+            raise ValueError("ZeRO optimizer needs DistributedDataParallel(use_distributed_optimizer=True)")
+        self.scaler = loss_scaler
+        self.step_count = 0
+        dev = ddp.param_data.device
+        self.device = dev
+        # (start, end) pieces of the flat buffers this rank updates, with their region keys.
+        self.pieces = []
+        if self.zero:
+            for b in ddp.buckets:
+                s, e = ddp.shard_range(b)
+                self.pieces.append((s, e, b.region))
+        else:
+            for key, (s, e) in ddp.regions.items():
+                self.pieces.append((s, e, key))
+        n = sum(e - s for s, e, _ in self.pieces)
+        self.master = torch.empty(n, dtype=torch.float32, device=dev)
+        self.exp_avg = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.exp_avg_sq = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.master_off = []
+        o = 0
+        with torch.no_grad():
+            for s, e, _ in self.pieces:
+                self.master[o:o + (e - s)].copy_(ddp.param_data[s:e].float())
+                self.master_off.append(o)
+                o += e - s
+        self.param_is_fp32 = ddp.param_data.dtype == torch.float32
+        self.found_inf = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.grad_norm = torch.zeros(1, dtype=torch.float32, device=dev)
+        self.param_groups = [{"lr": lr, "weight_decay": weight_decay}]
+
+    # ------------------------------------------------------------------ helpers
+    def _norm_groups(self):
+        st = ps.get_state()
+        groups = []
+        if self.zero and self.ddp.dp > 1:
+            groups.append(self.ddp.dp_group)
+        if st.mp_group is not None and (st.tp > 1 or st.pp > 1):
+            groups.append(st.mp_group)
+        return groups
+
+    def _sumsq(self, x):
+        if _ext.use_kernels(x):
+            return _ext.ext().sumsq(x, self.found_inf)
+        xf = x.float()
+        if not torch.isfinite(xf).all():
+            self.found_inf.fill_(1)
+        return (xf * xf).sum().view(1)
+
+    @torch.no_grad()
+    def step(self, lr: Optional[float] = None):
+        """One optimizer step over the reduced gradients. Returns the device grad-norm tensor."""
+        if lr is not None:
+            self.lr = lr
+        self.param_groups[0]["lr"] = self.lr
+        ddp = self.ddp
+        g = ddp.grad_data
+        self.found_inf.zero_()
+        total = torch.zeros(1, dtype=torch.float32, device=self.device)
+        for s, e, key in self.pieces:
+            if key[1] and e > s:                        # counts toward the norm on this rank
+                total += self._sumsq(g[s:e])
+            elif e > s and self.scaler is not None:   # still check for inf/nan
+                self._sumsq(g[s:e])
+        for grp in self._norm_groups():
+            dist.all_reduce(total, group=grp)
+            dist.all_reduce(self.found_inf, op=dist.ReduceOp.MAX, group=grp)
+        inv_scale = 1.0
+        scale_t = None
+        if self.scaler is not None:
+            scale_t = self.scaler.scale
+        use_k = _ext.use_kernels(g)
+        if use_k:
+            mul, norm = _ext.ext().clip_coef(total, float(self.clip_grad), 1.0)
+            if scale_t is not None:
+                mul = mul / scale_t
+                norm = norm / scale_t
+                if self.clip_grad > 0:
+                    # clip coefficient must use the unscaled norm
+                    coef = torch.clamp(self.clip_grad / (norm + 1e-6), max=1.0)
+                    mul = coef / scale_t
+        else:
+            norm = torch.sqrt(total)
+            if scale_t is not None:
+                norm = norm / scale_t
+            coef = torch.clamp(self.clip_grad / (norm + 1e-6), max=1.0) if self.clip_grad > 0 else torch.ones_like(norm)
+            mul = coef / (scale_t if scale_t is not None else 1.0)
+        self.grad_norm = norm
+        self.step_count += 1
+        t = self.step_count
+        bc1 = 1 - self.beta1 ** t
+        bc2 = 1 - self.beta2 ** t
+        for (s, e, key), mo in zip(self.pieces, self.master_off):
+            if e <= s:
+                continue
+            n = e - s
+            wd = self.weight_decay if key[0] else 0.0
+            mst, m, v = self.master[mo:mo + n], self.exp_avg[mo:mo + n], self.exp_avg_sq[mo:mo + n]
+            gr = g[s:e]
+            if gr.dtype != torch.float32:
+                gr = gr.float()
+            if use_k:
+                model_out = None if self.param_is_fp32 else ddp.param_data[s:e]
+                _ext.ext().adam(mst, gr, m, v, model_out, self.lr, self.beta1, self.beta2, self.eps, wd, t,
+                                self.adamw, mul, self.found_inf)
+                if self.param_is_fp32:
+                    ddp.param_data[s:e].copy_(mst)
+            else:
+                ok = (self.found_inf == 0).float()
+                gg = gr * mul
+                if not self.adamw and wd:
+                    gg = gg + wd * mst
+                m.mul_(1 - (1 - self.beta1) * ok).add_(gg * ((1 - self.beta1) * ok))
+                v.mul_(1 - (1 - self.beta2) * ok).add_(gg * gg * ((1 - self.beta2) * ok))
+                denom = v.sqrt() / math.sqrt(bc2) + self.eps
+                upd = (m / bc1) / denom
+                if self.adamw and wd:
+                    upd = upd + wd * mst
+                mst.sub_(self.lr * upd * ok)
+                ddp.param_data[s:e].copy_(mst.to(ddp.param_data.dtype))
+        if self.scaler is not None:
+            self.scaler.update(self.found_inf)
+        if self.zero:
+            ddp.all_gather_params()
+        return self.grad_norm
+
+    def zero_grad(self, set_to_none=True):
+        self.ddp.zero_grad_buffer()
+
+    # ------------------------------------------------------------------ checkpoint
+    def state_dict(self):
+        d = {"step": self.step_count, "master": self.master, "exp_avg": self.exp_avg,
+             "exp_avg_sq": self.exp_avg_sq, "lr": self.lr, "zero": self.zero,
+             "pieces": [(s, e) for s, e, _ in self.pieces]}
+        if self.scaler is not None:
+            d["scaler"] = self.scaler.state_dict()
+        return d
+
+    def load_state_dict(self, d):
+        self.step_count = int(d["step"])
+        self.master.copy_(d["master"])
+        self.exp_avg.copy_(d["exp_avg"])
+        self.exp_avg_sq.copy_(d["exp_avg_sq"])
+        self.lr = d.get("lr", self.lr)
+        if self.scaler is not None and "scaler" in d:
+            self.scaler.load_state_dict(d["scaler"])
+        with torch.no_grad():
+            for (s, e, _), mo in zip(self.pieces, self.master_off):
+                self.ddp.param_data[s:e].copy_(self.master[mo:mo + (e - s)].to(self.ddp.param_data.dtype))
+        if self.zero:
+            self.ddp.all_gather_params()

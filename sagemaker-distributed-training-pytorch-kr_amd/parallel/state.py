@@ -1,0 +1,195 @@
+"""Process-group topology: tensor / pipeline / data / model-parallel / embedding groups.
+
+MI355X-native equivalent of Megatron's ``megatron.core.parallel_state`` (the
+reference's log shows rank 0 creating world/TP/PP/DP/MP communicators, NB3:1214, and
+`megatron/data/gpt_dataset.py:462-469` all-reduces over the DP and PP groups).
+
+Rank layout (identical to Megatron so checkpoints and logs line up): TP is the fastest-varying
+dimension, then DP, then PP.  world = tp * dp * pp.
+
+    tp group : consecutive ranks                     e.g. TP2 PP2 DP2 -> {0,1} {2,3} {4,5} {6,7}
+    dp group : same (pp stage, tp rank)                                  {0,2} {1,3} {4,6} {5,7}
+    pp group : stride world/pp                                           {0,4} {1,5} {2,6} {3,7}
+
+On one MI355X node every GPU pair has its own xGMI link (fully connected, no switch), so the
+layout does not change link contention; it is kept for compatibility.
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass, field
+from typing import List, Optional
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class ParallelState:
+    tp: int = 1
+    pp: int = 1
+    dp: int = 1
+    rank: int = 0
+    world: int = 1
+    tp_group: object = None
+    pp_group: object = None
+    dp_group: object = None
+    mp_group: object = None          # tp x pp (model-parallel)
+    embd_group: object = None        # first + last pipeline stage (tied embeddings)
+    tp_ranks: List[int] = field(default_factory=list)
+    pp_ranks: List[int] = field(default_factory=list)
+    dp_ranks: List[int] = field(default_factory=list)
+    embd_ranks: List[int] = field(default_factory=list)
+    virtual_pp: Optional[int] = None
+    virtual_pp_rank: int = 0
+
+    # ---- ranks inside groups
+    @property
+    def tp_rank(self) -> int:
+        return self.tp_ranks.index(self.rank) if self.tp_ranks else 0
+
+    @property
+    def pp_rank(self) -> int:
+        return self.pp_ranks.index(self.rank) if self.pp_ranks else 0
+
+    @property
+    def dp_rank(self) -> int:
+        return self.dp_ranks.index(self.rank) if self.dp_ranks else 0
+
+    def is_first_stage(self, ignore_virtual: bool = False) -> bool:
+        if not ignore_virtual and self.virtual_pp is not None and self.virtual_pp_rank != 0:
+            return False
+        return self.pp_rank == 0
+
+    def is_last_stage(self, ignore_virtual: bool = False) -> bool:
+        if not ignore_virtual and self.virtual_pp is not None and self.virtual_pp_rank != self.virtual_pp - 1:
+            return False
+        return self.pp_rank == self.pp - 1
+
+    @property
+    def next_pp_rank(self) -> int:
+        return self.pp_ranks[(self.pp_rank + 1) % self.pp]
+
+    @property
+    def prev_pp_rank(self) -> int:
+        return self.pp_ranks[(self.pp_rank - 1) % self.pp]
+
+
+_STATE: Optional[ParallelState] = None
+
+
+def _new_group(ranks, backend=None):
+    if len(ranks) == 1 and dist.get_world_size() > 1:
+        # Single-rank groups are still created so every rank calls new_group identically.
+        return dist.new_group(ranks, backend=backend)
+    return dist.new_group(ranks, backend=backend)
+
+
+def initialize_model_parallel(tensor_model_parallel_size: int = 1, pipeline_model_parallel_size: int = 1,
+                              virtual_pipeline_model_parallel_size: Optional[int] = None) -> ParallelState:
+    """Create every group. Must be called on all ranks after ``init_process_group``."""
+    global _STATE
+    tp, pp = int(tensor_model_parallel_size), int(pipeline_model_parallel_size)
+    if not dist.is_initialized():
+        _STATE = ParallelState(tp=1, pp=1, dp=1, rank=0, world=1, tp_ranks=[0], pp_ranks=[0], dp_ranks=[0],
+                               embd_ranks=[0])
+        if tp != 1 or pp != 1:
+            raise RuntimeError("model parallelism requires torch.distributed to be initialised")
+        return _STATE
+    world, rank = dist.get_world_size(), dist.get_rank()
+    if world % (tp * pp) != 0:
+        raise RuntimeError(f"world size {world} not divisible by tp({tp}) * pp({pp})")
+    dp = world // (tp * pp)
+    st = ParallelState(tp=tp, pp=pp, dp=dp, rank=rank, world=world, virtual_pp=virtual_pipeline_model_parallel_size)
+    stage = world // pp
+    # data-parallel groups
+    for p in range(pp):
+        for t in range(tp):
+            ranks = [p * stage + d * tp + t for d in range(dp)]
+            g = _new_group(ranks)
+            if rank in ranks:
+                st.dp_group, st.dp_ranks = g, ranks
+    # tensor-parallel groups
+    for i in range(world // tp):
+        ranks = list(range(i * tp, (i + 1) * tp))
+        g = _new_group(ranks)
+        if rank in ranks:
+            st.tp_group, st.tp_ranks = g, ranks
+    # model-parallel (tp x pp) groups: same dp index
+    for d in range(dp):
+        ranks = [p * stage + d * tp + t for p in range(pp) for t in range(tp)]
+        g = _new_group(sorted(ranks))
+        if rank in ranks:
+            st.mp_group = g
+    # pipeline groups + embedding groups
+    for i in range(stage):
+        ranks = list(range(i, world, stage))
+        g = _new_group(ranks)
+        if rank in ranks:
+            st.pp_group, st.pp_ranks = g, ranks
+        embd = [ranks[0], ranks[-1]] if len(ranks) > 1 else [ranks[0]]
+        ge = _new_group(embd)
+        if rank in embd:
+            st.embd_group, st.embd_ranks = ge, embd
+    _STATE = st
+    return st
+
+
+def get_state() -> ParallelState:
+    global _STATE
+    if _STATE is None:
+        _STATE = ParallelState(tp_ranks=[0], pp_ranks=[0], dp_ranks=[0], embd_ranks=[0])
+    return _STATE
+
+
+def destroy_model_parallel():
+    global _STATE
+    _STATE = None
+
+
+# Megatron-style accessors -------------------------------------------------------------------
+
+def get_tensor_model_parallel_world_size() -> int:
+    return get_state().tp
+
+
+def get_tensor_model_parallel_rank() -> int:
+    return get_state().tp_rank
+
+
+def get_tensor_model_parallel_group():
+    return get_state().tp_group
+
+
+def get_pipeline_model_parallel_world_size() -> int:
+    return get_state().pp
+
+
+def get_pipeline_model_parallel_rank() -> int:
+    return get_state().pp_rank
+
+
+def get_data_parallel_world_size() -> int:
+    return get_state().dp
+
+
+def get_data_parallel_rank() -> int:
+    return get_state().dp_rank
+
+
+def get_data_parallel_group():
+    return get_state().dp_group
+
+
+def env_rank_info():
+    """(rank, local_rank, world_size) from torchrun or the OMPI_COMM_WORLD_* contract
+    (the reference's `pretrain_gpt.py:10-13` remaps OMPI -> torch env vars)."""
+    def first(*names, default=None):
+        for n in names:
+            if n in os.environ:
+                return int(os.environ[n])
+        return default
+    rank = first("RANK", "OMPI_COMM_WORLD_RANK", default=0)
+    local = first("LOCAL_RANK", "OMPI_COMM_WORLD_LOCAL_RANK", default=0)
+    world = first("WORLD_SIZE", "OMPI_COMM_WORLD_SIZE", default=1)
+    return rank, local, world

@@ -1,0 +1,437 @@
+"""Megatron-style tensor and sequence parallelism over RCCL.
+
+Equivalent of ``megatron.core.tensor_parallel`` as exercised by the reference recipe (SURVEY P4,
+P6, K7, K13, U4: Column/RowParallelLinear, VocabParallelEmbedding, broadcast_data, the async
+TP all-reduce `megatron/arguments.py:837-842`, sequence parallelism `:848-849` and gradient
+accumulation fusion `:850-854` in /root/reference/3_training_megatron-lm).
+
+Design notes (MI355X-first):
+  * Weight gradients are accumulated straight into the fp32 ``param.main_grad`` view of the
+    contiguous DDP buffer (K7), after which the layer tells the DDP reducer the parameter is
+    ready, so the bucket's RCCL all-reduce / reduce-scatter launches while backward continues.
+  * The input-gradient collective (TP all-reduce, or the SP reduce-scatter) is issued
+    asynchronously and overlapped with the weight-gradient GEMM.
+  * Weights are initialised from a TP-invariant generator (full tensor, then this rank's shard)
+    so a TP=k model starts bit-identical to the TP=1 model: this is what the parallel-equivalence
+    tests rely on.
+"""
+from __future__ import annotations
+
+import hashlib
+import math
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import state as ps
+
+# --------------------------------------------------------------------------------------------
+# collectives helpers
+
+
+def _tp_size():
+    return ps.get_state().tp
+
+
+def _tp_group():
+    return ps.get_state().tp_group
+
+
+def _all_reduce(x, group, async_op=False):
+    if dist.get_world_size(group) == 1:
+        return None
+    return dist.all_reduce(x, group=group, async_op=async_op)
+
+
+def _gather_dim0(x, group):
+    ws = dist.get_world_size(group)
+    if ws == 1:
+        return x
+    out = torch.empty((x.shape[0] * ws,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+    dist.all_gather_into_tensor(out, x.contiguous(), group=group)
+    return out
+
+
+def _reduce_scatter_dim0(x, group, async_op=False):
+    ws = dist.get_world_size(group)
+    if ws == 1:
+        return x, None
+    assert x.shape[0] % ws == 0, "sequence length must divide the TP size"
+    out = torch.empty((x.shape[0] // ws,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+    h = dist.reduce_scatter_tensor(out, x.contiguous(), group=group, async_op=async_op)
+    return out, h
+
+
+def _split_dim(x, dim, group):
+    ws = dist.get_world_size(group)
+    if ws == 1:
+        return x
+    r = dist.get_rank(group)
+    return x.chunk(ws, dim=dim)[r].contiguous()
+
+
+def _gather_dim(x, dim, group):
+    ws = dist.get_world_size(group)
+    if ws == 1:
+        return x
+    if dim == 0:
+        return _gather_dim0(x, group)
+    parts = [torch.empty_like(x) for _ in range(ws)]
+    dist.all_gather(parts, x.contiguous(), group=group)
+    return torch.cat(parts, dim=dim)
+
+
+class _CopyToTP(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        return x
+
+    @staticmethod
+    def backward(ctx, g):
+        g = g.contiguous()
+        _all_reduce(g, _tp_group())
+        return g
+
+
+class _ReduceFromTP(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        x = x.contiguous()
+        _all_reduce(x, _tp_group())
+        return x
+
+    @staticmethod
+    def backward(ctx, g):
+        return g
+
+
+class _ScatterToTP(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        return _split_dim(x, -1, _tp_group())
+
+    @staticmethod
+    def backward(ctx, g):
+        return _gather_dim(g, -1, _tp_group())
+
+
+class _GatherFromTP(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        return _gather_dim(x, -1, _tp_group())
+
+    @staticmethod
+    def backward(ctx, g):
+        return _split_dim(g, -1, _tp_group())
+
+
+class _ScatterToSP(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        return _split_dim(x, 0, _tp_group())
+
+    @staticmethod
+    def backward(ctx, g):
+        return _gather_dim0(g, _tp_group())
+
+
+class _GatherFromSP(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, tp_output_grad):
+        ctx.tp_output_grad = tp_output_grad
+        return _gather_dim0(x, _tp_group())
+
+    @staticmethod
+    def backward(ctx, g):
+        if ctx.tp_output_grad:
+            return _reduce_scatter_dim0(g, _tp_group())[0], None
+        return _split_dim(g, 0, _tp_group()), None
+
+
+class _ReduceScatterToSP(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        return _reduce_scatter_dim0(x, _tp_group())[0]
+
+    @staticmethod
+    def backward(ctx, g):
+        return _gather_dim0(g, _tp_group())
+
+
+def copy_to_tensor_model_parallel_region(x):
+    return _CopyToTP.apply(x) if _tp_size() > 1 else x
+
+
+def reduce_from_tensor_model_parallel_region(x):
+    return _ReduceFromTP.apply(x) if _tp_size() > 1 else x
+
+
+def scatter_to_tensor_model_parallel_region(x):
+    return _ScatterToTP.apply(x) if _tp_size() > 1 else x
+
+
+def gather_from_tensor_model_parallel_region(x):
+    return _GatherFromTP.apply(x) if _tp_size() > 1 else x
+
+
+def scatter_to_sequence_parallel_region(x):
+    return _ScatterToSP.apply(x) if _tp_size() > 1 else x
+
+
+def gather_from_sequence_parallel_region(x, tensor_parallel_output_grad=True):
+    return _GatherFromSP.apply(x, tensor_parallel_output_grad) if _tp_size() > 1 else x
+
+
+def reduce_scatter_to_sequence_parallel_region(x):
+    return _ReduceScatterToSP.apply(x) if _tp_size() > 1 else x
+
+
+# --------------------------------------------------------------------------------------------
+# Linear with async grad communication + fused fp32 wgrad accumulation (K7)
+
+
+def _accumulate_wgrad(weight, dw):
+    mg = getattr(weight, "main_grad", None)
+    if mg is None:
+        return dw
+    if dw is not None:
+        mg.add_(dw.view_as(mg))
+    cb = getattr(weight, "_smdt_grad_ready", None)
+    if cb is not None:
+        cb(weight)
+    return None
+
+
+class LinearWithGradAccumulationAndAsyncCommunication(torch.autograd.Function):
+    """y = x W^T (+ b) with Megatron's backward schedule:
+
+    dgrad GEMM -> launch (async) TP all-reduce or SP reduce-scatter of dgrad -> wgrad GEMM into
+    fp32 main_grad -> wait. With ``sequence_parallel`` the input is all-gathered along the
+    sequence dim in forward (and re-gathered in backward, saving memory).
+    """
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, sequence_parallel, async_grad_allreduce):
+        ctx.sp = sequence_parallel
+        ctx.async_ar = async_grad_allreduce
+        ctx.has_bias = bias is not None
+        ctx.save_for_backward(x, weight)
+        total = _gather_dim0(x, _tp_group()) if sequence_parallel else x
+        return F.linear(total, weight, bias)
+
+    @staticmethod
+    def backward(ctx, g):
+        x, weight = ctx.saved_tensors
+        group = _tp_group()
+        tp = dist.get_world_size(group) if group is not None else 1
+        total = _gather_dim0(x, group) if (ctx.sp and tp > 1) else x
+        g = g.contiguous()
+        gi = g.matmul(weight)
+        handle = None
+        if ctx.sp and tp > 1:
+            gi_out, handle = _reduce_scatter_dim0(gi, group, async_op=True)
+        else:
+            gi_out = gi
+            if ctx.async_ar and tp > 1:
+                handle = dist.all_reduce(gi_out, group=group, async_op=True)
+        g2 = g.reshape(-1, g.shape[-1])
+        t2 = total.reshape(-1, total.shape[-1])
+        dw = g2.t().matmul(t2)
+        dw = _accumulate_wgrad(weight, dw)
+        db = g2.sum(0) if ctx.has_bias else None
+        if handle is not None:
+            handle.wait()
+        return gi_out, dw, db, None, None
+
+
+def linear_with_grad_accumulation_and_async_allreduce(x, weight, bias, sequence_parallel=False,
+                                                      async_grad_allreduce=False):
+    return LinearWithGradAccumulationAndAsyncCommunication.apply(x, weight, bias, sequence_parallel,
+                                                                 async_grad_allreduce)
+
+
+# --------------------------------------------------------------------------------------------
+# TP-invariant initialisation
+
+
+def _key_seed(base_seed: int, key: str) -> int:
+    h = hashlib.sha1(f"{base_seed}:{key}".encode()).digest()
+    return int.from_bytes(h[:8], "little") & ((1 << 62) - 1)
+
+
+@torch.no_grad()
+def init_full_then_shard(shape, std: float, key: str, base_seed: int, dtype, device, shard_dim: Optional[int],
+                         rank: int, world: int, chunks=None):
+    """Normal(0, std) init of the FULL tensor from a deterministic generator, then return this
+    rank's shard along ``shard_dim``. ``chunks`` (a list of sizes along shard_dim) shards each
+    chunk separately (fused QKV / gate-up weights keep per-rank [q|k|v] groups)."""
+    dev = torch.device(device) if device is not None else torch.device("cpu")
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(_key_seed(base_seed, key))
+    full = torch.empty(shape, dtype=torch.float32, device=dev)
+    if std == 0:
+        full.zero_()
+    else:
+        full.normal_(0.0, std, generator=gen)
+    if shard_dim is None or world == 1:
+        return full.to(dtype)
+    if chunks is None:
+        return full.chunk(world, dim=shard_dim)[rank].contiguous().to(dtype)
+    parts = torch.split(full, chunks, dim=shard_dim)
+    return torch.cat([p.chunk(world, dim=shard_dim)[rank] for p in parts], dim=shard_dim).contiguous().to(dtype)
+
+
+class ColumnParallelLinear(nn.Module):
+    """Y = X A with A split along its output dim: rank holds A[:, rank-slice]."""
+
+    def __init__(self, input_size, output_size, bias=True, gather_output=False, init_std=0.02, key="col",
+                 seed=1234, params_dtype=torch.float32, device=None, sequence_parallel=False,
+                 skip_bias_add=False, chunks=None, async_tensor_model_parallel_allreduce=True):
+        super().__init__()
+        st = ps.get_state()
+        self.tp, self.rank = st.tp, st.tp_rank
+        assert output_size % self.tp == 0, f"{output_size} not divisible by TP {self.tp}"
+        self.input_size, self.output_size = input_size, output_size
+        self.out_local = output_size // self.tp
+        self.gather_output = gather_output
+        self.sequence_parallel = sequence_parallel and self.tp > 1
+        self.skip_bias_add = skip_bias_add
+        self.async_ar = async_tensor_model_parallel_allreduce and self.tp > 1 and not self.sequence_parallel
+        w = init_full_then_shard((output_size, input_size), init_std, key + ".weight", seed, params_dtype, device, 0,
+                                 self.rank, self.tp, chunks)
+        self.weight = nn.Parameter(w)
+        self.weight.tensor_model_parallel = True
+        self.weight.partition_dim = 0
+        if bias:
+            self.bias = nn.Parameter(torch.zeros(self.out_local, dtype=params_dtype, device=device))
+            self.bias.tensor_model_parallel = True
+            self.bias.partition_dim = 0
+        else:
+            self.register_parameter("bias", None)
+
+    def forward(self, x):
+        if not (self.async_ar or self.sequence_parallel):
+            x = copy_to_tensor_model_parallel_region(x)
+        b = None if self.skip_bias_add else self.bias
+        y = linear_with_grad_accumulation_and_async_allreduce(x, self.weight, b, self.sequence_parallel,
+                                                              self.async_ar)
+        if self.gather_output:
+            y = gather_from_tensor_model_parallel_region(y)
+        return (y, self.bias) if self.skip_bias_add else y
+
+
+class RowParallelLinear(nn.Module):
+    """Y = X A with A split along its input dim; partial outputs are all-reduced (or
+    reduce-scattered along the sequence with sequence parallelism)."""
+
+    def __init__(self, input_size, output_size, bias=True, input_is_parallel=True, init_std=0.02, key="row",
+                 seed=1234, params_dtype=torch.float32, device=None, sequence_parallel=False,
+                 skip_bias_add=False):
+        super().__init__()
+        st = ps.get_state()
+        self.tp, self.rank = st.tp, st.tp_rank
+        assert input_size % self.tp == 0
+        self.input_size, self.output_size = input_size, output_size
+        self.in_local = input_size // self.tp
+        self.input_is_parallel = input_is_parallel
+        self.sequence_parallel = sequence_parallel and self.tp > 1
+        self.skip_bias_add = skip_bias_add
+        w = init_full_then_shard((output_size, input_size), init_std, key + ".weight", seed, params_dtype, device, 1,
+                                 self.rank, self.tp)
+        self.weight = nn.Parameter(w)
+        self.weight.tensor_model_parallel = True
+        self.weight.partition_dim = 1
+        if bias:
+            self.bias = nn.Parameter(torch.zeros(output_size, dtype=params_dtype, device=device))
+            self.bias.sequence_parallel = self.sequence_parallel
+        else:
+            self.register_parameter("bias", None)
+
+    def forward(self, x):
+        if not self.input_is_parallel:
+            x = scatter_to_tensor_model_parallel_region(x)
+        y = linear_with_grad_accumulation_and_async_allreduce(x, self.weight, None, False, False)
+        if self.sequence_parallel:
+            y = reduce_scatter_to_sequence_parallel_region(y)
+        else:
+            y = reduce_from_tensor_model_parallel_region(y)
+        if self.skip_bias_add:
+            return y, self.bias
+        return y + self.bias if self.bias is not None else y
+
+
+class VocabParallelEmbedding(nn.Module):
+    """Embedding table split along the vocab dim; out-of-range rows contribute zeros and the
+    partial lookups are summed across TP (all-reduce, or reduce-scatter with SP)."""
+
+    def __init__(self, num_embeddings, embedding_dim, init_std=0.02, key="embedding", seed=1234,
+                 params_dtype=torch.float32, device=None):
+        super().__init__()
+        st = ps.get_state()
+        self.tp, self.rank = st.tp, st.tp_rank
+        assert num_embeddings % self.tp == 0, "pad the vocab to a multiple of TP (make-vocab-size-divisible-by)"
+        self.num_embeddings = num_embeddings
+        self.per = num_embeddings // self.tp
+        self.vocab_start = self.rank * self.per
+        self.vocab_end = self.vocab_start + self.per
+        w = init_full_then_shard((num_embeddings, embedding_dim), init_std, key + ".weight", seed, params_dtype,
+                                 device, 0, self.rank, self.tp)
+        self.weight = nn.Parameter(w)
+        self.weight.tensor_model_parallel = True
+        self.weight.partition_dim = 0
+
+    def forward(self, ids, reduce=True):
+        if self.tp > 1:
+            mask = (ids < self.vocab_start) | (ids >= self.vocab_end)
+            local = (ids - self.vocab_start).masked_fill(mask, 0)
+            out = F.embedding(local, self.weight)
+            out = out.masked_fill(mask.unsqueeze(-1), 0.0)
+            if reduce:
+                out = reduce_from_tensor_model_parallel_region(out)
+            return out
+        return F.embedding(ids, self.weight)
+
+
+# --------------------------------------------------------------------------------------------
+# data broadcast within TP (U4)
+
+
+def broadcast_data(keys, data, datatype, src_rank=None):
+    """Broadcast {key: int tensor} from TP rank 0 to the TP group (sizes first, then a flat
+    buffer), like Megatron's ``tensor_parallel.broadcast_data`` (`pretrain_gpt.py:75`)."""
+    st = ps.get_state()
+    if st.tp == 1 or st.tp_group is None:
+        return {k: data[k].to(datatype) for k in keys}
+    src = st.tp_ranks[0] if src_rank is None else src_rank
+    dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
+    if st.tp_rank == 0:
+        sizes = []
+        for k in keys:
+            s = list(data[k].shape)
+            sizes.append(len(s))
+            sizes += s
+        sz = torch.tensor(sizes + [0] * (32 * len(keys) - len(sizes)), dtype=torch.long, device=dev)
+    else:
+        sz = torch.zeros(32 * len(keys), dtype=torch.long, device=dev)
+    dist.broadcast(sz, src, group=st.tp_group)
+    shapes, i = [], 0
+    szl = sz.tolist()
+    for _ in keys:
+        nd = szl[i]
+        shapes.append(szl[i + 1:i + 1 + nd])
+        i += 1 + nd
+    total = sum(math.prod(s) for s in shapes)
+    if st.tp_rank == 0:
+        flat = torch.cat([data[k].to(dev).contiguous().view(-1).to(datatype) for k in keys])
+    else:
+        flat = torch.empty(total, dtype=datatype, device=dev)
+    dist.broadcast(flat, src, group=st.tp_group)
+    out, off = {}, 0
+    for k, s in zip(keys, shapes):
+        n = math.prod(s)
+        out[k] = flat[off:off + n].view(s)
+        off += n
+    return out

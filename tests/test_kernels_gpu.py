@@ -1,0 +1,268 @@
+"""Numerics of every gfx950 HIP kernel against a plain PyTorch fp32 reference of the same op.
+
+All tests need the MI355X and the in-tree ``smdt_amd/_C.so`` (they fail loudly if it cannot
+load: the GPU path never falls back to eager PyTorch).
+"""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from smdt_amd.ops import _ext
+from smdt_amd.ops import functional as SF
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _C():
+    return _ext.ext()
+
+
+def test_extension_loaded_from_tree():
+    C = _C()
+    import os
+    import smdt_amd
+    assert os.path.dirname(os.path.realpath(C.__file__)) == os.path.dirname(os.path.realpath(smdt_amd.__file__))
+
+
+@pytest.mark.parametrize("H", [768, 1024, 4096])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("rms", [False, True])
+def test_layernorm_fwd_bwd(H, dtype, rms):
+    torch.manual_seed(0)
+    rows = 333
+    x = torch.randn(rows, H, device=DEV, dtype=dtype, requires_grad=True)
+    g = (1 + 0.1 * torch.randn(H, device=DEV, dtype=dtype)).requires_grad_()
+    b = (0.1 * torch.randn(H, device=DEV, dtype=dtype)).requires_grad_() if not rms else None
+    y, s = SF.bias_dropout_add_norm(x, None, None, g, b, 0.0, False, 1e-5, rms)
+    xr = x.detach().float().requires_grad_()
+    gr = g.detach().float().requires_grad_()
+    br = b.detach().float().requires_grad_() if b is not None else None
+    if rms:
+        yr = xr * torch.rsqrt(xr.pow(2).mean(-1, keepdim=True) + 1e-5) * gr
+    else:
+        yr = F.layer_norm(xr, (H,), gr, br, 1e-5)
+    tol = 2e-2 if dtype == torch.bfloat16 else 1e-4
+    torch.testing.assert_close(y.float(), yr, atol=tol, rtol=tol)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    yr.backward(dy.float())
+    torch.testing.assert_close(x.grad.float(), xr.grad, atol=5 * tol, rtol=5 * tol)
+    torch.testing.assert_close(g.grad.float(), gr.grad, atol=tol * math.sqrt(rows) * 4, rtol=5 * tol)
+    if b is not None:
+        torch.testing.assert_close(b.grad.float(), br.grad, atol=tol * math.sqrt(rows) * 4, rtol=5 * tol)
+
+
+def test_fused_bias_residual_layernorm():
+    torch.manual_seed(1)
+    rows, H = 512, 1024
+    dt = torch.bfloat16
+    x = torch.randn(rows, H, device=DEV, dtype=dt, requires_grad=True)
+    res = torch.randn(rows, H, device=DEV, dtype=dt, requires_grad=True)
+    bias = (0.1 * torch.randn(H, device=DEV, dtype=dt)).requires_grad_()
+    g = (1 + 0.1 * torch.randn(H, device=DEV, dtype=dt)).requires_grad_()
+    be = (0.1 * torch.randn(H, device=DEV, dtype=dt)).requires_grad_()
+    y, s = SF.bias_dropout_add_norm(x, bias, res, g, be, 0.0, True, 1e-5, False)
+    leaves = [x, res, bias, g, be]
+    ref = [t.detach().float().requires_grad_() for t in leaves]
+    sr = ref[1] + (ref[0] + ref[2])
+    yr = F.layer_norm(sr, (H,), ref[3], ref[4], 1e-5)
+    torch.testing.assert_close(s.float(), sr, atol=3e-2, rtol=2e-2)
+    torch.testing.assert_close(y.float(), yr, atol=5e-2, rtol=3e-2)
+    dy, ds = torch.randn_like(y), torch.randn_like(s)
+    torch.autograd.backward([y, s], [dy, ds])
+    torch.autograd.backward([yr, sr], [dy.float(), ds.float()])
+    for a, r in zip(leaves, ref):
+        torch.testing.assert_close(a.grad.float(), r.grad, atol=0.5, rtol=5e-2)
+
+
+def test_fused_dropout_mask_consistency():
+    torch.manual_seed(2)
+    rows, H, p = 256, 1024, 0.25
+    dt = torch.bfloat16
+    x = torch.randn(rows, H, device=DEV, dtype=dt, requires_grad=True)
+    res = torch.zeros(rows, H, device=DEV, dtype=dt)
+    g = torch.ones(H, device=DEV, dtype=dt, requires_grad=True)
+    be = torch.zeros(H, device=DEV, dtype=dt, requires_grad=True)
+    y, s = SF.bias_dropout_add_norm(x, None, res, g, be, p, True, 1e-5, False)
+    kept = (s != 0)
+    frac = kept.float().mean().item()
+    assert abs(frac - (1 - p)) < 0.02
+    torch.testing.assert_close(s[kept].float(), (x.detach()[kept].float() / (1 - p)), atol=2e-2, rtol=1e-2)
+    s.backward(torch.ones_like(s))
+    # ds = 1 everywhere -> dx = mask / (1 - p): zero exactly where dropped
+    assert torch.all(x.grad[~kept] == 0)
+    torch.testing.assert_close(x.grad[kept].float(), torch.full_like(x.grad[kept].float(), 1 / (1 - p)),
+                               atol=1e-2, rtol=1e-2)
+
+
+@pytest.mark.parametrize("approx", ["tanh", "none"])
+def test_bias_gelu(approx):
+    torch.manual_seed(3)
+    x = torch.randn(1000, 4096, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    b = torch.randn(4096, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    y = SF.bias_gelu(x, b, approx)
+    xr, br = x.detach().float().requires_grad_(), b.detach().float().requires_grad_()
+    yr = F.gelu(xr + br, approximate=approx)
+    torch.testing.assert_close(y.float(), yr, atol=2e-2, rtol=2e-2)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    yr.backward(dy.float())
+    torch.testing.assert_close(x.grad.float(), xr.grad, atol=3e-2, rtol=3e-2)
+    torch.testing.assert_close(b.grad.float(), br.grad, atol=1.0, rtol=2e-2)
+
+
+def test_swiglu():
+    torch.manual_seed(4)
+    x = torch.randn(777, 2 * 1024, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    y = SF.swiglu(x)
+    xr = x.detach().float().requires_grad_()
+    g, u = xr.chunk(2, -1)
+    yr = F.silu(g) * u
+    torch.testing.assert_close(y.float(), yr, atol=3e-2, rtol=2e-2)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    yr.backward(dy.float())
+    torch.testing.assert_close(x.grad.float(), xr.grad, atol=5e-2, rtol=3e-2)
+
+
+@pytest.mark.parametrize("sk", [128, 1024, 2048])
+@pytest.mark.parametrize("causal", [True, False])
+def test_scaled_masked_softmax(sk, causal):
+    torch.manual_seed(5)
+    x = torch.randn(2, 4, sk, sk, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    scale = 0.125
+    y = SF.scaled_masked_softmax(x, None, scale, causal)
+    xr = x.detach().float().requires_grad_()
+    s = xr * scale
+    if causal:
+        s = s.masked_fill(torch.ones(sk, sk, device=DEV, dtype=torch.bool).triu(1), float("-inf"))
+    yr = torch.softmax(s, -1)
+    torch.testing.assert_close(y.float(), yr, atol=1e-2, rtol=2e-2)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    yr.backward(dy.float())
+    torch.testing.assert_close(x.grad.float(), xr.grad, atol=1e-2, rtol=5e-2)
+
+
+def test_softmax_explicit_mask():
+    torch.manual_seed(6)
+    x = torch.randn(2, 3, 64, 256, device=DEV, dtype=torch.bfloat16)
+    mask = torch.rand(2, 1, 64, 256, device=DEV) < 0.3
+    y = SF.scaled_masked_softmax(x, mask, 1.0, False)
+    yr = torch.softmax(x.float().masked_fill(mask, float("-inf")), -1)
+    torch.testing.assert_close(y.float(), yr, atol=1e-2, rtol=2e-2)
+
+
+def test_fused_adam_matches_reference():
+    torch.manual_seed(7)
+    n = 1_000_003
+    p = torch.randn(n, device=DEV)
+    g = torch.randn(n, device=DEV)
+    m = torch.zeros(n, device=DEV)
+    v = torch.zeros(n, device=DEV)
+    model = torch.empty(n, device=DEV, dtype=torch.bfloat16)
+    pr, mr, vr = p.clone(), m.clone(), v.clone()
+    lr, b1, b2, eps, wd = 1e-3, 0.9, 0.95, 1e-8, 0.1
+    mul = torch.tensor([0.5], device=DEV)
+    for step in (1, 2, 3):
+        _C().adam(p, g, m, v, model, lr, b1, b2, eps, wd, step, True, mul, None)
+        gg = g * 0.5
+        mr.mul_(b1).add_(gg, alpha=1 - b1)
+        vr.mul_(b2).addcmul_(gg, gg, value=1 - b2)
+        denom = (vr.sqrt() / math.sqrt(1 - b2 ** step)) + eps
+        pr.mul_(1 - lr * wd)
+        pr.addcdiv_(mr, denom, value=-lr / (1 - b1 ** step))
+    torch.testing.assert_close(p, pr, atol=1e-6, rtol=1e-5)
+    torch.testing.assert_close(model.float(), pr, atol=1e-2, rtol=1e-2)
+    found = torch.ones(1, device=DEV, dtype=torch.int32)
+    before = p.clone()
+    _C().adam(p, g, m, v, model, lr, b1, b2, eps, wd, 4, True, mul, found)
+    assert torch.equal(p, before), "found_inf must skip the step"
+
+
+def test_sumsq_and_inf_detection():
+    x = torch.randn(3_000_001, device=DEV)
+    found = torch.zeros(1, device=DEV, dtype=torch.int32)
+    s = _C().sumsq(x, found)
+    torch.testing.assert_close(s, (x.double() ** 2).sum().float().view(1), rtol=1e-4, atol=1e-2)
+    assert found.item() == 0
+    x[12345] = float("inf")
+    _C().sumsq(x, found)
+    assert found.item() == 1
+    xb = torch.randn(100_000, device=DEV, dtype=torch.bfloat16)
+    sb = _C().sumsq(xb, None)
+    torch.testing.assert_close(sb, (xb.double() ** 2).sum().float().view(1), rtol=1e-3, atol=1e-2)
+
+
+def test_rope_inplace_and_inverse():
+    torch.manual_seed(8)
+    s, b, nh, d = 64, 3, 4, 128
+    x = torch.randn(s * b, nh, d, device=DEV, dtype=torch.bfloat16)
+    cos, sin = SF.rope_tables(s, d, device=DEV)
+    y = x.clone()
+    _C().rope_(y, cos, sin, d, b, s, False)
+    pos = torch.arange(s * b, device=DEV) // b
+    yr = SF._rope_ref(x, cos, sin, d, pos)
+    torch.testing.assert_close(y.float(), yr.float(), atol=2e-2, rtol=2e-2)
+    _C().rope_(y, cos, sin, d, b, s, True)
+    torch.testing.assert_close(y.float(), x.float(), atol=3e-2, rtol=3e-2)
+
+
+@pytest.mark.parametrize("V", [50304, 1000])
+def test_cross_entropy(V):
+    torch.manual_seed(9)
+    N = 300
+    logits = torch.randn(N, V, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    tgt = torch.randint(0, V, (N,), device=DEV)
+    tgt[5] = -100
+    loss = SF.cross_entropy(logits, tgt)
+    lr = logits.detach().float().requires_grad_()
+    ref = F.cross_entropy(lr, tgt, reduction="none", ignore_index=-100)
+    torch.testing.assert_close(loss, ref, atol=2e-2, rtol=1e-2)
+    w = torch.randn(N, device=DEV)
+    (loss * w).sum().backward()
+    (ref * w).sum().backward()
+    torch.testing.assert_close(logits.grad.float(), lr.grad, atol=2e-3, rtol=5e-2)
+
+
+@pytest.mark.parametrize("D", [64, 128])
+@pytest.mark.parametrize("causal", [True, False])
+@pytest.mark.parametrize("heads", [(4, 4), (8, 2)])
+def test_flash_attention(D, causal, heads):
+    torch.manual_seed(10)
+    B, S = 2, 256
+    H, Hkv = heads
+    q = torch.randn(B, S, H, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    k = torch.randn(B, S, Hkv, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    v = torch.randn(B, S, Hkv, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    scale = 1 / math.sqrt(D)
+    o = SF.flash_attention(q, k, v, scale, causal)
+    qr, kr, vr = (t.detach().float().requires_grad_() for t in (q, k, v))
+    orf = SF.attention_ref(qr, kr, vr, scale, causal)
+    torch.testing.assert_close(o.float(), orf, atol=2e-2, rtol=2e-2)
+    do = torch.randn_like(o)
+    o.backward(do)
+    orf.backward(do.float())
+    for a, r in ((q, qr), (k, kr), (v, vr)):
+        err = (a.grad.float() - r.grad).abs().max().item()
+        assert err < 0.05 * max(1.0, r.grad.abs().max().item()), err
+
+
+def test_flash_attention_qkv_seq_first_matches_unfused():
+    torch.manual_seed(11)
+    S, B, nh, hd = 256, 2, 4, 64
+    qkv = torch.randn(S, B, 3 * nh * hd, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    o = SF.flash_attention_qkv(qkv, nh, nh, hd, seq_first=True, causal=True)
+    qr = qkv.detach().float().requires_grad_()
+    q, k, v = SF._qkv_views(qr, nh, nh, hd, True)
+    orf = SF.attention_ref(q, k, v, 1 / math.sqrt(hd), True).transpose(0, 1).flatten(-2)
+    torch.testing.assert_close(o.float(), orf, atol=2e-2, rtol=2e-2)
+    do = torch.randn_like(o)
+    o.backward(do)
+    orf.backward(do.float())
+    err = (qkv.grad.float() - qr.grad).abs().max().item()
+    assert err < 0.05 * max(1.0, qr.grad.abs().max().item())
