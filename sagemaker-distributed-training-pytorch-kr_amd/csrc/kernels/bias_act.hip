@@ -141,18 +141,7 @@ __global__ __launch_bounds__(256) void swiglu_bwd_kernel(const T* __restrict__ d
 __global__ __launch_bounds__(256) void col_partials_reduce_kernel(const float* __restrict__ part,
                                                                  int nslices, int N,
                                                                  float* __restrict__ out) {
-  int col = blockIdx.x * 256 + threadIdx.x;
-  if (col >= N) return;
-  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-  int s = 0;
-  for (; s + 3 < nslices; s += 4) {
-    a0 += part[(int64_t)s * N + col];
-    a1 += part[(int64_t)(s + 1) * N + col];
-    a2 += part[(int64_t)(s + 2) * N + col];
-    a3 += part[(int64_t)(s + 3) * N + col];
-  }
-  for (; s < nslices; ++s) a0 += part[(int64_t)s * N + col];
-  out[col] = (a0 + a1) + (a2 + a3);
+  colsum_block(part, nslices, N, N, out);
 }
 
 // Rows per slice so that (column blocks) x (row slices) ~ 1024 blocks.
@@ -207,7 +196,7 @@ extern "C" hipError_t smdt_bias_act_bwd(int dtype, int act, const void* dy, cons
   else { if (act == 0) SMDT_BA_BWD(float, 0); else SMDT_BA_BWD(float, 1); }
 #undef SMDT_BA_BWD
   if (dbias) {
-    hipLaunchKernelGGL(col_partials_reduce_kernel, dim3((N + 255) / 256), dim3(256), 0, st,
+    hipLaunchKernelGGL(col_partials_reduce_kernel, dim3((N + 31) / 32), dim3(256), 0, st,
                        partials, slices, N, dbias);
   }
   return hipGetLastError();
@@ -215,7 +204,7 @@ extern "C" hipError_t smdt_bias_act_bwd(int dtype, int act, const void* dy, cons
 
 extern "C" hipError_t smdt_col_sum(const float* partials, int nslices, int N, float* out,
                                    hipStream_t st) {
-  hipLaunchKernelGGL(col_partials_reduce_kernel, dim3((N + 255) / 256), dim3(256), 0, st,
+  hipLaunchKernelGGL(col_partials_reduce_kernel, dim3((N + 31) / 32), dim3(256), 0, st,
                      partials, nslices, N, out);
   return hipGetLastError();
 }

@@ -161,6 +161,35 @@ __device__ __forceinline__ void philox_uniform4(uint64_t seed, uint64_t offset, 
   u[3] = r.w * kInv;
 }
 
+// Column sums of an fp32 [nrows, ncols] slab with row stride `rs` (the second stage of every
+// "per-block partials" reduction: dgamma / dbeta / dbias). Block = 256 threads arranged as
+// 32 columns x 8 row groups (128-byte coalesced row segments, 8x more loads in flight than a
+// thread-per-column loop); the 8 group sums are combined in a fixed order (deterministic).
+// Launch with grid.x = ceil(ncols / 32).
+__device__ __forceinline__ void colsum_block(const float* __restrict__ part, int nrows, int64_t rs,
+                                             int ncols, float* __restrict__ out) {
+  __shared__ float red[8][33];
+  const int cl = threadIdx.x & 31, rg = threadIdx.x >> 5;
+  const int col = blockIdx.x * 32 + cl;
+  float a0 = 0.f, a1 = 0.f;
+  if (col < ncols) {
+    int r = rg;
+    for (; r + 8 < nrows; r += 16) {
+      a0 += part[(int64_t)r * rs + col];
+      a1 += part[(int64_t)(r + 8) * rs + col];
+    }
+    if (r < nrows) a0 += part[(int64_t)r * rs + col];
+  }
+  red[rg][cl] = a0 + a1;
+  __syncthreads();
+  if (rg == 0 && col < ncols) {
+    float s = 0.f;
+#pragma unroll
+    for (int g = 0; g < 8; ++g) s += red[g][cl];
+    out[col] = s;
+  }
+}
+
 // Number of blocks for a grid-stride memory-bound kernel (Guideline 11:
 // cap at ~8 blocks per CU over 256 CUs).
 inline int stream_grid(int64_t work_items, int per_block) {

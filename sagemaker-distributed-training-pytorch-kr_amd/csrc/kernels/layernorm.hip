@@ -305,23 +305,11 @@ __global__ __launch_bounds__(256) void ln_partials_reduce_kernel(const float* __
                                                                 float* __restrict__ dgamma,
                                                                 float* __restrict__ dbeta,
                                                                 float* __restrict__ dbias) {
-  // blockIdx.y selects the quantity; each thread owns one column and walks the blocks
-  // (consecutive threads -> consecutive columns: coalesced).
+  // blockIdx.y selects the quantity (slab rows have stride 3H).
   const int q = blockIdx.y;
   float* out = q == 0 ? dgamma : (q == 1 ? dbeta : dbias);
   if (out == nullptr) return;
-  int col = blockIdx.x * 256 + threadIdx.x;
-  if (col >= H) return;
-  float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f, acc3 = 0.f;
-  int b = 0;
-  for (; b + 3 < nblocks; b += 4) {
-    acc0 += part[((int64_t)b * 3 + q) * H + col];
-    acc1 += part[((int64_t)(b + 1) * 3 + q) * H + col];
-    acc2 += part[((int64_t)(b + 2) * 3 + q) * H + col];
-    acc3 += part[((int64_t)(b + 3) * 3 + q) * H + col];
-  }
-  for (; b < nblocks; ++b) acc0 += part[((int64_t)b * 3 + q) * H + col];
-  out[col] = (acc0 + acc1) + (acc2 + acc3);
+  colsum_block(part + (int64_t)q * H, nblocks, 3 * (int64_t)H, H, out);
 }
 
 template <typename T, typename W, int G>
@@ -428,7 +416,7 @@ extern "C" hipError_t smdt_layernorm_bwd(int dtype, int wdtype, const void* dy, 
   else if (dtype == 0 && wdtype == 0) e = ln_bwd_typed<float, float>(a, st);
   else return hipErrorInvalidValue;
   if (e != hipSuccess) return e;
-  dim3 grid((H + 255) / 256, 3);
+  dim3 grid((H + 31) / 32, 3);
   hipLaunchKernelGGL(ln_partials_reduce_kernel, grid, dim3(256), 0, st, partials, nblocks, H,
                      dgamma, rms ? nullptr : dbeta, dbias);
   return hipGetLastError();

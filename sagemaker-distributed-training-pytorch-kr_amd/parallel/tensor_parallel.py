@@ -19,6 +19,7 @@ from __future__ import annotations
 
 import hashlib
 import math
+import os
 from typing import Optional
 
 import torch
@@ -193,12 +194,23 @@ def reduce_scatter_to_sequence_parallel_region(x):
 # Linear with async grad communication + fused fp32 wgrad accumulation (K7)
 
 
-def _accumulate_wgrad(weight, dw):
+_FUSED_WGRAD = os.environ.get("SMDT_FUSED_WGRAD", "1") == "1"
+
+
+def _wgrad(weight, g2, t2):
+    """dW = g2^T t2. With a DDP ``main_grad`` the product is accumulated straight into the fp32
+    buffer by ONE hipBLASLt GEMM (bf16 inputs, fp32 C/D, beta = 1: ``addmm(..., out_dtype=fp32)``)
+    instead of a bf16 GEMM + a separate fp32 add pass (K7 gradient-accumulation fusion). Returns
+    the gradient to hand back to autograd (None when it went to ``main_grad``)."""
     mg = getattr(weight, "main_grad", None)
     if mg is None:
-        return dw
-    if dw is not None:
-        mg.add_(dw.view_as(mg))
+        return g2.t().matmul(t2)
+    if (_FUSED_WGRAD and mg.dtype == torch.float32 and g2.dtype in (torch.bfloat16, torch.float16)
+            and g2.is_cuda and mg.is_contiguous()):
+        torch.addmm(mg.view(g2.shape[1], t2.shape[1]), g2.t(), t2, out_dtype=torch.float32,
+                    out=mg.view(g2.shape[1], t2.shape[1]))
+    else:
+        mg.add_(g2.t().matmul(t2).view_as(mg))
     cb = getattr(weight, "_smdt_grad_ready", None)
     if cb is not None:
         cb(weight)
@@ -239,8 +251,7 @@ class LinearWithGradAccumulationAndAsyncCommunication(torch.autograd.Function):
                 handle = dist.all_reduce(gi_out, group=group, async_op=True)
         g2 = g.reshape(-1, g.shape[-1])
         t2 = total.reshape(-1, total.shape[-1])
-        dw = g2.t().matmul(t2)
-        dw = _accumulate_wgrad(weight, dw)
+        dw = _wgrad(weight, g2, t2)
         db = g2.sum(0) if ctx.has_bias else None
         if handle is not None:
             handle.wait()
