@@ -221,6 +221,15 @@ class MixedPrecisionAdam:
     def zero_grad(self, set_to_none=True):
         self.ddp.zero_grad_buffer()
 
+    @torch.no_grad()
+    def reload_model_params(self):
+        """Refresh the fp32 masters from the model buffer (after loading weights only)."""
+        for (s, e, _), mo in zip(self.pieces, self.master_off):
+            self.master[mo:mo + (e - s)].copy_(self.ddp.param_data[s:e].float())
+
+    def get_loss_scale(self):
+        return self.scaler.scale if self.scaler is not None else None
+
     # ------------------------------------------------------------------ checkpoint
     def state_dict(self):
         d = {"step": self.step_count, "master": self.master, "exp_avg": self.exp_avg,

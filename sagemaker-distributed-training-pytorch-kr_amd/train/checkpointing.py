@@ -1,0 +1,176 @@
+"""Megatron-layout checkpoints.
+
+Layout kept from the reference's Megatron recipe (`--save /opt/ml/model/`, "saving checkpoint at
+iteration 2000", NB3:4582)::
+
+    <save>/latest_checkpointed_iteration.txt          # "2000" (or "release")
+    <save>/iter_0002000/mp_rank_TT[_PPP]/model_optim_rng.pt
+    <save>/iter_0002000/mp_rank_TT[_PPP]/distrib_optim_dpDDD.pt   # ZeRO shards (one per DP rank)
+
+Files hold only tensors and plain Python containers (args are stored as a primitive dict), so
+they load with ``torch.load(..., weights_only=True)``. Writes go to a temp name and are renamed,
+and the tracker file is written last by global rank 0 after a barrier, so a crash never leaves a
+"latest" pointing at a half-written iteration. Flags honoured: ``--save``, ``--save-interval``,
+``--load``, ``--no-save-optim``, ``--no-save-rng``, ``--no-load-optim``, ``--no-load-rng``,
+``--finetune``, ``--exit-on-missing-checkpoint``, ``--use-checkpoint-args``
+(/root/reference/3_training_megatron-lm/megatron/arguments.py:922-956).
+"""
+from __future__ import annotations
+
+import os
+import time
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+from ..parallel import state as ps
+from ..parallel.random import load_rng_state_dict, rng_state_dict
+
+CHECKPOINT_VERSION = 3.0
+TRACKER = "latest_checkpointed_iteration.txt"
+
+
+def _rank0():
+    return (not dist.is_initialized()) or dist.get_rank() == 0
+
+
+def _barrier():
+    if dist.is_initialized():
+        dist.barrier()
+
+
+def checkpoint_dir(root: str, iteration: int, release: bool = False) -> str:
+    st = ps.get_state()
+    d = "release" if release else f"iter_{iteration:07d}"
+    sub = f"mp_rank_{st.tp_rank:02d}" if st.pp == 1 else f"mp_rank_{st.tp_rank:02d}_{st.pp_rank:03d}"
+    return os.path.join(root, d, sub)
+
+
+def _args_to_dict(args) -> dict:
+    out = {}
+    for k, v in vars(args).items():
+        if isinstance(v, (int, float, str, bool)) or v is None:
+            out[k] = v
+        elif isinstance(v, (list, tuple)) and all(isinstance(x, (int, float, str, bool)) for x in v):
+            out[k] = list(v)
+        elif isinstance(v, torch.dtype):
+            out[k] = str(v)
+    return out
+
+
+def _atomic_save(obj, path):
+    os.makedirs(os.path.dirname(path), exist_ok=True)
+    tmp = f"{path}.tmp{os.getpid()}"
+    torch.save(obj, tmp)
+    os.replace(tmp, path)
+
+
+def _unwrap(model):
+    return model.module if hasattr(model, "module") else model
+
+
+def save_checkpoint(iteration: int, model, optimizer=None, scheduler=None, args=None, save_dir: Optional[str] = None,
+                    extra: Optional[dict] = None):
+    save_dir = save_dir or args.save
+    t0 = time.time()
+    if _rank0():
+        print(f"saving checkpoint at iteration {iteration:7d} to {save_dir}", flush=True)
+    st = ps.get_state()
+    d = checkpoint_dir(save_dir, iteration)
+    no_optim = bool(getattr(args, "no_save_optim", False)) if args is not None else False
+    no_rng = bool(getattr(args, "no_save_rng", False)) if args is not None else False
+    zero = optimizer is not None and getattr(optimizer, "zero", False)
+    if st.dp_rank == 0:
+        sd = {"checkpoint_version": CHECKPOINT_VERSION, "iteration": iteration,
+              "model": _unwrap(model).state_dict()}
+        if args is not None:
+            sd["args"] = _args_to_dict(args)
+        if optimizer is not None and not no_optim and not zero:
+            sd["optimizer"] = optimizer.state_dict()
+        if scheduler is not None and not no_optim:
+            sd["opt_param_scheduler"] = scheduler.state_dict()
+        if not no_rng:
+            sd["rng_state"] = _rng_for_save()
+        if extra:
+            sd.update(extra)
+        _atomic_save(sd, os.path.join(d, "model_optim_rng.pt"))
+    if zero and not no_optim:
+        _atomic_save({"iteration": iteration, "optimizer": optimizer.state_dict()},
+                     os.path.join(d, f"distrib_optim_dp{st.dp_rank:03d}.pt"))
+    _barrier()
+    if _rank0():
+        with open(os.path.join(save_dir, TRACKER), "w") as f:
+            f.write(str(iteration))
+        print(f"  successfully saved checkpoint at iteration {iteration:7d} to {save_dir}", flush=True)
+    _barrier()
+    return time.time() - t0
+
+
+def _rng_for_save():
+    r = rng_state_dict()
+    # numpy / python states are tuples with non-tensor payloads: keep the tensor-able parts only
+    out = {k: v for k, v in r.items() if k in ("default", "tp", "torch_cpu", "torch_cuda")}
+    np_state = r.get("numpy")
+    if np_state is not None:
+        out["numpy_keys"] = torch.from_numpy(np_state[1].astype("int64"))
+        out["numpy_pos"] = int(np_state[2])
+    return out
+
+
+def read_tracker(load_dir: str):
+    p = os.path.join(load_dir, TRACKER)
+    if not os.path.isfile(p):
+        return None, False
+    s = open(p).read().strip()
+    if s == "release":
+        return 0, True
+    return int(s), False
+
+
+def load_checkpoint(model, optimizer=None, scheduler=None, args=None, load_dir: Optional[str] = None,
+                    strict: bool = True) -> int:
+    """Returns the iteration to resume from (0 when nothing was loaded)."""
+    load_dir = load_dir or (args.load if args is not None else None)
+    if not load_dir:
+        return 0
+    it, release = read_tracker(load_dir)
+    if it is None:
+        if args is not None and getattr(args, "exit_on_missing_checkpoint", False):
+            raise SystemExit(f"--exit-on-missing-checkpoint: no checkpoint under {load_dir}")
+        if _rank0():
+            print(f"WARNING: could not find the metadata file {os.path.join(load_dir, TRACKER)}; "
+                  "training from random initialization", flush=True)
+        return 0
+    d = checkpoint_dir(load_dir, it, release)
+    sd = torch.load(os.path.join(d, "model_optim_rng.pt"), map_location="cpu", weights_only=True)
+    _unwrap(model).load_state_dict(sd["model"], strict=strict)
+    finetune = bool(getattr(args, "finetune", False)) if args is not None else False
+    no_load_optim = bool(getattr(args, "no_load_optim", False)) if args is not None else False
+    no_load_rng = bool(getattr(args, "no_load_rng", False)) if args is not None else False
+    if optimizer is not None and not (finetune or no_load_optim or release):
+        if getattr(optimizer, "zero", False):
+            st = ps.get_state()
+            p = os.path.join(d, f"distrib_optim_dp{st.dp_rank:03d}.pt")
+            if os.path.isfile(p):
+                optimizer.load_state_dict(torch.load(p, map_location="cpu", weights_only=True)["optimizer"])
+        elif "optimizer" in sd:
+            optimizer.load_state_dict(sd["optimizer"])
+        if scheduler is not None and "opt_param_scheduler" in sd:
+            scheduler.load_state_dict(sd["opt_param_scheduler"])
+    elif optimizer is not None:
+        # weights were loaded into the model: refresh fp32 masters from them
+        sync = getattr(optimizer, "reload_model_params", None)
+        if sync is not None:
+            sync()
+    if "rng_state" in sd and not (finetune or no_load_rng or release):
+        r = dict(sd["rng_state"])
+        load_rng_state_dict({k: v for k, v in r.items() if k in ("default", "tp", "torch_cpu", "torch_cuda")})
+    if args is not None and "args" in sd:
+        for k in ("consumed_train_samples", "consumed_valid_samples"):
+            if k in sd["args"]:
+                setattr(args, k, sd["args"][k])
+    _barrier()
+    if _rank0():
+        print(f"  successfully loaded checkpoint from {load_dir} at iteration {it}", flush=True)
+    return 0 if (finetune or release) else it
