@@ -11,13 +11,22 @@
 //     ("A·X"), provided the A operand uses the matching permuted k order;
 //   * `ds_read_b64_tr_b16` delivers that permuted A operand (a column gather of 4 consecutive
 //     rows) from a plain row-major LDS tile, so no transpose copy is ever made.
-// Hence every kernel here computes the "swapped" products so the softmax row index sits on
-// the lane:
+// Hence every kernel computes the "swapped" products so the softmax row index sits on the lane:
 //   forward  : S^T = K.Q^T  (query on lane)  -> online softmax in registers -> O^T += V^T.P^T
 //   dK/dV    : S   = Q.K^T  (key on lane)    -> dV^T += dO^T.P,  dK^T += Q^T.dS
 //   dQ       : S^T = K.Q^T  (query on lane)  -> dQ^T += K^T.dS^T
 // dK/dV and dQ run as two kernels (FA2 split) so there are no float atomics: deterministic
 // results and no atomic-rate floor (HIP guide Guideline 12).
+//
+// v2 performance structure (measured VALU-bound in v1: 942 VALU vs 16 MFMA per tile):
+//   * every LDS fragment address is a per-lane base computed ONCE plus a compile-time
+//     immediate (the XOR swizzle only depends on row bits 0..3, so 16-row tile offsets are
+//     constants) -> no address arithmetic inside the loops;
+//   * softmax works in the log2 domain with raw `v_exp_f32` (__builtin_amdgcn_exp2f) and one
+//     FMA per element; the row max / sum cross the two half-waves with v_permlane32_swap;
+//   * the causal mask is applied only on the diagonal tile of each wave (uniform branch);
+//   * K/V (resp. Q/dO) tiles are double-buffered in LDS with register staging issued before
+//     the MFMA work of the current tile (T14), so each tile needs ONE barrier.
 //
 // LDS tiles are 64 rows x D bf16 with an XOR swizzle of the 16-byte chunk index that makes
 // BOTH the row reads (ds_read_b128, 4x16-lane groups) and the transposed reads
@@ -36,6 +45,7 @@ namespace fa {
 using s16x4 = __attribute__((ext_vector_type(4))) short;
 using s16x8 = __attribute__((ext_vector_type(8))) short;
 using lds_s16x4 = __attribute__((address_space(3))) s16x4;
+using bf4 = __attribute__((ext_vector_type(4))) __bf16;
 
 constexpr int kBlockRows = 128;  // rows owned by a workgroup (4 waves x 32)
 constexpr int kTile = 64;        // rows per streamed LDS tile
@@ -52,45 +62,64 @@ __device__ __forceinline__ f32x16 zero16() {
   return z;
 }
 
-// Byte offset of 16-byte chunk c of row r inside a [64][D] bf16 LDS tile (see header).
+__device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// max / sum of x with the value held by lane ^ 32 (same query / key, other half-wave).
+__device__ __forceinline__ float xhalf_max(float x) {
+  auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float xhalf_sum(float x) {
+  auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
 template <int D>
-__device__ __forceinline__ int toff(int r, int c) {
-  int f;
-  if constexpr (D == 128) {
-    f = ((r & 3) << 2) | ((r >> 2) & 3);
-  } else {
-    f = (((r >> 1) & 1) << 2) | ((r >> 2) & 3);
+struct Geo {
+  static constexpr int RB = D * 2;             // bytes per tile row
+  static constexpr int TB = kTile * RB;        // bytes per tile
+  static constexpr int KS = D / 16;            // MFMA k-steps over D
+  static constexpr int DT = D / 32;            // 32-wide d tiles
+  static constexpr int CH = D / 8;             // 16-byte chunks per row
+  // Swizzle: depends on row bits 0..3 only, so offsets of rows r and r + 16 k differ by a
+  // constant.
+  __device__ static __forceinline__ int f(int r) {
+    if constexpr (D == 128) return ((r & 3) << 2) | ((r >> 2) & 3);
+    else return (((r >> 1) & 1) << 2) | ((r >> 2) & 3);
   }
-  return r * (D * 2) + 16 * (c ^ f);
-}
+  __device__ static __forceinline__ int off(int r, int c) { return r * RB + 16 * (c ^ f(r)); }
+};
 
-// Row operand fragment for k-step ks: lane holds row (rbase + lane&31), elements
-// [16 ks + 8 h, +8) with h = lane >> 5.
+// Per-lane LDS offsets, computed once per kernel.
 template <int D>
-__device__ __forceinline__ bf16x8 row_frag(const char* lds, int rbase, int ks, int lane) {
-  const int r = rbase + (lane & 31);
-  const int c = 2 * ks + (lane >> 5);
-  return *reinterpret_cast<const bf16x8*>(lds + toff<D>(r, c));
-}
-
-// Transposed fragment: A[i = col dbase + (lane&31)][k] for k-step s over tile rows
-// rbase + 16 s + ..., in the permuted k order that matches an accumulator-derived B operand:
-// element j <-> row 16 s + 8 (j >> 2) + 4 h + (j & 3).
-template <int D>
-__device__ __forceinline__ bf16x8 tr_frag(const char* lds, int rbase, int s, int dbase,
-                                          int lane) {
-  const int q = (lane >> 2) & 3, p = lane & 3;
-  const int col = dbase + 16 * ((lane >> 4) & 1) + 4 * p;
-  const int c = col >> 3;
-  const int inb = 8 * (p & 1);
-  const int r0 = rbase + 16 * s + 4 * (lane >> 5) + q;
-  const lds_s16x4* a0 = (const lds_s16x4*)(lds + toff<D>(r0, c) + inb);
-  const lds_s16x4* a1 = (const lds_s16x4*)(lds + toff<D>(r0 + 8, c) + inb);
-  s16x4 x = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)a0);
-  s16x4 y = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)a1);
-  s16x8 z = __builtin_shufflevector(x, y, 0, 1, 2, 3, 4, 5, 6, 7);
-  return __builtin_bit_cast(bf16x8, z);
-}
+struct Frag {
+  int row[D / 16];     // row fragment of k-step ks for tile rows 0..31
+  int tr[D / 32][2];   // transposed fragment of d-tile dt, k-step 0, rows 0..15 (two 4-row blocks)
+  __device__ __forceinline__ void init(int lane) {
+    const int l31 = lane & 31, h = lane >> 5;
+#pragma unroll
+    for (int ks = 0; ks < D / 16; ++ks) row[ks] = Geo<D>::off(l31, 2 * ks + h);
+    const int q = (lane >> 2) & 3, p = lane & 3, g = (lane >> 4) & 1;
+    const int r0 = 4 * h + q;
+#pragma unroll
+    for (int dt = 0; dt < D / 32; ++dt) {
+      const int c = 4 * dt + 2 * g + (p >> 1);
+      tr[dt][0] = Geo<D>::off(r0, c) + 8 * (p & 1);
+      tr[dt][1] = Geo<D>::off(r0 + 8, c) + 8 * (p & 1);
+    }
+  }
+  // A-operand row fragment: rows rbase..rbase+31 (rbase multiple of 32), elements 16 ks + 8 h..
+  __device__ __forceinline__ bf16x8 rowf(const char* tile, int rbase, int ks) const {
+    return *reinterpret_cast<const bf16x8*>(tile + rbase * Geo<D>::RB + row[ks]);
+  }
+  // A-operand transposed fragment over tile rows rbase + 16 s + (permuted), columns 32 dt + lane&31.
+  __device__ __forceinline__ bf16x8 trf(const char* tile, int rbase, int s, int dt) const {
+    const char* b = tile + (rbase + 16 * s) * Geo<D>::RB;
+    s16x4 x = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(b + tr[dt][0]));
+    s16x4 y = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(b + tr[dt][1]));
+    return __builtin_bit_cast(bf16x8, __builtin_shufflevector(x, y, 0, 1, 2, 3, 4, 5, 6, 7));
+  }
+};
 
 // Pack accumulator registers 8 s .. 8 s + 7 into a bf16 operand fragment.
 __device__ __forceinline__ bf16x8 pack8(const f32x16& x, int s) {
@@ -103,37 +132,36 @@ __device__ __forceinline__ bf16x8 pack8(const f32x16& x, int s) {
 // Row of accumulator register i for lane half h (32x32 C/D map).
 __device__ __forceinline__ int acc_row(int i, int h) { return (i & 3) + 8 * (i >> 2) + 4 * h; }
 
-// Global -> register staging of a 64-row tile (CH = D/8 16-byte chunks per row; 256 threads).
+// Global -> register staging of a 64-row tile (256 threads, 16-byte chunks).
 template <int D>
 struct Stage {
-  static constexpr int CH = D / 8;
-  static constexpr int N = kTile * CH / 256;  // chunks per thread
+  static constexpr int N = kTile * Geo<D>::CH / 256;
   u16x8 v[N];
-  __device__ __forceinline__ void load(const bf16* base, int64_t row_stride, int row0, int nrows) {
+  int lds_off[N];
+  int64_t goff[N];     // element offset of chunk i relative to the tile's first row
+  int rowi[N];
+  __device__ __forceinline__ void init(int64_t row_stride) {
 #pragma unroll
     for (int i = 0; i < N; ++i) {
       const int idx = threadIdx.x + 256 * i;
-      const int r = idx / CH, c = idx % CH;
-      if (row0 + r < nrows) {
-        v[i] = *reinterpret_cast<const u16x8*>(base + (int64_t)(row0 + r) * row_stride + c * 8);
-      } else {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) v[i][j] = 0;
-      }
+      const int r = idx / Geo<D>::CH, c = idx % Geo<D>::CH;
+      rowi[i] = r;
+      lds_off[i] = Geo<D>::off(r, c);
+      goff[i] = (int64_t)r * row_stride + c * 8;
     }
   }
-  __device__ __forceinline__ void store(char* lds) const {
+  __device__ __forceinline__ void load(const bf16* tile_base) {
 #pragma unroll
-    for (int i = 0; i < N; ++i) {
-      const int idx = threadIdx.x + 256 * i;
-      const int r = idx / CH, c = idx % CH;
-      *reinterpret_cast<u16x8*>(lds + toff<D>(r, c)) = v[i];
-    }
+    for (int i = 0; i < N; ++i) v[i] = *reinterpret_cast<const u16x8*>(tile_base + goff[i]);
+  }
+  __device__ __forceinline__ void store(char* tile) const {
+#pragma unroll
+    for (int i = 0; i < N; ++i) *reinterpret_cast<u16x8*>(tile + lds_off[i]) = v[i];
   }
 };
 
-// Direct global load of a row-operand fragment (used for the operands that stay in registers
-// for a whole kernel): lane holds row (row0 + lane&31), elements [16 ks + 8 h, +8).
+// Direct global load of a row-operand fragment that stays in registers for the whole kernel:
+// lane holds row (row0 + lane&31), elements [16 ks + 8 h, +8).
 template <int D>
 __device__ __forceinline__ void load_reg_frags(const bf16* base, int64_t row_stride, int row0,
                                                int lane, bf16x8 (&f)[D / 16]) {
@@ -147,17 +175,18 @@ struct Strides {
 };
 
 // ---------------------------------------------------------------------------------------
-// Forward. Workgroup = 4 waves = 128 query rows of one (b, h); K/V streamed in 64-key tiles.
+// Forward. Workgroup = 4 waves = 128 query rows of one (b, h); K/V streamed in 64-key tiles,
+// double-buffered.
 template <int D, bool CAUSAL>
-__global__ __launch_bounds__(256) void fwd_kernel(const bf16* __restrict__ Q,
-                                                  const bf16* __restrict__ K,
-                                                  const bf16* __restrict__ V, bf16* __restrict__ O,
-                                                  float* __restrict__ LSE, int B, int H, int Hkv,
-                                                  int S, Strides qs, Strides ks_, Strides vs,
-                                                  Strides os, float scale) {
-  __shared__ __attribute__((aligned(16))) char lds[2 * kTile * D * 2];
-  char* k_lds = lds;
-  char* v_lds = lds + kTile * D * 2;
+__global__ __launch_bounds__(256, D == 64 ? 2 : 1) void fwd_kernel(const bf16* __restrict__ Q,
+                                                     const bf16* __restrict__ K,
+                                                     const bf16* __restrict__ V,
+                                                     bf16* __restrict__ O, float* __restrict__ LSE,
+                                                     int B, int H, int Hkv, int S, Strides qs,
+                                                     Strides ks_, Strides vs, Strides os,
+                                                     float scale) {
+  using G = Geo<D>;
+  __shared__ __attribute__((aligned(16))) char lds[2 * 2 * G::TB];  // [buf][K|V]
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5;
   const int nqb = S / kBlockRows;
@@ -169,82 +198,80 @@ __global__ __launch_bounds__(256) void fwd_kernel(const bf16* __restrict__ Q,
   const int qw = q0 + 32 * w;  // this wave's first query row
   const int my_q = qw + (lane & 31);
 
-  const bf16* Qb = Q + b * qs.sb + hq * qs.sh;
   const bf16* Kb = K + b * ks_.sb + hk * ks_.sh;
   const bf16* Vb = V + b * vs.sb + hk * vs.sh;
 
-  bf16x8 qf[D / 16];
-  load_reg_frags<D>(Qb, qs.ss, qw, lane, qf);
+  Frag<D> fr;
+  fr.init(lane);
+  bf16x8 qf[G::KS];
+  load_reg_frags<D>(Q + b * qs.sb + hq * qs.sh, qs.ss, qw, lane, qf);
 
-  f32x16 o[D / 32];
+  f32x16 o[G::DT];
 #pragma unroll
-  for (int t = 0; t < D / 32; ++t) o[t] = zero16();
-  float m = -INFINITY, l = 0.f;
+  for (int t = 0; t < G::DT; ++t) o[t] = zero16();
+  float m = -INFINITY, l = 0.f;  // running max (log2 domain) and denominator
   const float c2 = scale * kLog2e;
 
   const int kend = CAUSAL ? (q0 + kBlockRows) : S;
   const int ntiles = kend / kTile;
   Stage<D> sk, sv;
-  sk.load(Kb, ks_.ss, 0, S);
-  sv.load(Vb, vs.ss, 0, S);
-  sk.store(k_lds);
-  sv.store(v_lds);
+  sk.init(ks_.ss);
+  sv.init(vs.ss);
+  sk.load(Kb);
+  sv.load(Vb);
+  sk.store(lds);
+  sv.store(lds + G::TB);
   __syncthreads();
 
   for (int t = 0; t < ntiles; ++t) {
     const int kb = t * kTile;
     const bool more = t + 1 < ntiles;
+    const char* kt = lds + (t & 1) * 2 * G::TB;
+    const char* vt = kt + G::TB;
     if (more) {
-      sk.load(Kb, ks_.ss, kb + kTile, S);
-      sv.load(Vb, vs.ss, kb + kTile, S);
+      sk.load(Kb + (int64_t)(kb + kTile) * ks_.ss);
+      sv.load(Vb + (int64_t)(kb + kTile) * vs.ss);
     }
-    const bool active = !CAUSAL || kb <= qw + 31;
-    if (active) {
+    if (!CAUSAL || kb <= qw + 31) {
       // S^T tiles: rows = keys (registers), column = this lane's query.
       f32x16 st[2];
 #pragma unroll
       for (int tt = 0; tt < 2; ++tt) {
         st[tt] = zero16();
 #pragma unroll
-        for (int kk = 0; kk < D / 16; ++kk)
-          st[tt] = mfma(row_frag<D>(k_lds, 32 * tt, kk, lane), qf[kk], st[tt]);
+        for (int kk = 0; kk < G::KS; ++kk) st[tt] = mfma(fr.rowf(kt, 32 * tt, kk), qf[kk], st[tt]);
       }
-      float tmax = -INFINITY;
+      if (CAUSAL && kb + kTile - 1 > qw) {  // diagonal tile for this wave: mask key > query
 #pragma unroll
-      for (int tt = 0; tt < 2; ++tt) {
+        for (int tt = 0; tt < 2; ++tt)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          float sv2 = st[tt][i] * c2;
-          if (CAUSAL) {
-            const int key = kb + 32 * tt + acc_row(i, h);
-            if (key > my_q) sv2 = -INFINITY;
-          }
-          st[tt][i] = sv2;
-          tmax = fmaxf(tmax, sv2);
-        }
+          for (int i = 0; i < 16; ++i)
+            if (kb + 32 * tt + acc_row(i, h) > my_q) st[tt][i] = -INFINITY;
       }
-      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+      float tmax = st[0][0];
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) tmax = fmaxf(tmax, st[tt][i]);
+      tmax = xhalf_max(tmax) * c2;
       const float mnew = fmaxf(m, tmax);
       const float base = mnew == -INFINITY ? 0.f : mnew;
-      const float alpha = exp2f(m - base);
+      const float alpha = fexp2(m - base);
       float rs = 0.f;
 #pragma unroll
-      for (int tt = 0; tt < 2; ++tt) {
+      for (int tt = 0; tt < 2; ++tt)
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-          float p = exp2f(st[tt][i] - base);
+          const float p = fexp2(fmaf(st[tt][i], c2, -base));
           st[tt][i] = p;
           rs += p;
         }
-      }
-      rs += __shfl_xor(rs, 32, 64);
-      l = l * alpha + rs;
+      l = l * alpha + xhalf_sum(rs);
       m = mnew;
 #pragma unroll
-      for (int dt = 0; dt < D / 32; ++dt) {
+      for (int dt = 0; dt < G::DT; ++dt)
 #pragma unroll
         for (int i = 0; i < 16; ++i) o[dt][i] *= alpha;
-      }
       // O^T[d, q] += V^T[d, keys] . P^T[keys, q]
 #pragma unroll
       for (int tt = 0; tt < 2; ++tt) {
@@ -252,15 +279,14 @@ __global__ __launch_bounds__(256) void fwd_kernel(const bf16* __restrict__ Q,
         for (int s = 0; s < 2; ++s) {
           const bf16x8 pb = pack8(st[tt], s);
 #pragma unroll
-          for (int dt = 0; dt < D / 32; ++dt)
-            o[dt] = mfma(tr_frag<D>(v_lds, 32 * tt, s, 32 * dt, lane), pb, o[dt]);
+          for (int dt = 0; dt < G::DT; ++dt) o[dt] = mfma(fr.trf(vt, 32 * tt, s, dt), pb, o[dt]);
         }
       }
     }
-    __syncthreads();
     if (more) {
-      sk.store(k_lds);
-      sv.store(v_lds);
+      char* nk = lds + ((t + 1) & 1) * 2 * G::TB;
+      sk.store(nk);
+      sv.store(nk + G::TB);
     }
     __syncthreads();
   }
@@ -269,19 +295,16 @@ __global__ __launch_bounds__(256) void fwd_kernel(const bf16* __restrict__ Q,
   const float inv = l > 0.f ? 1.f / l : 0.f;
   bf16* Ob = O + b * os.sb + hq * os.sh + (int64_t)my_q * os.ss;
 #pragma unroll
-  for (int dt = 0; dt < D / 32; ++dt) {
+  for (int dt = 0; dt < G::DT; ++dt) {
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
-      using bf4 = __attribute__((ext_vector_type(4))) __bf16;
       bf4 v4;
 #pragma unroll
       for (int j = 0; j < 4; ++j) v4[j] = (bf16)(o[dt][4 * g + j] * inv);
       *reinterpret_cast<bf4*>(Ob + 32 * dt + 8 * g + 4 * h) = v4;
     }
   }
-  if (h == 0) {
-    LSE[((int64_t)b * H + hq) * S + my_q] = (m + __log2f(l)) * 0.6931471805599453f;
-  }
+  if (h == 0) LSE[((int64_t)b * H + hq) * S + my_q] = (m + __log2f(l)) * 0.6931471805599453f;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -318,22 +341,20 @@ __global__ __launch_bounds__(256) void delta_kernel(const bf16* __restrict__ O,
 // ---------------------------------------------------------------------------------------
 // dK / dV. Workgroup = 4 waves = 128 keys of one (b, kv-head); each wave keeps K, V of its 32
 // keys and dK^T, dV^T in registers while the workgroup sweeps the query heads of the group and
-// their 64-row query tiles (Q, dO, lse, delta staged in LDS).
+// their 64-row query tiles (Q, dO, lse*log2e, delta staged in double-buffered LDS).
 template <int D, bool CAUSAL>
-__global__ __launch_bounds__(256) void bwd_dkdv_kernel(
+__global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dkdv_kernel(
     const bf16* __restrict__ Q, const bf16* __restrict__ K, const bf16* __restrict__ V,
     const bf16* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ DELTA,
     bf16* __restrict__ dK, bf16* __restrict__ dV, int B, int H, int Hkv, int S, Strides qs,
     Strides ks_, Strides vs, Strides dos, Strides dks, Strides dvs, float scale) {
-  __shared__ __attribute__((aligned(16))) char lds[2 * kTile * D * 2 + 2 * kTile * 4];
-  char* q_lds = lds;
-  char* do_lds = lds + kTile * D * 2;
-  float* lse_lds = reinterpret_cast<float*>(lds + 2 * kTile * D * 2);
-  float* del_lds = lse_lds + kTile;
+  using G = Geo<D>;
+  constexpr int BUF = 2 * G::TB + 2 * kTile * 4;  // Q | dO | lse | delta
+  __shared__ __attribute__((aligned(16))) char lds[2 * BUF];
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5;
   const int nkb = S / kBlockRows;
-  const int kblk = CAUSAL ? (int)(blockIdx.x % nkb) : (int)(blockIdx.x % nkb);
+  const int kblk = (int)(blockIdx.x % nkb);  // early key blocks see the most query tiles
   const int bhk = blockIdx.x / nkb;
   const int b = bhk / Hkv, hk = bhk % Hkv;
   const int group = H / Hkv;
@@ -341,13 +362,15 @@ __global__ __launch_bounds__(256) void bwd_dkdv_kernel(
   const int kw = k0 + 32 * w;
   const int my_key = kw + (lane & 31);
 
-  bf16x8 kf[D / 16], vf[D / 16];
+  Frag<D> fr;
+  fr.init(lane);
+  bf16x8 kf[G::KS], vf[G::KS];
   load_reg_frags<D>(K + b * ks_.sb + hk * ks_.sh, ks_.ss, kw, lane, kf);
   load_reg_frags<D>(V + b * vs.sb + hk * vs.sh, vs.ss, kw, lane, vf);
 
-  f32x16 dk[D / 32], dv[D / 32];
+  f32x16 dk[G::DT], dv[G::DT];
 #pragma unroll
-  for (int t = 0; t < D / 32; ++t) dk[t] = dv[t] = zero16();
+  for (int t = 0; t < G::DT; ++t) dk[t] = dv[t] = zero16();
   const float c2 = scale * kLog2e;
 
   const int qstart = CAUSAL ? k0 : 0;
@@ -355,57 +378,66 @@ __global__ __launch_bounds__(256) void bwd_dkdv_kernel(
   const int total = ntiles * group;
 
   Stage<D> sq, sdo;
-  auto tile_coords = [&](int it, int& hq, int& qb) {
-    hq = hk * group + it / ntiles;
-    qb = qstart + (it % ntiles) * kTile;
-  };
-  {
-    int hq, qb;
-    tile_coords(0, hq, qb);
-    sq.load(Q + b * qs.sb + hq * qs.sh, qs.ss, qb, S);
-    sdo.load(dO + b * dos.sb + hq * dos.sh, dos.ss, qb, S);
-    sq.store(q_lds);
-    sdo.store(do_lds);
+  sq.init(qs.ss);
+  sdo.init(dos.ss);
+  float nl = 0.f, nd = 0.f;
+  auto issue = [&](int it) {
+    const int hq = hk * group + it / ntiles;
+    const int qb = qstart + (it % ntiles) * kTile;
+    sq.load(Q + b * qs.sb + hq * qs.sh + (int64_t)qb * qs.ss);
+    sdo.load(dO + b * dos.sb + hq * dos.sh + (int64_t)qb * dos.ss);
     if (threadIdx.x < kTile) {
-      lse_lds[threadIdx.x] = LSE[((int64_t)b * H + hq) * S + qb + threadIdx.x] * kLog2e;
-      del_lds[threadIdx.x] = DELTA[((int64_t)b * H + hq) * S + qb + threadIdx.x];
+      const int64_t li = ((int64_t)b * H + hq) * S + qb + threadIdx.x;
+      nl = LSE[li] * kLog2e;
+      nd = DELTA[li];
     }
-    __syncthreads();
-  }
+  };
+  auto commit = [&](char* buf) {
+    sq.store(buf);
+    sdo.store(buf + G::TB);
+    if (threadIdx.x < kTile) {
+      reinterpret_cast<float*>(buf + 2 * G::TB)[threadIdx.x] = nl;
+      reinterpret_cast<float*>(buf + 2 * G::TB + kTile * 4)[threadIdx.x] = nd;
+    }
+  };
+  issue(0);
+  commit(lds);
+  __syncthreads();
 
   for (int it = 0; it < total; ++it) {
-    int hq, qb;
-    tile_coords(it, hq, qb);
+    const int qb = qstart + (it % ntiles) * kTile;
     const bool more = it + 1 < total;
-    int nhq = 0, nqb = 0;
-    float nl = 0.f, nd = 0.f;
-    if (more) {
-      tile_coords(it + 1, nhq, nqb);
-      sq.load(Q + b * qs.sb + nhq * qs.sh, qs.ss, nqb, S);
-      sdo.load(dO + b * dos.sb + nhq * dos.sh, dos.ss, nqb, S);
-      if (threadIdx.x < kTile) {
-        nl = LSE[((int64_t)b * H + nhq) * S + nqb + threadIdx.x] * kLog2e;
-        nd = DELTA[((int64_t)b * H + nhq) * S + nqb + threadIdx.x];
-      }
-    }
+    const char* buf = lds + (it & 1) * BUF;
+    const char* q_l = buf;
+    const char* do_l = buf + G::TB;
+    const float* lse_l = reinterpret_cast<const float*>(buf + 2 * G::TB);
+    const float* del_l = lse_l + kTile;
+    if (more) issue(it + 1);
 #pragma unroll
     for (int qs2 = 0; qs2 < 2; ++qs2) {
       const int qsub = qb + 32 * qs2;
       if (CAUSAL && qsub + 31 < kw) continue;  // all queries precede all of this wave's keys
-      // S[q, key] = Q . K^T  (key on lane, query rows in registers)
+      // S[q, key] = Q . K^T ; dP[q, key] = dO . V^T   (key on lane, query rows in registers)
       f32x16 s = zero16(), dp = zero16();
 #pragma unroll
-      for (int kk = 0; kk < D / 16; ++kk) {
-        s = mfma(row_frag<D>(q_lds, 32 * qs2, kk, lane), kf[kk], s);
-        dp = mfma(row_frag<D>(do_lds, 32 * qs2, kk, lane), vf[kk], dp);
+      for (int kk = 0; kk < G::KS; ++kk) {
+        s = mfma(fr.rowf(q_l, 32 * qs2, kk), kf[kk], s);
+        dp = mfma(fr.rowf(do_l, 32 * qs2, kk), vf[kk], dp);
       }
+      const bool diag = CAUSAL && qsub < kw + 31;
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int qr = 32 * qs2 + acc_row(i, h);
-        float p = exp2f(s[i] * c2 - lse_lds[qr]);
-        if (CAUSAL && my_key > qb + qr) p = 0.f;
-        s[i] = p;                            // P
-        dp[i] = p * (dp[i] - del_lds[qr]);   // dS
+      for (int g = 0; g < 4; ++g) {
+        const int r0 = 32 * qs2 + 8 * g + 4 * h;  // 4 consecutive query rows of this group
+        const f32x4 lv = *reinterpret_cast<const f32x4*>(lse_l + r0);
+        const f32x4 dl = *reinterpret_cast<const f32x4*>(del_l + r0);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int i = 4 * g + j;
+          float p = fexp2(fmaf(s[i], c2, -lv[j]));
+          if (diag && my_key > qb + r0 + j) p = 0.f;
+          s[i] = p;                        // P
+          dp[i] = p * (dp[i] - dl[j]);     // dS
+        }
       }
       // dV^T[d, key] += dO^T[d, q] . P[q, key] ; dK^T[d, key] += Q^T[d, q] . dS[q, key]
 #pragma unroll
@@ -413,30 +445,21 @@ __global__ __launch_bounds__(256) void bwd_dkdv_kernel(
         const bf16x8 pb = pack8(s, st);
         const bf16x8 db = pack8(dp, st);
 #pragma unroll
-        for (int dt = 0; dt < D / 32; ++dt) {
-          dv[dt] = mfma(tr_frag<D>(do_lds, 32 * qs2, st, 32 * dt, lane), pb, dv[dt]);
-          dk[dt] = mfma(tr_frag<D>(q_lds, 32 * qs2, st, 32 * dt, lane), db, dk[dt]);
+        for (int dt = 0; dt < G::DT; ++dt) {
+          dv[dt] = mfma(fr.trf(do_l, 32 * qs2, st, dt), pb, dv[dt]);
+          dk[dt] = mfma(fr.trf(q_l, 32 * qs2, st, dt), db, dk[dt]);
         }
       }
     }
-    __syncthreads();
-    if (more) {
-      sq.store(q_lds);
-      sdo.store(do_lds);
-      if (threadIdx.x < kTile) {
-        lse_lds[threadIdx.x] = nl;
-        del_lds[threadIdx.x] = nd;
-      }
-    }
+    if (more) commit(lds + ((it + 1) & 1) * BUF);
     __syncthreads();
   }
 
   // dK[key, d] = scale * dK^T ; dV[key, d] = dV^T (key on lane, d in registers)
   bf16* dKb = dK + b * dks.sb + hk * dks.sh + (int64_t)my_key * dks.ss;
   bf16* dVb = dV + b * dvs.sb + hk * dvs.sh + (int64_t)my_key * dvs.ss;
-  using bf4 = __attribute__((ext_vector_type(4))) __bf16;
 #pragma unroll
-  for (int dt = 0; dt < D / 32; ++dt) {
+  for (int dt = 0; dt < G::DT; ++dt) {
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       bf4 a, c;
@@ -452,16 +475,16 @@ __global__ __launch_bounds__(256) void bwd_dkdv_kernel(
 }
 
 // ---------------------------------------------------------------------------------------
-// dQ. Workgroup = 4 waves = 128 query rows of one (b, h); K/V streamed in 64-key tiles.
+// dQ. Workgroup = 4 waves = 128 query rows of one (b, h); K/V streamed in 64-key tiles,
+// double-buffered.
 template <int D, bool CAUSAL>
-__global__ __launch_bounds__(256) void bwd_dq_kernel(
+__global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dq_kernel(
     const bf16* __restrict__ Q, const bf16* __restrict__ K, const bf16* __restrict__ V,
     const bf16* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ DELTA,
     bf16* __restrict__ dQ, int B, int H, int Hkv, int S, Strides qs, Strides ks_, Strides vs,
     Strides dos, Strides dqs, float scale) {
-  __shared__ __attribute__((aligned(16))) char lds[2 * kTile * D * 2];
-  char* k_lds = lds;
-  char* v_lds = lds + kTile * D * 2;
+  using G = Geo<D>;
+  __shared__ __attribute__((aligned(16))) char lds[2 * 2 * G::TB];
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5;
   const int nqb = S / kBlockRows;
@@ -472,7 +495,9 @@ __global__ __launch_bounds__(256) void bwd_dq_kernel(
   const int qw = q0 + 32 * w;
   const int my_q = qw + (lane & 31);
 
-  bf16x8 qf[D / 16], dof[D / 16];
+  Frag<D> fr;
+  fr.init(lane);
+  bf16x8 qf[G::KS], dof[G::KS];
   load_reg_frags<D>(Q + b * qs.sb + hq * qs.sh, qs.ss, qw, lane, qf);
   load_reg_frags<D>(dO + b * dos.sb + hq * dos.sh, dos.ss, qw, lane, dof);
   const float lse2 = LSE[((int64_t)b * H + hq) * S + my_q] * kLog2e;
@@ -482,40 +507,45 @@ __global__ __launch_bounds__(256) void bwd_dq_kernel(
   const bf16* Kb = K + b * ks_.sb + hk * ks_.sh;
   const bf16* Vb = V + b * vs.sb + hk * vs.sh;
 
-  f32x16 dq[D / 32];
+  f32x16 dq[G::DT];
 #pragma unroll
-  for (int t = 0; t < D / 32; ++t) dq[t] = zero16();
+  for (int t = 0; t < G::DT; ++t) dq[t] = zero16();
 
   const int kend = CAUSAL ? (q0 + kBlockRows) : S;
   const int ntiles = kend / kTile;
   Stage<D> sk, sv;
-  sk.load(Kb, ks_.ss, 0, S);
-  sv.load(Vb, vs.ss, 0, S);
-  sk.store(k_lds);
-  sv.store(v_lds);
+  sk.init(ks_.ss);
+  sv.init(vs.ss);
+  sk.load(Kb);
+  sv.load(Vb);
+  sk.store(lds);
+  sv.store(lds + G::TB);
   __syncthreads();
 
   for (int t = 0; t < ntiles; ++t) {
     const int kb = t * kTile;
     const bool more = t + 1 < ntiles;
+    const char* kt = lds + (t & 1) * 2 * G::TB;
+    const char* vt = kt + G::TB;
     if (more) {
-      sk.load(Kb, ks_.ss, kb + kTile, S);
-      sv.load(Vb, vs.ss, kb + kTile, S);
+      sk.load(Kb + (int64_t)(kb + kTile) * ks_.ss);
+      sv.load(Vb + (int64_t)(kb + kTile) * vs.ss);
     }
 #pragma unroll
     for (int tt = 0; tt < 2; ++tt) {
-      if (CAUSAL && kb + 32 * tt > qw + 31) continue;
+      const int ksub = kb + 32 * tt;
+      if (CAUSAL && ksub > qw + 31) continue;
       f32x16 st = zero16(), dpt = zero16();
 #pragma unroll
-      for (int kk = 0; kk < D / 16; ++kk) {
-        st = mfma(row_frag<D>(k_lds, 32 * tt, kk, lane), qf[kk], st);
-        dpt = mfma(row_frag<D>(v_lds, 32 * tt, kk, lane), dof[kk], dpt);
+      for (int kk = 0; kk < G::KS; ++kk) {
+        st = mfma(fr.rowf(kt, 32 * tt, kk), qf[kk], st);
+        dpt = mfma(fr.rowf(vt, 32 * tt, kk), dof[kk], dpt);
       }
+      const bool diag = CAUSAL && ksub + 31 > qw;
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        const int key = kb + 32 * tt + acc_row(i, h);
-        float p = exp2f(st[i] * c2 - lse2);
-        if (CAUSAL && key > my_q) p = 0.f;
+        float p = fexp2(fmaf(st[i], c2, -lse2));
+        if (diag && ksub + acc_row(i, h) > my_q) p = 0.f;
         dpt[i] = p * (dpt[i] - dl);  // dS^T
       }
       // dQ^T[d, q] += K^T[d, keys] . dS^T[keys, q]
@@ -523,22 +553,20 @@ __global__ __launch_bounds__(256) void bwd_dq_kernel(
       for (int s = 0; s < 2; ++s) {
         const bf16x8 db = pack8(dpt, s);
 #pragma unroll
-        for (int dt = 0; dt < D / 32; ++dt)
-          dq[dt] = mfma(tr_frag<D>(k_lds, 32 * tt, s, 32 * dt, lane), db, dq[dt]);
+        for (int dt = 0; dt < G::DT; ++dt) dq[dt] = mfma(fr.trf(kt, 32 * tt, s, dt), db, dq[dt]);
       }
     }
-    __syncthreads();
     if (more) {
-      sk.store(k_lds);
-      sv.store(v_lds);
+      char* nk = lds + ((t + 1) & 1) * 2 * G::TB;
+      sk.store(nk);
+      sv.store(nk + G::TB);
     }
     __syncthreads();
   }
 
   bf16* dQb = dQ + b * dqs.sb + hq * dqs.sh + (int64_t)my_q * dqs.ss;
-  using bf4 = __attribute__((ext_vector_type(4))) __bf16;
 #pragma unroll
-  for (int dt = 0; dt < D / 32; ++dt) {
+  for (int dt = 0; dt < G::DT; ++dt) {
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       bf4 a;
