@@ -85,18 +85,19 @@ def build_kernels(verbose=False, jobs=None):
         objs.append(obj)
         if _newer([src] + hdrs, obj):
             jobs_list.append([HIPCC] + common + ["-c", src, "-o", obj])
-    # Bindings: host-only C++ that includes ATen; compiled by hipcc so HIP headers resolve.
-    bsrc = os.path.join(CSRC, "bindings.cpp")
-    bobj = os.path.join(BUILD, "bindings.o")
-    objs.append(bobj)
-    if _newer([bsrc] + hdrs, bobj):
-        binc = []
-        for d in incs + _py_includes():
-            binc += ["-I", d]
-        jobs_list.append([HIPCC, "-O2", "-std=c++17", "-fPIC", "-D__HIP_PLATFORM_AMD__", "-DUSE_ROCM",
-                          f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-DTORCH_EXTENSION_NAME=_C",
-                          "-DTORCH_API_INCLUDE_EXTENSION_H", "-I", CSRC, "-Wno-deprecated-declarations",
-                          "-Wno-unused-result"] + binc + ["-c", bsrc, "-o", bobj])
+    # Host TUs that include ATen (bindings, hipBLASLt plans): compiled by hipcc so HIP headers
+    # resolve; no device code in them.
+    binc = []
+    for d in incs + _py_includes():
+        binc += ["-I", d]
+    for bsrc in sorted(glob.glob(os.path.join(CSRC, "*.cpp"))):
+        bobj = os.path.join(BUILD, os.path.basename(bsrc) + ".o")
+        objs.append(bobj)
+        if _newer([bsrc] + hdrs, bobj):
+            jobs_list.append([HIPCC, "-O2", "-std=c++17", "-fPIC", "-D__HIP_PLATFORM_AMD__", "-DUSE_ROCM",
+                              f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-DTORCH_EXTENSION_NAME=_C",
+                              "-DTORCH_API_INCLUDE_EXTENSION_H", "-I", CSRC, "-Wno-deprecated-declarations",
+                              "-Wno-unused-result"] + binc + ["-c", bsrc, "-o", bobj])
     jobs = jobs or min(8, os.cpu_count() or 4)
     with cf.ThreadPoolExecutor(jobs) as ex:
         list(ex.map(lambda c: _run(c, verbose), jobs_list))
@@ -104,6 +105,7 @@ def build_kernels(verbose=False, jobs=None):
     if jobs_list or not os.path.exists(out):
         link = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", out] + objs + [
             "-L", libdir, "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python",
+            "-l:libhipblaslt.so",
             f"-Wl,-rpath,{libdir}"]
         _run(link, verbose)
     return out

@@ -381,8 +381,11 @@ std::vector<Tensor> flash_bwd(Tensor q, Tensor k, Tensor v, Tensor o, Tensor dou
 
 }  // namespace
 
+void register_blaslt(pybind11::module_& m);
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "smdt_amd gfx950 (MI355X) HIP kernel library";
+  register_blaslt(m);
   m.def("layernorm_fwd", &layernorm_fwd);
   m.def("layernorm_bwd", &layernorm_bwd);
   m.def("bias_act_fwd", &bias_act_fwd);

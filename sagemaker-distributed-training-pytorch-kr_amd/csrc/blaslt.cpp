@@ -1,0 +1,116 @@
+// hipBLASLt GEMMs the framework needs that torch cannot express as ONE library call.
+//
+// wgrad_accumulate: main_grad(fp32, [N, K]) += dy(bf16/fp16, [M, N])^T . x([M, K]) in a single
+// hipBLASLt matmul with C = D = main_grad and beta = 1 (Megatron's gradient-accumulation fusion,
+// `fused_weight_gradient_mlp_cuda`; flag `--no-gradient-accumulation-fusion` at
+// /root/reference/3_training_megatron-lm/megatron/arguments.py:850-854). torch's
+// `addmm(out_dtype=fp32)` lowers to an fp32-output GEMM followed by a separate add kernel, i.e.
+// one extra read+write of every fp32 gradient per micro-batch; this path removes it.
+//
+// Plain library GEMM (the hot fused ops are hand-written HIP); descriptors and the heuristic's
+// algorithm are cached per (device, shape, dtype).
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <hipblaslt/hipblaslt.h>
+
+#include <map>
+#include <mutex>
+#include <tuple>
+
+namespace {
+
+struct Plan {
+  hipblasLtMatmulDesc_t desc = nullptr;
+  hipblasLtMatrixLayout_t la = nullptr, lb = nullptr, lc = nullptr;
+  hipblasLtMatmulAlgo_t algo;
+  size_t ws = 0;
+  bool ok = false;
+};
+
+struct DevState {
+  hipblasLtHandle_t handle = nullptr;
+  torch::Tensor workspace;
+  std::map<std::tuple<int64_t, int64_t, int64_t, int>, Plan> plans;
+};
+
+std::mutex g_mu;
+std::map<int, DevState> g_state;
+constexpr size_t kWorkspace = 64ull << 20;
+
+bool chk(hipblasStatus_t s) { return s == HIPBLAS_STATUS_SUCCESS; }
+
+DevState& state_for(int dev, const torch::TensorOptions& opts) {
+  auto& st = g_state[dev];
+  if (!st.handle) {
+    TORCH_CHECK(chk(hipblasLtCreate(&st.handle)), "hipblasLtCreate failed");
+    st.workspace = torch::empty({(int64_t)kWorkspace}, opts.dtype(at::kByte));
+  }
+  return st;
+}
+
+Plan make_plan(DevState& st, int64_t M, int64_t N, int64_t K, hipDataType in_t) {
+  // Column-major view: D[K x N] (ld K) = A[K x M] (x, ld K) . op(B) with B[N x M] (dy, ld N), op = T.
+  Plan p;
+  if (!chk(hipblasLtMatmulDescCreate(&p.desc, HIPBLAS_COMPUTE_32F, HIP_R_32F))) return p;
+  hipblasOperation_t ta = HIPBLAS_OP_N, tb = HIPBLAS_OP_T;
+  hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_TRANSA, &ta, sizeof(ta));
+  hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_TRANSB, &tb, sizeof(tb));
+  if (!chk(hipblasLtMatrixLayoutCreate(&p.la, in_t, K, M, K))) return p;
+  if (!chk(hipblasLtMatrixLayoutCreate(&p.lb, in_t, N, M, N))) return p;
+  if (!chk(hipblasLtMatrixLayoutCreate(&p.lc, HIP_R_32F, K, N, K))) return p;
+  hipblasLtMatmulPreference_t pref;
+  if (!chk(hipblasLtMatmulPreferenceCreate(&pref))) return p;
+  size_t ws = kWorkspace;
+  hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &ws, sizeof(ws));
+  hipblasLtMatmulHeuristicResult_t res[8];
+  int n = 0;
+  hipblasStatus_t s = hipblasLtMatmulAlgoGetHeuristic(st.handle, p.desc, p.la, p.lb, p.lc, p.lc, pref, 8, res, &n);
+  hipblasLtMatmulPreferenceDestroy(pref);
+  if (!chk(s) || n <= 0) return p;
+  for (int i = 0; i < n; ++i) {
+    if (res[i].state == HIPBLAS_STATUS_SUCCESS && res[i].workspaceSize <= kWorkspace) {
+      p.algo = res[i].algo;
+      p.ws = res[i].workspaceSize;
+      p.ok = true;
+      break;
+    }
+  }
+  return p;
+}
+
+// Returns false (and does nothing) when the shape/dtype is unsupported so the caller can fall
+// back; raises on a failed launch.
+bool wgrad_accumulate(torch::Tensor main_grad, torch::Tensor dy, torch::Tensor x) {
+  if (!main_grad.is_cuda() || main_grad.scalar_type() != at::kFloat || !main_grad.is_contiguous()) return false;
+  if (dy.dim() != 2 || x.dim() != 2 || !dy.is_contiguous() || !x.is_contiguous()) return false;
+  if (dy.scalar_type() != x.scalar_type()) return false;
+  hipDataType in_t;
+  if (dy.scalar_type() == at::kBFloat16) in_t = HIP_R_16BF;
+  else if (dy.scalar_type() == at::kHalf) in_t = HIP_R_16F;
+  else return false;
+  const int64_t M = dy.size(0), N = dy.size(1), K = x.size(1);
+  if (x.size(0) != M || main_grad.numel() != N * K) return false;
+  std::lock_guard<std::mutex> lk(g_mu);
+  const int dev = main_grad.get_device();
+  DevState& st = state_for(dev, main_grad.options());
+  auto key = std::make_tuple(M, N, K, (int)in_t);
+  auto it = st.plans.find(key);
+  if (it == st.plans.end()) it = st.plans.emplace(key, make_plan(st, M, N, K, in_t)).first;
+  Plan& p = it->second;
+  if (!p.ok) return false;
+  const float alpha = 1.f, beta = 1.f;
+  hipStream_t stream = c10::hip::getCurrentHIPStream().stream();
+  hipblasStatus_t s = hipblasLtMatmul(st.handle, p.desc, &alpha, x.data_ptr(), p.la, dy.data_ptr(), p.lb, &beta,
+                                      main_grad.data_ptr(), p.lc, main_grad.data_ptr(), p.lc, &p.algo,
+                                      st.workspace.data_ptr(), p.ws, stream);
+  TORCH_CHECK(chk(s), "hipblasLtMatmul (wgrad_accumulate) failed: status ", (int)s);
+  return true;
+}
+
+}  // namespace
+
+void register_blaslt(pybind11::module_& m) {
+  m.def("wgrad_accumulate", &wgrad_accumulate,
+        "main_grad(fp32 [N,K]) += dy([M,N])^T @ x([M,K]) in one hipBLASLt GEMM (beta = 1); "
+        "returns False if unsupported");
+}

@@ -43,7 +43,7 @@ int decode_status(int st) {
 // Returns (job_status, per-rank statuses, first_failed_rank or -1).
 py::tuple run_ranks(const std::vector<std::vector<std::string>>& argvs,
                     const std::vector<std::vector<std::string>>& envs, double grace, double max_run,
-                    const std::string& cwd) {
+                    const std::string& cwd, int out_fd) {
   const size_t n = argvs.size();
   if (n == 0 || envs.size() != n) throw std::invalid_argument("run_ranks: need one argv and one env per rank");
   std::vector<pid_t> pids(n, -1);
@@ -70,6 +70,11 @@ py::tuple run_ranks(const std::vector<std::vector<std::string>>& argvs,
       signal(SIGINT, SIG_DFL);
       signal(SIGTERM, SIG_DFL);
       if (!cwd.empty() && chdir(cwd.c_str()) != 0) _exit(126);
+      if (out_fd >= 0) {  // merge the rank's stdout/stderr into the supervisor's log pipe
+        dup2(out_fd, 1);
+        dup2(out_fd, 2);
+        if (out_fd > 2) close(out_fd);
+      }
       execvpe(av[0], av.data(), ev.data());
       _exit(127);
     }
@@ -131,7 +136,7 @@ py::tuple run_ranks(const std::vector<std::vector<std::string>>& argvs,
 
 void register_supervisor(py::module_& m) {
   m.def("run_ranks", &run_ranks, py::arg("argvs"), py::arg("envs"), py::arg("grace") = 10.0,
-        py::arg("max_run") = 0.0, py::arg("cwd") = std::string(),
+        py::arg("max_run") = 0.0, py::arg("cwd") = std::string(), py::arg("out_fd") = -1,
         "Fork/exec one process per rank in a shared process group; fail fast on the first "
         "non-zero exit; returns (job_status, [rank statuses], first_failed_rank).");
 }

@@ -27,6 +27,7 @@ import torch.distributed as dist
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ..ops import _ext
 from . import state as ps
 
 # --------------------------------------------------------------------------------------------
@@ -205,11 +206,12 @@ def _wgrad(weight, g2, t2):
     mg = getattr(weight, "main_grad", None)
     if mg is None:
         return g2.t().matmul(t2)
+    done = False
     if (_FUSED_WGRAD and mg.dtype == torch.float32 and g2.dtype in (torch.bfloat16, torch.float16)
             and g2.is_cuda and mg.is_contiguous()):
-        torch.addmm(mg.view(g2.shape[1], t2.shape[1]), g2.t(), t2, out_dtype=torch.float32,
-                    out=mg.view(g2.shape[1], t2.shape[1]))
-    else:
+        # ONE hipBLASLt GEMM with C = D = main_grad, beta = 1 (see csrc/blaslt.cpp).
+        done = _ext.ext().wgrad_accumulate(mg, g2.contiguous(), t2.contiguous())
+    if not done:
         mg.add_(g2.t().matmul(t2).view_as(mg))
     cb = getattr(weight, "_smdt_grad_ready", None)
     if cb is not None:
