@@ -61,7 +61,28 @@ def parse():
     p.add_argument("--no-flash", action="store_true")
     p.add_argument("--recompute", choices=["none", "full"], default="none")
     p.add_argument("--profile-steps", type=int, default=0)
+    p.add_argument("--tunableop", type=int, default=1,
+                   help="autotune torch's hipBLASLt GEMMs per shape during the (untimed) warmup")
+    p.add_argument("--tune-ms", type=int, default=40)
     return p.parse_args()
+
+
+def enable_gemm_tuning(a, rank):
+    """PyTorch TunableOp: time every hipBLASLt / rocBLAS solution per GEMM shape on first use and
+    keep the fastest (the shapes are fixed, so this completes inside the first warmup step)."""
+    if not (a.tunableop and torch.cuda.is_available()):
+        return False
+    try:
+        import tempfile
+        import torch.cuda.tunable as tun
+        tun.enable(True)
+        tun.tuning_enable(True)
+        tun.set_max_tuning_duration(a.tune_ms)
+        tun.set_filename(os.path.join(tempfile.gettempdir(), f"smdt_tunableop_r{rank}.csv"))
+        return True
+    except Exception as e:  # pragma: no cover
+        print(f"[bench] TunableOp unavailable: {e!r}", file=sys.stderr)
+        return False
 
 
 def main():
@@ -72,6 +93,7 @@ def main():
     n = world
     st = ps.initialize_model_parallel(a.tp, a.pp)
     model_parallel_seed(1234)
+    tuned = enable_gemm_tuning(a, rank)
     dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
     vocab = pad_vocab_size(a.vocab_size, 128, a.tp)
     cfg = TransformerConfig(num_layers=a.num_layers, hidden_size=a.hidden_size,
@@ -119,8 +141,12 @@ def main():
         opt.step(lr)
         return losses
 
+    tw = time.perf_counter()
     for _ in range(a.warmup):
         train_step()
+    if rank == 0:
+        print(f"[bench] warmup ({a.warmup} steps, incl. GEMM autotune) took {time.perf_counter() - tw:.1f}s",
+              file=sys.stderr, flush=True)
     if dist.is_initialized():
         dist.barrier()
     if torch.cuda.is_available():
@@ -163,7 +189,8 @@ def main():
                        "seq_len": S, "micro_batch": mbs, "grad_accum": a.grad_accum,
                        "parallelism": f"tp{a.tp}pp{a.pp}dp{st.dp}" + ("+zero" if zero else ""),
                        "flash_attn": not a.no_flash, "hidden_dropout": a.hidden_dropout,
-                       "attention_dropout": a.attention_dropout, "recompute": a.recompute},
+                       "attention_dropout": a.attention_dropout, "recompute": a.recompute,
+                       "gemm_autotune": tuned},
             "model_tflops_per_gpu": round(tps * fpt / n / 1e12, 2),
             "baseline": "41 model-TFLOP/s/GPU (reference GPT-2-small, 16xA100, BASELINE.md) at equal model FLOPs",
             "final_loss": loss_val,

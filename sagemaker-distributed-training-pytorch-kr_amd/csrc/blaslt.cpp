@@ -62,18 +62,53 @@ Plan make_plan(DevState& st, int64_t M, int64_t N, int64_t K, hipDataType in_t) 
   if (!chk(hipblasLtMatmulPreferenceCreate(&pref))) return p;
   size_t ws = kWorkspace;
   hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &ws, sizeof(ws));
-  hipblasLtMatmulHeuristicResult_t res[8];
+  constexpr int kCand = 16;
+  hipblasLtMatmulHeuristicResult_t res[kCand];
   int n = 0;
-  hipblasStatus_t s = hipblasLtMatmulAlgoGetHeuristic(st.handle, p.desc, p.la, p.lb, p.lc, p.lc, pref, 8, res, &n);
+  hipblasStatus_t s = hipblasLtMatmulAlgoGetHeuristic(st.handle, p.desc, p.la, p.lb, p.lc, p.lc, pref, kCand, res, &n);
   hipblasLtMatmulPreferenceDestroy(pref);
   if (!chk(s) || n <= 0) return p;
+  // Autotune once per shape: the heuristic's first pick is a non-split-K tile that leaves a
+  // long-K / small-output wgrad (K = tokens) at ~1 workgroup per CU; time every candidate on
+  // scratch buffers and keep the fastest.
+  int best = -1;
+  float best_ms = 1e30f;
+  torch::Tensor a = torch::randn({M, K}, torch::TensorOptions().device(torch::kCUDA, st.workspace.get_device()))
+                        .to(in_t == HIP_R_16BF ? at::kBFloat16 : at::kHalf);
+  torch::Tensor b = torch::randn({M, N}, a.options());
+  torch::Tensor c = torch::zeros({N, K}, a.options().dtype(at::kFloat));
+  hipStream_t stream = c10::hip::getCurrentHIPStream().stream();
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0);
+  hipEventCreate(&e1);
+  const float alpha = 1.f, beta = 1.f;
   for (int i = 0; i < n; ++i) {
-    if (res[i].state == HIPBLAS_STATUS_SUCCESS && res[i].workspaceSize <= kWorkspace) {
-      p.algo = res[i].algo;
-      p.ws = res[i].workspaceSize;
-      p.ok = true;
-      break;
+    if (res[i].state != HIPBLAS_STATUS_SUCCESS || res[i].workspaceSize > kWorkspace) continue;
+    bool okc = true;
+    for (int w = 0; w < 2 && okc; ++w)
+      okc = chk(hipblasLtMatmul(st.handle, p.desc, &alpha, a.data_ptr(), p.la, b.data_ptr(), p.lb, &beta, c.data_ptr(),
+                                p.lc, c.data_ptr(), p.lc, &res[i].algo, st.workspace.data_ptr(), res[i].workspaceSize,
+                                stream));
+    if (!okc) continue;
+    hipEventRecord(e0, stream);
+    for (int r = 0; r < 5; ++r)
+      hipblasLtMatmul(st.handle, p.desc, &alpha, a.data_ptr(), p.la, b.data_ptr(), p.lb, &beta, c.data_ptr(), p.lc,
+                      c.data_ptr(), p.lc, &res[i].algo, st.workspace.data_ptr(), res[i].workspaceSize, stream);
+    hipEventRecord(e1, stream);
+    hipEventSynchronize(e1);
+    float ms = 0.f;
+    hipEventElapsedTime(&ms, e0, e1);
+    if (ms < best_ms) {
+      best_ms = ms;
+      best = i;
     }
+  }
+  hipEventDestroy(e0);
+  hipEventDestroy(e1);
+  if (best >= 0) {
+    p.algo = res[best].algo;
+    p.ws = res[best].workspaceSize;
+    p.ok = true;
   }
   return p;
 }

@@ -30,6 +30,7 @@ import torch
 import torch.distributed as dist
 import torch.nn as nn
 
+from ..ops import _ext
 from . import state as ps
 
 
@@ -72,9 +73,17 @@ class DistributedDataParallel(nn.Module):
 
     def __init__(self, module: nn.Module, dp_group=None, grad_dtype=torch.float32, bucket_size: int = 40_000_000,
                  overlap_grad_reduce: bool = True, use_distributed_optimizer: bool = False,
-                 average_in_collective: bool = True):
+                 average_in_collective: bool = True, torch_compat: bool = False):
+        """``torch_compat=True`` gives drop-in ``torch.nn.parallel.DistributedDataParallel``
+        semantics for scripts that drive a stock ``torch.optim`` optimizer: gradient sync is
+        finalised automatically at the end of ``backward()`` (autograd-engine callback),
+        reduced gradients are exposed as ``param.grad`` (views of the flat buffer) and the
+        buffer is re-zeroed by the next forward."""
         super().__init__()
         self.module = module
+        self.torch_compat = torch_compat
+        self._needs_zero = False
+        self._callback_queued = False
         st = ps.get_state()
         self.st = st
         self.dp_group = dp_group if dp_group is not None else st.dp_group
@@ -164,14 +173,34 @@ class DistributedDataParallel(nn.Module):
 
     # ---------------------------------------------------------------- forward
     def forward(self, *args, **kwargs):
+        if self.torch_compat and self._needs_zero and torch.is_grad_enabled():
+            self.grad_data.zero_()
+            self._needs_zero = False
         return self.module(*args, **kwargs)
 
     # ---------------------------------------------------------------- grad plumbing
     def _post_accumulate(self, p):
+        if self.torch_compat and not self._callback_queued:
+            self._callback_queued = True
+            torch.autograd.Variable._execution_engine.queue_callback(self._auto_finalize)
         if p.grad is not None:
-            p.main_grad.add_(p.grad.view_as(p.main_grad))
+            g = p.grad
+            if g.data_ptr() != p.main_grad.data_ptr():
+                if g.is_cuda and g.dtype != p.main_grad.dtype and g.is_contiguous() and _ext.available():
+                    # fused cast + accumulate (torch's mixed-dtype add is a slow generic path)
+                    _ext.ext().cast_(g, p.main_grad, True)
+                else:
+                    p.main_grad.add_(g.view_as(p.main_grad))
             p.grad = None
         self._on_grad_ready(p)
+
+    def _auto_finalize(self):
+        self._callback_queued = False
+        if self.sync_enabled:
+            self.finish_grad_sync()
+            for p in self.params:
+                p.grad = p.main_grad
+            self._needs_zero = True
 
     def _on_grad_ready(self, p):
         b = self.param_bucket.get(id(p))
