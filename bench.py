@@ -64,25 +64,41 @@ def parse():
     p.add_argument("--tunableop", type=int, default=1,
                    help="autotune torch's hipBLASLt GEMMs per shape during the (untimed) warmup")
     p.add_argument("--tune-ms", type=int, default=40)
+    p.add_argument("--tune-out", type=str, default=None)
     return p.parse_args()
 
 
+TUNED_GEMMS = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "tunableop",
+                           "gfx950_gpt345m_results.csv")
+
+
 def enable_gemm_tuning(a, rank):
-    """PyTorch TunableOp: time every hipBLASLt / rocBLAS solution per GEMM shape on first use and
-    keep the fastest (the shapes are fixed, so this completes inside the first warmup step)."""
+    """PyTorch TunableOp over torch's hipBLASLt / rocBLAS GEMMs.
+
+    --tunableop 1 (default): load the per-shape winners measured on MI355X and committed under
+    profiles/tunableop/ (no tuning at run time); tune on first use only if that file is absent.
+    --tunableop 2: re-tune every shape (minutes) and write the results to --tune-out.
+    --tunableop 0: library heuristics only.
+    """
     if not (a.tunableop and torch.cuda.is_available()):
-        return False
+        return "off"
     try:
         import tempfile
         import torch.cuda.tunable as tun
         tun.enable(True)
+        if a.tunableop == 1 and os.path.exists(TUNED_GEMMS):
+            tun.tuning_enable(False)
+            tun.set_filename(os.path.join(tempfile.gettempdir(), f"smdt_tunableop_unused_r{rank}.csv"))
+            ok = tun.read_file(TUNED_GEMMS)
+            return "preloaded" if ok is not False else "preload-failed"
         tun.tuning_enable(True)
         tun.set_max_tuning_duration(a.tune_ms)
-        tun.set_filename(os.path.join(tempfile.gettempdir(), f"smdt_tunableop_r{rank}.csv"))
-        return True
+        out = a.tune_out or os.path.join(tempfile.gettempdir(), "smdt_tunableop_r%d.csv")
+        tun.set_filename(out % rank if "%d" in out else out)
+        return "tuning"
     except Exception as e:  # pragma: no cover
         print(f"[bench] TunableOp unavailable: {e!r}", file=sys.stderr)
-        return False
+        return "unavailable"
 
 
 def main():

@@ -82,6 +82,10 @@ class GPTModel(nn.Module):
                 self.output_weight.shared_embedding = True
         if pre_process and post_process is False and not cfg.untie_embeddings_and_output_weights and st.pp > 1:
             self.embedding.weight.shared_embedding = True
+        if pre_process and post_process and not cfg.untie_embeddings_and_output_weights:
+            # tied LM head on the same stage: the weight receives its gradient twice (fused wgrad
+            # into main_grad + the lookup's autograd accumulation)
+            self.embedding.weight._smdt_grad_contributions = 2
         self.input_tensor = None
         if cfg.position_embedding_type == "rope":
             rot = int(cfg.kv_channels * cfg.rotary_percent)

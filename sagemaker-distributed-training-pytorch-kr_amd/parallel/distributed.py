@@ -41,7 +41,7 @@ class Bucket:
     start: int          # element offset in the flat buffers
     end: int            # (padded) end
     params: List[nn.Parameter] = field(default_factory=list)
-    pending: set = field(default_factory=set)
+    pending: dict = field(default_factory=dict)
     handle: object = None
     launched: bool = False
 
@@ -206,13 +206,20 @@ class DistributedDataParallel(nn.Module):
         b = self.param_bucket.get(id(p))
         if b is None:
             return
-        b.pending.discard(id(p))
+        # A parameter fed by several gradient paths (tied embedding: LM-head wgrad straight into
+        # main_grad + the lookup's autograd accumulation) declares `_smdt_grad_contributions`;
+        # it is ready only after the last one.
+        left = b.pending.get(id(p), 0) - 1
+        if left > 0:
+            b.pending[id(p)] = left
+            return
+        b.pending.pop(id(p), None)
         if self.sync_enabled and self.overlap and not b.pending and not b.launched:
             self._launch(b)
 
     def _reset_pending(self):
         for b in self.buckets:
-            b.pending = {id(p) for p in b.params}
+            b.pending = {id(p): int(getattr(p, "_smdt_grad_contributions", 1)) for p in b.params}
             b.launched = False
             b.handle = None
 

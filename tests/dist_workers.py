@@ -1,0 +1,155 @@
+"""Worker bodies for the multi-process (gloo, CPU) tests. Importable by spawned children."""
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+TINY = dict(num_layers=2, hidden_size=64, num_attention_heads=4, max_position_embeddings=32,
+            padded_vocab_size=128, hidden_dropout=0.0, attention_dropout=0.0, params_dtype=torch.float32,
+            use_flash_attn=True, seed=7)
+
+
+def _batch(seed=0, b=4, s=32, v=128):
+    g = torch.Generator().manual_seed(seed)
+    toks = torch.randint(0, v, (b, s + 1), generator=g)
+    return toks[:, :-1].contiguous(), toks[:, 1:].contiguous()
+
+
+def gpt_reference(steps=1, sp=False, cfg_over=None):
+    """Single-process TP=1 run: per-token loss + named full gradients."""
+    from smdt_amd.models.gpt import GPTModel
+    from smdt_amd.models.transformer import TransformerConfig
+    from smdt_amd.parallel import state as ps
+    ps.destroy_model_parallel()
+    cfg = TransformerConfig(**{**TINY, **(cfg_over or {})})
+    m = GPTModel(cfg)
+    tokens, labels = _batch()
+    loss = m(tokens, None, None, labels=labels)
+    loss.mean().backward()
+    grads = {n: p.grad.detach().clone() for n, p in m.named_parameters() if p.grad is not None}
+    return loss.detach(), grads
+
+
+def gpt_tp_worker(rank, world, tp, pp, sp, cfg_over=None):
+    import torch.distributed as dist
+    from smdt_amd.comm import init_distributed
+    from smdt_amd.models.gpt import GPTModel, allreduce_word_embedding_grads
+    from smdt_amd.models.transformer import TransformerConfig
+    from smdt_amd.parallel import state as ps
+    from smdt_amd.train.schedules import get_forward_backward_func
+    init_distributed("gloo")
+    st = ps.initialize_model_parallel(tp, pp)
+    cfg = TransformerConfig(**{**TINY, **(cfg_over or {}), "sequence_parallel": sp})
+    m = GPTModel(cfg, pre_process=st.is_first_stage(), post_process=st.is_last_stage())
+    tokens, labels = _batch()
+    if pp == 1:
+        loss = m(tokens, None, None, labels=labels)
+        loss.mean().backward()
+        out_loss = loss.detach()
+    else:
+        it = iter([(tokens, labels)] * 4)
+        mb = 2
+        toks_mb = tokens.chunk(2)
+        labs_mb = labels.chunk(2)
+        data = iter(list(zip(toks_mb, labs_mb)))
+
+        def fstep(di, model):
+            t, l = next(di)
+            o = model(t, None, None, labels=l)
+
+            def lf(x):
+                return x.mean(), {"loss": x.detach()}
+            return o, lf
+        fb = get_forward_backward_func()
+        seq = 32 // tp if sp else 32
+        res = fb(fstep, data, m, 2, tensor_shape=(seq, mb, 64), dtype=torch.float32)
+        allreduce_word_embedding_grads(m)
+        out_loss = torch.cat([r["loss"] for r in res]) if res else None
+    grads = {n: p.grad.detach().clone() for n, p in m.named_parameters() if p.grad is not None}
+    # sequence-parallel replicated params: sum partial grads over TP (what the DDP wrapper does)
+    if sp and tp > 1:
+        for n, p in m.named_parameters():
+            if getattr(p, "sequence_parallel", False) and n in grads:
+                dist.all_reduce(grads[n], group=st.tp_group)
+    meta = {"tp_rank": st.tp_rank, "pp_rank": st.pp_rank, "first": st.first_layer if hasattr(st, "first_layer") else None,
+            "layer_offset": m.first_layer}
+    dist.destroy_process_group()
+    return out_loss, grads, meta
+
+
+def ddp_worker(rank, world, zero, steps=3):
+    """DDP (+ZeRO) on a tiny GPT: returns final params after `steps` optimizer steps on a
+    per-rank shard of a fixed global batch (so the result must equal single-process training on
+    the whole batch)."""
+    import torch.distributed as dist
+    from smdt_amd.comm import init_distributed
+    from smdt_amd.models.gpt import GPTModel
+    from smdt_amd.models.transformer import TransformerConfig
+    from smdt_amd.optim.optimizer import MixedPrecisionAdam
+    from smdt_amd.parallel import state as ps
+    from smdt_amd.parallel.distributed import DistributedDataParallel
+    init_distributed("gloo")
+    ps.initialize_model_parallel(1, 1)
+    cfg = TransformerConfig(**TINY)
+    m = GPTModel(cfg)
+    ddp = DistributedDataParallel(m, bucket_size=20000, use_distributed_optimizer=zero)
+    opt = MixedPrecisionAdam(ddp, lr=1e-2, weight_decay=0.1, clip_grad=1.0)
+    tokens, labels = _batch(b=4)
+    shard = slice(rank * (4 // world), (rank + 1) * (4 // world))
+    first_grads = None
+    for _ in range(steps):
+        ddp.zero_grad_buffer()
+        loss = ddp(tokens[shard], None, None, labels=labels[shard]).mean()
+        loss.backward()
+        ddp.finish_grad_sync()
+        if first_grads is None:
+            if zero:  # only this rank's shard of each bucket is reduced: gather for comparison
+                full = ddp.grad_data.clone()
+                for b in ddp.buckets:
+                    s, e = ddp.shard_range(b)
+                    dist.all_gather_into_tensor(full[b.start:b.end], ddp.grad_data[s:e].clone())
+            else:
+                full = ddp.grad_data.clone()
+            first_grads = {n: full[ddp.param_index[id(p)][0]:ddp.param_index[id(p)][0] + p.numel()].view_as(p).clone()
+                           for n, p in m.named_parameters()}
+        opt.step()
+    out = {n: p.detach().clone() for n, p in m.named_parameters()}
+    dist.destroy_process_group()
+    return out, first_grads
+
+
+def single_train(steps=3):
+    from smdt_amd.models.gpt import GPTModel
+    from smdt_amd.models.transformer import TransformerConfig
+    from smdt_amd.optim.optimizer import MixedPrecisionAdam
+    from smdt_amd.parallel import state as ps
+    from smdt_amd.parallel.distributed import DistributedDataParallel
+    ps.destroy_model_parallel()
+    cfg = TransformerConfig(**TINY)
+    m = GPTModel(cfg)
+    ddp = DistributedDataParallel(m, bucket_size=20000)
+    opt = MixedPrecisionAdam(ddp, lr=1e-2, weight_decay=0.1, clip_grad=1.0)
+    tokens, labels = _batch(b=4)
+    first_grads = None
+    for _ in range(steps):
+        ddp.zero_grad_buffer()
+        loss = ddp(tokens, None, None, labels=labels).mean()
+        loss.backward()
+        ddp.finish_grad_sync()
+        if first_grads is None:
+            first_grads = {n: p.main_grad.detach().clone() for n, p in m.named_parameters()}
+        opt.step()
+    return {n: p.detach().clone() for n, p in m.named_parameters()}, first_grads
+
+
+def mnist_ddp_worker(rank, world, data_dir, model_dir):
+    os.environ["SM_MODEL_DIR"] = model_dir
+    os.environ["SM_CHANNEL_TRAINING"] = data_dir
+    sys.path.insert(0, os.path.join(ROOT, "recipes", "1_training_mnist_ddp"))
+    import pytorch_mnist_ddp
+    acc = pytorch_mnist_ddp.main(["--epochs", "1", "--backend", "gloo", "--log-interval", "20", "--save-model"])
+    return acc
