@@ -279,7 +279,7 @@ void rope_(Tensor x, Tensor cos_t, Tensor sin_t, int64_t rot, int64_t pos_div, i
 }
 
 // ------------------------------------------------------------------ cross entropy
-std::vector<Tensor> ce_stats(Tensor logits, Tensor target, int64_t vstart) {
+std::vector<Tensor> ce_stats(Tensor logits, Tensor target, int64_t vstart, int64_t vvalid) {
   need_contig(logits, "logits");
   need_contig(target, "target");
   TORCH_CHECK(target.scalar_type() == at::kLong, "ce: int64 targets");
@@ -288,14 +288,14 @@ std::vector<Tensor> ce_stats(Tensor logits, Tensor target, int64_t vstart) {
   auto f32 = logits.options().dtype(at::kFloat);
   auto mx = torch::empty({rows}, f32), se = torch::empty({rows}, f32), tg = torch::empty({rows}, f32);
   check(smdt_ce_stats(dcode(logits), logits.data_ptr(), target.data_ptr<int64_t>(), rows, (int)V,
-                      vstart, mx.data_ptr<float>(), se.data_ptr<float>(), tg.data_ptr<float>(),
+                      (int)(vvalid > 0 ? vvalid : V), vstart, mx.data_ptr<float>(), se.data_ptr<float>(), tg.data_ptr<float>(),
                       cur_stream()),
         "ce_stats");
   return {mx, se, tg};
 }
 
 void ce_bwd(Tensor logits, Tensor target, Tensor gmax, Tensor gsum, Tensor dloss, Tensor out,
-            int64_t vstart, int64_t ignore_index) {
+            int64_t vstart, int64_t ignore_index, int64_t vvalid) {
   need_contig(logits, "logits");
   need_contig(out, "dlogits");
   TORCH_CHECK(out.sizes() == logits.sizes() && out.dtype() == logits.dtype(), "ce_bwd: out mismatch");
@@ -306,7 +306,8 @@ void ce_bwd(Tensor logits, Tensor target, Tensor gmax, Tensor gsum, Tensor dloss
   }
   check(smdt_ce_bwd(dcode(logits), logits.data_ptr(), target.data_ptr<int64_t>(),
                     gmax.data_ptr<float>(), gsum.data_ptr<float>(), dloss.data_ptr<float>(),
-                    out.data_ptr(), rows, (int)V, vstart, ignore_index, cur_stream()),
+                    out.data_ptr(), rows, (int)V, (int)(vvalid > 0 ? vvalid : V), vstart,
+                    ignore_index, cur_stream()),
         "ce_bwd");
 }
 

@@ -9,7 +9,9 @@
 // picks up the target logit when the target falls in this rank's vocab slice. The three
 // per-row statistics are what the tensor-parallel path all-reduces (MAX, then SUM, SUM).
 // Backward writes (softmax - onehot) * dloss straight into the gradient buffer, which may
-// alias the logits (in-place, no extra [tokens, V] allocation).
+// alias the logits (in-place, no extra [tokens, V] allocation). Columns >= Vvalid are vocab
+// padding (HF models whose vocab is padded to a multiple of 128): they count as -inf and get a
+// zero gradient.
 #include "common.h"
 #include "launchers.h"
 
@@ -18,7 +20,8 @@ namespace smdt {
 template <typename T>
 __global__ __launch_bounds__(256) void ce_stats_kernel(const T* __restrict__ logits,
                                                        const int64_t* __restrict__ target,
-                                                       int64_t rows, int V, int64_t vstart,
+                                                       int64_t rows, int V, int Vvalid,
+                                                       int64_t vstart,
                                                        float* __restrict__ row_max,
                                                        float* __restrict__ row_sumexp,
                                                        float* __restrict__ row_tgt) {
@@ -28,10 +31,15 @@ __global__ __launch_bounds__(256) void ce_stats_kernel(const T* __restrict__ log
   const T* lr = logits + row * V;
   float m = -INFINITY, s = 0.f;
   constexpr int VE = 8;
-  const int nvec = V / VE;
+  const int nvec = (Vvalid + VE - 1) / VE;  // vectors holding >= 1 real column (V % 8 == 0)
   for (int i = threadIdx.x; i < nvec; i += 256) {
     float v[VE];
     load_vec<T, VE>(lr + i * VE, v);
+    if ((i + 1) * VE > Vvalid) {
+#pragma unroll
+      for (int j = 0; j < VE; ++j)
+        if (i * VE + j >= Vvalid) v[j] = -INFINITY;
+    }
     float lm = v[0];
 #pragma unroll
     for (int j = 1; j < VE; ++j) lm = fmaxf(lm, v[j]);
@@ -39,13 +47,13 @@ __global__ __launch_bounds__(256) void ce_stats_kernel(const T* __restrict__ log
     float acc = 0.f;
 #pragma unroll
     for (int j = 0; j < VE; ++j) acc += __expf(v[j] - nm);
-    s = s * __expf(m - nm) + acc;
+    s = (m == -INFINITY ? 0.f : s * __expf(m - nm)) + acc;
     m = nm;
   }
-  for (int i = nvec * VE + threadIdx.x; i < V; i += 256) {
+  for (int i = nvec * VE + threadIdx.x; i < Vvalid; i += 256) {
     float v = to_f32(lr[i]);
     float nm = fmaxf(m, v);
-    s = s * __expf(m - nm) + __expf(v - nm);
+    s = (m == -INFINITY ? 0.f : s * __expf(m - nm)) + __expf(v - nm);
     m = nm;
   }
   // Merge (m, s) pairs: wave level then block level.
@@ -72,7 +80,7 @@ __global__ __launch_bounds__(256) void ce_stats_kernel(const T* __restrict__ log
     row_max[row] = M;
     row_sumexp[row] = S;
     int64_t t = target[row] - vstart;
-    row_tgt[row] = (t >= 0 && t < V) ? to_f32(lr[t]) : 0.f;
+    row_tgt[row] = (t >= 0 && t < Vvalid) ? to_f32(lr[t]) : 0.f;
   }
 }
 
@@ -84,7 +92,8 @@ __global__ __launch_bounds__(256) void ce_bwd_kernel(const T* __restrict__ logit
                                                      const float* __restrict__ gsum,
                                                      const float* __restrict__ dloss,
                                                      T* __restrict__ dlogits, int64_t rows, int V,
-                                                     int64_t vstart, int64_t ignore_index) {
+                                                     int Vvalid, int64_t vstart,
+                                                     int64_t ignore_index) {
   const int64_t row = blockIdx.x;
   if (row >= rows) return;
   const T* lr = logits + row * V;
@@ -101,14 +110,14 @@ __global__ __launch_bounds__(256) void ce_bwd_kernel(const T* __restrict__ logit
     load_vec<T, VE>(lr + i * VE, v);
 #pragma unroll
     for (int j = 0; j < VE; ++j) {
-      float p = __expf(v[j] - M) * inv;
+      float p = i * VE + j < Vvalid ? __expf(v[j] - M) * inv : 0.f;
       if (i * VE + j == t) p -= 1.f;
       v[j] = p * g;
     }
     store_vec<T, VE>(dr + i * VE, v);
   }
   for (int i = nvec * VE + threadIdx.x; i < V; i += 256) {
-    float p = __expf(to_f32(lr[i]) - M) * inv;
+    float p = i < Vvalid ? __expf(to_f32(lr[i]) - M) * inv : 0.f;
     if (i == t) p -= 1.f;
     dr[i] = from_f32<T>(p * g);
   }
@@ -119,22 +128,23 @@ __global__ __launch_bounds__(256) void ce_bwd_kernel(const T* __restrict__ logit
 using namespace smdt;
 
 extern "C" hipError_t smdt_ce_stats(int dtype, const void* logits, const int64_t* target,
-                                    int64_t rows, int V, int64_t vstart, float* row_max,
-                                    float* row_sumexp, float* row_tgt, hipStream_t st) {
-  if (V % 8 != 0) return hipErrorInvalidValue;
-  if (dtype == 1) hipLaunchKernelGGL(ce_stats_kernel<bf16>, dim3(rows), dim3(256), 0, st, (const bf16*)logits, target, rows, V, vstart, row_max, row_sumexp, row_tgt);
-  else if (dtype == 2) hipLaunchKernelGGL(ce_stats_kernel<f16>, dim3(rows), dim3(256), 0, st, (const f16*)logits, target, rows, V, vstart, row_max, row_sumexp, row_tgt);
-  else hipLaunchKernelGGL(ce_stats_kernel<float>, dim3(rows), dim3(256), 0, st, (const float*)logits, target, rows, V, vstart, row_max, row_sumexp, row_tgt);
+                                    int64_t rows, int V, int Vvalid, int64_t vstart,
+                                    float* row_max, float* row_sumexp, float* row_tgt,
+                                    hipStream_t st) {
+  if (V % 8 != 0 || Vvalid < 1 || Vvalid > V) return hipErrorInvalidValue;
+  if (dtype == 1) hipLaunchKernelGGL(ce_stats_kernel<bf16>, dim3(rows), dim3(256), 0, st, (const bf16*)logits, target, rows, V, Vvalid, vstart, row_max, row_sumexp, row_tgt);
+  else if (dtype == 2) hipLaunchKernelGGL(ce_stats_kernel<f16>, dim3(rows), dim3(256), 0, st, (const f16*)logits, target, rows, V, Vvalid, vstart, row_max, row_sumexp, row_tgt);
+  else hipLaunchKernelGGL(ce_stats_kernel<float>, dim3(rows), dim3(256), 0, st, (const float*)logits, target, rows, V, Vvalid, vstart, row_max, row_sumexp, row_tgt);
   return hipGetLastError();
 }
 
 extern "C" hipError_t smdt_ce_bwd(int dtype, const void* logits, const int64_t* target,
                                   const float* gmax, const float* gsum, const float* dloss,
-                                  void* dlogits, int64_t rows, int V, int64_t vstart,
-                                  int64_t ignore_index, hipStream_t st) {
-  if (V % 8 != 0) return hipErrorInvalidValue;
-  if (dtype == 1) hipLaunchKernelGGL(ce_bwd_kernel<bf16>, dim3(rows), dim3(256), 0, st, (const bf16*)logits, target, gmax, gsum, dloss, (bf16*)dlogits, rows, V, vstart, ignore_index);
-  else if (dtype == 2) hipLaunchKernelGGL(ce_bwd_kernel<f16>, dim3(rows), dim3(256), 0, st, (const f16*)logits, target, gmax, gsum, dloss, (f16*)dlogits, rows, V, vstart, ignore_index);
-  else hipLaunchKernelGGL(ce_bwd_kernel<float>, dim3(rows), dim3(256), 0, st, (const float*)logits, target, gmax, gsum, dloss, (float*)dlogits, rows, V, vstart, ignore_index);
+                                  void* dlogits, int64_t rows, int V, int Vvalid,
+                                  int64_t vstart, int64_t ignore_index, hipStream_t st) {
+  if (V % 8 != 0 || Vvalid < 1 || Vvalid > V) return hipErrorInvalidValue;
+  if (dtype == 1) hipLaunchKernelGGL(ce_bwd_kernel<bf16>, dim3(rows), dim3(256), 0, st, (const bf16*)logits, target, gmax, gsum, dloss, (bf16*)dlogits, rows, V, Vvalid, vstart, ignore_index);
+  else if (dtype == 2) hipLaunchKernelGGL(ce_bwd_kernel<f16>, dim3(rows), dim3(256), 0, st, (const f16*)logits, target, gmax, gsum, dloss, (f16*)dlogits, rows, V, Vvalid, vstart, ignore_index);
+  else hipLaunchKernelGGL(ce_bwd_kernel<float>, dim3(rows), dim3(256), 0, st, (const float*)logits, target, gmax, gsum, dloss, (float*)dlogits, rows, V, Vvalid, vstart, ignore_index);
   return hipGetLastError();
 }

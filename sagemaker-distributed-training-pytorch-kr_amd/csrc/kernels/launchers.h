@@ -65,11 +65,11 @@ hipError_t smdt_rope(int dtype, void* x, int64_t ntok, int nh, int64_t tok_strid
 
 // cross_entropy.hip
 hipError_t smdt_ce_stats(int dtype, const void* logits, const int64_t* target, int64_t rows,
-                         int V, int64_t vstart, float* row_max, float* row_sumexp,
+                         int V, int Vvalid, int64_t vstart, float* row_max, float* row_sumexp,
                          float* row_tgt, hipStream_t st);
 hipError_t smdt_ce_bwd(int dtype, const void* logits, const int64_t* target, const float* gmax,
                        const float* gsum, const float* dloss, void* dlogits, int64_t rows, int V,
-                       int64_t vstart, int64_t ignore_index, hipStream_t st);
+                       int Vvalid, int64_t vstart, int64_t ignore_index, hipStream_t st);
 
 // flash_attn.hip
 hipError_t smdt_flash_fwd(int dtype, const void* q, const void* k, const void* v, void* o,

@@ -58,7 +58,7 @@ class GPTModel(nn.Module):
                                                        key="embedding.word", seed=cfg.seed,
                                                        params_dtype=cfg.params_dtype, device=device)
             if cfg.position_embedding_type == "learned_absolute":
-                w = tp.init_full_then_shard((cfg.max_position_embeddings, cfg.hidden_size), std,
+                w = tp.init_full_then_shard((cfg.max_position_embeddings + cfg.position_offset, cfg.hidden_size), std,
                                             "embedding.position.weight", cfg.seed, cfg.params_dtype, device, None, 0, 1)
                 self.position_embeddings = nn.Parameter(w)
             else:
@@ -87,6 +87,8 @@ class GPTModel(nn.Module):
             # into main_grad + the lookup's autograd accumulation)
             self.embedding.weight._smdt_grad_contributions = 2
         self.input_tensor = None
+        # > 0: logits columns >= this are vocab padding and are excluded from the loss (HF models)
+        self.loss_vocab_size = 0
         if cfg.position_embedding_type == "rope":
             rot = int(cfg.kv_channels * cfg.rotary_percent)
             rot -= rot % 16
@@ -116,6 +118,8 @@ class GPTModel(nn.Module):
                 e = tp.reduce_from_tensor_model_parallel_region(e)
         if self.position_embeddings is not None:
             pos = position_ids.transpose(0, 1)                   # [s, b]
+            if self.cfg.position_offset:
+                pos = pos + self.cfg.position_offset
             pe = self.position_embeddings[pos]                   # [s, b, h]
             if self.sp:
                 pe = tp.scatter_to_sequence_parallel_region(pe)
@@ -148,7 +152,8 @@ class GPTModel(nn.Module):
         st = ps.get_state()
         vstart = st.tp_rank * (self.cfg.padded_vocab_size // st.tp) if self.parallel_output else 0
         group = st.tp_group if (st.tp > 1 and self.parallel_output) else None
-        loss = SF.cross_entropy(logits, labels.transpose(0, 1), vstart, group, inplace_grad=True)
+        loss = SF.cross_entropy(logits, labels.transpose(0, 1), vstart, group, inplace_grad=True,
+                                vocab_size=self.loss_vocab_size)
         return loss.transpose(0, 1).contiguous()                 # [b, s]
 
 

@@ -47,6 +47,7 @@ class TransformerConfig:
     rotary_percent: float = 1.0
     rotary_base: float = 10000.0
     max_position_embeddings: int = 1024
+    position_offset: int = 0                     # OPT's learned positions start at row 2
     padded_vocab_size: int = 50304
     untie_embeddings_and_output_weights: bool = False
     init_method_std: float = 0.02
@@ -240,6 +241,8 @@ class ParallelMLP(nn.Module):
             h = SF.swiglu(h)
         elif act == "squared_relu":
             h = F.relu(h + b if b is not None else h).pow(2)
+        elif act == "relu":  # OPT
+            h = F.relu(h + b if b is not None else h)
         else:
             raise ValueError(f"unknown activation {act}")
         return self.fc2(h)

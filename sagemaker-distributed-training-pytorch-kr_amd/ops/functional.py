@@ -407,11 +407,11 @@ def apply_rope(x, cos, sin, pos_div: int, pos_mod: int, rot: Optional[int] = Non
 
 class _FusedCE(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, logits, target, vstart, group, ignore_index, inplace_grad):
+    def forward(ctx, logits, target, vstart, group, ignore_index, inplace_grad, vvalid):
         C = _ext.ext()
         lg = logits.contiguous()
         t = target.contiguous().view(-1)
-        mx, se, tg = C.ce_stats(lg.view(-1, lg.shape[-1]), t, vstart)
+        mx, se, tg = C.ce_stats(lg.view(-1, lg.shape[-1]), t, vstart, vvalid)
         if group is not None and torch.distributed.get_world_size(group) > 1:
             gmax = mx.clone()
             torch.distributed.all_reduce(gmax, op=torch.distributed.ReduceOp.MAX, group=group)
@@ -422,41 +422,53 @@ class _FusedCE(torch.autograd.Function):
         loss = torch.log(se) + mx - tg
         loss = torch.where(t == ignore_index, torch.zeros_like(loss), loss)
         ctx.save_for_backward(lg, t, mx, se)
-        ctx.cfg = (vstart, ignore_index, inplace_grad)
+        ctx.cfg = (vstart, ignore_index, inplace_grad, vvalid)
         return loss.view(target.shape)
 
     @staticmethod
     def backward(ctx, dloss):
         lg, t, mx, se = ctx.saved_tensors
-        vstart, ignore_index, inplace_grad = ctx.cfg
+        vstart, ignore_index, inplace_grad, vvalid = ctx.cfg
         C = _ext.ext()
         out = lg if inplace_grad else torch.empty_like(lg)
         C.ce_bwd(lg.view(-1, lg.shape[-1]), t, mx, se, dloss.contiguous().view(-1).float(),
-                 out.view(-1, lg.shape[-1]), vstart, ignore_index)
-        return out, None, None, None, None, None
+                 out.view(-1, lg.shape[-1]), vstart, ignore_index, vvalid)
+        return out, None, None, None, None, None, None
 
 
 def cross_entropy(logits, target, vocab_start: int = 0, group=None, ignore_index: int = -100,
-                  inplace_grad: bool = False):
+                  inplace_grad: bool = False, vocab_size: int = 0):
     """Per-token CE loss (fp32) for logits [..., V_local] holding vocab slice
     [vocab_start, vocab_start + V_local). With ``group`` the logits are vocab-parallel and the
     three per-row statistics are all-reduced (MAX, SUM, SUM) across it.
 
     ``inplace_grad=True`` writes dlogits over the logits buffer (saves a [tokens, V] tensor);
     only valid when nothing else reads the logits after the loss.
+    ``vocab_size`` > 0 marks global columns >= vocab_size as padding (excluded from the softmax,
+    zero gradient) — HF semantics for a vocab padded to a multiple of 128.
     """
+    vvalid = 0
+    if vocab_size > 0:
+        vvalid = min(max(int(vocab_size) - int(vocab_start), 0), logits.shape[-1])
+        assert vvalid > 0, "a vocab shard holds only padding; use a smaller padding multiple"
+        if vvalid == logits.shape[-1]:
+            vvalid = 0
     if _ext.use_kernels(logits) and logits.shape[-1] % 8 == 0:
-        return _FusedCE.apply(logits, target, int(vocab_start), group, int(ignore_index), bool(inplace_grad))
-    return _ce_ref(logits, target, vocab_start, group, ignore_index)
+        return _FusedCE.apply(logits, target, int(vocab_start), group, int(ignore_index), bool(inplace_grad),
+                              vvalid)
+    return _ce_ref(logits, target, vocab_start, group, ignore_index, vvalid)
 
 
 class _CERef(torch.autograd.Function):
     """Vocab-parallel CE in plain PyTorch (CPU path), same math as the fused kernel."""
 
     @staticmethod
-    def forward(ctx, logits, target, vstart, group, ignore_index):
+    def forward(ctx, logits, target, vstart, group, ignore_index, vvalid=0):
         lf = logits.float()
         V = lf.shape[-1]
+        if vvalid:
+            lf = lf.clone()
+            lf[..., vvalid:] = float("-inf")
         mx = lf.max(-1).values
         ws = 1
         if group is not None:
@@ -485,8 +497,8 @@ class _CERef(torch.autograd.Function):
         p = ex / se.unsqueeze(-1)
         oh = torch.zeros_like(p).scatter_(-1, idx.unsqueeze(-1), inr.unsqueeze(-1).float())
         d = (p - oh) * g.masked_fill(ign, 0.0).unsqueeze(-1)
-        return d.to(ctx.dtype), None, None, None, None
+        return d.to(ctx.dtype), None, None, None, None, None
 
 
-def _ce_ref(logits, target, vocab_start, group, ignore_index):
-    return _CERef.apply(logits, target, int(vocab_start), group, int(ignore_index))
+def _ce_ref(logits, target, vocab_start, group, ignore_index, vvalid=0):
+    return _CERef.apply(logits, target, int(vocab_start), group, int(ignore_index), int(vvalid))

@@ -1,0 +1,78 @@
+"""HF-compatible causal LMs: weight conversion and loss parity against ``transformers``.
+
+The Alpaca recipe loads ``AutoModelForCausalLM`` (reference 4_training_alpaca_deepspeed/train.py:214)
+and saves HF checkpoints (train.py:245-246). These tests build tiny OPT / LLaMA(GQA) / GPT-2
+models with our stack, save them in HF layout, load them with ``transformers`` and compare
+losses/logits; then load back and check the round trip.
+"""
+import tempfile
+
+import pytest
+import torch
+
+from smdt_amd.models.hf import HFCausalLM, config_from_hf
+
+transformers = pytest.importorskip("transformers")
+
+CFGS = {
+    "opt": dict(model_type="opt", hidden_size=64, num_hidden_layers=2, num_attention_heads=4, ffn_dim=128,
+                vocab_size=100, max_position_embeddings=64, activation_function="relu", do_layer_norm_before=True,
+                enable_bias=True, word_embed_proj_dim=64, pad_token_id=1, bos_token_id=2, eos_token_id=2),
+    "llama": dict(model_type="llama", hidden_size=64, num_hidden_layers=2, num_attention_heads=4,
+                  num_key_value_heads=2, intermediate_size=96, vocab_size=100, max_position_embeddings=64,
+                  rms_norm_eps=1e-6, rope_theta=10000.0, hidden_act="silu", tie_word_embeddings=False,
+                  bos_token_id=1, eos_token_id=2),
+    "gpt2": dict(model_type="gpt2", n_embd=64, n_layer=2, n_head=4, vocab_size=100, n_positions=64,
+                 activation_function="gelu_new", bos_token_id=0, eos_token_id=0),
+}
+
+
+@pytest.mark.parametrize("kind", sorted(CFGS))
+def test_loss_and_logits_match_transformers(kind):
+    torch.manual_seed(0)
+    m = HFCausalLM(CFGS[kind], params_dtype=torch.float32).eval()
+    ids = torch.randint(0, 100, (2, 16))
+    labels = ids.clone()
+    labels[:, :3] = -100  # prompt tokens masked like the SFT collator
+    with tempfile.TemporaryDirectory() as d:
+        m.save_pretrained(d)
+        ref = transformers.AutoModelForCausalLM.from_pretrained(d, dtype=torch.float32,
+                                                                attn_implementation="eager").eval()
+        back = HFCausalLM.from_pretrained(d, params_dtype=torch.float32).eval()
+    with torch.no_grad():
+        r = ref(input_ids=ids, labels=labels)
+        loss, _ = m(ids, labels=labels)
+        loss2, _ = back(ids, labels=labels)
+        _, logits = m(ids)
+    torch.testing.assert_close(loss, r.loss, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(loss2, r.loss, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(logits, r.logits, rtol=1e-4, atol=1e-4)
+
+
+def test_padded_vocab_excluded_from_loss():
+    m = HFCausalLM(CFGS["opt"], params_dtype=torch.float32)
+    assert m.cfg.padded_vocab_size == 128
+    ids = torch.randint(0, 100, (1, 8))
+    loss, _ = m(ids, labels=ids)
+    loss.backward()
+    g = m.model.embedding.weight.grad
+    # padding rows get no gradient through the LM head (lookups never touch them either)
+    assert g[100:].abs().max() == 0
+
+
+def test_resize_token_embeddings_grows_padded_vocab():
+    m = HFCausalLM(CFGS["llama"], params_dtype=torch.float32)
+    m.resize_token_embeddings(130)
+    assert m.vocab_size == 130 and m.cfg.padded_vocab_size == 256
+    assert m.model.embedding.weight.shape[0] == 256 and m.model.output_weight.shape[0] == 256
+    ids = torch.randint(0, 130, (1, 8))
+    loss, _ = m(ids, labels=ids)
+    assert torch.isfinite(loss)
+
+
+def test_builtin_configs():
+    from smdt_amd.models.hf import BUILTIN
+    c = config_from_hf(BUILTIN["facebook/opt-125m"])
+    assert (c.num_layers, c.hidden_size, c.activation, c.position_offset) == (12, 768, "relu", 2)
+    c = config_from_hf(BUILTIN["llama-7b"])
+    assert (c.num_layers, c.hidden_size, c.ffn_hidden_size, c.normalization) == (32, 4096, 11008, "RMSNorm")

@@ -229,6 +229,23 @@ def test_cross_entropy(V):
     torch.testing.assert_close(logits.grad.float(), lr.grad, atol=2e-3, rtol=5e-2)
 
 
+@pytest.mark.parametrize("vocab", [1000, 1017, 1024 - 8])
+def test_cross_entropy_padded_vocab(vocab):
+    """Columns >= vocab are padding: excluded from the softmax and given zero gradient."""
+    torch.manual_seed(11)
+    N, V = 200, 1024
+    logits = torch.randn(N, V, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    tgt = torch.randint(0, vocab, (N,), device=DEV)
+    loss = SF.cross_entropy(logits, tgt, vocab_size=vocab)
+    lr = logits.detach()[:, :vocab].float().requires_grad_()
+    ref = F.cross_entropy(lr, tgt, reduction="none")
+    torch.testing.assert_close(loss, ref, atol=2e-2, rtol=1e-2)
+    loss.sum().backward()
+    ref.sum().backward()
+    torch.testing.assert_close(logits.grad[:, :vocab].float(), lr.grad, atol=2e-3, rtol=5e-2)
+    assert logits.grad[:, vocab:].abs().max().item() == 0
+
+
 @pytest.mark.parametrize("D", [64, 128])
 @pytest.mark.parametrize("causal", [True, False])
 @pytest.mark.parametrize("heads", [(4, 4), (8, 2)])
