@@ -109,6 +109,7 @@ py::tuple build_blending_indices(py::array_t<double, py::array::c_style | py::ar
 }  // namespace
 
 void register_supervisor(py::module_& m);
+void register_cpu_adam(py::module_& m);
 
 PYBIND11_MODULE(_runtime, m) {
   m.doc() = "smdt_amd host runtime: dataset index builders and the rank supervisor";
@@ -116,4 +117,5 @@ PYBIND11_MODULE(_runtime, m) {
         py::arg("num_epochs"), py::arg("tokens_per_epoch"));
   m.def("build_blending_indices", &build_blending_indices, py::arg("weights"), py::arg("size"));
   register_supervisor(m);
+  register_cpu_adam(m);
 }

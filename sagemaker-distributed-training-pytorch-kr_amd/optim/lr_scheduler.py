@@ -101,7 +101,7 @@ class WarmupDecayLR:
         self.optimizer = optimizer
         self.total = int(total_num_steps)
         self.min_lr, self.max_lr = float(warmup_min_lr), float(warmup_max_lr)
-        self.warm = max(int(warmup_num_steps), 1)
+        self.warm = max(int(warmup_num_steps), 2)  # DeepSpeed clamps to 2 (log warmup divides by log(warm))
         self.warmup_type = warmup_type
         self.last = -1
         self.step()
@@ -114,6 +114,54 @@ class WarmupDecayLR:
                 g = n / self.warm
             return self.min_lr + (self.max_lr - self.min_lr) * g
         return self.max_lr * max(0.0, (self.total - n) / max(1.0, self.total - self.warm))
+
+    def step(self):
+        self.last += 1
+        lr = self.get_lr(self.last)
+        if hasattr(self.optimizer, "lr"):
+            self.optimizer.lr = lr
+        for g in getattr(self.optimizer, "param_groups", []):
+            g["lr"] = lr
+        return lr
+
+    def get_last_lr(self):
+        return [self.get_lr(self.last)]
+
+    def state_dict(self):
+        return {"last": self.last}
+
+    def load_state_dict(self, d):
+        self.last = int(d["last"]) - 1
+        self.step()
+
+
+class LambdaWarmupScheduler:
+    """HF ``get_scheduler`` equivalents (``--lr_scheduler_type``): linear / cosine / constant /
+    constant_with_warmup / polynomial(power 1) with ``num_warmup_steps`` linear warmup from 0."""
+
+    def __init__(self, optimizer, kind: str, base_lr: float, num_warmup_steps: int, num_training_steps: int,
+                 min_lr_ratio: float = 0.0):
+        self.optimizer = optimizer
+        self.kind = kind
+        self.base_lr = float(base_lr)
+        self.warm = int(num_warmup_steps)
+        self.total = max(int(num_training_steps), 1)
+        self.min_ratio = min_lr_ratio
+        self.last = -1
+        self.step()
+
+    def factor(self, n):
+        if n < self.warm:
+            return n / max(1, self.warm)
+        if self.kind in ("constant", "constant_with_warmup"):
+            return 1.0
+        prog = (n - self.warm) / max(1, self.total - self.warm)
+        if self.kind == "cosine":
+            return max(0.0, 0.5 * (1.0 + math.cos(math.pi * prog)))
+        return max(self.min_ratio, 1.0 - prog)      # linear / polynomial
+
+    def get_lr(self, n):
+        return self.base_lr * self.factor(n)
 
     def step(self):
         self.last += 1

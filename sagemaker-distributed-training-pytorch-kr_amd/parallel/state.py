@@ -132,7 +132,12 @@ def initialize_model_parallel(tensor_model_parallel_size: int = 1, pipeline_mode
         if rank in embd:
             st.embd_group, st.embd_ranks = ge, embd
     _STATE = st
+    st.initialized = True
     return st
+
+
+def model_parallel_is_initialized() -> bool:
+    return _STATE is not None and getattr(_STATE, "initialized", False)
 
 
 def get_state() -> ParallelState:

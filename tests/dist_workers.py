@@ -153,3 +153,51 @@ def mnist_ddp_worker(rank, world, data_dir, model_dir):
     import pytorch_mnist_ddp
     acc = pytorch_mnist_ddp.main(["--epochs", "1", "--backend", "gloo", "--log-interval", "20", "--save-model"])
     return acc
+
+
+# ---------------------------------------------------------------------------------- SFT / ZeRO
+SFT_LLAMA = dict(model_type="llama", hidden_size=64, num_hidden_layers=2, num_attention_heads=4,
+                 num_key_value_heads=2, intermediate_size=96, vocab_size=120, max_position_embeddings=64,
+                 rms_norm_eps=1e-6, rope_theta=10000.0, tie_word_embeddings=False)
+
+
+def sft_batches(n=8, b=2, s=16, v=120, seed=3):
+    g = torch.Generator().manual_seed(seed)
+    out = []
+    for _ in range(n):
+        ids = torch.randint(0, v, (b, s), generator=g)
+        lab = ids.clone()
+        lab[:, :4] = -100
+        out.append((ids, lab))
+    return out
+
+
+def zero_sft_worker(rank, world, stage, ga, steps, offload=False):
+    """Data-parallel SFT steps with the ZeroEngine; global batch = world * 2 * ga rows of
+    ``sft_batches``. Returns full params after ``steps`` optimizer steps."""
+    from smdt_amd.comm import init_distributed
+    from smdt_amd.models.hf import HFCausalLM
+    from smdt_amd.parallel import state as ps
+    from smdt_amd.train.zero import ZeroEngine
+    ps.destroy_model_parallel()
+    init_distributed("gloo")
+    ps.initialize_model_parallel(1, 1)
+    torch.manual_seed(0)
+    m = HFCausalLM(SFT_LLAMA, params_dtype=torch.float32)
+    cfg = {"optimizer": {"type": "AdamW", "params": {"lr": 1e-3, "betas": [0.9, 0.99], "eps": 1e-8,
+                                                     "weight_decay": 0.1}},
+           "gradient_accumulation_steps": ga, "gradient_clipping": 1.0,
+           "zero_optimization": {"stage": stage, **({"offload_optimizer": {"device": "cpu"}} if offload else {})}}
+    eng = ZeroEngine(m, cfg, log=lambda *_: None)
+    data = sft_batches(n=steps * ga * 2 // world * world + 8)
+    k = 0
+    for _ in range(steps):
+        for _ in range(ga):
+            # each optimizer step consumes world*ga micro-batches in order; rank r takes every world-th
+            ids = torch.cat([data[k + j * world + rank][0] for j in range(1)])
+            lab = torch.cat([data[k + j * world + rank][1] for j in range(1)])
+            k += world
+            loss, _ = m(ids, labels=lab)
+            eng.backward(loss * world / world)
+            eng.step()
+    return {n: p.detach().clone() for n, p in m.named_parameters()}

@@ -1,0 +1,191 @@
+"""SFT path: Alpaca preprocessing, DeepSpeed-config resolution, ZeRO engine equivalence,
+CPU-offload Adam, checkpoint/resume and zero_to_fp32 (reference
+4_training_alpaca_deepspeed/train.py and configs/default_offload_opt_param.json)."""
+import json
+import os
+
+import pytest
+import torch
+
+from smdt_amd.data import sft
+from smdt_amd.train import hf_args
+from smdt_amd.train.zero import resolve_ds_config
+
+from _dist import run_workers  # noqa: E402
+import dist_workers as W  # noqa: E402
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+DS_CFG = os.path.join(REPO, "recipes", "4_training_alpaca_deepspeed", "configs", "default_offload_opt_param.json")
+NB4 = ("--model_name_or_path facebook/opt-125m --data_path /opt/ml/input/data/training/alpaca_data.json "
+       "--bf16 False --output_dir /opt/ml/model --num_train_epochs 1 --per_device_train_batch_size 4 "
+       "--per_device_eval_batch_size 4 --gradient_accumulation_steps 8 --evaluation_strategy no "
+       "--save_strategy steps --save_steps 2000 --save_total_limit 1 --learning_rate 2e-05 --weight_decay 0.0 "
+       "--warmup_ratio 0.03 --deepspeed " + DS_CFG + " --tf32 False --cache_dir /opt/ml/input/data/cache_dir "
+       "--report_to none").split()
+
+
+def _parse(argv):
+    p = hf_args.ArgumentParser((hf_args.ModelArguments, hf_args.DataArguments, hf_args.TrainingArguments))
+    return p.parse_args_into_dataclasses(argv)
+
+
+def test_nb4_cli_parses():
+    m, d, t = _parse(NB4)
+    assert m.model_name_or_path == "facebook/opt-125m"
+    assert (t.per_device_train_batch_size, t.gradient_accumulation_steps, t.learning_rate) == (4, 8, 2e-5)
+    assert t.bf16 is False and t.tf32 is False and t.save_total_limit == 1 and t.deepspeed == DS_CFG
+    with pytest.raises(ValueError):
+        _parse(NB4 + ["--no_such_flag", "1"])
+
+
+def test_ds_auto_resolution_matches_hf_rules():
+    _, _, t = _parse(NB4)
+    raw = json.load(open(DS_CFG))
+    cfg = resolve_ds_config(raw, t, hidden_size=768, world_size=16, num_training_steps=101)
+    assert cfg["train_micro_batch_size_per_gpu"] == 4 and cfg["gradient_accumulation_steps"] == 8
+    assert cfg["train_batch_size"] == 512                                   # NB4: 4 x 8 x 16
+    assert cfg["gradient_clipping"] == 1.0
+    assert cfg["optimizer"]["params"] == {"lr": 2e-5, "betas": [0.9, 0.999], "eps": 1e-8, "weight_decay": 0.0}
+    sp = cfg["scheduler"]["params"]
+    assert (sp["warmup_min_lr"], sp["warmup_max_lr"], sp["warmup_num_steps"], sp["total_num_steps"]) == \
+        (0, 2e-5, 4, 101)                                                   # ceil(0.03 * 101) = 4
+    z = cfg["zero_optimization"]
+    assert z["reduce_bucket_size"] == 768 * 768
+    assert z["stage3_prefetch_bucket_size"] == int(0.9 * 768 * 768)
+    assert z["stage3_param_persistence_threshold"] == 7680                 # NB4:1629 threshold
+    assert cfg["bf16"]["enabled"] is False
+
+
+def test_ds_explicit_mismatch_raises():
+    _, _, t = _parse(NB4)
+    raw = json.load(open(DS_CFG))
+    raw["train_micro_batch_size_per_gpu"] = 16
+    with pytest.raises(ValueError, match="differ"):
+        resolve_ds_config(raw, t, 768, 16, 101)
+
+
+def test_preprocess_masks_prompt_and_collator_pads():
+    tok = sft.load_tokenizer("facebook/opt-125m", model_max_length=64)
+    assert len(tok) == 50265 and tok.pad_token_id == 1 and tok.eos_token == "</s>"
+    data = [{"instruction": "Give three tips.", "input": "", "output": "Eat well. Sleep."},
+            {"instruction": "Translate", "input": "hello world", "output": "hola mundo"}]
+    src, tgt = sft.format_examples(data, tok.eos_token)
+    assert src[0].endswith("### Response:") and "### Input:\nhello world" in src[1]
+    d = sft.preprocess(src, tgt, tok)
+    for ids, lab, s in zip(d["input_ids"], d["labels"], src):
+        n_src = len(tok(s, return_tensors="pt").input_ids[0])
+        assert (lab[:n_src] == sft.IGNORE_INDEX).all()
+        assert torch.equal(lab[n_src:], ids[n_src:])
+        assert ids[-1].item() == tok.eos_token_id
+    col = sft.DataCollatorForSupervisedDataset(tok, pad_to_multiple_of=32)
+    b = col([{"input_ids": i, "labels": l} for i, l in zip(d["input_ids"], d["labels"])])
+    assert b["input_ids"].shape[1] % 32 == 0
+    assert (b["labels"][b["input_ids"] == tok.pad_token_id] == -100).all()
+    assert torch.equal(b["attention_mask"], b["input_ids"].ne(tok.pad_token_id))
+
+
+def test_pad_to_multiple_does_not_change_loss():
+    from smdt_amd.models.hf import HFCausalLM
+    torch.manual_seed(0)
+    m = HFCausalLM(W.SFT_LLAMA, params_dtype=torch.float32).eval()
+    ids, lab = W.sft_batches(1, b=2, s=20)[0]
+    with torch.no_grad():
+        l1, _ = m(ids, labels=lab)
+        ids2 = torch.cat([ids, torch.zeros(2, 12, dtype=torch.long)], 1)
+        lab2 = torch.cat([lab, torch.full((2, 12), -100)], 1)
+        l2, _ = m(ids2, labels=lab2)
+    torch.testing.assert_close(l1, l2, rtol=1e-6, atol=1e-6)
+
+
+def test_length_grouped_sampler_covers_dataset_once():
+    lens = torch.randint(5, 300, (103,)).tolist()
+    seen = []
+    for r in range(2):
+        s = sft.LengthGroupedSampler(lens, batch_size=4, rank=r, world=2, seed=1)
+        seen += list(iter(s))
+    assert sorted(set(seen)) == list(range(103))
+
+
+def test_cpu_adam_matches_torch_adamw():
+    from smdt_amd import _runtime
+    torch.manual_seed(0)
+    n = 100_003
+    p = torch.randn(n)
+    g = torch.randn(n)
+    m = torch.zeros(n)
+    v = torch.zeros(n)
+    ref = p.clone().requires_grad_()
+    opt = torch.optim.AdamW([ref], lr=1e-2, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1)
+    out = torch.empty(n, dtype=torch.int16)
+    for step in range(1, 4):
+        ref.grad = g.clone() * 0.5
+        opt.step()
+        _runtime.cpu_adam(p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), out.data_ptr(), n, 1e-2, 0.9,
+                          0.95, 1e-8, 0.1, step, True, 0.5, 4)
+    torch.testing.assert_close(p, ref.detach(), rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(out.view(torch.bfloat16).float(), p.to(torch.bfloat16).float())
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("stage,offload", [(0, False), (2, False), (3, False), (2, True)])
+def test_zero_world2_matches_world1(stage, offload):
+    ref = run_workers(W.zero_sft_worker, 1, 0, 2, 3, False)[0]       # GA 2 on one rank
+    outs = run_workers(W.zero_sft_worker, 2, stage, 1, 3, offload)    # GA 1 on two ranks
+    for r in range(2):
+        for k, v in ref.items():
+            torch.testing.assert_close(outs[r][k], v, rtol=2e-4, atol=2e-5, msg=f"rank {r} {k}")
+
+
+def _trainer_args(tmp_path, **over):
+    argv = ["--output_dir", str(tmp_path / "out"), "--per_device_train_batch_size", "2",
+            "--gradient_accumulation_steps", "2", "--learning_rate", "1e-3", "--logging_steps", "1",
+            "--save_steps", "3", "--max_steps", "6", "--deepspeed", DS_CFG, "--pad_to_multiple_of", "8",
+            "--warmup_steps", "2", "--seed", "5"]
+    for k, v in over.items():
+        argv += [f"--{k}", str(v)]
+    return _parse(argv)[2]
+
+
+def _tiny_trainer(tmp_path, args):
+    from smdt_amd.models.hf import HFCausalLM
+    from smdt_amd.parallel import state as ps
+    from smdt_amd.train.sft_trainer import Trainer
+    ps.destroy_model_parallel()
+    torch.manual_seed(0)
+    model = HFCausalLM(W.SFT_LLAMA, params_dtype=torch.float32)
+    tok = sft.HashWordTokenizer(120, 48, pad_token="<pad>", special_ids={"<pad>": 0, "</s>": 1, "<s>": 2, "<unk>": 3})
+    path = tmp_path / "alpaca.json"
+    if not path.exists():
+        sft.write_synthetic_alpaca(str(path), 40, seed=1)
+    ds = sft.SupervisedDataset(str(path), tok)
+    return Trainer(model=model, tokenizer=tok, args=args, train_dataset=ds,
+                   data_collator=sft.DataCollatorForSupervisedDataset(tok, 8))
+
+
+def test_trainer_checkpoint_resume_and_zero_to_fp32(tmp_path):
+    from smdt_amd.train.zero import get_fp32_state_dict_from_zero_checkpoint
+    t = _tiny_trainer(tmp_path, _trainer_args(tmp_path))
+    met = t.train()
+    full = {k: v.detach().clone() for k, v in t.model.named_parameters()}
+    losses = [h["loss"] for h in t.state["log_history"] if "loss" in h]
+    assert len(losses) == 6 and met["train_samples_per_second"] > 0
+    ck = tmp_path / "out" / "checkpoint-6"
+    assert (ck / "latest").read_text() == "global_step6"
+    assert (ck / "global_step6" / "mp_rank_00_model_states.pt").exists()
+    assert (tmp_path / "out" / "checkpoint-3").exists()
+    sd = get_fp32_state_dict_from_zero_checkpoint(str(ck))
+    for k, v in full.items():
+        torch.testing.assert_close(sd["model." + k] if "model." + k in sd else sd[k], v)
+    # resuming from the step-3 checkpoint reproduces the uninterrupted run
+    t3 = _tiny_trainer(tmp_path, _trainer_args(tmp_path, output_dir=tmp_path / "out2",
+                                               resume_from_checkpoint=tmp_path / "out" / "checkpoint-3"))
+    t3.train()
+    for k, v in full.items():
+        torch.testing.assert_close(dict(t3.model.named_parameters())[k].detach(), v, rtol=1e-5, atol=1e-6)
+
+
+def test_save_total_limit_rotates(tmp_path):
+    t = _tiny_trainer(tmp_path, _trainer_args(tmp_path, save_total_limit=1, save_steps=2))
+    t.train()
+    cks = sorted(p.name for p in (tmp_path / "out").iterdir() if p.name.startswith("checkpoint-"))
+    assert cks == ["checkpoint-6"]
