@@ -55,7 +55,7 @@ def parse():
     p.add_argument("--num-attention-heads", type=int, default=16)
     p.add_argument("--vocab-size", type=int, default=50257)
     p.add_argument("--hidden-dropout", type=float, default=0.1)
-    p.add_argument("--attention-dropout", type=float, default=0.0)
+    p.add_argument("--attention-dropout", type=float, default=0.1)  # Megatron default (reference run)
     p.add_argument("--zero", type=int, default=1, help="ZeRO-1/2 distributed optimizer when DP > 1")
     p.add_argument("--bucket-size", type=int, default=40_000_000)
     p.add_argument("--no-flash", action="store_true")

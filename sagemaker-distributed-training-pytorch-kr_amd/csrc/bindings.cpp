@@ -324,7 +324,8 @@ void fa_check(const Tensor& t, const char* n) {
 
 // `out` (optional) is a preallocated [B, S, H, D] view with any strides (e.g. the [s, b, h]
 // activation layout used by the transformer trunk).
-std::vector<Tensor> flash_fwd(Tensor q, Tensor k, Tensor v, double scale, bool causal, OptT out) {
+std::vector<Tensor> flash_fwd(Tensor q, Tensor k, Tensor v, double scale, bool causal, OptT out,
+                              double dropout_p, int64_t seed, int64_t offset) {
   fa_check(q, "q"); fa_check(k, "k"); fa_check(v, "v");
   const int64_t B = q.size(0), S = q.size(1), H = q.size(2), D = q.size(3), Hkv = k.size(2);
   TORCH_CHECK(k.size(0) == B && k.size(1) == S && k.size(3) == D && v.sizes() == k.sizes(), "flash: k/v shape mismatch");
@@ -341,7 +342,8 @@ std::vector<Tensor> flash_fwd(Tensor q, Tensor k, Tensor v, double scale, bool c
   check(smdt_flash_fwd(1, q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr<float>(),
                        (int)B, (int)H, (int)Hkv, (int)S, (int)D, q.stride(0), q.stride(1), q.stride(2),
                        k.stride(0), k.stride(1), k.stride(2), v.stride(0), v.stride(1), v.stride(2),
-                       o.stride(0), o.stride(1), o.stride(2), (float)scale, causal ? 1 : 0, cur_stream()),
+                       o.stride(0), o.stride(1), o.stride(2), (float)scale, causal ? 1 : 0, (float)dropout_p,
+                       (uint64_t)seed, (uint64_t)offset, cur_stream()),
         "flash_fwd");
   return {o, lse};
 }
@@ -349,7 +351,8 @@ std::vector<Tensor> flash_fwd(Tensor q, Tensor k, Tensor v, double scale, bool c
 // dq / dk / dv (optional) are preallocated [B, S, H(kv), D] views with any strides, typically
 // views into one fused d(QKV) buffer so the QKV projection backward needs no concatenation.
 std::vector<Tensor> flash_bwd(Tensor q, Tensor k, Tensor v, Tensor o, Tensor dout, Tensor lse,
-                              double scale, bool causal, OptT dq_out, OptT dk_out, OptT dv_out) {
+                              double scale, bool causal, OptT dq_out, OptT dk_out, OptT dv_out,
+                              double dropout_p, int64_t seed, int64_t offset) {
   fa_check(q, "q"); fa_check(k, "k"); fa_check(v, "v"); fa_check(o, "o");
   const int64_t B = q.size(0), S = q.size(1), H = q.size(2), D = q.size(3), Hkv = k.size(2);
   TORCH_CHECK((D == 64 || D == 128) && S % 128 == 0 && H % Hkv == 0, "flash_bwd: unsupported shape");
@@ -375,7 +378,7 @@ std::vector<Tensor> flash_bwd(Tensor q, Tensor k, Tensor v, Tensor o, Tensor dou
   check(smdt_flash_bwd(1, q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), dout.data_ptr(),
                        lse.data_ptr<float>(), delta.data_ptr<float>(), dq.data_ptr(), dk.data_ptr(),
                        dv.data_ptr(), (int)B, (int)H, (int)Hkv, (int)S, (int)D, st, (float)scale,
-                       causal ? 1 : 0, cur_stream()),
+                       causal ? 1 : 0, (float)dropout_p, (uint64_t)seed, (uint64_t)offset, cur_stream()),
         "flash_bwd");
   return {dq, dk, dv};
 }
@@ -403,6 +406,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("rope_", &rope_);
   m.def("ce_stats", &ce_stats);
   m.def("ce_bwd", &ce_bwd);
-  m.def("flash_fwd", &flash_fwd);
-  m.def("flash_bwd", &flash_bwd);
+  namespace py = pybind11;
+  m.def("flash_fwd", &flash_fwd, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("scale"), py::arg("causal"),
+        py::arg("out") = py::none(), py::arg("dropout_p") = 0.0, py::arg("seed") = 0, py::arg("offset") = 0);
+  m.def("flash_bwd", &flash_bwd, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("o"), py::arg("dout"),
+        py::arg("lse"), py::arg("scale"), py::arg("causal"), py::arg("dq") = py::none(), py::arg("dk") = py::none(),
+        py::arg("dv") = py::none(), py::arg("dropout_p") = 0.0, py::arg("seed") = 0, py::arg("offset") = 0);
 }

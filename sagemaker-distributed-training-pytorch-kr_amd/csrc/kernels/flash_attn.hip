@@ -174,17 +174,47 @@ struct Strides {
   int64_t sb, ss, sh;
 };
 
+// Attention dropout. Element (b, h, q, k) is kept iff hash(q * S + k, key(b, h)) >= thr
+// (thr = p * 2^32); kept probabilities are scaled by inv = 1 / (1 - p). The forward and both
+// backward kernels re-derive the identical mask from the counter (no mask tensor in HBM). The
+// hash is a keyed two-round multiply/xor-shift mixer (~8 VALU per element): Philox-7 costs ~4x
+// that per element and would dominate the MFMA work of the attention tile on CDNA4.
+struct Drop {
+  uint32_t thr, key0, key1;
+  float inv;
+};
+
+__device__ __forceinline__ uint32_t fmix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x85EBCA6Bu;
+  x ^= x >> 13;
+  x *= 0xC2B2AE35u;
+  x ^= x >> 16;
+  return x;
+}
+__device__ __forceinline__ uint32_t drop_key(const Drop& d, int bh) {
+  return fmix32(d.key0 + (uint32_t)bh * 0x632BE5ABu) ^ d.key1;
+}
+__device__ __forceinline__ bool drop_keep(uint32_t counter, uint32_t key, uint32_t thr) {
+  uint32_t x = counter ^ key;
+  x *= 0x9E3779B1u;
+  x ^= x >> 15;
+  x *= 0x85EBCA77u;
+  x ^= x >> 13;
+  return x >= thr;
+}
+
 // ---------------------------------------------------------------------------------------
 // Forward. Workgroup = 4 waves = 128 query rows of one (b, h); K/V streamed in 64-key tiles,
 // double-buffered.
-template <int D, bool CAUSAL>
+template <int D, bool CAUSAL, bool DROP>
 __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void fwd_kernel(const bf16* __restrict__ Q,
                                                      const bf16* __restrict__ K,
                                                      const bf16* __restrict__ V,
                                                      bf16* __restrict__ O, float* __restrict__ LSE,
                                                      int B, int H, int Hkv, int S, Strides qs,
                                                      Strides ks_, Strides vs, Strides os,
-                                                     float scale) {
+                                                     float scale, Drop drop) {
   using G = Geo<D>;
   __shared__ __attribute__((aligned(16))) char lds[2 * 2 * G::TB];  // [buf][K|V]
 
@@ -214,6 +244,8 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void fwd_kernel(const bf16* _
 
   const int kend = CAUSAL ? (q0 + kBlockRows) : S;
   const int ntiles = kend / kTile;
+  const uint32_t dkey = DROP ? drop_key(drop, bh) : 0u;
+  const uint32_t dbase = (uint32_t)my_q * (uint32_t)S + 4u * h;  // counter of key row 0 (+ kb)
   Stage<D> sk, sv;
   sk.init(ks_.ss);
   sv.init(vs.ss);
@@ -263,8 +295,12 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void fwd_kernel(const bf16* _
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           const float p = fexp2(fmaf(st[tt][i], c2, -base));
-          st[tt][i] = p;
-          rs += p;
+          rs += p;  // the softmax denominator uses the un-dropped probabilities
+          if constexpr (DROP)
+            st[tt][i] = drop_keep(dbase + kb + 32 * tt + (i & 3) + 8 * (i >> 2), dkey, drop.thr)
+                            ? p * drop.inv : 0.f;
+          else
+            st[tt][i] = p;
         }
       l = l * alpha + xhalf_sum(rs);
       m = mnew;
@@ -342,12 +378,12 @@ __global__ __launch_bounds__(256) void delta_kernel(const bf16* __restrict__ O,
 // dK / dV. Workgroup = 4 waves = 128 keys of one (b, kv-head); each wave keeps K, V of its 32
 // keys and dK^T, dV^T in registers while the workgroup sweeps the query heads of the group and
 // their 64-row query tiles (Q, dO, lse*log2e, delta staged in double-buffered LDS).
-template <int D, bool CAUSAL>
+template <int D, bool CAUSAL, bool DROP>
 __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dkdv_kernel(
     const bf16* __restrict__ Q, const bf16* __restrict__ K, const bf16* __restrict__ V,
     const bf16* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ DELTA,
     bf16* __restrict__ dK, bf16* __restrict__ dV, int B, int H, int Hkv, int S, Strides qs,
-    Strides ks_, Strides vs, Strides dos, Strides dks, Strides dvs, float scale) {
+    Strides ks_, Strides vs, Strides dos, Strides dks, Strides dvs, float scale, Drop drop) {
   using G = Geo<D>;
   constexpr int BUF = 2 * G::TB + 2 * kTile * 4;  // Q | dO | lse | delta
   __shared__ __attribute__((aligned(16))) char lds[2 * BUF];
@@ -407,6 +443,8 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dkdv_kernel(
   for (int it = 0; it < total; ++it) {
     const int qb = qstart + (it % ntiles) * kTile;
     const bool more = it + 1 < total;
+    const uint32_t dkey = DROP ? drop_key(drop, b * H + hk * group + it / ntiles) : 0u;
+    const uint32_t dbase = (uint32_t)(qb + 4 * h) * (uint32_t)S + (uint32_t)my_key;
     const char* buf = lds + (it & 1) * BUF;
     const char* q_l = buf;
     const char* do_l = buf + G::TB;
@@ -435,8 +473,15 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dkdv_kernel(
           const int i = 4 * g + j;
           float p = fexp2(fmaf(s[i], c2, -lv[j]));
           if (diag && my_key > qb + r0 + j) p = 0.f;
-          s[i] = p;                        // P
-          dp[i] = p * (dp[i] - dl[j]);     // dS
+          if constexpr (DROP) {
+            const bool keep = drop_keep(dbase + (uint32_t)(32 * qs2 + 8 * g + j) * (uint32_t)S, dkey,
+                                        drop.thr);
+            s[i] = keep ? p * drop.inv : 0.f;                   // dropped P (feeds dV)
+            dp[i] = p * ((keep ? dp[i] * drop.inv : 0.f) - dl[j]);  // dS
+          } else {
+            s[i] = p;                        // P
+            dp[i] = p * (dp[i] - dl[j]);     // dS
+          }
         }
       }
       // dV^T[d, key] += dO^T[d, q] . P[q, key] ; dK^T[d, key] += Q^T[d, q] . dS[q, key]
@@ -477,12 +522,12 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dkdv_kernel(
 // ---------------------------------------------------------------------------------------
 // dQ. Workgroup = 4 waves = 128 query rows of one (b, h); K/V streamed in 64-key tiles,
 // double-buffered.
-template <int D, bool CAUSAL>
+template <int D, bool CAUSAL, bool DROP>
 __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dq_kernel(
     const bf16* __restrict__ Q, const bf16* __restrict__ K, const bf16* __restrict__ V,
     const bf16* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ DELTA,
     bf16* __restrict__ dQ, int B, int H, int Hkv, int S, Strides qs, Strides ks_, Strides vs,
-    Strides dos, Strides dqs, float scale) {
+    Strides dos, Strides dqs, float scale, Drop drop) {
   using G = Geo<D>;
   __shared__ __attribute__((aligned(16))) char lds[2 * 2 * G::TB];
 
@@ -503,6 +548,8 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dq_kernel(
   const float lse2 = LSE[((int64_t)b * H + hq) * S + my_q] * kLog2e;
   const float dl = DELTA[((int64_t)b * H + hq) * S + my_q];
   const float c2 = scale * kLog2e;
+  const uint32_t dkey = DROP ? drop_key(drop, bh) : 0u;
+  const uint32_t dbase = (uint32_t)my_q * (uint32_t)S + 4u * h;
 
   const bf16* Kb = K + b * ks_.sb + hk * ks_.sh;
   const bf16* Vb = V + b * vs.sb + hk * vs.sh;
@@ -546,7 +593,12 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dq_kernel(
       for (int i = 0; i < 16; ++i) {
         float p = fexp2(fmaf(st[i], c2, -lse2));
         if (diag && ksub + acc_row(i, h) > my_q) p = 0.f;
-        dpt[i] = p * (dpt[i] - dl);  // dS^T
+        if constexpr (DROP) {
+          const bool keep = drop_keep(dbase + ksub + (i & 3) + 8 * (i >> 2), dkey, drop.thr);
+          dpt[i] = p * ((keep ? dpt[i] * drop.inv : 0.f) - dl);  // dS^T
+        } else {
+          dpt[i] = p * (dpt[i] - dl);  // dS^T
+        }
       }
       // dQ^T[d, q] += K^T[d, keys] . dS^T[keys, q]
 #pragma unroll
@@ -584,8 +636,28 @@ using namespace smdt;
 using namespace smdt::fa;
 
 static bool fa_shape_ok(int dtype, int H, int Hkv, int S, int D) {
-  return dtype == 1 && (D == 64 || D == 128) && S % kBlockRows == 0 && S > 0 && Hkv > 0 &&
-         H % Hkv == 0;
+  return dtype == 1 && (D == 64 || D == 128) && S % kBlockRows == 0 && S > 0 && S <= 65536 &&
+         Hkv > 0 && H % Hkv == 0;
+}
+
+static uint32_t host_fmix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x85EBCA6Bu;
+  x ^= x >> 13;
+  x *= 0xC2B2AE35u;
+  x ^= x >> 16;
+  return x;
+}
+
+// keys: key0 from the seed, key1 from the per-call offset (see drop_key / drop_keep).
+static Drop make_drop(float p, uint64_t seed, uint64_t offset) {
+  Drop d;
+  double t = (double)p * 4294967296.0;
+  d.thr = t >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)t;
+  d.inv = p < 1.f ? 1.f / (1.f - p) : 0.f;
+  d.key0 = host_fmix32((uint32_t)seed ^ host_fmix32((uint32_t)(seed >> 32) + 0x9E3779B9u));
+  d.key1 = host_fmix32((uint32_t)offset * 0x27D4EB2Fu ^ host_fmix32((uint32_t)(offset >> 32) + 0x165667B1u));
+  return d;
 }
 
 extern "C" hipError_t smdt_flash_fwd(int dtype, const void* q, const void* k, const void* v,
@@ -593,16 +665,22 @@ extern "C" hipError_t smdt_flash_fwd(int dtype, const void* q, const void* k, co
                                      int64_t q_sb, int64_t q_ss, int64_t q_sh, int64_t k_sb,
                                      int64_t k_ss, int64_t k_sh, int64_t v_sb, int64_t v_ss,
                                      int64_t v_sh, int64_t o_sb, int64_t o_ss, int64_t o_sh,
-                                     float scale, int causal, hipStream_t st) {
-  if (!fa_shape_ok(dtype, H, Hkv, S, D)) return hipErrorInvalidValue;
+                                     float scale, int causal, float dropout_p, uint64_t seed,
+                                     uint64_t offset, hipStream_t st) {
+  if (!fa_shape_ok(dtype, H, Hkv, S, D) || dropout_p < 0.f || dropout_p >= 1.f) return hipErrorInvalidValue;
   Strides qs{q_sb, q_ss, q_sh}, ks{k_sb, k_ss, k_sh}, vs{v_sb, v_ss, v_sh}, os{o_sb, o_ss, o_sh};
   dim3 grid((unsigned)((int64_t)B * H * (S / kBlockRows)));
-#define SMDT_FA_FWD(DD, CC)                                                                     \
-  hipLaunchKernelGGL((fwd_kernel<DD, CC>), grid, dim3(256), 0, st, (const bf16*)q,             \
+  const Drop dr = make_drop(dropout_p, seed, offset);
+  const bool drop = dropout_p > 0.f;
+#define SMDT_FA_FWD(DD, CC, DR)                                                                 \
+  hipLaunchKernelGGL((fwd_kernel<DD, CC, DR>), grid, dim3(256), 0, st, (const bf16*)q,         \
                      (const bf16*)k, (const bf16*)v, (bf16*)o, lse, B, H, Hkv, S, qs, ks, vs, os, \
-                     scale)
-  if (D == 64) { if (causal) SMDT_FA_FWD(64, true); else SMDT_FA_FWD(64, false); }
-  else { if (causal) SMDT_FA_FWD(128, true); else SMDT_FA_FWD(128, false); }
+                     scale, dr)
+#define SMDT_FA_FWD2(DD, CC) \
+  do { if (drop) SMDT_FA_FWD(DD, CC, true); else SMDT_FA_FWD(DD, CC, false); } while (0)
+  if (D == 64) { if (causal) SMDT_FA_FWD2(64, true); else SMDT_FA_FWD2(64, false); }
+  else { if (causal) SMDT_FA_FWD2(128, true); else SMDT_FA_FWD2(128, false); }
+#undef SMDT_FA_FWD2
 #undef SMDT_FA_FWD
   return hipGetLastError();
 }
@@ -611,8 +689,11 @@ extern "C" hipError_t smdt_flash_bwd(int dtype, const void* q, const void* k, co
                                      const void* o, const void* dout, const float* lse,
                                      float* delta, void* dq, void* dk, void* dv, int B, int H,
                                      int Hkv, int S, int D, const int64_t* strides, float scale,
-                                     int causal, hipStream_t st) {
-  if (!fa_shape_ok(dtype, H, Hkv, S, D)) return hipErrorInvalidValue;
+                                     int causal, float dropout_p, uint64_t seed, uint64_t offset,
+                                     hipStream_t st) {
+  if (!fa_shape_ok(dtype, H, Hkv, S, D) || dropout_p < 0.f || dropout_p >= 1.f) return hipErrorInvalidValue;
+  const Drop dr = make_drop(dropout_p, seed, offset);
+  const bool drop = dropout_p > 0.f;
   // strides: 8 x (batch, seq, head) element strides for q, k, v, o, dO, dQ, dK, dV.
   Strides qs{strides[0], strides[1], strides[2]}, ks{strides[3], strides[4], strides[5]},
       vs{strides[6], strides[7], strides[8]}, os{strides[9], strides[10], strides[11]},
@@ -628,17 +709,20 @@ extern "C" hipError_t smdt_flash_bwd(int dtype, const void* q, const void* k, co
   }
   dim3 gkv((unsigned)((int64_t)B * Hkv * (S / kBlockRows)));
   dim3 gq((unsigned)((int64_t)B * H * (S / kBlockRows)));
-#define SMDT_FA_BWD(DD, CC)                                                                      \
+#define SMDT_FA_BWD(DD, CC, DR)                                                                  \
   do {                                                                                           \
-    hipLaunchKernelGGL((bwd_dkdv_kernel<DD, CC>), gkv, dim3(256), 0, st, (const bf16*)q,        \
+    hipLaunchKernelGGL((bwd_dkdv_kernel<DD, CC, DR>), gkv, dim3(256), 0, st, (const bf16*)q,    \
                        (const bf16*)k, (const bf16*)v, (const bf16*)dout, lse, delta, (bf16*)dk,  \
-                       (bf16*)dv, B, H, Hkv, S, qs, ks, vs, dos, dks, dvs, scale);                \
-    hipLaunchKernelGGL((bwd_dq_kernel<DD, CC>), gq, dim3(256), 0, st, (const bf16*)q,           \
+                       (bf16*)dv, B, H, Hkv, S, qs, ks, vs, dos, dks, dvs, scale, dr);            \
+    hipLaunchKernelGGL((bwd_dq_kernel<DD, CC, DR>), gq, dim3(256), 0, st, (const bf16*)q,       \
                        (const bf16*)k, (const bf16*)v, (const bf16*)dout, lse, delta, (bf16*)dq,  \
-                       B, H, Hkv, S, qs, ks, vs, dos, dqs, scale);                                \
+                       B, H, Hkv, S, qs, ks, vs, dos, dqs, scale, dr);                            \
   } while (0)
-  if (D == 64) { if (causal) SMDT_FA_BWD(64, true); else SMDT_FA_BWD(64, false); }
-  else { if (causal) SMDT_FA_BWD(128, true); else SMDT_FA_BWD(128, false); }
+#define SMDT_FA_BWD2(DD, CC) \
+  do { if (drop) SMDT_FA_BWD(DD, CC, true); else SMDT_FA_BWD(DD, CC, false); } while (0)
+  if (D == 64) { if (causal) SMDT_FA_BWD2(64, true); else SMDT_FA_BWD2(64, false); }
+  else { if (causal) SMDT_FA_BWD2(128, true); else SMDT_FA_BWD2(128, false); }
+#undef SMDT_FA_BWD2
 #undef SMDT_FA_BWD
   return hipGetLastError();
 }

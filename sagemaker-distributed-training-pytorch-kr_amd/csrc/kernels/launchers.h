@@ -76,10 +76,12 @@ hipError_t smdt_flash_fwd(int dtype, const void* q, const void* k, const void* v
                           float* lse, int B, int H, int Hkv, int S, int D, int64_t q_sb,
                           int64_t q_ss, int64_t q_sh, int64_t k_sb, int64_t k_ss, int64_t k_sh,
                           int64_t v_sb, int64_t v_ss, int64_t v_sh, int64_t o_sb, int64_t o_ss,
-                          int64_t o_sh, float scale, int causal, hipStream_t st);
+                          int64_t o_sh, float scale, int causal, float dropout_p, uint64_t seed,
+                          uint64_t offset, hipStream_t st);
 hipError_t smdt_flash_bwd(int dtype, const void* q, const void* k, const void* v, const void* o,
                           const void* dout, const float* lse, float* delta, void* dq, void* dk,
                           void* dv, int B, int H, int Hkv, int S, int D, const int64_t* strides,
-                          float scale, int causal, hipStream_t st);
+                          float scale, int causal, float dropout_p, uint64_t seed,
+                          uint64_t offset, hipStream_t st);
 
 }  // extern "C"

@@ -163,9 +163,12 @@ class ParallelAttention(nn.Module):
         if self.rope is not None:
             cos, sin, rot = self.rope
             qkv = _RopeQKV.apply(qkv, cos, sin, rot, self.nh, self.nkv, self.hd)
-        use_flash = (self.cfg.use_flash_attn and (not training or self.cfg.attention_dropout == 0.0))
-        if use_flash:
-            ctx = SF.flash_attention_qkv(qkv, self.nh, self.nkv, self.hd, seq_first=True, causal=True)
+        if self.cfg.use_flash_attn:
+            # attention dropout runs inside the flash kernels; heads are TP-sharded, so the mask
+            # comes from the per-TP-rank stream (Megatron forks the model-parallel tracker here)
+            p = self.cfg.attention_dropout if training else 0.0
+            ctx = SF.flash_attention_qkv(qkv, self.nh, self.nkv, self.hd, seq_first=True, causal=True,
+                                         dropout_p=p, rng=get_rng("tp"))
         else:
             ctx = self.core_attention_unfused(qkv, training)
         return self.proj(ctx)                                    # (out, bias)

@@ -252,7 +252,7 @@ def _qkv_views(qkv, nh, nkv, hd, seq_first):
 
 class _FlashAttnQKV(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, qkv, nh, nkv, hd, seq_first, scale, causal):
+    def forward(ctx, qkv, nh, nkv, hd, seq_first, scale, causal, dropout_p=0.0, seed=0, offset=0):
         C = _ext.ext()
         q, k, v = _qkv_views(qkv, nh, nkv, hd, seq_first)
         if seq_first:
@@ -263,15 +263,15 @@ class _FlashAttnQKV(torch.autograd.Function):
             B, S = qkv.shape[0], qkv.shape[1]
             out = qkv.new_empty(B, S, nh, hd)
             ov = out
-        _, lse = C.flash_fwd(q, k, v, scale, causal, ov)
+        _, lse = C.flash_fwd(q, k, v, scale, causal, ov, dropout_p, seed, offset)
         ctx.save_for_backward(qkv, out, lse)
-        ctx.cfg = (nh, nkv, hd, seq_first, scale, causal)
+        ctx.cfg = (nh, nkv, hd, seq_first, scale, causal, dropout_p, seed, offset)
         return out.flatten(-2)
 
     @staticmethod
     def backward(ctx, dout):
         qkv, out, lse = ctx.saved_tensors
-        nh, nkv, hd, seq_first, scale, causal = ctx.cfg
+        nh, nkv, hd, seq_first, scale, causal, dropout_p, seed, offset = ctx.cfg
         C = _ext.ext()
         q, k, v = _qkv_views(qkv, nh, nkv, hd, seq_first)
         dqkv = torch.empty_like(qkv)
@@ -281,28 +281,68 @@ class _FlashAttnQKV(torch.autograd.Function):
         if seq_first:
             do = do.transpose(0, 1)
             o = o.transpose(0, 1)
-        C.flash_bwd(q, k, v, o, do, lse, scale, causal, dq, dk, dv)
-        return dqkv, None, None, None, None, None, None
+        C.flash_bwd(q, k, v, o, do, lse, scale, causal, dq, dk, dv, dropout_p, seed, offset)
+        return dqkv, None, None, None, None, None, None, None, None, None
 
 
 class _FlashAttn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, q, k, v, scale, causal):
+    def forward(ctx, q, k, v, scale, causal, dropout_p=0.0, seed=0, offset=0):
         C = _ext.ext()
-        o, lse = C.flash_fwd(q, k, v, scale, causal, None)
+        o, lse = C.flash_fwd(q, k, v, scale, causal, None, dropout_p, seed, offset)
         ctx.save_for_backward(q, k, v, o, lse)
-        ctx.scale, ctx.causal = scale, causal
+        ctx.cfg = (scale, causal, dropout_p, seed, offset)
         return o
 
     @staticmethod
     def backward(ctx, do):
         q, k, v, o, lse = ctx.saved_tensors
-        dq, dk, dv = _ext.ext().flash_bwd(q, k, v, o, do, lse, ctx.scale, ctx.causal, None, None, None)
-        return dq, dk, dv, None, None
+        scale, causal, p, seed, offset = ctx.cfg
+        dq, dk, dv = _ext.ext().flash_bwd(q, k, v, o, do, lse, scale, causal, None, None, None, p, seed, offset)
+        return dq, dk, dv, None, None, None, None, None
 
 
-def attention_ref(q, k, v, scale, causal):
-    """Reference attention on [B, S, H, D] (GQA by head repetition), fp32 math."""
+_M32 = 0xFFFFFFFF
+
+
+def _fmix32_t(x):
+    x = x ^ (x >> 16)
+    x = (x * 0x85EBCA6B) & _M32
+    x = x ^ (x >> 13)
+    x = (x * 0xC2B2AE35) & _M32
+    return x ^ (x >> 16)
+
+
+def _fmix32_i(x: int) -> int:
+    x &= _M32
+    x ^= x >> 16
+    x = (x * 0x85EBCA6B) & _M32
+    x ^= x >> 13
+    x = (x * 0xC2B2AE35) & _M32
+    return x ^ (x >> 16)
+
+
+def flash_dropout_keep_mask(B: int, H: int, S: int, p: float, seed: int, offset: int, device=None):
+    """Bit-exact twin of the flash kernels' dropout mask: bool [B, H, S(q), S(k)], True = kept
+    (see ``drop_keep`` in flash_attn.hip)."""
+    thr = min(int(p * 4294967296.0), _M32)
+    key0 = _fmix32_i((seed & _M32) ^ _fmix32_i(((seed >> 32) + 0x9E3779B9) & _M32))
+    key1 = _fmix32_i((((offset & _M32) * 0x27D4EB2F) & _M32) ^ _fmix32_i(((offset >> 32) + 0x165667B1) & _M32))
+    bh = torch.arange(B * H, dtype=torch.int64, device=device)
+    kbh = _fmix32_t((key0 + bh * 0x632BE5AB) & _M32) ^ key1                       # [BH]
+    cnt = (torch.arange(S, dtype=torch.int64, device=device)[:, None] * S
+           + torch.arange(S, dtype=torch.int64, device=device)[None, :])            # [S, S]
+    x = cnt[None] ^ kbh[:, None, None]
+    x = (x * 0x9E3779B1) & _M32
+    x = x ^ (x >> 15)
+    x = (x * 0x85EBCA77) & _M32
+    x = x ^ (x >> 13)
+    return (x >= thr).view(B, H, S, S)
+
+
+def attention_ref(q, k, v, scale, causal, dropout_p: float = 0.0, keep=None):
+    """Reference attention on [B, S, H, D] (GQA by head repetition), fp32 math. ``keep``
+    ([B, H, S, S] bool) is the dropout keep-mask (``flash_dropout_keep_mask``)."""
     B, S, H, D = q.shape
     Hkv = k.shape[2]
     if Hkv != H:
@@ -314,6 +354,11 @@ def attention_ref(q, k, v, scale, causal):
         cm = torch.ones(S, S, dtype=torch.bool, device=q.device).triu(1)
         s = s.masked_fill(cm, float("-inf"))
     p = torch.softmax(s, dim=-1)
+    if dropout_p > 0:
+        if keep is None:
+            p = torch.nn.functional.dropout(p, dropout_p, training=True)
+        else:
+            p = p * keep / (1.0 - dropout_p)
     o = torch.matmul(p, vf).transpose(1, 2)
     return o.to(q.dtype)
 
@@ -324,29 +369,40 @@ def flash_supported(q, k) -> bool:
             and q.stride(-1) == 1 and k.stride(-1) == 1)
 
 
-def flash_attention(q, k, v, scale: Optional[float] = None, causal: bool = True):
+def flash_attention(q, k, v, scale: Optional[float] = None, causal: bool = True, dropout_p: float = 0.0,
+                    rng: Optional[PhiloxState] = None):
     """Attention over [B, S, H, D] tensors (any batch/seq/head strides, unit last stride);
     ``k``/``v`` may have fewer heads (GQA)."""
     if scale is None:
         scale = 1.0 / math.sqrt(q.shape[-1])
+    seed, off = _rng(rng).next() if dropout_p > 0 else (0, 0)
     if _ext.use_kernels(q) and flash_supported(q, k):
-        return _FlashAttn.apply(q, k, v, float(scale), bool(causal))
-    return attention_ref(q, k, v, scale, causal)
+        return _FlashAttn.apply(q, k, v, float(scale), bool(causal), float(dropout_p), int(seed), int(off))
+    keep = flash_dropout_keep_mask(q.shape[0], q.shape[2], q.shape[1], dropout_p, seed, off, q.device) \
+        if dropout_p > 0 else None
+    return attention_ref(q, k, v, scale, causal, dropout_p, keep)
 
 
 def flash_attention_qkv(qkv, nh: int, nkv: int, hd: int, seq_first: bool = True, causal: bool = True,
-                        scale: Optional[float] = None):
+                        scale: Optional[float] = None, dropout_p: float = 0.0, rng: Optional[PhiloxState] = None):
     """Attention straight off a fused QKV projection output.
 
     ``qkv`` is [S, B, (nh + 2 nkv) hd] (``seq_first``) or [B, S, ...]; returns [S, B, nh hd]
-    (resp. [B, S, nh hd]). Backward produces ONE fused d(qkv) buffer.
+    (resp. [B, S, nh hd]). Backward produces ONE fused d(qkv) buffer. ``dropout_p`` > 0 applies
+    attention-probability dropout inside the kernels (mask re-derived from ``rng``'s
+    (seed, offset) in backward — nothing is stored).
     """
     if scale is None:
         scale = 1.0 / math.sqrt(hd)
     q, k, v = _qkv_views(qkv, nh, nkv, hd, seq_first)
+    seed, off = _rng(rng).next() if dropout_p > 0 else (0, 0)
     if _ext.use_kernels(qkv) and qkv.is_contiguous() and flash_supported(q, k) and (nh + 2 * nkv) * hd % 8 == 0:
-        return _FlashAttnQKV.apply(qkv, nh, nkv, hd, bool(seq_first), float(scale), bool(causal))
-    o = attention_ref(q, k, v, scale, causal)  # [B, S, H, D]
+        return _FlashAttnQKV.apply(qkv, nh, nkv, hd, bool(seq_first), float(scale), bool(causal),
+                                   float(dropout_p), int(seed), int(off))
+    keep = None
+    if dropout_p > 0:
+        keep = flash_dropout_keep_mask(q.shape[0], nh, q.shape[1], dropout_p, seed, off, qkv.device)
+    o = attention_ref(q, k, v, scale, causal, dropout_p, keep)  # [B, S, H, D]
     if seq_first:
         o = o.transpose(0, 1)
     return o.flatten(-2).contiguous()

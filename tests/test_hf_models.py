@@ -76,3 +76,14 @@ def test_builtin_configs():
     assert (c.num_layers, c.hidden_size, c.activation, c.position_offset) == (12, 768, "relu", 2)
     c = config_from_hf(BUILTIN["llama-7b"])
     assert (c.num_layers, c.hidden_size, c.ffn_hidden_size, c.normalization) == (32, 4096, 11008, "RMSNorm")
+
+
+def test_flash_dropout_mask_twin_properties():
+    from smdt_amd.ops.functional import flash_dropout_keep_mask
+    m1 = flash_dropout_keep_mask(2, 3, 128, 0.1, 42, 5)
+    m2 = flash_dropout_keep_mask(2, 3, 128, 0.1, 42, 5)
+    m3 = flash_dropout_keep_mask(2, 3, 128, 0.1, 42, 6)
+    assert torch.equal(m1, m2) and not torch.equal(m1, m3)
+    assert abs((1 - m1.float().mean().item()) - 0.1) < 0.01
+    # heads and batches draw independent masks
+    assert not torch.equal(m1[0, 0], m1[0, 1]) and not torch.equal(m1[0, 0], m1[1, 0])

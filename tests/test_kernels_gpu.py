@@ -269,6 +269,39 @@ def test_flash_attention(D, causal, heads):
         assert err < 0.05 * max(1.0, r.grad.abs().max().item()), err
 
 
+@pytest.mark.parametrize("D", [64, 128])
+@pytest.mark.parametrize("causal", [True, False])
+@pytest.mark.parametrize("heads", [(4, 4), (8, 2)])
+def test_flash_attention_dropout(D, causal, heads):
+    """In-kernel attention dropout == reference attention with the bit-exact twin of the
+    kernels' keep-mask (forward and all three gradients)."""
+    torch.manual_seed(12)
+    B, S = 2, 256
+    H, Hkv = heads
+    p, seed, off = 0.1, 1234, 77
+    q = torch.randn(B, S, H, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    k = torch.randn(B, S, Hkv, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    v = torch.randn(B, S, Hkv, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    scale = 1 / math.sqrt(D)
+    o = SF._FlashAttn.apply(q, k, v, scale, causal, p, seed, off)
+    keep = SF.flash_dropout_keep_mask(B, H, S, p, seed, off, DEV)
+    rate = 1 - keep.float().mean().item()
+    assert abs(rate - p) < 0.01, rate
+    qr, kr, vr = (t.detach().float().requires_grad_() for t in (q, k, v))
+    orf = SF.attention_ref(qr, kr, vr, scale, causal, p, keep)
+    torch.testing.assert_close(o.float(), orf, atol=2e-2, rtol=2e-2)
+    do = torch.randn_like(o)
+    o.backward(do)
+    orf.backward(do.float())
+    for a, r in ((q, qr), (k, kr), (v, vr)):
+        err = (a.grad.float() - r.grad).abs().max().item()
+        assert err < 0.05 * max(1.0, r.grad.abs().max().item()), err
+    # a different offset gives a different mask; same (seed, offset) is reproducible
+    o2 = SF._FlashAttn.apply(q.detach(), k.detach(), v.detach(), scale, causal, p, seed, off)
+    o3 = SF._FlashAttn.apply(q.detach(), k.detach(), v.detach(), scale, causal, p, seed, off + 1)
+    assert torch.equal(o2, o.detach()) and not torch.equal(o3, o2)
+
+
 def test_flash_attention_qkv_seq_first_matches_unfused():
     torch.manual_seed(11)
     S, B, nh, hd = 256, 2, 4, 64
