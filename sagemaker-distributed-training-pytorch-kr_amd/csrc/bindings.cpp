@@ -71,9 +71,19 @@ std::vector<Tensor> layernorm_fwd(Tensor x, OptT res, OptT bias, Tensor gamma, O
   return {y, make_s ? s : x, mean, rstd};
 }
 
+// dgamma_acc / dbeta_acc / dbias_acc (optional): fp32 [H] buffers (DDP main_grad views) the
+// parameter gradients are ACCUMULATED into instead of being returned.
+static Tensor acc_target(const OptT& t, int64_t H, const char* n) {
+  if (!t) return Tensor();
+  TORCH_CHECK(t->scalar_type() == at::kFloat && t->is_contiguous() && t->numel() == H, n,
+              ": accumulate target must be a contiguous fp32 tensor of ", H, " elements");
+  return *t;
+}
+
 std::vector<Tensor> layernorm_bwd(Tensor dy, OptT ds_in, Tensor s, Tensor gamma, Tensor mean,
                                   Tensor rstd, double p_drop, int64_t seed, int64_t offset,
-                                  bool rms, bool want_dx, bool want_dbias) {
+                                  bool rms, bool want_dx, bool want_dbias, OptT dgamma_acc,
+                                  OptT dbeta_acc, OptT dbias_acc) {
   need_contig(dy, "dy");
   need_contig(s, "s");
   need_contig(gamma, "gamma");
@@ -87,16 +97,19 @@ std::vector<Tensor> layernorm_bwd(Tensor dy, OptT ds_in, Tensor s, Tensor gamma,
   const int nb = smdt_ln_bwd_nblocks(rows, (int)H);
   auto f32 = s.options().dtype(at::kFloat);
   auto partials = torch::empty({nb, 3, H}, f32);
-  auto dgamma = torch::empty({H}, f32);
-  Tensor dbeta = rms ? Tensor() : torch::empty({H}, f32);
-  Tensor dbias = want_dbias ? torch::empty({H}, f32) : Tensor();
+  Tensor ga = acc_target(dgamma_acc, H, "dgamma_acc"), ba = acc_target(dbeta_acc, H, "dbeta_acc"),
+         bia = acc_target(dbias_acc, H, "dbias_acc");
+  const int acc_mask = (ga.defined() ? 1 : 0) | (ba.defined() ? 2 : 0) | (bia.defined() ? 4 : 0);
+  auto dgamma = ga.defined() ? ga : torch::empty({H}, f32);
+  Tensor dbeta = rms ? Tensor() : (ba.defined() ? ba : torch::empty({H}, f32));
+  Tensor dbias = want_dbias ? (bia.defined() ? bia : torch::empty({H}, f32)) : Tensor();
   check(smdt_layernorm_bwd(dcode(s), dcode(gamma), dy.data_ptr(), optr(ds_in), s.data_ptr(),
                            gamma.data_ptr(), rms ? nullptr : mean.data_ptr<float>(),
                            rstd.data_ptr<float>(), ds.data_ptr(), dx.data_ptr(),
                            partials.data_ptr<float>(), nb, dgamma.data_ptr<float>(),
                            rms ? nullptr : dbeta.data_ptr<float>(),
                            want_dbias ? dbias.data_ptr<float>() : nullptr, rows, (int)H,
-                           (float)p_drop, (uint64_t)seed, (uint64_t)offset, rms ? 1 : 0,
+                           (float)p_drop, (uint64_t)seed, (uint64_t)offset, rms ? 1 : 0, acc_mask,
                            cur_stream()),
         "layernorm_bwd");
   return {ds, dx, dgamma, rms ? dgamma.new_empty({0}) : dbeta,
@@ -115,7 +128,8 @@ Tensor bias_act_fwd(Tensor x, OptT bias, int64_t act) {
   return y;
 }
 
-std::vector<Tensor> bias_act_bwd(Tensor dy, Tensor x, OptT bias, int64_t act, bool want_dbias) {
+std::vector<Tensor> bias_act_bwd(Tensor dy, Tensor x, OptT bias, int64_t act, bool want_dbias,
+                                 OptT dbias_acc) {
   need_contig(dy, "dy");
   need_contig(x, "x");
   TORCH_CHECK(dy.sizes() == x.sizes() && dy.dtype() == x.dtype(), "bias_act_bwd: shape mismatch");
@@ -125,12 +139,12 @@ std::vector<Tensor> bias_act_bwd(Tensor dy, Tensor x, OptT bias, int64_t act, bo
   if (want_dbias) {
     const int slices = smdt_bias_act_slices(rows, (int)N);
     part = torch::empty({slices, N}, x.options().dtype(at::kFloat));
-    dbias = torch::empty({N}, x.options().dtype(at::kFloat));
+    dbias = dbias_acc ? acc_target(dbias_acc, N, "dbias_acc") : torch::empty({N}, x.options().dtype(at::kFloat));
   }
   check(smdt_bias_act_bwd(dcode(x), (int)act, dy.data_ptr(), x.data_ptr(), optr(bias),
                           dx.data_ptr(), want_dbias ? part.data_ptr<float>() : nullptr,
                           want_dbias ? dbias.data_ptr<float>() : nullptr, rows, (int)N,
-                          cur_stream()),
+                          dbias_acc ? 1 : 0, cur_stream()),
         "bias_act_bwd");
   return {dx, want_dbias ? dbias : dx.new_empty({0})};
 }
@@ -278,6 +292,19 @@ void rope_(Tensor x, Tensor cos_t, Tensor sin_t, int64_t rot, int64_t pos_div, i
         "rope");
 }
 
+// ------------------------------------------------------------------ bias gradient
+// out[N] (fp32) = / += column sums of dy [.., N]
+void bias_grad(Tensor dy, Tensor out, bool accumulate) {
+  need_contig(dy, "dy");
+  const int64_t N = dy.size(-1), rows = dy.numel() / N;
+  Tensor o = acc_target(out, N, "bias_grad out");
+  const int slices = smdt_bias_act_slices(rows, (int)N);
+  auto part = torch::empty({slices, N}, dy.options().dtype(at::kFloat));
+  check(smdt_bias_grad(dcode(dy), dy.data_ptr(), rows, (int)N, part.data_ptr<float>(),
+                       o.data_ptr<float>(), accumulate ? 1 : 0, cur_stream()),
+        "bias_grad");
+}
+
 // ------------------------------------------------------------------ cross entropy
 std::vector<Tensor> ce_stats(Tensor logits, Tensor target, int64_t vstart, int64_t vvalid) {
   need_contig(logits, "logits");
@@ -391,9 +418,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "smdt_amd gfx950 (MI355X) HIP kernel library";
   register_blaslt(m);
   m.def("layernorm_fwd", &layernorm_fwd);
-  m.def("layernorm_bwd", &layernorm_bwd);
+  using pybind11::arg;
+  m.def("layernorm_bwd", &layernorm_bwd, arg("dy"), arg("ds_in"), arg("s"), arg("gamma"), arg("mean"),
+        arg("rstd"), arg("p_drop"), arg("seed"), arg("offset"), arg("rms"), arg("want_dx"), arg("want_dbias"),
+        arg("dgamma_acc") = pybind11::none(), arg("dbeta_acc") = pybind11::none(),
+        arg("dbias_acc") = pybind11::none());
   m.def("bias_act_fwd", &bias_act_fwd);
-  m.def("bias_act_bwd", &bias_act_bwd);
+  m.def("bias_act_bwd", &bias_act_bwd, arg("dy"), arg("x"), arg("bias"), arg("act"), arg("want_dbias"),
+        arg("dbias_acc") = pybind11::none());
   m.def("swiglu_fwd", &swiglu_fwd);
   m.def("swiglu_bwd", &swiglu_bwd);
   m.def("softmax_fwd", &softmax_fwd);
@@ -404,6 +436,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("scale_", &scale_);
   m.def("cast_", &cast_);
   m.def("rope_", &rope_);
+  m.def("bias_grad", &bias_grad);
   m.def("ce_stats", &ce_stats);
   m.def("ce_bwd", &ce_bwd);
   namespace py = pybind11;

@@ -140,8 +140,31 @@ __global__ __launch_bounds__(256) void swiglu_bwd_kernel(const T* __restrict__ d
 
 __global__ __launch_bounds__(256) void col_partials_reduce_kernel(const float* __restrict__ part,
                                                                  int nslices, int N,
-                                                                 float* __restrict__ out) {
-  colsum_block(part, nslices, N, N, out);
+                                                                 float* __restrict__ out,
+                                                                 int accumulate) {
+  colsum_block(part, nslices, N, N, out, accumulate != 0);
+}
+
+// Column sums of a [rows, N] matrix (a linear layer's bias gradient), phase 1: per row-slice
+// fp32 partials; phase 2 is col_partials_reduce_kernel.
+template <typename T>
+__global__ __launch_bounds__(256) void col_sum_rows_kernel(const T* __restrict__ x,
+                                                          float* __restrict__ part, int64_t rows,
+                                                          int N, int rows_per_slice) {
+  const int c = (blockIdx.x * 256 + threadIdx.x) * 8;
+  if (c >= N) return;
+  const int64_t r0 = (int64_t)blockIdx.y * rows_per_slice;
+  const int64_t r1 = r0 + rows_per_slice < rows ? r0 + rows_per_slice : rows;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int64_t r = r0; r < r1; ++r) {
+    float v[8];
+    load_vec<T, 8>(x + r * N + c, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] += v[j];
+  }
+  float* o = part + (int64_t)blockIdx.y * N + c;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = acc[j];
 }
 
 // Rows per slice so that (column blocks) x (row slices) ~ 1024 blocks.
@@ -182,7 +205,8 @@ extern "C" hipError_t smdt_bias_act_fwd(int dtype, int act, const void* x, const
 
 extern "C" hipError_t smdt_bias_act_bwd(int dtype, int act, const void* dy, const void* x,
                                         const void* bias, void* dx, float* partials,
-                                        float* dbias, int64_t rows, int N, hipStream_t st) {
+                                        float* dbias, int64_t rows, int N, int accumulate,
+                                        hipStream_t st) {
   if (N % 8 != 0 || rows <= 0) return hipErrorInvalidValue;
   int rps;
   int slices = act_slices(rows, N, &rps);
@@ -197,15 +221,29 @@ extern "C" hipError_t smdt_bias_act_bwd(int dtype, int act, const void* dy, cons
 #undef SMDT_BA_BWD
   if (dbias) {
     hipLaunchKernelGGL(col_partials_reduce_kernel, dim3((N + 31) / 32), dim3(256), 0, st,
-                       partials, slices, N, dbias);
+                       partials, slices, N, dbias, accumulate);
   }
   return hipGetLastError();
 }
 
 extern "C" hipError_t smdt_col_sum(const float* partials, int nslices, int N, float* out,
-                                   hipStream_t st) {
+                                   int accumulate, hipStream_t st) {
   hipLaunchKernelGGL(col_partials_reduce_kernel, dim3((N + 31) / 32), dim3(256), 0, st,
-                     partials, nslices, N, out);
+                     partials, nslices, N, out, accumulate);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t smdt_bias_grad(int dtype, const void* dy, int64_t rows, int N,
+                                     float* partials, float* out, int accumulate, hipStream_t st) {
+  if (N % 8 != 0 || rows <= 0) return hipErrorInvalidValue;
+  int rps;
+  int slices = act_slices(rows, N, &rps);
+  dim3 grid((N / 8 + 255) / 256, slices);
+  if (dtype == 1) hipLaunchKernelGGL(col_sum_rows_kernel<bf16>, grid, dim3(256), 0, st, (const bf16*)dy, partials, rows, N, rps);
+  else if (dtype == 2) hipLaunchKernelGGL(col_sum_rows_kernel<f16>, grid, dim3(256), 0, st, (const f16*)dy, partials, rows, N, rps);
+  else hipLaunchKernelGGL(col_sum_rows_kernel<float>, grid, dim3(256), 0, st, (const float*)dy, partials, rows, N, rps);
+  hipLaunchKernelGGL(col_partials_reduce_kernel, dim3((N + 31) / 32), dim3(256), 0, st, partials,
+                     slices, N, out, accumulate);
   return hipGetLastError();
 }
 

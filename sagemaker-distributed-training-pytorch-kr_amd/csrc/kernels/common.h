@@ -166,8 +166,10 @@ __device__ __forceinline__ void philox_uniform4(uint64_t seed, uint64_t offset, 
 // 32 columns x 8 row groups (128-byte coalesced row segments, 8x more loads in flight than a
 // thread-per-column loop); the 8 group sums are combined in a fixed order (deterministic).
 // Launch with grid.x = ceil(ncols / 32).
+// out[col] (=|+=) sum_r part[r * rs + col]; accumulate=true adds into an existing fp32 buffer
+// (e.g. a DDP main_grad), so no separate cast/add pass is needed.
 __device__ __forceinline__ void colsum_block(const float* __restrict__ part, int nrows, int64_t rs,
-                                             int ncols, float* __restrict__ out) {
+                                             int ncols, float* __restrict__ out, bool accumulate = false) {
   __shared__ float red[8][33];
   const int cl = threadIdx.x & 31, rg = threadIdx.x >> 5;
   const int col = blockIdx.x * 32 + cl;
@@ -186,7 +188,7 @@ __device__ __forceinline__ void colsum_block(const float* __restrict__ part, int
     float s = 0.f;
 #pragma unroll
     for (int g = 0; g < 8; ++g) s += red[g][cl];
-    out[col] = s;
+    out[col] = accumulate ? out[col] + s : s;
   }
 }
 

@@ -174,11 +174,13 @@ struct Strides {
   int64_t sb, ss, sh;
 };
 
-// Attention dropout. Element (b, h, q, k) is kept iff hash(q * S + k, key(b, h)) >= thr
-// (thr = p * 2^32); kept probabilities are scaled by inv = 1 / (1 - p). The forward and both
-// backward kernels re-derive the identical mask from the counter (no mask tensor in HBM). The
-// hash is a keyed two-round multiply/xor-shift mixer (~8 VALU per element): Philox-7 costs ~4x
-// that per element and would dominate the MFMA work of the attention tile on CDNA4.
+// Attention dropout. Elements (q, 2j) and (q, 2j + 1) share one 32-bit hash of the pair
+// counter (q * S + 2j) / 2 keyed by (seed, offset, b, h): the low 16 bits decide the even key,
+// the high 16 bits the odd key (kept iff >= thr = p * 2^16; kept probabilities are scaled by
+// inv = 1 / (1 - thr / 2^16)). The forward and both backward kernels re-derive the identical
+// mask from the counter, so no mask tensor is stored. The hash is a keyed two-round
+// multiply/xor-shift mixer (~8 VALU per pair); Philox-7 would cost ~8x that per element and
+// dominate the MFMA work of an attention tile on CDNA4.
 struct Drop {
   uint32_t thr, key0, key1;
   float inv;
@@ -195,14 +197,17 @@ __device__ __forceinline__ uint32_t fmix32(uint32_t x) {
 __device__ __forceinline__ uint32_t drop_key(const Drop& d, int bh) {
   return fmix32(d.key0 + (uint32_t)bh * 0x632BE5ABu) ^ d.key1;
 }
-__device__ __forceinline__ bool drop_keep(uint32_t counter, uint32_t key, uint32_t thr) {
-  uint32_t x = counter ^ key;
+__device__ __forceinline__ uint32_t drop_hash(uint32_t pair, uint32_t key) {
+  uint32_t x = pair ^ key;
   x *= 0x9E3779B1u;
   x ^= x >> 15;
   x *= 0x85EBCA77u;
   x ^= x >> 13;
-  return x >= thr;
+  return x;
 }
+// keep decisions of the even / odd key of a pair
+__device__ __forceinline__ bool keep_lo(uint32_t h, uint32_t thr) { return (h & 0xFFFFu) >= thr; }
+__device__ __forceinline__ bool keep_hi(uint32_t h, uint32_t thr) { return (h >> 16) >= thr; }
 
 // ---------------------------------------------------------------------------------------
 // Forward. Workgroup = 4 waves = 128 query rows of one (b, h); K/V streamed in 64-key tiles,
@@ -245,7 +250,7 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void fwd_kernel(const bf16* _
   const int kend = CAUSAL ? (q0 + kBlockRows) : S;
   const int ntiles = kend / kTile;
   const uint32_t dkey = DROP ? drop_key(drop, bh) : 0u;
-  const uint32_t dbase = (uint32_t)my_q * (uint32_t)S + 4u * h;  // counter of key row 0 (+ kb)
+  const uint32_t dpair = ((uint32_t)my_q * (uint32_t)S + 4u * h) >> 1;  // pair counter of key row 0
   Stage<D> sk, sv;
   sk.init(ks_.ss);
   sv.init(vs.ss);
@@ -296,12 +301,18 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void fwd_kernel(const bf16* _
         for (int i = 0; i < 16; ++i) {
           const float p = fexp2(fmaf(st[tt][i], c2, -base));
           rs += p;  // the softmax denominator uses the un-dropped probabilities
-          if constexpr (DROP)
-            st[tt][i] = drop_keep(dbase + kb + 32 * tt + (i & 3) + 8 * (i >> 2), dkey, drop.thr)
-                            ? p * drop.inv : 0.f;
-          else
-            st[tt][i] = p;
+          st[tt][i] = p;
         }
+      if constexpr (DROP) {
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+          for (int i = 0; i < 16; i += 2) {  // registers i, i+1 = keys 2j, 2j+1
+            const uint32_t hv = drop_hash(dpair + ((kb + 32 * tt + (i & 3) + 8 * (i >> 2)) >> 1), dkey);
+            st[tt][i] = keep_lo(hv, drop.thr) ? st[tt][i] * drop.inv : 0.f;
+            st[tt][i + 1] = keep_hi(hv, drop.thr) ? st[tt][i + 1] * drop.inv : 0.f;
+          }
+      }
       l = l * alpha + xhalf_sum(rs);
       m = mnew;
 #pragma unroll
@@ -444,7 +455,8 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dkdv_kernel(
     const int qb = qstart + (it % ntiles) * kTile;
     const bool more = it + 1 < total;
     const uint32_t dkey = DROP ? drop_key(drop, b * H + hk * group + it / ntiles) : 0u;
-    const uint32_t dbase = (uint32_t)(qb + 4 * h) * (uint32_t)S + (uint32_t)my_key;
+    const uint32_t dpair = ((uint32_t)(qb + 4 * h) * (uint32_t)S + (uint32_t)my_key) >> 1;
+    const uint32_t shalf = (uint32_t)S >> 1;
     const char* buf = lds + (it & 1) * BUF;
     const char* q_l = buf;
     const char* do_l = buf + G::TB;
@@ -474,8 +486,8 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dkdv_kernel(
           float p = fexp2(fmaf(s[i], c2, -lv[j]));
           if (diag && my_key > qb + r0 + j) p = 0.f;
           if constexpr (DROP) {
-            const bool keep = drop_keep(dbase + (uint32_t)(32 * qs2 + 8 * g + j) * (uint32_t)S, dkey,
-                                        drop.thr);
+            const uint32_t hv = drop_hash(dpair + (uint32_t)(32 * qs2 + 8 * g + j) * shalf, dkey);
+            const bool keep = (my_key & 1) ? keep_hi(hv, drop.thr) : keep_lo(hv, drop.thr);
             s[i] = keep ? p * drop.inv : 0.f;                   // dropped P (feeds dV)
             dp[i] = p * ((keep ? dp[i] * drop.inv : 0.f) - dl[j]);  // dS
           } else {
@@ -549,7 +561,7 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dq_kernel(
   const float dl = DELTA[((int64_t)b * H + hq) * S + my_q];
   const float c2 = scale * kLog2e;
   const uint32_t dkey = DROP ? drop_key(drop, bh) : 0u;
-  const uint32_t dbase = (uint32_t)my_q * (uint32_t)S + 4u * h;
+  const uint32_t dpair = ((uint32_t)my_q * (uint32_t)S + 4u * h) >> 1;
 
   const bf16* Kb = K + b * ks_.sb + hk * ks_.sh;
   const bf16* Vb = V + b * vs.sb + hk * vs.sh;
@@ -591,14 +603,16 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dq_kernel(
       const bool diag = CAUSAL && ksub + 31 > qw;
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
+        if constexpr (DROP) {
+          if ((i & 1) == 0) {
+            const uint32_t hv = drop_hash(dpair + ((ksub + (i & 3) + 8 * (i >> 2)) >> 1), dkey);
+            if (!keep_lo(hv, drop.thr)) dpt[i] = 0.f;
+            if (!keep_hi(hv, drop.thr)) dpt[i + 1] = 0.f;
+          }
+        }
         float p = fexp2(fmaf(st[i], c2, -lse2));
         if (diag && ksub + acc_row(i, h) > my_q) p = 0.f;
-        if constexpr (DROP) {
-          const bool keep = drop_keep(dbase + ksub + (i & 3) + 8 * (i >> 2), dkey, drop.thr);
-          dpt[i] = p * ((keep ? dpt[i] * drop.inv : 0.f) - dl);  // dS^T
-        } else {
-          dpt[i] = p * (dpt[i] - dl);  // dS^T
-        }
+        dpt[i] = p * ((DROP ? dpt[i] * drop.inv : dpt[i]) - dl);  // dS^T
       }
       // dQ^T[d, q] += K^T[d, keys] . dS^T[keys, q]
 #pragma unroll
@@ -649,12 +663,12 @@ static uint32_t host_fmix32(uint32_t x) {
   return x;
 }
 
-// keys: key0 from the seed, key1 from the per-call offset (see drop_key / drop_keep).
+// keys: key0 from the seed, key1 from the per-call offset (see drop_key / drop_hash).
 static Drop make_drop(float p, uint64_t seed, uint64_t offset) {
   Drop d;
-  double t = (double)p * 4294967296.0;
-  d.thr = t >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)t;
-  d.inv = p < 1.f ? 1.f / (1.f - p) : 0.f;
+  d.thr = (uint32_t)((double)p * 65536.0 + 0.5);
+  if (d.thr > 65535u) d.thr = 65535u;
+  d.inv = (float)(65536.0 / (65536.0 - (double)d.thr));  // exact for the realised drop rate
   d.key0 = host_fmix32((uint32_t)seed ^ host_fmix32((uint32_t)(seed >> 32) + 0x9E3779B9u));
   d.key1 = host_fmix32((uint32_t)offset * 0x27D4EB2Fu ^ host_fmix32((uint32_t)(offset >> 32) + 0x165667B1u));
   return d;

@@ -21,7 +21,7 @@ hipError_t smdt_layernorm_bwd(int dtype, int wdtype, const void* dy, const void*
                               const float* rstd, void* ds_out, void* dx_out, float* partials,
                               int nblocks, float* dgamma, float* dbeta, float* dbias,
                               int64_t rows, int H, float p_drop, uint64_t seed, uint64_t offset,
-                              int rms, hipStream_t st);
+                              int rms, int acc_mask, hipStream_t st);
 
 // bias_act.hip
 int smdt_bias_act_slices(int64_t rows, int N);
@@ -29,8 +29,12 @@ hipError_t smdt_bias_act_fwd(int dtype, int act, const void* x, const void* bias
                              int64_t rows, int N, hipStream_t st);
 hipError_t smdt_bias_act_bwd(int dtype, int act, const void* dy, const void* x, const void* bias,
                              void* dx, float* partials, float* dbias, int64_t rows, int N,
-                             hipStream_t st);
-hipError_t smdt_col_sum(const float* partials, int nslices, int N, float* out, hipStream_t st);
+                             int accumulate, hipStream_t st);
+hipError_t smdt_col_sum(const float* partials, int nslices, int N, float* out, int accumulate,
+                        hipStream_t st);
+// column sums of dy [rows, N] into out[N] (fp32; accumulate = add into out)
+hipError_t smdt_bias_grad(int dtype, const void* dy, int64_t rows, int N, float* partials,
+                          float* out, int accumulate, hipStream_t st);
 hipError_t smdt_swiglu_fwd(int dtype, const void* x, void* y, int64_t rows, int F,
                            hipStream_t st);
 hipError_t smdt_swiglu_bwd(int dtype, const void* dy, const void* x, void* dx, int64_t rows,

@@ -304,12 +304,13 @@ __global__ __launch_bounds__(256) void ln_partials_reduce_kernel(const float* __
                                                                 int nblocks, int H,
                                                                 float* __restrict__ dgamma,
                                                                 float* __restrict__ dbeta,
-                                                                float* __restrict__ dbias) {
-  // blockIdx.y selects the quantity (slab rows have stride 3H).
+                                                                float* __restrict__ dbias,
+                                                                int acc_mask) {
+  // blockIdx.y selects the quantity (slab rows have stride 3H); bit q of acc_mask = accumulate.
   const int q = blockIdx.y;
   float* out = q == 0 ? dgamma : (q == 1 ? dbeta : dbias);
   if (out == nullptr) return;
-  colsum_block(part + (int64_t)q * H, nblocks, 3 * (int64_t)H, H, out);
+  colsum_block(part + (int64_t)q * H, nblocks, 3 * (int64_t)H, H, out, (acc_mask >> q) & 1);
 }
 
 template <typename T, typename W, int G>
@@ -404,7 +405,7 @@ extern "C" hipError_t smdt_layernorm_bwd(int dtype, int wdtype, const void* dy, 
                                          float* partials, int nblocks, float* dgamma,
                                          float* dbeta, float* dbias, int64_t rows, int H,
                                          float p_drop, uint64_t seed, uint64_t offset, int rms,
-                                         hipStream_t st) {
+                                         int acc_mask, hipStream_t st) {
   if (H % 8 != 0 || H > 16384) return hipErrorInvalidValue;
   LnBwdArgs a{dy, ds_in, s, gamma, mean, rstd, ds_out, dx_out, partials, rows, H, p_drop, seed,
               offset, rms, dbias != nullptr, nblocks};
@@ -418,6 +419,6 @@ extern "C" hipError_t smdt_layernorm_bwd(int dtype, int wdtype, const void* dy, 
   if (e != hipSuccess) return e;
   dim3 grid((H + 31) / 32, 3);
   hipLaunchKernelGGL(ln_partials_reduce_kernel, grid, dim3(256), 0, st, partials, nblocks, H,
-                     dgamma, rms ? nullptr : dbeta, dbias);
+                     dgamma, rms ? nullptr : dbeta, dbias, acc_mask);
   return hipGetLastError();
 }

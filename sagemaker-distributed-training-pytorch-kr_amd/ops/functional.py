@@ -69,6 +69,24 @@ def _ln_ref(s, gamma, beta, eps, rms):
     return y.to(s.dtype)
 
 
+def grad_accumulate_target(t):
+    """The fp32 DDP ``main_grad`` of parameter ``t`` if a kernel may accumulate the parameter's
+    gradient straight into it (then the kernel owner calls ``t._smdt_grad_ready``), else None."""
+    if t is None or not isinstance(t, torch.nn.Parameter):
+        return None
+    mg = getattr(t, "main_grad", None)
+    if (mg is None or mg.dtype != torch.float32 or not mg.is_cuda or not mg.is_contiguous()
+            or getattr(t, "_smdt_grad_ready", None) is None):
+        return None
+    return mg
+
+
+def _mark_ready(*params):
+    for t in params:
+        if t is not None:
+            t._smdt_grad_ready(t)
+
+
 class _BDALayerNorm(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, bias, residual, gamma, beta, p, eps, rms, seed, offset):
@@ -76,6 +94,7 @@ class _BDALayerNorm(torch.autograd.Function):
         y, s, mean, rstd = C.layernorm_fwd(x.contiguous(), None if residual is None else residual.contiguous(),
                                            bias, gamma, beta, eps, p, seed, offset, rms, True)
         ctx.save_for_backward(s, gamma, mean, rstd)
+        ctx.pref = (bias, gamma, beta)  # parameter objects: their main_grad / readiness hooks
         ctx.cfg = (p, seed, offset, rms, bias is not None, residual is not None, beta is not None,
                    gamma.dtype, None if bias is None else bias.dtype)
         return y, s
@@ -87,10 +106,19 @@ class _BDALayerNorm(torch.autograd.Function):
         C = _ext.ext()
         dy = dy.contiguous()
         ds = None if ds is None else ds.contiguous()
+        bias_p, gamma_p, beta_p = ctx.pref
+        # bias / gamma / beta gradients go straight into fp32 main_grad when DDP owns them
+        ta = grad_accumulate_target(gamma_p)
+        tb = grad_accumulate_target(beta_p) if has_beta else None
+        tc = grad_accumulate_target(bias_p) if has_bias else None
         d_s, dx, dgamma, dbeta, dbias = C.layernorm_bwd(dy, ds, s, gamma, mean, rstd, p, seed, offset, rms,
-                                                        True, has_bias)
-        return (dx, dbias.to(bdt) if has_bias else None, d_s if has_res else None,
-                dgamma.to(gdt), dbeta.to(gdt) if has_beta else None, None, None, None, None, None)
+                                                        True, has_bias, ta, tb, tc)
+        _mark_ready(gamma_p if ta is not None else None, beta_p if tb is not None else None,
+                    bias_p if tc is not None else None)
+        g_gamma = None if ta is not None else dgamma.to(gdt)
+        g_beta = None if (not has_beta or tb is not None) else dbeta.to(gdt)
+        g_bias = None if (not has_bias or tc is not None) else dbias.to(bdt)
+        return (dx, g_bias, d_s if has_res else None, g_gamma, g_beta, None, None, None, None, None)
 
 
 def bias_dropout_add_norm(x, bias, residual, gamma, beta, p: float, training: bool, eps: float = 1e-5,
@@ -147,6 +175,7 @@ class _BiasAct(torch.autograd.Function):
         x = x.contiguous()
         y = C.bias_act_fwd(x, bias, act)
         ctx.save_for_backward(x, bias)
+        ctx.bias_p = bias
         ctx.act = act
         ctx.has_bias = bias is not None
         return y
@@ -155,7 +184,11 @@ class _BiasAct(torch.autograd.Function):
     def backward(ctx, dy):
         x, bias = ctx.saved_tensors
         C = _ext.ext()
-        dx, dbias = C.bias_act_bwd(dy.contiguous(), x, bias, ctx.act, ctx.has_bias)
+        tgt = grad_accumulate_target(ctx.bias_p) if ctx.has_bias else None
+        dx, dbias = C.bias_act_bwd(dy.contiguous(), x, bias, ctx.act, ctx.has_bias, tgt)
+        if tgt is not None:
+            _mark_ready(ctx.bias_p)
+            return dx, None, None
         return dx, (dbias.to(bias.dtype) if ctx.has_bias else None), None
 
 
@@ -322,22 +355,29 @@ def _fmix32_i(x: int) -> int:
     return x ^ (x >> 16)
 
 
+def flash_dropout_thr(p: float):
+    """(16-bit threshold, keep scale) the kernels use for drop probability ``p``."""
+    thr = min(int(p * 65536.0 + 0.5), 65535)
+    return thr, 65536.0 / (65536.0 - thr)
+
+
 def flash_dropout_keep_mask(B: int, H: int, S: int, p: float, seed: int, offset: int, device=None):
     """Bit-exact twin of the flash kernels' dropout mask: bool [B, H, S(q), S(k)], True = kept
-    (see ``drop_keep`` in flash_attn.hip)."""
-    thr = min(int(p * 4294967296.0), _M32)
+    (see ``drop_hash`` in flash_attn.hip). Keys 2j and 2j+1 of a query share one hash."""
+    thr, _ = flash_dropout_thr(p)
     key0 = _fmix32_i((seed & _M32) ^ _fmix32_i(((seed >> 32) + 0x9E3779B9) & _M32))
     key1 = _fmix32_i((((offset & _M32) * 0x27D4EB2F) & _M32) ^ _fmix32_i(((offset >> 32) + 0x165667B1) & _M32))
     bh = torch.arange(B * H, dtype=torch.int64, device=device)
-    kbh = _fmix32_t((key0 + bh * 0x632BE5AB) & _M32) ^ key1                       # [BH]
-    cnt = (torch.arange(S, dtype=torch.int64, device=device)[:, None] * S
-           + torch.arange(S, dtype=torch.int64, device=device)[None, :])            # [S, S]
-    x = cnt[None] ^ kbh[:, None, None]
+    kbh = _fmix32_t((key0 + bh * 0x632BE5AB) & _M32) ^ key1                        # [BH]
+    pair = (torch.arange(S, dtype=torch.int64, device=device)[:, None] * S
+            + torch.arange(0, S, 2, dtype=torch.int64, device=device)[None, :]) >> 1  # [S, S/2]
+    x = pair[None] ^ kbh[:, None, None]
     x = (x * 0x9E3779B1) & _M32
     x = x ^ (x >> 15)
     x = (x * 0x85EBCA77) & _M32
     x = x ^ (x >> 13)
-    return (x >= thr).view(B, H, S, S)
+    keep = torch.stack([(x & 0xFFFF) >= thr, (x >> 16) >= thr], dim=-1)            # [BH, S, S/2, 2]
+    return keep.reshape(B, H, S, S)
 
 
 def attention_ref(q, k, v, scale, causal, dropout_p: float = 0.0, keep=None):
@@ -358,7 +398,7 @@ def attention_ref(q, k, v, scale, causal, dropout_p: float = 0.0, keep=None):
         if keep is None:
             p = torch.nn.functional.dropout(p, dropout_p, training=True)
         else:
-            p = p * keep / (1.0 - dropout_p)
+            p = p * keep * flash_dropout_thr(dropout_p)[1]
     o = torch.matmul(p, vf).transpose(1, 2)
     return o.to(q.dtype)
 

@@ -28,6 +28,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops import _ext
+from ..ops import functional as SF
 from . import state as ps
 
 # --------------------------------------------------------------------------------------------
@@ -232,6 +233,7 @@ class LinearWithGradAccumulationAndAsyncCommunication(torch.autograd.Function):
         ctx.sp = sequence_parallel
         ctx.async_ar = async_grad_allreduce
         ctx.has_bias = bias is not None
+        ctx.bias_p = bias
         ctx.save_for_backward(x, weight)
         total = _gather_dim0(x, _tp_group()) if sequence_parallel else x
         return F.linear(total, weight, bias)
@@ -254,7 +256,14 @@ class LinearWithGradAccumulationAndAsyncCommunication(torch.autograd.Function):
         g2 = g.reshape(-1, g.shape[-1])
         t2 = total.reshape(-1, total.shape[-1])
         dw = _wgrad(weight, g2, t2)
-        db = g2.sum(0) if ctx.has_bias else None
+        db = None
+        if ctx.has_bias:
+            tgt = SF.grad_accumulate_target(ctx.bias_p)
+            if tgt is not None and g2.is_contiguous() and g2.shape[-1] % 8 == 0:
+                _ext.ext().bias_grad(g2, tgt, True)  # column sums accumulated into fp32 main_grad
+                ctx.bias_p._smdt_grad_ready(ctx.bias_p)
+            else:
+                db = g2.sum(0)
         if handle is not None:
             handle.wait()
         return gi_out, dw, db, None, None
