@@ -174,13 +174,14 @@ struct Strides {
   int64_t sb, ss, sh;
 };
 
-// Attention dropout. Elements (q, 2j) and (q, 2j + 1) share one 32-bit hash of the pair
-// counter (q * S + 2j) / 2 keyed by (seed, offset, b, h): the low 16 bits decide the even key,
-// the high 16 bits the odd key (kept iff >= thr = p * 2^16; kept probabilities are scaled by
-// inv = 1 / (1 - thr / 2^16)). The forward and both backward kernels re-derive the identical
-// mask from the counter, so no mask tensor is stored. The hash is a keyed two-round
-// multiply/xor-shift mixer (~8 VALU per pair); Philox-7 would cost ~8x that per element and
-// dominate the MFMA work of an attention tile on CDNA4.
+// Attention dropout. The 2x2 block (q, k), q, k in {2i, 2i+1} x {2j, 2j+1} shares one 32-bit
+// hash of the block counter (q/2) * (S/2) + k/2 keyed by (seed, offset, b, h); byte
+// 2 (q & 1) + (k & 1) of it decides the element (kept iff byte >= thr = round(p * 256); kept
+// probabilities are scaled by inv = 256 / (256 - thr) — 8-bit thresholds as in FlashAttention-2).
+// Every kernel (query-on-lane or key-on-lane) uses 2 bytes per hash, so hashing costs half an
+// evaluation per element everywhere. The forward and both backward kernels re-derive the identical
+// mask, no mask tensor is stored. The hash is a keyed two-round multiply/xor-shift mixer;
+// Philox-7 would cost several times more VALU than the MFMA work of an attention tile on CDNA4.
 struct Drop {
   uint32_t thr, key0, key1;
   float inv;
@@ -205,9 +206,7 @@ __device__ __forceinline__ uint32_t drop_hash(uint32_t pair, uint32_t key) {
   x ^= x >> 13;
   return x;
 }
-// keep decisions of the even / odd key of a pair
-__device__ __forceinline__ bool keep_lo(uint32_t h, uint32_t thr) { return (h & 0xFFFFu) >= thr; }
-__device__ __forceinline__ bool keep_hi(uint32_t h, uint32_t thr) { return (h >> 16) >= thr; }
+__device__ __forceinline__ bool keep_byte(uint32_t h, int sh, uint32_t thr) { return ((h >> sh) & 0xFFu) >= thr; }
 
 // ---------------------------------------------------------------------------------------
 // Forward. Workgroup = 4 waves = 128 query rows of one (b, h); K/V streamed in 64-key tiles,
@@ -250,7 +249,9 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void fwd_kernel(const bf16* _
   const int kend = CAUSAL ? (q0 + kBlockRows) : S;
   const int ntiles = kend / kTile;
   const uint32_t dkey = DROP ? drop_key(drop, bh) : 0u;
-  const uint32_t dpair = ((uint32_t)my_q * (uint32_t)S + 4u * h) >> 1;  // pair counter of key row 0
+  const uint32_t shalf = (uint32_t)S >> 1;
+  const uint32_t dblk = (uint32_t)(my_q >> 1) * shalf + 2u * h;  // block counter of key row 0
+  const int dsh = 16 * (my_q & 1);                                // byte 2 (q & 1) + (k & 1)
   Stage<D> sk, sv;
   sk.init(ks_.ss);
   sv.init(vs.ss);
@@ -308,9 +309,9 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void fwd_kernel(const bf16* _
         for (int tt = 0; tt < 2; ++tt)
 #pragma unroll
           for (int i = 0; i < 16; i += 2) {  // registers i, i+1 = keys 2j, 2j+1
-            const uint32_t hv = drop_hash(dpair + ((kb + 32 * tt + (i & 3) + 8 * (i >> 2)) >> 1), dkey);
-            st[tt][i] = keep_lo(hv, drop.thr) ? st[tt][i] * drop.inv : 0.f;
-            st[tt][i + 1] = keep_hi(hv, drop.thr) ? st[tt][i + 1] * drop.inv : 0.f;
+            const uint32_t hv = drop_hash(dblk + ((kb + 32 * tt + (i & 3) + 8 * (i >> 2)) >> 1), dkey);
+            st[tt][i] = keep_byte(hv, dsh, drop.thr) ? st[tt][i] * drop.inv : 0.f;
+            st[tt][i + 1] = keep_byte(hv, dsh + 8, drop.thr) ? st[tt][i + 1] * drop.inv : 0.f;
           }
       }
       l = l * alpha + xhalf_sum(rs);
@@ -455,8 +456,9 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dkdv_kernel(
     const int qb = qstart + (it % ntiles) * kTile;
     const bool more = it + 1 < total;
     const uint32_t dkey = DROP ? drop_key(drop, b * H + hk * group + it / ntiles) : 0u;
-    const uint32_t dpair = ((uint32_t)(qb + 4 * h) * (uint32_t)S + (uint32_t)my_key) >> 1;
     const uint32_t shalf = (uint32_t)S >> 1;
+    const uint32_t dblk = (uint32_t)((qb + 4 * h) >> 1) * shalf + (uint32_t)(my_key >> 1);
+    const int dsh = 8 * (my_key & 1);
     const char* buf = lds + (it & 1) * BUF;
     const char* q_l = buf;
     const char* do_l = buf + G::TB;
@@ -480,14 +482,16 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dkdv_kernel(
         const int r0 = 32 * qs2 + 8 * g + 4 * h;  // 4 consecutive query rows of this group
         const f32x4 lv = *reinterpret_cast<const f32x4*>(lse_l + r0);
         const f32x4 dl = *reinterpret_cast<const f32x4*>(del_l + r0);
+        uint32_t hvq = 0u;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int i = 4 * g + j;
           float p = fexp2(fmaf(s[i], c2, -lv[j]));
           if (diag && my_key > qb + r0 + j) p = 0.f;
           if constexpr (DROP) {
-            const uint32_t hv = drop_hash(dpair + (uint32_t)(32 * qs2 + 8 * g + j) * shalf, dkey);
-            const bool keep = (my_key & 1) ? keep_hi(hv, drop.thr) : keep_lo(hv, drop.thr);
+            // rows j, j^1 (queries 2i, 2i+1) share the hash of their 2x2 block
+            if ((j & 1) == 0) hvq = drop_hash(dblk + (uint32_t)((32 * qs2 + 8 * g + j) >> 1) * shalf, dkey);
+            const bool keep = keep_byte(hvq, dsh + 16 * (j & 1), drop.thr);
             s[i] = keep ? p * drop.inv : 0.f;                   // dropped P (feeds dV)
             dp[i] = p * ((keep ? dp[i] * drop.inv : 0.f) - dl[j]);  // dS
           } else {
@@ -561,7 +565,8 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dq_kernel(
   const float dl = DELTA[((int64_t)b * H + hq) * S + my_q];
   const float c2 = scale * kLog2e;
   const uint32_t dkey = DROP ? drop_key(drop, bh) : 0u;
-  const uint32_t dpair = ((uint32_t)my_q * (uint32_t)S + 4u * h) >> 1;
+  const uint32_t dblk = (uint32_t)(my_q >> 1) * ((uint32_t)S >> 1) + 2u * h;
+  const int dsh = 16 * (my_q & 1);
 
   const bf16* Kb = K + b * ks_.sb + hk * ks_.sh;
   const bf16* Vb = V + b * vs.sb + hk * vs.sh;
@@ -605,9 +610,9 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dq_kernel(
       for (int i = 0; i < 16; ++i) {
         if constexpr (DROP) {
           if ((i & 1) == 0) {
-            const uint32_t hv = drop_hash(dpair + ((ksub + (i & 3) + 8 * (i >> 2)) >> 1), dkey);
-            if (!keep_lo(hv, drop.thr)) dpt[i] = 0.f;
-            if (!keep_hi(hv, drop.thr)) dpt[i + 1] = 0.f;
+            const uint32_t hv = drop_hash(dblk + ((ksub + (i & 3) + 8 * (i >> 2)) >> 1), dkey);
+            if (!keep_byte(hv, dsh, drop.thr)) dpt[i] = 0.f;
+            if (!keep_byte(hv, dsh + 8, drop.thr)) dpt[i + 1] = 0.f;
           }
         }
         float p = fexp2(fmaf(st[i], c2, -lse2));
@@ -666,9 +671,9 @@ static uint32_t host_fmix32(uint32_t x) {
 // keys: key0 from the seed, key1 from the per-call offset (see drop_key / drop_hash).
 static Drop make_drop(float p, uint64_t seed, uint64_t offset) {
   Drop d;
-  d.thr = (uint32_t)((double)p * 65536.0 + 0.5);
-  if (d.thr > 65535u) d.thr = 65535u;
-  d.inv = (float)(65536.0 / (65536.0 - (double)d.thr));  // exact for the realised drop rate
+  d.thr = (uint32_t)((double)p * 256.0 + 0.5);
+  if (d.thr > 255u) d.thr = 255u;
+  d.inv = (float)(256.0 / (256.0 - (double)d.thr));  // exact for the realised drop rate
   d.key0 = host_fmix32((uint32_t)seed ^ host_fmix32((uint32_t)(seed >> 32) + 0x9E3779B9u));
   d.key1 = host_fmix32((uint32_t)offset * 0x27D4EB2Fu ^ host_fmix32((uint32_t)(offset >> 32) + 0x165667B1u));
   return d;

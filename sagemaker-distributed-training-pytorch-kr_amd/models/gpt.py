@@ -161,6 +161,13 @@ def allreduce_word_embedding_grads(model: GPTModel):
     """Sum tied word-embedding grads between the first and last pipeline stage (Megatron's
     embedding group)."""
     st = ps.get_state()
+    if isinstance(model, nn.ModuleList):  # interleaved pipeline chunks
+        if st.is_first_stage(ignore_virtual=True):
+            model = model[0]
+        elif st.is_last_stage(ignore_virtual=True):
+            model = model[-1]
+        else:
+            return
     if st.pp == 1 or model.cfg.untie_embeddings_and_output_weights or st.embd_group is None:
         return
     if not (st.is_first_stage(ignore_virtual=True) or st.is_last_stage(ignore_virtual=True)):

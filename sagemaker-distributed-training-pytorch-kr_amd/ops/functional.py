@@ -356,27 +356,32 @@ def _fmix32_i(x: int) -> int:
 
 
 def flash_dropout_thr(p: float):
-    """(16-bit threshold, keep scale) the kernels use for drop probability ``p``."""
-    thr = min(int(p * 65536.0 + 0.5), 65535)
-    return thr, 65536.0 / (65536.0 - thr)
+    """(8-bit threshold, keep scale) the kernels use for drop probability ``p``: the realised drop
+    rate is round(p * 256) / 256 (FlashAttention-2 also thresholds random bytes)."""
+    thr = min(int(p * 256.0 + 0.5), 255)
+    return thr, 256.0 / (256.0 - thr)
 
 
 def flash_dropout_keep_mask(B: int, H: int, S: int, p: float, seed: int, offset: int, device=None):
     """Bit-exact twin of the flash kernels' dropout mask: bool [B, H, S(q), S(k)], True = kept
-    (see ``drop_hash`` in flash_attn.hip). Keys 2j and 2j+1 of a query share one hash."""
+    (see ``drop_hash`` in flash_attn.hip): each 2x2 (query, key) block shares one hash, byte
+    2 (q & 1) + (k & 1) decides the element."""
     thr, _ = flash_dropout_thr(p)
     key0 = _fmix32_i((seed & _M32) ^ _fmix32_i(((seed >> 32) + 0x9E3779B9) & _M32))
     key1 = _fmix32_i((((offset & _M32) * 0x27D4EB2F) & _M32) ^ _fmix32_i(((offset >> 32) + 0x165667B1) & _M32))
     bh = torch.arange(B * H, dtype=torch.int64, device=device)
-    kbh = _fmix32_t((key0 + bh * 0x632BE5AB) & _M32) ^ key1                        # [BH]
-    pair = (torch.arange(S, dtype=torch.int64, device=device)[:, None] * S
-            + torch.arange(0, S, 2, dtype=torch.int64, device=device)[None, :]) >> 1  # [S, S/2]
-    x = pair[None] ^ kbh[:, None, None]
+    kbh = _fmix32_t((key0 + bh * 0x632BE5AB) & _M32) ^ key1                          # [BH]
+    half = S // 2
+    blk = (torch.arange(half, dtype=torch.int64, device=device)[:, None] * half
+           + torch.arange(half, dtype=torch.int64, device=device)[None, :])            # [S/2, S/2]
+    x = blk[None] ^ kbh[:, None, None]
     x = (x * 0x9E3779B1) & _M32
     x = x ^ (x >> 15)
     x = (x * 0x85EBCA77) & _M32
     x = x ^ (x >> 13)
-    keep = torch.stack([(x & 0xFFFF) >= thr, (x >> 16) >= thr], dim=-1)            # [BH, S, S/2, 2]
+    by = torch.stack([(x >> (8 * i)) & 0xFF for i in range(4)], dim=-1) >= thr           # [BH, S/2, S/2, 4]
+    # byte 2 qb + kb -> [BH, S/2, S/2, 2(q), 2(k)] -> [BH, S/2, 2, S/2, 2]
+    keep = by.view(B * H, half, half, 2, 2).permute(0, 1, 3, 2, 4)
     return keep.reshape(B, H, S, S)
 
 

@@ -65,13 +65,16 @@ def _p2p(send_next=None, send_prev=None, recv_next_shape=None, recv_prev_shape=N
     st = ps.get_state()
     ops = []
     rp = rn = None
-    if send_prev is not None:
-        ops.append(dist.P2POp(dist.isend, send_prev.contiguous(), st.prev_pp_rank))
+    # Canonical order — activations (to next / from prev) before gradients (to prev / from next)
+    # on every rank — so the per-peer message streams match even when next == prev (a 2-rank
+    # ring in the interleaved schedule): RCCL pairs point-to-point ops per peer in issue order.
+    if send_next is not None:
+        ops.append(dist.P2POp(dist.isend, send_next.contiguous(), st.next_pp_rank))
     if recv_prev_shape is not None:
         rp = torch.empty(recv_prev_shape, dtype=dtype, device=device, requires_grad=True)
         ops.append(dist.P2POp(dist.irecv, rp, st.prev_pp_rank))
-    if send_next is not None:
-        ops.append(dist.P2POp(dist.isend, send_next.contiguous(), st.next_pp_rank))
+    if send_prev is not None:
+        ops.append(dist.P2POp(dist.isend, send_prev.contiguous(), st.prev_pp_rank))
     if recv_next_shape is not None:
         rn = torch.empty(recv_next_shape, dtype=dtype, device=device, requires_grad=True)
         ops.append(dist.P2POp(dist.irecv, rn, st.next_pp_rank))
@@ -172,8 +175,177 @@ def forward_backward_pipelining_without_interleaving(forward_step_func: Callable
     return losses
 
 
+# ------------------------------------------------------------------- interleaved (virtual) 1F1B
+
+
+def _chunks_of(model):
+    core = model.module if hasattr(model, "module") else model
+    if isinstance(core, torch.nn.ModuleList):
+        return list(core), model
+    if isinstance(model, list):
+        return model, model
+    return [core], model
+
+
+def _p2p_pair(send_next=None, send_prev=None, recv_prev=False, recv_next=False, shape=None, dtype=None,
+              device=None):
+    rp, rn = _p2p(send_next=send_next, send_prev=send_prev, recv_prev_shape=shape if recv_prev else None,
+                  recv_next_shape=shape if recv_next else None, dtype=dtype, device=device)
+    return rp, rn
+
+
+def forward_backward_pipelining_with_interleaving(forward_step_func: Callable, data_iterator, model,
+                                                  num_microbatches: int, tensor_shape, dtype=torch.bfloat16,
+                                                  forward_only: bool = False, **_):
+    """Interleaved 1F1B over ``vpp`` model chunks per pipeline rank (Megatron's virtual pipeline,
+    `--num-layers-per-virtual-pipeline-stage`). Chunk c of rank r holds global stage c * pp + r,
+    so activations travel the rank ring pp times per micro-batch; the pipeline bubble shrinks
+    by a factor vpp. ``data_iterator`` may be one iterator (tee'd per chunk) or a list.
+
+    Micro-batch k (of vpp * num_microbatches forward/backward units) runs on chunk
+    ``(k % (pp * vpp)) // pp`` (reversed for backward); warm-up depth on rank r is
+    ``2 (pp - r - 1) + (vpp - 1) pp``.
+    """
+    import itertools
+
+    chunks, ddp = _chunks_of(model)
+    vpp = len(chunks)
+    st = ps.get_state()
+    pp, r = st.pp, st.pp_rank
+    if num_microbatches % pp != 0:
+        raise ValueError(f"interleaved schedule needs num_microbatches ({num_microbatches}) divisible by pp ({pp})")
+    if not isinstance(data_iterator, (list, tuple)):
+        data_iterator = list(itertools.tee(data_iterator, vpp)) if data_iterator is not None else [None] * vpp
+    dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
+    gate = _SyncGate([ddp] if hasattr(ddp, "no_sync") else [])
+    gate.set(False)
+    total = num_microbatches * vpp
+    all_warmup = False
+    if forward_only:
+        warm = total
+    elif num_microbatches == pp:
+        warm, all_warmup = total, True
+    else:
+        warm = min((pp - r - 1) * 2 + (vpp - 1) * pp, total)
+    remaining = total - warm
+    inputs = [[] for _ in range(vpp)]
+    outputs = [[] for _ in range(vpp)]
+    ograds = [[] for _ in range(vpp)]
+    losses = []
+    n_backward = [0]
+
+    def chunk_id(k, forward):
+        c = (k % (pp * vpp)) // pp
+        return c if forward else vpp - c - 1
+
+    def set_vr(c):
+        st.virtual_pp_rank = c
+
+    def fwd_step(k):
+        c = chunk_id(k, True)
+        set_vr(c)
+        if st.is_first_stage() and len(inputs[c]) == len(outputs[c]):
+            inputs[c].append(None)
+        inp = inputs[c][-1]
+        chunks[c].set_input_tensor(inp)
+        out, loss_func = forward_step_func(data_iterator[c], chunks[c])
+        if st.is_last_stage():
+            loss, info = loss_func(out)
+            losses.append(info)
+            out = loss / num_microbatches
+        outputs[c].append(out)
+        return out
+
+    def bwd_step(k):
+        c = chunk_id(k, False)
+        set_vr(c)
+        if st.is_last_stage() and len(ograds[c]) == 0:
+            ograds[c].append(None)
+        inp, out, gout = inputs[c].pop(0), outputs[c].pop(0), ograds[c].pop(0)
+        n_backward[0] += 1
+        gate.set(n_backward[0] == total)
+        if inp is not None:
+            inp.retain_grad()
+        if gout is None:
+            torch.autograd.backward(out)
+        else:
+            torch.autograd.backward(out, grad_tensors=gout)
+        return None if inp is None else inp.grad
+
+    kw = dict(shape=tensor_shape, dtype=dtype, device=dev)
+    set_vr(0)
+    if not st.is_first_stage(ignore_virtual=True):
+        inputs[0].append(_p2p_pair(recv_prev=True, **kw)[0])
+    for k in range(warm):
+        out = fwd_step(k)
+        nxt = chunk_id(k + 1, True)
+        recv_prev = not (st.is_first_stage(ignore_virtual=True) and nxt == 0) and k != total - 1
+        if st.is_last_stage():
+            out = None
+        if k == warm - 1 and not forward_only and not all_warmup:
+            recv_next = not st.is_last_stage(ignore_virtual=True)
+            rp, rn = _p2p_pair(send_next=out, recv_prev=recv_prev, recv_next=recv_next, **kw)
+            ograds[vpp - 1].append(rn)
+        else:
+            rp, _ = _p2p_pair(send_next=out, recv_prev=recv_prev, **kw)
+        if recv_prev:
+            inputs[nxt].append(rp)
+    for k in range(remaining):
+        fk, bk = k + warm, k
+        out = fwd_step(fk)
+        gin = bwd_step(bk)
+        set_vr(chunk_id(fk, True))
+        if st.is_last_stage():
+            out = None
+        set_vr(chunk_id(bk, False))
+        if st.is_first_stage():
+            gin = None
+        recv_prev = True
+        if st.is_first_stage(ignore_virtual=True):
+            nxt_f = chunk_id(fk - (pp - 1), True)
+            if nxt_f == vpp - 1:
+                recv_prev = False
+            nxt_f += 1
+        else:
+            nxt_f = chunk_id(fk + 1, True)
+        recv_next = True
+        if st.is_last_stage(ignore_virtual=True):
+            nxt_b = chunk_id(bk - (pp - 1), False)
+            if nxt_b == 0:
+                recv_next = False
+            nxt_b -= 1
+        else:
+            nxt_b = chunk_id(bk + 1, False)
+        if k == remaining - 1:
+            recv_prev = False
+        rp, rn = _p2p_pair(send_next=out, send_prev=gin, recv_prev=recv_prev, recv_next=recv_next, **kw)
+        if recv_prev:
+            inputs[nxt_f].append(rp)
+        if recv_next:
+            ograds[nxt_b].append(rn)
+    if not forward_only:
+        if all_warmup:
+            set_vr(vpp - 1)
+            ograds[vpp - 1].append(None if st.is_last_stage(ignore_virtual=True)
+                                   else _p2p_pair(recv_next=True, **kw)[1])
+        for k in range(remaining, total):
+            gin = bwd_step(k)
+            if st.is_first_stage():
+                gin = None
+            nxt_b = chunk_id(k + 1, False)
+            recv_next = not (st.is_last_stage(ignore_virtual=True) and nxt_b == vpp - 1) and k != total - 1
+            _, rn = _p2p_pair(send_prev=gin, recv_next=recv_next, **kw)
+            if recv_next:
+                ograds[nxt_b].append(rn)
+    set_vr(0)
+    gate.set(True)
+    return losses
+
+
 def get_forward_backward_func():
     st = ps.get_state()
     if st.pp > 1:
+        if st.virtual_pp is not None and st.virtual_pp > 1:
+            return forward_backward_pipelining_with_interleaving
         return forward_backward_pipelining_without_interleaving
     return forward_backward_no_pipelining

@@ -94,7 +94,16 @@ def initialize_megatron(extra_args_provider=None, args_defaults=None, ignore_unk
 def get_model(model_provider_func, args):
     st = ps.get_state()
     dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
-    model = model_provider_func(pre_process=st.is_first_stage(), post_process=st.is_last_stage())
+    if st.pp > 1 and st.virtual_pp is not None and st.virtual_pp > 1:
+        # interleaved pipeline: vpp model chunks per rank, one flat DDP buffer over all of them
+        chunks = []
+        for c in range(st.virtual_pp):
+            st.virtual_pp_rank = c
+            chunks.append(model_provider_func(pre_process=st.is_first_stage(), post_process=st.is_last_stage()))
+        st.virtual_pp_rank = 0
+        model = torch.nn.ModuleList(chunks)
+    else:
+        model = model_provider_func(pre_process=st.is_first_stage(), post_process=st.is_last_stage())
     model = model.to(device=dev, dtype=args.params_dtype)
     n = sum(p.numel() for p in model.parameters())
     if st.dp_rank == 0:
@@ -377,7 +386,8 @@ def pretrain(train_valid_test_dataset_provider, model_provider, model_type, forw
     timers("train/valid/test-data-iterators-setup").stop()
     print_rank_0(f"[after dataloaders are built] datetime: {datetime.now().strftime('%Y-%m-%d %H:%M:%S')}")
     timers.log(["model-and-optimizer-setup", "train/valid/test-data-iterators-setup"], barrier=True)
-    model_cfg = getattr(unwrap_model(model), "cfg", None)
+    core = unwrap_model(model)
+    model_cfg = getattr(core[0] if isinstance(core, torch.nn.ModuleList) else core, "cfg", None)
     iteration = 0
     if not args.skip_train and args.train_iters:
         iteration = train(forward_step_func, model, optimizer, scheduler, train_iter, valid_iter, args, model_cfg)

@@ -201,3 +201,51 @@ def zero_sft_worker(rank, world, stage, ga, steps, offload=False):
             eng.backward(loss * world / world)
             eng.step()
     return {n: p.detach().clone() for n, p in m.named_parameters()}
+
+
+def gpt_vpp_worker(rank, world, nmb):
+    """Interleaved pipeline (pp=2, vpp=2 chunks of 1 layer each, 4 layers): returns the last
+    stage's per-token losses and every local gradient keyed by its single-model name."""
+    import torch.distributed as dist
+    import torch.nn as nn
+    from smdt_amd.comm import init_distributed
+    from smdt_amd.models.gpt import GPTModel, allreduce_word_embedding_grads
+    from smdt_amd.models.transformer import TransformerConfig
+    from smdt_amd.parallel import state as ps
+    from smdt_amd.train.schedules import get_forward_backward_func
+    init_distributed("gloo")
+    st = ps.initialize_model_parallel(1, 2, 2)
+    cfg = TransformerConfig(**{**TINY, "num_layers": 4})
+    chunks = []
+    for c in range(2):
+        st.virtual_pp_rank = c
+        chunks.append(GPTModel(cfg, pre_process=st.is_first_stage(), post_process=st.is_last_stage()))
+    st.virtual_pp_rank = 0
+    model = nn.ModuleList(chunks)
+    tokens, labels = _batch()
+    data = iter(list(zip(tokens.chunk(nmb), labels.chunk(nmb))))
+
+    def fstep(di, m):
+        t, l = next(di)
+        o = m(t, None, None, labels=l)
+        return o, (lambda x: (x.mean(), {"loss": x.detach()}))
+
+    fb = get_forward_backward_func()
+    res = fb(fstep, data, model, nmb, tensor_shape=(32, 4 // nmb, 64), dtype=torch.float32)
+    allreduce_word_embedding_grads(model)
+    grads = {}
+    for m in chunks:
+        for n, p in m.named_parameters():
+            if p.grad is None:
+                continue
+            name = n
+            if n.startswith("decoder.layers."):
+                parts = n.split(".")
+                parts[2] = str(int(parts[2]) + m.first_layer)
+                name = ".".join(parts)
+            if n == "output_weight":
+                name = "embedding.weight"
+            grads[name] = p.grad.detach().clone()
+    loss = torch.cat([r["loss"] for r in res]) if res else None
+    dist.destroy_process_group()
+    return loss, grads
