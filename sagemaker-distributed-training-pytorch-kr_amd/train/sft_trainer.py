@@ -40,6 +40,7 @@ from ..data.sft import DistributedRandomSampler, LengthGroupedSampler
 from ..optim.lr_scheduler import LambdaWarmupScheduler
 from ..parallel import state as ps
 from .zero import ZeroEngine, load_ds_config, resolve_ds_config
+from ..utils.debug import collective_check_from_env, maybe_inject_fault
 
 PREFIX_CHECKPOINT_DIR = "checkpoint"
 TRAINER_STATE_NAME = "trainer_state.json"
@@ -203,6 +204,7 @@ class Trainer:
                     continue
                 ids = batch["input_ids"].to(self.device, non_blocking=True)
                 labels = batch["labels"].to(self.device, non_blocking=True)
+                maybe_inject_fault(self.state["global_step"] + 1, self.rank)
                 loss, _ = self.model(ids, attention_mask=None, labels=labels)
                 eng.backward(loss)
                 tr_loss += loss.detach().float() / ga
@@ -210,6 +212,7 @@ class Trainer:
                 gn = eng.step()
                 if gn is None:
                     continue
+                collective_check_from_env(self.state["global_step"] + 1)
                 self.state["global_step"] += 1
                 self.state["epoch"] = epoch + (step + 1) / len(loader)
                 steps_since_log += 1

@@ -45,6 +45,7 @@ from .checkpointing import load_checkpoint, save_checkpoint
 from .schedules import get_forward_backward_func
 from .timers import Timers
 from .utils import report_memory, unwrap_model
+from ..utils.debug import StepWatchdog, collective_check_from_env, maybe_inject_fault
 
 
 class ModelType:
@@ -310,9 +311,13 @@ def train(forward_step_func, model, optimizer, scheduler, train_iter, valid_iter
     print_rank_0("training ...")
     t_last = time.time()
     it_since = 0
+    watchdog_s = float(os.environ.get("SMDT_STEP_TIMEOUT", "0") or 0)
     while iteration < args.train_iters:
         _profiler(args, iteration, True)
-        loss_dict, lr, grad_norm = train_step(forward_step_func, train_iter, model, optimizer, scheduler, args)
+        maybe_inject_fault(iteration + 1)
+        with StepWatchdog(watchdog_s):
+            loss_dict, lr, grad_norm = train_step(forward_step_func, train_iter, model, optimizer, scheduler, args)
+        collective_check_from_env(iteration + 1)
         iteration += 1
         it_since += 1
         args.iteration = iteration
