@@ -36,6 +36,8 @@
 // so the kernels read Q, K, V directly out of a fused QKV projection output. lse / delta are
 // fp32 [B, H, S]. Requirements (checked by the launcher): S % 128 == 0, D in {64, 128},
 // H % Hkv == 0, 16-byte aligned rows.
+#include <cmath>
+
 #include "common.h"
 #include "launchers.h"
 
@@ -184,7 +186,9 @@ struct Strides {
 // Philox-7 would cost several times more VALU than the MFMA work of an attention tile on CDNA4.
 struct Drop {
   uint32_t thr, key0, key1;
-  float inv;
+  float inv;      // 1 / (1 - p_realised)
+  float keep;     // 1 - p_realised  (= 1 / inv)
+  float log2inv;  // log2(inv): folded into the exponent so p' = p * inv costs nothing
 };
 
 __device__ __forceinline__ uint32_t fmix32(uint32_t x) {
@@ -198,15 +202,21 @@ __device__ __forceinline__ uint32_t fmix32(uint32_t x) {
 __device__ __forceinline__ uint32_t drop_key(const Drop& d, int bh) {
   return fmix32(d.key0 + (uint32_t)bh * 0x632BE5ABu) ^ d.key1;
 }
-__device__ __forceinline__ uint32_t drop_hash(uint32_t pair, uint32_t key) {
-  uint32_t x = pair ^ key;
-  x *= 0x9E3779B1u;
-  x ^= x >> 15;
-  x *= 0x85EBCA77u;
-  x ^= x >> 13;
-  return x;
+__device__ __forceinline__ uint32_t drop_hash(uint32_t blk, uint32_t key) {
+  // full-rate ops only (v_mul_u32_u24, xor, shift): v_mul_lo_u32 is a quarter-rate instruction
+  uint32_t x = blk ^ key;
+  x = __umul24(x ^ (x >> 16), 0x45D9F3u);
+  x = __umul24(x ^ (x >> 16), 0x45D9F3u);
+  return x ^ (x >> 16);
 }
 __device__ __forceinline__ bool keep_byte(uint32_t h, int sh, uint32_t thr) { return ((h >> sh) & 0xFFu) >= thr; }
+
+using f2 = __attribute__((ext_vector_type(2))) float;
+// packed exp2(x * c - b) of two values (one v_pk_fma_f32 + two v_exp_f32)
+__device__ __forceinline__ f2 pexp2(float x0, float x1, float c, float b0, float b1) {
+  const f2 a = __builtin_elementwise_fma((f2){x0, x1}, (f2){c, c}, (f2){-b0, -b1});
+  return (f2){fexp2(a.x), fexp2(a.y)};
+}
 
 // ---------------------------------------------------------------------------------------
 // Forward. Workgroup = 4 waves = 128 query rows of one (b, h); K/V streamed in 64-key tiles,
@@ -292,34 +302,39 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void fwd_kernel(const bf16* _
 #pragma unroll
         for (int i = 0; i < 16; ++i) tmax = fmaxf(tmax, st[tt][i]);
       tmax = xhalf_max(tmax) * c2;
-      const float mnew = fmaxf(m, tmax);
-      const float base = mnew == -INFINITY ? 0.f : mnew;
-      const float alpha = fexp2(m - base);
-      float rs = 0.f;
+      // Lazy rescale: the reference max m only moves when a tile's max exceeds it by more than
+      // 8 (log2 domain, p <= 2^8 stays exact enough in fp32 / bf16), so most tiles skip the
+      // alpha pass over O and l. The branch is wave-uniform (ballot).
+      if (__builtin_amdgcn_ballot_w64(tmax > m + 8.f) != 0) {
+        const float mnew = fmaxf(m, tmax);
+        const float alpha = m == -INFINITY ? 0.f : fexp2(m - mnew);
+        l *= alpha;
+#pragma unroll
+        for (int dt = 0; dt < G::DT; ++dt) o[dt] *= alpha;
+        m = mnew;
+      }
+      const float base = m == -INFINITY ? 0.f : m;
+      f2 rs2 = {0.f, 0.f};
 #pragma unroll
       for (int tt = 0; tt < 2; ++tt)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const float p = fexp2(fmaf(st[tt][i], c2, -base));
-          rs += p;  // the softmax denominator uses the un-dropped probabilities
-          st[tt][i] = p;
+        for (int i = 0; i < 16; i += 2) {
+          const f2 p = pexp2(st[tt][i], st[tt][i + 1], c2, base, base);
+          rs2 += p;  // the softmax denominator uses the un-dropped probabilities
+          st[tt][i] = p.x;
+          st[tt][i + 1] = p.y;
         }
-      if constexpr (DROP) {
+      if constexpr (DROP) {  // zero dropped entries; the 1/(1-p) scale is applied in the epilogue
 #pragma unroll
         for (int tt = 0; tt < 2; ++tt)
 #pragma unroll
           for (int i = 0; i < 16; i += 2) {  // registers i, i+1 = keys 2j, 2j+1
             const uint32_t hv = drop_hash(dblk + ((kb + 32 * tt + (i & 3) + 8 * (i >> 2)) >> 1), dkey);
-            st[tt][i] = keep_byte(hv, dsh, drop.thr) ? st[tt][i] * drop.inv : 0.f;
-            st[tt][i + 1] = keep_byte(hv, dsh + 8, drop.thr) ? st[tt][i + 1] * drop.inv : 0.f;
+            if (!keep_byte(hv, dsh, drop.thr)) st[tt][i] = 0.f;
+            if (!keep_byte(hv, dsh + 8, drop.thr)) st[tt][i + 1] = 0.f;
           }
       }
-      l = l * alpha + xhalf_sum(rs);
-      m = mnew;
-#pragma unroll
-      for (int dt = 0; dt < G::DT; ++dt)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) o[dt][i] *= alpha;
+      l += xhalf_sum(rs2.x + rs2.y);
       // O^T[d, q] += V^T[d, keys] . P^T[keys, q]
 #pragma unroll
       for (int tt = 0; tt < 2; ++tt) {
@@ -339,8 +354,8 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void fwd_kernel(const bf16* _
     __syncthreads();
   }
 
-  // Epilogue: O[q, d] = O^T / l ; lse = (m + log2 l) * ln 2.
-  const float inv = l > 0.f ? 1.f / l : 0.f;
+  // Epilogue: O[q, d] = O^T / l (x 1/(1-p) with dropout) ; lse = (m + log2 l) * ln 2.
+  const float inv = l > 0.f ? (DROP ? drop.inv : 1.f) / l : 0.f;
   bf16* Ob = O + b * os.sb + hq * os.sh + (int64_t)my_q * os.ss;
 #pragma unroll
   for (int dt = 0; dt < G::DT; ++dt) {
@@ -436,8 +451,9 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dkdv_kernel(
     sdo.load(dO + b * dos.sb + hq * dos.sh + (int64_t)qb * dos.ss);
     if (threadIdx.x < kTile) {
       const int64_t li = ((int64_t)b * H + hq) * S + qb + threadIdx.x;
-      nl = LSE[li] * kLog2e;
-      nd = DELTA[li];
+      // dropout: p' = p / (1 - p_drop) via the exponent, delta' = delta (1 - p_drop)
+      nl = LSE[li] * kLog2e - (DROP ? drop.log2inv : 0.f);
+      nd = DROP ? DELTA[li] * drop.keep : DELTA[li];
     }
   };
   auto commit = [&](char* buf) {
@@ -484,20 +500,30 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dkdv_kernel(
         const f32x4 dl = *reinterpret_cast<const f32x4*>(del_l + r0);
         uint32_t hvq = 0u;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        for (int j = 0; j < 4; j += 2) {
           const int i = 4 * g + j;
-          float p = fexp2(fmaf(s[i], c2, -lv[j]));
-          if (diag && my_key > qb + r0 + j) p = 0.f;
-          if constexpr (DROP) {
-            // rows j, j^1 (queries 2i, 2i+1) share the hash of their 2x2 block
-            if ((j & 1) == 0) hvq = drop_hash(dblk + (uint32_t)((32 * qs2 + 8 * g + j) >> 1) * shalf, dkey);
-            const bool keep = keep_byte(hvq, dsh + 16 * (j & 1), drop.thr);
-            s[i] = keep ? p * drop.inv : 0.f;                   // dropped P (feeds dV)
-            dp[i] = p * ((keep ? dp[i] * drop.inv : 0.f) - dl[j]);  // dS
-          } else {
-            s[i] = p;                        // P
-            dp[i] = p * (dp[i] - dl[j]);     // dS
+          f2 p = pexp2(s[i], s[i + 1], c2, lv[j], lv[j + 1]);
+          if (diag) {
+            if (my_key > qb + r0 + j) p.x = 0.f;
+            if (my_key > qb + r0 + j + 1) p.y = 0.f;
           }
+          f2 d = {dp[i], dp[i + 1]};
+          if constexpr (DROP) {
+            // rows j, j+1 (queries 2i, 2i+1) share the hash of their 2x2 block; p is already
+            // p / (1 - p_drop) and dl = delta (1 - p_drop) (folded at staging)
+            hvq = drop_hash(dblk + (uint32_t)((32 * qs2 + 8 * g + j) >> 1) * shalf, dkey);
+            const bool k0 = keep_byte(hvq, dsh, drop.thr), k1 = keep_byte(hvq, dsh + 16, drop.thr);
+            s[i] = k0 ? p.x : 0.f;       // dropped, rescaled P (feeds dV)
+            s[i + 1] = k1 ? p.y : 0.f;
+            if (!k0) d.x = 0.f;
+            if (!k1) d.y = 0.f;
+          } else {
+            s[i] = p.x;
+            s[i + 1] = p.y;
+          }
+          const f2 ds = p * (d - (f2){dl[j], dl[j + 1]});  // dS (packed)
+          dp[i] = ds.x;
+          dp[i + 1] = ds.y;
         }
       }
       // dV^T[d, key] += dO^T[d, q] . P[q, key] ; dK^T[d, key] += Q^T[d, q] . dS[q, key]
@@ -561,8 +587,9 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dq_kernel(
   bf16x8 qf[G::KS], dof[G::KS];
   load_reg_frags<D>(Q + b * qs.sb + hq * qs.sh, qs.ss, qw, lane, qf);
   load_reg_frags<D>(dO + b * dos.sb + hq * dos.sh, dos.ss, qw, lane, dof);
-  const float lse2 = LSE[((int64_t)b * H + hq) * S + my_q] * kLog2e;
-  const float dl = DELTA[((int64_t)b * H + hq) * S + my_q];
+  const float lse2 = LSE[((int64_t)b * H + hq) * S + my_q] * kLog2e - (DROP ? drop.log2inv : 0.f);
+  const float dl = DROP ? DELTA[((int64_t)b * H + hq) * S + my_q] * drop.keep
+                        : DELTA[((int64_t)b * H + hq) * S + my_q];
   const float c2 = scale * kLog2e;
   const uint32_t dkey = DROP ? drop_key(drop, bh) : 0u;
   const uint32_t dblk = (uint32_t)(my_q >> 1) * ((uint32_t)S >> 1) + 2u * h;
@@ -607,17 +634,21 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dq_kernel(
       }
       const bool diag = CAUSAL && ksub + 31 > qw;
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        if constexpr (DROP) {
-          if ((i & 1) == 0) {
-            const uint32_t hv = drop_hash(dblk + ((ksub + (i & 3) + 8 * (i >> 2)) >> 1), dkey);
-            if (!keep_byte(hv, dsh, drop.thr)) dpt[i] = 0.f;
-            if (!keep_byte(hv, dsh + 8, drop.thr)) dpt[i + 1] = 0.f;
-          }
+      for (int i = 0; i < 16; i += 2) {
+        f2 p = pexp2(st[i], st[i + 1], c2, lse2, lse2);  // lse2 carries -log2(1-p) with dropout
+        if (diag) {
+          if (ksub + acc_row(i, h) > my_q) p.x = 0.f;
+          if (ksub + acc_row(i + 1, h) > my_q) p.y = 0.f;
         }
-        float p = fexp2(fmaf(st[i], c2, -lse2));
-        if (diag && ksub + acc_row(i, h) > my_q) p = 0.f;
-        dpt[i] = p * ((DROP ? dpt[i] * drop.inv : dpt[i]) - dl);  // dS^T
+        f2 d = {dpt[i], dpt[i + 1]};
+        if constexpr (DROP) {
+          const uint32_t hv = drop_hash(dblk + ((ksub + (i & 3) + 8 * (i >> 2)) >> 1), dkey);
+          if (!keep_byte(hv, dsh, drop.thr)) d.x = 0.f;
+          if (!keep_byte(hv, dsh + 8, drop.thr)) d.y = 0.f;
+        }
+        const f2 ds = p * (d - (f2){dl, dl});  // dS^T (packed)
+        dpt[i] = ds.x;
+        dpt[i + 1] = ds.y;
       }
       // dQ^T[d, q] += K^T[d, keys] . dS^T[keys, q]
 #pragma unroll
@@ -674,6 +705,8 @@ static Drop make_drop(float p, uint64_t seed, uint64_t offset) {
   d.thr = (uint32_t)((double)p * 256.0 + 0.5);
   if (d.thr > 255u) d.thr = 255u;
   d.inv = (float)(256.0 / (256.0 - (double)d.thr));  // exact for the realised drop rate
+  d.keep = (float)((256.0 - (double)d.thr) / 256.0);
+  d.log2inv = (float)std::log2(256.0 / (256.0 - (double)d.thr));
   d.key0 = host_fmix32((uint32_t)seed ^ host_fmix32((uint32_t)(seed >> 32) + 0x9E3779B9u));
   d.key1 = host_fmix32((uint32_t)offset * 0x27D4EB2Fu ^ host_fmix32((uint32_t)(offset >> 32) + 0x165667B1u));
   return d;

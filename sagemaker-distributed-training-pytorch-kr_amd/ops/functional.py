@@ -375,10 +375,9 @@ def flash_dropout_keep_mask(B: int, H: int, S: int, p: float, seed: int, offset:
     blk = (torch.arange(half, dtype=torch.int64, device=device)[:, None] * half
            + torch.arange(half, dtype=torch.int64, device=device)[None, :])            # [S/2, S/2]
     x = blk[None] ^ kbh[:, None, None]
-    x = (x * 0x9E3779B1) & _M32
-    x = x ^ (x >> 15)
-    x = (x * 0x85EBCA77) & _M32
-    x = x ^ (x >> 13)
+    x = (((x ^ (x >> 16)) & 0xFFFFFF) * 0x45D9F3) & _M32   # v_mul_u32_u24
+    x = (((x ^ (x >> 16)) & 0xFFFFFF) * 0x45D9F3) & _M32
+    x = x ^ (x >> 16)
     by = torch.stack([(x >> (8 * i)) & 0xFF for i in range(4)], dim=-1) >= thr           # [BH, S/2, S/2, 4]
     # byte 2 qb + kb -> [BH, S/2, S/2, 2(q), 2(k)] -> [BH, S/2, 2, S/2, 2]
     keep = by.view(B * H, half, half, 2, 2).permute(0, 1, 3, 2, 4)
