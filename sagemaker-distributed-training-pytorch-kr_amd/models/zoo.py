@@ -4,16 +4,19 @@ from __future__ import annotations
 import torch.nn as nn
 
 from . import resnet as _resnet
+from . import swin as _swin
 from .mnist import Net as MnistNet
 
 
 def available():
-    return _resnet.available() + ["mnist_cnn"]
+    return _resnet.available() + _swin.available() + ["mnist_cnn"]
 
 
 def create(name: str, num_classes: int = 1000) -> nn.Module:
     if name in _resnet.available():
         return _resnet.resnet(name, num_classes=num_classes)
+    if name in _swin.available():
+        return _swin.swin(name, num_classes=num_classes)
     if name == "mnist_cnn":
         return MnistNet()
     raise ValueError(f"unknown model '{name}'; available: {available()}")
