@@ -41,6 +41,7 @@ def main():
     p.add_argument("--d", type=int, default=64)
     p.add_argument("--causal", type=int, default=1)
     p.add_argument("--sdpa", type=int, default=1)
+    p.add_argument("--dropout", type=float, default=0.0)
     a = p.parse_args()
     B, H, S, D = a.b, a.h, a.s, a.d
     Hkv = a.hkv or H
@@ -50,16 +51,16 @@ def main():
     v = torch.randn(B, S, Hkv, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
     do = torch.randn(B, S, H, D, device="cuda", dtype=torch.bfloat16)
     flops = 4 * B * H * S * S * D * (0.5 if a.causal else 1.0)
-    res = {"shape": [B, S, H, Hkv, D], "causal": bool(a.causal)}
+    res = {"shape": [B, S, H, Hkv, D], "causal": bool(a.causal), "dropout": a.dropout}
 
     def ours_f():
-        return SF.flash_attention(q, k, v, 1 / math.sqrt(D), bool(a.causal))
+        return SF.flash_attention(q, k, v, 1 / math.sqrt(D), bool(a.causal), dropout_p=a.dropout)
     o = ours_f()
     tf = timeit(lambda: ours_f())
     tb = timeit(lambda: torch.autograd.grad(o, (q, k, v), do, retain_graph=True))
     res["ours_fwd_ms"], res["ours_bwd_ms"] = tf, tb
     res["ours_fwd_tflops"], res["ours_bwd_tflops"] = flops / tf / 1e9, 2.5 * flops / tb / 1e9
-    if a.sdpa and Hkv == H:
+    if a.sdpa and Hkv == H and a.dropout == 0:
         qt, kt, vt = (t.detach().transpose(1, 2).contiguous().requires_grad_() for t in (q, k, v))
         dot = do.transpose(1, 2).contiguous()
         try:

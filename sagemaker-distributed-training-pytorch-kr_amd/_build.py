@@ -16,6 +16,7 @@ from __future__ import annotations
 
 import concurrent.futures as cf
 import glob
+import hashlib
 import os
 import shutil
 import subprocess
@@ -63,6 +64,12 @@ def _run(cmd, verbose):
     return r.stdout
 
 
+# Per-file device-compiler flags (measured choices). flash_attn: the SLP vectorizer packs the
+# softmax f32 math into v_pk_*_f32, which pins register pairs and measured 4 % slower in the
+# backward (profiles/r1_attn_dropout/ab_attention.log).
+KERNEL_FLAGS = {"flash_attn.hip": ["-fno-slp-vectorize"]}
+
+
 def kernel_sources():
     return sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
 
@@ -78,13 +85,22 @@ def build_kernels(verbose=False, jobs=None):
     hdrs = headers()
     common = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", CSRC, "-I", os.path.join(CSRC, "kernels"),
               "-Wno-unused-result", "-Wno-pass-failed"]
+    # SMDT_KERNEL_FLAGS="file.hip:-flag,-flag;other.hip:-flag" adds per-file flags (A/B builds);
+    # the object name carries a hash of them so a flag change forces a rebuild.
+    extra = dict(KERNEL_FLAGS)
+    for item in filter(None, os.environ.get("SMDT_KERNEL_FLAGS", "").split(";")):
+        f, _, fl = item.partition(":")
+        extra[f.strip()] = [x for x in fl.split(",") if x]
     jobs_list = []
     objs = []
     for src in kernel_sources():
-        obj = os.path.join(BUILD, os.path.basename(src) + ".o")
+        base = os.path.basename(src)
+        fl = extra.get(base, [])
+        tag = ("." + hashlib.sha1(" ".join(fl).encode()).hexdigest()[:8]) if fl else ""
+        obj = os.path.join(BUILD, base + tag + ".o")
         objs.append(obj)
         if _newer([src] + hdrs, obj):
-            jobs_list.append([HIPCC] + common + ["-c", src, "-o", obj])
+            jobs_list.append([HIPCC] + common + fl + ["-c", src, "-o", obj])
     # Host TUs that include ATen (bindings, hipBLASLt plans): compiled by hipcc so HIP headers
     # resolve; no device code in them.
     binc = []

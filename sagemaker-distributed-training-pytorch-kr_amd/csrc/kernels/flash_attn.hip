@@ -211,11 +211,13 @@ __device__ __forceinline__ uint32_t drop_hash(uint32_t blk, uint32_t key) {
 }
 __device__ __forceinline__ bool keep_byte(uint32_t h, int sh, uint32_t thr) { return ((h >> sh) & 0xFFu) >= thr; }
 
-using f2 = __attribute__((ext_vector_type(2))) float;
-// packed exp2(x * c - b) of two values (one v_pk_fma_f32 + two v_exp_f32)
-__device__ __forceinline__ f2 pexp2(float x0, float x1, float c, float b0, float b1) {
-  const f2 a = __builtin_elementwise_fma((f2){x0, x1}, (f2){c, c}, (f2){-b0, -b1});
-  return (f2){fexp2(a.x), fexp2(a.y)};
+// Two exp2(x * c - b) values. Deliberately scalar v_fma_f32: packed v_pk_fma_f32 measured
+// slower in these loops (it pins register pairs and is not faster per element on gfx950).
+struct f2s {
+  float x, y;
+};
+__device__ __forceinline__ f2s pexp2(float x0, float x1, float c, float b0, float b1) {
+  return {fexp2(fmaf(x0, c, -b0)), fexp2(fmaf(x1, c, -b1))};
 }
 
 // ---------------------------------------------------------------------------------------
@@ -314,13 +316,14 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void fwd_kernel(const bf16* _
         m = mnew;
       }
       const float base = m == -INFINITY ? 0.f : m;
-      f2 rs2 = {0.f, 0.f};
+      float rs0 = 0.f, rs1 = 0.f;  // two chains: the denominator uses the un-dropped p
 #pragma unroll
       for (int tt = 0; tt < 2; ++tt)
 #pragma unroll
         for (int i = 0; i < 16; i += 2) {
-          const f2 p = pexp2(st[tt][i], st[tt][i + 1], c2, base, base);
-          rs2 += p;  // the softmax denominator uses the un-dropped probabilities
+          const f2s p = pexp2(st[tt][i], st[tt][i + 1], c2, base, base);
+          rs0 += p.x;
+          rs1 += p.y;
           st[tt][i] = p.x;
           st[tt][i + 1] = p.y;
         }
@@ -334,7 +337,7 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void fwd_kernel(const bf16* _
             if (!keep_byte(hv, dsh + 8, drop.thr)) st[tt][i + 1] = 0.f;
           }
       }
-      l += xhalf_sum(rs2.x + rs2.y);
+      l += xhalf_sum(rs0 + rs1);
       // O^T[d, q] += V^T[d, keys] . P^T[keys, q]
 #pragma unroll
       for (int tt = 0; tt < 2; ++tt) {
@@ -502,12 +505,12 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dkdv_kernel(
 #pragma unroll
         for (int j = 0; j < 4; j += 2) {
           const int i = 4 * g + j;
-          f2 p = pexp2(s[i], s[i + 1], c2, lv[j], lv[j + 1]);
+          f2s p = pexp2(s[i], s[i + 1], c2, lv[j], lv[j + 1]);
           if (diag) {
             if (my_key > qb + r0 + j) p.x = 0.f;
             if (my_key > qb + r0 + j + 1) p.y = 0.f;
           }
-          f2 d = {dp[i], dp[i + 1]};
+          f2s d = {dp[i], dp[i + 1]};
           if constexpr (DROP) {
             // rows j, j+1 (queries 2i, 2i+1) share the hash of their 2x2 block; p is already
             // p / (1 - p_drop) and dl = delta (1 - p_drop) (folded at staging)
@@ -521,9 +524,8 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dkdv_kernel(
             s[i] = p.x;
             s[i + 1] = p.y;
           }
-          const f2 ds = p * (d - (f2){dl[j], dl[j + 1]});  // dS (packed)
-          dp[i] = ds.x;
-          dp[i + 1] = ds.y;
+          dp[i] = p.x * (d.x - dl[j]);  // dS
+          dp[i + 1] = p.y * (d.y - dl[j + 1]);
         }
       }
       // dV^T[d, key] += dO^T[d, q] . P[q, key] ; dK^T[d, key] += Q^T[d, q] . dS[q, key]
@@ -635,20 +637,19 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dq_kernel(
       const bool diag = CAUSAL && ksub + 31 > qw;
 #pragma unroll
       for (int i = 0; i < 16; i += 2) {
-        f2 p = pexp2(st[i], st[i + 1], c2, lse2, lse2);  // lse2 carries -log2(1-p) with dropout
+        f2s p = pexp2(st[i], st[i + 1], c2, lse2, lse2);  // lse2 carries -log2(1-p) with dropout
         if (diag) {
           if (ksub + acc_row(i, h) > my_q) p.x = 0.f;
           if (ksub + acc_row(i + 1, h) > my_q) p.y = 0.f;
         }
-        f2 d = {dpt[i], dpt[i + 1]};
+        f2s d = {dpt[i], dpt[i + 1]};
         if constexpr (DROP) {
           const uint32_t hv = drop_hash(dblk + ((ksub + (i & 3) + 8 * (i >> 2)) >> 1), dkey);
           if (!keep_byte(hv, dsh, drop.thr)) d.x = 0.f;
           if (!keep_byte(hv, dsh + 8, drop.thr)) d.y = 0.f;
         }
-        const f2 ds = p * (d - (f2){dl, dl});  // dS^T (packed)
-        dpt[i] = ds.x;
-        dpt[i + 1] = ds.y;
+        dpt[i] = p.x * (d.x - dl);  // dS^T
+        dpt[i + 1] = p.y * (d.y - dl);
       }
       // dQ^T[d, q] += K^T[d, keys] . dS^T[keys, q]
 #pragma unroll

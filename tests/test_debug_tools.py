@@ -81,3 +81,21 @@ def test_step_watchdog_dumps_stacks_and_aborts():
                        text=True, timeout=60)
     assert p.returncode == -6, p.returncode
     assert "step exceeded" in p.stderr and "_fault_worker.py" in p.stderr
+
+
+def _smddp_worker(rank, world):
+    import torch.distributed as dist
+    import smdt_amd.comm.smddp  # noqa: F401  (registers backend "smddp")
+    dist.init_process_group(backend="smddp")
+    t = torch.full((4,), float(rank + 1))
+    dist.all_reduce(t)
+    be = dist.get_backend()
+    dist.destroy_process_group()
+    return t.tolist(), be
+
+
+@pytest.mark.slow
+def test_smddp_backend_name_works_unmodified():
+    outs = run_workers(_smddp_worker, 2)
+    for vals, be in outs:
+        assert vals == [3.0] * 4 and be == "smddp"
