@@ -70,6 +70,13 @@ def parse():
 
 TUNED_GEMMS = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "tunableop",
                            "gfx950_gpt345m_results.csv")
+# hipBLASLt algorithm indices of the fused fp32-accumulate wgrad GEMMs, tuned over every algorithm
+# hipBLASLt ships for the problem type (SMDT_WGRAD_TUNE=full) on MI355X; reused as-is so the
+# selection does not vary run to run.
+WGRAD_CACHE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "tunableop",
+                           "wgrad_gfx950.csv")
+if os.path.exists(WGRAD_CACHE):
+    os.environ.setdefault("SMDT_WGRAD_CACHE", WGRAD_CACHE)
 
 
 def enable_gemm_tuning(a, rank):

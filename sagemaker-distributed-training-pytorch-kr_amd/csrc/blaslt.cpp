@@ -12,10 +12,17 @@
 #include <torch/extension.h>
 #include <c10/hip/HIPStream.h>
 #include <hipblaslt/hipblaslt.h>
+#include <hipblaslt/hipblaslt-ext.hpp>
 
+#include <cstdio>
+#include <cstdlib>
+#include <fstream>
 #include <map>
 #include <mutex>
+#include <sstream>
+#include <string>
 #include <tuple>
+#include <vector>
 
 namespace {
 
@@ -62,12 +69,63 @@ Plan make_plan(DevState& st, int64_t M, int64_t N, int64_t K, hipDataType in_t) 
   if (!chk(hipblasLtMatmulPreferenceCreate(&pref))) return p;
   size_t ws = kWorkspace;
   hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &ws, sizeof(ws));
-  constexpr int kCand = 16;
-  hipblasLtMatmulHeuristicResult_t res[kCand];
-  int n = 0;
-  hipblasStatus_t s = hipblasLtMatmulAlgoGetHeuristic(st.handle, p.desc, p.la, p.lb, p.lc, p.lc, pref, kCand, res, &n);
+  // Candidates: the heuristic's top 16, or (SMDT_WGRAD_TUNE=full) every algorithm hipBLASLt has
+  // for this problem type. A per-shape winner cached in SMDT_WGRAD_CACHE (csv: M,N,K,dtype,algo
+  // index, us) is reused without re-timing, which also makes the selection reproducible run to run.
+  std::vector<hipblasLtMatmulHeuristicResult_t> cands;
+  const char* cache_path = std::getenv("SMDT_WGRAD_CACHE");
+  const int dt_code = in_t == HIP_R_16BF ? 1 : 2;
+  if (cache_path) {
+    std::ifstream f(cache_path);
+    std::string line;
+    while (std::getline(f, line)) {
+      long long m, n, k;
+      int d, idx;
+      if (std::sscanf(line.c_str(), "%lld,%lld,%lld,%d,%d", &m, &n, &k, &d, &idx) == 5 && m == M && n == N &&
+          k == K && d == dt_code) {
+        std::vector<int> ids{idx};
+        std::vector<hipblasLtMatmulHeuristicResult_t> r;
+        if (chk(hipblaslt_ext::getAlgosFromIndex(st.handle, ids, r)) && !r.empty()) {
+          size_t wsz = 0;
+          const float one = 1.f;
+          if (chk(hipblaslt_ext::matmulIsAlgoSupported(st.handle, p.desc, &one, p.la, p.lb, &one, p.lc, p.lc,
+                                                       r[0].algo, wsz)) && wsz <= kWorkspace) {
+            hipblasLtMatmulPreferenceDestroy(pref);
+            p.algo = r[0].algo;
+            p.ws = wsz;
+            p.ok = true;
+            return p;
+          }
+        }
+      }
+    }
+  }
+  {
+    constexpr int kCand = 16;
+    hipblasLtMatmulHeuristicResult_t res[kCand];
+    int n = 0;
+    if (chk(hipblasLtMatmulAlgoGetHeuristic(st.handle, p.desc, p.la, p.lb, p.lc, p.lc, pref, kCand, res, &n)))
+      for (int i = 0; i < n; ++i) cands.push_back(res[i]);
+  }
   hipblasLtMatmulPreferenceDestroy(pref);
-  if (!chk(s) || n <= 0) return p;
+  const char* mode = std::getenv("SMDT_WGRAD_TUNE");
+  if (mode && std::string(mode) == "full") {
+    std::vector<hipblasLtMatmulHeuristicResult_t> all;
+    if (chk(hipblaslt_ext::getAllAlgos(st.handle, hipblaslt_ext::GemmType::HIPBLASLT_GEMM, HIPBLAS_OP_N, HIPBLAS_OP_T,
+                                       in_t, in_t, HIP_R_32F, HIP_R_32F, HIPBLAS_COMPUTE_32F, all))) {
+      const float one = 1.f;
+      for (auto& r : all) {
+        size_t wsz = 0;
+        if (chk(hipblaslt_ext::matmulIsAlgoSupported(st.handle, p.desc, &one, p.la, p.lb, &one, p.lc, p.lc, r.algo,
+                                                     wsz)) && wsz <= kWorkspace) {
+          r.workspaceSize = wsz;
+          r.state = HIPBLAS_STATUS_SUCCESS;
+          cands.push_back(r);
+        }
+      }
+    }
+  }
+  if (cands.empty()) return p;
   // Autotune once per shape: the heuristic's first pick is a non-split-K tile that leaves a
   // long-K / small-output wgrad (K = tokens) at ~1 workgroup per CU; time every candidate on
   // scratch buffers and keep the fastest.
@@ -82,33 +140,38 @@ Plan make_plan(DevState& st, int64_t M, int64_t N, int64_t K, hipDataType in_t) 
   hipEventCreate(&e0);
   hipEventCreate(&e1);
   const float alpha = 1.f, beta = 1.f;
-  for (int i = 0; i < n; ++i) {
-    if (res[i].state != HIPBLAS_STATUS_SUCCESS || res[i].workspaceSize > kWorkspace) continue;
+  for (size_t i = 0; i < cands.size(); ++i) {
+    auto& r = cands[i];
+    if (r.state != HIPBLAS_STATUS_SUCCESS || r.workspaceSize > kWorkspace) continue;
     bool okc = true;
     for (int w = 0; w < 2 && okc; ++w)
       okc = chk(hipblasLtMatmul(st.handle, p.desc, &alpha, a.data_ptr(), p.la, b.data_ptr(), p.lb, &beta, c.data_ptr(),
-                                p.lc, c.data_ptr(), p.lc, &res[i].algo, st.workspace.data_ptr(), res[i].workspaceSize,
-                                stream));
+                                p.lc, c.data_ptr(), p.lc, &r.algo, st.workspace.data_ptr(), r.workspaceSize, stream));
     if (!okc) continue;
     hipEventRecord(e0, stream);
-    for (int r = 0; r < 5; ++r)
+    for (int rep = 0; rep < 5; ++rep)
       hipblasLtMatmul(st.handle, p.desc, &alpha, a.data_ptr(), p.la, b.data_ptr(), p.lb, &beta, c.data_ptr(), p.lc,
-                      c.data_ptr(), p.lc, &res[i].algo, st.workspace.data_ptr(), res[i].workspaceSize, stream);
+                      c.data_ptr(), p.lc, &r.algo, st.workspace.data_ptr(), r.workspaceSize, stream);
     hipEventRecord(e1, stream);
     hipEventSynchronize(e1);
     float ms = 0.f;
     hipEventElapsedTime(&ms, e0, e1);
     if (ms < best_ms) {
       best_ms = ms;
-      best = i;
+      best = (int)i;
     }
   }
   hipEventDestroy(e0);
   hipEventDestroy(e1);
   if (best >= 0) {
-    p.algo = res[best].algo;
-    p.ws = res[best].workspaceSize;
+    p.algo = cands[best].algo;
+    p.ws = cands[best].workspaceSize;
     p.ok = true;
+    if (cache_path) {
+      std::ofstream f(cache_path, std::ios::app);
+      f << M << "," << N << "," << K << "," << dt_code << "," << hipblaslt_ext::getIndexFromAlgo(p.algo) << ","
+        << (best_ms / 5.f * 1000.f) << "\n";
+    }
   }
   return p;
 }
