@@ -91,8 +91,12 @@ def check_sagemaker(args):
     if os.environ.get("SM_MODEL_DIR") is not None:
         args.data_path = os.environ.get("SM_CHANNEL_TRAINING", args.data_path)
         args.model_dir = os.environ["SM_MODEL_DIR"]
+        # reference: args.save_model = SM_MODEL_DIR (truthy) under SageMaker -> the model is saved
+        if args.save_model is None:
+            args.save_model = True
     else:
         args.model_dir = os.getcwd()
+    args.save_model = bool(args.save_model)
     return args
 
 
@@ -106,7 +110,7 @@ def main(argv=None):
     parser.add_argument("--seed", type=int, default=1, metavar="S")
     parser.add_argument("--log-interval", type=int, default=10, metavar="N")
     parser.add_argument("--save-model", type=lambda s: str(s).lower() not in ("false", "0", "no"), nargs="?",
-                        const=True, default=False)
+                        const=True, default=None)
     parser.add_argument("--verbose", type=lambda s: str(s).lower() not in ("false", "0", "no"), nargs="?",
                         const=True, default=False)
     parser.add_argument("--data-path", type=str, default="../data")

@@ -299,7 +299,8 @@ def validate_args(args, defaults=None):
         "global batch size must be divisible by micro-batch-size * data-parallel-size"
     args.num_micro_batches = args.global_batch_size // (args.micro_batch_size * args.data_parallel_size)
     if args.num_layers_per_virtual_pipeline_stage is not None:
-        assert args.pipeline_model_parallel_size > 2, "interleaved schedule needs pipeline size > 2"
+        # Megatron requires pp > 2 here; the canonical p2p op order (train/schedules.py) makes pp = 2 safe
+        assert args.pipeline_model_parallel_size >= 2, "interleaved schedule needs pipeline parallelism"
         assert args.num_layers % args.num_layers_per_virtual_pipeline_stage == 0
         args.virtual_pipeline_model_parallel_size = (args.num_layers // args.pipeline_model_parallel_size //
                                                      args.num_layers_per_virtual_pipeline_stage)

@@ -1,0 +1,111 @@
+"""Data helpers (C++ runtime vs Python twins, mmap indexed dataset) and the Megatron recipe
+surface: NB3's hyperparameters parse with the verbatim flag names, derived sizes, and a tiny
+pretrain_gpt run that checkpoints and resumes in the Megatron layout."""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from smdt_amd import _runtime
+from smdt_amd.data import gpt_dataset as G
+from smdt_amd.data import indexed_dataset as I
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_cpp_sample_idx_matches_python_twin(seed):
+    rng = np.random.RandomState(seed)
+    sizes = rng.randint(1, 300, size=400).astype(np.int32)
+    docs = np.arange(len(sizes), dtype=np.int32)
+    epochs, seq = 3, 128
+    doc_idx = G.build_doc_idx(docs, epochs, rng, False).astype(np.int32)
+    tpe = int(sizes.sum())
+    a = _runtime.build_sample_idx(sizes, doc_idx, seq, epochs, tpe)
+    b = G.build_sample_idx_py(sizes, doc_idx, seq, epochs, tpe)
+    np.testing.assert_array_equal(np.asarray(a), b)
+
+
+def test_cpp_blending_indices_track_weights():
+    w = np.array([0.5, 0.3, 0.2])
+    d, s = _runtime.build_blending_indices(w, 1000)
+    d, s = np.asarray(d), np.asarray(s)
+    counts = np.bincount(d, minlength=3)
+    np.testing.assert_allclose(counts / 1000, w, atol=2e-3)
+    for k in range(3):  # per-dataset sample indices are 0..count-1 in order
+        np.testing.assert_array_equal(s[d == k], np.arange(counts[k]))
+
+
+def test_mmap_indexed_dataset_roundtrip(tmp_path):
+    prefix = str(tmp_path / "corpus_text_document")
+    I.write_synthetic_corpus(prefix, num_docs=50, vocab_size=1000, mean_len=40, seed=3)
+    ds = I.make_dataset(prefix, "mmap")
+    assert len(ds) == 50
+    assert ds.sizes.sum() == sum(len(ds[i]) for i in range(50))
+    assert all(int(ds[i][-1]) == 999 for i in range(50))  # every document ends with EOD
+
+
+def test_gpt_dataset_samples_and_index_cache(tmp_path):
+    prefix = str(tmp_path / "c_text_document")
+    I.write_synthetic_corpus(prefix, num_docs=200, vocab_size=500, mean_len=60, seed=4)
+    tr, va, te = G.build_train_valid_test_datasets([prefix], "mmap", "949,50,1", [64, 8, 8], 32, 1234, True)
+    x = tr[0]["text"]
+    assert x.shape == (33,) and len(tr) >= 64
+    cache = [f for f in os.listdir(tmp_path / "index-cache") if f.endswith(".npy")] \
+        if os.path.isdir(tmp_path / "index-cache") else [f for f in os.listdir(tmp_path) if f.endswith(".npy")]
+    assert cache, "index mappings were not cached"
+    tr2, _, _ = G.build_train_valid_test_datasets([prefix], "mmap", "949,50,1", [64, 8, 8], 32, 1234, True)
+    np.testing.assert_array_equal(tr2[5]["text"], tr[5]["text"])
+
+
+NB3 = {"num-layers": 12, "hidden-size": 768, "num-attention-heads": 12, "seq-length": 1024,
+       "max-position-embeddings": 1024, "micro-batch-size": 12, "global-batch-size": 192, "lr": 0.0005,
+       "train-iters": 4000, "lr-decay-iters": 150000, "lr-decay-style": "cosine", "lr-warmup-iters": 2000,
+       "weight-decay": .1, "adam-beta2": .999, "fp16": "true", "log-interval": 10, "save-interval": 2000,
+       "eval-interval": 200, "eval-iters": 10, "data-path": "/opt/ml/input/data/dataset/codeparrot_content_document",
+       "vocab-file": "/opt/ml/input/data/dataset/gpt2-vocab.json",
+       "merge-file": "/opt/ml/input/data/dataset/gpt2-merges.txt", "save": "/opt/ml/model/",
+       "tensor-model-parallel-size": 4, "pipeline-model-parallel-size": 1}
+
+
+def test_nb3_hyperparameters_parse_and_derive(monkeypatch):
+    from smdt_amd.launch.hyperparameters import hyperparameters_to_cli
+    from smdt_amd.train import arguments as A
+    monkeypatch.setenv("WORLD_SIZE", "16")
+    monkeypatch.setenv("RANK", "3")
+    args = A.parse_args(argv=hyperparameters_to_cli(NB3))
+    args = A.validate_args(args, {"tokenizer_type": "GPT2BPETokenizer"})
+    assert args.data_parallel_size == 4 and args.num_micro_batches == 4
+    assert args.fp16 is True and args.params_dtype == torch.float16
+    assert args.tokenizer_type == "GPT2BPETokenizer"
+    from smdt_amd.data.tokenizer import vocab_size_with_padding
+    args.padded_vocab_size = vocab_size_with_padding(50257, args.make_vocab_size_divisible_by,
+                                                     args.tensor_model_parallel_size)
+    assert args.padded_vocab_size == 50688        # NB3:1212 "(50257 -> 50688)"
+    cfg = A.core_transformer_config_from_args(args)
+    assert (cfg.num_layers, cfg.hidden_size, cfg.num_attention_heads) == (12, 768, 12)
+
+
+@pytest.mark.slow
+def test_pretrain_gpt_checkpoint_and_resume(tmp_path):
+    script = os.path.join(REPO, "recipes", "3_training_megatron-lm", "pretrain_gpt.py")
+    common = ["--num-layers", "2", "--hidden-size", "64", "--num-attention-heads", "4", "--seq-length", "64",
+              "--max-position-embeddings", "64", "--micro-batch-size", "2", "--global-batch-size", "4",
+              "--lr", "0.001", "--lr-decay-style", "cosine", "--lr-warmup-iters", "1", "--mock-data",
+              "--log-interval", "1", "--eval-interval", "100", "--eval-iters", "1", "--save", str(tmp_path / "ck"),
+              "--save-interval", "3", "--vocab-size", "512", "--tokenizer-type", "NullTokenizer"]
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT="29531")
+    r = subprocess.run([sys.executable, script, "--train-iters", "3"] + common, env=env, capture_output=True,
+                       text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    assert "iteration        3/       3" in r.stdout or "iteration 3/3" in r.stdout.replace("  ", " ")
+    assert (tmp_path / "ck" / "latest_checkpointed_iteration.txt").read_text().strip() == "3"
+    assert (tmp_path / "ck" / "iter_0000003" / "mp_rank_00" / "model_optim_rng.pt").exists()
+    r2 = subprocess.run([sys.executable, script, "--train-iters", "5", "--load", str(tmp_path / "ck")] + common,
+                        env=env, capture_output=True, text=True, timeout=600)
+    assert r2.returncode == 0, r2.stdout[-2000:] + r2.stderr[-3000:]
+    out = r2.stdout.replace("  ", " ")
+    assert "iteration 4/" in " ".join(out.split()) and "iteration 1/" not in " ".join(out.split())
