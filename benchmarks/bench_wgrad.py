@@ -39,6 +39,14 @@ def main():
         flops = 2.0 * M * N * K
         r = {"shape": name, "M": M, "N": N, "K": K}
         r["blaslt_fp32_acc_us"] = timeit(lambda: C.wgrad_accumulate(mg, g, x))
+        r["mfma_fp32_acc_us"] = timeit(lambda: C.wgrad_mfma(mg, g, x, 0))
+        r["mfma_nosplit_us"] = timeit(lambda: C.wgrad_mfma(mg, g, x, 1))
+        # correctness: one accumulate into zeros vs an fp32 reference on a 2048-row slice
+        ms = 2048
+        ref = g[:ms].float().t() @ x[:ms].float()
+        out = torch.zeros_like(mg)
+        C.wgrad_mfma(out, g[:ms].contiguous(), x[:ms].contiguous(), 0)
+        r["mfma_max_rel_err"] = float((out - ref).abs().max() / ref.abs().max())
         r["torch_nt_bf16_us"] = timeit(lambda: torch.mm(g.t(), x))
         gt, xt = g.t().contiguous(), x.t().contiguous()
         r["torch_tn_bf16_us"] = timeit(lambda: torch.mm(gt, xt.t()))

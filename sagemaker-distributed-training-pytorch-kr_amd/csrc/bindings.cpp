@@ -292,6 +292,20 @@ void rope_(Tensor x, Tensor cos_t, Tensor sin_t, int64_t rot, int64_t pos_div, i
         "rope");
 }
 
+// ------------------------------------------------------------------ weight gradient (MFMA)
+// main_grad[N, K] (fp32) += dy[M, N]^T . x[M, K]; returns false when the shape is unsupported.
+bool wgrad_mfma(Tensor main_grad, Tensor dy, Tensor x, int64_t max_splits) {
+  if (!main_grad.is_cuda() || main_grad.scalar_type() != at::kFloat || !main_grad.is_contiguous()) return false;
+  if (dy.dim() != 2 || x.dim() != 2 || !dy.is_contiguous() || !x.is_contiguous()) return false;
+  if (dy.scalar_type() != at::kBFloat16 || x.scalar_type() != at::kBFloat16) return false;
+  const int64_t M = dy.size(0), N = dy.size(1), K = x.size(1);
+  if (x.size(0) != M || main_grad.numel() != N * K || !smdt_wgrad_supported(M, N, K)) return false;
+  check(smdt_wgrad_accumulate(dy.data_ptr(), x.data_ptr(), main_grad.data_ptr<float>(), M, N, K, (int)max_splits,
+                              cur_stream()),
+        "wgrad_mfma");
+  return true;
+}
+
 // ------------------------------------------------------------------ bias gradient
 // out[N] (fp32) = / += column sums of dy [.., N]
 void bias_grad(Tensor dy, Tensor out, bool accumulate) {
@@ -437,6 +451,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("cast_", &cast_);
   m.def("rope_", &rope_);
   m.def("bias_grad", &bias_grad);
+  m.def("wgrad_mfma", &wgrad_mfma, arg("main_grad"), arg("dy"), arg("x"), arg("max_splits") = 0);
   m.def("ce_stats", &ce_stats);
   m.def("ce_bwd", &ce_bwd);
   namespace py = pybind11;

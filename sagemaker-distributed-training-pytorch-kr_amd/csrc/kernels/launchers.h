@@ -88,4 +88,9 @@ hipError_t smdt_flash_bwd(int dtype, const void* q, const void* k, const void* v
                           float scale, int causal, float dropout_p, uint64_t seed,
                           uint64_t offset, hipStream_t st);
 
+// wgrad_gemm.hip: main_grad[N, K] (fp32) += dy[M, N]^T . x[M, K] (bf16)
+int smdt_wgrad_supported(int64_t M, int64_t N, int64_t K);
+hipError_t smdt_wgrad_accumulate(const void* dy, const void* x, float* main_grad, int64_t M, int64_t N,
+                                 int64_t K, int max_splits, hipStream_t st);
+
 }  // extern "C"

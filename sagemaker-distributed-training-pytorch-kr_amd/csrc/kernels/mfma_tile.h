@@ -1,0 +1,137 @@
+// Shared MFMA tile machinery for gfx950 kernels that stream 64-row bf16 tiles through LDS and
+// read them both by rows (ds_read_b128) and by columns (ds_read_b64_tr_b16): the flash-attention
+// kernels and the weight-gradient GEMM.
+//
+//   * v_mfma_f32_32x32x16_bf16: lane l holds A[i = l & 31][k = 8 (l >> 5) + j] and
+//     B[k = 8 (l >> 5) + j][n = l & 31]; the 32x32 f32 result lands as
+//     D[row = (r & 3) + 8 (r >> 2) + 4 (l >> 5)][col = l & 31] in register r (acc_row).
+//   * Geo<D>: a 64-row x D-col bf16 LDS tile with an XOR swizzle of the 16-byte chunk index
+//     (depends on row bits 0..3 only) that keeps BOTH the row reads and the transposed reads
+//     bank-conflict free for D = 64 / 128.
+//   * Frag<D>::trf returns the A-operand fragment of tile COLUMN 32 dt + (l & 31) over 16 tile
+//     rows (rbase + 16 s + a fixed permutation). The permutation depends only on the lane half,
+//     so two trf fragments of tiles with the same row structure also pair as (A, B) operands of
+//     a product that sums over the tile ROWS (A^T . B with both operands row-major).
+#pragma once
+#include "common.h"
+
+namespace smdt {
+namespace mt {
+
+using s16x4 = __attribute__((ext_vector_type(4))) short;
+using s16x8 = __attribute__((ext_vector_type(8))) short;
+using lds_s16x4 = __attribute__((address_space(3))) s16x4;
+using bf4 = __attribute__((ext_vector_type(4))) __bf16;
+
+constexpr int kTile = 64;        // rows per streamed LDS tile
+
+__device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ f32x16 zero16() {
+  f32x16 z;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) z[i] = 0.f;
+  return z;
+}
+
+template <int D>
+struct Geo {
+  static constexpr int RB = D * 2;             // bytes per tile row
+  static constexpr int TB = kTile * RB;        // bytes per tile
+  static constexpr int KS = D / 16;            // MFMA k-steps over D
+  static constexpr int DT = D / 32;            // 32-wide d tiles
+  static constexpr int CH = D / 8;             // 16-byte chunks per row
+  // Swizzle: depends on row bits 0..3 only, so offsets of rows r and r + 16 k differ by a
+  // constant.
+  __device__ static __forceinline__ int f(int r) {
+    if constexpr (D == 128) return ((r & 3) << 2) | ((r >> 2) & 3);
+    else return (((r >> 1) & 1) << 2) | ((r >> 2) & 3);
+  }
+  __device__ static __forceinline__ int off(int r, int c) { return r * RB + 16 * (c ^ f(r)); }
+};
+
+// Per-lane LDS offsets, computed once per kernel.
+template <int D>
+struct Frag {
+  int row[D / 16];     // row fragment of k-step ks for tile rows 0..31
+  int tr[D / 32][2];   // transposed fragment of d-tile dt, k-step 0, rows 0..15 (two 4-row blocks)
+  __device__ __forceinline__ void init(int lane) {
+    const int l31 = lane & 31, h = lane >> 5;
+#pragma unroll
+    for (int ks = 0; ks < D / 16; ++ks) row[ks] = Geo<D>::off(l31, 2 * ks + h);
+    const int q = (lane >> 2) & 3, p = lane & 3, g = (lane >> 4) & 1;
+    const int r0 = 4 * h + q;
+#pragma unroll
+    for (int dt = 0; dt < D / 32; ++dt) {
+      const int c = 4 * dt + 2 * g + (p >> 1);
+      tr[dt][0] = Geo<D>::off(r0, c) + 8 * (p & 1);
+      tr[dt][1] = Geo<D>::off(r0 + 8, c) + 8 * (p & 1);
+    }
+  }
+  // A-operand row fragment: rows rbase..rbase+31 (rbase multiple of 32), elements 16 ks + 8 h..
+  __device__ __forceinline__ bf16x8 rowf(const char* tile, int rbase, int ks) const {
+    return *reinterpret_cast<const bf16x8*>(tile + rbase * Geo<D>::RB + row[ks]);
+  }
+  // A-operand transposed fragment over tile rows rbase + 16 s + (permuted), columns 32 dt + lane&31.
+  __device__ __forceinline__ bf16x8 trf(const char* tile, int rbase, int s, int dt) const {
+    const char* b = tile + (rbase + 16 * s) * Geo<D>::RB;
+    s16x4 x = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(b + tr[dt][0]));
+    s16x4 y = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(b + tr[dt][1]));
+    return __builtin_bit_cast(bf16x8, __builtin_shufflevector(x, y, 0, 1, 2, 3, 4, 5, 6, 7));
+  }
+};
+
+// Pack accumulator registers 8 s .. 8 s + 7 into a bf16 operand fragment.
+__device__ __forceinline__ bf16x8 pack8(const f32x16& x, int s) {
+  bf16x8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = (bf16)x[8 * s + j];
+  return r;
+}
+
+// Row of accumulator register i for lane half h (32x32 C/D map).
+__device__ __forceinline__ int acc_row(int i, int h) { return (i & 3) + 8 * (i >> 2) + 4 * h; }
+
+// Global -> register staging of a 64-row tile (256 threads, 16-byte chunks).
+template <int D>
+struct Stage {
+  static constexpr int N = kTile * Geo<D>::CH / 256;
+  u16x8 v[N];
+  int lds_off[N];
+  int64_t goff[N];     // element offset of chunk i relative to the tile's first row
+  int rowi[N];
+  __device__ __forceinline__ void init(int64_t row_stride) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const int idx = threadIdx.x + 256 * i;
+      const int r = idx / Geo<D>::CH, c = idx % Geo<D>::CH;
+      rowi[i] = r;
+      lds_off[i] = Geo<D>::off(r, c);
+      goff[i] = (int64_t)r * row_stride + c * 8;
+    }
+  }
+  __device__ __forceinline__ void load(const bf16* tile_base) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) v[i] = *reinterpret_cast<const u16x8*>(tile_base + goff[i]);
+  }
+  __device__ __forceinline__ void store(char* tile) const {
+#pragma unroll
+    for (int i = 0; i < N; ++i) *reinterpret_cast<u16x8*>(tile + lds_off[i]) = v[i];
+  }
+};
+
+// Direct global load of a row-operand fragment that stays in registers for the whole kernel:
+// lane holds row (row0 + lane&31), elements [16 ks + 8 h, +8).
+template <int D>
+__device__ __forceinline__ void load_reg_frags(const bf16* base, int64_t row_stride, int row0,
+                                               int lane, bf16x8 (&f)[D / 16]) {
+  const bf16* p = base + (int64_t)(row0 + (lane & 31)) * row_stride + 8 * (lane >> 5);
+#pragma unroll
+  for (int ks = 0; ks < D / 16; ++ks) f[ks] = *reinterpret_cast<const bf16x8*>(p + 16 * ks);
+}
+
+
+}  // namespace mt
+}  // namespace smdt

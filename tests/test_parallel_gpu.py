@@ -68,3 +68,19 @@ def test_ddp_main_grads_match_autograd_grads():
         ref = pb[n].grad.float()
         err = (p.main_grad - ref).abs().max().item()
         assert err <= 0.02 * max(1.0, ref.abs().max().item()), (n, err)
+
+
+@pytest.mark.parametrize("shape", [(4096, 1024, 1024), (1024, 384, 256), (2048, 256, 512)])
+@pytest.mark.parametrize("max_splits", [0, 1])
+def test_wgrad_mfma_kernel_matches_fp32_reference(shape, max_splits):
+    """Hand-written MFMA wgrad (tr-LDS operands, split-K atomics / plain RMW) vs fp32 matmul."""
+    from smdt_amd.ops import _ext
+    torch.manual_seed(2)
+    M, N, K = shape
+    g = torch.randn(M, N, device="cuda", dtype=torch.bfloat16)
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    base = torch.randn(N, K, device="cuda", dtype=torch.float32)
+    mg = base.clone()
+    assert _ext.ext().wgrad_mfma(mg, g, x, max_splits)
+    ref = base + g.float().t() @ x.float()
+    torch.testing.assert_close(mg, ref, atol=2e-2 * (M ** 0.5), rtol=1e-3)
