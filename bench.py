@@ -128,7 +128,8 @@ def main():
                             recompute_method="uniform" if a.recompute == "full" else None)
     model = GPTModel(cfg, pre_process=st.is_first_stage(), post_process=st.is_last_stage(), device=dev)
     zero = bool(a.zero) and st.dp > 1
-    ddp = DistributedDataParallel(model, bucket_size=a.bucket_size, use_distributed_optimizer=zero)
+    ddp = DistributedDataParallel(model, bucket_size=a.bucket_size, use_distributed_optimizer=zero,
+                                  overlap_param_gather=zero)
     opt = MixedPrecisionAdam(ddp, lr=1.5e-4, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.01, clip_grad=1.0)
     sched = OptimizerParamScheduler(opt, max_lr=1.5e-4, min_lr=1e-5, lr_warmup_steps=10, lr_decay_steps=10000,
                                     lr_decay_style="cosine")

@@ -73,6 +73,7 @@ class CPUOffloadAdam(MixedPrecisionAdam):
             self.lr = lr
         self.param_groups[0]["lr"] = self.lr
         ddp = self.ddp
+        ddp.wait_param_gather()
         g = ddp.grad_data
         self.found_inf.zero_()
         total = torch.zeros(1, dtype=torch.float32, device=self.device)

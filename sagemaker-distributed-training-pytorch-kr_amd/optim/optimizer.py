@@ -148,6 +148,8 @@ class MixedPrecisionAdam:
             self.lr = lr
         self.param_groups[0]["lr"] = self.lr
         ddp = self.ddp
+        if hasattr(ddp, "wait_param_gather"):
+            ddp.wait_param_gather()
         g = ddp.grad_data
         self.found_inf.zero_()
         total = torch.zeros(1, dtype=torch.float32, device=self.device)

@@ -44,6 +44,7 @@ class Bucket:
     pending: dict = field(default_factory=dict)
     handle: object = None
     launched: bool = False
+    ag_handle: object = None   # in-flight ZeRO param all-gather (overlap_param_gather)
 
     @property
     def numel(self):
@@ -73,7 +74,8 @@ class DistributedDataParallel(nn.Module):
 
     def __init__(self, module: nn.Module, dp_group=None, grad_dtype=torch.float32, bucket_size: int = 40_000_000,
                  overlap_grad_reduce: bool = True, use_distributed_optimizer: bool = False,
-                 average_in_collective: bool = True, torch_compat: bool = False):
+                 average_in_collective: bool = True, torch_compat: bool = False,
+                 overlap_param_gather: bool = False):
         """``torch_compat=True`` gives drop-in ``torch.nn.parallel.DistributedDataParallel``
         semantics for scripts that drive a stock ``torch.optim`` optimizer: gradient sync is
         finalised automatically at the end of ``backward()`` (autograd-engine callback),
@@ -153,6 +155,18 @@ class DistributedDataParallel(nn.Module):
                 p._smdt_grad_ready = self._on_grad_ready
         self._hooks = [p.register_post_accumulate_grad_hook(self._post_accumulate) for p in params]
         self.regions = self._region_ranges()
+        # ZeRO param all-gather overlapped with the next forward (Megatron --overlap-param-gather):
+        # the gathers are issued asynchronously bucket by bucket in forward order after the
+        # optimizer step, and a forward pre-hook on each module waits only for the buckets that
+        # hold its own parameters.
+        self.overlap_param_gather = bool(overlap_param_gather and use_distributed_optimizer and self.dp > 1)
+        self._pg_hooks = []
+        if self.overlap_param_gather:
+            for mod in module.modules():
+                own = [p for p in mod._parameters.values() if p is not None and id(p) in self.param_bucket]
+                if own:
+                    bks = sorted({self.param_bucket[id(p)].index for p in own})
+                    self._pg_hooks.append(mod.register_forward_pre_hook(self._make_gather_wait(bks)))
         self._reset_pending()
         if self.dp > 1:
             self.broadcast_params()
@@ -260,6 +274,7 @@ class DistributedDataParallel(nn.Module):
 
     def finish_grad_sync(self):
         """Launch what is left, wait for every bucket, then fix up sequence-parallel grads."""
+        self.wait_param_gather()  # params a forward never touched
         self.start_grad_sync()
         for b in self.buckets:
             if b.handle is not None:
@@ -284,18 +299,33 @@ class DistributedDataParallel(nn.Module):
 
     @torch.no_grad()
     def all_gather_params(self):
-        """ZeRO: after each rank updated its shard of ``param_data``, gather the full buffer."""
+        """ZeRO: after each rank updated its shard of ``param_data``, gather the full buffer.
+        With ``overlap_param_gather`` the gathers are left in flight (forward order: the last
+        bucket holds the first layers) and waited for by the forward pre-hooks."""
         if self.dp == 1:
             return
-        handles = []
-        for b in self.buckets:
+        self.wait_param_gather()
+        for b in reversed(self.buckets):
             s, e = self.shard_range(b)
-            handles.append(dist.all_gather_into_tensor(self.param_data[b.start:b.end], self.param_data[s:e],
-                                                       group=self.dp_group, async_op=True))
-        for h in handles:
-            h.wait()
+            b.ag_handle = dist.all_gather_into_tensor(self.param_data[b.start:b.end], self.param_data[s:e],
+                                                      group=self.dp_group, async_op=True)
+        if not self.overlap_param_gather:
+            self.wait_param_gather()
+
+    def wait_param_gather(self, indices=None):
+        for b in (self.buckets if indices is None else (self.buckets[i] for i in indices)):
+            h = getattr(b, "ag_handle", None)
+            if h is not None:
+                h.wait()
+                b.ag_handle = None
+
+    def _make_gather_wait(self, indices):
+        def hook(_mod, _inp):
+            self.wait_param_gather(indices)
+        return hook
 
     def state_dict(self, *args, **kwargs):
+        self.wait_param_gather()
         return self.module.state_dict(*args, **kwargs)
 
     def load_state_dict(self, sd, strict=True):

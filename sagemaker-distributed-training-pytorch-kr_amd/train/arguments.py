@@ -177,6 +177,7 @@ _GROUPS = {
         ("--model-parallel-size", dict(type=int, default=None)),
         ("--num-layers-per-virtual-pipeline-stage", dict(type=int, default=None)),
         ("--overlap-p2p-communication", dict(action="store_true")),
+        ("--overlap-param-gather", dict(action="store_true")),
         ("--distributed-backend", dict(default="nccl", choices=["nccl", "gloo", "smddp", "rccl"])),
         ("--distributed-timeout-minutes", dict(type=int, default=10)),
         ("--DDP-impl", dict(default="local", choices=["local", "torch"])),

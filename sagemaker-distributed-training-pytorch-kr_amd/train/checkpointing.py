@@ -74,6 +74,8 @@ def save_checkpoint(iteration: int, model, optimizer=None, scheduler=None, args=
                     extra: Optional[dict] = None):
     save_dir = save_dir or args.save
     t0 = time.time()
+    if hasattr(model, "wait_param_gather"):  # overlapped ZeRO all-gather still in flight
+        model.wait_param_gather()
     if _rank0():
         print(f"saving checkpoint at iteration {iteration:7d} to {save_dir}", flush=True)
     st = ps.get_state()

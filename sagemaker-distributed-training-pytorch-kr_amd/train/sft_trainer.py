@@ -267,6 +267,8 @@ class Trainer:
         if ds is None:
             return {}
         loader, _ = self._build_loader(ds, self.args.per_device_eval_batch_size, shuffle=False)
+        if self.engine is not None:
+            self.engine.wait_for_params()
         self.model.eval()
         tot = torch.zeros(2, dtype=torch.float64, device=self.device)
         for batch in loader:
@@ -293,6 +295,8 @@ class Trainer:
         """HF-format weights (config.json + model.safetensors) + tokenizer + training args from
         rank 0; parameters are resident (stages 0-3 here), so no gather is needed."""
         out = output_dir or self.args.output_dir
+        if self.engine is not None:
+            self.engine.wait_for_params()
         if self.is_main:
             os.makedirs(out, exist_ok=True)
             self.model.save_pretrained(out)

@@ -113,7 +113,8 @@ def get_model(model_provider_func, args):
     grad_dtype = torch.float32 if (args.accumulate_allreduce_grads_in_fp32 or args.params_dtype != torch.float32) \
         else args.params_dtype
     ddp = DistributedDataParallel(model, grad_dtype=grad_dtype, bucket_size=args.ddp_bucket_size,
-                                  use_distributed_optimizer=args.use_distributed_optimizer and st.dp > 1)
+                                  use_distributed_optimizer=args.use_distributed_optimizer and st.dp > 1,
+                                  overlap_param_gather=getattr(args, "overlap_param_gather", False))
     return ddp
 
 

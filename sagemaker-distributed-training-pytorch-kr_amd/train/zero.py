@@ -129,7 +129,8 @@ class ZeroEngine:
         self.offload_optimizer = off_o.get("device") == "cpu"
         self.ddp = DistributedDataParallel(model, dp_group=dp_group, grad_dtype=torch.float32, bucket_size=bucket,
                                            overlap_grad_reduce=bool(z.get("overlap_comm", True)),
-                                           use_distributed_optimizer=self.stage >= 1)
+                                           use_distributed_optimizer=self.stage >= 1,
+                                           overlap_param_gather=self.stage >= 1)
         ocfg = ds_config.get("optimizer", {"type": "AdamW", "params": {}})
         otype = ocfg.get("type", "AdamW").lower()
         if otype not in ("adamw", "adam", "fusedadam", "cpuadam"):
@@ -217,6 +218,11 @@ class ZeroEngine:
     def get_lr(self):
         return [self.optimizer.lr]
 
+    def wait_for_params(self):
+        """Finish the in-flight (overlapped) ZeRO param all-gather before reading parameters
+        outside a forward pass (saving, evaluation on another module, returning weights)."""
+        self.ddp.wait_param_gather()
+
     # ------------------------------------------------------------------ checkpoints
     def _param_meta(self):
         names = {id(p): n for n, p in self.module.named_parameters()}
@@ -227,6 +233,7 @@ class ZeroEngine:
         return meta
 
     def save_checkpoint(self, save_dir: str, tag: Optional[str] = None, client_state: Optional[Dict] = None):
+        self.wait_for_params()
         tag = tag or f"global_step{self.global_steps}"
         d = os.path.join(save_dir, tag)
         rank = dist.get_rank() if dist.is_initialized() else 0

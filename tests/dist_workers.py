@@ -81,7 +81,7 @@ def gpt_tp_worker(rank, world, tp, pp, sp, cfg_over=None):
     return out_loss, grads, meta
 
 
-def ddp_worker(rank, world, zero, steps=3):
+def ddp_worker(rank, world, zero, steps=3, overlap_pg=False):
     """DDP (+ZeRO) on a tiny GPT: returns final params after `steps` optimizer steps on a
     per-rank shard of a fixed global batch (so the result must equal single-process training on
     the whole batch)."""
@@ -96,7 +96,8 @@ def ddp_worker(rank, world, zero, steps=3):
     ps.initialize_model_parallel(1, 1)
     cfg = TransformerConfig(**TINY)
     m = GPTModel(cfg)
-    ddp = DistributedDataParallel(m, bucket_size=20000, use_distributed_optimizer=zero)
+    ddp = DistributedDataParallel(m, bucket_size=20000, use_distributed_optimizer=zero,
+                                  overlap_param_gather=overlap_pg)
     opt = MixedPrecisionAdam(ddp, lr=1e-2, weight_decay=0.1, clip_grad=1.0)
     tokens, labels = _batch(b=4)
     shard = slice(rank * (4 // world), (rank + 1) * (4 // world))
@@ -117,6 +118,7 @@ def ddp_worker(rank, world, zero, steps=3):
             first_grads = {n: full[ddp.param_index[id(p)][0]:ddp.param_index[id(p)][0] + p.numel()].view_as(p).clone()
                            for n, p in m.named_parameters()}
         opt.step()
+    ddp.wait_param_gather()
     out = {n: p.detach().clone() for n, p in m.named_parameters()}
     dist.destroy_process_group()
     return out, first_grads
@@ -200,6 +202,7 @@ def zero_sft_worker(rank, world, stage, ga, steps, offload=False):
             loss, _ = m(ids, labels=lab)
             eng.backward(loss * world / world)
             eng.step()
+    eng.wait_for_params()
     return {n: p.detach().clone() for n, p in m.named_parameters()}
 
 
