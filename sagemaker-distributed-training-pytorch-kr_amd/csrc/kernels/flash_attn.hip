@@ -102,6 +102,27 @@ __device__ __forceinline__ uint32_t drop_hash(uint32_t blk, uint32_t key) {
 }
 __device__ __forceinline__ bool keep_byte(uint32_t h, int sh, uint32_t thr) { return ((h >> sh) & 0xFFu) >= thr; }
 
+// Operand prescale: x * c rounded back to bf16 (one-time, register-resident fragments).
+__device__ __forceinline__ bf16x8 scale8(bf16x8 x, float c) {
+  bf16x8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = (bf16)((float)x[j] * c);
+  return r;
+}
+// An opaque copy: keeps the compiler from hoisting a loop-invariant splat16 out of the tile
+// loop (which pins 16 extra VGPRs per splat for the whole kernel).
+__device__ __forceinline__ float opaque(float x) {
+  float v;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(v) : "v"(x));
+  return v;
+}
+__device__ __forceinline__ f32x16 splat16(float v) {
+  f32x16 z;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) z[i] = v;
+  return z;
+}
+
 // Two exp2(x * c - b) values. Deliberately scalar v_fma_f32: packed v_pk_fma_f32 measured
 // slower in these loops (it pins register pairs and is not faster per element on gfx950).
 struct f2s {
@@ -142,12 +163,17 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void fwd_kernel(const bf16* _
   fr.init(lane);
   bf16x8 qf[G::KS];
   load_reg_frags<D>(Q + b * qs.sb + hq * qs.sh, qs.ss, qw, lane, qf);
+  // Q is prescaled by scale * log2(e), so S^T comes out in the log2 domain, and the score
+  // accumulator starts at -m (the reference max): p = exp2(S) needs no per-element FMA.
+  const float c2 = scale * kLog2e;
+#pragma unroll
+  for (int kk = 0; kk < G::KS; ++kk) qf[kk] = scale8(qf[kk], c2);
 
   f32x16 o[G::DT];
 #pragma unroll
   for (int t = 0; t < G::DT; ++t) o[t] = zero16();
-  float m = -INFINITY, l = 0.f;  // running max (log2 domain) and denominator
-  const float c2 = scale * kLog2e;
+  // Reference max m (log2 domain) starts at 0 and moves lazily (see below); l = denominator.
+  float m = 0.f, l = 0.f;
 
   const int kend = CAUSAL ? (q0 + kBlockRows) : S;
   const int ntiles = kend / kTile;
@@ -174,11 +200,11 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void fwd_kernel(const bf16* _
       sv.load(Vb + (int64_t)(kb + kTile) * vs.ss);
     }
     if (!CAUSAL || kb <= qw + 31) {
-      // S^T tiles: rows = keys (registers), column = this lane's query.
+      // S^T tiles (log2 domain, minus m): rows = keys (registers), column = this lane's query.
       f32x16 st[2];
 #pragma unroll
       for (int tt = 0; tt < 2; ++tt) {
-        st[tt] = zero16();
+        st[tt] = splat16(-m);
 #pragma unroll
         for (int kk = 0; kk < G::KS; ++kk) st[tt] = mfma(fr.rowf(kt, 32 * tt, kk), qf[kk], st[tt]);
       }
@@ -194,29 +220,31 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void fwd_kernel(const bf16* _
       for (int tt = 0; tt < 2; ++tt)
 #pragma unroll
         for (int i = 0; i < 16; ++i) tmax = fmaxf(tmax, st[tt][i]);
-      tmax = xhalf_max(tmax) * c2;
-      // Lazy rescale: the reference max m only moves when a tile's max exceeds it by more than
-      // 8 (log2 domain, p <= 2^8 stays exact enough in fp32 / bf16), so most tiles skip the
-      // alpha pass over O and l. The branch is wave-uniform (ballot).
-      if (__builtin_amdgcn_ballot_w64(tmax > m + 8.f) != 0) {
-        const float mnew = fmaxf(m, tmax);
-        const float alpha = m == -INFINITY ? 0.f : fexp2(m - mnew);
+      tmax = xhalf_max(tmax);  // this tile's row max relative to m
+      // Lazy rescale: m only moves when the tile max exceeds it by more than 8 (p <= 2^8 stays
+      // exact enough in fp32 / bf16), or — before anything was accumulated — when the scores sit
+      // far below it (so they cannot all underflow). Wave-uniform branch (ballot); rare.
+      const bool up = tmax > 8.f, down = l == 0.f && tmax < -64.f && tmax != -INFINITY;
+      if (__builtin_amdgcn_ballot_w64(up || down) != 0) {
+        const float d = (up || down) ? tmax : 0.f;
+        const float alpha = fexp2(-d);
         l *= alpha;
 #pragma unroll
         for (int dt = 0; dt < G::DT; ++dt) o[dt] *= alpha;
-        m = mnew;
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt) st[tt] -= d;
+        m += d;
       }
-      const float base = m == -INFINITY ? 0.f : m;
       float rs0 = 0.f, rs1 = 0.f;  // two chains: the denominator uses the un-dropped p
 #pragma unroll
       for (int tt = 0; tt < 2; ++tt)
 #pragma unroll
         for (int i = 0; i < 16; i += 2) {
-          const f2s p = pexp2(st[tt][i], st[tt][i + 1], c2, base, base);
-          rs0 += p.x;
-          rs1 += p.y;
-          st[tt][i] = p.x;
-          st[tt][i + 1] = p.y;
+          const float p0 = fexp2(st[tt][i]), p1 = fexp2(st[tt][i + 1]);
+          rs0 += p0;
+          rs1 += p1;
+          st[tt][i] = p0;
+          st[tt][i + 1] = p1;
         }
       if constexpr (DROP) {  // zero dropped entries; the 1/(1-p) scale is applied in the epilogue
 #pragma unroll
@@ -324,6 +352,8 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dkdv_kernel(
   bf16x8 kf[G::KS], vf[G::KS];
   load_reg_frags<D>(K + b * ks_.sb + hk * ks_.sh, ks_.ss, kw, lane, kf);
   load_reg_frags<D>(V + b * vs.sb + hk * vs.sh, vs.ss, kw, lane, vf);
+#pragma unroll
+  for (int kk = 0; kk < G::KS; ++kk) kf[kk] = scale8(kf[kk], scale * kLog2e);  // S in log2 domain
 
   f32x16 dk[G::DT], dv[G::DT];
 #pragma unroll
@@ -338,9 +368,11 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dkdv_kernel(
   sq.init(qs.ss);
   sdo.init(dos.ss);
   float nl = 0.f, nd = 0.f;
-  auto issue = [&](int it) {
-    const int hq = hk * group + it / ntiles;
-    const int qb = qstart + (it % ntiles) * kTile;
+  // (query head, query tile) of a work item, kept as running counters: no integer division
+  // on the scalar unit inside the loop.
+  auto issue = [&](int ih, int iq) {
+    const int hq = hk * group + ih;
+    const int qb = qstart + iq * kTile;
     sq.load(Q + b * qs.sb + hq * qs.sh + (int64_t)qb * qs.ss);
     sdo.load(dO + b * dos.sb + hq * dos.sh + (int64_t)qb * dos.ss);
     if (threadIdx.x < kTile) {
@@ -358,29 +390,43 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dkdv_kernel(
       reinterpret_cast<float*>(buf + 2 * G::TB + kTile * 4)[threadIdx.x] = nd;
     }
   };
-  issue(0);
+  issue(0, 0);
   commit(lds);
   __syncthreads();
 
+  const uint32_t shalf = (uint32_t)S >> 1;
+  const int dsh = 8 * (my_key & 1);
+  int ch = 0, cq = 0;  // current work item
   for (int it = 0; it < total; ++it) {
-    const int qb = qstart + (it % ntiles) * kTile;
+    const int qb = qstart + cq * kTile;
     const bool more = it + 1 < total;
-    const uint32_t dkey = DROP ? drop_key(drop, b * H + hk * group + it / ntiles) : 0u;
-    const uint32_t shalf = (uint32_t)S >> 1;
+    const int nh = cq + 1 == ntiles ? ch + 1 : ch, nq = cq + 1 == ntiles ? 0 : cq + 1;
+    const uint32_t dkey = DROP ? drop_key(drop, b * H + hk * group + ch) : 0u;
     const uint32_t dblk = (uint32_t)((qb + 4 * h) >> 1) * shalf + (uint32_t)(my_key >> 1);
-    const int dsh = 8 * (my_key & 1);
     const char* buf = lds + (it & 1) * BUF;
     const char* q_l = buf;
     const char* do_l = buf + G::TB;
     const float* lse_l = reinterpret_cast<const float*>(buf + 2 * G::TB);
     const float* del_l = lse_l + kTile;
-    if (more) issue(it + 1);
+    if (more) issue(nh, nq);
 #pragma unroll
     for (int qs2 = 0; qs2 < 2; ++qs2) {
       const int qsub = qb + 32 * qs2;
       if (CAUSAL && qsub + 31 < kw) continue;  // all queries precede all of this wave's keys
-      // S[q, key] = Q . K^T ; dP[q, key] = dO . V^T   (key on lane, query rows in registers)
-      f32x16 s = zero16(), dp = zero16();
+      // S'[q, key] = Q . K'^T - lse ; dP'[q, key] = dO . V^T - delta  (key on lane, query rows
+      // in registers): the row constants are the accumulators' initial values.
+      f32x16 s, dp;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int r0 = 32 * qs2 + 8 * g + 4 * h;  // 4 consecutive query rows of this group
+        const f32x4 lv = *reinterpret_cast<const f32x4*>(lse_l + r0);
+        const f32x4 dl = *reinterpret_cast<const f32x4*>(del_l + r0);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          s[4 * g + j] = -lv[j];
+          dp[4 * g + j] = DROP ? 0.f : -dl[j];  // dropout needs the raw dP (delta applied below)
+        }
+      }
 #pragma unroll
       for (int kk = 0; kk < G::KS; ++kk) {
         s = mfma(fr.rowf(q_l, 32 * qs2, kk), kf[kk], s);
@@ -389,34 +435,33 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dkdv_kernel(
       const bool diag = CAUSAL && qsub < kw + 31;
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        const int r0 = 32 * qs2 + 8 * g + 4 * h;  // 4 consecutive query rows of this group
-        const f32x4 lv = *reinterpret_cast<const f32x4*>(lse_l + r0);
-        const f32x4 dl = *reinterpret_cast<const f32x4*>(del_l + r0);
+        const int r0 = 32 * qs2 + 8 * g + 4 * h;
+        const f32x4 dlg = DROP ? *reinterpret_cast<const f32x4*>(del_l + r0) : f32x4{0.f, 0.f, 0.f, 0.f};
         uint32_t hvq = 0u;
 #pragma unroll
         for (int j = 0; j < 4; j += 2) {
           const int i = 4 * g + j;
-          f2s p = pexp2(s[i], s[i + 1], c2, lv[j], lv[j + 1]);
+          float p0 = fexp2(s[i]), p1 = fexp2(s[i + 1]);  // with dropout: p / (1 - p_drop)
           if (diag) {
-            if (my_key > qb + r0 + j) p.x = 0.f;
-            if (my_key > qb + r0 + j + 1) p.y = 0.f;
+            if (my_key > qb + r0 + j) p0 = 0.f;
+            if (my_key > qb + r0 + j + 1) p1 = 0.f;
           }
-          f2s d = {dp[i], dp[i + 1]};
+          float d0 = dp[i], d1 = dp[i + 1];
           if constexpr (DROP) {
-            // rows j, j+1 (queries 2i, 2i+1) share the hash of their 2x2 block; p is already
-            // p / (1 - p_drop) and dl = delta (1 - p_drop) (folded at staging)
+            // rows j, j+1 (queries 2i, 2i+1) share the hash of their 2x2 block; dropped
+            // entries: P' -> 0 for dV, dP -> 0, so dS = p' (keep ? dP : 0) - p' delta'
             hvq = drop_hash(dblk + (uint32_t)((32 * qs2 + 8 * g + j) >> 1) * shalf, dkey);
             const bool k0 = keep_byte(hvq, dsh, drop.thr), k1 = keep_byte(hvq, dsh + 16, drop.thr);
-            s[i] = k0 ? p.x : 0.f;       // dropped, rescaled P (feeds dV)
-            s[i + 1] = k1 ? p.y : 0.f;
-            if (!k0) d.x = 0.f;
-            if (!k1) d.y = 0.f;
+            s[i] = k0 ? p0 : 0.f;
+            s[i + 1] = k1 ? p1 : 0.f;
+            d0 = (k0 ? d0 : 0.f) - dlg[j];
+            d1 = (k1 ? d1 : 0.f) - dlg[j + 1];
           } else {
-            s[i] = p.x;
-            s[i + 1] = p.y;
+            s[i] = p0;
+            s[i + 1] = p1;
           }
-          dp[i] = p.x * (d.x - dl[j]);  // dS
-          dp[i + 1] = p.y * (d.y - dl[j + 1]);
+          dp[i] = p0 * d0;  // dS
+          dp[i + 1] = p1 * d1;
         }
       }
       // dV^T[d, key] += dO^T[d, q] . P[q, key] ; dK^T[d, key] += Q^T[d, q] . dS[q, key]
@@ -433,6 +478,8 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dkdv_kernel(
     }
     if (more) commit(lds + ((it + 1) & 1) * BUF);
     __syncthreads();
+    ch = nh;
+    cq = nq;
   }
 
   // dK[key, d] = scale * dK^T ; dV[key, d] = dV^T (key on lane, d in registers)
@@ -480,6 +527,8 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dq_kernel(
   bf16x8 qf[G::KS], dof[G::KS];
   load_reg_frags<D>(Q + b * qs.sb + hq * qs.sh, qs.ss, qw, lane, qf);
   load_reg_frags<D>(dO + b * dos.sb + hq * dos.sh, dos.ss, qw, lane, dof);
+#pragma unroll
+  for (int kk = 0; kk < G::KS; ++kk) qf[kk] = scale8(qf[kk], scale * kLog2e);  // S^T in log2 domain
   const float lse2 = LSE[((int64_t)b * H + hq) * S + my_q] * kLog2e - (DROP ? drop.log2inv : 0.f);
   const float dl = DROP ? DELTA[((int64_t)b * H + hq) * S + my_q] * drop.keep
                         : DELTA[((int64_t)b * H + hq) * S + my_q];
@@ -519,7 +568,8 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dq_kernel(
     for (int tt = 0; tt < 2; ++tt) {
       const int ksub = kb + 32 * tt;
       if (CAUSAL && ksub > qw + 31) continue;
-      f32x16 st = zero16(), dpt = zero16();
+      // row constants as the initial accumulators: S' = S log2(e) scale - lse, dP' = dP - delta
+      f32x16 st = splat16(opaque(-lse2)), dpt = splat16(opaque(-dl));
 #pragma unroll
       for (int kk = 0; kk < G::KS; ++kk) {
         st = mfma(fr.rowf(kt, 32 * tt, kk), qf[kk], st);
@@ -528,19 +578,19 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dq_kernel(
       const bool diag = CAUSAL && ksub + 31 > qw;
 #pragma unroll
       for (int i = 0; i < 16; i += 2) {
-        f2s p = pexp2(st[i], st[i + 1], c2, lse2, lse2);  // lse2 carries -log2(1-p) with dropout
+        float p0 = fexp2(st[i]), p1 = fexp2(st[i + 1]);  // with dropout: p / (1 - p_drop)
         if (diag) {
-          if (ksub + acc_row(i, h) > my_q) p.x = 0.f;
-          if (ksub + acc_row(i + 1, h) > my_q) p.y = 0.f;
+          if (ksub + acc_row(i, h) > my_q) p0 = 0.f;
+          if (ksub + acc_row(i + 1, h) > my_q) p1 = 0.f;
         }
-        f2s d = {dpt[i], dpt[i + 1]};
-        if constexpr (DROP) {
+        float d0 = dpt[i], d1 = dpt[i + 1];
+        if constexpr (DROP) {  // dropped: dP contributes 0, dS = p' (0 - delta')
           const uint32_t hv = drop_hash(dblk + ((ksub + (i & 3) + 8 * (i >> 2)) >> 1), dkey);
-          if (!keep_byte(hv, dsh, drop.thr)) d.x = 0.f;
-          if (!keep_byte(hv, dsh + 8, drop.thr)) d.y = 0.f;
+          if (!keep_byte(hv, dsh, drop.thr)) d0 = -dl;
+          if (!keep_byte(hv, dsh + 8, drop.thr)) d1 = -dl;
         }
-        dpt[i] = p.x * (d.x - dl);  // dS^T
-        dpt[i + 1] = p.y * (d.y - dl);
+        dpt[i] = p0 * d0;  // dS^T
+        dpt[i + 1] = p1 * d1;
       }
       // dQ^T[d, q] += K^T[d, keys] . dS^T[keys, q]
 #pragma unroll

@@ -16,6 +16,7 @@ read once per sub-block. Layer 0 folds the embedding dropout into the same kerne
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field
 from typing import Optional
 
@@ -210,6 +211,62 @@ def _apply_rope_parts(flat, cos, sin, rot, nh, nkv, hd, b, s, inverse):
         k.copy_(SF._rope_ref(k, cos.to(flat.device), sin.to(flat.device), rot, pos, inverse))
 
 
+class _FusedGeluMLP(torch.autograd.Function):
+    """fc1 -> bias + GeLU(tanh) -> fc2 with the activation folded into hipBLASLt epilogues (TP = 1):
+    forward  GELU_AUX_BIAS writes gelu(x W1^T + b1) and the pre-activation in the fc1 GEMM;
+    backward DGELU_BGRAD turns the fc2 dgrad GEMM into d(pre-activation) and emits the fc1 bias
+    gradient, so the two bias-GeLU elementwise passes (K5) and their HBM round trips disappear.
+    Weight gradients go through the fused fp32 main_grad accumulation like every linear."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2):
+        C = _ext_mod().ext()
+        shp = x.shape
+        x2 = x.reshape(-1, shp[-1])
+        if not x2.is_contiguous():
+            x2 = x2.contiguous()
+        M, f = x2.shape[0], w1.shape[0]
+        act = x2.new_empty(M, f)
+        aux = x2.new_empty(M, f)
+        if not C.linear_gelu_fwd(x2, w1, b1, act, aux):
+            raise RuntimeError("linear_gelu_fwd: no hipBLASLt solution")
+        y = torch.nn.functional.linear(act, w2)
+        ctx.save_for_backward(x2, w1, w2, act, aux)
+        ctx.b1 = b1
+        ctx.shp = shp
+        return y.view(*shp[:-1], w2.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w1, w2, act, aux = ctx.saved_tensors
+        C = _ext_mod().ext()
+        dy2 = dy.reshape(-1, dy.shape[-1]).contiguous()
+        dw2 = tp._wgrad(w2, dy2, act)
+        d_pre = torch.empty_like(aux)
+        bg = torch.empty(aux.shape[1], dtype=torch.float32, device=aux.device)
+        if not C.linear_dgelu_bwd(dy2, w2, aux, d_pre, bg):
+            raise RuntimeError("linear_dgelu_bwd: no hipBLASLt solution")
+        b1 = ctx.b1
+        tgt = SF.grad_accumulate_target(b1)
+        if tgt is not None:
+            tgt.add_(bg)
+            b1._smdt_grad_ready(b1)
+            db1 = None
+        else:
+            db1 = bg.to(b1.dtype)
+        dx = d_pre.matmul(w1)
+        dw1 = tp._wgrad(w1, d_pre, x2)
+        return dx.view(ctx.shp), dw1, db1, dw2
+
+
+def _ext_mod():
+    from ..ops import _ext
+    return _ext
+
+
+_FUSED_MLP_STATE = {"ok": os.environ.get("SMDT_FUSED_MLP_EPILOGUE", "1") == "1"}
+
+
 class ParallelMLP(nn.Module):
     def __init__(self, cfg: TransformerConfig, layer_number: int, device=None):
         super().__init__()
@@ -230,7 +287,21 @@ class ParallelMLP(nn.Module):
                                         params_dtype=cfg.params_dtype, device=device,
                                         sequence_parallel=cfg.sequence_parallel, skip_bias_add=True)
 
+    def _fused_ok(self, x):
+        return (_FUSED_MLP_STATE["ok"] and self.cfg.activation == "gelu" and self.cfg.bias_gelu_fusion
+                and self.fc1.bias is not None and self.fc1.tp == 1 and not self.fc1.sequence_parallel
+                and x.is_cuda and x.dtype in (torch.bfloat16, torch.float16) and _ext_mod().use_kernels(x)
+                and self.fc1.weight.dtype == x.dtype)
+
     def forward(self, x):
+        if self._fused_ok(x):
+            try:
+                y = _FusedGeluMLP.apply(x, self.fc1.weight, self.fc1.bias, self.fc2.weight)
+                return y, self.fc2.bias
+            except RuntimeError as e:  # no epilogue solution in this hipBLASLt build: use K5 kernels
+                if "no hipBLASLt solution" not in str(e):
+                    raise
+                _FUSED_MLP_STATE["ok"] = False
         h, b = self.fc1(x)
         act = self.cfg.activation
         if act in ("gelu", "gelu_erf"):
