@@ -13,7 +13,7 @@ sys.path.insert(0, ".")
 from smdt_amd.ops import _ext  # noqa: E402
 
 SHAPES = {"qkv": (3072, 1024), "proj": (1024, 1024), "fc1": (4096, 1024), "fc2": (1024, 4096),
-          "lm_head": (50304, 1024)}
+          "lm_head": (50304, 1024), "square_256_tiles": (4096, 4096)}
 
 
 def timeit(fn, iters=20):
@@ -31,8 +31,11 @@ def timeit(fn, iters=20):
 
 def main():
     M = 16384
+    only = sys.argv[1].split(",") if len(sys.argv) > 1 else None
     C = _ext.ext()
     for name, (N, K) in SHAPES.items():
+        if only and name not in only:
+            continue
         g = torch.randn(M, N, device="cuda", dtype=torch.bfloat16)
         x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
         mg = torch.zeros(N, K, device="cuda", dtype=torch.float32)
@@ -57,5 +60,36 @@ def main():
         print(json.dumps({k: (round(v, 1) if isinstance(v, float) else v) for k, v in r.items()}), flush=True)
 
 
+def grouped(layers=4):
+    """Deferred-wgrad form: every layer's QKV / proj / fc1 / fc2 weight gradient in ONE grouped
+    launch (no split-K) vs the same GEMMs one by one (hipBLASLt and the split-K MFMA kernel)."""
+    M = 16384
+    C = _ext.ext()
+    probs = []
+    for _ in range(layers):
+        for name in ("qkv", "proj", "fc1", "fc2"):
+            N, K = SHAPES[name]
+            probs.append((torch.zeros(N, K, device="cuda"), torch.randn(M, N, device="cuda", dtype=torch.bfloat16),
+                          torch.randn(M, K, device="cuda", dtype=torch.bfloat16)))
+    mgs, dys, xs = (list(t) for t in zip(*probs))
+    flops = sum(2.0 * M * d.shape[1] * x.shape[1] for d, x in zip(dys, xs))
+    r = {"shape": f"grouped_{layers}_layers", "problems": len(probs)}
+    r["grouped_us"] = timeit(lambda: C.wgrad_grouped(mgs, dys, xs))
+    r["blaslt_each_us"] = timeit(lambda: [C.wgrad_accumulate(m, d, x) for m, d, x in probs])
+    r["mfma_each_us"] = timeit(lambda: [C.wgrad_mfma(m, d, x, 0) for m, d, x in probs])
+    for k in list(r):
+        if k.endswith("_us"):
+            r[k.replace("_us", "_tflops")] = round(flops / (r[k] * 1e-6) / 1e12, 1)
+    # correctness of the grouped path on a 1024-row slice
+    sl = [(torch.zeros_like(m), d[:1024].contiguous(), x[:1024].contiguous()) for m, d, x in probs[:4]]
+    C.wgrad_grouped([a for a, _, _ in sl], [b for _, b, _ in sl], [c for _, _, c in sl])
+    r["grouped_max_rel_err"] = max(float((a - b.float().t() @ c.float()).abs().max() / (b.float().t() @ c.float()).abs().max())
+                                   for a, b, c in sl)
+    print(json.dumps({k: (round(v, 4) if isinstance(v, float) else v) for k, v in r.items()}), flush=True)
+
+
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 1 and sys.argv[1].startswith("grouped"):
+        grouped(int(sys.argv[2]) if len(sys.argv) > 2 else 4)
+    else:
+        main()

@@ -306,6 +306,27 @@ bool wgrad_mfma(Tensor main_grad, Tensor dy, Tensor x, int64_t max_splits) {
   return true;
 }
 
+// Grouped form: main_grads[i] += dys[i]^T . xs[i] for every i in ONE launch per 32 problems.
+// Returns false (and does nothing) when any problem is unsupported. The targets must not overlap.
+bool wgrad_grouped(std::vector<Tensor> main_grads, std::vector<Tensor> dys, std::vector<Tensor> xs) {
+  const size_t n = main_grads.size();
+  TORCH_CHECK(dys.size() == n && xs.size() == n, "wgrad_grouped: list lengths differ");
+  std::vector<SmdtWgradProblem> probs(n);
+  for (size_t i = 0; i < n; ++i) {
+    const Tensor &mg = main_grads[i], &dy = dys[i], &x = xs[i];
+    if (!mg.is_cuda() || mg.scalar_type() != at::kFloat || !mg.is_contiguous()) return false;
+    if (dy.dim() != 2 || x.dim() != 2 || !dy.is_contiguous() || !x.is_contiguous()) return false;
+    if (dy.scalar_type() != at::kBFloat16 || x.scalar_type() != at::kBFloat16) return false;
+    if (dy.get_device() != mg.get_device() || x.get_device() != mg.get_device()) return false;
+    const int64_t M = dy.size(0), N = dy.size(1), K = x.size(1);
+    if (x.size(0) != M || mg.numel() != N * K || !smdt_wgrad_supported(M, N, K)) return false;
+    probs[i] = SmdtWgradProblem{dy.data_ptr(), x.data_ptr(), mg.data_ptr<float>(), M, N, K};
+  }
+  if (n == 0) return true;
+  check(smdt_wgrad_grouped(probs.data(), (int)n, cur_stream()), "wgrad_grouped");
+  return true;
+}
+
 // ------------------------------------------------------------------ bias gradient
 // out[N] (fp32) = / += column sums of dy [.., N]
 void bias_grad(Tensor dy, Tensor out, bool accumulate) {
@@ -452,6 +473,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("rope_", &rope_);
   m.def("bias_grad", &bias_grad);
   m.def("wgrad_mfma", &wgrad_mfma, arg("main_grad"), arg("dy"), arg("x"), arg("max_splits") = 0);
+  m.def("wgrad_grouped", &wgrad_grouped, arg("main_grads"), arg("dys"), arg("xs"));
   m.def("ce_stats", &ce_stats);
   m.def("ce_bwd", &ce_bwd);
   namespace py = pybind11;

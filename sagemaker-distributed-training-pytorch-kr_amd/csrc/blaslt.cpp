@@ -257,6 +257,9 @@ EPlan make_eplan(DevState& st, int kind, int64_t m, int64_t n, int64_t k, hipDat
   int cnt = 0;
   hipblasStatus_t s = hipblasLtMatmulAlgoGetHeuristic(st.handle, p.desc, p.la, p.lb, p.ld, p.ld, pref, kCand, res, &cnt);
   hipblasLtMatmulPreferenceDestroy(pref);
+  if (std::getenv("SMDT_BLASLT_DEBUG"))
+    fprintf(stderr, "[smdt blaslt] epilogue kind %d m=%ld n=%ld k=%ld: heuristic status %d, %d candidates\n", kind,
+            (long)m, (long)n, (long)k, (int)s, cnt);
   if (!chk(s) || cnt <= 0) return p;
   hipStream_t stream = c10::hip::getCurrentHIPStream().stream();
   hipEvent_t e0, e1;
@@ -285,6 +288,8 @@ EPlan make_eplan(DevState& st, int kind, int64_t m, int64_t n, int64_t k, hipDat
   }
   hipEventDestroy(e0);
   hipEventDestroy(e1);
+  if (std::getenv("SMDT_BLASLT_DEBUG"))
+    fprintf(stderr, "[smdt blaslt] epilogue kind %d: best candidate %d (%.3f ms / 3 runs)\n", kind, best, best_ms);
   if (best >= 0) {
     p.algo = res[best].algo;
     p.ws = res[best].workspaceSize;

@@ -92,5 +92,14 @@ hipError_t smdt_flash_bwd(int dtype, const void* q, const void* k, const void* v
 int smdt_wgrad_supported(int64_t M, int64_t N, int64_t K);
 hipError_t smdt_wgrad_accumulate(const void* dy, const void* x, float* main_grad, int64_t M, int64_t N,
                                  int64_t K, int max_splits, hipStream_t st);
+struct SmdtWgradProblem {
+  const void* dy;      // [M, N] bf16
+  const void* x;       // [M, K] bf16
+  float* main_grad;    // [N, K] fp32, += dy^T x
+  int64_t M, N, K;
+};
+// Many independent wgrad accumulations in one launch per 32 (no split-K, no atomics). The
+// main_grad targets of one call must not overlap.
+hipError_t smdt_wgrad_grouped(const SmdtWgradProblem* probs, int n, hipStream_t st);
 
 }  // extern "C"

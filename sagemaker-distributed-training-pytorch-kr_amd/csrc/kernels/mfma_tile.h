@@ -46,7 +46,7 @@ struct Geo {
   // Swizzle: depends on row bits 0..3 only, so offsets of rows r and r + 16 k differ by a
   // constant.
   __device__ static __forceinline__ int f(int r) {
-    if constexpr (D == 128) return ((r & 3) << 2) | ((r >> 2) & 3);
+    if constexpr (D >= 128) return ((r & 3) << 2) | ((r >> 2) & 3);
     else return (((r >> 1) & 1) << 2) | ((r >> 2) & 3);
   }
   __device__ static __forceinline__ int off(int r, int c) { return r * RB + 16 * (c ^ f(r)); }
@@ -57,18 +57,27 @@ template <int D>
 struct Frag {
   int row[D / 16];     // row fragment of k-step ks for tile rows 0..31
   int tr[D / 32][2];   // transposed fragment of d-tile dt, k-step 0, rows 0..15 (two 4-row blocks)
+  // Offset of the transposed read of d-tile dt, 4-row block `blk` (rows 4 h + (lane >> 2 & 3) + 8 blk).
+  __device__ static __forceinline__ int tr_off(int lane, int dt, int blk) {
+    const int h = lane >> 5, q = (lane >> 2) & 3, p = lane & 3, g = (lane >> 4) & 1;
+    return Geo<D>::off(4 * h + q + 8 * blk, 4 * dt + 2 * g + (p >> 1)) + 8 * (p & 1);
+  }
   __device__ __forceinline__ void init(int lane) {
     const int l31 = lane & 31, h = lane >> 5;
 #pragma unroll
     for (int ks = 0; ks < D / 16; ++ks) row[ks] = Geo<D>::off(l31, 2 * ks + h);
-    const int q = (lane >> 2) & 3, p = lane & 3, g = (lane >> 4) & 1;
-    const int r0 = 4 * h + q;
 #pragma unroll
     for (int dt = 0; dt < D / 32; ++dt) {
-      const int c = 4 * dt + 2 * g + (p >> 1);
-      tr[dt][0] = Geo<D>::off(r0, c) + 8 * (p & 1);
-      tr[dt][1] = Geo<D>::off(r0 + 8, c) + 8 * (p & 1);
+      tr[dt][0] = tr_off(lane, dt, 0);
+      tr[dt][1] = tr_off(lane, dt, 1);
     }
+  }
+  // Transposed fragment at precomputed offsets (o0, o1) = (tr_off(.., 0), tr_off(.., 1)).
+  __device__ static __forceinline__ bf16x8 trf_at(const char* tile, int rbase, int s, int o0, int o1) {
+    const char* b = tile + (rbase + 16 * s) * Geo<D>::RB;
+    s16x4 x = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(b + o0));
+    s16x4 y = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(b + o1));
+    return __builtin_bit_cast(bf16x8, __builtin_shufflevector(x, y, 0, 1, 2, 3, 4, 5, 6, 7));
   }
   // A-operand row fragment: rows rbase..rbase+31 (rbase multiple of 32), elements 16 ks + 8 h..
   __device__ __forceinline__ bf16x8 rowf(const char* tile, int rbase, int ks) const {
@@ -76,10 +85,7 @@ struct Frag {
   }
   // A-operand transposed fragment over tile rows rbase + 16 s + (permuted), columns 32 dt + lane&31.
   __device__ __forceinline__ bf16x8 trf(const char* tile, int rbase, int s, int dt) const {
-    const char* b = tile + (rbase + 16 * s) * Geo<D>::RB;
-    s16x4 x = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(b + tr[dt][0]));
-    s16x4 y = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(b + tr[dt][1]));
-    return __builtin_bit_cast(bf16x8, __builtin_shufflevector(x, y, 0, 1, 2, 3, 4, 5, 6, 7));
+    return trf_at(tile, rbase, s, tr[dt][0], tr[dt][1]);
   }
 };
 

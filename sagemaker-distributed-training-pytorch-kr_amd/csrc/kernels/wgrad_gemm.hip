@@ -5,19 +5,32 @@
 //
 // Why a hand-written kernel: the reduction index m (tokens) is the SLOW index of both operands.
 // Library GEMMs treat that as the "NT" layout and stage each operand through an LDS transpose;
-// on MI355X hipBLASLt's best NT fp32-output kernels reach 0.36-1.0 PF/s on the GPT-2 345M wgrad
-// shapes (profiles/r1_attn_dropout/wgrad_variants.jsonl) vs 1.1-1.4 for the same GEMMs with the
-// reduction index contiguous. gfx950's ds_read_b64_tr_b16 reads a row-major [m][n] LDS tile by
-// COLUMNS, which is exactly an MFMA operand fragment with 8 consecutive m per lane — so both
-// operands are staged row-major (plain 16-byte global loads, no transpose anywhere) and read
-// transposed from LDS (mfma_tile.h, the same images the flash-attention kernels use).
+// gfx950's ds_read_b64_tr_b16 reads a row-major [m][n] LDS tile by COLUMNS, which is exactly an
+// MFMA operand fragment with 8 consecutive m per lane — so both operands are staged row-major and
+// read transposed from LDS (mfma_tile.h, the same images the flash-attention kernels use). No
+// transpose pass exists anywhere.
 //
-// Structure: 128 x 128 output tile per workgroup (4 waves, 2 x 2, each 64 x 64 = 2 x 2 MFMA
-// 32x32x16 accumulators), 64-row m stages double-buffered in LDS (2 x 32 KB) with register
-// staging issued before the MFMA work of the current stage (one barrier per stage). Small
-// outputs are split along m (split-K) so the grid covers the 256 CUs; split partials are added
-// with hardware fp32 atomics, a single split does a plain read-modify-write (deterministic).
-// Blocks are remapped so consecutive work items (same split, same n-block) share an XCD's L2.
+// Tile: 256 (n) x 256 (k) output per workgroup, 8 waves as 2 (n) x 4 (k), each wave 128 x 64 =
+// 4 x 2 MFMA 32x32x16 accumulators. 32-row m stages of both operands are copied global -> LDS by
+// global_load_lds_dwordx4 (no VGPR staging, no ds_write pass): the LDS image is lane-linear, so
+// the XOR swizzle that keeps the transposed reads bank-conflict free is applied to the per-lane
+// SOURCE address. Four stage buffers form a ring with three stages in flight: a stage waits
+// with a counted vmcnt for its own DMA only, then one raw s_barrier publishes it (measured on
+// MI355X: with one stage in flight the kernel spent ~35 % of its time waiting for the DMA —
+// benchmarks/wgrad_micro.hip). Each buffer is its own __shared__ object so the compiler can
+// see that reads of one buffer do not alias the DMA into another and does not drain the queue.
+//
+// Two launch forms:
+//   * smdt_wgrad_accumulate: one GEMM; small outputs are split along m (split-K) to cover the
+//     256 CUs and the split partials are added with fp32 atomics (~1.3 TB/s chip-wide, so the
+//     split count is chosen against that cost); one split does a plain read-modify-write.
+//   * smdt_wgrad_grouped: many independent GEMMs (e.g. several layers' QKV / proj / fc1 / fc2
+//     weight gradients queued by the deferred-wgrad path) in ONE launch, every tile over its full
+//     m range: no split-K, no atomics, deterministic, and the tile count of a whole group fills
+//     the machine where a single small GEMM cannot.
+// Work items are ordered (problem, n-group, k, n-in-group) and remapped so that the consecutive
+// items an XCD runs share A and B strips in that XCD's L2. Partial tiles (N or K not a multiple
+// of 256, as the 50304-row LM head) load clamped columns and skip their stores.
 #include "common.h"
 #include "launchers.h"
 #include "mfma_tile.h"
@@ -26,97 +39,237 @@ namespace smdt {
 namespace wg {
 
 using namespace mt;
-using G = Geo<128>;
-constexpr int BN = 128, BK = 128, BM = kTile;
+constexpr int BT = 256;              // output tile edge (n and k)
+constexpr int BM = 32;               // m rows per stage
+using G = Geo<BT>;                   // rows of 512 B, XOR-swizzled 16-byte chunks (row bits 0..3)
+using F = Frag<BT>;
+constexpr int SB = BM * G::RB;       // bytes per operand stage image (16 KB)
+constexpr int kThreads = 512;
+constexpr int kWaves = kThreads / 64;
+constexpr int kGlds = SB / 1024 / kWaves;  // 1 KB wave-instructions per operand per stage per wave (2)
+constexpr int kNBuf = 4;
 
-template <bool ATOMIC>
-__global__ __launch_bounds__(256, 2) void wgrad_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
-                                                     float* __restrict__ C, int M, int N, int K, int ntn,
-                                                     int ntk, int m_per_split, int nblocks) {
-  __shared__ __attribute__((aligned(16))) char lds[2 * 2 * G::TB];  // [buf][A | B], 64 KB
+using lds_void = __attribute__((address_space(3))) void;
 
-  // XCD-aware bijective remap (blocks are dispatched round-robin over the 8 XCDs).
-  const int orig = blockIdx.x;
-  const int xcd = orig & 7, q = nblocks >> 3, r = nblocks & 7;
-  const int w = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
-  const int tk = w % ntk;
-  const int t2 = w / ntk;
-  const int tn = t2 % ntn;
-  const int split = t2 / ntn;
-  const int n0 = tn * BN, k0 = tk * BK;
-  const int mstart = split * m_per_split;
-  const int mend = min(M, mstart + m_per_split);
-  const int nst = (mend - mstart) / BM;
+// s_waitcnt with vmcnt = n and the other counters left alone (gfx9 encoding).
+template <int n>
+__device__ __forceinline__ void wait_vm() {
+  static_assert(n >= 0 && n < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((n & 15) | ((n >> 4) << 14) | (7 << 4) | (15 << 8));
+}
 
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, h = lane >> 5;
-  const int wr = wv >> 1, wc = wv & 1;  // wave tile: n rows [64 wr, +64), k cols [64 wc, +64)
-
-  Frag<128> fr;
-  fr.init(lane);
-  f32x16 acc[2][2];
+// Copy one 32 x 256 bf16 stage of an operand into its LDS image. Wave instruction i (of 16)
+// fills image rows 2i, 2i+1; lane l lands at slot (row 2i + l/32, chunk l%32) and therefore
+// loads the global chunk whose swizzled position that is: chunk (l % 32) ^ f(row).
+struct Glds {
+  int off[kGlds];   // element offsets within the stage (row * ld + clamped column)
+  __device__ __forceinline__ void init(int wave, int lane, int ld, int col0, int ncols) {
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+    for (int j = 0; j < kGlds; ++j) {
+      const int r = 2 * (wave * kGlds + j) + (lane >> 5);
+      const int c = (lane & 31) ^ G::f(r);
+      int col = col0 + 8 * c;
+      if (col > ncols - 8) col = ncols - 8;  // partial tile: any in-bounds column, never stored
+      off[j] = r * ld + col;
+    }
+  }
+  __device__ __forceinline__ void issue(const bf16* stage_base, char* img, int wave) const {
+#pragma unroll
+    for (int j = 0; j < kGlds; ++j)
+      __builtin_amdgcn_global_load_lds((const void*)(stage_base + off[j]),
+                                       (lds_void*)(img + (wave * kGlds + j) * 1024), 16, 0, 0);
+  }
+};
+
+// One 256 x 256 output tile over stages [0, nst) of 32 rows starting at A/B row mstart.
+// VAR is a diagnostic knob for benchmarks/wgrad_micro.hip only (the library uses VAR = 0):
+// bit 0 skips the in-loop DMA, bit 2 the fragment reads.
+template <bool ATOMIC, int VAR>
+__device__ __forceinline__ void tile_gemm(const bf16* __restrict__ A, const bf16* __restrict__ B,
+                                          float* __restrict__ C, int N, int K, int n0, int k0, int64_t mstart,
+                                          int nst, char* L0, char* L1, char* L2, char* L3) {
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), h = lane >> 5;
+  const int wn = wave >> 2, wk = wave & 3;  // wave tile: n rows [128 wn, +128), k cols [64 wk, +64)
+
+  int oa[4][2], ob[2][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    oa[i][0] = F::tr_off(lane, 4 * wn + i, 0);
+    oa[i][1] = F::tr_off(lane, 4 * wn + i, 1);
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    ob[j][0] = F::tr_off(lane, 2 * wk + j, 0);
+    ob[j][1] = F::tr_off(lane, 2 * wk + j, 1);
+  }
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = zero16();
 
-  Stage<128> sa, sb;
-  sa.init(N);
-  sb.init(K);
-  const bf16* Ab = A + (int64_t)mstart * N + n0;
-  const bf16* Bb = B + (int64_t)mstart * K + k0;
-  if (nst > 0) {
-    sa.load(Ab);
-    sb.load(Bb);
-    sa.store(lds);
-    sb.store(lds + G::TB);
-  }
-  __syncthreads();
+  Glds ga, gb;
+  ga.init(wave, lane, N, n0, N);
+  gb.init(wave, lane, K, k0, K);
+  const bf16* Ab = A + mstart * N;
+  const bf16* Bb = B + mstart * K;
+  const int64_t sa = (int64_t)BM * N, sbk = (int64_t)BM * K;
 
-  for (int t = 0; t < nst; ++t) {
-    const bool more = t + 1 < nst;
-    const char* at = lds + (t & 1) * 2 * G::TB;
-    const char* bt = at + G::TB;
-    if (more) {
-      sa.load(Ab + (int64_t)(t + 1) * BM * N);
-      sb.load(Bb + (int64_t)(t + 1) * BM * K);
-    }
+  auto issue = [&](int s, char* img) {
+    ga.issue(Ab + s * sa, img, wave);
+    gb.issue(Bb + s * sbk, img + SB, wave);
+  };
+  // Prologue: stages 0 .. kNBuf-2 in flight, wait for stage 0. Every stage issues exactly one
+  // DMA (past the end it re-reads the last stage into a buffer nobody reads again), so the
+  // counted waits below are uniform and the compiler's own wait insertion stays out of the loop.
+  issue(0, L0);
+  issue(min(1, nst - 1), L1);
+  issue(min(2, nst - 1), L2);
+  wait_vm<2 * 2 * kGlds>();
+  __builtin_amdgcn_s_barrier();
+
+  // Stage s: prefetch stage s+kNBuf-1 into `pre` (the buffer stage s-1 read, released by the
+  // barrier that ended it), MFMA over `cur`, retire stage s+1's DMA, barrier.
+  auto stage = [&](int s, const char* cur, char* pre) {
+    if (!(VAR & 1)) issue(min(s + kNBuf - 1, nst - 1), pre);
+    const char* at = cur;
+    const char* bt = cur + SB;
 #pragma unroll
-    for (int rb = 0; rb < 64; rb += 32) {
+    for (int ks = 0; ks < BM / 16; ++ks) {
+      bf16x8 b0, b1;
+      if constexpr (VAR & 4) {
+        const f32x4 t4 = {acc[0][0][4 * ks], acc[0][1][4 * ks], acc[1][0][4 * ks], acc[1][1][4 * ks]};
+        b0 = __builtin_bit_cast(bf16x8, t4);
+        b1 = b0;
+      } else {
+        b0 = F::trf_at(bt, 0, ks, ob[0][0], ob[0][1]);
+        b1 = F::trf_at(bt, 0, ks, ob[1][0], ob[1][1]);
+      }
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const bf16x8 a0 = fr.trf(at, rb, s, 2 * wr), a1 = fr.trf(at, rb, s, 2 * wr + 1);
-        const bf16x8 b0 = fr.trf(bt, rb, s, 2 * wc), b1 = fr.trf(bt, rb, s, 2 * wc + 1);
-        acc[0][0] = mfma(a0, b0, acc[0][0]);
-        acc[0][1] = mfma(a0, b1, acc[0][1]);
-        acc[1][0] = mfma(a1, b0, acc[1][0]);
-        acc[1][1] = mfma(a1, b1, acc[1][1]);
+      for (int i = 0; i < 4; ++i) {
+        bf16x8 a;
+        if constexpr (VAR & 4) a = b1;
+        else a = F::trf_at(at, 0, ks, oa[i][0], oa[i][1]);
+        acc[i][0] = mfma(a, b0, acc[i][0]);
+        acc[i][1] = mfma(a, b1, acc[i][1]);
       }
     }
-    if (more) {
-      char* nb = lds + ((t + 1) & 1) * 2 * G::TB;
-      sa.store(nb);
-      sb.store(nb + G::TB);
-    }
-    __syncthreads();
+    // Stages s+2 .. s+kNBuf-1 stay in flight; stage s+1 must have landed.
+    wait_vm<(kNBuf - 2) * 2 * kGlds>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  };
+  int s = 0;
+  for (; s + kNBuf <= nst; s += kNBuf) {
+    stage(s, L0, L3);
+    stage(s + 1, L1, L0);
+    stage(s + 2, L2, L1);
+    stage(s + 3, L3, L2);
   }
+  if (s < nst) stage(s, L0, L3);
+  if (s + 1 < nst) stage(s + 1, L1, L0);
+  if (s + 2 < nst) stage(s + 2, L2, L1);
+  wait_vm<0>();  // drain the trailing re-reads before the workgroup's LDS is released
 
-  // Epilogue: register r of acc[i][j] is C[n0 + 64 wr + 32 i + acc_row(r, h)][k0 + 64 wc + 32 j + lane&31];
-  // the 32 lanes of a half write 32 consecutive fp32 (128 B) per register.
+  // Epilogue: register r of acc[i][j] is C[n0 + 128 wn + 32 i + acc_row(r, h)][k0 + 64 wk + 32 j + lane&31];
+  // the 32 lanes of a half write 32 consecutive fp32 (128 B) per register. Full 32-row blocks
+  // issue all 16 loads before the adds (one round trip per block, not per element).
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int j = 0; j < 2; ++j) {
+    const int k = k0 + 64 * wk + 32 * j + (lane & 31);
+    const bool kok = k < K;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      float* cp = C + (int64_t)(n0 + 64 * wr + 32 * i) * K + (k0 + 64 * wc + 32 * j + (lane & 31));
+    for (int i = 0; i < 4; ++i) {
+      const int nb = n0 + 128 * wn + 32 * i;
+      float* cp = C + (int64_t)nb * K + k;
+      if (nb + 32 <= N && kok) {
+        if constexpr (ATOMIC) {
 #pragma unroll
-      for (int r2 = 0; r2 < 16; ++r2) {
-        float* p = cp + (int64_t)acc_row(r2, h) * K;
-        if constexpr (ATOMIC)
-          unsafeAtomicAdd(p, acc[i][j][r2]);
-        else
-          *p += acc[i][j][r2];
+          for (int r2 = 0; r2 < 16; ++r2) unsafeAtomicAdd(cp + (int64_t)acc_row(r2, h) * K, acc[i][j][r2]);
+        } else {
+          float old[16];
+#pragma unroll
+          for (int r2 = 0; r2 < 16; ++r2) old[r2] = cp[(int64_t)acc_row(r2, h) * K];
+#pragma unroll
+          for (int r2 = 0; r2 < 16; ++r2) cp[(int64_t)acc_row(r2, h) * K] = old[r2] + acc[i][j][r2];
+        }
+      } else if (kok) {
+        for (int r2 = 0; r2 < 16; ++r2) {
+          const int rr = acc_row(r2, h);
+          if (nb + rr >= N) continue;
+          float* p = cp + (int64_t)rr * K;
+          if constexpr (ATOMIC)
+            unsafeAtomicAdd(p, acc[i][j][r2]);
+          else
+            *p += acc[i][j][r2];
+        }
       }
     }
+  }
 }
+
+// XCD-aware bijective remap: hardware dispatches block b to XCD b % 8; give each XCD a
+// contiguous range of work items.
+__device__ __forceinline__ int xcd_remap(int orig, int nblocks) {
+  const int xcd = orig & 7, q = nblocks >> 3, rem = nblocks & 7;
+  return (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + (orig >> 3);
+}
+
+// Tile t of an ntn x ntk grid in groups of gn n-tiles x all k-tiles, n fastest inside a group.
+__device__ __forceinline__ void tile_coords(int t, int ntn, int ntk, int gn, int& tn, int& tk) {
+  const int grp = t / (gn * ntk);
+  const int gn_eff = min(gn, ntn - grp * gn);
+  const int tg = t - grp * gn * ntk;
+  tn = grp * gn + tg % gn_eff;
+  tk = tg / gn_eff;
+}
+
+#define WG_LDS                                                    \
+  __shared__ __attribute__((aligned(1024))) char L0[2 * SB];      \
+  __shared__ __attribute__((aligned(1024))) char L1[2 * SB];      \
+  __shared__ __attribute__((aligned(1024))) char L2[2 * SB];      \
+  __shared__ __attribute__((aligned(1024))) char L3[2 * SB];
+
+template <bool ATOMIC, int VAR = 0>
+__global__ __launch_bounds__(kThreads, 1) void wgrad_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
+                                                          float* __restrict__ C, int M, int N, int K, int ntn,
+                                                          int ntk, int gn, int m_per_split, int nblocks) {
+  WG_LDS
+  const int w = xcd_remap(blockIdx.x, nblocks);
+  const int tiles = ntn * ntk;
+  const int split = w / tiles;
+  int tn, tk;
+  tile_coords(w - split * tiles, ntn, ntk, gn, tn, tk);
+  const int mstart = split * m_per_split;
+  const int nst = (min(M, mstart + m_per_split) - mstart) / BM;
+  tile_gemm<ATOMIC, VAR>(A, B, C, N, K, tn * BT, tk * BT, mstart, nst, L0, L1, L2, L3);
+}
+
+struct Problem {
+  const bf16* A;
+  const bf16* B;
+  float* C;
+  int M, N, K, ntn, ntk, gn, tile0;
+};
+constexpr int kMaxGroup = 32;
+struct Group {
+  Problem p[kMaxGroup];
+  int nprob, nblocks;
+};
+
+// The problem table travels in the kernel arguments (< 2 KB), read from the kernarg segment.
+__global__ __launch_bounds__(kThreads, 1) void wgrad_grouped_kernel(const Group g) {
+  WG_LDS
+  const int w = xcd_remap(blockIdx.x, g.nblocks);
+  int pi = 0;
+  while (pi + 1 < g.nprob && w >= g.p[pi + 1].tile0) ++pi;
+  const Problem& P = g.p[pi];
+  int tn, tk;
+  tile_coords(w - P.tile0, P.ntn, P.ntk, P.gn, tn, tk);
+  tile_gemm<false, 0>(P.A, P.B, P.C, P.N, P.K, tn * BT, tk * BT, 0, P.M / BM, L0, L1, L2, L3);
+}
+
+inline int group_width(int ntk) { return ntk <= 4 ? 8 : 4; }
 
 }  // namespace wg
 }  // namespace smdt
@@ -124,30 +277,75 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const bf16* __restrict__ 
 using namespace smdt;
 
 extern "C" int smdt_wgrad_supported(int64_t M, int64_t N, int64_t K) {
-  return M > 0 && M % wg::BM == 0 && N % wg::BN == 0 && K % wg::BK == 0 && M < (1ll << 31) &&
-         N * K < (1ll << 31);
+  return M > 0 && M % wg::BM == 0 && N >= 8 && K >= 8 && N % 8 == 0 && K % 8 == 0 && M < (1ll << 31) &&
+         N * K < (1ll << 31) && (int64_t)wg::BM * (N > K ? N : K) < (1ll << 31);
 }
 
 extern "C" hipError_t smdt_wgrad_accumulate(const void* dy, const void* x, float* main_grad, int64_t M,
                                             int64_t N, int64_t K, int max_splits, hipStream_t st) {
   if (!smdt_wgrad_supported(M, N, K)) return hipErrorInvalidValue;
-  const int ntn = (int)(N / wg::BN), ntk = (int)(K / wg::BK);
+  const int ntn = (int)((N + wg::BT - 1) / wg::BT), ntk = (int)((K + wg::BT - 1) / wg::BT);
   const int tiles = ntn * ntk;
-  // Enough blocks for 2 per CU on 256 CUs, splits of >= 16 stages each.
-  int splits = (512 + tiles - 1) / tiles;
-  const int max_by_m = (int)(M / (16 * wg::BM));
-  if (splits > max_by_m) splits = max_by_m > 0 ? max_by_m : 1;
-  if (max_splits > 0 && splits > max_splits) splits = max_splits;
-  if (splits < 1) splits = 1;
-  int64_t stages = M / wg::BM;
+  const int64_t stages = M / wg::BM;
+  // Split count: modelled time = rounds of 256 blocks x (stages per split + the atomic epilogue,
+  // which costs about as much as 48 stages of 32 rows when every CU adds a 256 KB partial).
+  int splits = 1;
+  if (max_splits != 1) {
+    const int cap = max_splits > 0 ? max_splits : 16;
+    double best_t = 1e30;
+    for (int s = 1; s <= cap; ++s) {
+      if (s > 1 && stages / s < 8) break;
+      const int64_t blocks = (int64_t)tiles * s;
+      const int64_t rounds = (blocks + 255) / 256;
+      const double per = (double)((stages + s - 1) / s) +
+                         (s > 1 ? 48.0 * (double)(blocks < 256 ? blocks : 256) / 256.0 : 0.0);
+      const double t = rounds * per;
+      if (t < best_t * 0.97) {
+        best_t = t;
+        splits = s;
+      }
+    }
+  }
   const int m_per_split = (int)(((stages + splits - 1) / splits) * wg::BM);
   splits = (int)((M + m_per_split - 1) / m_per_split);
   const int nblocks = tiles * splits;
+  const int gn = wg::group_width(ntk);
   if (splits > 1)
-    hipLaunchKernelGGL((wg::wgrad_kernel<true>), dim3(nblocks), dim3(256), 0, st, (const bf16*)dy, (const bf16*)x,
-                       main_grad, (int)M, (int)N, (int)K, ntn, ntk, m_per_split, nblocks);
+    hipLaunchKernelGGL((wg::wgrad_kernel<true>), dim3(nblocks), dim3(wg::kThreads), 0, st, (const bf16*)dy,
+                       (const bf16*)x, main_grad, (int)M, (int)N, (int)K, ntn, ntk, gn, m_per_split, nblocks);
   else
-    hipLaunchKernelGGL((wg::wgrad_kernel<false>), dim3(nblocks), dim3(256), 0, st, (const bf16*)dy, (const bf16*)x,
-                       main_grad, (int)M, (int)N, (int)K, ntn, ntk, m_per_split, nblocks);
+    hipLaunchKernelGGL((wg::wgrad_kernel<false>), dim3(nblocks), dim3(wg::kThreads), 0, st, (const bf16*)dy,
+                       (const bf16*)x, main_grad, (int)M, (int)N, (int)K, ntn, ntk, gn, m_per_split, nblocks);
+  return hipGetLastError();
+}
+
+// Grouped form: one launch per 32 problems, the table passed by value.
+extern "C" hipError_t smdt_wgrad_grouped(const SmdtWgradProblem* probs, int n, hipStream_t st) {
+  for (int i = 0; i < n; ++i)
+    if (!smdt_wgrad_supported(probs[i].M, probs[i].N, probs[i].K)) return hipErrorInvalidValue;
+  for (int base = 0; base < n; base += wg::kMaxGroup) {
+    wg::Group g;
+    const int cnt = n - base < wg::kMaxGroup ? n - base : wg::kMaxGroup;
+    int tiles = 0;
+    for (int i = 0; i < cnt; ++i) {
+      const SmdtWgradProblem& q = probs[base + i];
+      wg::Problem& p = g.p[i];
+      p.A = (const bf16*)q.dy;
+      p.B = (const bf16*)q.x;
+      p.C = q.main_grad;
+      p.M = (int)q.M;
+      p.N = (int)q.N;
+      p.K = (int)q.K;
+      p.ntn = (int)((q.N + wg::BT - 1) / wg::BT);
+      p.ntk = (int)((q.K + wg::BT - 1) / wg::BT);
+      p.gn = wg::group_width(p.ntk);
+      p.tile0 = tiles;
+      tiles += p.ntn * p.ntk;
+    }
+    for (int i = cnt; i < wg::kMaxGroup; ++i) g.p[i] = g.p[cnt - 1];
+    g.nprob = cnt;
+    g.nblocks = tiles;
+    hipLaunchKernelGGL(wg::wgrad_grouped_kernel, dim3(tiles), dim3(wg::kThreads), 0, st, g);
+  }
   return hipGetLastError();
 }

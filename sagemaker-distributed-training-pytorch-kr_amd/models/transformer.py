@@ -302,6 +302,8 @@ class ParallelMLP(nn.Module):
                 if "no hipBLASLt solution" not in str(e):
                     raise
                 _FUSED_MLP_STATE["ok"] = False
+                import sys
+                print(f"[smdt] fused GeLU MLP disabled ({e}); using the bias-GeLU kernels", file=sys.stderr)
         h, b = self.fc1(x)
         act = self.cfg.activation
         if act in ("gelu", "gelu_erf"):

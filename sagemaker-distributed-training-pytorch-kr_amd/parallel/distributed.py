@@ -268,6 +268,8 @@ class DistributedDataParallel(nn.Module):
             self.sync_enabled = prev
 
     def start_grad_sync(self):
+        from .tensor_parallel import flush_deferred_wgrad
+        flush_deferred_wgrad()          # queued weight-gradient GEMMs mark their params ready
         for b in self.buckets:
             if not b.launched:
                 self._launch(b)

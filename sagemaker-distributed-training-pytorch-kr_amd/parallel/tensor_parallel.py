@@ -197,21 +197,138 @@ def reduce_scatter_to_sequence_parallel_region(x):
 
 
 _FUSED_WGRAD = os.environ.get("SMDT_FUSED_WGRAD", "1") == "1"
+# Which fused fp32-accumulate wgrad GEMM runs: "mfma" (hand-written gfx950 kernel,
+# csrc/kernels/wgrad_gemm.hip), "blaslt" (hipBLASLt beta = 1) or "auto" (time both once per shape
+# on scratch buffers and keep the faster). The MFMA kernel measured faster than hipBLASLt on every
+# GPT-2 345M shape (BENCHMARKS.md), so it is the default.
+_WGRAD_IMPL = os.environ.get("SMDT_WGRAD_IMPL", "mfma")
+_WGRAD_CHOICE = {}
+
+
+def _time_us(fn, reps=3):
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    fn()
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    e.synchronize()
+    return s.elapsed_time(e) * 1e3 / reps
+
+
+def _wgrad_impl(C, mg, g2, t2):
+    if _WGRAD_IMPL != "auto" or g2.dtype != torch.bfloat16:
+        return _WGRAD_IMPL if g2.dtype == torch.bfloat16 else "blaslt"
+    key = (g2.shape[0], g2.shape[1], t2.shape[1], g2.device.index)
+    impl = _WGRAD_CHOICE.get(key)
+    if impl is None:
+        scratch = torch.zeros_like(mg)
+        impl = "blaslt"
+        if C.wgrad_mfma(scratch, g2, t2, 0):
+            tm = _time_us(lambda: C.wgrad_mfma(scratch, g2, t2, 0))
+            tb = _time_us(lambda: C.wgrad_accumulate(scratch, g2, t2))
+            impl = "mfma" if tm < tb else "blaslt"
+        _WGRAD_CHOICE[key] = impl
+    return impl
+
+
+class DeferredWgrad:
+    """Deferred, grouped weight-gradient GEMMs.
+
+    Backward produces one wgrad GEMM per linear layer; on their own the small ones (the 1024 x
+    1024 attention projection, the QKV GEMM) cannot fill 256 CUs without split-K, and split-K
+    pays fp32 atomics (~1.3 TB/s chip-wide). Instead ``_wgrad`` queues (main_grad, dY, X) and
+    the queue is flushed as ONE grouped launch of the gfx950 MFMA kernel
+    (csrc/kernels/wgrad_gemm.hip, ``smdt_wgrad_grouped``): every tile runs over the full token
+    range, no atomics, deterministic. The queue holds dY / X alive until the flush (a few hundred
+    MB per layer at GPT-2 345M scale: trivial next to 288 GB of HBM), flushes once it holds
+    ``flush_tiles`` output tiles (several layers, so gradient buckets still become ready while
+    backward runs and DDP overlaps their RCCL reduction), and is drained by DDP's
+    ``start/finish_grad_sync`` before any gradient is read. A weight is reported ready to DDP
+    only when its GEMM has been issued. Tensors are version-checked at flush time: an in-place
+    write into a queued dY or X raises instead of producing a wrong gradient.
+    """
+
+    def __init__(self):
+        self.enabled = os.environ.get("SMDT_DEFER_WGRAD", "1") == "1"
+        self.flush_tiles = int(os.environ.get("SMDT_DEFER_WGRAD_TILES", "1024"))
+        self.allow_cpu = False          # tests: exercise the queue logic with a torch fallback
+        self.items = []
+        self.targets = set()
+        self.tiles = 0
+
+    def eligible(self, mg, g2, t2):
+        if not self.enabled or mg.dtype != torch.float32 or not mg.is_contiguous():
+            return False
+        if g2.dim() != 2 or t2.dim() != 2:
+            return False
+        M, N, K = g2.shape[0], g2.shape[1], t2.shape[1]
+        if M % 32 or N % 8 or K % 8 or mg.numel() != N * K:
+            return False
+        if g2.is_cuda:
+            return (_FUSED_WGRAD and g2.dtype == torch.bfloat16 and t2.dtype == torch.bfloat16
+                    and _ext.use_kernels(g2))
+        return self.allow_cpu
+
+    def push(self, weight, mg, g2, t2):
+        key = mg.data_ptr()
+        if key in self.targets:         # same main_grad twice (grad accumulation): keep order
+            self.flush()
+        g2, t2 = g2.contiguous(), t2.contiguous()
+        self.items.append((weight, mg, g2, t2, g2._version, t2._version))
+        self.targets.add(key)
+        self.tiles += -(-g2.shape[1] // 256) * -(-t2.shape[1] // 256)
+        if self.tiles >= self.flush_tiles or len(self.items) >= 32:
+            self.flush()
+
+    def flush(self):
+        if not self.items:
+            return
+        items, self.items, self.targets, self.tiles = self.items, [], set(), 0
+        for _, _, g2, t2, vg, vt in items:
+            if g2._version != vg or t2._version != vt:
+                raise RuntimeError("deferred wgrad: a queued dY / X tensor was modified in place before the "
+                                   "flush; disable with SMDT_DEFER_WGRAD=0 and report the op that did it")
+        cuda = [it for it in items if it[2].is_cuda]
+        done = False
+        if cuda:
+            done = _ext.ext().wgrad_grouped([it[1] for it in cuda], [it[2] for it in cuda], [it[3] for it in cuda])
+        for weight, mg, g2, t2, _, _ in items:
+            if not (g2.is_cuda and done):
+                mg.add_(g2.t().matmul(t2).view_as(mg))
+            cb = getattr(weight, "_smdt_grad_ready", None)
+            if cb is not None:
+                cb(weight)
+
+
+DEFERRED_WGRAD = DeferredWgrad()
+
+
+def flush_deferred_wgrad():
+    DEFERRED_WGRAD.flush()
 
 
 def _wgrad(weight, g2, t2):
     """dW = g2^T t2. With a DDP ``main_grad`` the product is accumulated straight into the fp32
-    buffer by ONE hipBLASLt GEMM (bf16 inputs, fp32 C/D, beta = 1: ``addmm(..., out_dtype=fp32)``)
-    instead of a bf16 GEMM + a separate fp32 add pass (K7 gradient-accumulation fusion). Returns
-    the gradient to hand back to autograd (None when it went to ``main_grad``)."""
+    buffer (K7 gradient-accumulation fusion): queued for the grouped MFMA launch
+    (``DeferredWgrad``), or ONE GEMM now (the MFMA kernel or hipBLASLt with beta = 1) instead of a
+    bf16 GEMM + a separate fp32 add pass. Returns the gradient to hand back to autograd (None
+    when it goes to ``main_grad``)."""
     mg = getattr(weight, "main_grad", None)
     if mg is None:
         return g2.t().matmul(t2)
+    if DEFERRED_WGRAD.eligible(mg, g2, t2):
+        DEFERRED_WGRAD.push(weight, mg, g2, t2)
+        return None
     done = False
     if (_FUSED_WGRAD and mg.dtype == torch.float32 and g2.dtype in (torch.bfloat16, torch.float16)
             and g2.is_cuda and mg.is_contiguous()):
-        # ONE hipBLASLt GEMM with C = D = main_grad, beta = 1 (see csrc/blaslt.cpp).
-        done = _ext.ext().wgrad_accumulate(mg, g2.contiguous(), t2.contiguous())
+        C = _ext.ext()
+        g2, t2 = g2.contiguous(), t2.contiguous()
+        if _wgrad_impl(C, mg, g2, t2) == "mfma":
+            done = C.wgrad_mfma(mg, g2, t2, 0)
+        if not done:
+            done = C.wgrad_accumulate(mg, g2, t2)
     if not done:
         mg.add_(g2.t().matmul(t2).view_as(mg))
     cb = getattr(weight, "_smdt_grad_ready", None)

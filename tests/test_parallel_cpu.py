@@ -92,3 +92,48 @@ def test_interleaved_pipeline_matches_single_rank(nmb):
             _close(g, ref[n])
             seen.add(n)
     assert seen == set(ref), set(ref) ^ seen
+
+
+def test_deferred_wgrad_queue_semantics(monkeypatch):
+    """DeferredWgrad (CPU fallback): ready only at flush, duplicate target flushes first (order kept),
+    threshold flush, and an in-place write into a queued operand is caught."""
+    from smdt_amd.parallel import tensor_parallel as tp
+    q = tp.DeferredWgrad()
+    q.allow_cpu = True
+    q.flush_tiles = 3
+    monkeypatch.setattr(tp, "DEFERRED_WGRAD", q)
+    torch.manual_seed(0)
+    ready = []
+
+    def mk(o, i):
+        w = torch.nn.Parameter(torch.randn(o, i))
+        w.main_grad = torch.zeros(o, i)
+        w._smdt_grad_ready = lambda p: ready.append(p)
+        return w
+
+    a, b = mk(16, 8), mk(8, 8)
+    g1, x1 = torch.randn(64, 16), torch.randn(64, 8)
+    assert tp._wgrad(a, g1, x1) is None and not ready
+    g2, x2 = torch.randn(64, 8), torch.randn(64, 8)
+    tp._wgrad(b, g2, x2)
+    assert not ready and len(q.items) == 2
+    g3, x3 = torch.randn(64, 16), torch.randn(64, 8)
+    tp._wgrad(a, g3, x3)            # same target again: the first two are flushed first
+    assert ready == [a, b] and len(q.items) == 1
+    q.flush()
+    assert ready == [a, b, a]
+    torch.testing.assert_close(a.main_grad, g1.t() @ x1 + g3.t() @ x3)
+    torch.testing.assert_close(b.main_grad, g2.t() @ x2)
+    # threshold: 1024-wide weights are 4 x 4 = 16 tiles >= 3 -> immediate flush
+    c = mk(1024, 1024)
+    tp._wgrad(c, torch.randn(32, 1024), torch.randn(32, 1024))
+    assert ready[-1] is c and not q.items
+    # in-place modification of a queued operand is an error, not a silent wrong gradient
+    g4 = torch.randn(64, 16)
+    tp._wgrad(a, g4, torch.randn(64, 8))
+    g4.mul_(2)
+    with pytest.raises(RuntimeError, match="modified in place"):
+        q.flush()
+    # ineligible shapes (tokens not a multiple of 32) run immediately
+    tp._wgrad(b, torch.randn(33, 8), torch.randn(33, 8))
+    assert ready[-1] is b and not q.items

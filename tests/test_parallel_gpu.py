@@ -25,6 +25,26 @@ def test_wgrad_accumulates_into_fp32_main_grad(fused, monkeypatch):
     torch.testing.assert_close(w.main_grad, ref, atol=0.25, rtol=1e-2)
 
 
+def test_deferred_wgrad_grouped_flush_on_gpu():
+    """Eligible shapes are queued and issued as one grouped MFMA launch at flush time."""
+    torch.manual_seed(0)
+    ws, refs, ready = [], [], []
+    for out_f, in_f in [(384, 256), (1024, 1024), (256, 520)]:
+        w = torch.nn.Parameter(torch.randn(out_f, in_f, device="cuda", dtype=torch.bfloat16))
+        w.main_grad = torch.randn(out_f, in_f, device="cuda", dtype=torch.float32)
+        w._smdt_grad_ready = lambda p: ready.append(p)
+        g = torch.randn(1024, out_f, device="cuda", dtype=torch.bfloat16)
+        x = torch.randn(1024, in_f, device="cuda", dtype=torch.bfloat16)
+        refs.append(w.main_grad.clone() + g.float().t() @ x.float())
+        assert tp._wgrad(w, g, x) is None
+        ws.append(w)
+    assert ready == [] and len(tp.DEFERRED_WGRAD.items) == 3
+    tp.flush_deferred_wgrad()
+    assert len(ready) == 3 and not tp.DEFERRED_WGRAD.items
+    for w, ref in zip(ws, refs):
+        torch.testing.assert_close(w.main_grad, ref, atol=0.5, rtol=1e-2)
+
+
 def test_linear_autograd_single_rank_matches_torch():
     torch.manual_seed(1)
     x = torch.randn(64, 8, 256, device="cuda", dtype=torch.bfloat16, requires_grad=True)
@@ -84,6 +104,25 @@ def test_wgrad_mfma_kernel_matches_fp32_reference(shape, max_splits):
     assert _ext.ext().wgrad_mfma(mg, g, x, max_splits)
     ref = base + g.float().t() @ x.float()
     torch.testing.assert_close(mg, ref, atol=2e-2 * (M ** 0.5), rtol=1e-3)
+
+
+def test_wgrad_grouped_matches_fp32_reference():
+    """One grouped launch over problems of different shapes (incl. partial tiles) == per-problem fp32."""
+    from smdt_amd.ops import _ext
+    torch.manual_seed(3)
+    shapes = [(2048, 1024, 1024), (2048, 384, 256), (1024, 3072, 1024), (4096, 256, 520)]
+    mgs, dys, xs, refs = [], [], [], []
+    for M, N, K in shapes:
+        g = torch.randn(M, N, device="cuda", dtype=torch.bfloat16)
+        x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+        base = torch.randn(N, K, device="cuda", dtype=torch.float32)
+        mgs.append(base.clone())
+        dys.append(g)
+        xs.append(x)
+        refs.append(base + g.float().t() @ x.float())
+    assert _ext.ext().wgrad_grouped(mgs, dys, xs)
+    for (M, _, _), mg, ref in zip(shapes, mgs, refs):
+        torch.testing.assert_close(mg, ref, atol=2e-2 * (M ** 0.5), rtol=1e-3)
 
 
 def test_fused_gelu_mlp_epilogues_match_unfused():
