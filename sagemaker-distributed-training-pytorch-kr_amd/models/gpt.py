@@ -120,7 +120,7 @@ class GPTModel(nn.Module):
             pos = position_ids.transpose(0, 1)                   # [s, b]
             if self.cfg.position_offset:
                 pos = pos + self.cfg.position_offset
-            pe = self.position_embeddings[pos]                   # [s, b, h]
+            pe = tp.embedding_lookup(pos, self.position_embeddings)  # [s, b, h]
             if self.sp:
                 pe = tp.scatter_to_sequence_parallel_region(pe)
             e = e + pe

@@ -197,15 +197,20 @@ class DistributedDataParallel(nn.Module):
         if self.torch_compat and not self._callback_queued:
             self._callback_queued = True
             torch.autograd.Variable._execution_engine.queue_callback(self._auto_finalize)
-        if p.grad is not None:
-            g = p.grad
-            if g.data_ptr() != p.main_grad.data_ptr():
-                if g.is_cuda and g.dtype != p.main_grad.dtype and g.is_contiguous() and _ext.available():
-                    # fused cast + accumulate (torch's mixed-dtype add is a slow generic path)
-                    _ext.ext().cast_(g, p.main_grad, True)
-                else:
-                    p.main_grad.add_(g.view_as(p.main_grad))
-            p.grad = None
+        # The hook also fires when a backward returned None for the parameter, i.e. when a kernel
+        # accumulated into main_grad itself (or queued that work: deferred wgrad) and reports
+        # readiness through ``_smdt_grad_ready`` — counting that as ready would launch the
+        # bucket's reduction before the gradient exists.
+        if p.grad is None:
+            return
+        g = p.grad
+        if g.data_ptr() != p.main_grad.data_ptr():
+            if g.is_cuda and g.dtype != p.main_grad.dtype and g.is_contiguous() and _ext.available():
+                # fused cast + accumulate (torch's mixed-dtype add is a slow generic path)
+                _ext.ext().cast_(g, p.main_grad, True)
+            else:
+                p.main_grad.add_(g.view_as(p.main_grad))
+        p.grad = None
         self._on_grad_ready(p)
 
     def _auto_finalize(self):

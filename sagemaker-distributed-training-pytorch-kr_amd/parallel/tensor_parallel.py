@@ -281,6 +281,7 @@ class DeferredWgrad:
         if self.tiles >= self.flush_tiles or len(self.items) >= 32:
             self.flush()
 
+    @torch.no_grad()
     def flush(self):
         if not self.items:
             return
@@ -502,6 +503,44 @@ class RowParallelLinear(nn.Module):
         return y + self.bias if self.bias is not None else y
 
 
+class _EmbeddingLookup(torch.autograd.Function):
+    """out = weight[ids]. Backward scatters the rows with ``index_add_`` (device atomics, no host
+    synchronisation — torch's sort-based embedding backward stalls the CPU on the GPU and leaves
+    the tail of every backward launch-bound), straight into the fp32 DDP ``main_grad`` when the
+    weight has one (K7-style fusion: no dense bf16 [V, H] gradient, no cast pass)."""
+
+    @staticmethod
+    def forward(ctx, ids, weight):
+        ctx.save_for_backward(ids)
+        ctx.weight = weight
+        return F.embedding(ids, weight)
+
+    @staticmethod
+    def backward(ctx, g):
+        (ids,) = ctx.saved_tensors
+        w = ctx.weight
+        flat = ids.reshape(-1)
+        g2 = g.reshape(-1, g.shape[-1]).float()
+        mg = getattr(w, "main_grad", None)
+        if mg is not None and mg.dtype == torch.float32:
+            mg.index_add_(0, flat, g2)
+            cb = getattr(w, "_smdt_grad_ready", None)
+            if cb is not None:
+                cb(w)
+            return None, None
+        dw = torch.zeros(w.shape, dtype=torch.float32, device=g.device)
+        dw.index_add_(0, flat, g2)
+        return None, dw.to(w.dtype)
+
+
+def embedding_lookup(ids, weight):
+    """weight[ids] with the synchronisation-free backward above (torch's own path when
+    deterministic algorithms are requested: atomics make the fp32 sum order run-dependent)."""
+    if torch.are_deterministic_algorithms_enabled() or not torch.is_grad_enabled() or not weight.requires_grad:
+        return F.embedding(ids, weight)
+    return _EmbeddingLookup.apply(ids, weight)
+
+
 class VocabParallelEmbedding(nn.Module):
     """Embedding table split along the vocab dim; out-of-range rows contribute zeros and the
     partial lookups are summed across TP (all-reduce, or reduce-scatter with SP)."""
@@ -526,12 +565,12 @@ class VocabParallelEmbedding(nn.Module):
         if self.tp > 1:
             mask = (ids < self.vocab_start) | (ids >= self.vocab_end)
             local = (ids - self.vocab_start).masked_fill(mask, 0)
-            out = F.embedding(local, self.weight)
+            out = embedding_lookup(local, self.weight)
             out = out.masked_fill(mask.unsqueeze(-1), 0.0)
             if reduce:
                 out = reduce_from_tensor_model_parallel_region(out)
             return out
-        return F.embedding(ids, self.weight)
+        return embedding_lookup(ids, self.weight)
 
 
 # --------------------------------------------------------------------------------------------

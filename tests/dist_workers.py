@@ -81,10 +81,11 @@ def gpt_tp_worker(rank, world, tp, pp, sp, cfg_over=None):
     return out_loss, grads, meta
 
 
-def ddp_worker(rank, world, zero, steps=3, overlap_pg=False):
+def ddp_worker(rank, world, zero, steps=3, overlap_pg=False, defer=False):
     """DDP (+ZeRO) on a tiny GPT: returns final params after `steps` optimizer steps on a
     per-rank shard of a fixed global batch (so the result must equal single-process training on
-    the whole batch)."""
+    the whole batch). ``defer``: weight gradients go through the deferred grouped-wgrad queue
+    (CPU fallback), flushed every couple of GEMMs so buckets become ready mid-backward."""
     import torch.distributed as dist
     from smdt_amd.comm import init_distributed
     from smdt_amd.models.gpt import GPTModel
@@ -94,6 +95,10 @@ def ddp_worker(rank, world, zero, steps=3, overlap_pg=False):
     from smdt_amd.parallel.distributed import DistributedDataParallel
     init_distributed("gloo")
     ps.initialize_model_parallel(1, 1)
+    if defer:
+        from smdt_amd.parallel import tensor_parallel as tp
+        tp.DEFERRED_WGRAD.allow_cpu = True
+        tp.DEFERRED_WGRAD.flush_tiles = 2
     cfg = TransformerConfig(**TINY)
     m = GPTModel(cfg)
     ddp = DistributedDataParallel(m, bucket_size=20000, use_distributed_optimizer=zero,

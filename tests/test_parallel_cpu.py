@@ -68,10 +68,11 @@ def test_tp2_pp2_dp1_world4():
     torch.testing.assert_close(last[0].view(-1), ref_loss.view(-1), atol=2e-4, rtol=2e-4)
 
 
-@pytest.mark.parametrize("zero,overlap_pg", [(False, False), (True, False), (True, True)])
-def test_data_parallel_and_zero_match_single_process(zero, overlap_pg):
+@pytest.mark.parametrize("zero,overlap_pg,defer", [(False, False, False), (True, False, False), (True, True, False),
+                                                   (False, False, True), (True, True, True)])
+def test_data_parallel_and_zero_match_single_process(zero, overlap_pg, defer):
     ref, ref_g = W.single_train()
-    outs = run_workers(W.ddp_worker, 2, zero, 3, overlap_pg)
+    outs = run_workers(W.ddp_worker, 2, zero, 3, overlap_pg, defer)
     for params, grads in outs:
         for n, g in grads.items():   # reduced gradients: exact up to fp32 summation order
             torch.testing.assert_close(g, ref_g[n], atol=1e-6, rtol=1e-4)
