@@ -58,6 +58,9 @@ def init_distributed(backend: str | None = None, timeout_minutes: int = 10, set_
     bridge_ompi_env()
     rank, local, world = env_rank_info()
     be = resolve_backend(backend)
+    if backend is not None and backend.lower() in SMDDP_ALIASES:
+        from . import xgmi
+        xgmi.note_smddp_requested()  # DDP buckets that fit go through the xGMI IPC all-reduce
     if set_device and torch.cuda.is_available():
         torch.cuda.set_device(local % max(torch.cuda.device_count(), 1))
     if world > 1 and not dist.is_initialized():

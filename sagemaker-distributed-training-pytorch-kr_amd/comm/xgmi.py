@@ -1,0 +1,274 @@
+"""Single-node all-reduce over xGMI peer memory — the MI355X-native counterpart of SMDDP's fused
+all-reduce and of NCCL's intra-node P2P path (SURVEY C2', C4, §5.8, §7.4 item 1).
+
+Every rank allocates one staging buffer (4 regions: two call-parity halves x {input copy,
+reduced slice}) and one uncached signal buffer, exports both with ``hipIpcGetMemHandle`` and maps
+every peer's with ``hipIpcOpenMemHandle`` (dmabuf IPC on this ROCm). One kernel
+(``csrc/kernels/xgmi_allreduce.hip``) then reads all 7 peers over their own xGMI links at once:
+
+* one-shot (message <= ``ONE_SHOT_MAX_BYTES[world]``): every rank reduces the whole tensor;
+* two-shot: reduce-scatter through peer reads, then an all-gather of the reduced slices;
+
+both accumulate in fp32 in rank order, so every rank gets bit-identical results. Anything the
+kernel does not take — messages larger than the staging region, sizes that are not a multiple of
+16 bytes, non-contiguous or CPU tensors, groups that span hosts or are not 2 / 4 / 8 ranks, async
+calls — goes to RCCL (``dist.all_reduce``) unchanged.
+
+The reference has no custom all-reduce (stock NCCL / SMDDP collectives). Its TP
+all-reduces are 18.9 MB each (NB3) and its MNIST gradients 4.8 MB — the message range
+this path is for. It is used by the tensor-parallel layers (sync all-reduces) and by the DDP
+reducer for buckets that fit the staging region, when ``SMDT_XGMI_ALLREDUCE=1`` or when the job
+asked for the ``smddp`` backend (``SMDT_XGMI_ALLREDUCE=0`` turns it off).
+
+An engine's calls must be issued in the same order on every rank of its group and on ONE stream
+(the kernel double-buffers on a per-call counter); separate engines are used per group / stream.
+"""
+from __future__ import annotations
+
+import os
+import socket
+import warnings
+from typing import List, Optional
+
+import torch
+import torch.distributed as dist
+
+from ..ops import _ext
+
+# One-shot reads (W-1) full copies per rank; two-shot moves 2/W of the message per link but pays a
+# second barrier. Crossover chosen for 7 x ~64 GB/s-per-direction links vs ~5 us per barrier.
+ONE_SHOT_MAX_BYTES = {2: 4 << 20, 4: 1 << 20, 8: 512 << 10}
+DEFAULT_REGION_BYTES = 64 << 20
+DEFAULT_BLOCKS = 128
+
+_SMDDP_REQUESTED = False
+
+
+def note_smddp_requested():
+    """Called by ``init_distributed`` when a script asked for ``backend="smddp"``."""
+    global _SMDDP_REQUESTED
+    _SMDDP_REQUESTED = True
+
+
+def wanted() -> bool:
+    v = os.environ.get("SMDT_XGMI_ALLREDUCE")
+    if v is not None:
+        return v == "1"
+    return _SMDDP_REQUESTED
+
+
+def choose_algorithm(nbytes: int, world: int) -> str:
+    return "one_shot" if nbytes <= ONE_SHOT_MAX_BYTES.get(world, 0) else "two_shot"
+
+
+def eligible(t: torch.Tensor, world: int, region_bytes: int) -> bool:
+    nbytes = t.numel() * t.element_size()
+    return (t.is_cuda and t.is_contiguous() and t.dtype in (torch.float32, torch.bfloat16, torch.float16)
+            and world in (2, 4, 8) and 0 < nbytes <= region_bytes and nbytes % 16 == 0
+            and t.data_ptr() % 16 == 0)
+
+
+class _EventHandle:
+    """``work.wait()``-compatible handle of a call issued on the engine's side stream."""
+
+    def __init__(self, event):
+        self.event = event
+
+    def wait(self):
+        torch.cuda.current_stream().wait_event(self.event)
+        return True
+
+    def is_completed(self):
+        return self.event.query()
+
+
+class XgmiAllReduce:
+    """All-reduce engine for one process group whose ranks share a node (one GPU per rank)."""
+
+    def __init__(self, group=None, region_bytes: int = DEFAULT_REGION_BYTES, blocks: int = DEFAULT_BLOCKS,
+                 validate: bool = True):
+        self.C = _ext.ext()
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        if self.world not in (2, 4, 8):
+            raise ValueError(f"xGMI all-reduce supports 2, 4 or 8 ranks, not {self.world}")
+        self.region = (int(region_bytes) + 4095) // 4096 * 4096
+        self.blocks = int(blocks)
+        self.calls = 0
+        self._stream = None
+        self._opened: List[int] = []
+        self._data = self._sig = None
+        self.active = False
+        hosts = [None] * self.world
+        dist.all_gather_object(hosts, socket.gethostname(), group=group)
+        if len(set(hosts)) != 1:
+            raise RuntimeError(f"xGMI all-reduce needs every rank of the group on one node, got {sorted(set(hosts))}")
+        err = None
+        try:
+            self._data = self.C.ipc_malloc(4 * self.region, False)
+            self._sig = self.C.ipc_malloc(self.C.ar_signal_bytes(), True)
+            mine = (self.C.ipc_get_handle(self._data), self.C.ipc_get_handle(self._sig))
+        except RuntimeError as e:  # still take part in the collectives below
+            err, mine = e, None
+        handles = [None] * self.world
+        dist.all_gather_object(handles, mine, group=group)
+        self.data_ptrs: List[int] = []
+        self.sig_ptrs: List[int] = []
+        if err is None and all(h is not None for h in handles):
+            try:
+                for r, (hd, hs) in enumerate(handles):
+                    if r == self.rank:
+                        self.data_ptrs.append(self._data)
+                        self.sig_ptrs.append(self._sig)
+                    else:
+                        pd = self.C.ipc_open(hd)
+                        self._opened.append(pd)
+                        ps_ = self.C.ipc_open(hs)
+                        self._opened.append(ps_)
+                        self.data_ptrs.append(pd)
+                        self.sig_ptrs.append(ps_)
+            except RuntimeError as e:
+                err = e
+        ok = self._agree(err is None)
+        if not ok:
+            self.close()
+            raise RuntimeError(f"xGMI all-reduce setup failed on some rank ({err!r} here)")
+        self.active = True
+        if validate and not self._validate():
+            self.close()
+            raise RuntimeError("xGMI all-reduce failed its validation against RCCL")
+
+    # ------------------------------------------------------------------ helpers
+    def _agree(self, ok: bool) -> bool:
+        dev = torch.device("cuda", torch.cuda.current_device())
+        flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.group)
+        return bool(flag.item())
+
+    def _validate(self) -> bool:
+        """Exact check against RCCL on integer-valued fp32 data (order-independent sums), one
+        one-shot and one two-shot size, run twice so both buffer halves are exercised."""
+        dev = torch.device("cuda", torch.cuda.current_device())
+        good = True
+        n2 = ONE_SHOT_MAX_BYTES[self.world] // 4 * 2 + 1024
+        for n in (4096, min(n2, self.region // 4)):
+            for rep in range(2):
+                x = (torch.arange(n, device=dev, dtype=torch.float32) % 97) + 1000.0 * self.rank + rep
+                ref = x.clone()
+                dist.all_reduce(ref, group=self.group)
+                self.all_reduce(x)
+                good &= bool(torch.equal(x, ref))
+        torch.cuda.synchronize()
+        good &= self.error() == 0
+        return self._agree(good)
+
+    # ------------------------------------------------------------------ API
+    def fits(self, t: torch.Tensor) -> bool:
+        return self.active and eligible(t, self.world, self.region)
+
+    def all_reduce(self, t: torch.Tensor, op: str = "sum") -> bool:
+        """In-place all-reduce of ``t`` on the current stream; False (nothing done) when the
+        tensor is not eligible, so the caller falls back to RCCL."""
+        if not self.fits(t):
+            return False
+        scale = 1.0 / self.world if op == "avg" else 1.0
+        two = choose_algorithm(t.numel() * t.element_size(), self.world) == "two_shot"
+        self.C.xgmi_allreduce(t, t, self.data_ptrs, self.sig_ptrs, self.rank, 1, self.region, two, self.blocks, scale)
+        self.calls += 1
+        return True
+
+    def all_reduce_async(self, t: torch.Tensor, op: str = "sum") -> Optional[_EventHandle]:
+        """The same on the engine's own stream, ordered after the current stream's work; returns
+        a handle whose ``wait()`` makes the current stream wait (None: not eligible)."""
+        if not self.fits(t):
+            return None
+        if self._stream is None:
+            self._stream = torch.cuda.Stream(device=t.device)
+        cur = torch.cuda.current_stream(t.device)
+        self._stream.wait_stream(cur)
+        with torch.cuda.stream(self._stream):
+            self.all_reduce(t, op)
+            ev = torch.cuda.Event()
+            ev.record(self._stream)
+        t.record_stream(self._stream)
+        return _EventHandle(ev)
+
+    def error(self) -> int:
+        return int(self.C.ar_read_error(self._sig)) if self._sig is not None else 0
+
+    def check(self):
+        """Raise if any call of this engine timed out waiting for a peer (synchronises)."""
+        torch.cuda.synchronize()
+        e = self.error()
+        if e:
+            raise RuntimeError(f"xGMI all-reduce: a peer did not arrive (error word {e}); outputs were NaN-filled")
+
+    def close(self):
+        """Collective: unmap the peers' buffers, then free this rank's own."""
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+        if dist.is_initialized():
+            dist.barrier(group=self.group)
+        for p in self._opened:
+            try:
+                self.C.ipc_close(p)
+            except RuntimeError:  # pragma: no cover
+                pass
+        self._opened = []
+        if dist.is_initialized():
+            dist.barrier(group=self.group)
+        for p in (self._data, self._sig):
+            if p is not None:
+                self.C.ipc_free(p)
+        self._data = self._sig = None
+        self.active = False
+
+
+def create_for_group(group, **kw) -> Optional[XgmiAllReduce]:
+    """Collective over ``group``: an engine when xGMI all-reduce is wanted and possible, else None
+    (with a warning when it was wanted but could not be set up)."""
+    if not (wanted() and dist.is_initialized() and torch.cuda.is_available()):
+        return None
+    if dist.get_backend(group) != "nccl":
+        return None
+    ws = dist.get_world_size(group)
+    if ws not in (2, 4, 8):
+        return None
+    try:
+        return XgmiAllReduce(group, **kw)
+    except (RuntimeError, ValueError) as e:
+        warnings.warn(f"xGMI all-reduce disabled for this group: {e}")
+        return None
+
+
+class XgmiLoopback:
+    """W virtual ranks in ONE process and ONE launch (tests and microbenchmarks on a single GPU):
+    the exact kernel, barrier protocol and double-buffering, with plain device buffers instead of
+    IPC mappings."""
+
+    def __init__(self, world: int, region_bytes: int = 8 << 20, blocks: Optional[int] = None):
+        assert world in (2, 4, 8)
+        self.C = _ext.ext()
+        self.world = world
+        self.region = (int(region_bytes) + 4095) // 4096 * 4096
+        self.blocks = blocks or max(1, min(DEFAULT_BLOCKS, 512 // world))
+        self.data_ptrs = [self.C.ipc_malloc(4 * self.region, False) for _ in range(world)]
+        self.sig_ptrs = [self.C.ipc_malloc(self.C.ar_signal_bytes(), True) for _ in range(world)]
+
+    def all_reduce(self, x: torch.Tensor, two_shot: bool, scale: float = 1.0, out: Optional[torch.Tensor] = None):
+        """x: [world, n] (row r = virtual rank r's input). Returns [world, n] (out may be x)."""
+        out = torch.empty_like(x) if out is None else out
+        self.C.xgmi_allreduce(x, out, self.data_ptrs, self.sig_ptrs, 0, self.world, self.region, two_shot,
+                              self.blocks, scale)
+        return out
+
+    def errors(self) -> List[int]:
+        torch.cuda.synchronize()
+        return [int(self.C.ar_read_error(s)) for s in self.sig_ptrs]
+
+    def close(self):
+        torch.cuda.synchronize()
+        for p in self.data_ptrs + self.sig_ptrs:
+            self.C.ipc_free(p)
+        self.data_ptrs, self.sig_ptrs = [], []

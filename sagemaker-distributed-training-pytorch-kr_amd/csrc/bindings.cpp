@@ -445,6 +445,74 @@ std::vector<Tensor> flash_bwd(Tensor q, Tensor k, Tensor v, Tensor o, Tensor dou
   return {dq, dk, dv};
 }
 
+// ------------------------------------------------------------------ xGMI all-reduce (HIP IPC)
+// Raw device pointers cross the Python boundary as int64 (they are IPC mappings, not tensors).
+void* vp(int64_t p) { return reinterpret_cast<void*>(static_cast<uintptr_t>(p)); }
+
+int64_t ipc_malloc(int64_t bytes, bool uncached) {
+  TORCH_CHECK(bytes > 0, "ipc_malloc: bytes must be positive");
+  void* p = nullptr;
+  check(smdt_ipc_malloc(bytes, uncached ? 1 : 0, &p), "ipc_malloc");
+  return (int64_t)(uintptr_t)p;
+}
+
+void ipc_free(int64_t p) { check(smdt_ipc_free(vp(p)), "ipc_free"); }
+
+pybind11::bytes ipc_get_handle(int64_t p) {
+  std::string h((size_t)smdt_ipc_handle_bytes(), '\0');
+  check(smdt_ipc_get_handle(vp(p), h.data()), "ipc_get_handle");
+  return pybind11::bytes(h);
+}
+
+int64_t ipc_open(pybind11::bytes handle) {
+  const std::string h = handle;
+  TORCH_CHECK((int)h.size() == smdt_ipc_handle_bytes(), "ipc_open: handle must be ", smdt_ipc_handle_bytes(), " bytes");
+  void* p = nullptr;
+  check(smdt_ipc_open(h.data(), &p), "ipc_open");
+  return (int64_t)(uintptr_t)p;
+}
+
+void ipc_close(int64_t p) { check(smdt_ipc_close(vp(p)), "ipc_close"); }
+
+int64_t ar_read_error(int64_t sig) {
+  int e = 0;
+  check(smdt_ar_read_error(vp(sig), &e), "ar_read_error");
+  return e;
+}
+
+// out = scale * sum_ranks(in). nranks_local > 1 (loopback tests): in/out are [nranks_local, n]
+// and ranks rank .. rank + nranks_local - 1 run in one launch.
+void xgmi_allreduce(Tensor in, Tensor out, std::vector<int64_t> data_ptrs, std::vector<int64_t> sig_ptrs,
+                    int64_t rank, int64_t nranks_local, int64_t region_bytes, bool two_shot, int64_t blocks,
+                    double scale) {
+  need_contig(in, "in");
+  need_contig(out, "out");
+  TORCH_CHECK(in.sizes() == out.sizes() && in.dtype() == out.dtype() && in.device() == out.device(),
+              "xgmi_allreduce: in / out mismatch");
+  const int world = (int)data_ptrs.size();
+  TORCH_CHECK(sig_ptrs.size() == data_ptrs.size() && world >= 2 && world <= smdt_ar_max_ranks(),
+              "xgmi_allreduce: need 2..", smdt_ar_max_ranks(), " ranks");
+  TORCH_CHECK(blocks >= 1 && blocks <= smdt_ar_max_blocks(), "xgmi_allreduce: blocks out of range");
+  int64_t n = in.numel(), stride = 0;
+  if (nranks_local > 1) {
+    TORCH_CHECK(in.dim() >= 2 && in.size(0) == nranks_local, "xgmi_allreduce loopback: in must be [nranks_local, ...]");
+    TORCH_CHECK(blocks * nranks_local <= 512, "xgmi_allreduce loopback: blocks x ranks must stay co-resident (<= 512)");
+    n /= nranks_local;
+    stride = n;
+  }
+  std::vector<void*> d(world), s(world);
+  for (int r = 0; r < world; ++r) {
+    d[r] = vp(data_ptrs[r]);
+    s[r] = vp(sig_ptrs[r]);
+  }
+  TORCH_CHECK(in.is_cuda() && in.device().index() == c10::hip::current_device(),
+              "xgmi_allreduce: tensors must live on the current device");
+  check(smdt_xgmi_allreduce(dcode(in), in.data_ptr(), out.data_ptr(), stride, n, (float)scale, d.data(), s.data(),
+                            world, (int)rank, (int)nranks_local, region_bytes, two_shot ? 1 : 0, (int)blocks,
+                            cur_stream()),
+        "xgmi_allreduce");
+}
+
 }  // namespace
 
 void register_blaslt(pybind11::module_& m);
@@ -479,6 +547,17 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   namespace py = pybind11;
   m.def("flash_fwd", &flash_fwd, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("scale"), py::arg("causal"),
         py::arg("out") = py::none(), py::arg("dropout_p") = 0.0, py::arg("seed") = 0, py::arg("offset") = 0);
+  m.def("ipc_malloc", &ipc_malloc, py::arg("bytes"), py::arg("uncached"));
+  m.def("ipc_free", &ipc_free);
+  m.def("ipc_get_handle", &ipc_get_handle);
+  m.def("ipc_open", &ipc_open);
+  m.def("ipc_close", &ipc_close);
+  m.def("ar_read_error", &ar_read_error);
+  m.def("ar_signal_bytes", &smdt_ar_signal_bytes);
+  m.def("ar_max_blocks", &smdt_ar_max_blocks);
+  m.def("xgmi_allreduce", &xgmi_allreduce, py::arg("input"), py::arg("out"), py::arg("data_ptrs"), py::arg("sig_ptrs"),
+        py::arg("rank"), py::arg("nranks_local"), py::arg("region_bytes"), py::arg("two_shot"), py::arg("blocks"),
+        py::arg("scale") = 1.0);
   m.def("flash_bwd", &flash_bwd, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("o"), py::arg("dout"),
         py::arg("lse"), py::arg("scale"), py::arg("causal"), py::arg("dq") = py::none(), py::arg("dk") = py::none(),
         py::arg("dv") = py::none(), py::arg("dropout_p") = 0.0, py::arg("seed") = 0, py::arg("offset") = 0);

@@ -102,4 +102,24 @@ struct SmdtWgradProblem {
 // main_grad targets of one call must not overlap.
 hipError_t smdt_wgrad_grouped(const SmdtWgradProblem* probs, int n, hipStream_t st);
 
+// xgmi_allreduce.hip: single-node all-reduce over HIP-IPC-mapped peer buffers.
+int smdt_ar_max_ranks();
+int smdt_ar_max_blocks();
+int64_t smdt_ar_signal_bytes();
+int smdt_ipc_handle_bytes();
+hipError_t smdt_ipc_malloc(int64_t bytes, int uncached, void** ptr);  // zero-filled
+hipError_t smdt_ipc_free(void* ptr);
+hipError_t smdt_ipc_get_handle(void* ptr, void* handle_out);
+hipError_t smdt_ipc_open(const void* handle, void** ptr);
+hipError_t smdt_ipc_close(void* ptr);
+hipError_t smdt_ar_read_error(void* sig, int* err);
+// out = scale * sum over ranks of in (n elements, n * esize % 16 == 0). data_ptrs / sig_ptrs: the
+// world ranks' staging (4 x region_bytes) and signal buffers. nranks_local > 1 = loopback: ranks
+// rank .. rank + nranks_local - 1 in one launch, in/out strided by io_stride elements per rank.
+// `blocks` is fixed per engine (every call of one engine must pass the same value).
+hipError_t smdt_xgmi_allreduce(int dtype, const void* in, void* out, int64_t io_stride, int64_t n, float scale,
+                               void* const* data_ptrs, void* const* sig_ptrs, int world, int rank,
+                               int nranks_local, int64_t region_bytes, int two_shot, int blocks,
+                               hipStream_t st);
+
 }  // extern "C"

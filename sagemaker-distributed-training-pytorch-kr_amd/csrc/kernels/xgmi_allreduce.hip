@@ -1,0 +1,350 @@
+// Single-node all-reduce over xGMI peer memory (SURVEY C2', C4, §5.8, §7.4 item 1): every rank
+// maps every other rank's staging buffer through HIP IPC and reads it directly, so ONE kernel
+// drives all 7 xGMI links of an MI355X at once instead of a ring's one link per direction.
+//
+// Reference context: the reference all-reduces DDP buckets and TP activations through NCCL /
+// SMDDP (`1_training_mnist_ddp/pytorch_mnist_ddp.py:87-104`, TP=4 all-reduces of 18.9 MB per
+// layer in NB3) and has no custom all-reduce; nothing here is modelled on code.
+//
+// Algorithms (chosen per call by the host):
+//   one-shot : stage my input into my region A, signal every peer, wait for every peer, then
+//              reduce the WHOLE tensor by reading all W staging regions (latency-optimal).
+//   two-shot : same staging + barrier, then rank r reduces only slice r of each block's range
+//              (a reduce-scatter through peer reads), publishes it in region B, a second barrier,
+//              and every rank gathers the W-1 other slices (each link carries 2/W of the message).
+// Both accumulate in fp32 in rank order 0..W-1, so every rank ends with bit-identical results
+// (TP replicas must stay identical).
+//
+// Cross-device visibility (MI355X_MICROARCH.md "visibility", system scope because the consumer is
+// another GPU): every staged byte is stored with sc0|sc1 (write-through) buffer stores, every wave
+// drains with s_waitcnt vmcnt(0), the block joins a barrier, and ONE lane per peer then stores the
+// epoch flag into that peer's signal buffer with a system-scope atomic store. Consumers poll their
+// own (uncached) signal words with system-scope relaxed loads and read peer data ONLY with sc0|sc1
+// buffer loads, which bypass both cache levels: no stale line can be hit.
+//
+// Reuse without an end barrier: staging is double-buffered on the parity of a per-block call
+// counter kept in device memory (hipGraph-replayable, no host-side epoch). The grid size is a
+// fixed property of an engine, so every block index takes part in every call and all counters
+// (hence all parities) advance together. A rank can be at most one call ahead of any peer (its
+// next barrier needs that peer's flag, which the peer only sets after finishing the previous
+// call in stream order), so it only ever overwrites the half a slower peer has finished reading.
+// Flags are compared with ">=" on monotonically increasing epochs for the same reason.
+//
+// Every spin is bounded: on timeout the block records a sticky error word in its own signal
+// buffer, fills its output range with NaN and exits, so a missing peer can never hang the GPU and
+// a failed reduction cannot pass silently (the host can also read the word back).
+//
+// Loopback mode (tests on ONE GPU): gridDim.y = W virtual ranks in ONE launch, rank = blockIdx.y,
+// in/out strided by `io_stride` per rank; the host keeps W x blocks small enough that every
+// workgroup is co-resident, so the barriers between them make progress.
+#include <stddef.h>
+
+#include "common.h"
+#include "launchers.h"
+
+namespace smdt {
+namespace ar {
+
+constexpr int kMaxRanks = 8;
+constexpr int kMaxBlocks = 256;
+constexpr int kThreads = 512;
+constexpr uint32_t kSpinLimit = 1u << 22;  // polls of an uncached word (~1 us each): seconds
+
+struct SignalBuf {
+  uint32_t flag[kMaxBlocks][kMaxRanks];  // flag[b][src]: written remotely by rank src's block b
+  uint32_t counter[kMaxBlocks];          // this rank's call counter per block (local only)
+  uint32_t error;                        // != 0: a spin timed out (sticky)
+  uint32_t pad[3];
+};
+
+struct Peers {
+  char* data[kMaxRanks];      // staging buffers: 4 regions of region_bytes (2 halves x {A, B})
+  SignalBuf* sig[kMaxRanks];  // signal buffers
+};
+
+using gu32 = __attribute__((address_space(1))) uint32_t;
+using u32x4 = __attribute__((ext_vector_type(4))) unsigned;
+
+__device__ __forceinline__ void store_sys(uint32_t* p, uint32_t v) {
+  __hip_atomic_store((gu32*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);  // global, never flat
+}
+__device__ __forceinline__ uint32_t load_sys(const uint32_t* p) {
+  return __hip_atomic_load((gu32*)const_cast<uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Poll my own flag word until it reaches `epoch`; give up when the sticky error is set or the
+// spin limit runs out (then set the error). Returns false on failure.
+__device__ __forceinline__ bool wait_ge(SignalBuf* me, const uint32_t* f, uint32_t epoch) {
+  for (uint32_t spins = 0;; ++spins) {
+    const uint32_t v = load_sys(f);
+    if ((int32_t)(v - epoch) >= 0) return true;
+    if ((spins & 255u) == 255u && load_sys(&me->error) != 0u) return false;
+    if (spins > kSpinLimit) {
+      store_sys(&me->error, 1u);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+}
+
+// Barrier among block b of every rank: publish `epoch` to every peer, then wait for every peer's
+// epoch. Each wave drains its own staging stores (vmcnt(0)) before the workgroup barrier that
+// orders all of them ahead of the flag stores.
+template <int W>
+__device__ __forceinline__ bool block_barrier(const Peers& P, int rank, int b, uint32_t epoch, int* s_ok) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const int t = threadIdx.x;
+  if (t < W) {
+    store_sys(&P.sig[t]->flag[b][rank], epoch);
+    if (!wait_ge(P.sig[rank], &P.sig[rank]->flag[b][t], epoch)) *s_ok = 0;
+  }
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps loads below
+  return *s_ok != 0;
+}
+
+constexpr int kSysAux = 1 | 16;  // sc0 | sc1: system coherent, bypasses L1 and L2
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+
+template <typename T> constexpr int E16 = 16 / (int)sizeof(T);
+
+template <typename T>
+__device__ __forceinline__ void acc16(float (&a)[E16<T>], u32x4 raw) {
+  if constexpr (sizeof(T) == 4) {
+    const f32x4 v = __builtin_bit_cast(f32x4, raw);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) a[j] += v[j];
+  } else {
+    const u16x8 v = __builtin_bit_cast(u16x8, raw);
+#pragma unroll
+    for (int j = 0; j < E16<T>; ++j) {
+      const unsigned short bits = v[j];
+      T x;
+      __builtin_memcpy(&x, &bits, 2);
+      a[j] += to_f32(x);
+    }
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ u32x4 pack16(const float (&a)[E16<T>], float scale) {
+  if constexpr (sizeof(T) == 4) {
+    f32x4 r;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) r[j] = a[j] * scale;
+    return __builtin_bit_cast(u32x4, r);
+  } else {
+    u16x8 v;
+#pragma unroll
+    for (int j = 0; j < E16<T>; ++j) {
+      const T x = from_f32<T>(a[j] * scale);
+      unsigned short bits;
+      __builtin_memcpy(&bits, &x, 2);
+      v[j] = bits;
+    }
+    return __builtin_bit_cast(u32x4, v);
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ void nan_fill(u32x4* __restrict__ out, int64_t v0, int64_t v1) {
+  uint32_t w = 0x7fc00000u;                                   // fp32 quiet NaN
+  if constexpr (std::is_same<T, bf16>::value) w = 0x7fc07fc0u;  // 2 x bf16 NaN
+  if constexpr (std::is_same<T, f16>::value) w = 0x7e007e00u;   // 2 x fp16 NaN
+  const u32x4 q = {w, w, w, w};
+  for (int64_t v = v0 + threadIdx.x; v < v1; v += kThreads) out[v] = q;
+}
+
+// out[v] = scale * sum_r region(r)[v] for v in [v0, v1), summed in rank order. kPublish also
+// stages the result (sc0|sc1) into my region B for the two-shot gather.
+template <typename T, int W, bool kPublish>
+__device__ __forceinline__ void reduce_range(const Peers& P, int64_t reg_off, uint32_t reg_bytes, int64_t v0,
+                                             int64_t v1, float scale, u32x4* __restrict__ out,
+                                             __amdgpu_buffer_rsrc_t pub) {
+  __amdgpu_buffer_rsrc_t src[W];
+#pragma unroll
+  for (int r = 0; r < W; ++r) src[r] = rsrc(P.data[r] + reg_off, reg_bytes);
+  for (int64_t v = v0 + threadIdx.x; v < v1; v += kThreads) {
+    u32x4 raw[W];
+#pragma unroll
+    for (int r = 0; r < W; ++r) raw[r] = __builtin_amdgcn_raw_buffer_load_b128(src[r], (int)(v * 16), 0, kSysAux);
+    float a[E16<T>];
+#pragma unroll
+    for (int j = 0; j < E16<T>; ++j) a[j] = 0.f;
+#pragma unroll
+    for (int r = 0; r < W; ++r) acc16<T>(a, raw[r]);
+    const u32x4 o = pack16<T>(a, scale);
+    out[v] = o;
+    if constexpr (kPublish) __builtin_amdgcn_raw_buffer_store_b128(o, pub, (int)(v * 16), 0, kSysAux);
+  }
+}
+
+template <typename T, int W, bool kTwoShot>
+__global__ __launch_bounds__(kThreads) void allreduce_kernel(Peers P, int rank0, const u32x4* __restrict__ in,
+                                                             u32x4* __restrict__ out, int64_t io_stride,
+                                                             int64_t nvec, int64_t chunk, int64_t region_bytes,
+                                                             float scale) {
+  __shared__ uint32_t s_counter;
+  __shared__ int s_ok;
+  const int b = blockIdx.x;
+  const int rank = rank0 + (int)blockIdx.y;
+  in += (int64_t)blockIdx.y * io_stride;
+  out += (int64_t)blockIdx.y * io_stride;
+  SignalBuf* me = P.sig[rank];
+  const int64_t v0 = (int64_t)b * chunk < nvec ? (int64_t)b * chunk : nvec;
+  const int64_t v1 = v0 + chunk < nvec ? v0 + chunk : nvec;
+  if (threadIdx.x == 0) {
+    s_counter = load_sys(&me->counter[b]);
+    s_ok = load_sys(&me->error) == 0u;
+  }
+  __syncthreads();
+  if (!s_ok) {  // a previous call failed: never wait on peers again (the host must rebuild)
+    nan_fill<T>(out, v0, v1);
+    return;
+  }
+  const uint32_t c = s_counter;
+  const uint32_t half = (c >> 1) & 1u;
+  const uint32_t rb = (uint32_t)region_bytes;
+  const int64_t offA = (int64_t)(2 * half) * region_bytes;
+  const int64_t offB = offA + region_bytes;
+
+  {  // 1) stage my input, write-through, so peers read it from memory
+    const auto mine = rsrc(P.data[rank] + offA, rb);
+    for (int64_t v = v0 + threadIdx.x; v < v1; v += kThreads)
+      __builtin_amdgcn_raw_buffer_store_b128(in[v], mine, (int)(v * 16), 0, kSysAux);
+  }
+  if (!block_barrier<W>(P, rank, b, c + 1, &s_ok)) {
+    nan_fill<T>(out, v0, v1);
+    return;
+  }
+
+  if constexpr (!kTwoShot) {
+    reduce_range<T, W, false>(P, offA, rb, v0, v1, scale, out, rsrc(nullptr, 0));
+  } else {
+    // 2) reduce-scatter: I own slice `rank` of this block's range; publish it in my region B
+    const int64_t sl = (v1 - v0 + W - 1) / W;
+    auto lo = [&](int r) { const int64_t x = v0 + (int64_t)r * sl; return x < v1 ? x : v1; };
+    auto hi = [&](int r) { const int64_t x = lo(r) + sl; return x < v1 ? x : v1; };
+    reduce_range<T, W, true>(P, offA, rb, lo(rank), hi(rank), scale, out, rsrc(P.data[rank] + offB, rb));
+    if (!block_barrier<W>(P, rank, b, c + 2, &s_ok)) {
+      nan_fill<T>(out, v0, v1);
+      return;
+    }
+    // 3) all-gather the other ranks' slices from their region B
+#pragma unroll
+    for (int r = 0; r < W; ++r) {
+      if (r == rank) continue;
+      const auto src = rsrc(P.data[r] + offB, rb);
+      const int64_t g1 = hi(r);
+      for (int64_t v = lo(r) + threadIdx.x; v < g1; v += kThreads)
+        out[v] = __builtin_amdgcn_raw_buffer_load_b128(src, (int)(v * 16), 0, kSysAux);
+    }
+  }
+  if (threadIdx.x == 0) store_sys(&me->counter[b], c + 2);
+}
+
+template <typename T, int W>
+hipError_t launch_w(const Peers& P, int rank0, int nranks_local, const void* in, void* out, int64_t io_stride,
+                    int64_t nvec, int blocks, int64_t region_bytes, float scale, int two_shot, hipStream_t st) {
+  const int64_t chunk = (nvec + blocks - 1) / blocks;
+  const dim3 grid(blocks, nranks_local);  // ALL blocks, also those whose range is empty
+  if (two_shot)
+    hipLaunchKernelGGL((allreduce_kernel<T, W, true>), grid, dim3(kThreads), 0, st, P, rank0,
+                       (const u32x4*)in, (u32x4*)out, io_stride, nvec, chunk, region_bytes, scale);
+  else
+    hipLaunchKernelGGL((allreduce_kernel<T, W, false>), grid, dim3(kThreads), 0, st, P, rank0,
+                       (const u32x4*)in, (u32x4*)out, io_stride, nvec, chunk, region_bytes, scale);
+  return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_t(const Peers& P, int world, int rank0, int nranks_local, const void* in, void* out,
+                    int64_t io_stride, int64_t nvec, int blocks, int64_t region_bytes, float scale,
+                    int two_shot, hipStream_t st) {
+  switch (world) {
+    case 2: return launch_w<T, 2>(P, rank0, nranks_local, in, out, io_stride, nvec, blocks, region_bytes, scale, two_shot, st);
+    case 4: return launch_w<T, 4>(P, rank0, nranks_local, in, out, io_stride, nvec, blocks, region_bytes, scale, two_shot, st);
+    case 8: return launch_w<T, 8>(P, rank0, nranks_local, in, out, io_stride, nvec, blocks, region_bytes, scale, two_shot, st);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace ar
+}  // namespace smdt
+
+using namespace smdt;
+
+extern "C" {
+
+int smdt_ar_max_ranks() { return ar::kMaxRanks; }
+int smdt_ar_max_blocks() { return ar::kMaxBlocks; }
+int64_t smdt_ar_signal_bytes() { return (int64_t)sizeof(ar::SignalBuf); }
+int smdt_ipc_handle_bytes() { return (int)sizeof(hipIpcMemHandle_t); }
+
+hipError_t smdt_ipc_malloc(int64_t bytes, int uncached, void** ptr) {
+  hipError_t e = uncached ? hipExtMallocWithFlags(ptr, (size_t)bytes, hipDeviceMallocUncached)
+                          : hipMalloc(ptr, (size_t)bytes);
+  if (e != hipSuccess) return e;
+  e = hipMemset(*ptr, 0, (size_t)bytes);
+  if (e != hipSuccess) return e;
+  return hipDeviceSynchronize();
+}
+
+hipError_t smdt_ipc_free(void* ptr) { return hipFree(ptr); }
+
+hipError_t smdt_ipc_get_handle(void* ptr, void* handle_out) {
+  hipIpcMemHandle_t h;
+  const hipError_t e = hipIpcGetMemHandle(&h, ptr);
+  if (e == hipSuccess) __builtin_memcpy(handle_out, &h, sizeof(h));
+  return e;
+}
+
+hipError_t smdt_ipc_open(const void* handle, void** ptr) {
+  hipIpcMemHandle_t h;
+  __builtin_memcpy(&h, handle, sizeof(h));
+  return hipIpcOpenMemHandle(ptr, h, hipIpcMemLazyEnablePeerAccess);
+}
+
+hipError_t smdt_ipc_close(void* ptr) { return hipIpcCloseMemHandle(ptr); }
+
+// Sticky error word of one signal buffer (0 = fine). Synchronous device -> host copy.
+hipError_t smdt_ar_read_error(void* sig, int* err) {
+  uint32_t v = 0;
+  const hipError_t e = hipMemcpy(&v, (char*)sig + offsetof(ar::SignalBuf, error), 4, hipMemcpyDeviceToHost);
+  *err = (int)v;
+  return e;
+}
+
+hipError_t smdt_xgmi_allreduce(int dtype, const void* in, void* out, int64_t io_stride, int64_t n, float scale,
+                               void* const* data_ptrs, void* const* sig_ptrs, int world, int rank,
+                               int nranks_local, int64_t region_bytes, int two_shot, int blocks,
+                               hipStream_t st) {
+  if (world < 2 || world > ar::kMaxRanks || rank < 0 || nranks_local < 1 || rank + nranks_local > world)
+    return hipErrorInvalidValue;
+  if (blocks < 1 || blocks > ar::kMaxBlocks) return hipErrorInvalidValue;
+  const int esz = dtype == 0 ? 4 : 2;
+  if (n <= 0 || (n * esz) % 16 != 0 || n * esz > region_bytes || region_bytes > (1ll << 31) - 16 ||
+      region_bytes % 16 != 0)
+    return hipErrorInvalidValue;
+  if ((((uintptr_t)in | (uintptr_t)out) & 15) != 0 || (io_stride * esz) % 16 != 0) return hipErrorInvalidValue;
+  ar::Peers P{};
+  for (int r = 0; r < world; ++r) {
+    if (!data_ptrs[r] || !sig_ptrs[r]) return hipErrorInvalidValue;
+    P.data[r] = (char*)data_ptrs[r];
+    P.sig[r] = (ar::SignalBuf*)sig_ptrs[r];
+  }
+  const int64_t nvec = n * esz / 16;
+  const int64_t vstride = io_stride * esz / 16;
+  switch (dtype) {
+    case 0: return ar::launch_t<float>(P, world, rank, nranks_local, in, out, vstride, nvec, blocks, region_bytes, scale, two_shot, st);
+    case 1: return ar::launch_t<bf16>(P, world, rank, nranks_local, in, out, vstride, nvec, blocks, region_bytes, scale, two_shot, st);
+    case 2: return ar::launch_t<f16>(P, world, rank, nranks_local, in, out, vstride, nvec, blocks, region_bytes, scale, two_shot, st);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // extern "C"

@@ -97,6 +97,12 @@ class DistributedDataParallel(nn.Module):
         self.sync_enabled = True
         backend = dist.get_backend(self.dp_group) if self.dp > 1 else "none"
         self.use_avg = average_in_collective and backend == "nccl"
+        # Buckets that fit its staging region are all-reduced by the xGMI IPC kernel on its own
+        # stream (comm/xgmi.py: SMDT_XGMI_ALLREDUCE=1, or a job that asked for backend "smddp").
+        self.xgmi = None
+        if self.dp > 1 and backend == "nccl" and not use_distributed_optimizer:
+            from ..comm import xgmi as _xgmi
+            self.xgmi = _xgmi.create_for_group(self.dp_group)
 
         params = [p for p in module.parameters() if p.requires_grad]
         seen = set()
@@ -257,7 +263,9 @@ class DistributedDataParallel(nn.Module):
                 view.div_(self.dp)
                 b.handle = dist.reduce_scatter_tensor(out, view, group=self.dp_group, async_op=True)
         else:
-            if self.use_avg:
+            if self.xgmi is not None and self.xgmi.fits(view):
+                b.handle = self.xgmi.all_reduce_async(view, op="avg")
+            elif self.use_avg:
                 b.handle = dist.all_reduce(view, op=dist.ReduceOp.AVG, group=self.dp_group, async_op=True)
             else:
                 view.div_(self.dp)

@@ -133,7 +133,19 @@ def initialize_model_parallel(tensor_model_parallel_size: int = 1, pipeline_mode
             st.embd_group, st.embd_ranks = ge, embd
     _STATE = st
     st.initialized = True
+    # xGMI IPC all-reduce for the TP group (SMDT_XGMI_ALLREDUCE=1; collective over the TP group)
+    if tp > 1:
+        from ..comm import xgmi
+        st.tp_xgmi = xgmi.create_for_group(st.tp_group)
     return st
+
+
+def xgmi_engine(group):
+    """The xGMI all-reduce engine bound to ``group`` (only the TP group has one), else None."""
+    st = _STATE
+    if st is None or group is None or group is not st.tp_group:
+        return None
+    return getattr(st, "tp_xgmi", None)
 
 
 def model_parallel_is_initialized() -> bool:

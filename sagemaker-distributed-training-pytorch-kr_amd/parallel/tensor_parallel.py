@@ -46,6 +46,10 @@ def _tp_group():
 def _all_reduce(x, group, async_op=False):
     if dist.get_world_size(group) == 1:
         return None
+    if not async_op:
+        eng = ps.xgmi_engine(group)  # xGMI IPC all-reduce (comm/xgmi.py) when enabled for the group
+        if eng is not None and eng.all_reduce(x):
+            return None
     return dist.all_reduce(x, group=group, async_op=async_op)
 
 
