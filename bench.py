@@ -166,8 +166,11 @@ def main():
         return losses
 
     tw = time.perf_counter()
-    for _ in range(a.warmup):
+    for i in range(a.warmup):
         train_step()
+        if rank == 0:  # progress line per warmup step (first-use GEMM tuning can take minutes)
+            print(f"[bench] warmup step {i + 1}/{a.warmup} done at {time.perf_counter() - tw:.1f}s",
+                  file=sys.stderr, flush=True)
     if rank == 0:
         print(f"[bench] warmup ({a.warmup} steps, incl. GEMM autotune) took {time.perf_counter() - tw:.1f}s",
               file=sys.stderr, flush=True)
