@@ -1,0 +1,115 @@
+"""Oxford-Pet DDP training throughput (BASELINE config #2 / NB2) on synthetic images.
+
+One training step is exactly the recipe's (`recipes/2_training_oxford-pet_ddp/pytorch_oxford_ddp.py`
+train loop, reference `2_training_oxford-pet_ddp/pytorch_oxford_ddp.py:268-330`): uint8 batch on the
+GPU -> batched GPU augmentation -> bf16 autocast channels-last forward -> fp32 CE -> backward with
+the framework's bucketed DDP reducer -> torch Adam (fused). Images are random uint8 of the
+reference's shape; weights are random init (no network for datasets / checkpoints).
+
+    python benchmarks/bench_vision.py --model swin_b --size 128 --batch 40      # NB2 per-GPU config
+    python benchmarks/bench_vision.py --model resnet50 --size 224 --batch 64    # recipe default
+    torchrun --nproc-per-node N --master-addr 127.0.0.1 benchmarks/bench_vision.py ...
+
+Prints one JSON line (rank 0): whole-job images/s, timed over --steps after --warmup, max over
+ranks. The reference published ~1,429 img/s for swin_b fp32 128x128 on 16x V100 (BASELINE.md,
+NB2:3333 corrected for its log_interval division).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+import torch.nn as nn  # noqa: E402
+
+from smdt_amd.comm import init_distributed  # noqa: E402
+from smdt_amd.data.image_folder import GpuAugment  # noqa: E402
+from smdt_amd.models import zoo  # noqa: E402
+from smdt_amd.parallel.distributed import DistributedDataParallel as DDP  # noqa: E402
+
+REF_IMG_S_PER_GPU = {"swin_b": 1429.0 / 16}  # NB2, 16x V100, fp32
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--model", default="swin_b")
+    p.add_argument("--size", type=int, default=128)
+    p.add_argument("--batch", type=int, default=40, help="per-GPU batch")
+    p.add_argument("--num-classes", type=int, default=37)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    p.add_argument("--channels-last", type=int, default=1)
+    a = p.parse_args()
+    rank, local, world, _ = init_distributed("nccl")
+    dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
+    torch.manual_seed(0)
+    torch.backends.cudnn.benchmark = True
+    model = zoo.create(a.model)
+    zoo.reset_classifier(model, a.num_classes)
+    mf = torch.channels_last if (a.channels_last and dev.type == "cuda") else torch.contiguous_format
+    model = DDP(model.to(dev, memory_format=mf), torch_compat=True)
+    crit = nn.CrossEntropyLoss()
+    opt = torch.optim.Adam(model.parameters(), lr=1e-4, fused=dev.type == "cuda")
+    aug = GpuAugment((a.size, a.size), train=True, channels_last=mf == torch.channels_last)
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(rank)
+    # uint8 source images slightly larger than the crop (decoding is the dataloader's job)
+    src = torch.randint(0, 256, (a.batch, 3, a.size + a.size // 4, a.size + a.size // 4), dtype=torch.uint8,
+                        device=dev)
+    tgt = torch.randint(0, a.num_classes, (a.batch,), device=dev)
+    bf16 = a.dtype == "bf16"
+
+    def step():
+        x = aug(src, gen)
+        opt.zero_grad(set_to_none=True)
+        with torch.autocast(device_type=dev.type, dtype=torch.bfloat16, enabled=bf16):
+            out = model(x)
+            loss = crit(out.float(), tgt)
+        loss.backward()
+        opt.step()
+        return loss
+
+    tw = time.perf_counter()
+    for i in range(a.warmup):
+        step()
+        if rank == 0:
+            print(f"[bench_vision] warmup {i + 1}/{a.warmup} at {time.perf_counter() - tw:.1f}s", file=sys.stderr,
+                  flush=True)
+    if dist.is_initialized():
+        dist.barrier()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        loss = step()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    if dist.is_initialized():
+        dist.barrier()
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+    if dist.is_initialized():
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    el = float(el.item())
+    ips = a.batch * world * a.steps / el
+    if rank == 0:
+        ref = REF_IMG_S_PER_GPU.get(a.model)
+        print(json.dumps({
+            "metric": "Oxford-Pet DDP train images/sec (whole job)", "value": round(ips, 1), "unit": "images/s",
+            "n_gpus": world, "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(1000 * el / a.steps, 3),
+            "dtype": a.dtype, "data": "synthetic uint8 images + GPU augmentation; random-init weights",
+            "config": {"model": a.model, "image": a.size, "batch_per_gpu": a.batch,
+                       "channels_last": bool(a.channels_last)},
+            "vs_reference_per_gpu": round(ips / world / ref, 2) if ref else None,
+            "final_loss": float(loss.item())}), flush=True)
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

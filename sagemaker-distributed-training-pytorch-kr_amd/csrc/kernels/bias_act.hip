@@ -13,18 +13,24 @@
 
 namespace smdt {
 
+// tanh(u) = 1 - 2 / (1 + 2^(2 u log2 e)): one v_exp_f32 + one v_rcp_f32 instead of libm tanhf,
+// whose ~20-instruction sequence made the bias-GeLU kernels VALU-bound at [16k, 4096]. Saturates
+// to +-1 for large |u| (exp2 -> inf / 0); absolute error ~1e-7, far below bf16 resolution.
+__device__ __forceinline__ float fast_tanh(float u) {
+  return 1.f - 2.f * __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(u * 2.8853900817779268f));
+}
 __device__ __forceinline__ float gelu_tanh(float x) {
   constexpr float k0 = 0.7978845608028654f;  // sqrt(2/pi)
   constexpr float k1 = 0.044715f;
   float u = k0 * (x + k1 * x * x * x);
-  return 0.5f * x * (1.f + tanhf(u));
+  return 0.5f * x * (1.f + fast_tanh(u));
 }
 __device__ __forceinline__ float gelu_tanh_grad(float x) {
   constexpr float k0 = 0.7978845608028654f;
   constexpr float k1 = 0.044715f;
   float x2 = x * x;
   float u = k0 * (x + k1 * x2 * x);
-  float t = tanhf(u);
+  float t = fast_tanh(u);
   return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k0 * (1.f + 3.f * k1 * x2);
 }
 __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.7071067811865476f)); }
@@ -34,6 +40,13 @@ __device__ __forceinline__ float gelu_erf_grad(float x) {
   return cdf + x * pdf;
 }
 __device__ __forceinline__ float silu(float x) { return x / (1.f + __expf(-x)); }
+
+template <int ACT>
+__device__ __forceinline__ float act_fwd(float z) { return ACT == 0 ? gelu_tanh(z) : gelu_erf(z); }
+template <int ACT>
+__device__ __forceinline__ float act_grad(float z) { return ACT == 0 ? gelu_tanh_grad(z) : gelu_erf_grad(z); }
+
+constexpr int kRows = 4;  // rows per thread whose loads are issued together (memory-level parallelism)
 
 // act: 0 = gelu_tanh, 1 = gelu_erf
 template <typename T, int ACT>
@@ -49,16 +62,22 @@ __global__ __launch_bounds__(256) void bias_act_fwd_kernel(const T* __restrict__
     for (int j = 0; j < 8; ++j) b[j] = 0.f;
   int64_t r0 = (int64_t)blockIdx.y * rows_per_slice;
   int64_t r1 = r0 + rows_per_slice < rows ? r0 + rows_per_slice : rows;
-  for (int64_t r = r0; r < r1; ++r) {
+  auto row_op = [&](int64_t r, const Raw8<T>& rx) {
     float v[8];
-    load_vec<T, 8>(x + r * N + ch * 8, v);
+    cvt_raw8<T>(rx, v);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      float z = v[j] + b[j];
-      v[j] = ACT == 0 ? gelu_tanh(z) : gelu_erf(z);
-    }
+    for (int j = 0; j < 8; ++j) v[j] = act_fwd<ACT>(v[j] + b[j]);
     store_vec<T, 8>(y + r * N + ch * 8, v);
+  };
+  int64_t r = r0;
+  for (; r + kRows <= r1; r += kRows) {
+    Raw8<T> rx[kRows];
+#pragma unroll
+    for (int u = 0; u < kRows; ++u) rx[u] = load_raw8(x + (r + u) * N + ch * 8);
+#pragma unroll
+    for (int u = 0; u < kRows; ++u) row_op(r + u, rx[u]);
   }
+  for (; r < r1; ++r) row_op(r, load_raw8(x + r * N + ch * 8));
 }
 
 template <typename T, int ACT>
@@ -79,19 +98,30 @@ __global__ __launch_bounds__(256) void bias_act_bwd_kernel(const T* __restrict__
     for (int j = 0; j < 8; ++j) b[j] = 0.f;
   int64_t r0 = (int64_t)blockIdx.y * rows_per_slice;
   int64_t r1 = r0 + rows_per_slice < rows ? r0 + rows_per_slice : rows;
-  for (int64_t r = r0; r < r1; ++r) {
+  auto row_op = [&](int64_t r, const Raw8<T>& rx, const Raw8<T>& rg) {
     float v[8], g[8];
-    load_vec<T, 8>(x + r * N + ch * 8, v);
-    load_vec<T, 8>(dy + r * N + ch * 8, g);
+    cvt_raw8<T>(rx, v);
+    cvt_raw8<T>(rg, g);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      float z = v[j] + b[j];
-      float d = g[j] * (ACT == 0 ? gelu_tanh_grad(z) : gelu_erf_grad(z));
+      const float d = g[j] * act_grad<ACT>(v[j] + b[j]);
       v[j] = d;
       acc[j] += to_f32(from_f32<T>(d));
     }
     store_vec<T, 8>(dx + r * N + ch * 8, v);
+  };
+  int64_t r = r0;
+  for (; r + kRows <= r1; r += kRows) {
+    Raw8<T> rx[kRows], rg[kRows];
+#pragma unroll
+    for (int u = 0; u < kRows; ++u) {
+      rx[u] = load_raw8(x + (r + u) * N + ch * 8);
+      rg[u] = load_raw8(dy + (r + u) * N + ch * 8);
+    }
+#pragma unroll
+    for (int u = 0; u < kRows; ++u) row_op(r + u, rx[u], rg[u]);
   }
+  for (; r < r1; ++r) row_op(r, load_raw8(x + r * N + ch * 8), load_raw8(dy + r * N + ch * 8));
   if (partials) store_vec<float, 8>(partials + (int64_t)blockIdx.y * N + ch * 8, acc);
 }
 

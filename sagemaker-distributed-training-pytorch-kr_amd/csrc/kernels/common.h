@@ -93,6 +93,42 @@ __device__ __forceinline__ void store_vec(T* __restrict__ p, const float (&in)[N
 // Elements per 16-byte access for T.
 template <typename T> constexpr int vec_elems() { return 16 / (int)sizeof(T); }
 
+// 8 elements of T kept in their raw (unconverted) form: one 16-byte register quad for 16-bit T,
+// two for fp32. Lets a kernel issue the next row's loads before converting the current row's
+// (software pipelining without paying the fp32 registers of the prefetched data).
+using u32x4 = __attribute__((ext_vector_type(4))) unsigned;
+template <typename T>
+struct Raw8 {
+  u32x4 v[sizeof(T) / 2];
+};
+template <typename T>
+__device__ __forceinline__ Raw8<T> load_raw8(const T* __restrict__ p) {
+  Raw8<T> r;
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(T) / 2); ++i) r.v[i] = reinterpret_cast<const u32x4*>(p)[i];
+  return r;
+}
+template <typename T>
+__device__ __forceinline__ void cvt_raw8(const Raw8<T>& r, float (&out)[8]) {
+  if constexpr (sizeof(T) == 2) {
+    const u16x8 v = __builtin_bit_cast(u16x8, r.v[0]);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const unsigned short bits = v[j];
+      T t;
+      __builtin_memcpy(&t, &bits, 2);
+      out[j] = to_f32(t);
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const f32x4 f = __builtin_bit_cast(f32x4, r.v[i]);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) out[4 * i + j] = f[j];
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // wave64 reductions. __shfl_xor lowers to DPP / ds_swizzle / ds_bpermute as the
 // compiler sees fit; all 64 lanes participate.

@@ -205,10 +205,43 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(LnBwdArgs a) {
     if (ch < nchunk) load_vec<W, 8>((const W*)a.gamma + ch * 8, g[c]);
   }
 
-  for (int64_t row = (int64_t)blockIdx.x * groups_per_block + group; row < a.rows;
-       row += (int64_t)gridDim.x * groups_per_block) {
-    const float mu = a.rms ? 0.f : a.mean[row];
-    const float rs = a.rstd[row];
+  // Software pipeline over the group's rows: the NEXT row's s / dy / ds_in (raw 16-byte vectors)
+  // and its mean / rstd are loaded before the current row's two cross-lane reductions, so every
+  // lane keeps two rows of loads in flight (one row in flight left this kernel at ~3 TB/s).
+  const T* __restrict__ sp = (const T*)a.s;
+  const T* __restrict__ dyp = (const T*)a.dy;
+  const T* __restrict__ dip = (const T*)a.ds_in;
+  const int64_t rstep = (int64_t)gridDim.x * groups_per_block;
+  Raw8<T> ns[C], ndy[C], ndi[C];
+#pragma unroll
+  for (int c = 0; c < C; ++c) ns[c] = ndy[c] = ndi[c] = Raw8<T>{};
+  float nmu = 0.f, nrs = 0.f;
+  auto fetch = [&](int64_t r) {
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      const int ch = c * G + tid_in_group;
+      if (ch < nchunk) {
+        ns[c] = load_raw8(sp + r * H + ch * 8);
+        ndy[c] = load_raw8(dyp + r * H + ch * 8);
+        if (has_dsin) ndi[c] = load_raw8(dip + r * H + ch * 8);
+      }
+    }
+    nmu = a.rms ? 0.f : a.mean[r];
+    nrs = a.rstd[r];
+  };
+  int64_t row = (int64_t)blockIdx.x * groups_per_block + group;
+  if (row < a.rows) fetch(row);
+  for (; row < a.rows; row += rstep) {
+    Raw8<T> cs[C], cdy[C], cdi[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      cs[c] = ns[c];
+      cdy[c] = ndy[c];
+      cdi[c] = ndi[c];
+    }
+    const float mu = nmu;
+    const float rs = nrs;
+    if (row + rstep < a.rows) fetch(row + rstep);
     float xh[C][8], dyg[C][8];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
@@ -216,8 +249,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(LnBwdArgs a) {
       int ch = c * G + tid_in_group;
       if (ch < nchunk) {
         float dy[8];
-        load_vec<T, 8>((const T*)a.s + row * H + ch * 8, xh[c]);
-        load_vec<T, 8>((const T*)a.dy + row * H + ch * 8, dy);
+        cvt_raw8<T>(cs[c], xh[c]);
+        cvt_raw8<T>(cdy[c], dy);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           xh[c][j] = (xh[c][j] - mu) * rs;
@@ -243,7 +276,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(LnBwdArgs a) {
         for (int j = 0; j < 8; ++j) ds[j] = rs * (dyg[c][j] - m1 - xh[c][j] * m2);
         if (has_dsin) {
           float e[8];
-          load_vec<T, 8>((const T*)a.ds_in + row * H + ch * 8, e);
+          cvt_raw8<T>(cdi[c], e);
 #pragma unroll
           for (int j = 0; j < 8; ++j) ds[j] += e[j];
         }

@@ -144,7 +144,7 @@ class DistributedDataParallel(nn.Module):
                 self.param_index[id(p)] = (off, n)
                 cur.params.append(p)
                 self.param_bucket[id(p)] = cur
-                off += n
+                off += _round_up(n, 16)  # every param view 16-element aligned (vector kernels need 16 B)
             if cur is not None:
                 cur.end = _round_up(off, align)
                 off = cur.end
@@ -155,9 +155,10 @@ class DistributedDataParallel(nn.Module):
         with torch.no_grad():
             for p in params:
                 o, n = self.param_index[id(p)]
-                self.param_data[o:o + n].copy_(p.data.view(-1))
-                p.data = self.param_data[o:o + n].view_as(p)
-                p.main_grad = self.grad_data[o:o + n].view_as(p)
+                pv = _dense_view(self.param_data[o:o + n], p)
+                pv.copy_(p.data)
+                p.data = pv
+                p.main_grad = _dense_view(self.grad_data[o:o + n], p)
                 p._smdt_grad_ready = self._on_grad_ready
         self._hooks = [p.register_post_accumulate_grad_hook(self._post_accumulate) for p in params]
         self.regions = self._region_ranges()
@@ -211,7 +212,8 @@ class DistributedDataParallel(nn.Module):
             return
         g = p.grad
         if g.data_ptr() != p.main_grad.data_ptr():
-            if g.is_cuda and g.dtype != p.main_grad.dtype and g.is_contiguous() and _ext.available():
+            if (g.is_cuda and g.dtype != p.main_grad.dtype and g.is_contiguous() and p.main_grad.is_contiguous()
+                    and _ext.available()):
                 # fused cast + accumulate (torch's mixed-dtype add is a slow generic path)
                 _ext.ext().cast_(g, p.main_grad, True)
             else:
@@ -345,6 +347,16 @@ class DistributedDataParallel(nn.Module):
 
     def load_state_dict(self, sd, strict=True):
         return self.module.load_state_dict(sd, strict=strict)
+
+
+def _dense_view(flat: torch.Tensor, p: torch.Tensor) -> torch.Tensor:
+    """``flat`` (p.numel() elements) viewed with p's shape AND strides: a channels-last conv weight
+    (dense but permuted strides) keeps its memory format inside the flat DDP buffers."""
+    dense_permuted = ((p.dim() == 4 and p.is_contiguous(memory_format=torch.channels_last))
+                      or (p.dim() == 5 and p.is_contiguous(memory_format=torch.channels_last_3d)))
+    if p.is_contiguous() or not dense_permuted:
+        return flat.view(p.shape)
+    return flat.as_strided(p.shape, p.stride())
 
 
 def _round_up(x, m):

@@ -41,3 +41,30 @@ def test_shifted_window_mask_blocks_cross_region_attention():
     assert b.shape == (4, 2, 49, 49)
     # the last window (bottom-right) mixes 4 regions after the roll: some pairs are masked
     assert (b[3] < -50).any() and not (b[0] < -50).any()
+
+
+def test_ddp_keeps_channels_last_weights():
+    """DDP's flat param / grad buffers keep a channels-last conv weight's strides (the Oxford recipe
+    moves the model to channels-last before wrapping it), and grads match an unwrapped copy."""
+    import torch
+    from smdt_amd.parallel.distributed import DistributedDataParallel as DDP
+
+    torch.manual_seed(0)
+
+    def net():
+        return torch.nn.Sequential(torch.nn.Conv2d(3, 8, 3), torch.nn.ReLU(), torch.nn.Flatten(),
+                                   torch.nn.Linear(8 * 6 * 6, 4))
+
+    m = net()
+    m2 = net()
+    m2.load_state_dict(m.state_dict())
+    m = m.to(memory_format=torch.channels_last)
+    d = DDP(m, torch_compat=True)
+    assert m[0].weight.is_contiguous(memory_format=torch.channels_last)
+    for a, b in zip(m.parameters(), m2.parameters()):
+        assert torch.equal(a, b)
+    x = torch.randn(2, 3, 8, 8).to(memory_format=torch.channels_last)
+    d(x).sum().backward()
+    m2(x.contiguous()).sum().backward()
+    for a, b in zip(m.parameters(), m2.parameters()):
+        torch.testing.assert_close(a.grad, b.grad)
