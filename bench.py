@@ -79,6 +79,15 @@ if os.path.exists(WGRAD_CACHE):
     os.environ.setdefault("SMDT_WGRAD_CACHE", WGRAD_CACHE)
 
 
+def model_label(a, vocab):
+    """The BASELINE config's name for the default shape; the explicit shape for any other."""
+    shape = f"{a.num_layers}L h{a.hidden_size} {a.num_attention_heads}A, vocab {vocab}"
+    if (a.num_layers, a.hidden_size, a.num_attention_heads, a.seq_length) == (24, 1024, 16, 1024):
+        return f"gpt2-345m ({shape})"
+    known = {(12, 768, 12): "gpt2-small", (32, 4096, 32): "gpt3-6.7b"}
+    return f"{known.get((a.num_layers, a.hidden_size, a.num_attention_heads), 'gpt')} ({shape}, seq {a.seq_length})"
+
+
 def enable_gemm_tuning(a, rank):
     """PyTorch TunableOp over torch's hipBLASLt / rocBLAS GEMMs.
 
@@ -212,7 +221,7 @@ def main():
             "vs_baseline": round(tps / ref_tps, 3),
             "dtype": "bf16",
             "data": "synthetic (random tokens, CodeParrot-shaped [mbs, 1025] int64; random-init weights)",
-            "config": {"model": "gpt2-345m (24L h1024 16A, vocab 50304)", "global_batch": global_batch,
+            "config": {"model": model_label(a, vocab), "global_batch": global_batch,
                        "seq_len": S, "micro_batch": mbs, "grad_accum": a.grad_accum,
                        "parallelism": f"tp{a.tp}pp{a.pp}dp{st.dp}" + ("+zero" if zero else ""),
                        "flash_attn": not a.no_flash, "hidden_dropout": a.hidden_dropout,
