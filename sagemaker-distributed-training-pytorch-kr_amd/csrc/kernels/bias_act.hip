@@ -186,12 +186,21 @@ __global__ __launch_bounds__(256) void col_sum_rows_kernel(const T* __restrict__
   const int64_t r0 = (int64_t)blockIdx.y * rows_per_slice;
   const int64_t r1 = r0 + rows_per_slice < rows ? r0 + rows_per_slice : rows;
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  for (int64_t r = r0; r < r1; ++r) {
+  auto add_row = [&](const Raw8<T>& raw) {
     float v[8];
-    load_vec<T, 8>(x + r * N + c, v);
+    cvt_raw8<T>(raw, v);
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[j] += v[j];
+  };
+  int64_t r = r0;
+  for (; r + kRows <= r1; r += kRows) {  // kRows loads in flight, rows still summed in order
+    Raw8<T> raw[kRows];
+#pragma unroll
+    for (int u = 0; u < kRows; ++u) raw[u] = load_raw8(x + (r + u) * N + c);
+#pragma unroll
+    for (int u = 0; u < kRows; ++u) add_row(raw[u]);
   }
+  for (; r < r1; ++r) add_row(load_raw8(x + r * N + c));
   float* o = part + (int64_t)blockIdx.y * N + c;
 #pragma unroll
   for (int j = 0; j < 8; ++j) o[j] = acc[j];

@@ -209,16 +209,18 @@ __device__ __forceinline__ void colsum_block(const float* __restrict__ part, int
   __shared__ float red[8][33];
   const int cl = threadIdx.x & 31, rg = threadIdx.x >> 5;
   const int col = blockIdx.x * 32 + cl;
-  float a0 = 0.f, a1 = 0.f;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;  // 4 independent chains: 4 loads in flight per lane
   if (col < ncols) {
     int r = rg;
-    for (; r + 8 < nrows; r += 16) {
+    for (; r + 24 < nrows; r += 32) {
       a0 += part[(int64_t)r * rs + col];
       a1 += part[(int64_t)(r + 8) * rs + col];
+      a2 += part[(int64_t)(r + 16) * rs + col];
+      a3 += part[(int64_t)(r + 24) * rs + col];
     }
-    if (r < nrows) a0 += part[(int64_t)r * rs + col];
+    for (; r < nrows; r += 8) a0 += part[(int64_t)r * rs + col];
   }
-  red[rg][cl] = a0 + a1;
+  red[rg][cl] = (a0 + a1) + (a2 + a3);
   __syncthreads();
   if (rg == 0 && col < ncols) {
     float s = 0.f;

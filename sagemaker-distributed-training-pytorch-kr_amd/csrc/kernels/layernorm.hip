@@ -13,8 +13,8 @@
 //    so dgamma / dbeta / dbias partial sums stay in registers across all rows handled by
 //    the wave and are flushed once per block -> [nblocks, H] fp32 partials, summed by a
 //    second tiny kernel (no float atomics; bitwise reproducible).
-//  * Dropout uses a stateless Philox counter keyed on (row, col), so the backward pass
-//    recomputes the mask instead of storing it.
+//  * Dropout uses a stateless keyed hash of (row, col) (see dropout_mask8), so the backward
+//    pass recomputes the mask instead of storing it.
 #include "common.h"
 #include "launchers.h"
 
@@ -66,17 +66,34 @@ __device__ __forceinline__ float group_sum(float v, float* scratch) {
   }
 }
 
-__device__ __forceinline__ void dropout_mask8(uint64_t seed, uint64_t offset, int64_t row, int H,
-                                              int col, float p, float (&keep)[8]) {
-  // Counter = linear element index / 4: one Philox call per 4 elements.
-  int64_t base = (row * (int64_t)H + col) >> 2;
-  float u[4];
-  philox_uniform4(seed, offset, (uint64_t)base, u);
+// Hidden-dropout keep mask: one murmur3-finalizer hash per element PAIR (counter = linear pair
+// index, keyed by (seed, offset)) and a 16-bit threshold per element; the realised drop rate
+// thr / 65536 is what the keep scale uses. About 6x less VALU per element than Philox-4x32-7,
+// which left the fused LN kernels VALU-bound; forward and backward re-derive the same mask.
+__device__ __forceinline__ uint32_t fmix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x85EBCA6Bu;
+  x ^= x >> 13;
+  x *= 0xC2B2AE35u;
+  return x ^ (x >> 16);
+}
+__device__ __forceinline__ uint32_t drop_thr16(float p) { return (uint32_t)(p * 65536.f + 0.5f); }
+__device__ __forceinline__ float drop_scale16(uint32_t thr) { return 65536.f / (65536.f - (float)thr); }
+__device__ __forceinline__ uint32_t ln_drop_key(uint64_t seed, uint64_t offset) {
+  return fmix32((uint32_t)seed ^ fmix32((uint32_t)(seed >> 32) + 0x9E3779B9u * ((uint32_t)offset + 1u)) ^
+                fmix32((uint32_t)(offset >> 32) + 0x27D4EB2Fu));
+}
+// keep[j] (1 / 0) for the 8 elements starting at (row, col), col % 8 == 0.
+__device__ __forceinline__ void dropout_mask8(uint32_t key, int64_t row, int H, int col, uint32_t thr,
+                                              float (&keep)[8]) {
+  const uint64_t pair = ((uint64_t)row * (uint64_t)H + (uint64_t)col) >> 1;
+  const uint32_t k = key ^ ((uint32_t)(pair >> 32) * 0x9E3779B1u);
 #pragma unroll
-  for (int j = 0; j < 4; ++j) keep[j] = u[j] >= p ? 1.f : 0.f;
-  philox_uniform4(seed, offset, (uint64_t)(base + 1), u);
-#pragma unroll
-  for (int j = 0; j < 4; ++j) keep[4 + j] = u[j] >= p ? 1.f : 0.f;
+  for (int j = 0; j < 4; ++j) {
+    const uint32_t h = fmix32(((uint32_t)pair + (uint32_t)j) ^ k);
+    keep[2 * j] = (h & 0xFFFFu) >= thr ? 1.f : 0.f;
+    keep[2 * j + 1] = (h >> 16) >= thr ? 1.f : 0.f;
+  }
 }
 
 template <typename T, typename W, int G, int C>
@@ -91,7 +108,9 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(LnFwdArgs a) {
   const bool has_bias = a.bias != nullptr;
   const bool drop = a.p_drop > 0.f;
   const bool write_s = a.s_out != nullptr;
-  const float keep_scale = drop ? 1.f / (1.f - a.p_drop) : 1.f;
+  const uint32_t dthr = drop ? drop_thr16(a.p_drop) : 0u;
+  const uint32_t dkey = drop ? ln_drop_key(a.seed, a.offset) : 0u;
+  const float keep_scale = drop ? drop_scale16(dthr) : 1.f;
 
   // gamma / beta / bias are row-invariant: load once.
   float g[C][8], b[C][8], bi[C][8];
@@ -123,7 +142,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(LnFwdArgs a) {
           for (int j = 0; j < 8; ++j) v[c][j] += bi[c][j];
         if (drop) {
           float keep[8];
-          dropout_mask8(a.seed, a.offset, row, H, ch * 8, a.p_drop, keep);
+          dropout_mask8(dkey, row, H, ch * 8, dthr, keep);
           for (int j = 0; j < 8; ++j) v[c][j] *= keep[j] * keep_scale;
         }
         if (has_res) {
@@ -191,7 +210,9 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(LnBwdArgs a) {
   const int group = threadIdx.x / G;
   const int nchunk = H / 8;
   const bool drop = a.p_drop > 0.f;
-  const float keep_scale = drop ? 1.f / (1.f - a.p_drop) : 1.f;
+  const uint32_t dthr = drop ? drop_thr16(a.p_drop) : 0u;
+  const uint32_t dkey = drop ? ln_drop_key(a.seed, a.offset) : 0u;
+  const float keep_scale = drop ? drop_scale16(dthr) : 1.f;
   const bool has_dsin = a.ds_in != nullptr;
   const bool separate_dx = a.dx_out != nullptr && a.dx_out != a.ds_out;
 
@@ -284,7 +305,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(LnBwdArgs a) {
         float dx[8];
         if (drop) {
           float keep[8];
-          dropout_mask8(a.seed, a.offset, row, H, ch * 8, a.p_drop, keep);
+          dropout_mask8(dkey, row, H, ch * 8, dthr, keep);
 #pragma unroll
           for (int j = 0; j < 8; ++j) dx[j] = ds[j] * keep[j] * keep_scale;
         } else {
