@@ -132,6 +132,39 @@ __device__ __forceinline__ f2s pexp2(float x0, float x1, float c, float b0, floa
   return {fexp2(fmaf(x0, c, -b0)), fexp2(fmaf(x1, c, -b1))};
 }
 
+// s_waitcnt with vmcnt = n and the other counters left alone (gfx9 encoding).
+template <int n>
+__device__ __forceinline__ void wait_vm() {
+  static_assert(n >= 0 && n < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((n & 15) | ((n >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+using lds_void = __attribute__((address_space(3))) void;
+
+// LDS-DMA of one 64-row x D bf16 tile into its swizzled Geo<D> image: wave-instruction i writes
+// 1 KB of LDS lane-linearly (rows 1024 / RB * i ..), so lane l lands at (row, slot l % CH) and
+// loads the global chunk whose swizzled position that is: chunk slot ^ f(row).
+template <int D>
+struct GldsTile {
+  static constexpr int kRowsPerInst = 1024 / Geo<D>::RB;             // 8 (D = 64) / 4 (D = 128)
+  static constexpr int kPerWave = kTile * Geo<D>::RB / 1024 / 4;      // 2 / 4 per wave (4 waves)
+  int off[kPerWave];  // element offset of this lane's chunk from the tile's first row
+  __device__ __forceinline__ void init(int w, int lane, int64_t row_stride) {
+#pragma unroll
+    for (int j = 0; j < kPerWave; ++j) {
+      const int i = w * kPerWave + j;
+      const int r = i * kRowsPerInst + lane / Geo<D>::CH;
+      const int c = (lane % Geo<D>::CH) ^ Geo<D>::f(r);
+      off[j] = (int)(r * row_stride) + 8 * c;
+    }
+  }
+  __device__ __forceinline__ void issue(const bf16* tile_base, char* img, int w) const {
+#pragma unroll
+    for (int j = 0; j < kPerWave; ++j)
+      __builtin_amdgcn_global_load_lds((const void*)(tile_base + off[j]),
+                                       (lds_void*)(img + (w * kPerWave + j) * 1024), 16, 0, 0);
+  }
+};
+
 // ---------------------------------------------------------------------------------------
 // Forward. Workgroup = 4 waves = 128 query rows of one (b, h); K/V streamed in 64-key tiles,
 // double-buffered.
@@ -144,7 +177,12 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void fwd_kernel(const bf16* _
                                                      Strides ks_, Strides vs, Strides os,
                                                      float scale, Drop drop) {
   using G = Geo<D>;
-  __shared__ __attribute__((aligned(16))) char lds[2 * 2 * G::TB];  // [buf][K|V]
+  // Three [K | V] tile buffers (separate objects: the compiler sees that the LDS-DMA into one does
+  // not alias the fragment reads of another, so it leaves the DMA queue alone).
+  // D = 64: three [K | V] buffers, two tiles in flight; D = 128 (twice the bytes): two buffers,
+  // so two workgroups still fit a CU's 160 KB of LDS.
+  constexpr int kBuf = D == 64 ? 3 : 2;
+  __shared__ __attribute__((aligned(16))) char L0[2 * G::TB], L1[2 * G::TB], L2[kBuf == 3 ? 2 * G::TB : 16];
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5;
   const int nqb = S / kBlockRows;
@@ -181,24 +219,28 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void fwd_kernel(const bf16* _
   const uint32_t shalf = (uint32_t)S >> 1;
   const uint32_t dblk = (uint32_t)(my_q >> 1) * shalf + 2u * h;  // block counter of key row 0
   const int dsh = 16 * (my_q & 1);                                // byte 2 (q & 1) + (k & 1)
-  Stage<D> sk, sv;
-  sk.init(ks_.ss);
-  sv.init(vs.ss);
-  sk.load(Kb);
-  sv.load(Vb);
-  sk.store(lds);
-  sv.store(lds + G::TB);
-  __syncthreads();
+  // K/V tiles stream global -> LDS by LDS-DMA (global_load_lds, no VGPR staging, no ds_write
+  // pass) through a 3-buffer ring with two tiles in flight: tile t waits only for its own DMA
+  // (counted vmcnt) and one raw s_barrier publishes it.
+  GldsTile<D> gk, gv;
+  gk.init(w, lane, ks_.ss);
+  gv.init(w, lane, vs.ss);
+  auto issue = [&](int t, char* img) {
+    gk.issue(Kb + (int64_t)t * kTile * ks_.ss, img, w);
+    gv.issue(Vb + (int64_t)t * kTile * vs.ss, img + G::TB, w);
+  };
+  constexpr int kPer = 2 * GldsTile<D>::kPerWave;  // DMA wave-instructions per tile and wave
+  issue(0, L0);
+  if constexpr (kBuf == 3) issue(ntiles > 1 ? 1 : 0, L1);
+  wait_vm<(kBuf - 2) * kPer>();
+  __builtin_amdgcn_s_barrier();
 
-  for (int t = 0; t < ntiles; ++t) {
+  // Every call issues exactly one tile's DMA (past the end it re-reads the last tile into a
+  // buffer nobody reads again), so the counted waits stay uniform.
+  auto tile = [&](int t, const char* kt, char* pre) {
     const int kb = t * kTile;
-    const bool more = t + 1 < ntiles;
-    const char* kt = lds + (t & 1) * 2 * G::TB;
     const char* vt = kt + G::TB;
-    if (more) {
-      sk.load(Kb + (int64_t)(kb + kTile) * ks_.ss);
-      sv.load(Vb + (int64_t)(kb + kTile) * vs.ss);
-    }
+    issue(t + kBuf - 1 < ntiles ? t + kBuf - 1 : ntiles - 1, pre);
     if (!CAUSAL || kb <= qw + 31) {
       // S^T tiles (log2 domain, minus m): rows = keys (registers), column = this lane's query.
       f32x16 st[2];
@@ -268,13 +310,23 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void fwd_kernel(const bf16* _
         }
       }
     }
-    if (more) {
-      char* nk = lds + ((t + 1) & 1) * 2 * G::TB;
-      sk.store(nk);
-      sv.store(nk + G::TB);
+    wait_vm<(kBuf - 2) * kPer>();  // tile t + 1 landed (t + 2 may still be in flight)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  };
+  if constexpr (kBuf == 3) {
+    for (int t = 0; t < ntiles; t += 3) {
+      tile(t, L0, L2);
+      if (t + 1 < ntiles) tile(t + 1, L1, L0);
+      if (t + 2 < ntiles) tile(t + 2, L2, L1);
     }
-    __syncthreads();
+  } else {
+    for (int t = 0; t < ntiles; t += 2) {
+      tile(t, L0, L1);
+      if (t + 1 < ntiles) tile(t + 1, L1, L0);
+    }
   }
+  wait_vm<0>();  // drain the trailing re-read before the workgroup's LDS is released
 
   // Epilogue: O[q, d] = O^T / l (x 1/(1-p) with dropout) ; lse = (m + log2 l) * ln 2.
   const float inv = l > 0.f ? (DROP ? drop.inv : 1.f) / l : 0.f;
@@ -511,7 +563,10 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dq_kernel(
     bf16* __restrict__ dQ, int B, int H, int Hkv, int S, Strides qs, Strides ks_, Strides vs,
     Strides dos, Strides dqs, float scale, Drop drop) {
   using G = Geo<D>;
-  __shared__ __attribute__((aligned(16))) char lds[2 * 2 * G::TB];
+  // D = 64: three [K | V] buffers, two tiles in flight; D = 128 (twice the bytes): two buffers,
+  // so two workgroups still fit a CU's 160 KB of LDS.
+  constexpr int kBuf = D == 64 ? 3 : 2;
+  __shared__ __attribute__((aligned(16))) char L0[2 * G::TB], L1[2 * G::TB], L2[kBuf == 3 ? 2 * G::TB : 16];
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5;
   const int nqb = S / kBlockRows;
@@ -546,24 +601,24 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dq_kernel(
 
   const int kend = CAUSAL ? (q0 + kBlockRows) : S;
   const int ntiles = kend / kTile;
-  Stage<D> sk, sv;
-  sk.init(ks_.ss);
-  sv.init(vs.ss);
-  sk.load(Kb);
-  sv.load(Vb);
-  sk.store(lds);
-  sv.store(lds + G::TB);
-  __syncthreads();
+  // K/V tiles by LDS-DMA through a 3-buffer ring, two tiles in flight (as in the forward).
+  GldsTile<D> gk, gv;
+  gk.init(w, lane, ks_.ss);
+  gv.init(w, lane, vs.ss);
+  auto issue = [&](int t, char* img) {
+    gk.issue(Kb + (int64_t)t * kTile * ks_.ss, img, w);
+    gv.issue(Vb + (int64_t)t * kTile * vs.ss, img + G::TB, w);
+  };
+  constexpr int kPer = 2 * GldsTile<D>::kPerWave;
+  issue(0, L0);
+  if constexpr (kBuf == 3) issue(ntiles > 1 ? 1 : 0, L1);
+  wait_vm<(kBuf - 2) * kPer>();
+  __builtin_amdgcn_s_barrier();
 
-  for (int t = 0; t < ntiles; ++t) {
+  auto tile = [&](int t, const char* kt, char* pre) {
     const int kb = t * kTile;
-    const bool more = t + 1 < ntiles;
-    const char* kt = lds + (t & 1) * 2 * G::TB;
     const char* vt = kt + G::TB;
-    if (more) {
-      sk.load(Kb + (int64_t)(kb + kTile) * ks_.ss);
-      sv.load(Vb + (int64_t)(kb + kTile) * vs.ss);
-    }
+    issue(t + kBuf - 1 < ntiles ? t + kBuf - 1 : ntiles - 1, pre);
 #pragma unroll
     for (int tt = 0; tt < 2; ++tt) {
       const int ksub = kb + 32 * tt;
@@ -600,13 +655,23 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dq_kernel(
         for (int dt = 0; dt < G::DT; ++dt) dq[dt] = mfma(fr.trf(kt, 32 * tt, s, dt), db, dq[dt]);
       }
     }
-    if (more) {
-      char* nk = lds + ((t + 1) & 1) * 2 * G::TB;
-      sk.store(nk);
-      sv.store(nk + G::TB);
+    wait_vm<(kBuf - 2) * kPer>();  // tile t + 1 landed (t + 2 may still be in flight)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  };
+  if constexpr (kBuf == 3) {
+    for (int t = 0; t < ntiles; t += 3) {
+      tile(t, L0, L2);
+      if (t + 1 < ntiles) tile(t + 1, L1, L0);
+      if (t + 2 < ntiles) tile(t + 2, L2, L1);
     }
-    __syncthreads();
+  } else {
+    for (int t = 0; t < ntiles; t += 2) {
+      tile(t, L0, L1);
+      if (t + 1 < ntiles) tile(t + 1, L1, L0);
+    }
   }
+  wait_vm<0>();
 
   bf16* dQb = dQ + b * dqs.sb + hq * dqs.sh + (int64_t)my_q * dqs.ss;
 #pragma unroll
