@@ -141,7 +141,9 @@ class XgmiAllReduce:
 
     # ------------------------------------------------------------------ helpers
     def _agree(self, ok: bool) -> bool:
-        dev = torch.device("cuda", torch.cuda.current_device())
+        # gloo groups (multi-process tests on one GPU) agree on the host; RCCL on the device
+        on_host = dist.get_backend(self.group) == "gloo"
+        dev = torch.device("cpu") if on_host else torch.device("cuda", torch.cuda.current_device())
         flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
         dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.group)
         return bool(flag.item())

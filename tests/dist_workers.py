@@ -257,3 +257,43 @@ def gpt_vpp_worker(rank, world, nmb):
     loss = torch.cat([r["loss"] for r in res]) if res else None
     dist.destroy_process_group()
     return loss, grads
+
+
+def xgmi_ipc_worker(rank, world, port, outdir):
+    """One rank of the cross-PROCESS test: real HIP-IPC handle exchange and peer mappings, all
+    ranks on cuda:0 (a gloo group carries the handles; the all-reduce itself is the kernel)."""
+    import os
+    import pickle
+    import traceback
+
+    import torch
+    from smdt_amd.comm import xgmi
+
+    os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "RANK": str(rank),
+                       "WORLD_SIZE": str(world)})
+    res = {"ok": [], "err": None, "error_word": None}
+    try:
+        import torch.distributed as dist
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        torch.cuda.set_device(0)
+        eng = xgmi.XgmiAllReduce(None, region_bytes=16 << 20, blocks=32, validate=False)
+        # one-shot (<= 4 MiB at world 2) and two-shot sizes in both dtypes
+        for n, dtype in ((4096, torch.float32), (1 << 21, torch.float32), (3 << 20, torch.bfloat16),
+                         (8192, torch.bfloat16)):
+            for rep in range(3):
+                base = torch.arange(n, device="cuda", dtype=torch.float32) % 97 + rep
+                x = (base + 1000.0 * rank).to(dtype)
+                ref = (base + 0.0).to(dtype).float()
+                for r in range(1, world):
+                    ref = ref + (base + 1000.0 * r).to(dtype).float()
+                ref = ref.to(dtype)
+                assert eng.all_reduce(x)
+                torch.cuda.synchronize()
+                res["ok"].append(bool(torch.equal(x, ref)))
+        res["error_word"] = eng.error()
+        eng.close()
+        dist.destroy_process_group()
+    except Exception:  # reported by the parent
+        res["err"] = traceback.format_exc()
+    with open(os.path.join(outdir, f"r{rank}.pkl"), "wb") as f:
+        pickle.dump(res, f)

@@ -87,3 +87,37 @@ def test_loopback_in_place_and_rejects_oversize():
         assert lb.errors() == [0] * 4
     finally:
         lb.close()
+
+
+@pytest.mark.gpu
+def test_cross_process_ipc_allreduce_world2():
+    import os
+    import pickle
+    import tempfile
+
+    import torch.multiprocessing as mp
+
+    import dist_workers as W
+    from _dist import free_port
+
+    world = 2
+    port = free_port()
+    with tempfile.TemporaryDirectory() as d:
+        ctx = mp.get_context("spawn")
+        procs = [ctx.Process(target=W.xgmi_ipc_worker, args=(r, world, port, d)) for r in range(world)]
+        for p in procs:
+            p.start()
+        for p in procs:
+            p.join(90)
+        for p in procs:
+            if p.is_alive():
+                p.kill()
+        out = []
+        for r in range(world):
+            path = os.path.join(d, f"r{r}.pkl")
+            assert os.path.exists(path), f"rank {r} wrote no result (exit {procs[r].exitcode})"
+            with open(path, "rb") as f:  # written by this test's own workers
+                out.append(pickle.load(f))
+    for r, res in enumerate(out):
+        assert res["err"] is None, f"rank {r}:\n{res['err']}"
+        assert res["error_word"] == 0 and all(res["ok"]) and len(res["ok"]) == 12, (r, res)
