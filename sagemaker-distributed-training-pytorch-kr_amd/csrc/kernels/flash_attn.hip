@@ -212,6 +212,7 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void fwd_kernel(const bf16* _
   for (int t = 0; t < G::DT; ++t) o[t] = zero16();
   // Reference max m (log2 domain) starts at 0 and moves lazily (see below); l = denominator.
   float m = 0.f, l = 0.f;
+  f32x16 negm = zero16();  // -m in all 16 registers: the score MFMAs' initial accumulator
 
   const int kend = CAUSAL ? (q0 + kBlockRows) : S;
   const int ntiles = kend / kTile;
@@ -246,9 +247,9 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void fwd_kernel(const bf16* _
       f32x16 st[2];
 #pragma unroll
       for (int tt = 0; tt < 2; ++tt) {
-        st[tt] = splat16(-m);
+        st[tt] = mfma(fr.rowf(kt, 32 * tt, 0), qf[0], negm);  // starts at -m: no per-tile splat
 #pragma unroll
-        for (int kk = 0; kk < G::KS; ++kk) st[tt] = mfma(fr.rowf(kt, 32 * tt, kk), qf[kk], st[tt]);
+        for (int kk = 1; kk < G::KS; ++kk) st[tt] = mfma(fr.rowf(kt, 32 * tt, kk), qf[kk], st[tt]);
       }
       if (CAUSAL && kb + kTile - 1 > qw) {  // diagonal tile for this wave: mask key > query
 #pragma unroll
@@ -276,6 +277,7 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void fwd_kernel(const bf16* _
 #pragma unroll
         for (int tt = 0; tt < 2; ++tt) st[tt] -= d;
         m += d;
+        negm = splat16(-m);
       }
       float rs0 = 0.f, rs1 = 0.f;  // two chains: the denominator uses the un-dropped p
 #pragma unroll
@@ -587,6 +589,9 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dq_kernel(
   const float lse2 = LSE[((int64_t)b * H + hq) * S + my_q] * kLog2e - (DROP ? drop.log2inv : 0.f);
   const float dl = DROP ? DELTA[((int64_t)b * H + hq) * S + my_q] * drop.keep
                         : DELTA[((int64_t)b * H + hq) * S + my_q];
+  // Row constants as the S / dP MFMAs' initial accumulators, register-resident for the whole
+  // loop (no per-subtile splat).
+  const f32x16 st0 = splat16(-lse2), dp0 = splat16(-dl);
   const float c2 = scale * kLog2e;
   const uint32_t dkey = DROP ? drop_key(drop, bh) : 0u;
   const uint32_t dblk = (uint32_t)(my_q >> 1) * ((uint32_t)S >> 1) + 2u * h;
@@ -624,9 +629,10 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dq_kernel(
       const int ksub = kb + 32 * tt;
       if (CAUSAL && ksub > qw + 31) continue;
       // row constants as the initial accumulators: S' = S log2(e) scale - lse, dP' = dP - delta
-      f32x16 st = splat16(opaque(-lse2)), dpt = splat16(opaque(-dl));
+      f32x16 st = mfma(fr.rowf(kt, 32 * tt, 0), qf[0], st0);
+      f32x16 dpt = mfma(fr.rowf(vt, 32 * tt, 0), dof[0], dp0);
 #pragma unroll
-      for (int kk = 0; kk < G::KS; ++kk) {
+      for (int kk = 1; kk < G::KS; ++kk) {
         st = mfma(fr.rowf(kt, 32 * tt, kk), qf[kk], st);
         dpt = mfma(fr.rowf(vt, 32 * tt, kk), dof[kk], dpt);
       }
