@@ -388,8 +388,10 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dkdv_kernel(
     bf16* __restrict__ dK, bf16* __restrict__ dV, int B, int H, int Hkv, int S, Strides qs,
     Strides ks_, Strides vs, Strides dos, Strides dks, Strides dvs, float scale, Drop drop) {
   using G = Geo<D>;
-  constexpr int BUF = 2 * G::TB + 2 * kTile * 4;  // Q | dO | lse | delta
-  __shared__ __attribute__((aligned(16))) char lds[2 * BUF];
+  constexpr int BUF = 2 * G::TB + 2 * kTile * 4;  // Q | dO | lse | delta (raw rows)
+  // D = 64: three stage buffers, two work items in flight; D = 128: two (LDS budget).
+  constexpr int kBuf = D == 64 ? 3 : 2;
+  __shared__ __attribute__((aligned(16))) char L0[BUF], L1[BUF], L2[kBuf == 3 ? BUF : 16];
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5;
   const int nkb = S / kBlockRows;
@@ -418,123 +420,141 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dkdv_kernel(
   const int ntiles = (S - qstart) / kTile;
   const int total = ntiles * group;
 
-  Stage<D> sq, sdo;
-  sq.init(qs.ss);
-  sdo.init(dos.ss);
-  float nl = 0.f, nd = 0.f;
-  // (query head, query tile) of a work item, kept as running counters: no integer division
-  // on the scalar unit inside the loop.
-  auto issue = [&](int ih, int iq) {
+  // Q / dO tiles and the tile's raw lse / delta rows stream in by LDS-DMA through a ring of kBuf
+  // stage buffers (waves 0 / 1 also move the 64 lse / 64 delta floats of the tile). Work items
+  // (query head, query tile) advance as running counters: no integer division in the loop.
+  GldsTile<D> gq, gdo;
+  gq.init(w, lane, qs.ss);
+  gdo.init(w, lane, dos.ss);
+  constexpr int kPer = 2 * GldsTile<D>::kPerWave;
+  int ih_n = 0, iq_n = 0, issued = 0;  // next work item to stream in
+  auto issue = [&](char* buf) {
+    // every call issues one item's DMA (past the end: the last item again, into a buffer nobody
+    // reads), so the counted waits stay uniform
+    const int ih = issued < total ? ih_n : group - 1, iq = issued < total ? iq_n : ntiles - 1;
     const int hq = hk * group + ih;
     const int qb = qstart + iq * kTile;
-    sq.load(Q + b * qs.sb + hq * qs.sh + (int64_t)qb * qs.ss);
-    sdo.load(dO + b * dos.sb + hq * dos.sh + (int64_t)qb * dos.ss);
-    if (threadIdx.x < kTile) {
-      const int64_t li = ((int64_t)b * H + hq) * S + qb + threadIdx.x;
-      // dropout: p' = p / (1 - p_drop) via the exponent, delta' = delta (1 - p_drop)
-      nl = LSE[li] * kLog2e - (DROP ? drop.log2inv : 0.f);
-      nd = DROP ? DELTA[li] * drop.keep : DELTA[li];
+    gq.issue(Q + b * qs.sb + hq * qs.sh + (int64_t)qb * qs.ss, buf, w);
+    gdo.issue(dO + b * dos.sb + hq * dos.sh + (int64_t)qb * dos.ss, buf + G::TB, w);
+    if (w < 2) {
+      const float* row = (w == 0 ? LSE : DELTA) + ((int64_t)b * H + hq) * S + qb;
+      __builtin_amdgcn_global_load_lds((const void*)(row + lane), (lds_void*)(buf + 2 * G::TB + w * kTile * 4), 4, 0, 0);
+    }
+    ++issued;
+    if (++iq_n == ntiles) {
+      iq_n = 0;
+      ++ih_n;
     }
   };
-  auto commit = [&](char* buf) {
-    sq.store(buf);
-    sdo.store(buf + G::TB);
-    if (threadIdx.x < kTile) {
-      reinterpret_cast<float*>(buf + 2 * G::TB)[threadIdx.x] = nl;
-      reinterpret_cast<float*>(buf + 2 * G::TB + kTile * 4)[threadIdx.x] = nd;
-    }
+  auto wait_next = [&]() {  // the next item's DMA has landed (a later one may still be in flight)
+    if (w < 2) wait_vm<(kBuf - 2) * (kPer + 1)>();
+    else wait_vm<(kBuf - 2) * kPer>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
   };
-  issue(0, 0);
-  commit(lds);
-  __syncthreads();
+  issue(L0);
+  if constexpr (kBuf == 3) issue(L1);
+  wait_next();
 
   const uint32_t shalf = (uint32_t)S >> 1;
   const int dsh = 8 * (my_key & 1);
   int ch = 0, cq = 0;  // current work item
-  for (int it = 0; it < total; ++it) {
+  auto item = [&](const char* buf, char* pre) {
     const int qb = qstart + cq * kTile;
-    const bool more = it + 1 < total;
-    const int nh = cq + 1 == ntiles ? ch + 1 : ch, nq = cq + 1 == ntiles ? 0 : cq + 1;
     const uint32_t dkey = DROP ? drop_key(drop, b * H + hk * group + ch) : 0u;
     const uint32_t dblk = (uint32_t)((qb + 4 * h) >> 1) * shalf + (uint32_t)(my_key >> 1);
-    const char* buf = lds + (it & 1) * BUF;
     const char* q_l = buf;
     const char* do_l = buf + G::TB;
     const float* lse_l = reinterpret_cast<const float*>(buf + 2 * G::TB);
     const float* del_l = lse_l + kTile;
-    if (more) issue(nh, nq);
-#pragma unroll
-    for (int qs2 = 0; qs2 < 2; ++qs2) {
-      const int qsub = qb + 32 * qs2;
-      if (CAUSAL && qsub + 31 < kw) continue;  // all queries precede all of this wave's keys
-      // S'[q, key] = Q . K'^T - lse ; dP'[q, key] = dO . V^T - delta  (key on lane, query rows
-      // in registers): the row constants are the accumulators' initial values.
-      f32x16 s, dp;
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int r0 = 32 * qs2 + 8 * g + 4 * h;  // 4 consecutive query rows of this group
-        const f32x4 lv = *reinterpret_cast<const f32x4*>(lse_l + r0);
-        const f32x4 dl = *reinterpret_cast<const f32x4*>(del_l + r0);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          s[4 * g + j] = -lv[j];
-          dp[4 * g + j] = DROP ? 0.f : -dl[j];  // dropout needs the raw dP (delta applied below)
-        }
-      }
-#pragma unroll
-      for (int kk = 0; kk < G::KS; ++kk) {
-        s = mfma(fr.rowf(q_l, 32 * qs2, kk), kf[kk], s);
-        dp = mfma(fr.rowf(do_l, 32 * qs2, kk), vf[kk], dp);
-      }
-      const bool diag = CAUSAL && qsub < kw + 31;
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int r0 = 32 * qs2 + 8 * g + 4 * h;
-        const f32x4 dlg = DROP ? *reinterpret_cast<const f32x4*>(del_l + r0) : f32x4{0.f, 0.f, 0.f, 0.f};
-        uint32_t hvq = 0u;
-#pragma unroll
-        for (int j = 0; j < 4; j += 2) {
-          const int i = 4 * g + j;
-          float p0 = fexp2(s[i]), p1 = fexp2(s[i + 1]);  // with dropout: p / (1 - p_drop)
-          if (diag) {
-            if (my_key > qb + r0 + j) p0 = 0.f;
-            if (my_key > qb + r0 + j + 1) p1 = 0.f;
+    issue(pre);
+  #pragma unroll
+      for (int qs2 = 0; qs2 < 2; ++qs2) {
+        const int qsub = qb + 32 * qs2;
+        if (CAUSAL && qsub + 31 < kw) continue;  // all queries precede all of this wave's keys
+        // S'[q, key] = Q . K'^T - lse ; dP'[q, key] = dO . V^T - delta  (key on lane, query rows
+        // in registers): the row constants are the accumulators' initial values.
+        f32x16 s, dp;
+  #pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int r0 = 32 * qs2 + 8 * g + 4 * h;  // 4 consecutive query rows of this group
+          const f32x4 lv = *reinterpret_cast<const f32x4*>(lse_l + r0);
+          const f32x4 dl = *reinterpret_cast<const f32x4*>(del_l + r0);
+  #pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            s[4 * g + j] = fmaf(-lv[j], kLog2e, DROP ? drop.log2inv : 0.f);  // -(lse log2e - log2 inv)
+            dp[4 * g + j] = DROP ? 0.f : -dl[j];  // dropout needs the raw dP (delta applied below)
           }
-          float d0 = dp[i], d1 = dp[i + 1];
-          if constexpr (DROP) {
-            // rows j, j+1 (queries 2i, 2i+1) share the hash of their 2x2 block; dropped
-            // entries: P' -> 0 for dV, dP -> 0, so dS = p' (keep ? dP : 0) - p' delta'
-            hvq = drop_hash(dblk + (uint32_t)((32 * qs2 + 8 * g + j) >> 1) * shalf, dkey);
-            const bool k0 = keep_byte(hvq, dsh, drop.thr), k1 = keep_byte(hvq, dsh + 16, drop.thr);
-            s[i] = k0 ? p0 : 0.f;
-            s[i + 1] = k1 ? p1 : 0.f;
-            d0 = (k0 ? d0 : 0.f) - dlg[j];
-            d1 = (k1 ? d1 : 0.f) - dlg[j + 1];
-          } else {
-            s[i] = p0;
-            s[i + 1] = p1;
+        }
+  #pragma unroll
+        for (int kk = 0; kk < G::KS; ++kk) {
+          s = mfma(fr.rowf(q_l, 32 * qs2, kk), kf[kk], s);
+          dp = mfma(fr.rowf(do_l, 32 * qs2, kk), vf[kk], dp);
+        }
+        const bool diag = CAUSAL && qsub < kw + 31;
+  #pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int r0 = 32 * qs2 + 8 * g + 4 * h;
+          const f32x4 dlg = DROP ? *reinterpret_cast<const f32x4*>(del_l + r0) * drop.keep : f32x4{0.f, 0.f, 0.f, 0.f};
+          uint32_t hvq = 0u;
+  #pragma unroll
+          for (int j = 0; j < 4; j += 2) {
+            const int i = 4 * g + j;
+            float p0 = fexp2(s[i]), p1 = fexp2(s[i + 1]);  // with dropout: p / (1 - p_drop)
+            if (diag) {
+              if (my_key > qb + r0 + j) p0 = 0.f;
+              if (my_key > qb + r0 + j + 1) p1 = 0.f;
+            }
+            float d0 = dp[i], d1 = dp[i + 1];
+            if constexpr (DROP) {
+              // rows j, j+1 (queries 2i, 2i+1) share the hash of their 2x2 block; dropped
+              // entries: P' -> 0 for dV, dP -> 0, so dS = p' (keep ? dP : 0) - p' delta'
+              hvq = drop_hash(dblk + (uint32_t)((32 * qs2 + 8 * g + j) >> 1) * shalf, dkey);
+              const bool k0 = keep_byte(hvq, dsh, drop.thr), k1 = keep_byte(hvq, dsh + 16, drop.thr);
+              s[i] = k0 ? p0 : 0.f;
+              s[i + 1] = k1 ? p1 : 0.f;
+              d0 = (k0 ? d0 : 0.f) - dlg[j];
+              d1 = (k1 ? d1 : 0.f) - dlg[j + 1];
+            } else {
+              s[i] = p0;
+              s[i + 1] = p1;
+            }
+            dp[i] = p0 * d0;  // dS
+            dp[i + 1] = p1 * d1;
           }
-          dp[i] = p0 * d0;  // dS
-          dp[i + 1] = p1 * d1;
+        }
+        // dV^T[d, key] += dO^T[d, q] . P[q, key] ; dK^T[d, key] += Q^T[d, q] . dS[q, key]
+  #pragma unroll
+        for (int st = 0; st < 2; ++st) {
+          const bf16x8 pb = pack8(s, st);
+          const bf16x8 db = pack8(dp, st);
+  #pragma unroll
+          for (int dt = 0; dt < G::DT; ++dt) {
+            dv[dt] = mfma(fr.trf(do_l, 32 * qs2, st, dt), pb, dv[dt]);
+            dk[dt] = mfma(fr.trf(q_l, 32 * qs2, st, dt), db, dk[dt]);
+          }
         }
       }
-      // dV^T[d, key] += dO^T[d, q] . P[q, key] ; dK^T[d, key] += Q^T[d, q] . dS[q, key]
-#pragma unroll
-      for (int st = 0; st < 2; ++st) {
-        const bf16x8 pb = pack8(s, st);
-        const bf16x8 db = pack8(dp, st);
-#pragma unroll
-        for (int dt = 0; dt < G::DT; ++dt) {
-          dv[dt] = mfma(fr.trf(do_l, 32 * qs2, st, dt), pb, dv[dt]);
-          dk[dt] = mfma(fr.trf(q_l, 32 * qs2, st, dt), db, dk[dt]);
-        }
-      }
+    if (++cq == ntiles) {
+      cq = 0;
+      ++ch;
     }
-    if (more) commit(lds + ((it + 1) & 1) * BUF);
-    __syncthreads();
-    ch = nh;
-    cq = nq;
+    wait_next();
+  };
+  if constexpr (kBuf == 3) {
+    for (int it = 0; it < total; it += 3) {
+      item(L0, L2);
+      if (it + 1 < total) item(L1, L0);
+      if (it + 2 < total) item(L2, L1);
+    }
+  } else {
+    for (int it = 0; it < total; it += 2) {
+      item(L0, L1);
+      if (it + 1 < total) item(L1, L0);
+    }
   }
+  wait_vm<0>();  // drain the trailing re-reads before the workgroup's LDS is released
+
 
   // dK[key, d] = scale * dK^T ; dV[key, d] = dV^T (key on lane, d in registers)
   bf16* dKb = dK + b * dks.sb + hk * dks.sh + (int64_t)my_key * dks.ss;
