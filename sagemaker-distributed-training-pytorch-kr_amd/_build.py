@@ -148,6 +148,38 @@ def build_runtime(verbose=False):
     return out
 
 
+SANITIZE_FLAGS = ["-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=address,undefined",
+                  "-fno-sanitize-recover=undefined"]
+
+
+def build_runtime_sanitized(out_dir, verbose=False):
+    """Build the host runtime with AddressSanitizer + UBSan into ``out_dir/_runtime.so``
+    (SURVEY §5.2 "address-sanitizer build target"). Host code only: GPU ASan is not used.
+
+    The module must be imported by a Python started with ``LD_PRELOAD`` of
+    ``sanitizer_preload()`` (``scripts/sanitize_runtime.py`` does this)."""
+    srcs = sorted(glob.glob(os.path.join(CSRC, "runtime", "*.cpp")))
+    os.makedirs(out_dir, exist_ok=True)
+    out = os.path.join(out_dir, "_runtime" + (sysconfig.get_config_var("EXT_SUFFIX") or ".so"))
+    if _newer(srcs + headers(), out):
+        inc = []
+        for d in _py_includes():
+            inc += ["-I", d]
+        _run([CXX, "-std=c++17", "-fPIC", "-shared", "-Wall"] + SANITIZE_FLAGS + ["-I", CSRC] + inc + srcs
+             + ["-o", out, "-lpthread"], verbose)
+    return out
+
+
+def sanitizer_preload():
+    """Runtime libraries that must be preloaded into the interpreter for a sanitized module."""
+    libs = []
+    for name in ("libasan.so", "libubsan.so"):
+        p = subprocess.run([CXX, f"-print-file-name={name}"], capture_output=True, text=True).stdout.strip()
+        if p and os.path.isabs(p) and os.path.exists(p):
+            libs.append(os.path.realpath(p))
+    return libs
+
+
 def build_all(verbose=False):
     rt = build_runtime(verbose)
     k = build_kernels(verbose)

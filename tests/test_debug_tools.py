@@ -99,3 +99,13 @@ def test_smddp_backend_name_works_unmodified():
     outs = run_workers(_smddp_worker, 2)
     for vals, be in outs:
         assert vals == [3.0] * 4 and be == "smddp"
+
+
+def test_host_runtime_under_asan_ubsan(tmp_path):
+    """the native host runtime (index builders, cpu_adam, supervisor) built with
+    -fsanitize=address,undefined and checked against NumPy twins (scripts/sanitize_runtime.py)."""
+    env = dict(os.environ, SMDT_ASAN_DIR=str(tmp_path / "asan"))
+    r = subprocess.run([sys.executable, os.path.join(HERE, "..", "scripts", "sanitize_runtime.py")],
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "runtime OK under ASan+UBSan" in r.stdout
