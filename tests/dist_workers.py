@@ -297,3 +297,23 @@ def xgmi_ipc_worker(rank, world, port, outdir):
         res["err"] = traceback.format_exc()
     with open(os.path.join(outdir, f"r{rank}.pkl"), "wb") as f:
         pickle.dump(res, f)
+
+
+def ulysses_worker(rank, world, nh, nkv, s=32, b=2, d=16):
+    """Context-parallel (Ulysses all-to-all) attention on this rank's sequence chunk: returns the
+    local output and the local q/k/v gradients for comparison with full-sequence attention."""
+    import torch.distributed as dist
+    from smdt_amd.parallel import context_parallel as cpar
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        g = torch.Generator().manual_seed(7)
+        q = torch.randn(s, b, nh, d, generator=g, dtype=torch.float64)
+        k = torch.randn(s, b, nkv, d, generator=g, dtype=torch.float64)
+        v = torch.randn(s, b, nkv, d, generator=g, dtype=torch.float64)
+        dy = torch.randn(s, b, nh, d, generator=g, dtype=torch.float64)
+        ql, kl, vl = (cpar.split_sequence(t).requires_grad_(True) for t in (q, k, v))
+        out = cpar.ulysses_attention(ql, kl, vl)
+        out.backward(cpar.split_sequence(dy))
+        return out.detach(), ql.grad, kl.grad, vl.grad
+    finally:
+        dist.destroy_process_group()

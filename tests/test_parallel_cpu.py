@@ -138,3 +138,23 @@ def test_deferred_wgrad_queue_semantics(monkeypatch):
     # ineligible shapes (tokens not a multiple of 32) run immediately
     tp._wgrad(b, torch.randn(33, 8), torch.randn(33, 8))
     assert ready[-1] is b and not q.items
+
+
+@pytest.mark.parametrize("cp,nh,nkv", [(2, 4, 4), (4, 8, 8), (4, 8, 2), (2, 6, 3)])
+def test_ulysses_context_parallel_matches_full_attention(cp, nh, nkv):
+    """P10 stretch: Ulysses all-to-all context parallelism over gloo reproduces full-sequence causal
+    attention (forward and q/k/v gradients, MHA and GQA) on every rank's sequence chunk."""
+    from smdt_amd.ops.functional import attention_ref
+    s, b, d = 32, 2, 16
+    res = run_workers(W.ulysses_worker, cp, nh, nkv, s, b, d)
+    g = torch.Generator().manual_seed(7)
+    q = torch.randn(s, b, nh, d, generator=g, dtype=torch.float64).requires_grad_(True)
+    k = torch.randn(s, b, nkv, d, generator=g, dtype=torch.float64).requires_grad_(True)
+    v = torch.randn(s, b, nkv, d, generator=g, dtype=torch.float64).requires_grad_(True)
+    dy = torch.randn(s, b, nh, d, generator=g, dtype=torch.float64)
+    ref = attention_ref(q.transpose(0, 1), k.transpose(0, 1), v.transpose(0, 1), d ** -0.5, True, 0.0, None)
+    ref = ref.transpose(0, 1)
+    ref.backward(dy)
+    for r, (out, dq, dk, dv) in enumerate(res):
+        for got, full in ((out, ref.detach()), (dq, q.grad), (dk, k.grad), (dv, v.grad)):
+            _close(got, full.chunk(cp, 0)[r], tol=1e-9)
