@@ -45,6 +45,7 @@ class Bucket:
     handle: object = None
     launched: bool = False
     ag_handle: object = None   # in-flight ZeRO param all-gather (overlap_param_gather)
+    alone: bool = False        # holds only the pipeline-tied word embedding
 
     @property
     def numel(self):
@@ -135,11 +136,19 @@ class DistributedDataParallel(nn.Module):
             cur: Optional[Bucket] = None
             for p in regions[key]:
                 n = p.numel()
+                # The pipeline-tied word embedding (first and last stage) sits alone in its bucket
+                # so both stages shard it identically under ZeRO: the embedding-group gradient
+                # all-reduce after the reduce-scatter then sums matching shards.
+                alone = bool(getattr(p, "shared_embedding", False)) and st.pp > 1
+                if cur is not None and cur.params and (alone or cur.alone):
+                    cur.end = _round_up(off, align)
+                    off = cur.end
+                    cur = None
                 if cur is None or (off - cur.start + n > bucket_size and cur.params):
                     if cur is not None:
                         cur.end = _round_up(off, align)
                         off = cur.end
-                    cur = Bucket(len(self.buckets), key, off, off)
+                    cur = Bucket(len(self.buckets), key, off, off, alone=alone)
                     self.buckets.append(cur)
                 self.param_index[id(p)] = (off, n)
                 cur.params.append(p)
@@ -231,7 +240,9 @@ class DistributedDataParallel(nn.Module):
 
     def _on_grad_ready(self, p):
         b = self.param_bucket.get(id(p))
-        if b is None:
+        if b is None or not self.sync_enabled:
+            # Gradients of no_sync micro-batches are only accumulated: readiness is counted for
+            # the synchronising pass alone (the counts are re-armed when sync is re-enabled).
             return
         # A parameter fed by several gradient paths (tied embedding: LM-head wgrad straight into
         # main_grad + the lookup's autograd accumulation) declares `_smdt_grad_contributions`;
@@ -273,14 +284,28 @@ class DistributedDataParallel(nn.Module):
                 view.div_(self.dp)
                 b.handle = dist.all_reduce(view, group=self.dp_group, async_op=True)
 
+    def set_sync_enabled(self, enabled: bool):
+        """Gate bucket launches (gradient accumulation / pipeline schedules).
+
+        Re-enabling sync first drains the deferred weight-gradient queue — GEMMs queued by the
+        no_sync micro-batches must land, and report readiness, while counting is still off — and
+        then re-arms every bucket's pending count, so the synchronising pass launches a bucket
+        only after all of ITS gradients were accumulated."""
+        enabled = bool(enabled)
+        if enabled and not self.sync_enabled:
+            from .tensor_parallel import flush_deferred_wgrad
+            flush_deferred_wgrad()
+            self._reset_pending()
+        self.sync_enabled = enabled
+
     @contextlib.contextmanager
     def no_sync(self):
         prev = self.sync_enabled
-        self.sync_enabled = False
+        self.set_sync_enabled(False)
         try:
             yield
         finally:
-            self.sync_enabled = prev
+            self.set_sync_enabled(prev)
 
     def start_grad_sync(self):
         from .tensor_parallel import flush_deferred_wgrad

@@ -150,24 +150,37 @@ def load_checkpoint(model, optimizer=None, scheduler=None, args=None, load_dir: 
     finetune = bool(getattr(args, "finetune", False)) if args is not None else False
     no_load_optim = bool(getattr(args, "no_load_optim", False)) if args is not None else False
     no_load_rng = bool(getattr(args, "no_load_rng", False)) if args is not None else False
+    optim_loaded = False
     if optimizer is not None and not (finetune or no_load_optim or release):
         if getattr(optimizer, "zero", False):
             st = ps.get_state()
             p = os.path.join(d, f"distrib_optim_dp{st.dp_rank:03d}.pt")
             if os.path.isfile(p):
                 optimizer.load_state_dict(torch.load(p, map_location="cpu", weights_only=True)["optimizer"])
+                optim_loaded = True
+            elif not bool(getattr(args, "no_save_optim", False)):
+                # a ZeRO checkpoint whose shard for this DP rank is missing cannot resume the
+                # optimizer: say so (the masters are refreshed from the loaded weights below)
+                print(f"WARNING: rank {dist.get_rank() if dist.is_initialized() else 0}: ZeRO optimizer shard "
+                      f"{p} not found; optimizer state restarts from the loaded weights", flush=True)
         elif "optimizer" in sd:
             optimizer.load_state_dict(sd["optimizer"])
+            optim_loaded = True
         if scheduler is not None and "opt_param_scheduler" in sd:
             scheduler.load_state_dict(sd["opt_param_scheduler"])
-    elif optimizer is not None:
-        # weights were loaded into the model: refresh fp32 masters from them
+    if optimizer is not None and not optim_loaded:
+        # The optimizer was built before the load, so its fp32 masters still hold the random-init
+        # weights: refresh them from the loaded model, or the first step writes them back.
         sync = getattr(optimizer, "reload_model_params", None)
         if sync is not None:
             sync()
     if "rng_state" in sd and not (finetune or no_load_rng or release):
         r = dict(sd["rng_state"])
-        load_rng_state_dict({k: v for k, v in r.items() if k in ("default", "tp", "torch_cpu", "torch_cuda")})
+        rs = {k: v for k, v in r.items() if k in ("default", "tp", "torch_cpu", "torch_cuda")}
+        if "numpy_keys" in r:  # data-side randomness (shuffles, augmentation) resumes too
+            import numpy as np
+            rs["numpy"] = ("MT19937", r["numpy_keys"].numpy().astype(np.uint32), int(r["numpy_pos"]), 0, 0.0)
+        load_rng_state_dict(rs)
     if args is not None and "args" in sd:
         for k in ("consumed_train_samples", "consumed_valid_samples"):
             if k in sd["args"]:

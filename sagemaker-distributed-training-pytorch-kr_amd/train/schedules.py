@@ -31,7 +31,10 @@ class _SyncGate:
 
     def set(self, enabled: bool):
         for d in self.ddps:
-            d.sync_enabled = enabled
+            if hasattr(d, "set_sync_enabled"):
+                d.set_sync_enabled(enabled)
+            else:
+                d.sync_enabled = enabled
 
 
 def forward_backward_no_pipelining(forward_step_func: Callable, data_iterator, model, num_microbatches: int,

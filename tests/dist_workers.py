@@ -317,3 +317,52 @@ def ulysses_worker(rank, world, nh, nkv, s=32, b=2, d=16):
         return out.detach(), ql.grad, kl.grad, vl.grad
     finally:
         dist.destroy_process_group()
+
+
+def gpt_layout_worker(rank, world, tp, pp, nmb, zero, defer=False, sp=False):
+    """DDP-wrapped tiny GPT under a TP x PP x DP layout with ``nmb`` micro-batches per step (gradient
+    accumulation for pp == 1, 1F1B otherwise): returns the reduced fp32 main_grad of every local
+    parameter. The global batch (4 sequences) is split over the DP ranks, so the reduced gradients
+    must equal the single-process full-batch gradients (bucket readiness across
+    no_sync micro-batches)."""
+    import torch.distributed as dist
+    from smdt_amd.comm import init_distributed
+    from smdt_amd.models.gpt import GPTModel, allreduce_word_embedding_grads
+    from smdt_amd.models.transformer import TransformerConfig
+    from smdt_amd.parallel import state as ps
+    from smdt_amd.parallel.distributed import DistributedDataParallel
+    from smdt_amd.train.schedules import get_forward_backward_func
+    init_distributed("gloo")
+    st = ps.initialize_model_parallel(tp, pp)
+    if defer:
+        from smdt_amd.parallel import tensor_parallel as tpm
+        tpm.DEFERRED_WGRAD.allow_cpu = True
+        tpm.DEFERRED_WGRAD.flush_tiles = 2
+    cfg = TransformerConfig(**{**TINY, "sequence_parallel": sp})
+    m = GPTModel(cfg, pre_process=st.is_first_stage(), post_process=st.is_last_stage())
+    ddp = DistributedDataParallel(m, bucket_size=6000, use_distributed_optimizer=zero)
+    tokens, labels = _batch()
+    per = 4 // st.dp
+    sl = slice(st.dp_rank * per, (st.dp_rank + 1) * per)
+    data = iter(list(zip(tokens[sl].chunk(nmb), labels[sl].chunk(nmb))))
+
+    def fstep(di, model):
+        t, lab = next(di)
+        o = model(t, None, None, labels=lab)
+        return o, (lambda x: (x.mean(), {"loss": x.detach()}))
+    ddp.zero_grad_buffer()
+    fb = get_forward_backward_func()
+    seq = 32 // tp if (sp and tp > 1) else 32
+    fb(fstep, data, ddp, nmb, tensor_shape=(seq, per // nmb, 64), dtype=torch.float32)
+    ddp.finish_grad_sync()
+    allreduce_word_embedding_grads(m)
+    full = ddp.grad_data.clone()
+    if zero and st.dp > 1:
+        for b in ddp.buckets:
+            s, e = ddp.shard_range(b)
+            dist.all_gather_into_tensor(full[b.start:b.end], ddp.grad_data[s:e].clone(), group=st.dp_group)
+    grads = {n: full[ddp.param_index[id(p)][0]:ddp.param_index[id(p)][0] + p.numel()].view_as(p).clone()
+             for n, p in m.named_parameters()}
+    meta = {"tp_rank": st.tp_rank, "pp_rank": st.pp_rank, "layer_offset": m.first_layer}
+    dist.destroy_process_group()
+    return None, grads, meta

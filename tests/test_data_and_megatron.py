@@ -109,3 +109,36 @@ def test_pretrain_gpt_checkpoint_and_resume(tmp_path):
     assert r2.returncode == 0, r2.stdout[-2000:] + r2.stderr[-3000:]
     out = r2.stdout.replace("  ", " ")
     assert "iteration 4/" in " ".join(out.split()) and "iteration 1/" not in " ".join(out.split())
+
+
+def test_load_without_optimizer_state_refreshes_masters(tmp_path):
+    """weights loaded from a --no-save-optim checkpoint must reach the fp32 masters
+    (the optimizer is built before the load), and the NumPy RNG state resumes too."""
+    import argparse
+    import numpy as np
+    from smdt_amd.models.gpt import GPTModel
+    from smdt_amd.models.transformer import TransformerConfig
+    from smdt_amd.optim.optimizer import MixedPrecisionAdam
+    from smdt_amd.parallel import state as ps
+    from smdt_amd.parallel.distributed import DistributedDataParallel
+    from smdt_amd.train import checkpointing as ck
+    ps.destroy_model_parallel()
+
+    def build(seed):
+        cfg = TransformerConfig(num_layers=1, hidden_size=32, num_attention_heads=2, max_position_embeddings=16,
+                                padded_vocab_size=64, params_dtype=torch.float32, seed=seed)
+        ddp = DistributedDataParallel(GPTModel(cfg))
+        return ddp, MixedPrecisionAdam(ddp, lr=1e-3)
+    ddp_a, opt_a = build(1)
+    args = argparse.Namespace(save=str(tmp_path), load=str(tmp_path), no_save_optim=True)
+    np.random.seed(123)
+    ck.save_checkpoint(5, ddp_a, opt_a, None, args)
+    want = np.random.rand(3)
+    ddp_b, opt_b = build(2)
+    assert not torch.equal(ddp_b.param_data, ddp_a.param_data)
+    np.random.seed(999)
+    assert ck.load_checkpoint(ddp_b, opt_b, None, args) == 5
+    torch.testing.assert_close(ddp_b.param_data, ddp_a.param_data)
+    for (s, e, _), mo in zip(opt_b.pieces, opt_b.master_off):
+        torch.testing.assert_close(opt_b.master[mo:mo + e - s], ddp_a.param_data[s:e].float())
+    np.testing.assert_array_equal(np.random.rand(3), want)

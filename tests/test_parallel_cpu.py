@@ -158,3 +158,18 @@ def test_ulysses_context_parallel_matches_full_attention(cp, nh, nkv):
     for r, (out, dq, dk, dv) in enumerate(res):
         for got, full in ((out, ref.detach()), (dq, q.grad), (dk, k.grad), (dv, v.grad)):
             _close(got, full.chunk(cp, 0)[r], tol=1e-9)
+
+
+@pytest.mark.parametrize("world,tp,pp,nmb,zero,defer,sp", [
+    (2, 1, 1, 2, False, False, False),   # dp2 x GA2 (no_sync micro-batch, then the sync pass)
+    (2, 1, 1, 2, True, True, False),     # dp2 x GA2, ZeRO reduce-scatter, deferred grouped wgrad
+    (4, 1, 2, 2, False, False, False),   # pp2 x dp2 1F1B with DDP buckets
+    (4, 1, 2, 2, True, False, False),    # pp2 x dp2 + ZeRO (tied embedding shards must line up)
+    (8, 2, 2, 2, True, True, True),      # the BASELINE layout tp2 pp2 dp2 + SP + ZeRO
+])
+def test_ddp_gradient_accumulation_matches_single_process(world, tp, pp, nmb, zero, defer, sp):
+    """Reduced gradients after multi-micro-batch steps under DDP equal the full-batch gradients."""
+    ref_loss, ref = W.gpt_reference()
+    outs = run_workers(W.gpt_layout_worker, world, tp, pp, nmb, zero, defer, sp)
+    for _, grads, meta in outs:
+        _check_tp_grads(ref, grads, meta, tp)
