@@ -13,6 +13,21 @@ against that 41 TFLOP/s/GPU, i.e. value / (41e12 * n_gpus / flops_per_token(345M
 
 Launch: ``python bench.py`` (1 GPU) or
 ``python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N``.
+
+Layouts (``--layout``):
+  * ``baseline`` (default) — BASELINE.json config #3, GPT-2 345M at TP=2 PP=2 DP=2 on 8 GPUs
+    (/root/reference/3_training_megatron-lm/megatron/arguments.py:1002-1005 sets TP/PP; the
+    reference's own run, NB3:399-428, used TP4 DP4). The model-parallel shape grows with N and is
+    then replicated: N=1 tp1pp1, N=2 tp2, N=4 tp2pp2, N=8 tp2pp2dp2, sequence parallelism whenever
+    tp > 1, ZeRO-1 across DP.
+  * ``dp`` — DP-N + ZeRO-1 (every GPU holds the whole model).
+  ``--tp/--pp`` override either layout.
+
+Scaling is WEAK: every GPU processes ``--seqs-per-gpu`` (32) sequences of 1024 tokens per step
+at every N, so global batch = 32 N. A DP replica (tp x pp GPUs) therefore runs 32 tp pp sequences
+per step: with pp == 1 as one micro-batch (capped at 64 sequences, else gradient accumulation),
+with pp > 1 as micro-batches of 16 — 8 micro-batches at tp2pp2 keep the 1F1B bubble
+(pp - 1) / m at 12.5 %.
 """
 from __future__ import annotations
 
@@ -28,7 +43,7 @@ import torch.distributed as dist
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 from smdt_amd.comm import init_distributed  # noqa: E402
-from smdt_amd.models.gpt import GPTModel, gpt_flops_per_token, pad_vocab_size  # noqa: E402
+from smdt_amd.models.gpt import GPTModel, allreduce_word_embedding_grads, gpt_flops_per_token, pad_vocab_size  # noqa: E402
 from smdt_amd.models.transformer import TransformerConfig  # noqa: E402
 from smdt_amd.optim.optimizer import MixedPrecisionAdam  # noqa: E402
 from smdt_amd.optim.lr_scheduler import OptimizerParamScheduler  # noqa: E402
@@ -45,13 +60,16 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--tp", type=int, default=1)
-    p.add_argument("--pp", type=int, default=1)
-    # 32 x 1024 tokens per GPU per micro-batch: the 288 GB of HBM holds it without recompute, it
-    # measured +5 % tokens/s over 16 on one MI355X (profiles/r1_mbs/) and halves the gradient
-    # bytes synchronised per token at N > 1.
-    p.add_argument("--micro-batch-size", type=int, default=32)
-    p.add_argument("--grad-accum", type=int, default=1, help="micro-batches per step per DP rank")
+    p.add_argument("--layout", choices=["baseline", "dp"], default="baseline")
+    p.add_argument("--tp", type=int, default=None)
+    p.add_argument("--pp", type=int, default=None)
+    p.add_argument("--sequence-parallel", type=int, default=None, help="default: on when tp > 1")
+    # 32 x 1024 tokens per GPU per step: the 288 GB of HBM holds it without recompute, it measured
+    # +5 % tokens/s over 16 on one MI355X (profiles/r1_mbs/) and halves the gradient bytes
+    # synchronised per token at N > 1.
+    p.add_argument("--seqs-per-gpu", type=int, default=32, help="sequences per GPU per step (weak scaling)")
+    p.add_argument("--micro-batch-size", type=int, default=None)
+    p.add_argument("--grad-accum", type=int, default=None, help="micro-batches per step per DP rank")
     p.add_argument("--seq-length", type=int, default=1024)
     p.add_argument("--num-layers", type=int, default=24)
     p.add_argument("--hidden-size", type=int, default=1024)
@@ -120,12 +138,35 @@ def enable_gemm_tuning(a, rank):
         return "unavailable"
 
 
+BASELINE_LAYOUT = {1: (1, 1), 2: (2, 1), 4: (2, 2), 8: (2, 2)}  # N -> (tp, pp); dp = N / (tp pp)
+
+
+def choose_layout(a, world):
+    """(tp, pp, sp, micro_batch, grad_accum) for ``world`` GPUs (see the module docstring)."""
+    tp, pp = BASELINE_LAYOUT.get(world, (1, 1)) if a.layout == "baseline" else (1, 1)
+    tp = a.tp if a.tp is not None else tp
+    pp = a.pp if a.pp is not None else pp
+    if world % (tp * pp):
+        raise SystemExit(f"[bench] world {world} is not divisible by tp {tp} x pp {pp}")
+    sp = bool(a.sequence_parallel) if a.sequence_parallel is not None else tp > 1
+    replica = a.seqs_per_gpu * tp * pp          # sequences per DP replica per step
+    if a.micro_batch_size is not None:
+        mbs = a.micro_batch_size
+    elif pp == 1:
+        mbs = min(replica, 64)
+    else:
+        mbs = max(1, min(16, replica // (4 * pp)))  # >= 4 pp micro-batches: bubble <= 20 %
+    ga = a.grad_accum if a.grad_accum is not None else max(1, replica // mbs)
+    return tp, pp, sp, mbs, ga
+
+
 def main():
     a = parse()
     rank, local, world, backend = init_distributed("nccl")
     if world != a.gpus and rank == 0:
         print(f"[bench] note: --gpus {a.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
     n = world
+    a.tp, a.pp, sp, a.micro_batch_size, a.grad_accum = choose_layout(a, world)
     st = ps.initialize_model_parallel(a.tp, a.pp)
     model_parallel_seed(1234)
     tuned = enable_gemm_tuning(a, rank)
@@ -135,7 +176,7 @@ def main():
                             num_attention_heads=a.num_attention_heads, max_position_embeddings=a.seq_length,
                             padded_vocab_size=vocab, hidden_dropout=a.hidden_dropout,
                             attention_dropout=a.attention_dropout, params_dtype=torch.bfloat16,
-                            sequence_parallel=a.tp > 1, use_flash_attn=not a.no_flash,
+                            sequence_parallel=sp and a.tp > 1, use_flash_attn=not a.no_flash,
                             recompute_granularity="full" if a.recompute == "full" else None,
                             recompute_method="uniform" if a.recompute == "full" else None)
     model = GPTModel(cfg, pre_process=st.is_first_stage(), post_process=st.is_last_stage(), device=dev)
@@ -173,6 +214,7 @@ def main():
         ddp.zero_grad_buffer()
         losses = fb(forward_step, it, ddp, a.grad_accum, tensor_shape=shape, dtype=torch.bfloat16)
         ddp.finish_grad_sync()
+        allreduce_word_embedding_grads(model)   # tied embedding: first + last pipeline stage
         lr = sched.step(1)
         opt.step(lr)
         return losses
@@ -207,9 +249,13 @@ def main():
     tps = tokens_per_step * a.steps / elapsed
     fpt = gpt_flops_per_token(cfg, S, recompute=False)
     ref_tps = REF_TFLOPS_PER_GPU * n / fpt
-    loss_val = None
+    # the loss lives on the last pipeline stage: share it so rank 0 can report it
+    lv = torch.zeros(1, dtype=torch.float32, device=dev)
     if last:
-        loss_val = float(torch.stack([d["lm loss"] for d in last]).mean().item())
+        lv[0] = torch.stack([d["lm loss"] for d in last]).float().mean()
+    if dist.is_initialized() and st.pp > 1:
+        dist.all_reduce(lv, op=dist.ReduceOp.MAX)
+    loss_val = float(lv.item())
     if rank == 0:
         rec = {
             "metric": "tokens/sec (whole node) GPT-2 345M pretrain",
@@ -226,7 +272,9 @@ def main():
             "data": "synthetic (random tokens, CodeParrot-shaped [mbs, 1025] int64; random-init weights)",
             "config": {"model": model_label(a, vocab), "global_batch": global_batch,
                        "seq_len": S, "micro_batch": mbs, "grad_accum": a.grad_accum,
-                       "parallelism": f"tp{a.tp}pp{a.pp}dp{st.dp}" + ("+zero" if zero else ""),
+                       "parallelism": f"tp{a.tp}pp{a.pp}dp{st.dp}" + ("+sp" if cfg.sequence_parallel else "")
+                       + ("+zero1" if zero else ""),
+                       "layout": a.layout, "scaling_note": f"weak: {a.seqs_per_gpu} seqs x {S} tokens per GPU per step",
                        "flash_attn": not a.no_flash, "hidden_dropout": a.hidden_dropout,
                        "attention_dropout": a.attention_dropout, "recompute": a.recompute,
                        "gemm_autotune": tuned},
