@@ -50,7 +50,7 @@ from smdt_amd.optim.lr_scheduler import OptimizerParamScheduler  # noqa: E402
 from smdt_amd.parallel import state as ps  # noqa: E402
 from smdt_amd.parallel.distributed import DistributedDataParallel  # noqa: E402
 from smdt_amd.parallel.random import model_parallel_seed  # noqa: E402
-from smdt_amd.train.schedules import get_forward_backward_func  # noqa: E402
+from smdt_amd.train.schedules import configure_p2p, get_forward_backward_func  # noqa: E402
 
 REF_TFLOPS_PER_GPU = 41.0e12  # reference GPT-2-small on A100 (derived)
 
@@ -207,6 +207,7 @@ def main():
             return loss, {"lm loss": loss.detach()}
         return out, loss_func
 
+    configure_p2p(overlap=True)   # pipeline receives are waited for at their consumer
     fb = get_forward_backward_func()
     shape = (S // a.tp if cfg.sequence_parallel else S, mbs, cfg.hidden_size)
 

@@ -378,23 +378,195 @@ class LinearWithGradAccumulationAndAsyncCommunication(torch.autograd.Function):
         g2 = g.reshape(-1, g.shape[-1])
         t2 = total.reshape(-1, total.shape[-1])
         dw = _wgrad(weight, g2, t2)
-        db = None
-        if ctx.has_bias:
-            tgt = SF.grad_accumulate_target(ctx.bias_p)
-            if tgt is not None and g2.is_contiguous() and g2.shape[-1] % 8 == 0:
-                _ext.ext().bias_grad(g2, tgt, True)  # column sums accumulated into fp32 main_grad
-                ctx.bias_p._smdt_grad_ready(ctx.bias_p)
-            else:
-                db = g2.sum(0)
+        db = _bias_grad(ctx.bias_p, g2) if ctx.has_bias else None
         if handle is not None:
+            # the collective is in flight: run the queued weight-gradient GEMMs beside it
+            DEFERRED_WGRAD.flush()
             handle.wait()
         return gi_out, dw, db, None, None
 
 
 def linear_with_grad_accumulation_and_async_allreduce(x, weight, bias, sequence_parallel=False,
                                                       async_grad_allreduce=False):
+    if sequence_parallel and _TP_OVERLAP and _tp_size() > 1:
+        return _ColumnSPLinear.apply(x, weight, bias)
     return LinearWithGradAccumulationAndAsyncCommunication.apply(x, weight, bias, sequence_parallel,
                                                                  async_grad_allreduce)
+
+
+# --------------------------------------------------------------------------------------------
+# Sequence-parallel linears with the TP collective fused into the GEMM as a ring (collective
+# matmul): the all-gather / reduce-scatter moves one sequence chunk per step over RCCL p2p while
+# the GEMM of the previous / next chunk runs, instead of a monolithic collective followed by a
+# monolithic GEMM. On MI355X the TP pair talks over ONE xGMI link (~64-77 GB/s per direction),
+# which at GPT-2 345M shapes moves a layer's activations slower than the MFMA cores consume them,
+# so every byte in flight must have a GEMM beside it. Backward collectives additionally drain the
+# deferred weight-gradient queue before they are waited for (Megatron's "launch dgrad collective
+# -> wgrad GEMM -> wait", arguments.py:837-842, with the grouped MFMA wgrad as the overlapped work).
+
+_TP_OVERLAP = os.environ.get("SMDT_TP_OVERLAP", "1") == "1"
+
+
+def _ring(group):
+    ws = dist.get_world_size(group)
+    r = dist.get_rank(group)
+    ranks = dist.get_process_group_ranks(group)
+    return ws, r, ranks[(r + 1) % ws], ranks[(r - 1) % ws]
+
+
+def _exchange(send, recv, nxt, prv, group):
+    """One ring step: send to next and receive from prev in ONE p2p group (matched per peer in
+    issue order, so a 2-rank ring with next == prev cannot deadlock)."""
+    return dist.batch_isend_irecv([dist.P2POp(dist.isend, send, nxt, group),
+                                   dist.P2POp(dist.irecv, recv, prv, group)])
+
+
+def _mm_into(dst, a, w, bias=None):
+    """dst[..., o] = a[..., k] @ w[o, k]^T (+ bias) written in place (hipBLASLt out= GEMM)."""
+    a2 = a.reshape(-1, a.shape[-1])
+    d2 = dst.view(-1, dst.shape[-1])
+    if bias is not None:
+        torch.addmm(bias, a2, w.t(), out=d2)
+    else:
+        torch.mm(a2, w.t(), out=d2)
+
+
+def ag_ring(x, group, chunk_fn=None, before_last_wait=None):
+    """All-gather ``x`` along dim 0 over ``group`` as a ring; ``chunk_fn(c, chunk)`` runs on chunk c
+    as soon as it is resident, while the next chunk is in flight. Returns the gathered tensor."""
+    ws, r, nxt, prv = _ring(group)
+    n = x.shape[0]
+    total = x.new_empty((n * ws,) + tuple(x.shape[1:]))
+    total[r * n:(r + 1) * n].copy_(x)
+    for s in range(ws):
+        c = (r - s) % ws
+        works = None
+        if s < ws - 1:
+            nc = (c - 1) % ws
+            works = _exchange(total[c * n:(c + 1) * n], total[nc * n:(nc + 1) * n], nxt, prv, group)
+        if chunk_fn is not None:
+            chunk_fn(c, x if s == 0 else total[c * n:(c + 1) * n])
+        if works is not None:
+            if s == ws - 2 and before_last_wait is not None:
+                before_last_wait()
+            for w in works:
+                w.wait()
+    return total
+
+
+def rs_ring(partial_fn, group, before_last_wait=None):
+    """Reduce-scatter along dim 0 over ``group`` as a ring, where chunk c of the tensor being
+    reduced is produced on demand by ``partial_fn(c)`` (a GEMM on c's rows): step s computes the
+    next partial while the previous one is in flight. Returns this rank's reduced chunk."""
+    ws, r, nxt, prv = _ring(group)
+    works, incoming, keep = None, None, []
+    for s in range(ws):
+        c = (r - s - 1) % ws
+        part = partial_fn(c)
+        if works is not None:
+            if s == ws - 1 and before_last_wait is not None:
+                before_last_wait()
+            for w in works:
+                w.wait()
+            part = part.add_(incoming)
+        if s == ws - 1:
+            return part
+        incoming = torch.empty_like(part)
+        keep.append(part)
+        works = _exchange(part, incoming, nxt, prv, group)
+    return None  # unreachable
+
+
+def _flush_wgrad():
+    DEFERRED_WGRAD.flush()
+
+
+class _ColumnSPLinear(torch.autograd.Function):
+    """Column-parallel linear on a sequence-parallel input: forward = ring all-gather fused with
+    the GEMM (the gathered input is kept for the weight gradient: 288 GB of HBM makes the
+    backward re-gather unnecessary); backward = dgrad GEMM fused with a ring reduce-scatter, the
+    weight gradient queued and drained while the last chunk is in flight."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        group = _tp_group()
+        x = x.contiguous()
+        n = x.shape[0]
+        ws = dist.get_world_size(group)
+        out = x.new_empty((n * ws,) + tuple(x.shape[1:-1]) + (weight.shape[0],))
+        total = ag_ring(x, group, lambda c, ch: _mm_into(out[c * n:(c + 1) * n], ch, weight, bias))
+        ctx.save_for_backward(total, weight)
+        ctx.bias_p = bias
+        ctx.n = n
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        total, weight = ctx.saved_tensors
+        group = _tp_group()
+        g = g.contiguous()
+        n = ctx.n
+        res = {}
+
+        def wgrad():
+            g2 = g.reshape(-1, g.shape[-1])
+            res["dw"] = _wgrad(weight, g2, total.reshape(-1, total.shape[-1]))
+            res["db"] = _bias_grad(ctx.bias_p, g2)
+            _flush_wgrad()
+        gi = rs_ring(lambda c: g[c * n:(c + 1) * n].matmul(weight), group, wgrad)
+        if "dw" not in res:   # world 1 ring: no wait happened
+            wgrad()
+        return gi, res["dw"], res["db"]
+
+
+class _RowSPLinear(torch.autograd.Function):
+    """Row-parallel linear whose output is reduce-scattered along the sequence: forward = per-chunk
+    GEMMs fused with a ring reduce-scatter; backward = ring all-gather of the output gradient
+    fused with the dgrad GEMM (queued weight gradients drained while the last chunk travels)."""
+
+    @staticmethod
+    def forward(ctx, x, weight):
+        group = _tp_group()
+        x = x.contiguous()
+        ws = dist.get_world_size(group)
+        assert x.shape[0] % ws == 0, "sequence length must divide the TP size"
+        n = x.shape[0] // ws
+        y = rs_ring(lambda c: torch.nn.functional.linear(x[c * n:(c + 1) * n], weight), group)
+        ctx.save_for_backward(x, weight)
+        ctx.n = n
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        x, weight = ctx.saved_tensors
+        group = _tp_group()
+        g = g.contiguous()
+        n = ctx.n
+        gi = x.new_empty(x.shape)
+        gfull = ag_ring(g, group, lambda c, ch: torch.matmul(ch, weight, out=gi[c * n:(c + 1) * n]),
+                        before_last_wait=_flush_wgrad)
+        dw = _wgrad(weight, gfull.reshape(-1, gfull.shape[-1]), x.reshape(-1, x.shape[-1]))
+        return gi, dw
+
+
+def _bias_grad(bias_p, g2):
+    """Column sums of g2 into the bias' fp32 main_grad (returns None) or as a tensor."""
+    if bias_p is None:
+        return None
+    tgt = SF.grad_accumulate_target(bias_p)
+    if tgt is not None and g2.is_contiguous() and g2.shape[-1] % 8 == 0:
+        _ext.ext().bias_grad(g2, tgt, True)
+        bias_p._smdt_grad_ready(bias_p)
+        return None
+    return g2.sum(0)
+
+
+def column_sp_linear(x, weight, bias):
+    return _ColumnSPLinear.apply(x, weight, bias)
+
+
+def row_sp_linear(x, weight):
+    return _RowSPLinear.apply(x, weight)
 
 
 # --------------------------------------------------------------------------------------------
@@ -497,10 +669,13 @@ class RowParallelLinear(nn.Module):
     def forward(self, x):
         if not self.input_is_parallel:
             x = scatter_to_tensor_model_parallel_region(x)
-        y = linear_with_grad_accumulation_and_async_allreduce(x, self.weight, None, False, False)
-        if self.sequence_parallel:
+        if self.sequence_parallel and _TP_OVERLAP:
+            y = _RowSPLinear.apply(x, self.weight)
+        elif self.sequence_parallel:
+            y = linear_with_grad_accumulation_and_async_allreduce(x, self.weight, None, False, False)
             y = reduce_scatter_to_sequence_parallel_region(y)
         else:
+            y = linear_with_grad_accumulation_and_async_allreduce(x, self.weight, None, False, False)
             y = reduce_from_tensor_model_parallel_region(y)
         if self.skip_bias_add:
             return y, self.bias

@@ -64,27 +64,172 @@ def forward_backward_no_pipelining(forward_step_func: Callable, data_iterator, m
 # ------------------------------------------------------------------------------------ p2p
 
 
+class P2PConfig:
+    """Pipeline p2p behaviour (Megatron flags, /root/reference/3_training_megatron-lm/megatron/
+    arguments.py:1014-1037):
+
+    * ``overlap`` (--overlap-p2p-communication): receives are not waited for where they are
+      issued but right before their consumer (the next forward / backward), so the RCCL transfer
+      runs beside the compute issued in between (on ROCm a wait is a stream dependency, not a
+      host block, so deferring it is what lets the MFMA work start).
+    * ``scatter_gather`` (default on; --no-scatter-gather-tensors-in-pipeline turns it off): with
+      TP > 1 and no sequence parallelism each TP rank sends only its 1/tp slice of the (TP-
+      replicated) activation and the receiver all-gathers it over TP — tp x fewer p2p bytes.
+    * ``deallocate_outputs`` (Megatron's deallocate_pipeline_outputs): once an activation was sent
+      to the next stage its data is dropped (only its autograd graph is needed), and backward
+      runs through the autograd engine directly.
+
+    Send-only groups are never waited for where they are issued; every in-flight send is
+    retired at the end of the schedule.
+    """
+
+    def __init__(self, overlap=False, scatter_gather=True, deallocate_outputs=True):
+        self.overlap = overlap
+        self.scatter_gather = scatter_gather
+        self.deallocate_outputs = deallocate_outputs
+
+
+_P2P = P2PConfig()
+_INFLIGHT_SENDS: List = []
+
+
+def configure_p2p(args=None, **kw):
+    """Set the pipeline p2p behaviour from parsed Megatron args (or keywords)."""
+    global _P2P
+    if args is not None:
+        if getattr(args, "use_ring_exchange_p2p", False):
+            raise ValueError("--use-ring-exchange-p2p needs torch.distributed.ring_exchange (a patched PyTorch "
+                             "build); on ROCm use the default batched RCCL p2p")
+        kw.setdefault("overlap", bool(getattr(args, "overlap_p2p_communication", False)))
+        kw.setdefault("scatter_gather", bool(getattr(args, "scatter_gather_tensors_in_pipeline", True)))
+        kw.setdefault("deallocate_outputs", bool(getattr(args, "deallocate_pipeline_outputs", True)))
+    _P2P = P2PConfig(**kw)
+    return _P2P
+
+
+def get_p2p_config():
+    return _P2P
+
+
+_SCHED = {"sp": False}
+
+
+def _enter_schedule(model):
+    """Per-schedule p2p context: scatter-gather applies only to TP-replicated activations (no
+    sequence parallelism — SP activations are already TP-sharded)."""
+    m = model[0] if isinstance(model, (list, tuple)) else model
+    core = m.module if hasattr(m, "module") else m
+    if isinstance(core, torch.nn.ModuleList) and len(core):
+        core = core[0]
+    cfg = getattr(core, "cfg", None)
+    _SCHED["sp"] = bool(getattr(cfg, "sequence_parallel", False))
+
+
+def _sg_active():
+    st = ps.get_state()
+    return _P2P.scatter_gather and st.tp > 1 and st.tp_group is not None and not _SCHED["sp"]
+
+
+def _sg_slice(t):
+    st = ps.get_state()
+    return t.contiguous().view(-1).chunk(st.tp)[st.tp_rank].contiguous()
+
+
+def _finish_recv(t):
+    """Wait for a received tensor's transfer (deferred under ``overlap``) and, with scatter-gather,
+    all-gather its TP slices back into the full activation. Returns the usable tensor."""
+    if t is None:
+        return None
+    holder = getattr(t, "_smdt_works", None)
+    if holder is not None and holder[0] is not None:
+        # one p2p group may carry both receives: its works are waited exactly once (a second
+        # wait on a retired gloo send blocks for a send that never comes)
+        works, holder[0] = holder[0], None
+        for w in works:
+            w.wait()
+    t._smdt_works = None
+    full_shape = getattr(t, "_smdt_sg_shape", None)
+    if full_shape is not None:
+        st = ps.get_state()
+        full = torch.empty((t.numel() * st.tp,), dtype=t.dtype, device=t.device)
+        dist.all_gather_into_tensor(full, t.detach(), group=st.tp_group)
+        out = full.view(full_shape).requires_grad_(True)
+        t._smdt_sg_shape = None
+        t._smdt_full = out
+        return out
+    full = getattr(t, "_smdt_full", None)
+    return t if full is None else full
+
+
 def _p2p(send_next=None, send_prev=None, recv_next_shape=None, recv_prev_shape=None, dtype=None, device=None):
     st = ps.get_state()
     ops = []
     rp = rn = None
+    sg = _sg_active()
+
+    def _recv_buf(shape):
+        if sg:
+            n = 1
+            for d in shape:
+                n *= d
+            t = torch.empty((n // st.tp,), dtype=dtype, device=device)
+            t._smdt_sg_shape = tuple(shape)
+            return t
+        return torch.empty(shape, dtype=dtype, device=device, requires_grad=True)
+
+    def _send_buf(t):
+        # a detached alias: dropping the activation's data after the send cannot free the storage
+        # the transfer still reads (the work keeps the alias alive)
+        return _sg_slice(t.detach()) if sg else t.detach().contiguous()
     # Canonical order — activations (to next / from prev) before gradients (to prev / from next)
     # on every rank — so the per-peer message streams match even when next == prev (a 2-rank
     # ring in the interleaved schedule): RCCL pairs point-to-point ops per peer in issue order.
     if send_next is not None:
-        ops.append(dist.P2POp(dist.isend, send_next.contiguous(), st.next_pp_rank))
+        ops.append(dist.P2POp(dist.isend, _send_buf(send_next), st.next_pp_rank))
     if recv_prev_shape is not None:
-        rp = torch.empty(recv_prev_shape, dtype=dtype, device=device, requires_grad=True)
+        rp = _recv_buf(recv_prev_shape)
         ops.append(dist.P2POp(dist.irecv, rp, st.prev_pp_rank))
     if send_prev is not None:
-        ops.append(dist.P2POp(dist.isend, send_prev.contiguous(), st.prev_pp_rank))
+        ops.append(dist.P2POp(dist.isend, _send_buf(send_prev), st.prev_pp_rank))
     if recv_next_shape is not None:
-        rn = torch.empty(recv_next_shape, dtype=dtype, device=device, requires_grad=True)
+        rn = _recv_buf(recv_next_shape)
         ops.append(dist.P2POp(dist.irecv, rn, st.next_pp_rank))
-    if ops:
-        for r in dist.batch_isend_irecv(ops):
-            r.wait()
+    if not ops:
+        return rp, rn
+    works = dist.batch_isend_irecv(ops)
+    if rp is None and rn is None:
+        _INFLIGHT_SENDS.extend(works)        # send-only: retired at the end of the schedule
+        return rp, rn
+    holder = [works]
+    for t in (rp, rn):
+        if t is not None:
+            t._smdt_works = holder
+    if not _P2P.overlap:
+        rp, rn = _finish_recv(rp), _finish_recv(rn)
     return rp, rn
+
+
+def _retire_sends():
+    while _INFLIGHT_SENDS:
+        _INFLIGHT_SENDS.pop().wait()
+
+
+def _drop_output(out):
+    """Megatron's deallocate_output_tensor: after ``out`` went to the next stage only its graph
+    is needed; its [s, b, h] data is replaced by one element."""
+    if _P2P.deallocate_outputs and out is not None and out.grad_fn is not None and out._base is None:
+        out.data = torch.empty((1,), device=out.device, dtype=out.dtype)
+
+
+def _run_backward(out, gout):
+    if gout is None:
+        torch.autograd.backward(out)
+    elif out.numel() != gout.numel():    # data was dropped after the send: call the engine directly
+        torch.autograd.Variable._execution_engine.run_backward(
+            tensors=(out,), grad_tensors=(gout,), keep_graph=False, create_graph=False, inputs=(),
+            allow_unreachable=True, accumulate_grad=True)
+    else:
+        torch.autograd.backward(out, grad_tensors=gout)
 
 
 def forward_backward_pipelining_without_interleaving(forward_step_func: Callable, data_iterator, model,
@@ -93,6 +238,7 @@ def forward_backward_pipelining_without_interleaving(forward_step_func: Callable
     """1F1B. ``tensor_shape`` is the [s(/tp), b, h] activation exchanged between stages."""
     models = model if isinstance(model, list) else [model]
     m = models[0]
+    _enter_schedule(m)
     st = ps.get_state()
     dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
     first, last = st.is_first_stage(), st.is_last_stage()
@@ -107,6 +253,7 @@ def forward_backward_pipelining_without_interleaving(forward_step_func: Callable
 
     def fwd(inp):
         core = m.module if hasattr(m, "module") else m
+        inp = _finish_recv(inp)
         core.set_input_tensor(inp)
         out, loss_func = forward_step_func(data_iterator, m)
         if last:
@@ -118,12 +265,10 @@ def forward_backward_pipelining_without_interleaving(forward_step_func: Callable
     def bwd(inp, out, gout):
         n_backward[0] += 1
         gate.set(n_backward[0] == num_microbatches)
+        inp, gout = _finish_recv(inp), _finish_recv(gout)
         if inp is not None:
             inp.retain_grad()
-        if gout is None:
-            torch.autograd.backward(out)
-        else:
-            torch.autograd.backward(out, grad_tensors=gout)
+        _run_backward(out, gout)
         return None if inp is None else inp.grad
 
     def recv_fwd():
@@ -137,6 +282,7 @@ def forward_backward_pipelining_without_interleaving(forward_step_func: Callable
         out = fwd(inp)
         if not last:
             _p2p(send_next=out)
+            _drop_output(out)
         inputs.append(inp)
         outputs.append(out)
     inp = recv_fwd() if steady > 0 else None
@@ -153,6 +299,7 @@ def forward_backward_pipelining_without_interleaving(forward_step_func: Callable
             gout = None
         else:
             gout = _p2p(send_next=out, recv_next_shape=tensor_shape, dtype=dtype, device=dev)[1]
+            _drop_output(out)
         inputs.append(inp)
         outputs.append(out)
         i0, o0 = inputs.pop(0), outputs.pop(0)
@@ -174,6 +321,7 @@ def forward_backward_pipelining_without_interleaving(forward_step_func: Callable
             gin = bwd(i0, o0, gout)
             if not first:
                 _p2p(send_prev=gin)
+    _retire_sends()
     gate.set(True)
     return losses
 
@@ -212,6 +360,7 @@ def forward_backward_pipelining_with_interleaving(forward_step_func: Callable, d
     import itertools
 
     chunks, ddp = _chunks_of(model)
+    _enter_schedule(chunks[0])
     vpp = len(chunks)
     st = ps.get_state()
     pp, r = st.pp, st.pp_rank
@@ -249,7 +398,7 @@ def forward_backward_pipelining_with_interleaving(forward_step_func: Callable, d
         set_vr(c)
         if st.is_first_stage() and len(inputs[c]) == len(outputs[c]):
             inputs[c].append(None)
-        inp = inputs[c][-1]
+        inp = inputs[c][-1] = _finish_recv(inputs[c][-1])
         chunks[c].set_input_tensor(inp)
         out, loss_func = forward_step_func(data_iterator[c], chunks[c])
         if st.is_last_stage():
@@ -264,15 +413,12 @@ def forward_backward_pipelining_with_interleaving(forward_step_func: Callable, d
         set_vr(c)
         if st.is_last_stage() and len(ograds[c]) == 0:
             ograds[c].append(None)
-        inp, out, gout = inputs[c].pop(0), outputs[c].pop(0), ograds[c].pop(0)
+        inp, out, gout = inputs[c].pop(0), outputs[c].pop(0), _finish_recv(ograds[c].pop(0))
         n_backward[0] += 1
         gate.set(n_backward[0] == total)
         if inp is not None:
             inp.retain_grad()
-        if gout is None:
-            torch.autograd.backward(out)
-        else:
-            torch.autograd.backward(out, grad_tensors=gout)
+        _run_backward(out, gout)
         return None if inp is None else inp.grad
 
     kw = dict(shape=tensor_shape, dtype=dtype, device=dev)
@@ -288,9 +434,11 @@ def forward_backward_pipelining_with_interleaving(forward_step_func: Callable, d
         if k == warm - 1 and not forward_only and not all_warmup:
             recv_next = not st.is_last_stage(ignore_virtual=True)
             rp, rn = _p2p_pair(send_next=out, recv_prev=recv_prev, recv_next=recv_next, **kw)
+            _drop_output(out)
             ograds[vpp - 1].append(rn)
         else:
             rp, _ = _p2p_pair(send_next=out, recv_prev=recv_prev, **kw)
+            _drop_output(out)
         if recv_prev:
             inputs[nxt].append(rp)
     for k in range(remaining):
@@ -322,6 +470,7 @@ def forward_backward_pipelining_with_interleaving(forward_step_func: Callable, d
         if k == remaining - 1:
             recv_prev = False
         rp, rn = _p2p_pair(send_next=out, send_prev=gin, recv_prev=recv_prev, recv_next=recv_next, **kw)
+        _drop_output(out)
         if recv_prev:
             inputs[nxt_f].append(rp)
         if recv_next:
@@ -341,6 +490,7 @@ def forward_backward_pipelining_with_interleaving(forward_step_func: Callable, d
             if recv_next:
                 ograds[nxt_b].append(rn)
     set_vr(0)
+    _retire_sends()
     gate.set(True)
     return losses
 

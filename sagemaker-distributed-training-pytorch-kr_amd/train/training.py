@@ -373,6 +373,8 @@ def train(forward_step_func, model, optimizer, scheduler, train_iter, valid_iter
 def pretrain(train_valid_test_dataset_provider, model_provider, model_type, forward_step_func,
              process_non_loss_data_func=None, extra_args_provider=None, args_defaults=None, argv=None):
     args = initialize_megatron(extra_args_provider, args_defaults, argv=argv)
+    from .schedules import configure_p2p
+    configure_p2p(args)   # --overlap-p2p-communication / --no-scatter-gather-tensors-in-pipeline
     timers = A.get_timers()
     timers("model-and-optimizer-setup", log_level=0).start(barrier=True)
     model, optimizer, scheduler = setup_model_and_optimizer(model_provider, args)

@@ -34,7 +34,7 @@ def gpt_reference(steps=1, sp=False, cfg_over=None):
     return loss.detach(), grads
 
 
-def gpt_tp_worker(rank, world, tp, pp, sp, cfg_over=None):
+def gpt_tp_worker(rank, world, tp, pp, sp, cfg_over=None, p2p=None):
     import torch.distributed as dist
     from smdt_amd.comm import init_distributed
     from smdt_amd.models.gpt import GPTModel, allreduce_word_embedding_grads
@@ -43,6 +43,8 @@ def gpt_tp_worker(rank, world, tp, pp, sp, cfg_over=None):
     from smdt_amd.train.schedules import get_forward_backward_func
     init_distributed("gloo")
     st = ps.initialize_model_parallel(tp, pp)
+    from smdt_amd.train import schedules
+    schedules.configure_p2p(**(p2p or {}))
     cfg = TransformerConfig(**{**TINY, **(cfg_over or {}), "sequence_parallel": sp})
     m = GPTModel(cfg, pre_process=st.is_first_stage(), post_process=st.is_last_stage())
     tokens, labels = _batch()
@@ -211,7 +213,7 @@ def zero_sft_worker(rank, world, stage, ga, steps, offload=False):
     return {n: p.detach().clone() for n, p in m.named_parameters()}
 
 
-def gpt_vpp_worker(rank, world, nmb):
+def gpt_vpp_worker(rank, world, nmb, p2p=None):
     """Interleaved pipeline (pp=2, vpp=2 chunks of 1 layer each, 4 layers): returns the last
     stage's per-token losses and every local gradient keyed by its single-model name."""
     import torch.distributed as dist
@@ -223,6 +225,8 @@ def gpt_vpp_worker(rank, world, nmb):
     from smdt_amd.train.schedules import get_forward_backward_func
     init_distributed("gloo")
     st = ps.initialize_model_parallel(1, 2, 2)
+    from smdt_amd.train import schedules
+    schedules.configure_p2p(**(p2p or {}))
     cfg = TransformerConfig(**{**TINY, "num_layers": 4})
     chunks = []
     for c in range(2):
@@ -366,3 +370,68 @@ def gpt_layout_worker(rank, world, tp, pp, nmb, zero, defer=False, sp=False):
     meta = {"tp_rank": st.tp_rank, "pp_rank": st.pp_rank, "layer_offset": m.first_layer}
     dist.destroy_process_group()
     return None, grads, meta
+
+
+def tp_overlap_order_worker(rank, world):
+    """Records the order of ring p2p launches, weight-gradient GEMMs and waits in the backward of
+    the sequence-parallel column / row linears, and checks their numerics against plain ops."""
+    import torch.distributed as dist
+    from smdt_amd.comm import init_distributed
+    from smdt_amd.parallel import state as ps
+    from smdt_amd.parallel import tensor_parallel as T
+    init_distributed("gloo")
+    ps.initialize_model_parallel(world, 1)
+    T.DEFERRED_WGRAD.allow_cpu = True
+    events = []
+    real_exchange, real_wgrad = T._exchange, T._wgrad
+
+    class _W:
+        def __init__(self, w):
+            self.w = w
+
+        def wait(self):
+            events.append("wait")
+            return self.w.wait()
+
+    def exchange(*a, **k):
+        events.append("launch")
+        return [_W(w) for w in real_exchange(*a, **k)]
+
+    def wgrad(weight, g2, t2):
+        events.append("wgrad")
+        return real_wgrad(weight, g2, t2)
+    T._exchange, T._wgrad = exchange, wgrad
+    g = torch.Generator().manual_seed(5)
+    S, B, H, O = 8, 2, 16, 32
+    xs = torch.randn(S, B, H, generator=g, dtype=torch.float64)
+    w1 = torch.randn(O, H, generator=g, dtype=torch.float64)     # column: full weight (rank shard below)
+    b1 = torch.randn(O, generator=g, dtype=torch.float64)
+    w2 = torch.randn(H, O, generator=g, dtype=torch.float64)     # row
+    dy = torch.randn(S, B, H, generator=g, dtype=torch.float64)
+    n = S // world
+    o = O // world
+    wc = torch.nn.Parameter(w1[rank * o:(rank + 1) * o].clone())
+    bc = torch.nn.Parameter(b1[rank * o:(rank + 1) * o].clone())
+    wr = torch.nn.Parameter(w2[:, rank * o:(rank + 1) * o].clone())
+    for p in (wc, bc, wr):
+        p.main_grad = torch.zeros_like(p)
+        p._smdt_grad_ready = lambda _p: None
+    x = xs[rank * n:(rank + 1) * n].clone().requires_grad_(True)
+    h = T.column_sp_linear(x, wc, bc)
+    y = T.row_sp_linear(h, wr)
+    events.append("backward")
+    y.backward(dy[rank * n:(rank + 1) * n])
+    T.DEFERRED_WGRAD.flush()
+    # reference on the full problem
+    xr = xs.clone().requires_grad_(True)
+    w1r, b1r, w2r = (t.clone().requires_grad_(True) for t in (w1, b1, w2))
+    yr = torch.nn.functional.linear(torch.nn.functional.linear(xr, w1r, b1r), w2r)
+    yr.backward(dy)
+    torch.testing.assert_close(y.detach(), yr.detach()[rank * n:(rank + 1) * n])
+    torch.testing.assert_close(x.grad, xr.grad[rank * n:(rank + 1) * n])
+    torch.testing.assert_close(wc.main_grad, w1r.grad[rank * o:(rank + 1) * o])
+    bgrad = bc.main_grad + (bc.grad if bc.grad is not None else 0)   # CPU: returned to autograd
+    torch.testing.assert_close(bgrad, b1r.grad[rank * o:(rank + 1) * o])
+    torch.testing.assert_close(wr.main_grad, w2r.grad[:, rank * o:(rank + 1) * o])
+    dist.destroy_process_group()
+    return events

@@ -39,13 +39,14 @@ def _check_tp_grads(ref, grads, meta, tp):
             _close(g, full.chunk(tp, 1)[r])
 
 
-@pytest.mark.parametrize("sp", [False, True])
-def test_tensor_parallel_matches_single_rank(sp):
+@pytest.mark.parametrize("tp,sp", [(2, False), (2, True), (4, True), (4, False)])
+def test_tensor_parallel_matches_single_rank(tp, sp):
+    """tp 4 + SP exercises the multi-step collective-matmul rings (send next / recv prev)."""
     ref_loss, ref = W.gpt_reference()
-    outs = run_workers(W.gpt_tp_worker, 2, 2, 1, sp)
+    outs = run_workers(W.gpt_tp_worker, tp, tp, 1, sp)
     for loss, grads, meta in outs:
         _close(loss, ref_loss)
-        _check_tp_grads(ref, grads, meta, 2)
+        _check_tp_grads(ref, grads, meta, tp)
 
 
 def test_pipeline_parallel_matches_single_rank():
@@ -59,9 +60,13 @@ def test_pipeline_parallel_matches_single_rank():
         _check_tp_grads({k: v for k, v in ref.items()}, grads, meta, 1)
 
 
-def test_tp2_pp2_dp1_world4():
+@pytest.mark.parametrize("sp,p2p", [(True, None), (False, None), (False, {"overlap": True}),
+                                    (False, {"scatter_gather": False, "deallocate_outputs": False})])
+def test_tp2_pp2_dp1_world4(sp, p2p):
+    """Without SP the p2p activations are TP-replicated: scatter-gather sends 1/tp of each and
+    all-gathers on receipt; --overlap-p2p-communication defers every receive wait to its consumer."""
     ref_loss, ref = W.gpt_reference()
-    outs = run_workers(W.gpt_tp_worker, 4, 2, 2, True)
+    outs = run_workers(W.gpt_tp_worker, 4, 2, 2, sp, None, p2p)
     for loss, grads, meta in outs:
         _check_tp_grads(ref, grads, meta, 2)
     last = [o for o in outs if o[2]["pp_rank"] == 1][0]
@@ -80,12 +85,12 @@ def test_data_parallel_and_zero_match_single_process(zero, overlap_pg, defer):
             torch.testing.assert_close(p, ref[n], atol=5e-3, rtol=1e-3)
 
 
-@pytest.mark.parametrize("nmb", [2, 4])
-def test_interleaved_pipeline_matches_single_rank(nmb):
+@pytest.mark.parametrize("nmb,p2p", [(2, None), (4, None), (2, {"overlap": True}), (4, {"overlap": True})])
+def test_interleaved_pipeline_matches_single_rank(nmb, p2p):
     """pp=2 x vpp=2 (4 layers, chunk c of rank r = global stage 2c + r); nmb == pp exercises the
     all-warm-up path, nmb == 2 pp the steady 1F1B phase."""
     ref_loss, ref = W.gpt_reference(cfg_over={"num_layers": 4})
-    outs = run_workers(W.gpt_vpp_worker, 2, nmb)
+    outs = run_workers(W.gpt_vpp_worker, 2, nmb, p2p)
     torch.testing.assert_close(outs[1][0].view(-1), ref_loss.view(-1), atol=2e-4, rtol=2e-4)
     seen = set()
     for _, grads in outs:
@@ -173,3 +178,42 @@ def test_ddp_gradient_accumulation_matches_single_process(world, tp, pp, nmb, ze
     outs = run_workers(W.gpt_layout_worker, world, tp, pp, nmb, zero, defer, sp)
     for _, grads, meta in outs:
         _check_tp_grads(ref, grads, meta, tp)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_sp_linear_rings_overlap_wgrad_with_comm(world):
+    """Collective-matmul SP linears: numerics match plain linears, and in backward each ring's last
+    transfer is launched BEFORE the weight-gradient GEMM runs and waited for only AFTER it."""
+    for ev in run_workers(W.tp_overlap_order_worker, world):
+        bwd = ev[ev.index("backward") + 1:]
+        # row linear backward (ring all-gather) first, then the column linear (ring reduce-scatter)
+        steps = world - 1
+        assert bwd.count("launch") == 2 * steps
+        col = bwd[bwd.index("wgrad") + 1:]          # after the row linear's own wgrad
+        i_w = col.index("wgrad")
+        assert "launch" in col[:i_w], col             # column dgrad ring launched first
+        assert col[i_w + 1:] and set(col[i_w + 1:]) == {"wait"}, col   # last transfer waited after the wgrad
+
+
+def test_pipeline_output_deallocation_keeps_backward_exact():
+    """deallocate_pipeline_outputs: a sent activation keeps only its graph (1-element data) and the
+    engine-level backward still produces the exact input gradient."""
+    from smdt_amd.train import schedules as S
+    S.configure_p2p()
+    x = torch.randn(8, 4, requires_grad=True)
+    w = torch.randn(4, 4)
+    out = torch.tanh(x @ w)
+    g = torch.randn(8, 4)
+    ref = torch.autograd.grad(torch.tanh(x @ w), x, g)[0]
+    S._drop_output(out)
+    assert out.numel() == 1
+    S._run_backward(out, g)
+    torch.testing.assert_close(x.grad, ref)
+
+
+def test_ring_exchange_p2p_flag_is_rejected():
+    import argparse
+    from smdt_amd.train import schedules as S
+    with pytest.raises(ValueError, match="ring_exchange"):
+        S.configure_p2p(argparse.Namespace(use_ring_exchange_p2p=True))
+    S.configure_p2p()
