@@ -297,10 +297,11 @@ void rope_(Tensor x, Tensor cos_t, Tensor sin_t, int64_t rot, int64_t pos_div, i
 bool wgrad_mfma(Tensor main_grad, Tensor dy, Tensor x, int64_t max_splits) {
   if (!main_grad.is_cuda() || main_grad.scalar_type() != at::kFloat || !main_grad.is_contiguous()) return false;
   if (dy.dim() != 2 || x.dim() != 2 || !dy.is_contiguous() || !x.is_contiguous()) return false;
-  if (dy.scalar_type() != at::kBFloat16 || x.scalar_type() != at::kBFloat16) return false;
+  if ((dy.scalar_type() != at::kBFloat16 && dy.scalar_type() != at::kHalf) || x.scalar_type() != dy.scalar_type())
+    return false;
   const int64_t M = dy.size(0), N = dy.size(1), K = x.size(1);
   if (x.size(0) != M || main_grad.numel() != N * K || !smdt_wgrad_supported(M, N, K)) return false;
-  check(smdt_wgrad_accumulate(dy.data_ptr(), x.data_ptr(), main_grad.data_ptr<float>(), M, N, K, (int)max_splits,
+  check(smdt_wgrad_accumulate_t(dcode(dy), dy.data_ptr(), x.data_ptr(), main_grad.data_ptr<float>(), M, N, K, (int)max_splits,
                               cur_stream()),
         "wgrad_mfma");
   return true;
@@ -316,14 +317,16 @@ bool wgrad_grouped(std::vector<Tensor> main_grads, std::vector<Tensor> dys, std:
     const Tensor &mg = main_grads[i], &dy = dys[i], &x = xs[i];
     if (!mg.is_cuda() || mg.scalar_type() != at::kFloat || !mg.is_contiguous()) return false;
     if (dy.dim() != 2 || x.dim() != 2 || !dy.is_contiguous() || !x.is_contiguous()) return false;
-    if (dy.scalar_type() != at::kBFloat16 || x.scalar_type() != at::kBFloat16) return false;
+    if ((dy.scalar_type() != at::kBFloat16 && dy.scalar_type() != at::kHalf) || x.scalar_type() != dy.scalar_type() ||
+        dy.scalar_type() != dys[0].scalar_type())
+      return false;
     if (dy.get_device() != mg.get_device() || x.get_device() != mg.get_device()) return false;
     const int64_t M = dy.size(0), N = dy.size(1), K = x.size(1);
     if (x.size(0) != M || mg.numel() != N * K || !smdt_wgrad_supported(M, N, K)) return false;
     probs[i] = SmdtWgradProblem{dy.data_ptr(), x.data_ptr(), mg.data_ptr<float>(), M, N, K};
   }
   if (n == 0) return true;
-  check(smdt_wgrad_grouped(probs.data(), (int)n, cur_stream()), "wgrad_grouped");
+  check(smdt_wgrad_grouped_t(dcode(dys[0]), probs.data(), (int)n, cur_stream()), "wgrad_grouped");
   return true;
 }
 
@@ -378,7 +381,7 @@ void ce_bwd(Tensor logits, Tensor target, Tensor gmax, Tensor gsum, Tensor dloss
 void fa_check(const Tensor& t, const char* n) {
   need_cuda(t, n);
   TORCH_CHECK(t.dim() == 4 && t.stride(3) == 1, "flash: '", n, "' must be [B, S, H, D] with unit last stride");
-  TORCH_CHECK(t.scalar_type() == at::kBFloat16, "flash: bf16 only");
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16 || t.scalar_type() == at::kHalf, "flash: bf16 / fp16 only");
   TORCH_CHECK(t.stride(0) % 8 == 0 && t.stride(1) % 8 == 0 && t.stride(2) % 8 == 0 &&
                   reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0,
               "flash: '", n, "' must keep 16-byte row alignment");
@@ -389,6 +392,7 @@ void fa_check(const Tensor& t, const char* n) {
 std::vector<Tensor> flash_fwd(Tensor q, Tensor k, Tensor v, double scale, bool causal, OptT out,
                               double dropout_p, int64_t seed, int64_t offset) {
   fa_check(q, "q"); fa_check(k, "k"); fa_check(v, "v");
+  TORCH_CHECK(k.scalar_type() == q.scalar_type() && v.scalar_type() == q.scalar_type(), "flash: q/k/v dtypes differ");
   const int64_t B = q.size(0), S = q.size(1), H = q.size(2), D = q.size(3), Hkv = k.size(2);
   TORCH_CHECK(k.size(0) == B && k.size(1) == S && k.size(3) == D && v.sizes() == k.sizes(), "flash: k/v shape mismatch");
   TORCH_CHECK((D == 64 || D == 128) && S % 128 == 0 && H % Hkv == 0, "flash: needs D in {64,128}, S % 128 == 0, H % Hkv == 0");
@@ -401,7 +405,8 @@ std::vector<Tensor> flash_fwd(Tensor q, Tensor k, Tensor v, double scale, bool c
     o = torch::empty({B, S, H, D}, q.options());
   }
   auto lse = torch::empty({B, H, S}, q.options().dtype(at::kFloat));
-  check(smdt_flash_fwd(1, q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr<float>(),
+  TORCH_CHECK(o.scalar_type() == q.scalar_type(), "flash: out dtype mismatch");
+  check(smdt_flash_fwd(dcode(q), q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr<float>(),
                        (int)B, (int)H, (int)Hkv, (int)S, (int)D, q.stride(0), q.stride(1), q.stride(2),
                        k.stride(0), k.stride(1), k.stride(2), v.stride(0), v.stride(1), v.stride(2),
                        o.stride(0), o.stride(1), o.stride(2), (float)scale, causal ? 1 : 0, (float)dropout_p,
@@ -416,6 +421,8 @@ std::vector<Tensor> flash_bwd(Tensor q, Tensor k, Tensor v, Tensor o, Tensor dou
                               double scale, bool causal, OptT dq_out, OptT dk_out, OptT dv_out,
                               double dropout_p, int64_t seed, int64_t offset) {
   fa_check(q, "q"); fa_check(k, "k"); fa_check(v, "v"); fa_check(o, "o");
+  TORCH_CHECK(k.scalar_type() == q.scalar_type() && v.scalar_type() == q.scalar_type() &&
+              o.scalar_type() == q.scalar_type() && dout.scalar_type() == q.scalar_type(), "flash_bwd: dtypes differ");
   const int64_t B = q.size(0), S = q.size(1), H = q.size(2), D = q.size(3), Hkv = k.size(2);
   TORCH_CHECK((D == 64 || D == 128) && S % 128 == 0 && H % Hkv == 0, "flash_bwd: unsupported shape");
   TORCH_CHECK(dout.sizes() == o.sizes(), "flash_bwd: dout shape mismatch");
@@ -437,7 +444,7 @@ std::vector<Tensor> flash_bwd(Tensor q, Tensor k, Tensor v, Tensor o, Tensor dou
   const Tensor* ts[8] = {&q, &k, &v, &o, &dout, &dq, &dk, &dv};
   for (int i = 0; i < 8; ++i)
     for (int j = 0; j < 3; ++j) st[3 * i + j] = ts[i]->stride(j);
-  check(smdt_flash_bwd(1, q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), dout.data_ptr(),
+  check(smdt_flash_bwd(dcode(q), q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), dout.data_ptr(),
                        lse.data_ptr<float>(), delta.data_ptr<float>(), dq.data_ptr(), dk.data_ptr(),
                        dv.data_ptr(), (int)B, (int)H, (int)Hkv, (int)S, (int)D, st, (float)scale,
                        causal ? 1 : 0, (float)dropout_p, (uint64_t)seed, (uint64_t)offset, cur_stream()),

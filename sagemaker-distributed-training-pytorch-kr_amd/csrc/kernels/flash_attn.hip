@@ -103,10 +103,12 @@ __device__ __forceinline__ uint32_t drop_hash(uint32_t blk, uint32_t key) {
 __device__ __forceinline__ bool keep_byte(uint32_t h, int sh, uint32_t thr) { return ((h >> sh) & 0xFFu) >= thr; }
 
 // Operand prescale: x * c rounded back to bf16 (one-time, register-resident fragments).
-__device__ __forceinline__ bf16x8 scale8(bf16x8 x, float c) {
-  bf16x8 r;
+template <class V>
+__device__ __forceinline__ V scale8(V x, float c) {
+  using EE = std::remove_cv_t<std::remove_reference_t<decltype(x[0])>>;
+  V r;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) r[j] = (bf16)((float)x[j] * c);
+  for (int j = 0; j < 8; ++j) r[j] = (EE)((float)x[j] * c);
   return r;
 }
 // An opaque copy: keeps the compiler from hoisting a loop-invariant splat16 out of the tile
@@ -157,7 +159,8 @@ struct GldsTile {
       off[j] = (int)(r * row_stride) + 8 * c;
     }
   }
-  __device__ __forceinline__ void issue(const bf16* tile_base, char* img, int w) const {
+  template <class E>
+  __device__ __forceinline__ void issue(const E* tile_base, char* img, int w) const {
 #pragma unroll
     for (int j = 0; j < kPerWave; ++j)
       __builtin_amdgcn_global_load_lds((const void*)(tile_base + off[j]),
@@ -168,11 +171,11 @@ struct GldsTile {
 // ---------------------------------------------------------------------------------------
 // Forward. Workgroup = 4 waves = 128 query rows of one (b, h); K/V streamed in 64-key tiles,
 // double-buffered.
-template <int D, bool CAUSAL, bool DROP>
-__global__ __launch_bounds__(256, D == 64 ? 2 : 1) void fwd_kernel(const bf16* __restrict__ Q,
-                                                     const bf16* __restrict__ K,
-                                                     const bf16* __restrict__ V,
-                                                     bf16* __restrict__ O, float* __restrict__ LSE,
+template <int D, bool CAUSAL, bool DROP, class E>
+__global__ __launch_bounds__(256, D == 64 ? 2 : 1) void fwd_kernel(const E* __restrict__ Q,
+                                                     const E* __restrict__ K,
+                                                     const E* __restrict__ V,
+                                                     E* __restrict__ O, float* __restrict__ LSE,
                                                      int B, int H, int Hkv, int S, Strides qs,
                                                      Strides ks_, Strides vs, Strides os,
                                                      float scale, Drop drop) {
@@ -194,12 +197,12 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void fwd_kernel(const bf16* _
   const int qw = q0 + 32 * w;  // this wave's first query row
   const int my_q = qw + (lane & 31);
 
-  const bf16* Kb = K + b * ks_.sb + hk * ks_.sh;
-  const bf16* Vb = V + b * vs.sb + hk * vs.sh;
+  const E* Kb = K + b * ks_.sb + hk * ks_.sh;
+  const E* Vb = V + b * vs.sb + hk * vs.sh;
 
-  Frag<D> fr;
+  Frag<D, E> fr;
   fr.init(lane);
-  bf16x8 qf[G::KS];
+  v8_t<E> qf[G::KS];
   load_reg_frags<D>(Q + b * qs.sb + hq * qs.sh, qs.ss, qw, lane, qf);
   // Q is prescaled by scale * log2(e), so S^T comes out in the log2 domain, and the score
   // accumulator starts at -m (the reference max): p = exp2(S) needs no per-element FMA.
@@ -306,7 +309,7 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void fwd_kernel(const bf16* _
       for (int tt = 0; tt < 2; ++tt) {
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
-          const bf16x8 pb = pack8(st[tt], s);
+          const v8_t<E> pb = pack8<E>(st[tt], s);
 #pragma unroll
           for (int dt = 0; dt < G::DT; ++dt) o[dt] = mfma(fr.trf(vt, 32 * tt, s, dt), pb, o[dt]);
         }
@@ -332,15 +335,15 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void fwd_kernel(const bf16* _
 
   // Epilogue: O[q, d] = O^T / l (x 1/(1-p) with dropout) ; lse = (m + log2 l) * ln 2.
   const float inv = l > 0.f ? (DROP ? drop.inv : 1.f) / l : 0.f;
-  bf16* Ob = O + b * os.sb + hq * os.sh + (int64_t)my_q * os.ss;
+  E* Ob = O + b * os.sb + hq * os.sh + (int64_t)my_q * os.ss;
 #pragma unroll
   for (int dt = 0; dt < G::DT; ++dt) {
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
-      bf4 v4;
+      v4_t<E> v4;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) v4[j] = (bf16)(o[dt][4 * g + j] * inv);
-      *reinterpret_cast<bf4*>(Ob + 32 * dt + 8 * g + 4 * h) = v4;
+      for (int j = 0; j < 4; ++j) v4[j] = (E)(o[dt][4 * g + j] * inv);
+      *reinterpret_cast<v4_t<E>*>(Ob + 32 * dt + 8 * g + 4 * h) = v4;
     }
   }
   if (h == 0) LSE[((int64_t)b * H + hq) * S + my_q] = (m + __log2f(l)) * 0.6931471805599453f;
@@ -348,9 +351,9 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void fwd_kernel(const bf16* _
 
 // ---------------------------------------------------------------------------------------
 // delta[b, h, q] = sum_d dO[q, d] * O[q, d]
-template <int D>
-__global__ __launch_bounds__(256) void delta_kernel(const bf16* __restrict__ O,
-                                                    const bf16* __restrict__ dO,
+template <int D, class E>
+__global__ __launch_bounds__(256) void delta_kernel(const E* __restrict__ O,
+                                                    const E* __restrict__ dO,
                                                     float* __restrict__ delta, int B, int H,
                                                     int S, Strides os, Strides dos) {
   // 8 lanes per row, each lane D/8 contiguous elements.
@@ -361,14 +364,14 @@ __global__ __launch_bounds__(256) void delta_kernel(const bf16* __restrict__ O,
   const int q = (int)(row % S);
   const int64_t bh = row / S;
   const int b = (int)(bh / H), hh = (int)(bh % H);
-  const bf16* o = O + b * os.sb + hh * os.sh + (int64_t)q * os.ss + part * (D / 8);
-  const bf16* g = dO + b * dos.sb + hh * dos.sh + (int64_t)q * dos.ss + part * (D / 8);
+  const E* o = O + b * os.sb + hh * os.sh + (int64_t)q * os.ss + part * (D / 8);
+  const E* g = dO + b * dos.sb + hh * dos.sh + (int64_t)q * dos.ss + part * (D / 8);
   float acc = 0.f;
 #pragma unroll
   for (int c = 0; c < D / 64; ++c) {
     float a[8], bb[8];
-    load_vec<bf16, 8>(o + 8 * c, a);
-    load_vec<bf16, 8>(g + 8 * c, bb);
+    load_vec<E, 8>(o + 8 * c, a);
+    load_vec<E, 8>(g + 8 * c, bb);
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc += a[j] * bb[j];
   }
@@ -381,11 +384,11 @@ __global__ __launch_bounds__(256) void delta_kernel(const bf16* __restrict__ O,
 // dK / dV. Workgroup = 4 waves = 128 keys of one (b, kv-head); each wave keeps K, V of its 32
 // keys and dK^T, dV^T in registers while the workgroup sweeps the query heads of the group and
 // their 64-row query tiles (Q, dO, lse*log2e, delta staged in double-buffered LDS).
-template <int D, bool CAUSAL, bool DROP>
+template <int D, bool CAUSAL, bool DROP, class E>
 __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dkdv_kernel(
-    const bf16* __restrict__ Q, const bf16* __restrict__ K, const bf16* __restrict__ V,
-    const bf16* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ DELTA,
-    bf16* __restrict__ dK, bf16* __restrict__ dV, int B, int H, int Hkv, int S, Strides qs,
+    const E* __restrict__ Q, const E* __restrict__ K, const E* __restrict__ V,
+    const E* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ DELTA,
+    E* __restrict__ dK, E* __restrict__ dV, int B, int H, int Hkv, int S, Strides qs,
     Strides ks_, Strides vs, Strides dos, Strides dks, Strides dvs, float scale, Drop drop) {
   using G = Geo<D>;
   constexpr int BUF = 2 * G::TB + 2 * kTile * 4;  // Q | dO | lse | delta (raw rows)
@@ -403,9 +406,9 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dkdv_kernel(
   const int kw = k0 + 32 * w;
   const int my_key = kw + (lane & 31);
 
-  Frag<D> fr;
+  Frag<D, E> fr;
   fr.init(lane);
-  bf16x8 kf[G::KS], vf[G::KS];
+  v8_t<E> kf[G::KS], vf[G::KS];
   load_reg_frags<D>(K + b * ks_.sb + hk * ks_.sh, ks_.ss, kw, lane, kf);
   load_reg_frags<D>(V + b * vs.sb + hk * vs.sh, vs.ss, kw, lane, vf);
 #pragma unroll
@@ -526,8 +529,8 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dkdv_kernel(
         // dV^T[d, key] += dO^T[d, q] . P[q, key] ; dK^T[d, key] += Q^T[d, q] . dS[q, key]
   #pragma unroll
         for (int st = 0; st < 2; ++st) {
-          const bf16x8 pb = pack8(s, st);
-          const bf16x8 db = pack8(dp, st);
+          const v8_t<E> pb = pack8<E>(s, st);
+          const v8_t<E> db = pack8<E>(dp, st);
   #pragma unroll
           for (int dt = 0; dt < G::DT; ++dt) {
             dv[dt] = mfma(fr.trf(do_l, 32 * qs2, st, dt), pb, dv[dt]);
@@ -557,20 +560,20 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dkdv_kernel(
 
 
   // dK[key, d] = scale * dK^T ; dV[key, d] = dV^T (key on lane, d in registers)
-  bf16* dKb = dK + b * dks.sb + hk * dks.sh + (int64_t)my_key * dks.ss;
-  bf16* dVb = dV + b * dvs.sb + hk * dvs.sh + (int64_t)my_key * dvs.ss;
+  E* dKb = dK + b * dks.sb + hk * dks.sh + (int64_t)my_key * dks.ss;
+  E* dVb = dV + b * dvs.sb + hk * dvs.sh + (int64_t)my_key * dvs.ss;
 #pragma unroll
   for (int dt = 0; dt < G::DT; ++dt) {
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
-      bf4 a, c;
+      v4_t<E> a, c;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        a[j] = (bf16)(dk[dt][4 * g + j] * scale);
-        c[j] = (bf16)dv[dt][4 * g + j];
+        a[j] = (E)(dk[dt][4 * g + j] * scale);
+        c[j] = (E)dv[dt][4 * g + j];
       }
-      *reinterpret_cast<bf4*>(dKb + 32 * dt + 8 * g + 4 * h) = a;
-      *reinterpret_cast<bf4*>(dVb + 32 * dt + 8 * g + 4 * h) = c;
+      *reinterpret_cast<v4_t<E>*>(dKb + 32 * dt + 8 * g + 4 * h) = a;
+      *reinterpret_cast<v4_t<E>*>(dVb + 32 * dt + 8 * g + 4 * h) = c;
     }
   }
 }
@@ -578,11 +581,11 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dkdv_kernel(
 // ---------------------------------------------------------------------------------------
 // dQ. Workgroup = 4 waves = 128 query rows of one (b, h); K/V streamed in 64-key tiles,
 // double-buffered.
-template <int D, bool CAUSAL, bool DROP>
+template <int D, bool CAUSAL, bool DROP, class E>
 __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dq_kernel(
-    const bf16* __restrict__ Q, const bf16* __restrict__ K, const bf16* __restrict__ V,
-    const bf16* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ DELTA,
-    bf16* __restrict__ dQ, int B, int H, int Hkv, int S, Strides qs, Strides ks_, Strides vs,
+    const E* __restrict__ Q, const E* __restrict__ K, const E* __restrict__ V,
+    const E* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ DELTA,
+    E* __restrict__ dQ, int B, int H, int Hkv, int S, Strides qs, Strides ks_, Strides vs,
     Strides dos, Strides dqs, float scale, Drop drop) {
   using G = Geo<D>;
   // D = 64: three [K | V] buffers, two tiles in flight; D = 128 (twice the bytes): two buffers,
@@ -599,9 +602,9 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dq_kernel(
   const int qw = q0 + 32 * w;
   const int my_q = qw + (lane & 31);
 
-  Frag<D> fr;
+  Frag<D, E> fr;
   fr.init(lane);
-  bf16x8 qf[G::KS], dof[G::KS];
+  v8_t<E> qf[G::KS], dof[G::KS];
   load_reg_frags<D>(Q + b * qs.sb + hq * qs.sh, qs.ss, qw, lane, qf);
   load_reg_frags<D>(dO + b * dos.sb + hq * dos.sh, dos.ss, qw, lane, dof);
 #pragma unroll
@@ -617,8 +620,8 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dq_kernel(
   const uint32_t dblk = (uint32_t)(my_q >> 1) * ((uint32_t)S >> 1) + 2u * h;
   const int dsh = 16 * (my_q & 1);
 
-  const bf16* Kb = K + b * ks_.sb + hk * ks_.sh;
-  const bf16* Vb = V + b * vs.sb + hk * vs.sh;
+  const E* Kb = K + b * ks_.sb + hk * ks_.sh;
+  const E* Vb = V + b * vs.sb + hk * vs.sh;
 
   f32x16 dq[G::DT];
 #pragma unroll
@@ -676,7 +679,7 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dq_kernel(
       // dQ^T[d, q] += K^T[d, keys] . dS^T[keys, q]
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        const bf16x8 db = pack8(dpt, s);
+        const v8_t<E> db = pack8<E>(dpt, s);
 #pragma unroll
         for (int dt = 0; dt < G::DT; ++dt) dq[dt] = mfma(fr.trf(kt, 32 * tt, s, dt), db, dq[dt]);
       }
@@ -699,15 +702,15 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dq_kernel(
   }
   wait_vm<0>();
 
-  bf16* dQb = dQ + b * dqs.sb + hq * dqs.sh + (int64_t)my_q * dqs.ss;
+  E* dQb = dQ + b * dqs.sb + hq * dqs.sh + (int64_t)my_q * dqs.ss;
 #pragma unroll
   for (int dt = 0; dt < G::DT; ++dt) {
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
-      bf4 a;
+      v4_t<E> a;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) a[j] = (bf16)(dq[dt][4 * g + j] * scale);
-      *reinterpret_cast<bf4*>(dQb + 32 * dt + 8 * g + 4 * h) = a;
+      for (int j = 0; j < 4; ++j) a[j] = (E)(dq[dt][4 * g + j] * scale);
+      *reinterpret_cast<v4_t<E>*>(dQb + 32 * dt + 8 * g + 4 * h) = a;
     }
   }
 }
@@ -719,7 +722,7 @@ using namespace smdt;
 using namespace smdt::fa;
 
 static bool fa_shape_ok(int dtype, int H, int Hkv, int S, int D) {
-  return dtype == 1 && (D == 64 || D == 128) && S % kBlockRows == 0 && S > 0 && S <= 65536 &&
+  return (dtype == 1 || dtype == 2) && (D == 64 || D == 128) && S % kBlockRows == 0 && S > 0 && S <= 65536 &&
          Hkv > 0 && H % Hkv == 0;
 }
 
@@ -758,9 +761,16 @@ extern "C" hipError_t smdt_flash_fwd(int dtype, const void* q, const void* k, co
   const Drop dr = make_drop(dropout_p, seed, offset);
   const bool drop = dropout_p > 0.f;
 #define SMDT_FA_FWD(DD, CC, DR)                                                                 \
-  hipLaunchKernelGGL((fwd_kernel<DD, CC, DR>), grid, dim3(256), 0, st, (const bf16*)q,         \
-                     (const bf16*)k, (const bf16*)v, (bf16*)o, lse, B, H, Hkv, S, qs, ks, vs, os, \
-                     scale, dr)
+  do {                                                                                          \
+    if (dtype == 2)                                                                             \
+      hipLaunchKernelGGL((fwd_kernel<DD, CC, DR, f16>), grid, dim3(256), 0, st, (const f16*)q,  \
+                         (const f16*)k, (const f16*)v, (f16*)o, lse, B, H, Hkv, S, qs, ks, vs, os, \
+                         scale, dr);                                                            \
+    else                                                                                        \
+      hipLaunchKernelGGL((fwd_kernel<DD, CC, DR, bf16>), grid, dim3(256), 0, st, (const bf16*)q, \
+                         (const bf16*)k, (const bf16*)v, (bf16*)o, lse, B, H, Hkv, S, qs, ks, vs, os, \
+                         scale, dr);                                                            \
+  } while (0)
 #define SMDT_FA_FWD2(DD, CC) \
   do { if (drop) SMDT_FA_FWD(DD, CC, true); else SMDT_FA_FWD(DD, CC, false); } while (0)
   if (D == 64) { if (causal) SMDT_FA_FWD2(64, true); else SMDT_FA_FWD2(64, false); }
@@ -787,27 +797,37 @@ extern "C" hipError_t smdt_flash_bwd(int dtype, const void* q, const void* k, co
   {
     int64_t rows = (int64_t)B * H * S;
     dim3 grid((unsigned)((rows * 8 + 255) / 256));
-    if (D == 64)
-      hipLaunchKernelGGL((delta_kernel<64>), grid, dim3(256), 0, st, (const bf16*)o, (const bf16*)dout, delta, B, H, S, os, dos);
-    else
-      hipLaunchKernelGGL((delta_kernel<128>), grid, dim3(256), 0, st, (const bf16*)o, (const bf16*)dout, delta, B, H, S, os, dos);
+    if (dtype == 2) {
+      if (D == 64)
+        hipLaunchKernelGGL((delta_kernel<64, f16>), grid, dim3(256), 0, st, (const f16*)o, (const f16*)dout, delta, B, H, S, os, dos);
+      else
+        hipLaunchKernelGGL((delta_kernel<128, f16>), grid, dim3(256), 0, st, (const f16*)o, (const f16*)dout, delta, B, H, S, os, dos);
+    } else {
+      if (D == 64)
+        hipLaunchKernelGGL((delta_kernel<64, bf16>), grid, dim3(256), 0, st, (const bf16*)o, (const bf16*)dout, delta, B, H, S, os, dos);
+      else
+        hipLaunchKernelGGL((delta_kernel<128, bf16>), grid, dim3(256), 0, st, (const bf16*)o, (const bf16*)dout, delta, B, H, S, os, dos);
+    }
   }
   dim3 gkv((unsigned)((int64_t)B * Hkv * (S / kBlockRows)));
   dim3 gq((unsigned)((int64_t)B * H * (S / kBlockRows)));
-#define SMDT_FA_BWD(DD, CC, DR)                                                                  \
+#define SMDT_FA_BWD_T(DD, CC, DR, ET)                                                            \
   do {                                                                                           \
-    hipLaunchKernelGGL((bwd_dkdv_kernel<DD, CC, DR>), gkv, dim3(256), 0, st, (const bf16*)q,    \
-                       (const bf16*)k, (const bf16*)v, (const bf16*)dout, lse, delta, (bf16*)dk,  \
-                       (bf16*)dv, B, H, Hkv, S, qs, ks, vs, dos, dks, dvs, scale, dr);            \
-    hipLaunchKernelGGL((bwd_dq_kernel<DD, CC, DR>), gq, dim3(256), 0, st, (const bf16*)q,       \
-                       (const bf16*)k, (const bf16*)v, (const bf16*)dout, lse, delta, (bf16*)dq,  \
+    hipLaunchKernelGGL((bwd_dkdv_kernel<DD, CC, DR, ET>), gkv, dim3(256), 0, st, (const ET*)q,  \
+                       (const ET*)k, (const ET*)v, (const ET*)dout, lse, delta, (ET*)dk,          \
+                       (ET*)dv, B, H, Hkv, S, qs, ks, vs, dos, dks, dvs, scale, dr);              \
+    hipLaunchKernelGGL((bwd_dq_kernel<DD, CC, DR, ET>), gq, dim3(256), 0, st, (const ET*)q,     \
+                       (const ET*)k, (const ET*)v, (const ET*)dout, lse, delta, (ET*)dq,          \
                        B, H, Hkv, S, qs, ks, vs, dos, dqs, scale, dr);                            \
   } while (0)
+#define SMDT_FA_BWD(DD, CC, DR) \
+  do { if (dtype == 2) SMDT_FA_BWD_T(DD, CC, DR, f16); else SMDT_FA_BWD_T(DD, CC, DR, bf16); } while (0)
 #define SMDT_FA_BWD2(DD, CC) \
   do { if (drop) SMDT_FA_BWD(DD, CC, true); else SMDT_FA_BWD(DD, CC, false); } while (0)
   if (D == 64) { if (causal) SMDT_FA_BWD2(64, true); else SMDT_FA_BWD2(64, false); }
   else { if (causal) SMDT_FA_BWD2(128, true); else SMDT_FA_BWD2(128, false); }
 #undef SMDT_FA_BWD2
 #undef SMDT_FA_BWD
+#undef SMDT_FA_BWD_T
   return hipGetLastError();
 }

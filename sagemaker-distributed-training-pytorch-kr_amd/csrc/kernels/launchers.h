@@ -88,8 +88,10 @@ hipError_t smdt_flash_bwd(int dtype, const void* q, const void* k, const void* v
                           float scale, int causal, float dropout_p, uint64_t seed,
                           uint64_t offset, hipStream_t st);
 
-// wgrad_gemm.hip: main_grad[N, K] (fp32) += dy[M, N]^T . x[M, K] (bf16)
+// wgrad_gemm.hip: main_grad[N, K] (fp32) += dy[M, N]^T . x[M, K] (bf16, or fp16 with dtype 2)
 int smdt_wgrad_supported(int64_t M, int64_t N, int64_t K);
+hipError_t smdt_wgrad_accumulate_t(int dtype, const void* dy, const void* x, float* main_grad, int64_t M,
+                                   int64_t N, int64_t K, int max_splits, hipStream_t st);
 hipError_t smdt_wgrad_accumulate(const void* dy, const void* x, float* main_grad, int64_t M, int64_t N,
                                  int64_t K, int max_splits, hipStream_t st);
 struct SmdtWgradProblem {
@@ -101,6 +103,7 @@ struct SmdtWgradProblem {
 // Many independent wgrad accumulations in one launch per 32 (no split-K, no atomics). The
 // main_grad targets of one call must not overlap.
 hipError_t smdt_wgrad_grouped(const SmdtWgradProblem* probs, int n, hipStream_t st);
+hipError_t smdt_wgrad_grouped_t(int dtype, const SmdtWgradProblem* probs, int n, hipStream_t st);
 
 // xgmi_allreduce.hip: single-node all-reduce over HIP-IPC-mapped peer buffers.
 int smdt_ar_max_ranks();

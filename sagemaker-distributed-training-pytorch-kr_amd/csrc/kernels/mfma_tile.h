@@ -22,11 +22,25 @@ using s16x4 = __attribute__((ext_vector_type(4))) short;
 using s16x8 = __attribute__((ext_vector_type(8))) short;
 using lds_s16x4 = __attribute__((address_space(3))) s16x4;
 using bf4 = __attribute__((ext_vector_type(4))) __bf16;
+using f16x8 = __attribute__((ext_vector_type(8))) _Float16;
+using h4 = __attribute__((ext_vector_type(4))) _Float16;
+
+// Element type -> MFMA operand vector (8 elements) and 4-element store vector. Both 16-bit types
+// share every LDS layout and DMA path; only the MFMA opcode and the fp32 -> 16-bit rounding differ.
+template <class E> struct Vec;
+template <> struct Vec<bf16> { using v8 = bf16x8; using v4 = bf4; };
+template <> struct Vec<f16> { using v8 = f16x8; using v4 = h4; };
+template <class E> using v8_t = typename Vec<E>::v8;
+template <class E> using v4_t = typename Vec<E>::v4;
 
 constexpr int kTile = 64;        // rows per streamed LDS tile
 
 __device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+// fp16 operands (Megatron --fp16): v_mfma_f32_32x32x16_f16, same lane / register maps.
+__device__ __forceinline__ f32x16 mfma(f16x8 a, f16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
 }
 
 __device__ __forceinline__ f32x16 zero16() {
@@ -52,9 +66,10 @@ struct Geo {
   __device__ static __forceinline__ int off(int r, int c) { return r * RB + 16 * (c ^ f(r)); }
 };
 
-// Per-lane LDS offsets, computed once per kernel.
-template <int D>
+// Per-lane LDS offsets, computed once per kernel. E = element type of the tiles.
+template <int D, class E = bf16>
 struct Frag {
+  using V = v8_t<E>;
   int row[D / 16];     // row fragment of k-step ks for tile rows 0..31
   int tr[D / 32][2];   // transposed fragment of d-tile dt, k-step 0, rows 0..15 (two 4-row blocks)
   // Offset of the transposed read of d-tile dt, 4-row block `blk` (rows 4 h + (lane >> 2 & 3) + 8 blk).
@@ -73,27 +88,28 @@ struct Frag {
     }
   }
   // Transposed fragment at precomputed offsets (o0, o1) = (tr_off(.., 0), tr_off(.., 1)).
-  __device__ static __forceinline__ bf16x8 trf_at(const char* tile, int rbase, int s, int o0, int o1) {
+  __device__ static __forceinline__ V trf_at(const char* tile, int rbase, int s, int o0, int o1) {
     const char* b = tile + (rbase + 16 * s) * Geo<D>::RB;
     s16x4 x = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(b + o0));
     s16x4 y = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(b + o1));
-    return __builtin_bit_cast(bf16x8, __builtin_shufflevector(x, y, 0, 1, 2, 3, 4, 5, 6, 7));
+    return __builtin_bit_cast(V, __builtin_shufflevector(x, y, 0, 1, 2, 3, 4, 5, 6, 7));
   }
   // A-operand row fragment: rows rbase..rbase+31 (rbase multiple of 32), elements 16 ks + 8 h..
-  __device__ __forceinline__ bf16x8 rowf(const char* tile, int rbase, int ks) const {
-    return *reinterpret_cast<const bf16x8*>(tile + rbase * Geo<D>::RB + row[ks]);
+  __device__ __forceinline__ V rowf(const char* tile, int rbase, int ks) const {
+    return *reinterpret_cast<const V*>(tile + rbase * Geo<D>::RB + row[ks]);
   }
   // A-operand transposed fragment over tile rows rbase + 16 s + (permuted), columns 32 dt + lane&31.
-  __device__ __forceinline__ bf16x8 trf(const char* tile, int rbase, int s, int dt) const {
+  __device__ __forceinline__ V trf(const char* tile, int rbase, int s, int dt) const {
     return trf_at(tile, rbase, s, tr[dt][0], tr[dt][1]);
   }
 };
 
-// Pack accumulator registers 8 s .. 8 s + 7 into a bf16 operand fragment.
-__device__ __forceinline__ bf16x8 pack8(const f32x16& x, int s) {
-  bf16x8 r;
+// Pack accumulator registers 8 s .. 8 s + 7 into a 16-bit operand fragment.
+template <class E = bf16>
+__device__ __forceinline__ v8_t<E> pack8(const f32x16& x, int s) {
+  v8_t<E> r;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) r[j] = (bf16)x[8 * s + j];
+  for (int j = 0; j < 8; ++j) r[j] = (E)x[8 * s + j];
   return r;
 }
 
@@ -130,12 +146,12 @@ struct Stage {
 
 // Direct global load of a row-operand fragment that stays in registers for the whole kernel:
 // lane holds row (row0 + lane&31), elements [16 ks + 8 h, +8).
-template <int D>
-__device__ __forceinline__ void load_reg_frags(const bf16* base, int64_t row_stride, int row0,
-                                               int lane, bf16x8 (&f)[D / 16]) {
-  const bf16* p = base + (int64_t)(row0 + (lane & 31)) * row_stride + 8 * (lane >> 5);
+template <int D, class E>
+__device__ __forceinline__ void load_reg_frags(const E* base, int64_t row_stride, int row0,
+                                               int lane, v8_t<E> (&f)[D / 16]) {
+  const E* p = base + (int64_t)(row0 + (lane & 31)) * row_stride + 8 * (lane >> 5);
 #pragma unroll
-  for (int ks = 0; ks < D / 16; ++ks) f[ks] = *reinterpret_cast<const bf16x8*>(p + 16 * ks);
+  for (int ks = 0; ks < D / 16; ++ks) f[ks] = *reinterpret_cast<const v8_t<E>*>(p + 16 * ks);
 }
 
 

@@ -1,5 +1,5 @@
 // Weight-gradient GEMM with fp32 accumulation into the DDP main_grad:
-//     C[n, k] (fp32) += sum_m A[m, n] * B[m, k]       A = dY [M, N], B = X [M, K], bf16 row-major
+//     C[n, k] (fp32) += sum_m A[m, n] * B[m, k]       A = dY [M, N], B = X [M, K], bf16 / fp16 row-major
 // (Megatron's gradient-accumulation fusion; /root/reference/3_training_megatron-lm/
 // megatron/arguments.py:850-854).
 //
@@ -42,7 +42,6 @@ using namespace mt;
 constexpr int BT = 256;              // output tile edge (n and k)
 constexpr int BM = 32;               // m rows per stage
 using G = Geo<BT>;                   // rows of 512 B, XOR-swizzled 16-byte chunks (row bits 0..3)
-using F = Frag<BT>;
 constexpr int SB = BM * G::RB;       // bytes per operand stage image (16 KB)
 constexpr int kThreads = 512;
 constexpr int kWaves = kThreads / 64;
@@ -73,7 +72,8 @@ struct Glds {
       off[j] = r * ld + col;
     }
   }
-  __device__ __forceinline__ void issue(const bf16* stage_base, char* img, int wave) const {
+  template <class E>
+  __device__ __forceinline__ void issue(const E* stage_base, char* img, int wave) const {
 #pragma unroll
     for (int j = 0; j < kGlds; ++j)
       __builtin_amdgcn_global_load_lds((const void*)(stage_base + off[j]),
@@ -84,12 +84,14 @@ struct Glds {
 // One 256 x 256 output tile over stages [0, nst) of 32 rows starting at A/B row mstart.
 // VAR is a diagnostic knob for benchmarks/wgrad_micro.hip only (the library uses VAR = 0):
 // bit 0 skips the in-loop DMA, bit 2 the fragment reads.
-template <bool ATOMIC, int VAR>
-__device__ __forceinline__ void tile_gemm(const bf16* __restrict__ A, const bf16* __restrict__ B,
+template <bool ATOMIC, int VAR, class E>
+__device__ __forceinline__ void tile_gemm(const E* __restrict__ A, const E* __restrict__ B,
                                           float* __restrict__ C, int N, int K, int n0, int k0, int64_t mstart,
                                           int nst, char* L0, char* L1, char* L2, char* L3) {
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), h = lane >> 5;
   const int wn = wave >> 2, wk = wave & 3;  // wave tile: n rows [128 wn, +128), k cols [64 wk, +64)
+  using F = Frag<BT, E>;
+  using V = v8_t<E>;
 
   int oa[4][2], ob[2][2];
 #pragma unroll
@@ -111,8 +113,8 @@ __device__ __forceinline__ void tile_gemm(const bf16* __restrict__ A, const bf16
   Glds ga, gb;
   ga.init(wave, lane, N, n0, N);
   gb.init(wave, lane, K, k0, K);
-  const bf16* Ab = A + mstart * N;
-  const bf16* Bb = B + mstart * K;
+  const E* Ab = A + mstart * N;
+  const E* Bb = B + mstart * K;
   const int64_t sa = (int64_t)BM * N, sbk = (int64_t)BM * K;
 
   auto issue = [&](int s, char* img) {
@@ -136,10 +138,10 @@ __device__ __forceinline__ void tile_gemm(const bf16* __restrict__ A, const bf16
     const char* bt = cur + SB;
 #pragma unroll
     for (int ks = 0; ks < BM / 16; ++ks) {
-      bf16x8 b0, b1;
+      V b0, b1;
       if constexpr (VAR & 4) {
         const f32x4 t4 = {acc[0][0][4 * ks], acc[0][1][4 * ks], acc[1][0][4 * ks], acc[1][1][4 * ks]};
-        b0 = __builtin_bit_cast(bf16x8, t4);
+        b0 = __builtin_bit_cast(V, t4);
         b1 = b0;
       } else {
         b0 = F::trf_at(bt, 0, ks, ob[0][0], ob[0][1]);
@@ -147,7 +149,7 @@ __device__ __forceinline__ void tile_gemm(const bf16* __restrict__ A, const bf16
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        bf16x8 a;
+        V a;
         if constexpr (VAR & 4) a = b1;
         else a = F::trf_at(at, 0, ks, oa[i][0], oa[i][1]);
         acc[i][0] = mfma(a, b0, acc[i][0]);
@@ -230,8 +232,8 @@ __device__ __forceinline__ void tile_coords(int t, int ntn, int ntk, int gn, int
   __shared__ __attribute__((aligned(1024))) char L2[2 * SB];      \
   __shared__ __attribute__((aligned(1024))) char L3[2 * SB];
 
-template <bool ATOMIC, int VAR = 0>
-__global__ __launch_bounds__(kThreads, 1) void wgrad_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
+template <bool ATOMIC, int VAR = 0, class E = bf16>
+__global__ __launch_bounds__(kThreads, 1) void wgrad_kernel(const E* __restrict__ A, const E* __restrict__ B,
                                                           float* __restrict__ C, int M, int N, int K, int ntn,
                                                           int ntk, int gn, int m_per_split, int nblocks) {
   WG_LDS
@@ -242,12 +244,12 @@ __global__ __launch_bounds__(kThreads, 1) void wgrad_kernel(const bf16* __restri
   tile_coords(w - split * tiles, ntn, ntk, gn, tn, tk);
   const int mstart = split * m_per_split;
   const int nst = (min(M, mstart + m_per_split) - mstart) / BM;
-  tile_gemm<ATOMIC, VAR>(A, B, C, N, K, tn * BT, tk * BT, mstart, nst, L0, L1, L2, L3);
+  tile_gemm<ATOMIC, VAR, E>(A, B, C, N, K, tn * BT, tk * BT, mstart, nst, L0, L1, L2, L3);
 }
 
 struct Problem {
-  const bf16* A;
-  const bf16* B;
+  const void* A;
+  const void* B;
   float* C;
   int M, N, K, ntn, ntk, gn, tile0;
 };
@@ -258,6 +260,7 @@ struct Group {
 };
 
 // The problem table travels in the kernel arguments (< 2 KB), read from the kernarg segment.
+template <class E>
 __global__ __launch_bounds__(kThreads, 1) void wgrad_grouped_kernel(const Group g) {
   WG_LDS
   const int w = xcd_remap(blockIdx.x, g.nblocks);
@@ -266,7 +269,8 @@ __global__ __launch_bounds__(kThreads, 1) void wgrad_grouped_kernel(const Group 
   const Problem& P = g.p[pi];
   int tn, tk;
   tile_coords(w - P.tile0, P.ntn, P.ntk, P.gn, tn, tk);
-  tile_gemm<false, 0>(P.A, P.B, P.C, P.N, P.K, tn * BT, tk * BT, 0, P.M / BM, L0, L1, L2, L3);
+  tile_gemm<false, 0, E>((const E*)P.A, (const E*)P.B, P.C, P.N, P.K, tn * BT, tk * BT, 0, P.M / BM, L0, L1, L2,
+                         L3);
 }
 
 inline int group_width(int ntk) { return ntk <= 4 ? 8 : 4; }
@@ -283,6 +287,12 @@ extern "C" int smdt_wgrad_supported(int64_t M, int64_t N, int64_t K) {
 
 extern "C" hipError_t smdt_wgrad_accumulate(const void* dy, const void* x, float* main_grad, int64_t M,
                                             int64_t N, int64_t K, int max_splits, hipStream_t st) {
+  return smdt_wgrad_accumulate_t(1, dy, x, main_grad, M, N, K, max_splits, st);
+}
+
+extern "C" hipError_t smdt_wgrad_accumulate_t(int dtype, const void* dy, const void* x, float* main_grad, int64_t M,
+                                              int64_t N, int64_t K, int max_splits, hipStream_t st) {
+  if (dtype != 1 && dtype != 2) return hipErrorInvalidValue;
   if (!smdt_wgrad_supported(M, N, K)) return hipErrorInvalidValue;
   const int ntn = (int)((N + wg::BT - 1) / wg::BT), ntk = (int)((K + wg::BT - 1) / wg::BT);
   const int tiles = ntn * ntk;
@@ -310,17 +320,25 @@ extern "C" hipError_t smdt_wgrad_accumulate(const void* dy, const void* x, float
   splits = (int)((M + m_per_split - 1) / m_per_split);
   const int nblocks = tiles * splits;
   const int gn = wg::group_width(ntk);
-  if (splits > 1)
-    hipLaunchKernelGGL((wg::wgrad_kernel<true>), dim3(nblocks), dim3(wg::kThreads), 0, st, (const bf16*)dy,
-                       (const bf16*)x, main_grad, (int)M, (int)N, (int)K, ntn, ntk, gn, m_per_split, nblocks);
-  else
-    hipLaunchKernelGGL((wg::wgrad_kernel<false>), dim3(nblocks), dim3(wg::kThreads), 0, st, (const bf16*)dy,
-                       (const bf16*)x, main_grad, (int)M, (int)N, (int)K, ntn, ntk, gn, m_per_split, nblocks);
+#define SMDT_WG(AT, ET)                                                                                     \
+  hipLaunchKernelGGL((wg::wgrad_kernel<AT, 0, ET>), dim3(nblocks), dim3(wg::kThreads), 0, st, (const ET*)dy, \
+                     (const ET*)x, main_grad, (int)M, (int)N, (int)K, ntn, ntk, gn, m_per_split, nblocks)
+  if (dtype == 2) {
+    if (splits > 1) SMDT_WG(true, f16); else SMDT_WG(false, f16);
+  } else {
+    if (splits > 1) SMDT_WG(true, bf16); else SMDT_WG(false, bf16);
+  }
+#undef SMDT_WG
   return hipGetLastError();
 }
 
 // Grouped form: one launch per 32 problems, the table passed by value.
 extern "C" hipError_t smdt_wgrad_grouped(const SmdtWgradProblem* probs, int n, hipStream_t st) {
+  return smdt_wgrad_grouped_t(1, probs, n, st);
+}
+
+extern "C" hipError_t smdt_wgrad_grouped_t(int dtype, const SmdtWgradProblem* probs, int n, hipStream_t st) {
+  if (dtype != 1 && dtype != 2) return hipErrorInvalidValue;
   for (int i = 0; i < n; ++i)
     if (!smdt_wgrad_supported(probs[i].M, probs[i].N, probs[i].K)) return hipErrorInvalidValue;
   for (int base = 0; base < n; base += wg::kMaxGroup) {
@@ -330,8 +348,8 @@ extern "C" hipError_t smdt_wgrad_grouped(const SmdtWgradProblem* probs, int n, h
     for (int i = 0; i < cnt; ++i) {
       const SmdtWgradProblem& q = probs[base + i];
       wg::Problem& p = g.p[i];
-      p.A = (const bf16*)q.dy;
-      p.B = (const bf16*)q.x;
+      p.A = q.dy;
+      p.B = q.x;
       p.C = q.main_grad;
       p.M = (int)q.M;
       p.N = (int)q.N;
@@ -345,7 +363,10 @@ extern "C" hipError_t smdt_wgrad_grouped(const SmdtWgradProblem* probs, int n, h
     for (int i = cnt; i < wg::kMaxGroup; ++i) g.p[i] = g.p[cnt - 1];
     g.nprob = cnt;
     g.nblocks = tiles;
-    hipLaunchKernelGGL(wg::wgrad_grouped_kernel, dim3(tiles), dim3(wg::kThreads), 0, st, g);
+    if (dtype == 2)
+      hipLaunchKernelGGL(wg::wgrad_grouped_kernel<f16>, dim3(tiles), dim3(wg::kThreads), 0, st, g);
+    else
+      hipLaunchKernelGGL(wg::wgrad_grouped_kernel<bf16>, dim3(tiles), dim3(wg::kThreads), 0, st, g);
   }
   return hipGetLastError();
 }

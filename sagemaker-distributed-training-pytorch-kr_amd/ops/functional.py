@@ -11,6 +11,7 @@ enable/disable flags wired up in ``smdt_amd.models.transformer``.
 from __future__ import annotations
 
 import math
+import os
 from typing import Optional
 
 import torch
@@ -387,6 +388,8 @@ def flash_dropout_keep_mask(B: int, H: int, S: int, p: float, seed: int, offset:
 def attention_ref(q, k, v, scale, causal, dropout_p: float = 0.0, keep=None):
     """Reference attention on [B, S, H, D] (GQA by head repetition), fp32 math. ``keep``
     ([B, H, S, S] bool) is the dropout keep-mask (``flash_dropout_keep_mask``)."""
+    if q.is_cuda and os.environ.get("SMDT_ASSERT_FLASH") == "1":
+        raise RuntimeError("SMDT_ASSERT_FLASH=1: reference attention reached on the GPU")
     B, S, H, D = q.shape
     Hkv = k.shape[2]
     if Hkv != H:
@@ -408,9 +411,41 @@ def attention_ref(q, k, v, scale, causal, dropout_p: float = 0.0, keep=None):
 
 
 def flash_supported(q, k) -> bool:
+    """True when the kernels take q / k exactly as they are (no padding)."""
     B, S, H, D = q.shape
-    return (q.dtype == torch.bfloat16 and D in (64, 128) and S % 128 == 0 and H % k.shape[2] == 0
-            and q.stride(-1) == 1 and k.stride(-1) == 1)
+    return (q.dtype in (torch.bfloat16, torch.float16) and D in (64, 128) and S % 128 == 0
+            and H % k.shape[2] == 0 and q.stride(-1) == 1 and k.stride(-1) == 1)
+
+
+def _flash_plan(q, k, causal: bool):
+    """(S_pad, D_pad) the gfx950 kernels run this attention at, or raise — a GPU tensor never
+    drops to the materialised S x S reference (ops/_ext.py policy).
+
+    Padding is exact where it is used: head dims below 64 / 128 are zero-padded (zero q / k
+    columns add nothing to q.k, zero v columns produce output columns that are sliced off, and
+    the softmax scale stays 1 / sqrt(D_orig)); a causal sequence is padded at its END (no real
+    query attends to a later key). A non-causal sequence that is not a multiple of 128 would
+    need key masking and is rejected."""
+    B, S, H, D = q.shape
+    if q.dtype not in (torch.bfloat16, torch.float16):
+        raise RuntimeError(f"flash attention on the GPU runs bf16 / fp16, got {q.dtype}; cast the model "
+                           "(--bf16 / --fp16) or disable flash attention (--no-flash-attn)")
+    if H % k.shape[2]:
+        raise RuntimeError(f"flash attention: {H} query heads are not a multiple of {k.shape[2]} kv heads")
+    if D > 128:
+        raise RuntimeError(f"flash attention: head dim {D} > 128 is not supported by the gfx950 kernels")
+    Dp = 64 if D <= 64 else 128
+    Sp = -(-S // 128) * 128
+    if Sp != S and not causal:
+        raise RuntimeError(f"flash attention: non-causal sequence length {S} must be a multiple of 128")
+    return Sp, Dp
+
+
+def _pad_bshd(t, Sp, Dp):
+    S, D = t.shape[1], t.shape[3]
+    if Sp == S and Dp == D:
+        return t
+    return torch.nn.functional.pad(t, (0, Dp - D, 0, 0, 0, Sp - S))
 
 
 def flash_attention(q, k, v, scale: Optional[float] = None, causal: bool = True, dropout_p: float = 0.0,
@@ -420,8 +455,14 @@ def flash_attention(q, k, v, scale: Optional[float] = None, causal: bool = True,
     if scale is None:
         scale = 1.0 / math.sqrt(q.shape[-1])
     seed, off = _rng(rng).next() if dropout_p > 0 else (0, 0)
-    if _ext.use_kernels(q) and flash_supported(q, k):
-        return _FlashAttn.apply(q, k, v, float(scale), bool(causal), float(dropout_p), int(seed), int(off))
+    if _ext.use_kernels(q):
+        S, D = q.shape[1], q.shape[3]
+        Sp, Dp = _flash_plan(q, k, causal)
+        if (Sp, Dp) == (S, D) and flash_supported(q, k):
+            return _FlashAttn.apply(q, k, v, float(scale), bool(causal), float(dropout_p), int(seed), int(off))
+        qp, kp, vp = (_pad_bshd(t.contiguous() if t.stride(-1) != 1 else t, Sp, Dp) for t in (q, k, v))
+        o = _FlashAttn.apply(qp, kp, vp, float(scale), bool(causal), float(dropout_p), int(seed), int(off))
+        return o[:, :S, :, :D]
     keep = flash_dropout_keep_mask(q.shape[0], q.shape[2], q.shape[1], dropout_p, seed, off, q.device) \
         if dropout_p > 0 else None
     return attention_ref(q, k, v, scale, causal, dropout_p, keep)
@@ -434,22 +475,29 @@ def flash_attention_qkv(qkv, nh: int, nkv: int, hd: int, seq_first: bool = True,
     ``qkv`` is [S, B, (nh + 2 nkv) hd] (``seq_first``) or [B, S, ...]; returns [S, B, nh hd]
     (resp. [B, S, nh hd]). Backward produces ONE fused d(qkv) buffer. ``dropout_p`` > 0 applies
     attention-probability dropout inside the kernels (mask re-derived from ``rng``'s
-    (seed, offset) in backward — nothing is stored).
+    (seed, offset) in backward — nothing is stored). Shapes the kernels cannot read in place
+    (S % 128 != 0, head dim not 64 / 128) go through the padded separate-q/k/v path.
     """
     if scale is None:
         scale = 1.0 / math.sqrt(hd)
     q, k, v = _qkv_views(qkv, nh, nkv, hd, seq_first)
-    seed, off = _rng(rng).next() if dropout_p > 0 else (0, 0)
-    if _ext.use_kernels(qkv) and qkv.is_contiguous() and flash_supported(q, k) and (nh + 2 * nkv) * hd % 8 == 0:
-        return _FlashAttnQKV.apply(qkv, nh, nkv, hd, bool(seq_first), float(scale), bool(causal),
-                                   float(dropout_p), int(seed), int(off))
-    keep = None
-    if dropout_p > 0:
-        keep = flash_dropout_keep_mask(q.shape[0], nh, q.shape[1], dropout_p, seed, off, qkv.device)
-    o = attention_ref(q, k, v, scale, causal, dropout_p, keep)  # [B, S, H, D]
+    if _ext.use_kernels(qkv):
+        if qkv.is_contiguous() and flash_supported(q, k) and (nh + 2 * nkv) * hd % 8 == 0:
+            seed, off = _rng(rng).next() if dropout_p > 0 else (0, 0)
+            return _FlashAttnQKV.apply(qkv, nh, nkv, hd, bool(seq_first), float(scale), bool(causal),
+                                       float(dropout_p), int(seed), int(off))
+        o = flash_attention(q, k, v, scale, causal, dropout_p, rng)          # [B, S, H, D]
+    else:
+        seed, off = _rng(rng).next() if dropout_p > 0 else (0, 0)
+        keep = None
+        if dropout_p > 0:
+            keep = flash_dropout_keep_mask(q.shape[0], nh, q.shape[1], dropout_p, seed, off, qkv.device)
+        o = attention_ref(q, k, v, scale, causal, dropout_p, keep)  # [B, S, H, D]
     if seq_first:
         o = o.transpose(0, 1)
     return o.flatten(-2).contiguous()
+
+
 # --------------------------------------------------------------------------------------------
 # Rotary embedding
 

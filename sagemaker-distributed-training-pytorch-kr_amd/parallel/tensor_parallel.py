@@ -221,8 +221,8 @@ def _time_us(fn, reps=3):
 
 
 def _wgrad_impl(C, mg, g2, t2):
-    if _WGRAD_IMPL != "auto" or g2.dtype != torch.bfloat16:
-        return _WGRAD_IMPL if g2.dtype == torch.bfloat16 else "blaslt"
+    if _WGRAD_IMPL != "auto" or g2.dtype not in (torch.bfloat16, torch.float16):
+        return _WGRAD_IMPL if g2.dtype in (torch.bfloat16, torch.float16) else "blaslt"
     key = (g2.shape[0], g2.shape[1], t2.shape[1], g2.device.index)
     impl = _WGRAD_CHOICE.get(key)
     if impl is None:
@@ -270,7 +270,7 @@ class DeferredWgrad:
         if M % 32 or N % 8 or K % 8 or mg.numel() != N * K:
             return False
         if g2.is_cuda:
-            return (_FUSED_WGRAD and g2.dtype == torch.bfloat16 and t2.dtype == torch.bfloat16
+            return (_FUSED_WGRAD and g2.dtype in (torch.bfloat16, torch.float16) and t2.dtype == g2.dtype
                     and _ext.use_kernels(g2))
         return self.allow_cpu
 

@@ -246,16 +246,17 @@ def test_cross_entropy_padded_vocab(vocab):
     assert logits.grad[:, vocab:].abs().max().item() == 0
 
 
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("D", [64, 128])
 @pytest.mark.parametrize("causal", [True, False])
 @pytest.mark.parametrize("heads", [(4, 4), (8, 2)])
-def test_flash_attention(D, causal, heads):
+def test_flash_attention(D, causal, heads, dt):
     torch.manual_seed(10)
     B, S = 2, 256
     H, Hkv = heads
-    q = torch.randn(B, S, H, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
-    k = torch.randn(B, S, Hkv, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
-    v = torch.randn(B, S, Hkv, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    q = torch.randn(B, S, H, D, device=DEV, dtype=dt, requires_grad=True)
+    k = torch.randn(B, S, Hkv, D, device=DEV, dtype=dt, requires_grad=True)
+    v = torch.randn(B, S, Hkv, D, device=DEV, dtype=dt, requires_grad=True)
     scale = 1 / math.sqrt(D)
     o = SF.flash_attention(q, k, v, scale, causal)
     qr, kr, vr = (t.detach().float().requires_grad_() for t in (q, k, v))
@@ -269,19 +270,20 @@ def test_flash_attention(D, causal, heads):
         assert err < 0.05 * max(1.0, r.grad.abs().max().item()), err
 
 
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("D", [64, 128])
 @pytest.mark.parametrize("causal", [True, False])
 @pytest.mark.parametrize("heads", [(4, 4), (8, 2)])
-def test_flash_attention_dropout(D, causal, heads):
+def test_flash_attention_dropout(D, causal, heads, dt):
     """In-kernel attention dropout == reference attention with the bit-exact twin of the
     kernels' keep-mask (forward and all three gradients)."""
     torch.manual_seed(12)
     B, S = 2, 256
     H, Hkv = heads
     p, seed, off = 0.1, 1234, 77
-    q = torch.randn(B, S, H, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
-    k = torch.randn(B, S, Hkv, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
-    v = torch.randn(B, S, Hkv, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    q = torch.randn(B, S, H, D, device=DEV, dtype=dt, requires_grad=True)
+    k = torch.randn(B, S, Hkv, D, device=DEV, dtype=dt, requires_grad=True)
+    v = torch.randn(B, S, Hkv, D, device=DEV, dtype=dt, requires_grad=True)
     scale = 1 / math.sqrt(D)
     o = SF._FlashAttn.apply(q, k, v, scale, causal, p, seed, off)
     keep = SF.flash_dropout_keep_mask(B, H, S, p, seed, off, DEV)
@@ -316,3 +318,74 @@ def test_flash_attention_qkv_seq_first_matches_unfused():
     orf.backward(do.float())
     err = (qkv.grad.float() - qr.grad).abs().max().item()
     assert err < 0.05 * max(1.0, qr.grad.abs().max().item())
+
+
+def _attn_check(q, k, v, scale, causal, tol=0.05):
+    o = SF.flash_attention(q, k, v, scale, causal)
+    qr, kr, vr = (t.detach().float().requires_grad_() for t in (q, k, v))
+    orf = SF.attention_ref(qr, kr, vr, scale, causal)
+    err = (o.float() - orf).abs().max().item()
+    assert err < 2e-2 * max(1.0, orf.abs().max().item()), err
+    do = torch.randn_like(o)
+    o.backward(do)
+    orf.backward(do.float())
+    for a, r in ((q, qr), (k, kr), (v, vr)):
+        err = (a.grad.float() - r.grad).abs().max().item()
+        assert err < tol * max(1.0, r.grad.abs().max().item()), err
+
+
+@pytest.mark.parametrize("S,dt", [(1024, torch.bfloat16), (2048, torch.bfloat16), (2048, torch.float16)])
+def test_flash_attention_production_shapes_gqa_d128(S, dt):
+    """LLaMA / GPT-3 6.7B-like attention: D = 128, GQA 32 q / 8 kv heads, long sequences."""
+    torch.manual_seed(13)
+    B, H, Hkv, D = 1, 32, 8, 128
+    q = torch.randn(B, S, H, D, device=DEV, dtype=dt, requires_grad=True)
+    k = torch.randn(B, S, Hkv, D, device=DEV, dtype=dt, requires_grad=True)
+    v = torch.randn(B, S, Hkv, D, device=DEV, dtype=dt, requires_grad=True)
+    _attn_check(q, k, v, 1 / math.sqrt(D), True)
+
+
+@pytest.mark.parametrize("S,D", [(200, 64), (256, 80), (130, 32)])
+def test_flash_attention_padded_shapes_run_on_kernels(S, D):
+    """Causal S % 128 != 0 and head dims outside {64, 128} are zero-padded onto the kernels (exact);
+    nothing drops to the S x S reference on the GPU."""
+    torch.manual_seed(14)
+    B, H = 2, 4
+    q, k, v = (torch.randn(B, S, H, D, device=DEV, dtype=torch.bfloat16, requires_grad=True) for _ in range(3))
+    calls = []
+    real = SF.attention_ref
+    SF.attention_ref = lambda *a, **kw: calls.append(1) or real(*a, **kw)
+    try:
+        o = SF.flash_attention(q, k, v, 1 / math.sqrt(D), True)
+    finally:
+        SF.attention_ref = real
+    assert not calls and o.shape == (B, S, H, D)
+    _attn_check(q, k, v, 1 / math.sqrt(D), True)
+
+
+def test_flash_attention_rejects_unsupported_on_gpu():
+    q = torch.randn(1, 256, 4, 64, device=DEV, dtype=torch.float32)
+    with pytest.raises(RuntimeError, match="bf16 / fp16"):
+        SF.flash_attention(q, q, q, 0.125, True)
+    qb = torch.randn(1, 200, 4, 64, device=DEV, dtype=torch.bfloat16)
+    with pytest.raises(RuntimeError, match="multiple of 128"):
+        SF.flash_attention(qb, qb, qb, 0.125, False)
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+def test_wgrad_mfma_fp16_and_bf16(dt):
+    """Hand-written MFMA wgrad (single and grouped launch) in both 16-bit types vs fp32 matmul."""
+    torch.manual_seed(15)
+    C = _ext.ext()
+    M, N, K = 2048, 1024, 768
+    dy = torch.randn(M, N, device=DEV, dtype=dt)
+    x = torch.randn(M, K, device=DEV, dtype=dt)
+    ref = dy.float().t() @ x.float()
+    mg = torch.ones(N, K, device=DEV, dtype=torch.float32)
+    assert C.wgrad_mfma(mg, dy, x, 0)
+    torch.testing.assert_close(mg, ref + 1, atol=0.05, rtol=1e-3)
+    mg2 = torch.zeros(N, K, device=DEV, dtype=torch.float32)
+    mg3 = torch.zeros(K, N, device=DEV, dtype=torch.float32)
+    assert C.wgrad_grouped([mg2, mg3], [dy, x], [x, dy])
+    torch.testing.assert_close(mg2, ref, atol=0.05, rtol=1e-3)
+    torch.testing.assert_close(mg3, ref.t(), atol=0.05, rtol=1e-3)
