@@ -37,7 +37,7 @@ class CPUOffloadAdam(MixedPrecisionAdam):
         self.zero = ddp.zero if use_distributed_optimizer is None else use_distributed_optimizer
         self.scaler = loss_scaler
         self.step_count = 0
-        self.device = ddp.param_data.device
+        self.device = ddp.grad_data.device
         self.pieces = []
         if self.zero:
             for b in ddp.buckets:

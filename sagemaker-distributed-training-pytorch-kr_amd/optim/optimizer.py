@@ -96,7 +96,7 @@ class MixedPrecisionAdam:
             raise ValueError("ZeRO optimizer needs DistributedDataParallel(use_distributed_optimizer=True)")
         self.scaler = loss_scaler
         self.step_count = 0
-        dev = ddp.param_data.device
+        dev = ddp.grad_data.device   # ZeRO-3 + offload_param: the param shards live on the host
         self.device = dev
         # (start, end) pieces of the flat buffers this rank updates, with their region keys.
         self.pieces = []
@@ -197,13 +197,19 @@ class MixedPrecisionAdam:
                 gr = gr.float()
             if use_k:
                 model_out = None if self.param_is_fp32 else ddp.param_data[s:e]
+                host_out = None
+                if model_out is not None and not model_out.is_cuda:   # offloaded ZeRO-3 param shard
+                    host_out, model_out = model_out, torch.empty(n, dtype=model_out.dtype, device=mst.device)
                 _ext.ext().adam(mst, gr, m, v, model_out, self.lr, self.beta1, self.beta2, self.eps, wd, t,
                                 self.adamw, mul, self.found_inf)
+                if host_out is not None:
+                    host_out.copy_(model_out)
                 if self.param_is_fp32:
                     ddp.param_data[s:e].copy_(mst)
             else:
                 ok = (self.found_inf == 0).float()
-                gg = gr * mul
+                # an overflow step must leave every state untouched: inf * 0 would be NaN
+                gg = torch.where(self.found_inf == 0, gr * mul, torch.zeros_like(gr))
                 if not self.adamw and wd:
                     gg = gg + wd * mst
                 m.mul_(1 - (1 - self.beta1) * ok).add_(gg * ((1 - self.beta1) * ok))

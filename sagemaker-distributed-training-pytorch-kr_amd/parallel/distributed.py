@@ -46,6 +46,7 @@ class Bucket:
     launched: bool = False
     ag_handle: object = None   # in-flight ZeRO param all-gather (overlap_param_gather)
     alone: bool = False        # holds only the pipeline-tied word embedding
+    shard_off: int = 0         # offset of this rank's shard in the ZeRO-2/3 shard stores
 
     @property
     def numel(self):
@@ -76,7 +77,7 @@ class DistributedDataParallel(nn.Module):
     def __init__(self, module: nn.Module, dp_group=None, grad_dtype=torch.float32, bucket_size: int = 40_000_000,
                  overlap_grad_reduce: bool = True, use_distributed_optimizer: bool = False,
                  average_in_collective: bool = True, torch_compat: bool = False,
-                 overlap_param_gather: bool = False):
+                 overlap_param_gather: bool = False, zero_stage: int = 1):
         """``torch_compat=True`` gives drop-in ``torch.nn.parallel.DistributedDataParallel``
         semantics for scripts that drive a stock ``torch.optim`` optimizer: gradient sync is
         finalised automatically at the end of ``backward()`` (autograd-engine callback),
@@ -94,6 +95,14 @@ class DistributedDataParallel(nn.Module):
         self.dp_rank = dist.get_rank(self.dp_group) if self.dp > 1 else 0
         self.overlap = overlap_grad_reduce
         self.zero = use_distributed_optimizer
+        # ZeRO stage of the GRADIENTS: 1 keeps a full fp32 buffer on every rank (reduce-scatter
+        # into it, the optimizer reads only its shard); >= 2 keeps only this rank's shard of
+        # every bucket (``grad_store``, numel / dp) — a bucket's full fp32 buffer exists only
+        # while its gradients are being accumulated and is dropped once its reduce-scatter
+        # launched (DeepSpeed stage 2: reduced every micro-batch, accumulated into the shard).
+        self.zero_stage = int(zero_stage) if use_distributed_optimizer else 0
+        if self.zero_stage >= 2 and (torch_compat or ps.get_state().pp > 1):
+            raise ValueError("ZeRO stage >= 2 gradient sharding needs the explicit-step API and pp == 1")
         self.grad_dtype = grad_dtype
         self.sync_enabled = True
         backend = dist.get_backend(self.dp_group) if self.dp > 1 else "none"
@@ -160,14 +169,31 @@ class DistributedDataParallel(nn.Module):
         self.numel = off
         self.params = params
         self.param_data = torch.zeros(self.numel, dtype=pdtype, device=dev)
-        self.grad_data = torch.zeros(self.numel, dtype=grad_dtype, device=dev)
+        self.shapes = {id(p): (tuple(p.shape), tuple(p.stride())) for p in params}
+        self.grad_store = None
+        self.zero3 = None                                # ZeroParamPartitioner (parallel/zero3.py)
+        self._staging: Dict[int, torch.Tensor] = {}    # bucket index -> full fp32 bucket (stage >= 2)
+        self._rs_inflight: Dict[int, tuple] = {}       # bucket index -> (handle, tmp shard or None)
+        if self.zero_stage >= 2:
+            off = 0
+            for b in self.buckets:
+                b.shard_off = off
+                off += b.numel // self.dp
+            self.grad_store = torch.zeros(off, dtype=grad_dtype, device=dev)
+            self.grad_data = ShardedFlat(self, self.grad_store)
+            self._store_fresh = set(range(len(self.buckets)))
+        else:
+            self.grad_data = torch.zeros(self.numel, dtype=grad_dtype, device=dev)
         with torch.no_grad():
             for p in params:
                 o, n = self.param_index[id(p)]
                 pv = _dense_view(self.param_data[o:o + n], p)
                 pv.copy_(p.data)
                 p.data = pv
-                p.main_grad = _dense_view(self.grad_data[o:o + n], p)
+                if self.zero_stage >= 2:
+                    _make_lazy_grad_param(p, self)
+                else:
+                    p.main_grad = _dense_view(self.grad_data[o:o + n], p)
                 p._smdt_grad_ready = self._on_grad_ready
         self._hooks = [p.register_post_accumulate_grad_hook(self._post_accumulate) for p in params]
         self.regions = self._region_ranges()
@@ -240,6 +266,15 @@ class DistributedDataParallel(nn.Module):
 
     def _on_grad_ready(self, p):
         b = self.param_bucket.get(id(p))
+        if b is not None and self.zero_stage >= 2:
+            left = b.pending.get(id(p), 0) - 1
+            if left > 0:
+                b.pending[id(p)] = left
+                return
+            b.pending.pop(id(p), None)
+            if self.overlap and not b.pending and b.index in self._staging:
+                self._launch(b)
+            return
         if b is None or not self.sync_enabled:
             # Gradients of no_sync micro-batches are only accumulated: readiness is counted for
             # the synchronising pass alone (the counts are re-armed when sync is re-enabled).
@@ -263,6 +298,9 @@ class DistributedDataParallel(nn.Module):
 
     def _launch(self, b: Bucket):
         b.launched = True
+        if self.zero_stage >= 2:
+            self._launch_sharded(b)
+            return
         if self.dp == 1:
             return
         view = self.grad_data[b.start:b.end]
@@ -283,6 +321,68 @@ class DistributedDataParallel(nn.Module):
             else:
                 view.div_(self.dp)
                 b.handle = dist.all_reduce(view, group=self.dp_group, async_op=True)
+
+    # ---------------------------------------------------------------- ZeRO-2 gradient shards
+    def bucket_at(self, i: int) -> Bucket:
+        """The bucket holding flat element ``i``."""
+        import bisect
+        if not hasattr(self, "_starts"):
+            self._starts = [b.start for b in self.buckets]
+        return self.buckets[bisect.bisect_right(self._starts, i) - 1]
+
+    def _main_grad(self, p) -> torch.Tensor:
+        """Stage >= 2: p's fp32 gradient view inside its bucket's accumulation buffer, allocated
+        (zeroed) on first touch in a micro-batch."""
+        b = self.param_bucket[id(p)]
+        buf = self._staging.get(b.index)
+        if buf is None:
+            buf = torch.zeros(b.numel, dtype=self.grad_dtype, device=self.grad_store.device)
+            self._staging[b.index] = buf
+        o, n = self.param_index[id(p)]
+        shape, stride = self.shapes[id(p)]
+        flat = buf[o - b.start:o - b.start + n]
+        return flat.view(shape) if _is_dense(shape, stride) else flat.as_strided(shape, stride)
+
+    def _retire_rs(self, b: Bucket):
+        """Wait for bucket b's previous reduce-scatter and fold its shard into ``grad_store``."""
+        inflight = self._rs_inflight.pop(b.index, None)
+        if inflight is None:
+            return
+        handle, tmp = inflight
+        if handle is not None:
+            handle.wait()
+        if tmp is not None:
+            sh = self.grad_store[b.shard_off:b.shard_off + b.numel // self.dp]
+            sh.add_(tmp)
+
+    def _launch_sharded(self, b: Bucket):
+        """Reduce-scatter bucket b's accumulation buffer into this rank's shard, drop the buffer,
+        and re-arm the bucket for the next micro-batch."""
+        self._retire_rs(b)
+        buf = self._staging.pop(b.index, None)
+        b.pending = {id(q): int(getattr(q, "_smdt_grad_contributions", 1)) for q in b.params}
+        b.launched = False
+        if buf is None:
+            return
+        n = b.numel // self.dp
+        sh = self.grad_store[b.shard_off:b.shard_off + n]
+        fresh = b.index in self._store_fresh
+        self._store_fresh.discard(b.index)
+        out = sh if fresh else torch.empty_like(sh)
+        if self.dp == 1:
+            out.copy_(buf)
+            handle = None
+        elif self.use_avg:
+            handle = dist.reduce_scatter_tensor(out, buf, op=dist.ReduceOp.AVG, group=self.dp_group, async_op=True)
+        else:
+            buf.div_(self.dp)
+            handle = dist.reduce_scatter_tensor(out, buf, group=self.dp_group, async_op=True)
+        self._rs_inflight[b.index] = (handle, None if fresh else out)
+
+    def bucket_shard_grad(self, b: Bucket) -> torch.Tensor:
+        """This rank's reduced gradient shard of bucket b (any stage, after finish_grad_sync)."""
+        s, e = self.shard_range(b)
+        return self.grad_data[s:e]
 
     def set_sync_enabled(self, enabled: bool):
         """Gate bucket launches (gradient accumulation / pipeline schedules).
@@ -317,6 +417,23 @@ class DistributedDataParallel(nn.Module):
     def finish_grad_sync(self):
         """Launch what is left, wait for every bucket, then fix up sequence-parallel grads."""
         self.wait_param_gather()  # params a forward never touched
+        if self.zero_stage >= 2:
+            from .tensor_parallel import flush_deferred_wgrad
+            flush_deferred_wgrad()
+            for b in self.buckets:
+                if b.index in self._staging:
+                    self._launch_sharded(b)
+            for b in self.buckets:
+                self._retire_rs(b)
+            st = self.st
+            if st.tp > 1 and st.tp_group is not None:
+                for b in self.buckets:
+                    if b.region[2]:
+                        dist.all_reduce(self.bucket_shard_grad(b), group=st.tp_group)
+            self._reset_pending()
+            if self.zero3 is not None:
+                self.zero3.end_of_backward()
+            return
         self.start_grad_sync()
         for b in self.buckets:
             if b.handle is not None:
@@ -329,10 +446,20 @@ class DistributedDataParallel(nn.Module):
         self._reset_pending()
 
     def zero_grad_buffer(self):
-        self.grad_data.zero_()
+        if self.zero_stage >= 2:
+            for b in self.buckets:
+                self._retire_rs(b)
+            self._staging.clear()
+            self._store_fresh = set(range(len(self.buckets)))   # the next reduce-scatter writes
+        else:
+            self.grad_data.zero_()
         for p in self.params:
             p.grad = None
         self._reset_pending()
+
+    def grad_memory_numel(self) -> int:
+        """Elements of persistent gradient storage on this rank (ZeRO-2: ~ numel / dp)."""
+        return self.grad_store.numel() if self.grad_store is not None else self.grad_data.numel()
 
     @torch.no_grad()
     def broadcast_params(self):
@@ -344,6 +471,9 @@ class DistributedDataParallel(nn.Module):
         """ZeRO: after each rank updated its shard of ``param_data``, gather the full buffer.
         With ``overlap_param_gather`` the gathers are left in flight (forward order: the last
         bucket holds the first layers) and waited for by the forward pre-hooks."""
+        if self.zero3 is not None:      # stage 3: only the persistent buckets stay gathered
+            self.zero3.after_step()
+            return
         if self.dp == 1:
             return
         self.wait_param_gather()
@@ -368,7 +498,14 @@ class DistributedDataParallel(nn.Module):
 
     def state_dict(self, *args, **kwargs):
         self.wait_param_gather()
+        if self.zero3 is not None:
+            with self.zero3.gathered():
+                return {k: v.detach().clone() for k, v in self.module.state_dict(*args, **kwargs).items()}
         return self.module.state_dict(*args, **kwargs)
+
+    def gathered_params(self):
+        """Context in which every parameter is materialised (a no-op below ZeRO-3)."""
+        return self.zero3.gathered() if self.zero3 is not None else contextlib.nullcontext()
 
     def load_state_dict(self, sd, strict=True):
         return self.module.load_state_dict(sd, strict=strict)
@@ -386,3 +523,58 @@ def _dense_view(flat: torch.Tensor, p: torch.Tensor) -> torch.Tensor:
 
 def _round_up(x, m):
     return ((x + m - 1) // m) * m
+
+
+def _is_dense(shape, stride) -> bool:
+    exp, st = 1, []
+    for d in reversed(shape):
+        st.append(exp)
+        exp *= d
+    return tuple(reversed(st)) == tuple(stride) or len(shape) == 0
+
+
+class ShardedFlat:
+    """Stand-in for a flat buffer of which this rank stores only its shard of every bucket
+    (``store``, laid out bucket by bucket). Indexable by global ``[s:e]`` ranges that lie inside
+    this rank's shard of one bucket — exactly the ranges the ZeRO optimizer touches — so the
+    optimizer code is the same for every stage."""
+
+    def __init__(self, ddp, store: torch.Tensor):
+        self.ddp, self.store = ddp, store
+        self.dtype, self.device = store.dtype, store.device
+        self.is_cuda = store.is_cuda
+
+    def __getitem__(self, sl):
+        s, e = sl.start, sl.stop
+        b = self.ddp.bucket_at(s)
+        bs, be = self.ddp.shard_range(b)
+        if not (bs <= s and e <= be):
+            raise IndexError(f"[{s}:{e}] is outside this rank's shard [{bs}:{be}] of bucket {b.index}")
+        o = b.shard_off + (s - bs)
+        return self.store[o:o + (e - s)]
+
+    def zero_(self):
+        self.store.zero_()
+        return self
+
+    def numel(self):
+        return self.store.numel()
+
+
+class _LazyGradParameter(nn.Parameter):
+    """A Parameter whose ``main_grad`` is resolved by its ZeRO-2 DDP on access (the fp32 bucket
+    buffer it points into exists only while the bucket accumulates)."""
+
+    @property
+    def main_grad(self):
+        return self._smdt_ddp._main_grad(self)
+
+    @main_grad.setter
+    def main_grad(self, v):
+        raise AttributeError("main_grad of a ZeRO-2 parameter is owned by its DistributedDataParallel")
+
+
+def _make_lazy_grad_param(p, ddp):
+    p._smdt_ddp = ddp
+    if type(p) is nn.Parameter:
+        p.__class__ = _LazyGradParameter

@@ -1,0 +1,240 @@
+"""ZeRO stage 3: parameter partitioning with on-demand, prefetched all-gathers.
+
+The reference's Alpaca job runs DeepSpeed ZeRO-3 with ``offload_param: cpu``
+(/root/reference/4_training_alpaca_deepspeed/configs/default_offload_opt_param.json:23-41; the log
+shows the partitioned init "num_elems = 0.16B", NB4:1580, and the offload, NB4:1629). This is the
+MI355X-native equivalent, layered on the flat bucketed DDP buffers (parallel/distributed.py):
+
+* every DP rank keeps only its shard of each parameter bucket (``store``: numel / dp elements, in
+  HBM, or in pinned host memory with ``offload_param``); the full bucket exists only while a
+  block that uses it runs;
+* the model is cut into *blocks* — every child of an ``nn.ModuleList`` (a transformer layer) plus
+  the root (embeddings, final norm, LM head); a block's forward / backward pre-hook gathers the
+  buckets holding its parameters (one RCCL ``all_gather_into_tensor`` per bucket, the H2D copy
+  of an offloaded shard first), its post-hook releases them; reference counts make nested and
+  re-entrant use (activation recompute, the tied LM head inside the root) safe;
+* the order in which buckets are first gathered is traced during the first forward and the
+  first backward; later gathers prefetch the next buckets of that trace, up to
+  ``prefetch_numel`` elements, asynchronously on RCCL's stream, so the gather of layer i + 1
+  runs beside the MFMA work of layer i (``stage3_prefetch_bucket_size``);
+* buckets whose parameters are all below ``persistence_threshold`` elements (biases, norms) stay
+  gathered — re-gathered once after each optimizer step (``stage3_param_persistence_threshold``);
+* gradients take the ZeRO-2 path of the DDP (bucket accumulation buffer -> reduce-scatter into
+  the fp32 gradient shard), so gradient memory is ~ 1/dp as well.
+
+Released parameters keep their Python objects with a 0-element placeholder as ``.data``;
+autograd functions that saved the parameter itself (every linear / embedding / norm of the
+model zoo does) see the re-gathered storage in backward.
+"""
+from __future__ import annotations
+
+import contextlib
+from typing import Dict, List, Optional
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+
+from .distributed import DistributedDataParallel, ShardedFlat, _is_dense
+
+
+class ZeroParamPartitioner:
+    def __init__(self, ddp: DistributedDataParallel, persistence_threshold: int = 0, prefetch_numel: int = 0,
+                 offload: bool = False):
+        if not (ddp.zero and ddp.zero_stage >= 3):
+            raise ValueError("ZeroParamPartitioner needs DistributedDataParallel(use_distributed_optimizer=True, "
+                             "zero_stage=3)")
+        self.ddp = ddp
+        self.dp = ddp.dp
+        self.dev = ddp.grad_store.device
+        self.dtype = ddp.param_dtype
+        self.offload = bool(offload)
+        self.prefetch_numel = int(prefetch_numel)
+        self.persistent = {b.index: max(p.numel() for p in b.params) <= persistence_threshold for b in ddp.buckets}
+        total = sum(b.numel // self.dp for b in ddp.buckets)
+        pin = self.offload and torch.cuda.is_available()
+        self.store = torch.empty(total, dtype=self.dtype, device="cpu" if self.offload else self.dev,
+                                 pin_memory=pin)
+        self.full: Dict[int, torch.Tensor] = {}
+        self.refs: Dict[int, int] = {b.index: 0 for b in ddp.buckets}
+        self.inflight: Dict[int, tuple] = {}
+        self.trace = {"fwd": [], "bwd": []}
+        self._traced = {"fwd": False, "bwd": False}
+        old = ddp.param_data
+        with torch.no_grad():
+            for b in ddp.buckets:
+                s, e = ddp.shard_range(b)
+                self.store[b.shard_off:b.shard_off + (e - s)].copy_(old[s:e])
+                if self.persistent[b.index]:
+                    self.full[b.index] = old[b.start:b.end].clone()
+        ddp.param_data = ShardedFlat(ddp, self.store)
+        ddp.zero3 = self
+        for b in ddp.buckets:
+            if self.persistent[b.index]:
+                self._attach(b, self.full[b.index])
+            else:
+                self._detach(b)
+        del old
+        self._hooks = []
+        self.blocks = self._find_blocks(ddp.module)
+        for mod, bks in self.blocks:
+            self._install(mod, bks, root=mod is ddp.module)
+
+    # ------------------------------------------------------------------ layout
+    def _find_blocks(self, root: nn.Module):
+        """[(module, bucket indices)] — ModuleList children, then the root for everything else."""
+        blocks: List[nn.Module] = []
+        for m in root.modules():
+            if isinstance(m, nn.ModuleList):
+                blocks.extend(m.children())
+        owned = set()
+        out = []
+        for blk in blocks:
+            ids = {id(p) for p in blk.parameters() if id(p) in self.ddp.param_bucket}
+            owned |= ids
+            out.append((blk, sorted({self.ddp.param_bucket[i].index for i in ids})))
+        rest = {id(p) for p in root.parameters() if id(p) in self.ddp.param_bucket} - owned
+        out.append((root, sorted({self.ddp.param_bucket[i].index for i in rest})))
+        return out
+
+    def _install(self, mod: nn.Module, bks: List[int], root: bool):
+        acq_f = lambda *_: self.acquire(bks, "fwd")           # noqa: E731
+        rel = lambda *_: self.release(bks)                     # noqa: E731
+        acq_b = lambda *_: self.acquire(bks, "bwd")            # noqa: E731
+        self._hooks.append(mod.register_forward_pre_hook(acq_f))
+        self._hooks.append(mod.register_forward_hook(lambda *_: rel()))
+        self._hooks.append(mod.register_full_backward_pre_hook(lambda *_: acq_b()))
+        if not root:   # the root's inputs (token ids) carry no gradient: released at end_of_backward
+            self._hooks.append(mod.register_full_backward_hook(lambda *_: rel()))
+
+    def _views(self, b, buf):
+        for p in b.params:
+            o, n = self.ddp.param_index[id(p)]
+            shape, stride = self.ddp.shapes[id(p)]
+            flat = buf[o - b.start:o - b.start + n]
+            yield p, (flat.view(shape) if _is_dense(shape, stride) else flat.as_strided(shape, stride))
+
+    def _attach(self, b, buf):
+        for p, v in self._views(b, buf):
+            p.data = v
+
+    def _detach(self, b):
+        ph = torch.empty(0, dtype=self.dtype, device=self.dev)
+        for p in b.params:
+            p.data = ph
+
+    # ------------------------------------------------------------------ gathers
+    def _gather_async(self, b):
+        n = b.numel // self.dp
+        shard = self.store[b.shard_off:b.shard_off + n]
+        if self.offload:
+            shard = shard.to(self.dev, non_blocking=True)
+        buf = torch.empty(b.numel, dtype=self.dtype, device=self.dev)
+        if self.dp == 1:
+            buf.copy_(shard)
+            return None, buf
+        h = dist.all_gather_into_tensor(buf, shard, group=self.ddp.dp_group, async_op=True)
+        return h, buf
+
+    def _materialise(self, i):
+        b = self.ddp.buckets[i]
+        if i in self.full:
+            return
+        h, buf = self.inflight.pop(i) if i in self.inflight else self._gather_async(b)
+        if h is not None:
+            h.wait()
+        self.full[i] = buf
+        self._attach(b, buf)
+
+    def _prefetch_after(self, i, phase):
+        if self.prefetch_numel <= 0 or not self._traced.get(phase, False):
+            return
+        tr = self.trace[phase]
+        try:
+            k = tr.index(i)
+        except ValueError:
+            return
+        budget = self.prefetch_numel
+        for j in tr[k + 1:]:
+            if budget <= 0:
+                break
+            if j in self.full or j in self.inflight or self.persistent[j]:
+                continue
+            self.inflight[j] = self._gather_async(self.ddp.buckets[j])
+            budget -= self.ddp.buckets[j].numel
+
+    @torch.no_grad()
+    def acquire(self, bks, phase="fwd"):
+        for i in bks:
+            if self.persistent[i]:
+                continue
+            if phase in self.trace and not self._traced[phase] and i not in self.trace[phase]:
+                self.trace[phase].append(i)
+            self.refs[i] += 1
+            self._materialise(i)
+            self._prefetch_after(i, phase)
+
+    def release(self, bks):
+        for i in bks:
+            if self.persistent[i]:
+                continue
+            self.refs[i] = max(self.refs[i] - 1, 0)
+            if self.refs[i] == 0 and i in self.full:
+                del self.full[i]
+                self._detach(self.ddp.buckets[i])
+
+    def end_of_forward_trace(self):
+        self._traced["fwd"] = True
+
+    def end_of_backward(self):
+        """Called by the DDP when the gradient sync finished: drop what backward still holds and
+        freeze the traces (the first iteration defines the prefetch order)."""
+        for i, h in list(self.inflight.items()):
+            if h[0] is not None:
+                h[0].wait()
+        self.inflight.clear()
+        for i in list(self.full):
+            if not self.persistent[i]:
+                self.refs[i] = 0
+                del self.full[i]
+                self._detach(self.ddp.buckets[i])
+        if self.trace["fwd"]:
+            self._traced["fwd"] = True
+        if self.trace["bwd"]:
+            self._traced["bwd"] = True
+
+    @torch.no_grad()
+    def after_step(self):
+        """The optimizer wrote new shards: refresh the persistent (always gathered) buckets."""
+        for b in self.ddp.buckets:
+            if self.persistent[b.index]:
+                h, buf = self._gather_async(b)
+                if h is not None:
+                    h.wait()
+                self.full[b.index].copy_(buf)
+
+    @contextlib.contextmanager
+    def gathered(self):
+        """All parameters materialised (checkpoint save, state_dict, evaluation outside hooks)."""
+        bks = [b.index for b in self.ddp.buckets]
+        self.acquire(bks, "other")
+        try:
+            yield
+        finally:
+            self.release(bks)
+
+    def param_memory_numel(self) -> Dict[str, int]:
+        """Persistent parameter storage on this rank: the shard store (HBM or host) and the
+        always-gathered small buckets."""
+        pers = sum(self.ddp.buckets[i].numel for i, v in self.persistent.items() if v)
+        return {"shard": self.store.numel(), "persistent": pers, "device": str(self.store.device)}
+
+    def remove_hooks(self):
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []
+
+
+def partition_parameters(ddp: DistributedDataParallel, persistence_threshold: int = 0, prefetch_numel: int = 0,
+                         offload: bool = False) -> ZeroParamPartitioner:
+    return ZeroParamPartitioner(ddp, persistence_threshold, prefetch_numel, offload)

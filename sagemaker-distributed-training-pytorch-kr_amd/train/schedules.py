@@ -37,8 +37,15 @@ class _SyncGate:
                 d.sync_enabled = enabled
 
 
+def _scaled(loss, num_microbatches, grad_scale):
+    """Megatron's ``optimizer.scale_loss``: 1 / num_microbatches and the fp16 loss scale (a device
+    tensor — no host sync) applied to the loss before backward."""
+    loss = loss / num_microbatches
+    return loss * grad_scale if grad_scale is not None else loss
+
+
 def forward_backward_no_pipelining(forward_step_func: Callable, data_iterator, model, num_microbatches: int,
-                                   forward_only: bool = False, **_):
+                                   forward_only: bool = False, grad_scale=None, **_):
     """Gradient accumulation over ``num_microbatches``; returns the list of loss dicts.
 
     ``forward_step_func(data_iterator, model) -> (output_tensor, loss_func)`` with
@@ -56,7 +63,7 @@ def forward_backward_no_pipelining(forward_step_func: Callable, data_iterator, m
         loss, info = loss_func(out)
         losses.append(info)
         if not forward_only:
-            (loss / num_microbatches).backward()
+            _scaled(loss, num_microbatches, grad_scale).backward()
     gate.set(True)
     return losses
 
@@ -234,7 +241,7 @@ def _run_backward(out, gout):
 
 def forward_backward_pipelining_without_interleaving(forward_step_func: Callable, data_iterator, model,
                                                      num_microbatches: int, tensor_shape, dtype=torch.bfloat16,
-                                                     forward_only: bool = False, **_):
+                                                     forward_only: bool = False, grad_scale=None, **_):
     """1F1B. ``tensor_shape`` is the [s(/tp), b, h] activation exchanged between stages."""
     models = model if isinstance(model, list) else [model]
     m = models[0]
@@ -259,7 +266,7 @@ def forward_backward_pipelining_without_interleaving(forward_step_func: Callable
         if last:
             loss, info = loss_func(out)
             losses.append(info)
-            return loss / num_microbatches
+            return _scaled(loss, num_microbatches, grad_scale)
         return out
 
     def bwd(inp, out, gout):
@@ -347,7 +354,7 @@ def _p2p_pair(send_next=None, send_prev=None, recv_prev=False, recv_next=False, 
 
 def forward_backward_pipelining_with_interleaving(forward_step_func: Callable, data_iterator, model,
                                                   num_microbatches: int, tensor_shape, dtype=torch.bfloat16,
-                                                  forward_only: bool = False, **_):
+                                                  forward_only: bool = False, grad_scale=None, **_):
     """Interleaved 1F1B over ``vpp`` model chunks per pipeline rank (Megatron's virtual pipeline,
     `--num-layers-per-virtual-pipeline-stage`). Chunk c of rank r holds global stage c * pp + r,
     so activations travel the rank ring pp times per micro-batch; the pipeline bubble shrinks
@@ -404,7 +411,7 @@ def forward_backward_pipelining_with_interleaving(forward_step_func: Callable, d
         if st.is_last_stage():
             loss, info = loss_func(out)
             losses.append(info)
-            out = loss / num_microbatches
+            out = _scaled(loss, num_microbatches, grad_scale)
         outputs[c].append(out)
         return out
 

@@ -23,6 +23,7 @@ kernels (flash attention, fused norm/residual, fused CE). No host synchronisatio
 from __future__ import annotations
 
 import glob
+import contextlib
 import json
 import math
 import os
@@ -293,13 +294,18 @@ class Trainer:
 
     def save_model(self, output_dir: Optional[str] = None):
         """HF-format weights (config.json + model.safetensors) + tokenizer + training args from
-        rank 0; parameters are resident (stages 0-3 here), so no gather is needed."""
+        rank 0; under ZeRO-3 every rank takes part in gathering the partitioned parameters."""
         out = output_dir or self.args.output_dir
+        ctx = contextlib.nullcontext()
         if self.engine is not None:
             self.engine.wait_for_params()
+            ctx = self.engine.gathered_params()
+        with ctx:
+            sd = {k: v.detach().cpu().clone() for k, v in self.model.model.state_dict().items()} \
+                if self.is_main and hasattr(self.model, "model") else None
         if self.is_main:
             os.makedirs(out, exist_ok=True)
-            self.model.save_pretrained(out)
+            self.model.save_pretrained(out, state_dict=sd) if sd is not None else self.model.save_pretrained(out)
             if self.tokenizer is not None and hasattr(self.tokenizer, "save_pretrained"):
                 self.tokenizer.save_pretrained(out)
             with open(os.path.join(out, "training_args.json"), "w") as f:

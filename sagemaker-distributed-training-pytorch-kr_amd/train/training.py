@@ -240,8 +240,10 @@ def train_step(forward_step_func, data_iterator, model, optimizer, scheduler, ar
     st = ps.get_state()
     seq = args.seq_length // args.tensor_model_parallel_size if args.sequence_parallel else args.seq_length
     timers("forward-backward", log_level=1).start(barrier=args.barrier_with_L1_time)
+    scaler = getattr(optimizer, "scaler", None)
     losses = fb(forward_step_func, data_iterator, model, args.num_micro_batches,
-                tensor_shape=(seq, args.micro_batch_size, args.hidden_size), dtype=args.params_dtype)
+                tensor_shape=(seq, args.micro_batch_size, args.hidden_size), dtype=args.params_dtype,
+                grad_scale=scaler.scale if scaler is not None else None)
     model.finish_grad_sync()
     allreduce_word_embedding_grads(unwrap_model(model))
     timers("forward-backward").stop()
@@ -330,7 +332,8 @@ def train(forward_step_func, model, optimizer, scheduler, train_iter, valid_iter
             now = time.time()
             elapsed = (now - t_last) / it_since
             t_last, it_since = now, 0
-            fi = int(optimizer.found_inf.item()) if optimizer.scaler is not None else 0
+            # bf16 runs have no scaler, but the Adam kernel still skips a step with inf / nan grads
+            fi = int(optimizer.found_inf.item()) if hasattr(optimizer, "found_inf") else 0
             ls = float(optimizer.scaler.scale.item()) if optimizer.scaler is not None else None
             gn = float(grad_norm.item()) if grad_norm is not None else None
             if gn is not None and not math.isfinite(gn):

@@ -8,14 +8,17 @@ train.py:243-244). This module is the MI355X-native equivalent:
 * ``resolve_ds_config``  — HF's "auto" rules (micro batch, GA, global batch, clipping, AdamW
   lr/betas/eps/wd, WarmupDecayLR min/max/warmup/total, reduce/prefetch/persistence sizes from the
   hidden size) + consistency checks for explicit values;
-* ``ZeroEngine``         — stage 0: bucketed all-reduce; stages 1-2: bucketed grad
-  reduce-scatter overlapped with backward into a flat fp32 buffer, fused AdamW HIP kernel on this
-  rank's fp32 shard (master + moments), bf16 param all-gather. Stage 3 is accepted and run with
-  stage-2 partitioning of grads/optimizer state while the (bf16) parameters stay resident: one
-  MI355X holds 288 GB, so OPT-125m…LLaMA-7B params (≤13.5 GB) never need per-layer gathers —
-  the reference's CPU param paging exists to fit A100-40GB and is pure overhead here. Optimizer
-  offload to CPU (``offload_optimizer.device == "cpu"``) runs AdamW on the host with the native
-  multithreaded kernel in ``_runtime`` (DeepSpeed's cpu_adam equivalent);
+* ``ZeroEngine``         — stage 0: bucketed all-reduce; stage 1: bucketed grad reduce-scatter
+  overlapped with backward into a full flat fp32 buffer, fused AdamW HIP kernel on this rank's
+  fp32 shard (master + moments), bf16 param all-gather; stage 2: the same with the gradients
+  themselves partitioned — a bucket's fp32 buffer lives only while it accumulates, the persistent
+  gradient storage is this rank's shard (parallel/distributed.py, ``zero_stage``); stage 3: the
+  bf16 parameters partitioned too, gathered per transformer layer with traced prefetch and
+  released after use (parallel/zero3.py), ``stage3_prefetch_bucket_size`` /
+  ``stage3_param_persistence_threshold`` honoured, and ``offload_param: cpu`` keeping the shards in
+  pinned host memory (H2D before each gather). Optimizer offload to CPU
+  (``offload_optimizer.device == "cpu"``) runs AdamW on the host with the native multithreaded
+  kernel in ``_runtime`` (DeepSpeed's cpu_adam equivalent);
 * checkpoints in DeepSpeed's layout (``global_stepN/mp_rank_00_model_states.pt``,
   ``{bf16_,}zero_pp_rank_R_mp_rank_00_optim_states.pt``, ``latest``) and ``zero_to_fp32``
   consolidation.
@@ -109,6 +112,7 @@ class ZeroEngine:
         self.ga = int(ds_config.get("gradient_accumulation_steps", 1))
         self.micro_steps = 0
         self.global_steps = 0
+        self.skipped_steps = 0
         self.clip = float(ds_config.get("gradient_clipping", 0.0) or 0.0)
         dtype = torch.bfloat16 if self.bf16 else torch.float16 if self.fp16 else torch.float32
         with torch.no_grad():  # parameters only: RoPE tables and other buffers stay fp32
@@ -119,18 +123,33 @@ class ZeroEngine:
             model.cfg.params_dtype = dtype
         bucket = int(z.get("reduce_bucket_size", 5e8)) if not _is_auto(z.get("reduce_bucket_size")) else int(5e8)
         bucket = max(bucket, MIN_BUCKET)
-        if self.stage == 3:
-            log(f"[zero] stage 3 requested: grads/optimizer state partitioned as stage 2, params resident "
-                f"({sum(p.numel() for p in model.parameters()) / 1e9:.2f} B params; 288 GB HBM per GPU)")
         off_p = z.get("offload_param", {}) or {}
-        if off_p.get("device") in ("cpu", "nvme"):
-            log("[zero] offload_param ignored: parameters stay in HBM (no CPU<->GPU paging)")
+        self.offload_param = off_p.get("device") in ("cpu", "nvme")
+        if self.offload_param and self.stage < 3:
+            raise ValueError("offload_param needs zero_optimization.stage 3")
+        if off_p.get("device") == "nvme":
+            log("[zero] offload_param nvme: shards kept in pinned host memory instead")
         off_o = z.get("offload_optimizer", {}) or {}
-        self.offload_optimizer = off_o.get("device") == "cpu"
+        self.offload_optimizer = off_o.get("device") in ("cpu", "nvme")
         self.ddp = DistributedDataParallel(model, dp_group=dp_group, grad_dtype=torch.float32, bucket_size=bucket,
                                            overlap_grad_reduce=bool(z.get("overlap_comm", True)),
                                            use_distributed_optimizer=self.stage >= 1,
-                                           overlap_param_gather=self.stage >= 1)
+                                           overlap_param_gather=self.stage in (1, 2),
+                                           zero_stage=max(self.stage, 1))
+        self.partitioner = None
+        if self.stage >= 3:
+            from ..parallel.zero3 import ZeroParamPartitioner
+
+            def _num(key, default):
+                v = z.get(key, default)
+                return default if _is_auto(v) else int(v)
+            self.partitioner = ZeroParamPartitioner(
+                self.ddp, persistence_threshold=_num("stage3_param_persistence_threshold", 100_000),
+                prefetch_numel=_num("stage3_prefetch_bucket_size", 50_000_000), offload=self.offload_param)
+            mem = self.partitioner.param_memory_numel()
+            log(f"[zero] stage 3: {sum(p.numel() for p in model.parameters() if p.numel()) / 1e9:.2f} B params "
+                f"resident before partitioning -> shard {mem['shard'] / 1e9:.3f} B elements on {mem['device']} "
+                f"+ {mem['persistent'] / 1e6:.2f} M persistent; grad shard {self.ddp.grad_memory_numel() / 1e9:.3f} B")
         ocfg = ds_config.get("optimizer", {"type": "AdamW", "params": {}})
         otype = ocfg.get("type", "AdamW").lower()
         if otype not in ("adamw", "adam", "fusedadam", "cpuadam"):
@@ -209,11 +228,20 @@ class ZeroEngine:
             return None
         self.ddp.finish_grad_sync()
         gn = self.optimizer.step()
-        if self.lr_scheduler is not None:
+        # DeepSpeed skips the LR schedule on an fp16 overflow step (_take_model_step); the check
+        # costs one host sync per boundary step and only runs with a loss scaler.
+        overflow = self.optimizer.scaler is not None and bool(self.optimizer.found_inf.item())
+        if overflow:
+            self.skipped_steps += 1
+        elif self.lr_scheduler is not None:
             self.lr_scheduler.step()
         self.ddp.zero_grad_buffer()
         self.global_steps += 1
         return gn
+
+    def gathered_params(self):
+        """Context with every parameter materialised (ZeRO-3 saves / evaluation); no-op below 3."""
+        return self.ddp.gathered_params()
 
     def get_lr(self):
         return [self.optimizer.lr]
@@ -229,7 +257,7 @@ class ZeroEngine:
         meta = {}
         for p in self.ddp.params:
             o, n = self.ddp.param_index[id(p)]
-            meta[names[id(p)]] = (o, n, tuple(p.shape))
+            meta[names[id(p)]] = (o, n, tuple(self.ddp.shapes[id(p)][0]))
         return meta
 
     def save_checkpoint(self, save_dir: str, tag: Optional[str] = None, client_state: Optional[Dict] = None):
@@ -243,8 +271,10 @@ class ZeroEngine:
         opt = {"optimizer_state_dict": self.optimizer.state_dict(), "zero_stage": self.stage,
                "partition_count": self.ddp.dp, "ds_config": self.cfg, "ds_version": "smdt-zero-1"}
         _atomic_save(opt, os.path.join(d, f"{pre}zero_pp_rank_{dp_rank}_mp_rank_00_optim_states.pt"))
+        with self.gathered_params():
+            module_sd = {k: v.detach().cpu().clone() for k, v in self.module.state_dict().items()} if rank == 0 else None
         if rank == 0:
-            state = {"module": {k: v.detach().cpu() for k, v in self.module.state_dict().items()},
+            state = {"module": module_sd,
                      "param_meta": self._param_meta(), "numel": self.ddp.numel,
                      "buffer_names": [], "global_steps": self.global_steps, "micro_steps": self.micro_steps,
                      "lr_scheduler": self.lr_scheduler.state_dict() if self.lr_scheduler else None,
@@ -266,9 +296,22 @@ class ZeroEngine:
         st = torch.load(os.path.join(d, "mp_rank_00_model_states.pt"), map_location="cpu", weights_only=True)
         with torch.no_grad():
             own = dict(self.module.named_parameters())
-            for k, v in st["module"].items():
-                if k in own:
-                    own[k].copy_(v)
+            if self.partitioner is not None:     # write straight into this rank's shards
+                meta = st["param_meta"]
+                for k, v in st["module"].items():
+                    if k in meta:
+                        o, n, _ = meta[k]
+                        flat = v.reshape(-1).to(self.ddp.param_dtype)
+                        for b in self.ddp.buckets:
+                            s0, e0 = self.ddp.shard_range(b)
+                            lo, hi = max(o, s0), min(o + n, e0)
+                            if lo < hi:
+                                self.ddp.param_data[lo:hi].copy_(flat[lo - o:hi - o])
+                self.ddp.all_gather_params()
+            else:
+                for k, v in st["module"].items():
+                    if k in own:
+                        own[k].copy_(v)
         self.global_steps = int(st["global_steps"])
         self.micro_steps = int(st["micro_steps"])
         if self.lr_scheduler is not None and st.get("lr_scheduler"):

@@ -181,7 +181,7 @@ def sft_batches(n=8, b=2, s=16, v=120, seed=3):
     return out
 
 
-def zero_sft_worker(rank, world, stage, ga, steps, offload=False):
+def zero_sft_worker(rank, world, stage, ga, steps, offload=False, offload_param=False, with_mem=False):
     """Data-parallel SFT steps with the ZeroEngine; global batch = world * 2 * ga rows of
     ``sft_batches``. Returns full params after ``steps`` optimizer steps."""
     from smdt_amd.comm import init_distributed
@@ -196,7 +196,9 @@ def zero_sft_worker(rank, world, stage, ga, steps, offload=False):
     cfg = {"optimizer": {"type": "AdamW", "params": {"lr": 1e-3, "betas": [0.9, 0.99], "eps": 1e-8,
                                                      "weight_decay": 0.1}},
            "gradient_accumulation_steps": ga, "gradient_clipping": 1.0,
-           "zero_optimization": {"stage": stage, **({"offload_optimizer": {"device": "cpu"}} if offload else {})}}
+           "zero_optimization": {"stage": stage, **({"offload_optimizer": {"device": "cpu"}} if offload else {}),
+                                 **({"offload_param": {"device": "cpu"}} if offload_param else {}),
+                                 "stage3_param_persistence_threshold": 200, "stage3_prefetch_bucket_size": 4000}}
     eng = ZeroEngine(m, cfg, log=lambda *_: None)
     data = sft_batches(n=steps * ga * 2 // world * world + 8)
     k = 0
@@ -210,7 +212,14 @@ def zero_sft_worker(rank, world, stage, ga, steps, offload=False):
             eng.backward(loss * world / world)
             eng.step()
     eng.wait_for_params()
-    return {n: p.detach().clone() for n, p in m.named_parameters()}
+    total = sum(eng.ddp.shapes[id(p)][0].numel() if hasattr(eng.ddp.shapes[id(p)][0], "numel")
+                else int(torch.tensor(eng.ddp.shapes[id(p)][0]).prod()) for p in eng.ddp.params)
+    mem = {"total": total, "grad": eng.ddp.grad_memory_numel(),
+           "param": (eng.partitioner.param_memory_numel() if eng.partitioner is not None else None),
+           "param_numel_now": sum(p.numel() for p in m.parameters())}
+    with eng.gathered_params():
+        out = {n: p.detach().clone() for n, p in m.named_parameters()}
+    return (out, mem) if with_mem else out
 
 
 def gpt_vpp_worker(rank, world, nmb, p2p=None):

@@ -1,6 +1,7 @@
 """Data helpers (C++ runtime vs Python twins, mmap indexed dataset) and the Megatron recipe
 surface: NB3's hyperparameters parse with the verbatim flag names, derived sizes, and a tiny
 pretrain_gpt run that checkpoints and resumes in the Megatron layout."""
+import math
 import os
 import subprocess
 import sys
@@ -142,3 +143,31 @@ def test_load_without_optimizer_state_refreshes_masters(tmp_path):
     for (s, e, _), mo in zip(opt_b.pieces, opt_b.master_off):
         torch.testing.assert_close(opt_b.master[mo:mo + e - s], ddp_a.param_data[s:e].float())
     np.testing.assert_array_equal(np.random.rand(3), want)
+
+
+@pytest.mark.slow
+def test_pretrain_gpt_fp16_applies_loss_scale(tmp_path):
+    """--fp16: the schedules multiply the loss by the dynamic loss scale before backward (Megatron's
+    optimizer.scale_loss) and the optimizer divides it back out — the reported grad norm is the
+    unscaled one, an overflow step is skipped without corrupting the weights, and training
+    continues with finite losses."""
+    import re
+    script = os.path.join(REPO, "recipes", "3_training_megatron-lm", "pretrain_gpt.py")
+    args = ["--num-layers", "2", "--hidden-size", "64", "--num-attention-heads", "4", "--seq-length", "64",
+            "--max-position-embeddings", "64", "--micro-batch-size", "2", "--global-batch-size", "4",
+            "--lr", "0.001", "--lr-warmup-iters", "1", "--mock-data", "--log-interval", "1", "--eval-interval",
+            "100", "--eval-iters", "1", "--vocab-size", "512", "--tokenizer-type", "NullTokenizer",
+            "--fp16", "true", "--train-iters", "4", "--initial-loss-scale", "4294967296", "--hysteresis", "1"]
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT="29533")
+    r = subprocess.run([sys.executable, script] + args, env=env, capture_output=True, text=True, timeout=600,
+                       cwd=str(tmp_path))
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if "lm loss:" in ln and "iteration" in ln]
+    assert len(lines) == 4
+    losses = [float(re.search(r"lm loss: (\S+)", ln).group(1)) for ln in lines]
+    scales = [float(re.search(r"loss scale: (\S+)", ln).group(1)) for ln in lines]
+    norms = [re.search(r"grad norm: (\S+)", ln).group(1) for ln in lines]
+    assert all(math.isfinite(x) for x in losses), lines
+    assert scales[-1] < scales[0], scales            # overflowing steps halved the scale
+    finite = [float(n) for n in norms if n not in ("nan", "inf")]
+    assert all(n < 100 for n in finite), norms       # unscaled norms (scaled ones would be ~1e9)

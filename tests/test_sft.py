@@ -127,13 +127,30 @@ def test_cpu_adam_matches_torch_adamw():
 
 
 @pytest.mark.slow
-@pytest.mark.parametrize("stage,offload", [(0, False), (2, False), (3, False), (2, True)])
-def test_zero_world2_matches_world1(stage, offload):
-    ref = run_workers(W.zero_sft_worker, 1, 0, 2, 3, False)[0]       # GA 2 on one rank
-    outs = run_workers(W.zero_sft_worker, 2, stage, 1, 3, offload)    # GA 1 on two ranks
+@pytest.mark.parametrize("stage,ga,offload,offload_param", [
+    (0, 1, False, False), (1, 1, False, False), (2, 1, False, False), (2, 2, False, False), (3, 1, False, False),
+    (3, 2, False, False), (2, 1, True, False), (3, 1, True, True), (3, 1, False, True)])
+def test_zero_world2_matches_world1(stage, ga, offload, offload_param):
+    """Every ZeRO stage (2: partitioned gradients; 3: + partitioned parameters gathered per layer,
+    optionally offloaded to pinned host memory, with CPU Adam) reproduces single-rank training."""
+    ref = run_workers(W.zero_sft_worker, 1, 0, 2 * ga, 3, False)[0]      # GA 2*ga on one rank
+    outs = run_workers(W.zero_sft_worker, 2, stage, ga, 3, offload, offload_param)   # GA ga on two ranks
     for r in range(2):
         for k, v in ref.items():
             torch.testing.assert_close(outs[r][k], v, rtol=2e-4, atol=2e-5, msg=f"rank {r} {k}")
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_zero_stage3_memory_is_partitioned(world):
+    """Per-rank persistent gradient and parameter storage ~ total / dp under ZeRO-3 (plus the small
+    always-gathered buckets), and the model holds no full parameter between steps."""
+    outs = run_workers(W.zero_sft_worker, world, 3, 1, 1, False, False, True)
+    for _, mem in outs:
+        total = mem["total"]
+        assert mem["grad"] <= total / world * 1.05 + 4096, mem
+        assert mem["param"]["shard"] <= total / world * 1.05 + 4096, mem
+        assert mem["param"]["persistent"] < 0.05 * total, mem
+        assert mem["param_numel_now"] <= mem["param"]["persistent"] + 4096, mem
 
 
 def _trainer_args(tmp_path, **over):
@@ -166,7 +183,8 @@ def test_trainer_checkpoint_resume_and_zero_to_fp32(tmp_path):
     from smdt_amd.train.zero import get_fp32_state_dict_from_zero_checkpoint
     t = _tiny_trainer(tmp_path, _trainer_args(tmp_path))
     met = t.train()
-    full = {k: v.detach().clone() for k, v in t.model.named_parameters()}
+    with t.engine.gathered_params():            # ZeRO-3 (the reference config): params are partitioned
+        full = {k: v.detach().clone() for k, v in t.model.named_parameters()}
     losses = [h["loss"] for h in t.state["log_history"] if "loss" in h]
     assert len(losses) == 6 and met["train_samples_per_second"] > 0
     ck = tmp_path / "out" / "checkpoint-6"
@@ -180,8 +198,10 @@ def test_trainer_checkpoint_resume_and_zero_to_fp32(tmp_path):
     t3 = _tiny_trainer(tmp_path, _trainer_args(tmp_path, output_dir=tmp_path / "out2",
                                                resume_from_checkpoint=tmp_path / "out" / "checkpoint-3"))
     t3.train()
+    with t3.engine.gathered_params():
+        got = {k: v.detach().clone() for k, v in t3.model.named_parameters()}
     for k, v in full.items():
-        torch.testing.assert_close(dict(t3.model.named_parameters())[k].detach(), v, rtol=1e-5, atol=1e-6)
+        torch.testing.assert_close(got[k], v, rtol=1e-5, atol=1e-6)
 
 
 def test_save_total_limit_rotates(tmp_path):
