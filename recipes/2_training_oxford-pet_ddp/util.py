@@ -12,7 +12,6 @@ Differences (documented, deliberate):
     ``model.head.out_features = num_classes``, leaving a 1000-way head, util.py:53-54);
   * the S3 sync helpers become local directory syncs (the job API has no S3).
 """
-import codecs
 import json
 import logging
 import os
@@ -49,30 +48,33 @@ def torch_model(model_name, num_classes=0, pretrained=True):
 
 
 def accuracy(output, target, topk=(1,)):
-    """Computes the accuracy over the k top predictions for the specified values of k"""
+    """Top-k precision (percent) of ``output`` logits [N, C] against ``target`` [N], one 1-element
+    tensor per k. One ``topk`` call for the largest k; a hit at rank j counts for every k > j."""
     with torch.no_grad():
-        maxk = max(topk)
-        batch_size = target.size(0)
-        _, pred = output.topk(maxk, 1, True, True)
-        pred = pred.t()
-        correct = pred.eq(target.view(1, -1).expand_as(pred)).contiguous()
-        res = []
-        for k in topk:
-            correct_k = correct[:k].reshape(-1).float().sum(0, keepdim=True)
-            res.append(correct_k.mul_(100.0 / batch_size))
-        return res
+        kmax = max(topk)
+        idx = output.topk(kmax, dim=1, largest=True, sorted=True).indices          # [N, kmax]
+        hit_at = (idx == target.unsqueeze(1)).float()                               # [N, kmax]
+        cum = hit_at.cumsum(dim=1).clamp_(max=1.0).sum(dim=0)                       # hits within top-j
+        scale = 100.0 / max(target.numel(), 1)
+        return [cum[k - 1:k] * scale for k in topk]
 
 
 def save_model(state, is_best, args):
+    """Write ``state`` to <model_dir>/checkpoint.pth (temp file + rename, so a crash never leaves
+    a truncated checkpoint) and mirror it to model_best.pth when ``is_best``."""
     logger.info("Saving the model.")
-    filename = os.path.join(args.model_dir, "checkpoint.pth")
-    torch.save(state, filename, _use_new_zipfile_serialization=False)
+    os.makedirs(args.model_dir, exist_ok=True)
+    target = os.path.join(args.model_dir, "checkpoint.pth")
+    tmp = target + ".part"
+    torch.save(state, tmp)
+    os.replace(tmp, target)
     if is_best:
-        shutil.copyfile(filename, os.path.join(args.model_dir, "model_best.pth"))
+        shutil.copy2(target, os.path.join(args.model_dir, "model_best.pth"))
 
 
-class AverageMeter(object):
-    """Computes and stores the average and current value"""
+class AverageMeter:
+    """Running value / count-weighted mean of a metric; ``str()`` renders "name val (avg)" with the
+    format spec ``fmt`` (e.g. ":6.3f")."""
 
     def __init__(self, name, fmt=":f"):
         self.name = name
@@ -80,63 +82,60 @@ class AverageMeter(object):
         self.reset()
 
     def reset(self):
-        self.val = 0
-        self.avg = 0
-        self.sum = 0
+        self.val = self.avg = self.sum = 0
         self.count = 0
 
     def update(self, val, n=1):
         self.val = val
-        self.sum += val * n
         self.count += n
+        self.sum += val * n
         self.avg = self.sum / self.count
 
     def __str__(self):
-        fmtstr = "{name} {val" + self.fmt + "} ({avg" + self.fmt + "})"
-        return fmtstr.format(**self.__dict__)
+        spec = self.fmt[1:] if self.fmt.startswith(":") else self.fmt
+        return f"{self.name} {format(self.val, spec)} ({format(self.avg, spec)})"
 
 
-class ProgressMeter(object):
+class ProgressMeter:
+    """Prints "<prefix>[ batch/total]" followed by every meter, tab separated."""
+
     def __init__(self, num_batches, meters, prefix=""):
-        self.batch_fmtstr = self._get_batch_fmtstr(num_batches)
-        self.meters = meters
+        self.total = int(num_batches)
+        self.width = len(str(self.total))
+        self.meters = list(meters)
         self.prefix = prefix
 
     def display(self, batch):
-        entries = [self.prefix + self.batch_fmtstr.format(batch)]
-        entries += [str(meter) for meter in self.meters]
-        print("\t".join(entries))
-
-    def _get_batch_fmtstr(self, num_batches):
-        num_digits = len(str(num_batches // 1))
-        fmt = "{:" + str(num_digits) + "d}"
-        return "[" + fmt + "/" + fmt.format(num_batches) + "]"
+        head = f"{self.prefix}[{batch:{self.width}d}/{self.total:{self.width}d}]"
+        print("\t".join([head] + [str(m) for m in self.meters]))
 
 
 def adjust_learning_rate(optimizer, epoch, step, len_epoch, args):
-    """Step decay (x0.1 at epoch 30, 60, 80+) with a 5-epoch linear warmup."""
-    factor = epoch // 30
-    if epoch >= 80:
-        factor = factor + 1
-    lr = args.lr * (0.1 ** factor)
+    """Step decay — one x0.1 per 30 epochs plus an extra one from epoch 80 — with a per-step linear
+    warm-up over the first 5 epochs, written into every param group."""
+    decays = epoch // 30 + int(epoch >= 80)
+    lr = args.lr * 0.1 ** decays
     if epoch < 5:
-        lr = lr * float(1 + step + epoch * len_epoch) / (5.0 * len_epoch)
+        lr *= (epoch * len_epoch + step + 1) / (5 * len_epoch)
     if args.rank == 0:
-        print("epoch = {}, step = {}, lr = {}".format(epoch, step, lr))
-    for param_group in optimizer.param_groups:
-        param_group["lr"] = lr
+        print(f"epoch = {epoch}, step = {step}, lr = {lr}")
+    for group in optimizer.param_groups:
+        group["lr"] = lr
 
 
 def save_history(path, history):
-    history_for_json = {k: list(map(float, v)) for k, v in history.items()}
-    with codecs.open(path, "w", encoding="utf-8") as f:
-        json.dump(history_for_json, f, separators=(",", ":"), sort_keys=True, indent=4)
+    """JSON dump of {metric: [floats]} (tensors / numpy scalars converted)."""
+    plain = {name: [float(x) for x in values] for name, values in history.items()}
+    with open(path, "w", encoding="utf-8") as f:
+        f.write(json.dumps(plain, sort_keys=True, indent=4, separators=(",", ":")))
 
 
 def to_python_float(t):
-    if hasattr(t, "item"):
-        return t.item()
-    elif hasattr(t, "index"):
+    """A Python number from a 0-d / 1-element tensor, a sequence, or a number."""
+    item = getattr(t, "item", None)
+    if callable(item):
+        return item()
+    if isinstance(t, (list, tuple)):
         return t[0]
     return t
 

@@ -22,6 +22,8 @@ import numpy as np
 import torch
 import torch.nn.functional as F
 
+from . import augment as A
+
 IMG_EXTENSIONS = (".jpg", ".jpeg", ".png", ".ppm", ".bmp", ".pgm", ".tif", ".tiff", ".webp")
 IMAGENET_MEAN = (0.485, 0.456, 0.406)
 IMAGENET_STD = (0.229, 0.224, 0.225)
@@ -80,12 +82,14 @@ class GpuAugment:
     """Batched train / eval transforms on the device (uint8 NCHW in, normalised float out)."""
 
     def __init__(self, out_size=(224, 224), train=True, scale=(0.08, 1.0), ratio=(3 / 4, 4 / 3), vflip_p=0.5,
-                 noise_p=0.5, blur_p=0.3, color_p=0.5, mean=IMAGENET_MEAN, std=IMAGENET_STD,
+                 noise_p=0.2, blur_p=0.2, color_p=0.3, hsv_p=0.3, mean=IMAGENET_MEAN, std=IMAGENET_STD,
                  dtype=torch.float32, channels_last=True):
         self.out_size = out_size
         self.train = train
         self.scale, self.ratio = scale, ratio
+        # defaults = the reference pipeline's probabilities (pytorch_oxford_ddp.py:140-160)
         self.vflip_p, self.noise_p, self.blur_p, self.color_p = vflip_p, noise_p, blur_p, color_p
+        self.hsv_p = hsv_p
         self.mean = torch.tensor(mean).view(1, 3, 1, 1)
         self.std = torch.tensor(std).view(1, 3, 1, 1)
         self.dtype = dtype
@@ -117,23 +121,18 @@ class GpuAugment:
             theta[:, 1, 2] = cy * 2 - 1
             grid = F.affine_grid(theta, (n, 3) + tuple(self.out_size), align_corners=False)
             x = F.grid_sample(x, grid, mode="bilinear", padding_mode="reflection", align_corners=False)
-            # brightness / contrast / saturation jitter on a subset
-            cm = (torch.rand(n, 1, 1, 1, device=dev, generator=generator) < self.color_p).float()
-            b = 1 + cm * (torch.rand(n, 1, 1, 1, device=dev, generator=generator) * 0.4 - 0.2)
-            c = 1 + cm * (torch.rand(n, 1, 1, 1, device=dev, generator=generator) * 0.4 - 0.2)
-            s = 1 + cm * (torch.rand(n, 1, 1, 1, device=dev, generator=generator) * 0.6 - 0.3)
-            mu = x.mean(dim=(1, 2, 3), keepdim=True)
-            x = (x - mu) * c + mu * b
-            gray = x.mean(dim=1, keepdim=True)
-            x = (x - gray) * s + gray
-            # random 3x3 box blur (depthwise conv) on a subset
-            bm = (torch.rand(n, 1, 1, 1, device=dev, generator=generator) < self.blur_p).float()
-            k = torch.full((3, 1, 3, 3), 1 / 9.0, device=dev)
-            xb = F.conv2d(F.pad(x, (1, 1, 1, 1), mode="reflect"), k, groups=3)
-            x = bm * xb + (1 - bm) * x
-            # gaussian noise on a subset
-            nm = (torch.rand(n, 1, 1, 1, device=dev, generator=generator) < self.noise_p).float()
-            x = x + nm * torch.randn(x.shape, device=dev, generator=generator) * 0.03
+            # the reference's albumentations order and probabilities (data/augment.py)
+            x = A.apply_masked(x, torch.rand(n, device=dev, generator=generator) < self.noise_p,
+                               lambda t: A.gauss_noise(t, generator))
+            x = A.one_of(x, self.blur_p, [(0.2, lambda t: A.motion_blur(t, generator)),
+                                          (0.1, lambda t: A.median_blur(t, 3)),
+                                          (0.1, lambda t: A.box_blur(t, 3))], generator)
+            x = A.one_of(x, self.color_p, [(0.5, lambda t: A.clahe(t, 2.0)),
+                                           (0.5, lambda t: A.sharpen(t, generator)),
+                                           (0.5, lambda t: A.emboss(t, generator)),
+                                           (0.5, lambda t: A.brightness_contrast(t, generator))], generator)
+            x = A.apply_masked(x, torch.rand(n, device=dev, generator=generator) < self.hsv_p,
+                               lambda t: A.hue_saturation_value(t, generator))
             x = x.clamp_(0, 1)
         else:
             if tuple(x.shape[-2:]) != tuple(self.out_size):

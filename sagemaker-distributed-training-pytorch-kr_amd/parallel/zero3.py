@@ -98,6 +98,11 @@ class ZeroParamPartitioner:
         return out
 
     def _install(self, mod: nn.Module, bks: List[int], root: bool):
+        # The root's inputs are token ids: torch warns that its full backward pre-hook fires on
+        # output gradients only — which is exactly when the root's buckets are needed.
+        import warnings
+        warnings.filterwarnings("ignore", message="Full backward hook is firing when gradients are computed with "
+                                "respect to module outputs")
         acq_f = lambda *_: self.acquire(bks, "fwd")           # noqa: E731
         rel = lambda *_: self.release(bks)                     # noqa: E731
         acq_b = lambda *_: self.acquire(bks, "bwd")            # noqa: E731

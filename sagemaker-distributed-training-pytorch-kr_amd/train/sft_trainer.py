@@ -187,7 +187,10 @@ class Trainer:
         self._log0(f"  Total train batch size (w. parallel, distributed & accumulation) = {total_bs:,}")
         self._log0(f"  Gradient Accumulation steps = {ga:,}")
         self._log0(f"  Total optimization steps = {max_steps:,}")
-        self._log0(f"  Number of trainable parameters = {sum(p.numel() for p in self.model.parameters()):,}")
+        shapes = self.engine.ddp.shapes if self.engine is not None else {}   # ZeRO-3: logical shapes
+        nparam = sum(math.prod(shapes[id(p)][0]) if id(p) in shapes else p.numel()
+                     for p in self.model.parameters() if p.requires_grad)
+        self._log0(f"  Number of trainable parameters = {nparam:,}")
         self.model.train()
         tr_loss = torch.zeros((), dtype=torch.float32, device=self.device)
         total_loss = torch.zeros((), dtype=torch.float32, device=self.device)
