@@ -67,6 +67,7 @@ class TransformerConfig:
     recompute_granularity: Optional[str] = None  # "full" | "selective"
     recompute_method: Optional[str] = None       # "uniform" | "block"
     recompute_num_layers: Optional[int] = None
+    distribute_saved_activations: bool = False   # full recompute: saved layer inputs split across TP
 
     def __post_init__(self):
         if self.num_query_groups is None:
@@ -170,6 +171,11 @@ class ParallelAttention(nn.Module):
             p = self.cfg.attention_dropout if training else 0.0
             ctx = SF.flash_attention_qkv(qkv, self.nh, self.nkv, self.hd, seq_first=True, causal=True,
                                          dropout_p=p, rng=get_rng("tp"))
+        elif training and self.cfg.recompute_granularity == "selective" and torch.is_grad_enabled():
+            # Megatron's selective recompute: only the [b, np, s, s] scores / probabilities /
+            # dropout of the unfused core attention are dropped and recomputed in backward (the
+            # flash kernels never store them, so with flash there is nothing to recompute)
+            ctx = rng_checkpoint(lambda t: self.core_attention_unfused(t, training), qkv)
         else:
             ctx = self.core_attention_unfused(qkv, training)
         return self.proj(ctx)                                    # (out, bias)
@@ -360,6 +366,11 @@ class ParallelTransformer(nn.Module):
             n = cfg.recompute_num_layers or len(self.layers)
             if cfg.recompute_method == "block" and i >= n:
                 return layer(x, xb, res)
+            if cfg.distribute_saved_activations and ps.get_state().tp > 1 and not cfg.sequence_parallel:
+                from ..parallel.random import distributed_checkpoint
+                if res is None:
+                    return distributed_checkpoint(lambda a, b_: layer(a, b_, None), x, xb)
+                return distributed_checkpoint(layer, x, xb, res)
             if xb is None:
                 return rng_checkpoint(lambda a, r: layer(a, None, r), x, res)
             return rng_checkpoint(layer, x, xb, res)

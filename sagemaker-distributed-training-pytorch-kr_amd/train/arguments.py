@@ -299,6 +299,13 @@ def validate_args(args, defaults=None):
     assert args.global_batch_size % (args.micro_batch_size * args.data_parallel_size) == 0, \
         "global batch size must be divisible by micro-batch-size * data-parallel-size"
     args.num_micro_batches = args.global_batch_size // (args.micro_batch_size * args.data_parallel_size)
+    if args.rampup_batch_size:
+        if len(args.rampup_batch_size) != 3:
+            raise ValueError("--rampup-batch-size expects <start batch size> <batch size increment> <ramp-up samples>")
+        args.rampup_batch_size = [int(v) for v in args.rampup_batch_size]
+        if args.train_iters is not None and args.train_samples is None:
+            raise ValueError("--rampup-batch-size needs --train-samples (iteration counts vary while ramping)"
+                             " — Megatron's rule")
     if args.num_layers_per_virtual_pipeline_stage is not None:
         # Megatron requires pp > 2 here; the canonical p2p op order (train/schedules.py) makes pp = 2 safe
         assert args.pipeline_model_parallel_size >= 2, "interleaved schedule needs pipeline parallelism"
@@ -344,6 +351,12 @@ def validate_args(args, defaults=None):
         args.sequence_parallel = False
     if args.sequence_parallel:
         args.async_tensor_model_parallel_allreduce = False
+    if args.distribute_saved_activations:
+        # Megatron's rules: only with full recompute and without sequence parallelism
+        if args.recompute_granularity != "full":
+            raise ValueError("--distribute-saved-activations needs --recompute-granularity full")
+        if args.sequence_parallel:
+            raise ValueError("--distribute-saved-activations cannot be combined with --sequence-parallel")
     for k in ("no_save_optim", "no_save_rng", "no_load_optim", "no_load_rng", "use_cpu_initialization"):
         if getattr(args, k) is None:
             setattr(args, k, False)
@@ -389,7 +402,54 @@ def core_transformer_config_from_args(args) -> TransformerConfig:
         bias_dropout_fusion=args.bias_dropout_fusion, use_flash_attn=args.use_flash_attn,
         apply_query_key_layer_scaling=args.apply_query_key_layer_scaling,
         recompute_granularity=args.recompute_granularity, recompute_method=args.recompute_method,
-        recompute_num_layers=args.recompute_num_layers)
+        recompute_num_layers=args.recompute_num_layers,
+        distribute_saved_activations=bool(args.distribute_saved_activations))
+
+
+# ------------------------------------------------------------------------ micro-batch calculator (U2)
+class MicroBatchCalculator:
+    """Megatron's num-microbatches calculator: constant, or ``--rampup-batch-size <start> <incr>
+    <ramp samples>`` (/root/reference/3_training_megatron-lm/megatron/arguments.py:734-745): the
+    global batch grows from ``start`` by ``incr`` every ramp_samples / ((global - start) / incr)
+    consumed samples until it reaches ``--global-batch-size``; micro-batches per step =
+    current global batch / (micro batch x data-parallel size)."""
+
+    def __init__(self, global_batch_size: int, micro_batch_size: int, dp: int, rampup=None):
+        self.gbs, self.mbs, self.dp = int(global_batch_size), int(micro_batch_size), int(dp)
+        self.per = self.mbs * self.dp
+        self.rampup = None
+        if rampup:
+            start, incr, samples = (int(v) for v in rampup)
+            if start <= 0 or incr <= 0 or samples < 0:
+                raise ValueError(f"--rampup-batch-size values must be positive, got {rampup}")
+            diff = self.gbs - start
+            if diff < 0 or diff % incr:
+                raise ValueError(f"global batch {self.gbs} - start {start} must be a non-negative multiple of {incr}")
+            if start % self.per or incr % self.per:
+                raise ValueError(f"ramp-up start {start} and increment {incr} must be multiples of micro batch "
+                                 f"x dp = {self.per}")
+            self.rampup = (start, incr, samples, samples / max(diff // incr, 1))
+        self.current = self.gbs if self.rampup is None else self.rampup[0]
+
+    def update(self, consumed_samples: int):
+        if self.rampup is not None:
+            start, incr, samples, per_incr = self.rampup
+            if consumed_samples > samples:
+                self.current = self.gbs
+            else:
+                self.current = min(self.gbs, start + int(consumed_samples / per_incr) * incr)
+        return self.current
+
+    @property
+    def num_micro_batches(self) -> int:
+        return self.current // self.per
+
+    def describe(self) -> str:
+        if self.rampup is None:
+            return f"setting number of micro-batches to constant {self.num_micro_batches}"
+        start, incr, samples, _ = self.rampup
+        return (f"will use batch size rampup starting from global batch size {start} to global batch size "
+                f"{self.gbs} with batch size increments {incr} over {samples} samples.")
 
 
 # ------------------------------------------------------------------------ global singletons (U2)

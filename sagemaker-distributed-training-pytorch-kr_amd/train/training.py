@@ -69,7 +69,18 @@ def initialize_megatron(extra_args_provider=None, args_defaults=None, ignore_unk
     ps.initialize_model_parallel(args.tensor_model_parallel_size, args.pipeline_model_parallel_size,
                                  args.virtual_pipeline_model_parallel_size)
     model_parallel_seed(args.seed, args.data_parallel_random_init)
-    print_rank_0(f"setting number of micro-batches to constant {args.num_micro_batches}")
+    args.mb_calculator = A.MicroBatchCalculator(args.global_batch_size, args.micro_batch_size,
+                                                args.data_parallel_size, args.rampup_batch_size)
+    print_rank_0(args.mb_calculator.describe())
+    args.current_global_batch_size = args.mb_calculator.current
+    if args.rampup_batch_size and args.train_samples:
+        # Megatron's update_train_iters: iterations while ramping + the rest at the full batch
+        consumed, iters = 0, 0
+        while consumed < args.train_samples:
+            consumed += args.mb_calculator.update(consumed)
+            iters += 1
+        args.mb_calculator.update(0)
+        args.train_iters = iters
     tok = None
     if args.tokenizer_type is not None and not (args.mock_data and args.vocab_file is None):
         tok, padded = build_tokenizer(args.tokenizer_type, args.vocab_file, args.merge_file, args.tokenizer_model,
@@ -199,7 +210,7 @@ def training_log(loss_dict, total_loss_dict, lr, iteration, loss_scale, report_m
     s += f" consumed samples: {args.consumed_train_samples:12d} |"
     s += f" elapsed time per iteration (ms): {elapsed_per_iter * 1000.0:.1f} |"
     s += f" learning rate: {lr:.3E} |"
-    s += f" global batch size: {args.global_batch_size:5d} |"
+    s += f" global batch size: {getattr(args, 'current_global_batch_size', args.global_batch_size):5d} |"
     for k in sorted(total_loss_dict):
         if k in ("skipped", "iters", "nan"):
             continue
@@ -318,13 +329,19 @@ def train(forward_step_func, model, optimizer, scheduler, train_iter, valid_iter
     while iteration < args.train_iters:
         _profiler(args, iteration, True)
         maybe_inject_fault(iteration + 1)
+        mbc = getattr(args, "mb_calculator", None)
+        if mbc is not None:   # --rampup-batch-size: micro-batches per step follow consumed samples
+            args.current_global_batch_size = mbc.update(args.consumed_train_samples)
+            args.num_micro_batches = mbc.num_micro_batches
+        else:
+            args.current_global_batch_size = args.global_batch_size
         with StepWatchdog(watchdog_s):
             loss_dict, lr, grad_norm = train_step(forward_step_func, train_iter, model, optimizer, scheduler, args)
         collective_check_from_env(iteration + 1)
         iteration += 1
         it_since += 1
         args.iteration = iteration
-        args.consumed_train_samples += args.global_batch_size
+        args.consumed_train_samples += args.current_global_batch_size
         _profiler(args, iteration, False)
         if iteration % args.log_interval == 0:
             if torch.cuda.is_available():

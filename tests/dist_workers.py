@@ -444,3 +444,31 @@ def tp_overlap_order_worker(rank, world):
     torch.testing.assert_close(wr.main_grad, w2r.grad[:, rank * o:(rank + 1) * o])
     dist.destroy_process_group()
     return events
+
+
+def saved_bytes_worker(rank, world, tp, cfg_over):
+    """TP run of the tiny GPT with ``cfg_over`` (recompute settings): returns (loss, grads, meta,
+    bytes of tensors autograd saved during forward)."""
+    import torch.distributed as dist
+    from smdt_amd.comm import init_distributed
+    from smdt_amd.models.gpt import GPTModel
+    from smdt_amd.models.transformer import TransformerConfig
+    from smdt_amd.parallel import state as ps
+    init_distributed("gloo")
+    st = ps.initialize_model_parallel(tp, 1)
+    cfg = TransformerConfig(**{**TINY, **cfg_over})
+    m = GPTModel(cfg)
+    tokens, labels = _batch()
+    seen = {}
+
+    def pack(t):
+        seen[id(t)] = t.numel() * t.element_size() if t.layout == torch.strided else 0
+        return t
+    with torch.autograd.graph.saved_tensors_hooks(pack, lambda t: t):
+        loss = m(tokens, None, None, labels=labels)
+    loss.mean().backward()
+    grads = {n: p.grad.detach().clone() for n, p in m.named_parameters() if p.grad is not None}
+    meta = {"tp_rank": st.tp_rank, "pp_rank": 0, "layer_offset": 0}
+    if dist.is_initialized():
+        dist.destroy_process_group()
+    return loss.detach(), grads, meta, sum(seen.values())

@@ -171,3 +171,25 @@ def test_pretrain_gpt_fp16_applies_loss_scale(tmp_path):
     assert scales[-1] < scales[0], scales            # overflowing steps halved the scale
     finite = [float(n) for n in norms if n not in ("nan", "inf")]
     assert all(n < 100 for n in finite), norms       # unscaled norms (scaled ones would be ~1e9)
+
+
+@pytest.mark.slow
+def test_pretrain_gpt_rampup_batch_size(tmp_path):
+    """--rampup-batch-size 2 2 24 with --train-samples: the logged global batch size ramps 2 -> 4 -> 6
+    -> 8 (micro-batches per step follow consumed samples) and training ends at the sample budget."""
+    import re
+    script = os.path.join(REPO, "recipes", "3_training_megatron-lm", "pretrain_gpt.py")
+    args = ["--num-layers", "2", "--hidden-size", "64", "--num-attention-heads", "4", "--seq-length", "64",
+            "--max-position-embeddings", "64", "--micro-batch-size", "2", "--global-batch-size", "8",
+            "--rampup-batch-size", "2", "2", "24", "--train-samples", "60", "--lr", "0.001",
+            "--mock-data", "--log-interval", "1", "--eval-interval", "1000", "--eval-iters", "1",
+            "--vocab-size", "512", "--tokenizer-type", "NullTokenizer"]
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT="29539")
+    r = subprocess.run([sys.executable, script] + args, env=env, capture_output=True, text=True, timeout=600,
+                       cwd=str(tmp_path))
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    gbs = [int(x) for x in re.findall(r"global batch size:\s+(\d+)", r.stdout)]
+    cons = [int(x) for x in re.findall(r"consumed samples:\s+(\d+)", r.stdout)]
+    assert gbs[0] == 2 and gbs[-1] == 8 and gbs == sorted(gbs) and {2, 4, 6, 8} <= set(gbs), gbs
+    assert cons[-1] >= 60 and cons[-2] < 60, cons
+    assert "batch size rampup starting from global batch size 2" in r.stdout

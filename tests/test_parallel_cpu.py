@@ -217,3 +217,41 @@ def test_ring_exchange_p2p_flag_is_rejected():
     with pytest.raises(ValueError, match="ring_exchange"):
         S.configure_p2p(argparse.Namespace(use_ring_exchange_p2p=True))
     S.configure_p2p()
+
+
+def test_distribute_saved_activations_shards_checkpoint_inputs():
+    """--distribute-saved-activations: full-recompute gradients unchanged, and each TP rank keeps
+    only a 1/tp slice of every checkpointed layer input (fewer saved bytes than plain recompute)."""
+    ref_loss, ref = W.gpt_reference()
+    full = {"recompute_granularity": "full", "recompute_method": "uniform"}
+    plain = run_workers(W.saved_bytes_worker, 2, 2, full)
+    dist_ = run_workers(W.saved_bytes_worker, 2, 2, {**full, "distribute_saved_activations": True})
+    for loss, grads, meta, _ in dist_:
+        _close(loss, ref_loss)
+        _check_tp_grads(ref, grads, meta, 2)
+    assert dist_[0][3] < plain[0][3], (dist_[0][3], plain[0][3])
+
+
+def test_selective_recompute_drops_attention_scores():
+    """Selective recompute (unfused attention): identical gradients, fewer bytes saved in forward
+    (the [b, np, s, s] scores / probabilities are recomputed)."""
+    outs = {g: run_workers(W.saved_bytes_worker, 1, 1, {"use_flash_attn": False, "recompute_granularity": g})[0]
+            for g in (None, "selective")}
+    for n, g in outs[None][1].items():
+        torch.testing.assert_close(outs["selective"][1][n], g, atol=1e-6, rtol=1e-5)
+    assert outs["selective"][3] < outs[None][3]
+
+
+def test_rampup_batch_size_calculator():
+    from smdt_amd.train.arguments import MicroBatchCalculator
+    c = MicroBatchCalculator(global_batch_size=32, micro_batch_size=2, dp=2, rampup=[8, 8, 96])
+    seen = []
+    consumed = 0
+    while consumed <= 140:
+        seen.append(c.update(consumed))
+        consumed += seen[-1]
+    assert seen[0] == 8 and seen[-1] == 32 and seen == sorted(seen)
+    assert set(seen) == {8, 16, 24, 32}                  # +8 every 96 / 3 = 32 samples
+    assert c.num_micro_batches == 32 // 4
+    with pytest.raises(ValueError):
+        MicroBatchCalculator(32, 2, 2, rampup=[6, 8, 96])  # not a multiple of mbs x dp
