@@ -33,7 +33,8 @@ from smdt_amd.parallel import state as ps  # noqa: E402
 from smdt_amd.parallel import tensor_parallel  # noqa: E402
 from smdt_amd.train.arguments import core_transformer_config_from_args, get_args, get_timers, get_tokenizer  # noqa: E402
 from smdt_amd.train.training import ModelType, pretrain  # noqa: E402
-from smdt_amd.train.utils import average_losses_across_data_parallel_group, get_ltor_masks_and_position_ids  # noqa: E402
+from smdt_amd.train.utils import (average_losses_across_data_parallel_group, context_parallel_slice,  # noqa: E402
+                                  get_ltor_masks_and_position_ids)
 
 
 def model_provider(pre_process=True, post_process=True):
@@ -59,6 +60,8 @@ def get_batch(data_iterator):
     attention_mask, loss_mask, position_ids = get_ltor_masks_and_position_ids(
         tokens, tokenizer.eod, args.reset_position_ids, args.reset_attention_mask, args.eod_mask_loss,
         build_attention_mask=need_mask)
+    # --context-parallel-size: this rank keeps its contiguous chunk of the sequence
+    tokens, labels, loss_mask, position_ids = context_parallel_slice(tokens, labels, loss_mask, position_ids)
     return tokens, labels, loss_mask, attention_mask, position_ids
 
 

@@ -138,7 +138,9 @@ class GPTModel(nn.Module):
     def forward(self, tokens, position_ids=None, attention_mask=None, labels=None):
         if self.pre_process:
             if position_ids is None:
-                position_ids = torch.arange(tokens.shape[1], device=tokens.device).unsqueeze(0).expand_as(tokens)
+                # with context parallelism ``tokens`` is this rank's chunk cp_rank of the sequence
+                off = ps.get_state().cp_rank * tokens.shape[1]
+                position_ids = (torch.arange(tokens.shape[1], device=tokens.device) + off).unsqueeze(0).expand_as(tokens)
             x = self._embed(tokens, position_ids)
         else:
             x = self.input_tensor

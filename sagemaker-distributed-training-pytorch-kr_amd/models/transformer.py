@@ -160,11 +160,32 @@ class ParallelAttention(nn.Module):
         ctx = torch.bmm(probs.view(b * self.nh, s, s), vh)          # [b*nh, s, d]
         return ctx.view(b, self.nh, s, self.hd).permute(2, 0, 1, 3).reshape(s, b, self.nh * self.hd)
 
+    def core_attention_context_parallel(self, qkv, training):
+        """Context parallelism: ``qkv`` holds this CP rank's contiguous
+        sequence chunk; two all-to-alls re-shard it to the FULL sequence for nh/cp heads around the
+        unchanged causal flash kernel (parallel/context_parallel.py) and back."""
+        from ..parallel.context_parallel import ulysses_attention
+        st = ps.get_state()
+        q, k, v = SF._qkv_views(qkv, self.nh, self.nkv, self.hd, False)   # [s/cp, b, heads, d]
+        p = self.cfg.attention_dropout if training else 0.0
+        if not self.cfg.use_flash_attn:
+            raise NotImplementedError("context parallelism runs attention through the flash kernels "
+                                      "(--use-flash-attn)")
+        ctx = ulysses_attention(q, k, v, group=st.cp_group, causal=True, scale=1.0 / math.sqrt(self.hd),
+                                dropout_p=p, rng=get_rng("tp"))
+        return ctx.reshape(ctx.shape[0], ctx.shape[1], self.nh * self.hd)
+
     def forward(self, x, training=True):
         qkv = self.qkv(x)                                        # [s, b, (nh + 2 nkv) d]
+        cp = ps.get_state().cp
         if self.rope is not None:
             cos, sin, rot = self.rope
+            if cp > 1:  # this rank's positions: chunk cp_rank of the full sequence
+                off = ps.get_state().cp_rank * qkv.shape[0]
+                cos, sin = cos[off: off + qkv.shape[0]], sin[off: off + qkv.shape[0]]
             qkv = _RopeQKV.apply(qkv, cos, sin, rot, self.nh, self.nkv, self.hd)
+        if cp > 1:
+            return self.proj(self.core_attention_context_parallel(qkv, training))
         if self.cfg.use_flash_attn:
             # attention dropout runs inside the flash kernels; heads are TP-sharded, so the mask
             # comes from the per-TP-rank stream (Megatron forks the model-parallel tracker here)

@@ -90,7 +90,8 @@ class DistributedDataParallel(nn.Module):
         self._callback_queued = False
         st = ps.get_state()
         self.st = st
-        self.dp_group = dp_group if dp_group is not None else st.dp_group
+        # gradient reduction over dp x cp: context-parallel ranks hold the same parameters
+        self.dp_group = dp_group if dp_group is not None else (st.dp_cp_group or st.dp_group)
         self.dp = dist.get_world_size(self.dp_group) if (dist.is_initialized() and self.dp_group is not None) else 1
         self.dp_rank = dist.get_rank(self.dp_group) if self.dp > 1 else 0
         self.overlap = overlap_grad_reduce
@@ -463,7 +464,7 @@ class DistributedDataParallel(nn.Module):
 
     @torch.no_grad()
     def broadcast_params(self):
-        src = self.st.dp_ranks[0] if self.st.dp_ranks else 0
+        src = dist.get_global_rank(self.dp_group, 0) if self.dp > 1 else dist.get_rank()
         dist.broadcast(self.param_data, src=src, group=self.dp_group)
 
     @torch.no_grad()

@@ -30,11 +30,15 @@ def get_rng(kind: str = "default") -> PhiloxState:
 def model_parallel_seed(seed: int, data_parallel_random_init: bool = False):
     """Seed torch / numpy / python and both Philox streams, Megatron-style:
     default = seed + 100 * pp_rank (+ 10 * dp_rank with data-parallel random init),
-    tensor-parallel = default + 2718 + tp_rank."""
+    tensor-parallel = default + 2718 + tp_rank. Context-parallel ranks see different tokens (and,
+    inside Ulysses attention, different heads), so cp_rank > 0 shifts both streams by 7919 * cp_rank
+    (cp = 1 leaves every seed unchanged)."""
     st = ps.get_state()
     s = seed + 100 * st.pp_rank
     if data_parallel_random_init:
         s += 10 * st.dp_rank
+    if getattr(st, "cp", 1) > 1:
+        s += 7919 * st.cp_rank
     _pyrandom.seed(s)
     np.random.seed(s % (2 ** 32))
     torch.manual_seed(s)

@@ -5,10 +5,14 @@ reference's log shows rank 0 creating world/TP/PP/DP/MP communicators, NB3:1214,
 `megatron/data/gpt_dataset.py:462-469` all-reduces over the DP and PP groups).
 
 Rank layout (identical to Megatron so checkpoints and logs line up): TP is the fastest-varying
-dimension, then DP, then PP.  world = tp * dp * pp.
+dimension, then CP (context parallel, Megatron-core's order), then DP, then PP.
+world = tp * cp * dp * pp.
 
     tp group : consecutive ranks                     e.g. TP2 PP2 DP2 -> {0,1} {2,3} {4,5} {6,7}
-    dp group : same (pp stage, tp rank)                                  {0,2} {1,3} {4,6} {5,7}
+    cp group : same (pp, dp, tp), stride tp           (cp = 1: singletons)
+    dp group : same (pp stage, cp rank, tp rank)                         {0,2} {1,3} {4,6} {5,7}
+    dp_cp    : same (pp stage, tp rank) — the gradient-reduction group (CP ranks hold the same
+               parameters and see different tokens, so their gradients are averaged like DP's)
     pp group : stride world/pp                                           {0,4} {1,5} {2,6} {3,7}
 
 On one MI355X node every GPU pair has its own xGMI link (fully connected, no switch), so the
@@ -29,16 +33,21 @@ class ParallelState:
     tp: int = 1
     pp: int = 1
     dp: int = 1
+    cp: int = 1
     rank: int = 0
     world: int = 1
     tp_group: object = None
     pp_group: object = None
     dp_group: object = None
+    cp_group: object = None
+    dp_cp_group: object = None       # gradient reduction over dp x cp (== dp_group when cp == 1)
     mp_group: object = None          # tp x pp (model-parallel)
     embd_group: object = None        # first + last pipeline stage (tied embeddings)
     tp_ranks: List[int] = field(default_factory=list)
     pp_ranks: List[int] = field(default_factory=list)
     dp_ranks: List[int] = field(default_factory=list)
+    cp_ranks: List[int] = field(default_factory=list)
+    dp_cp_ranks: List[int] = field(default_factory=list)
     embd_ranks: List[int] = field(default_factory=list)
     virtual_pp: Optional[int] = None
     virtual_pp_rank: int = 0
@@ -55,6 +64,15 @@ class ParallelState:
     @property
     def dp_rank(self) -> int:
         return self.dp_ranks.index(self.rank) if self.dp_ranks else 0
+
+    @property
+    def cp_rank(self) -> int:
+        return self.cp_ranks.index(self.rank) if self.cp_ranks else 0
+
+    @property
+    def dp_cp_rank(self) -> int:
+        """Rank in the gradient-reduction (dp x cp) group: the ZeRO shard index."""
+        return self.dp_cp_ranks.index(self.rank) if self.dp_cp_ranks else self.dp_rank
 
     def is_first_stage(self, ignore_virtual: bool = False) -> bool:
         if not ignore_virtual and self.virtual_pp is not None and self.virtual_pp_rank != 0:
@@ -86,41 +104,67 @@ def _new_group(ranks, backend=None):
 
 
 def initialize_model_parallel(tensor_model_parallel_size: int = 1, pipeline_model_parallel_size: int = 1,
-                              virtual_pipeline_model_parallel_size: Optional[int] = None) -> ParallelState:
+                              virtual_pipeline_model_parallel_size: Optional[int] = None,
+                              context_parallel_size: int = 1) -> ParallelState:
     """Create every group. Must be called on all ranks after ``init_process_group``."""
     global _STATE
-    tp, pp = int(tensor_model_parallel_size), int(pipeline_model_parallel_size)
+    tp, pp, cp = int(tensor_model_parallel_size), int(pipeline_model_parallel_size), int(context_parallel_size)
     if not dist.is_initialized():
         _STATE = ParallelState(tp=1, pp=1, dp=1, rank=0, world=1, tp_ranks=[0], pp_ranks=[0], dp_ranks=[0],
-                               embd_ranks=[0])
-        if tp != 1 or pp != 1:
-            raise RuntimeError("model parallelism requires torch.distributed to be initialised")
+                               cp_ranks=[0], dp_cp_ranks=[0], embd_ranks=[0])
+        if tp != 1 or pp != 1 or cp != 1:
+            raise RuntimeError("model / context parallelism requires torch.distributed to be initialised")
         return _STATE
     world, rank = dist.get_world_size(), dist.get_rank()
-    if world % (tp * pp) != 0:
-        raise RuntimeError(f"world size {world} not divisible by tp({tp}) * pp({pp})")
-    dp = world // (tp * pp)
-    st = ParallelState(tp=tp, pp=pp, dp=dp, rank=rank, world=world, virtual_pp=virtual_pipeline_model_parallel_size)
+    if world % (tp * pp * cp) != 0:
+        raise RuntimeError(f"world size {world} not divisible by tp({tp}) * pp({pp}) * cp({cp})")
+    dp = world // (tp * pp * cp)
+    st = ParallelState(tp=tp, pp=pp, dp=dp, cp=cp, rank=rank, world=world,
+                       virtual_pp=virtual_pipeline_model_parallel_size)
     stage = world // pp
-    # data-parallel groups
+
+    def rk(p, d, c, t):
+        return p * stage + d * (tp * cp) + c * tp + t
+
+    # data-parallel groups (same pp stage, cp rank, tp rank)
     for p in range(pp):
-        for t in range(tp):
-            ranks = [p * stage + d * tp + t for d in range(dp)]
-            g = _new_group(ranks)
-            if rank in ranks:
-                st.dp_group, st.dp_ranks = g, ranks
+        for c in range(cp):
+            for t in range(tp):
+                ranks = [rk(p, d, c, t) for d in range(dp)]
+                g = _new_group(ranks)
+                if rank in ranks:
+                    st.dp_group, st.dp_ranks = g, ranks
+    # context-parallel groups (same pp, dp, tp) and the dp x cp gradient groups (same pp, tp)
+    if cp > 1:
+        for p in range(pp):
+            for d in range(dp):
+                for t in range(tp):
+                    ranks = [rk(p, d, c, t) for c in range(cp)]
+                    g = _new_group(ranks)
+                    if rank in ranks:
+                        st.cp_group, st.cp_ranks = g, ranks
+        for p in range(pp):
+            for t in range(tp):
+                ranks = sorted(rk(p, d, c, t) for d in range(dp) for c in range(cp))
+                g = _new_group(ranks)
+                if rank in ranks:
+                    st.dp_cp_group, st.dp_cp_ranks = g, ranks
+    else:
+        st.cp_ranks = [rank]
+        st.dp_cp_group, st.dp_cp_ranks = st.dp_group, st.dp_ranks
     # tensor-parallel groups
     for i in range(world // tp):
         ranks = list(range(i * tp, (i + 1) * tp))
         g = _new_group(ranks)
         if rank in ranks:
             st.tp_group, st.tp_ranks = g, ranks
-    # model-parallel (tp x pp) groups: same dp index
+    # model-parallel (tp x pp) groups: same dp and cp index
     for d in range(dp):
-        ranks = [p * stage + d * tp + t for p in range(pp) for t in range(tp)]
-        g = _new_group(sorted(ranks))
-        if rank in ranks:
-            st.mp_group = g
+        for c in range(cp):
+            ranks = sorted(rk(p, d, c, t) for p in range(pp) for t in range(tp))
+            g = _new_group(ranks)
+            if rank in ranks:
+                st.mp_group = g
     # pipeline groups + embedding groups
     for i in range(stage):
         ranks = list(range(i, world, stage))
@@ -155,7 +199,8 @@ def model_parallel_is_initialized() -> bool:
 def get_state() -> ParallelState:
     global _STATE
     if _STATE is None:
-        _STATE = ParallelState(tp_ranks=[0], pp_ranks=[0], dp_ranks=[0], embd_ranks=[0])
+        _STATE = ParallelState(tp_ranks=[0], pp_ranks=[0], dp_ranks=[0], cp_ranks=[0], dp_cp_ranks=[0],
+                               embd_ranks=[0])
     return _STATE
 
 
@@ -194,8 +239,21 @@ def get_data_parallel_rank() -> int:
     return get_state().dp_rank
 
 
-def get_data_parallel_group():
-    return get_state().dp_group
+def get_data_parallel_group(with_context_parallel: bool = False):
+    st = get_state()
+    return st.dp_cp_group if with_context_parallel else st.dp_group
+
+
+def get_context_parallel_world_size() -> int:
+    return get_state().cp
+
+
+def get_context_parallel_rank() -> int:
+    return get_state().cp_rank
+
+
+def get_context_parallel_group():
+    return get_state().cp_group
 
 
 def env_rank_info():

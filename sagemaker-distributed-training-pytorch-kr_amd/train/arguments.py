@@ -172,6 +172,8 @@ _GROUPS = {
     ],
     "distributed": [
         ("--tensor-model-parallel-size", dict(type=int, default=1)),
+        # Megatron-core's flag; Ulysses all-to-all context parallelism (parallel/context_parallel.py)
+        ("--context-parallel-size", dict(type=int, default=1)),
         ("--pipeline-model-parallel-size", dict(type=int, default=1)),
         ("--pipeline-model-parallel-split-rank", dict(type=int, default=None)),
         ("--model-parallel-size", dict(type=int, default=None)),
@@ -273,13 +275,20 @@ def validate_args(args, defaults=None):
     assert args.world_size % args.tensor_model_parallel_size == 0, "world size not divisible by TP"
     args.pipeline_model_parallel_size = min(args.pipeline_model_parallel_size,
                                             args.world_size // args.tensor_model_parallel_size)
-    mp = args.tensor_model_parallel_size * args.pipeline_model_parallel_size
-    assert args.world_size % mp == 0, "world size not divisible by TP * PP"
+    mp = args.tensor_model_parallel_size * args.pipeline_model_parallel_size * args.context_parallel_size
+    assert args.world_size % mp == 0, "world size not divisible by TP * PP * CP"
     args.data_parallel_size = args.world_size // mp
     if args.rank == 0:
         print(f"using world size: {args.world_size}, data-parallel-size: {args.data_parallel_size}, "
+              f"context-parallel size: {args.context_parallel_size}, "
               f"tensor-model-parallel size: {args.tensor_model_parallel_size}, "
               f"pipeline-model-parallel size: {args.pipeline_model_parallel_size} ", flush=True)
+    if args.context_parallel_size > 1:
+        heads = args.num_attention_heads // args.tensor_model_parallel_size
+        assert heads % args.context_parallel_size == 0, \
+            "context parallelism re-shards attention heads: (heads / TP) must be divisible by CP"
+        assert args.seq_length is None or args.seq_length % args.context_parallel_size == 0, \
+            "sequence length must be divisible by the context-parallel size"
     assert args.batch_size is None, "--batch-size argument is no longer valid, use --micro-batch-size instead"
     assert args.warmup is None, "--warmup argument is no longer valid, use --lr-warmup-fraction instead"
     assert args.model_parallel_size is None, "--model-parallel-size is no longer valid, use --tensor-model-parallel-size"

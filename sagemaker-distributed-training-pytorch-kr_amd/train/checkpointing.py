@@ -83,7 +83,7 @@ def save_checkpoint(iteration: int, model, optimizer=None, scheduler=None, args=
     no_optim = bool(getattr(args, "no_save_optim", False)) if args is not None else False
     no_rng = bool(getattr(args, "no_save_rng", False)) if args is not None else False
     zero = optimizer is not None and getattr(optimizer, "zero", False)
-    if st.dp_rank == 0:
+    if st.dp_rank == 0 and st.cp_rank == 0:
         sd = {"checkpoint_version": CHECKPOINT_VERSION, "iteration": iteration,
               "model": _unwrap(model).state_dict()}
         if args is not None:
@@ -99,7 +99,7 @@ def save_checkpoint(iteration: int, model, optimizer=None, scheduler=None, args=
         _atomic_save(sd, os.path.join(d, "model_optim_rng.pt"))
     if zero and not no_optim:
         _atomic_save({"iteration": iteration, "optimizer": optimizer.state_dict()},
-                     os.path.join(d, f"distrib_optim_dp{st.dp_rank:03d}.pt"))
+                     os.path.join(d, f"distrib_optim_dp{st.dp_cp_rank:03d}.pt"))
     _barrier()
     if _rank0():
         with open(os.path.join(save_dir, TRACKER), "w") as f:
@@ -154,7 +154,7 @@ def load_checkpoint(model, optimizer=None, scheduler=None, args=None, load_dir: 
     if optimizer is not None and not (finetune or no_load_optim or release):
         if getattr(optimizer, "zero", False):
             st = ps.get_state()
-            p = os.path.join(d, f"distrib_optim_dp{st.dp_rank:03d}.pt")
+            p = os.path.join(d, f"distrib_optim_dp{st.dp_cp_rank:03d}.pt")
             if os.path.isfile(p):
                 optimizer.load_state_dict(torch.load(p, map_location="cpu", weights_only=True)["optimizer"])
                 optim_loaded = True

@@ -67,7 +67,7 @@ def initialize_megatron(extra_args_provider=None, args_defaults=None, ignore_unk
     args.rank, args.world_size, args.local_rank = rank, world, local
     A.validate_args(args, args_defaults or {})
     ps.initialize_model_parallel(args.tensor_model_parallel_size, args.pipeline_model_parallel_size,
-                                 args.virtual_pipeline_model_parallel_size)
+                                 args.virtual_pipeline_model_parallel_size, args.context_parallel_size)
     model_parallel_seed(args.seed, args.data_parallel_random_init)
     args.mb_calculator = A.MicroBatchCalculator(args.global_batch_size, args.micro_batch_size,
                                                 args.data_parallel_size, args.rampup_batch_size)
@@ -124,7 +124,7 @@ def get_model(model_provider_func, args):
     grad_dtype = torch.float32 if (args.accumulate_allreduce_grads_in_fp32 or args.params_dtype != torch.float32) \
         else args.params_dtype
     ddp = DistributedDataParallel(model, grad_dtype=grad_dtype, bucket_size=args.ddp_bucket_size,
-                                  use_distributed_optimizer=args.use_distributed_optimizer and st.dp > 1,
+                                  use_distributed_optimizer=args.use_distributed_optimizer and st.dp * st.cp > 1,
                                   overlap_param_gather=getattr(args, "overlap_param_gather", False))
     return ddp
 
@@ -249,7 +249,8 @@ def train_step(forward_step_func, data_iterator, model, optimizer, scheduler, ar
     model.zero_grad_buffer()
     fb = get_forward_backward_func()
     st = ps.get_state()
-    seq = args.seq_length // args.tensor_model_parallel_size if args.sequence_parallel else args.seq_length
+    seq = args.seq_length // getattr(args, "context_parallel_size", 1)
+    seq = seq // args.tensor_model_parallel_size if args.sequence_parallel else seq
     timers("forward-backward", log_level=1).start(barrier=args.barrier_with_L1_time)
     scaler = getattr(optimizer, "scaler", None)
     losses = fb(forward_step_func, data_iterator, model, args.num_micro_batches,
@@ -273,7 +274,8 @@ def evaluate(forward_step_func, data_iterator, model, args, verbose=False):
     model.eval()
     totals = {}
     fb = get_forward_backward_func()
-    seq = args.seq_length // args.tensor_model_parallel_size if args.sequence_parallel else args.seq_length
+    seq = args.seq_length // getattr(args, "context_parallel_size", 1)
+    seq = seq // args.tensor_model_parallel_size if args.sequence_parallel else seq
     with torch.no_grad():
         for _ in range(args.eval_iters):
             losses = fb(forward_step_func, data_iterator, model, args.num_micro_batches, forward_only=True,

@@ -46,13 +46,33 @@ def get_ltor_masks_and_position_ids(data, eod_token, reset_position_ids=False, r
 
 
 def average_losses_across_data_parallel_group(losses):
-    """All-reduce scalars over DP and divide by the DP size (once per micro-batch)."""
+    """All-reduce scalars over DP (x CP: context-parallel ranks hold different tokens of the same
+    samples) and divide by the group size (once per micro-batch)."""
     avg = torch.cat([l.clone().detach().view(1).float() for l in losses])
     st = ps.get_state()
-    if dist.is_initialized() and st.dp > 1 and st.dp_group is not None:
-        dist.all_reduce(avg, group=st.dp_group)
-        avg = avg / st.dp
+    group = st.dp_cp_group if getattr(st, "cp", 1) > 1 else st.dp_group
+    n = st.dp * getattr(st, "cp", 1)
+    if dist.is_initialized() and n > 1 and group is not None:
+        dist.all_reduce(avg, group=group)
+        avg = avg / n
     return avg
+
+
+def context_parallel_slice(*tensors, dim: int = 1):
+    """This context-parallel rank's contiguous sequence chunk of each [b, s, ...] batch tensor
+    (tokens, labels, loss mask, position ids); identity when cp = 1."""
+    st = ps.get_state()
+    cp = getattr(st, "cp", 1)
+    if cp == 1:
+        return tensors if len(tensors) != 1 else tensors[0]
+    out = []
+    for t in tensors:
+        if t is None:
+            out.append(None)
+            continue
+        assert t.shape[dim] % cp == 0, f"sequence {t.shape[dim]} not divisible by context-parallel size {cp}"
+        out.append(t.chunk(cp, dim=dim)[st.cp_rank].contiguous())
+    return tuple(out) if len(out) != 1 else out[0]
 
 
 def report_memory(name: str) -> str:

@@ -332,6 +332,49 @@ def ulysses_worker(rank, world, nh, nkv, s=32, b=2, d=16):
         dist.destroy_process_group()
 
 
+def gpt_cp_worker(rank, world, tp, cp, sp, cfg_over=None, with_ddp=False):
+    """GPT forward/backward with context parallelism (Ulysses) x TP: each CP rank feeds its sequence
+    chunk; gradients are averaged over the dp x cp group (by the DDP wrapper when ``with_ddp``).
+    Returns the local per-token loss, the full-equivalent gradients and the ranks."""
+    import torch.distributed as dist
+    from smdt_amd.comm import init_distributed
+    from smdt_amd.models.gpt import GPTModel
+    from smdt_amd.models.transformer import TransformerConfig
+    from smdt_amd.parallel import state as ps
+    from smdt_amd.train.utils import context_parallel_slice
+    init_distributed("gloo")
+    st = ps.initialize_model_parallel(tp, 1, None, cp)
+    cfg = TransformerConfig(**{**TINY, **(cfg_over or {}), "sequence_parallel": sp})
+    m = GPTModel(cfg)
+    tokens, labels = _batch()
+    tl, ll = context_parallel_slice(tokens, labels)
+    if with_ddp:
+        from smdt_amd.parallel.distributed import DistributedDataParallel
+        ddp = DistributedDataParallel(m, grad_dtype=torch.float32)
+        ddp.zero_grad_buffer()
+    loss = m(tl, None, None, labels=ll)
+    loss.mean().backward()
+    if with_ddp:
+        ddp.finish_grad_sync()
+        grads = {n: p.main_grad.detach().clone().view_as(p) for n, p in m.named_parameters()}
+    else:
+        grads = {}
+        for n, p in m.named_parameters():
+            if p.grad is None:
+                continue
+            g = p.grad.detach().clone()
+            dist.all_reduce(g, group=st.dp_cp_group)
+            grads[n] = g / cp
+    if sp and tp > 1 and not with_ddp:
+        for n, p in m.named_parameters():
+            if getattr(p, "sequence_parallel", False) and n in grads:
+                dist.all_reduce(grads[n], group=st.tp_group)
+    meta = {"tp_rank": st.tp_rank, "cp_rank": st.cp_rank, "layer_offset": m.first_layer,
+            "cp_ranks": list(st.cp_ranks), "dp_cp_ranks": list(st.dp_cp_ranks)}
+    dist.destroy_process_group()
+    return loss.detach(), grads, meta
+
+
 def gpt_layout_worker(rank, world, tp, pp, nmb, zero, defer=False, sp=False):
     """DDP-wrapped tiny GPT under a TP x PP x DP layout with ``nmb`` micro-batches per step (gradient
     accumulation for pp == 1, 1F1B otherwise): returns the reduced fp32 main_grad of every local

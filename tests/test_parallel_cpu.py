@@ -165,6 +165,24 @@ def test_ulysses_context_parallel_matches_full_attention(cp, nh, nkv):
             _close(got, full.chunk(cp, 0)[r], tol=1e-9)
 
 
+@pytest.mark.parametrize("tp,cp,sp,over,ddp", [
+    (1, 2, False, None, False),
+    (1, 4, False, None, True),                                            # cp4 through the DDP wrapper
+    (2, 2, True, None, True),                                             # tp2 x cp2 + SP (world 4)
+    (1, 2, False, {"position_embedding_type": "rope", "num_query_groups": 2}, False),   # RoPE + GQA
+])
+def test_gpt_context_parallel_matches_single_rank(tp, cp, sp, over, ddp):
+    """P10 / §5.7: --context-parallel-size wired through the model. Each CP rank feeds its sequence
+    chunk (positions offset by cp_rank), attention re-shards heads by all-to-all, and gradients
+    averaged over dp x cp equal the single-process full-sequence gradients."""
+    ref_loss, ref = W.gpt_reference(cfg_over=over)
+    outs = run_workers(W.gpt_cp_worker, tp * cp, tp, cp, sp, over, ddp)
+    for loss, grads, meta in outs:
+        assert len(meta["cp_ranks"]) == cp and len(meta["dp_cp_ranks"]) == cp
+        _close(loss, ref_loss.chunk(cp, 1)[meta["cp_rank"]])
+        _check_tp_grads(ref, grads, meta, tp)
+
+
 @pytest.mark.parametrize("world,tp,pp,nmb,zero,defer,sp", [
     (2, 1, 1, 2, False, False, False),   # dp2 x GA2 (no_sync micro-batch, then the sync pass)
     (2, 1, 1, 2, True, True, False),     # dp2 x GA2, ZeRO reduce-scatter, deferred grouped wgrad
