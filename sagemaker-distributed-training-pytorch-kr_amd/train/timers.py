@@ -149,3 +149,14 @@ class Timers:
         last = (not dist.is_initialized()) or dist.get_rank() == dist.get_world_size() - 1
         if s is not None and last:
             print(s, flush=True)
+
+    def write(self, names, writer, iteration, normalizer=1.0, reset=False, barrier=False):
+        """Megatron's ``Timers.write``: max-over-ranks time of each timer as ``<name>-time``
+        scalars (collective: every rank calls it; only ranks with a writer write)."""
+        names = [n for n in names if n in self._timers]
+        if not names:
+            return
+        t = self._gather(names, reset, barrier) / normalizer
+        if writer is not None:
+            for i, n in enumerate(names):
+                writer.add_scalar(f"{n}-time", t[:, i].max().item(), iteration)

@@ -196,9 +196,60 @@ def _tokens_per_iter(args):
     return args.global_batch_size * args.seq_length
 
 
+_TB = {"writer": None}
+
+
+def get_tensorboard_writer():
+    """The event-file writer of the LAST rank when ``--tensorboard-dir`` is set (Megatron's
+    ``_set_tensorboard_writer``), else None."""
+    return _TB["writer"]
+
+
+def _set_tensorboard_writer(args):
+    last = (not dist.is_initialized()) or dist.get_rank() == dist.get_world_size() - 1
+    if getattr(args, "tensorboard_dir", None) and last and _TB["writer"] is None:
+        from ..utils.tensorboard import SummaryWriter
+        print("> setting tensorboard ...", flush=True)
+        _TB["writer"] = SummaryWriter(args.tensorboard_dir, max_queue=args.tensorboard_queue_size)
+
+
+def _tensorboard_log(writer, loss_dict, lr, iteration, loss_scale, grad_norm, args, timers):
+    """Megatron's scalar set (learning-rate, batch-size, each loss, loss-scale, world-size,
+    grad-norm, memory; the ``vs samples`` twins keyed by consumed samples)."""
+    samples = args.consumed_train_samples
+    if args.log_timers_to_tensorboard:   # collective: every rank calls it
+        timers.write(["forward-backward", "optimizer", "batch-generator"], writer, iteration)
+    if writer is None:
+        return
+    if args.log_learning_rate_to_tensorboard:
+        writer.add_scalar("learning-rate", lr, iteration)
+        writer.add_scalar("learning-rate vs samples", lr, samples)
+    if args.log_batch_size_to_tensorboard:
+        bs = getattr(args, "current_global_batch_size", args.global_batch_size)
+        writer.add_scalar("batch-size", bs, iteration)
+        writer.add_scalar("batch-size vs samples", bs, samples)
+    for k, v in loss_dict.items():
+        writer.add_scalar(k, v, iteration)
+        writer.add_scalar(k + " vs samples", v, samples)
+    if args.log_loss_scale_to_tensorboard and loss_scale is not None:
+        writer.add_scalar("loss-scale", loss_scale, iteration)
+        writer.add_scalar("loss-scale vs samples", loss_scale, samples)
+    if args.log_world_size_to_tensorboard:
+        writer.add_scalar("world-size", dist.get_world_size() if dist.is_initialized() else 1, iteration)
+    if grad_norm is not None:
+        writer.add_scalar("grad-norm", grad_norm, iteration)
+        writer.add_scalar("grad-norm vs samples", grad_norm, samples)
+    if args.log_memory_to_tensorboard and torch.cuda.is_available():
+        writer.add_scalar("mem-reserved-bytes", torch.cuda.memory_reserved(), iteration)
+        writer.add_scalar("mem-allocated-bytes", torch.cuda.memory_allocated(), iteration)
+        writer.add_scalar("mem-max-allocated-bytes", torch.cuda.max_memory_allocated(), iteration)
+
+
 def training_log(loss_dict, total_loss_dict, lr, iteration, loss_scale, report_memory_flag, skipped, grad_norm,
                  args, elapsed_per_iter, model_cfg=None):
     timers = A.get_timers()
+    if getattr(args, "tensorboard_dir", None) and iteration % args.tensorboard_log_interval == 0:
+        _tensorboard_log(get_tensorboard_writer(), loss_dict, lr, iteration, loss_scale, grad_norm, args, timers)
     for k, v in loss_dict.items():
         total_loss_dict[k] = total_loss_dict.get(k, 0.0) + float(v)
     total_loss_dict["skipped"] = total_loss_dict.get("skipped", 0) + int(skipped)
@@ -292,8 +343,16 @@ def evaluate(forward_step_func, data_iterator, model, args, verbose=False):
 def evaluate_and_print_results(prefix, forward_step_func, data_iterator, model, args):
     res = evaluate(forward_step_func, data_iterator, model, args)
     s = f" validation loss at {prefix} | "
+    writer = get_tensorboard_writer()
     for k, v in res.items():
         s += f"{k} value: {v:.6E} | {k} PPL: {math.exp(min(20, v)):.6E} | "
+        if writer is not None:
+            writer.add_scalar(f"{k} validation", v, args.iteration)
+            writer.add_scalar(f"{k} validation vs samples", v, args.consumed_train_samples)
+            if args.log_validation_ppl_to_tensorboard:
+                writer.add_scalar(f"{k} validation ppl", math.exp(min(20, v)), args.iteration)
+    if writer is not None:
+        writer.flush()
     length = len(s) + 1
     print_rank_last("-" * length)
     print_rank_last(s)
@@ -395,6 +454,7 @@ def train(forward_step_func, model, optimizer, scheduler, train_iter, valid_iter
 def pretrain(train_valid_test_dataset_provider, model_provider, model_type, forward_step_func,
              process_non_loss_data_func=None, extra_args_provider=None, args_defaults=None, argv=None):
     args = initialize_megatron(extra_args_provider, args_defaults, argv=argv)
+    _set_tensorboard_writer(args)
     from .schedules import configure_p2p
     configure_p2p(args)   # --overlap-p2p-communication / --no-scatter-gather-tensors-in-pipeline
     timers = A.get_timers()
@@ -429,4 +489,6 @@ def pretrain(train_valid_test_dataset_provider, model_provider, model_type, forw
                                    args)
     if args.do_test and args.eval_iters > 0:
         evaluate_and_print_results(f"iteration {iteration} on test set", forward_step_func, test_iter, model, args)
+    if get_tensorboard_writer() is not None:
+        get_tensorboard_writer().flush()
     return model, optimizer

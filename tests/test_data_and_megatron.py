@@ -193,3 +193,61 @@ def test_pretrain_gpt_rampup_batch_size(tmp_path):
     assert gbs[0] == 2 and gbs[-1] == 8 and gbs == sorted(gbs) and {2, 4, 6, 8} <= set(gbs), gbs
     assert cons[-1] >= 60 and cons[-2] < 60, cons
     assert "batch size rampup starting from global batch size 2" in r.stdout
+
+
+def test_tensorboard_event_file_format(tmp_path):
+    """the dependency-free event writer emits CRC-32C-framed TFRecords holding
+    tensorflow.Event protobufs (checked against the standard CRC-32C test vector and a parse-back)."""
+    from smdt_amd.utils import tensorboard as tb
+    assert tb.crc32c(b"123456789") == 0xE3069283
+    w = tb.SummaryWriter(str(tmp_path), max_queue=2)
+    for i in range(5):
+        w.add_scalar("lm loss", 10.0 - i, i + 1)
+    w.add_scalars("timers", {"fwd": 1.5, "bwd": 2.5}, 7)
+    w.close()
+    files = list(tmp_path.glob("events.out.tfevents.*"))
+    assert len(files) == 1
+    recs = list(tb.read_records(str(files[0])))
+    assert b"brain.Event:2" in recs[0]
+    sc = tb.read_scalars(str(files[0]))
+    assert [(s, t) for s, t, _ in sc[:5]] == [(i + 1, "lm loss") for i in range(5)]
+    assert [v for _, _, v in sc[:5]] == [10.0, 9.0, 8.0, 7.0, 6.0]
+    assert ("timers/bwd", 2.5) in [(t, v) for _, t, v in sc]
+    raw = files[0].read_bytes()
+    bad = raw[:-1] + bytes([raw[-1] ^ 1])
+    files[0].write_bytes(bad)
+    with pytest.raises(ValueError):
+        tb.read_scalars(str(files[0]))
+
+
+@pytest.mark.slow
+def test_pretrain_gpt_writes_tensorboard_and_runs_context_parallel(tmp_path):
+    """--tensorboard-dir with the Megatron log flags writes learning-rate / lm loss / grad-norm /
+    batch-size / timer scalars per iteration on the last rank; the run uses --context-parallel-size 2
+    (world 2, gloo) so the CP batch slicing and dp x cp loss averaging run end to end."""
+    from smdt_amd.utils import tensorboard as tb
+    script = os.path.join(REPO, "recipes", "3_training_megatron-lm", "pretrain_gpt.py")
+    args = ["--num-layers", "2", "--hidden-size", "64", "--num-attention-heads", "4", "--seq-length", "64",
+            "--max-position-embeddings", "64", "--micro-batch-size", "2", "--global-batch-size", "4",
+            "--lr", "0.001", "--lr-warmup-iters", "1", "--mock-data", "--log-interval", "1",
+            "--eval-interval", "2", "--eval-iters", "1", "--vocab-size", "512", "--tokenizer-type", "NullTokenizer",
+            "--train-iters", "3", "--tensorboard-dir", str(tmp_path / "tb"), "--log-timers-to-tensorboard",
+            "--log-batch-size-to-tensorboard", "--log-validation-ppl-to-tensorboard", "--context-parallel-size", "2",
+            "--timing-log-level", "1",
+            "--distributed-backend", "gloo"]
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", "2", "--master-addr",
+                        "127.0.0.1", "--master-port", "29547", script] + args, env=env, capture_output=True,
+                       text=True, timeout=600, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "context-parallel size: 2" in r.stdout
+    files = list((tmp_path / "tb").glob("events.out.tfevents.*"))
+    assert len(files) == 1, files      # only the last rank writes
+    sc = tb.read_scalars(str(files[0]))
+    tags = {t for _, t, _ in sc}
+    for want in ("learning-rate", "lm loss", "lm loss vs samples", "grad-norm", "batch-size",
+                 "forward-backward-time", "lm loss validation", "lm loss validation ppl"):
+        assert want in tags, (want, sorted(tags))
+    steps = sorted(s for s, t, _ in sc if t == "lm loss")
+    assert steps == [1, 2, 3]
+    assert all(math.isfinite(v) for _, _, v in sc)
