@@ -8,17 +8,22 @@ every peer's with ``hipIpcOpenMemHandle`` (dmabuf IPC on this ROCm). One kernel
 
 * one-shot (message <= ``ONE_SHOT_MAX_BYTES[world]``): every rank reduces the whole tensor;
 * two-shot: reduce-scatter through peer reads, then an all-gather of the reduced slices;
+* reduce-scatter / all-gather (ZeRO gradient shards and parameter gathers): one barrier, each link
+  carries 1/W of the message;
 
-both accumulate in fp32 in rank order, so every rank gets bit-identical results. Anything the
-kernel does not take — messages larger than the staging region, sizes that are not a multiple of
-16 bytes, non-contiguous or CPU tensors, groups that span hosts or are not 2 / 4 / 8 ranks, async
-calls — goes to RCCL (``dist.all_reduce``) unchanged.
+reductions accumulate in fp32 in rank order, so every rank gets bit-identical results. Messages
+larger than the staging region run as a sequence of region-sized calls (an all-reduce in flat
+pieces, a reduce-scatter / all-gather in column bands of every slice). Anything the kernel does not
+take — sizes that are not a multiple of 16 bytes, non-contiguous or CPU tensors, groups that span
+hosts or are not 2 / 4 / 8 ranks — goes to RCCL unchanged.
 
 The reference has no custom all-reduce (stock NCCL / SMDDP collectives). Its TP
 all-reduces are 18.9 MB each (NB3) and its MNIST gradients 4.8 MB — the message range
 this path is for. It is used by the tensor-parallel layers (sync all-reduces) and by the DDP
-reducer for buckets that fit the staging region, when ``SMDT_XGMI_ALLREDUCE=1`` or when the job
-asked for the ``smddp`` backend (``SMDT_XGMI_ALLREDUCE=0`` turns it off).
+reducer (bucket all-reduces, ZeRO reduce-scatters and parameter all-gathers) when
+``SMDT_XGMI_ALLREDUCE=1`` or when the job asked for the ``smddp`` backend — through
+``init_distributed("smddp")`` or a direct ``dist.init_process_group(backend="smddp")``
+(``SMDT_XGMI_ALLREDUCE=0`` turns it off).
 
 An engine's calls must be issued in the same order on every rank of its group and on ONE stream
 (the kernel double-buffers on a per-call counter); separate engines are used per group / stream.
@@ -50,22 +55,45 @@ def note_smddp_requested():
     _SMDDP_REQUESTED = True
 
 
-def wanted() -> bool:
+def wanted(group=None) -> bool:
     v = os.environ.get("SMDT_XGMI_ALLREDUCE")
     if v is not None:
         return v == "1"
-    return _SMDDP_REQUESTED
+    if _SMDDP_REQUESTED:
+        return True
+    # a script that called dist.init_process_group(backend="smddp") directly
+    try:
+        return dist.is_initialized() and dist.get_backend(group) == "smddp"
+    except (RuntimeError, ValueError):
+        return False
+
+
+def rccl_backend(group=None) -> bool:
+    """True when ``group``'s collectives run on RCCL (``nccl``, or the ``smddp`` alias of it)."""
+    try:
+        return dist.get_backend(group) in ("nccl", "smddp")
+    except (RuntimeError, ValueError):
+        return False
 
 
 def choose_algorithm(nbytes: int, world: int) -> str:
     return "one_shot" if nbytes <= ONE_SHOT_MAX_BYTES.get(world, 0) else "two_shot"
 
 
-def eligible(t: torch.Tensor, world: int, region_bytes: int) -> bool:
+_MODE = {"one_shot": 0, "two_shot": 1, "reduce_scatter": 2, "all_gather": 3}
+
+
+def eligible(t: torch.Tensor, world: int, region_bytes: int = 0) -> bool:
+    """A tensor the kernel takes (any size: larger messages are chunked by the engine)."""
     nbytes = t.numel() * t.element_size()
     return (t.is_cuda and t.is_contiguous() and t.dtype in (torch.float32, torch.bfloat16, torch.float16)
-            and world in (2, 4, 8) and 0 < nbytes <= region_bytes and nbytes % 16 == 0
-            and t.data_ptr() % 16 == 0)
+            and world in (2, 4, 8) and 0 < nbytes and nbytes % 16 == 0 and t.data_ptr() % 16 == 0)
+
+
+def _bands(n: int, per_call: int, align: int):
+    """[lo, hi) pieces of [0, n), each at most ``per_call`` and (but the last) a multiple of align."""
+    step = max(align, per_call // align * align)
+    return [(lo, min(n, lo + step)) for lo in range(0, n, step)]
 
 
 class _EventHandle:
@@ -96,6 +124,7 @@ class XgmiAllReduce:
         self.region = (int(region_bytes) + 4095) // 4096 * 4096
         self.blocks = int(blocks)
         self.calls = 0
+        self.bytes_moved = 0
         self._stream = None
         self._opened: List[int] = []
         self._data = self._sig = None
@@ -169,32 +198,86 @@ class XgmiAllReduce:
     def fits(self, t: torch.Tensor) -> bool:
         return self.active and eligible(t, self.world, self.region)
 
+    def _call(self, mode: str, inp: torch.Tensor, out: torch.Tensor, n: int, slice_stride: int, scale: float):
+        self.C.xgmi_collective(_MODE[mode], inp, out, self.data_ptrs, self.sig_ptrs, self.rank, 1, self.region,
+                               self.blocks, n, slice_stride, scale)
+        self.calls += 1
+        self.bytes_moved += n * inp.element_size() * (self.world if mode in ("reduce_scatter", "all_gather") else 1)
+
     def all_reduce(self, t: torch.Tensor, op: str = "sum") -> bool:
-        """In-place all-reduce of ``t`` on the current stream; False (nothing done) when the
-        tensor is not eligible, so the caller falls back to RCCL."""
+        """In-place all-reduce of ``t`` on the current stream (region-sized pieces); False
+        (nothing done) when the tensor is not eligible, so the caller falls back to RCCL."""
         if not self.fits(t):
             return False
         scale = 1.0 / self.world if op == "avg" else 1.0
-        two = choose_algorithm(t.numel() * t.element_size(), self.world) == "two_shot"
-        self.C.xgmi_allreduce(t, t, self.data_ptrs, self.sig_ptrs, self.rank, 1, self.region, two, self.blocks, scale)
-        self.calls += 1
+        flat = t.view(-1)
+        per = self.region // t.element_size()
+        for lo, hi in _bands(flat.numel(), per, 16 // t.element_size()):
+            piece = flat[lo:hi]
+            mode = choose_algorithm((hi - lo) * t.element_size(), self.world)
+            self._call(mode, piece, piece, hi - lo, 0, scale)
         return True
+
+    def reduce_scatter(self, out: torch.Tensor, inp: torch.Tensor, op: str = "sum") -> bool:
+        """``dist.reduce_scatter_tensor`` semantics: ``inp`` = W contiguous slices, ``out`` = this
+        rank's reduced slice (it may be the input's own slice, in place). False: not eligible."""
+        W = self.world
+        if not (self.fits(inp) and out.is_contiguous() and out.dtype == inp.dtype and out.is_cuda
+                and inp.numel() == W * out.numel() and out.data_ptr() % 16 == 0):
+            return False
+        ns = out.numel()
+        es = inp.element_size()
+        if (ns * es) % 16:
+            return False
+        scale = 1.0 / W if op == "avg" else 1.0
+        fi, fo = inp.view(-1), out.view(-1)
+        for lo, hi in _bands(ns, self.region // (W * es), 16 // es):
+            self._call("reduce_scatter", fi[lo:], fo[lo:hi], hi - lo, ns, scale)
+        return True
+
+    def all_gather(self, out: torch.Tensor, inp: torch.Tensor) -> bool:
+        """``dist.all_gather_into_tensor`` semantics (``inp`` may be ``out``'s own slice)."""
+        W = self.world
+        if not (self.fits(out) and inp.is_contiguous() and inp.dtype == out.dtype and inp.is_cuda
+                and out.numel() == W * inp.numel() and inp.data_ptr() % 16 == 0):
+            return False
+        ns = inp.numel()
+        es = out.element_size()
+        if (ns * es) % 16:
+            return False
+        fi, fo = inp.view(-1), out.view(-1)
+        for lo, hi in _bands(ns, self.region // es, 16 // es):
+            self._call("all_gather", fi[lo:hi], fo[lo:], hi - lo, ns, 1.0)
+        return True
+
+    def _async(self, fn, tensors, *args) -> Optional[_EventHandle]:
+        dev = tensors[0].device
+        if self._stream is None:
+            self._stream = torch.cuda.Stream(device=dev)
+        cur = torch.cuda.current_stream(dev)
+        self._stream.wait_stream(cur)
+        with torch.cuda.stream(self._stream):
+            ok = fn(*args)
+            ev = torch.cuda.Event()
+            ev.record(self._stream)
+        if not ok:
+            return None
+        for t in tensors:
+            t.record_stream(self._stream)
+        return _EventHandle(ev)
 
     def all_reduce_async(self, t: torch.Tensor, op: str = "sum") -> Optional[_EventHandle]:
         """The same on the engine's own stream, ordered after the current stream's work; returns
         a handle whose ``wait()`` makes the current stream wait (None: not eligible)."""
         if not self.fits(t):
             return None
-        if self._stream is None:
-            self._stream = torch.cuda.Stream(device=t.device)
-        cur = torch.cuda.current_stream(t.device)
-        self._stream.wait_stream(cur)
-        with torch.cuda.stream(self._stream):
-            self.all_reduce(t, op)
-            ev = torch.cuda.Event()
-            ev.record(self._stream)
-        t.record_stream(self._stream)
-        return _EventHandle(ev)
+        return self._async(self.all_reduce, [t], t, op)
+
+    def reduce_scatter_async(self, out, inp, op: str = "sum") -> Optional[_EventHandle]:
+        return self._async(self.reduce_scatter, [out, inp], out, inp, op)
+
+    def all_gather_async(self, out, inp) -> Optional[_EventHandle]:
+        return self._async(self.all_gather, [out, inp], out, inp)
 
     def error(self) -> int:
         return int(self.C.ar_read_error(self._sig)) if self._sig is not None else 0
@@ -230,9 +313,9 @@ class XgmiAllReduce:
 def create_for_group(group, **kw) -> Optional[XgmiAllReduce]:
     """Collective over ``group``: an engine when xGMI all-reduce is wanted and possible, else None
     (with a warning when it was wanted but could not be set up)."""
-    if not (wanted() and dist.is_initialized() and torch.cuda.is_available()):
+    if not (dist.is_initialized() and torch.cuda.is_available() and wanted(group)):
         return None
-    if dist.get_backend(group) != "nccl":
+    if not rccl_backend(group):
         return None
     ws = dist.get_world_size(group)
     if ws not in (2, 4, 8):
@@ -263,6 +346,23 @@ class XgmiLoopback:
         out = torch.empty_like(x) if out is None else out
         self.C.xgmi_allreduce(x, out, self.data_ptrs, self.sig_ptrs, 0, self.world, self.region, two_shot,
                               self.blocks, scale)
+        return out
+
+    def reduce_scatter(self, x: torch.Tensor, scale: float = 1.0, out: Optional[torch.Tensor] = None):
+        """x: [world, W * ns] (row r = virtual rank r's W slices). Returns [world, ns]: row r = the
+        reduced slice r (``out`` may be a strided view into x, e.g. each rank's own slice)."""
+        W = self.world
+        ns = x.shape[1] // W
+        out = torch.empty(W, ns, dtype=x.dtype, device=x.device) if out is None else out
+        self.C.xgmi_collective(2, x, out, self.data_ptrs, self.sig_ptrs, 0, W, self.region, self.blocks, ns, ns, scale)
+        return out
+
+    def all_gather(self, x: torch.Tensor, out: Optional[torch.Tensor] = None):
+        """x: [world, ns] (row r = virtual rank r's slice). Returns [world, W * ns]."""
+        W = self.world
+        ns = x.shape[1]
+        out = torch.empty(W, W * ns, dtype=x.dtype, device=x.device) if out is None else out
+        self.C.xgmi_collective(3, x, out, self.data_ptrs, self.sig_ptrs, 0, W, self.region, self.blocks, ns, ns, 1.0)
         return out
 
     def errors(self) -> List[int]:

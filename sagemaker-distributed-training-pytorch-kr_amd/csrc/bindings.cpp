@@ -520,6 +520,51 @@ void xgmi_allreduce(Tensor in, Tensor out, std::vector<int64_t> data_ptrs, std::
         "xgmi_allreduce");
 }
 
+// General form: mode 0/1 all-reduce (n = elements), 2 reduce-scatter, 3 all-gather (n = elements
+// per slice, slices slice_stride elements apart in the input (RS) / output (AG)). in / out are raw
+// views (the reduce-scatter output may alias the input's slice `rank`, the all-gather input may
+// alias the output's). Loopback (nranks_local > 1): in / out are [nranks_local, ...] with one row
+// per virtual rank. Every element the kernel touches is bounds-checked here against the tensors.
+void xgmi_collective(int64_t mode, Tensor in, Tensor out, std::vector<int64_t> data_ptrs, std::vector<int64_t> sig_ptrs,
+                     int64_t rank, int64_t nranks_local, int64_t region_bytes, int64_t blocks, int64_t n,
+                     int64_t slice_stride, double scale) {
+  TORCH_CHECK(mode >= 0 && mode <= 3, "xgmi_collective: mode must be 0..3");
+  TORCH_CHECK(in.dtype() == out.dtype() && in.device() == out.device(), "xgmi_collective: in / out mismatch");
+  TORCH_CHECK(in.is_cuda() && in.device().index() == c10::hip::current_device(),
+              "xgmi_collective: tensors must live on the current device");
+  const int world = (int)data_ptrs.size();
+  TORCH_CHECK(sig_ptrs.size() == data_ptrs.size() && world >= 2 && world <= smdt_ar_max_ranks(),
+              "xgmi_collective: need 2..", smdt_ar_max_ranks(), " ranks");
+  TORCH_CHECK(blocks >= 1 && blocks <= smdt_ar_max_blocks(), "xgmi_collective: blocks out of range");
+  TORCH_CHECK(n > 0, "xgmi_collective: empty message");
+  int64_t in_per = in.numel(), out_per = out.numel(), in_rs = 0, out_rs = 0;
+  if (nranks_local > 1) {
+    TORCH_CHECK(in.dim() == 2 && out.dim() == 2 && in.size(0) == nranks_local && out.size(0) == nranks_local &&
+                    in.stride(1) == 1 && out.stride(1) == 1,
+                "xgmi_collective loopback: in / out must be [nranks_local, m] with unit inner stride");
+    TORCH_CHECK(blocks * nranks_local <= 512, "xgmi_collective loopback: blocks x ranks must stay co-resident (<= 512)");
+    in_per = in.size(1);
+    out_per = out.size(1);
+    in_rs = in.stride(0);
+    out_rs = out.stride(0);
+  } else {
+    TORCH_CHECK(in.is_contiguous() && out.is_contiguous(), "xgmi_collective: contiguous tensors");
+  }
+  const int64_t span = (int64_t)(world - 1) * slice_stride + n;
+  const int64_t need_in = mode == 2 ? span : n, need_out = mode == 3 ? span : n;
+  TORCH_CHECK(in_per >= need_in && out_per >= need_out, "xgmi_collective: tensors too small for n = ", n,
+              ", slice stride ", slice_stride);
+  std::vector<void*> d(world), s(world);
+  for (int r = 0; r < world; ++r) {
+    d[r] = vp(data_ptrs[r]);
+    s[r] = vp(sig_ptrs[r]);
+  }
+  check(smdt_xgmi_collective((int)mode, dcode(in), in.data_ptr(), out.data_ptr(), in_rs, out_rs, n, slice_stride,
+                             (float)scale, d.data(), s.data(), world, (int)rank, (int)nranks_local, region_bytes,
+                             (int)blocks, cur_stream()),
+        "xgmi_collective");
+}
+
 }  // namespace
 
 void register_blaslt(pybind11::module_& m);
@@ -565,6 +610,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("xgmi_allreduce", &xgmi_allreduce, py::arg("input"), py::arg("out"), py::arg("data_ptrs"), py::arg("sig_ptrs"),
         py::arg("rank"), py::arg("nranks_local"), py::arg("region_bytes"), py::arg("two_shot"), py::arg("blocks"),
         py::arg("scale") = 1.0);
+  m.def("xgmi_collective", &xgmi_collective, py::arg("mode"), py::arg("input"), py::arg("out"), py::arg("data_ptrs"),
+        py::arg("sig_ptrs"), py::arg("rank"), py::arg("nranks_local"), py::arg("region_bytes"), py::arg("blocks"),
+        py::arg("n"), py::arg("slice_stride"), py::arg("scale") = 1.0);
   m.def("flash_bwd", &flash_bwd, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("o"), py::arg("dout"),
         py::arg("lse"), py::arg("scale"), py::arg("causal"), py::arg("dq") = py::none(), py::arg("dk") = py::none(),
         py::arg("dv") = py::none(), py::arg("dropout_p") = 0.0, py::arg("seed") = 0, py::arg("offset") = 0);

@@ -69,14 +69,23 @@ struct Strides {
 
 // Attention dropout. The 2x2 block (q, k), q, k in {2i, 2i+1} x {2j, 2j+1} shares one 32-bit
 // hash of the block counter (q/2) * (S/2) + k/2 keyed by (seed, offset, b, h); byte
-// 2 (q & 1) + (k & 1) of it decides the element (kept iff byte >= thr = round(p * 256); kept
-// probabilities are scaled by inv = 256 / (256 - thr) — 8-bit thresholds as in FlashAttention-2).
-// Every kernel (query-on-lane or key-on-lane) uses 2 bytes per hash, so hashing costs half an
-// evaluation per element everywhere. The forward and both backward kernels re-derive the identical
-// mask, no mask tensor is stored. The hash is a keyed two-round multiply/xor-shift mixer;
-// Philox-7 would cost several times more VALU than the MFMA work of an attention tile on CDNA4.
+// 2 (q & 1) + (k & 1) of it decides the element: kept iff its low 7 bits >= T = round(p * 128)
+// (kept probabilities scaled by inv = 128 / (128 - T)). The forward and both backward kernels
+// re-derive the identical mask, no mask tensor is stored.
+//
+// VALU budget (the attention loops are VALU-issue-bound, profiles/r1_fa_glds): a lane needs only
+// the 2 bytes of its row (column) of each block, and its neighbour lane (q ^ 1 or k ^ 1) needs the
+// other 2 of the SAME words. So each lane hashes every other block, the pair swap the words by one
+// DPP move, and a v_perm_b32 gathers the 4 bytes this lane needs into one word; the 4 threshold
+// tests then run as ONE SWAR add ((w & 0x7F7F7F7F) + (128 - T) x 0x01010101: bit 7 + 8b is the
+// decision of byte b), and the decisions land on packed 16-bit operand pairs with one
+// v_pk_ashrrev_i16 per pair (sign bits 15 / 31 -> 0xFFFF / 0 halves) and one AND. Per element that
+// is ~1/4 hash + ~1/2 masking instruction instead of 1/2 hash + 3 (extract, compare, select).
+// The hash is a keyed two-round multiply/xor-shift mixer; Philox-7 would cost several times more
+// VALU than the MFMA work of an attention tile on CDNA4.
 struct Drop {
   uint32_t thr, key0, key1;
+  uint32_t k4;    // (128 - T) in every byte: the SWAR threshold addend
   float inv;      // 1 / (1 - p_realised)
   float keep;     // 1 - p_realised  (= 1 / inv)
   float log2inv;  // log2(inv): folded into the exponent so p' = p * inv costs nothing
@@ -100,7 +109,46 @@ __device__ __forceinline__ uint32_t drop_hash(uint32_t blk, uint32_t key) {
   x = __umul24(x ^ (x >> 16), 0x45D9F3u);
   return x ^ (x >> 16);
 }
-__device__ __forceinline__ bool keep_byte(uint32_t h, int sh, uint32_t thr) { return ((h >> sh) & 0xFFu) >= thr; }
+// The partner lane's value (lane ^ 1): DPP quad_perm [1, 0, 3, 2].
+__device__ __forceinline__ uint32_t swap_lane1(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, true);
+}
+// Keep decisions of two slots (block words of slot 2u computed by the even lane, 2u + 1 by the odd
+// one; ``h`` is this lane's word). ``sel`` (per lane) gathers [slot 2u lo, slot 2u+1 lo, slot 2u hi,
+// slot 2u+1 hi] bytes; the result has the decision of that byte at bit 7 / 15 / 23 / 31.
+__device__ __forceinline__ uint32_t keep_bits(uint32_t h, uint32_t sel, uint32_t k4) {
+  const uint32_t w = __builtin_amdgcn_perm(h, swap_lane1(h), sel);
+  return (w & 0x7F7F7F7Fu) + k4;
+}
+// 16-bit all-ones / zero halves from sign bits 15 / 31 (v_pk_ashrrev_i16).
+__device__ __forceinline__ uint32_t half_masks(uint32_t t) {
+  using s2 = __attribute__((ext_vector_type(2))) short;
+  s2 v = __builtin_bit_cast(s2, t);
+  v = v >> (short)15;
+  return __builtin_bit_cast(uint32_t, v);
+}
+// Packed-pair masks of slot 2u (bits 7 / 23) and slot 2u + 1 (bits 15 / 31).
+__device__ __forceinline__ uint32_t mask_even_slot(uint32_t t) { return half_masks(t << 8); }
+__device__ __forceinline__ uint32_t mask_odd_slot(uint32_t t) { return half_masks(t); }
+// All-ones / zero of decision bit ``b`` (v_bfe_i32): per-element fp32 masking.
+// (v_bfe_i32 by hand: left to itself the compiler turns the sign-extend into test + compare + select.)
+template <int b>
+__device__ __forceinline__ float and_bit(float x, uint32_t t) {
+  int32_t m;
+  asm("v_bfe_i32 %0, %1, %2, 1" : "=v"(m) : "v"(t), "n"(b));
+  return __int_as_float(__float_as_int(x) & m);
+}
+// AND the four packed pairs of a 16-bit operand fragment with their masks.
+template <class V>
+__device__ __forceinline__ V and_pairs(V x, uint32_t m0, uint32_t m1, uint32_t m2, uint32_t m3) {
+  using u4 = __attribute__((ext_vector_type(4))) uint32_t;
+  u4 w = __builtin_bit_cast(u4, x);
+  w[0] &= m0;
+  w[1] &= m1;
+  w[2] &= m2;
+  w[3] &= m3;
+  return __builtin_bit_cast(V, w);
+}
 
 // Operand prescale: x * c rounded back to bf16 (one-time, register-resident fragments).
 template <class V>
@@ -221,8 +269,10 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void fwd_kernel(const E* __re
   const int ntiles = kend / kTile;
   const uint32_t dkey = DROP ? drop_key(drop, bh) : 0u;
   const uint32_t shalf = (uint32_t)S >> 1;
-  const uint32_t dblk = (uint32_t)(my_q >> 1) * shalf + 2u * h;  // block counter of key row 0
-  const int dsh = 16 * (my_q & 1);                                // byte 2 (q & 1) + (k & 1)
+  // block counter of this lane's first hashed key pair (key rows 4 h .. ; odd queries hash the
+  // odd slots) and its byte gather: even q keeps bytes 0 / 1, odd q bytes 2 / 3
+  const uint32_t dblk = (uint32_t)(my_q >> 1) * shalf + 2u * h + (uint32_t)(my_q & 1);
+  const uint32_t dsel = (my_q & 1) ? 0x07030602u : 0x01050004u;
   // K/V tiles stream global -> LDS by LDS-DMA (global_load_lds, no VGPR staging, no ds_write
   // pass) through a 3-buffer ring with two tiles in flight: tile t waits only for its own DMA
   // (counted vmcnt) and one raw s_barrier publishes it.
@@ -293,14 +343,18 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void fwd_kernel(const E* __re
           st[tt][i] = p0;
           st[tt][i + 1] = p1;
         }
-      if constexpr (DROP) {  // zero dropped entries; the 1/(1-p) scale is applied in the epilogue
+      // dropout: packed-pair masks of the 8 key-pair slots of each 32-key sub-tile (slot m =
+      // registers 2m, 2m + 1); dropped entries leave P.V only (l sums the un-dropped p) and the
+      // 1/(1-p) scale is applied in the epilogue
+      uint32_t dm[2][8];
+      if constexpr (DROP) {
 #pragma unroll
         for (int tt = 0; tt < 2; ++tt)
 #pragma unroll
-          for (int i = 0; i < 16; i += 2) {  // registers i, i+1 = keys 2j, 2j+1
-            const uint32_t hv = drop_hash(dblk + ((kb + 32 * tt + (i & 3) + 8 * (i >> 2)) >> 1), dkey);
-            if (!keep_byte(hv, dsh, drop.thr)) st[tt][i] = 0.f;
-            if (!keep_byte(hv, dsh + 8, drop.thr)) st[tt][i + 1] = 0.f;
+          for (int u = 0; u < 4; ++u) {
+            const uint32_t t = keep_bits(drop_hash(dblk + ((kb + 32 * tt) >> 1) + 4 * u, dkey), dsel, drop.k4);
+            dm[tt][2 * u] = mask_even_slot(t);
+            dm[tt][2 * u + 1] = mask_odd_slot(t);
           }
       }
       l += xhalf_sum(rs0 + rs1);
@@ -309,7 +363,8 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void fwd_kernel(const E* __re
       for (int tt = 0; tt < 2; ++tt) {
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
-          const v8_t<E> pb = pack8<E>(st[tt], s);
+          v8_t<E> pb = pack8<E>(st[tt], s);
+          if constexpr (DROP) pb = and_pairs(pb, dm[tt][4 * s], dm[tt][4 * s + 1], dm[tt][4 * s + 2], dm[tt][4 * s + 3]);
 #pragma unroll
           for (int dt = 0; dt < G::DT; ++dt) o[dt] = mfma(fr.trf(vt, 32 * tt, s, dt), pb, o[dt]);
         }
@@ -460,12 +515,13 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dkdv_kernel(
   wait_next();
 
   const uint32_t shalf = (uint32_t)S >> 1;
-  const int dsh = 8 * (my_key & 1);
+  // even keys keep bytes 0 / 2 of each block word, odd keys bytes 1 / 3; odd keys hash odd slots
+  const uint32_t dsel = (my_key & 1) ? 0x07030501u : 0x02060004u;
   int ch = 0, cq = 0;  // current work item
   auto item = [&](const char* buf, char* pre) {
     const int qb = qstart + cq * kTile;
     const uint32_t dkey = DROP ? drop_key(drop, b * H + hk * group + ch) : 0u;
-    const uint32_t dblk = (uint32_t)((qb + 4 * h) >> 1) * shalf + (uint32_t)(my_key >> 1);
+    const uint32_t dblk = ((uint32_t)((qb + 4 * h) >> 1) + (uint32_t)(my_key & 1)) * shalf + (uint32_t)(my_key >> 1);
     const char* q_l = buf;
     const char* do_l = buf + G::TB;
     const float* lse_l = reinterpret_cast<const float*>(buf + 2 * G::TB);
@@ -495,11 +551,19 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dkdv_kernel(
           dp = mfma(fr.rowf(do_l, 32 * qs2, kk), vf[kk], dp);
         }
         const bool diag = CAUSAL && qsub < kw + 31;
+        // dropout: slot m = registers 2m, 2m + 1 (queries 2i, 2i + 1 of one block); dropped
+        // entries: P' -> 0 for dV (packed-pair masks), dP -> 0, so dS = p' (keep ? dP : 0) - p' delta'
+        uint32_t dm[8];
   #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const int r0 = 32 * qs2 + 8 * g + 4 * h;
           const f32x4 dlg = DROP ? *reinterpret_cast<const f32x4*>(del_l + r0) * drop.keep : f32x4{0.f, 0.f, 0.f, 0.f};
-          uint32_t hvq = 0u;
+          uint32_t t = 0u;
+          if constexpr (DROP) {
+            t = keep_bits(drop_hash(dblk + (uint32_t)(16 * qs2 + 4 * g) * shalf, dkey), dsel, drop.k4);
+            dm[2 * g] = mask_even_slot(t);
+            dm[2 * g + 1] = mask_odd_slot(t);
+          }
   #pragma unroll
           for (int j = 0; j < 4; j += 2) {
             const int i = 4 * g + j;
@@ -510,18 +574,16 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dkdv_kernel(
             }
             float d0 = dp[i], d1 = dp[i + 1];
             if constexpr (DROP) {
-              // rows j, j+1 (queries 2i, 2i+1) share the hash of their 2x2 block; dropped
-              // entries: P' -> 0 for dV, dP -> 0, so dS = p' (keep ? dP : 0) - p' delta'
-              hvq = drop_hash(dblk + (uint32_t)((32 * qs2 + 8 * g + j) >> 1) * shalf, dkey);
-              const bool k0 = keep_byte(hvq, dsh, drop.thr), k1 = keep_byte(hvq, dsh + 16, drop.thr);
-              s[i] = k0 ? p0 : 0.f;
-              s[i + 1] = k1 ? p1 : 0.f;
-              d0 = (k0 ? d0 : 0.f) - dlg[j];
-              d1 = (k1 ? d1 : 0.f) - dlg[j + 1];
-            } else {
-              s[i] = p0;
-              s[i + 1] = p1;
+              if (j == 0) {
+                d0 = and_bit<7>(d0, t) - dlg[j];
+                d1 = and_bit<23>(d1, t) - dlg[j + 1];
+              } else {
+                d0 = and_bit<15>(d0, t) - dlg[j];
+                d1 = and_bit<31>(d1, t) - dlg[j + 1];
+              }
             }
+            s[i] = p0;
+            s[i + 1] = p1;
             dp[i] = p0 * d0;  // dS
             dp[i + 1] = p1 * d1;
           }
@@ -529,7 +591,8 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dkdv_kernel(
         // dV^T[d, key] += dO^T[d, q] . P[q, key] ; dK^T[d, key] += Q^T[d, q] . dS[q, key]
   #pragma unroll
         for (int st = 0; st < 2; ++st) {
-          const v8_t<E> pb = pack8<E>(s, st);
+          v8_t<E> pb = pack8<E>(s, st);
+          if constexpr (DROP) pb = and_pairs(pb, dm[4 * st], dm[4 * st + 1], dm[4 * st + 2], dm[4 * st + 3]);
           const v8_t<E> db = pack8<E>(dp, st);
   #pragma unroll
           for (int dt = 0; dt < G::DT; ++dt) {
@@ -614,11 +677,12 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dq_kernel(
                         : DELTA[((int64_t)b * H + hq) * S + my_q];
   // Row constants as the S / dP MFMAs' initial accumulators, register-resident for the whole
   // loop (no per-subtile splat).
-  const f32x16 st0 = splat16(-lse2), dp0 = splat16(-dl);
+  // (with dropout dP starts at 0: dropped entries need the raw dP masked before - delta')
+  const f32x16 st0 = splat16(-lse2), dp0 = splat16(DROP ? 0.f : -dl);
   const float c2 = scale * kLog2e;
   const uint32_t dkey = DROP ? drop_key(drop, bh) : 0u;
-  const uint32_t dblk = (uint32_t)(my_q >> 1) * ((uint32_t)S >> 1) + 2u * h;
-  const int dsh = 16 * (my_q & 1);
+  const uint32_t dblk = (uint32_t)(my_q >> 1) * ((uint32_t)S >> 1) + 2u * h + (uint32_t)(my_q & 1);
+  const uint32_t dsel = (my_q & 1) ? 0x07030602u : 0x01050004u;
 
   const E* Kb = K + b * ks_.sb + hk * ks_.sh;
   const E* Vb = V + b * vs.sb + hk * vs.sh;
@@ -660,6 +724,11 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dq_kernel(
         dpt = mfma(fr.rowf(vt, 32 * tt, kk), dof[kk], dpt);
       }
       const bool diag = CAUSAL && ksub + 31 > qw;
+      uint32_t tb[4];  // keep bits of slots 2u (bits 7 / 23) and 2u + 1 (bits 15 / 31)
+      if constexpr (DROP) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) tb[u] = keep_bits(drop_hash(dblk + (ksub >> 1) + 4 * u, dkey), dsel, drop.k4);
+      }
 #pragma unroll
       for (int i = 0; i < 16; i += 2) {
         float p0 = fexp2(st[i]), p1 = fexp2(st[i + 1]);  // with dropout: p / (1 - p_drop)
@@ -669,9 +738,14 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dq_kernel(
         }
         float d0 = dpt[i], d1 = dpt[i + 1];
         if constexpr (DROP) {  // dropped: dP contributes 0, dS = p' (0 - delta')
-          const uint32_t hv = drop_hash(dblk + ((ksub + (i & 3) + 8 * (i >> 2)) >> 1), dkey);
-          if (!keep_byte(hv, dsh, drop.thr)) d0 = -dl;
-          if (!keep_byte(hv, dsh + 8, drop.thr)) d1 = -dl;
+          const uint32_t t = tb[i >> 2];
+          if ((i & 2) == 0) {
+            d0 = and_bit<7>(d0, t) - dl;
+            d1 = and_bit<23>(d1, t) - dl;
+          } else {
+            d0 = and_bit<15>(d0, t) - dl;
+            d1 = and_bit<31>(d1, t) - dl;
+          }
         }
         dpt[i] = p0 * d0;  // dS^T
         dpt[i + 1] = p1 * d1;
@@ -738,11 +812,12 @@ static uint32_t host_fmix32(uint32_t x) {
 // keys: key0 from the seed, key1 from the per-call offset (see drop_key / drop_hash).
 static Drop make_drop(float p, uint64_t seed, uint64_t offset) {
   Drop d;
-  d.thr = (uint32_t)((double)p * 256.0 + 0.5);
-  if (d.thr > 255u) d.thr = 255u;
-  d.inv = (float)(256.0 / (256.0 - (double)d.thr));  // exact for the realised drop rate
-  d.keep = (float)((256.0 - (double)d.thr) / 256.0);
-  d.log2inv = (float)std::log2(256.0 / (256.0 - (double)d.thr));
+  d.thr = (uint32_t)((double)p * 128.0 + 0.5);  // 7-bit threshold (SWAR test, see Drop)
+  if (d.thr > 127u) d.thr = 127u;
+  d.k4 = (128u - d.thr) * 0x01010101u;
+  d.inv = (float)(128.0 / (128.0 - (double)d.thr));  // exact for the realised drop rate
+  d.keep = (float)((128.0 - (double)d.thr) / 128.0);
+  d.log2inv = (float)std::log2(128.0 / (128.0 - (double)d.thr));
   d.key0 = host_fmix32((uint32_t)seed ^ host_fmix32((uint32_t)(seed >> 32) + 0x9E3779B9u));
   d.key1 = host_fmix32((uint32_t)offset * 0x27D4EB2Fu ^ host_fmix32((uint32_t)(offset >> 32) + 0x165667B1u));
   return d;

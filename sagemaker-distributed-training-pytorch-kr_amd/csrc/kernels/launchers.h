@@ -124,5 +124,11 @@ hipError_t smdt_xgmi_allreduce(int dtype, const void* in, void* out, int64_t io_
                                void* const* data_ptrs, void* const* sig_ptrs, int world, int rank,
                                int nranks_local, int64_t region_bytes, int two_shot, int blocks,
                                hipStream_t st);
+// General form (xgmi_allreduce.hip header): mode 0 one-shot / 1 two-shot all-reduce, 2 reduce-scatter,
+// 3 all-gather; in/out_rank_stride: loopback rows (elements).
+hipError_t smdt_xgmi_collective(int mode, int dtype, const void* in, void* out, int64_t in_rank_stride,
+                                int64_t out_rank_stride, int64_t n, int64_t slice_stride, float scale,
+                                void* const* data_ptrs, void* const* sig_ptrs, int world, int rank, int nranks_local,
+                                int64_t region_bytes, int blocks, hipStream_t st);
 
 }  // extern "C"

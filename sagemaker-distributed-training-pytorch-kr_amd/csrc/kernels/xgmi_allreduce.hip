@@ -7,13 +7,23 @@
 // layer in NB3) and has no custom all-reduce; nothing here is modelled on code.
 //
 // Algorithms (chosen per call by the host):
-//   one-shot : stage my input into my region A, signal every peer, wait for every peer, then
-//              reduce the WHOLE tensor by reading all W staging regions (latency-optimal).
-//   two-shot : same staging + barrier, then rank r reduces only slice r of each block's range
-//              (a reduce-scatter through peer reads), publishes it in region B, a second barrier,
-//              and every rank gathers the W-1 other slices (each link carries 2/W of the message).
-// Both accumulate in fp32 in rank order 0..W-1, so every rank ends with bit-identical results
-// (TP replicas must stay identical).
+//   one-shot       : stage my input into my region A, signal every peer, wait for every peer,
+//                    then reduce the WHOLE tensor by reading all W staging regions (latency-optimal).
+//   two-shot       : same staging + barrier, then rank r reduces only slice r of each block's range
+//                    (a reduce-scatter through peer reads), publishes it in region B, a second
+//                    barrier, and every rank gathers the W-1 other slices (each link carries 2/W of
+//                    the message).
+//   reduce-scatter : input = W slices of ns vectors (slice d at in + d * slice stride); block b
+//                    stages sub-range b of EVERY slice, one barrier, then reduces sub-range b of
+//                    slice `rank` over the W staged copies (ZeRO gradient shards; each link carries
+//                    1/W of the message).
+//   all-gather     : input = ns vectors; block b stages its sub-range, one barrier, then copies
+//                    sub-range b of every peer's staged slice into out slice r (ZeRO parameters).
+// Reductions accumulate in fp32 in rank order 0..W-1, so every rank ends with bit-identical results
+// (TP replicas must stay identical). A block's staging and reading ranges coincide, so the
+// per-block barrier is all the ordering a call needs, and an output that aliases the input (ZeRO's
+// in-place reduce-scatter into the bucket, in-place all-gather) is safe: a block overwrites only
+// bytes it staged itself before its barrier.
 //
 // Cross-device visibility (MI355X_MICROARCH.md "visibility", system scope because the consumer is
 // another GPU): every staged byte is stored with sc0|sc1 (write-through) buffer stores, every wave
@@ -183,55 +193,107 @@ __device__ __forceinline__ void reduce_range(const Peers& P, int64_t reg_off, ui
   }
 }
 
-template <typename T, int W, bool kTwoShot>
-__global__ __launch_bounds__(kThreads) void allreduce_kernel(Peers P, int rank0, const u32x4* __restrict__ in,
-                                                             u32x4* __restrict__ out, int64_t io_stride,
-                                                             int64_t nvec, int64_t chunk, int64_t region_bytes,
-                                                             float scale) {
+enum Mode { kOneShot = 0, kTwoShot = 1, kReduceScatter = 2, kAllGather = 3 };
+
+// Call arguments (by value). Vector (16-byte) units throughout. Loopback: blockIdx.y = virtual
+// rank, whose in / out start in_rank_stride / out_rank_stride vectors after the previous one's.
+struct Args {
+  const u32x4* in;
+  u32x4* out;
+  int64_t in_rank_stride, out_rank_stride;
+  int64_t nvec;          // all-reduce: vectors of the tensor; RS / AG: vectors per slice
+  int64_t slice_stride;  // RS: between input slices; AG: between output slices
+  int64_t chunk;         // vectors per block (per slice for RS / AG)
+  int64_t region_bytes;
+  float scale;
+};
+
+template <typename T, int W, int MODE>
+__global__ __launch_bounds__(kThreads) void collective_kernel(Peers P, int rank0, Args a) {
   __shared__ uint32_t s_counter;
   __shared__ int s_ok;
   const int b = blockIdx.x;
   const int rank = rank0 + (int)blockIdx.y;
-  in += (int64_t)blockIdx.y * io_stride;
-  out += (int64_t)blockIdx.y * io_stride;
+  const u32x4* __restrict__ in = a.in + (int64_t)blockIdx.y * a.in_rank_stride;
+  u32x4* __restrict__ out = a.out + (int64_t)blockIdx.y * a.out_rank_stride;
   SignalBuf* me = P.sig[rank];
+  const int64_t nvec = a.nvec, chunk = a.chunk;
   const int64_t v0 = (int64_t)b * chunk < nvec ? (int64_t)b * chunk : nvec;
   const int64_t v1 = v0 + chunk < nvec ? v0 + chunk : nvec;
+  // ranges this block writes (NaN-filled on failure)
+  auto fail = [&]() {
+    if constexpr (MODE == kReduceScatter) {
+      nan_fill<T>(out, v0, v1);
+    } else if constexpr (MODE == kAllGather) {
+      for (int r = 0; r < W; ++r) nan_fill<T>(out + (int64_t)r * a.slice_stride, v0, v1);
+    } else {
+      nan_fill<T>(out, v0, v1);
+    }
+  };
   if (threadIdx.x == 0) {
     s_counter = load_sys(&me->counter[b]);
     s_ok = load_sys(&me->error) == 0u;
   }
   __syncthreads();
   if (!s_ok) {  // a previous call failed: never wait on peers again (the host must rebuild)
-    nan_fill<T>(out, v0, v1);
+    fail();
     return;
   }
   const uint32_t c = s_counter;
   const uint32_t half = (c >> 1) & 1u;
-  const uint32_t rb = (uint32_t)region_bytes;
-  const int64_t offA = (int64_t)(2 * half) * region_bytes;
-  const int64_t offB = offA + region_bytes;
+  const uint32_t rb = (uint32_t)a.region_bytes;
+  const int64_t offA = (int64_t)(2 * half) * a.region_bytes;
+  const int64_t offB = offA + a.region_bytes;
 
   {  // 1) stage my input, write-through, so peers read it from memory
     const auto mine = rsrc(P.data[rank] + offA, rb);
-    for (int64_t v = v0 + threadIdx.x; v < v1; v += kThreads)
-      __builtin_amdgcn_raw_buffer_store_b128(in[v], mine, (int)(v * 16), 0, kSysAux);
+    if constexpr (MODE == kReduceScatter) {
+#pragma unroll
+      for (int d = 0; d < W; ++d) {
+        const u32x4* src = in + (int64_t)d * a.slice_stride;
+        const int64_t base = (int64_t)d * nvec;
+        for (int64_t v = v0 + threadIdx.x; v < v1; v += kThreads)
+          __builtin_amdgcn_raw_buffer_store_b128(src[v], mine, (int)((base + v) * 16), 0, kSysAux);
+      }
+    } else {
+      for (int64_t v = v0 + threadIdx.x; v < v1; v += kThreads)
+        __builtin_amdgcn_raw_buffer_store_b128(in[v], mine, (int)(v * 16), 0, kSysAux);
+    }
   }
   if (!block_barrier<W>(P, rank, b, c + 1, &s_ok)) {
-    nan_fill<T>(out, v0, v1);
+    fail();
     return;
   }
 
-  if constexpr (!kTwoShot) {
-    reduce_range<T, W, false>(P, offA, rb, v0, v1, scale, out, rsrc(nullptr, 0));
+  if constexpr (MODE == kOneShot) {
+    reduce_range<T, W, false>(P, offA, rb, v0, v1, a.scale, out, rsrc(nullptr, 0));
+  } else if constexpr (MODE == kReduceScatter) {
+    // 2) my slice's sub-range, summed over the W staged copies (rank order)
+    u32x4* o = out - (int64_t)rank * nvec;  // reduce_range indexes by the staged position
+    reduce_range<T, W, false>(P, offA, rb, (int64_t)rank * nvec + v0, (int64_t)rank * nvec + v1, a.scale, o,
+                              rsrc(nullptr, 0));
+  } else if constexpr (MODE == kAllGather) {
+    // 2) every rank's sub-range (mine from my own input)
+#pragma unroll
+    for (int r = 0; r < W; ++r) {
+      u32x4* o = out + (int64_t)r * a.slice_stride;
+      if (r == rank) {
+        if (in != o)
+          for (int64_t v = v0 + threadIdx.x; v < v1; v += kThreads) o[v] = in[v];
+        continue;
+      }
+      const auto src = rsrc(P.data[r] + offA, rb);
+      for (int64_t v = v0 + threadIdx.x; v < v1; v += kThreads)
+        o[v] = __builtin_amdgcn_raw_buffer_load_b128(src, (int)(v * 16), 0, kSysAux);
+    }
   } else {
     // 2) reduce-scatter: I own slice `rank` of this block's range; publish it in my region B
     const int64_t sl = (v1 - v0 + W - 1) / W;
     auto lo = [&](int r) { const int64_t x = v0 + (int64_t)r * sl; return x < v1 ? x : v1; };
     auto hi = [&](int r) { const int64_t x = lo(r) + sl; return x < v1 ? x : v1; };
-    reduce_range<T, W, true>(P, offA, rb, lo(rank), hi(rank), scale, out, rsrc(P.data[rank] + offB, rb));
+    reduce_range<T, W, true>(P, offA, rb, lo(rank), hi(rank), a.scale, out, rsrc(P.data[rank] + offB, rb));
     if (!block_barrier<W>(P, rank, b, c + 2, &s_ok)) {
-      nan_fill<T>(out, v0, v1);
+      fail();
       return;
     }
     // 3) all-gather the other ranks' slices from their region B
@@ -248,27 +310,25 @@ __global__ __launch_bounds__(kThreads) void allreduce_kernel(Peers P, int rank0,
 }
 
 template <typename T, int W>
-hipError_t launch_w(const Peers& P, int rank0, int nranks_local, const void* in, void* out, int64_t io_stride,
-                    int64_t nvec, int blocks, int64_t region_bytes, float scale, int two_shot, hipStream_t st) {
-  const int64_t chunk = (nvec + blocks - 1) / blocks;
+hipError_t launch_w(int mode, const Peers& P, int rank0, int nranks_local, const Args& a, int blocks, hipStream_t st) {
   const dim3 grid(blocks, nranks_local);  // ALL blocks, also those whose range is empty
-  if (two_shot)
-    hipLaunchKernelGGL((allreduce_kernel<T, W, true>), grid, dim3(kThreads), 0, st, P, rank0,
-                       (const u32x4*)in, (u32x4*)out, io_stride, nvec, chunk, region_bytes, scale);
-  else
-    hipLaunchKernelGGL((allreduce_kernel<T, W, false>), grid, dim3(kThreads), 0, st, P, rank0,
-                       (const u32x4*)in, (u32x4*)out, io_stride, nvec, chunk, region_bytes, scale);
+  switch (mode) {
+    case kOneShot: hipLaunchKernelGGL((collective_kernel<T, W, kOneShot>), grid, dim3(kThreads), 0, st, P, rank0, a); break;
+    case kTwoShot: hipLaunchKernelGGL((collective_kernel<T, W, kTwoShot>), grid, dim3(kThreads), 0, st, P, rank0, a); break;
+    case kReduceScatter: hipLaunchKernelGGL((collective_kernel<T, W, kReduceScatter>), grid, dim3(kThreads), 0, st, P, rank0, a); break;
+    case kAllGather: hipLaunchKernelGGL((collective_kernel<T, W, kAllGather>), grid, dim3(kThreads), 0, st, P, rank0, a); break;
+    default: return hipErrorInvalidValue;
+  }
   return hipGetLastError();
 }
 
 template <typename T>
-hipError_t launch_t(const Peers& P, int world, int rank0, int nranks_local, const void* in, void* out,
-                    int64_t io_stride, int64_t nvec, int blocks, int64_t region_bytes, float scale,
-                    int two_shot, hipStream_t st) {
+hipError_t launch_t(int mode, const Peers& P, int world, int rank0, int nranks_local, const Args& a, int blocks,
+                    hipStream_t st) {
   switch (world) {
-    case 2: return launch_w<T, 2>(P, rank0, nranks_local, in, out, io_stride, nvec, blocks, region_bytes, scale, two_shot, st);
-    case 4: return launch_w<T, 4>(P, rank0, nranks_local, in, out, io_stride, nvec, blocks, region_bytes, scale, two_shot, st);
-    case 8: return launch_w<T, 8>(P, rank0, nranks_local, in, out, io_stride, nvec, blocks, region_bytes, scale, two_shot, st);
+    case 2: return launch_w<T, 2>(mode, P, rank0, nranks_local, a, blocks, st);
+    case 4: return launch_w<T, 4>(mode, P, rank0, nranks_local, a, blocks, st);
+    case 8: return launch_w<T, 8>(mode, P, rank0, nranks_local, a, blocks, st);
     default: return hipErrorInvalidValue;
   }
 }
@@ -319,32 +379,56 @@ hipError_t smdt_ar_read_error(void* sig, int* err) {
   return e;
 }
 
-hipError_t smdt_xgmi_allreduce(int dtype, const void* in, void* out, int64_t io_stride, int64_t n, float scale,
-                               void* const* data_ptrs, void* const* sig_ptrs, int world, int rank,
-                               int nranks_local, int64_t region_bytes, int two_shot, int blocks,
-                               hipStream_t st) {
+// mode: 0 one-shot / 1 two-shot all-reduce (n = elements of the tensor), 2 reduce-scatter (n =
+// elements per slice; input slices slice_stride elements apart, output n elements), 3 all-gather
+// (n = elements per slice; output slices slice_stride elements apart). io strides: loopback only.
+hipError_t smdt_xgmi_collective(int mode, int dtype, const void* in, void* out, int64_t in_rank_stride,
+                                int64_t out_rank_stride, int64_t n, int64_t slice_stride, float scale,
+                                void* const* data_ptrs, void* const* sig_ptrs, int world, int rank, int nranks_local,
+                                int64_t region_bytes, int blocks, hipStream_t st) {
+  if (mode < 0 || mode > 3) return hipErrorInvalidValue;
   if (world < 2 || world > ar::kMaxRanks || rank < 0 || nranks_local < 1 || rank + nranks_local > world)
     return hipErrorInvalidValue;
   if (blocks < 1 || blocks > ar::kMaxBlocks) return hipErrorInvalidValue;
   const int esz = dtype == 0 ? 4 : 2;
-  if (n <= 0 || (n * esz) % 16 != 0 || n * esz > region_bytes || region_bytes > (1ll << 31) - 16 ||
+  const int64_t staged = mode == 2 ? n * world : n;  // elements one rank stages
+  if (n <= 0 || (n * esz) % 16 != 0 || staged * esz > region_bytes || region_bytes > (1ll << 31) - 16 ||
       region_bytes % 16 != 0)
     return hipErrorInvalidValue;
-  if ((((uintptr_t)in | (uintptr_t)out) & 15) != 0 || (io_stride * esz) % 16 != 0) return hipErrorInvalidValue;
+  if (mode >= 2 && (slice_stride < n || (slice_stride * esz) % 16 != 0)) return hipErrorInvalidValue;
+  if ((((uintptr_t)in | (uintptr_t)out) & 15) != 0 || (in_rank_stride * esz) % 16 != 0 ||
+      (out_rank_stride * esz) % 16 != 0)
+    return hipErrorInvalidValue;
   ar::Peers P{};
   for (int r = 0; r < world; ++r) {
     if (!data_ptrs[r] || !sig_ptrs[r]) return hipErrorInvalidValue;
     P.data[r] = (char*)data_ptrs[r];
     P.sig[r] = (ar::SignalBuf*)sig_ptrs[r];
   }
-  const int64_t nvec = n * esz / 16;
-  const int64_t vstride = io_stride * esz / 16;
+  ar::Args a;
+  a.in = (const ar::u32x4*)in;
+  a.out = (ar::u32x4*)out;
+  a.in_rank_stride = in_rank_stride * esz / 16;
+  a.out_rank_stride = out_rank_stride * esz / 16;
+  a.nvec = n * esz / 16;
+  a.slice_stride = mode >= 2 ? slice_stride * esz / 16 : 0;
+  a.chunk = (a.nvec + blocks - 1) / blocks;
+  a.region_bytes = region_bytes;
+  a.scale = scale;
   switch (dtype) {
-    case 0: return ar::launch_t<float>(P, world, rank, nranks_local, in, out, vstride, nvec, blocks, region_bytes, scale, two_shot, st);
-    case 1: return ar::launch_t<bf16>(P, world, rank, nranks_local, in, out, vstride, nvec, blocks, region_bytes, scale, two_shot, st);
-    case 2: return ar::launch_t<f16>(P, world, rank, nranks_local, in, out, vstride, nvec, blocks, region_bytes, scale, two_shot, st);
+    case 0: return ar::launch_t<float>(mode, P, world, rank, nranks_local, a, blocks, st);
+    case 1: return ar::launch_t<bf16>(mode, P, world, rank, nranks_local, a, blocks, st);
+    case 2: return ar::launch_t<f16>(mode, P, world, rank, nranks_local, a, blocks, st);
     default: return hipErrorInvalidValue;
   }
+}
+
+hipError_t smdt_xgmi_allreduce(int dtype, const void* in, void* out, int64_t io_stride, int64_t n, float scale,
+                               void* const* data_ptrs, void* const* sig_ptrs, int world, int rank,
+                               int nranks_local, int64_t region_bytes, int two_shot, int blocks,
+                               hipStream_t st) {
+  return smdt_xgmi_collective(two_shot ? 1 : 0, dtype, in, out, io_stride, io_stride, n, 0, scale, data_ptrs,
+                              sig_ptrs, world, rank, nranks_local, region_bytes, blocks, st);
 }
 
 }  // extern "C"

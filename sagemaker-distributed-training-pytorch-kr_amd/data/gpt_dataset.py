@@ -195,7 +195,7 @@ def _index_mappings(name, data_prefix, documents, sizes, splits_string, num_samp
             ok = 0
     if dist.is_initialized():
         st = ps.get_state()
-        dev = torch.device("cuda", torch.cuda.current_device()) if (torch.cuda.is_available() and dist.get_backend() == "nccl") else torch.device("cpu")
+        dev = torch.device("cuda", torch.cuda.current_device()) if (torch.cuda.is_available() and dist.get_backend() in ("nccl", "smddp")) else torch.device("cpu")
         c = torch.tensor([ok], dtype=torch.long, device=dev)
         dist.barrier()
         dist.all_reduce(c)  # world: every rank must see the files (node-local builders)

@@ -357,16 +357,17 @@ def _fmix32_i(x: int) -> int:
 
 
 def flash_dropout_thr(p: float):
-    """(8-bit threshold, keep scale) the kernels use for drop probability ``p``: the realised drop
-    rate is round(p * 256) / 256 (FlashAttention-2 also thresholds random bytes)."""
-    thr = min(int(p * 256.0 + 0.5), 255)
-    return thr, 256.0 / (256.0 - thr)
+    """(7-bit threshold, keep scale) the kernels use for drop probability ``p``: the realised drop
+    rate is round(p * 128) / 128 (the kernels test the low 7 bits of each random byte with one
+    SWAR add per 4 bytes; FlashAttention-2 thresholds random bytes too)."""
+    thr = min(int(p * 128.0 + 0.5), 127)
+    return thr, 128.0 / (128.0 - thr)
 
 
 def flash_dropout_keep_mask(B: int, H: int, S: int, p: float, seed: int, offset: int, device=None):
     """Bit-exact twin of the flash kernels' dropout mask: bool [B, H, S(q), S(k)], True = kept
     (see ``drop_hash`` in flash_attn.hip): each 2x2 (query, key) block shares one hash, byte
-    2 (q & 1) + (k & 1) decides the element."""
+    2 (q & 1) + (k & 1) decides the element (kept iff its low 7 bits >= the threshold)."""
     thr, _ = flash_dropout_thr(p)
     key0 = _fmix32_i((seed & _M32) ^ _fmix32_i(((seed >> 32) + 0x9E3779B9) & _M32))
     key1 = _fmix32_i((((offset & _M32) * 0x27D4EB2F) & _M32) ^ _fmix32_i(((offset >> 32) + 0x165667B1) & _M32))
@@ -379,7 +380,7 @@ def flash_dropout_keep_mask(B: int, H: int, S: int, p: float, seed: int, offset:
     x = (((x ^ (x >> 16)) & 0xFFFFFF) * 0x45D9F3) & _M32   # v_mul_u32_u24
     x = (((x ^ (x >> 16)) & 0xFFFFFF) * 0x45D9F3) & _M32
     x = x ^ (x >> 16)
-    by = torch.stack([(x >> (8 * i)) & 0xFF for i in range(4)], dim=-1) >= thr           # [BH, S/2, S/2, 4]
+    by = torch.stack([(x >> (8 * i)) & 0x7F for i in range(4)], dim=-1) >= thr           # [BH, S/2, S/2, 4]
     # byte 2 qb + kb -> [BH, S/2, S/2, 2(q), 2(k)] -> [BH, S/2, 2, S/2, 2]
     keep = by.view(B * H, half, half, 2, 2).permute(0, 1, 3, 2, 4)
     return keep.reshape(B, H, S, S)

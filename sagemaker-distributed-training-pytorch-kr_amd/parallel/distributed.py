@@ -106,14 +106,15 @@ class DistributedDataParallel(nn.Module):
             raise ValueError("ZeRO stage >= 2 gradient sharding needs the explicit-step API and pp == 1")
         self.grad_dtype = grad_dtype
         self.sync_enabled = True
-        backend = dist.get_backend(self.dp_group) if self.dp > 1 else "none"
-        self.use_avg = average_in_collective and backend == "nccl"
-        # Buckets that fit its staging region are all-reduced by the xGMI IPC kernel on its own
-        # stream (comm/xgmi.py: SMDT_XGMI_ALLREDUCE=1, or a job that asked for backend "smddp").
-        self.xgmi = None
-        if self.dp > 1 and backend == "nccl" and not use_distributed_optimizer:
-            from ..comm import xgmi as _xgmi
-            self.xgmi = _xgmi.create_for_group(self.dp_group)
+        from ..comm import xgmi as _xgmi
+        # "smddp" is RCCL underneath (comm/smddp.py): AVG reductions and the xGMI path apply to it
+        rccl = self.dp > 1 and _xgmi.rccl_backend(self.dp_group)
+        self.use_avg = average_in_collective and rccl
+        # Bucket all-reduces, ZeRO reduce-scatters and parameter all-gathers run on the xGMI IPC
+        # kernel on its own stream (comm/xgmi.py: SMDT_XGMI_ALLREDUCE=1, or a job that asked for
+        # the "smddp" backend); messages larger than its staging region are chunked by the engine.
+        self.xgmi = _xgmi.create_for_group(self.dp_group) if rccl else None
+        self._syncs = 0
 
         params = [p for p in module.parameters() if p.requires_grad]
         seen = set()
@@ -308,7 +309,10 @@ class DistributedDataParallel(nn.Module):
         if self.zero:
             s, e = self.shard_range(b)
             out = self.grad_data[s:e]
-            if self.use_avg:
+            h = self.xgmi.reduce_scatter_async(out, view, op="avg") if self.xgmi is not None else None
+            if h is not None:
+                b.handle = h
+            elif self.use_avg:
                 b.handle = dist.reduce_scatter_tensor(out, view, op=dist.ReduceOp.AVG, group=self.dp_group,
                                                       async_op=True)
             else:
@@ -370,9 +374,12 @@ class DistributedDataParallel(nn.Module):
         fresh = b.index in self._store_fresh
         self._store_fresh.discard(b.index)
         out = sh if fresh else torch.empty_like(sh)
+        h = self.xgmi.reduce_scatter_async(out, buf, op="avg") if (self.xgmi is not None and self.dp > 1) else None
         if self.dp == 1:
             out.copy_(buf)
             handle = None
+        elif h is not None:
+            handle = h
         elif self.use_avg:
             handle = dist.reduce_scatter_tensor(out, buf, op=dist.ReduceOp.AVG, group=self.dp_group, async_op=True)
         else:
@@ -426,6 +433,7 @@ class DistributedDataParallel(nn.Module):
                     self._launch_sharded(b)
             for b in self.buckets:
                 self._retire_rs(b)
+            self._check_xgmi()
             st = self.st
             if st.tp > 1 and st.tp_group is not None:
                 for b in self.buckets:
@@ -439,12 +447,24 @@ class DistributedDataParallel(nn.Module):
         for b in self.buckets:
             if b.handle is not None:
                 b.handle.wait()
+        self._check_xgmi()
         st = self.st
         if st.tp > 1 and st.tp_group is not None:
             for key, (s, e) in self.regions.items():
                 if key[2]:  # sequence-parallel params: sum partial grads over the TP group
                     dist.all_reduce(self.grad_data[s:e], group=st.tp_group)
         self._reset_pending()
+
+    XGMI_CHECK_EVERY = 64
+
+    def _check_xgmi(self):
+        """Every ``XGMI_CHECK_EVERY`` syncs read the xGMI engine's sticky error word (a peer that
+        never arrived NaN-fills the outputs): raise instead of training on silently."""
+        if self.xgmi is None:
+            return
+        self._syncs += 1
+        if self._syncs % self.XGMI_CHECK_EVERY == 0:
+            self.xgmi.check()
 
     def zero_grad_buffer(self):
         if self.zero_stage >= 2:
@@ -480,8 +500,10 @@ class DistributedDataParallel(nn.Module):
         self.wait_param_gather()
         for b in reversed(self.buckets):
             s, e = self.shard_range(b)
-            b.ag_handle = dist.all_gather_into_tensor(self.param_data[b.start:b.end], self.param_data[s:e],
-                                                      group=self.dp_group, async_op=True)
+            full, mine = self.param_data[b.start:b.end], self.param_data[s:e]
+            h = self.xgmi.all_gather_async(full, mine) if self.xgmi is not None else None
+            b.ag_handle = h if h is not None else dist.all_gather_into_tensor(full, mine, group=self.dp_group,
+                                                                               async_op=True)
         if not self.overlap_param_gather:
             self.wait_param_gather()
 

@@ -113,7 +113,7 @@ class Timers:
             dist.barrier()
         ws = dist.get_world_size() if dist.is_initialized() else 1
         rk = dist.get_rank() if dist.is_initialized() else 0
-        dev = torch.device("cuda", torch.cuda.current_device()) if (torch.cuda.is_available() and dist.is_initialized() and dist.get_backend() == "nccl") else torch.device("cpu")
+        dev = torch.device("cuda", torch.cuda.current_device()) if (torch.cuda.is_available() and dist.is_initialized() and dist.get_backend() in ("nccl", "smddp")) else torch.device("cpu")
         t = torch.zeros(ws, len(names), dtype=torch.float, device=dev)
         for i, n in enumerate(names):
             if n in self._timers:

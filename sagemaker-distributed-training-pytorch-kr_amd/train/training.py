@@ -435,7 +435,7 @@ def train(forward_step_func, model, optimizer, scheduler, train_iter, valid_iter
         if args.exit_duration_in_mins:
             done = torch.tensor([int((time.time() - _START_TIME) / 60.0 > args.exit_duration_in_mins)])
             if dist.is_initialized():
-                if torch.cuda.is_available() and dist.get_backend() == "nccl":
+                if torch.cuda.is_available() and dist.get_backend() in ("nccl", "smddp"):
                     done = done.cuda()
                 dist.all_reduce(done, op=dist.ReduceOp.MAX)
             if done.item():
@@ -469,7 +469,7 @@ def pretrain(train_valid_test_dataset_provider, model_provider, model_type, forw
     st = ps.get_state()
     flags = torch.tensor([int(valid_iter is not None), int(test_iter is not None)], dtype=torch.long)
     if st.tp > 1 and st.tp_group is not None:
-        if torch.cuda.is_available() and dist.get_backend() == "nccl":
+        if torch.cuda.is_available() and dist.get_backend() in ("nccl", "smddp"):
             flags = flags.cuda()
         dist.broadcast(flags, st.tp_ranks[0], group=st.tp_group)
     args.do_valid, args.do_test = bool(flags[0].item()), bool(flags[1].item())

@@ -303,6 +303,28 @@ def xgmi_ipc_worker(rank, world, port, outdir):
                 assert eng.all_reduce(x)
                 torch.cuda.synchronize()
                 res["ok"].append(bool(torch.equal(x, ref)))
+        # chunked all-reduce (message 3 x the region), reduce-scatter (in place into the
+        # bucket's own slice, as ZeRO does) and all-gather (in place), exact on integer data
+        n_big = 3 * (16 << 20) // 4 + 1024
+        big = torch.arange(n_big, device="cuda", dtype=torch.float32) % 89 + 7.0 * rank
+        ref_big = sum(torch.arange(n_big, device="cuda", dtype=torch.float32) % 89 + 7.0 * r for r in range(world))
+        assert eng.all_reduce(big)
+        torch.cuda.synchronize()
+        res["ok"].append(bool(torch.equal(big, ref_big)))
+        for ns in (4096, 5 * (16 << 20) // (4 * world) + 512):   # the second needs 3 column bands
+            full = torch.arange(world * ns, device="cuda", dtype=torch.float32) % 53 + 3.0 * rank
+            want = sum(torch.arange(world * ns, device="cuda", dtype=torch.float32) % 53 + 3.0 * r
+                       for r in range(world)).view(world, ns)[rank].clone()
+            mine = full.view(world, ns)[rank]
+            assert eng.reduce_scatter(mine, full)
+            torch.cuda.synchronize()
+            res["ok"].append(bool(torch.equal(mine, want)))
+            buf = torch.full((world * ns,), -1.0, device="cuda")
+            buf.view(world, ns)[rank].copy_(torch.arange(ns, device="cuda", dtype=torch.float32) + 100.0 * rank)
+            assert eng.all_gather(buf, buf.view(world, ns)[rank])
+            torch.cuda.synchronize()
+            want_ag = torch.cat([torch.arange(ns, device="cuda", dtype=torch.float32) + 100.0 * r for r in range(world)])
+            res["ok"].append(bool(torch.equal(buf, want_ag)))
         res["error_word"] = eng.error()
         eng.close()
         dist.destroy_process_group()

@@ -120,4 +120,64 @@ def test_cross_process_ipc_allreduce_world2():
                 out.append(pickle.load(f))
     for r, res in enumerate(out):
         assert res["err"] is None, f"rank {r}:\n{res['err']}"
-        assert res["error_word"] == 0 and all(res["ok"]) and len(res["ok"]) == 12, (r, res)
+        assert res["error_word"] == 0 and all(res["ok"]) and len(res["ok"]) == 17, (r, res)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 4, 8])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_loopback_reduce_scatter_and_all_gather(world, dtype):
+    """ZeRO's collectives on the xGMI kernel: reduce-scatter (also in place into each rank's own
+    slice of its bucket) and all-gather (also in place), W virtual ranks in one launch."""
+    torch.manual_seed(10 + world)
+    lb = xgmi.XgmiLoopback(world, region_bytes=4 << 20)
+    try:
+        esz = torch.tensor([], dtype=dtype).element_size()
+        for ns in (16 // esz, 999 * 16 // esz, (4 << 20) // esz // world):
+            for rep in range(3):
+                x = torch.randn(world, world * ns, device="cuda", dtype=dtype)
+                scale = 1.0 / world if rep == 1 else 1.0
+                ref = _ref(x, scale).view(world, ns)             # slice d of the reduced tensor
+                out = lb.reduce_scatter(x, scale)
+                for r in range(world):
+                    if dtype == torch.float32:
+                        assert torch.equal(out[r], ref[r]), (ns, rep, r)
+                    else:
+                        torch.testing.assert_close(out[r].float(), ref[r].float(), atol=0, rtol=1e-2)
+                # in place: rank r's output is its own slice r of its input row
+                own = x.as_strided((world, ns), ((world + 1) * ns, 1))
+                lb.reduce_scatter(x, scale, out=own)
+                assert torch.equal(own.clone(), out)
+                # all-gather: row r of the result = every rank's slice in rank order
+                sl = torch.randn(world, ns, device="cuda", dtype=dtype)
+                g = lb.all_gather(sl)
+                for r in range(world):
+                    assert torch.equal(g[r], sl.reshape(-1))
+                y = torch.zeros(world, world * ns, device="cuda", dtype=dtype)
+                yown = y.as_strided((world, ns), ((world + 1) * ns, 1))
+                yown.copy_(sl)
+                lb.all_gather(yown, out=y)
+                assert torch.equal(y, g)
+        assert lb.errors() == [0] * world
+    finally:
+        lb.close()
+
+
+def test_chunking_bands_cover_and_align():
+    b = xgmi._bands(1000, 96, 4)
+    assert b[0] == (0, 96) and b[-1][1] == 1000 and all(hi - lo <= 96 for lo, hi in b)
+    assert all(lo % 4 == 0 for lo, _ in b) and all(b[i][1] == b[i + 1][0] for i in range(len(b) - 1))
+    assert xgmi._bands(8, 3, 4) == [(0, 4), (4, 8)]
+
+
+def test_smddp_backend_name_turns_xgmi_on(monkeypatch):
+    """A script that calls dist.init_process_group(backend="smddp") directly (no init_distributed)
+    still gets the xGMI collectives and RCCL's AVG reductions."""
+    import torch.distributed as dist
+    monkeypatch.delenv("SMDT_XGMI_ALLREDUCE", raising=False)
+    monkeypatch.setattr(xgmi, "_SMDDP_REQUESTED", False)
+    monkeypatch.setattr(dist, "is_initialized", lambda: True)
+    monkeypatch.setattr(dist, "get_backend", lambda group=None: "smddp")
+    assert xgmi.wanted() and xgmi.rccl_backend()
+    monkeypatch.setattr(dist, "get_backend", lambda group=None: "gloo")
+    assert not xgmi.wanted() and not xgmi.rccl_backend()
