@@ -207,170 +207,9 @@ bool wgrad_accumulate(torch::Tensor main_grad, torch::Tensor dy, torch::Tensor x
 }
 
 
-// ---------------------------------------------------------------------------------------------
-// GEMMs with fused epilogues (the MLP's bias + GeLU, Megatron bias_gelu / K5 folded into the
-// GEMM that produces or consumes the activation):
-//   linear_gelu_fwd : out = gelu(x w^T + b), aux = x w^T + b          (HIPBLASLT_EPILOGUE_GELU_AUX_BIAS)
-//   linear_dgelu_bwd: out = (dy w2) * gelu'(aux), bgrad = sum_rows(out) (HIPBLASLT_EPILOGUE_DGELU_BGRAD)
-// Column-major views: D[N x M] = op(A) op(B) with row-major activations read as their transposes.
-struct EPlan {
-  hipblasLtMatmulDesc_t desc = nullptr;
-  hipblasLtMatrixLayout_t la = nullptr, lb = nullptr, ld = nullptr;
-  hipblasLtMatmulAlgo_t algo;
-  size_t ws = 0;
-  bool ok = false;
-  hipDataType bias_t = HIP_R_32F;
-};
-std::map<std::tuple<int, int64_t, int64_t, int64_t, int>, EPlan> g_eplans;
-
-// kind 0: fwd (A = w [N,K] -> op T, B = x [M,K] -> op N, m=N n=M k=K)
-// kind 1: dgrad (A = w2 [N2,N] -> op N, B = dy [M,N2] -> op N, m=N n=M k=N2)
-EPlan make_eplan(DevState& st, int kind, int64_t m, int64_t n, int64_t k, hipDataType io_t, const void* A,
-                 const void* B, void* D, void* bias_io, void* bias_f32, void* aux) {
-  EPlan p;
-  // This hipBLASLt build does not ship every epilogue / bias / aux type combination: try the
-  // natural one first, then fp32 bias and the default (= D) aux type.
-  // (kind 1's bias is the fp32 bgrad output: fp32 only.)
-  const hipDataType bias_opts[2] = {kind == 0 ? io_t : HIP_R_32F, HIP_R_32F};
-  hipblasLtMatmulHeuristicResult_t res[16];
-  int cnt = 0;
-  for (int variant = 0; variant < 4 && cnt <= 0; ++variant) {
-    if (p.desc) hipblasLtMatmulDescDestroy(p.desc);
-    if (p.la) hipblasLtMatrixLayoutDestroy(p.la);
-    if (p.lb) hipblasLtMatrixLayoutDestroy(p.lb);
-    if (p.ld) hipblasLtMatrixLayoutDestroy(p.ld);
-    p = EPlan();
-    if (!chk(hipblasLtMatmulDescCreate(&p.desc, HIPBLAS_COMPUTE_32F, HIP_R_32F))) return p;
-    hipblasOperation_t ta = kind == 0 ? HIPBLAS_OP_T : HIPBLAS_OP_N, tb = HIPBLAS_OP_N;
-    hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_TRANSA, &ta, sizeof(ta));
-    hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_TRANSB, &tb, sizeof(tb));
-    hipblasLtEpilogue_t epi = kind == 0 ? HIPBLASLT_EPILOGUE_GELU_AUX_BIAS : HIPBLASLT_EPILOGUE_DGELU_BGRAD;
-    hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_EPILOGUE, &epi, sizeof(epi));
-    hipDataType bias_t = bias_opts[variant & 1];
-    p.bias_t = bias_t;
-    void* bias = bias_t == HIP_R_32F ? bias_f32 : bias_io;
-    hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_BIAS_DATA_TYPE, &bias_t, sizeof(bias_t));
-    if (variant < 2) {
-      hipDataType aux_t = io_t;
-      hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_EPILOGUE_AUX_DATA_TYPE, &aux_t, sizeof(aux_t));
-    }
-    int64_t aux_ld = m;
-    hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_EPILOGUE_AUX_LD, &aux_ld, sizeof(aux_ld));
-    hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &bias, sizeof(bias));
-    hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_EPILOGUE_AUX_POINTER, &aux, sizeof(aux));
-    // A: op(A) is m x k
-    if (kind == 0) {
-      if (!chk(hipblasLtMatrixLayoutCreate(&p.la, io_t, k, m, k))) return p;   // w [N,K] row-major = K x N col-major
-    } else {
-      if (!chk(hipblasLtMatrixLayoutCreate(&p.la, io_t, m, k, m))) return p;   // w2 [N2,N] = N x N2 col-major
-    }
-    if (!chk(hipblasLtMatrixLayoutCreate(&p.lb, io_t, k, n, k))) return p;     // [M, k] row-major = k x M
-    if (!chk(hipblasLtMatrixLayoutCreate(&p.ld, io_t, m, n, m))) return p;     // [M, m] row-major = m x M
-    hipblasLtMatmulPreference_t pref;
-    if (!chk(hipblasLtMatmulPreferenceCreate(&pref))) return p;
-    size_t wsz = kWorkspace;
-    hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &wsz, sizeof(wsz));
-    cnt = 0;
-    hipblasStatus_t s = hipblasLtMatmulAlgoGetHeuristic(st.handle, p.desc, p.la, p.lb, p.ld, p.ld, pref, 16, res, &cnt);
-    hipblasLtMatmulPreferenceDestroy(pref);
-    if (std::getenv("SMDT_BLASLT_DEBUG"))
-      fprintf(stderr, "[smdt blaslt] epilogue kind %d variant %d m=%ld n=%ld k=%ld: heuristic status %d, %d candidates\n",
-              kind, variant, (long)m, (long)n, (long)k, (int)s, cnt);
-    if (!chk(s)) cnt = 0;
-  }
-  if (cnt <= 0) return p;
-  hipStream_t stream = c10::hip::getCurrentHIPStream().stream();
-  hipEvent_t e0, e1;
-  hipEventCreate(&e0);
-  hipEventCreate(&e1);
-  const float alpha = 1.f, beta = 0.f;
-  int best = -1;
-  float best_ms = 1e30f;
-  for (int i = 0; i < cnt; ++i) {
-    if (res[i].state != HIPBLAS_STATUS_SUCCESS || res[i].workspaceSize > kWorkspace) continue;
-    bool okc = chk(hipblasLtMatmul(st.handle, p.desc, &alpha, A, p.la, B, p.lb, &beta, D, p.ld, D, p.ld,
-                                   &res[i].algo, st.workspace.data_ptr(), res[i].workspaceSize, stream));
-    if (!okc) continue;
-    hipEventRecord(e0, stream);
-    for (int r = 0; r < 3; ++r)
-      hipblasLtMatmul(st.handle, p.desc, &alpha, A, p.la, B, p.lb, &beta, D, p.ld, D, p.ld, &res[i].algo,
-                      st.workspace.data_ptr(), res[i].workspaceSize, stream);
-    hipEventRecord(e1, stream);
-    hipEventSynchronize(e1);
-    float ms = 0.f;
-    hipEventElapsedTime(&ms, e0, e1);
-    if (ms < best_ms) {
-      best_ms = ms;
-      best = i;
-    }
-  }
-  hipEventDestroy(e0);
-  hipEventDestroy(e1);
-  if (std::getenv("SMDT_BLASLT_DEBUG"))
-    fprintf(stderr, "[smdt blaslt] epilogue kind %d: best candidate %d (%.3f ms / 3 runs)\n", kind, best, best_ms);
-  if (best >= 0) {
-    p.algo = res[best].algo;
-    p.ws = res[best].workspaceSize;
-    p.ok = true;
-  }
-  return p;
-}
-
-bool run_eplan(int kind, int64_t m, int64_t n, int64_t k, const torch::Tensor& like, const void* A, const void* B,
-               void* D, const torch::Tensor& bias, void* aux) {
-  hipDataType io_t = like.scalar_type() == at::kBFloat16 ? HIP_R_16BF : HIP_R_16F;
-  std::lock_guard<std::mutex> lk(g_mu);
-  const int dev = like.get_device();
-  DevState& st = state_for(dev, like.options());
-  // kind 0 may run with an fp32 copy of the bf16/fp16 bias; kind 1's bias is already fp32.
-  torch::Tensor bias_f32 = bias.scalar_type() == at::kFloat ? bias : bias.to(at::kFloat);
-  auto key = std::make_tuple(kind, m, n, k, (int)io_t);
-  auto it = g_eplans.find(key);
-  if (it == g_eplans.end())
-    it = g_eplans.emplace(key, make_eplan(st, kind, m, n, k, io_t, A, B, D, bias.data_ptr(), bias_f32.data_ptr(), aux))
-             .first;
-  EPlan& p = it->second;
-  if (!p.ok) return false;
-  void* bptr = p.bias_t == HIP_R_32F ? bias_f32.data_ptr() : bias.data_ptr();
-  hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &bptr, sizeof(bptr));
-  hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_EPILOGUE_AUX_POINTER, &aux, sizeof(aux));
-  const float alpha = 1.f, beta = 0.f;
-  hipStream_t stream = c10::hip::getCurrentHIPStream().stream();
-  hipblasStatus_t s = hipblasLtMatmul(st.handle, p.desc, &alpha, A, p.la, B, p.lb, &beta, D, p.ld, D, p.ld, &p.algo,
-                                      st.workspace.data_ptr(), p.ws, stream);
-  TORCH_CHECK(chk(s), "hipblasLtMatmul (epilogue kind ", kind, ") failed: status ", (int)s);
-  return true;
-}
-
-bool io_ok(const torch::Tensor& t) {
-  return t.is_cuda() && t.is_contiguous() && (t.scalar_type() == at::kBFloat16 || t.scalar_type() == at::kHalf);
-}
-
-// out = gelu(x w^T + b) and aux = x w^T + b   (x [M,K], w [N,K], b [N], out/aux [M,N])
-bool linear_gelu_fwd(torch::Tensor x, torch::Tensor w, torch::Tensor b, torch::Tensor out, torch::Tensor aux) {
-  if (!io_ok(x) || !io_ok(w) || !io_ok(b) || !io_ok(out) || !io_ok(aux)) return false;
-  if (x.dim() != 2 || w.dim() != 2 || x.scalar_type() != w.scalar_type()) return false;
-  const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
-  if (w.size(1) != K || b.numel() != N || out.numel() != M * N || aux.numel() != M * N) return false;
-  return run_eplan(0, N, M, K, x, w.data_ptr(), x.data_ptr(), out.data_ptr(), b, aux.data_ptr());
-}
-
-// out = (dy w2) * gelu'(aux), bgrad (fp32 [N]) = column sums of out   (dy [M,N2], w2 [N2,N], aux/out [M,N])
-bool linear_dgelu_bwd(torch::Tensor dy, torch::Tensor w2, torch::Tensor aux, torch::Tensor out, torch::Tensor bgrad) {
-  if (!io_ok(dy) || !io_ok(w2) || !io_ok(aux) || !io_ok(out)) return false;
-  if (!bgrad.is_cuda() || bgrad.scalar_type() != at::kFloat || !bgrad.is_contiguous()) return false;
-  if (dy.dim() != 2 || w2.dim() != 2) return false;
-  const int64_t M = dy.size(0), N2 = dy.size(1), N = w2.size(1);
-  if (w2.size(0) != N2 || aux.numel() != M * N || out.numel() != M * N || bgrad.numel() != N) return false;
-  return run_eplan(1, N, M, N2, dy, w2.data_ptr(), dy.data_ptr(), out.data_ptr(), bgrad, aux.data_ptr());
-}
-
 }  // namespace
 
 void register_blaslt(pybind11::module_& m) {
-  m.def("linear_gelu_fwd", &linear_gelu_fwd, "out = gelu(x w^T + b), aux = pre-activation (hipBLASLt epilogue)");
-  m.def("linear_dgelu_bwd", &linear_dgelu_bwd,
-        "out = (dy w2) * gelu'(aux), bgrad = column sums of out (hipBLASLt DGELU_BGRAD epilogue)");
   m.def("wgrad_accumulate", &wgrad_accumulate,
         "main_grad(fp32 [N,K]) += dy([M,N])^T @ x([M,K]) in one hipBLASLt GEMM (beta = 1); "
         "returns False if unsupported");

@@ -1,0 +1,336 @@
+// Linear-layer forward GEMM with fused epilogues on gfx950 MFMA:
+//
+//     Y[m, n] = sum_k X[m, k] W[n, k]            (EPI 0)
+//     Y[m, n] = sum_k X[m, k] W[n, k] + b[n]     (EPI 1)
+//     H = X W^T + b,  Y = GeLU_tanh(H)           (EPI 2: the MLP's fc1 + bias-GeLU, both stored)
+//
+// X [M, K] and W [N, K] are row-major with the reduction index k CONTIGUOUS in both (the "NT"
+// layout of a torch.nn.Linear forward). This replaces Megatron's separate bias-GeLU fusion pass
+// after the fc1 GEMM (--no-bias-gelu-fusion, /root/reference/3_training_megatron-lm/
+// megatron/arguments.py:819-821): the activation is applied to the fp32 accumulator before the one
+// rounding to bf16, and the pre-activation H (needed by the backward's GeLU derivative) is written
+// by the same epilogue, so the [tokens, 4h] intermediate makes one trip to HBM instead of three.
+//
+// Structure (shares mfma_tile.h with the flash-attention and weight-gradient kernels):
+//   * 256 x 256 output tile per workgroup, 8 waves as 2 (m) x 4 (n), each wave 128 m x 64 n =
+//     8 x 4 accumulators of v_mfma_f32_16x16x32 (bf16 or fp16 operands), one MFMA k-step per stage;
+//   * k is staged 32 at a time: a stage of each operand is 256 rows x 64 B, copied global -> LDS by
+//     global_load_lds_dwordx4 (1 KB = 16 rows per wave-instruction, no VGPR staging, no ds_write
+//     pass) into an XOR-swizzled image (swizzle applied to the per-lane SOURCE address),
+//     read back by rows with ds_read_b128, bank-conflict free;
+//   * a ring of four stage buffers, three stages in flight: one counted vmcnt + one barrier per
+//     stage; the grid is persistent (one workgroup per CU) and the stage stream runs on across a
+//     block's tiles, so a tile's epilogue overlaps the DMA of the next tile's first stages;
+//   * the "swapped" product D = W . X^T puts the token index m on the MFMA lane and 4 consecutive
+//     output features n in registers: the epilogue applies the per-feature bias / GeLU straight
+//     from registers and stages each 32-row slab through LDS so every store is a coalesced 16-byte
+//     piece of a 128-byte row segment;
+//   * tiles are ordered in groups of 8 m-tiles x all n-tiles and remapped so that each XCD runs a
+//     contiguous range (the W strip and 8 X strips stay in that XCD's L2).
+// Partial tiles (M or N not a multiple of 256, e.g. the 50304-row LM head) load clamped rows and
+// skip their stores. Requirements (host-checked): K % 128 == 0, N % 8 == 0, 16-byte aligned rows.
+#include "activations.h"
+#include "common.h"
+#include "launchers.h"
+#include "mfma_tile.h"
+
+namespace smdt {
+namespace lg {
+
+using namespace mt;
+constexpr int BT = 256;                  // output tile edge (m and n)
+constexpr int BK = 32;                   // k per stage
+constexpr int RB = BK * 2;               // bytes per staged row (64)
+constexpr int SB = BT * RB;              // bytes per operand stage image (16 KB)
+constexpr int kThreads = 512;
+constexpr int kWaves = kThreads / 64;
+constexpr int kRowsPerInst = 1024 / RB;            // 16 rows per 1-KB wave-instruction
+constexpr int kInst = SB / 1024 / kWaves;          // 2 wave-instructions per operand per stage
+constexpr int kNBuf = 4;                           // stage ring: 3 stages in flight
+constexpr int kPer = 2 * kInst;                    // DMA wave-instructions per stage and wave
+constexpr int kGroupM = 8;
+
+// 64-byte rows of 4 16-byte chunks; chunk c of row r sits at slot c ^ ((r >> 2) & 3). The 16 lanes
+// of a ds_read_b128 quarter-wave read rows r0 .. r0 + 15 at one chunk: (r & 3, (r >> 2) & 3) covers
+// all 16 combinations, so the 16 x 16 bytes land in 16 distinct bank groups — conflict free.
+__device__ __forceinline__ int swz(int r) { return (r >> 2) & 3; }
+__device__ __forceinline__ int lds_off(int r, int c) { return r * RB + 16 * (c ^ swz(r)); }
+
+using lds_void = __attribute__((address_space(3))) void;
+
+__device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x4 mfma16(f16x8 a, f16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+
+template <int n>
+__device__ __forceinline__ void wait_vm() {
+  static_assert(n >= 0 && n < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((n & 15) | ((n >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+
+// One operand's 256-row x 32-k stage: wave-instruction I fills image rows 16 I .. 16 I + 15; lane l
+// lands at (row 16 I + l / 4, slot l % 4) and loads the global chunk whose swizzled slot that is.
+// Offsets are relative to the tile's first row; rows past the end are clamped (never stored).
+struct Glds {
+  int rel[kInst];  // row * ld + 8 * chunk of this lane's piece, relative to the tile origin
+  __device__ __forceinline__ void init(int wave, int lane, int ld, int row0, int nrows) {
+#pragma unroll
+    for (int j = 0; j < kInst; ++j) {
+      const int r = (wave * kInst + j) * kRowsPerInst + lane / 4;
+      const int c = (lane % 4) ^ swz(r);
+      int row = row0 + r;
+      if (row > nrows - 1) row = nrows - 1;
+      rel[j] = (row - row0) * ld + 8 * c;
+    }
+  }
+  template <class E>
+  __device__ __forceinline__ void issue(const E* base, char* img, int wave) const {
+#pragma unroll
+    for (int j = 0; j < kInst; ++j)
+      __builtin_amdgcn_global_load_lds((const void*)(base + rel[j]), (lds_void*)(img + (wave * kInst + j) * 1024), 16,
+                                       0, 0);
+  }
+};
+
+// Persistent-grid tile order: round r of the grid gives XCD x (blocks b with b % 8 == x) the 32
+// consecutive tiles r * G + 32 x .., and tiles are numbered in groups of kGroupM m-tiles x all
+// n-tiles (m fastest), so an XCD's concurrent tiles share 8 X strips and a few W strips in its L2.
+__device__ __forceinline__ void tile_of(int t, int ntm, int ntn, int& tm, int& tn) {
+  const int grp = t / (kGroupM * ntn);
+  const int gm = min(kGroupM, ntm - grp * kGroupM);
+  const int tg = t - grp * kGroupM * ntn;
+  tm = grp * kGroupM + tg % gm;
+  tn = tg / gm;
+}
+
+template <int EPI, class E>
+__global__ __launch_bounds__(kThreads, 1) void linear_fwd_kernel(const E* __restrict__ X, const E* __restrict__ W,
+                                                                 const E* __restrict__ bias, E* __restrict__ Y,
+                                                                 E* __restrict__ H, int M, int N, int K, int ldx,
+                                                                 int ldw, int ldy, int ntm, int ntn) {
+  __shared__ __attribute__((aligned(1024))) char L0[2 * SB];
+  __shared__ __attribute__((aligned(1024))) char L1[2 * SB];
+  __shared__ __attribute__((aligned(1024))) char L2[2 * SB];
+  __shared__ __attribute__((aligned(1024))) char L3[2 * SB];
+  const int ntiles = ntm * ntn;
+  const int G = gridDim.x;
+  const int b = blockIdx.x;
+  // logical tile of this block's i-th round (XCD-contiguous ranges, see tile_of)
+  const int xcd = b & 7, slot = b >> 3, per_xcd = G >> 3;
+  auto logical = [&](int i) { return i * G + xcd * per_xcd + slot; };
+  int my_tiles = 0;
+  while (logical(my_tiles) < ntiles) ++my_tiles;
+
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), h = lane >> 5;
+  const int wm = wave >> 2, wn = wave & 3;  // wave tile: m [128 wm, +128), n [64 wn, +64)
+  using V = v8_t<E>;
+  // v_mfma_f32_16x16x32: lane l holds rows (l & 15) of a 16-row operand block at k = 8 (l >> 4) .. +8,
+  // i.e. 16-byte chunk (l >> 4) of the 64-byte staged row; the 4 result registers are rows
+  // 4 (l >> 4) .. +4 (features), column l & 15 (token). 16x16x32 rather than 32x32x16: the chip
+  // holds a higher clock on it (MI355X_MICROARCH.md, DVFS give-back item 7), same cycles per FLOP.
+  const int l15 = lane & 15, lq = lane >> 4;
+  const int rdo = lds_off(l15, lq);
+
+  const int nst = K / BK;  // a multiple of kNBuf: every tile starts at ring position 0
+  // DMA cursor over this block's stage stream: tile di, stage ds (past the end: the last stage
+  // again, re-read into a buffer nobody reads any more, so every step issues exactly one stage)
+  Glds gx, gw;
+  int di = 0, ds = 0;
+  const E* Xb = X;
+  const E* Wb = W;
+  auto set_tile = [&](int i) {
+    int tm, tn;
+    tile_of(logical(i), ntm, ntn, tm, tn);
+    gx.init(wave, lane, ldx, tm * BT, M);
+    gw.init(wave, lane, ldw, tn * BT, N);
+    Xb = X + (int64_t)tm * BT * ldx;
+    Wb = W + (int64_t)tn * BT * ldw;
+  };
+  auto issue_next = [&](char* img) {
+    gx.issue(Xb + ds * BK, img, wave);
+    gw.issue(Wb + ds * BK, img + SB, wave);
+    if (++ds == nst) {
+      if (di + 1 < my_tiles) {
+        ++di;
+        ds = 0;
+        set_tile(di);
+      } else {
+        ds = nst - 1;
+      }
+    }
+  };
+
+  f32x4 acc[4][8];  // [16-feature block ni][16-token block mi] of the wave's 64 x 128 tile
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // Epilogue of tile i, staged through this wave's 4 KB of L3 (free here: the tile's last step read
+  // it, the next tile's first step refills it after the closing barrier). Per 32-token slab the
+  // wave writes its 32 x 64 block row-major (16-byte chunk c of row m at slot c ^ (m & 7)), reads
+  // it back 16 B per lane and stores whole 128-byte row segments: 4 coalesced dwordx4 stores per
+  // slab instead of 8 dwordx2 stores that touch 64 rows each (the store-issue-bound tail,
+  // MI355X_MICROARCH.md "attention epilogue store tail").
+  char* const wreg = L3 + wave * 4096;
+  auto slab_out = [&](E* __restrict__ out, int mb, int nb) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int row = 8 * q + lane / 8, c = lane & 7;
+      const v8_t<E> v = *reinterpret_cast<const v8_t<E>*>(wreg + row * 128 + 16 * (c ^ (row & 7)));
+      const int m = mb + row, n = nb + 8 * c;
+      if (m < M && n < N) *reinterpret_cast<v8_t<E>*>(out + (int64_t)m * ldy + n) = v;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  };
+  auto epilogue = [&](int i) {
+    int tm, tn;
+    tile_of(logical(i), ntm, ntn, tm, tn);
+    const int m0 = tm * BT, n0 = tn * BT;
+    // register r of acc[ni][mi] = D[n = 64 wn + 16 ni + 4 lq + r][m = 128 wm + 16 mi + l15]
+    float bv[4][4];
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+      const int n = n0 + 64 * wn + 16 * ni + 4 * lq;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) bv[ni][e] = 0.f;
+      if constexpr (EPI >= 1) {
+        if (n < N) {
+          const v4_t<E> b4 = *reinterpret_cast<const v4_t<E>*>(bias + n);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) bv[ni][e] = (float)b4[e];
+        }
+      }
+    }
+#pragma unroll
+    for (int sl = 0; sl < 4; ++sl) {  // 32-token slabs: token blocks mi = 2 sl, 2 sl + 1
+      const int mb = m0 + 128 * wm + 32 * sl, nb = n0 + 64 * wn;
+#pragma unroll
+      for (int pass = 0; pass < (EPI == 2 ? 2 : 1); ++pass) {  // EPI 2: pre-activation, then GeLU
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+          const int row = 16 * half + l15;
+#pragma unroll
+          for (int ni = 0; ni < 4; ++ni) {
+            v4_t<E> v;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float x = acc[ni][2 * sl + half][e] + bv[ni][e];
+              v[e] = (E)(EPI == 2 && pass == 1 ? gelu_tanh(x) : x);
+            }
+            const int c = 2 * ni + (lq >> 1);  // 16-byte chunk of the 128-byte LDS row
+            *reinterpret_cast<v4_t<E>*>(wreg + row * 128 + 16 * (c ^ (row & 7)) + 8 * (lq & 1)) = v;
+          }
+        }
+        slab_out(EPI == 2 && pass == 0 ? H : Y, mb, nb);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int ii = 0; ii < 8; ++ii) acc[j][ii] = f32x4{0.f, 0.f, 0.f, 0.f};
+    __builtin_amdgcn_s_barrier();  // every wave is done with L3 before the next step's DMA into it
+  };
+  // global stores one epilogue leaves in flight per wave (they count in vmcnt)
+  constexpr int kEpiStores = 16 * (EPI == 2 ? 2 : 1);
+
+  if (my_tiles == 0) return;
+  set_tile(0);
+  // Prologue: stages 0 .. 2 in flight, wait for stage 0.
+  issue_next(L0);
+  issue_next(L1);
+  issue_next(L2);
+  wait_vm<2 * kPer>();
+  __builtin_amdgcn_s_barrier();
+
+  // One step: prefetch the stage 3 ahead into `pre` (the buffer the previous step read, released
+  // by the barrier that ended it), MFMA over `cur`, retire the next stage's DMA, barrier.
+  // kRelaxed: the first step after an epilogue, whose stores sit between the DMA it waits for and
+  // the newest one.
+  auto step = [&](const char* cur, char* pre, auto relaxed) {
+    issue_next(pre);
+    __builtin_amdgcn_sched_barrier(0);  // keep the DMA at the head of the step (the scheduler sinks it)
+    const char* xt = cur;
+    const char* wt = cur + SB;
+    // 4 feature fragments + 8 token fragments (12 ds_read_b128) feed 32 MFMAs
+    V wf[4];
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) wf[ni] = *reinterpret_cast<const V*>(wt + (64 * wn + 16 * ni) * RB + rdo);
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi) {
+      const V xf = *reinterpret_cast<const V*>(xt + (128 * wm + 16 * mi) * RB + rdo);
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) acc[ni][mi] = mfma16(wf[ni], xf, acc[ni][mi]);  // D[n][m]
+    }
+    if constexpr (decltype(relaxed)::value)
+      wait_vm<(kNBuf - 2) * kPer + kEpiStores>();
+    else
+      wait_vm<(kNBuf - 2) * kPer>();  // the next stage landed (two more may still be in flight)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  };
+  using Strict = std::integral_constant<bool, false>;
+  using Relaxed = std::integral_constant<bool, true>;
+  for (int i = 0; i < my_tiles; ++i) {
+    if (i == 0) step(L0, L3, Strict{});
+    else step(L0, L3, Relaxed{});
+    step(L1, L0, Strict{});
+    step(L2, L1, Strict{});
+    step(L3, L2, Strict{});
+    for (int st = kNBuf; st < nst; st += kNBuf) {
+      step(L0, L3, Strict{});
+      step(L1, L0, Strict{});
+      step(L2, L1, Strict{});
+      step(L3, L2, Strict{});
+    }
+    // the next tile's first three stages are in flight while this tile's results are stored
+    epilogue(i);
+  }
+  wait_vm<0>();  // drain the trailing re-reads (and the last stores) before the LDS is released
+}
+
+}  // namespace lg
+}  // namespace smdt
+
+using namespace smdt;
+
+extern "C" int smdt_linear_fwd_supported(int64_t M, int64_t N, int64_t K) {
+  return M > 0 && N >= 8 && K >= lg::BK * lg::kNBuf && K % (lg::BK * lg::kNBuf) == 0 && N % 8 == 0 && M < (1ll << 31) &&
+         (int64_t)lg::BT * (K > N ? K : N) < (1ll << 31) && M * K < (1ll << 31) && N * K < (1ll << 31) &&
+         M * N < (1ll << 31);
+}
+
+// epi: 0 = plain, 1 = + bias, 2 = + bias -> GeLU(tanh) into y with the pre-activation into h.
+extern "C" hipError_t smdt_linear_fwd(int dtype, int epi, const void* x, const void* w, const void* bias, void* y,
+                                      void* h, int64_t M, int64_t N, int64_t K, int64_t ldx, int64_t ldw,
+                                      int64_t ldy, hipStream_t st) {
+  if (dtype != 1 && dtype != 2) return hipErrorInvalidValue;
+  if (epi < 0 || epi > 2 || !smdt_linear_fwd_supported(M, N, K)) return hipErrorInvalidValue;
+  if ((epi >= 1 && !bias) || (epi == 2 && !h)) return hipErrorInvalidValue;
+  if (ldx % 8 || ldw % 8 || ldy % 8 || ldx < K || ldw < K || ldy < N) return hipErrorInvalidValue;
+  const int ntm = (int)((M + lg::BT - 1) / lg::BT), ntn = (int)((N + lg::BT - 1) / lg::BT);
+  // persistent grid: one workgroup per CU (a multiple of 8 so every XCD gets the same share)
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      cus = 256;
+  }
+  int nb = ntm * ntn < cus ? ntm * ntn : cus;
+  nb = (nb + 7) / 8 * 8;
+  const dim3 grid((unsigned)nb);
+#define SMDT_LG(EP, ET)                                                                                           \
+  hipLaunchKernelGGL((lg::linear_fwd_kernel<EP, ET>), grid, dim3(lg::kThreads), 0, st, (const ET*)x, (const ET*)w, \
+                     (const ET*)bias, (ET*)y, (ET*)h, (int)M, (int)N, (int)K, (int)ldx, (int)ldw, (int)ldy, ntm, ntn)
+  if (dtype == 2) {
+    if (epi == 0) SMDT_LG(0, f16); else if (epi == 1) SMDT_LG(1, f16); else SMDT_LG(2, f16);
+  } else {
+    if (epi == 0) SMDT_LG(0, bf16); else if (epi == 1) SMDT_LG(1, bf16); else SMDT_LG(2, bf16);
+  }
+#undef SMDT_LG
+  return hipGetLastError();
+}

@@ -238,52 +238,43 @@ def _apply_rope_parts(flat, cos, sin, rot, nh, nkv, hd, b, s, inverse):
         k.copy_(SF._rope_ref(k, cos.to(flat.device), sin.to(flat.device), rot, pos, inverse))
 
 
-class _FusedGeluMLP(torch.autograd.Function):
-    """fc1 -> bias + GeLU(tanh) -> fc2 with the activation folded into hipBLASLt epilogues (TP = 1):
-    forward  GELU_AUX_BIAS writes gelu(x W1^T + b1) and the pre-activation in the fc1 GEMM;
-    backward DGELU_BGRAD turns the fc2 dgrad GEMM into d(pre-activation) and emits the fc1 bias
-    gradient, so the two bias-GeLU elementwise passes (K5) and their HBM round trips disappear.
-    Weight gradients go through the fused fp32 main_grad accumulation like every linear."""
+class _Fc1BiasGelu(torch.autograd.Function):
+    """fc1 GEMM + bias + GeLU(tanh) in ONE hand-written MFMA kernel (csrc/kernels/linear_gemm.hip,
+    epilogue 2): the activation is applied to the fp32 accumulator and the pre-activation (which the
+    backward's GeLU derivative needs) is written by the same epilogue, so the separate bias-GeLU
+    pass (K5) and its [tokens, 4h] round trip disappear from the forward.
+    Backward: d(pre) = d(act) * gelu'(pre) with the fp32 bias gradient (bias_act kernel, bias
+    already inside pre) -> dx = d(pre) W1 (hipBLASLt), dW1 = d(pre)^T x into main_grad (deferred
+    grouped MFMA wgrad). TP = 1 without sequence parallelism (the column-parallel collectives of
+    ColumnParallelLinear are not needed there)."""
 
     @staticmethod
-    def forward(ctx, x, w1, b1, w2):
+    def forward(ctx, x, w1, b1):
         C = _ext_mod().ext()
         shp = x.shape
         x2 = x.reshape(-1, shp[-1])
-        if not x2.is_contiguous():
+        if x2.stride(-1) != 1 or x2.stride(0) % 8:
             x2 = x2.contiguous()
-        M, f = x2.shape[0], w1.shape[0]
-        act = x2.new_empty(M, f)
-        aux = x2.new_empty(M, f)
-        if not C.linear_gelu_fwd(x2, w1, b1, act, aux):
-            raise RuntimeError("linear_gelu_fwd: no hipBLASLt solution")
-        y = torch.nn.functional.linear(act, w2)
-        ctx.save_for_backward(x2, w1, w2, act, aux)
-        ctx.b1 = b1
-        ctx.shp = shp
-        return y.view(*shp[:-1], w2.shape[0])
+        act, pre = C.linear_fwd(x2, w1, b1, 2)
+        ctx.save_for_backward(x2, pre)
+        ctx.w1, ctx.b1, ctx.shp = w1, b1, shp
+        return act.view(*shp[:-1], w1.shape[0])
 
     @staticmethod
-    def backward(ctx, dy):
-        x2, w1, w2, act, aux = ctx.saved_tensors
+    def backward(ctx, dact):
+        x2, pre = ctx.saved_tensors
+        w1, b1 = ctx.w1, ctx.b1
         C = _ext_mod().ext()
-        dy2 = dy.reshape(-1, dy.shape[-1]).contiguous()
-        dw2 = tp._wgrad(w2, dy2, act)
-        d_pre = torch.empty_like(aux)
-        bg = torch.empty(aux.shape[1], dtype=torch.float32, device=aux.device)
-        if not C.linear_dgelu_bwd(dy2, w2, aux, d_pre, bg):
-            raise RuntimeError("linear_dgelu_bwd: no hipBLASLt solution")
-        b1 = ctx.b1
         tgt = SF.grad_accumulate_target(b1)
+        dpre, db = C.bias_act_bwd(dact.reshape(pre.shape).contiguous(), pre, None, 0, True, tgt)
         if tgt is not None:
-            tgt.add_(bg)
             b1._smdt_grad_ready(b1)
             db1 = None
         else:
-            db1 = bg.to(b1.dtype)
-        dx = d_pre.matmul(w1)
-        dw1 = tp._wgrad(w1, d_pre, x2)
-        return dx.view(ctx.shp), dw1, db1, dw2
+            db1 = db.to(b1.dtype)
+        dx = dpre.matmul(w1)
+        dw1 = tp._wgrad(w1, dpre, x2)
+        return dx.view(ctx.shp), dw1, db1
 
 
 def _ext_mod():
@@ -291,7 +282,11 @@ def _ext_mod():
     return _ext
 
 
-_FUSED_MLP_STATE = {"ok": os.environ.get("SMDT_FUSED_MLP_EPILOGUE", "1") == "1"}
+# SMDT_FUSED_FC1=1 runs fc1 + bias + GeLU as the fused MFMA GEMM. Off by default: measured on
+# MI355X at the bench shape (profiles/r2_linear_gemm/) the fused kernel takes 316 us per layer in
+# the training step against 211 us (TunableOp-tuned hipBLASLt fc1) + 89 us (bias-GeLU kernel), its
+# main loop running at ~1.1 PF/s vs hipBLASLt's ~1.3 PF/s; it wins only in isolation (326 vs 337 us).
+_FUSED_FC1 = {"ok": os.environ.get("SMDT_FUSED_FC1", "0") == "1"}
 
 
 class ParallelMLP(nn.Module):
@@ -315,22 +310,17 @@ class ParallelMLP(nn.Module):
                                         sequence_parallel=cfg.sequence_parallel, skip_bias_add=True)
 
     def _fused_ok(self, x):
-        return (_FUSED_MLP_STATE["ok"] and self.cfg.activation == "gelu" and self.cfg.bias_gelu_fusion
-                and self.fc1.bias is not None and self.fc1.tp == 1 and not self.fc1.sequence_parallel
+        fc1 = self.fc1
+        return (_FUSED_FC1["ok"] and self.cfg.activation == "gelu" and self.cfg.bias_gelu_fusion
+                and fc1.bias is not None and fc1.tp == 1 and not fc1.sequence_parallel
                 and x.is_cuda and x.dtype in (torch.bfloat16, torch.float16) and _ext_mod().use_kernels(x)
-                and self.fc1.weight.dtype == x.dtype)
+                and fc1.weight.dtype == x.dtype and fc1.bias.dtype == x.dtype
+                and _ext_mod().ext().linear_fwd_supported(x.numel() // x.shape[-1], fc1.weight.shape[0],
+                                                          fc1.weight.shape[1]))
 
     def forward(self, x):
         if self._fused_ok(x):
-            try:
-                y = _FusedGeluMLP.apply(x, self.fc1.weight, self.fc1.bias, self.fc2.weight)
-                return y, self.fc2.bias
-            except RuntimeError as e:  # no epilogue solution in this hipBLASLt build: use K5 kernels
-                if "no hipBLASLt solution" not in str(e):
-                    raise
-                _FUSED_MLP_STATE["ok"] = False
-                import sys
-                print(f"[smdt] fused GeLU MLP disabled ({e}); using the bias-GeLU kernels", file=sys.stderr)
+            return self.fc2(_Fc1BiasGelu.apply(x, self.fc1.weight, self.fc1.bias))
         h, b = self.fc1(x)
         act = self.cfg.activation
         if act in ("gelu", "gelu_erf"):

@@ -389,3 +389,39 @@ def test_wgrad_mfma_fp16_and_bf16(dt):
     assert C.wgrad_grouped([mg2, mg3], [dy, x], [x, dy])
     torch.testing.assert_close(mg2, ref, atol=0.05, rtol=1e-3)
     torch.testing.assert_close(mg3, ref.t(), atol=0.05, rtol=1e-3)
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("shape", [(4096, 4096, 1024), (1000, 520, 256), (2048, 50304 // 8, 128), (256, 8, 128), (300, 264, 512)])
+@pytest.mark.parametrize("epi", [0, 1, 2])
+def test_linear_fwd_mfma_matches_fp32_reference(shape, epi, dt):
+    """Hand-written NT GEMM (linear_gemm.hip) incl. partial tiles and the fused bias / bias + GeLU
+    epilogues vs an fp32 torch reference (the pre-activation h is returned too)."""
+    C = _ext.ext()
+    torch.manual_seed(11)
+    M, N, K = shape
+    x = torch.randn(M, K, device=DEV, dtype=dt)
+    w = torch.randn(N, K, device=DEV, dtype=dt) * K ** -0.5
+    b = torch.randn(N, device=DEV, dtype=dt)
+    out = C.linear_fwd(x, w, b if epi else None, epi)
+    ref = x.float() @ w.float().t()
+    if epi:
+        ref = ref + b.float()
+    tol = dict(atol=2e-2, rtol=2e-2)
+    if epi == 2:
+        y, h = out
+        torch.testing.assert_close(h.float(), ref, **tol)
+        torch.testing.assert_close(y.float(), F.gelu(ref, approximate="tanh"), **tol)
+    else:
+        torch.testing.assert_close(out[0].float(), ref, **tol)
+
+
+def test_linear_fwd_strided_input_and_rejects_bad_shapes():
+    C = _ext.ext()
+    x = torch.randn(512, 2048, device=DEV, dtype=torch.bfloat16)[:, :1024]   # row stride 2048
+    w = torch.randn(768, 1024, device=DEV, dtype=torch.bfloat16) * 0.03
+    (y,) = C.linear_fwd(x, w, None, 0)
+    torch.testing.assert_close(y.float(), x.float() @ w.float().t(), atol=2e-2, rtol=2e-2)
+    with pytest.raises(RuntimeError):
+        C.linear_fwd(torch.randn(64, 100, device=DEV, dtype=torch.bfloat16),
+                     torch.randn(64, 100, device=DEV, dtype=torch.bfloat16), None, 0)   # K % 64 != 0

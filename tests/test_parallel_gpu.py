@@ -125,8 +125,9 @@ def test_wgrad_grouped_matches_fp32_reference():
         torch.testing.assert_close(mg, ref, atol=2e-2 * (M ** 0.5), rtol=1e-3)
 
 
-def test_fused_gelu_mlp_epilogues_match_unfused():
-    """hipBLASLt GELU_AUX_BIAS / DGELU_BGRAD MLP == the K5 bias-GeLU kernel path."""
+def test_fused_fc1_bias_gelu_mlp_matches_unfused():
+    """fc1 + bias + GeLU in the hand-written MFMA GEMM epilogue (models/transformer._Fc1BiasGelu)
+    == hipBLASLt + the K5 bias-GeLU kernel path: outputs, input grads and weight / bias grads."""
     from smdt_amd.models import transformer as T
     from smdt_amd.parallel import state as ps
     ps.destroy_model_parallel()
@@ -139,9 +140,12 @@ def test_fused_gelu_mlp_epilogues_match_unfused():
         mlp.fc1.bias.normal_(0, 0.5)
     x = torch.randn(128, 4, 256, device="cuda", dtype=torch.bfloat16, requires_grad=True)
     dy = torch.randn(128, 4, 256, device="cuda", dtype=torch.bfloat16)
+    prev = T._FUSED_FC1["ok"]
+    T._FUSED_FC1["ok"] = True
+    assert mlp._fused_ok(x)
     outs = []
     for fused in (True, False):
-        T._FUSED_MLP_STATE["ok"] = fused
+        T._FUSED_FC1["ok"] = fused
         for p in mlp.parameters():
             p.grad = None
         x.grad = None
@@ -149,8 +153,9 @@ def test_fused_gelu_mlp_epilogues_match_unfused():
         y.backward(dy)
         outs.append((y.float(), x.grad.float(), {n: p.grad.float() for n, p in mlp.named_parameters()
                                                   if p.grad is not None}))
-    T._FUSED_MLP_STATE["ok"] = True
+    T._FUSED_FC1["ok"] = prev
     (y1, dx1, g1), (y2, dx2, g2) = outs
+    assert set(g1) == set(g2) and "fc1.bias" in g1 and "fc1.weight" in g1
     torch.testing.assert_close(y1, y2, atol=3e-2, rtol=3e-2)
     torch.testing.assert_close(dx1, dx2, atol=5e-2, rtol=5e-2)
     for n in g2:
