@@ -46,13 +46,15 @@ def main():
         x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
         w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) * 0.02
         b = torch.randn(N, device="cuda", dtype=torch.bfloat16) * 0.1
-        t_ours = timeit(lambda: C.linear_fwd(x, w, b, 1))
+        t_ours = timeit(lambda: C.linear_fwd(x, w, b, 1, 8))
+        t_ours4 = timeit(lambda: C.linear_fwd(x, w, b, 1, 4))
         t_lib = timeit(lambda: F.linear(x, w, b))
         fl = 2.0 * M * N * K
-        rec = {"gemm": name, "M": M, "N": N, "K": K, "ours_ms": t_ours, "hipblaslt_ms": t_lib,
-               "ours_tflops": fl / t_ours / 1e9, "hipblaslt_tflops": fl / t_lib / 1e9}
+        rec = {"gemm": name, "M": M, "N": N, "K": K, "ours_ms": t_ours, "ours4_ms": t_ours4, "hipblaslt_ms": t_lib,
+               "ours_tflops": fl / t_ours / 1e9, "ours4_tflops": fl / t_ours4 / 1e9, "hipblaslt_tflops": fl / t_lib / 1e9}
         if name == "fc1":
-            t_fused = timeit(lambda: C.linear_fwd(x, w, b, 2))
+            t_fused = timeit(lambda: C.linear_fwd(x, w, b, 2, 8))
+            rec["fused4_bias_gelu_ms"] = timeit(lambda: C.linear_fwd(x, w, b, 2, 4))
             t_unf = timeit(lambda: SF.bias_gelu(F.linear(x, w), b, "tanh"))
             rec.update({"fused_bias_gelu_ms": t_fused, "hipblaslt_plus_bias_gelu_ms": t_unf})
         print(json.dumps(rec), flush=True)

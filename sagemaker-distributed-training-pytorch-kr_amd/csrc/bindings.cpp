@@ -523,7 +523,7 @@ void xgmi_allreduce(Tensor in, Tensor out, std::vector<int64_t> data_ptrs, std::
 // Forward linear GEMM with fused epilogue (linear_gemm.hip): x [M, K] (unit inner stride), w [N, K]
 // contiguous, bias [N] or None. epi 0: y = x w^T; 1: + bias; 2: h = x w^T + bias, y = gelu(h).
 // Returns [y] or [y, h].
-std::vector<Tensor> linear_fwd(Tensor x, Tensor w, c10::optional<Tensor> bias, int64_t epi) {
+std::vector<Tensor> linear_fwd(Tensor x, Tensor w, c10::optional<Tensor> bias, int64_t epi, int64_t waves) {
   need_cuda(x, "x");
   need_cuda(w, "w");
   TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && x.stride(1) == 1 && w.is_contiguous() && x.size(1) == w.size(1),
@@ -544,7 +544,7 @@ std::vector<Tensor> linear_fwd(Tensor x, Tensor w, c10::optional<Tensor> bias, i
   Tensor y = at::empty({M, N}, x.options());
   Tensor h = epi == 2 ? at::empty({M, N}, x.options()) : Tensor();
   check(smdt_linear_fwd(dcode(x), (int)epi, x.data_ptr(), w.data_ptr(), bp, y.data_ptr(),
-                        epi == 2 ? h.data_ptr() : nullptr, M, N, K, x.stride(0), K, N, cur_stream()),
+                        epi == 2 ? h.data_ptr() : nullptr, M, N, K, x.stride(0), K, N, (int)waves, cur_stream()),
         "linear_fwd");
   if (epi == 2) return {y, h};
   return {y};
@@ -640,7 +640,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("xgmi_allreduce", &xgmi_allreduce, py::arg("input"), py::arg("out"), py::arg("data_ptrs"), py::arg("sig_ptrs"),
         py::arg("rank"), py::arg("nranks_local"), py::arg("region_bytes"), py::arg("two_shot"), py::arg("blocks"),
         py::arg("scale") = 1.0);
-  m.def("linear_fwd", &linear_fwd, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("epi"));
+  m.def("linear_fwd", &linear_fwd, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("epi"),
+        py::arg("waves") = 0);
   m.def("linear_fwd_supported", &smdt_linear_fwd_supported);
   m.def("xgmi_collective", &xgmi_collective, py::arg("mode"), py::arg("input"), py::arg("out"), py::arg("data_ptrs"),
         py::arg("sig_ptrs"), py::arg("rank"), py::arg("nranks_local"), py::arg("region_bytes"), py::arg("blocks"),

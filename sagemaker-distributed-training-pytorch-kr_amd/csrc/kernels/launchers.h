@@ -109,7 +109,8 @@ hipError_t smdt_wgrad_grouped_t(int dtype, const SmdtWgradProblem* probs, int n,
 // epi 0 plain / 1 bias / 2 bias + GeLU. K % 128 == 0, N % 8 == 0, leading dims multiples of 8.
 int smdt_linear_fwd_supported(int64_t M, int64_t N, int64_t K);
 hipError_t smdt_linear_fwd(int dtype, int epi, const void* x, const void* w, const void* bias, void* y, void* h,
-                           int64_t M, int64_t N, int64_t K, int64_t ldx, int64_t ldw, int64_t ldy, hipStream_t st);
+                           int64_t M, int64_t N, int64_t K, int64_t ldx, int64_t ldw, int64_t ldy, int waves,
+                           hipStream_t st);
 
 // xgmi_allreduce.hip: single-node all-reduce over HIP-IPC-mapped peer buffers.
 int smdt_ar_max_ranks();

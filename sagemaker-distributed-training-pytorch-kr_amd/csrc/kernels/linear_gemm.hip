@@ -29,6 +29,8 @@
 //     contiguous range (the W strip and 8 X strips stay in that XCD's L2).
 // Partial tiles (M or N not a multiple of 256, e.g. the 50304-row LM head) load clamped rows and
 // skip their stores. Requirements (host-checked): K % 128 == 0, N % 8 == 0, 16-byte aligned rows.
+#include <stdlib.h>
+
 #include "activations.h"
 #include "common.h"
 #include "launchers.h"
@@ -42,13 +44,26 @@ constexpr int BT = 256;                  // output tile edge (m and n)
 constexpr int BK = 32;                   // k per stage
 constexpr int RB = BK * 2;               // bytes per staged row (64)
 constexpr int SB = BT * RB;              // bytes per operand stage image (16 KB)
-constexpr int kThreads = 512;
-constexpr int kWaves = kThreads / 64;
 constexpr int kRowsPerInst = 1024 / RB;            // 16 rows per 1-KB wave-instruction
-constexpr int kInst = SB / 1024 / kWaves;          // 2 wave-instructions per operand per stage
 constexpr int kNBuf = 4;                           // stage ring: 3 stages in flight
-constexpr int kPer = 2 * kInst;                    // DMA wave-instructions per stage and wave
 constexpr int kGroupM = 8;
+
+// Wave layouts of the 256 x 256 tile: NW = 8 waves as 2 (m) x 4 (n), 128 x 64 each (12 fragment
+// reads per 32 MFMAs), or NW = 4 waves as 2 x 2, 128 x 128 each (16 reads per 64 MFMAs, half the
+// LDS traffic and barrier participants; the 256 accumulator registers live in AGPRs).
+template <int NW>
+struct Cfg {
+  static constexpr int kThreads = 64 * NW;
+  static constexpr int WN = NW == 8 ? 64 : 128;          // features per wave
+  static constexpr int NI = WN / 16;                      // 16-feature blocks per wave
+  static constexpr int kInst = SB / 1024 / NW;            // DMA wave-instructions per operand per stage
+  static constexpr int kPer = 2 * kInst;
+  static constexpr int ERB = WN * 2;                      // bytes per epilogue LDS row
+  static constexpr int ECH = ERB / 16;                    // 16-byte chunks per epilogue row
+  static constexpr int ERI = 64 / ECH;                    // epilogue rows per wave-instruction
+  __device__ static __forceinline__ int wm(int wave) { return NW == 8 ? wave >> 2 : wave >> 1; }
+  __device__ static __forceinline__ int wn(int wave) { return NW == 8 ? wave & 3 : wave & 1; }
+};
 
 // 64-byte rows of 4 16-byte chunks; chunk c of row r sits at slot c ^ ((r >> 2) & 3). The 16 lanes
 // of a ds_read_b128 quarter-wave read rows r0 .. r0 + 15 at one chunk: (r & 3, (r >> 2) & 3) covers
@@ -74,6 +89,7 @@ __device__ __forceinline__ void wait_vm() {
 // One operand's 256-row x 32-k stage: wave-instruction I fills image rows 16 I .. 16 I + 15; lane l
 // lands at (row 16 I + l / 4, slot l % 4) and loads the global chunk whose swizzled slot that is.
 // Offsets are relative to the tile's first row; rows past the end are clamped (never stored).
+template <int kInst>
 struct Glds {
   int rel[kInst];  // row * ld + 8 * chunk of this lane's piece, relative to the tile origin
   __device__ __forceinline__ void init(int wave, int lane, int ld, int row0, int nrows) {
@@ -106,8 +122,8 @@ __device__ __forceinline__ void tile_of(int t, int ntm, int ntn, int& tm, int& t
   tn = tg / gm;
 }
 
-template <int EPI, class E>
-__global__ __launch_bounds__(kThreads, 1) void linear_fwd_kernel(const E* __restrict__ X, const E* __restrict__ W,
+template <int EPI, class E, int NW>
+__global__ __launch_bounds__(64 * NW, 1) void linear_fwd_kernel(const E* __restrict__ X, const E* __restrict__ W,
                                                                  const E* __restrict__ bias, E* __restrict__ Y,
                                                                  E* __restrict__ H, int M, int N, int K, int ldx,
                                                                  int ldw, int ldy, int ntm, int ntn) {
@@ -124,8 +140,10 @@ __global__ __launch_bounds__(kThreads, 1) void linear_fwd_kernel(const E* __rest
   int my_tiles = 0;
   while (logical(my_tiles) < ntiles) ++my_tiles;
 
-  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), h = lane >> 5;
-  const int wm = wave >> 2, wn = wave & 3;  // wave tile: m [128 wm, +128), n [64 wn, +64)
+  using C = Cfg<NW>;
+  constexpr int NI = C::NI, WN = C::WN, kPer = C::kPer;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = C::wm(wave), wn = C::wn(wave);  // wave tile: m [128 wm, +128), n [WN wn, +WN)
   using V = v8_t<E>;
   // v_mfma_f32_16x16x32: lane l holds rows (l & 15) of a 16-row operand block at k = 8 (l >> 4) .. +8,
   // i.e. 16-byte chunk (l >> 4) of the 64-byte staged row; the 4 result registers are rows
@@ -137,7 +155,7 @@ __global__ __launch_bounds__(kThreads, 1) void linear_fwd_kernel(const E* __rest
   const int nst = K / BK;  // a multiple of kNBuf: every tile starts at ring position 0
   // DMA cursor over this block's stage stream: tile di, stage ds (past the end: the last stage
   // again, re-read into a buffer nobody reads any more, so every step issues exactly one stage)
-  Glds gx, gw;
+  Glds<C::kInst> gx, gw;
   int di = 0, ds = 0;
   const E* Xb = X;
   const E* Wb = W;
@@ -163,9 +181,9 @@ __global__ __launch_bounds__(kThreads, 1) void linear_fwd_kernel(const E* __rest
     }
   };
 
-  f32x4 acc[4][8];  // [16-feature block ni][16-token block mi] of the wave's 64 x 128 tile
+  f32x4 acc[NI][8];  // [16-feature block ni][16-token block mi] of the wave's WN x 128 tile
 #pragma unroll
-  for (int j = 0; j < 4; ++j)
+  for (int j = 0; j < NI; ++j)
 #pragma unroll
     for (int i = 0; i < 8; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
@@ -175,13 +193,13 @@ __global__ __launch_bounds__(kThreads, 1) void linear_fwd_kernel(const E* __rest
   // it back 16 B per lane and stores whole 128-byte row segments: 4 coalesced dwordx4 stores per
   // slab instead of 8 dwordx2 stores that touch 64 rows each (the store-issue-bound tail,
   // MI355X_MICROARCH.md "attention epilogue store tail").
-  char* const wreg = L3 + wave * 4096;
+  char* const wreg = L3 + wave * (32 * C::ERB);
   auto slab_out = [&](E* __restrict__ out, int mb, int nb) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int row = 8 * q + lane / 8, c = lane & 7;
-      const v8_t<E> v = *reinterpret_cast<const v8_t<E>*>(wreg + row * 128 + 16 * (c ^ (row & 7)));
+    for (int q = 0; q < 32 / C::ERI; ++q) {
+      const int row = C::ERI * q + lane / C::ECH, c = lane % C::ECH;
+      const v8_t<E> v = *reinterpret_cast<const v8_t<E>*>(wreg + row * C::ERB + 16 * (c ^ (row % C::ECH)));
       const int m = mb + row, n = nb + 8 * c;
       if (m < M && n < N) *reinterpret_cast<v8_t<E>*>(out + (int64_t)m * ldy + n) = v;
     }
@@ -192,10 +210,10 @@ __global__ __launch_bounds__(kThreads, 1) void linear_fwd_kernel(const E* __rest
     tile_of(logical(i), ntm, ntn, tm, tn);
     const int m0 = tm * BT, n0 = tn * BT;
     // register r of acc[ni][mi] = D[n = 64 wn + 16 ni + 4 lq + r][m = 128 wm + 16 mi + l15]
-    float bv[4][4];
+    float bv[NI][4];
 #pragma unroll
-    for (int ni = 0; ni < 4; ++ni) {
-      const int n = n0 + 64 * wn + 16 * ni + 4 * lq;
+    for (int ni = 0; ni < NI; ++ni) {
+      const int n = n0 + WN * wn + 16 * ni + 4 * lq;
 #pragma unroll
       for (int e = 0; e < 4; ++e) bv[ni][e] = 0.f;
       if constexpr (EPI >= 1) {
@@ -208,35 +226,36 @@ __global__ __launch_bounds__(kThreads, 1) void linear_fwd_kernel(const E* __rest
     }
 #pragma unroll
     for (int sl = 0; sl < 4; ++sl) {  // 32-token slabs: token blocks mi = 2 sl, 2 sl + 1
-      const int mb = m0 + 128 * wm + 32 * sl, nb = n0 + 64 * wn;
+      const int mb = m0 + 128 * wm + 32 * sl, nb = n0 + WN * wn;
 #pragma unroll
       for (int pass = 0; pass < (EPI == 2 ? 2 : 1); ++pass) {  // EPI 2: pre-activation, then GeLU
 #pragma unroll
         for (int half = 0; half < 2; ++half) {
           const int row = 16 * half + l15;
 #pragma unroll
-          for (int ni = 0; ni < 4; ++ni) {
+          for (int ni = 0; ni < NI; ++ni) {
             v4_t<E> v;
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
               const float x = acc[ni][2 * sl + half][e] + bv[ni][e];
               v[e] = (E)(EPI == 2 && pass == 1 ? gelu_tanh(x) : x);
             }
-            const int c = 2 * ni + (lq >> 1);  // 16-byte chunk of the 128-byte LDS row
-            *reinterpret_cast<v4_t<E>*>(wreg + row * 128 + 16 * (c ^ (row & 7)) + 8 * (lq & 1)) = v;
+            const int c = 2 * ni + (lq >> 1);  // 16-byte chunk of the LDS row
+            *reinterpret_cast<v4_t<E>*>(wreg + row * C::ERB + 16 * (c ^ (row % C::ECH)) + 8 * (lq & 1)) = v;
           }
         }
         slab_out(EPI == 2 && pass == 0 ? H : Y, mb, nb);
       }
     }
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+    for (int j = 0; j < NI; ++j)
 #pragma unroll
       for (int ii = 0; ii < 8; ++ii) acc[j][ii] = f32x4{0.f, 0.f, 0.f, 0.f};
     __builtin_amdgcn_s_barrier();  // every wave is done with L3 before the next step's DMA into it
   };
   // global stores one epilogue leaves in flight per wave (they count in vmcnt)
-  constexpr int kEpiStores = 16 * (EPI == 2 ? 2 : 1);
+  constexpr int kEpiStores = 4 * (32 / C::ERI) * (EPI == 2 ? 2 : 1);
+  constexpr int kRelaxedWait = (kNBuf - 2) * kPer + kEpiStores < 63 ? (kNBuf - 2) * kPer + kEpiStores : 63;
 
   if (my_tiles == 0) return;
   set_tile(0);
@@ -256,18 +275,18 @@ __global__ __launch_bounds__(kThreads, 1) void linear_fwd_kernel(const E* __rest
     __builtin_amdgcn_sched_barrier(0);  // keep the DMA at the head of the step (the scheduler sinks it)
     const char* xt = cur;
     const char* wt = cur + SB;
-    // 4 feature fragments + 8 token fragments (12 ds_read_b128) feed 32 MFMAs
-    V wf[4];
+    // NI feature fragments + 8 token fragments feed 8 NI MFMAs
+    V wf[NI];
 #pragma unroll
-    for (int ni = 0; ni < 4; ++ni) wf[ni] = *reinterpret_cast<const V*>(wt + (64 * wn + 16 * ni) * RB + rdo);
+    for (int ni = 0; ni < NI; ++ni) wf[ni] = *reinterpret_cast<const V*>(wt + (WN * wn + 16 * ni) * RB + rdo);
 #pragma unroll
     for (int mi = 0; mi < 8; ++mi) {
       const V xf = *reinterpret_cast<const V*>(xt + (128 * wm + 16 * mi) * RB + rdo);
 #pragma unroll
-      for (int ni = 0; ni < 4; ++ni) acc[ni][mi] = mfma16(wf[ni], xf, acc[ni][mi]);  // D[n][m]
+      for (int ni = 0; ni < NI; ++ni) acc[ni][mi] = mfma16(wf[ni], xf, acc[ni][mi]);  // D[n][m]
     }
     if constexpr (decltype(relaxed)::value)
-      wait_vm<(kNBuf - 2) * kPer + kEpiStores>();
+      wait_vm<kRelaxedWait>();
     else
       wait_vm<(kNBuf - 2) * kPer>();  // the next stage landed (two more may still be in flight)
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -305,9 +324,17 @@ extern "C" int smdt_linear_fwd_supported(int64_t M, int64_t N, int64_t K) {
 }
 
 // epi: 0 = plain, 1 = + bias, 2 = + bias -> GeLU(tanh) into y with the pre-activation into h.
+// waves: 8 or 4 (wave layouts, see Cfg); 0 = the default (SMDT_LINEAR_WAVES, else 8).
 extern "C" hipError_t smdt_linear_fwd(int dtype, int epi, const void* x, const void* w, const void* bias, void* y,
                                       void* h, int64_t M, int64_t N, int64_t K, int64_t ldx, int64_t ldw,
-                                      int64_t ldy, hipStream_t st) {
+                                      int64_t ldy, int waves, hipStream_t st) {
+  static int def_waves = 0;
+  if (!def_waves) {
+    const char* e = getenv("SMDT_LINEAR_WAVES");
+    def_waves = (e && atoi(e) == 4) ? 4 : 8;
+  }
+  if (waves == 0) waves = def_waves;
+  if (waves != 4 && waves != 8) return hipErrorInvalidValue;
   if (dtype != 1 && dtype != 2) return hipErrorInvalidValue;
   if (epi < 0 || epi > 2 || !smdt_linear_fwd_supported(M, N, K)) return hipErrorInvalidValue;
   if ((epi >= 1 && !bias) || (epi == 2 && !h)) return hipErrorInvalidValue;
@@ -323,14 +350,17 @@ extern "C" hipError_t smdt_linear_fwd(int dtype, int epi, const void* x, const v
   int nb = ntm * ntn < cus ? ntm * ntn : cus;
   nb = (nb + 7) / 8 * 8;
   const dim3 grid((unsigned)nb);
-#define SMDT_LG(EP, ET)                                                                                           \
-  hipLaunchKernelGGL((lg::linear_fwd_kernel<EP, ET>), grid, dim3(lg::kThreads), 0, st, (const ET*)x, (const ET*)w, \
+#define SMDT_LG1(EP, ET, NW)                                                                                       \
+  hipLaunchKernelGGL((lg::linear_fwd_kernel<EP, ET, NW>), grid, dim3(64 * NW), 0, st, (const ET*)x, (const ET*)w,  \
                      (const ET*)bias, (ET*)y, (ET*)h, (int)M, (int)N, (int)K, (int)ldx, (int)ldw, (int)ldy, ntm, ntn)
+#define SMDT_LG(EP, ET) \
+  do { if (waves == 4) SMDT_LG1(EP, ET, 4); else SMDT_LG1(EP, ET, 8); } while (0)
   if (dtype == 2) {
     if (epi == 0) SMDT_LG(0, f16); else if (epi == 1) SMDT_LG(1, f16); else SMDT_LG(2, f16);
   } else {
     if (epi == 0) SMDT_LG(0, bf16); else if (epi == 1) SMDT_LG(1, bf16); else SMDT_LG(2, bf16);
   }
 #undef SMDT_LG
+#undef SMDT_LG1
   return hipGetLastError();
 }

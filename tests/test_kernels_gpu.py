@@ -394,7 +394,8 @@ def test_wgrad_mfma_fp16_and_bf16(dt):
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("shape", [(4096, 4096, 1024), (1000, 520, 256), (2048, 50304 // 8, 128), (256, 8, 128), (300, 264, 512)])
 @pytest.mark.parametrize("epi", [0, 1, 2])
-def test_linear_fwd_mfma_matches_fp32_reference(shape, epi, dt):
+@pytest.mark.parametrize("waves", [8, 4])
+def test_linear_fwd_mfma_matches_fp32_reference(shape, epi, dt, waves):
     """Hand-written NT GEMM (linear_gemm.hip) incl. partial tiles and the fused bias / bias + GeLU
     epilogues vs an fp32 torch reference (the pre-activation h is returned too)."""
     C = _ext.ext()
@@ -403,7 +404,7 @@ def test_linear_fwd_mfma_matches_fp32_reference(shape, epi, dt):
     x = torch.randn(M, K, device=DEV, dtype=dt)
     w = torch.randn(N, K, device=DEV, dtype=dt) * K ** -0.5
     b = torch.randn(N, device=DEV, dtype=dt)
-    out = C.linear_fwd(x, w, b if epi else None, epi)
+    out = C.linear_fwd(x, w, b if epi else None, epi, waves)
     ref = x.float() @ w.float().t()
     if epi:
         ref = ref + b.float()
