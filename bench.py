@@ -80,6 +80,8 @@ def parse():
     p.add_argument("--zero", type=int, default=1, help="ZeRO-1/2 distributed optimizer when DP > 1")
     p.add_argument("--bucket-size", type=int, default=40_000_000)
     p.add_argument("--no-flash", action="store_true")
+    p.add_argument("--fused-ce", action="store_true",
+                   help="chunked LM head + CE with its backward in forward (never materialises the logits)")
     p.add_argument("--recompute", choices=["none", "full"], default="none")
     p.add_argument("--profile-steps", type=int, default=0)
     p.add_argument("--tunableop", type=int, default=1,
@@ -178,7 +180,8 @@ def main():
                             attention_dropout=a.attention_dropout, params_dtype=torch.bfloat16,
                             sequence_parallel=sp and a.tp > 1, use_flash_attn=not a.no_flash,
                             recompute_granularity="full" if a.recompute == "full" else None,
-                            recompute_method="uniform" if a.recompute == "full" else None)
+                            recompute_method="uniform" if a.recompute == "full" else None,
+                            fused_lm_head_ce=a.fused_ce)
     model = GPTModel(cfg, pre_process=st.is_first_stage(), post_process=st.is_last_stage(), device=dev)
     zero = bool(a.zero) and st.dp > 1
     ddp = DistributedDataParallel(model, bucket_size=a.bucket_size, use_distributed_optimizer=zero,
@@ -239,6 +242,8 @@ def main():
         last = train_step()
     if torch.cuda.is_available():
         torch.cuda.synchronize()
+    from smdt_amd.ops import functional as SF
+    SF.fused_linear_ce_check()   # (after the timed region) the fused LM head saw a plain mean
     if dist.is_initialized():
         dist.barrier()
     el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)

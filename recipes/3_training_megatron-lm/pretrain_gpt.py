@@ -79,7 +79,8 @@ def forward_step(data_iterator, model):
     timers("batch-generator", log_level=2).start()
     tokens, labels, loss_mask, attention_mask, position_ids = get_batch(data_iterator)
     timers("batch-generator").stop()
-    output_tensor = model(tokens, position_ids, attention_mask, labels=labels)
+    # the loss mask tells the fused LM head + CE the reduction loss_func applies
+    output_tensor = model(tokens, position_ids, attention_mask, labels=labels, loss_mask=loss_mask)
     return output_tensor, partial(loss_func, loss_mask)
 
 

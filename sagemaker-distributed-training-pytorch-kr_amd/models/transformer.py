@@ -68,6 +68,12 @@ class TransformerConfig:
     recompute_method: Optional[str] = None       # "uniform" | "block"
     recompute_num_layers: Optional[int] = None
     distribute_saved_activations: bool = False   # full recompute: saved layer inputs split across TP
+    # LM head + CE fused and chunked over tokens, backward computed in forward (GPTModel; TP = 1).
+    # Only for callers that reduce the per-token losses with the weights they declare (the loss
+    # mask, or a plain mean): --fused-lm-head-ce (Megatron recipe) / --fused-ce (bench.py). Saves the
+    # logits' memory; slower at GPT-2 345M (profiles/r2_fused_ce/README.md).
+    fused_lm_head_ce: bool = False
+    lm_head_ce_chunk: int = 2048
 
     def __post_init__(self):
         if self.num_query_groups is None:

@@ -313,6 +313,22 @@ def flush_deferred_wgrad():
     DEFERRED_WGRAD.flush()
 
 
+def accumulate_wgrad(mg, g2, t2):
+    """mg (fp32 [N, K]) += g2^T t2 now: the MFMA wgrad kernel or hipBLASLt beta = 1, whichever the
+    per-shape timing picked (no deferral, no readiness callback)."""
+    done = False
+    if (_FUSED_WGRAD and mg.dtype == torch.float32 and g2.dtype in (torch.bfloat16, torch.float16)
+            and g2.is_cuda and mg.is_contiguous()):
+        C = _ext.ext()
+        g2, t2 = g2.contiguous(), t2.contiguous()
+        if _wgrad_impl(C, mg, g2, t2) == "mfma":
+            done = C.wgrad_mfma(mg, g2, t2, 0)
+        if not done:
+            done = C.wgrad_accumulate(mg, g2, t2)
+    if not done:
+        mg.add_(g2.t().matmul(t2).view_as(mg))
+
+
 def _wgrad(weight, g2, t2):
     """dW = g2^T t2. With a DDP ``main_grad`` the product is accumulated straight into the fp32
     buffer (K7 gradient-accumulation fusion): queued for the grouped MFMA launch
@@ -325,17 +341,7 @@ def _wgrad(weight, g2, t2):
     if DEFERRED_WGRAD.eligible(mg, g2, t2):
         DEFERRED_WGRAD.push(weight, mg, g2, t2)
         return None
-    done = False
-    if (_FUSED_WGRAD and mg.dtype == torch.float32 and g2.dtype in (torch.bfloat16, torch.float16)
-            and g2.is_cuda and mg.is_contiguous()):
-        C = _ext.ext()
-        g2, t2 = g2.contiguous(), t2.contiguous()
-        if _wgrad_impl(C, mg, g2, t2) == "mfma":
-            done = C.wgrad_mfma(mg, g2, t2, 0)
-        if not done:
-            done = C.wgrad_accumulate(mg, g2, t2)
-    if not done:
-        mg.add_(g2.t().matmul(t2).view_as(mg))
+    accumulate_wgrad(mg, g2, t2)
     cb = getattr(weight, "_smdt_grad_ready", None)
     if cb is not None:
         cb(weight)

@@ -37,6 +37,7 @@ from ..data.tokenizer import build_tokenizer, vocab_size_with_padding
 from ..models.gpt import allreduce_word_embedding_grads, gpt_flops_per_token
 from ..optim.lr_scheduler import OptimizerParamScheduler
 from ..optim.optimizer import ConstantLossScaler, DynamicLossScaler, MixedPrecisionAdam
+from ..ops import functional as SF
 from ..parallel import state as ps
 from ..parallel.distributed import DistributedDataParallel
 from ..parallel.random import model_parallel_seed
@@ -248,6 +249,8 @@ def _tensorboard_log(writer, loss_dict, lr, iteration, loss_scale, grad_norm, ar
 def training_log(loss_dict, total_loss_dict, lr, iteration, loss_scale, report_memory_flag, skipped, grad_norm,
                  args, elapsed_per_iter, model_cfg=None):
     timers = A.get_timers()
+    if iteration % args.log_interval == 0:
+        SF.fused_linear_ce_check()  # the fused LM head's declared reduction matched the real one
     if getattr(args, "tensorboard_dir", None) and iteration % args.tensorboard_log_interval == 0:
         _tensorboard_log(get_tensorboard_writer(), loss_dict, lr, iteration, loss_scale, grad_norm, args, timers)
     for k, v in loss_dict.items():
