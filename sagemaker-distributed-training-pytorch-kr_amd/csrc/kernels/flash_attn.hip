@@ -130,8 +130,10 @@ __device__ __forceinline__ uint32_t half_masks(uint32_t t) {
 // Packed-pair masks of slot 2u (bits 7 / 23) and slot 2u + 1 (bits 15 / 31).
 __device__ __forceinline__ uint32_t mask_even_slot(uint32_t t) { return half_masks(t << 8); }
 __device__ __forceinline__ uint32_t mask_odd_slot(uint32_t t) { return half_masks(t); }
-// All-ones / zero of decision bit ``b`` (v_bfe_i32): per-element fp32 masking.
-// (v_bfe_i32 by hand: left to itself the compiler turns the sign-extend into test + compare + select.)
+// x if keep bit b of t is set, else 0: v_bfe_i32 (all-ones / zero) + v_and. Only the bfe is asm (left
+// to itself the compiler turns the sign-extend into test + compare + select); x comes straight out
+// of an MFMA and must be read by a compiler-visible instruction (inline asm reading an MFMA result
+// is not covered by the hazard padding).
 template <int b>
 __device__ __forceinline__ float and_bit(float x, uint32_t t) {
   int32_t m;
@@ -405,12 +407,16 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void fwd_kernel(const E* __re
 }
 
 // ---------------------------------------------------------------------------------------
-// delta[b, h, q] = sum_d dO[q, d] * O[q, d]
+// The backward kernels' per-query row constants, ready to be loaded straight into MFMA
+// accumulators (no VALU in their loops):
+//   ndl[b, h, q]   = -keep * sum_d dO[q, d] O[q, d]      (-delta', the dP accumulator's start)
+//   nlse2[b, h, q] = -(lse log2 e - log2 inv)           (the S accumulator's start, log2 domain)
 template <int D, class E>
 __global__ __launch_bounds__(256) void delta_kernel(const E* __restrict__ O,
                                                     const E* __restrict__ dO,
-                                                    float* __restrict__ delta, int B, int H,
-                                                    int S, Strides os, Strides dos) {
+                                                    float* __restrict__ delta, const float* __restrict__ LSE,
+                                                    float* __restrict__ NLSE2, float dscale, float lsub, int B,
+                                                    int H, int S, Strides os, Strides dos) {
   // 8 lanes per row, each lane D/8 contiguous elements.
   const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int64_t row = gid / 8;
@@ -432,7 +438,8 @@ __global__ __launch_bounds__(256) void delta_kernel(const E* __restrict__ O,
   }
 #pragma unroll
   for (int off = 4; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 8);
-  if (part == 0) delta[row] = acc;
+  if (part == 0) delta[row] = -acc * dscale;
+  if (part == 1) NLSE2[row] = lsub - LSE[row] * kLog2e;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -533,6 +540,8 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dkdv_kernel(
         if (CAUSAL && qsub + 31 < kw) continue;  // all queries precede all of this wave's keys
         // S'[q, key] = Q . K'^T - lse ; dP'[q, key] = dO . V^T - delta  (key on lane, query rows
         // in registers): the row constants are the accumulators' initial values.
+        // (the rows were prepared by delta_kernel: -(lse log2e - log2 inv) and -delta', so the
+        // accumulators start as plain LDS reads)
         f32x16 s, dp;
   #pragma unroll
         for (int g = 0; g < 4; ++g) {
@@ -541,8 +550,8 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dkdv_kernel(
           const f32x4 dl = *reinterpret_cast<const f32x4*>(del_l + r0);
   #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            s[4 * g + j] = fmaf(-lv[j], kLog2e, DROP ? drop.log2inv : 0.f);  // -(lse log2e - log2 inv)
-            dp[4 * g + j] = DROP ? 0.f : -dl[j];  // dropout needs the raw dP (delta applied below)
+            s[4 * g + j] = lv[j];
+            dp[4 * g + j] = DROP ? 0.f : dl[j];  // dropout masks the raw dP (delta' added below)
           }
         }
   #pragma unroll
@@ -557,7 +566,7 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dkdv_kernel(
   #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const int r0 = 32 * qs2 + 8 * g + 4 * h;
-          const f32x4 dlg = DROP ? *reinterpret_cast<const f32x4*>(del_l + r0) * drop.keep : f32x4{0.f, 0.f, 0.f, 0.f};
+          const f32x4 ndl = DROP ? *reinterpret_cast<const f32x4*>(del_l + r0) : f32x4{0.f, 0.f, 0.f, 0.f};
           uint32_t t = 0u;
           if constexpr (DROP) {
             t = keep_bits(drop_hash(dblk + (uint32_t)(16 * qs2 + 4 * g) * shalf, dkey), dsel, drop.k4);
@@ -573,13 +582,13 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dkdv_kernel(
               if (my_key > qb + r0 + j + 1) p1 = 0.f;
             }
             float d0 = dp[i], d1 = dp[i + 1];
-            if constexpr (DROP) {
+            if constexpr (DROP) {  // kept: dP - delta'; dropped: -delta'
               if (j == 0) {
-                d0 = and_bit<7>(d0, t) - dlg[j];
-                d1 = and_bit<23>(d1, t) - dlg[j + 1];
+                d0 = and_bit<7>(d0, t) + ndl[j];
+                d1 = and_bit<23>(d1, t) + ndl[j + 1];
               } else {
-                d0 = and_bit<15>(d0, t) - dlg[j];
-                d1 = and_bit<31>(d1, t) - dlg[j + 1];
+                d0 = and_bit<15>(d0, t) + ndl[j];
+                d1 = and_bit<31>(d1, t) + ndl[j + 1];
               }
             }
             s[i] = p0;
@@ -672,13 +681,11 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dq_kernel(
   load_reg_frags<D>(dO + b * dos.sb + hq * dos.sh, dos.ss, qw, lane, dof);
 #pragma unroll
   for (int kk = 0; kk < G::KS; ++kk) qf[kk] = scale8(qf[kk], scale * kLog2e);  // S^T in log2 domain
-  const float lse2 = LSE[((int64_t)b * H + hq) * S + my_q] * kLog2e - (DROP ? drop.log2inv : 0.f);
-  const float dl = DROP ? DELTA[((int64_t)b * H + hq) * S + my_q] * drop.keep
-                        : DELTA[((int64_t)b * H + hq) * S + my_q];
-  // Row constants as the S / dP MFMAs' initial accumulators, register-resident for the whole
-  // loop (no per-subtile splat).
-  // (with dropout dP starts at 0: dropped entries need the raw dP masked before - delta')
-  const f32x16 st0 = splat16(-lse2), dp0 = splat16(DROP ? 0.f : -dl);
+  // Row constants (prepared by delta_kernel: -(lse log2e - log2 inv), -delta') as the S / dP MFMAs'
+  // initial accumulators, register-resident for the whole loop (no per-subtile splat).
+  const float nlse2 = LSE[((int64_t)b * H + hq) * S + my_q];
+  const float ndl = DELTA[((int64_t)b * H + hq) * S + my_q];
+  const f32x16 st0 = splat16(nlse2), dp0 = splat16(DROP ? 0.f : ndl);  // dropout masks the raw dP
   const float c2 = scale * kLog2e;
   const uint32_t dkey = DROP ? drop_key(drop, bh) : 0u;
   const uint32_t dblk = (uint32_t)(my_q >> 1) * ((uint32_t)S >> 1) + 2u * h + (uint32_t)(my_q & 1);
@@ -737,14 +744,14 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dq_kernel(
           if (ksub + acc_row(i + 1, h) > my_q) p1 = 0.f;
         }
         float d0 = dpt[i], d1 = dpt[i + 1];
-        if constexpr (DROP) {  // dropped: dP contributes 0, dS = p' (0 - delta')
+        if constexpr (DROP) {  // kept: dP - delta'; dropped: dS = p' (0 - delta')
           const uint32_t t = tb[i >> 2];
           if ((i & 2) == 0) {
-            d0 = and_bit<7>(d0, t) - dl;
-            d1 = and_bit<23>(d1, t) - dl;
+            d0 = and_bit<7>(d0, t) + ndl;
+            d1 = and_bit<23>(d1, t) + ndl;
           } else {
-            d0 = and_bit<15>(d0, t) - dl;
-            d1 = and_bit<31>(d1, t) - dl;
+            d0 = and_bit<15>(d0, t) + ndl;
+            d1 = and_bit<31>(d1, t) + ndl;
           }
         }
         dpt[i] = p0 * d0;  // dS^T
@@ -869,19 +876,22 @@ extern "C" hipError_t smdt_flash_bwd(int dtype, const void* q, const void* k, co
       vs{strides[6], strides[7], strides[8]}, os{strides[9], strides[10], strides[11]},
       dos{strides[12], strides[13], strides[14]}, dqs{strides[15], strides[16], strides[17]},
       dks{strides[18], strides[19], strides[20]}, dvs{strides[21], strides[22], strides[23]};
+  // delta holds 2 x [B, H, S]: -delta' rows, then -(lse log2e - log2 inv) rows (see delta_kernel)
+  float* nlse2 = delta + (int64_t)B * H * S;
+  const float dscale = drop ? dr.keep : 1.f, lsub = drop ? dr.log2inv : 0.f;
   {
     int64_t rows = (int64_t)B * H * S;
     dim3 grid((unsigned)((rows * 8 + 255) / 256));
     if (dtype == 2) {
       if (D == 64)
-        hipLaunchKernelGGL((delta_kernel<64, f16>), grid, dim3(256), 0, st, (const f16*)o, (const f16*)dout, delta, B, H, S, os, dos);
+        hipLaunchKernelGGL((delta_kernel<64, f16>), grid, dim3(256), 0, st, (const f16*)o, (const f16*)dout, delta, lse, nlse2, dscale, lsub, B, H, S, os, dos);
       else
-        hipLaunchKernelGGL((delta_kernel<128, f16>), grid, dim3(256), 0, st, (const f16*)o, (const f16*)dout, delta, B, H, S, os, dos);
+        hipLaunchKernelGGL((delta_kernel<128, f16>), grid, dim3(256), 0, st, (const f16*)o, (const f16*)dout, delta, lse, nlse2, dscale, lsub, B, H, S, os, dos);
     } else {
       if (D == 64)
-        hipLaunchKernelGGL((delta_kernel<64, bf16>), grid, dim3(256), 0, st, (const bf16*)o, (const bf16*)dout, delta, B, H, S, os, dos);
+        hipLaunchKernelGGL((delta_kernel<64, bf16>), grid, dim3(256), 0, st, (const bf16*)o, (const bf16*)dout, delta, lse, nlse2, dscale, lsub, B, H, S, os, dos);
       else
-        hipLaunchKernelGGL((delta_kernel<128, bf16>), grid, dim3(256), 0, st, (const bf16*)o, (const bf16*)dout, delta, B, H, S, os, dos);
+        hipLaunchKernelGGL((delta_kernel<128, bf16>), grid, dim3(256), 0, st, (const bf16*)o, (const bf16*)dout, delta, lse, nlse2, dscale, lsub, B, H, S, os, dos);
     }
   }
   dim3 gkv((unsigned)((int64_t)B * Hkv * (S / kBlockRows)));
@@ -889,10 +899,10 @@ extern "C" hipError_t smdt_flash_bwd(int dtype, const void* q, const void* k, co
 #define SMDT_FA_BWD_T(DD, CC, DR, ET)                                                            \
   do {                                                                                           \
     hipLaunchKernelGGL((bwd_dkdv_kernel<DD, CC, DR, ET>), gkv, dim3(256), 0, st, (const ET*)q,  \
-                       (const ET*)k, (const ET*)v, (const ET*)dout, lse, delta, (ET*)dk,          \
+                       (const ET*)k, (const ET*)v, (const ET*)dout, nlse2, delta, (ET*)dk,        \
                        (ET*)dv, B, H, Hkv, S, qs, ks, vs, dos, dks, dvs, scale, dr);              \
     hipLaunchKernelGGL((bwd_dq_kernel<DD, CC, DR, ET>), gq, dim3(256), 0, st, (const ET*)q,     \
-                       (const ET*)k, (const ET*)v, (const ET*)dout, lse, delta, (ET*)dq,          \
+                       (const ET*)k, (const ET*)v, (const ET*)dout, nlse2, delta, (ET*)dq,        \
                        B, H, Hkv, S, qs, ks, vs, dos, dqs, scale, dr);                            \
   } while (0)
 #define SMDT_FA_BWD(DD, CC, DR) \

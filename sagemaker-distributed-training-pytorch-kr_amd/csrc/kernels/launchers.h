@@ -82,6 +82,7 @@ hipError_t smdt_flash_fwd(int dtype, const void* q, const void* k, const void* v
                           int64_t v_sb, int64_t v_ss, int64_t v_sh, int64_t o_sb, int64_t o_ss,
                           int64_t o_sh, float scale, int causal, float dropout_p, uint64_t seed,
                           uint64_t offset, hipStream_t st);
+// delta: fp32 scratch of 2 x B x H x S (the backward's prepared per-query row constants).
 hipError_t smdt_flash_bwd(int dtype, const void* q, const void* k, const void* v, const void* o,
                           const void* dout, const float* lse, float* delta, void* dq, void* dk,
                           void* dv, int B, int H, int Hkv, int S, int D, const int64_t* strides,
