@@ -42,7 +42,7 @@ import torch.distributed as dist
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
-from smdt_amd.comm import init_distributed  # noqa: E402
+from smdt_amd.comm import init_distributed, relay  # noqa: E402
 from smdt_amd.models.gpt import GPTModel, allreduce_word_embedding_grads, gpt_flops_per_token, pad_vocab_size  # noqa: E402
 from smdt_amd.models.transformer import TransformerConfig  # noqa: E402
 from smdt_amd.optim.optimizer import MixedPrecisionAdam  # noqa: E402
@@ -244,6 +244,7 @@ def main():
         torch.cuda.synchronize()
     from smdt_amd.ops import functional as SF
     SF.fused_linear_ce_check()   # (after the timed region) the fused LM head saw a plain mean
+    relay.check_all()            # (after the timed region) no TP-pair exchange timed out
     if dist.is_initialized():
         dist.barrier()
     el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)

@@ -11,6 +11,8 @@ all-gather (RCCL and xGMI) and all-to-all (RCCL) — prints one JSON line with t
     reduce-scatter  busbw = bytes * (W - 1) / W / t     (bytes = the full, unreduced tensor)
     all-gather      busbw = bytes * (W - 1) / W / t     (bytes = the gathered tensor)
     all-to-all      busbw = bytes * (W - 1) / W / t
+    pair exchange   busbw = bytes / t     (every rank swaps ``bytes`` with its TP partner r ^ 1;
+                                           RCCL p2p over the one direct link vs comm/relay.py)
 
 That is the per-GPU link traffic rate: on an MI355X node each GPU has 7 xGMI links, so W = 8
 collectives can approach 7 x the one-link rate while a W = 2 group is bound by its single link
@@ -34,10 +36,11 @@ import torch.distributed as dist
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-from smdt_amd.comm import xgmi  # noqa: E402
+from smdt_amd.comm import relay, xgmi  # noqa: E402
 
 FACTOR = {"all_reduce": lambda w: 2.0 * (w - 1) / w, "reduce_scatter": lambda w: (w - 1) / w,
-          "all_gather": lambda w: (w - 1) / w, "all_to_all": lambda w: (w - 1) / w}
+          "all_gather": lambda w: (w - 1) / w, "all_to_all": lambda w: (w - 1) / w,
+          "pair_exchange": lambda w: 1.0}
 
 
 def sizes(max_mb: float):
@@ -84,6 +87,15 @@ def run_distributed(a):
         except (RuntimeError, ValueError) as e:
             if rank == 0:
                 print(f"[bench_collectives] xGMI engine unavailable: {e}", flush=True)
+    # TP-pair exchange (pairs r, r ^ 1): RCCL p2p vs the multi-path relay, every pair at once
+    pairs = [dist.new_group([p, p + 1]) for p in range(0, W, 2)] if W % 2 == 0 else []
+    rly = None
+    if W in (4, 8):
+        try:
+            rly = relay.XgmiRelay(pairs[rank // 2])
+        except (RuntimeError, ValueError) as e:
+            if rank == 0:
+                print(f"[bench_collectives] xGMI relay unavailable: {e}", flush=True)
     for nbytes in sizes(a.max_mb):
         n = nbytes // 2 // W * W                    # bf16 elements, divisible by W
         full = torch.randn(n, device=dev, dtype=torch.bfloat16)
@@ -99,6 +111,13 @@ def run_distributed(a):
             cases += [("all_reduce", "xgmi", lambda: eng.all_reduce(full)),
                       ("reduce_scatter", "xgmi", lambda: eng.reduce_scatter(part, full)),
                       ("all_gather", "xgmi", lambda: eng.all_gather(out_full, part))]
+        if pairs:
+            pin, pout = torch.empty_like(full), torch.empty_like(full)
+            cases.append(("pair_exchange", "rccl", lambda: dist.batch_isend_irecv(
+                [dist.P2POp(dist.isend, full, rank ^ 1, pairs[rank // 2]),
+                 dist.P2POp(dist.irecv, pin, rank ^ 1, pairs[rank // 2])])[-1].wait()))
+            if rly is not None:
+                cases.append(("pair_exchange", "relay", lambda: rly.exchange(full, pout)))
         for op, impl, fn in cases:
             t = timed(fn, a.iters, a.warmup, sync)
             if rank == 0:
@@ -108,6 +127,9 @@ def run_distributed(a):
     if eng is not None:
         eng.check()
         eng.close()
+    if rly is not None:
+        rly.check()
+        rly.close()
     dist.barrier()
     dist.destroy_process_group()
 
@@ -133,6 +155,19 @@ def run_loopback(a):
         assert lb.errors() == [0] * W, lb.errors()
     finally:
         lb.close()
+    rl = relay.XgmiRelayLoopback(W, slot_bytes=a.region_mb << 20, sub=2)
+    try:
+        for nbytes in sizes(min(a.max_mb, W * a.region_mb // 2)):
+            n = nbytes // 2 // 8 * 8
+            x = torch.randn(W, n, device="cuda", dtype=torch.bfloat16)
+            y = torch.empty_like(x)
+            t = timed(lambda: rl.exchange(x, y), a.iters, a.warmup, sync)
+            emit({"op": "pair_exchange", "impl": "relay", "world": W, "bytes": n * 2, "ms": t * 1e3,
+                  "busbw_GBps": n * 2 / t / 1e9, "loopback": True,
+                  "note": "W virtual ranks on one GPU: kernel cost only, no xGMI links"})
+        assert rl.errors() == [0] * W, rl.errors()
+    finally:
+        rl.close()
 
 
 def main():

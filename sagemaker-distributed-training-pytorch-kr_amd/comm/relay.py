@@ -1,0 +1,330 @@
+"""Multi-path exchange for tensor-parallel pairs over every xGMI link of an MI355X node.
+
+A TP=2 layout (the BASELINE's TP2 x PP2 x DP2) moves each sequence-parallel chunk between the
+two GPUs of a pair once per ring step (``parallel/tensor_parallel.ag_ring`` / ``rs_ring``: 8
+exchanges of 16 MB per layer and micro-batch for GPT-2 345M at micro-batch 16). xGMI is point-to-
+point: the pair shares ONE link (~64-77 GB/s per direction) while each GPU's 6 other links idle,
+so RCCL's p2p send/recv moves a layer's activations slower than the MFMA cores consume them.
+
+``XgmiRelay`` cuts every message into W parts: 2 go directly into the partner's staging buffer,
+W - 2 are staged in the other GPUs' buffers and pulled from there by the partner
+(``csrc/kernels/xgmi_relay.hip``; the relays run no code). With all pairs of a node exchanging at
+once every directed link carries 2/W of a message — ~4x the one-link rate on 8 GPUs.
+
+Construction is collective over the WORLD (every GPU of the node is a waypoint). It is only kept
+when it (1) reproduces RCCL's exchange exactly and (2) is measured faster than RCCL's p2p
+exchange at the message sizes it will carry — the decision is made at run time from a timing on
+the real links, agreed by all ranks, and logged. ``SMDT_TP_RELAY=0`` turns it off, ``=1`` skips
+the speed test (correctness is always checked).
+
+The reference's TP collectives are stock NCCL; there is nothing to port.
+"""
+from __future__ import annotations
+
+import os
+import socket
+import time
+import warnings
+from typing import Dict, List, Optional
+
+import torch
+import torch.distributed as dist
+
+from ..ops import _ext
+from .xgmi import _EventHandle
+
+DEFAULT_SLOT_BYTES = 8 << 20      # per (flow, parity): parts of up to 4 MB -> 32 MB per call on 8 GPUs
+DEFAULT_SUB = 4                   # blocks per part and direction (2 x W x 4 = 64 blocks on 8 GPUs)
+_ENGINES: Dict[int, "XgmiRelay"] = {}
+
+
+def mode() -> str:
+    """'off' / 'auto' (validated + timed against RCCL) / 'on' (validated only)."""
+    v = os.environ.get("SMDT_TP_RELAY", "auto").lower()
+    return {"0": "off", "off": "off", "1": "on", "on": "on"}.get(v, "auto")
+
+
+def engine_for(group) -> Optional["XgmiRelay"]:
+    return _ENGINES.get(id(group)) if group is not None else None
+
+
+def eligible(send: torch.Tensor, recv: torch.Tensor) -> bool:
+    nbytes = send.numel() * send.element_size()
+    return (send.is_cuda and send.is_contiguous() and recv.is_contiguous() and send.dtype == recv.dtype
+            and send.numel() == recv.numel() and send.dtype in (torch.float32, torch.bfloat16, torch.float16)
+            and nbytes > 0 and nbytes % 16 == 0 and send.data_ptr() % 16 == 0 and recv.data_ptr() % 16 == 0)
+
+
+class XgmiRelay:
+    """Pairwise exchange engine for the size-2 ``pair_group`` of every rank (collective over WORLD)."""
+
+    def __init__(self, pair_group, slot_bytes: int = DEFAULT_SLOT_BYTES, sub: int = DEFAULT_SUB,
+                 validate: bool = True):
+        self.C = _ext.ext()
+        self.group = pair_group
+        self.world = dist.get_world_size()
+        self.rank = dist.get_rank()
+        if self.world not in (2, 4, 8):
+            raise ValueError(f"xGMI relay supports 2, 4 or 8 ranks, not {self.world}")
+        if dist.get_world_size(pair_group) != 2:
+            raise ValueError("xGMI relay exchanges within groups of 2 ranks")
+        self.slot = (int(slot_bytes) + 4095) // 4096 * 4096
+        self.sub = int(sub)
+        self.epoch = 0
+        self.min_bytes = 0
+        self.calls = 0
+        self._stream = None
+        self._opened: List[int] = []
+        self._stage = self._sig = None
+        self.active = False
+        mine_pair = [r for r in dist.get_process_group_ranks(pair_group) if r != self.rank][0]
+        info = [None] * self.world
+        dist.all_gather_object(info, (socket.gethostname(), mine_pair))
+        if len({h for h, _ in info}) != 1:
+            raise RuntimeError("xGMI relay needs every rank on one node")
+        self.partners = [p for _, p in info]
+        if any(self.partners[p] != r for r, p in enumerate(self.partners)):
+            raise RuntimeError(f"xGMI relay: pair groups are not symmetric: {self.partners}")
+        self.partner = mine_pair
+        err = None
+        try:
+            self._stage = self.C.ipc_malloc(self.world * 2 * self.slot, False)
+            self._sig = self.C.ipc_malloc(self.C.relay_signal_bytes(), True)
+            mine = (self.C.ipc_get_handle(self._stage), self.C.ipc_get_handle(self._sig))
+        except RuntimeError as e:
+            err, mine = e, None
+        handles = [None] * self.world
+        dist.all_gather_object(handles, mine)
+        self.stage_ptrs: List[int] = []
+        self.sig_ptrs: List[int] = []
+        if err is None and all(h is not None for h in handles):
+            try:
+                for r, (hd, hs) in enumerate(handles):
+                    if r == self.rank:
+                        self.stage_ptrs.append(self._stage)
+                        self.sig_ptrs.append(self._sig)
+                    else:
+                        pd = self.C.ipc_open(hd)
+                        self._opened.append(pd)
+                        ps_ = self.C.ipc_open(hs)
+                        self._opened.append(ps_)
+                        self.stage_ptrs.append(pd)
+                        self.sig_ptrs.append(ps_)
+            except RuntimeError as e:
+                err = e
+        if not self._agree(err is None):
+            self.close()
+            raise RuntimeError(f"xGMI relay setup failed on some rank ({err!r} here)")
+        self.active = True
+        if validate and not self._validate():
+            self.close()
+            raise RuntimeError("xGMI relay failed its validation against RCCL p2p")
+
+    # ------------------------------------------------------------------ helpers
+    def _agree(self, ok: bool) -> bool:
+        on_host = dist.get_backend() == "gloo"
+        dev = torch.device("cpu") if on_host else torch.device("cuda", torch.cuda.current_device())
+        flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        return bool(flag.item())
+
+    def _rccl_exchange(self, send, recv):
+        """The reference exchange: RCCL p2p (gloo test groups: through host copies)."""
+        host = dist.get_backend(self.group) == "gloo"
+        s, r = (send.cpu(), torch.empty(recv.shape, dtype=recv.dtype)) if host else (send, recv)
+        works = dist.batch_isend_irecv([dist.P2POp(dist.isend, s, self.partner, self.group),
+                                        dist.P2POp(dist.irecv, r, self.partner, self.group)])
+        for w in works:
+            w.wait()
+        if host:
+            recv.copy_(r)
+
+    def _validate(self) -> bool:
+        """Exact check against RCCL p2p on rank-tagged data: three calls (both slot parities and
+        the slot-reuse wait), an odd size that leaves parts short, bf16 and fp32, and a message
+        larger than one call."""
+        dev = torch.device("cuda", torch.cuda.current_device())
+        good = True
+        big = self.world * self.slot // 2 // 4 + 4096  # fp32 elements: more than one call
+        for n, dt in ((4096, torch.float32), (1000 * 8 + 8, torch.bfloat16), (big, torch.float32)):
+            for rep in range(3):
+                x = ((torch.arange(n, device=dev, dtype=torch.float32) % 251) + 1000.0 * self.rank + rep).to(dt)
+                ref = torch.empty_like(x)
+                self._rccl_exchange(x, ref)
+                got = torch.empty_like(x)
+                self.exchange(x, got)
+                good &= bool(torch.equal(got, ref))
+        torch.cuda.synchronize()
+        good &= self.error() == 0
+        return self._agree(good)
+
+    def tune(self, sizes=(1 << 20, 4 << 20, 16 << 20), iters: int = 10) -> Dict[int, tuple]:
+        """Time RCCL p2p vs the relay with every pair of the node exchanging at once (the training
+        pattern) and keep the relay for messages >= the smallest size where it wins on every rank
+        (disabled when it never wins). Returns {bytes: (rccl_ms, relay_ms)} (max over ranks)."""
+        dev = torch.device("cuda", torch.cuda.current_device())
+        res = {}
+        wins = []
+        for nb in sizes:
+            x = torch.randn(nb // 2, device=dev, dtype=torch.bfloat16)
+            y = torch.empty_like(x)
+            ts = []
+            for fn in (lambda: self._rccl_exchange(x, y), lambda: self.exchange(x, y)):
+                for _ in range(3):
+                    fn()
+                torch.cuda.synchronize()
+                dist.barrier()
+                t0 = time.perf_counter()
+                for _ in range(iters):
+                    fn()
+                torch.cuda.synchronize()
+                host = dist.get_backend() == "gloo"
+                t = torch.tensor([(time.perf_counter() - t0) / iters * 1e3], device="cpu" if host else dev)
+                dist.all_reduce(t, op=dist.ReduceOp.MAX)
+                ts.append(float(t.item()))
+            res[nb] = tuple(ts)
+            wins.append(ts[1] < ts[0])
+        self.min_bytes = next((nb for nb, w in zip(sizes, wins) if w and all(wins[sizes.index(nb):])), None)
+        if self.min_bytes is None:
+            self.active = False
+        return res
+
+    # ------------------------------------------------------------------ API
+    def fits(self, send, recv) -> bool:
+        return (self.active and eligible(send, recv)
+                and send.numel() * send.element_size() >= (self.min_bytes or 0))
+
+    def exchange(self, send: torch.Tensor, recv: torch.Tensor) -> bool:
+        """recv (this rank) <- send (partner), both flat-contiguous, on the current stream. Calls
+        must be issued in the same order and sizes on both partners (they are: ring steps)."""
+        if not (self.active and eligible(send, recv)):
+            return False
+        es = send.element_size()
+        per = self.world * (self.slot // 32) * 16 // es      # elements per call (2 parts per slot)
+        fs, fr = send.view(-1), recv.view(-1)
+        n = fs.numel()
+        step = max(16 // es, per // (16 // es) * (16 // es))
+        for lo in range(0, n, step):
+            hi = min(n, lo + step)
+            self.epoch += 1
+            self.C.xgmi_relay(fs[lo:hi], fr[lo:hi], self.stage_ptrs, self.sig_ptrs, self.partners, self.rank, 1,
+                              self.slot, self.sub, self.epoch)
+        self.calls += 1
+        return True
+
+    def exchange_async(self, send: torch.Tensor, recv: torch.Tensor) -> Optional[_EventHandle]:
+        """The same on the engine's side stream after the current stream's work; ``wait()`` on the
+        handle makes the current stream wait. None: not taken (use RCCL)."""
+        if not self.fits(send, recv):
+            return None
+        dev = send.device
+        if self._stream is None:
+            self._stream = torch.cuda.Stream(device=dev)
+        cur = torch.cuda.current_stream(dev)
+        self._stream.wait_stream(cur)
+        with torch.cuda.stream(self._stream):
+            self.exchange(send, recv)
+            ev = torch.cuda.Event()
+            ev.record(self._stream)
+        send.record_stream(self._stream)
+        recv.record_stream(self._stream)
+        return _EventHandle(ev)
+
+    def error(self) -> int:
+        return int(self.C.relay_read_error(self._sig)) if self._sig is not None else 0
+
+    def check(self):
+        torch.cuda.synchronize()
+        e = self.error()
+        if e:
+            raise RuntimeError(f"xGMI relay: the partner did not arrive (error word {e}); outputs were NaN-filled")
+
+    def close(self):
+        """Collective over WORLD: unmap the peers' buffers, then free this rank's own."""
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+        if dist.is_initialized():
+            dist.barrier()
+        for p in self._opened:
+            try:
+                self.C.ipc_close(p)
+            except RuntimeError:  # pragma: no cover
+                pass
+        self._opened = []
+        if dist.is_initialized():
+            dist.barrier()
+        for p in (self._stage, self._sig):
+            if p is not None:
+                self.C.ipc_free(p)
+        self._stage = self._sig = None
+        self.active = False
+        for k, v in list(_ENGINES.items()):
+            if v is self:
+                del _ENGINES[k]
+
+
+def check_all():
+    """Raise if any registered relay engine's partner timed out (synchronises; call at logging
+    points, not per step)."""
+    for eng in list(_ENGINES.values()):
+        eng.check()
+
+
+def create_for_pairs(pair_group, log=print) -> Optional[XgmiRelay]:
+    """Collective over WORLD: build, validate and (mode 'auto') time the relay for this rank's
+    TP pair; registered for ``pair_group`` when kept. None when off / not applicable / slower."""
+    m = mode()
+    if m == "off" or not (dist.is_initialized() and torch.cuda.is_available()):
+        return None
+    try:
+        if dist.get_backend() not in ("nccl", "smddp") or dist.get_world_size() not in (4, 8):
+            return None
+        eng = XgmiRelay(pair_group)
+    except (RuntimeError, ValueError) as e:
+        warnings.warn(f"xGMI relay disabled: {e}")
+        return None
+    if m == "auto":
+        res = eng.tune()
+        if dist.get_rank() == 0 and log is not None:
+            pretty = ", ".join(f"{nb >> 20} MB: rccl {a:.3f} ms / relay {b:.3f} ms" for nb, (a, b) in res.items())
+            log(f"[smdt] TP-pair exchange over all xGMI links: {pretty} -> "
+                + (f"relay for messages >= {eng.min_bytes >> 10} KB" if eng.active else "RCCL kept"))
+        if not eng.active:
+            eng.close()
+            return None
+    _ENGINES[id(pair_group)] = eng
+    return eng
+
+
+class XgmiRelayLoopback:
+    """W virtual ranks in ONE launch on one GPU (pairs (0,1), (2,3), ...): the exact kernel and
+    protocol with plain device buffers (tests / kernel-cost microbenchmarks)."""
+
+    def __init__(self, world: int, slot_bytes: int = 1 << 20, sub: int = 2):
+        assert world in (2, 4, 8)
+        self.C = _ext.ext()
+        self.world = world
+        self.slot = (int(slot_bytes) + 4095) // 4096 * 4096
+        self.sub = sub
+        self.epoch = 0
+        self.partners = [r ^ 1 for r in range(world)]
+        self.stage_ptrs = [self.C.ipc_malloc(world * 2 * self.slot, False) for _ in range(world)]
+        self.sig_ptrs = [self.C.ipc_malloc(self.C.relay_signal_bytes(), True) for _ in range(world)]
+
+    def exchange(self, x: torch.Tensor, out: Optional[torch.Tensor] = None, epoch: Optional[int] = None):
+        """x: [world, n] (row r = virtual rank r's message). Returns [world, n]: row r = row r^1 of x."""
+        out = torch.empty_like(x) if out is None else out
+        self.epoch = self.epoch + 1 if epoch is None else epoch
+        self.C.xgmi_relay(x, out, self.stage_ptrs, self.sig_ptrs, self.partners, 0, self.world, self.slot, self.sub,
+                          self.epoch)
+        return out
+
+    def errors(self) -> List[int]:
+        torch.cuda.synchronize()
+        return [int(self.C.relay_read_error(s)) for s in self.sig_ptrs]
+
+    def close(self):
+        torch.cuda.synchronize()
+        for p in self.stage_ptrs + self.sig_ptrs:
+            self.C.ipc_free(p)
+        self.stage_ptrs, self.sig_ptrs = [], []

@@ -595,6 +595,52 @@ void xgmi_collective(int64_t mode, Tensor in, Tensor out, std::vector<int64_t> d
         "xgmi_collective");
 }
 
+int64_t relay_read_error(int64_t sig) {
+  int e = 0;
+  check(smdt_relay_read_error(vp(sig), &e), "relay_read_error");
+  return e;
+}
+
+// Pairwise TP exchange over all xGMI links (xgmi_relay.hip): out (on this rank) = in of the
+// partner. Loopback (nranks_local > 1): in / out are [nranks_local, m] rows, one per virtual rank.
+void xgmi_relay(Tensor in, Tensor out, std::vector<int64_t> stage_ptrs, std::vector<int64_t> sig_ptrs,
+                std::vector<int64_t> partners, int64_t rank, int64_t nranks_local, int64_t slot_bytes, int64_t sub,
+                int64_t epoch) {
+  TORCH_CHECK(in.dtype() == out.dtype() && in.device() == out.device(), "xgmi_relay: in / out mismatch");
+  TORCH_CHECK(in.is_cuda() && in.device().index() == c10::hip::current_device(),
+              "xgmi_relay: tensors must live on the current device");
+  TORCH_CHECK(in.scalar_type() == at::kFloat || in.scalar_type() == at::kBFloat16 || in.scalar_type() == at::kHalf,
+              "xgmi_relay: fp32 / bf16 / fp16");
+  const int world = (int)stage_ptrs.size();
+  TORCH_CHECK(sig_ptrs.size() == stage_ptrs.size() && partners.size() == stage_ptrs.size() &&
+                  (world == 2 || world == 4 || world == 8),
+              "xgmi_relay: 2, 4 or 8 ranks");
+  TORCH_CHECK(sub >= 1 && sub <= smdt_relay_max_sub(), "xgmi_relay: sub out of range");
+  TORCH_CHECK(epoch >= 1 && epoch <= 0xffffffffll, "xgmi_relay: epoch must be a positive uint32");
+  int64_t n = in.numel(), in_rs = 0, out_rs = 0;
+  if (nranks_local > 1) {
+    TORCH_CHECK(in.dim() == 2 && out.dim() == 2 && in.size(0) == nranks_local && out.size(0) == nranks_local &&
+                    in.stride(1) == 1 && out.stride(1) == 1 && out.size(1) == in.size(1),
+                "xgmi_relay loopback: in / out must be [nranks_local, m] with unit inner stride");
+    TORCH_CHECK(2 * sub * world * nranks_local <= 512, "xgmi_relay loopback: blocks must stay co-resident (<= 512)");
+    n = in.size(1);
+    in_rs = in.stride(0);
+    out_rs = out.stride(0);
+  } else {
+    TORCH_CHECK(in.is_contiguous() && out.is_contiguous() && out.numel() == n, "xgmi_relay: contiguous, equal sizes");
+  }
+  std::vector<void*> d(world), s(world);
+  std::vector<int> p(world);
+  for (int r = 0; r < world; ++r) {
+    d[r] = vp(stage_ptrs[r]);
+    s[r] = vp(sig_ptrs[r]);
+    p[r] = (int)partners[r];
+  }
+  check(smdt_xgmi_relay(dcode(in), in.data_ptr(), out.data_ptr(), in_rs, out_rs, n, d.data(), s.data(), p.data(), world,
+                        (int)rank, (int)nranks_local, slot_bytes, (int)sub, (uint32_t)epoch, cur_stream()),
+        "xgmi_relay");
+}
+
 }  // namespace
 
 void register_blaslt(pybind11::module_& m);
@@ -646,6 +692,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("xgmi_collective", &xgmi_collective, py::arg("mode"), py::arg("input"), py::arg("out"), py::arg("data_ptrs"),
         py::arg("sig_ptrs"), py::arg("rank"), py::arg("nranks_local"), py::arg("region_bytes"), py::arg("blocks"),
         py::arg("n"), py::arg("slice_stride"), py::arg("scale") = 1.0);
+  m.def("xgmi_relay", &xgmi_relay, py::arg("input"), py::arg("out"), py::arg("stage_ptrs"), py::arg("sig_ptrs"),
+        py::arg("partners"), py::arg("rank"), py::arg("nranks_local"), py::arg("slot_bytes"), py::arg("sub"),
+        py::arg("epoch"));
+  m.def("relay_signal_bytes", &smdt_relay_signal_bytes);
+  m.def("relay_read_error", &relay_read_error);
   m.def("flash_bwd", &flash_bwd, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("o"), py::arg("dout"),
         py::arg("lse"), py::arg("scale"), py::arg("causal"), py::arg("dq") = py::none(), py::arg("dk") = py::none(),
         py::arg("dv") = py::none(), py::arg("dropout_p") = 0.0, py::arg("seed") = 0, py::arg("offset") = 0);

@@ -139,4 +139,15 @@ hipError_t smdt_xgmi_collective(int mode, int dtype, const void* in, void* out, 
                                 void* const* data_ptrs, void* const* sig_ptrs, int world, int rank, int nranks_local,
                                 int64_t region_bytes, int blocks, hipStream_t st);
 
+// xgmi_relay.hip: pairwise exchange of a TP pair routed over every xGMI link of the node (direct
+// parts + relay parts staged in the other GPUs' buffers). stage_ptrs: world x (world x 2 x slot_bytes)
+// staging buffers; partners[r] = r's TP partner; epoch = engine call counter (>= 1, same on both
+// partners). n elements (n * esize % 16 == 0, 2 * ceil(n / world) vectors <= slot).
+int64_t smdt_relay_signal_bytes();
+int smdt_relay_max_sub();
+hipError_t smdt_relay_read_error(void* sig, int* err);
+hipError_t smdt_xgmi_relay(int dtype, const void* in, void* out, int64_t in_rank_stride, int64_t out_rank_stride,
+                           int64_t n, void* const* stage_ptrs, void* const* sig_ptrs, const int* partners, int world,
+                           int rank, int nranks_local, int64_t slot_bytes, int sub, uint32_t epoch, hipStream_t st);
+
 }  // extern "C"

@@ -51,6 +51,7 @@
 
 #include "common.h"
 #include "launchers.h"
+#include "xgmi_sync.h"
 
 namespace smdt {
 namespace ar {
@@ -72,15 +73,10 @@ struct Peers {
   SignalBuf* sig[kMaxRanks];  // signal buffers
 };
 
-using gu32 = __attribute__((address_space(1))) uint32_t;
-using u32x4 = __attribute__((ext_vector_type(4))) unsigned;
-
-__device__ __forceinline__ void store_sys(uint32_t* p, uint32_t v) {
-  __hip_atomic_store((gu32*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);  // global, never flat
-}
-__device__ __forceinline__ uint32_t load_sys(const uint32_t* p) {
-  return __hip_atomic_load((gu32*)const_cast<uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
+using xg::load_sys;
+using xg::rsrc;
+using xg::store_sys;
+using xg::u32x4;
 
 // Poll my own flag word until it reaches `epoch`; give up when the sticky error is set or the
 // spin limit runs out (then set the error). Returns false on failure.
@@ -114,11 +110,7 @@ __device__ __forceinline__ bool block_barrier(const Peers& P, int rank, int b, u
   return *s_ok != 0;
 }
 
-constexpr int kSysAux = 1 | 16;  // sc0 | sc1: system coherent, bypasses L1 and L2
-
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base, uint32_t bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
-}
+using xg::kSysAux;
 
 template <typename T> constexpr int E16 = 16 / (int)sizeof(T);
 
@@ -162,10 +154,7 @@ __device__ __forceinline__ u32x4 pack16(const float (&a)[E16<T>], float scale) {
 
 template <typename T>
 __device__ __forceinline__ void nan_fill(u32x4* __restrict__ out, int64_t v0, int64_t v1) {
-  uint32_t w = 0x7fc00000u;                                   // fp32 quiet NaN
-  if constexpr (std::is_same<T, bf16>::value) w = 0x7fc07fc0u;  // 2 x bf16 NaN
-  if constexpr (std::is_same<T, f16>::value) w = 0x7e007e00u;   // 2 x fp16 NaN
-  const u32x4 q = {w, w, w, w};
+  const u32x4 q = xg::nan16<T>();
   for (int64_t v = v0 + threadIdx.x; v < v1; v += kThreads) out[v] = q;
 }
 

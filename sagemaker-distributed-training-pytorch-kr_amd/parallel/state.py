@@ -181,6 +181,11 @@ def initialize_model_parallel(tensor_model_parallel_size: int = 1, pipeline_mode
     if tp > 1:
         from ..comm import xgmi
         st.tp_xgmi = xgmi.create_for_group(st.tp_group)
+    # TP pairs exchange over every xGMI link of the node (collective over WORLD; kept only when
+    # validated and measured faster than RCCL p2p, comm/relay.py)
+    if tp == 2 and world in (4, 8):
+        from ..comm import relay
+        st.tp_relay = relay.create_for_pairs(st.tp_group)
     return st
 
 

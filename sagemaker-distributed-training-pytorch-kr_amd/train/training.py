@@ -32,6 +32,7 @@ import torch
 import torch.distributed as dist
 
 from ..comm import init_distributed, print_rank_0, print_rank_last
+from ..comm import relay as _relay
 from ..data.gpt_dataset import SyntheticGPTDataset, build_pretraining_data_loader
 from ..data.tokenizer import build_tokenizer, vocab_size_with_padding
 from ..models.gpt import allreduce_word_embedding_grads, gpt_flops_per_token
@@ -251,6 +252,7 @@ def training_log(loss_dict, total_loss_dict, lr, iteration, loss_scale, report_m
     timers = A.get_timers()
     if iteration % args.log_interval == 0:
         SF.fused_linear_ce_check()  # the fused LM head's declared reduction matched the real one
+        _relay.check_all()          # no TP-pair exchange timed out (outputs would be NaN)
     if getattr(args, "tensorboard_dir", None) and iteration % args.tensorboard_log_interval == 0:
         _tensorboard_log(get_tensorboard_writer(), loss_dict, lr, iteration, loss_scale, grad_norm, args, timers)
     for k, v in loss_dict.items():

@@ -537,3 +537,69 @@ def saved_bytes_worker(rank, world, tp, cfg_over):
     if dist.is_initialized():
         dist.destroy_process_group()
     return loss.detach(), grads, meta, sum(seen.values())
+
+
+def relay_ipc_worker(rank, world, port, outdir):
+    """One rank of the cross-process relay test: 4 processes on cuda:0, TP pairs (0,1) and (2,3),
+    gloo carrying the IPC handles and the reference p2p; the exchanges themselves are the kernel."""
+    import os
+    import pickle
+    import traceback
+
+    import torch
+
+    os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "RANK": str(rank),
+                       "WORLD_SIZE": str(world)})
+    res = {"ok": [], "err": None, "error_word": None}
+    try:
+        import torch.distributed as dist
+        from smdt_amd.comm import relay
+        from smdt_amd.parallel import tensor_parallel as tpl
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        torch.cuda.set_device(0)
+        groups = [dist.new_group([0, 1]), dist.new_group([2, 3])]
+        pg = groups[rank // 2]
+        partner = rank ^ 1
+        eng = relay.XgmiRelay(pg, slot_bytes=1 << 20, sub=2, validate=True)  # checked against p2p
+        res["ok"].append(eng.active)
+        # the run-time speed test runs and reaches one decision on every rank (timings through
+        # gloo's host copies are meaningless here; the decision logic is what is exercised)
+        t = eng.tune(sizes=(64 << 10, 256 << 10), iters=2)
+        res["ok"].append(sorted(t) == [64 << 10, 256 << 10] and eng.active == (eng.min_bytes is not None))
+        eng.active, eng.min_bytes = True, 0
+        # a message of 3 calls (fp32) and a short bf16 one
+        for n, dt in ((3 * world * (1 << 20) // 2 // 4 + 400, torch.float32), (777 * 8, torch.bfloat16)):
+            base = torch.arange(n, device="cuda", dtype=torch.float32) % 113
+            x = (base + 10.0 * rank).to(dt)
+            y = torch.empty_like(x)
+            assert eng.exchange(x, y)
+            torch.cuda.synchronize()
+            res["ok"].append(bool(torch.equal(y, (base + 10.0 * partner).to(dt))))
+        x = torch.full((4096,), float(rank), device="cuda")
+        y = torch.empty_like(x)
+        h = eng.exchange_async(x, y)
+        h.wait()
+        torch.cuda.synchronize()
+        res["ok"].append(bool((y == partner).all()))
+        # the tensor-parallel ring steps routed through the relay
+        relay._ENGINES[id(pg)] = eng
+        me = dist.get_rank(pg)
+        for dt in (torch.float32, torch.bfloat16):
+            mk = lambda r: (torch.arange(8 * 16, device="cuda", dtype=torch.float32).view(8, 16) + 100.0 * r).to(dt)
+            total = tpl.ag_ring(mk(rank), pg)
+            parts = [mk(rank), mk(partner)] if me == 0 else [mk(partner), mk(rank)]
+            torch.cuda.synchronize()
+            res["ok"].append(bool(torch.equal(total, torch.cat(parts))))
+            full = lambda r: (torch.arange(16 * 16, device="cuda", dtype=torch.float32).view(16, 16) % 7 * (r + 1)).to(dt)
+            got = tpl.rs_ring(lambda c: full(rank)[c * 8:(c + 1) * 8].clone(), pg)
+            exp = (full(rank).float() + full(partner).float())[me * 8:(me + 1) * 8].to(dt)
+            torch.cuda.synchronize()
+            res["ok"].append(bool(torch.equal(got, exp)))
+        del relay._ENGINES[id(pg)]
+        res["error_word"] = eng.error()
+        eng.close()
+        dist.destroy_process_group()
+    except Exception:
+        res["err"] = traceback.format_exc()
+    with open(os.path.join(outdir, f"r{rank}.pkl"), "wb") as f:
+        pickle.dump(res, f)
