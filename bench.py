@@ -242,15 +242,16 @@ def main():
         last = train_step()
     if torch.cuda.is_available():
         torch.cuda.synchronize()
-    from smdt_amd.ops import functional as SF
-    SF.fused_linear_ce_check()   # (after the timed region) the fused LM head saw a plain mean
-    relay.check_all()            # (after the timed region) no TP-pair exchange timed out
     if dist.is_initialized():
         dist.barrier()
     el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
     if dist.is_initialized():
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     elapsed = float(el.item())
+    from smdt_amd.comm import xgmi
+    from smdt_amd.ops import functional as SF
+    SF.fused_linear_ce_check()   # (after the timed region) the fused LM head saw a plain mean
+    relay.check_all()            # (after the timed region) no TP-pair exchange timed out
     global_batch = mbs * a.grad_accum * st.dp
     tokens_per_step = global_batch * S
     tps = tokens_per_step * a.steps / elapsed
@@ -289,6 +290,9 @@ def main():
             "baseline": "41 model-TFLOP/s/GPU (reference GPT-2-small, 16xA100, BASELINE.md) at equal model FLOPs",
             "final_loss": loss_val,
         }
+        comm = {**relay.TUNED, **xgmi.TUNED}
+        if comm:  # run-time RCCL-vs-kernel decisions on this node (comm/relay.py, comm/xgmi.py)
+            rec["comm_tuning"] = comm
         print(json.dumps(rec), flush=True)
     if dist.is_initialized():
         dist.destroy_process_group()

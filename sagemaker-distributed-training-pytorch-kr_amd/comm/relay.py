@@ -36,6 +36,7 @@ from .xgmi import _EventHandle
 DEFAULT_SLOT_BYTES = 8 << 20      # per (flow, parity): parts of up to 4 MB -> 32 MB per call on 8 GPUs
 DEFAULT_SUB = 4                   # blocks per part and direction (2 x W x 4 = 64 blocks on 8 GPUs)
 _ENGINES: Dict[int, "XgmiRelay"] = {}
+TUNED: Dict[str, dict] = {}  # run-time RCCL-vs-relay timings (bench JSON)
 
 
 def mode() -> str:
@@ -285,6 +286,9 @@ def create_for_pairs(pair_group, log=print) -> Optional[XgmiRelay]:
         return None
     if m == "auto":
         res = eng.tune()
+        TUNED["tp_pair"] = {f"{nb >> 20}MB": {"rccl_ms": round(a, 3), "relay_ms": round(b, 3)}
+                            for nb, (a, b) in res.items()}
+        TUNED["tp_pair"]["relay_min_bytes"] = eng.min_bytes if eng.active else None
         if dist.get_rank() == 0 and log is not None:
             pretty = ", ".join(f"{nb >> 20} MB: rccl {a:.3f} ms / relay {b:.3f} ms" for nb, (a, b) in res.items())
             log(f"[smdt] TP-pair exchange over all xGMI links: {pretty} -> "

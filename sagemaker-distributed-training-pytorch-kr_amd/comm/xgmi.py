@@ -32,8 +32,9 @@ from __future__ import annotations
 
 import os
 import socket
+import time
 import warnings
-from typing import List, Optional
+from typing import Dict, List, Optional
 
 import torch
 import torch.distributed as dist
@@ -47,12 +48,17 @@ DEFAULT_REGION_BYTES = 64 << 20
 DEFAULT_BLOCKS = 128
 
 _SMDDP_REQUESTED = False
+TUNED: Dict[str, dict] = {}  # run-time RCCL-vs-kernel timings of auto-mode engines (bench JSON)
 
 
 def note_smddp_requested():
     """Called by ``init_distributed`` when a script asked for ``backend="smddp"``."""
     global _SMDDP_REQUESTED
     _SMDDP_REQUESTED = True
+
+
+def explicitly_off() -> bool:
+    return os.environ.get("SMDT_XGMI_ALLREDUCE") == "0"
 
 
 def wanted(group=None) -> bool:
@@ -123,6 +129,8 @@ class XgmiAllReduce:
             raise ValueError(f"xGMI all-reduce supports 2, 4 or 8 ranks, not {self.world}")
         self.region = (int(region_bytes) + 4095) // 4096 * 4096
         self.blocks = int(blocks)
+        # ops this engine takes; ``tune`` turns off the ones RCCL does faster on this node
+        self.use = {"all_reduce": True, "reduce_scatter": True, "all_gather": True}
         self.calls = 0
         self.bytes_moved = 0
         self._stream = None
@@ -194,6 +202,65 @@ class XgmiAllReduce:
         good &= self.error() == 0
         return self._agree(good)
 
+    def tune(self, nbytes: int = 32 << 20, iters: int = 8) -> Dict[str, tuple]:
+        """Time every op against RCCL at ``nbytes`` (bf16) on this group's real links and keep
+        only those where the kernel is faster on every rank. Returns {op: (rccl_ms, xgmi_ms,
+        rccl_busbw_GBps, xgmi_busbw_GBps)} (times: max over ranks)."""
+        W = self.world
+        dev = torch.device("cuda", torch.cuda.current_device())
+        n = max(W * 8, nbytes // 2 // (W * 8) * (W * 8))
+        full = torch.randn(n, device=dev, dtype=torch.bfloat16)
+        part = torch.empty(n // W, device=dev, dtype=torch.bfloat16)
+        out = torch.empty_like(full)
+        g = self.group
+        if dist.get_backend(g) == "gloo":  # multi-process tests on one GPU: host-side reference ops
+            def ref_ar():
+                dist.all_reduce(full.cpu(), group=g)
+
+            def ref_rs():
+                c = full.cpu()
+                dist.all_reduce(c, group=g)
+                part.copy_(c.view(W, -1)[self.rank])
+
+            def ref_ag():
+                lst = [torch.empty(part.shape, dtype=part.dtype) for _ in range(W)]
+                dist.all_gather(lst, part.cpu(), group=g)
+                out.copy_(torch.cat(lst))
+        else:
+            def ref_ar():
+                dist.all_reduce(full, group=g)
+
+            def ref_rs():
+                dist.reduce_scatter_tensor(part, full, group=g)
+
+            def ref_ag():
+                dist.all_gather_into_tensor(out, part, group=g)
+        cases = {
+            "all_reduce": (ref_ar, lambda: self.all_reduce(full), 2.0 * (W - 1) / W),
+            "reduce_scatter": (ref_rs, lambda: self.reduce_scatter(part, full), (W - 1) / W),
+            "all_gather": (ref_ag, lambda: self.all_gather(out, part), (W - 1) / W),
+        }
+        res = {}
+        for op, (ref_fn, our_fn, factor) in cases.items():
+            ts = []
+            for fn in (ref_fn, our_fn):
+                for _ in range(2):
+                    fn()
+                torch.cuda.synchronize()
+                dist.barrier(group=self.group)
+                t0 = time.perf_counter()
+                for _ in range(iters):
+                    fn()
+                torch.cuda.synchronize()
+                t = torch.tensor([(time.perf_counter() - t0) / iters],
+                                 device="cpu" if dist.get_backend(g) == "gloo" else dev)
+                dist.all_reduce(t, op=dist.ReduceOp.MAX, group=g)
+                ts.append(float(t.item()))
+            self.use[op] = ts[1] < ts[0]
+            res[op] = (ts[0] * 1e3, ts[1] * 1e3, n * 2 * factor / ts[0] / 1e9, n * 2 * factor / ts[1] / 1e9)
+        self.check()
+        return res
+
     # ------------------------------------------------------------------ API
     def fits(self, t: torch.Tensor) -> bool:
         return self.active and eligible(t, self.world, self.region)
@@ -207,7 +274,7 @@ class XgmiAllReduce:
     def all_reduce(self, t: torch.Tensor, op: str = "sum") -> bool:
         """In-place all-reduce of ``t`` on the current stream (region-sized pieces); False
         (nothing done) when the tensor is not eligible, so the caller falls back to RCCL."""
-        if not self.fits(t):
+        if not (self.use["all_reduce"] and self.fits(t)):
             return False
         scale = 1.0 / self.world if op == "avg" else 1.0
         flat = t.view(-1)
@@ -222,7 +289,7 @@ class XgmiAllReduce:
         """``dist.reduce_scatter_tensor`` semantics: ``inp`` = W contiguous slices, ``out`` = this
         rank's reduced slice (it may be the input's own slice, in place). False: not eligible."""
         W = self.world
-        if not (self.fits(inp) and out.is_contiguous() and out.dtype == inp.dtype and out.is_cuda
+        if not (self.use["reduce_scatter"] and self.fits(inp) and out.is_contiguous() and out.dtype == inp.dtype and out.is_cuda
                 and inp.numel() == W * out.numel() and out.data_ptr() % 16 == 0):
             return False
         ns = out.numel()
@@ -238,7 +305,7 @@ class XgmiAllReduce:
     def all_gather(self, out: torch.Tensor, inp: torch.Tensor) -> bool:
         """``dist.all_gather_into_tensor`` semantics (``inp`` may be ``out``'s own slice)."""
         W = self.world
-        if not (self.fits(out) and inp.is_contiguous() and inp.dtype == out.dtype and inp.is_cuda
+        if not (self.use["all_gather"] and self.fits(out) and inp.is_contiguous() and inp.dtype == out.dtype and inp.is_cuda
                 and out.numel() == W * inp.numel() and inp.data_ptr() % 16 == 0):
             return False
         ns = inp.numel()
@@ -269,7 +336,7 @@ class XgmiAllReduce:
     def all_reduce_async(self, t: torch.Tensor, op: str = "sum") -> Optional[_EventHandle]:
         """The same on the engine's own stream, ordered after the current stream's work; returns
         a handle whose ``wait()`` makes the current stream wait (None: not eligible)."""
-        if not self.fits(t):
+        if not (self.use["all_reduce"] and self.fits(t)):
             return None
         return self._async(self.all_reduce, [t], t, op)
 
@@ -310,10 +377,16 @@ class XgmiAllReduce:
         self.active = False
 
 
-def create_for_group(group, **kw) -> Optional[XgmiAllReduce]:
-    """Collective over ``group``: an engine when xGMI all-reduce is wanted and possible, else None
-    (with a warning when it was wanted but could not be set up)."""
-    if not (dist.is_initialized() and torch.cuda.is_available() and wanted(group)):
+def create_for_group(group, auto: bool = False, log=print, **kw) -> Optional[XgmiAllReduce]:
+    """Collective over ``group``: an engine when xGMI collectives are wanted and possible, else
+    None (with a warning when wanted but not set up). ``auto`` (the DDP gradient / parameter
+    collectives): when neither ``SMDT_XGMI_ALLREDUCE`` nor the smddp backend decided, build the
+    engine anyway, validate it, time each op against RCCL on this node and keep the ops it wins
+    (rank 0 logs the bus bandwidths); None when it wins none."""
+    if not (dist.is_initialized() and torch.cuda.is_available()):
+        return None
+    explicit = wanted(group)
+    if not explicit and not (auto and not explicitly_off()):
         return None
     if not rccl_backend(group):
         return None
@@ -321,10 +394,28 @@ def create_for_group(group, **kw) -> Optional[XgmiAllReduce]:
     if ws not in (2, 4, 8):
         return None
     try:
-        return XgmiAllReduce(group, **kw)
+        eng = XgmiAllReduce(group, **kw)
     except (RuntimeError, ValueError) as e:
         warnings.warn(f"xGMI all-reduce disabled for this group: {e}")
         return None
+    if explicit:
+        return eng
+    try:
+        res = eng.tune()
+    except RuntimeError as e:
+        warnings.warn(f"xGMI collectives disabled for this group: {e}")
+        eng.close()
+        return None
+    TUNED[f"dp{ws}"] = {op: {"rccl_ms": round(a, 3), "xgmi_ms": round(b, 3), "xgmi": eng.use[op]}
+                        for op, (a, b, _, _) in res.items()}
+    if dist.get_rank() == dist.get_global_rank(group, 0) and log is not None:
+        pretty = ", ".join(f"{op} rccl {a:.2f} ms ({c:.0f} GB/s) / xgmi {b:.2f} ms ({d:.0f} GB/s)"
+                           for op, (a, b, c, d) in res.items())
+        log(f"[smdt] DP group of {ws}: {pretty} -> xGMI kernel for {[k for k, v in eng.use.items() if v] or 'nothing'}")
+    if not any(eng.use.values()):
+        eng.close()
+        return None
+    return eng
 
 
 class XgmiLoopback:

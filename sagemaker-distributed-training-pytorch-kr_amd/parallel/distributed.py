@@ -111,9 +111,10 @@ class DistributedDataParallel(nn.Module):
         rccl = self.dp > 1 and _xgmi.rccl_backend(self.dp_group)
         self.use_avg = average_in_collective and rccl
         # Bucket all-reduces, ZeRO reduce-scatters and parameter all-gathers run on the xGMI IPC
-        # kernel on its own stream (comm/xgmi.py: SMDT_XGMI_ALLREDUCE=1, or a job that asked for
-        # the "smddp" backend); messages larger than its staging region are chunked by the engine.
-        self.xgmi = _xgmi.create_for_group(self.dp_group) if rccl else None
+        # kernel on its own stream (comm/xgmi.py) when SMDT_XGMI_ALLREDUCE=1 / the "smddp"
+        # backend asks for it, or — by default — for each op a run-time timing on this node shows
+        # faster than RCCL (SMDT_XGMI_ALLREDUCE=0: never); larger messages are chunked.
+        self.xgmi = _xgmi.create_for_group(self.dp_group, auto=True) if rccl else None
         self._syncs = 0
 
         params = [p for p in module.parameters() if p.requires_grad]
@@ -319,8 +320,9 @@ class DistributedDataParallel(nn.Module):
                 view.div_(self.dp)
                 b.handle = dist.reduce_scatter_tensor(out, view, group=self.dp_group, async_op=True)
         else:
-            if self.xgmi is not None and self.xgmi.fits(view):
-                b.handle = self.xgmi.all_reduce_async(view, op="avg")
+            h = self.xgmi.all_reduce_async(view, op="avg") if self.xgmi is not None else None
+            if h is not None:
+                b.handle = h
             elif self.use_avg:
                 b.handle = dist.all_reduce(view, op=dist.ReduceOp.AVG, group=self.dp_group, async_op=True)
             else:

@@ -325,6 +325,11 @@ def xgmi_ipc_worker(rank, world, port, outdir):
             torch.cuda.synchronize()
             want_ag = torch.cat([torch.arange(ns, device="cuda", dtype=torch.float32) + 100.0 * r for r in range(world)])
             res["ok"].append(bool(torch.equal(buf, want_ag)))
+        # the auto-mode speed test: every op timed against the (host-side, under gloo) reference,
+        # one decision per op shared by both ranks, results recorded for the bench JSON
+        t = eng.tune(nbytes=1 << 20, iters=2)
+        res["ok"].append(sorted(t) == ["all_gather", "all_reduce", "reduce_scatter"]
+                         and all(isinstance(v, bool) for v in eng.use.values()))
         res["error_word"] = eng.error()
         eng.close()
         dist.destroy_process_group()

@@ -120,7 +120,7 @@ def test_cross_process_ipc_allreduce_world2():
                 out.append(pickle.load(f))
     for r, res in enumerate(out):
         assert res["err"] is None, f"rank {r}:\n{res['err']}"
-        assert res["error_word"] == 0 and all(res["ok"]) and len(res["ok"]) == 17, (r, res)
+        assert res["error_word"] == 0 and all(res["ok"]) and len(res["ok"]) == 18, (r, res)
 
 
 @pytest.mark.gpu
