@@ -48,9 +48,10 @@ constexpr int kRowsPerInst = 1024 / RB;            // 16 rows per 1-KB wave-inst
 constexpr int kNBuf = 4;                           // stage ring: 3 stages in flight
 constexpr int kGroupM = 8;
 
-// Wave layouts of the 256 x 256 tile: NW = 8 waves as 2 (m) x 4 (n), 128 x 64 each (12 fragment
-// reads per 32 MFMAs), or NW = 4 waves as 2 x 2, 128 x 128 each (16 reads per 64 MFMAs, half the
-// LDS traffic and barrier participants; the 256 accumulator registers live in AGPRs).
+// Wave layout of the 256 x 256 tile for linear_fwd_kernel: NW = 8 waves as 2 (m) x 4 (n), 128 x 64
+// each (12 fragment reads per 32 MFMAs). The 4-wave layout (2 x 2 waves of 128 x 128, 16 reads per
+// 64 MFMAs) is linear_fwd_p4_kernel below, software-pipelined because one wave per SIMD has no
+// sibling to hide its LDS latency.
 template <int NW>
 struct Cfg {
   static constexpr int kThreads = 64 * NW;
@@ -312,6 +313,188 @@ __global__ __launch_bounds__(64 * NW, 1) void linear_fwd_kernel(const E* __restr
   wait_vm<0>();  // drain the trailing re-reads (and the last stores) before the LDS is released
 }
 
+
+// 4-wave software-pipelined variant: each wave owns 128 m x 128 n (8 x 8 accumulators of
+// v_mfma_f32_16x16x32, 256 AGPRs; half the LDS fragment bytes per MFMA of the 8-wave layout) and,
+// with one wave per SIMD, hides its own LDS latency: the fragments of stage s + 1 are read while
+// the second half of stage s's MFMAs runs. One barrier per stage sits in the MIDDLE of the stage:
+// it publishes stage s + 1's DMA to every wave and certifies that every wave has consumed stage s's
+// fragments, so the DMA of stage s + 4 is issued into stage s's buffer right after it (four
+// buffers, three stages in flight while one is read). The epilogue stages through its own 16 KB
+// (the ring is busy with the next tile's stages) in 16-row slabs.
+template <int EPI, class E>
+__global__ __launch_bounds__(256, 1) void linear_fwd_p4_kernel(const E* __restrict__ X, const E* __restrict__ W,
+                                                               const E* __restrict__ bias, E* __restrict__ Y,
+                                                               E* __restrict__ H, int M, int N, int K, int ldx,
+                                                               int ldw, int ldy, int ntm, int ntn) {
+  __shared__ __attribute__((aligned(1024))) char L0[2 * SB];
+  __shared__ __attribute__((aligned(1024))) char L1[2 * SB];
+  __shared__ __attribute__((aligned(1024))) char L2[2 * SB];
+  __shared__ __attribute__((aligned(1024))) char L3[2 * SB];
+  constexpr int ERB = 256;  // epilogue LDS row: 128 features x 2 B
+  __shared__ __attribute__((aligned(1024))) char LE[4 * 16 * ERB];
+  constexpr int kInst = SB / 1024 / 4;  // DMA wave-instructions per operand per stage (4)
+  constexpr int kPer = 2 * kInst;
+  const int ntiles = ntm * ntn;
+  const int G = gridDim.x;
+  const int b = blockIdx.x;
+  const int xcd = b & 7, slot = b >> 3, per_xcd = G >> 3;
+  auto logical = [&](int i) { return i * G + xcd * per_xcd + slot; };
+  int my_tiles = 0;
+  while (logical(my_tiles) < ntiles) ++my_tiles;
+  if (my_tiles == 0) return;
+
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 1, wn = wave & 1;  // wave tile: m [128 wm, +128), n [128 wn, +128)
+  using V = v8_t<E>;
+  const int l15 = lane & 15, lq = lane >> 4;
+  const int rdo = lds_off(l15, lq);
+  const int nst = K / BK;  // a multiple of 4: every tile starts at ring position 0
+
+  Glds<kInst> gx, gw;
+  int di = 0, ds = 0;
+  const E* Xb = X;
+  const E* Wb = W;
+  auto set_tile = [&](int i) {
+    int tm, tn;
+    tile_of(logical(i), ntm, ntn, tm, tn);
+    gx.init(wave, lane, ldx, tm * BT, M);
+    gw.init(wave, lane, ldw, tn * BT, N);
+    Xb = X + (int64_t)tm * BT * ldx;
+    Wb = W + (int64_t)tn * BT * ldw;
+  };
+  auto issue_next = [&](char* img) {
+    gx.issue(Xb + ds * BK, img, wave);
+    gw.issue(Wb + ds * BK, img + SB, wave);
+    if (++ds == nst) {
+      if (di + 1 < my_tiles) {
+        ++di;
+        ds = 0;
+        set_tile(di);
+      } else {
+        ds = nst - 1;
+      }
+    }
+  };
+
+  f32x4 acc[8][8];  // [16-feature block ni][16-token block mi]
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  V fa_w[8], fa_x[8], fb_w[8], fb_x[8];  // two fragment sets (stage s, stage s + 1)
+
+  auto load_frags = [&](const char* buf, V (&fw)[8], V (&fx)[8]) {
+#pragma unroll
+    for (int ni = 0; ni < 8; ++ni) fw[ni] = *reinterpret_cast<const V*>(buf + SB + (128 * wn + 16 * ni) * RB + rdo);
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi) fx[mi] = *reinterpret_cast<const V*>(buf + (128 * wm + 16 * mi) * RB + rdo);
+  };
+  auto half = [&](const V (&fw)[8], const V (&fx)[8], int h) {
+#pragma unroll
+    for (int mi = 4 * h; mi < 4 * h + 4; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < 8; ++ni) acc[ni][mi] = mfma16(fw[ni], fx[mi], acc[ni][mi]);  // D[n][m]
+  };
+
+  char* const wreg = LE + wave * (16 * ERB);
+  auto epilogue = [&](int i) {
+    int tm, tn;
+    tile_of(logical(i), ntm, ntn, tm, tn);
+    const int m0 = tm * BT, n0 = tn * BT;
+    float bv[8][4];
+#pragma unroll
+    for (int ni = 0; ni < 8; ++ni) {
+      const int n = n0 + 128 * wn + 16 * ni + 4 * lq;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) bv[ni][e] = 0.f;
+      if constexpr (EPI >= 1) {
+        if (n < N) {
+          const v4_t<E> b4 = *reinterpret_cast<const v4_t<E>*>(bias + n);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) bv[ni][e] = (float)b4[e];
+        }
+      }
+    }
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi) {  // 16-token slabs
+      const int mb = m0 + 128 * wm + 16 * mi, nb = n0 + 128 * wn;
+#pragma unroll
+      for (int pass = 0; pass < (EPI == 2 ? 2 : 1); ++pass) {
+#pragma unroll
+        for (int ni = 0; ni < 8; ++ni) {
+          v4_t<E> v;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float x = acc[ni][mi][e] + bv[ni][e];
+            v[e] = (E)(EPI == 2 && pass == 1 ? gelu_tanh(x) : x);
+          }
+          const int c = 2 * ni + (lq >> 1);  // 16-byte chunk of the 256-byte LDS row l15
+          *reinterpret_cast<v4_t<E>*>(wreg + l15 * ERB + 16 * (c ^ l15) + 8 * (lq & 1)) = v;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        E* __restrict__ out = EPI == 2 && pass == 0 ? H : Y;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {  // 4 rows x 16 chunks per wave-instruction
+          const int row = 4 * q + lane / 16, c = lane % 16;
+          const V v = *reinterpret_cast<const V*>(wreg + row * ERB + 16 * (c ^ row));
+          const int m = mb + row, n = nb + 8 * c;
+          if (m < M && n < N) *reinterpret_cast<V*>(out + (int64_t)m * ldy + n) = v;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int ii = 0; ii < 8; ++ii) acc[j][ii] = f32x4{0.f, 0.f, 0.f, 0.f};
+  };
+  constexpr int kEpiStores = 4 * 8 * (EPI == 2 ? 2 : 1);
+  constexpr int kRelaxedWait = 2 * kPer + kEpiStores < 63 ? 2 * kPer + kEpiStores : 63;
+
+  set_tile(0);
+  issue_next(L0);
+  issue_next(L1);
+  issue_next(L2);
+  issue_next(L3);
+  wait_vm<3 * kPer>();
+  asm volatile("s_barrier" ::: "memory");
+  load_frags(L0, fa_w, fa_x);
+
+  // Step over stage s (fragments in F, buffer cur), next stage's buffer nxt.
+  auto step = [&](char* cur, const char* nxt, V (&Fw)[8], V (&Fx)[8], V (&Gw)[8], V (&Gx)[8], auto relaxed) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // F landed
+    half(Fw, Fx, 0);
+    if constexpr (decltype(relaxed)::value)
+      wait_vm<kRelaxedWait>();
+    else
+      wait_vm<2 * kPer>();  // stage s + 1 landed (s + 2, s + 3 may still be in flight)
+    asm volatile("s_barrier" ::: "memory");
+    issue_next(cur);  // stage s + 4 into the buffer every wave has finished reading
+    load_frags(nxt, Gw, Gx);
+    __builtin_amdgcn_sched_barrier(0);
+    half(Fw, Fx, 1);
+  };
+  using Strict = std::integral_constant<bool, false>;
+  using Relaxed = std::integral_constant<bool, true>;
+  for (int i = 0; i < my_tiles; ++i) {
+    if (i == 0) step(L0, L1, fa_w, fa_x, fb_w, fb_x, Strict{});
+    else step(L0, L1, fa_w, fa_x, fb_w, fb_x, Relaxed{});
+    step(L1, L2, fb_w, fb_x, fa_w, fa_x, Strict{});
+    step(L2, L3, fa_w, fa_x, fb_w, fb_x, Strict{});
+    step(L3, L0, fb_w, fb_x, fa_w, fa_x, Strict{});
+    for (int st = 4; st < nst; st += 4) {
+      step(L0, L1, fa_w, fa_x, fb_w, fb_x, Strict{});
+      step(L1, L2, fb_w, fb_x, fa_w, fa_x, Strict{});
+      step(L2, L3, fa_w, fa_x, fb_w, fb_x, Strict{});
+      step(L3, L0, fb_w, fb_x, fa_w, fa_x, Strict{});
+    }
+    epilogue(i);
+  }
+  wait_vm<0>();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+}
+
 }  // namespace lg
 }  // namespace smdt
 
@@ -353,8 +536,11 @@ extern "C" hipError_t smdt_linear_fwd(int dtype, int epi, const void* x, const v
 #define SMDT_LG1(EP, ET, NW)                                                                                       \
   hipLaunchKernelGGL((lg::linear_fwd_kernel<EP, ET, NW>), grid, dim3(64 * NW), 0, st, (const ET*)x, (const ET*)w,  \
                      (const ET*)bias, (ET*)y, (ET*)h, (int)M, (int)N, (int)K, (int)ldx, (int)ldw, (int)ldy, ntm, ntn)
+#define SMDT_LG4(EP, ET)                                                                                          \
+  hipLaunchKernelGGL((lg::linear_fwd_p4_kernel<EP, ET>), grid, dim3(256), 0, st, (const ET*)x, (const ET*)w,          \
+                     (const ET*)bias, (ET*)y, (ET*)h, (int)M, (int)N, (int)K, (int)ldx, (int)ldw, (int)ldy, ntm, ntn)
 #define SMDT_LG(EP, ET) \
-  do { if (waves == 4) SMDT_LG1(EP, ET, 4); else SMDT_LG1(EP, ET, 8); } while (0)
+  do { if (waves == 4) SMDT_LG4(EP, ET); else SMDT_LG1(EP, ET, 8); } while (0)
   if (dtype == 2) {
     if (epi == 0) SMDT_LG(0, f16); else if (epi == 1) SMDT_LG(1, f16); else SMDT_LG(2, f16);
   } else {
@@ -362,5 +548,6 @@ extern "C" hipError_t smdt_linear_fwd(int dtype, int epi, const void* x, const v
   }
 #undef SMDT_LG
 #undef SMDT_LG1
+#undef SMDT_LG4
   return hipGetLastError();
 }
