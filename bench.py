@@ -23,11 +23,11 @@ Layouts (``--layout``):
   * ``dp`` — DP-N + ZeRO-1 (every GPU holds the whole model).
   ``--tp/--pp`` override either layout.
 
-Scaling is WEAK: every GPU processes ``--seqs-per-gpu`` (32) sequences of 1024 tokens per step
-at every N, so global batch = 32 N. A DP replica (tp x pp GPUs) therefore runs 32 tp pp sequences
-per step: with pp == 1 as one micro-batch (capped at 64 sequences, else gradient accumulation),
-with pp > 1 as micro-batches of 16 — 8 micro-batches at tp2pp2 keep the 1F1B bubble
-(pp - 1) / m at 12.5 %.
+Scaling is WEAK: every GPU processes ``--seqs-per-gpu`` (64) sequences of 1024 tokens per step
+at every N, so global batch = 64 N. A DP replica (tp x pp GPUs) therefore runs 64 tp pp sequences
+per step: with pp == 1 as micro-batches of up to 64 sequences (gradient accumulation beyond),
+with pp > 1 as micro-batches of 16 — 16 micro-batches at tp2pp2 keep the 1F1B bubble
+(pp - 1) / m at 6.25 %.
 """
 from __future__ import annotations
 
@@ -64,10 +64,11 @@ def parse():
     p.add_argument("--tp", type=int, default=None)
     p.add_argument("--pp", type=int, default=None)
     p.add_argument("--sequence-parallel", type=int, default=None, help="default: on when tp > 1")
-    # 32 x 1024 tokens per GPU per step: the 288 GB of HBM holds it without recompute, it measured
-    # +5 % tokens/s over 16 on one MI355X (profiles/r1_mbs/) and halves the gradient bytes
-    # synchronised per token at N > 1.
-    p.add_argument("--seqs-per-gpu", type=int, default=32, help="sequences per GPU per step (weak scaling)")
+    # 64 x 1024 tokens per GPU per step: the 288 GB of HBM holds it without recompute; on one
+    # MI355X it measured +3.2 % tokens/s over 32 (profiles/r2_mbs/; 32 was +5 % over 16), it halves
+    # the gradient / optimizer bytes per token, and at pp = 2 it gives 16 micro-batches per step
+    # (1F1B bubble (pp - 1) / m = 6 %).
+    p.add_argument("--seqs-per-gpu", type=int, default=64, help="sequences per GPU per step (weak scaling)")
     p.add_argument("--micro-batch-size", type=int, default=None)
     p.add_argument("--grad-accum", type=int, default=None, help="micro-batches per step per DP rank")
     p.add_argument("--seq-length", type=int, default=1024)
