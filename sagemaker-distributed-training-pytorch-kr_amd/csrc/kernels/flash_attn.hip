@@ -237,7 +237,8 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void fwd_kernel(const E* __re
   constexpr int kBuf = D == 64 ? 3 : 2;
   __shared__ __attribute__((aligned(16))) char L0[2 * G::TB], L1[2 * G::TB], L2[kBuf == 3 ? 2 * G::TB : 16];
 
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5;
+  const int lane = threadIdx.x & 63, h = lane >> 5;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: diagonal tests branch on SCC
   const int nqb = S / kBlockRows;
   // Heaviest (latest) causal blocks first: they have the most key tiles.
   const int qb = CAUSAL ? (nqb - 1 - (int)(blockIdx.x % nqb)) : (int)(blockIdx.x % nqb);
@@ -458,7 +459,8 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dkdv_kernel(
   constexpr int kBuf = D == 64 ? 3 : 2;
   __shared__ __attribute__((aligned(16))) char L0[BUF], L1[BUF], L2[kBuf == 3 ? BUF : 16];
 
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5;
+  const int lane = threadIdx.x & 63, h = lane >> 5;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: diagonal tests branch on SCC
   const int nkb = S / kBlockRows;
   const int kblk = (int)(blockIdx.x % nkb);  // early key blocks see the most query tiles
   const int bhk = blockIdx.x / nkb;
@@ -665,7 +667,8 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dq_kernel(
   constexpr int kBuf = D == 64 ? 3 : 2;
   __shared__ __attribute__((aligned(16))) char L0[2 * G::TB], L1[2 * G::TB], L2[kBuf == 3 ? 2 * G::TB : 16];
 
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5;
+  const int lane = threadIdx.x & 63, h = lane >> 5;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: diagonal tests branch on SCC
   const int nqb = S / kBlockRows;
   const int qb = CAUSAL ? (nqb - 1 - (int)(blockIdx.x % nqb)) : (int)(blockIdx.x % nqb);
   const int bh = blockIdx.x / nqb;
