@@ -526,6 +526,17 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dkdv_kernel(
   const uint32_t shalf = (uint32_t)S >> 1;
   // even keys keep bytes 0 / 2 of each block word, odd keys bytes 1 / 3; odd keys hash odd slots
   const uint32_t dsel = (my_key & 1) ? 0x07030501u : 0x02060004u;
+  // Causal mask as part of the S accumulator's initial value: a wave's 32 x 32 (query, key) block
+  // is either fully visible, fully masked (skipped) or exactly its diagonal block (qsub == kw),
+  // whose pattern (key > query) is the same for every diagonal block. dgb[i] = -1e30 where this
+  // lane's key follows register i's query, folded in as lse_row + dgb[i] * dflag (dflag = 1 on the
+  // diagonal block, else 0): one FMA per element that replaces the add of the row constant, so
+  // no compare / select runs after the exponential (exp2(-1e30) = 0).
+  float dgb[16];
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) dgb[4 * g + j] = (lane & 31) > 8 * g + 4 * h + j ? -1e30f : 0.f;
   int ch = 0, cq = 0;  // current work item
   auto item = [&](const char* buf, char* pre) {
     const int qb = qstart + cq * kTile;
@@ -545,6 +556,7 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dkdv_kernel(
         // (the rows were prepared by delta_kernel: -(lse log2e - log2 inv) and -delta', so the
         // accumulators start as plain LDS reads)
         f32x16 s, dp;
+        const float dflag = (CAUSAL && qsub == kw) ? 1.f : 0.f;  // wave-uniform
   #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const int r0 = 32 * qs2 + 8 * g + 4 * h;  // 4 consecutive query rows of this group
@@ -552,7 +564,7 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dkdv_kernel(
           const f32x4 dl = *reinterpret_cast<const f32x4*>(del_l + r0);
   #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            s[4 * g + j] = lv[j];
+            s[4 * g + j] = CAUSAL ? fmaf(dgb[4 * g + j], dflag, lv[j]) : lv[j];
             dp[4 * g + j] = DROP ? 0.f : dl[j];  // dropout masks the raw dP (delta' added below)
           }
         }
@@ -561,7 +573,6 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dkdv_kernel(
           s = mfma(fr.rowf(q_l, 32 * qs2, kk), kf[kk], s);
           dp = mfma(fr.rowf(do_l, 32 * qs2, kk), vf[kk], dp);
         }
-        const bool diag = CAUSAL && qsub < kw + 31;
         // dropout: slot m = registers 2m, 2m + 1 (queries 2i, 2i + 1 of one block); dropped
         // entries: P' -> 0 for dV (packed-pair masks), dP -> 0, so dS = p' (keep ? dP : 0) - p' delta'
         uint32_t dm[8];
@@ -578,11 +589,8 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dkdv_kernel(
   #pragma unroll
           for (int j = 0; j < 4; j += 2) {
             const int i = 4 * g + j;
-            float p0 = fexp2(s[i]), p1 = fexp2(s[i + 1]);  // with dropout: p / (1 - p_drop)
-            if (diag) {
-              if (my_key > qb + r0 + j) p0 = 0.f;
-              if (my_key > qb + r0 + j + 1) p1 = 0.f;
-            }
+            // with dropout: p / (1 - p_drop); 0 where the causal mask was folded into s
+            const float p0 = fexp2(s[i]), p1 = fexp2(s[i + 1]);
             float d0 = dp[i], d1 = dp[i + 1];
             if constexpr (DROP) {  // kept: dP - delta'; dropped: -delta'
               if (j == 0) {
