@@ -7,9 +7,9 @@ mkdir -p $R/gpurun_out/attn_ks
 cd /tmp && export TMPDIR=/tmp
 for dp in 0 0.1; do
   timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/attn_ks/d$dp -o run --output-format csv -- \
-    python3 $R/benchmarks/bench_attention.py --sdpa 0 --dropout $dp > $R/gpurun_out/attn_ks/d$dp.log 2>&1
+    python3 $R/benchmarks/bench_attention.py --sdpa 0 --b 32 --h 16 --s 1024 --d 64 --dropout $dp > $R/gpurun_out/attn_ks/d$dp.log 2>&1
   rc=$?
   [ $rc -ne 0 ] && { echo "rc=$rc"; exit $rc; }
   tail -1 $R/gpurun_out/attn_ks/d$dp.log
-  python3 $R/scripts/kstats.py $(ls $R/gpurun_out/attn_ks/d$dp/*kernel_stats.csv | head -1) | grep -E "fa::|fa[0-9]|kernel" | head -6
+  python3 $R/scripts/kstats.py $(ls $R/gpurun_out/attn_ks/d$dp/*kernel_stats.csv | head -1) | head -8
 done
