@@ -22,7 +22,6 @@ The reference's TP collectives are stock NCCL; there is n
 from __future__ import annotations
 
 import os
-import socket
 import time
 import warnings
 from typing import Dict, List, Optional
@@ -31,7 +30,7 @@ import torch
 import torch.distributed as dist
 
 from ..ops import _ext
-from .xgmi import _EventHandle
+from .xgmi import IpcEngine, _EventHandle
 
 DEFAULT_SLOT_BYTES = 8 << 20      # per (flow, parity): parts of up to 4 MB -> 32 MB per call on 8 GPUs
 DEFAULT_SUB = 4                   # blocks per part and direction (2 x W x 4 = 64 blocks on 8 GPUs)
@@ -56,12 +55,11 @@ def eligible(send: torch.Tensor, recv: torch.Tensor) -> bool:
             and nbytes > 0 and nbytes % 16 == 0 and send.data_ptr() % 16 == 0 and recv.data_ptr() % 16 == 0)
 
 
-class XgmiRelay:
+class XgmiRelay(IpcEngine):
     """Pairwise exchange engine for the size-2 ``pair_group`` of every rank (collective over WORLD)."""
 
     def __init__(self, pair_group, slot_bytes: int = DEFAULT_SLOT_BYTES, sub: int = DEFAULT_SUB,
                  validate: bool = True):
-        self.C = _ext.ext()
         self.group = pair_group
         self.world = dist.get_world_size()
         self.rank = dist.get_rank()
@@ -75,60 +73,23 @@ class XgmiRelay:
         self.min_bytes = 0
         self.calls = 0
         self._stream = None
-        self._opened: List[int] = []
-        self._stage = self._sig = None
+        self._sig = None
         self.active = False
-        mine_pair = [r for r in dist.get_process_group_ranks(pair_group) if r != self.rank][0]
-        info = [None] * self.world
-        dist.all_gather_object(info, (socket.gethostname(), mine_pair))
-        if len({h for h, _ in info}) != 1:
-            raise RuntimeError("xGMI relay needs every rank on one node")
-        self.partners = [p for _, p in info]
+        self.partner = [r for r in dist.get_process_group_ranks(pair_group) if r != self.rank][0]
+        partners = [None] * self.world
+        dist.all_gather_object(partners, self.partner)
+        self.partners = [int(p) for p in partners]
         if any(self.partners[p] != r for r, p in enumerate(self.partners)):
             raise RuntimeError(f"xGMI relay: pair groups are not symmetric: {self.partners}")
-        self.partner = mine_pair
-        err = None
-        try:
-            self._stage = self.C.ipc_malloc(self.world * 2 * self.slot, False)
-            self._sig = self.C.ipc_malloc(self.C.relay_signal_bytes(), True)
-            mine = (self.C.ipc_get_handle(self._stage), self.C.ipc_get_handle(self._sig))
-        except RuntimeError as e:
-            err, mine = e, None
-        handles = [None] * self.world
-        dist.all_gather_object(handles, mine)
-        self.stage_ptrs: List[int] = []
-        self.sig_ptrs: List[int] = []
-        if err is None and all(h is not None for h in handles):
-            try:
-                for r, (hd, hs) in enumerate(handles):
-                    if r == self.rank:
-                        self.stage_ptrs.append(self._stage)
-                        self.sig_ptrs.append(self._sig)
-                    else:
-                        pd = self.C.ipc_open(hd)
-                        self._opened.append(pd)
-                        ps_ = self.C.ipc_open(hs)
-                        self._opened.append(ps_)
-                        self.stage_ptrs.append(pd)
-                        self.sig_ptrs.append(ps_)
-            except RuntimeError as e:
-                err = e
-        if not self._agree(err is None):
-            self.close()
-            raise RuntimeError(f"xGMI relay setup failed on some rank ({err!r} here)")
+        self.stage_ptrs, self.sig_ptrs = self._setup_ipc(None, [(self.world * 2 * self.slot, False),
+                                                                (_ext.ext().relay_signal_bytes(), True)])
+        self._sig = self.sig_ptrs[self.rank]
         self.active = True
         if validate and not self._validate():
             self.close()
             raise RuntimeError("xGMI relay failed its validation against RCCL p2p")
 
     # ------------------------------------------------------------------ helpers
-    def _agree(self, ok: bool) -> bool:
-        on_host = dist.get_backend() == "gloo"
-        dev = torch.device("cpu") if on_host else torch.device("cuda", torch.cuda.current_device())
-        flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
-        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
-        return bool(flag.item())
-
     def _rccl_exchange(self, send, recv):
         """The reference exchange: RCCL p2p (gloo test groups: through host copies)."""
         host = dist.get_backend(self.group) == "gloo"
@@ -242,22 +203,8 @@ class XgmiRelay:
 
     def close(self):
         """Collective over WORLD: unmap the peers' buffers, then free this rank's own."""
-        if torch.cuda.is_available():
-            torch.cuda.synchronize()
-        if dist.is_initialized():
-            dist.barrier()
-        for p in self._opened:
-            try:
-                self.C.ipc_close(p)
-            except RuntimeError:  # pragma: no cover
-                pass
-        self._opened = []
-        if dist.is_initialized():
-            dist.barrier()
-        for p in (self._stage, self._sig):
-            if p is not None:
-                self.C.ipc_free(p)
-        self._stage = self._sig = None
+        self._close_ipc()
+        self._sig = None
         self.active = False
         for k, v in list(_ENGINES.items()):
             if v is self:

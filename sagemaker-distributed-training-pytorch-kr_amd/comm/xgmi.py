@@ -116,12 +116,81 @@ class _EventHandle:
         return self.event.query()
 
 
-class XgmiAllReduce:
+class IpcEngine:
+    """Shared plumbing of the xGMI engines: every rank of ``group`` (None = WORLD) allocates its
+    buffers (``specs`` = [(bytes, uncached)]), exports them with hipIpcGetMemHandle and maps every
+    peer's; ``ptrs[i][r]`` is buffer i of rank r as seen from this process. Construction and
+    ``close`` are collective over the group, and every rank reaches the same verdict."""
+
+    def _setup_ipc(self, group, specs):
+        self.C = _ext.ext()
+        self._ipc_group = group
+        self._own: List[int] = []
+        self._opened: List[int] = []
+        rank, world = dist.get_rank(group), dist.get_world_size(group)
+        hosts = [None] * world
+        dist.all_gather_object(hosts, socket.gethostname(), group=group)
+        if len(set(hosts)) != 1:
+            raise RuntimeError(f"xGMI engines need every rank of the group on one node, got {sorted(set(hosts))}")
+        err = None
+        try:
+            for nbytes, uncached in specs:
+                self._own.append(self.C.ipc_malloc(int(nbytes), bool(uncached)))
+            mine = tuple(self.C.ipc_get_handle(p) for p in self._own)
+        except RuntimeError as e:  # still take part in the collectives below
+            err, mine = e, None
+        handles = [None] * world
+        dist.all_gather_object(handles, mine, group=group)
+        ptrs: List[List[int]] = [[] for _ in specs]
+        if err is None and all(h is not None for h in handles):
+            try:
+                for r, hs in enumerate(handles):
+                    for i, h in enumerate(hs):
+                        if r == rank:
+                            ptrs[i].append(self._own[i])
+                        else:
+                            p = self.C.ipc_open(h)
+                            self._opened.append(p)
+                            ptrs[i].append(p)
+            except RuntimeError as e:
+                err = e
+        if not self._agree(err is None):
+            self._close_ipc()
+            raise RuntimeError(f"xGMI IPC setup failed on some rank ({err!r} here)")
+        return ptrs
+
+    def _agree(self, ok: bool) -> bool:
+        # gloo groups (multi-process tests on one GPU) agree on the host; RCCL on the device
+        on_host = dist.get_backend(self._ipc_group) == "gloo"
+        dev = torch.device("cpu") if on_host else torch.device("cuda", torch.cuda.current_device())
+        flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self._ipc_group)
+        return bool(flag.item())
+
+    def _close_ipc(self):
+        """Collective: unmap the peers' buffers, then free this rank's own."""
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+        if dist.is_initialized():
+            dist.barrier(group=self._ipc_group)
+        for p in self._opened:
+            try:
+                self.C.ipc_close(p)
+            except RuntimeError:  # pragma: no cover
+                pass
+        self._opened = []
+        if dist.is_initialized():
+            dist.barrier(group=self._ipc_group)
+        for p in self._own:
+            self.C.ipc_free(p)
+        self._own = []
+
+
+class XgmiAllReduce(IpcEngine):
     """All-reduce engine for one process group whose ranks share a node (one GPU per rank)."""
 
     def __init__(self, group=None, region_bytes: int = DEFAULT_REGION_BYTES, blocks: int = DEFAULT_BLOCKS,
                  validate: bool = True):
-        self.C = _ext.ext()
         self.group = group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
@@ -134,57 +203,17 @@ class XgmiAllReduce:
         self.calls = 0
         self.bytes_moved = 0
         self._stream = None
-        self._opened: List[int] = []
-        self._data = self._sig = None
         self.active = False
-        hosts = [None] * self.world
-        dist.all_gather_object(hosts, socket.gethostname(), group=group)
-        if len(set(hosts)) != 1:
-            raise RuntimeError(f"xGMI all-reduce needs every rank of the group on one node, got {sorted(set(hosts))}")
-        err = None
-        try:
-            self._data = self.C.ipc_malloc(4 * self.region, False)
-            self._sig = self.C.ipc_malloc(self.C.ar_signal_bytes(), True)
-            mine = (self.C.ipc_get_handle(self._data), self.C.ipc_get_handle(self._sig))
-        except RuntimeError as e:  # still take part in the collectives below
-            err, mine = e, None
-        handles = [None] * self.world
-        dist.all_gather_object(handles, mine, group=group)
-        self.data_ptrs: List[int] = []
-        self.sig_ptrs: List[int] = []
-        if err is None and all(h is not None for h in handles):
-            try:
-                for r, (hd, hs) in enumerate(handles):
-                    if r == self.rank:
-                        self.data_ptrs.append(self._data)
-                        self.sig_ptrs.append(self._sig)
-                    else:
-                        pd = self.C.ipc_open(hd)
-                        self._opened.append(pd)
-                        ps_ = self.C.ipc_open(hs)
-                        self._opened.append(ps_)
-                        self.data_ptrs.append(pd)
-                        self.sig_ptrs.append(ps_)
-            except RuntimeError as e:
-                err = e
-        ok = self._agree(err is None)
-        if not ok:
-            self.close()
-            raise RuntimeError(f"xGMI all-reduce setup failed on some rank ({err!r} here)")
+        self._sig = None
+        self.data_ptrs, self.sig_ptrs = self._setup_ipc(group, [(4 * self.region, False),
+                                                                (_ext.ext().ar_signal_bytes(), True)])
+        self._sig = self.sig_ptrs[self.rank]
         self.active = True
         if validate and not self._validate():
             self.close()
             raise RuntimeError("xGMI all-reduce failed its validation against RCCL")
 
     # ------------------------------------------------------------------ helpers
-    def _agree(self, ok: bool) -> bool:
-        # gloo groups (multi-process tests on one GPU) agree on the host; RCCL on the device
-        on_host = dist.get_backend(self.group) == "gloo"
-        dev = torch.device("cpu") if on_host else torch.device("cuda", torch.cuda.current_device())
-        flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
-        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.group)
-        return bool(flag.item())
-
     def _validate(self) -> bool:
         """Exact check against RCCL on integer-valued fp32 data (order-independent sums), one
         one-shot and one two-shot size, run twice so both buffer halves are exercised."""
@@ -357,23 +386,9 @@ class XgmiAllReduce:
             raise RuntimeError(f"xGMI all-reduce: a peer did not arrive (error word {e}); outputs were NaN-filled")
 
     def close(self):
-        """Collective: unmap the peers' buffers, then free this rank's own."""
-        if torch.cuda.is_available():
-            torch.cuda.synchronize()
-        if dist.is_initialized():
-            dist.barrier(group=self.group)
-        for p in self._opened:
-            try:
-                self.C.ipc_close(p)
-            except RuntimeError:  # pragma: no cover
-                pass
-        self._opened = []
-        if dist.is_initialized():
-            dist.barrier(group=self.group)
-        for p in (self._data, self._sig):
-            if p is not None:
-                self.C.ipc_free(p)
-        self._data = self._sig = None
+        """Collective over the group: unmap the peers' buffers, then free this rank's own."""
+        self._close_ipc()
+        self._sig = None
         self.active = False
 
 
