@@ -608,3 +608,80 @@ def relay_ipc_worker(rank, world, port, outdir):
         res["err"] = traceback.format_exc()
     with open(os.path.join(outdir, f"r{rank}.pkl"), "wb") as f:
         pickle.dump(res, f)
+
+
+def relay_tp_mlp_worker(rank, world, port, outdir):
+    """One rank of the relay-backed tensor-parallel MLP test: 4 processes on cuda:0, TP pairs
+    (0,1) (2,3) with sequence parallelism; every TP ring exchange (forward all-gather /
+    reduce-scatter, backward reduce-scatter / all-gather) goes through the xGMI relay kernel over
+    HIP-IPC mappings. Each rank checks its output / gradient shards against an fp32 reference of
+    the full MLP computed in-process."""
+    import os
+    import pickle
+    import traceback
+
+    import torch
+
+    os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "RANK": str(rank),
+                       "WORLD_SIZE": str(world)})
+    res = {"err": None, "rel": {}, "calls": 0, "error_word": None}
+    try:
+        import torch.distributed as dist
+        import torch.nn.functional as F
+        from smdt_amd.comm import relay
+        from smdt_amd.parallel import state as ps
+        from smdt_amd.parallel import tensor_parallel as tpl
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        torch.cuda.set_device(0)
+        st = ps.initialize_model_parallel(2)
+        eng = relay.XgmiRelay(st.tp_group, slot_bytes=1 << 20, sub=2)
+        relay._ENGINES[id(st.tp_group)] = eng
+        h, ffn, s, b = 256, 1024, 128, 4
+        dev = torch.device("cuda", 0)
+        fc1 = tpl.ColumnParallelLinear(h, ffn, bias=True, key="fc1", params_dtype=torch.bfloat16, device=dev,
+                                       sequence_parallel=True)
+        fc2 = tpl.RowParallelLinear(ffn, h, bias=False, key="fc2", params_dtype=torch.bfloat16, device=dev,
+                                    sequence_parallel=True)
+        with torch.no_grad():
+            fc1.bias.copy_(torch.linspace(-0.5, 0.5, ffn, device=dev)[st.tp_rank * (ffn // 2):][: ffn // 2])
+        w1 = tpl.init_full_then_shard((ffn, h), 0.02, "fc1.weight", 1234, torch.float32, dev, None, 0, 1)
+        w2 = tpl.init_full_then_shard((h, ffn), 0.02, "fc2.weight", 1234, torch.float32, dev, None, 0, 1)
+        w1 = w1.to(torch.bfloat16).float().requires_grad_(True)
+        w2 = w2.to(torch.bfloat16).float().requires_grad_(True)
+        b1 = torch.linspace(-0.5, 0.5, ffn, device=dev).to(torch.bfloat16).float().requires_grad_(True)
+        g = torch.Generator(device=dev)
+        g.manual_seed(100 + rank // 2)  # one input per TP pair
+        x_full = torch.randn(s, b, h, device=dev, generator=g).to(torch.bfloat16)
+        gy_full = torch.randn(s, b, h, device=dev, generator=g)
+        lo, hi = st.tp_rank * (s // 2), (st.tp_rank + 1) * (s // 2)
+        for it in range(2):  # two iterations: both slot parities and the freed-slot handshake
+            x = x_full[lo:hi].clone().requires_grad_(True)
+            y = fc2(F.gelu(fc1(x), approximate="tanh"))
+            (y.float() * gy_full[lo:hi]).sum().backward()
+            tpl.DEFERRED_WGRAD.flush()
+            torch.cuda.synchronize()
+            xr = x_full.float().requires_grad_(True)
+            for t in (w1, w2, b1):
+                t.grad = None
+            yr = F.linear(F.gelu(F.linear(xr, w1, b1), approximate="tanh"), w2)
+            (yr * gy_full).sum().backward()
+
+            def rel(a, r):
+                return float((a.float() - r).norm() / (r.norm() + 1e-12))
+            f0, f1 = st.tp_rank * (ffn // 2), (st.tp_rank + 1) * (ffn // 2)
+            res["rel"][f"y{it}"] = rel(y, yr[lo:hi].detach())
+            res["rel"][f"dx{it}"] = rel(x.grad, xr.grad[lo:hi])
+            res["rel"][f"dw1_{it}"] = rel(fc1.weight.grad, w1.grad[f0:f1])
+            res["rel"][f"db1_{it}"] = rel(fc1.bias.grad, b1.grad[f0:f1])
+            res["rel"][f"dw2_{it}"] = rel(fc2.weight.grad, w2.grad[:, f0:f1])
+            for p in (fc1.weight, fc1.bias, fc2.weight):
+                p.grad = None
+        res["calls"] = eng.calls
+        res["error_word"] = eng.error()
+        del relay._ENGINES[id(st.tp_group)]
+        eng.close()
+        dist.destroy_process_group()
+    except Exception:
+        res["err"] = traceback.format_exc()
+    with open(os.path.join(outdir, f"r{rank}.pkl"), "wb") as f:
+        pickle.dump(res, f)
