@@ -48,13 +48,13 @@ __global__ __launch_bounds__(256) void bias_act_fwd_kernel(const T* __restrict__
     cvt_raw8<T>(rx, v);
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[j] = act_fwd<ACT>(v[j] + b[j]);
-    store_vec<T, 8>(y + r * N + ch * 8, v);
+    store_vec<T, 8>(y + r * N + ch * 8, v);  // plain store: fc2's GEMM reads y right after
   };
   int64_t r = r0;
   for (; r + kRows <= r1; r += kRows) {
     Raw8<T> rx[kRows];
 #pragma unroll
-    for (int u = 0; u < kRows; ++u) rx[u] = load_raw8(x + (r + u) * N + ch * 8);
+    for (int u = 0; u < kRows; ++u) rx[u] = load_raw8_nt(x + (r + u) * N + ch * 8);
 #pragma unroll
     for (int u = 0; u < kRows; ++u) row_op(r + u, rx[u]);
   }
@@ -89,15 +89,16 @@ __global__ __launch_bounds__(256) void bias_act_bwd_kernel(const T* __restrict__
       v[j] = d;
       acc[j] += to_f32(from_f32<T>(d));
     }
-    store_vec<T, 8>(dx + r * N + ch * 8, v);
+    if constexpr (sizeof(T) == 2) store_vec8_nt<T>(dx + r * N + ch * 8, v);
+    else store_vec<T, 8>(dx + r * N + ch * 8, v);
   };
   int64_t r = r0;
   for (; r + kRows <= r1; r += kRows) {
     Raw8<T> rx[kRows], rg[kRows];
 #pragma unroll
     for (int u = 0; u < kRows; ++u) {
-      rx[u] = load_raw8(x + (r + u) * N + ch * 8);
-      rg[u] = load_raw8(dy + (r + u) * N + ch * 8);
+      rx[u] = load_raw8_nt(x + (r + u) * N + ch * 8);
+      rg[u] = load_raw8_nt(dy + (r + u) * N + ch * 8);
     }
 #pragma unroll
     for (int u = 0; u < kRows; ++u) row_op(r + u, rx[u], rg[u]);
@@ -177,7 +178,7 @@ __global__ __launch_bounds__(256) void col_sum_rows_kernel(const T* __restrict__
   for (; r + kRows <= r1; r += kRows) {  // kRows loads in flight, rows still summed in order
     Raw8<T> raw[kRows];
 #pragma unroll
-    for (int u = 0; u < kRows; ++u) raw[u] = load_raw8(x + (r + u) * N + c);
+    for (int u = 0; u < kRows; ++u) raw[u] = load_raw8_nt(x + (r + u) * N + c);
 #pragma unroll
     for (int u = 0; u < kRows; ++u) add_row(raw[u]);
   }

@@ -34,7 +34,7 @@ __global__ __launch_bounds__(256) void ce_stats_kernel(const T* __restrict__ log
   const int nvec = (Vvalid + VE - 1) / VE;  // vectors holding >= 1 real column (V % 8 == 0)
   for (int i = threadIdx.x; i < nvec; i += 256) {
     float v[VE];
-    load_vec<T, VE>(lr + i * VE, v);
+    load_vec<T, VE, true>(lr + i * VE, v);  // logits stream once
     if ((i + 1) * VE > Vvalid) {
 #pragma unroll
       for (int j = 0; j < VE; ++j)
@@ -107,7 +107,7 @@ __global__ __launch_bounds__(256) void ce_bwd_kernel(const T* __restrict__ logit
   const int nvec = V / VE;
   for (int i = threadIdx.x; i < nvec; i += 256) {
     float v[VE];
-    load_vec<T, VE>(lr + i * VE, v);
+    load_vec<T, VE, true>(lr + i * VE, v);  // logits stream once
 #pragma unroll
     for (int j = 0; j < VE; ++j) {
       float p = i * VE + j < Vvalid ? __expf(v[j] - M) * inv : 0.f;

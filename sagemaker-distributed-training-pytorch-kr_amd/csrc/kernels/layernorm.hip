@@ -137,7 +137,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(LnFwdArgs a) {
     for (int c = 0; c < C; ++c) {
       int ch = c * G + tid_in_group;
       if (ch < nchunk) {
-        load_vec<T, 8>(xr + ch * 8, v[c]);
+        load_vec<T, 8, true>(xr + ch * 8, v[c]);  // streamed once: nontemporal
         if (has_bias)
           for (int j = 0; j < 8; ++j) v[c][j] += bi[c][j];
         if (drop) {
@@ -147,7 +147,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(LnFwdArgs a) {
         }
         if (has_res) {
           float r[8];
-          load_vec<T, 8>((const T*)a.res + row * H + ch * 8, r);
+          load_vec<T, 8, true>((const T*)a.res + row * H + ch * 8, r);
           for (int j = 0; j < 8; ++j) v[c][j] += r[j];
         }
         if (write_s) {
@@ -242,9 +242,9 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(LnBwdArgs a) {
     for (int c = 0; c < C; ++c) {
       const int ch = c * G + tid_in_group;
       if (ch < nchunk) {
-        ns[c] = load_raw8(sp + r * H + ch * 8);
-        ndy[c] = load_raw8(dyp + r * H + ch * 8);
-        if (has_dsin) ndi[c] = load_raw8(dip + r * H + ch * 8);
+        ns[c] = load_raw8_nt(sp + r * H + ch * 8);  // streamed once: nontemporal
+        ndy[c] = load_raw8_nt(dyp + r * H + ch * 8);
+        if (has_dsin) ndi[c] = load_raw8_nt(dip + r * H + ch * 8);
       }
     }
     nmu = a.rms ? 0.f : a.mean[r];

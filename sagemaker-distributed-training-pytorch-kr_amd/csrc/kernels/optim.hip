@@ -41,10 +41,11 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
   const float rbc2 = rsqrtf(a.bc2);
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nvec;
        i += (int64_t)gridDim.x * 256) {
-    f32x4 p = reinterpret_cast<f32x4*>(a.master)[i];
-    f32x4 g = reinterpret_cast<const f32x4*>(a.grad)[i];
-    f32x4 m = reinterpret_cast<f32x4*>(a.exp_avg)[i];
-    f32x4 v = reinterpret_cast<f32x4*>(a.exp_avg_sq)[i];
+    // every state word is touched once per step: nontemporal loads
+    f32x4 p = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(a.master) + i);
+    f32x4 g = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(a.grad) + i);
+    f32x4 m = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(a.exp_avg) + i);
+    f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(a.exp_avg_sq) + i);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       float gj = g[j] * gm;
