@@ -130,15 +130,16 @@ __device__ __forceinline__ uint32_t half_masks(uint32_t t) {
 // Packed-pair masks of slot 2u (bits 7 / 23) and slot 2u + 1 (bits 15 / 31).
 __device__ __forceinline__ uint32_t mask_even_slot(uint32_t t) { return half_masks(t << 8); }
 __device__ __forceinline__ uint32_t mask_odd_slot(uint32_t t) { return half_masks(t); }
-// x if keep bit b of t is set, else 0: v_bfe_i32 (all-ones / zero) + v_and. Only the bfe is asm (left
-// to itself the compiler turns the sign-extend into test + compare + select); x comes straight out
-// of an MFMA and must be read by a compiler-visible instruction (inline asm reading an MFMA result
-// is not covered by the hazard padding).
+// keep bit b of t ? x : y with x, y fp32: v_bfe_i32 (all-ones / zero; only the bfe is asm, left to
+// itself the compiler turns the sign-extend into test + compare + select) and a compiler-visible
+// (x & m) | (y & ~m), which the backend selects as ONE v_bfi_b32. x comes straight out of an MFMA
+// and must be read by a compiler-emitted instruction (inline asm reading an MFMA result is not
+// covered by the hazard padding).
 template <int b>
-__device__ __forceinline__ float and_bit(float x, uint32_t t) {
+__device__ __forceinline__ float sel_bit(float x, float y, uint32_t t) {
   int32_t m;
   asm("v_bfe_i32 %0, %1, %2, 1" : "=v"(m) : "v"(t), "n"(b));
-  return __int_as_float(__float_as_int(x) & m);
+  return __int_as_float((__float_as_int(x) & m) | (__float_as_int(y) & ~m));
 }
 // AND the four packed pairs of a 16-bit operand fragment with their masks.
 template <class V>
@@ -565,7 +566,7 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dkdv_kernel(
   #pragma unroll
           for (int j = 0; j < 4; ++j) {
             s[4 * g + j] = CAUSAL ? fmaf(dgb[4 * g + j], dflag, lv[j]) : lv[j];
-            dp[4 * g + j] = DROP ? 0.f : dl[j];  // dropout masks the raw dP (delta' added below)
+            dp[4 * g + j] = dl[j];  // dP' = dP - delta' (dropped entries select -delta' below)
           }
         }
   #pragma unroll
@@ -594,11 +595,11 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dkdv_kernel(
             float d0 = dp[i], d1 = dp[i + 1];
             if constexpr (DROP) {  // kept: dP - delta'; dropped: -delta'
               if (j == 0) {
-                d0 = and_bit<7>(d0, t) + ndl[j];
-                d1 = and_bit<23>(d1, t) + ndl[j + 1];
+                d0 = sel_bit<7>(d0, ndl[j], t);
+                d1 = sel_bit<23>(d1, ndl[j + 1], t);
               } else {
-                d0 = and_bit<15>(d0, t) + ndl[j];
-                d1 = and_bit<31>(d1, t) + ndl[j + 1];
+                d0 = sel_bit<15>(d0, ndl[j], t);
+                d1 = sel_bit<31>(d1, ndl[j + 1], t);
               }
             }
             s[i] = p0;
@@ -696,7 +697,7 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dq_kernel(
   // initial accumulators, register-resident for the whole loop (no per-subtile splat).
   const float nlse2 = LSE[((int64_t)b * H + hq) * S + my_q];
   const float ndl = DELTA[((int64_t)b * H + hq) * S + my_q];
-  const f32x16 st0 = splat16(nlse2), dp0 = splat16(DROP ? 0.f : ndl);  // dropout masks the raw dP
+  const f32x16 st0 = splat16(nlse2), dp0 = splat16(ndl);  // dP' = dP - delta' (dropout selects below)
   const float c2 = scale * kLog2e;
   const uint32_t dkey = DROP ? drop_key(drop, bh) : 0u;
   const uint32_t dblk = (uint32_t)(my_q >> 1) * ((uint32_t)S >> 1) + 2u * h + (uint32_t)(my_q & 1);
@@ -758,11 +759,11 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dq_kernel(
         if constexpr (DROP) {  // kept: dP - delta'; dropped: dS = p' (0 - delta')
           const uint32_t t = tb[i >> 2];
           if ((i & 2) == 0) {
-            d0 = and_bit<7>(d0, t) + ndl;
-            d1 = and_bit<23>(d1, t) + ndl;
+            d0 = sel_bit<7>(d0, ndl, t);
+            d1 = sel_bit<23>(d1, ndl, t);
           } else {
-            d0 = and_bit<15>(d0, t) + ndl;
-            d1 = and_bit<31>(d1, t) + ndl;
+            d0 = sel_bit<15>(d0, ndl, t);
+            d1 = sel_bit<31>(d1, ndl, t);
           }
         }
         dpt[i] = p0 * d0;  // dS^T
