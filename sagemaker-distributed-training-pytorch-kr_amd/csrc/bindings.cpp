@@ -274,6 +274,18 @@ void cast_(Tensor x, Tensor y, bool accumulate) {
         "cast");
 }
 
+// ------------------------------------------------------------------ 2-D transpose (16-bit)
+// out [C, R] = x [R, C]^T, contiguous (feeds the dgrad GEMMs in the TN layout).
+Tensor transpose2d(Tensor x) {
+  need_contig(x, "x");
+  TORCH_CHECK(x.dim() == 2, "transpose2d: x must be 2-D");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kHalf, "transpose2d: bf16 / fp16 only");
+  TORCH_CHECK(x.size(0) % 8 == 0 && x.size(1) % 8 == 0, "transpose2d: both dims must be multiples of 8");
+  auto out = torch::empty({x.size(1), x.size(0)}, x.options());
+  check(smdt_transpose16(x.data_ptr(), out.data_ptr(), x.size(0), x.size(1), cur_stream()), "transpose2d");
+  return out;
+}
+
 // ------------------------------------------------------------------ RoPE
 // x: [ntok, nh, d] strided view (last dim contiguous), rotary applied in place to the first
 // `rot` elements of each head.
@@ -667,6 +679,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("scale_", &scale_);
   m.def("cast_", &cast_);
   m.def("rope_", &rope_);
+  m.def("transpose2d", &transpose2d);
   m.def("bias_grad", &bias_grad);
   m.def("wgrad_mfma", &wgrad_mfma, arg("main_grad"), arg("dy"), arg("x"), arg("max_splits") = 0);
   m.def("wgrad_grouped", &wgrad_grouped, arg("main_grads"), arg("dys"), arg("xs"));

@@ -67,6 +67,9 @@ hipError_t smdt_rope(int dtype, void* x, int64_t ntok, int nh, int64_t tok_strid
                      int64_t head_stride, int rot, const float* cos_t, const float* sin_t,
                      int pos_div, int pos_mod, int backward, hipStream_t st);
 
+// transpose.hip
+hipError_t smdt_transpose16(const void* in, void* out, int64_t R, int64_t C, hipStream_t st);
+
 // cross_entropy.hip
 hipError_t smdt_ce_stats(int dtype, const void* logits, const int64_t* target, int64_t rows,
                          int V, int Vvalid, int64_t vstart, float* row_max, float* row_sumexp,

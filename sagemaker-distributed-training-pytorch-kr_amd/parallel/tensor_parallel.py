@@ -349,6 +349,39 @@ def _wgrad(weight, g2, t2):
     return None
 
 
+# dgrad layout: dX = dY W with W [out, in] row-major is hipBLASLt's "NN" GEMM on this ROCm build,
+# 14-24 % slower than the "TN" GEMM the forward runs in (F.linear, W^T read K-contiguous). A
+# contiguous W^T made by the LDS tile-transpose kernel (ops: transpose2d, ~25 us per GPT-2 345M
+# layer) turns every dgrad into F.linear(dY, W^T): 42.5 -> 37.4 ms of dgrad per step at 64 x 1024
+# tokens (benchmarks/bench_dgrad.py, profiles/r2_dgrad_tn/). The copy is made per backward call
+# (no cache to invalidate when the optimizer or a checkpoint load rewrites the weight).
+_DGRAD_TN = os.environ.get("SMDT_DGRAD_TN", "1") == "1"
+
+
+def _dgrad_weight_t(weight):
+    """W^T [in, out] contiguous for the TN dgrad, or None to use dY @ W directly."""
+    if (_DGRAD_TN and weight.is_cuda and weight.dim() == 2 and weight.is_contiguous()
+            and weight.dtype in (torch.bfloat16, torch.float16)
+            and weight.shape[0] % 8 == 0 and weight.shape[1] % 8 == 0 and _ext.available()):
+        return _ext.ext().transpose2d(weight)
+    return None
+
+
+def dgrad(g, weight, wt=None):
+    """dX = g @ weight (g [..., out], weight [out, in]); ``wt`` = weight^T from _dgrad_weight_t."""
+    if wt is None:
+        return g.matmul(weight)
+    return F.linear(g, wt)
+
+
+def dgrad_into(dst, g, weight, wt=None):
+    """dst[...] = g @ weight written in place."""
+    if wt is None:
+        torch.matmul(g, weight, out=dst)
+    else:
+        _mm_into(dst, g, wt)
+
+
 class LinearWithGradAccumulationAndAsyncCommunication(torch.autograd.Function):
     """y = x W^T (+ b) with Megatron's backward schedule:
 
@@ -374,7 +407,7 @@ class LinearWithGradAccumulationAndAsyncCommunication(torch.autograd.Function):
         tp = dist.get_world_size(group) if group is not None else 1
         total = _gather_dim0(x, group) if (ctx.sp and tp > 1) else x
         g = g.contiguous()
-        gi = g.matmul(weight)
+        gi = dgrad(g, weight, _dgrad_weight_t(weight))
         handle = None
         if ctx.sp and tp > 1:
             gi_out, handle = _reduce_scatter_dim0(gi, group, async_op=True)
@@ -528,7 +561,8 @@ class _ColumnSPLinear(torch.autograd.Function):
             res["dw"] = _wgrad(weight, g2, total.reshape(-1, total.shape[-1]))
             res["db"] = _bias_grad(ctx.bias_p, g2)
             _flush_wgrad()
-        gi = rs_ring(lambda c: g[c * n:(c + 1) * n].matmul(weight), group, wgrad)
+        wt = _dgrad_weight_t(weight)
+        gi = rs_ring(lambda c: dgrad(g[c * n:(c + 1) * n], weight, wt), group, wgrad)
         if "dw" not in res:   # world 1 ring: no wait happened
             wgrad()
         return gi, res["dw"], res["db"]
@@ -558,7 +592,8 @@ class _RowSPLinear(torch.autograd.Function):
         g = g.contiguous()
         n = ctx.n
         gi = x.new_empty(x.shape)
-        gfull = ag_ring(g, group, lambda c, ch: torch.matmul(ch, weight, out=gi[c * n:(c + 1) * n]),
+        wt = _dgrad_weight_t(weight)
+        gfull = ag_ring(g, group, lambda c, ch: dgrad_into(gi[c * n:(c + 1) * n], ch, weight, wt),
                         before_last_wait=_flush_wgrad)
         dw = _wgrad(weight, gfull.reshape(-1, gfull.shape[-1]), x.reshape(-1, x.shape[-1]))
         return gi, dw

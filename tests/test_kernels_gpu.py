@@ -426,3 +426,33 @@ def test_linear_fwd_strided_input_and_rejects_bad_shapes():
     with pytest.raises(RuntimeError):
         C.linear_fwd(torch.randn(64, 100, device=DEV, dtype=torch.bfloat16),
                      torch.randn(64, 100, device=DEV, dtype=torch.bfloat16), None, 0)   # K % 64 != 0
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("shape", [(1024, 1024), (3072, 1024), (1024, 4096), (50304, 1024), (200, 136), (8, 8)])
+def test_transpose2d(dt, shape):
+    x = torch.randn(*shape, device="cuda").to(dt)
+    y = _ext.ext().transpose2d(x)
+    assert y.shape == (shape[1], shape[0]) and y.is_contiguous()
+    assert torch.equal(y, x.t().contiguous())
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+def test_linear_dgrad_tn_matches_nn(dt):
+    """The TN dgrad (F.linear with a transposed weight copy) against fp32 dY @ W, through the
+    Megatron linear autograd function."""
+    from smdt_amd.parallel import tensor_parallel as tp
+    torch.manual_seed(0)
+    x = torch.randn(4, 256, 1024, device="cuda", dtype=dt, requires_grad=True)
+    w = (torch.randn(3072, 1024, device="cuda") * 0.02).to(dt).requires_grad_(True)
+    y = tp.LinearWithGradAccumulationAndAsyncCommunication.apply(x, w, None, False, False)
+    g = torch.randn_like(y)
+    y.backward(g)
+    ref = g.float().matmul(w.float())
+    err = (x.grad.float() - ref).abs().max().item()
+    assert err <= 2e-2 * ref.abs().max().item(), err
+    wt = tp._dgrad_weight_t(w.detach())
+    assert wt is not None, "TN dgrad path not taken on the GPU"
+    out = torch.empty_like(x.grad)
+    tp.dgrad_into(out, g, w.detach(), wt)
+    assert torch.equal(out, tp.dgrad(g, w.detach(), wt))
