@@ -199,7 +199,7 @@ def main():
             yield torch.randint(0, a.vocab_size, (mbs, S + 1), device=dev, generator=gen)
 
     it = batches()
-    pos = torch.arange(S, device=dev).unsqueeze(0).expand(mbs, S)
+    pos = None   # positions 0 .. S-1 in every sequence (the model's broadcast position-table slice)
 
     def forward_step(data_iter, m):
         toks = next(data_iter)

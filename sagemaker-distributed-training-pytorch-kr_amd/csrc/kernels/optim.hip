@@ -57,9 +57,11 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
       if (a.adamw) p[j] -= a.lr * a.weight_decay * p[j];
       p[j] -= step_size * upd;
     }
-    reinterpret_cast<f32x4*>(a.master)[i] = p;
-    reinterpret_cast<f32x4*>(a.exp_avg)[i] = m;
-    reinterpret_cast<f32x4*>(a.exp_avg_sq)[i] = v;
+    // ... and written once: nontemporal stores (the 10.7 GB per-step state stream of GPT-2 345M
+    // does not fit any cache level, so there is nothing to keep resident)
+    __builtin_nontemporal_store(p, reinterpret_cast<f32x4*>(a.master) + i);
+    __builtin_nontemporal_store(m, reinterpret_cast<f32x4*>(a.exp_avg) + i);
+    __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(a.exp_avg_sq) + i);
     if constexpr (!std::is_same<TO, float>::value) {
       if (a.model_out) {
         TO* o = reinterpret_cast<TO*>(a.model_out) + i * 4;
@@ -72,7 +74,7 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
           __builtin_memcpy(&bits, &t, 2);
           w[j] = bits;
         }
-        *reinterpret_cast<v4*>(o) = w;
+        __builtin_nontemporal_store(w, reinterpret_cast<v4*>(o));
       }
     }
   }

@@ -107,16 +107,20 @@ class GPTModel(nn.Module):
             return self.embedding.weight
         return self.output_weight
 
-    def _embed(self, tokens, position_ids):
+    def _embed(self, tokens, position_ids, pos_start=None):
+        """[s, b, h] embeddings. ``pos_start`` (int): positions are pos_start + arange(s) in every
+        sequence, so the position table is a slice broadcast over the batch (no gather, and a
+        batch-sum backward instead of a [s * b]-row scatter)."""
         st = ps.get_state()
-        e = self.embedding(tokens, reduce=False)                  # [b, s, h] (TP-partial)
-        e = e.transpose(0, 1).contiguous()                        # [s, b, h]
+        e = self.embedding(tokens.t(), reduce=False)              # [s, b, h] (TP-partial), no transpose copy
         if st.tp > 1:
             if self.sp:
                 e = tp.reduce_scatter_to_sequence_parallel_region(e)
             else:
                 e = tp.reduce_from_tensor_model_parallel_region(e)
-        if self.position_embeddings is not None:
+        if self.position_embeddings is not None and pos_start is not None and not self.sp:
+            e = tp.add_position_slice(e, self.position_embeddings, pos_start + self.cfg.position_offset)
+        elif self.position_embeddings is not None:
             pos = position_ids.transpose(0, 1)                   # [s, b]
             if self.cfg.position_offset:
                 pos = pos + self.cfg.position_offset
@@ -149,11 +153,13 @@ class GPTModel(nn.Module):
         (Megatron: sum(loss * mask) / sum(mask)); lets the fused LM head compute its backward in
         forward. Without it the fused head assumes a plain mean over the tokens."""
         if self.pre_process:
+            pos_start = getattr(position_ids, "_smdt_arange_start", None) if position_ids is not None else None
             if position_ids is None:
                 # with context parallelism ``tokens`` is this rank's chunk cp_rank of the sequence
                 off = ps.get_state().cp_rank * tokens.shape[1]
+                pos_start = off
                 position_ids = (torch.arange(tokens.shape[1], device=tokens.device) + off).unsqueeze(0).expand_as(tokens)
-            x = self._embed(tokens, position_ids)
+            x = self._embed(tokens, position_ids, pos_start)
         else:
             x = self.input_tensor
         out = self.decoder(x, None, None)

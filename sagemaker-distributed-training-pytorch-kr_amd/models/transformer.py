@@ -250,7 +250,7 @@ class _Fc1BiasGelu(torch.autograd.Function):
     backward's GeLU derivative needs) is written by the same epilogue, so the separate bias-GeLU
     pass (K5) and its [tokens, 4h] round trip disappear from the forward.
     Backward: d(pre) = d(act) * gelu'(pre) with the fp32 bias gradient (bias_act kernel, bias
-    already inside pre) -> dx = d(pre) W1 (hipBLASLt), dW1 = d(pre)^T x into main_grad (deferred
+    already inside pre) -> dx = d(pre) W1 (hipBLASLt, TN layout via a transposed W1), dW1 = d(pre)^T x into main_grad (deferred
     grouped MFMA wgrad). TP = 1 without sequence parallelism (the column-parallel collectives of
     ColumnParallelLinear are not needed there)."""
 
@@ -278,7 +278,7 @@ class _Fc1BiasGelu(torch.autograd.Function):
             db1 = None
         else:
             db1 = db.to(b1.dtype)
-        dx = dpre.matmul(w1)
+        dx = tp.dgrad(dpre, w1, tp._dgrad_weight_t(w1))
         dw1 = tp._wgrad(w1, dpre, x2)
         return dx.view(ctx.shp), dw1, db1
 

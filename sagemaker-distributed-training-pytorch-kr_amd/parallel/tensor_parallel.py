@@ -762,6 +762,42 @@ class _EmbeddingLookup(torch.autograd.Function):
         return None, dw.to(w.dtype)
 
 
+class _AddPositionSlice(torch.autograd.Function):
+    """e [s, b, h] + weight[start:start + s] broadcast over b. Backward: de = g, and the table's
+    gradient is the batch sum of g (one reduction) added to rows start..start + s of the fp32
+    ``main_grad`` (torch's embedding backward would scatter s * b rows with atomics)."""
+
+    @staticmethod
+    def forward(ctx, e, weight, start):
+        s = e.shape[0]
+        ctx.weight, ctx.start = weight, start
+        return e + weight[start:start + s].unsqueeze(1)
+
+    @staticmethod
+    def backward(ctx, g):
+        w, start = ctx.weight, ctx.start
+        s = g.shape[0]
+        gs = g.sum(1, dtype=torch.float32)                          # [s, h]
+        mg = getattr(w, "main_grad", None)
+        if mg is not None and mg.dtype == torch.float32:
+            mg[start:start + s].add_(gs)
+            cb = getattr(w, "_smdt_grad_ready", None)
+            if cb is not None:
+                cb(w)
+            return g, None, None
+        dw = torch.zeros(w.shape, dtype=torch.float32, device=g.device)
+        dw[start:start + s] = gs
+        return g, dw.to(w.dtype), None
+
+
+def add_position_slice(e, weight, start: int):
+    """e + weight[start:start + e.shape[0]] (learned absolute positions shared by every sequence)."""
+    assert start + e.shape[0] <= weight.shape[0], "sequence longer than the position table"
+    if not torch.is_grad_enabled() or not weight.requires_grad:
+        return e + weight[start:start + e.shape[0]].unsqueeze(1)
+    return _AddPositionSlice.apply(e, weight, int(start))
+
+
 def embedding_lookup(ids, weight):
     """weight[ids] with the synchronisation-free backward above (torch's own path when
     deterministic algorithms are requested: atomics make the fp32 sum order run-dependent)."""

@@ -42,6 +42,10 @@ def get_ltor_masks_and_position_ids(data, eod_token, reset_position_ids=False, r
                     prev = j + 1
     if attention_mask is not None:
         attention_mask = attention_mask < 0.5
+    if not reset_position_ids:
+        # plain 0 .. s-1 in every row: lets GPTModel add the position table as a broadcast slice
+        # (a tensor derived from this one by slicing / copying loses the mark and takes the gather)
+        position_ids._smdt_arange_start = 0
     return attention_mask, loss_mask, position_ids
 
 

@@ -251,3 +251,37 @@ def test_pretrain_gpt_writes_tensorboard_and_runs_context_parallel(tmp_path):
     steps = sorted(s for s, t, _ in sc if t == "lm loss")
     assert steps == [1, 2, 3]
     assert all(math.isfinite(v) for _, _, v in sc)
+
+
+@pytest.mark.parametrize("offset", [0, 3])
+def test_gpt_position_slice_matches_gathered_positions(offset):
+    """Default positions (no position_ids) take the broadcast-slice path with a batch-sum
+    backward into main_grad; explicit position_ids take the gather / scatter path. Same loss,
+    same main_grad for every parameter."""
+    from smdt_amd.models.gpt import GPTModel
+    from smdt_amd.models.transformer import TransformerConfig
+    from smdt_amd.parallel import state as ps
+    from smdt_amd.parallel.distributed import DistributedDataParallel
+    ps.destroy_model_parallel()
+    cfg = TransformerConfig(num_layers=1, hidden_size=32, num_attention_heads=2, max_position_embeddings=16,
+                            padded_vocab_size=64, params_dtype=torch.float32, seed=7, position_offset=offset,
+                            hidden_dropout=0.0, attention_dropout=0.0)
+    ddp = DistributedDataParallel(GPTModel(cfg))
+    model = ddp.module if hasattr(ddp, "module") else ddp
+    tok = torch.randint(0, 64, (3, 9))
+    grads = []
+    for pos in (None, torch.arange(8).unsqueeze(0).expand(3, 8)):
+        ddp.zero_grad_buffer()
+        loss = model(tok[:, :-1], position_ids=pos, labels=tok[:, 1:]).float().mean()
+        loss.backward()
+        ddp.finish_grad_sync()
+        grads.append((loss.detach(), ddp.grad_data.clone()))
+    torch.testing.assert_close(grads[0][0], grads[1][0])
+    torch.testing.assert_close(grads[0][1], grads[1][1], rtol=1e-5, atol=1e-6)
+    assert grads[0][1].abs().sum() > 0
+    # Megatron's get_batch positions are marked as plain aranges (slice path); reset ones are not
+    from smdt_amd.train.utils import get_ltor_masks_and_position_ids
+    _, _, p_plain = get_ltor_masks_and_position_ids(tok[:, :-1], 0)
+    _, _, p_reset = get_ltor_masks_and_position_ids(tok[:, :-1], 0, reset_position_ids=True)
+    assert getattr(p_plain, "_smdt_arange_start", None) == 0
+    assert getattr(p_reset, "_smdt_arange_start", None) is None
