@@ -448,8 +448,16 @@ __global__ __launch_bounds__(256) void delta_kernel(const E* __restrict__ O,
 // dK / dV. Workgroup = 4 waves = 128 keys of one (b, kv-head); each wave keeps K, V of its 32
 // keys and dK^T, dV^T in registers while the workgroup sweeps the query heads of the group and
 // their 64-row query tiles (Q, dO, lse*log2e, delta staged in double-buffered LDS).
+// Workgroups per CU requested from the compiler for the D = 64 backward kernels (A/B knobs:
+// 3 caps them at 168 VGPRs, which spills).
+#ifndef SMDT_FA_DQ_OCC
+#define SMDT_FA_DQ_OCC 2
+#endif
+#ifndef SMDT_FA_DKDV_OCC
+#define SMDT_FA_DKDV_OCC 2
+#endif
 template <int D, bool CAUSAL, bool DROP, class E>
-__global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dkdv_kernel(
+__global__ __launch_bounds__(256, D == 64 ? SMDT_FA_DKDV_OCC : 1) void bwd_dkdv_kernel(
     const E* __restrict__ Q, const E* __restrict__ K, const E* __restrict__ V,
     const E* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ DELTA,
     E* __restrict__ dK, E* __restrict__ dV, int B, int H, int Hkv, int S, Strides qs,
@@ -665,7 +673,7 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dkdv_kernel(
 // dQ. Workgroup = 4 waves = 128 query rows of one (b, h); K/V streamed in 64-key tiles,
 // double-buffered.
 template <int D, bool CAUSAL, bool DROP, class E>
-__global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dq_kernel(
+__global__ __launch_bounds__(256, D == 64 ? SMDT_FA_DQ_OCC : 1) void bwd_dq_kernel(
     const E* __restrict__ Q, const E* __restrict__ K, const E* __restrict__ V,
     const E* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ DELTA,
     E* __restrict__ dQ, int B, int H, int Hkv, int S, Strides qs, Strides ks_, Strides vs,

@@ -33,23 +33,26 @@ VOCAB_TP2 = 50304 // 2
 
 
 def shapes():
+    # Dgrad GEMMs run in the TN layout: dX = F.linear(dY, W^T) / torch.mm(dY, W^T.t(), out=)
+    # with a contiguous W^T (parallel/tensor_parallel.py ``dgrad`` / ``dgrad_into``), so the
+    # backward shapes below are "linear" / "mm" calls with N = in-features, K = out-features.
     # N = 1 (tp1, micro-batch 64): the backward dgrad GEMMs (the forward ones are tuned by
     # ``bench.py --tunableop 2``, whose first warmup step reaches them first)
     mt = S * 64
-    out = [("matmul", mt, H, 50304), ("matmul", mt, FFN, H), ("matmul", mt, H, FFN), ("matmul", mt, H, H),
-           ("matmul", mt, H, 3 * H)]
+    out = [("linear", mt, H, 50304), ("linear", mt, H, FFN), ("linear", mt, FFN, H), ("linear", mt, H, H),
+           ("linear", mt, H, 3 * H)]
     for mbs in (64, 16):
         m = S // 2 * mbs  # one ring chunk of a sequence-parallel [s / tp, b, h] activation
         # forward column-parallel (qkv with bias, fc1 without: bias-GeLU is a separate kernel)
         out += [("addmm", m, 3 * H // 2, H), ("mm", m, FFN // 2, H)]
         # forward row-parallel chunks (proj, fc2)
         out += [("linear", m, H, H // 2), ("linear", m, H, FFN // 2)]
-        # backward: column dgrad chunks g[m, out/2] @ W[out/2, h]; row dgrad g[m, h] @ W[h, in/2]
-        out += [("matmul", m, H, 3 * H // 2), ("matmul", m, H, FFN // 2),
-                ("matmul", m, H // 2, H), ("matmul", m, FFN // 2, H)]
-        # vocab-parallel LM head over the gathered sequence: forward and dgrad
-        mt = S * mbs
-        out += [("linear", mt, VOCAB_TP2, H), ("matmul", mt, H, VOCAB_TP2)]
+        # backward: column dgrad chunks F.linear(g[m, out/2], W^T[h, out/2]);
+        # row dgrad chunks mm(g[m, h], W^T[in/2, h].t(), out=)
+        out += [("linear", m, H, 3 * H // 2), ("linear", m, H, FFN // 2),
+                ("mm", m, H // 2, H), ("mm", m, FFN // 2, H)]
+        # vocab-parallel LM head, one ring chunk: forward mm into the gathered output, dgrad
+        out += [("mm", m, VOCAB_TP2, H), ("linear", m, H, VOCAB_TP2)]
     return out
 
 
