@@ -419,29 +419,32 @@ __global__ __launch_bounds__(256) void delta_kernel(const E* __restrict__ O,
                                                     float* __restrict__ delta, const float* __restrict__ LSE,
                                                     float* __restrict__ NLSE2, float dscale, float lsub, int B,
                                                     int H, int S, Strides os, Strides dos) {
-  // 8 lanes per row, each lane D/8 contiguous elements.
-  const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int64_t row = gid / 8;
-  const int part = (int)(gid % 8);
-  if (row >= (int64_t)B * H * S) return;
-  const int q = (int)(row % S);
-  const int64_t bh = row / S;
-  const int b = (int)(bh / H), hh = (int)(bh % H);
+  // 8 lanes per row, each lane D/8 contiguous elements. Rows are enumerated (b, q, h) with the
+  // head fastest, the order of the [B, S, H, D] activations, so a wave reads one contiguous
+  // span; 32-bit index math (the launcher checks B * H * S < 2^31).
+  const int gid = blockIdx.x * 256 + threadIdx.x;
+  const int row = gid >> 3;
+  const int part = gid & 7;
+  if (row >= B * H * S) return;
+  const int hh = row % H;
+  const int t = row / H;
+  const int q = t % S, b = t / S;
   const E* o = O + b * os.sb + hh * os.sh + (int64_t)q * os.ss + part * (D / 8);
   const E* g = dO + b * dos.sb + hh * dos.sh + (int64_t)q * dos.ss + part * (D / 8);
   float acc = 0.f;
 #pragma unroll
   for (int c = 0; c < D / 64; ++c) {
     float a[8], bb[8];
-    load_vec<E, 8>(o + 8 * c, a);
-    load_vec<E, 8>(g + 8 * c, bb);
+    load_vec<E, 8, true>(o + 8 * c, a);   // read once here: stream past the caches
+    load_vec<E, 8, true>(g + 8 * c, bb);
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc += a[j] * bb[j];
   }
 #pragma unroll
   for (int off = 4; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 8);
-  if (part == 0) delta[row] = -acc * dscale;
-  if (part == 1) NLSE2[row] = lsub - LSE[row] * kLog2e;
+  const int out = (b * H + hh) * S + q;   // lse / delta are [B, H, S]
+  if (part == 0) delta[out] = -acc * dscale;
+  if (part == 1) NLSE2[out] = lsub - LSE[out] * kLog2e;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -901,6 +904,7 @@ extern "C" hipError_t smdt_flash_bwd(int dtype, const void* q, const void* k, co
   const float dscale = drop ? dr.keep : 1.f, lsub = drop ? dr.log2inv : 0.f;
   {
     int64_t rows = (int64_t)B * H * S;
+    if (rows * 8 >= (int64_t(1) << 31)) return hipErrorInvalidValue;  // delta_kernel indexes in 32 bits
     dim3 grid((unsigned)((rows * 8 + 255) / 256));
     if (dtype == 2) {
       if (D == 64)
