@@ -26,11 +26,14 @@
 //     split count is chosen against that cost); one split does a plain read-modify-write.
 //   * smdt_wgrad_grouped: many independent GEMMs (e.g. several layers' QKV / proj / fc1 / fc2
 //     weight gradients queued by the deferred-wgrad path) in ONE launch, every tile over its full
-//     m range: no split-K, no atomics, deterministic, and the tile count of a whole group fills
-//     the machine where a single small GEMM cannot.
+//     m range, deterministic, and the tile count of a whole group fills the machine where a
+//     single small GEMM cannot. Only the tiles past the last full round of 256 are split along m
+//     with fp32 atomics (see wgrad_grouped_kernel).
 // Work items are ordered (problem, n-group, k, n-in-group) and remapped so that the consecutive
 // items an XCD runs share A and B strips in that XCD's L2. Partial tiles (N or K not a multiple
 // of 256, as the 50304-row LM head) load clamped columns and skip their stores.
+#include <cstdlib>
+
 #include "common.h"
 #include "launchers.h"
 #include "mfma_tile.h"
@@ -256,21 +259,49 @@ struct Problem {
 constexpr int kMaxGroup = 32;
 struct Group {
   Problem p[kMaxGroup];
-  int nprob, nblocks;
+  int nprob;
+  int nfull;    // blocks 0 .. nfull-1: whole tiles (a multiple of 256 when a tail is split)
+  int splits;   // the tail tiles nfull .. : `splits` blocks each, `mps` stages of the m range apiece
+  int mps;
 };
 
 // The problem table travels in the kernel arguments (< 2 KB), read from the kernarg segment.
+//
+// Tail split: whole tiles run in rounds of 256 (one workgroup per CU), so a launch of 256 q + r
+// tiles costs q + 1 full rounds even when r is small. The GPT-2 345M LM head alone is
+// 197 x 4 = 788 tiles (3 rounds + 20), so every step paid a round with 236 CUs idle. The last r
+// tiles of the launch are therefore cut along m into ~256 / r pieces that run together in one
+// short round and add their partial sums with fp32 atomics (tail tiles only: their sum order is
+// not fixed; everything else stays deterministic). The whole tiles keep the XCD-aware order; the
+// pieces go round-robin over the XCDs.
 template <class E>
 __global__ __launch_bounds__(kThreads, 1) void wgrad_grouped_kernel(const Group g) {
   WG_LDS
-  const int w = xcd_remap(blockIdx.x, g.nblocks);
+  const int bid = blockIdx.x;
+  int w, piece = -1;
+  if (bid < g.nfull) {
+    w = xcd_remap(bid, g.nfull);
+  } else {
+    const int j = bid - g.nfull;
+    w = g.nfull + j / g.splits;
+    piece = j % g.splits;
+  }
   int pi = 0;
   while (pi + 1 < g.nprob && w >= g.p[pi + 1].tile0) ++pi;
   const Problem& P = g.p[pi];
   int tn, tk;
   tile_coords(w - P.tile0, P.ntn, P.ntk, P.gn, tn, tk);
-  tile_gemm<false, 0, E>((const E*)P.A, (const E*)P.B, P.C, P.N, P.K, tn * BT, tk * BT, 0, P.M / BM, L0, L1, L2,
-                         L3);
+  const int stages = P.M / BM;
+  if (piece < 0) {
+    tile_gemm<false, 0, E>((const E*)P.A, (const E*)P.B, P.C, P.N, P.K, tn * BT, tk * BT, 0, stages, L0, L1, L2,
+                           L3);
+  } else {
+    const int s0 = piece * g.mps;
+    const int nst = min(stages, s0 + g.mps) - s0;
+    if (nst <= 0) return;  // a smaller-M problem in the tail: nothing left for this piece (whole block exits)
+    tile_gemm<true, 0, E>((const E*)P.A, (const E*)P.B, P.C, P.N, P.K, tn * BT, tk * BT, (int64_t)s0 * BM, nst,
+                          L0, L1, L2, L3);
+  }
 }
 
 inline int group_width(int ntk) { return ntk <= 4 ? 8 : 4; }
@@ -332,6 +363,14 @@ extern "C" hipError_t smdt_wgrad_accumulate_t(int dtype, const void* dy, const v
   return hipGetLastError();
 }
 
+static bool wg_tail_split_enabled() {
+  static const int on = [] {
+    const char* v = getenv("SMDT_WGRAD_TAIL_SPLIT");
+    return (v && v[0] == '0') ? 0 : 1;
+  }();
+  return on != 0;
+}
+
 // Grouped form: one launch per 32 problems, the table passed by value.
 extern "C" hipError_t smdt_wgrad_grouped(const SmdtWgradProblem* probs, int n, hipStream_t st) {
   return smdt_wgrad_grouped_t(1, probs, n, st);
@@ -362,11 +401,35 @@ extern "C" hipError_t smdt_wgrad_grouped_t(int dtype, const SmdtWgradProblem* pr
     }
     for (int i = cnt; i < wg::kMaxGroup; ++i) g.p[i] = g.p[cnt - 1];
     g.nprob = cnt;
-    g.nblocks = tiles;
+    // Tail split (see wgrad_grouped_kernel): r = tiles mod 256 tail tiles, ~256 / r pieces each
+    // of at least 8 stages; off with SMDT_WGRAD_TAIL_SPLIT=0.
+    const int r = tiles % 256;
+    int splits = 1, mps = 0;
+    if (r > 0 && wg_tail_split_enabled()) {
+      int max_stages = 0;
+      for (int i = 0; i < cnt; ++i) max_stages = max_stages > g.p[i].M / wg::BM ? max_stages : g.p[i].M / wg::BM;
+      splits = 256 / r;
+      if (splits > 16) splits = 16;
+      if (splits > max_stages / 8) splits = max_stages / 8;
+      if (splits > 1) {
+        mps = (max_stages + splits - 1) / splits;
+        splits = (max_stages + mps - 1) / mps;
+      }
+    }
+    if (splits <= 1) {
+      g.nfull = tiles;
+      g.splits = 1;
+      g.mps = 0;
+    } else {
+      g.nfull = tiles - r;
+      g.splits = splits;
+      g.mps = mps;
+    }
+    const int nblocks = g.nfull + (tiles - g.nfull) * g.splits;
     if (dtype == 2)
-      hipLaunchKernelGGL(wg::wgrad_grouped_kernel<f16>, dim3(tiles), dim3(wg::kThreads), 0, st, g);
+      hipLaunchKernelGGL(wg::wgrad_grouped_kernel<f16>, dim3(nblocks), dim3(wg::kThreads), 0, st, g);
     else
-      hipLaunchKernelGGL(wg::wgrad_grouped_kernel<bf16>, dim3(tiles), dim3(wg::kThreads), 0, st, g);
+      hipLaunchKernelGGL(wg::wgrad_grouped_kernel<bf16>, dim3(nblocks), dim3(wg::kThreads), 0, st, g);
   }
   return hipGetLastError();
 }

@@ -125,6 +125,26 @@ def test_wgrad_grouped_matches_fp32_reference():
         torch.testing.assert_close(mg, ref, atol=2e-2 * (M ** 0.5), rtol=1e-3)
 
 
+def test_wgrad_grouped_tail_split_matches_fp32_reference():
+    """A grouped launch of 256 whole tiles + a 12-tile tail (partial N and K tiles): the tail is cut
+    along m into pieces that add with fp32 atomics; every target must still equal base + dy^T x."""
+    from smdt_amd.ops import _ext
+    torch.manual_seed(5)
+    shapes = [(2048, 1024, 1024)] * 16 + [(2048, 1000, 520)]
+    mgs, dys, xs, refs = [], [], [], []
+    for M, N, K in shapes:
+        g = torch.randn(M, N, device="cuda", dtype=torch.bfloat16)
+        x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+        base = torch.randn(N, K, device="cuda", dtype=torch.float32)
+        mgs.append(base.clone())
+        dys.append(g)
+        xs.append(x)
+        refs.append(base + g.float().t() @ x.float())
+    assert _ext.ext().wgrad_grouped(mgs, dys, xs)
+    for (M, _, _), mg, ref in zip(shapes, mgs, refs):
+        torch.testing.assert_close(mg, ref, atol=2e-2 * (M ** 0.5), rtol=1e-3)
+
+
 def test_fused_fc1_bias_gelu_mlp_matches_unfused():
     """fc1 + bias + GeLU in the hand-written MFMA GEMM epilogue (models/transformer._Fc1BiasGelu)
     == hipBLASLt + the K5 bias-GeLU kernel path: outputs, input grads and weight / bias grads."""
