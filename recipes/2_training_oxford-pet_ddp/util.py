@@ -77,19 +77,20 @@ class AverageMeter:
     format spec ``fmt`` (e.g. ":6.3f")."""
 
     def __init__(self, name, fmt=":f"):
-        self.name = name
-        self.fmt = fmt
+        self.name, self.fmt = name, fmt
         self.reset()
 
     def reset(self):
-        self.val = self.avg = self.sum = 0
-        self.count = 0
+        self.val, self.sum, self.count = 0, 0, 0
+
+    @property
+    def avg(self):
+        return self.sum / self.count if self.count else 0
 
     def update(self, val, n=1):
+        """Record ``val`` as the mean of ``n`` samples."""
         self.val = val
-        self.count += n
-        self.sum += val * n
-        self.avg = self.sum / self.count
+        self.sum, self.count = self.sum + val * n, self.count + n
 
     def __str__(self):
         spec = self.fmt[1:] if self.fmt.startswith(":") else self.fmt
