@@ -253,7 +253,19 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void fwd_kernel(const E* __re
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: diagonal tests branch on SCC
   const int nqb = S / kBlockRows;
   // Heaviest (latest) causal blocks first: they have the most key tiles.
-#if SMDT_FA_ORDER == 1
+#if SMDT_FA_ORDER == 2
+  // per XCD, pair-major: the row blocks of one (b, h) run together on one XCD, heaviest first
+  const int nbh = gridDim.x / nqb;
+  int qb, bh;
+  if ((nbh & 7) == 0) {
+    const int slot = blockIdx.x >> 3, r = slot % nqb;
+    bh = (slot / nqb) * 8 + (blockIdx.x & 7);
+    qb = CAUSAL ? nqb - 1 - r : r;
+  } else {
+    qb = CAUSAL ? (nqb - 1 - (int)(blockIdx.x / nbh)) : (int)(blockIdx.x / nbh);
+    bh = blockIdx.x % nbh;
+  }
+#elif SMDT_FA_ORDER == 1
   // global longest-first: every (b, h)'s heaviest block, then the next-heaviest, ...
   const int nbh = gridDim.x / nqb;
   const int qb = CAUSAL ? (nqb - 1 - (int)(blockIdx.x / nbh)) : (int)(blockIdx.x / nbh);
@@ -492,7 +504,18 @@ __global__ __launch_bounds__(256, D == 64 ? SMDT_FA_DKDV_OCC : 1) void bwd_dkdv_
   const int lane = threadIdx.x & 63, h = lane >> 5;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: diagonal tests branch on SCC
   const int nkb = S / kBlockRows;
-#if SMDT_FA_ORDER == 1
+#if SMDT_FA_ORDER == 2
+  const int nbhk = gridDim.x / nkb;
+  int kblk, bhk;
+  if ((nbhk & 7) == 0) {
+    const int slot = blockIdx.x >> 3;
+    kblk = slot % nkb;
+    bhk = (slot / nkb) * 8 + (blockIdx.x & 7);
+  } else {
+    kblk = (int)(blockIdx.x / nbhk);
+    bhk = blockIdx.x % nbhk;
+  }
+#elif SMDT_FA_ORDER == 1
   const int nbhk = gridDim.x / nkb;
   const int kblk = (int)(blockIdx.x / nbhk);  // global longest-first
   const int bhk = blockIdx.x % nbhk;
@@ -714,7 +737,19 @@ __global__ __launch_bounds__(256, D == 64 ? SMDT_FA_DQ_OCC : 1) void bwd_dq_kern
   const int lane = threadIdx.x & 63, h = lane >> 5;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: diagonal tests branch on SCC
   const int nqb = S / kBlockRows;
-#if SMDT_FA_ORDER == 1
+#if SMDT_FA_ORDER == 2
+  // per XCD, pair-major: the row blocks of one (b, h) run together on one XCD, heaviest first
+  const int nbh = gridDim.x / nqb;
+  int qb, bh;
+  if ((nbh & 7) == 0) {
+    const int slot = blockIdx.x >> 3, r = slot % nqb;
+    bh = (slot / nqb) * 8 + (blockIdx.x & 7);
+    qb = CAUSAL ? nqb - 1 - r : r;
+  } else {
+    qb = CAUSAL ? (nqb - 1 - (int)(blockIdx.x / nbh)) : (int)(blockIdx.x / nbh);
+    bh = blockIdx.x % nbh;
+  }
+#elif SMDT_FA_ORDER == 1
   // global longest-first: every (b, h)'s heaviest block, then the next-heaviest, ...
   const int nbh = gridDim.x / nqb;
   const int qb = CAUSAL ? (nqb - 1 - (int)(blockIdx.x / nbh)) : (int)(blockIdx.x / nbh);
