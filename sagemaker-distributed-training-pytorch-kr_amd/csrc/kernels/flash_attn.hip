@@ -486,6 +486,12 @@ __global__ __launch_bounds__(256) void delta_kernel(const E* __restrict__ O,
 #ifndef SMDT_FA_DQ_OCC
 #define SMDT_FA_DQ_OCC 2
 #endif
+// dQ: re-make the two accumulator splats (-lse', -delta') per 32-key sub-tile instead of pinning
+// them for the whole kernel: 178 -> 140 VGPRs, 2 -> 3 waves per SIMD, no spills; measured bwd
+// 1.014 / 1.041 -> 0.991 / 1.004 ms at B64 (profiles/r2_attn_order/ab_b64_dq_remat.log).
+#ifndef SMDT_FA_DQ_REMAT
+#define SMDT_FA_DQ_REMAT 1
+#endif
 #ifndef SMDT_FA_DKDV_OCC
 #define SMDT_FA_DKDV_OCC 2
 #endif
@@ -774,7 +780,15 @@ __global__ __launch_bounds__(256, D == 64 ? SMDT_FA_DQ_OCC : 1) void bwd_dq_kern
   // initial accumulators, register-resident for the whole loop (no per-subtile splat).
   const float nlse2 = LSE[((int64_t)b * H + hq) * S + my_q];
   const float ndl = DELTA[((int64_t)b * H + hq) * S + my_q];
+#if SMDT_FA_DQ_REMAT
+  // the two accumulator splats are re-made per sub-tile (opaque: not hoisted), freeing 32 VGPRs
+#define SMDT_DQ_ST0 splat16(opaque(nlse2))
+#define SMDT_DQ_DP0 splat16(opaque(ndl))
+#else
   const f32x16 st0 = splat16(nlse2), dp0 = splat16(ndl);  // dP' = dP - delta' (dropout selects below)
+#define SMDT_DQ_ST0 st0
+#define SMDT_DQ_DP0 dp0
+#endif
   const float c2 = scale * kLog2e;
   const uint32_t dkey = DROP ? drop_key(drop, bh) : 0u;
   const uint32_t dblk = (uint32_t)(my_q >> 1) * ((uint32_t)S >> 1) + 2u * h + (uint32_t)(my_q & 1);
@@ -812,8 +826,8 @@ __global__ __launch_bounds__(256, D == 64 ? SMDT_FA_DQ_OCC : 1) void bwd_dq_kern
       const int ksub = kb + 32 * tt;
       if (CAUSAL && ksub > qw + 31) continue;
       // row constants as the initial accumulators: S' = S log2(e) scale - lse, dP' = dP - delta
-      f32x16 st = mfma(fr.rowf(kt, 32 * tt, 0), qf[0], st0);
-      f32x16 dpt = mfma(fr.rowf(vt, 32 * tt, 0), dof[0], dp0);
+      f32x16 st = mfma(fr.rowf(kt, 32 * tt, 0), qf[0], SMDT_DQ_ST0);
+      f32x16 dpt = mfma(fr.rowf(vt, 32 * tt, 0), dof[0], SMDT_DQ_DP0);
 #pragma unroll
       for (int kk = 1; kk < G::KS; ++kk) {
         st = mfma(fr.rowf(kt, 32 * tt, kk), qf[kk], st);
