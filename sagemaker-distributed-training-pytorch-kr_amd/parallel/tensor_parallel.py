@@ -362,7 +362,8 @@ def _dgrad_weight_t(weight):
     """W^T [in, out] contiguous for the TN dgrad, or None to use dY @ W directly."""
     if (_DGRAD_TN and weight.is_cuda and weight.dim() == 2 and weight.is_contiguous()
             and weight.dtype in (torch.bfloat16, torch.float16)
-            and weight.shape[0] % 8 == 0 and weight.shape[1] % 8 == 0 and _ext.available()):
+            and weight.shape[0] % 8 == 0 and weight.shape[1] % 8 == 0
+            and _ext.use_kernels(weight)):   # raises on a GPU box without the extension
         return _ext.ext().transpose2d(weight)
     return None
 
