@@ -41,6 +41,11 @@ def shapes():
     mt = S * 64
     out = [("linear", mt, H, 50304), ("linear", mt, H, FFN), ("linear", mt, FFN, H), ("linear", mt, H, H),
            ("linear", mt, H, 3 * H)]
+    if os.environ.get("SMDT_TUNE_N1_FORWARD", "0") == "1":
+        # N = 1 forward: qkv with bias (addmm), proj / fc1 / fc2 without (the bias goes to the
+        # fused LN / bias-GeLU kernels), LM head
+        out += [("addmm", mt, 3 * H, H), ("mm", mt, H, H), ("mm", mt, FFN, H), ("mm", mt, H, FFN),
+                ("mm", mt, 50304, H)]
     for mbs in (64, 16):
         m = S // 2 * mbs  # one ring chunk of a sequence-parallel [s / tp, b, h] activation
         # forward column-parallel (qkv with bias, fc1 without: bias-GeLU is a separate kernel)
