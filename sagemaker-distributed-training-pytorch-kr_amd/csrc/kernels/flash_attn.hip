@@ -443,6 +443,8 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void fwd_kernel(const E* __re
 // accumulators (no VALU in their loops):
 //   ndl[b, h, q]   = -keep * sum_d dO[q, d] O[q, d]      (-delta', the dP accumulator's start)
 //   nlse2[b, h, q] = -(lse log2 e - log2 inv)           (the S accumulator's start, log2 domain)
+constexpr int kDeltaRows = 4;  // rows per 8-lane group in delta_kernel
+
 template <int D, class E>
 __global__ __launch_bounds__(256) void delta_kernel(const E* __restrict__ O,
                                                     const E* __restrict__ dO,
@@ -452,29 +454,48 @@ __global__ __launch_bounds__(256) void delta_kernel(const E* __restrict__ O,
   // 8 lanes per row, each lane D/8 contiguous elements. Rows are enumerated (b, q, h) with the
   // head fastest, the order of the [B, S, H, D] activations, so a wave reads one contiguous
   // span; 32-bit index math (the launcher checks B * H * S < 2^31).
+  // Each 8-lane group handles kDeltaRows consecutive rows with all their loads issued before the
+  // first reduction (memory-level parallelism: the kernel is a pure stream).
   const int gid = blockIdx.x * 256 + threadIdx.x;
-  const int row = gid >> 3;
+  const int r0 = (gid >> 3) * kDeltaRows;
   const int part = gid & 7;
-  if (row >= B * H * S) return;
-  const int hh = row % H;
-  const int t = row / H;
-  const int q = t % S, b = t / S;
-  const E* o = O + b * os.sb + hh * os.sh + (int64_t)q * os.ss + part * (D / 8);
-  const E* g = dO + b * dos.sb + hh * dos.sh + (int64_t)q * dos.ss + part * (D / 8);
-  float acc = 0.f;
+  const int nrows = B * H * S;
+  if (r0 >= nrows) return;
+  float a[kDeltaRows][D / 8], bb[kDeltaRows][D / 8];
+  int outi[kDeltaRows];
 #pragma unroll
-  for (int c = 0; c < D / 64; ++c) {
-    float a[8], bb[8];
-    load_vec<E, 8, true>(o + 8 * c, a);   // read once here: stream past the caches
-    load_vec<E, 8, true>(g + 8 * c, bb);
+  for (int k = 0; k < kDeltaRows; ++k) {
+    const int row = r0 + k < nrows ? r0 + k : nrows - 1;   // tail rows re-read the last row, unstored
+    const int hh = row % H;
+    const int t = row / H;
+    const int q = t % S, b = t / S;
+    const E* o = O + b * os.sb + hh * os.sh + (int64_t)q * os.ss + part * (D / 8);
+    const E* g = dO + b * dos.sb + hh * dos.sh + (int64_t)q * dos.ss + part * (D / 8);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc += a[j] * bb[j];
+    for (int c = 0; c < D / 64; ++c) {
+      float ta[8], tb[8];
+      load_vec<E, 8, true>(o + 8 * c, ta);   // read once here: stream past the caches
+      load_vec<E, 8, true>(g + 8 * c, tb);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        a[k][8 * c + j] = ta[j];
+        bb[k][8 * c + j] = tb[j];
+      }
+    }
+    outi[k] = (b * H + hh) * S + q;   // lse / delta are [B, H, S]
   }
 #pragma unroll
-  for (int off = 4; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 8);
-  const int out = (b * H + hh) * S + q;   // lse / delta are [B, H, S]
-  if (part == 0) delta[out] = -acc * dscale;
-  if (part == 1) NLSE2[out] = lsub - LSE[out] * kLog2e;
+  for (int k = 0; k < kDeltaRows; ++k) {
+    float acc = 0.f;
+#pragma unroll
+    for (int j = 0; j < D / 8; ++j) acc += a[k][j] * bb[k][j];
+#pragma unroll
+    for (int off = 4; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 8);
+    if (r0 + k < nrows) {
+      if (part == 0) delta[outi[k]] = -acc * dscale;
+      if (part == 1) NLSE2[outi[k]] = lsub - LSE[outi[k]] * kLog2e;
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -985,7 +1006,7 @@ extern "C" hipError_t smdt_flash_bwd(int dtype, const void* q, const void* k, co
   {
     int64_t rows = (int64_t)B * H * S;
     if (rows * 8 >= (int64_t(1) << 31)) return hipErrorInvalidValue;  // delta_kernel indexes in 32 bits
-    dim3 grid((unsigned)((rows * 8 + 255) / 256));
+    dim3 grid((unsigned)(((rows + kDeltaRows - 1) / kDeltaRows * 8 + 255) / 256));
     if (dtype == 2) {
       if (D == 64)
         hipLaunchKernelGGL((delta_kernel<64, f16>), grid, dim3(256), 0, st, (const f16*)o, (const f16*)dout, delta, lse, nlse2, dscale, lsub, B, H, S, os, dos);
