@@ -15,13 +15,22 @@ Launch: ``python bench.py`` (1 GPU) or
 ``python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N``.
 
 Layouts (``--layout``):
-  * ``baseline`` (default) — BASELINE.json config #3, GPT-2 345M at TP=2 PP=2 DP=2 on 8 GPUs
+  * ``baseline`` (default) — N=8 is BASELINE.json config #3, GPT-2 345M at TP=2 PP=2 DP=2 + SP
     (/root/reference/3_training_megatron-lm/megatron/arguments.py:1002-1005 sets TP/PP; the
-    reference's own run, NB3:399-428, used TP4 DP4). The model-parallel shape grows with N and is
-    then replicated: N=1 tp1pp1, N=2 tp2, N=4 tp2pp2, N=8 tp2pp2dp2, sequence parallelism whenever
-    tp > 1, ZeRO-1 across DP.
-  * ``dp`` — DP-N + ZeRO-1 (every GPU holds the whole model).
-  ``--tp/--pp`` override either layout.
+    reference's own run, NB3:399-428, used TP4 DP4). N=2 and N=4 run DP-N + ZeRO-1: a TP pair
+    shares ONE xGMI link, and at N=2 the sequence-parallel exchanges of a tp2 step (~24.6 GB per
+    direction) would take longer than the step's compute, while DP-N moves ~2 GB per step per
+    rank across all of a GPU's links and overlaps it with backward (BENCHMARKS.md "link budget").
+  * ``dp`` — DP-N + ZeRO-1 at every N (every GPU holds the whole model).
+  * ``tp`` — model parallelism first: N=2 tp2, N=4 tp2pp2, N=8 tp2pp2dp2 (+SP).
+  ``--tp/--pp`` override any layout. The JSON line names the layout and its parallelism.
+
+Self-explanation (``--comm-stats 1``, default): the JSON line carries ``phase_ms`` — the step split
+from CUDA events on the compute stream into forward/backward compute, TP-exchange wait, pipeline
+p2p wait + bubble, ZeRO parameter-gather wait, DP gradient sync, optimizer and the device idle gap
+between steps (comm/stats.py; the pieces sum to the step) — and ``comm``: per axis (tp / pp / dp /
+embd / mp) and op the calls, MB, ms and bus GB/s per step, keyed by the transport that carried them
+(rccl / xgmi / relay). No host-device synchronisation is added to the timed loop.
 
 Scaling is WEAK: every GPU processes ``--seqs-per-gpu`` (64) sequences of 1024 tokens per step
 at every N, so global batch = 64 N. A DP replica (tp x pp GPUs) therefore runs 64 tp pp sequences
@@ -60,7 +69,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--layout", choices=["baseline", "dp"], default="baseline")
+    p.add_argument("--layout", choices=["baseline", "dp", "tp"], default="baseline")
     p.add_argument("--tp", type=int, default=None)
     p.add_argument("--pp", type=int, default=None)
     p.add_argument("--sequence-parallel", type=int, default=None, help="default: on when tp > 1")
@@ -79,7 +88,9 @@ def parse():
     p.add_argument("--hidden-dropout", type=float, default=0.1)
     p.add_argument("--attention-dropout", type=float, default=0.1)  # Megatron default (reference run)
     p.add_argument("--zero", type=int, default=1, help="ZeRO-1/2 distributed optimizer when DP > 1")
-    p.add_argument("--bucket-size", type=int, default=40_000_000)
+    p.add_argument("--bucket-size", type=int, default=None,
+                   help="DDP bucket elements (default: auto, 8-32 MB from a start-up link timing)")
+    p.add_argument("--comm-stats", type=int, default=1, help="phase_ms / per-collective stats in the JSON")
     p.add_argument("--no-flash", action="store_true")
     p.add_argument("--fused-ce", action="store_true",
                    help="chunked LM head + CE with its backward in forward (never materialises the logits)")
@@ -141,12 +152,17 @@ def enable_gemm_tuning(a, rank):
         return "unavailable"
 
 
-BASELINE_LAYOUT = {1: (1, 1), 2: (2, 1), 4: (2, 2), 8: (2, 2)}  # N -> (tp, pp); dp = N / (tp pp)
+# N -> (tp, pp); dp = N / (tp pp)
+LAYOUTS = {
+    "baseline": {1: (1, 1), 2: (1, 1), 4: (1, 1), 8: (2, 2)},
+    "tp": {1: (1, 1), 2: (2, 1), 4: (2, 2), 8: (2, 2)},
+    "dp": {},
+}
 
 
 def choose_layout(a, world):
     """(tp, pp, sp, micro_batch, grad_accum) for ``world`` GPUs (see the module docstring)."""
-    tp, pp = BASELINE_LAYOUT.get(world, (1, 1)) if a.layout == "baseline" else (1, 1)
+    tp, pp = LAYOUTS[a.layout].get(world, (1, 1))
     tp = a.tp if a.tp is not None else tp
     pp = a.pp if a.pp is not None else pp
     if world % (tp * pp):
@@ -165,6 +181,9 @@ def choose_layout(a, world):
 
 def main():
     a = parse()
+    from smdt_amd.comm import buckets as comm_buckets
+    from smdt_amd.comm import stats as comm_stats
+    comm_stats.enable(bool(a.comm_stats))   # before the process group: RCCL per-work timing
     rank, local, world, backend = init_distributed("nccl")
     if world != a.gpus and rank == 0:
         print(f"[bench] note: --gpus {a.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
@@ -215,13 +234,19 @@ def main():
     fb = get_forward_backward_func()
     shape = (S // a.tp if cfg.sequence_parallel else S, mbs, cfg.hidden_size)
 
-    def train_step():
+    def train_step(stats=False):
+        if stats:
+            comm_stats.begin_step()
         ddp.zero_grad_buffer()
         losses = fb(forward_step, it, ddp, a.grad_accum, tensor_shape=shape, dtype=torch.bfloat16)
+        comm_stats.mark("fwd_bwd")
         ddp.finish_grad_sync()
         allreduce_word_embedding_grads(model)   # tied embedding: first + last pipeline stage
+        comm_stats.mark("grad_sync")
         lr = sched.step(1)
         opt.step(lr)
+        comm_stats.mark("optimizer")
+        comm_stats.end_step()
         return losses
 
     tw = time.perf_counter()
@@ -240,7 +265,7 @@ def main():
     t0 = time.perf_counter()
     last = None
     for _ in range(a.steps):
-        last = train_step()
+        last = train_step(stats=bool(a.comm_stats))
     if torch.cuda.is_available():
         torch.cuda.synchronize()
     if dist.is_initialized():
@@ -249,6 +274,12 @@ def main():
     if dist.is_initialized():
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     elapsed = float(el.item())
+    ms_step = 1000 * elapsed / a.steps
+    explain = comm_stats.summary(ms_step) if a.comm_stats else None
+    phases_all = None
+    if explain is not None and dist.is_initialized() and world > 1:
+        phases_all = [None] * world
+        dist.all_gather_object(phases_all, (st.pp_rank, explain["phase_ms"]))
     from smdt_amd.comm import xgmi
     from smdt_amd.ops import functional as SF
     SF.fused_linear_ce_check()   # (after the timed region) the fused LM head saw a plain mean
@@ -273,7 +304,7 @@ def main():
             "n_gpus": n,
             "steps": a.steps,
             "warmup": a.warmup,
-            "ms_per_step": round(1000 * elapsed / a.steps, 3),
+            "ms_per_step": round(ms_step, 3),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": round(tps / ref_tps, 3),
@@ -283,7 +314,10 @@ def main():
                        "seq_len": S, "micro_batch": mbs, "grad_accum": a.grad_accum,
                        "parallelism": f"tp{a.tp}pp{a.pp}dp{st.dp}" + ("+sp" if cfg.sequence_parallel else "")
                        + ("+zero1" if zero else ""),
-                       "layout": a.layout, "scaling_note": f"weak: {a.seqs_per_gpu} seqs x {S} tokens per GPU per step",
+                       "layout": a.layout, "tp": a.tp, "pp": a.pp, "dp": st.dp,
+                       "ddp_bucket": {"elements": ddp.bucket_size, "count": len(ddp.buckets),
+                                      **comm_buckets.TUNED},
+                       "scaling_note": f"weak: {a.seqs_per_gpu} seqs x {S} tokens per GPU per step",
                        "flash_attn": not a.no_flash, "hidden_dropout": a.hidden_dropout,
                        "attention_dropout": a.attention_dropout, "recompute": a.recompute,
                        "gemm_autotune": tuned},
@@ -294,9 +328,20 @@ def main():
         comm = {**relay.TUNED, **xgmi.TUNED}
         if comm:  # run-time RCCL-vs-kernel decisions on this node (comm/relay.py, comm/xgmi.py)
             rec["comm_tuning"] = comm
+        if explain is not None:
+            rec["phase_ms"] = _mean_phases([p for _, p in phases_all]) if phases_all else explain["phase_ms"]
+            if phases_all and st.pp > 1:
+                rec["phase_ms_by_pp_stage"] = {
+                    str(k): _mean_phases([p for r, p in phases_all if r == k]) for k in range(st.pp)}
+            rec["comm"] = explain["comm"]   # rank 0's collectives, per step
         print(json.dumps(rec), flush=True)
     if dist.is_initialized():
         dist.destroy_process_group()
+
+
+def _mean_phases(ps_):
+    keys = ps_[0].keys()
+    return {k: round(sum(p[k] for p in ps_) / len(ps_), 3) for k in keys}
 
 
 if __name__ == "__main__":

@@ -30,7 +30,7 @@ import torch
 import torch.distributed as dist
 
 from ..ops import _ext
-from .xgmi import IpcEngine, _EventHandle
+from .xgmi import IpcEngine, _EventHandle, _timing_event
 
 DEFAULT_SLOT_BYTES = 8 << 20      # per (flow, parity): parts of up to 4 MB -> 32 MB per call on 8 GPUs
 DEFAULT_SUB = 4                   # blocks per part and direction (2 x W x 4 = 64 blocks on 8 GPUs)
@@ -185,12 +185,13 @@ class XgmiRelay(IpcEngine):
         cur = torch.cuda.current_stream(dev)
         self._stream.wait_stream(cur)
         with torch.cuda.stream(self._stream):
+            ev0 = _timing_event(self._stream)
             self.exchange(send, recv)
-            ev = torch.cuda.Event()
+            ev = torch.cuda.Event(enable_timing=ev0 is not None)
             ev.record(self._stream)
         send.record_stream(self._stream)
         recv.record_stream(self._stream)
-        return _EventHandle(ev)
+        return _EventHandle(ev, ev0)
 
     def error(self) -> int:
         return int(self.C.relay_read_error(self._sig)) if self._sig is not None else 0

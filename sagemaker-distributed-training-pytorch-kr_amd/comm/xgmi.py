@@ -102,11 +102,26 @@ def _bands(n: int, per_call: int, align: int):
     return [(lo, min(n, lo + step)) for lo in range(0, n, step)]
 
 
+def _timing_event(stream):
+    """A start event on ``stream`` when per-collective stats are being collected, else None."""
+    from . import stats
+    if not stats.active():
+        return None
+    ev = torch.cuda.Event(enable_timing=True)
+    ev.record(stream)
+    return ev
+
+
 class _EventHandle:
     """``work.wait()``-compatible handle of a call issued on the engine's side stream."""
 
-    def __init__(self, event):
+    def __init__(self, event, start=None):
         self.event = event
+        self.start = start          # recorded before the call when comm stats are on
+
+    def timing(self):
+        """(start, end) events of the call for comm/stats.py, or None."""
+        return (self.start, self.event) if self.start is not None else None
 
     def wait(self):
         torch.cuda.current_stream().wait_event(self.event)
@@ -353,14 +368,15 @@ class XgmiAllReduce(IpcEngine):
         cur = torch.cuda.current_stream(dev)
         self._stream.wait_stream(cur)
         with torch.cuda.stream(self._stream):
+            ev0 = _timing_event(self._stream)
             ok = fn(*args)
-            ev = torch.cuda.Event()
+            ev = torch.cuda.Event(enable_timing=ev0 is not None)
             ev.record(self._stream)
         if not ok:
             return None
         for t in tensors:
             t.record_stream(self._stream)
-        return _EventHandle(ev)
+        return _EventHandle(ev, ev0)
 
     def all_reduce_async(self, t: torch.Tensor, op: str = "sum") -> Optional[_EventHandle]:
         """The same on the engine's own stream, ordered after the current stream's work; returns

@@ -206,7 +206,9 @@ def allreduce_word_embedding_grads(model: GPTModel):
     if g is None:
         g = w.grad
     if g is not None:
-        dist.all_reduce(g, group=st.embd_group)
+        from ..comm import stats as _cs
+        with _cs.blocking("all_reduce", st.embd_group, g.numel() * g.element_size()):
+            dist.all_reduce(g, group=st.embd_group)
 
 
 def gpt_flops_per_token(cfg: TransformerConfig, seq_len: int, recompute: bool = False) -> float:

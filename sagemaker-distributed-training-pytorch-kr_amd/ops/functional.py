@@ -562,11 +562,13 @@ class _FusedCE(torch.autograd.Function):
         t = target.contiguous().view(-1)
         mx, se, tg = C.ce_stats(lg.view(-1, lg.shape[-1]), t, vstart, vvalid)
         if group is not None and torch.distributed.get_world_size(group) > 1:
+            from ..comm import stats as _cs
             gmax = mx.clone()
-            torch.distributed.all_reduce(gmax, op=torch.distributed.ReduceOp.MAX, group=group)
-            se = se * torch.exp(mx - gmax)
-            torch.distributed.all_reduce(se, group=group)
-            torch.distributed.all_reduce(tg, group=group)
+            with _cs.blocking("all_reduce", group, 3 * gmax.numel() * gmax.element_size()):
+                torch.distributed.all_reduce(gmax, op=torch.distributed.ReduceOp.MAX, group=group)
+                se = se * torch.exp(mx - gmax)
+                torch.distributed.all_reduce(se, group=group)
+                torch.distributed.all_reduce(tg, group=group)
             mx = gmax
         loss = torch.log(se) + mx - tg
         loss = torch.where(t == ignore_index, torch.zeros_like(loss), loss)

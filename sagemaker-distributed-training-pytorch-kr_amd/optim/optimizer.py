@@ -26,6 +26,7 @@ from typing import Optional
 import torch
 import torch.distributed as dist
 
+from ..comm import stats as _cs
 from ..ops import _ext
 from ..parallel import state as ps
 from ..parallel.distributed import DistributedDataParallel
@@ -159,8 +160,9 @@ class MixedPrecisionAdam:
             elif e > s and self.scaler is not None:   # still check for inf/nan
                 self._sumsq(g[s:e])
         for grp in self._norm_groups():
-            dist.all_reduce(total, group=grp)
-            dist.all_reduce(self.found_inf, op=dist.ReduceOp.MAX, group=grp)
+            with _cs.blocking("all_reduce", grp, 8):
+                dist.all_reduce(total, group=grp)
+                dist.all_reduce(self.found_inf, op=dist.ReduceOp.MAX, group=grp)
         inv_scale = 1.0
         scale_t = None
         if self.scaler is not None:

@@ -14,11 +14,11 @@ MI355X-first layout:
   * each region is cut into *buckets* (reverse registration order ~ backward order); when the
     last gradient of a bucket lands, the bucket's all-reduce (or reduce-scatter for ZeRO) is
     launched asynchronously on RCCL while backward continues;
-  * bucket sizes default to 40 M elements (160 MB fp32): over the 8-GPU xGMI mesh a ring
-    collective is per-link bound (≈153 GB/s per link) and needs tens of MB per call to amortise
-    launch / protocol latency; fewer, larger collectives also keep RCCL's CU footprint off the
-    GEMMs for longer stretches. Every bucket is padded to a multiple of dp * 64 elements so
-    reduce-scatter shards stay 256-byte aligned.
+  * bucket sizes default to "auto" (comm/buckets.py): 8-32 MB chosen at start-up from a
+    latency / bandwidth timing of the DP group's links, at least 4 buckets per rank, so the first
+    reduce-scatter launches early in backward while each call still amortises its launch /
+    protocol latency. Every bucket is padded to a multiple of dp * 64 elements so reduce-scatter
+    shards stay 256-byte aligned.
 """
 from __future__ import annotations
 
@@ -30,6 +30,8 @@ import torch
 import torch.distributed as dist
 import torch.nn as nn
 
+from ..comm import buckets as _buckets
+from ..comm import stats as _cs
 from ..ops import _ext
 from . import state as ps
 
@@ -74,7 +76,7 @@ class DistributedDataParallel(nn.Module):
         ddp.finish_grad_sync()
     """
 
-    def __init__(self, module: nn.Module, dp_group=None, grad_dtype=torch.float32, bucket_size: int = 40_000_000,
+    def __init__(self, module: nn.Module, dp_group=None, grad_dtype=torch.float32, bucket_size="auto",
                  overlap_grad_reduce: bool = True, use_distributed_optimizer: bool = False,
                  average_in_collective: bool = True, torch_compat: bool = False,
                  overlap_param_gather: bool = False, zero_stage: int = 1):
@@ -118,6 +120,13 @@ class DistributedDataParallel(nn.Module):
         self._syncs = 0
 
         params = [p for p in module.parameters() if p.requires_grad]
+        total = sum(p.numel() for p in {id(p): p for p in params}.values())
+        if bucket_size in (None, "auto", 0):
+            # one bucket per region when nothing is reduced; else sized for this group's links
+            # (comm/buckets.py: 8-32 MB from a start-up latency / bandwidth timing, >= 4 buckets)
+            bucket_size = 40_000_000 if self.dp == 1 else _buckets.auto_bucket_elems(
+                self.dp_group, total, torch.finfo(grad_dtype).bits // 8)
+        self.bucket_size = int(bucket_size)
         seen = set()
         uniq = []
         for p in params:
@@ -307,27 +316,34 @@ class DistributedDataParallel(nn.Module):
         if self.dp == 1:
             return
         view = self.grad_data[b.start:b.end]
+        nb = view.numel() * view.element_size()
         if self.zero:
             s, e = self.shard_range(b)
             out = self.grad_data[s:e]
             h = self.xgmi.reduce_scatter_async(out, view, op="avg") if self.xgmi is not None else None
             if h is not None:
                 b.handle = h
-            elif self.use_avg:
+                _cs.collective("reduce_scatter", self.dp_group, nb, transport="xgmi", events=h.timing())
+                return
+            if self.use_avg:
                 b.handle = dist.reduce_scatter_tensor(out, view, op=dist.ReduceOp.AVG, group=self.dp_group,
                                                       async_op=True)
             else:
                 view.div_(self.dp)
                 b.handle = dist.reduce_scatter_tensor(out, view, group=self.dp_group, async_op=True)
+            _cs.collective("reduce_scatter", self.dp_group, nb, work=b.handle)
         else:
             h = self.xgmi.all_reduce_async(view, op="avg") if self.xgmi is not None else None
             if h is not None:
                 b.handle = h
-            elif self.use_avg:
+                _cs.collective("all_reduce", self.dp_group, nb, transport="xgmi", events=h.timing())
+                return
+            if self.use_avg:
                 b.handle = dist.all_reduce(view, op=dist.ReduceOp.AVG, group=self.dp_group, async_op=True)
             else:
                 view.div_(self.dp)
                 b.handle = dist.all_reduce(view, group=self.dp_group, async_op=True)
+            _cs.collective("all_reduce", self.dp_group, nb, work=b.handle)
 
     # ---------------------------------------------------------------- ZeRO-2 gradient shards
     def bucket_at(self, i: int) -> Bucket:
@@ -377,16 +393,21 @@ class DistributedDataParallel(nn.Module):
         self._store_fresh.discard(b.index)
         out = sh if fresh else torch.empty_like(sh)
         h = self.xgmi.reduce_scatter_async(out, buf, op="avg") if (self.xgmi is not None and self.dp > 1) else None
+        nb = buf.numel() * buf.element_size()
         if self.dp == 1:
             out.copy_(buf)
             handle = None
         elif h is not None:
             handle = h
-        elif self.use_avg:
-            handle = dist.reduce_scatter_tensor(out, buf, op=dist.ReduceOp.AVG, group=self.dp_group, async_op=True)
+            _cs.collective("reduce_scatter", self.dp_group, nb, transport="xgmi", events=h.timing())
         else:
-            buf.div_(self.dp)
-            handle = dist.reduce_scatter_tensor(out, buf, group=self.dp_group, async_op=True)
+            if self.use_avg:
+                handle = dist.reduce_scatter_tensor(out, buf, op=dist.ReduceOp.AVG, group=self.dp_group,
+                                                    async_op=True)
+            else:
+                buf.div_(self.dp)
+                handle = dist.reduce_scatter_tensor(out, buf, group=self.dp_group, async_op=True)
+            _cs.collective("reduce_scatter", self.dp_group, nb, work=handle)
         self._rs_inflight[b.index] = (handle, None if fresh else out)
 
     def bucket_shard_grad(self, b: Bucket) -> torch.Tensor:
@@ -440,7 +461,9 @@ class DistributedDataParallel(nn.Module):
             if st.tp > 1 and st.tp_group is not None:
                 for b in self.buckets:
                     if b.region[2]:
-                        dist.all_reduce(self.bucket_shard_grad(b), group=st.tp_group)
+                        g = self.bucket_shard_grad(b)
+                        with _cs.blocking("all_reduce", st.tp_group, g.numel() * g.element_size()):
+                            dist.all_reduce(g, group=st.tp_group)
             self._reset_pending()
             if self.zero3 is not None:
                 self.zero3.end_of_backward()
@@ -454,7 +477,8 @@ class DistributedDataParallel(nn.Module):
         if st.tp > 1 and st.tp_group is not None:
             for key, (s, e) in self.regions.items():
                 if key[2]:  # sequence-parallel params: sum partial grads over the TP group
-                    dist.all_reduce(self.grad_data[s:e], group=st.tp_group)
+                    with _cs.blocking("all_reduce", st.tp_group, (e - s) * self.grad_data.element_size()):
+                        dist.all_reduce(self.grad_data[s:e], group=st.tp_group)
         self._reset_pending()
 
     XGMI_CHECK_EVERY = 64
@@ -504,8 +528,13 @@ class DistributedDataParallel(nn.Module):
             s, e = self.shard_range(b)
             full, mine = self.param_data[b.start:b.end], self.param_data[s:e]
             h = self.xgmi.all_gather_async(full, mine) if self.xgmi is not None else None
-            b.ag_handle = h if h is not None else dist.all_gather_into_tensor(full, mine, group=self.dp_group,
-                                                                               async_op=True)
+            nb = full.numel() * full.element_size()
+            if h is not None:
+                b.ag_handle = h
+                _cs.collective("all_gather", self.dp_group, nb, transport="xgmi", events=h.timing())
+            else:
+                b.ag_handle = dist.all_gather_into_tensor(full, mine, group=self.dp_group, async_op=True)
+                _cs.collective("all_gather", self.dp_group, nb, work=b.ag_handle)
         if not self.overlap_param_gather:
             self.wait_param_gather()
 
@@ -513,7 +542,8 @@ class DistributedDataParallel(nn.Module):
         for b in (self.buckets if indices is None else (self.buckets[i] for i in indices)):
             h = getattr(b, "ag_handle", None)
             if h is not None:
-                h.wait()
+                with _cs.waiting("dp"):
+                    h.wait()
                 b.ag_handle = None
 
     def _make_gather_wait(self, indices):

@@ -28,6 +28,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..comm import relay as _relay
+from ..comm import stats as _cs
 from ..ops import _ext
 from ..ops import functional as SF
 from . import state as ps
@@ -44,14 +45,25 @@ def _tp_group():
     return ps.get_state().tp_group
 
 
+def _nbytes(t):
+    return t.numel() * t.element_size()
+
+
 def _all_reduce(x, group, async_op=False):
     if dist.get_world_size(group) == 1:
         return None
     if not async_op:
         eng = ps.xgmi_engine(group)  # xGMI IPC all-reduce (comm/xgmi.py) when enabled for the group
-        if eng is not None and eng.all_reduce(x):
-            return None
-    return dist.all_reduce(x, group=group, async_op=async_op)
+        if eng is not None and eng.use["all_reduce"] and eng.fits(x):
+            with _cs.blocking("all_reduce", group, _nbytes(x), "xgmi"):
+                done = eng.all_reduce(x)
+            if done:
+                return None
+        with _cs.blocking("all_reduce", group, _nbytes(x)):
+            return dist.all_reduce(x, group=group)
+    h = dist.all_reduce(x, group=group, async_op=True)
+    _cs.collective("all_reduce", group, _nbytes(x), work=h)
+    return h
 
 
 def _gather_dim0(x, group):
@@ -59,7 +71,8 @@ def _gather_dim0(x, group):
     if ws == 1:
         return x
     out = torch.empty((x.shape[0] * ws,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
-    dist.all_gather_into_tensor(out, x.contiguous(), group=group)
+    with _cs.blocking("all_gather", group, _nbytes(out)):
+        dist.all_gather_into_tensor(out, x.contiguous(), group=group)
     return out
 
 
@@ -69,8 +82,24 @@ def _reduce_scatter_dim0(x, group, async_op=False):
         return x, None
     assert x.shape[0] % ws == 0, "sequence length must divide the TP size"
     out = torch.empty((x.shape[0] // ws,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
-    h = dist.reduce_scatter_tensor(out, x.contiguous(), group=group, async_op=async_op)
+    if not async_op:
+        with _cs.blocking("reduce_scatter", group, _nbytes(x)):
+            dist.reduce_scatter_tensor(out, x.contiguous(), group=group)
+        return out, None
+    h = dist.reduce_scatter_tensor(out, x.contiguous(), group=group, async_op=True)
+    _cs.collective("reduce_scatter", group, _nbytes(x), work=h)
     return out, h
+
+
+def _wait_works(works, group):
+    """Wait (on the current stream) for in-flight works of ``group``'s collectives."""
+    if not _cs._ON:
+        for w in works:
+            w.wait()
+        return
+    with _cs.waiting(_cs.axis_of(group)):
+        for w in works:
+            w.wait()
 
 
 def _split_dim(x, dim, group):
@@ -415,7 +444,7 @@ class LinearWithGradAccumulationAndAsyncCommunication(torch.autograd.Function):
         else:
             gi_out = gi
             if ctx.async_ar and tp > 1:
-                handle = dist.all_reduce(gi_out, group=group, async_op=True)
+                handle = _all_reduce(gi_out, group, async_op=True)
         g2 = g.reshape(-1, g.shape[-1])
         t2 = total.reshape(-1, total.shape[-1])
         dw = _wgrad(weight, g2, t2)
@@ -423,7 +452,7 @@ class LinearWithGradAccumulationAndAsyncCommunication(torch.autograd.Function):
         if handle is not None:
             # the collective is in flight: run the queued weight-gradient GEMMs beside it
             DEFERRED_WGRAD.flush()
-            handle.wait()
+            _wait_works([handle], group)
         return gi_out, dw, db, None, None
 
 
@@ -465,9 +494,12 @@ def _exchange(send, recv, nxt, prv, group):
         if eng is not None:
             h = eng.exchange_async(send, recv)
             if h is not None:
+                _cs.collective("p2p", group, _nbytes(send), transport="relay", events=h.timing())
                 return [h]
-    return dist.batch_isend_irecv([dist.P2POp(dist.isend, send, nxt, group),
-                                   dist.P2POp(dist.irecv, recv, prv, group)])
+    works = dist.batch_isend_irecv([dist.P2POp(dist.isend, send, nxt, group),
+                                    dist.P2POp(dist.irecv, recv, prv, group)])
+    _cs.collective("p2p", group, _nbytes(send), work=works[0] if len(works) == 1 else None)
+    return works
 
 
 def _mm_into(dst, a, w, bias=None):
@@ -498,8 +530,7 @@ def ag_ring(x, group, chunk_fn=None, before_last_wait=None):
         if works is not None:
             if s == ws - 2 and before_last_wait is not None:
                 before_last_wait()
-            for w in works:
-                w.wait()
+            _wait_works(works, group)
     return total
 
 
@@ -515,8 +546,7 @@ def rs_ring(partial_fn, group, before_last_wait=None):
         if works is not None:
             if s == ws - 1 and before_last_wait is not None:
                 before_last_wait()
-            for w in works:
-                w.wait()
+            _wait_works(works, group)
             part = part.add_(incoming)
         if s == ws - 1:
             return part

@@ -196,7 +196,7 @@ _GROUPS = {
         ("--empty-unused-memory-level", dict(default=0, type=int, choices=[0, 1, 2])),
         ("--standalone-embedding-stage", dict(action="store_true")),
         ("--use-distributed-optimizer", dict(action="store_true")),
-        ("--ddp-bucket-size", dict(type=int, default=40_000_000)),
+        ("--ddp-bucket-size", dict(type=int, default=None)),  # None: auto (comm/buckets.py)
     ],
     "validation": [
         ("--eval-iters", dict(type=int, default=100)),

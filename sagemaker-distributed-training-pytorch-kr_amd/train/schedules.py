@@ -16,6 +16,7 @@ from typing import Callable, List, Optional
 import torch
 import torch.distributed as dist
 
+from ..comm import stats as _cs
 from ..parallel import state as ps
 
 
@@ -152,14 +153,16 @@ def _finish_recv(t):
         # one p2p group may carry both receives: its works are waited exactly once (a second
         # wait on a retired gloo send blocks for a send that never comes)
         works, holder[0] = holder[0], None
-        for w in works:
-            w.wait()
+        with _cs.waiting("pp"):
+            for w in works:
+                w.wait()
     t._smdt_works = None
     full_shape = getattr(t, "_smdt_sg_shape", None)
     if full_shape is not None:
         st = ps.get_state()
         full = torch.empty((t.numel() * st.tp,), dtype=t.dtype, device=t.device)
-        dist.all_gather_into_tensor(full, t.detach(), group=st.tp_group)
+        with _cs.blocking("all_gather", st.tp_group, full.numel() * full.element_size()):
+            dist.all_gather_into_tensor(full, t.detach(), group=st.tp_group)
         out = full.view(full_shape).requires_grad_(True)
         t._smdt_sg_shape = None
         t._smdt_full = out
@@ -204,6 +207,9 @@ def _p2p(send_next=None, send_prev=None, recv_next_shape=None, recv_prev_shape=N
     if not ops:
         return rp, rn
     works = dist.batch_isend_irecv(ops)
+    if _cs._ON:
+        sent = sum(o.tensor.numel() * o.tensor.element_size() for o in ops if o.op is dist.isend)
+        _cs.collective("p2p", st.pp_group, sent, work=works[0] if len(works) == 1 else None)
     if rp is None and rn is None:
         _INFLIGHT_SENDS.extend(works)        # send-only: retired at the end of the schedule
         return rp, rn
@@ -217,8 +223,9 @@ def _p2p(send_next=None, send_prev=None, recv_next_shape=None, recv_prev_shape=N
 
 
 def _retire_sends():
-    while _INFLIGHT_SENDS:
-        _INFLIGHT_SENDS.pop().wait()
+    with _cs.waiting("pp"):
+        while _INFLIGHT_SENDS:
+            _INFLIGHT_SENDS.pop().wait()
 
 
 def _drop_output(out):

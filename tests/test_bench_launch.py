@@ -1,6 +1,7 @@
-"""bench.py itself under torch.distributed.run with 8 gloo ranks on CPU (tiny shapes): the 8-rank
-path the driver launches on an 8-GPU node starts, runs the BASELINE layout (tp2 pp2 dp2 + SP) and
-the DP layout, and rank 0 prints one well-formed JSON line."""
+"""bench.py itself under torch.distributed.run with 2 / 4 / 8 gloo ranks on CPU (tiny shapes): the
+paths the driver launches on an 8-GPU node start, run their layouts (DP + ZeRO-1 at N = 2 / 4, the
+BASELINE tp2 pp2 dp2 + SP at N = 8, DP at N = 8), and rank 0 prints one well-formed JSON line whose
+``phase_ms`` accounts for the measured step."""
 import argparse
 import json
 import os
@@ -26,29 +27,62 @@ def _ns(**kw):
 def test_choose_layout_per_world_size():
     import bench
     assert bench.choose_layout(_ns(), 1) == (1, 1, False, 32, 1)
-    assert bench.choose_layout(_ns(), 2) == (2, 1, True, 64, 1)
-    assert bench.choose_layout(_ns(), 4) == (2, 2, True, 16, 8)
+    # N = 2 / 4: DP + ZeRO-1 (a tp2 pair shares one xGMI link: link-bound below N = 1, BENCHMARKS.md)
+    assert bench.choose_layout(_ns(), 2) == (1, 1, False, 32, 1)
+    assert bench.choose_layout(_ns(), 4) == (1, 1, False, 32, 1)
     assert bench.choose_layout(_ns(), 8) == (2, 2, True, 16, 8)      # BASELINE config #3
     assert bench.choose_layout(_ns(layout="dp"), 8) == (1, 1, False, 32, 1)
+    assert bench.choose_layout(_ns(layout="tp"), 2) == (2, 1, True, 64, 1)
+    assert bench.choose_layout(_ns(layout="tp"), 4) == (2, 2, True, 16, 8)
     tp, pp, sp, mbs, ga = bench.choose_layout(_ns(), 8)
     assert (pp - 1) / ga <= 0.2                                      # 1F1B bubble
     assert mbs * ga * 8 // (tp * pp) == 32 * 8                       # weak scaling: 32 seqs / GPU
 
 
-@pytest.mark.slow
-@pytest.mark.parametrize("layout,want", [("baseline", "tp2pp2dp2+sp+zero1"), ("dp", "tp1pp1dp8+zero1")])
-def test_bench_eight_ranks_gloo(layout, want, tmp_path):
+def _run_bench(n, layout, tmp_path, extra=()):
     env = dict(os.environ, CUDA_VISIBLE_DEVICES="", MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="1")
     from _dist import free_port
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
            "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.join(ROOT, "bench.py"),
-           "--gpus", "8", "--layout", layout] + TINY
+           "--gpus", str(n), "--layout", layout] + TINY + list(extra)
     r = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout
-    rec = json.loads(lines[0])
-    assert rec["n_gpus"] == 8 and rec["steps"] == 2 and rec["warmup"] == 1
-    assert rec["config"]["parallelism"] == want
-    assert rec["config"]["global_batch"] == 4 * 8
+    return json.loads(lines[0])
+
+
+def _check_phases(rec):
+    ph = rec["phase_ms"]
+    parts = [v for k, v in ph.items() if k not in ("sum", "ms_per_step")]
+    assert all(v >= 0 for v in parts), ph
+    assert abs(sum(parts) - ph["sum"]) < 0.01 * max(1.0, ph["sum"])
+    # the phases (CUDA events on GPU, host clocks on CPU) account for the whole measured step
+    assert abs(ph["sum"] - rec["ms_per_step"]) <= 0.10 * rec["ms_per_step"], (ph, rec["ms_per_step"])
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("n,layout,want", [
+    (2, "baseline", "tp1pp1dp2+zero1"),
+    (4, "baseline", "tp1pp1dp4+zero1"),
+    (8, "baseline", "tp2pp2dp2+sp+zero1"),
+    (8, "dp", "tp1pp1dp8+zero1"),
+])
+def test_bench_ranks_gloo(n, layout, want, tmp_path):
+    """The driver's N = 2 / 4 / 8 launches (gloo on CPU): one JSON line naming the layout, with a
+    phase breakdown that sums to the step and per-axis collective accounting."""
+    rec = _run_bench(n, layout, tmp_path)
+    assert rec["n_gpus"] == n and rec["steps"] == 2 and rec["warmup"] == 1
+    assert rec["config"]["parallelism"] == want and rec["config"]["layout"] == layout
+    assert rec["config"]["global_batch"] == 4 * n
     assert rec["value"] > 0 and rec["final_loss"] > 0
+    _check_phases(rec)
+    comm = rec["comm"]
+    assert "dp" in comm and comm["dp"]["MB"] > 0
+    ops = comm["dp"]["ops"]
+    assert any(k.startswith("reduce_scatter/") for k in ops) and any(k.startswith("all_gather/") for k in ops)
+    assert rec["config"]["ddp_bucket"]["count"] >= 1
+    if "tp2" in want:
+        assert comm["tp"]["calls"] > 0 and comm["pp"]["calls"] > 0
+        assert set(rec["phase_ms_by_pp_stage"]) == {"0", "1"}
+        assert rec["phase_ms"]["tp_exchange_wait"] >= 0 and rec["phase_ms"]["pp_p2p_wait_and_bubble"] > 0
