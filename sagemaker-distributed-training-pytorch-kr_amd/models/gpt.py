@@ -145,8 +145,10 @@ class GPTModel(nn.Module):
         st = ps.get_state()
         w = self.output_weight if self.output_weight is not None else self.embedding.weight
         return (self.cfg.fused_lm_head_ce and os.environ.get("SMDT_FUSED_LM_CE", "1") == "1" and st.tp == 1
-                and not self.sp and h.is_cuda and _ext.use_kernels(h) and h.dtype in (torch.bfloat16, torch.float16)
+                and not self.sp and h.is_cuda and _ext.use_kernels(h) and h.dtype == torch.bfloat16
                 and w.dtype == h.dtype and w.shape[0] % 8 == 0)
+        # bf16 only: the head forms w_t * (softmax - onehot) and dH in the activation dtype during
+        # forward, before the loss scale exists; in fp16 those ~1e-10 products flush to zero.
 
     def forward(self, tokens, position_ids=None, attention_mask=None, labels=None, loss_mask=None):
         """``loss_mask`` [b, s] (optional): the per-token weights of the caller's loss reduction

@@ -97,6 +97,11 @@ def save_checkpoint(iteration: int, model, optimizer=None, scheduler=None, args=
         if extra:
             sd.update(extra)
         _atomic_save(sd, os.path.join(d, "model_optim_rng.pt"))
+    if st.cp > 1 and st.dp_rank == 0 and st.cp_rank > 0 and not no_rng:
+        # Context-parallel ranks run shifted Philox streams (parallel/random.py): each keeps its own
+        # so a resumed run draws the same dropout masks as one that never stopped.
+        _atomic_save({"iteration": iteration, "rng_state": _rng_for_save()},
+                     os.path.join(d, f"rng_cp{st.cp_rank:03d}.pt"))
     if zero and not no_optim:
         _atomic_save({"iteration": iteration, "optimizer": optimizer.state_dict()},
                      os.path.join(d, f"distrib_optim_dp{st.dp_cp_rank:03d}.pt"))
@@ -174,8 +179,13 @@ def load_checkpoint(model, optimizer=None, scheduler=None, args=None, load_dir: 
         sync = getattr(optimizer, "reload_model_params", None)
         if sync is not None:
             sync()
-    if "rng_state" in sd and not (finetune or no_load_rng or release):
-        r = dict(sd["rng_state"])
+    st = ps.get_state()
+    rng_src = sd
+    if st.cp > 1 and st.cp_rank > 0:
+        p = os.path.join(d, f"rng_cp{st.cp_rank:03d}.pt")
+        rng_src = torch.load(p, map_location="cpu", weights_only=True) if os.path.isfile(p) else {}
+    if "rng_state" in rng_src and not (finetune or no_load_rng or release):
+        r = dict(rng_src["rng_state"])
         rs = {k: v for k, v in r.items() if k in ("default", "tp", "torch_cpu", "torch_cuda")}
         if "numpy_keys" in r:  # data-side randomness (shuffles, augmentation) resumes too
             import numpy as np

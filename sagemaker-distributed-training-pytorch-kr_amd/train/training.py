@@ -142,17 +142,26 @@ def setup_model_and_optimizer(model_provider_func, args):
     opt = MixedPrecisionAdam(ddp, lr=args.lr, betas=(args.adam_beta1, args.adam_beta2), eps=args.adam_eps,
                              weight_decay=args.weight_decay, adamw=True, clip_grad=args.clip_grad,
                              loss_scaler=scaler)
-    if args.train_iters:
+    if args.train_samples:
+        # Sample-based training (Megatron's rule, also under --rampup-batch-size, where
+        # initialize_megatron derived train_iters): warmup / decay are counted in SAMPLES and the
+        # scheduler advances by each step's global batch, so a ramping batch warms up correctly.
+        decay = args.lr_decay_samples or args.train_samples
+        warm = args.lr_warmup_samples or 0
+        if args.lr_warmup_fraction is not None:
+            warm = int(args.lr_warmup_fraction * decay)
+        wd_steps = args.train_samples
+        args.lr_step_unit = "samples"
+    else:
         decay = args.lr_decay_iters or args.train_iters
         warm = args.lr_warmup_iters
         if args.lr_warmup_fraction is not None:
             warm = int(args.lr_warmup_fraction * decay)
-    else:
-        decay = (args.lr_decay_samples or args.train_samples) // args.global_batch_size
-        warm = (args.lr_warmup_samples or 0) // args.global_batch_size
+        wd_steps = args.train_iters or decay
+        args.lr_step_unit = "iterations"
     sched = OptimizerParamScheduler(opt, args.lr, args.min_lr, warm, decay, args.lr_decay_style,
                                     args.start_weight_decay, args.end_weight_decay,
-                                    args.train_iters or decay, args.weight_decay_incr_style,
+                                    wd_steps, args.weight_decay_incr_style,
                                     args.use_checkpoint_opt_param_scheduler, args.override_opt_param_scheduler)
     args.iteration = 0
     args.consumed_train_samples = 0
@@ -316,7 +325,8 @@ def train_step(forward_step_func, data_iterator, model, optimizer, scheduler, ar
     allreduce_word_embedding_grads(unwrap_model(model))
     timers("forward-backward").stop()
     timers("optimizer", log_level=1).start(barrier=args.barrier_with_L1_time)
-    lr = scheduler.step(1)
+    samples = getattr(args, "lr_step_unit", "iterations") == "samples"
+    lr = scheduler.step(getattr(args, "current_global_batch_size", args.global_batch_size) if samples else 1)
     grad_norm = optimizer.step(lr)
     timers("optimizer").stop()
     out = {}

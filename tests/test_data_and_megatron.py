@@ -182,6 +182,7 @@ def test_pretrain_gpt_rampup_batch_size(tmp_path):
     args = ["--num-layers", "2", "--hidden-size", "64", "--num-attention-heads", "4", "--seq-length", "64",
             "--max-position-embeddings", "64", "--micro-batch-size", "2", "--global-batch-size", "8",
             "--rampup-batch-size", "2", "2", "24", "--train-samples", "60", "--lr", "0.001",
+            "--lr-warmup-samples", "24", "--lr-decay-style", "constant",
             "--mock-data", "--log-interval", "1", "--eval-interval", "1000", "--eval-iters", "1",
             "--vocab-size", "512", "--tokenizer-type", "NullTokenizer"]
     env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT="29539")
@@ -193,6 +194,11 @@ def test_pretrain_gpt_rampup_batch_size(tmp_path):
     assert gbs[0] == 2 and gbs[-1] == 8 and gbs == sorted(gbs) and {2, 4, 6, 8} <= set(gbs), gbs
     assert cons[-1] >= 60 and cons[-2] < 60, cons
     assert "batch size rampup starting from global batch size 2" in r.stdout
+    # the LR warms up over 24 SAMPLES, stepped by each iteration's (ramping) global batch
+    lrs = [float(x) for x in re.findall(r"learning rate:\s+([0-9.eE+-]+)", r.stdout)]
+    assert abs(lrs[0] - 0.001 * 2 / 24) < 1e-7, lrs
+    assert abs(lrs[1] - 0.001 * 4 / 24) < 1e-7, lrs   # batch 2 for the first 8 samples
+    assert lrs[-1] == 0.001 and lrs == sorted(lrs), lrs
 
 
 def test_tensorboard_event_file_format(tmp_path):

@@ -183,6 +183,15 @@ def test_gpt_context_parallel_matches_single_rank(tp, cp, sp, over, ddp):
         _check_tp_grads(ref, grads, meta, tp)
 
 
+def test_context_parallel_rng_resume(tmp_path):
+    """every CP rank restores its own (shifted) RNG streams from a checkpoint, so dropout
+    masks after a resume match an uninterrupted run and stay decorrelated across CP ranks."""
+    outs = run_workers(W.cp_rng_resume_worker, 2, str(tmp_path))
+    assert sorted(o["cp_rank"] for o in outs) == [0, 1]
+    assert all(o["same"] for o in outs), outs
+    assert outs[0]["mask"] != outs[1]["mask"]
+
+
 @pytest.mark.parametrize("world,tp,pp,nmb,zero,defer,sp", [
     (2, 1, 1, 2, False, False, False),   # dp2 x GA2 (no_sync micro-batch, then the sync pass)
     (2, 1, 1, 2, True, True, False),     # dp2 x GA2, ZeRO reduce-scatter, deferred grouped wgrad
