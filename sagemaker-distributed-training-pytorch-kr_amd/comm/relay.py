@@ -17,6 +17,13 @@ exchange at the message sizes it will carry — the decision is made at run time
 the real links, agreed by all ranks, and logged. ``SMDT_TP_RELAY=0`` turns it off, ``=1`` skips
 the speed test (correctness is always checked).
 
+Timeouts: every wait of the relay kernel gives up after ``spin_limit`` polls of an uncached word
+(default 2^22, i.e. seconds; ``set_spin_limit``), NaN-fills and sets a sticky error word. That
+bound is far above any collective, but a host stall of seconds on one partner (a slow filesystem,
+a rank-local evaluation) can reach it; the health monitor (comm/health.py) then agrees on the error
+over the world at the next step boundary and switches every engine off — the run continues on RCCL
+p2p, the step that saw NaN activations is skipped by found-inf. Nothing stays poisoned.
+
 The reference's TP collectives are stock NCCL; there is nothing to port.
 """
 from __future__ import annotations
@@ -30,6 +37,7 @@ import torch
 import torch.distributed as dist
 
 from ..ops import _ext
+from . import health
 from .xgmi import IpcEngine, _EventHandle, _timing_event
 
 DEFAULT_SLOT_BYTES = 8 << 20      # per (flow, parity): parts of up to 4 MB -> 32 MB per call on 8 GPUs
@@ -88,6 +96,11 @@ class XgmiRelay(IpcEngine):
         if validate and not self._validate():
             self.close()
             raise RuntimeError("xGMI relay failed its validation against RCCL p2p")
+        health.register(self)
+
+    _WORD_OFFSET = "relay_word_offset"
+    # [s / tp, mbs, h] bf16 = 512 x 16 x 1024 x 2 B at the N = 8 bench layout (tp2, mbs 16)
+    RING_CHUNK_BYTES = 16 << 20
 
     # ------------------------------------------------------------------ helpers
     def _rccl_exchange(self, send, recv):
@@ -108,8 +121,10 @@ class XgmiRelay(IpcEngine):
         dev = torch.device("cuda", torch.cuda.current_device())
         good = True
         big = self.world * self.slot // 2 // 4 + 4096  # fp32 elements: more than one call
-        for n, dt in ((4096, torch.float32), (1000 * 8 + 8, torch.bfloat16), (big, torch.float32)):
-            for rep in range(3):
+        ring = self.RING_CHUNK_BYTES // 2              # bf16: one SP ring chunk of the N = 8 bench
+        for n, dt, reps in ((4096, torch.float32, 3), (1000 * 8 + 8, torch.bfloat16, 3), (big, torch.float32, 3),
+                            (ring, torch.bfloat16, 1)):
+            for rep in range(reps):
                 x = ((torch.arange(n, device=dev, dtype=torch.float32) % 251) + 1000.0 * self.rank + rep).to(dt)
                 ref = torch.empty_like(x)
                 self._rccl_exchange(x, ref)
@@ -213,10 +228,12 @@ class XgmiRelay(IpcEngine):
 
 
 def check_all():
-    """Raise if any registered relay engine's partner timed out (synchronises; call at logging
-    points, not per step)."""
+    """Raise if an ACTIVE relay engine's partner timed out (synchronises; call at logging points,
+    not per step). An engine the health monitor already switched off (comm/health.py) is skipped:
+    its error was handled by falling back to RCCL."""
     for eng in list(_ENGINES.values()):
-        eng.check()
+        if eng.active:
+            eng.check()
 
 
 def create_for_pairs(pair_group, log=print) -> Optional[XgmiRelay]:

@@ -40,6 +40,7 @@ import torch
 import torch.distributed as dist
 
 from ..ops import _ext
+from . import health
 
 # One-shot reads (W-1) full copies per rank; two-shot moves 2/W of the message per link but pays a
 # second barrier. Crossover chosen for 7 x ~64 GB/s-per-direction links vs ~5 us per barrier.
@@ -174,6 +175,29 @@ class IpcEngine:
             raise RuntimeError(f"xGMI IPC setup failed on some rank ({err!r} here)")
         return ptrs
 
+    _WORD_OFFSET = "ar_word_offset"
+
+    def _word(self, which: int) -> torch.Tensor:
+        """Word ``which`` (0 sticky error, 1 spin limit) of this rank's signal buffer, as a device
+        tensor aliasing the uncached memory."""
+        return self.C.signal_word(self._sig, getattr(self.C, self._WORD_OFFSET)(which))
+
+    def error_tensor(self) -> torch.Tensor:
+        if getattr(self, "_err_t", None) is None:
+            self._err_t = self._word(0)
+        return self._err_t
+
+    def set_spin_limit(self, polls: int):
+        """Polls of a peer flag before a wait gives up (0: the kernel default, ~seconds). Tests lower
+        it to inject a timeout."""
+        self._word(1).fill_(int(polls))
+        torch.cuda.synchronize()
+
+    def deactivate(self, reason: str = ""):
+        """Stop taking calls (callers fall back to RCCL); buffers stay mapped until ``close``."""
+        self.active = False
+        self.deactivated = reason or "deactivated"
+
     def _agree(self, ok: bool) -> bool:
         # gloo groups (multi-process tests on one GPU) agree on the host; RCCL on the device
         on_host = dist.get_backend(self._ipc_group) == "gloo"
@@ -227,21 +251,42 @@ class XgmiAllReduce(IpcEngine):
         if validate and not self._validate():
             self.close()
             raise RuntimeError("xGMI all-reduce failed its validation against RCCL")
+        health.register(self)
 
     # ------------------------------------------------------------------ helpers
+    VALIDATE_BUCKET_BYTES = 32 << 20     # the largest DP bucket comm/buckets.py picks
+
     def _validate(self) -> bool:
-        """Exact check against RCCL on integer-valued fp32 data (order-independent sums), one
-        one-shot and one two-shot size, run twice so both buffer halves are exercised."""
+        """Exact check against RCCL on integer-valued data (order-independent sums) at the sizes
+        and modes training sends: one-shot and two-shot all-reduce (twice, both buffer halves), an
+        all-reduce 1.5x the staging region (chunked), and an fp32 reduce-scatter (in place, the
+        ZeRO pattern) plus a bf16 all-gather at the largest gradient-bucket size, which cross a
+        region band when the region is smaller than the bucket."""
         dev = torch.device("cuda", torch.cuda.current_device())
-        good = True
-        n2 = ONE_SHOT_MAX_BYTES[self.world] // 4 * 2 + 1024
-        for n in (4096, min(n2, self.region // 4)):
-            for rep in range(2):
+        W, good = self.world, True
+        n2 = ONE_SHOT_MAX_BYTES[W] // 4 * 2 + 1024
+        big = self.region * 3 // 2 // 4 // 16 * 16 + 16
+        for n, reps in ((4096, 2), (min(n2, self.region // 4), 2), (big, 1)):
+            for rep in range(reps):
                 x = (torch.arange(n, device=dev, dtype=torch.float32) % 97) + 1000.0 * self.rank + rep
                 ref = x.clone()
                 dist.all_reduce(ref, group=self.group)
                 self.all_reduce(x)
                 good &= bool(torch.equal(x, ref))
+        ns = self.VALIDATE_BUCKET_BYTES // 4 // W // 64 * 64
+        full = (torch.arange(W * ns, device=dev, dtype=torch.float32) % 89) + 7.0 * self.rank
+        want = full.clone()
+        dist.all_reduce(want, group=self.group)
+        mine = full.view(W, ns)[self.rank]
+        if self.reduce_scatter(mine, full):
+            good &= bool(torch.equal(mine, want.view(W, ns)[self.rank]))
+        nb = self.VALIDATE_BUCKET_BYTES // 2 // W // 64 * 64
+        part = ((torch.arange(nb, device=dev, dtype=torch.float32) % 251) + 256.0 * self.rank).to(torch.bfloat16)
+        ref_ag = torch.empty(W * nb, device=dev, dtype=torch.bfloat16)
+        dist.all_gather_into_tensor(ref_ag, part, group=self.group)
+        got = torch.empty_like(ref_ag)
+        if self.all_gather(got, part):
+            good &= bool(torch.equal(got, ref_ag))
         torch.cuda.synchronize()
         good &= self.error() == 0
         return self._agree(good)

@@ -493,6 +493,15 @@ int64_t ipc_open(pybind11::bytes handle) {
 
 void ipc_close(int64_t p) { check(smdt_ipc_close(vp(p)), "ipc_close"); }
 
+// One uint32 word of an engine's (uncached) signal buffer as an int32 tensor aliasing device
+// memory: the DDP reads the sticky error word back asynchronously (no host sync in the step), and
+// tests lower the spin limit to inject a timeout. The tensor does not own the memory.
+Tensor signal_word(int64_t sig, int64_t byte_offset) {
+  TORCH_CHECK(sig != 0 && byte_offset >= 0 && byte_offset % 4 == 0, "signal_word: bad pointer / offset");
+  auto opts = torch::TensorOptions().dtype(torch::kInt32).device(torch::kCUDA, c10::hip::current_device());
+  return torch::from_blob(static_cast<char*>(vp(sig)) + byte_offset, {1}, opts);
+}
+
 int64_t ar_read_error(int64_t sig) {
   int e = 0;
   check(smdt_ar_read_error(vp(sig), &e), "ar_read_error");
@@ -694,6 +703,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("ipc_open", &ipc_open);
   m.def("ipc_close", &ipc_close);
   m.def("ar_read_error", &ar_read_error);
+  m.def("signal_word", &signal_word, py::arg("sig"), py::arg("byte_offset"));
+  m.def("ar_word_offset", &smdt_ar_word_offset);
+  m.def("relay_word_offset", &smdt_relay_word_offset);
   m.def("ar_signal_bytes", &smdt_ar_signal_bytes);
   m.def("ar_max_blocks", &smdt_ar_max_blocks);
   m.def("xgmi_allreduce", &xgmi_allreduce, py::arg("input"), py::arg("out"), py::arg("data_ptrs"), py::arg("sig_ptrs"),

@@ -127,6 +127,7 @@ hipError_t smdt_ipc_get_handle(void* ptr, void* handle_out);
 hipError_t smdt_ipc_open(const void* handle, void** ptr);
 hipError_t smdt_ipc_close(void* ptr);
 hipError_t smdt_ar_read_error(void* sig, int* err);
+int64_t smdt_ar_word_offset(int which);
 // out = scale * sum over ranks of in (n elements, n * esize % 16 == 0). data_ptrs / sig_ptrs: the
 // world ranks' staging (4 x region_bytes) and signal buffers. nranks_local > 1 = loopback: ranks
 // rank .. rank + nranks_local - 1 in one launch, in/out strided by io_stride elements per rank.
@@ -149,6 +150,7 @@ hipError_t smdt_xgmi_collective(int mode, int dtype, const void* in, void* out, 
 int64_t smdt_relay_signal_bytes();
 int smdt_relay_max_sub();
 hipError_t smdt_relay_read_error(void* sig, int* err);
+int64_t smdt_relay_word_offset(int which);
 hipError_t smdt_xgmi_relay(int dtype, const void* in, void* out, int64_t in_rank_stride, int64_t out_rank_stride,
                            int64_t n, void* const* stage_ptrs, void* const* sig_ptrs, const int* partners, int world,
                            int rank, int nranks_local, int64_t slot_bytes, int sub, uint32_t epoch, hipStream_t st);

@@ -65,7 +65,8 @@ struct SignalBuf {
   uint32_t flag[kMaxBlocks][kMaxRanks];  // flag[b][src]: written remotely by rank src's block b
   uint32_t counter[kMaxBlocks];          // this rank's call counter per block (local only)
   uint32_t error;                        // != 0: a spin timed out (sticky)
-  uint32_t pad[3];
+  uint32_t spin_limit;                   // polls before giving up (0: kSpinLimit); set by the host
+  uint32_t pad[2];
 };
 
 struct Peers {
@@ -81,11 +82,13 @@ using xg::u32x4;
 // Poll my own flag word until it reaches `epoch`; give up when the sticky error is set or the
 // spin limit runs out (then set the error). Returns false on failure.
 __device__ __forceinline__ bool wait_ge(SignalBuf* me, const uint32_t* f, uint32_t epoch) {
+  const uint32_t lim0 = load_sys(&me->spin_limit);
+  const uint32_t lim = lim0 != 0u ? lim0 : kSpinLimit;
   for (uint32_t spins = 0;; ++spins) {
     const uint32_t v = load_sys(f);
     if ((int32_t)(v - epoch) >= 0) return true;
     if ((spins & 255u) == 255u && load_sys(&me->error) != 0u) return false;
-    if (spins > kSpinLimit) {
+    if (spins > lim) {
       store_sys(&me->error, 1u);
       return false;
     }
@@ -332,6 +335,10 @@ extern "C" {
 int smdt_ar_max_ranks() { return ar::kMaxRanks; }
 int smdt_ar_max_blocks() { return ar::kMaxBlocks; }
 int64_t smdt_ar_signal_bytes() { return (int64_t)sizeof(ar::SignalBuf); }
+// byte offset of a host-visible word of the signal buffer: 0 = sticky error, 1 = spin limit
+int64_t smdt_ar_word_offset(int which) {
+  return which == 0 ? (int64_t)offsetof(ar::SignalBuf, error) : (int64_t)offsetof(ar::SignalBuf, spin_limit);
+}
 int smdt_ipc_handle_bytes() { return (int)sizeof(hipIpcMemHandle_t); }
 
 hipError_t smdt_ipc_malloc(int64_t bytes, int uncached, void** ptr) {

@@ -45,8 +45,9 @@ constexpr uint32_t kSpinLimit = 1u << 22;
 struct SignalBuf {
   uint32_t ready[kMaxRanks][kMaxSub];  // written by my partner's send blocks
   uint32_t freed[kMaxRanks][kMaxSub];  // written by my partner's recv blocks
-  uint32_t error;                      // != 0: a spin timed out (sticky)
-  uint32_t pad[3];
+  uint32_t error;                        // != 0: a spin timed out (sticky)
+  uint32_t spin_limit;                   // polls before giving up (0: kSpinLimit); set by the host
+  uint32_t pad[2];
 };
 
 struct Peers {
@@ -67,11 +68,13 @@ struct Args {
 };
 
 __device__ __forceinline__ bool wait_ge(SignalBuf* me, const uint32_t* f, uint32_t epoch) {
+  const uint32_t lim0 = load_sys(&me->spin_limit);
+  const uint32_t lim = lim0 != 0u ? lim0 : kSpinLimit;
   for (uint32_t spins = 0;; ++spins) {
     const uint32_t v = load_sys(f);
     if ((int32_t)(v - epoch) >= 0) return true;
     if ((spins & 255u) == 255u && load_sys(&me->error) != 0u) return false;
-    if (spins > kSpinLimit) {
+    if (spins > lim) {
       store_sys(&me->error, 1u);
       return false;
     }
@@ -192,6 +195,9 @@ using namespace smdt;
 extern "C" {
 
 int64_t smdt_relay_signal_bytes() { return (int64_t)sizeof(relay::SignalBuf); }
+int64_t smdt_relay_word_offset(int which) {
+  return which == 0 ? (int64_t)offsetof(relay::SignalBuf, error) : (int64_t)offsetof(relay::SignalBuf, spin_limit);
+}
 int smdt_relay_max_sub() { return relay::kMaxSub; }
 
 hipError_t smdt_relay_read_error(void* sig, int* err) {

@@ -26,6 +26,7 @@ from typing import Optional
 import torch
 import torch.distributed as dist
 
+from ..comm import health as _health
 from ..comm import stats as _cs
 from ..ops import _ext
 from ..parallel import state as ps
@@ -123,6 +124,9 @@ class MixedPrecisionAdam:
         self.found_inf = torch.zeros(1, dtype=torch.int32, device=dev)
         self.grad_norm = torch.zeros(1, dtype=torch.float32, device=dev)
         self.param_groups = [{"lr": lr, "weight_decay": weight_decay}]
+        # an xGMI engine that timed out NaN-filled gathered parameters: rewrite them from the
+        # masters and re-gather over RCCL (comm/health.py)
+        _health.on_fallback(self.repair_params)
 
     # ------------------------------------------------------------------ helpers
     def _norm_groups(self):
@@ -227,6 +231,20 @@ class MixedPrecisionAdam:
         if self.zero:
             ddp.all_gather_params()
         return self.grad_norm
+
+    @torch.no_grad()
+    def repair_params(self):
+        """Model-dtype parameters <- fp32 masters for this rank's pieces, then (ZeRO) re-gather the
+        full buffer: undoes NaN-filled parameter gathers after a collective timed out."""
+        ddp = self.ddp
+        if hasattr(ddp, "wait_param_gather"):
+            ddp.wait_param_gather()
+        for (s, e, _), mo in zip(self.pieces, self.master_off):
+            if e > s:
+                ddp.param_data[s:e].copy_(self.master[mo:mo + (e - s)].to(ddp.param_data.dtype))
+        if self.zero:
+            ddp.all_gather_params()
+            ddp.wait_param_gather()
 
     def zero_grad(self, set_to_none=True):
         self.ddp.zero_grad_buffer()

@@ -31,6 +31,7 @@ import torch.distributed as dist
 import torch.nn as nn
 
 from ..comm import buckets as _buckets
+from ..comm import health as _health
 from ..comm import stats as _cs
 from ..ops import _ext
 from . import state as ps
@@ -481,18 +482,17 @@ class DistributedDataParallel(nn.Module):
                         dist.all_reduce(self.grad_data[s:e], group=st.tp_group)
         self._reset_pending()
 
-    XGMI_CHECK_EVERY = 64
-
     def _check_xgmi(self):
-        """Every ``XGMI_CHECK_EVERY`` syncs read the xGMI engine's sticky error word (a peer that
-        never arrived NaN-fills the outputs): raise instead of training on silently."""
-        if self.xgmi is None:
-            return
+        """Once per sync, the engines' sticky error words are agreed over the world without a host
+        sync (comm/health.py): a peer that never arrived (its outputs were NaN-filled, so that step
+        is skipped by found-inf) switches every xGMI engine off and the run continues on RCCL."""
         self._syncs += 1
-        if self._syncs % self.XGMI_CHECK_EVERY == 0:
-            self.xgmi.check()
+        _health.monitor().launch()
 
     def zero_grad_buffer(self):
+        _health.monitor().consume()      # the previous step's engine-error flag (comm/health.py)
+        if self.xgmi is not None and not self.xgmi.active:
+            self.xgmi = None
         if self.zero_stage >= 2:
             for b in self.buckets:
                 self._retire_rs(b)

@@ -713,3 +713,156 @@ def cp_rng_resume_worker(rank, world, save_dir):
     out = {"cp_rank": st.cp_rank, "same": after_save == resumed, "mask": after_save[0]}
     dist.destroy_process_group()
     return out
+
+
+class _FakeXgmi:
+    """Stand-in for comm/xgmi.XgmiAllReduce on gloo: the same call protocol, with a timeout that
+    can be injected — from call ``trip_at`` on, this rank's outputs are NaN-filled and its sticky
+    error word is set, exactly what the kernel does when a peer never arrives."""
+
+    class _H:
+        def wait(self):
+            return True
+
+        def timing(self):
+            return None
+
+    def __init__(self, group, trip_at=None):
+        import torch.distributed as dist
+        self.group, self.trip_at, self.calls, self.active = group, trip_at, 0, True
+        self.ws = dist.get_world_size(group)
+        self.err = torch.zeros(1, dtype=torch.int32)
+
+    def error_tensor(self):
+        return self.err
+
+    def deactivate(self, reason=""):
+        self.active = False
+
+    def _after(self, out):
+        self.calls += 1
+        if self.trip_at is not None and self.calls >= self.trip_at:
+            self.err.fill_(1)
+        if int(self.err[0]):
+            out.fill_(float("nan"))
+        return self._H()
+
+    def reduce_scatter_async(self, out, inp, op="sum"):
+        import torch.distributed as dist
+        if not self.active:
+            return None
+        dist.reduce_scatter_tensor(out, inp, group=self.group)
+        if op == "avg":
+            out.div_(self.ws)
+        return self._after(out)
+
+    def all_gather_async(self, out, inp):
+        import torch.distributed as dist
+        if not self.active:
+            return None
+        dist.all_gather_into_tensor(out, inp.clone(), group=self.group)
+        return self._after(out)
+
+    def all_reduce_async(self, t, op="sum"):
+        import torch.distributed as dist
+        if not self.active:
+            return None
+        dist.all_reduce(t, group=self.group)
+        if op == "avg":
+            t.div_(self.ws)
+        return self._after(t)
+
+
+def xgmi_fallback_worker(rank, world, trip_rank, trip_step, steps=6):
+    """DDP + ZeRO-1 + MixedPrecisionAdam on an engine that times out on ``trip_rank`` in the first
+    gradient reduce-scatter of step ``trip_step`` (1-based): the health monitor must switch every rank to the default transport at the same
+    step, warn once, repair the gathered parameters, and keep every loss finite."""
+    import math
+    import warnings
+    import torch.distributed as dist
+    from smdt_amd.comm import health
+    from smdt_amd.optim.optimizer import MixedPrecisionAdam
+    from smdt_amd.parallel import state as ps
+    from smdt_amd.parallel.distributed import DistributedDataParallel
+    dist.init_process_group("gloo")
+    ps.initialize_model_parallel(1, 1)
+    health.reset()
+    torch.manual_seed(0)
+    model = torch.nn.Sequential(torch.nn.Linear(32, 64), torch.nn.GELU(), torch.nn.Linear(64, 32))
+    ddp = DistributedDataParallel(model, bucket_size=1024, use_distributed_optimizer=True)
+    per_step = 2 * len(ddp.buckets)                   # one reduce-scatter + one all-gather per bucket
+    eng = _FakeXgmi(ddp.dp_group, (trip_step - 1) * per_step + 1 if rank == trip_rank else None)
+    ddp.xgmi = eng
+    health.register(eng)
+    opt = MixedPrecisionAdam(ddp, lr=1e-2, weight_decay=0.0, clip_grad=1.0)
+    gen = torch.Generator().manual_seed(100 + rank)
+    losses, active = [], []
+    with warnings.catch_warnings(record=True) as caught:
+        warnings.simplefilter("always")
+        for _ in range(steps):
+            ddp.zero_grad_buffer()
+            x = torch.randn(8, 32, generator=gen)
+            loss = (ddp(x) - x).pow(2).mean()
+            loss.backward()
+            ddp.finish_grad_sync()
+            opt.step()
+            losses.append(float(loss))
+            active.append(eng.active)
+    params = torch.cat([p.detach().flatten() for p in model.parameters()])
+    gathered = [torch.empty_like(params) for _ in range(world)]
+    dist.all_gather(gathered, params)
+    out = {"losses": losses, "active": active, "events": list(health.EVENTS),
+           "warned": any("timed-out peer" in str(w.message) for w in caught),
+           "finite": all(math.isfinite(v) for v in losses) and bool(torch.isfinite(params).all()),
+           "replicas_equal": all(torch.equal(gathered[0], g) for g in gathered)}
+    dist.destroy_process_group()
+    return out
+
+
+def xgmi_timeout_worker(rank, world, port, outdir):
+    """Real kernel, real IPC (both ranks on cuda:0, gloo carries the handles): rank 0's spin limit is
+    lowered and rank 1 arrives late, so rank 0's call times out — its sticky error word is set
+    (read through the aliasing device tensor), its output is NaN-filled, and the health monitor
+    switches BOTH ranks' engines off at the same step."""
+    import os
+    import pickle
+    import time
+    import traceback
+
+    import torch
+    from smdt_amd.comm import health, xgmi
+
+    os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "RANK": str(rank),
+                       "WORLD_SIZE": str(world)})
+    res = {"err": None}
+    try:
+        import torch.distributed as dist
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        torch.cuda.set_device(0)
+        health.reset()
+        eng = xgmi.XgmiAllReduce(None, region_bytes=4 << 20, blocks=8, validate=False)
+        x = torch.ones(4096, device="cuda")
+        assert eng.all_reduce(x)                      # a healthy call first
+        torch.cuda.synchronize()
+        res["first_ok"] = bool(torch.equal(x, torch.full_like(x, float(world))))
+        if rank == 0:
+            eng.set_spin_limit(2000)                  # ~ms instead of ~seconds
+        dist.barrier()
+        if rank == 1:
+            time.sleep(1.0)                           # arrive long after rank 0 gave up
+        y = torch.ones(4096, device="cuda")
+        eng.all_reduce(y)
+        torch.cuda.synchronize()
+        res["nan_out"] = bool(torch.isnan(y).all())
+        res["error_word"] = int(eng.error_tensor().item())
+        mon = health.monitor()
+        mon.launch()                                  # end of "step k": agree on the flag
+        mon.consume()                                 # start of "step k + 1": fall back
+        res["active_after"] = eng.active
+        res["events"] = list(health.EVENTS)
+        eng.close()
+        dist.destroy_process_group()
+    except Exception:  # reported by the parent
+        res["err"] = traceback.format_exc()
+    with open(os.path.join(outdir, f"r{rank}.pkl"), "wb") as f:
+        pickle.dump(res, f)

@@ -107,3 +107,19 @@ def test_stats_off_is_inert():
     stats.collective("all_reduce", None, 10)
     stats.end_step()
     assert not stats.active()
+
+
+def test_xgmi_timeout_falls_back_to_rccl():
+    """an injected engine timeout on ONE rank (step 2's first reduce-scatter)
+    switches both ranks to the default transport at the same step, with one warning; the failed
+    step is skipped, parameters are repaired, every loss stays finite and the replicas agree."""
+    import dist_workers as W
+    res = run_workers(W.xgmi_fallback_worker, 2, 0, 2)
+    for r, out in enumerate(res):
+        assert out["finite"], out
+        assert out["replicas_equal"], out
+        assert len(out["events"]) == 1 and out["events"][0]["error"] == 1
+        # deactivated at the start of step 3, before its forward, on both ranks
+        assert out["active"] == [True, True, False, False, False, False], out["active"]
+    assert res[0]["active"] == res[1]["active"]
+    assert res[0]["warned"] and not res[1]["warned"]
