@@ -85,6 +85,13 @@ def parse():
     p.add_argument("--hidden-size", type=int, default=1024)
     p.add_argument("--num-attention-heads", type=int, default=16)
     p.add_argument("--vocab-size", type=int, default=50257)
+    # per-rank shape emulation on one GPU (benchmarks/predict_scaling.py): a TP rank's heads / FFN
+    p.add_argument("--kv-channels", type=int, default=None)
+    p.add_argument("--ffn-hidden-size", type=int, default=None)
+    p.add_argument("--emulate-first-stage", action="store_true",
+                   help="(pp = 1 emulation) no LM head: the model outputs hidden states, as pipeline stage 0")
+    p.add_argument("--pp-last-layers", type=int, default=None,
+                   help="layers on the last pipeline stage (default: balanced against the LM head + CE)")
     p.add_argument("--hidden-dropout", type=float, default=0.1)
     p.add_argument("--attention-dropout", type=float, default=0.1)  # Megatron default (reference run)
     p.add_argument("--zero", type=int, default=1, help="ZeRO-1/2 distributed optimizer when DP > 1")
@@ -117,7 +124,8 @@ if os.path.exists(WGRAD_CACHE):
 def model_label(a, vocab):
     """The BASELINE config's name for the default shape; the explicit shape for any other."""
     shape = f"{a.num_layers}L h{a.hidden_size} {a.num_attention_heads}A, vocab {vocab}"
-    if (a.num_layers, a.hidden_size, a.num_attention_heads, a.seq_length) == (24, 1024, 16, 1024):
+    if ((a.num_layers, a.hidden_size, a.num_attention_heads, a.seq_length) == (24, 1024, 16, 1024)
+            and a.kv_channels in (None, 64) and a.ffn_hidden_size in (None, 4096)):
         return f"gpt2-345m ({shape})"
     known = {(12, 768, 12): "gpt2-small", (32, 4096, 32): "gpt3-6.7b"}
     return f"{known.get((a.num_layers, a.hidden_size, a.num_attention_heads), 'gpt')} ({shape}, seq {a.seq_length})"
@@ -150,6 +158,24 @@ def enable_gemm_tuning(a, rank):
     except Exception as e:  # pragma: no cover
         print(f"[bench] TunableOp unavailable: {e!r}", file=sys.stderr)
         return "unavailable"
+
+
+def balanced_last_stage_layers(num_layers, pp, h, s, vocab):
+    """Transformer layers on the last pipeline stage so that it — which also runs the LM head and
+    the cross-entropy — costs what every other stage does. Per token, a layer costs
+    72 h^2 (1 + s / 6h) FLOPs (fwd + bwd) and the head 6 V h (Megatron's formula), i.e.
+    r = V / (12 h (1 + s / 6h)) layers' worth (3.5 for GPT-2 345M): the last stage gets
+    (L - (pp - 1) r) / pp layers, rounded so the other stages split the rest evenly."""
+    r = vocab / (12.0 * h * (1.0 + s / (6.0 * h)))
+    want = (num_layers - (pp - 1) * r) / pp
+    best = None
+    for n in range(1, num_layers - pp + 2):
+        if (num_layers - n) % (pp - 1):
+            continue
+        cost = max(n + r, (num_layers - n) / (pp - 1))
+        if best is None or cost < best[0] - 1e-9 or (abs(cost - best[0]) < 1e-9 and abs(n - want) < abs(best[1] - want)):
+            best = (cost, n)
+    return best[1]
 
 
 # N -> (tp, pp); dp = N / (tp pp)
@@ -194,15 +220,21 @@ def main():
     tuned = enable_gemm_tuning(a, rank)
     dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
     vocab = pad_vocab_size(a.vocab_size, 128, a.tp)
+    last_layers = a.pp_last_layers
+    if last_layers is None and a.pp > 1:
+        last_layers = balanced_last_stage_layers(a.num_layers, a.pp, a.hidden_size, a.seq_length, vocab)
     cfg = TransformerConfig(num_layers=a.num_layers, hidden_size=a.hidden_size,
                             num_attention_heads=a.num_attention_heads, max_position_embeddings=a.seq_length,
                             padded_vocab_size=vocab, hidden_dropout=a.hidden_dropout,
+                            kv_channels=a.kv_channels, ffn_hidden_size=a.ffn_hidden_size,
+                            decoder_last_pipeline_num_layers=last_layers,
                             attention_dropout=a.attention_dropout, params_dtype=torch.bfloat16,
                             sequence_parallel=sp and a.tp > 1, use_flash_attn=not a.no_flash,
                             recompute_granularity="full" if a.recompute == "full" else None,
                             recompute_method="uniform" if a.recompute == "full" else None,
                             fused_lm_head_ce=a.fused_ce)
-    model = GPTModel(cfg, pre_process=st.is_first_stage(), post_process=st.is_last_stage(), device=dev)
+    model = GPTModel(cfg, pre_process=st.is_first_stage(),
+                     post_process=st.is_last_stage() and not a.emulate_first_stage, device=dev)
     zero = bool(a.zero) and st.dp > 1
     ddp = DistributedDataParallel(model, bucket_size=a.bucket_size, use_distributed_optimizer=zero,
                                   overlap_param_gather=zero)
@@ -315,6 +347,8 @@ def main():
                        "parallelism": f"tp{a.tp}pp{a.pp}dp{st.dp}" + ("+sp" if cfg.sequence_parallel else "")
                        + ("+zero1" if zero else ""),
                        "layout": a.layout, "tp": a.tp, "pp": a.pp, "dp": st.dp,
+                       "pp_layers": ([(a.num_layers - last_layers) // (a.pp - 1)] * (a.pp - 1) + [last_layers]
+                                     if a.pp > 1 else [a.num_layers]),
                        "ddp_bucket": {"elements": ddp.bucket_size, "count": len(ddp.buckets),
                                       **comm_buckets.TUNED},
                        "scaling_note": f"weak: {a.seqs_per_gpu} seqs x {S} tokens per GPU per step",

@@ -39,13 +39,24 @@ class GPT2BPETokenizer(AbstractTokenizer):
     name = "GPT2BPETokenizer"
 
     def __init__(self, vocab_file: str, merge_file: str):
+        import inspect
+        import json
         from transformers import GPT2Tokenizer
-        self.tok = GPT2Tokenizer(vocab_file=vocab_file, merges_file=merge_file, errors="replace")
-        self.eod_id = self.tok.convert_tokens_to_ids("<|endoftext|>")
+        with open(vocab_file, encoding="utf-8") as f:
+            self.encoder = json.load(f)
+        params = inspect.signature(GPT2Tokenizer.__init__).parameters
+        if "vocab" in params:   # transformers >= 5: the tokenizers-backed class takes the data itself
+            with open(merge_file, encoding="utf-8") as f:
+                merges = [tuple(ln.split()) for ln in f.read().split("\n")
+                          if ln and not ln.startswith("#version") and len(ln.split()) == 2]
+            self.tok = GPT2Tokenizer(vocab=self.encoder, merges=merges, errors="replace")
+        else:
+            self.tok = GPT2Tokenizer(vocab_file=vocab_file, merges_file=merge_file, errors="replace")
+        self.eod_id = self.encoder.get("<|endoftext|>", self.tok.convert_tokens_to_ids("<|endoftext|>"))
 
     @property
     def vocab_size(self):
-        return len(self.tok.encoder)
+        return len(self.encoder)   # Megatron: len(encoder) of vocab.json (50,257 for GPT-2)
 
     def tokenize(self, text):
         return self.tok.encode(text)

@@ -28,12 +28,29 @@ def pad_vocab_size(orig: int, divisible_by: int = 128, tp_size: int = 1) -> int:
     return ((orig + m - 1) // m) * m
 
 
-def stage_layer_range(num_layers: int, pp: int, pp_rank: int, vpp: Optional[int] = None, vpp_rank: int = 0):
-    """(first_layer, count) for a (virtual) pipeline stage; layers split uniformly."""
+def stage_layer_range(num_layers: int, pp: int, pp_rank: int, vpp: Optional[int] = None, vpp_rank: int = 0,
+                      first: Optional[int] = None, last: Optional[int] = None):
+    """(first_layer, count) for a (virtual) pipeline stage. Layers split uniformly, except that
+    ``first`` / ``last`` (Megatron-core ``--decoder-first/last-pipeline-num-layers``) fix the
+    first / last stage's count and the middle stages share the rest evenly."""
+    if vpp is None and pp > 1 and (first is not None or last is not None):
+        counts = [None] * pp
+        if first is not None:
+            counts[0] = int(first)
+        if last is not None:
+            counts[-1] = int(last)
+        rest = num_layers - sum(c for c in counts if c is not None)
+        free = [i for i, c in enumerate(counts) if c is None]
+        if rest < 0 or (free and rest % len(free)) or (not free and rest != 0):
+            raise ValueError(f"cannot split {num_layers} layers over {pp} stages with first={first} last={last}")
+        for i in free:
+            counts[i] = rest // len(free)
+        return sum(counts[:pp_rank]), counts[pp_rank]
     if vpp is None:
         assert num_layers % pp == 0, "num_layers must be divisible by the pipeline size"
         n = num_layers // pp
         return pp_rank * n, n
+    assert first is None and last is None, "uneven pipeline splits are not supported with virtual stages"
     assert num_layers % (pp * vpp) == 0
     n = num_layers // (pp * vpp)
     return vpp_rank * (num_layers // vpp) + pp_rank * n, n
@@ -49,7 +66,9 @@ class GPTModel(nn.Module):
         self.parallel_output = parallel_output
         self.sp = cfg.sequence_parallel and st.tp > 1
         if layer_range is None:
-            layer_range = stage_layer_range(cfg.num_layers, st.pp, st.pp_rank, st.virtual_pp, st.virtual_pp_rank)
+            layer_range = stage_layer_range(cfg.num_layers, st.pp, st.pp_rank, st.virtual_pp, st.virtual_pp_rank,
+                                            cfg.decoder_first_pipeline_num_layers,
+                                            cfg.decoder_last_pipeline_num_layers)
         first, n = layer_range
         self.first_layer, self.num_local_layers = first, n
         std = cfg.init_method_std

@@ -38,6 +38,10 @@ class TransformerConfig:
     num_query_groups: Optional[int] = None       # GQA (None -> MHA)
     ffn_hidden_size: Optional[int] = None        # default 4h (GeLU) / 8h/3 rounded (SwiGLU)
     kv_channels: Optional[int] = None
+    # uneven pipeline split (Megatron-core --decoder-first/last-pipeline-num-layers): the last
+    # stage also runs the LM head + CE, so giving it fewer layers balances the pipeline
+    decoder_first_pipeline_num_layers: Optional[int] = None
+    decoder_last_pipeline_num_layers: Optional[int] = None
     hidden_dropout: float = 0.1
     attention_dropout: float = 0.1
     layernorm_epsilon: float = 1e-5

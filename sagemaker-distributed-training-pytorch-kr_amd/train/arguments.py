@@ -195,6 +195,8 @@ _GROUPS = {
         ("--use-cpu-initialization", dict(action="store_true", default=None)),
         ("--empty-unused-memory-level", dict(default=0, type=int, choices=[0, 1, 2])),
         ("--standalone-embedding-stage", dict(action="store_true")),
+        ("--decoder-first-pipeline-num-layers", dict(type=int, default=None)),
+        ("--decoder-last-pipeline-num-layers", dict(type=int, default=None)),
         ("--use-distributed-optimizer", dict(action="store_true")),
         ("--ddp-bucket-size", dict(type=int, default=None)),  # None: auto (comm/buckets.py)
     ],
@@ -402,6 +404,8 @@ def core_transformer_config_from_args(args) -> TransformerConfig:
     return TransformerConfig(
         num_layers=args.num_layers, hidden_size=args.hidden_size, num_attention_heads=args.num_attention_heads,
         num_query_groups=args.num_query_groups, ffn_hidden_size=args.ffn_hidden_size, kv_channels=args.kv_channels,
+        decoder_first_pipeline_num_layers=getattr(args, "decoder_first_pipeline_num_layers", None),
+        decoder_last_pipeline_num_layers=getattr(args, "decoder_last_pipeline_num_layers", None),
         hidden_dropout=args.hidden_dropout, attention_dropout=args.attention_dropout,
         layernorm_epsilon=args.layernorm_epsilon, normalization=args.normalization, activation=act,
         add_bias_linear=args.add_bias_linear, position_embedding_type=args.position_embedding_type,

@@ -433,7 +433,8 @@ def train(forward_step_func, model, optimizer, scheduler, train_iter, valid_iter
                 total["nan"] = total.get("nan", 0) + 1
             report_mem = training_log({k: float(v) for k, v in loss_dict.items()}, total, lr, iteration, ls,
                                       report_mem, fi, gn, args, elapsed, model_cfg)
-        if args.eval_interval and iteration % args.eval_interval == 0 and valid_iter is not None and args.do_valid:
+        # (TP ranks > 0 hold no iterator: get_batch broadcasts from TP rank 0, so all ranks evaluate)
+        if args.eval_interval and iteration % args.eval_interval == 0 and args.do_valid:
             evaluate_and_print_results(f"iteration {iteration}", forward_step_func, valid_iter, model, args)
         saved = False
         if args.save and args.save_interval and iteration % args.save_interval == 0:

@@ -49,9 +49,12 @@ def test_tensor_parallel_matches_single_rank(tp, sp):
         _check_tp_grads(ref, grads, meta, tp)
 
 
-def test_pipeline_parallel_matches_single_rank():
-    ref_loss, ref = W.gpt_reference()
-    outs = run_workers(W.gpt_tp_worker, 2, 1, 2, False)
+@pytest.mark.parametrize("over", [None, {"num_layers": 3, "decoder_last_pipeline_num_layers": 1}])
+def test_pipeline_parallel_matches_single_rank(over):
+    """pp = 2, uniform split and the uneven split bench.py uses to balance the LM head (first stage
+    2 layers, last stage 1 layer + head)."""
+    ref_loss, ref = W.gpt_reference(cfg_over=over)
+    outs = run_workers(W.gpt_tp_worker, 2, 1, 2, False, over)
     last = outs[1]
     # last stage sees the per-token losses of both micro-batches
     torch.testing.assert_close(last[0].view(-1), ref_loss.view(-1), atol=2e-4, rtol=2e-4)
