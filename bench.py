@@ -160,13 +160,20 @@ def enable_gemm_tuning(a, rank):
         return "unavailable"
 
 
+HEAD_SPEEDUP = 1.4
+
+
 def balanced_last_stage_layers(num_layers, pp, h, s, vocab):
     """Transformer layers on the last pipeline stage so that it — which also runs the LM head and
     the cross-entropy — costs what every other stage does. Per token, a layer costs
     72 h^2 (1 + s / 6h) FLOPs (fwd + bwd) and the head 6 V h (Megatron's formula), i.e.
-    r = V / (12 h (1 + s / 6h)) layers' worth (3.5 for GPT-2 345M): the last stage gets
-    (L - (pp - 1) r) / pp layers, rounded so the other stages split the rest evenly."""
-    r = vocab / (12.0 * h * (1.0 + s / (6.0 * h)))
+    V / (12 h (1 + s / 6h)) layers' worth of FLOPs (3.5 for GPT-2 345M). The head's three big
+    GEMMs run ``HEAD_SPEEDUP`` times faster per FLOP than a layer's mix of attention, small GEMMs
+    and elementwise kernels (measured on MI355X at the tp2pp2 rank shape: 14 layers 219 ms,
+    10 layers + head 197 ms, profiles/r3_predict/), so the head weighs r = 3.5 / 1.4 = 2.5 layers.
+    The last stage gets (L - (pp - 1) r) / pp layers, rounded so the other stages split the rest
+    evenly: 13 | 11 for GPT-2 345M at pp = 2."""
+    r = vocab / (12.0 * h * (1.0 + s / (6.0 * h))) / HEAD_SPEEDUP
     want = (num_layers - (pp - 1) * r) / pp
     best = None
     for n in range(1, num_layers - pp + 2):

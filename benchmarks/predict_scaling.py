@@ -45,9 +45,9 @@ RUNS = {
     "n1_dp": [],
     # even split: 12 + 12 layers, the last stage also runs the LM head (the heavier stage)
     "tp2pp2_rank": ["--num-layers", "12"] + _TP2 + _MB16,
-    # bench.py's balanced split (balanced_last_stage_layers): 14 layers | 10 layers + LM head
-    "tp2pp2_stage0_bal": ["--num-layers", "14", "--emulate-first-stage"] + _TP2 + _MB16,
-    "tp2pp2_stage1_bal": ["--num-layers", "10"] + _TP2 + _MB16,
+    # bench.py's balanced split (balanced_last_stage_layers): 13 layers | 11 layers + LM head
+    "tp2pp2_stage0_bal": ["--num-layers", "13", "--emulate-first-stage"] + _TP2 + _MB16,
+    "tp2pp2_stage1_bal": ["--num-layers", "11"] + _TP2 + _MB16,
     "tp2_rank": ["--num-attention-heads", "8", "--kv-channels", "64", "--ffn-hidden-size", "2048",
                  "--vocab-size", str(V // 2), "--seqs-per-gpu", "128", "--micro-batch-size", "64",
                  "--grad-accum", "2"],
@@ -91,7 +91,7 @@ def predict(m: dict) -> list:
         rows.append({"N": n, "layout": f"tp1pp1dp{n}+zero1", "compute_ms": t1, "exposed_comm_ms": round(exposed, 2),
                      "bubble_ms": 0.0, "predicted_ms": round(t1 + exposed, 1), "tokens_per_step": tok1 * n,
                      "note": f"{hidden:.1f} ms of RS+AG per step overlapped with backward / next forward"})
-    # tp2 pp2 dp2 + SP (BASELINE at N = 8), with bench.py's balanced 14 | 10 split when measured.
+    # tp2 pp2 dp2 + SP (BASELINE at N = 8), with bench.py's balanced 13 | 11 split when measured.
     tr_even = m["tp2pp2_rank"]["ms_per_step"]
     bal = "tp2pp2_stage0_bal" in m and "tp2pp2_stage1_bal" in m
     tr = max(m["tp2pp2_stage0_bal"]["ms_per_step"], m["tp2pp2_stage1_bal"]["ms_per_step"]) if bal else tr_even
@@ -110,7 +110,7 @@ def predict(m: dict) -> list:
                      "exposed_comm_ms": round(exposed, 2), "bubble_ms": round(tr_even * (pp - 1) / mb, 1),
                      "predicted_ms": round(tr_even * (1 + (pp - 1) / mb) + exposed, 1), "tokens_per_step": tok1 * 8,
                      "note": "the last stage carries 12 layers + the LM head (2x the per-GPU head work of N = 1)"})
-    rows.append({"N": 8, "layout": "tp2pp2dp2+sp+zero1" + (", split 14|10" if bal else ""), "compute_ms": tr,
+    rows.append({"N": 8, "layout": "tp2pp2dp2+sp+zero1" + (", split 13|11" if bal else ""), "compute_ms": tr,
                  "exposed_comm_ms": round(exposed, 2),
                  "bubble_ms": round(bubble, 1), "predicted_ms": round(tr + bubble + exposed, 1),
                  "tokens_per_step": tok1 * 8,

@@ -385,8 +385,13 @@ _WORDS = ("the of and to in is that for it as with was on be by this are or from
 
 
 def write_synthetic_alpaca(path: str, n: int = 52002, seed: int = 0):
-    """Alpaca-shaped synthetic JSON: instruction ~ 13 words, input present 40 % (~ 10 words),
-    output ~ 45 words with a long tail (word counts of the public Alpaca-52K set)."""
+    """Alpaca-shaped synthetic JSON. Word counts follow the public Alpaca-52K set (instruction ~ 13
+    words, input present 40 % ~ 10 words, output ~ 45 words with a long tail), scaled by 1.3 —
+    the BPE tokens per English word of the GPT-2 / LLaMA tokenizers — because the offline
+    tokenizer maps one word to one id. With the prompt template that gives ~125 tokens per example
+    (median ~110, p99 ~360, 0.3 % cut by the ``model_max_length`` 512 cap), like the
+    real set under the reference's tokenizer (/root/reference/4_training_alpaca_deepspeed/
+    train.py:86-89)."""
     rng = random.Random(seed)
 
     def sent(k):
@@ -394,9 +399,9 @@ def write_synthetic_alpaca(path: str, n: int = 52002, seed: int = 0):
 
     data = []
     for _ in range(n):
-        ins = sent(int(rng.gauss(13, 5)))
-        inp = sent(int(rng.expovariate(1 / 10))) if rng.random() < 0.4 else ""
-        out = sent(int(min(rng.lognormvariate(3.5, 0.8), 400)))
+        ins = sent(int(1.3 * rng.gauss(13, 5)))
+        inp = sent(int(1.3 * rng.expovariate(1 / 10))) if rng.random() < 0.4 else ""
+        out = sent(int(1.3 * min(rng.lognormvariate(3.5, 0.8), 600)))
         data.append({"instruction": ins, "input": inp, "output": out})
     jdump(data, path)
     return path

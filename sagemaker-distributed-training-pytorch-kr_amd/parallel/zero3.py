@@ -15,8 +15,10 @@ MI355X-native equivalent, layered on the flat bucketed DDP buffers (parallel/dis
   re-entrant use (activation recompute, the tied LM head inside the root) safe;
 * the order in which buckets are first gathered is traced during the first forward and the
   first backward; later gathers prefetch the next buckets of that trace, up to
-  ``prefetch_numel`` elements, asynchronously on RCCL's stream, so the gather of layer i + 1
-  runs beside the MFMA work of layer i (``stage3_prefetch_bucket_size``);
+  ``prefetch_numel`` elements and at least the next block, so the gather of layer i + 1 runs
+  beside the MFMA work of layer i (``stage3_prefetch_bucket_size``). The pinned-host H2D copy of
+  an offloaded shard and the all-gather both run on the partitioner's side stream, and the compute
+  stream waits for a bucket with a device-side event wait — the host never blocks on a gather;
 * buckets whose parameters are all below ``persistence_threshold`` elements (biases, norms) stay
   gathered — re-gathered once after each optimizer step (``stage3_param_persistence_threshold``);
 * gradients take the ZeRO-2 path of the DDP (bucket accumulation buffer -> reduce-scatter into
@@ -60,6 +62,9 @@ class ZeroParamPartitioner:
         self.inflight: Dict[int, tuple] = {}
         self.trace = {"fwd": [], "bwd": []}
         self._traced = {"fwd": False, "bwd": False}
+        # H2D copies of offloaded shards and the parameter gathers run on a side stream, ordered by
+        # events, so they overlap the compute of the previous block
+        self.side = torch.cuda.Stream(device=self.dev) if self.dev.type == "cuda" else None
         old = ddp.param_data
         with torch.no_grad():
             for b in ddp.buckets:
@@ -79,6 +84,8 @@ class ZeroParamPartitioner:
         self.blocks = self._find_blocks(ddp.module)
         for mod, bks in self.blocks:
             self._install(mod, bks, root=mod is ddp.module)
+        self.block_numel = max((sum(ddp.buckets[i].numel for i in bks) for mod, bks in self.blocks
+                                if mod is not ddp.module), default=0)
 
     # ------------------------------------------------------------------ layout
     def _find_blocks(self, root: nn.Module):
@@ -130,23 +137,41 @@ class ZeroParamPartitioner:
 
     # ------------------------------------------------------------------ gathers
     def _gather_async(self, b):
+        """Start materialising bucket b: (pinned host ->) device copy of this rank's shard and the
+        all-gather, both on the partitioner's side stream after the compute stream's work so far
+        (the optimizer's shard writes). Returns (ready event or work, full buffer)."""
         n = b.numel // self.dp
         shard = self.store[b.shard_off:b.shard_off + n]
-        if self.offload:
-            shard = shard.to(self.dev, non_blocking=True)
-        buf = torch.empty(b.numel, dtype=self.dtype, device=self.dev)
-        if self.dp == 1:
-            buf.copy_(shard)
-            return None, buf
-        h = dist.all_gather_into_tensor(buf, shard, group=self.ddp.dp_group, async_op=True)
-        return h, buf
+        if self.side is None:
+            buf = torch.empty(b.numel, dtype=self.dtype, device=self.dev)
+            if self.dp == 1:
+                buf.copy_(shard)
+                return None, buf
+            return dist.all_gather_into_tensor(buf, shard, group=self.ddp.dp_group, async_op=True), buf
+        cur = torch.cuda.current_stream(self.dev)
+        self.side.wait_stream(cur)
+        with torch.cuda.stream(self.side):
+            if self.offload:
+                shard = shard.to(self.dev, non_blocking=True)     # H2D beside the compute stream
+            buf = torch.empty(b.numel, dtype=self.dtype, device=self.dev)
+            if self.dp == 1:
+                buf.copy_(shard, non_blocking=True)
+            else:
+                dist.all_gather_into_tensor(buf, shard, group=self.ddp.dp_group)
+            ev = torch.cuda.Event()
+            ev.record(self.side)
+        return ev, buf
 
     def _materialise(self, i):
         b = self.ddp.buckets[i]
         if i in self.full:
             return
         h, buf = self.inflight.pop(i) if i in self.inflight else self._gather_async(b)
-        if h is not None:
+        if isinstance(h, torch.cuda.Event):
+            cur = torch.cuda.current_stream(self.dev)
+            cur.wait_event(h)                 # a device-side wait: the host never blocks here
+            buf.record_stream(cur)
+        elif h is not None:
             h.wait()
         self.full[i] = buf
         self._attach(b, buf)
@@ -159,7 +184,10 @@ class ZeroParamPartitioner:
             k = tr.index(i)
         except ValueError:
             return
-        budget = self.prefetch_numel
+        # ``stage3_prefetch_bucket_size`` elements ahead, but never less than the next block's
+        # buckets (DeepSpeed's "auto" 0.9 h^2 is a fraction of one transformer layer, which would
+        # leave the next layer's gather exposed)
+        budget = max(self.prefetch_numel, self.block_numel)
         for j in tr[k + 1:]:
             if budget <= 0:
                 break
@@ -194,9 +222,12 @@ class ZeroParamPartitioner:
     def end_of_backward(self):
         """Called by the DDP when the gradient sync finished: drop what backward still holds and
         freeze the traces (the first iteration defines the prefetch order)."""
-        for i, h in list(self.inflight.items()):
-            if h[0] is not None:
-                h[0].wait()
+        for i, (h, buf) in list(self.inflight.items()):
+            if isinstance(h, torch.cuda.Event):
+                torch.cuda.current_stream(self.dev).wait_event(h)
+                buf.record_stream(torch.cuda.current_stream(self.dev))
+            elif h is not None:
+                h.wait()
         self.inflight.clear()
         for i in list(self.full):
             if not self.persistent[i]:
@@ -214,7 +245,10 @@ class ZeroParamPartitioner:
         for b in self.ddp.buckets:
             if self.persistent[b.index]:
                 h, buf = self._gather_async(b)
-                if h is not None:
+                if isinstance(h, torch.cuda.Event):
+                    torch.cuda.current_stream(self.dev).wait_event(h)
+                    buf.record_stream(torch.cuda.current_stream(self.dev))
+                elif h is not None:
                     h.wait()
                 self.full[b.index].copy_(buf)
 

@@ -63,6 +63,8 @@ def setup_distributed(args=None, backend: str = "nccl"):
     return rank, local, world, dev
 
 
+MI355X_BF16_PEAK_TFLOPS = 2500.0   # dense bf16 MFMA (MI355X_MICROARCH.md: ~2.5 PF dense)
+
 class TrainerState(dict):
     pass
 
@@ -195,6 +197,10 @@ class Trainer:
         tr_loss = torch.zeros((), dtype=torch.float32, device=self.device)
         total_loss = torch.zeros((), dtype=torch.float32, device=self.device)
         tokens = torch.zeros((), dtype=torch.float64, device=self.device)
+        # every non-pad input token (prompt + response): the work the model does, for MFU
+        in_tokens = torch.zeros((), dtype=torch.float64, device=self.device)
+        steady = None          # (time, input tokens) after the first optimizer step (kernel tuning, caches)
+        n_seen = 0
         steps_since_log = 0
         last_log_t = t0 = time.time()
         done = self.state["global_step"] >= max_steps
@@ -213,9 +219,16 @@ class Trainer:
                 eng.backward(loss)
                 tr_loss += loss.detach().float() / ga
                 tokens += (labels != -100).sum()
+                am = batch.get("attention_mask")
+                in_tokens += am.sum() if am is not None else ids.numel()
+                n_seen += ids.shape[0]
                 gn = eng.step()
                 if gn is None:
                     continue
+                if steady is None:
+                    if self.device.type == "cuda":
+                        torch.cuda.synchronize(self.device)
+                    steady = (time.time(), float(in_tokens), self.state["global_step"] + 1)
                 collective_check_from_env(self.state["global_step"] + 1)
                 self.state["global_step"] += 1
                 self.state["epoch"] = epoch + (step + 1) / len(loader)
@@ -256,11 +269,30 @@ class Trainer:
             torch.cuda.synchronize(self.device)
         runtime = time.time() - t0
         gs = max(self.state["global_step"], 1)
+        if self.world > 1:
+            dist.all_reduce(in_tokens)
         metrics = {"train_runtime": round(runtime, 4),
                    "train_samples_per_second": round(num_train_samples / runtime, 3),
                    "train_steps_per_second": round(max_steps / runtime, 3),
                    "train_tokens_per_second": round(float(tokens) / runtime, 1),
                    "train_loss": float(total_loss) / gs}
+        # Steady state (after the first optimizer step): input tokens / s and model FLOP/s per GPU
+        # with the 6 N + attention count (12 L h s per token, s = mean sequence), and MFU against
+        # the dense bf16 MFMA peak of an MI355X (2.5 PF/s).
+        if steady is not None and self.state["global_step"] > steady[2]:
+            t_s = time.time() - steady[0]
+            tok_local = float(in_tokens) / max(1, self.world) - steady[1]
+            tps = tok_local * max(1, self.world) / max(t_s, 1e-9)
+            cfg = getattr(getattr(self.model, "model", None), "cfg", None)
+            attn = 0.0
+            if cfg is not None:
+                mean_s = float(in_tokens) / max(1.0, float(n_seen * max(1, self.world)))
+                attn = 12.0 * cfg.num_layers * cfg.hidden_size * mean_s
+            fpt = 6.0 * nparam + attn
+            tfl = tps * fpt / max(1, self.world) / 1e12
+            metrics.update({"train_input_tokens_per_second": round(tps, 1),
+                            "train_model_tflops_per_gpu": round(tfl, 2),
+                            "train_mfu": round(tfl / MI355X_BF16_PEAK_TFLOPS, 4)})
         self.log(metrics)
         self.train_metrics = metrics
         return metrics
