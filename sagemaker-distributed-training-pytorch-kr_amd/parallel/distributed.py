@@ -187,6 +187,9 @@ class DistributedDataParallel(nn.Module):
         self.zero3 = None                                # ZeroParamPartitioner (parallel/zero3.py)
         self._staging: Dict[int, torch.Tensor] = {}    # bucket index -> full fp32 bucket (stage >= 2)
         self._rs_inflight: Dict[int, tuple] = {}       # bucket index -> (handle, tmp shard or None)
+        # dp == 1 under stage >= 2: the "shard" is the whole bucket, so gradients accumulate
+        # straight into ``grad_store`` (no per-micro-batch staging buffer, zero-fill or copy).
+        self._direct = self.zero_stage >= 2 and self.dp == 1
         if self.zero_stage >= 2:
             off = 0
             for b in self.buckets:
@@ -285,7 +288,9 @@ class DistributedDataParallel(nn.Module):
                 b.pending[id(p)] = left
                 return
             b.pending.pop(id(p), None)
-            if self.overlap and not b.pending and b.index in self._staging:
+            if self._direct and not b.pending:   # nothing to reduce: re-arm for the next micro-batch
+                b.pending = {id(q): int(getattr(q, "_smdt_grad_contributions", 1)) for q in b.params}
+            elif self.overlap and not b.pending and b.index in self._staging:
                 self._launch(b)
             return
         if b is None or not self.sync_enabled:
@@ -358,6 +363,11 @@ class DistributedDataParallel(nn.Module):
         """Stage >= 2: p's fp32 gradient view inside its bucket's accumulation buffer, allocated
         (zeroed) on first touch in a micro-batch."""
         b = self.param_bucket[id(p)]
+        if self._direct:
+            o, n = self.param_index[id(p)]
+            shape, stride = self.shapes[id(p)]
+            flat = self.grad_store[b.shard_off + (o - b.start):b.shard_off + (o - b.start) + n]
+            return flat.view(shape) if _is_dense(shape, stride) else flat.as_strided(shape, stride)
         buf = self._staging.get(b.index)
         if buf is None:
             buf = torch.zeros(b.numel, dtype=self.grad_dtype, device=self.grad_store.device)
@@ -493,7 +503,9 @@ class DistributedDataParallel(nn.Module):
         _health.monitor().consume()      # the previous step's engine-error flag (comm/health.py)
         if self.xgmi is not None and not self.xgmi.active:
             self.xgmi = None
-        if self.zero_stage >= 2:
+        if self._direct:
+            self.grad_store.zero_()
+        elif self.zero_stage >= 2:
             for b in self.buckets:
                 self._retire_rs(b)
             self._staging.clear()

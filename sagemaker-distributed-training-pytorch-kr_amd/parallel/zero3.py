@@ -42,7 +42,7 @@ from .distributed import DistributedDataParallel, ShardedFlat, _is_dense
 
 class ZeroParamPartitioner:
     def __init__(self, ddp: DistributedDataParallel, persistence_threshold: int = 0, prefetch_numel: int = 0,
-                 offload: bool = False):
+                 offload: bool = False, max_live_numel: int = 0):
         if not (ddp.zero and ddp.zero_stage >= 3):
             raise ValueError("ZeroParamPartitioner needs DistributedDataParallel(use_distributed_optimizer=True, "
                              "zero_stage=3)")
@@ -52,6 +52,13 @@ class ZeroParamPartitioner:
         self.dtype = ddp.param_dtype
         self.offload = bool(offload)
         self.prefetch_numel = int(prefetch_numel)
+        # ``stage3_max_live_parameters``: a released bucket stays gathered while the gathered
+        # (non-persistent) elements stay within this budget, so gradient-accumulation micro-batches
+        # reuse the parameters gathered by the first one instead of re-fetching (and, offloaded,
+        # re-copying from host) every layer twice per micro-batch; everything is dropped when the
+        # optimizer is about to rewrite the shards (end_of_backward).
+        self.max_live_numel = int(max_live_numel)
+        self.live_numel = 0
         self.persistent = {b.index: max(p.numel() for p in b.params) <= persistence_threshold for b in ddp.buckets}
         total = sum(b.numel // self.dp for b in ddp.buckets)
         pin = self.offload and torch.cuda.is_available()
@@ -174,6 +181,7 @@ class ZeroParamPartitioner:
         elif h is not None:
             h.wait()
         self.full[i] = buf
+        self.live_numel += b.numel
         self._attach(b, buf)
 
     def _prefetch_after(self, i, phase):
@@ -212,9 +220,13 @@ class ZeroParamPartitioner:
             if self.persistent[i]:
                 continue
             self.refs[i] = max(self.refs[i] - 1, 0)
-            if self.refs[i] == 0 and i in self.full:
-                del self.full[i]
-                self._detach(self.ddp.buckets[i])
+            if self.refs[i] == 0 and i in self.full and self.live_numel > self.max_live_numel:
+                self._free(i)
+
+    def _free(self, i):
+        del self.full[i]
+        self.live_numel -= self.ddp.buckets[i].numel
+        self._detach(self.ddp.buckets[i])
 
     def end_of_forward_trace(self):
         self._traced["fwd"] = True
@@ -232,8 +244,7 @@ class ZeroParamPartitioner:
         for i in list(self.full):
             if not self.persistent[i]:
                 self.refs[i] = 0
-                del self.full[i]
-                self._detach(self.ddp.buckets[i])
+                self._free(i)
         if self.trace["fwd"]:
             self._traced["fwd"] = True
         if self.trace["bwd"]:
@@ -275,5 +286,5 @@ class ZeroParamPartitioner:
 
 
 def partition_parameters(ddp: DistributedDataParallel, persistence_threshold: int = 0, prefetch_numel: int = 0,
-                         offload: bool = False) -> ZeroParamPartitioner:
-    return ZeroParamPartitioner(ddp, persistence_threshold, prefetch_numel, offload)
+                         offload: bool = False, max_live_numel: int = 0) -> ZeroParamPartitioner:
+    return ZeroParamPartitioner(ddp, persistence_threshold, prefetch_numel, offload, max_live_numel)

@@ -123,6 +123,14 @@ class ZeroEngine:
             model.cfg.params_dtype = dtype
         bucket = int(z.get("reduce_bucket_size", 5e8)) if not _is_auto(z.get("reduce_bucket_size")) else int(5e8)
         bucket = max(bucket, MIN_BUCKET)
+        if self.stage >= 3:
+            # Stage 3 gathers / releases parameters per BUCKET, so buckets are at least one
+            # transformer block: the HF "auto" reduce_bucket_size (h^2, 0.59 M elements for OPT-125m)
+            # would cut a 7 M-parameter layer into 12 gathers, each with its hook bookkeeping.
+            blocks = [sum(p.numel() for p in c.parameters()) for m in model.modules()
+                      if isinstance(m, torch.nn.ModuleList) for c in m.children()]
+            if blocks:
+                bucket = max(bucket, max(blocks))
         off_p = z.get("offload_param", {}) or {}
         self.offload_param = off_p.get("device") in ("cpu", "nvme")
         if self.offload_param and self.stage < 3:
@@ -145,7 +153,8 @@ class ZeroEngine:
                 return default if _is_auto(v) else int(v)
             self.partitioner = ZeroParamPartitioner(
                 self.ddp, persistence_threshold=_num("stage3_param_persistence_threshold", 100_000),
-                prefetch_numel=_num("stage3_prefetch_bucket_size", 50_000_000), offload=self.offload_param)
+                prefetch_numel=_num("stage3_prefetch_bucket_size", 50_000_000), offload=self.offload_param,
+                max_live_numel=_num("stage3_max_live_parameters", 1_000_000_000))
             mem = self.partitioner.param_memory_numel()
             log(f"[zero] stage 3: {sum(p.numel() for p in model.parameters() if p.numel()) / 1e9:.2f} B params "
                 f"resident before partitioning -> shard {mem['shard'] / 1e9:.3f} B elements on {mem['device']} "

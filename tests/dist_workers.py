@@ -200,7 +200,7 @@ def zero_sft_worker(rank, world, stage, ga, steps, offload=False, offload_param=
                                  **({"offload_param": {"device": "cpu"}} if offload_param else {}),
                                  "stage3_param_persistence_threshold": 200, "stage3_prefetch_bucket_size": 4000}}
     eng = ZeroEngine(m, cfg, log=lambda *_: None)
-    data = sft_batches(n=steps * ga * 2 // world * world + 8)
+    data = sft_batches(n=steps * ga * world + 8)
     k = 0
     for _ in range(steps):
         for _ in range(ga):

@@ -140,6 +140,17 @@ def test_zero_world2_matches_world1(stage, ga, offload, offload_param):
             torch.testing.assert_close(outs[r][k], v, rtol=2e-4, atol=2e-5, msg=f"rank {r} {k}")
 
 
+@pytest.mark.slow
+def test_zero2_world8_matches_world1():
+    """ZeRO-2 over 8 gloo ranks (gradient shards of 1/8, one micro-batch each) == one rank
+    accumulating the same 8 micro-batches."""
+    ref = run_workers(W.zero_sft_worker, 1, 0, 8, 2, False)[0]
+    outs = run_workers(W.zero_sft_worker, 8, 2, 1, 2, False, False, timeout=600)
+    for r in range(8):
+        for k, v in ref.items():
+            torch.testing.assert_close(outs[r][k], v, rtol=2e-4, atol=2e-5, msg=f"rank {r} {k}")
+
+
 @pytest.mark.parametrize("world", [2, 4])
 def test_zero_stage3_memory_is_partitioned(world):
     """Per-rank persistent gradient and parameter storage ~ total / dp under ZeRO-3 (plus the small
