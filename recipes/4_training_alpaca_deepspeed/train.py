@@ -37,8 +37,10 @@ import torch  # noqa: E402
 
 from smdt_amd.data import sft  # noqa: E402
 from smdt_amd.models.hf import HFCausalLM  # noqa: E402
+from smdt_amd.parallel import zero_init  # noqa: E402
 from smdt_amd.train import hf_args  # noqa: E402
 from smdt_amd.train.sft_trainer import Trainer, setup_distributed  # noqa: E402
+from smdt_amd.train.zero import load_ds_config  # noqa: E402
 
 
 @dataclass
@@ -81,8 +83,15 @@ def train():
     rank, local, world, device = setup_distributed(training_args)
 
     dtype = torch.bfloat16 if training_args.bf16 else torch.float16 if training_args.fp16 else torch.float32
-    model = HFCausalLM.from_pretrained(model_args.model_name_or_path, params_dtype=dtype, device=device,
-                                       cache_dir=training_args.cache_dir)
+    # ZeRO-3: every rank keeps only its shard of each parameter from the moment it is built
+    # (DeepSpeed zero.Init; parallel/zero_init.py)
+    stage = int(load_ds_config(training_args.deepspeed).get("zero_optimization", {}).get("stage", 0))
+    with zero_init.Init(enabled=stage >= 3 and world > 1) as zi:
+        model = HFCausalLM.from_pretrained(model_args.model_name_or_path, params_dtype=dtype, device=device,
+                                           cache_dir=training_args.cache_dir)
+    if zi.params and rank == 0:
+        print(f"[zero.Init] {zi.params} parameters partitioned at construction over {zi.dp} ranks: "
+              f"{zi.shard_bytes / 1e6:.1f} MB of shards per rank (peak {zi.peak_bytes / 1e6:.1f} MB)", flush=True)
     tokenizer = sft.load_tokenizer(model_args.model_name_or_path, cache_dir=training_args.cache_dir,
                                    model_max_length=training_args.model_max_length,
                                    model_type=model.hf_config.get("model_type"))
@@ -95,7 +104,8 @@ def train():
         special["bos_token"] = sft.DEFAULT_BOS_TOKEN
     if tokenizer.unk_token is None:
         special["unk_token"] = sft.DEFAULT_UNK_TOKEN
-    smart_tokenizer_and_embedding_resize(special, tokenizer, model)
+    with zero_init.gathered([model.get_input_embeddings().weight, model.get_output_embeddings().weight]):
+        smart_tokenizer_and_embedding_resize(special, tokenizer, model)
 
     if not data_args.data_path or not os.path.exists(data_args.data_path):
         path = data_args.data_path or os.path.join(training_args.output_dir, "synthetic_alpaca.json")

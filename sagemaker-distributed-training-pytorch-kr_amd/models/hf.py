@@ -273,18 +273,23 @@ class HFCausalLM(nn.Module):
 
     @torch.no_grad()
     def load_our_state_dict(self, ours: Dict[str, torch.Tensor]):
+        """Copy a state dict in; parameters partitioned by parallel/zero_init.Init keep only their
+        shard of each tensor (no gather)."""
+        from ..parallel import zero_init as zi
         own = dict(self.model.named_parameters())
         for k, v in ours.items():
             if k not in own:
                 continue
             p = own[k]
-            if p.shape != v.shape:
-                if k in ("embedding.weight", "output_weight") and v.shape[0] <= p.shape[0]:
-                    p.zero_()
-                    p[: v.shape[0]].copy_(v.to(p.dtype))
-                    continue
-                raise ValueError(f"shape mismatch for {k}: {tuple(v.shape)} vs {tuple(p.shape)}")
-            p.copy_(v.to(p.dtype))
+            shape = zi.logical_shape(p)
+            if shape != tuple(v.shape):
+                if k in ("embedding.weight", "output_weight") and v.shape[0] <= shape[0]:
+                    full = torch.zeros(shape, dtype=p.dtype)
+                    full[: v.shape[0]].copy_(v.to(p.dtype))
+                    v = full
+                else:
+                    raise ValueError(f"shape mismatch for {k}: {tuple(v.shape)} vs {shape}")
+            zi.load_full_(p, v.to(p.device))
 
     def save_pretrained(self, out_dir: str, state_dict: Optional[Dict[str, torch.Tensor]] = None,
                         safe_serialization: bool = True):

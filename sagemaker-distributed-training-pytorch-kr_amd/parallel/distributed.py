@@ -35,6 +35,7 @@ from ..comm import health as _health
 from ..comm import stats as _cs
 from ..ops import _ext
 from . import state as ps
+from . import zero_init as _zi
 
 
 @dataclass
@@ -57,7 +58,7 @@ class Bucket:
 
 
 def _region_key(p: nn.Parameter, st) -> tuple:
-    wd = not (p.dim() < 2 or getattr(p, "no_weight_decay", False))
+    wd = not (len(_zi.logical_shape(p)) < 2 or getattr(p, "no_weight_decay", False))
     tp_dup = (st.tp > 1 and not getattr(p, "tensor_model_parallel", False) and st.tp_rank != 0)
     pp_dup = getattr(p, "shared_embedding", False) and not st.is_first_stage(ignore_virtual=True)
     count = not (tp_dup or pp_dup)
@@ -121,7 +122,11 @@ class DistributedDataParallel(nn.Module):
         self._syncs = 0
 
         params = [p for p in module.parameters() if p.requires_grad]
-        total = sum(p.numel() for p in {id(p): p for p in params}.values())
+        total = sum(_zi.logical_numel(p) for p in {id(p): p for p in params}.values())
+        # parameters built under parallel/zero_init.Init: only this rank's shard exists
+        self._zero_init = any(_zi.is_partitioned(p) for p in params)
+        if self._zero_init and self.zero_stage < 3:
+            raise ValueError("parameters built under zero_init.Init need ZeRO stage 3")
         if bucket_size in (None, "auto", 0):
             # one bucket per region when nothing is reduced; else sized for this group's links
             # (comm/buckets.py: 8-32 MB from a start-up latency / bandwidth timing, >= 4 buckets)
@@ -157,7 +162,7 @@ class DistributedDataParallel(nn.Module):
         for key in order:
             cur: Optional[Bucket] = None
             for p in regions[key]:
-                n = p.numel()
+                n = _zi.logical_numel(p)
                 # The pipeline-tied word embedding (first and last stage) sits alone in its bucket
                 # so both stages shard it identically under ZeRO: the embedding-group gradient
                 # all-reduce after the reduce-scatter then sums matching shards.
@@ -181,8 +186,10 @@ class DistributedDataParallel(nn.Module):
                 off = cur.end
         self.numel = off
         self.params = params
-        self.param_data = torch.zeros(self.numel, dtype=pdtype, device=dev)
-        self.shapes = {id(p): (tuple(p.shape), tuple(p.stride())) for p in params}
+        # (zero-init: the partitioner assembles the shards; the full buffer never exists)
+        self.param_data = torch.zeros(0 if self._zero_init else self.numel, dtype=pdtype, device=dev)
+        self.shapes = {id(p): ((_zi.logical_shape(p), _contig_strides(_zi.logical_shape(p)))
+                               if _zi.is_partitioned(p) else (tuple(p.shape), tuple(p.stride()))) for p in params}
         self.grad_store = None
         self.zero3 = None                                # ZeroParamPartitioner (parallel/zero3.py)
         self._staging: Dict[int, torch.Tensor] = {}    # bucket index -> full fp32 bucket (stage >= 2)
@@ -203,9 +210,10 @@ class DistributedDataParallel(nn.Module):
         with torch.no_grad():
             for p in params:
                 o, n = self.param_index[id(p)]
-                pv = _dense_view(self.param_data[o:o + n], p)
-                pv.copy_(p.data)
-                p.data = pv
+                if not self._zero_init:
+                    pv = _dense_view(self.param_data[o:o + n], p)
+                    pv.copy_(p.data)
+                    p.data = pv
                 if self.zero_stage >= 2:
                     _make_lazy_grad_param(p, self)
                 else:
@@ -226,7 +234,7 @@ class DistributedDataParallel(nn.Module):
                     bks = sorted({self.param_bucket[id(p)].index for p in own})
                     self._pg_hooks.append(mod.register_forward_pre_hook(self._make_gather_wait(bks)))
         self._reset_pending()
-        if self.dp > 1:
+        if self.dp > 1 and not self._zero_init:
             self.broadcast_params()
 
     # ---------------------------------------------------------------- layout helpers
@@ -586,6 +594,14 @@ def _dense_view(flat: torch.Tensor, p: torch.Tensor) -> torch.Tensor:
     if p.is_contiguous() or not dense_permuted:
         return flat.view(p.shape)
     return flat.as_strided(p.shape, p.stride())
+
+
+def _contig_strides(shape):
+    st, acc = [], 1
+    for d in reversed(shape):
+        st.append(acc)
+        acc *= d
+    return tuple(reversed(st))
 
 
 def _round_up(x, m):

@@ -59,7 +59,7 @@ class ZeroParamPartitioner:
         # optimizer is about to rewrite the shards (end_of_backward).
         self.max_live_numel = int(max_live_numel)
         self.live_numel = 0
-        self.persistent = {b.index: max(p.numel() for p in b.params) <= persistence_threshold for b in ddp.buckets}
+        self.persistent = {b.index: max(ddp.param_index[id(p)][1] for p in b.params) <= persistence_threshold for b in ddp.buckets}
         total = sum(b.numel // self.dp for b in ddp.buckets)
         pin = self.offload and torch.cuda.is_available()
         self.store = torch.empty(total, dtype=self.dtype, device="cpu" if self.offload else self.dev,
@@ -74,11 +74,14 @@ class ZeroParamPartitioner:
         self.side = torch.cuda.Stream(device=self.dev) if self.dev.type == "cuda" else None
         old = ddp.param_data
         with torch.no_grad():
-            for b in ddp.buckets:
-                s, e = ddp.shard_range(b)
-                self.store[b.shard_off:b.shard_off + (e - s)].copy_(old[s:e])
-                if self.persistent[b.index]:
-                    self.full[b.index] = old[b.start:b.end].clone()
+            if ddp._zero_init:
+                self._assemble_from_param_shards()
+            else:
+                for b in ddp.buckets:
+                    s, e = ddp.shard_range(b)
+                    self.store[b.shard_off:b.shard_off + (e - s)].copy_(old[s:e])
+                    if self.persistent[b.index]:
+                        self.full[b.index] = old[b.start:b.end].clone()
         ddp.param_data = ShardedFlat(ddp, self.store)
         ddp.zero3 = self
         for b in ddp.buckets:
@@ -93,6 +96,31 @@ class ZeroParamPartitioner:
             self._install(mod, bks, root=mod is ddp.module)
         self.block_numel = max((sum(ddp.buckets[i].numel for i in bks) for mod, bks in self.blocks
                                 if mod is not ddp.module), default=0)
+
+    def _assemble_from_param_shards(self):
+        """Bucket shards from the per-parameter shards left by zero_init.Init: each parameter is
+        all-gathered once (only ONE full parameter exists at a time), the part of it inside this
+        rank's shard of its bucket is kept, and the per-parameter shard is dropped. Small
+        (persistent) buckets keep their full copy, as in the resident path."""
+        from . import zero_init as zi
+        ddp = self.ddp
+        for b in ddp.buckets:
+            s, e = ddp.shard_range(b)
+            fullbuf = torch.zeros(b.numel, dtype=self.dtype, device=self.dev) if self.persistent[b.index] else None
+            for p in b.params:
+                o, n = ddp.param_index[id(p)]
+                full = (zi.gather_full(p, ddp.dp_group) if zi.is_partitioned(p) else p.data.reshape(-1)).to(self.dev, self.dtype)
+                lo, hi = max(o, s), min(o + n, e)
+                if lo < hi:
+                    self.store[b.shard_off + (lo - s):b.shard_off + (hi - s)].copy_(full[lo - o:hi - o])
+                if fullbuf is not None:
+                    fullbuf[o - b.start:o - b.start + n].copy_(full)
+                del full
+                if zi.is_partitioned(p):
+                    del p._zi_shard
+                    del p._zi_shape
+            if fullbuf is not None:
+                self.full[b.index] = fullbuf
 
     # ------------------------------------------------------------------ layout
     def _find_blocks(self, root: nn.Module):

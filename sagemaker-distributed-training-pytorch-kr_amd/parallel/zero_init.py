@@ -1,0 +1,162 @@
+"""Partitioned model construction for ZeRO-3 — the equivalent of DeepSpeed's ``zero.Init``.
+
+The reference's Alpaca job builds OPT-125m under ZeRO-3 so that every rank materialises only its
+partition of the weights while the model is being constructed ("num_elems = 0.16B" at load,
+/root/reference/4_training_alpaca_deepspeed.ipynb:1580; DS config
+configs/default_offload_opt_param.json:23-41). Here:
+
+    with zero_init.Init(dp_group):
+        model = HFCausalLM.from_pretrained(...)      # or any nn.Module constructor
+    engine = ZeroEngine(model, ds_config)            # stage 3
+
+Inside the context every parameter is cut the moment it is registered on its module: this rank
+keeps 1/dp of its flattened elements (``p._zi_shard``) and the parameter's storage is released
+(a 0-element placeholder; its logical shape is in ``p._zi_shape``). So at no time does a rank hold
+more than its shards plus the ONE parameter being constructed. DistributedDataParallel lays out
+its buckets from the logical shapes, and the stage-3 partitioner assembles its bucket shards from
+these per-parameter shards with one all-gather per parameter (transient: a single parameter at a
+time), so the full model never exists on any rank (parallel/zero3.py).
+
+Parameters are initialised exactly as without the context (the construction runs unchanged; only
+the storage is cut afterwards), so a partitioned build trains bit-identically to a resident one.
+Code that reads or writes a partitioned parameter's values afterwards (checkpoint loading, the
+recipe's embedding resize) uses ``gathered([...])`` — DeepSpeed's ``GatheredParameters``: the full
+value exists inside the block and the block's changes are cut back into the shards on exit — or
+``load_full_`` to set a parameter from a full tensor without any gather.
+"""
+from __future__ import annotations
+
+import contextlib
+import math
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+
+
+def is_partitioned(p) -> bool:
+    return hasattr(p, "_zi_shape")
+
+
+def logical_shape(p):
+    return tuple(p._zi_shape) if is_partitioned(p) else tuple(p.shape)
+
+
+def logical_numel(p) -> int:
+    return int(math.prod(p._zi_shape)) if is_partitioned(p) else p.numel()
+
+
+class Init:
+    """Context manager: parameters registered inside are partitioned over ``dp_group`` at once."""
+
+    def __init__(self, dp_group=None, enabled: bool = True):
+        self.enabled = bool(enabled)
+        self.group = dp_group
+        self.dp = dist.get_world_size(dp_group) if (dist.is_initialized() and enabled) else 1
+        self.rank = dist.get_rank(dp_group) if self.dp > 1 else 0
+        self.shard_bytes = 0          # bytes of shards kept so far
+        self.peak_bytes = 0           # max over registrations of shards kept + the parameter being cut
+        self.largest_param_bytes = 0
+        self.params = 0
+        self._orig = None
+
+    def __enter__(self):
+        if not self.enabled:
+            return self
+        self._orig = nn.Module.register_parameter
+        orig, me = self._orig, self
+
+        def register_parameter(mod, name, param):
+            orig(mod, name, param)
+            if param is not None and not is_partitioned(param) and param.numel() > 0 and param.device.type != "meta":
+                me._partition(param)
+        nn.Module.register_parameter = register_parameter
+        return self
+
+    def __exit__(self, *exc):
+        if self._orig is not None:
+            nn.Module.register_parameter = self._orig
+            self._orig = None
+        return False
+
+    @torch.no_grad()
+    def _partition(self, p: nn.Parameter):
+        full_bytes = p.numel() * p.element_size()
+        self.peak_bytes = max(self.peak_bytes, self.shard_bytes + full_bytes)
+        self.largest_param_bytes = max(self.largest_param_bytes, full_bytes)
+        _cut(p, self.dp, self.rank, self.group)
+        self.shard_bytes += p._zi_shard.numel() * p._zi_shard.element_size()
+        self.params += 1
+
+
+def _group_dims(group):
+    dp = dist.get_world_size(group) if dist.is_initialized() else 1
+    return dp, (dist.get_rank(group) if dp > 1 else 0)
+
+
+@torch.no_grad()
+def _cut(p, dp: int, rank: int, group, full=None):
+    """Keep this rank's 1/dp of ``full`` (default: p's own data) as p's shard; placeholder data."""
+    shape = tuple(p.shape) if full is None else tuple(full.shape)
+    flat = (p.data if full is None else full).reshape(-1)
+    n = flat.numel()
+    c = (n + dp - 1) // dp
+    shard = torch.zeros(c, dtype=p.dtype, device=p.device)
+    lo, hi = min(n, rank * c), min(n, (rank + 1) * c)
+    shard[:hi - lo].copy_(flat[lo:hi])
+    p._zi_shape = shape
+    p._zi_shard = shard
+    p._zi_group = group
+    p.data = torch.empty(0, dtype=p.dtype, device=p.device)
+
+
+@torch.no_grad()
+def gather_full(p, group=None) -> torch.Tensor:
+    """The flattened full value of a partitioned parameter over ``group`` (one all-gather;
+    transient). ``group`` must have the size the parameter was partitioned for."""
+    n = logical_numel(p)
+    shard = p._zi_shard
+    dp = dist.get_world_size(group) if dist.is_initialized() else 1
+    if shard.numel() != (n + dp - 1) // dp:
+        raise ValueError(f"a parameter partitioned for another group size cannot be gathered over {dp} ranks")
+    if dp == 1:
+        return shard[:n]
+    out = torch.empty(dp * shard.numel(), dtype=shard.dtype, device=shard.device)
+    dist.all_gather_into_tensor(out, shard, group=group)
+    return out[:n]
+
+
+@torch.no_grad()
+def load_full_(p, value: torch.Tensor):
+    """Set a parameter from its full value (every rank passes the same tensor; no collective)."""
+    if not is_partitioned(p):
+        p.data.copy_(value.to(p.dtype))
+        return
+    if tuple(value.shape) != logical_shape(p):
+        raise ValueError(f"shape {tuple(value.shape)} != {logical_shape(p)}")
+    _cut(p, *_group_dims(p._zi_group), p._zi_group, full=value.to(p.dtype))
+
+
+@contextlib.contextmanager
+def gathered(params, group=None):
+    """Collective: inside the block the partitioned ones among ``params`` hold their full value
+    (``p.data`` with the logical shape); on exit whatever the block wrote is cut back into the
+    shards. Every rank of the group must enter with the same parameters."""
+    ps = [p for p in dict.fromkeys(params) if p is not None and is_partitioned(p)]
+    for p in ps:
+        g = p._zi_group if group is None else group
+        p.data = gather_full(p, g).view(p._zi_shape).clone()
+        del p._zi_shard
+        del p._zi_shape
+    try:
+        yield
+    finally:
+        for p in ps:
+            g = p._zi_group if group is None else group
+            _cut(p, *_group_dims(g), g)
+
+
+def cast_(p, dtype):
+    """Cast a partitioned parameter's shard (and placeholder) to ``dtype``."""
+    p._zi_shard = p._zi_shard.to(dtype)
+    p.data = torch.empty(0, dtype=dtype, device=p.device)

@@ -146,7 +146,7 @@ class Trainer:
                                                             max_steps))
         self._log0(f"[zero] stage {self.engine.stage}, dtype "
                    f"{'bf16' if self.engine.bf16 else 'fp16' if self.engine.fp16 else 'fp32'}, "
-                   f"world {self.world}, {sum(p.numel() for p in self.model.parameters()) / 1e6:.1f} M params, "
+                   f"world {self.world}, {sum(math.prod(sh) for sh, _ in self.engine.ddp.shapes.values()) / 1e6:.1f} M params, "
                    f"{len(self.engine.ddp.buckets)} grad buckets")
 
     def _log0(self, msg):

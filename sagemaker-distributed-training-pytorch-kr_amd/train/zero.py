@@ -115,9 +115,13 @@ class ZeroEngine:
         self.skipped_steps = 0
         self.clip = float(ds_config.get("gradient_clipping", 0.0) or 0.0)
         dtype = torch.bfloat16 if self.bf16 else torch.float16 if self.fp16 else torch.float32
+        from ..parallel import zero_init as _zi
         with torch.no_grad():  # parameters only: RoPE tables and other buffers stay fp32
             for p in model.parameters():
-                if p.dtype != dtype:
+                if _zi.is_partitioned(p):
+                    if p._zi_shard.dtype != dtype:
+                        _zi.cast_(p, dtype)
+                elif p.dtype != dtype:
                     p.data = p.data.to(dtype)
         if hasattr(model, "cfg"):
             model.cfg.params_dtype = dtype
@@ -127,7 +131,7 @@ class ZeroEngine:
             # Stage 3 gathers / releases parameters per BUCKET, so buckets are at least one
             # transformer block: the HF "auto" reduce_bucket_size (h^2, 0.59 M elements for OPT-125m)
             # would cut a 7 M-parameter layer into 12 gathers, each with its hook bookkeeping.
-            blocks = [sum(p.numel() for p in c.parameters()) for m in model.modules()
+            blocks = [sum(_zi.logical_numel(p) for p in c.parameters()) for m in model.modules()
                       if isinstance(m, torch.nn.ModuleList) for c in m.children()]
             if blocks:
                 bucket = max(bucket, max(blocks))
@@ -156,8 +160,8 @@ class ZeroEngine:
                 prefetch_numel=_num("stage3_prefetch_bucket_size", 50_000_000), offload=self.offload_param,
                 max_live_numel=_num("stage3_max_live_parameters", 1_000_000_000))
             mem = self.partitioner.param_memory_numel()
-            log(f"[zero] stage 3: {sum(p.numel() for p in model.parameters() if p.numel()) / 1e9:.2f} B params "
-                f"resident before partitioning -> shard {mem['shard'] / 1e9:.3f} B elements on {mem['device']} "
+            log(f"[zero] stage 3: {self.ddp.numel / 1e9:.2f} B params "
+                f"({'partitioned at construction' if self.ddp._zero_init else 'resident before partitioning'}) -> shard {mem['shard'] / 1e9:.3f} B elements on {mem['device']} "
                 f"+ {mem['persistent'] / 1e6:.2f} M persistent; grad shard {self.ddp.grad_memory_numel() / 1e9:.3f} B")
         ocfg = ds_config.get("optimizer", {"type": "AdamW", "params": {}})
         otype = ocfg.get("type", "AdamW").lower()

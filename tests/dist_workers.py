@@ -181,18 +181,25 @@ def sft_batches(n=8, b=2, s=16, v=120, seed=3):
     return out
 
 
-def zero_sft_worker(rank, world, stage, ga, steps, offload=False, offload_param=False, with_mem=False):
+def zero_sft_worker(rank, world, stage, ga, steps, offload=False, offload_param=False, with_mem=False,
+                    zero_init=False):
     """Data-parallel SFT steps with the ZeroEngine; global batch = world * 2 * ga rows of
-    ``sft_batches``. Returns full params after ``steps`` optimizer steps."""
+    ``sft_batches``. Returns full params after ``steps`` optimizer steps. ``zero_init``: build the
+    model under parallel/zero_init.Init (stage 3)."""
     from smdt_amd.comm import init_distributed
     from smdt_amd.models.hf import HFCausalLM
     from smdt_amd.parallel import state as ps
+    from smdt_amd.parallel import zero_init as zi
     from smdt_amd.train.zero import ZeroEngine
     ps.destroy_model_parallel()
     init_distributed("gloo")
     ps.initialize_model_parallel(1, 1)
     torch.manual_seed(0)
-    m = HFCausalLM(SFT_LLAMA, params_dtype=torch.float32)
+    with zi.Init(enabled=zero_init) as ctx:
+        m = HFCausalLM(SFT_LLAMA, params_dtype=torch.float32)
+    init_stats = {"peak_bytes": ctx.peak_bytes, "shard_bytes": ctx.shard_bytes, "params": ctx.params,
+                  "largest_param_bytes": ctx.largest_param_bytes,
+                  "resident_bytes_after_build": sum(p.numel() * p.element_size() for p in m.parameters())}
     cfg = {"optimizer": {"type": "AdamW", "params": {"lr": 1e-3, "betas": [0.9, 0.99], "eps": 1e-8,
                                                      "weight_decay": 0.1}},
            "gradient_accumulation_steps": ga, "gradient_clipping": 1.0,
@@ -216,7 +223,7 @@ def zero_sft_worker(rank, world, stage, ga, steps, offload=False, offload_param=
                 else int(torch.tensor(eng.ddp.shapes[id(p)][0]).prod()) for p in eng.ddp.params)
     mem = {"total": total, "grad": eng.ddp.grad_memory_numel(),
            "param": (eng.partitioner.param_memory_numel() if eng.partitioner is not None else None),
-           "param_numel_now": sum(p.numel() for p in m.parameters())}
+           "param_numel_now": sum(p.numel() for p in m.parameters()), "init": init_stats}
     with eng.gathered_params():
         out = {n: p.detach().clone() for n, p in m.named_parameters()}
     return (out, mem) if with_mem else out

@@ -168,4 +168,6 @@ def test_nb4_alpaca_deepspeed_through_estimator(tmp_path):
     assert any(n.endswith("trainer_state.json") for n in names), names
     job = sess.job_dir('alpaca-local-0101-00000000000000')
     metrics = json.load(open(os.path.join(job, "metrics.json")))
-    assert metrics['train:loss'], open(os.path.join(job, "logs", "job.log")).read()[-3000:]
+    log = open(os.path.join(job, "logs", "job.log")).read()
+    assert metrics['train:loss'], log[-3000:]
+    assert "[zero.Init]" in log, log[-3000:]       # stage 3 config: partitioned construction
