@@ -614,15 +614,10 @@ __global__ __launch_bounds__(256, D == 64 ? SMDT_FA_DKDV_OCC : 1) void bwd_dkdv_
   const uint32_t dsel = (my_key & 1) ? 0x07030501u : 0x02060004u;
   // Causal mask as part of the S accumulator's initial value: a wave's 32 x 32 (query, key) block
   // is either fully visible, fully masked (skipped) or exactly its diagonal block (qsub == kw),
-  // whose pattern (key > query) is the same for every diagonal block. dgb[i] = -1e30 where this
-  // lane's key follows register i's query, folded in as lse_row + dgb[i] * dflag (dflag = 1 on the
-  // diagonal block, else 0): one FMA per element that replaces the add of the row constant, so
-  // no compare / select runs after the exponential (exp2(-1e30) = 0).
-  float dgb[16];
-#pragma unroll
-  for (int g = 0; g < 4; ++g)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) dgb[4 * g + j] = (lane & 31) > 8 * g + 4 * h + j ? -1e30f : 0.f;
+  // whose pattern (key > query) is the same for every diagonal block: there the initial value is
+  // -1e30 where this lane's key follows register i's query, so no compare / select runs after the
+  // exponential (exp2(-1e30) = 0). Only the diagonal items build that pattern (sd_init), so it
+  // holds no registers in the main loop.
   int ch = 0, cq = 0;  // current work item
   auto item = [&](const char* buf, char* pre) {
     const int qb = qstart + cq * kTile;
@@ -633,79 +628,110 @@ __global__ __launch_bounds__(256, D == 64 ? SMDT_FA_DKDV_OCC : 1) void bwd_dkdv_
     const float* lse_l = reinterpret_cast<const float*>(buf + 2 * G::TB);
     const float* del_l = lse_l + kTile;
     issue(pre);
-  #pragma unroll
-      for (int qs2 = 0; qs2 < 2; ++qs2) {
-        const int qsub = qb + 32 * qs2;
-        if (CAUSAL && qsub + 31 < kw) continue;  // all queries precede all of this wave's keys
-        // S'[q, key] = Q . K'^T - lse ; dP'[q, key] = dO . V^T - delta  (key on lane, query rows
-        // in registers): the row constants are the accumulators' initial values.
-        // (the rows were prepared by delta_kernel: -(lse log2e - log2 inv) and -delta', so the
-        // accumulators start as plain LDS reads)
-        f32x16 s, dp;
-        const float dflag = (CAUSAL && qsub == kw) ? 1.f : 0.f;  // wave-uniform
-  #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int r0 = 32 * qs2 + 8 * g + 4 * h;  // 4 consecutive query rows of this group
-          const f32x4 lv = *reinterpret_cast<const f32x4*>(lse_l + r0);
-          const f32x4 dl = *reinterpret_cast<const f32x4*>(del_l + r0);
-  #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            s[4 * g + j] = CAUSAL ? fmaf(dgb[4 * g + j], dflag, lv[j]) : lv[j];
-            dp[4 * g + j] = dl[j];  // dP' = dP - delta' (dropped entries select -delta' below)
-          }
-        }
-  #pragma unroll
-        for (int kk = 0; kk < G::KS; ++kk) {
-          s = mfma(fr.rowf(q_l, 32 * qs2, kk), kf[kk], s);
-          dp = mfma(fr.rowf(do_l, 32 * qs2, kk), vf[kk], dp);
-        }
-        // dropout: slot m = registers 2m, 2m + 1 (queries 2i, 2i + 1 of one block); dropped
-        // entries: P' -> 0 for dV (packed-pair masks), dP -> 0, so dS = p' (keep ? dP : 0) - p' delta'
-        uint32_t dm[8];
-  #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int r0 = 32 * qs2 + 8 * g + 4 * h;
-          const f32x4 ndl = DROP ? *reinterpret_cast<const f32x4*>(del_l + r0) : f32x4{0.f, 0.f, 0.f, 0.f};
-          uint32_t t = 0u;
-          if constexpr (DROP) {
-            t = keep_bits(drop_hash(dblk + (uint32_t)(16 * qs2 + 4 * g) * shalf, dkey), dsel, drop.k4);
-            dm[2 * g] = mask_even_slot(t);
-            dm[2 * g + 1] = mask_odd_slot(t);
-          }
-  #pragma unroll
-          for (int j = 0; j < 4; j += 2) {
-            const int i = 4 * g + j;
-            // with dropout: p / (1 - p_drop); 0 where the causal mask was folded into s
-            const float p0 = fexp2(s[i]), p1 = fexp2(s[i + 1]);
-            float d0 = dp[i], d1 = dp[i + 1];
-            if constexpr (DROP) {  // kept: dP - delta'; dropped: -delta'
-              if (j == 0) {
-                d0 = sel_bit<7>(d0, ndl[j], t);
-                d1 = sel_bit<23>(d1, ndl[j + 1], t);
-              } else {
-                d0 = sel_bit<15>(d0, ndl[j], t);
-                d1 = sel_bit<31>(d1, ndl[j + 1], t);
-              }
-            }
-            s[i] = p0;
-            s[i + 1] = p1;
-            dp[i] = p0 * d0;  // dS
-            dp[i + 1] = p1 * d1;
-          }
-        }
-        // dV^T[d, key] += dO^T[d, q] . P[q, key] ; dK^T[d, key] += Q^T[d, q] . dS[q, key]
-  #pragma unroll
-        for (int st = 0; st < 2; ++st) {
-          v8_t<E> pb = pack8<E>(s, st);
-          if constexpr (DROP) pb = and_pairs(pb, dm[4 * st], dm[4 * st + 1], dm[4 * st + 2], dm[4 * st + 3]);
-          const v8_t<E> db = pack8<E>(dp, st);
-  #pragma unroll
-          for (int dt = 0; dt < G::DT; ++dt) {
-            dv[dt] = mfma(fr.trf(do_l, 32 * qs2, st, dt), pb, dv[dt]);
-            dk[dt] = mfma(fr.trf(q_l, 32 * qs2, st, dt), db, dk[dt]);
-          }
+    // S'[q, key] = Q . K'^T - lse ; dP'[q, key] = dO . V^T - delta  (key on lane, query rows in
+    // registers): the row constants (prepared by delta_kernel: -(lse log2e - log2 inv) and
+    // -delta') are the accumulators' initial values, read straight from LDS.
+    auto sd_init = [&](int qs2, bool diag, f32x16& sa, f32x16& pa) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int r0 = 32 * qs2 + 8 * g + 4 * h;  // 4 consecutive query rows of this group
+        const f32x4 lv = *reinterpret_cast<const f32x4*>(lse_l + r0);
+        const f32x4 dl = *reinterpret_cast<const f32x4*>(del_l + r0);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          sa[4 * g + j] = lv[j];
+          if (CAUSAL && diag && (lane & 31) > 8 * g + 4 * h + j) sa[4 * g + j] = -1e30f;
+          pa[4 * g + j] = dl[j];  // dP' = dP - delta' (dropped entries select -delta' below)
         }
       }
+    };
+    auto sd_mma = [&](int qs2, f32x16& sa, f32x16& pa) {
+#pragma unroll
+      for (int kk = 0; kk < G::KS; ++kk) {
+        sa = mfma(fr.rowf(q_l, 32 * qs2, kk), kf[kk], sa);
+        pa = mfma(fr.rowf(do_l, 32 * qs2, kk), vf[kk], pa);
+      }
+    };
+    // P' = exp2(S') and dS = P' (dP - delta') -> 16-bit operands. Dropout: slot m = registers
+    // 2m, 2m + 1 (queries 2i, 2i + 1 of one block); dropped entries: P' -> 0 for dV (packed-pair
+    // masks), dP -> 0, so dS = p' (keep ? dP : 0) - p' delta'.
+    auto softmax_ds = [&](int qs2, f32x16& sa, f32x16& pa, v8_t<E> (&pb)[2], v8_t<E> (&db)[2]) {
+      uint32_t dm[8];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int r0 = 32 * qs2 + 8 * g + 4 * h;
+        const f32x4 ndl = DROP ? *reinterpret_cast<const f32x4*>(del_l + r0) : f32x4{0.f, 0.f, 0.f, 0.f};
+        uint32_t t = 0u;
+        if constexpr (DROP) {
+          t = keep_bits(drop_hash(dblk + (uint32_t)(16 * qs2 + 4 * g) * shalf, dkey), dsel, drop.k4);
+          dm[2 * g] = mask_even_slot(t);
+          dm[2 * g + 1] = mask_odd_slot(t);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; j += 2) {
+          const int i = 4 * g + j;
+          // with dropout: p / (1 - p_drop); 0 where the causal mask was folded into s
+          const float p0 = fexp2(sa[i]), p1 = fexp2(sa[i + 1]);
+          float d0 = pa[i], d1 = pa[i + 1];
+          if constexpr (DROP) {  // kept: dP - delta'; dropped: -delta'
+            if (j == 0) {
+              d0 = sel_bit<7>(d0, ndl[j], t);
+              d1 = sel_bit<23>(d1, ndl[j + 1], t);
+            } else {
+              d0 = sel_bit<15>(d0, ndl[j], t);
+              d1 = sel_bit<31>(d1, ndl[j + 1], t);
+            }
+          }
+          sa[i] = p0;
+          sa[i + 1] = p1;
+          pa[i] = p0 * d0;  // dS
+          pa[i + 1] = p1 * d1;
+        }
+      }
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+        pb[st] = pack8<E>(sa, st);
+        if constexpr (DROP) pb[st] = and_pairs(pb[st], dm[4 * st], dm[4 * st + 1], dm[4 * st + 2], dm[4 * st + 3]);
+        db[st] = pack8<E>(pa, st);
+      }
+    };
+    // dV^T[d, key] += dO^T[d, q] . P[q, key] ; dK^T[d, key] += Q^T[d, q] . dS[q, key]
+    auto acc_mma = [&](int qs2, const v8_t<E> (&pb)[2], const v8_t<E> (&db)[2]) {
+#pragma unroll
+      for (int st = 0; st < 2; ++st)
+#pragma unroll
+        for (int dt = 0; dt < G::DT; ++dt) {
+          dv[dt] = mfma(fr.trf(do_l, 32 * qs2, st, dt), pb[st], dv[dt]);
+          dk[dt] = mfma(fr.trf(q_l, 32 * qs2, st, dt), db[st], dk[dt]);
+        }
+    };
+    if (!CAUSAL || qb >= kw + 32) {
+      // Both 32-query halves fully visible (every item but the causal diagonal ones): one block
+      // of straight-line code whose two halves are independent, so the scheduler overlaps the
+      // softmax VALU of one half with the other half's MFMAs.
+      f32x16 s0, p0, s1, p1;
+      v8_t<E> pb0[2], db0[2], pb1[2], db1[2];
+      sd_init(0, false, s0, p0);
+      sd_init(1, false, s1, p1);
+      sd_mma(0, s0, p0);
+      sd_mma(1, s1, p1);
+      softmax_ds(0, s0, p0, pb0, db0);
+      acc_mma(0, pb0, db0);
+      softmax_ds(1, s1, p1, pb1, db1);
+      acc_mma(1, pb1, db1);
+    } else {
+#pragma unroll
+      for (int qs2 = 0; qs2 < 2; ++qs2) {
+        const int qsub = qb + 32 * qs2;
+        if (qsub + 31 < kw) continue;  // all queries precede all of this wave's keys
+        f32x16 sa, pa;
+        v8_t<E> pb[2], db[2];
+        sd_init(qs2, qsub == kw, sa, pa);   // the diagonal block folds its mask in
+        sd_mma(qs2, sa, pa);
+        softmax_ds(qs2, sa, pa, pb, db);
+        acc_mma(qs2, pb, db);
+      }
+    }
     if (++cq == ntiles) {
       cq = 0;
       ++ch;

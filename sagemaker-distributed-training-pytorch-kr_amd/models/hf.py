@@ -352,12 +352,53 @@ class HFCausalLM(nn.Module):
         return w
 
     # ---- forward
+    def _pack_index(self, attention_mask):
+        """Seq-first flat indices of the real tokens when the micro-batch can run padding-free
+        (models/transformer.py ``packed_sequences``): a right-padded CPU mask (no device sync),
+        no tensor / pipeline / context parallelism, and some padding to save. Else None."""
+        if (attention_mask is None or os.environ.get("SMDT_SFT_UNPAD", "1") != "1"
+                or attention_mask.device.type != "cpu" or attention_mask.dim() != 2):
+            return None
+        from ..parallel import state as ps
+        st = ps.get_state() if ps.model_parallel_is_initialized() else None
+        if st is not None and (st.tp > 1 or st.pp > 1 or st.cp > 1):
+            return None
+        m = attention_mask.bool()
+        if bool(m.all()) or not bool(m[:, 0].all()) or bool((m[:, 1:] & ~m[:, :-1]).any()):
+            return None                              # nothing to save, or not right-padded
+        ms = m.t().reshape(-1)
+        real = ms.nonzero().squeeze(1)
+        # round the token count up to a multiple of 64 with pad positions (pads never reach a real
+        # token under the causal mask and carry label -100): GEMM / wgrad tiles want M % 32 == 0
+        need = -real.numel() % 64
+        pads = (~ms).nonzero().squeeze(1)
+        if pads.numel() < need or real.numel() + need >= ms.numel():
+            return None
+        return torch.cat([real, pads[:need]]).sort().values
+
     def forward(self, input_ids, attention_mask=None, labels=None, **_):
-        """Returns (mean loss over label tokens, per-token loss [b, s]) with HF shift semantics."""
+        """Returns (mean loss over label tokens, per-token loss [b, s]) with HF shift semantics.
+        With a right-padded CPU ``attention_mask`` the model runs on the real tokens only."""
         if labels is None:
             return None, self.model(input_ids)[..., : self.vocab_size]
         shifted = torch.full_like(labels, -100)
         shifted[:, :-1] = labels[:, 1:]
+        idx = self._pack_index(attention_mask)
+        if idx is not None:
+            from .transformer import packed_sequences
+            b, L = input_ids.shape
+            idx = idx.to(input_ids.device, non_blocking=True)
+            tok = input_ids.t().reshape(-1).index_select(0, idx).unsqueeze(0)          # [1, T]
+            pos = torch.div(idx, b, rounding_mode="floor").unsqueeze(0)                # position in its row
+            lab = shifted.t().reshape(-1).index_select(0, idx).unsqueeze(0)
+            self.last_computed_tokens = int(idx.numel())
+            with packed_sequences(idx, b, L):
+                tl = self.model(tok, pos, None, labels=lab)                            # [1, T]
+            valid = (lab != -100).float()
+            loss = (tl.float() * valid).sum() / valid.sum().clamp(min=1.0)
+            tok_loss = tl.new_zeros(L * b).index_copy(0, idx, tl.reshape(-1)).view(L, b).t()
+            return loss, tok_loss
+        self.last_computed_tokens = int(input_ids.numel())
         tok_loss = self.model(input_ids, None, None, labels=shifted)
         valid = (shifted != -100).float()
         loss = (tok_loss.float() * valid).sum() / valid.sum().clamp(min=1.0)

@@ -122,6 +122,47 @@ class Norm(nn.Module):
         return self.fused(x, None, None, 0.0, False)[0]
 
 
+# ---------------------------------------------------------------------------------------------
+# Padding-free ("unpadded") micro-batches. An SFT micro-batch is right-padded to its longest
+# example; with causal attention a real token never sees a pad, so the pads only cost compute.
+# Under ``packed_sequences`` every token-wise op (embeddings, GEMMs, norms, MLP, LM head + CE)
+# runs on the T real tokens only ([T, 1, h]); attention alone scatters its fused QKV into the
+# padded [L, b] layout (zeros in the pad rows), runs RoPE + the causal flash kernels there and
+# gathers the T context rows back. Real-token outputs and all gradients equal the padded
+# computation's (models/hf.py ``HFCausalLM.forward`` sets it up from the attention mask).
+_PACK = {"idx": None, "b": 0, "L": 0}
+
+
+class packed_sequences:
+    """Context: ``idx`` (device int64 [T]) = seq-first flat positions s * b + bi of the real
+    tokens of a right-padded [b, L] batch."""
+
+    def __init__(self, idx, b: int, L: int):
+        self.state = {"idx": idx, "b": int(b), "L": int(L)}
+
+    def __enter__(self):
+        self.prev = dict(_PACK)
+        _PACK.update(self.state)
+        return self
+
+    def __exit__(self, *exc):
+        _PACK.update(self.prev)
+        return False
+
+
+def _unpack_rows(x):
+    """[T, 1, W] -> [L, b, W] with zero pad rows (differentiable)."""
+    idx, b, L = _PACK["idx"], _PACK["b"], _PACK["L"]
+    W = x.shape[-1]
+    return x.new_zeros(L * b, W).index_copy(0, idx, x.reshape(-1, W)).view(L, b, W)
+
+
+def _pack_rows(x):
+    """[L, b, C] -> [T, 1, C] (the real-token rows)."""
+    C = x.shape[-1]
+    return x.reshape(-1, C).index_select(0, _PACK["idx"]).unsqueeze(1)
+
+
 class ParallelAttention(nn.Module):
     def __init__(self, cfg: TransformerConfig, layer_number: int, device=None):
         super().__init__()
@@ -187,6 +228,11 @@ class ParallelAttention(nn.Module):
 
     def forward(self, x, training=True):
         qkv = self.qkv(x)                                        # [s, b, (nh + 2 nkv) d]
+        if _PACK["idx"] is not None:                              # padding-free micro-batch
+            return self.proj(_pack_rows(self._attend(_unpack_rows(qkv), training)))
+        return self.proj(self._attend(qkv, training))            # (out, bias)
+
+    def _attend(self, qkv, training):
         cp = ps.get_state().cp
         if self.rope is not None:
             cos, sin, rot = self.rope
@@ -195,7 +241,7 @@ class ParallelAttention(nn.Module):
                 cos, sin = cos[off: off + qkv.shape[0]], sin[off: off + qkv.shape[0]]
             qkv = _RopeQKV.apply(qkv, cos, sin, rot, self.nh, self.nkv, self.hd)
         if cp > 1:
-            return self.proj(self.core_attention_context_parallel(qkv, training))
+            return self.core_attention_context_parallel(qkv, training)
         if self.cfg.use_flash_attn:
             # attention dropout runs inside the flash kernels; heads are TP-sharded, so the mask
             # comes from the per-TP-rank stream (Megatron forks the model-parallel tracker here)
@@ -209,7 +255,7 @@ class ParallelAttention(nn.Module):
             ctx = rng_checkpoint(lambda t: self.core_attention_unfused(t, training), qkv)
         else:
             ctx = self.core_attention_unfused(qkv, training)
-        return self.proj(ctx)                                    # (out, bias)
+        return ctx
 
 
 class _RopeQKV(torch.autograd.Function):

@@ -18,6 +18,7 @@ from typing import Optional
 import torch
 import torch.distributed as dist
 
+from ..parallel import tensor_parallel as _tp
 from .optimizer import MixedPrecisionAdam
 
 
@@ -72,6 +73,7 @@ class CPUOffloadAdam(MixedPrecisionAdam):
         if lr is not None:
             self.lr = lr
         self.param_groups[0]["lr"] = self.lr
+        _tp.params_changed()
         ddp = self.ddp
         ddp.wait_param_gather()
         g = ddp.grad_data

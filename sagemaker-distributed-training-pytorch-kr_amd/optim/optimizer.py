@@ -31,6 +31,7 @@ from ..comm import stats as _cs
 from ..ops import _ext
 from ..parallel import state as ps
 from ..parallel.distributed import DistributedDataParallel
+from ..parallel import tensor_parallel as _tp
 
 
 class DynamicLossScaler:
@@ -152,6 +153,7 @@ class MixedPrecisionAdam:
         if lr is not None:
             self.lr = lr
         self.param_groups[0]["lr"] = self.lr
+        _tp.params_changed()
         ddp = self.ddp
         if hasattr(ddp, "wait_param_gather"):
             ddp.wait_param_gather()
@@ -236,6 +238,7 @@ class MixedPrecisionAdam:
     def repair_params(self):
         """Model-dtype parameters <- fp32 masters for this rank's pieces, then (ZeRO) re-gather the
         full buffer: undoes NaN-filled parameter gathers after a collective timed out."""
+        _tp.params_changed()
         ddp = self.ddp
         if hasattr(ddp, "wait_param_gather"):
             ddp.wait_param_gather()
@@ -252,6 +255,7 @@ class MixedPrecisionAdam:
     @torch.no_grad()
     def reload_model_params(self):
         """Refresh the fp32 masters from the model buffer (after loading weights only)."""
+        _tp.params_changed()
         for (s, e, _), mo in zip(self.pieces, self.master_off):
             self.master[mo:mo + (e - s)].copy_(self.ddp.param_data[s:e].float())
 

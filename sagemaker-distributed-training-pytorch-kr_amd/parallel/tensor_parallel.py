@@ -387,13 +387,37 @@ def _wgrad(weight, g2, t2):
 _DGRAD_TN = os.environ.get("SMDT_DGRAD_TN", "1") == "1"
 
 
+# W^T is kept from the first backward that needs it until the parameters next change, so gradient
+# accumulation (NB4: 8 micro-batches per step) and pipeline micro-batches transpose each weight
+# once per optimizer step instead of once per micro-batch (LLaMA-7B: 27 GB of transpose traffic
+# per micro-batch). Entries are keyed on the weight's storage and version counter, and the whole
+# cache is dropped by ``params_changed()``, which every optimizer step / parameter repair / master
+# reload calls before it writes parameters (those writes go through raw kernels that do not bump
+# version counters). SMDT_DGRAD_WT_CACHE=0 transposes per call.
+_WT_CACHE_ON = os.environ.get("SMDT_DGRAD_WT_CACHE", "1") == "1"
+_WT_CACHE: dict = {}
+
+
+def params_changed():
+    """Invalidate every cached W^T (call before any out-of-autograd parameter write)."""
+    _WT_CACHE.clear()
+
+
 def _dgrad_weight_t(weight):
     """W^T [in, out] contiguous for the TN dgrad, or None to use dY @ W directly."""
     if (_DGRAD_TN and weight.is_cuda and weight.dim() == 2 and weight.is_contiguous()
             and weight.dtype in (torch.bfloat16, torch.float16)
             and weight.shape[0] % 8 == 0 and weight.shape[1] % 8 == 0
             and _ext.use_kernels(weight)):   # raises on a GPU box without the extension
-        return _ext.ext().transpose2d(weight)
+        if not _WT_CACHE_ON:
+            return _ext.ext().transpose2d(weight)
+        key = (weight.data_ptr(), weight._version, tuple(weight.shape), weight.dtype)
+        hit = _WT_CACHE.get(id(weight))
+        if hit is not None and hit[0] == key:
+            return hit[1]
+        wt = _ext.ext().transpose2d(weight)
+        _WT_CACHE[id(weight)] = (key, wt)
+        return wt
     return None
 
 

@@ -199,6 +199,7 @@ class Trainer:
         tokens = torch.zeros((), dtype=torch.float64, device=self.device)
         # every non-pad input token (prompt + response): the work the model does, for MFU
         in_tokens = torch.zeros((), dtype=torch.float64, device=self.device)
+        pad_tokens = 0         # tokens computed including the padding of each micro-batch
         steady = None          # (time, input tokens) after the first optimizer step (kernel tuning, caches)
         n_seen = 0
         steps_since_log = 0
@@ -215,12 +216,14 @@ class Trainer:
                 ids = batch["input_ids"].to(self.device, non_blocking=True)
                 labels = batch["labels"].to(self.device, non_blocking=True)
                 maybe_inject_fault(self.state["global_step"] + 1, self.rank)
-                loss, _ = self.model(ids, attention_mask=None, labels=labels)
+                # the CPU attention mask lets the model skip the padding (models/hf.py)
+                loss, _ = self.model(ids, attention_mask=batch.get("attention_mask"), labels=labels)
                 eng.backward(loss)
                 tr_loss += loss.detach().float() / ga
                 tokens += (labels != -100).sum()
                 am = batch.get("attention_mask")
                 in_tokens += am.sum() if am is not None else ids.numel()
+                pad_tokens += getattr(self.model, "last_computed_tokens", None) or ids.numel()
                 n_seen += ids.shape[0]
                 gn = eng.step()
                 if gn is None:
@@ -292,7 +295,10 @@ class Trainer:
             tfl = tps * fpt / max(1, self.world) / 1e12
             metrics.update({"train_input_tokens_per_second": round(tps, 1),
                             "train_model_tflops_per_gpu": round(tfl, 2),
-                            "train_mfu": round(tfl / MI355X_BF16_PEAK_TFLOPS, 4)})
+                            "train_mfu": round(tfl / MI355X_BF16_PEAK_TFLOPS, 4),
+                            # share of the computed tokens (padded, or padding-free rounded up to
+                            # 64) that are real input tokens
+                            "train_nonpad_fraction": round(float(in_tokens) / max(1, pad_tokens * max(1, self.world)), 4)})
         self.log(metrics)
         self.train_metrics = metrics
         return metrics

@@ -304,6 +304,29 @@ def test_flash_attention_dropout(D, causal, heads, dt):
     assert torch.equal(o2, o.detach()) and not torch.equal(o3, o2)
 
 
+@pytest.mark.parametrize("S", [384, 512, 1024])
+@pytest.mark.parametrize("causal", [True, False])
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_flash_attention_d64_lengths(S, causal, p):
+    """D = 64 at several lengths: S % 256 == 0 runs the 64-queries-per-wave forward (several
+    256-row blocks, every causal diagonal case), S = 384 the 32-query one."""
+    torch.manual_seed(15)
+    B, H, D = 2, 4, 64
+    q, k, v = (torch.randn(B, S, H, D, device=DEV, dtype=torch.bfloat16, requires_grad=True) for _ in range(3))
+    scale = 1 / math.sqrt(D)
+    o = SF._FlashAttn.apply(q, k, v, scale, causal, p, 99, 5)
+    keep = SF.flash_dropout_keep_mask(B, H, S, p, 99, 5, DEV) if p > 0 else None
+    qr, kr, vr = (t.detach().float().requires_grad_() for t in (q, k, v))
+    orf = SF.attention_ref(qr, kr, vr, scale, causal, p, keep) if p > 0 else SF.attention_ref(qr, kr, vr, scale, causal)
+    torch.testing.assert_close(o.float(), orf, atol=2e-2, rtol=2e-2)
+    do = torch.randn_like(o)
+    o.backward(do)
+    orf.backward(do.float())
+    for a, r in ((q, qr), (k, kr), (v, vr)):
+        err = (a.grad.float() - r.grad).abs().max().item()
+        assert err < 0.05 * max(1.0, r.grad.abs().max().item()), err
+
+
 def test_flash_attention_qkv_seq_first_matches_unfused():
     torch.manual_seed(11)
     S, B, nh, hd = 256, 2, 4, 64
@@ -456,3 +479,24 @@ def test_linear_dgrad_tn_matches_nn(dt):
     out = torch.empty_like(x.grad)
     tp.dgrad_into(out, g, w.detach(), wt)
     assert torch.equal(out, tp.dgrad(g, w.detach(), wt))
+
+
+
+def test_dgrad_weight_t_cache_invalidation():
+    """W^T is reused while the weight is unchanged, rebuilt after an in-place torch write (version
+    counter) and after params_changed() (the optimizer's raw-kernel writes)."""
+    from smdt_amd.parallel import tensor_parallel as tp
+    w = torch.nn.Parameter(torch.randn(256, 128, device=DEV, dtype=torch.bfloat16))
+    a = tp._dgrad_weight_t(w)
+    assert a is tp._dgrad_weight_t(w)
+    with torch.no_grad():
+        w.add_(1.0)
+    b = tp._dgrad_weight_t(w)
+    assert b is not a and torch.equal(b, w.detach().t().contiguous())
+    raw = w.detach().view(-1)
+    _C().adam(torch.zeros(raw.numel(), device=DEV), torch.ones(raw.numel(), device=DEV),
+              torch.zeros(raw.numel(), device=DEV), torch.zeros(raw.numel(), device=DEV), raw, 1e-3, 0.9, 0.95,
+              1e-8, 0.0, 1, True, torch.ones(1, device=DEV), None)   # raw kernel write: no version bump
+    tp.params_changed()
+    c = tp._dgrad_weight_t(w)
+    assert c is not b and torch.equal(c, w.detach().t().contiguous())

@@ -240,3 +240,45 @@ def test_save_total_limit_rotates(tmp_path):
     t.train()
     cks = sorted(p.name for p in (tmp_path / "out").iterdir() if p.name.startswith("checkpoint-"))
     assert cks == ["checkpoint-6"]
+
+
+@pytest.mark.parametrize("mt", ["llama", "opt"])
+def test_padding_free_microbatch_matches_padded(mt, monkeypatch):
+    """A right-padded micro-batch run on its real tokens only (models/transformer.py
+    packed_sequences: attention alone sees the padded layout) gives the padded run's loss,
+    per-token losses and every gradient."""
+    from smdt_amd.models.hf import HFCausalLM
+    from smdt_amd.models import transformer as T
+    if mt == "llama":
+        cfg = W.SFT_LLAMA
+    else:
+        cfg = {"model_type": "opt", "hidden_size": 64, "num_hidden_layers": 2, "num_attention_heads": 4,
+               "ffn_dim": 128, "max_position_embeddings": 128, "vocab_size": 120, "word_embed_proj_dim": 64,
+               "do_layer_norm_before": True, "activation_function": "relu", "pad_token_id": 1, "enable_bias": True}
+    torch.manual_seed(0)
+    m = HFCausalLM(cfg, params_dtype=torch.float32).eval()
+    b, L = 4, 64
+    ids = torch.randint(3, 100, (b, L))
+    am = torch.zeros(b, L, dtype=torch.bool)
+    for i, n in enumerate([64, 40, 17, 9]):
+        am[i, :n] = True
+    ids[~am] = 0
+    lab = ids.clone()
+    lab[~am] = -100
+    lab[:, :3] = -100
+    monkeypatch.setenv("SMDT_SFT_UNPAD", "0")
+    l0, t0 = m(ids, attention_mask=am, labels=lab)
+    g0 = torch.autograd.grad(l0, list(m.parameters()))
+    monkeypatch.setenv("SMDT_SFT_UNPAD", "1")
+    calls = []
+    orig = T._unpack_rows
+    monkeypatch.setattr(T, "_unpack_rows", lambda x: calls.append(x.shape[0]) or orig(x))
+    l1, t1 = m(ids, attention_mask=am, labels=lab)
+    g1 = torch.autograd.grad(l1, list(m.parameters()))
+    assert calls and calls[0] == 192                    # 130 real tokens rounded up to 64 with pads
+    torch.testing.assert_close(l1, l0, rtol=1e-6, atol=1e-6)
+    keep = torch.zeros_like(am)
+    keep[:, :-1] = lab[:, 1:] != -100
+    torch.testing.assert_close(t1[keep], t0[keep], rtol=1e-5, atol=1e-6)
+    for a, c in zip(g0, g1):
+        torch.testing.assert_close(c, a, rtol=1e-4, atol=1e-6)
