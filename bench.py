@@ -35,8 +35,8 @@ embd / mp) and op the calls, MB, ms and bus GB/s per step, keyed by the transpor
 Scaling is WEAK: every GPU processes ``--seqs-per-gpu`` (64) sequences of 1024 tokens per step
 at every N, so global batch = 64 N. A DP replica (tp x pp GPUs) therefore runs 64 tp pp sequences
 per step: with pp == 1 as micro-batches of up to 64 sequences (gradient accumulation beyond),
-with pp > 1 as micro-batches of 16 — 16 micro-batches at tp2pp2 keep the 1F1B bubble
-(pp - 1) / m at 6.25 %.
+with pp > 1 as micro-batches of up to 32 — 8 micro-batches at tp2pp2: the 1F1B bubble (pp - 1) / m
+is 12.5 %, but the larger GEMMs more than pay for it (213 vs 220 ms per rank measured for 16 x 16).
 """
 from __future__ import annotations
 
@@ -75,8 +75,7 @@ def parse():
     p.add_argument("--sequence-parallel", type=int, default=None, help="default: on when tp > 1")
     # 64 x 1024 tokens per GPU per step: the 288 GB of HBM holds it without recompute; on one
     # MI355X it measured +3.2 % tokens/s over 32 (profiles/r2_mbs/; 32 was +5 % over 16), it halves
-    # the gradient / optimizer bytes per token, and at pp = 2 it gives 16 micro-batches per step
-    # (1F1B bubble (pp - 1) / m = 6 %).
+    # the gradient / optimizer bytes per token, and at pp = 2 it gives 8 micro-batches of 32 per step.
     p.add_argument("--seqs-per-gpu", type=int, default=64, help="sequences per GPU per step (weak scaling)")
     p.add_argument("--micro-batch-size", type=int, default=None)
     p.add_argument("--grad-accum", type=int, default=None, help="micro-batches per step per DP rank")
@@ -207,7 +206,10 @@ def choose_layout(a, world):
     elif pp == 1:
         mbs = min(replica, 64)
     else:
-        mbs = max(1, min(16, replica // (4 * pp)))  # >= 4 pp micro-batches: bubble <= 20 %
+        # >= 4 pp micro-batches (bubble <= 20 %), at most 32 sequences each: at N = 8 (256
+        # sequences per replica) 8 micro-batches of 32 measured 213 ms per rank incl. the 1F1B
+        # bubble vs 220 ms for 16 of 16 (benchmarks/predict_mbs.py, profiles/r3_predict/)
+        mbs = max(1, min(32, replica // (4 * pp)))
     ga = a.grad_accum if a.grad_accum is not None else max(1, replica // mbs)
     return tp, pp, sp, mbs, ga
 

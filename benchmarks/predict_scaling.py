@@ -11,8 +11,8 @@ them. Two inputs:
         1-GPU step itself;
       * tp2 pp2 dp2 (N = 8, BASELINE): a rank holds 12 of the 24 layers with half the heads (8 x 64)
         and half the FFN (2048), and the last stage half of the (tied) LM head (vocab 50304 / 2);
-        the replica's 4 GPUs process 4 x 64 = 256 sequences per step, as 16 micro-batches of 16.
-        Emulated as a 12-layer model of that width on 256 sequences (micro-batch 16, 16
+        the replica's 4 GPUs process 4 x 64 = 256 sequences per step, as 8 micro-batches of 32.
+        Emulated as a 12-layer model of that width on 256 sequences (micro-batch 32, 8
         micro-batches). Sequence parallelism would halve LayerNorm / dropout / residual work and
         the ring-chunked GEMMs run at M = 8192 instead of 16384: both are noted, not modelled;
       * tp2 (N = 2, the old default, ``--layout tp``): 24 layers at half width, 128 sequences.
@@ -40,7 +40,7 @@ H, L, S, V = 1024, 24, 1024, 50304
 PARAMS = 354.9e6            # GPT-2 345M with the padded vocab (tied embedding)
 
 _TP2 = ["--num-attention-heads", "8", "--kv-channels", "64", "--ffn-hidden-size", "2048", "--vocab-size", str(V // 2)]
-_MB16 = ["--seqs-per-gpu", "256", "--micro-batch-size", "16", "--grad-accum", "16"]
+_MB16 = ["--seqs-per-gpu", "256", "--micro-batch-size", "32", "--grad-accum", "8"]   # bench.py's N = 8 split
 RUNS = {
     "n1_dp": [],
     # even split: 12 + 12 layers, the last stage also runs the LM head (the heavier stage)
@@ -95,12 +95,12 @@ def predict(m: dict) -> list:
     tr_even = m["tp2pp2_rank"]["ms_per_step"]
     bal = "tp2pp2_stage0_bal" in m and "tp2pp2_stage1_bal" in m
     tr = max(m["tp2pp2_stage0_bal"]["ms_per_step"], m["tp2pp2_stage1_bal"]["ms_per_step"]) if bal else tr_even
-    mb, pp = 16, 2
+    mb, pp = 8, 2                                           # micro-batches per step, stages
     bubble = tr * (pp - 1) / mb
     grads = 4 * PARAMS / 4                                  # fp32 grads of a rank's quarter
     dp_tail = link_ms(16e6 / 2) + link_ms(8e6 / 2)          # last RS bucket + first AG bucket, dp2 = 1 link
     embd = link_ms(4 * (V // 2) * H)                        # tied-embedding grad all-reduce, first <-> last stage
-    tp_chunk = S // 2 * 16 * H * 2                          # [s/2, mbs, h] bf16 = 16 MB per ring step
+    tp_chunk = S // 2 * 32 * H * 2                          # [s/2, mbs, h] bf16 = 32 MB per ring step
     relay_links = 4.0                                       # relay on 8 GPUs: ~4x one link (docs/XGMI.md)
     tp_per_ex = link_ms(tp_chunk, relay_links)
     tp_total = tp_per_ex * 8 * 12 * mb                      # 8 exchanges / layer / micro-batch, 12 layers

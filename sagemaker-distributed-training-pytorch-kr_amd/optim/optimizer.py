@@ -21,6 +21,7 @@ style: only the owned shard of each bucket is needed after the collective).
 from __future__ import annotations
 
 import math
+import os
 from typing import Optional
 
 import torch
@@ -156,7 +157,7 @@ class MixedPrecisionAdam:
         _tp.params_changed()
         ddp = self.ddp
         if hasattr(ddp, "wait_param_gather"):
-            ddp.wait_param_gather()
+            ddp.wait_param_gather()          # (also the previous step's overlapped updates)
         g = ddp.grad_data
         self.found_inf.zero_()
         total = torch.zeros(1, dtype=torch.float32, device=self.device)
@@ -194,6 +195,12 @@ class MixedPrecisionAdam:
         t = self.step_count
         bc1 = 1 - self.beta1 ** t
         bc2 = 1 - self.beta2 ** t
+        if (use_k and self.zero and getattr(ddp, "overlap_optimizer", False) and ddp.zero3 is None
+                and not self.param_is_fp32 and len(self.pieces) == len(ddp.buckets)):
+            self._step_overlapped(g, mul, t)
+            if self.scaler is not None:
+                self.scaler.update(self.found_inf)
+            return self.grad_norm
         for (s, e, key), mo in zip(self.pieces, self.master_off):
             if e <= s:
                 continue
@@ -234,6 +241,37 @@ class MixedPrecisionAdam:
             ddp.all_gather_params()
         return self.grad_norm
 
+    def _step_overlapped(self, g, mul, t):
+        """The fused AdamW of every bucket on a side stream, in the forward order DDP computed
+        (``opt_bucket_order``), one event per bucket that the forward pre-hooks wait on; each
+        bucket's gradients are zeroed right after its update (DDP.zero_grad_buffer skips them)."""
+        ddp = self.ddp
+        cur = torch.cuda.current_stream(self.device)
+        if getattr(self, "_opt_stream", None) is None:
+            self._opt_stream = torch.cuda.Stream(device=self.device)
+        side = self._opt_stream
+        side.wait_stream(cur)                  # the norm, the clip coefficient, found_inf
+        delay = int(os.environ.get("SMDT_OPT_STREAM_DELAY", "0"))   # tests: widen the race window
+        with torch.cuda.stream(side):
+            for i in ddp.opt_bucket_order:
+                if delay:
+                    torch.cuda._sleep(delay)
+                s, e, key = self.pieces[i]
+                if e <= s:
+                    continue
+                mo, n = self.master_off[i], e - s
+                wd = self.weight_decay if key[0] else 0.0
+                gr = g[s:e]
+                _ext.ext().adam(self.master[mo:mo + n], gr, self.exp_avg[mo:mo + n], self.exp_avg_sq[mo:mo + n],
+                                ddp.param_data[s:e], self.lr, self.beta1, self.beta2, self.eps, wd, t, self.adamw,
+                                mul, self.found_inf)
+                gr.zero_()
+                ev = torch.cuda.Event()
+                ev.record(side)
+                ddp._opt_events[i] = ev
+        mul.record_stream(side)                # freed tensors must outlive the side-stream reads
+        ddp._async_zeroed = True
+
     @torch.no_grad()
     def repair_params(self):
         """Model-dtype parameters <- fp32 masters for this rank's pieces, then (ZeRO) re-gather the
@@ -256,6 +294,7 @@ class MixedPrecisionAdam:
     def reload_model_params(self):
         """Refresh the fp32 masters from the model buffer (after loading weights only)."""
         _tp.params_changed()
+        self.ddp.wait_param_gather()
         for (s, e, _), mo in zip(self.pieces, self.master_off):
             self.master[mo:mo + (e - s)].copy_(self.ddp.param_data[s:e].float())
 
@@ -264,6 +303,7 @@ class MixedPrecisionAdam:
 
     # ------------------------------------------------------------------ checkpoint
     def state_dict(self):
+        self.ddp.wait_param_gather()         # an overlapped update may still be writing the state
         d = {"step": self.step_count, "master": self.master, "exp_avg": self.exp_avg,
              "exp_avg_sq": self.exp_avg_sq, "lr": self.lr, "zero": self.zero,
              "pieces": [(s, e) for s, e, _ in self.pieces]}
@@ -272,6 +312,8 @@ class MixedPrecisionAdam:
         return d
 
     def load_state_dict(self, d):
+        self.ddp.wait_param_gather()
+        _tp.params_changed()
         self.step_count = int(d["step"])
         self.master.copy_(d["master"])
         self.exp_avg.copy_(d["exp_avg"])

@@ -23,6 +23,7 @@ MI355X-first layout:
 from __future__ import annotations
 
 import contextlib
+import os
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Tuple
 
@@ -233,6 +234,21 @@ class DistributedDataParallel(nn.Module):
                 if own:
                     bks = sorted({self.param_bucket[id(p)].index for p in own})
                     self._pg_hooks.append(mod.register_forward_pre_hook(self._make_gather_wait(bks)))
+        # Optimizer step overlapped with the next forward (one DP rank, ZeRO optimizer, HIP): the
+        # fused AdamW of each bucket runs on a side stream in FORWARD order and records an event;
+        # a forward pre-hook on every transformer block (and on the root, for the embeddings /
+        # head / final norm) makes the compute stream wait only for its own buckets. Each bucket's
+        # gradients are re-zeroed on the side stream right after its update. On LLaMA-7B the
+        # memory-bound update (30 B per parameter, ~36 ms) then runs under the forward GEMMs.
+        # SMDT_OVERLAP_OPTIMIZER=0 keeps the step synchronous.
+        self._opt_events: Dict[int, object] = {}
+        self._async_zeroed = False
+        self.overlap_optimizer = bool(use_distributed_optimizer and self.dp == 1 and dev.type == "cuda"
+                                      and st.pp == 1 and not torch_compat
+                                      and os.environ.get("SMDT_OVERLAP_OPTIMIZER", "1") == "1")
+        self.opt_bucket_order = list(reversed(range(len(self.buckets))))
+        if self.overlap_optimizer:
+            self._install_update_waits(module)
         self._reset_pending()
         if self.dp > 1 and not self._zero_init:
             self.broadcast_params()
@@ -511,7 +527,9 @@ class DistributedDataParallel(nn.Module):
         _health.monitor().consume()      # the previous step's engine-error flag (comm/health.py)
         if self.xgmi is not None and not self.xgmi.active:
             self.xgmi = None
-        if self._direct:
+        if self._async_zeroed:           # the overlapped optimizer re-zeroed every bucket
+            self._async_zeroed = False
+        elif self._direct:
             self.grad_store.zero_()
         elif self.zero_stage >= 2:
             for b in self.buckets:
@@ -559,12 +577,49 @@ class DistributedDataParallel(nn.Module):
             self.wait_param_gather()
 
     def wait_param_gather(self, indices=None):
+        """Parameters of the given buckets (default: all) are final on the current stream: the
+        overlapped ZeRO all-gather and / or the overlapped optimizer update have landed."""
+        if self._opt_events:
+            self.wait_param_update(indices)
         for b in (self.buckets if indices is None else (self.buckets[i] for i in indices)):
             h = getattr(b, "ag_handle", None)
             if h is not None:
                 with _cs.waiting("dp"):
                     h.wait()
                 b.ag_handle = None
+
+    def wait_param_update(self, indices=None):
+        cur = torch.cuda.current_stream(self.param_data.device) if self._opt_events else None
+        for i in (list(self._opt_events) if indices is None else indices):
+            ev = self._opt_events.pop(i, None)
+            if ev is not None:
+                cur.wait_event(ev)
+
+    def _install_update_waits(self, module):
+        """Forward pre-hooks for the overlapped optimizer (see __init__), and the bucket order
+        the optimizer updates in: the root's own buckets first, then block by block."""
+        blocks = [c for m in module.modules() if isinstance(m, nn.ModuleList) for c in m.children()]
+        owned, order, groups = set(), [], []
+        for blk in blocks:
+            ids = {id(p) for p in blk.parameters() if id(p) in self.param_bucket}
+            owned |= ids
+            groups.append((blk, sorted({self.param_bucket[i].index for i in ids})))
+        rest = {id(p) for p in module.parameters() if id(p) in self.param_bucket} - owned
+        groups.insert(0, (module, sorted({self.param_bucket[i].index for i in rest})))
+        for mod, bks in groups:
+            for i in bks:
+                if i not in order:
+                    order.append(i)
+            if bks:
+                self._pg_hooks.append(mod.register_forward_pre_hook(self._make_update_wait(bks)))
+        order += [i for i in range(len(self.buckets)) if i not in order]
+        self.opt_bucket_order = order
+
+    def _make_update_wait(self, indices):
+        def hook(_mod, _inp):
+            if self._opt_events:
+                self.wait_param_update(indices)
+        return hook
 
     def _make_gather_wait(self, indices):
         def hook(_mod, _inp):

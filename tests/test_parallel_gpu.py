@@ -181,3 +181,54 @@ def test_fused_fc1_bias_gelu_mlp_matches_unfused():
     for n in g2:
         err = (g1[n] - g2[n]).abs().max().item()
         assert err <= 0.03 * max(1.0, g2[n].abs().max().item()), (n, err)
+
+
+@pytest.mark.parametrize("stage", [1, 2])
+def test_overlapped_optimizer_step_matches_synchronous(stage, monkeypatch):
+    """One DP rank: the per-bucket fused AdamW on a side stream, waited for by the next forward's
+    block pre-hooks (parallel/distributed.py overlap_optimizer), gives the synchronous step's
+    losses, parameters and optimizer state. The side stream is delayed by ~1 ms before every
+    update (SMDT_OPT_STREAM_DELAY), so a missing wait would read stale weights; the tolerance
+    only absorbs run-to-run reduction-order noise (atomics in the wgrad tail)."""
+    from smdt_amd.models.hf import HFCausalLM
+    from smdt_amd.parallel import state as ps
+    from smdt_amd.train import zero as Z
+    from smdt_amd.train.zero import ZeroEngine
+    monkeypatch.setattr(Z, "MIN_BUCKET", 100_000)      # several buckets on this small model
+    cfg = dict(model_type="llama", hidden_size=256, num_hidden_layers=3, num_attention_heads=4,
+               num_key_value_heads=2, intermediate_size=512, max_position_embeddings=256, vocab_size=512,
+               rms_norm_eps=1e-6, rope_theta=10000.0, tie_word_embeddings=False)
+    ds = {"bf16": {"enabled": True}, "gradient_accumulation_steps": 2, "gradient_clipping": 1.0,
+          "optimizer": {"type": "AdamW", "params": {"lr": 1e-2, "weight_decay": 0.1}},
+          "zero_optimization": {"stage": stage, "reduce_bucket_size": 200_000}}
+    runs = []
+    monkeypatch.setenv("SMDT_OPT_STREAM_DELAY", "2000000")
+    for overlap in ("1", "0"):
+        monkeypatch.setenv("SMDT_OVERLAP_OPTIMIZER", overlap)
+        ps.destroy_model_parallel()
+        torch.manual_seed(0)
+        m = HFCausalLM(cfg, params_dtype=torch.bfloat16, device="cuda")
+        eng = ZeroEngine(m, ds, log=lambda *_: None)
+        assert eng.ddp.overlap_optimizer == (overlap == "1") and len(eng.ddp.buckets) > 2
+        g = torch.Generator(device="cuda").manual_seed(1)
+        losses = []
+        for _ in range(6):
+            ids = torch.randint(0, 500, (4, 128), device="cuda", generator=g)
+            loss, _ = m(ids, labels=ids)
+            eng.backward(loss)
+            eng.step()
+            losses.append(loss.detach().float())
+        eng.wait_for_params()
+        torch.cuda.synchronize()
+        runs.append((torch.stack(losses).cpu(), {n: p.detach().clone() for n, p in m.named_parameters()},
+                     eng.optimizer.exp_avg_sq.clone()))
+    (l1, p1, v1), (l2, p2, v2) = runs
+    # lr 1e-2: one step moves the loss by ~1e-1, so a forward on stale weights would show here
+    assert (l1[1:] - l1[:-1]).abs().max() > 1e-2
+    torch.testing.assert_close(l1, l2, atol=2e-3, rtol=0)
+    for n in p2:
+        # elements with near-zero gradients may flip their Adam direction on reduction-order
+        # noise (up to lr per step); everything else must agree
+        far = ((p1[n].float() - p2[n].float()).abs() > 2e-3 + 1e-2 * p2[n].float().abs()).float().mean().item()
+        assert far < 0.01, (n, far)
+    assert ((v1 - v2).abs() > 0.05 * v2.abs() + 1e-12).float().mean().item() < 0.01
