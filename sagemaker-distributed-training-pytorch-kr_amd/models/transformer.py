@@ -267,7 +267,9 @@ class _RopeQKV(torch.autograd.Function):
     @staticmethod
     def forward(ctx, qkv, cos, sin, rot, nh, nkv, hd):
         s, b, W = qkv.shape
-        if qkv.is_contiguous():
+        # a view (e.g. the [s, b, W] reshape of a TP linear's output under CP) cannot be marked
+        # dirty inside a custom Function, so it takes the copy
+        if qkv.is_contiguous() and qkv._base is None:
             out = qkv
             ctx.mark_dirty(qkv)
         else:
