@@ -98,8 +98,6 @@ def parse():
                    help="DDP bucket elements (default: auto, 8-32 MB from a start-up link timing)")
     p.add_argument("--comm-stats", type=int, default=1, help="phase_ms / per-collective stats in the JSON")
     p.add_argument("--no-flash", action="store_true")
-    p.add_argument("--fused-ce", action="store_true",
-                   help="chunked LM head + CE with its backward in forward (never materialises the logits)")
     p.add_argument("--recompute", choices=["none", "full"], default="none")
     p.add_argument("--profile-steps", type=int, default=0)
     p.add_argument("--tunableop", type=int, default=1,
@@ -240,8 +238,7 @@ def main():
                             attention_dropout=a.attention_dropout, params_dtype=torch.bfloat16,
                             sequence_parallel=sp and a.tp > 1, use_flash_attn=not a.no_flash,
                             recompute_granularity="full" if a.recompute == "full" else None,
-                            recompute_method="uniform" if a.recompute == "full" else None,
-                            fused_lm_head_ce=a.fused_ce)
+                            recompute_method="uniform" if a.recompute == "full" else None)
     model = GPTModel(cfg, pre_process=st.is_first_stage(),
                      post_process=st.is_last_stage() and not a.emulate_first_stage, device=dev)
     zero = bool(a.zero) and st.dp > 1
@@ -322,8 +319,6 @@ def main():
         phases_all = [None] * world
         dist.all_gather_object(phases_all, (st.pp_rank, explain["phase_ms"]))
     from smdt_amd.comm import xgmi
-    from smdt_amd.ops import functional as SF
-    SF.fused_linear_ce_check()   # (after the timed region) the fused LM head saw a plain mean
     relay.check_all()            # (after the timed region) no TP-pair exchange timed out
     global_batch = mbs * a.grad_accum * st.dp
     tokens_per_step = global_batch * S

@@ -541,36 +541,9 @@ void xgmi_allreduce(Tensor in, Tensor out, std::vector<int64_t> data_ptrs, std::
         "xgmi_allreduce");
 }
 
-// Forward linear GEMM with fused epilogue (linear_gemm.hip): x [M, K] (unit inner stride), w [N, K]
+
 // contiguous, bias [N] or None. epi 0: y = x w^T; 1: + bias; 2: h = x w^T + bias, y = gelu(h).
 // Returns [y] or [y, h].
-std::vector<Tensor> linear_fwd(Tensor x, Tensor w, c10::optional<Tensor> bias, int64_t epi, int64_t waves) {
-  need_cuda(x, "x");
-  need_cuda(w, "w");
-  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && x.stride(1) == 1 && w.is_contiguous() && x.size(1) == w.size(1),
-              "linear_fwd: x [M, K] (unit inner stride), w [N, K] contiguous");
-  TORCH_CHECK(x.scalar_type() == w.scalar_type() && (x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kHalf),
-              "linear_fwd: bf16 / fp16 operands of one dtype");
-  const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
-  TORCH_CHECK(smdt_linear_fwd_supported(M, N, K), "linear_fwd: unsupported shape M=", M, " N=", N, " K=", K);
-  TORCH_CHECK(x.stride(0) % 8 == 0 && ((uintptr_t)x.data_ptr() & 15) == 0 && ((uintptr_t)w.data_ptr() & 15) == 0,
-              "linear_fwd: 16-byte aligned rows");
-  const void* bp = nullptr;
-  if (epi >= 1) {
-    TORCH_CHECK(bias.has_value() && bias->is_contiguous() && bias->numel() == N && bias->scalar_type() == x.scalar_type(),
-                "linear_fwd: bias [N] of the operand dtype");
-    TORCH_CHECK(((uintptr_t)bias->data_ptr() & 7) == 0, "linear_fwd: 8-byte aligned bias");
-    bp = bias->data_ptr();
-  }
-  Tensor y = at::empty({M, N}, x.options());
-  Tensor h = epi == 2 ? at::empty({M, N}, x.options()) : Tensor();
-  check(smdt_linear_fwd(dcode(x), (int)epi, x.data_ptr(), w.data_ptr(), bp, y.data_ptr(),
-                        epi == 2 ? h.data_ptr() : nullptr, M, N, K, x.stride(0), K, N, (int)waves, cur_stream()),
-        "linear_fwd");
-  if (epi == 2) return {y, h};
-  return {y};
-}
-
 // General form: mode 0/1 all-reduce (n = elements), 2 reduce-scatter, 3 all-gather (n = elements
 // per slice, slices slice_stride elements apart in the input (RS) / output (AG)). in / out are raw
 // views (the reduce-scatter output may alias the input's slice `rank`, the all-gather input may
@@ -711,9 +684,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("xgmi_allreduce", &xgmi_allreduce, py::arg("input"), py::arg("out"), py::arg("data_ptrs"), py::arg("sig_ptrs"),
         py::arg("rank"), py::arg("nranks_local"), py::arg("region_bytes"), py::arg("two_shot"), py::arg("blocks"),
         py::arg("scale") = 1.0);
-  m.def("linear_fwd", &linear_fwd, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("epi"),
-        py::arg("waves") = 0);
-  m.def("linear_fwd_supported", &smdt_linear_fwd_supported);
   m.def("xgmi_collective", &xgmi_collective, py::arg("mode"), py::arg("input"), py::arg("out"), py::arg("data_ptrs"),
         py::arg("sig_ptrs"), py::arg("rank"), py::arg("nranks_local"), py::arg("region_bytes"), py::arg("blocks"),
         py::arg("n"), py::arg("slice_stride"), py::arg("scale") = 1.0);

@@ -1,5 +1,5 @@
 // GeLU (tanh form) and its derivative, shared by the elementwise bias-activation kernels
-// (bias_act.hip) and the fused GEMM epilogues (linear_gemm.hip).
+// (bias_act.hip).
 #pragma once
 #include "common.h"
 

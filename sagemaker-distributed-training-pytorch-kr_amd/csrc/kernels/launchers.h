@@ -109,13 +109,6 @@ struct SmdtWgradProblem {
 hipError_t smdt_wgrad_grouped(const SmdtWgradProblem* probs, int n, hipStream_t st);
 hipError_t smdt_wgrad_grouped_t(int dtype, const SmdtWgradProblem* probs, int n, hipStream_t st);
 
-// linear_gemm.hip: y[M, N] = x[M, K] . w[N, K]^T (+ bias) (-> GeLU into y, pre-activation into h);
-// epi 0 plain / 1 bias / 2 bias + GeLU. K % 128 == 0, N % 8 == 0, leading dims multiples of 8.
-int smdt_linear_fwd_supported(int64_t M, int64_t N, int64_t K);
-hipError_t smdt_linear_fwd(int dtype, int epi, const void* x, const void* w, const void* bias, void* y, void* h,
-                           int64_t M, int64_t N, int64_t K, int64_t ldx, int64_t ldw, int64_t ldy, int waves,
-                           hipStream_t st);
-
 // xgmi_allreduce.hip: single-node all-reduce over HIP-IPC-mapped peer buffers.
 int smdt_ar_max_ranks();
 int smdt_ar_max_blocks();

@@ -158,21 +158,9 @@ class GPTModel(nn.Module):
             logits = tp.gather_from_tensor_model_parallel_region(logits)
         return logits                                            # [s, b, V / tp]
 
-    def _fused_ce_ok(self, h):
-        import os
-        from ..ops import _ext
-        st = ps.get_state()
-        w = self.output_weight if self.output_weight is not None else self.embedding.weight
-        return (self.cfg.fused_lm_head_ce and os.environ.get("SMDT_FUSED_LM_CE", "1") == "1" and st.tp == 1
-                and not self.sp and h.is_cuda and _ext.use_kernels(h) and h.dtype == torch.bfloat16
-                and w.dtype == h.dtype and w.shape[0] % 8 == 0)
-        # bf16 only: the head forms w_t * (softmax - onehot) and dH in the activation dtype during
-        # forward, before the loss scale exists; in fp16 those ~1e-10 products flush to zero.
-
     def forward(self, tokens, position_ids=None, attention_mask=None, labels=None, loss_mask=None):
-        """``loss_mask`` [b, s] (optional): the per-token weights of the caller's loss reduction
-        (Megatron: sum(loss * mask) / sum(mask)); lets the fused LM head compute its backward in
-        forward. Without it the fused head assumes a plain mean over the tokens."""
+        """Returns per-token losses [b, s] when ``labels`` are given, else the logits. ``loss_mask``
+        is accepted for Megatron's forward_step signature; the caller applies it to the losses."""
         if self.pre_process:
             pos_start = getattr(position_ids, "_smdt_arange_start", None) if position_ids is not None else None
             if position_ids is None:
@@ -187,15 +175,6 @@ class GPTModel(nn.Module):
         if not self.post_process:
             px, pb, res = out
             return SF.bias_dropout_add(px, pb, res, self.cfg.hidden_dropout, self.training)
-        if labels is not None and self._fused_ce_ok(out):
-            w = self.output_weight if self.output_weight is not None else self.embedding.weight
-            lw = None
-            if loss_mask is not None:
-                m = loss_mask.float()
-                lw = (m / m.sum().clamp_min(1e-12)).transpose(0, 1)
-            loss = SF.linear_cross_entropy(out, w, labels.transpose(0, 1), lw, chunk=self.cfg.lm_head_ce_chunk,
-                                           vocab_size=self.loss_vocab_size)
-            return loss.transpose(0, 1).contiguous()                 # [b, s]
         logits = self.lm_logits(out)
         if labels is None:
             return logits.transpose(0, 1).contiguous()

@@ -16,7 +16,6 @@ read once per sub-block. Layer 0 folds the embedding dropout into the same kerne
 from __future__ import annotations
 
 import math
-import os
 from dataclasses import dataclass, field
 from typing import Optional
 
@@ -72,12 +71,6 @@ class TransformerConfig:
     recompute_method: Optional[str] = None       # "uniform" | "block"
     recompute_num_layers: Optional[int] = None
     distribute_saved_activations: bool = False   # full recompute: saved layer inputs split across TP
-    # LM head + CE fused and chunked over tokens, backward computed in forward (GPTModel; TP = 1).
-    # Only for callers that reduce the per-token losses with the weights they declare (the loss
-    # mask, or a plain mean): --fused-lm-head-ce (Megatron recipe) / --fused-ce (bench.py). Saves the
-    # logits' memory; slower at GPT-2 345M (profiles/r2_fused_ce/README.md).
-    fused_lm_head_ce: bool = False
-    lm_head_ce_chunk: int = 2048
 
     def __post_init__(self):
         if self.num_query_groups is None:
@@ -302,57 +295,6 @@ def _apply_rope_parts(flat, cos, sin, rot, nh, nkv, hd, b, s, inverse):
         k.copy_(SF._rope_ref(k, cos.to(flat.device), sin.to(flat.device), rot, pos, inverse))
 
 
-class _Fc1BiasGelu(torch.autograd.Function):
-    """fc1 GEMM + bias + GeLU(tanh) in ONE hand-written MFMA kernel (csrc/kernels/linear_gemm.hip,
-    epilogue 2): the activation is applied to the fp32 accumulator and the pre-activation (which the
-    backward's GeLU derivative needs) is written by the same epilogue, so the separate bias-GeLU
-    pass (K5) and its [tokens, 4h] round trip disappear from the forward.
-    Backward: d(pre) = d(act) * gelu'(pre) with the fp32 bias gradient (bias_act kernel, bias
-    already inside pre) -> dx = d(pre) W1 (hipBLASLt, TN layout via a transposed W1), dW1 = d(pre)^T x into main_grad (deferred
-    grouped MFMA wgrad). TP = 1 without sequence parallelism (the column-parallel collectives of
-    ColumnParallelLinear are not needed there)."""
-
-    @staticmethod
-    def forward(ctx, x, w1, b1):
-        C = _ext_mod().ext()
-        shp = x.shape
-        x2 = x.reshape(-1, shp[-1])
-        if x2.stride(-1) != 1 or x2.stride(0) % 8:
-            x2 = x2.contiguous()
-        act, pre = C.linear_fwd(x2, w1, b1, 2)
-        ctx.save_for_backward(x2, pre)
-        ctx.w1, ctx.b1, ctx.shp = w1, b1, shp
-        return act.view(*shp[:-1], w1.shape[0])
-
-    @staticmethod
-    def backward(ctx, dact):
-        x2, pre = ctx.saved_tensors
-        w1, b1 = ctx.w1, ctx.b1
-        C = _ext_mod().ext()
-        tgt = SF.grad_accumulate_target(b1)
-        dpre, db = C.bias_act_bwd(dact.reshape(pre.shape).contiguous(), pre, None, 0, True, tgt)
-        if tgt is not None:
-            b1._smdt_grad_ready(b1)
-            db1 = None
-        else:
-            db1 = db.to(b1.dtype)
-        dx = tp.dgrad(dpre, w1, tp._dgrad_weight_t(w1))
-        dw1 = tp._wgrad(w1, dpre, x2)
-        return dx.view(ctx.shp), dw1, db1
-
-
-def _ext_mod():
-    from ..ops import _ext
-    return _ext
-
-
-# SMDT_FUSED_FC1=1 runs fc1 + bias + GeLU as the fused MFMA GEMM. Off by default: measured on
-# MI355X at the bench shape (profiles/r2_linear_gemm/) the fused kernel takes 316 us per layer in
-# the training step against 211 us (TunableOp-tuned hipBLASLt fc1) + 89 us (bias-GeLU kernel), its
-# main loop running at ~1.1 PF/s vs hipBLASLt's ~1.3 PF/s; it wins only in isolation (326 vs 337 us).
-_FUSED_FC1 = {"ok": os.environ.get("SMDT_FUSED_FC1", "0") == "1"}
-
-
 class ParallelMLP(nn.Module):
     def __init__(self, cfg: TransformerConfig, layer_number: int, device=None):
         super().__init__()
@@ -373,18 +315,7 @@ class ParallelMLP(nn.Module):
                                         params_dtype=cfg.params_dtype, device=device,
                                         sequence_parallel=cfg.sequence_parallel, skip_bias_add=True)
 
-    def _fused_ok(self, x):
-        fc1 = self.fc1
-        return (_FUSED_FC1["ok"] and self.cfg.activation == "gelu" and self.cfg.bias_gelu_fusion
-                and fc1.bias is not None and fc1.tp == 1 and not fc1.sequence_parallel
-                and x.is_cuda and x.dtype in (torch.bfloat16, torch.float16) and _ext_mod().use_kernels(x)
-                and fc1.weight.dtype == x.dtype and fc1.bias.dtype == x.dtype
-                and _ext_mod().ext().linear_fwd_supported(x.numel() // x.shape[-1], fc1.weight.shape[0],
-                                                          fc1.weight.shape[1]))
-
     def forward(self, x):
-        if self._fused_ok(x):
-            return self.fc2(_Fc1BiasGelu.apply(x, self.fc1.weight, self.fc1.bias))
         h, b = self.fc1(x)
         act = self.cfg.activation
         if act in ("gelu", "gelu_erf"):

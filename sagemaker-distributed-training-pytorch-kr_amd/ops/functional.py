@@ -587,105 +587,6 @@ class _FusedCE(torch.autograd.Function):
         return out, None, None, None, None, None, None
 
 
-# ---------------------------------------------------------------------------------------------
-# Fused LM head + cross entropy, chunked over tokens (the [tokens, V] logits never exist whole)
-
-_FLCE_CHECK = {"dev": None}
-
-
-class _FusedLinearCE(torch.autograd.Function):
-    """loss_t = CE(h_t W^T, y_t) with the whole backward computed in the FORWARD, chunk by chunk,
-    while each chunk's logits are hot (a 2048-token chunk of a 50304-word vocab is 206 MB: it stays
-    in the 256 MB Infinity Cache between its GEMM, the CE kernels and the two gradient GEMMs):
-
-        logits_c = h_c W^T           (bf16 chunk buffer, reused)
-        stats -> loss_c ; dlogits_c = w_t (softmax - onehot)       in place (ce_stats / ce_bwd)
-        dH_c = dlogits_c W            dW_acc += dlogits_c^T h_c   (fp32, MFMA wgrad / hipBLASLt)
-
-    ``w_t`` is the per-token weight the caller's reduction will apply (Megatron's loss_func: loss
-    mask / its sum; a plain mean: 1 / T). The backward receives g_t = s w_t for a scalar s (the
-    micro-batch / loss-scale factor): s = sum_t g_t (sum w = 1), dh = s dH, W's main_grad += s dW_acc
-    — no LM-head GEMM runs in backward and the 3.3 GB logits tensor of the unfused path (GPT-2 345M,
-    32 x 1024 tokens) is never materialised. A device-side check records max |g - s w| relative to
-    |s w|; ``fused_linear_ce_check()`` raises on a non-proportional upstream gradient (a different
-    reduction than the one declared), which the training loops call at their logging points.
-    SURVEY K12/K13 (parallel_output=True path, /root/reference/3_training_megatron-lm/pretrain_gpt.py:51-57).
-    """
-
-    @staticmethod
-    def forward(ctx, h, weight, target, w, chunk, ignore_index, vvalid):
-        C = _ext.ext()
-        from ..parallel import tensor_parallel as tp
-        T, Hd = h.numel() // h.shape[-1], h.shape[-1]
-        V = weight.shape[0]
-        h2 = h.reshape(T, Hd)
-        if not h2.is_contiguous():
-            h2 = h2.contiguous()
-        t = target.reshape(T).contiguous()
-        wt = w.reshape(T).contiguous().float()
-        loss = torch.empty(T, dtype=torch.float32, device=h.device)
-        dH = torch.empty_like(h2)
-        dW = torch.zeros(V, Hd, dtype=torch.float32, device=h.device)
-        buf = torch.empty(min(chunk, T), V, dtype=h.dtype, device=h.device)
-        for c0 in range(0, T, chunk):
-            c1 = min(T, c0 + chunk)
-            hc, lg = h2[c0:c1], buf[: c1 - c0]
-            torch.matmul(hc, weight.t(), out=lg)
-            tc = t[c0:c1]
-            mx, se, tg = C.ce_stats(lg, tc, 0, vvalid)
-            lc = torch.log(se) + mx - tg
-            loss[c0:c1] = torch.where(tc == ignore_index, torch.zeros_like(lc), lc)
-            C.ce_bwd(lg, tc, mx, se, wt[c0:c1], lg, 0, ignore_index, vvalid)
-            torch.matmul(lg, weight, out=dH[c0:c1])
-            tp.accumulate_wgrad(dW, lg, hc)
-        ctx.save_for_backward(dH, dW, wt)
-        ctx.weight, ctx.shape = weight, h.shape
-        return loss.view(target.shape)
-
-    @staticmethod
-    def backward(ctx, g):
-        dH, dW, wt = ctx.saved_tensors
-        weight = ctx.weight
-        g = g.reshape(-1).float()
-        s = g.sum()
-        # proportionality check (no host sync): max |g - s w| / (max |s w| + tiny)
-        dev = (g - s * wt).abs().max() / ((s * wt).abs().max() + 1e-30)
-        _FLCE_CHECK["dev"] = dev if _FLCE_CHECK["dev"] is None else torch.maximum(_FLCE_CHECK["dev"], dev)
-        dh = (dH.float() * s).to(dH.dtype).view(ctx.shape)
-        tgt = grad_accumulate_target(weight)
-        if tgt is not None:
-            tgt.view_as(dW).add_(dW * s)
-            _mark_ready(weight)
-            dw = None
-        else:
-            dw = (dW * s).to(weight.dtype)
-        return dh, dw, None, None, None, None, None
-
-
-def fused_linear_ce_check(tol: float = 1e-3):
-    """Raise if a fused LM-head + CE backward saw an upstream gradient that was not a scalar
-    multiple of the per-token weights declared in forward (synchronises; resets the record)."""
-    dev = _FLCE_CHECK["dev"]
-    _FLCE_CHECK["dev"] = None
-    if dev is not None and float(dev) > tol:
-        raise RuntimeError(f"fused LM-head + cross entropy: the loss was reduced differently from the declared "
-                           f"per-token weights (relative deviation {float(dev):.3g}); pass the loss mask to the "
-                           f"model or disable the fused head (SMDT_FUSED_LM_CE=0)")
-
-
-def linear_cross_entropy(h, weight, target, loss_weights=None, chunk: int = 2048, ignore_index: int = -100,
-                         vocab_size: int = 0):
-    """Per-token CE of the LM head h W^T without materialising the logits (see _FusedLinearCE).
-    ``loss_weights`` [same shape as target]: the weights the caller's reduction applies to the
-    returned per-token losses (default: a mean over all tokens)."""
-    V = weight.shape[0]
-    vvalid = vocab_size if 0 < vocab_size < V else 0
-    if loss_weights is None:
-        loss_weights = torch.full(target.shape, 1.0 / max(target.numel(), 1), dtype=torch.float32,
-                                  device=target.device)
-    return _FusedLinearCE.apply(h, weight, target, loss_weights, int(chunk), int(ignore_index), int(vvalid))
-
-
 def cross_entropy(logits, target, vocab_start: int = 0, group=None, ignore_index: int = -100,
                   inplace_grad: bool = False, vocab_size: int = 0):
     """Per-token CE loss (fp32) for logits [..., V_local] holding vocab slice

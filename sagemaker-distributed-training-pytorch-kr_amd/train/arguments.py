@@ -113,10 +113,6 @@ _GROUPS = {
         ("--tensorboard-dir", dict(type=str, default=None)),
         ("--no-masked-softmax-fusion", dict(action="store_false", dest="masked_softmax_fusion")),
         ("--no-bias-gelu-fusion", dict(action="store_false", dest="bias_gelu_fusion")),
-        # MI355X addition: LM head + CE fused and chunked over tokens (ops.functional._FusedLinearCE):
-        # never materialises the [tokens, vocab] logits (-3.3 GB at GPT-2 345M mbs 32); opt-in, see
-        # profiles/r2_fused_ce/README.md for its speed
-        ("--fused-lm-head-ce", dict(action="store_true")),
         ("--no-bias-dropout-fusion", dict(action="store_false", dest="bias_dropout_fusion")),
         ("--use-flash-attn", dict(action="store_true")),
         ("--no-flash-attn", dict(action="store_true", help="force the unfused softmax path")),
@@ -420,8 +416,7 @@ def core_transformer_config_from_args(args) -> TransformerConfig:
         apply_query_key_layer_scaling=args.apply_query_key_layer_scaling,
         recompute_granularity=args.recompute_granularity, recompute_method=args.recompute_method,
         recompute_num_layers=args.recompute_num_layers,
-        distribute_saved_activations=bool(args.distribute_saved_activations),
-        fused_lm_head_ce=bool(getattr(args, "fused_lm_head_ce", False)))
+        distribute_saved_activations=bool(args.distribute_saved_activations))
 
 
 # ------------------------------------------------------------------------ micro-batch calculator (U2)

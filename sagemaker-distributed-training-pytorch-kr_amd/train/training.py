@@ -38,7 +38,6 @@ from ..data.tokenizer import build_tokenizer, vocab_size_with_padding
 from ..models.gpt import allreduce_word_embedding_grads, gpt_flops_per_token
 from ..optim.lr_scheduler import OptimizerParamScheduler
 from ..optim.optimizer import ConstantLossScaler, DynamicLossScaler, MixedPrecisionAdam
-from ..ops import functional as SF
 from ..parallel import state as ps
 from ..parallel.distributed import DistributedDataParallel
 from ..parallel.random import model_parallel_seed
@@ -260,7 +259,6 @@ def training_log(loss_dict, total_loss_dict, lr, iteration, loss_scale, report_m
                  args, elapsed_per_iter, model_cfg=None):
     timers = A.get_timers()
     if iteration % args.log_interval == 0:
-        SF.fused_linear_ce_check()  # the fused LM head's declared reduction matched the real one
         _relay.check_all()          # no TP-pair exchange timed out (outputs would be NaN)
     if getattr(args, "tensorboard_dir", None) and iteration % args.tensorboard_log_interval == 0:
         _tensorboard_log(get_tensorboard_writer(), loss_dict, lr, iteration, loss_scale, grad_norm, args, timers)

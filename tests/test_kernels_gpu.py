@@ -415,43 +415,6 @@ def test_wgrad_mfma_fp16_and_bf16(dt):
 
 
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
-@pytest.mark.parametrize("shape", [(4096, 4096, 1024), (1000, 520, 256), (2048, 50304 // 8, 128), (256, 8, 128), (300, 264, 512)])
-@pytest.mark.parametrize("epi", [0, 1, 2])
-@pytest.mark.parametrize("waves", [8, 4])
-def test_linear_fwd_mfma_matches_fp32_reference(shape, epi, dt, waves):
-    """Hand-written NT GEMM (linear_gemm.hip) incl. partial tiles and the fused bias / bias + GeLU
-    epilogues vs an fp32 torch reference (the pre-activation h is returned too)."""
-    C = _ext.ext()
-    torch.manual_seed(11)
-    M, N, K = shape
-    x = torch.randn(M, K, device=DEV, dtype=dt)
-    w = torch.randn(N, K, device=DEV, dtype=dt) * K ** -0.5
-    b = torch.randn(N, device=DEV, dtype=dt)
-    out = C.linear_fwd(x, w, b if epi else None, epi, waves)
-    ref = x.float() @ w.float().t()
-    if epi:
-        ref = ref + b.float()
-    tol = dict(atol=2e-2, rtol=2e-2)
-    if epi == 2:
-        y, h = out
-        torch.testing.assert_close(h.float(), ref, **tol)
-        torch.testing.assert_close(y.float(), F.gelu(ref, approximate="tanh"), **tol)
-    else:
-        torch.testing.assert_close(out[0].float(), ref, **tol)
-
-
-def test_linear_fwd_strided_input_and_rejects_bad_shapes():
-    C = _ext.ext()
-    x = torch.randn(512, 2048, device=DEV, dtype=torch.bfloat16)[:, :1024]   # row stride 2048
-    w = torch.randn(768, 1024, device=DEV, dtype=torch.bfloat16) * 0.03
-    (y,) = C.linear_fwd(x, w, None, 0)
-    torch.testing.assert_close(y.float(), x.float() @ w.float().t(), atol=2e-2, rtol=2e-2)
-    with pytest.raises(RuntimeError):
-        C.linear_fwd(torch.randn(64, 100, device=DEV, dtype=torch.bfloat16),
-                     torch.randn(64, 100, device=DEV, dtype=torch.bfloat16), None, 0)   # K % 64 != 0
-
-
-@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("shape", [(1024, 1024), (3072, 1024), (1024, 4096), (50304, 1024), (200, 136), (8, 8)])
 def test_transpose2d(dt, shape):
     x = torch.randn(*shape, device="cuda").to(dt)

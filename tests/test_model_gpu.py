@@ -70,56 +70,3 @@ def test_pretrain_gpt_nb3_fp16_flags_on_kernels(tmp_path):
     assert math.isfinite(loss), last[:400]
 
 
-@pytest.mark.parametrize("masked", [False, True])
-def test_fused_lm_head_ce_matches_unfused(masked):
-    """The chunked LM head + CE whose backward runs in forward (ops.functional._FusedLinearCE):
-    per-token losses, the gradients reaching the decoder and the tied embedding's fp32 main_grad
-    equal the unfused path (logits materialised, vocab CE kernels), for a plain mean and for
-    Megatron's masked mean; chunks smaller than the token count exercise the chunk loop."""
-    from smdt_amd.models.gpt import GPTModel
-    from smdt_amd.models.transformer import TransformerConfig
-    from smdt_amd.ops import functional as SF
-    from smdt_amd.parallel import state as ps
-    from smdt_amd.parallel.distributed import DistributedDataParallel
-    ps.destroy_model_parallel()
-    res = []
-    for fused in (True, False):
-        torch.manual_seed(5)
-        cfg = TransformerConfig(num_layers=2, hidden_size=256, num_attention_heads=4, max_position_embeddings=256,
-                                padded_vocab_size=1024, hidden_dropout=0.0, attention_dropout=0.0, seed=3,
-                                params_dtype=torch.bfloat16, fused_lm_head_ce=fused, lm_head_ce_chunk=384)
-        m = GPTModel(cfg, device="cuda")
-        ddp = DistributedDataParallel(m)
-        g = torch.Generator().manual_seed(4)
-        toks = torch.randint(0, 1000, (4, 257), generator=g).cuda()
-        mask = (torch.rand(4, 256, generator=g) > 0.3).float().cuda() if masked else torch.ones(4, 256).cuda()
-        ddp.zero_grad_buffer()
-        loss = m(toks[:, :-1], labels=toks[:, 1:], loss_mask=mask if masked else None)
-        (torch.sum(loss.float() * mask) / mask.sum() * 0.25).backward()     # 0.25: a micro-batch factor
-        ddp.finish_grad_sync()
-        res.append((loss.float().cpu(), {n: p.main_grad.float().cpu().clone() for n, p in m.named_parameters()}))
-    SF.fused_linear_ce_check()
-    (l1, g1), (l2, g2) = res
-    torch.testing.assert_close(l1, l2, atol=2e-2, rtol=1e-2)
-    for n in g2:
-        err = (g1[n] - g2[n]).norm() / g2[n].norm().clamp_min(1e-12)
-        assert err < 2e-2, (n, err.item())
-
-
-def test_fused_lm_head_ce_detects_undeclared_reduction():
-    """A reduction other than the declared weights (here a sum where a mean was declared with a
-    mask) is caught by fused_linear_ce_check instead of training on a wrong gradient."""
-    from smdt_amd.models.gpt import GPTModel
-    from smdt_amd.models.transformer import TransformerConfig
-    from smdt_amd.ops import functional as SF
-    from smdt_amd.parallel import state as ps
-    ps.destroy_model_parallel()
-    cfg = TransformerConfig(num_layers=1, hidden_size=256, num_attention_heads=4, max_position_embeddings=256,
-                            padded_vocab_size=1024, hidden_dropout=0.0, attention_dropout=0.0,
-                            params_dtype=torch.bfloat16, fused_lm_head_ce=True)
-    m = GPTModel(cfg, device="cuda")
-    toks = torch.randint(0, 1000, (2, 257), device="cuda")
-    loss = m(toks[:, :-1], labels=toks[:, 1:])          # declared: a plain mean
-    (loss.float() * torch.rand_like(loss.float())).sum().backward()
-    with pytest.raises(RuntimeError, match="reduced differently"):
-        SF.fused_linear_ce_check()
