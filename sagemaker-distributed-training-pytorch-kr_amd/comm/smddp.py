@@ -1,35 +1,148 @@
-"""``smddp`` process-group backend name for unmodified SageMaker data-parallel scripts.
+"""``smddp`` process-group backend for unmodified SageMaker data-parallel scripts.
 
 The reference's DDP recipes do ``import smdistributed.dataparallel.torch.torch_smddp`` and then
-``dist.init_process_group(backend="smddp")`` (pytorch_mnist_ddp.py:89-90,
-pytorch_oxford_ddp.py:206-211). Importing this module registers the same backend name with
-``torch.distributed``; its process groups are RCCL (ProcessGroupNCCL — on ROCm that IS RCCL over
-xGMI) for GPU tensors and Gloo for CPU tensors, so the rest of the script (all-reduce, DDP,
-barriers) runs unchanged on MI355X. SMDDP's parameter-server all-reduce exists to use EFA across
-p3/p4 nodes; inside one xGMI-connected node a ring all-reduce over the 7 links is the right
-algorithm, so nothing else is emulated.
+``dist.init_process_group(backend="smddp")`` (/root/reference/1_training_mnist_ddp/
+pytorch_mnist_ddp.py:89-90, /root/reference/2_training_oxford-pet_ddp/pytorch_oxford_ddp.py:206-211)
+and wrap the model in ``torch.nn.parallel.DistributedDataParallel``, whose bucket all-reduces then
+run on SMDDP's own all-reduce (NB2:387-404 logs its "balanced fusion buffers").
+
+Importing this module registers the same backend name. Its process group is a real backend, not
+an alias: ``SMDDPProcessGroup`` owns an RCCL group (ProcessGroupNCCL; on ROCm that IS RCCL over
+xGMI) — or Gloo for CPU tensors — and routes
+
+* GPU ``allreduce`` (SUM / AVG, one dense contiguous fp32 / bf16 / fp16 tensor, 16-byte multiple,
+  2 / 4 / 8 ranks on one node) through the single-launch xGMI all-reduce engine
+  (``comm/xgmi.py``: every peer read over its own link, one-shot below and two-shot above
+  ``ONE_SHOT_MAX_BYTES``, fp32 accumulation in rank order so every rank gets identical bits).
+  The engine is built collectively on the first eligible call, validated against RCCL and timed
+  per op, and kept only for the ops it wins on this node; it runs on the caller's current stream
+  and the returned Work is already complete (stream-ordered), which is exactly how torch DDP
+  consumes it. An engine error (a peer that never arrived) turns the path off for the rest of the
+  run (comm/health.py) and RCCL takes over;
+* every other collective straight to RCCL / Gloo.
+
+SMDDP's parameter-server all-reduce exists to use EFA across p3 / p4 nodes; inside one
+xGMI-connected node the peer-read all-reduce (small messages) and RCCL's rings (large ones) are the
+right algorithms, chosen per message size at run time. ``smddp_stats()`` reports how many calls
+and bytes took each path (the per-collective metrics of SURVEY §5.5).
 """
 from __future__ import annotations
 
 import datetime
+import threading
 
 import torch
 import torch.distributed as dist
 
 BACKEND = "smddp"
 _REGISTERED = False
+_STATS = {"xgmi_calls": 0, "xgmi_bytes": 0, "rccl_calls": 0, "rccl_bytes": 0}
+
+
+def smddp_stats() -> dict:
+    """Calls / bytes of this process's smddp all-reduces per path (xgmi engine vs RCCL / Gloo)."""
+    return dict(_STATS)
+
+
+def _done_work(result):
+    """A Work whose future already holds ``result`` (the engine ran on the current stream)."""
+    from torch._C._distributed_c10d import _create_work_from_future
+    fut = torch.futures.Future()
+    fut.set_result(result)
+    return _create_work_from_future(fut)
+
+
+class SMDDPProcessGroup(dist.ProcessGroup):
+    """The ``smddp`` backend object (see the module docstring)."""
+
+    def __init__(self, store, rank: int, size: int, timeout):
+        super().__init__(rank, size)
+        timeout = timeout if isinstance(timeout, datetime.timedelta) else datetime.timedelta(seconds=float(timeout))
+        if torch.cuda.is_available():
+            opts = dist.ProcessGroupNCCL.Options()
+            opts._timeout = timeout
+            self._inner = dist.ProcessGroupNCCL(store, rank, size, opts)
+        else:
+            opts = dist.ProcessGroupGloo._Options()
+            opts._timeout = timeout
+            opts._devices = [dist.ProcessGroupGloo.create_default_device()]
+            self._inner = dist.ProcessGroupGloo(store, rank, size, opts)
+        self._engine = None
+        self._state = "unset"       # unset -> building -> ready | off
+        self._lock = threading.Lock()
+
+    def getBackendName(self) -> str:
+        return BACKEND
+
+    # ---- xGMI all-reduce path ----------------------------------------------------------------
+    def _world_group(self):
+        """The dist-level handle of this backend when it is the default (world) group — the only
+        group SMDDP scripts use; subgroups stay on RCCL."""
+        try:
+            if dist.get_world_size() == self.size() and dist.get_rank() == self.rank():
+                return dist.group.WORLD
+        except (RuntimeError, ValueError):
+            pass
+        return None
+
+    def _xgmi(self, t: torch.Tensor):
+        if self._state == "off" or self._state == "building":
+            return None
+        if self._state == "unset":
+            from . import xgmi
+            if not (t.is_cuda and self.size() in (2, 4, 8)) or xgmi.explicitly_off():
+                self._state = "off"
+                return None
+            group = self._world_group()
+            if group is None:
+                self._state = "off"
+                return None
+            with self._lock:
+                self._state = "building"   # the engine's own set-up collectives go to RCCL
+                try:
+                    self._engine = xgmi.create_for_group(group, auto=True, tune=True, log=print)
+                finally:
+                    self._state = "ready" if self._engine is not None else "off"
+        eng = self._engine
+        if eng is None or not eng.active:
+            return None
+        return eng
+
+    def allreduce(self, tensors, opts=None):
+        opts = opts if opts is not None else dist.AllreduceOptions()
+        if len(tensors) == 1 and tensors[0].is_cuda:
+            t = tensors[0]
+            op = opts.reduceOp
+            kind = "sum" if op == dist.ReduceOp.SUM else ("avg" if op == dist.ReduceOp.AVG else None)
+            if kind is not None:
+                from . import xgmi
+                eng = self._xgmi(t) if xgmi.eligible(t, self.size()) else None
+                if eng is not None and eng.all_reduce(t, kind):
+                    _STATS["xgmi_calls"] += 1
+                    _STATS["xgmi_bytes"] += t.numel() * t.element_size()
+                    return _done_work(tensors)
+        _STATS["rccl_calls"] += 1
+        _STATS["rccl_bytes"] += sum(x.numel() * x.element_size() for x in tensors)
+        return self._inner.allreduce(tensors, opts)
+
+
+def _delegate(name):
+    def f(self, *args, **kwargs):
+        return getattr(self._inner, name)(*args, **kwargs)
+    f.__name__ = name
+    f.__doc__ = f"``{name}`` on the RCCL / Gloo group."
+    return f
+
+
+for _name in ("allreduce_coalesced", "allgather", "_allgather_base", "allgather_coalesced",
+              "allgather_into_tensor_coalesced", "alltoall", "alltoall_base", "barrier", "broadcast", "gather",
+              "recv", "recv_anysource", "reduce", "reduce_scatter", "_reduce_scatter_base",
+              "reduce_scatter_tensor_coalesced", "scatter", "send", "monitored_barrier"):
+    setattr(SMDDPProcessGroup, _name, _delegate(_name))
 
 
 def _create(store, rank, size, timeout):
-    timeout = timeout if isinstance(timeout, datetime.timedelta) else datetime.timedelta(seconds=float(timeout))
-    if torch.cuda.is_available():
-        opts = dist.ProcessGroupNCCL.Options()
-        opts._timeout = timeout
-        return dist.ProcessGroupNCCL(store, rank, size, opts)
-    opts = dist.ProcessGroupGloo._Options()
-    opts._timeout = timeout
-    opts._devices = [dist.ProcessGroupGloo.create_default_device()]
-    return dist.ProcessGroupGloo(store, rank, size, opts)
+    return SMDDPProcessGroup(store, rank, size, timeout)
 
 
 def register():

@@ -453,12 +453,13 @@ class XgmiAllReduce(IpcEngine):
         self.active = False
 
 
-def create_for_group(group, auto: bool = False, log=print, **kw) -> Optional[XgmiAllReduce]:
+def create_for_group(group, auto: bool = False, log=print, tune: bool = False, **kw) -> Optional[XgmiAllReduce]:
     """Collective over ``group``: an engine when xGMI collectives are wanted and possible, else
     None (with a warning when wanted but not set up). ``auto`` (the DDP gradient / parameter
     collectives): when neither ``SMDT_XGMI_ALLREDUCE`` nor the smddp backend decided, build the
     engine anyway, validate it, time each op against RCCL on this node and keep the ops it wins
-    (rank 0 logs the bus bandwidths); None when it wins none."""
+    (rank 0 logs the bus bandwidths); None when it wins none. ``tune``: time and select per op even
+    when the engine was asked for explicitly (the smddp process group)."""
     if not (dist.is_initialized() and torch.cuda.is_available()):
         return None
     explicit = wanted(group)
@@ -474,7 +475,7 @@ def create_for_group(group, auto: bool = False, log=print, **kw) -> Optional[Xgm
     except (RuntimeError, ValueError) as e:
         warnings.warn(f"xGMI all-reduce disabled for this group: {e}")
         return None
-    if explicit:
+    if explicit and not tune:
         return eng
     try:
         res = eng.tune()

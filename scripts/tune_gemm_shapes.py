@@ -8,7 +8,8 @@ head, for
 
     N = 1     tp1, micro-batch 64  (backward dgrad shapes)
     N = 2     tp2, micro-batch 64  (chunk rows = s / 2 * 64)
-    N = 4, 8  tp2, micro-batch 16  (chunk rows = s / 2 * 16)
+    N = 8     tp2, micro-batch 32  (chunk rows = s / 2 * 32; bench.py's N = 8 split since round 3)
+    (micro-batch 16: the round-2 N = 4 / 8 splits)
 
 GPT-2 345M: h = 1024, ffn 4096, 16 heads, vocab 50304 (padded for tp2: 25152 per rank).
 Results go to ``--out`` (merge into profiles/tunableop/ with ``--merge``).
@@ -32,21 +33,21 @@ H, FFN, S = 1024, 4096, 1024
 VOCAB_TP2 = 50304 // 2
 
 
-def shapes():
+def shapes(mbs_list=(64, 32, 16), n1=True):
     # Dgrad GEMMs run in the TN layout: dX = F.linear(dY, W^T) / torch.mm(dY, W^T.t(), out=)
     # with a contiguous W^T (parallel/tensor_parallel.py ``dgrad`` / ``dgrad_into``), so the
     # backward shapes below are "linear" / "mm" calls with N = in-features, K = out-features.
     # N = 1 (tp1, micro-batch 64): the backward dgrad GEMMs (the forward ones are tuned by
     # ``bench.py --tunableop 2``, whose first warmup step reaches them first)
     mt = S * 64
-    out = [("linear", mt, H, 50304), ("linear", mt, H, FFN), ("linear", mt, FFN, H), ("linear", mt, H, H),
+    out = [] if not n1 else [("linear", mt, H, 50304), ("linear", mt, H, FFN), ("linear", mt, FFN, H), ("linear", mt, H, H),
            ("linear", mt, H, 3 * H)]
-    if os.environ.get("SMDT_TUNE_N1_FORWARD", "0") == "1":
+    if n1 and os.environ.get("SMDT_TUNE_N1_FORWARD", "0") == "1":
         # N = 1 forward: qkv with bias (addmm), proj / fc1 / fc2 without (the bias goes to the
         # fused LN / bias-GeLU kernels), LM head
         out += [("addmm", mt, 3 * H, H), ("mm", mt, H, H), ("mm", mt, FFN, H), ("mm", mt, H, FFN),
                 ("mm", mt, 50304, H)]
-    for mbs in (64, 16):
+    for mbs in mbs_list:
         m = S // 2 * mbs  # one ring chunk of a sequence-parallel [s / tp, b, h] activation
         # forward column-parallel (qkv with bias, fc1 without: bias-GeLU is a separate kernel)
         out += [("addmm", m, 3 * H // 2, H), ("mm", m, FFN // 2, H)]
@@ -107,6 +108,8 @@ def main():
     p.add_argument("--tune-ms", type=int, default=60)
     p.add_argument("--iters", type=int, default=5, help="timed iterations per candidate solution")
     p.add_argument("--skip-lm-head", type=int, default=1, help="skip the vocab GEMMs (~5 min of search each)")
+    p.add_argument("--mbs", type=str, default="64,32,16", help="tp2 micro-batch sizes to tune")
+    p.add_argument("--skip-n1", action="store_true", help="skip the N = 1 dgrad shapes")
     p.add_argument("--merge", action="store_true", help="merge --out into the committed table afterwards")
     p.add_argument("--merge-only", action="store_true", help="only merge an existing --out (no GPU)")
     a = p.parse_args()
@@ -133,7 +136,7 @@ def main():
             time.sleep(30)
             print(f"... tuning ({time.time() - t_start:.0f} s)", flush=True)
     threading.Thread(target=beat, daemon=True).start()
-    for kind, m, n, k in shapes():
+    for kind, m, n, k in shapes(tuple(int(x) for x in a.mbs.split(",")), not a.skip_n1):
         if a.skip_lm_head and max(n, k) > 8192:
             continue
         t0 = time.time()

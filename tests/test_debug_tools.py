@@ -85,20 +85,54 @@ def test_step_watchdog_dumps_stacks_and_aborts():
 
 def _smddp_worker(rank, world):
     import torch.distributed as dist
-    import smdt_amd.comm.smddp  # noqa: F401  (registers backend "smddp")
+    import smdt_amd.comm.smddp as S  # registers backend "smddp"
     dist.init_process_group(backend="smddp")
     t = torch.full((4,), float(rank + 1))
     dist.all_reduce(t)
     be = dist.get_backend()
+    # the collectives a data-parallel script and the framework issue, all through the smddp group
+    b = torch.full((3,), float(rank))
+    dist.broadcast(b, src=1)
+    gl = [torch.zeros(2) for _ in range(world)]
+    dist.all_gather(gl, torch.full((2,), float(rank)))
+    gt = torch.zeros(2 * world)
+    dist.all_gather_into_tensor(gt, torch.full((2,), float(rank)))
+    rs = torch.zeros(2)
+    dist.reduce_scatter_tensor(rs, torch.arange(2.0 * world) + rank)
+    objs = [None] * world
+    dist.all_gather_object(objs, {"r": rank})
+    dist.barrier()
+    # unmodified torch DDP on the smddp group (the reference recipes' wrapping)
+    torch.manual_seed(0)
+    m = torch.nn.Linear(8, 4)
+    ddp = torch.nn.parallel.DistributedDataParallel(m)
+    x = torch.randn(6, 8, generator=torch.Generator().manual_seed(rank))
+    ddp(x).square().sum().backward()
+    g = m.weight.grad.clone()
+    ref = [torch.zeros_like(g) for _ in range(world)]
+    m2 = torch.nn.Linear(8, 4)
+    m2.load_state_dict(m.state_dict())
+    m2.zero_grad()
+    m2(x).square().sum().backward()
+    dist.all_gather(ref, m2.weight.grad)
+    ok = torch.allclose(g, sum(ref) / world, atol=1e-5)
+    stats = S.smddp_stats()
     dist.destroy_process_group()
-    return t.tolist(), be
+    return t.tolist(), be, b.tolist(), [v.tolist() for v in gl], gt.tolist(), rs.tolist(), objs, ok, stats
 
 
 @pytest.mark.slow
 def test_smddp_backend_name_works_unmodified():
+    """backend="smddp" (comm/smddp.SMDDPProcessGroup, a real c10d backend over RCCL / Gloo with the
+    xGMI all-reduce path for GPU tensors): the collectives and torch DDP of the reference's DDP
+    recipes run unchanged (CPU / Gloo here: every all-reduce takes the RCCL / Gloo path)."""
     outs = run_workers(_smddp_worker, 2)
-    for vals, be in outs:
+    for r, (vals, be, b, gl, gt, rs, objs, ok, stats) in enumerate(outs):
         assert vals == [3.0] * 4 and be == "smddp"
+        assert b == [1.0] * 3 and gl == [[0.0, 0.0], [1.0, 1.0]] and gt == [0.0, 0.0, 1.0, 1.0]
+        assert rs == [4.0 * r + 1, 4.0 * r + 3]          # sum over ranks of (arange(4) + rank)[2r:2r+2]
+        assert objs == [{"r": 0}, {"r": 1}] and ok
+        assert stats["rccl_calls"] >= 2 and stats["xgmi_calls"] == 0
 
 
 def test_host_runtime_under_asan_ubsan(tmp_path):
