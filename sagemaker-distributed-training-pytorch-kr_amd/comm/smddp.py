@@ -17,8 +17,9 @@ xGMI) — or Gloo for CPU tensors — and routes
   The engine is built collectively on the first eligible call, validated against RCCL and timed
   per op, and kept only for the ops it wins on this node; it runs on the caller's current stream
   and the returned Work is already complete (stream-ordered), which is exactly how torch DDP
-  consumes it. An engine error (a peer that never arrived) turns the path off for the rest of the
-  run (comm/health.py) and RCCL takes over;
+  consumes it. Every ``CHECK_EVERY`` engine calls the ranks agree (MAX over RCCL) on the
+  engine's sticky error word; a peer that never arrived turns the path off on every rank for the
+  rest of the run, with a warning, and RCCL takes over;
 * every other collective straight to RCCL / Gloo.
 
 SMDDP's parameter-server all-reduce exists to use EFA across p3 / p4 nodes; inside one
@@ -29,6 +30,7 @@ and bytes took each path (the per-collective metrics of SURVEY §5.5).
 from __future__ import annotations
 
 import datetime
+import os
 import threading
 
 import torch
@@ -37,6 +39,7 @@ import torch.distributed as dist
 BACKEND = "smddp"
 _REGISTERED = False
 _STATS = {"xgmi_calls": 0, "xgmi_bytes": 0, "rccl_calls": 0, "rccl_bytes": 0}
+CHECK_EVERY = 64   # engine all-reduces between two agreed error-word checks (one host sync each)
 
 
 def smddp_stats() -> dict:
@@ -58,7 +61,11 @@ class SMDDPProcessGroup(dist.ProcessGroup):
     def __init__(self, store, rank: int, size: int, timeout):
         super().__init__(rank, size)
         timeout = timeout if isinstance(timeout, datetime.timedelta) else datetime.timedelta(seconds=float(timeout))
-        if torch.cuda.is_available():
+        # SMDT_SMDDP_INNER=gloo: Gloo underneath even with a GPU (multi-process tests that share
+        # one GPU, where RCCL refuses two ranks on one device; the xGMI engine then runs over
+        # same-device IPC mappings without its RCCL validation / timing)
+        self._host_inner = not torch.cuda.is_available() or os.environ.get("SMDT_SMDDP_INNER") == "gloo"
+        if not self._host_inner:
             opts = dist.ProcessGroupNCCL.Options()
             opts._timeout = timeout
             self._inner = dist.ProcessGroupNCCL(store, rank, size, opts)
@@ -100,13 +107,29 @@ class SMDDPProcessGroup(dist.ProcessGroup):
             with self._lock:
                 self._state = "building"   # the engine's own set-up collectives go to RCCL
                 try:
-                    self._engine = xgmi.create_for_group(group, auto=True, tune=True, log=print)
+                    if self._host_inner:
+                        self._engine = xgmi.XgmiAllReduce(group, region_bytes=8 << 20, blocks=32, validate=False)
+                    else:
+                        self._engine = xgmi.create_for_group(group, auto=True, tune=True, log=print)
                 finally:
                     self._state = "ready" if self._engine is not None else "off"
         eng = self._engine
         if eng is None or not eng.active:
             return None
         return eng
+
+    def _check(self, eng, dev):
+        """Agree on the engine's sticky error word (every rank reaches this at the same call)."""
+        flag = torch.tensor([float(eng.error())], device=dev)
+        mx = dist.AllreduceOptions()
+        mx.reduceOp = dist.ReduceOp.MAX
+        self._inner.allreduce([flag], mx).wait()
+        if flag.item() > 0:
+            import warnings
+            warnings.warn("smddp: an xGMI all-reduce timed out waiting for a peer (its output was NaN-filled); "
+                          "all later all-reduces of this group run on RCCL")
+            eng.deactivate("peer timeout")
+            self._state = "off"
 
     def allreduce(self, tensors, opts=None):
         opts = opts if opts is not None else dist.AllreduceOptions()
@@ -120,6 +143,8 @@ class SMDDPProcessGroup(dist.ProcessGroup):
                 if eng is not None and eng.all_reduce(t, kind):
                     _STATS["xgmi_calls"] += 1
                     _STATS["xgmi_bytes"] += t.numel() * t.element_size()
+                    if _STATS["xgmi_calls"] % CHECK_EVERY == 0:
+                        self._check(eng, t.device)
                     return _done_work(tensors)
         _STATS["rccl_calls"] += 1
         _STATS["rccl_bytes"] += sum(x.numel() * x.element_size() for x in tensors)

@@ -873,3 +873,49 @@ def xgmi_timeout_worker(rank, world, port, outdir):
         res["err"] = traceback.format_exc()
     with open(os.path.join(outdir, f"r{rank}.pkl"), "wb") as f:
         pickle.dump(res, f)
+
+
+def smddp_torch_ddp_worker(rank, world, port, outdir):
+    """One rank of the smddp-backend GPU test: unmodified torch DDP on the ``smddp`` group, every
+    rank on cuda:0 (Gloo underneath, SMDT_SMDDP_INNER=gloo), bucket all-reduces through the xGMI
+    engine of comm/smddp.SMDDPProcessGroup; gradients vs the mean of per-rank local gradients."""
+    import os
+    import pickle
+    import traceback
+
+    import torch
+    os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "RANK": str(rank),
+                       "WORLD_SIZE": str(world), "SMDT_SMDDP_INNER": "gloo"})
+    res = {"err": None}
+    try:
+        import torch.distributed as dist
+        import smdt_amd.comm.smddp as S
+        torch.cuda.set_device(0)
+        dist.init_process_group("smddp", rank=rank, world_size=world)
+        torch.manual_seed(0)
+        m = torch.nn.Sequential(torch.nn.Linear(64, 256), torch.nn.GELU(), torch.nn.Linear(256, 32)).cuda()
+        ref_m = torch.nn.Sequential(torch.nn.Linear(64, 256), torch.nn.GELU(), torch.nn.Linear(256, 32)).cuda()
+        ref_m.load_state_dict(m.state_dict())
+        ddp = torch.nn.parallel.DistributedDataParallel(m)
+        ok = []
+        for step in range(3):
+            x = torch.randn(16, 64, generator=torch.Generator().manual_seed(10 * step + rank)).cuda()
+            m.zero_grad()
+            ddp(x).square().mean().backward()
+            ref_m.zero_grad()
+            ref_m(x).square().mean().backward()
+            for p, q in zip(m.parameters(), ref_m.parameters()):
+                mean = q.grad.cpu()
+                dist.all_reduce(mean)            # a CPU tensor: the Gloo path of the smddp group
+                ok.append(bool(torch.allclose(p.grad.cpu(), mean / world, atol=1e-5, rtol=1e-4)))
+        torch.cuda.synchronize()
+        grp = dist.distributed_c10d._get_default_group()
+        pg = grp._get_backend(torch.device("cuda"))
+        res.update(ok=ok, stats=S.smddp_stats(), backend=dist.get_backend(),
+                   error_word=pg._engine.error() if getattr(pg, "_engine", None) is not None else None)
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception:  # noqa: BLE001
+        res["err"] = traceback.format_exc()
+    with open(os.path.join(outdir, f"r{rank}.pkl"), "wb") as f:
+        pickle.dump(res, f)

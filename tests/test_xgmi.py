@@ -165,6 +165,44 @@ def test_cross_process_ipc_allreduce_world2():
 
 
 @pytest.mark.gpu
+def test_smddp_backend_torch_ddp_takes_xgmi_path():
+    """backend="smddp" + unmodified torch DDP, 2 processes on one GPU: the bucket all-reduces run
+    on the xGMI engine of comm/smddp.SMDDPProcessGroup and the gradients equal the mean of the
+    ranks' local gradients."""
+    import os
+    import pickle
+    import tempfile
+
+    import torch.multiprocessing as mp
+
+    import dist_workers as W
+    from _dist import free_port
+
+    world = 2
+    port = free_port()
+    with tempfile.TemporaryDirectory() as d:
+        ctx = mp.get_context("spawn")
+        procs = [ctx.Process(target=W.smddp_torch_ddp_worker, args=(r, world, port, d)) for r in range(world)]
+        for p in procs:
+            p.start()
+        for p in procs:
+            p.join(90)
+        for p in procs:
+            if p.is_alive():
+                p.kill()
+        out = []
+        for r in range(world):
+            path = os.path.join(d, f"r{r}.pkl")
+            assert os.path.exists(path), f"rank {r} wrote no result (exit {procs[r].exitcode})"
+            with open(path, "rb") as f:  # written by this test's own workers
+                out.append(pickle.load(f))
+    for r, res in enumerate(out):
+        assert res["err"] is None, f"rank {r}:\n{res['err']}"
+        assert res["backend"] == "smddp" and all(res["ok"]) and len(res["ok"]) == 12, (r, res)
+        assert res["stats"]["xgmi_calls"] >= 3 and res["error_word"] == 0, (r, res)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("world", [2, 4, 8])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_loopback_reduce_scatter_and_all_gather(world, dtype):
