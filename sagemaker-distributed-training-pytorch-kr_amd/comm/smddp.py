@@ -166,6 +166,22 @@ for _name in ("allreduce_coalesced", "allgather", "_allgather_base", "allgather_
     setattr(SMDDPProcessGroup, _name, _delegate(_name))
 
 
+def DistributedDataParallel(module, *args, bucket_cap_mb=None, process_group=None, **kwargs):
+    """``smdistributed.dataparallel.torch.parallel.DistributedDataParallel``: torch DDP whose
+    gradient buckets ("fusion buffers") are sized for this node's links — comm/buckets.py's 8-32 MB
+    from a start-up latency / bandwidth timing of the group's reduce-scatter, at least 4 buckets
+    per rank so the first all-reduce starts early in backward — instead of torch's fixed 25 MB.
+    An explicit ``bucket_cap_mb`` wins. Collective over the group (the timing)."""
+    from . import buckets
+    if bucket_cap_mb is None:
+        ps = [p for p in module.parameters() if p.requires_grad]
+        total = sum(p.numel() for p in ps)
+        esz = ps[0].element_size() if ps else 4
+        bucket_cap_mb = buckets.auto_bucket_elems(process_group or dist.group.WORLD, total, esz) * esz / 2 ** 20
+    return torch.nn.parallel.DistributedDataParallel(module, *args, bucket_cap_mb=bucket_cap_mb,
+                                                     process_group=process_group, **kwargs)
+
+
 def _create(store, rank, size, timeout):
     return SMDDPProcessGroup(store, rank, size, timeout)
 

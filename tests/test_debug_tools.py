@@ -105,7 +105,7 @@ def _smddp_worker(rank, world):
     # unmodified torch DDP on the smddp group (the reference recipes' wrapping)
     torch.manual_seed(0)
     m = torch.nn.Linear(8, 4)
-    ddp = torch.nn.parallel.DistributedDataParallel(m)
+    ddp = S.DistributedDataParallel(m)      # torch DDP, buckets sized by comm/buckets.py
     x = torch.randn(6, 8, generator=torch.Generator().manual_seed(rank))
     ddp(x).square().sum().backward()
     g = m.weight.grad.clone()
