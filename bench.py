@@ -217,7 +217,9 @@ def main():
     from smdt_amd.comm import buckets as comm_buckets
     from smdt_amd.comm import stats as comm_stats
     comm_stats.enable(bool(a.comm_stats))   # before the process group: RCCL per-work timing
-    rank, local, world, backend = init_distributed("nccl")
+    # SMDT_BENCH_BACKEND=gloo: rehearsal of the N > 1 code paths with every rank on ONE GPU (RCCL
+    # refuses two ranks on one device); the driver's runs use RCCL
+    rank, local, world, backend = init_distributed(os.environ.get("SMDT_BENCH_BACKEND", "nccl"))
     if world != a.gpus and rank == 0:
         print(f"[bench] note: --gpus {a.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
     n = world
