@@ -7,6 +7,8 @@ and both algorithms are exercised exactly as across GPUs (only the links differ)
 a plain fp32 sum in rank order 0..W-1, which is also the kernel's accumulation order, so fp32
 results must match bit for bit.
 """
+import os
+
 import pytest
 import torch
 
@@ -162,6 +164,38 @@ def test_cross_process_ipc_allreduce_world2():
     for r, res in enumerate(out):
         assert res["err"] is None, f"rank {r}:\n{res['err']}"
         assert res["error_word"] == 0 and all(res["ok"]) and len(res["ok"]) == 18, (r, res)
+
+
+@pytest.mark.gpu
+def test_smddp_backend_rccl_world1_torch_ddp():
+    """backend="smddp" on its production inner group (ProcessGroupNCCL = RCCL) in a fresh
+    process: torch DDP construction (broadcast), bucket all-reduce, barrier and all-gather all
+    route through SMDDPProcessGroup to RCCL on the GPU."""
+    import subprocess
+    import sys
+    from _dist import free_port
+    code = f"""
+import os, torch, torch.distributed as dist
+os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT="{free_port()}", RANK="0", WORLD_SIZE="1")
+import smdt_amd.comm.smddp as S
+torch.cuda.set_device(0)
+dist.init_process_group("smddp", rank=0, world_size=1)
+m = torch.nn.Linear(32, 16).cuda()
+ddp = S.DistributedDataParallel(m)
+ddp(torch.randn(8, 32, device="cuda")).sum().backward()
+t = torch.ones(4, device="cuda")
+dist.all_reduce(t)
+out = [torch.zeros(4, device="cuda")]
+dist.all_gather(out, t)
+dist.barrier()
+assert dist.get_backend() == "smddp" and torch.equal(out[0], t) and m.weight.grad is not None
+assert S.smddp_stats()["rccl_calls"] >= 2
+dist.destroy_process_group()
+print("SMDDP_OK")
+"""
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120,
+                       cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    assert r.returncode == 0 and "SMDDP_OK" in r.stdout, r.stdout[-2000:] + r.stderr[-3000:]
 
 
 @pytest.mark.gpu
