@@ -145,6 +145,7 @@ _GROUPS = {
     ],
     "checkpointing": [
         ("--save", dict(type=str, default=None)),
+        ("--async-save", dict(action="store_true")),   # Megatron-core: write checkpoints in the background
         ("--save-interval", dict(type=int, default=None)),
         ("--no-save-optim", dict(action="store_true", default=None)),
         ("--no-save-rng", dict(action="store_true", default=None)),

@@ -14,10 +14,20 @@ and the tracker file is written last by global rank 0 after a barrier, so a cras
 ``--load``, ``--no-save-optim``, ``--no-save-rng``, ``--no-load-optim``, ``--no-load-rng``,
 ``--finetune``, ``--exit-on-missing-checkpoint``, ``--use-checkpoint-args``
 (/root/reference/3_training_megatron-lm/megatron/arguments.py:922-956).
+
+``--async-save`` (Megatron-core's flag): the save only SNAPSHOTS the state — every device tensor
+is copied on the current stream into pinned host memory (stream-ordered, so the next step's kernels
+cannot change it) — and a writer thread serialises and renames the files while training goes on.
+The step pays the device-to-host copy only (GPT-2 345M with Adam state: ~5.7 GB at ~25-50 GB/s)
+instead of the serialisation and file writes (the reference logs 711.6 ms per save, NB3:4584).
+The tracker is written once every rank's writer has finished: ``finalize_async_save`` is called
+at the log interval (a MIN agreement over ranks, no wait) and before any exit or the next save
+(blocking), so ``latest`` never points at an unfinished iteration.
 """
 from __future__ import annotations
 
 import os
+import threading
 import time
 from typing import Optional
 
@@ -70,10 +80,84 @@ def _unwrap(model):
     return model.module if hasattr(model, "module") else model
 
 
+_PENDING = {"thread": None, "iteration": None, "save_dir": None, "error": None}
+
+
+def _snapshot(obj, copies):
+    """``obj`` with every tensor replaced by a host copy (device tensors: pinned, non-blocking on
+    the current stream; ``copies`` collects them so one event can cover all)."""
+    if isinstance(obj, torch.Tensor):
+        t = obj.detach()
+        if t.is_cuda:
+            h = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+            h.copy_(t, non_blocking=True)
+            copies.append(h)
+            return h
+        return t.clone()
+    if isinstance(obj, dict):
+        return type(obj)((k, _snapshot(v, copies)) for k, v in obj.items())
+    if isinstance(obj, tuple) and hasattr(obj, "_fields"):   # namedtuple
+        return type(obj)(*(_snapshot(v, copies) for v in obj))
+    if isinstance(obj, (list, tuple)):
+        return type(obj)(_snapshot(v, copies) for v in obj)
+    return obj
+
+
+def _writer(jobs, event):
+    try:
+        if event is not None:
+            event.synchronize()
+        for obj, path in jobs:
+            _atomic_save(obj, path)
+    except Exception as e:  # noqa: BLE001 - reported by finalize_async_save
+        _PENDING["error"] = e
+
+
+def _all_ranks(flag: bool) -> bool:
+    if not dist.is_initialized():
+        return flag
+    t = torch.tensor([int(flag)])
+    if torch.cuda.is_available() and dist.get_backend() in ("nccl", "smddp"):
+        t = t.cuda()
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return bool(t.item())
+
+
+def finalize_async_save(blocking: bool = True) -> bool:
+    """Collective. Completes a pending ``--async-save``: once every rank's writer thread is done,
+    global rank 0 writes the tracker. ``blocking=False`` only checks (returns False while a writer
+    is still running somewhere). Every rank must call it at the same points."""
+    th = _PENDING["thread"]
+    if th is None:            # the same on every rank: saves start collectively
+        return True
+    if blocking:
+        th.join()
+    if not _all_ranks(not th.is_alive()):
+        return False
+    ok = _all_ranks(_PENDING["error"] is None)
+    err = _PENDING["error"]
+    it, save_dir = _PENDING["iteration"], _PENDING["save_dir"]
+    _PENDING.update(thread=None, iteration=None, save_dir=None, error=None)
+    if not ok:
+        raise RuntimeError(f"async checkpoint write of iteration {it} failed"
+                           + (f" on this rank: {err}" if err is not None else " on another rank"))
+    _barrier()
+    if _rank0():
+        with open(os.path.join(save_dir, TRACKER), "w") as f:
+            f.write(str(it))
+        print(f"  successfully saved checkpoint at iteration {it:7d} to {save_dir} (async)", flush=True)
+    _barrier()
+    return True
+
+
 def save_checkpoint(iteration: int, model, optimizer=None, scheduler=None, args=None, save_dir: Optional[str] = None,
-                    extra: Optional[dict] = None):
+                    extra: Optional[dict] = None, async_save: Optional[bool] = None):
     save_dir = save_dir or args.save
+    if async_save is None:
+        async_save = bool(getattr(args, "async_save", False)) if args is not None else False
+    finalize_async_save(blocking=True)   # one save in flight at a time
     t0 = time.time()
+    jobs = []
     if hasattr(model, "wait_param_gather"):  # overlapped ZeRO all-gather still in flight
         model.wait_param_gather()
     if _rank0():
@@ -96,15 +180,28 @@ def save_checkpoint(iteration: int, model, optimizer=None, scheduler=None, args=
             sd["rng_state"] = _rng_for_save()
         if extra:
             sd.update(extra)
-        _atomic_save(sd, os.path.join(d, "model_optim_rng.pt"))
+        jobs.append((sd, os.path.join(d, "model_optim_rng.pt")))
     if st.cp > 1 and st.dp_rank == 0 and st.cp_rank > 0 and not no_rng:
         # Context-parallel ranks run shifted Philox streams (parallel/random.py): each keeps its own
         # so a resumed run draws the same dropout masks as one that never stopped.
-        _atomic_save({"iteration": iteration, "rng_state": _rng_for_save()},
-                     os.path.join(d, f"rng_cp{st.cp_rank:03d}.pt"))
+        jobs.append(({"iteration": iteration, "rng_state": _rng_for_save()},
+                     os.path.join(d, f"rng_cp{st.cp_rank:03d}.pt")))
     if zero and not no_optim:
-        _atomic_save({"iteration": iteration, "optimizer": optimizer.state_dict()},
-                     os.path.join(d, f"distrib_optim_dp{st.dp_cp_rank:03d}.pt"))
+        jobs.append(({"iteration": iteration, "optimizer": optimizer.state_dict()},
+                     os.path.join(d, f"distrib_optim_dp{st.dp_cp_rank:03d}.pt")))
+    if async_save:
+        copies = []
+        snap = [(_snapshot(obj, copies), path) for obj, path in jobs]
+        ev = None
+        if copies and torch.cuda.is_available():
+            ev = torch.cuda.Event()
+            ev.record()
+        th = threading.Thread(target=_writer, args=(snap, ev), name=f"smdt-ckpt-{iteration}", daemon=False)
+        _PENDING.update(thread=th, iteration=iteration, save_dir=save_dir, error=None)
+        th.start()
+        return time.time() - t0
+    for obj, path in jobs:
+        _atomic_save(obj, path)
     _barrier()
     if _rank0():
         with open(os.path.join(save_dir, TRACKER), "w") as f:

@@ -42,7 +42,7 @@ from ..parallel import state as ps
 from ..parallel.distributed import DistributedDataParallel
 from ..parallel.random import model_parallel_seed
 from . import arguments as A
-from .checkpointing import load_checkpoint, save_checkpoint
+from .checkpointing import finalize_async_save, load_checkpoint, save_checkpoint
 from .schedules import get_forward_backward_func
 from .timers import Timers
 from .utils import report_memory, unwrap_model
@@ -431,6 +431,8 @@ def train(forward_step_func, model, optimizer, scheduler, train_iter, valid_iter
                 total["nan"] = total.get("nan", 0) + 1
             report_mem = training_log({k: float(v) for k, v in loss_dict.items()}, total, lr, iteration, ls,
                                       report_mem, fi, gn, args, elapsed, model_cfg)
+            if getattr(args, "async_save", False):
+                finalize_async_save(blocking=False)   # tracker once every rank's writer is done
         # (TP ranks > 0 hold no iterator: get_batch broadcasts from TP rank 0, so all ranks evaluate)
         if args.eval_interval and iteration % args.eval_interval == 0 and args.do_valid:
             evaluate_and_print_results(f"iteration {iteration}", forward_step_func, valid_iter, model, args)
@@ -444,6 +446,7 @@ def train(forward_step_func, model, optimizer, scheduler, train_iter, valid_iter
         if args.exit_signal_handler and _SIGNAL["received"]:
             if args.save and not saved:
                 save_checkpoint(iteration, model, optimizer, scheduler, args)
+            finalize_async_save(blocking=True)
             print_rank_0("exiting program after receiving SIGTERM.")
             sys.exit(0)
         if args.exit_duration_in_mins:
@@ -455,11 +458,13 @@ def train(forward_step_func, model, optimizer, scheduler, train_iter, valid_iter
             if done.item():
                 if args.save and not saved:
                     save_checkpoint(iteration, model, optimizer, scheduler, args)
+                finalize_async_save(blocking=True)
                 print_rank_0(f"exiting program after {args.exit_duration_in_mins} minutes")
                 sys.exit(0)
         if args.exit_interval and iteration % args.exit_interval == 0:
             if args.save and not saved:
                 save_checkpoint(iteration, model, optimizer, scheduler, args)
+            finalize_async_save(blocking=True)
             print_rank_0(f"exiting program at iteration {iteration}")
             sys.exit(0)
     return iteration
@@ -498,6 +503,7 @@ def pretrain(train_valid_test_dataset_provider, model_provider, model_type, forw
         print_rank_0(f"[after training is done] datetime: {datetime.now().strftime('%Y-%m-%d %H:%M:%S')}")
         if args.save and iteration % (args.save_interval or 10 ** 12) != 0:
             save_checkpoint(iteration, model, optimizer, scheduler, args)
+        finalize_async_save(blocking=True)
     if args.do_valid and args.eval_iters > 0:
         evaluate_and_print_results(f"iteration {iteration} on validation set", forward_step_func, valid_iter, model,
                                    args)

@@ -91,13 +91,18 @@ def test_nb3_hyperparameters_parse_and_derive(monkeypatch):
 
 
 @pytest.mark.slow
-def test_pretrain_gpt_checkpoint_and_resume(tmp_path):
+@pytest.mark.parametrize("async_save", [False, True])
+def test_pretrain_gpt_checkpoint_and_resume(tmp_path, async_save):
+    """Megatron layout save at --save-interval and resume; with --async-save the files are written
+    by a background thread and the tracker only once the writers are done."""
     script = os.path.join(REPO, "recipes", "3_training_megatron-lm", "pretrain_gpt.py")
     common = ["--num-layers", "2", "--hidden-size", "64", "--num-attention-heads", "4", "--seq-length", "64",
               "--max-position-embeddings", "64", "--micro-batch-size", "2", "--global-batch-size", "4",
               "--lr", "0.001", "--lr-decay-style", "cosine", "--lr-warmup-iters", "1", "--mock-data",
               "--log-interval", "1", "--eval-interval", "100", "--eval-iters", "1", "--save", str(tmp_path / "ck"),
               "--save-interval", "3", "--vocab-size", "512", "--tokenizer-type", "NullTokenizer"]
+    if async_save:
+        common.append("--async-save")
     env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT="29531")
     r = subprocess.run([sys.executable, script, "--train-iters", "3"] + common, env=env, capture_output=True,
                        text=True, timeout=600)
@@ -105,6 +110,8 @@ def test_pretrain_gpt_checkpoint_and_resume(tmp_path):
     assert "iteration        3/       3" in r.stdout or "iteration 3/3" in r.stdout.replace("  ", " ")
     assert (tmp_path / "ck" / "latest_checkpointed_iteration.txt").read_text().strip() == "3"
     assert (tmp_path / "ck" / "iter_0000003" / "mp_rank_00" / "model_optim_rng.pt").exists()
+    if async_save:
+        assert "successfully saved checkpoint at iteration       3" in r.stdout and "(async)" in r.stdout
     r2 = subprocess.run([sys.executable, script, "--train-iters", "5", "--load", str(tmp_path / "ck")] + common,
                         env=env, capture_output=True, text=True, timeout=600)
     assert r2.returncode == 0, r2.stdout[-2000:] + r2.stderr[-3000:]
@@ -291,3 +298,32 @@ def test_gpt_position_slice_matches_gathered_positions(offset):
     _, _, p_reset = get_ltor_masks_and_position_ids(tok[:, :-1], 0, reset_position_ids=True)
     assert getattr(p_plain, "_smdt_arange_start", None) == 0
     assert getattr(p_reset, "_smdt_arange_start", None) is None
+
+
+def test_async_save_snapshots_state_at_save_time(tmp_path):
+    """--async-save: the files hold the state of the save call even when the weights change while
+    the writer thread runs; the tracker appears only after finalize_async_save."""
+    import argparse
+    from smdt_amd.models.gpt import GPTModel
+    from smdt_amd.models.transformer import TransformerConfig
+    from smdt_amd.optim.optimizer import MixedPrecisionAdam
+    from smdt_amd.parallel import state as ps
+    from smdt_amd.parallel.distributed import DistributedDataParallel
+    from smdt_amd.train import checkpointing as ck
+    ps.destroy_model_parallel()
+    cfg = TransformerConfig(num_layers=1, hidden_size=32, num_attention_heads=2, max_position_embeddings=16,
+                            padded_vocab_size=64, params_dtype=torch.float32)
+    ddp = DistributedDataParallel(GPTModel(cfg))
+    opt = MixedPrecisionAdam(ddp, lr=1e-3)
+    args = argparse.Namespace(save=str(tmp_path), async_save=True)
+    want = {k: v.clone() for k, v in ddp.module.state_dict().items()}
+    ck.save_checkpoint(7, ddp, opt, None, args)
+    with torch.no_grad():
+        for p in ddp.module.parameters():
+            p.add_(1.0)                       # training goes on while the writer runs
+    assert ck.finalize_async_save(blocking=True)
+    assert (tmp_path / ck.TRACKER).read_text().strip() == "7"
+    sd = torch.load(tmp_path / "iter_0000007" / "mp_rank_00" / "model_optim_rng.pt", weights_only=True)
+    for k, v in want.items():
+        assert torch.equal(sd["model"][k], v), k
+    assert ck.finalize_async_save(blocking=False)   # nothing pending any more
