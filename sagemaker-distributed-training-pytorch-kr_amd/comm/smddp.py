@@ -20,7 +20,8 @@ xGMI) — or Gloo for CPU tensors — and routes
   consumes it. Every ``CHECK_EVERY`` engine calls the ranks agree (MAX over RCCL) on the
   engine's sticky error word; a peer that never arrived turns the path off on every rank for the
   rest of the run, with a warning, and RCCL takes over;
-* every other collective straight to RCCL / Gloo.
+* every other collective straight to RCCL (GPU tensors) or to a host Gloo group (CPU tensors,
+  e.g. object collectives), created on first use.
 
 SMDDP's parameter-server all-reduce exists to use EFA across p3 / p4 nodes; inside one
 xGMI-connected node the peer-read all-reduce (small messages) and RCCL's rings (large ones) are the
@@ -74,12 +75,26 @@ class SMDDPProcessGroup(dist.ProcessGroup):
             opts._timeout = timeout
             opts._devices = [dist.ProcessGroupGloo.create_default_device()]
             self._inner = dist.ProcessGroupGloo(store, rank, size, opts)
+        self._store, self._timeout, self._cpu = store, timeout, None
         self._engine = None
         self._state = "unset"       # unset -> building -> ready | off
         self._lock = threading.Lock()
 
     def getBackendName(self) -> str:
         return BACKEND
+
+    def _route(self, args):
+        """RCCL for GPU tensors; a Gloo group (created on first use, collectively: every rank
+        issues the same collectives) for CPU tensors, e.g. object collectives on host buffers."""
+        t = _first_tensor(args)
+        if t is None or t.is_cuda or self._host_inner:
+            return self._inner
+        if self._cpu is None:
+            opts = dist.ProcessGroupGloo._Options()
+            opts._timeout = self._timeout
+            opts._devices = [dist.ProcessGroupGloo.create_default_device()]
+            self._cpu = dist.ProcessGroupGloo(dist.PrefixStore("smddp_cpu", self._store), self.rank(), self.size(), opts)
+        return self._cpu
 
     # ---- xGMI all-reduce path ----------------------------------------------------------------
     def _world_group(self):
@@ -148,14 +163,25 @@ class SMDDPProcessGroup(dist.ProcessGroup):
                     return _done_work(tensors)
         _STATS["rccl_calls"] += 1
         _STATS["rccl_bytes"] += sum(x.numel() * x.element_size() for x in tensors)
-        return self._inner.allreduce(tensors, opts)
+        return self._route(tensors).allreduce(tensors, opts)
+
+
+def _first_tensor(x):
+    if isinstance(x, torch.Tensor):
+        return x
+    if isinstance(x, (list, tuple)):
+        for v in x:
+            t = _first_tensor(v)
+            if t is not None:
+                return t
+    return None
 
 
 def _delegate(name):
     def f(self, *args, **kwargs):
-        return getattr(self._inner, name)(*args, **kwargs)
+        return getattr(self._route(args), name)(*args, **kwargs)
     f.__name__ = name
-    f.__doc__ = f"``{name}`` on the RCCL / Gloo group."
+    f.__doc__ = f"``{name}`` on the RCCL group (GPU tensors) or the host Gloo group (CPU tensors)."
     return f
 
 

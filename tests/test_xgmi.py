@@ -188,6 +188,11 @@ dist.all_reduce(t)
 out = [torch.zeros(4, device="cuda")]
 dist.all_gather(out, t)
 dist.barrier()
+objs = [None]
+dist.all_gather_object(objs, {{"r": 0}})
+c = torch.ones(3)
+dist.all_reduce(c)                       # a CPU tensor: the host Gloo group of the smddp backend
+assert objs == [{{"r": 0}}] and torch.equal(c, torch.ones(3))
 assert dist.get_backend() == "smddp" and torch.equal(out[0], t) and m.weight.grad is not None
 assert S.smddp_stats()["rccl_calls"] >= 2
 dist.destroy_process_group()
