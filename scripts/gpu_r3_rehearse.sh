@@ -9,9 +9,8 @@ O=gpurun_out/r3_rehearse
 mkdir -p $O
 run() {  # nproc, extra args, log name
   timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node $1 --master-addr 127.0.0.1 \
-    --master-port $((29500 + $1)) bench.py --gpus $1 --steps 2 --warmup 1 $2 > $O/$3.log 2>&1 || { tail -30 $O/$3.log; exit 1; }
+    --master-port $((29500 + $1)) bench.py --gpus $1 --steps 2 --warmup 1 --tunableop 0 $2 > $O/$3.log 2>&1 || { tail -30 $O/$3.log; exit 1; }
   echo "$3: $(grep '^{' $O/$3.log | tail -1 | cut -c1-400)"
 }
-run 2 "--seqs-per-gpu 16" n2_dp2
 run 4 "--seqs-per-gpu 8" n4_dp4
 run 8 "--seqs-per-gpu 8" n8_tp2pp2dp2

@@ -909,8 +909,7 @@ def smddp_torch_ddp_worker(rank, world, port, outdir):
                 dist.all_reduce(mean)            # a CPU tensor: the Gloo path of the smddp group
                 ok.append(bool(torch.allclose(p.grad.cpu(), mean / world, atol=1e-5, rtol=1e-4)))
         torch.cuda.synchronize()
-        grp = dist.distributed_c10d._get_default_group()
-        pg = grp._get_backend(torch.device("cuda"))
+        pg = dist.distributed_c10d._get_default_group()   # the SMDDPProcessGroup itself
         res.update(ok=ok, stats=S.smddp_stats(), backend=dist.get_backend(),
                    error_word=pg._engine.error() if getattr(pg, "_engine", None) is not None else None)
         dist.barrier()
