@@ -214,6 +214,9 @@ def choose_layout(a, world):
 
 def main():
     a = parse()
+    if os.environ.get("SMDT_BENCH_DUMP_AFTER"):   # diagnostics: every thread's stack after N s
+        import faulthandler
+        faulthandler.dump_traceback_later(float(os.environ["SMDT_BENCH_DUMP_AFTER"]), repeat=True)
     from smdt_amd.comm import buckets as comm_buckets
     from smdt_amd.comm import stats as comm_stats
     comm_stats.enable(bool(a.comm_stats))   # before the process group: RCCL per-work timing
