@@ -694,7 +694,7 @@ def relay_tp_mlp_worker(rank, world, port, outdir):
         pickle.dump(res, f)
 
 
-def cp_rng_resume_worker(rank, world, save_dir):
+def cp_rng_resume_worker(rank, world, save_dir, async_save=False):
     """cp = 2: save a checkpoint, keep drawing dropout masks, reload, draw again. Each CP rank must
     resume ITS OWN Philox streams (they are shifted per cp_rank), not cp_rank 0's."""
     import torch.distributed as dist
@@ -703,7 +703,7 @@ def cp_rng_resume_worker(rank, world, save_dir):
     from smdt_amd.models.transformer import TransformerConfig
     from smdt_amd.parallel import state as ps
     from smdt_amd.parallel.random import get_rng, model_parallel_seed
-    from smdt_amd.train.checkpointing import load_checkpoint, save_checkpoint
+    from smdt_amd.train.checkpointing import finalize_async_save, load_checkpoint, save_checkpoint
     init_distributed("gloo")
     st = ps.initialize_model_parallel(1, 1, None, 2)
     model_parallel_seed(1234)
@@ -712,8 +712,9 @@ def cp_rng_resume_worker(rank, world, save_dir):
     def mask():   # the fused dropout kernels' masks are a pure function of (seed, offset)
         return (get_rng("default").next(), get_rng("tp").next(), float(torch.rand(1)))
     mask()                                   # advance the streams a little before saving
-    save_checkpoint(3, m, save_dir=save_dir)
+    save_checkpoint(3, m, save_dir=save_dir, async_save=async_save)
     after_save = [mask(), mask()]
+    assert finalize_async_save(blocking=True)   # (no-op for a synchronous save)
     model_parallel_seed(99)                  # a fresh process would start elsewhere
     load_checkpoint(m, load_dir=save_dir)
     resumed = [mask(), mask()]

@@ -186,10 +186,12 @@ def test_gpt_context_parallel_matches_single_rank(tp, cp, sp, over, ddp):
         _check_tp_grads(ref, grads, meta, tp)
 
 
-def test_context_parallel_rng_resume(tmp_path):
+@pytest.mark.parametrize("async_save", [False, True])
+def test_context_parallel_rng_resume(tmp_path, async_save):
     """every CP rank restores its own (shifted) RNG streams from a checkpoint, so dropout
-    masks after a resume match an uninterrupted run and stay decorrelated across CP ranks."""
-    outs = run_workers(W.cp_rng_resume_worker, 2, str(tmp_path))
+    masks after a resume match an uninterrupted run and stay decorrelated across CP ranks (also
+    with --async-save: per-rank background writers, the tracker after both finished)."""
+    outs = run_workers(W.cp_rng_resume_worker, 2, str(tmp_path), async_save)
     assert sorted(o["cp_rank"] for o in outs) == [0, 1]
     assert all(o["same"] for o in outs), outs
     assert outs[0]["mask"] != outs[1]["mask"]
