@@ -153,6 +153,15 @@ def waiting(axis: str):
         _STEP.waits.append((axis, a, _stamp()))
 
 
+def _backend_label(group) -> str:
+    """The library behind ``group``'s collectives: rccl (nccl / smddp on GPU) or gloo."""
+    try:
+        import torch.distributed as dist
+        return "gloo" if dist.get_backend(group) == "gloo" else "rccl"
+    except (RuntimeError, ValueError):
+        return "rccl"
+
+
 def collective(op: str, group, nbytes: int, work=None, transport: str = "rccl", events=None):
     """Count an issued collective. ``work``: an async torch work (its RCCL timing is read once it
     completed); ``events``: (start, end) events of an xGMI engine call. ``nbytes``: see
@@ -160,6 +169,8 @@ def collective(op: str, group, nbytes: int, work=None, transport: str = "rccl", 
     if not (_ON and _STEP is not None):
         return
     has_work = work is not None and _CUDA
+    if transport == "rccl":
+        transport = _backend_label(group)
     rec = [axis_of(group), op, int(nbytes), _size(group), transport, None, events, None, has_work]
     _STEP.colls.append(rec)
     if has_work:
@@ -201,6 +212,8 @@ def blocking(op: str, group, nbytes: int, transport: str = "rccl", axis: Optiona
         _DEPTH[0] -= 1
         b = _stamp()
         _STEP.waits.append((ax, a, b))
+        if transport == "rccl":
+            transport = _backend_label(group)
         _STEP.colls.append([ax, op, int(nbytes), _size(group), transport, None, (a, b), "shared", False])
 
 

@@ -90,7 +90,7 @@ def test_stats_accounting_gloo():
         assert out["steps"] == 3
         dp = out["comm"]["dp"]
         assert dp["calls"] == 2 and abs(dp["MB"] - 2 * (1 << 16) * 4 / 1e6) < 1e-3
-        ar = dp["ops"]["all_reduce/rccl"]
+        ar = dp["ops"]["all_reduce/gloo"]     # labelled by the group's library
         assert ar["ms"] > 0 and ar["busbw_GBps"] is not None and ar["ranks"] == 2
         ph = out["phase_ms"]
         # the blocking all-reduce sat inside forward/backward: it is a DP wait, not compute
