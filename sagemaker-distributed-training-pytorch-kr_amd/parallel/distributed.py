@@ -459,8 +459,9 @@ class DistributedDataParallel(nn.Module):
         only after all of ITS gradients were accumulated."""
         enabled = bool(enabled)
         if enabled and not self.sync_enabled:
-            from .tensor_parallel import flush_deferred_wgrad
-            flush_deferred_wgrad()
+            from .tensor_parallel import DEFERRED_WGRAD, flush_deferred_wgrad
+            if not DEFERRED_WGRAD.hold:   # (a held accumulation window drains in its last pass)
+                flush_deferred_wgrad()
             self._reset_pending()
         self.sync_enabled = enabled
 

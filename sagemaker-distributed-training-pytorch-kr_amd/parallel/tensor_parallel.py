@@ -286,10 +286,24 @@ class DeferredWgrad:
     def __init__(self):
         self.enabled = os.environ.get("SMDT_DEFER_WGRAD", "1") == "1"
         self.flush_tiles = int(os.environ.get("SMDT_DEFER_WGRAD_TILES", "1024"))
+        # Gradient-accumulation window (set by the ZeRO engine, train/zero.py): while ``hold`` is
+        # on, nothing flushes on size and DDP's sync re-enable does not drain the queue, so the
+        # GEMMs of ALL micro-batches of a window meet in the queue. A weight queued again is
+        # MERGED (its dY / X segments are concatenated along the token dim at flush time): one
+        # GEMM over the window's tokens and ONE read-modify-write of the fp32 main_grad instead of
+        # one per micro-batch (LLaMA-7B: 54 GB of main_grad traffic per pass). Held dY / X are
+        # capped at SMDT_WGRAD_HOLD_GB of HBM (then the queue flushes as usual).
+        self.hold = False
+        self.hold_bytes_cap = int(float(os.environ.get("SMDT_WGRAD_HOLD_GB", "64")) * 2 ** 30)
         self.allow_cpu = False          # tests: exercise the queue logic with a torch fallback
         self.items = []
-        self.targets = set()
+        self.by_key = {}
         self.tiles = 0
+        self.held_bytes = 0
+
+    @property
+    def targets(self):
+        return set(self.by_key)
 
     def eligible(self, mg, g2, t2):
         if not self.enabled or mg.dtype != torch.float32 or not mg.is_contiguous():
@@ -306,29 +320,49 @@ class DeferredWgrad:
 
     def push(self, weight, mg, g2, t2):
         key = mg.data_ptr()
-        if key in self.targets:         # same main_grad twice (grad accumulation): keep order
-            self.flush()
         g2, t2 = g2.contiguous(), t2.contiguous()
-        self.items.append((weight, mg, g2, t2, g2._version, t2._version))
-        self.targets.add(key)
-        self.tiles += -(-g2.shape[1] // 256) * -(-t2.shape[1] // 256)
-        if self.tiles >= self.flush_tiles or len(self.items) >= 32:
+        seg = (g2, t2, g2._version, t2._version)
+        nbytes = g2.numel() * g2.element_size() + t2.numel() * t2.element_size()
+        it = self.by_key.get(key)
+        if it is not None and (it[3] or self.hold):
+            # the same main_grad again inside an accumulation window: merge (the sum over the
+            # concatenated token range is the same accumulation; one readiness report)
+            it[2].append(seg)
+        else:
+            if it is not None:          # same main_grad twice outside a window: keep order
+                self.flush()
+            it = [weight, mg, [seg], self.hold]
+            self.items.append(it)
+            self.by_key[key] = it
+            self.tiles += -(-g2.shape[1] // 256) * -(-t2.shape[1] // 256)
+        self.held_bytes += nbytes
+        if self.held_bytes > self.hold_bytes_cap:
+            self.flush()
+        elif not self.hold and (self.tiles >= self.flush_tiles or len(self.items) >= 32):
             self.flush()
 
     @torch.no_grad()
     def flush(self):
         if not self.items:
             return
-        items, self.items, self.targets, self.tiles = self.items, [], set(), 0
-        for _, _, g2, t2, vg, vt in items:
-            if g2._version != vg or t2._version != vt:
-                raise RuntimeError("deferred wgrad: a queued dY / X tensor was modified in place before the "
-                                   "flush; disable with SMDT_DEFER_WGRAD=0 and report the op that did it")
-        cuda = [it for it in items if it[2].is_cuda]
+        items, self.items, self.by_key, self.tiles, self.held_bytes = self.items, [], {}, 0, 0
+        work = []
+        for weight, mg, segs, _held in items:
+            for g2, t2, vg, vt in segs:
+                if g2._version != vg or t2._version != vt:
+                    raise RuntimeError("deferred wgrad: a queued dY / X tensor was modified in place before the "
+                                       "flush; disable with SMDT_DEFER_WGRAD=0 and report the op that did it")
+            if len(segs) == 1:
+                g2, t2 = segs[0][0], segs[0][1]
+            else:
+                g2 = torch.cat([sg[0] for sg in segs])
+                t2 = torch.cat([sg[1] for sg in segs])
+            work.append((weight, mg, g2, t2))
+        cuda = [it for it in work if it[2].is_cuda]
         done = False
         if cuda:
             done = _ext.ext().wgrad_grouped([it[1] for it in cuda], [it[2] for it in cuda], [it[3] for it in cuda])
-        for weight, mg, g2, t2, _, _ in items:
+        for weight, mg, g2, t2 in work:
             if not (g2.is_cuda and done):
                 mg.add_(g2.t().matmul(t2).view_as(mg))
             cb = getattr(weight, "_smdt_grad_ready", None)

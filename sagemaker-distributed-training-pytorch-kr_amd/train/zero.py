@@ -229,9 +229,25 @@ class ZeroEngine:
         loss = loss / self.ga
         if self.optimizer.scaler is not None:
             loss = loss * self.optimizer.scaler.scale
-        ctx = nullcontext() if self.is_gradient_accumulation_boundary() else self.ddp.no_sync()
+        boundary = self.is_gradient_accumulation_boundary()
+        if self._hold_wgrad():
+            # the window's weight-gradient GEMMs meet in the deferred queue and run once over all
+            # of its tokens in the boundary pass (parallel/tensor_parallel.DeferredWgrad.hold)
+            from ..parallel.tensor_parallel import DEFERRED_WGRAD
+            DEFERRED_WGRAD.hold = not boundary
+        ctx = nullcontext() if boundary else self.ddp.no_sync()
         with ctx:
             loss.backward()
+
+    def _hold_wgrad(self) -> bool:
+        """Merged accumulation-window wgrad applies when the no_sync micro-batches report no
+        readiness: stage 1 / 2 with one DP rank (the gradient store is written in place) or stage 1
+        at any DP size; not under ZeRO-3 (per-layer gathers / reduce-scatters) or a pipeline.
+        SMDT_WGRAD_MERGE_ACCUM=0 turns it off."""
+        if self.ga <= 1 or os.environ.get("SMDT_WGRAD_MERGE_ACCUM", "1") == "0" or self.partitioner is not None:
+            return False
+        st = ps.get_state()
+        return st.pp == 1 and (self.ddp.zero_stage < 2 or self.ddp._direct)
 
     def step(self):
         """Optimizer step at the accumulation boundary; returns the grad-norm tensor or None."""

@@ -148,6 +148,37 @@ def test_deferred_wgrad_queue_semantics(monkeypatch):
     assert ready[-1] is b and not q.items
 
 
+def test_deferred_wgrad_accumulation_window_merges(monkeypatch):
+    """DeferredWgrad.hold (the ZeRO engine's gradient-accumulation window): nothing flushes during
+    the window, every weight's micro-batch GEMMs merge into ONE product over the concatenated
+    tokens with ONE readiness report in the boundary pass, and the result equals the per-micro-
+    batch sum."""
+    from smdt_amd.parallel import tensor_parallel as tp
+    q = tp.DeferredWgrad()
+    q.allow_cpu = True
+    q.flush_tiles = 1                 # would flush after every push outside a window
+    monkeypatch.setattr(tp, "DEFERRED_WGRAD", q)
+    torch.manual_seed(1)
+    ready = []
+    w = torch.nn.Parameter(torch.randn(1024, 64))
+    w.main_grad = torch.zeros(1024, 64)
+    w._smdt_grad_ready = lambda p: ready.append(p)
+    gs = [torch.randn(32 * (i + 1), 1024) for i in range(4)]      # micro-batches of 32 .. 128 tokens
+    xs = [torch.randn(32 * (i + 1), 64) for i in range(4)]
+    calls = []
+    orig_cat = torch.cat
+    monkeypatch.setattr(torch, "cat", lambda t, *a, **k: calls.append(len(t)) or orig_cat(t, *a, **k))
+    q.hold = True
+    for g, x in zip(gs[:3], xs[:3]):
+        tp._wgrad(w, g, x)
+    assert not ready and len(q.items) == 1 and len(q.items[0][2]) == 3
+    q.hold = False                   # the boundary micro-batch
+    tp._wgrad(w, gs[3], xs[3])       # merges, then the size threshold flushes the window at once
+    assert ready == [w] and not q.items and calls == [4, 4]
+    ref = sum(g.t() @ x for g, x in zip(gs, xs))
+    torch.testing.assert_close(w.main_grad, ref, atol=2e-4, rtol=1e-4)   # fp32 summation order
+
+
 @pytest.mark.parametrize("cp,nh,nkv", [(2, 4, 4), (4, 8, 8), (4, 8, 2), (2, 6, 3)])
 def test_ulysses_context_parallel_matches_full_attention(cp, nh, nkv):
     """P10 stretch: Ulysses all-to-all context parallelism over gloo reproduces full-sequence causal

@@ -194,3 +194,60 @@ def test_overlapped_optimizer_step_matches_synchronous(stage, monkeypatch):
         far = ((p1[n].float() - p2[n].float()).abs() > 2e-3 + 1e-2 * p2[n].float().abs()).float().mean().item()
         assert far < 0.01, (n, far)
     assert ((v1 - v2).abs() > 0.05 * v2.abs() + 1e-12).float().mean().item() < 0.01
+
+
+@pytest.mark.gpu
+def test_merged_accumulation_window_wgrad_matches_per_microbatch():
+    """ZeRO engine, gradient accumulation 4 on one DP rank: with the merged window
+    (parallel/tensor_parallel.DeferredWgrad.hold) every weight's four micro-batch wgrad GEMMs run
+    as ONE grouped GEMM over the window's tokens; losses and parameters equal the per-micro-batch
+    path (SMDT_WGRAD_MERGE_ACCUM=0) up to fp32 summation order."""
+    import os
+    from smdt_amd.models.hf import HFCausalLM
+    from smdt_amd.parallel import state as ps
+    from smdt_amd.parallel import tensor_parallel as tp
+    from smdt_amd.train.zero import ZeroEngine
+    cfg = dict(model_type="llama", hidden_size=256, num_hidden_layers=2, num_attention_heads=4,
+               num_key_value_heads=2, intermediate_size=512, max_position_embeddings=256, vocab_size=512,
+               rms_norm_eps=1e-6, rope_theta=10000.0, tie_word_embeddings=False)
+    ds = {"bf16": {"enabled": True}, "gradient_accumulation_steps": 4, "gradient_clipping": 1.0,
+          "optimizer": {"type": "AdamW", "params": {"lr": 1e-2, "weight_decay": 0.1}},
+          "zero_optimization": {"stage": 2}}
+    q = tp.DEFERRED_WGRAD
+    orig_flush = type(q).flush
+    runs = []
+    for merge in ("1", "0"):
+        os.environ["SMDT_WGRAD_MERGE_ACCUM"] = merge
+        segs = []
+
+        def flush(self, _orig=orig_flush, _segs=segs):
+            _segs.extend(len(it[2]) for it in self.items)
+            return _orig(self)
+        type(q).flush = flush
+        try:
+            ps.destroy_model_parallel()
+            torch.manual_seed(0)
+            m = HFCausalLM(cfg, params_dtype=torch.bfloat16, device="cuda")
+            eng = ZeroEngine(m, ds, log=lambda *_: None)
+            g = torch.Generator(device="cuda").manual_seed(1)
+            losses = []
+            for _ in range(8):          # two optimizer steps
+                ids = torch.randint(0, 500, (2, 128), device="cuda", generator=g)
+                loss, _ = m(ids, labels=ids)
+                eng.backward(loss)
+                eng.step()
+                losses.append(loss.detach().float())
+            eng.wait_for_params()
+            torch.cuda.synchronize()
+        finally:
+            type(q).flush = orig_flush
+            os.environ.pop("SMDT_WGRAD_MERGE_ACCUM", None)
+            q.hold = False
+        runs.append((torch.stack(losses).cpu(), {n: p.detach().float().clone() for n, p in m.named_parameters()},
+                     max(segs) if segs else 0))
+    (l1, p1, s1), (l2, p2, s2) = runs
+    assert s1 == 4 and s2 == 1, (s1, s2)     # merged: 4 micro-batch segments per weight
+    torch.testing.assert_close(l1, l2, atol=2e-3, rtol=0)
+    for n in p2:
+        far = ((p1[n] - p2[n]).abs() > 2e-3 + 1e-2 * p2[n].abs()).float().mean().item()
+        assert far < 0.01, (n, far)
