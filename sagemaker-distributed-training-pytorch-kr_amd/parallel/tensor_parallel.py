@@ -328,10 +328,13 @@ class DeferredWgrad:
             # the same main_grad again inside an accumulation window: merge (the sum over the
             # concatenated token range is the same accumulation; one readiness report)
             it[2].append(seg)
+            it[4] = it[4] or not self.hold
         else:
             if it is not None:          # same main_grad twice outside a window: keep order
                 self.flush()
-            it = [weight, mg, [seg], self.hold]
+            # [weight, main_grad, segments, held (created inside a window), has its segment of
+            # the synchronising pass]
+            it = [weight, mg, [seg], self.hold, not self.hold]
             self.items.append(it)
             self.by_key[key] = it
             self.tiles += -(-g2.shape[1] // 256) * -(-t2.shape[1] // 256)
@@ -339,15 +342,31 @@ class DeferredWgrad:
         if self.held_bytes > self.hold_bytes_cap:
             self.flush()
         elif not self.hold and (self.tiles >= self.flush_tiles or len(self.items) >= 32):
-            self.flush()
+            self.flush(complete_only=True)
 
     @torch.no_grad()
-    def flush(self):
+    def flush(self, complete_only: bool = False):
+        """Issue the queued GEMMs (one grouped launch) and report readiness. ``complete_only`` (the
+        size-triggered flush of a synchronising pass): items of a held window whose weight has
+        not yet received this pass's gradient stay queued to merge with it. A held item flushed
+        without that gradient (a forced flush) accumulates but reports no readiness: the pass's
+        own item for the weight does."""
         if not self.items:
             return
-        items, self.items, self.by_key, self.tiles, self.held_bytes = self.items, [], {}, 0, 0
+        if complete_only:
+            items = [it for it in self.items if it[4]]
+            keep = [it for it in self.items if not it[4]]
+        else:
+            items, keep = self.items, []
+        if not items:
+            return
+        self.items = keep
+        self.by_key = {it[1].data_ptr(): it for it in keep}
+        self.tiles = sum(-(-it[2][0][0].shape[1] // 256) * -(-it[2][0][1].shape[1] // 256) for it in keep)
+        self.held_bytes = sum(sg[0].numel() * sg[0].element_size() + sg[1].numel() * sg[1].element_size()
+                              for it in keep for sg in it[2])
         work = []
-        for weight, mg, segs, _held in items:
+        for weight, mg, segs, _held, complete in items:
             for g2, t2, vg, vt in segs:
                 if g2._version != vg or t2._version != vt:
                     raise RuntimeError("deferred wgrad: a queued dY / X tensor was modified in place before the "
@@ -357,16 +376,16 @@ class DeferredWgrad:
             else:
                 g2 = torch.cat([sg[0] for sg in segs])
                 t2 = torch.cat([sg[1] for sg in segs])
-            work.append((weight, mg, g2, t2))
+            work.append((weight, mg, g2, t2, complete))
         cuda = [it for it in work if it[2].is_cuda]
         done = False
         if cuda:
             done = _ext.ext().wgrad_grouped([it[1] for it in cuda], [it[2] for it in cuda], [it[3] for it in cuda])
-        for weight, mg, g2, t2 in work:
+        for weight, mg, g2, t2, complete in work:
             if not (g2.is_cuda and done):
                 mg.add_(g2.t().matmul(t2).view_as(mg))
             cb = getattr(weight, "_smdt_grad_ready", None)
-            if cb is not None:
+            if cb is not None and complete:
                 cb(weight)
 
 
@@ -375,6 +394,23 @@ DEFERRED_WGRAD = DeferredWgrad()
 
 def flush_deferred_wgrad():
     DEFERRED_WGRAD.flush()
+
+
+def accumulation_window_ok(ddps) -> bool:
+    """Whether gradient accumulation over these DDP wrappers may hold + merge the micro-batches'
+    deferred wgrad GEMMs (DeferredWgrad.hold): the no_sync micro-batches must report no readiness
+    (stage 0 / 1, or stage 2 writing its single DP rank's gradient store in place), no ZeRO-3
+    partitioner, no pipeline. SMDT_WGRAD_MERGE_ACCUM=0 turns it off."""
+    if os.environ.get("SMDT_WGRAD_MERGE_ACCUM", "1") == "0" or not DEFERRED_WGRAD.enabled:
+        return False
+    if ps.get_state().pp != 1:
+        return False
+    for d in ddps:
+        if getattr(d, "zero3", None) is not None:
+            return False
+        if getattr(d, "zero_stage", 0) >= 2 and not getattr(d, "_direct", False):
+            return False
+    return True
 
 
 def accumulate_wgrad(mg, g2, t2):

@@ -53,13 +53,19 @@ def forward_backward_no_pipelining(forward_step_func: Callable, data_iterator, m
     ``loss_func(output_tensor) -> (loss, {name: reduced})`` (Megatron's contract,
     `pretrain_gpt.py:92-117`).
     """
+    from ..parallel.tensor_parallel import DEFERRED_WGRAD, accumulation_window_ok
     models = model if isinstance(model, list) else [model]
     m = models[0]
     gate = _SyncGate(models)
+    # the micro-batches' weight-gradient GEMMs merge per weight and run once, in the last
+    # backward (DeferredWgrad.hold): one fp32 main_grad update per iteration
+    hold = not forward_only and num_microbatches > 1 and accumulation_window_ok(gate.ddps)
     losses = []
     for i in range(num_microbatches):
         last = i == num_microbatches - 1
-        gate.set(last)
+        gate.set(last)                   # (re-enabling sync does not drain a held window)
+        if hold:
+            DEFERRED_WGRAD.hold = not last
         out, loss_func = forward_step_func(data_iterator, m)
         loss, info = loss_func(out)
         losses.append(info)

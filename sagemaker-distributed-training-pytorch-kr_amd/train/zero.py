@@ -240,14 +240,11 @@ class ZeroEngine:
             loss.backward()
 
     def _hold_wgrad(self) -> bool:
-        """Merged accumulation-window wgrad applies when the no_sync micro-batches report no
-        readiness: stage 1 / 2 with one DP rank (the gradient store is written in place) or stage 1
-        at any DP size; not under ZeRO-3 (per-layer gathers / reduce-scatters) or a pipeline.
-        SMDT_WGRAD_MERGE_ACCUM=0 turns it off."""
-        if self.ga <= 1 or os.environ.get("SMDT_WGRAD_MERGE_ACCUM", "1") == "0" or self.partitioner is not None:
+        """Merged accumulation-window wgrad (parallel/tensor_parallel.accumulation_window_ok)."""
+        if self.ga <= 1 or self.partitioner is not None:
             return False
-        st = ps.get_state()
-        return st.pp == 1 and (self.ddp.zero_stage < 2 or self.ddp._direct)
+        from ..parallel.tensor_parallel import accumulation_window_ok
+        return accumulation_window_ok([self.ddp])
 
     def step(self):
         """Optimizer step at the accumulation boundary; returns the grad-norm tensor or None."""
