@@ -3,7 +3,7 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(pwd)}"
 export TMPDIR=/tmp HSA_ENABLE_IPC_MODE_LEGACY=0
-O=gpurun_out/r3_sanity
+O=gpurun_out/${SANITY_OUT:-r3_sanity}
 mkdir -p $O
 timeout -k 10 900 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests -m gpu > $O/pytest_gpu.log 2>&1 || { tail -30 $O/pytest_gpu.log; exit 1; }
 tail -1 $O/pytest_gpu.log
