@@ -286,9 +286,9 @@ def _apply_rope_parts(flat, cos, sin, rot, nh, nkv, hd, b, s, inverse):
     k = flat[:, nh * hd:(nh + nkv) * hd].view(s * b, nkv, hd)
     from ..ops import _ext
     if _ext.use_kernels(flat):
-        C = _ext.ext()
-        C.rope_(q, cos, sin, rot, b, s, inverse)
-        C.rope_(k, cos, sin, rot, b, s, inverse)
+        # q and k heads are adjacent in every row of the fused buffer and rotate identically:
+        # ONE launch over the [tokens, nh + nkv, hd] view (row stride W)
+        _ext.ext().rope_(flat[:, :(nh + nkv) * hd].view(s * b, nh + nkv, hd), cos, sin, rot, b, s, inverse)
     else:
         pos = torch.arange(s * b, device=flat.device) // b
         q.copy_(SF._rope_ref(q, cos.to(flat.device), sin.to(flat.device), rot, pos, inverse))

@@ -341,8 +341,13 @@ class DeferredWgrad:
         self.held_bytes += nbytes
         if self.held_bytes > self.hold_bytes_cap:
             self.flush()
-        elif not self.hold and (self.tiles >= self.flush_tiles or len(self.items) >= 32):
-            self.flush(complete_only=True)
+        elif not self.hold:
+            # size trigger on what a flush would issue now (the complete items): held items still
+            # waiting for this pass's gradient neither count nor flush
+            ready = [x for x in self.items if x[4]]
+            tiles = sum(-(-x[2][0][0].shape[1] // 256) * -(-x[2][0][1].shape[1] // 256) for x in ready)
+            if tiles >= self.flush_tiles or len(ready) >= 32:
+                self.flush(complete_only=True)
 
     @torch.no_grad()
     def flush(self, complete_only: bool = False):
