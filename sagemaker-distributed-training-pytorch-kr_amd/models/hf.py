@@ -376,9 +376,12 @@ class HFCausalLM(nn.Module):
             return None
         return torch.cat([real, pads[:need]]).sort().values
 
-    def forward(self, input_ids, attention_mask=None, labels=None, **_):
+    def forward(self, input_ids, attention_mask=None, labels=None, row_groups=None, **_):
         """Returns (mean loss over label tokens, per-token loss [b, s]) with HF shift semantics.
-        With a right-padded CPU ``attention_mask`` the model runs on the real tokens only."""
+        With a right-padded CPU ``attention_mask`` the model runs on the real tokens only.
+        ``row_groups`` (CPU long [b], optional): rows belong to micro-batches 0..G-1 of a fused
+        accumulation window; the loss is then the mean over the groups of each group's own
+        token-mean (exactly what G accumulated micro-batch backwards of loss / G produce)."""
         if labels is None:
             return None, self.model(input_ids)[..., : self.vocab_size]
         shifted = torch.full_like(labels, -100)
@@ -395,14 +398,29 @@ class HFCausalLM(nn.Module):
             with packed_sequences(idx, b, L):
                 tl = self.model(tok, pos, None, labels=lab)                            # [1, T]
             valid = (lab != -100).float()
-            loss = (tl.float() * valid).sum() / valid.sum().clamp(min=1.0)
+            rows = torch.remainder(idx, b) if row_groups is not None else None
+            loss = _grouped_mean(tl.reshape(-1), valid.reshape(-1), rows, row_groups)
             tok_loss = tl.new_zeros(L * b).index_copy(0, idx, tl.reshape(-1)).view(L, b).t()
             return loss, tok_loss
         self.last_computed_tokens = int(input_ids.numel())
         tok_loss = self.model(input_ids, None, None, labels=shifted)
         valid = (shifted != -100).float()
-        loss = (tok_loss.float() * valid).sum() / valid.sum().clamp(min=1.0)
+        rows = (torch.arange(tok_loss.shape[0], device=tok_loss.device).unsqueeze(1).expand_as(tok_loss).reshape(-1)
+                if row_groups is not None else None)
+        loss = _grouped_mean(tok_loss.reshape(-1), valid.reshape(-1), rows, row_groups)
         return loss, tok_loss
+
+
+def _grouped_mean(tl, valid, rows, row_groups):
+    """Mean of per-group token-means (``row_groups[rows]`` = group of each token), or the plain
+    token-mean without groups."""
+    if row_groups is None:
+        return (tl.float() * valid).sum() / valid.sum().clamp(min=1.0)
+    grp = row_groups.to(tl.device, non_blocking=True).index_select(0, rows)
+    G = int(row_groups.max()) + 1
+    num = torch.zeros(G, device=tl.device, dtype=torch.float32).index_add_(0, grp, tl.float() * valid)
+    den = torch.zeros(G, device=tl.device, dtype=torch.float32).index_add_(0, grp, valid)
+    return (num / den.clamp(min=1.0)).mean()
 
 
 class _AttrDict(dict):

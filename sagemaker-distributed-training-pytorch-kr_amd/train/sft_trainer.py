@@ -205,6 +205,12 @@ class Trainer:
         steps_since_log = 0
         last_log_t = t0 = time.time()
         done = self.state["global_step"] >= max_steps
+        # MI355X: the GA micro-batches of an accumulation window run as ONE fused batch (288 GB
+        # hold it): the loss is the mean of the micro-batches' own token-means, so the gradient is
+        # the one GA accumulated backwards produce — one forward / backward / wgrad per step
+        # instead of GA small ones (host-bound at mbs 4). SMDT_SFT_FUSE_GA=0 runs them one by one.
+        fuse = ga > 1 and os.environ.get("SMDT_SFT_FUSE_GA", "1") == "1"
+        window = []
         for epoch in range(start_epoch, num_epochs):
             if done:
                 break
@@ -213,13 +219,26 @@ class Trainer:
                 if skip_batches:
                     skip_batches -= 1
                     continue
+                row_groups = None
+                if fuse and batch.get("attention_mask") is not None:
+                    window.append(batch)
+                    if len(window) < ga:
+                        continue
+                    batch, row_groups = _fuse_window(window)
+                    window = []
                 ids = batch["input_ids"].to(self.device, non_blocking=True)
                 labels = batch["labels"].to(self.device, non_blocking=True)
                 maybe_inject_fault(self.state["global_step"] + 1, self.rank)
                 # the CPU attention mask lets the model skip the padding (models/hf.py)
-                loss, _ = self.model(ids, attention_mask=batch.get("attention_mask"), labels=labels)
-                eng.backward(loss)
-                tr_loss += loss.detach().float() / ga
+                if row_groups is not None:
+                    loss, _ = self.model(ids, attention_mask=batch.get("attention_mask"), labels=labels,
+                                         row_groups=row_groups)
+                    eng.backward(loss, window=True)
+                    tr_loss += loss.detach().float()
+                else:
+                    loss, _ = self.model(ids, attention_mask=batch.get("attention_mask"), labels=labels)
+                    eng.backward(loss)
+                    tr_loss += loss.detach().float() / ga
                 tokens += (labels != -100).sum()
                 am = batch.get("attention_mask")
                 in_tokens += am.sum() if am is not None else ids.numel()
@@ -400,3 +419,19 @@ def sorted_checkpoints(output_dir):
 def get_last_checkpoint(output_dir):
     cks = sorted_checkpoints(output_dir)
     return cks[-1] if cks else None
+
+
+def _fuse_window(batches):
+    """GA collated micro-batches -> one right-padded batch (pads: id 0, label -100, mask 0) and
+    the micro-batch index of every row."""
+    L = max(b["input_ids"].shape[1] for b in batches)
+    ids, labs, masks, groups = [], [], [], []
+    for g, b in enumerate(batches):
+        n, l = b["input_ids"].shape
+        pad = L - l
+        ids.append(torch.nn.functional.pad(b["input_ids"], (0, pad), value=0))
+        labs.append(torch.nn.functional.pad(b["labels"], (0, pad), value=-100))
+        masks.append(torch.nn.functional.pad(b["attention_mask"].to(torch.bool), (0, pad), value=False))
+        groups.append(torch.full((n,), g, dtype=torch.long))
+    return (dict(input_ids=torch.cat(ids), labels=torch.cat(labs), attention_mask=torch.cat(masks)),
+            torch.cat(groups))

@@ -223,9 +223,19 @@ class ZeroEngine:
 
     __call__ = forward
 
-    def backward(self, loss):
+    def backward(self, loss, window: bool = False):
         """Scale by 1/GA (and the fp16 loss scale); reduction is launched from the grad hooks on
-        the last micro-batch of an accumulation window."""
+        the last micro-batch of an accumulation window. ``window``: ``loss`` already covers a
+        whole accumulation window (the GA micro-batches fused into one batch, each weighted 1/GA):
+        no 1/GA scaling, and this backward is the window's synchronising pass."""
+        if window:
+            from ..parallel.tensor_parallel import DEFERRED_WGRAD
+            DEFERRED_WGRAD.hold = False
+            self.micro_steps = (self.micro_steps // self.ga) * self.ga + self.ga - 1
+            if self.optimizer.scaler is not None:
+                loss = loss * self.optimizer.scaler.scale
+            loss.backward()
+            return
         loss = loss / self.ga
         if self.optimizer.scaler is not None:
             loss = loss * self.optimizer.scaler.scale

@@ -287,3 +287,57 @@ def test_padding_free_microbatch_matches_padded(mt, monkeypatch):
     torch.testing.assert_close(t1[keep], t0[keep], rtol=1e-5, atol=1e-6)
     for a, c in zip(g0, g1):
         torch.testing.assert_close(c, a, rtol=1e-4, atol=1e-6)
+
+
+def test_fused_accumulation_window_matches_micro_batches():
+    """SFT trainer's fused GA window (train/sft_trainer._fuse_window + HFCausalLM row_groups +
+    ZeroEngine.backward(window=True)): one batch carrying GA right-padded micro-batches of
+    different lengths gives the same losses and parameters as GA accumulated micro-batches."""
+    import dist_workers as W
+    from smdt_amd.models.hf import HFCausalLM
+    from smdt_amd.parallel import state as ps
+    from smdt_amd.train.sft_trainer import _fuse_window
+    from smdt_amd.train.zero import ZeroEngine
+    ga, steps = 4, 2
+    g = torch.Generator().manual_seed(5)
+    micro = []
+    for i in range(ga * steps):
+        L = 10 + 2 * (i % 3)
+        ids = torch.randint(1, 120, (2, L), generator=g)
+        mask = torch.ones(2, L, dtype=torch.bool)
+        mask[1, L - 3:] = False                      # right padding in the second row
+        lab = ids.clone()
+        lab[:, :3] = -100
+        lab[~mask] = -100
+        micro.append(dict(input_ids=ids, labels=lab, attention_mask=mask))
+    cfg = {"optimizer": {"type": "AdamW", "params": {"lr": 1e-3, "weight_decay": 0.0}},
+           "gradient_accumulation_steps": ga, "gradient_clipping": 1.0, "zero_optimization": {"stage": 2}}
+    runs = []
+    for fused in (False, True):
+        ps.destroy_model_parallel()
+        torch.manual_seed(0)
+        m = HFCausalLM(W.SFT_LLAMA, params_dtype=torch.float32)
+        eng = ZeroEngine(m, cfg, log=lambda *_: None)
+        losses = []
+        for s in range(steps):
+            win = micro[s * ga:(s + 1) * ga]
+            if fused:
+                b, groups = _fuse_window(win)
+                loss, _ = m(b["input_ids"], attention_mask=b["attention_mask"], labels=b["labels"], row_groups=groups)
+                eng.backward(loss, window=True)
+                losses.append(float(loss.detach()))
+                assert eng.step() is not None
+            else:
+                tot = 0.0
+                for b in win:
+                    loss, _ = m(b["input_ids"], attention_mask=b["attention_mask"], labels=b["labels"])
+                    eng.backward(loss)
+                    tot += float(loss.detach()) / ga
+                    gn = eng.step()
+                losses.append(tot)
+                assert gn is not None
+        runs.append((losses, {n: p.detach().clone() for n, p in m.named_parameters()}))
+    (l0, p0), (l1, p1) = runs
+    assert abs(l0[0] - l1[0]) < 1e-5 and abs(l0[1] - l1[1]) < 1e-4, (l0, l1)
+    for n in p0:
+        torch.testing.assert_close(p1[n], p0[n], atol=1e-5, rtol=1e-4, msg=n)
