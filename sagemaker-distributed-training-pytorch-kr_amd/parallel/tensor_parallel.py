@@ -401,12 +401,18 @@ def flush_deferred_wgrad():
     DEFERRED_WGRAD.flush()
 
 
-def accumulation_window_ok(ddps) -> bool:
+def accumulation_window_ok(ddps, default: bool = True) -> bool:
     """Whether gradient accumulation over these DDP wrappers may hold + merge the micro-batches'
     deferred wgrad GEMMs (DeferredWgrad.hold): the no_sync micro-batches must report no readiness
     (stage 0 / 1, or stage 2 writing its single DP rank's gradient store in place), no ZeRO-3
-    partitioner, no pipeline. SMDT_WGRAD_MERGE_ACCUM=0 turns it off."""
-    if os.environ.get("SMDT_WGRAD_MERGE_ACCUM", "1") == "0" or not DEFERRED_WGRAD.enabled:
+    partitioner, no pipeline. SMDT_WGRAD_MERGE_ACCUM=1 / 0 forces it on / off; otherwise
+    ``default`` decides. It pays for small micro-batches, where every micro-batch's wgrad is a
+    short K-loop plus a full fp32 main_grad read-modify-write (LLaMA-7B at ~500 tokens: +12 %,
+    profiles/r3_merge/), and costs for large ones, where the segment concatenation outweighs the
+    saved main_grad traffic (GPT-2 small at 12,288 tokens per micro-batch: 75.5 vs 63.2 ms,
+    profiles/r3_l4l/) — so the SFT engine defaults it on and the Megatron schedule off."""
+    env = os.environ.get("SMDT_WGRAD_MERGE_ACCUM")
+    if (env == "0" or (env is None and not default)) or not DEFERRED_WGRAD.enabled:
         return False
     if ps.get_state().pp != 1:
         return False

@@ -57,9 +57,10 @@ def forward_backward_no_pipelining(forward_step_func: Callable, data_iterator, m
     models = model if isinstance(model, list) else [model]
     m = models[0]
     gate = _SyncGate(models)
-    # the micro-batches' weight-gradient GEMMs merge per weight and run once, in the last
-    # backward (DeferredWgrad.hold): one fp32 main_grad update per iteration
-    hold = not forward_only and num_microbatches > 1 and accumulation_window_ok(gate.ddps)
+    # opt-in (SMDT_WGRAD_MERGE_ACCUM=1): the micro-batches' weight-gradient GEMMs merge per weight
+    # and run once, in the last backward (DeferredWgrad.hold): one fp32 main_grad update per
+    # iteration; it loses at Megatron's usual micro-batch sizes (profiles/r3_l4l/)
+    hold = not forward_only and num_microbatches > 1 and accumulation_window_ok(gate.ddps, default=False)
     losses = []
     for i in range(num_microbatches):
         last = i == num_microbatches - 1
