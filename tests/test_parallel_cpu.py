@@ -179,6 +179,31 @@ def test_deferred_wgrad_accumulation_window_merges(monkeypatch):
     torch.testing.assert_close(w.main_grad, ref, atol=2e-4, rtol=1e-4)   # fp32 summation order
 
 
+def test_accumulation_window_gate(monkeypatch):
+    """accumulation_window_ok: the ZeRO engine's default (on) and the Megatron schedule's (off,
+    profiles/r3_l4l/), SMDT_WGRAD_MERGE_ACCUM forcing either way, and the structural vetoes
+    (ZeRO-3 partitioner, stage 2 without its in-place single-rank store, queue disabled)."""
+    from types import SimpleNamespace as NS
+    from smdt_amd.parallel import tensor_parallel as tp
+    q = tp.DeferredWgrad()
+    monkeypatch.setattr(q, "enabled", True, raising=False)
+    monkeypatch.setattr(tp, "DEFERRED_WGRAD", q)
+    monkeypatch.delenv("SMDT_WGRAD_MERGE_ACCUM", raising=False)
+    plain = NS(zero_stage=1)
+    assert tp.accumulation_window_ok([plain]) is True
+    assert tp.accumulation_window_ok([plain], default=False) is False
+    monkeypatch.setenv("SMDT_WGRAD_MERGE_ACCUM", "1")
+    assert tp.accumulation_window_ok([plain], default=False) is True
+    assert tp.accumulation_window_ok([NS(zero_stage=3, zero3=object())]) is False
+    assert tp.accumulation_window_ok([NS(zero_stage=2)]) is False
+    assert tp.accumulation_window_ok([NS(zero_stage=2, _direct=True)]) is True
+    monkeypatch.setenv("SMDT_WGRAD_MERGE_ACCUM", "0")
+    assert tp.accumulation_window_ok([plain]) is False
+    monkeypatch.delenv("SMDT_WGRAD_MERGE_ACCUM")
+    q.enabled = False
+    assert tp.accumulation_window_ok([plain]) is False
+
+
 @pytest.mark.parametrize("cp,nh,nkv", [(2, 4, 4), (4, 8, 8), (4, 8, 2), (2, 6, 3)])
 def test_ulysses_context_parallel_matches_full_attention(cp, nh, nkv):
     """P10 stretch: Ulysses all-to-all context parallelism over gloo reproduces full-sequence causal
