@@ -315,28 +315,36 @@ class HFCausalLM(nn.Module):
 
     # ---- HF helpers used by smart_tokenizer_and_embedding_resize
     def resize_token_embeddings(self, new_num_tokens: int):
-        """Grow the (padded) vocab; rows beyond the old vocab are zero until the caller fills them."""
+        """Grow the (padded) vocab; rows beyond the old vocab are zero until the caller fills them.
+
+        The embedding / LM-head Parameter objects are kept and only their data grows, so a model
+        built under parallel/zero_init.Init — resized inside ``zero_init.gathered([...])``, as the
+        recipe does (train.py) — has the GROWN tensors cut back into shards when that block exits
+        (new Parameter objects would have stayed full on every rank while the old ones were
+        re-cut), and DDP flags such as the tied embedding's two gradient contributions stay."""
         self.vocab_size = int(new_num_tokens)
         self.hf_config["vocab_size"] = self.vocab_size
         self.model.loss_vocab_size = self.vocab_size
         need = _round_up(new_num_tokens, 128)
         if need <= self.cfg.padded_vocab_size:
             return self
+        from ..parallel import zero_init as zi
+
+        def grow(p):
+            if zi.is_partitioned(p):
+                raise RuntimeError("resize_token_embeddings on a partitioned parameter: call it inside "
+                                   "zero_init.gathered([...]) (recipes/4_training_alpaca_deepspeed/train.py)")
+            neww = torch.zeros(need, p.shape[1], dtype=p.dtype, device=p.device)
+            neww[: p.shape[0]] = p.data
+            p.data = neww
         self.cfg.padded_vocab_size = need
         with torch.no_grad():
-            for attr in ("embedding",):
-                emb = getattr(self.model, attr)
-                old = emb.weight
-                neww = torch.zeros(need, old.shape[1], dtype=old.dtype, device=old.device)
-                neww[: old.shape[0]] = old
-                emb.weight = nn.Parameter(neww)
-                emb.num_embeddings = emb.per = need
-                emb.vocab_end = need
+            emb = self.model.embedding
+            grow(emb.weight)
+            emb.num_embeddings = emb.per = need
+            emb.vocab_end = need
             if self.model.output_weight is not None:
-                old = self.model.output_weight
-                neww = torch.zeros(need, old.shape[1], dtype=old.dtype, device=old.device)
-                neww[: old.shape[0]] = old
-                self.model.output_weight = nn.Parameter(neww)
+                grow(self.model.output_weight)
             if not self.cfg.untie_embeddings_and_output_weights:
                 self.model.embedding.weight._smdt_grad_contributions = 2
         return self

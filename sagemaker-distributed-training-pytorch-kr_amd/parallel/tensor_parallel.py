@@ -292,9 +292,10 @@ class DeferredWgrad:
         # MERGED (its dY / X segments are concatenated along the token dim at flush time): one
         # GEMM over the window's tokens and ONE read-modify-write of the fp32 main_grad instead of
         # one per micro-batch (LLaMA-7B: 54 GB of main_grad traffic per pass). Held dY / X are
-        # capped at SMDT_WGRAD_HOLD_GB of HBM (then the queue flushes as usual).
+        # capped at SMDT_WGRAD_HOLD_GB, by default a quarter of the device memory free at the
+        # first push (then the queue flushes as usual).
         self.hold = False
-        self.hold_bytes_cap = int(float(os.environ.get("SMDT_WGRAD_HOLD_GB", "64")) * 2 ** 30)
+        self.hold_bytes_cap = None      # set at the first push (_hold_cap)
         self.allow_cpu = False          # tests: exercise the queue logic with a torch fallback
         self.items = []
         self.by_key = {}
@@ -318,7 +319,17 @@ class DeferredWgrad:
                     and _ext.use_kernels(g2))
         return self.allow_cpu
 
+    def _hold_cap(self, dev) -> int:
+        env = os.environ.get("SMDT_WGRAD_HOLD_GB")
+        if env is not None:
+            return int(float(env) * 2 ** 30)
+        if dev.type == "cuda":
+            return int(0.25 * torch.cuda.mem_get_info(dev)[0])
+        return 64 * 2 ** 30
+
     def push(self, weight, mg, g2, t2):
+        if self.hold_bytes_cap is None:
+            self.hold_bytes_cap = self._hold_cap(g2.device)
         key = mg.data_ptr()
         g2, t2 = g2.contiguous(), t2.contiguous()
         seg = (g2, t2, g2._version, t2._version)
@@ -398,6 +409,13 @@ DEFERRED_WGRAD = DeferredWgrad()
 
 
 def flush_deferred_wgrad():
+    DEFERRED_WGRAD.flush()
+
+
+def reset_wgrad_window():
+    """Leave hold mode and issue whatever is queued (end of a training loop, or one that stopped
+    inside an accumulation window)."""
+    DEFERRED_WGRAD.hold = False
     DEFERRED_WGRAD.flush()
 
 
@@ -482,6 +500,13 @@ _WT_CACHE: dict = {}
 def params_changed():
     """Invalidate every cached W^T (call before any out-of-autograd parameter write)."""
     _WT_CACHE.clear()
+
+
+def drop_cached_weight_t(params):
+    """Forget the W^T of these parameters (ZeRO-3 frees a gathered bucket: its transposes must go
+    with it, or the cache would end up holding a full bf16 copy of the model on every rank)."""
+    for p in params:
+        _WT_CACHE.pop(id(p), None)
 
 
 def _dgrad_weight_t(weight):

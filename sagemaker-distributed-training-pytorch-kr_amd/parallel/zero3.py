@@ -166,6 +166,8 @@ class ZeroParamPartitioner:
             p.data = v
 
     def _detach(self, b):
+        from .tensor_parallel import drop_cached_weight_t
+        drop_cached_weight_t(b.params)      # the dgrad W^T cache must not outlive the gather
         ph = torch.empty(0, dtype=self.dtype, device=self.dev)
         for p in b.params:
             p.data = ph

@@ -9,10 +9,15 @@ configs/default_offload_opt_param.json:23-41). Here:
         model = HFCausalLM.from_pretrained(...)      # or any nn.Module constructor
     engine = ZeroEngine(model, ds_config)            # stage 3
 
-Inside the context every parameter is cut the moment it is registered on its module: this rank
-keeps 1/dp of its flattened elements (``p._zi_shard``) and the parameter's storage is released
-(a 0-element placeholder; its logical shape is in ``p._zi_shape``). So at no time does a rank hold
-more than its shards plus the ONE parameter being constructed. DistributedDataParallel lays out
+Inside the context every parameter is cut when the constructor of the module that owns it
+returns (as DeepSpeed's zero.Init, which wraps ``nn.Module.__init__``): a module's own
+``reset_parameters()`` / init code therefore runs on the full tensor, then this rank keeps 1/dp of
+its flattened elements (``p._zi_shard``) and the parameter's storage is released (a 0-element
+placeholder; its logical shape is in ``p._zi_shape``). A rank never holds more than its shards plus
+the parameters of the ONE module being constructed (a transformer block's own tensors, not the
+model). A parameter assigned to a module outside of any constructor is cut at once. Code in a
+PARENT's constructor that touches an already-built child's parameters (e.g. a post-init pass over
+the whole model) must do so under ``gathered()``, exactly as with DeepSpeed. DistributedDataParallel lays out
 its buckets from the logical shapes, and the stage-3 partitioner assembles its bucket shards from
 these per-parameter shards with one all-gather per parameter (transient: a single parameter at a
 time), so the full model never exists on any rank (parallel/zero3.py).
@@ -47,7 +52,8 @@ def logical_numel(p) -> int:
 
 
 class Init:
-    """Context manager: parameters registered inside are partitioned over ``dp_group`` at once."""
+    """Context manager: parameters built inside are partitioned over ``dp_group`` as soon as the
+    constructor of the module that owns them returns (see the module docstring)."""
 
     def __init__(self, dp_group=None, enabled: bool = True):
         self.enabled = bool(enabled)
@@ -55,9 +61,10 @@ class Init:
         self.dp = dist.get_world_size(dp_group) if (dist.is_initialized() and enabled) else 1
         self.rank = dist.get_rank(dp_group) if self.dp > 1 else 0
         self.shard_bytes = 0          # bytes of shards kept so far
-        self.peak_bytes = 0           # max over registrations of shards kept + the parameter being cut
+        self.peak_bytes = 0           # max of shards kept + full parameters not yet cut
         self.largest_param_bytes = 0
         self.params = 0
+        self._pending = {}            # id -> bytes of full parameters waiting for their constructor
         self._orig = None
 
     def __enter__(self):
@@ -68,25 +75,83 @@ class Init:
 
         def register_parameter(mod, name, param):
             orig(mod, name, param)
-            if param is not None and not is_partitioned(param) and param.numel() > 0 and param.device.type != "meta":
-                me._partition(param)
+            # inside a constructor of ``mod``: cut when the outermost one returns (its init code
+            # still has to write the full tensor); otherwise now
+            if mod.__dict__.get("_zi_init_depth", 0) == 0:
+                me._maybe_partition(param)
+            elif param is not None and param.device.type != "meta" and not is_partitioned(param):
+                me._pending[id(param)] = (param.numel() * param.element_size(), id(mod))
+                me.peak_bytes = max(me.peak_bytes, me.shard_bytes + me._waiting())
         nn.Module.register_parameter = register_parameter
+        self._wrapped = {}
+        for cls in _module_classes():
+            self._wrap_init(cls)
+
+        def init_subclass(cls, **kw):     # classes defined inside the context
+            me._wrap_init(cls)
+        nn.Module.__init_subclass__ = classmethod(init_subclass)
         return self
 
     def __exit__(self, *exc):
         if self._orig is not None:
             nn.Module.register_parameter = self._orig
             self._orig = None
+            for cls, init in self._wrapped.items():
+                cls.__init__ = init
+            self._wrapped = {}
+            del nn.Module.__init_subclass__
         return False
+
+    def _wrap_init(self, cls):
+        init = cls.__dict__.get("__init__")
+        if init is None or cls in self._wrapped:
+            return
+        me = self
+
+        def __init__(mod, *args, **kwargs):
+            depth = mod.__dict__.get("_zi_init_depth", 0)
+            object.__setattr__(mod, "_zi_init_depth", depth + 1)
+            try:
+                init(mod, *args, **kwargs)
+            finally:
+                object.__setattr__(mod, "_zi_init_depth", depth)
+            if depth == 0:      # the outermost constructor of this object returned
+                mod.__dict__.pop("_zi_init_depth", None)
+                for p in mod.__dict__.get("_parameters", {}).values():
+                    me._maybe_partition(p)
+                for k in [k for k, v in me._pending.items() if v[1] == id(mod)]:
+                    del me._pending[k]        # replaced before the constructor returned
+        __init__.__wrapped__ = init
+        self._wrapped[cls] = init
+        cls.__init__ = __init__
+
+    def _waiting(self):
+        return sum(v[0] for v in self._pending.values())
+
+    def _maybe_partition(self, p):
+        if p is not None and not is_partitioned(p) and p.numel() > 0 and p.device.type != "meta":
+            self._partition(p)
 
     @torch.no_grad()
     def _partition(self, p: nn.Parameter):
         full_bytes = p.numel() * p.element_size()
-        self.peak_bytes = max(self.peak_bytes, self.shard_bytes + full_bytes)
+        waiting = self._waiting() + (0 if id(p) in self._pending else full_bytes)
+        self.peak_bytes = max(self.peak_bytes, self.shard_bytes + waiting)
         self.largest_param_bytes = max(self.largest_param_bytes, full_bytes)
         _cut(p, self.dp, self.rank, self.group)
+        self._pending.pop(id(p), None)
         self.shard_bytes += p._zi_shard.numel() * p._zi_shard.element_size()
         self.params += 1
+
+
+def _module_classes():
+    """nn.Module and every subclass defined so far."""
+    out, todo = [], [nn.Module]
+    while todo:
+        c = todo.pop()
+        out.append(c)
+        todo.extend(c.__subclasses__())
+    return list(dict.fromkeys(out))
 
 
 def _group_dims(group):

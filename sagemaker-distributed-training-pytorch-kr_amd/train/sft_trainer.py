@@ -153,6 +153,30 @@ class Trainer:
         if self.is_main:
             print(msg, flush=True)
 
+    # fraction of the free device memory a fused accumulation window may take for its activations
+    FUSE_MEM_FRACTION = 0.6
+
+    def _window_fits(self, window) -> bool:
+        """Whether GA micro-batches fused into one batch fit in free device memory: an upper
+        estimate of the activations autograd keeps for the fused batch (bf16 per token and layer:
+        ~10 h + 3 ffn values — norms, QKV, attention output, residuals, MLP intermediates — plus
+        the logits and their fp32 gradient) against SMDT_SFT_FUSE_MEM_FRACTION (0.6) of what
+        torch.cuda.mem_get_info reports free now. Always true off-GPU."""
+        if self.device.type != "cuda":
+            return True
+        cfg = getattr(getattr(self.model, "model", None), "cfg", None)
+        if cfg is None:
+            return True
+        toks = sum(int(b["attention_mask"].sum()) if b.get("attention_mask") is not None else b["input_ids"].numel()
+                   for b in window)
+        rows = sum(b["input_ids"].shape[0] for b in window)
+        toks = max(toks, rows * 64)           # padding-free micro-batches round up to 64 rows
+        ffn = getattr(cfg, "ffn_hidden_size", None) or 4 * cfg.hidden_size
+        per_tok = cfg.num_layers * (10 * cfg.hidden_size + 3 * ffn) * 2 + cfg.padded_vocab_size * 6
+        free, _ = torch.cuda.mem_get_info(self.device)
+        frac = float(os.environ.get("SMDT_SFT_FUSE_MEM_FRACTION", self.FUSE_MEM_FRACTION))
+        return toks * per_tok <= frac * free
+
     # ------------------------------------------------------------------ train
     def train(self, resume_from_checkpoint=None):
         a = self.args
@@ -205,83 +229,113 @@ class Trainer:
         steps_since_log = 0
         last_log_t = t0 = time.time()
         done = self.state["global_step"] >= max_steps
-        # MI355X: the GA micro-batches of an accumulation window run as ONE fused batch (288 GB
-        # hold it): the loss is the mean of the micro-batches' own token-means, so the gradient is
-        # the one GA accumulated backwards produce — one forward / backward / wgrad per step
-        # instead of GA small ones (host-bound at mbs 4). SMDT_SFT_FUSE_GA=0 runs them one by one.
+        # MI355X: the GA micro-batches of an accumulation window run as ONE fused batch: the loss is
+        # the mean of the micro-batches' own token-means, so the gradient is the one GA accumulated
+        # backwards produce — one forward / backward / wgrad per step instead of GA small ones
+        # (host-bound at mbs 4). The fused batch holds GA x the activations the DeepSpeed config
+        # was sized for, so each window is checked against the free device memory first
+        # (``_window_fits``) and runs micro-batch by micro-batch when it would not fit.
+        # SMDT_SFT_FUSE_GA=0 always runs them one by one.
         fuse = ga > 1 and os.environ.get("SMDT_SFT_FUSE_GA", "1") == "1"
         window = []
-        for epoch in range(start_epoch, num_epochs):
-            if done:
-                break
-            sampler.set_epoch(epoch)
-            for step, batch in enumerate(loader):
-                if skip_batches:
-                    skip_batches -= 1
-                    continue
-                row_groups = None
-                if fuse and batch.get("attention_mask") is not None:
-                    window.append(batch)
-                    if len(window) < ga:
-                        continue
-                    batch, row_groups = _fuse_window(window)
-                    window = []
-                ids = batch["input_ids"].to(self.device, non_blocking=True)
-                labels = batch["labels"].to(self.device, non_blocking=True)
-                maybe_inject_fault(self.state["global_step"] + 1, self.rank)
-                # the CPU attention mask lets the model skip the padding (models/hf.py)
-                if row_groups is not None:
-                    loss, _ = self.model(ids, attention_mask=batch.get("attention_mask"), labels=labels,
-                                         row_groups=row_groups)
-                    eng.backward(loss, window=True)
-                    tr_loss += loss.detach().float()
-                else:
-                    loss, _ = self.model(ids, attention_mask=batch.get("attention_mask"), labels=labels)
-                    eng.backward(loss)
-                    tr_loss += loss.detach().float() / ga
-                tokens += (labels != -100).sum()
-                am = batch.get("attention_mask")
-                in_tokens += am.sum() if am is not None else ids.numel()
-                pad_tokens += getattr(self.model, "last_computed_tokens", None) or ids.numel()
-                n_seen += ids.shape[0]
-                gn = eng.step()
-                if gn is None:
-                    continue
-                if steady is None:
-                    if self.device.type == "cuda":
-                        torch.cuda.synchronize(self.device)
-                    steady = (time.time(), float(in_tokens), self.state["global_step"] + 1)
-                collective_check_from_env(self.state["global_step"] + 1)
-                self.state["global_step"] += 1
-                self.state["epoch"] = epoch + (step + 1) / len(loader)
-                steps_since_log += 1
-                gs = self.state["global_step"]
-                if (a.logging_first_step and gs == 1) or (a.logging_steps > 0 and gs % int(a.logging_steps) == 0):
-                    t = tr_loss.clone()
-                    if self.world > 1:
-                        dist.all_reduce(t)
-                        t /= self.world
-                    total_loss += tr_loss
-                    now = time.time()
-                    self.log({"loss": round(float(t) / steps_since_log, 4),
-                              "learning_rate": eng.get_lr()[0],
-                              "grad_norm": round(float(gn), 4),
-                              "step_time_s": round((now - last_log_t) / steps_since_log, 4)})
-                    tr_loss.zero_()
-                    steps_since_log = 0
-                    last_log_t = now
-                if a.save_strategy == "steps" and a.save_steps > 0 and gs % int(a.save_steps) == 0:
-                    self._save_checkpoint()
-                if a.evaluation_strategy == "steps" and self.eval_dataset is not None and a.eval_steps \
-                        and gs % int(a.eval_steps) == 0:
-                    self.evaluate()
-                if gs >= max_steps:
-                    done = True
+        fused_windows = unfused_windows = 0
+
+        def run(batch, row_groups):
+            nonlocal tr_loss, tokens, in_tokens, pad_tokens, n_seen
+            ids = batch["input_ids"].to(self.device, non_blocking=True)
+            labels = batch["labels"].to(self.device, non_blocking=True)
+            maybe_inject_fault(self.state["global_step"] + 1, self.rank)
+            # the CPU attention mask lets the model skip the padding (models/hf.py)
+            if row_groups is not None:
+                loss, _ = self.model(ids, attention_mask=batch.get("attention_mask"), labels=labels,
+                                     row_groups=row_groups)
+                eng.backward(loss, window=True)
+                tr_loss += loss.detach().float()
+            else:
+                loss, _ = self.model(ids, attention_mask=batch.get("attention_mask"), labels=labels)
+                eng.backward(loss)
+                tr_loss += loss.detach().float() / ga
+            tokens += (labels != -100).sum()
+            am = batch.get("attention_mask")
+            in_tokens += am.sum() if am is not None else ids.numel()
+            pad_tokens += getattr(self.model, "last_computed_tokens", None) or ids.numel()
+            n_seen += ids.shape[0]
+
+        try:
+            for epoch in range(start_epoch, num_epochs):
+                if done:
                     break
-            if a.save_strategy == "epoch":
-                self._save_checkpoint()
-            if a.evaluation_strategy == "epoch" and self.eval_dataset is not None:
-                self.evaluate()
+                sampler.set_epoch(epoch)
+                for step, batch in enumerate(loader):
+                    if skip_batches:
+                        skip_batches -= 1
+                        continue
+                    if fuse and batch.get("attention_mask") is not None:
+                        window.append(batch)
+                        if len(window) < ga:
+                            continue
+                        if self._window_fits(window):
+                            fused, row_groups = _fuse_window(window)
+                            if fused_windows == 0:
+                                self._log0(f"[sft] fused accumulation window: {ga} micro-batches as one batch of "
+                                           f"{fused['input_ids'].shape[0]} rows")
+                            fused_windows += 1
+                            run(fused, row_groups)
+                        else:
+                            if unfused_windows == 0:
+                                self._log0("[sft] accumulation window would not fit as one batch: running its "
+                                           "micro-batches one by one")
+                            unfused_windows += 1
+                            for b in window[:-1]:
+                                run(b, None)
+                                eng.step()          # (not a boundary)
+                            run(window[-1], None)
+                        window = []
+                    else:
+                        run(batch, None)
+                    gn = eng.step()
+                    if gn is None:
+                        continue
+                    if steady is None:
+                        if self.device.type == "cuda":
+                            torch.cuda.synchronize(self.device)
+                        steady = (time.time(), float(in_tokens), self.state["global_step"] + 1)
+                    collective_check_from_env(self.state["global_step"] + 1)
+                    self.state["global_step"] += 1
+                    self.state["epoch"] = epoch + (step + 1) / len(loader)
+                    steps_since_log += 1
+                    gs = self.state["global_step"]
+                    if (a.logging_first_step and gs == 1) or (a.logging_steps > 0 and gs % int(a.logging_steps) == 0):
+                        t = tr_loss.clone()
+                        if self.world > 1:
+                            dist.all_reduce(t)
+                            t /= self.world
+                        total_loss += tr_loss
+                        now = time.time()
+                        self.log({"loss": round(float(t) / steps_since_log, 4),
+                                  "learning_rate": eng.get_lr()[0],
+                                  "grad_norm": round(float(gn), 4),
+                                  "step_time_s": round((now - last_log_t) / steps_since_log, 4)})
+                        tr_loss.zero_()
+                        steps_since_log = 0
+                        last_log_t = now
+                    if a.save_strategy == "steps" and a.save_steps > 0 and gs % int(a.save_steps) == 0:
+                        self._save_checkpoint()
+                    if a.evaluation_strategy == "steps" and self.eval_dataset is not None and a.eval_steps \
+                            and gs % int(a.eval_steps) == 0:
+                        self.evaluate()
+                    if gs >= max_steps:
+                        done = True
+                        break
+                if a.save_strategy == "epoch":
+                    self._save_checkpoint()
+                if a.evaluation_strategy == "epoch" and self.eval_dataset is not None:
+                    self.evaluate()
+        finally:
+            # a run stopped inside an accumulation window must not leave held weight gradients
+            # (and their dY / X) queued, or the queue in hold mode, for the next user
+            from ..parallel.tensor_parallel import reset_wgrad_window
+            reset_wgrad_window()
         total_loss += tr_loss
         if self.world > 1:
             dist.all_reduce(total_loss)

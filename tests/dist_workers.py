@@ -215,18 +215,93 @@ def zero_sft_worker(rank, world, stage, ga, steps, offload=False, offload_param=
             ids = torch.cat([data[k + j * world + rank][0] for j in range(1)])
             lab = torch.cat([data[k + j * world + rank][1] for j in range(1)])
             k += world
+            if stage == 3 and with_mem and k == steps * ga * world:     # before the last micro-batch
+                # stand-in dgrad W^T entries (the cache only fills on GPU): a bucket freed by
+                # the partitioner must drop its parameters' entries
+                from smdt_amd.parallel import tensor_parallel as _tpm
+                for p in m.parameters():
+                    _tpm._WT_CACHE[id(p)] = (None, torch.empty(1))
             loss, _ = m(ids, labels=lab)
             eng.backward(loss * world / world)
             eng.step()
     eng.wait_for_params()
+    wt_left = None
+    if stage == 3 and with_mem:
+        from smdt_amd.parallel import tensor_parallel as _tpm
+        part = eng.partitioner
+        wt_left = sum(1 for b in eng.ddp.buckets if not part.persistent[b.index]
+                      for p in b.params if id(p) in _tpm._WT_CACHE)
+        _tpm.params_changed()
     total = sum(eng.ddp.shapes[id(p)][0].numel() if hasattr(eng.ddp.shapes[id(p)][0], "numel")
                 else int(torch.tensor(eng.ddp.shapes[id(p)][0]).prod()) for p in eng.ddp.params)
     mem = {"total": total, "grad": eng.ddp.grad_memory_numel(),
            "param": (eng.partitioner.param_memory_numel() if eng.partitioner is not None else None),
-           "param_numel_now": sum(p.numel() for p in m.parameters()), "init": init_stats}
+           "param_numel_now": sum(p.numel() for p in m.parameters()), "init": init_stats,
+           "wt_cache_left": wt_left}
     with eng.gathered_params():
         out = {n: p.detach().clone() for n, p in m.named_parameters()}
     return (out, mem) if with_mem else out
+
+
+def zero_init_torch_modules_worker(rank, world):
+    """Stock torch modules (their own reset_parameters() runs in the constructor) built under
+    parallel/zero_init.Init over ``world`` gloo ranks: the gathered values equal a resident build
+    from the same seed, and nothing full stays resident (Init used to cut a parameter at
+    registration, before nn.Linear's init ran)."""
+    import torch.nn as nn
+    from smdt_amd.comm import init_distributed
+    from smdt_amd.parallel import zero_init as zi
+    init_distributed("gloo")
+
+    class Block(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.fc = nn.Linear(16, 12)
+            self.norm = nn.LayerNorm(12)
+            self.scale = nn.Parameter(torch.empty(12))
+            nn.init.uniform_(self.scale, 0.5, 1.5)     # the owner's init code writes the full tensor
+
+    def build():
+        torch.manual_seed(3)
+        return nn.ModuleList([nn.Embedding(10, 16), Block(), nn.Linear(12, 7, bias=False)])
+    ref = build()
+    with zi.Init() as ctx:
+        got = build()
+    out = {"params": ctx.params, "resident": sum(p.numel() for p in got.parameters()),
+           "peak": ctx.peak_bytes, "shard": ctx.shard_bytes,
+           "full": sum(p.numel() * p.element_size() for p in ref.parameters()), "equal": {}}
+    for (n, p), (_, q) in zip(ref.named_parameters(), got.named_parameters()):
+        out["equal"][n] = bool(torch.equal(zi.gather_full(q).view(p.shape), p.detach()))
+    return out
+
+
+def zero_init_resize_worker(rank, world):
+    """The Alpaca recipe's embedding resize on a model built under zero_init.Init (inside
+    ``gathered``): afterwards the GROWN embedding and LM head are partitioned, with the
+    old rows kept and the new ones set by the block."""
+    from smdt_amd.comm import init_distributed
+    from smdt_amd.models.hf import HFCausalLM
+    from smdt_amd.parallel import state as ps
+    from smdt_amd.parallel import zero_init as zi
+    ps.destroy_model_parallel()
+    init_distributed("gloo")
+    ps.initialize_model_parallel(1, 1)
+    torch.manual_seed(0)
+    ref = HFCausalLM(SFT_LLAMA, params_dtype=torch.float32)
+    torch.manual_seed(0)
+    with zi.Init():
+        m = HFCausalLM(SFT_LLAMA, params_dtype=torch.float32)
+    emb, head = m.model.embedding.weight, m.model.output_weight
+    old_rows = 120                        # (rows 120.. are padding, overwritten below)
+    with zi.gathered([emb, head]):
+        m.resize_token_embeddings(130)
+        emb.data[120:130] = 7.0
+    return {"part": [zi.is_partitioned(emb), zi.is_partitioned(head)],
+            "shape": [zi.logical_shape(emb), zi.logical_shape(head)],
+            "same_objects": emb is m.model.embedding.weight and head is m.model.output_weight,
+            "old_equal": bool(torch.equal(zi.gather_full(emb).view(-1, 64)[:old_rows], ref.model.embedding.weight.detach()[:old_rows])),
+            "new_rows": zi.gather_full(emb).view(-1, 64)[120:130].unique().tolist(),
+            "resident": sum(p.numel() for p in m.parameters())}
 
 
 def gpt_vpp_worker(rank, world, nmb, p2p=None):

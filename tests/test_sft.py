@@ -172,6 +172,7 @@ def test_zero_stage3_memory_is_partitioned(world):
         assert mem["param"]["shard"] <= total / world * 1.05 + 4096, mem
         assert mem["param"]["persistent"] < 0.05 * total, mem
         assert mem["param_numel_now"] <= mem["param"]["persistent"] + 4096, mem
+        assert mem["wt_cache_left"] == 0, mem      # no dgrad W^T of a freed bucket survives
 
 
 @pytest.mark.parametrize("world", [4])
@@ -192,6 +193,23 @@ def test_zero_init_partitioned_construction(world):
         assert mem["param"]["shard"] == rmem["param"]["shard"] and mem["grad"] == rmem["grad"]
         for k, v in rparams.items():
             torch.testing.assert_close(params[k], v, rtol=0, atol=0, msg=k)
+
+
+def test_zero_init_stock_torch_modules():
+    """nn.Linear / nn.LayerNorm / nn.Embedding and a module whose own constructor initialises its
+    parameter, built under zero_init.Init at world 2, equal the resident build (the constructor
+    finishes before the cut) and leave only shards behind."""
+    for o in run_workers(W.zero_init_torch_modules_worker, 2):
+        assert all(o["equal"].values()), o["equal"]
+        assert o["params"] == 7 and o["resident"] == 0, o
+        assert o["shard"] <= o["full"] / 2 + 4 * 7 and o["peak"] < o["full"], o
+
+
+def test_zero_init_embedding_resize_stays_partitioned():
+    for o in run_workers(W.zero_init_resize_worker, 2):
+        assert o["part"] == [True, True] and o["same_objects"], o
+        assert o["shape"] == [(256, 64), (256, 64)] and o["old_equal"] and o["new_rows"] == [7.0], o
+        assert o["resident"] == 0, o
 
 
 def _trainer_args(tmp_path, **over):
@@ -243,6 +261,28 @@ def test_trainer_checkpoint_resume_and_zero_to_fp32(tmp_path):
         got = {k: v.detach().clone() for k, v in t3.model.named_parameters()}
     for k, v in full.items():
         torch.testing.assert_close(got[k], v, rtol=1e-5, atol=1e-6)
+
+
+def test_window_that_does_not_fit_runs_micro_batches(tmp_path, monkeypatch):
+    """A fused accumulation window over the free-memory budget (Trainer._window_fits False) runs
+    its micro-batches one by one: same losses and parameters as SMDT_SFT_FUSE_GA=0."""
+    from smdt_amd.train.sft_trainer import Trainer
+    runs = []
+    for mode in ("off", "nofit"):
+        if mode == "off":
+            monkeypatch.setenv("SMDT_SFT_FUSE_GA", "0")
+        else:
+            monkeypatch.delenv("SMDT_SFT_FUSE_GA", raising=False)
+            monkeypatch.setattr(Trainer, "_window_fits", lambda self, window: False)
+        t = _tiny_trainer(tmp_path, _trainer_args(tmp_path, output_dir=tmp_path / mode, max_steps=3,
+                                                  save_steps=0))
+        t.train()
+        with t.engine.gathered_params():
+            runs.append(([h["loss"] for h in t.state["log_history"] if "loss" in h],
+                         {k: v.detach().clone() for k, v in t.model.named_parameters()}))
+    assert runs[0][0] == runs[1][0]
+    for k, v in runs[0][1].items():
+        torch.testing.assert_close(runs[1][1][k], v, rtol=0, atol=0)
 
 
 def test_save_total_limit_rotates(tmp_path):
