@@ -15,11 +15,16 @@ xGMI) — or Gloo for CPU tensors — and routes
   (``comm/xgmi.py``: every peer read over its own link, one-shot below and two-shot above
   ``ONE_SHOT_MAX_BYTES``, fp32 accumulation in rank order so every rank gets identical bits).
   The engine is built collectively on the first eligible call, validated against RCCL and timed
-  per op, and kept only for the ops it wins on this node; it runs on the caller's current stream
-  and the returned Work is already complete (stream-ordered), which is exactly how torch DDP
-  consumes it. Every ``CHECK_EVERY`` engine calls the ranks agree (MAX over RCCL) on the
-  engine's sticky error word; a peer that never arrived turns the path off on every rank for the
-  rest of the run, with a warning, and RCCL takes over;
+  per op, and kept only for the ops it wins on this node. Each all-reduce runs on the ENGINE'S
+  stream, ordered after the caller's work so far, and the returned Work carries a CUDA future
+  completed by an event on that stream: torch DDP's reducer keeps launching backward kernels on
+  the compute stream while the bucket travels, and its ``wait()`` at the end of backward is a
+  device-side stream wait (no host block) — the overlap that RCCL's own stream gives. Every
+  ``CHECK_EVERY`` engine calls the ranks agree on the engine's sticky error word WITHOUT a host
+  synchronisation in the hook path: the MAX all-reduce is issued on RCCL and copied to pinned
+  memory by a side stream, and that flag is read at the next check, ``CHECK_EVERY`` calls later
+  (every rank at the same call, so every rank decides alike). A peer that never arrived turns the
+  path off on every rank for the rest of the run, with a warning, and RCCL takes over;
 * every other collective straight to RCCL (GPU tensors) or to a host Gloo group (CPU tensors,
   e.g. object collectives), created on first use.
 
@@ -40,6 +45,9 @@ import torch.distributed as dist
 BACKEND = "smddp"
 _REGISTERED = False
 _STATS = {"xgmi_calls": 0, "xgmi_bytes": 0, "rccl_calls": 0, "rccl_bytes": 0}
+# (start, end) CUDA events of engine all-reduces while comm stats are on (tests / profiling: where
+# and when the bucket all-reduces ran)
+_TIMINGS: list = []
 CHECK_EVERY = 64   # engine all-reduces between two agreed error-word checks (one host sync each)
 
 
@@ -53,6 +61,18 @@ def _done_work(result):
     from torch._C._distributed_c10d import _create_work_from_future
     fut = torch.futures.Future()
     fut.set_result(result)
+    return _create_work_from_future(fut)
+
+
+def _stream_work(result, stream):
+    """A Work whose CUDA future completes on ``stream``: set inside that stream, the future records
+    an event there, and ``wait()`` / ``then()`` make the waiter's CURRENT stream wait for it (a
+    device-side dependency; the host never blocks)."""
+    from torch._C._distributed_c10d import _create_work_from_future
+    dev = result[0].device
+    fut = torch.futures.Future(devices=[dev])
+    with torch.cuda.stream(stream):
+        fut.set_result(result)
     return _create_work_from_future(fut)
 
 
@@ -79,6 +99,8 @@ class SMDDPProcessGroup(dist.ProcessGroup):
         self._engine = None
         self._state = "unset"       # unset -> building -> ready | off
         self._lock = threading.Lock()
+        self._pending = None        # (event, pinned flag) of the last error-word check
+        self._side = None
 
     def getBackendName(self) -> str:
         return BACKEND
@@ -134,17 +156,40 @@ class SMDDPProcessGroup(dist.ProcessGroup):
         return eng
 
     def _check(self, eng, dev):
-        """Agree on the engine's sticky error word (every rank reaches this at the same call)."""
-        flag = torch.tensor([float(eng.error())], device=dev)
+        """Every ``CHECK_EVERY`` engine calls (the same call on every rank): read the agreed flag of
+        the previous check — issued ``CHECK_EVERY`` calls ago, so its event has long completed and
+        reading it does not stall — then issue this one: MAX of the sticky error words over the
+        group on the inner group (async), copied to pinned memory by a side stream."""
+        pend, self._pending = self._pending, None
+        if pend is not None:
+            ev, pinned = pend
+            if ev is not None:
+                ev.synchronize()
+            if int(pinned[0]) > 0:
+                import warnings
+                warnings.warn("smddp: an xGMI all-reduce timed out waiting for a peer (its output was NaN-filled); "
+                              "all later all-reduces of this group run on RCCL")
+                eng.deactivate("peer timeout")
+                self._state = "off"
+                return
+        flag = (eng.error_tensor() != 0).to(torch.int32).view(1).to(dev)
         mx = dist.AllreduceOptions()
         mx.reduceOp = dist.ReduceOp.MAX
-        self._inner.allreduce([flag], mx).wait()
-        if flag.item() > 0:
-            import warnings
-            warnings.warn("smddp: an xGMI all-reduce timed out waiting for a peer (its output was NaN-filled); "
-                          "all later all-reduces of this group run on RCCL")
-            eng.deactivate("peer timeout")
-            self._state = "off"
+        if self._host_inner:             # (tests sharing one GPU: Gloo underneath)
+            self._inner.allreduce([flag], mx).wait()
+            self._pending = (None, flag.cpu())
+            return
+        work = self._inner.allreduce([flag], mx)
+        if self._side is None:
+            self._side = torch.cuda.Stream(device=dev)
+        pinned = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+        with torch.cuda.stream(self._side):
+            work.wait()                  # the side stream waits for RCCL, not the compute stream
+            pinned.copy_(flag, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(self._side)
+        flag.record_stream(self._side)
+        self._pending = (ev, pinned)
 
     def allreduce(self, tensors, opts=None):
         opts = opts if opts is not None else dist.AllreduceOptions()
@@ -155,12 +200,16 @@ class SMDDPProcessGroup(dist.ProcessGroup):
             if kind is not None:
                 from . import xgmi
                 eng = self._xgmi(t) if xgmi.eligible(t, self.size()) else None
-                if eng is not None and eng.all_reduce(t, kind):
+                h = eng.all_reduce_async(t, kind) if eng is not None else None
+                if h is not None:
                     _STATS["xgmi_calls"] += 1
                     _STATS["xgmi_bytes"] += t.numel() * t.element_size()
+                    if h.start is not None:
+                        _TIMINGS.append((h.start, h.event))
+                    work = _stream_work(tensors, eng._stream)
                     if _STATS["xgmi_calls"] % CHECK_EVERY == 0:
                         self._check(eng, t.device)
-                    return _done_work(tensors)
+                    return work
         _STATS["rccl_calls"] += 1
         _STATS["rccl_bytes"] += sum(x.numel() * x.element_size() for x in tensors)
         return self._route(tensors).allreduce(tensors, opts)

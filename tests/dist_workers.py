@@ -972,12 +972,31 @@ def smddp_torch_ddp_worker(rank, world, port, outdir):
         m = torch.nn.Sequential(torch.nn.Linear(64, 256), torch.nn.GELU(), torch.nn.Linear(256, 32)).cuda()
         ref_m = torch.nn.Sequential(torch.nn.Linear(64, 256), torch.nn.GELU(), torch.nn.Linear(256, 32)).cuda()
         ref_m.load_state_dict(m.state_dict())
-        ddp = torch.nn.parallel.DistributedDataParallel(m)
-        ok = []
-        for step in range(3):
+        # small buckets: several all-reduces per backward, launched while backward still runs
+        ddp = torch.nn.parallel.DistributedDataParallel(m, bucket_cap_mb=0.04)
+        from smdt_amd.comm import stats as cstats
+        ok, placement = [], []
+        for step in range(4):
             x = torch.randn(16, 64, generator=torch.Generator().manual_seed(10 * step + rank)).cuda()
             m.zero_grad()
+            if step >= 2:            # steady state (bucket rebuild and the engine build are over)
+                cstats.enable(True)
+                S._TIMINGS.clear()
+                torch.cuda.set_sync_debug_mode("error")   # any host sync in the hook path raises
+                b0 = torch.cuda.Event(enable_timing=True)
+                b1 = torch.cuda.Event(enable_timing=True)
+                b0.record()
             ddp(x).square().mean().backward()
+            if step >= 2:
+                b1.record()
+                torch.cuda.set_sync_debug_mode(0)
+                cstats.enable(False)
+                torch.cuda.synchronize()
+                pg = dist.distributed_c10d._get_default_group()
+                starts = [b0.elapsed_time(a) for a, _ in S._TIMINGS]
+                placement.append({"n": len(S._TIMINGS), "engine_stream": pg._engine._stream != torch.cuda.current_stream(),
+                                  "first_start_ms": min(starts) if starts else None,
+                                  "backward_ms": b0.elapsed_time(b1)})
             ref_m.zero_grad()
             ref_m(x).square().mean().backward()
             for p, q in zip(m.parameters(), ref_m.parameters()):
@@ -986,7 +1005,7 @@ def smddp_torch_ddp_worker(rank, world, port, outdir):
                 ok.append(bool(torch.allclose(p.grad.cpu(), mean / world, atol=1e-5, rtol=1e-4)))
         torch.cuda.synchronize()
         pg = dist.distributed_c10d._get_default_group()   # the SMDDPProcessGroup itself
-        res.update(ok=ok, stats=S.smddp_stats(), backend=dist.get_backend(),
+        res.update(ok=ok, stats=S.smddp_stats(), backend=dist.get_backend(), placement=placement,
                    error_word=pg._engine.error() if getattr(pg, "_engine", None) is not None else None)
         dist.barrier()
         dist.destroy_process_group()

@@ -206,8 +206,9 @@ print("SMDDP_OK")
 @pytest.mark.gpu
 def test_smddp_backend_torch_ddp_takes_xgmi_path():
     """backend="smddp" + unmodified torch DDP, 2 processes on one GPU: the bucket all-reduces run
-    on the xGMI engine of comm/smddp.SMDDPProcessGroup and the gradients equal the mean of the
-    ranks' local gradients."""
+    on the xGMI engine of comm/smddp.SMDDPProcessGroup, on the engine's own stream while backward
+    continues, with no host synchronisation in the hook path, and the gradients equal the mean of
+    the ranks' local gradients."""
     import os
     import pickle
     import tempfile
@@ -237,8 +238,13 @@ def test_smddp_backend_torch_ddp_takes_xgmi_path():
                 out.append(pickle.load(f))
     for r, res in enumerate(out):
         assert res["err"] is None, f"rank {r}:\n{res['err']}"
-        assert res["backend"] == "smddp" and all(res["ok"]) and len(res["ok"]) == 12, (r, res)
-        assert res["stats"]["xgmi_calls"] >= 3 and res["error_word"] == 0, (r, res)
+        assert res["backend"] == "smddp" and all(res["ok"]) and len(res["ok"]) == 16, (r, res)
+        assert res["stats"]["xgmi_calls"] >= 8 and res["error_word"] == 0, (r, res)
+        for pl in res["placement"]:
+            # several buckets per backward, all on the engine's own stream, the first one issued
+            # before backward returned (overlap), no host sync in the hook path (sync debug mode)
+            assert pl["n"] >= 2 and pl["engine_stream"], (r, pl)
+            assert pl["first_start_ms"] is not None and pl["first_start_ms"] < pl["backward_ms"], (r, pl)
 
 
 @pytest.mark.gpu
