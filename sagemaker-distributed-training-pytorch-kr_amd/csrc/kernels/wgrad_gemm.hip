@@ -86,25 +86,11 @@ struct Glds {
 
 // One 256 x 256 output tile over stages [0, nst) of 32 rows starting at A/B row mstart.
 // VAR is a diagnostic knob for benchmarks/wgrad_micro.hip only (the library uses VAR = 0):
-// bit 0 skips the in-loop DMA, bit 2 the fragment reads.
-// v_mfma_f32_16x16x32 operand fragment from a row-major [m][c] stage image: lane l (group
-// g = l >> 4, i = l & 15) gets column c0 + i over m = 8 g .. 8 g + 7, the A / B map of the
-// 16x16x32 MFMA (A[row l & 15][k = 8 (l >> 4) + j]). Two ds_read_b64_tr_b16 per fragment: block
-// `blk` covers rows 8 g + 4 blk + q, lane 4 q + p of the group addressing columns c0 + 4 p ..
-// (cdna_hip_programming.md T10).
-__device__ __forceinline__ int tr16_off(int lane, int c0, int blk) {
-  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
-  return G::off(8 * g + 4 * blk + q, (c0 >> 3) + (p >> 1)) + 8 * (p & 1);
-}
-
-__device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
-}
-__device__ __forceinline__ f32x4 mfma16(mt::f16x8 a, mt::f16x8 b, f32x4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
-}
-
-template <bool ATOMIC, int VAR, class E, int MF = 32>
+// bit 0 skips the in-loop DMA, bit 2 the fragment reads. (A v_mfma_f32_16x16x32 form of this
+// tile measured +1.7 % on the grouped microbenchmark and neutral-to-slower in the training step,
+// profiles/r3_wgrad16/: the kernel is bound by its LDS-DMA operand stream, not by the MFMA clock;
+// it was removed.)
+template <bool ATOMIC, int VAR, class E>
 __device__ __forceinline__ void tile_gemm(const E* __restrict__ A, const E* __restrict__ B,
                                           float* __restrict__ C, int N, int K, int n0, int k0, int64_t mstart,
                                           int nst, char* L0, char* L1, char* L2, char* L3) {
@@ -112,106 +98,6 @@ __device__ __forceinline__ void tile_gemm(const E* __restrict__ A, const E* __re
   const int wn = wave >> 2, wk = wave & 3;  // wave tile: n rows [128 wn, +128), k cols [64 wk, +64)
   using F = Frag<BT, E>;
   using V = v8_t<E>;
-  if constexpr (MF == 16) {
-    // Same tile, stage ring and DMA as the 32x32 form; the wave's 128 x 64 tile as 8 x 4
-    // accumulators of v_mfma_f32_16x16x32 (one MFMA per accumulator per 32-row stage). In bare
-    // MFMA loops the 16x16x32 shape holds a higher clock (~1.12-1.15x FLOP/s, MI355X_MICROARCH.md
-    // "DVFS give-back" item 7); here it measured +1.7 % / neutral (see wg_mfma16).
-    int oa[8][2], ob[4][2];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      oa[i][0] = tr16_off(lane, 128 * wn + 16 * i, 0);
-      oa[i][1] = tr16_off(lane, 128 * wn + 16 * i, 1);
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      ob[j][0] = tr16_off(lane, 64 * wk + 16 * j, 0);
-      ob[j][1] = tr16_off(lane, 64 * wk + 16 * j, 1);
-    }
-    f32x4 acc[8][4];
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    Glds ga, gb;
-    ga.init(wave, lane, N, n0, N);
-    gb.init(wave, lane, K, k0, K);
-    const E* Ab = A + mstart * N;
-    const E* Bb = B + mstart * K;
-    const int64_t sa = (int64_t)BM * N, sbk = (int64_t)BM * K;
-    auto issue = [&](int s, char* img) {
-      ga.issue(Ab + s * sa, img, wave);
-      gb.issue(Bb + s * sbk, img + SB, wave);
-    };
-    issue(0, L0);
-    issue(min(1, nst - 1), L1);
-    issue(min(2, nst - 1), L2);
-    wait_vm<2 * 2 * kGlds>();
-    __builtin_amdgcn_s_barrier();
-    auto stage = [&](int s, const char* cur, char* pre) {
-      issue(min(s + kNBuf - 1, nst - 1), pre);
-      const char* at = cur;
-      const char* bt = cur + SB;
-      V b[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) b[j] = F::trf_at(bt, 0, 0, ob[j][0], ob[j][1]);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const V a = F::trf_at(at, 0, 0, oa[i][0], oa[i][1]);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(a, b[j], acc[i][j]);
-      }
-      wait_vm<(kNBuf - 2) * 2 * kGlds>();
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-    };
-    int s = 0;
-    for (; s + kNBuf <= nst; s += kNBuf) {
-      stage(s, L0, L3);
-      stage(s + 1, L1, L0);
-      stage(s + 2, L2, L1);
-      stage(s + 3, L3, L2);
-    }
-    if (s < nst) stage(s, L0, L3);
-    if (s + 1 < nst) stage(s + 1, L1, L0);
-    if (s + 2 < nst) stage(s + 2, L2, L1);
-    wait_vm<0>();
-    // Epilogue: register r of acc[i][j] is C[n0 + 128 wn + 16 i + 4 (lane >> 4) + r][k0 + 64 wk + 16 j + (lane & 15)].
-    const int g = lane >> 4, l15 = lane & 15;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int k = k0 + 64 * wk + 16 * j + l15;
-      const bool kok = k < K;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int nb = n0 + 128 * wn + 16 * i + 4 * g;
-        float* cp = C + (int64_t)nb * K + k;
-        if (nb + 4 <= N && kok) {
-          if constexpr (ATOMIC) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) unsafeAtomicAdd(cp + (int64_t)r * K, acc[i][j][r]);
-          } else {
-            float old[4];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) old[r] = cp[(int64_t)r * K];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) cp[(int64_t)r * K] = old[r] + acc[i][j][r];
-          }
-        } else if (kok) {
-          for (int r = 0; r < 4; ++r) {
-            if (nb + r >= N) continue;
-            float* p = cp + (int64_t)r * K;
-            if constexpr (ATOMIC)
-              unsafeAtomicAdd(p, acc[i][j][r]);
-            else
-              *p += acc[i][j][r];
-          }
-        }
-      }
-    }
-    return;
-  }
-
   int oa[4][2], ob[2][2];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -351,7 +237,7 @@ __device__ __forceinline__ void tile_coords(int t, int ntn, int ntk, int gn, int
   __shared__ __attribute__((aligned(1024))) char L2[2 * SB];      \
   __shared__ __attribute__((aligned(1024))) char L3[2 * SB];
 
-template <bool ATOMIC, int VAR = 0, class E = bf16, int MF = 32>
+template <bool ATOMIC, int VAR = 0, class E = bf16>
 __global__ __launch_bounds__(kThreads, 1) void wgrad_kernel(const E* __restrict__ A, const E* __restrict__ B,
                                                           float* __restrict__ C, int M, int N, int K, int ntn,
                                                           int ntk, int gn, int m_per_split, int nblocks) {
@@ -363,7 +249,7 @@ __global__ __launch_bounds__(kThreads, 1) void wgrad_kernel(const E* __restrict_
   tile_coords(w - split * tiles, ntn, ntk, gn, tn, tk);
   const int mstart = split * m_per_split;
   const int nst = (min(M, mstart + m_per_split) - mstart) / BM;
-  tile_gemm<ATOMIC, VAR, E, MF>(A, B, C, N, K, tn * BT, tk * BT, mstart, nst, L0, L1, L2, L3);
+  tile_gemm<ATOMIC, VAR, E>(A, B, C, N, K, tn * BT, tk * BT, mstart, nst, L0, L1, L2, L3);
 }
 
 struct Problem {
@@ -390,7 +276,7 @@ struct Group {
 // short round and add their partial sums with fp32 atomics (tail tiles only: their sum order is
 // not fixed; everything else stays deterministic). The whole tiles keep the XCD-aware order; the
 // pieces go round-robin over the XCDs.
-template <class E, int MF>
+template <class E>
 __global__ __launch_bounds__(kThreads, 1) void wgrad_grouped_kernel(const Group g) {
   WG_LDS
   const int bid = blockIdx.x;
@@ -409,13 +295,13 @@ __global__ __launch_bounds__(kThreads, 1) void wgrad_grouped_kernel(const Group 
   tile_coords(w - P.tile0, P.ntn, P.ntk, P.gn, tn, tk);
   const int stages = P.M / BM;
   if (piece < 0) {
-    tile_gemm<false, 0, E, MF>((const E*)P.A, (const E*)P.B, P.C, P.N, P.K, tn * BT, tk * BT, 0, stages, L0, L1,
+    tile_gemm<false, 0, E>((const E*)P.A, (const E*)P.B, P.C, P.N, P.K, tn * BT, tk * BT, 0, stages, L0, L1,
                                L2, L3);
   } else {
     const int s0 = piece * g.mps;
     const int nst = min(stages, s0 + g.mps) - s0;
     if (nst <= 0) return;  // a smaller-M problem in the tail: nothing left for this piece (whole block exits)
-    tile_gemm<true, 0, E, MF>((const E*)P.A, (const E*)P.B, P.C, P.N, P.K, tn * BT, tk * BT, (int64_t)s0 * BM,
+    tile_gemm<true, 0, E>((const E*)P.A, (const E*)P.B, P.C, P.N, P.K, tn * BT, tk * BT, (int64_t)s0 * BM,
                               nst, L0, L1, L2, L3);
   }
 }
@@ -426,18 +312,6 @@ inline int group_width(int ntk) { return ntk <= 4 ? 8 : 4; }
 }  // namespace smdt
 
 using namespace smdt;
-
-// MFMA shape: 32 (v_mfma_f32_32x32x16, default) or 16 (16x16x32, SMDT_WGRAD_MFMA=16). Measured
-// on MI355X (profiles/r3_wgrad16/): 16x16x32 is +1.7 % on the grouped microbenchmark (1170 vs 1150
-// TF/s) and neutral-to-slower in the training step (162.5 / 162.7 vs 161.7 ms): the kernel is bound
-// by its LDS-DMA operand stream (~64 GB/s per CU at this tile size), not by the MFMA clock.
-static bool wg_mfma16() {
-  static const int on = [] {
-    const char* v = getenv("SMDT_WGRAD_MFMA");
-    return (v && v[0] == '1') ? 1 : 0;
-  }();
-  return on != 0;
-}
 
 extern "C" int smdt_wgrad_supported(int64_t M, int64_t N, int64_t K) {
   return M > 0 && M % wg::BM == 0 && N >= 8 && K >= 8 && N % 8 == 0 && K % 8 == 0 && M < (1ll << 31) &&
@@ -479,16 +353,13 @@ extern "C" hipError_t smdt_wgrad_accumulate_t(int dtype, const void* dy, const v
   splits = (int)((M + m_per_split - 1) / m_per_split);
   const int nblocks = tiles * splits;
   const int gn = wg::group_width(ntk);
-#define SMDT_WG(AT, ET, MF)                                                                                      \
-  hipLaunchKernelGGL((wg::wgrad_kernel<AT, 0, ET, MF>), dim3(nblocks), dim3(wg::kThreads), 0, st, (const ET*)dy, \
+#define SMDT_WG(AT, ET)                                                                                      \
+  hipLaunchKernelGGL((wg::wgrad_kernel<AT, 0, ET>), dim3(nblocks), dim3(wg::kThreads), 0, st, (const ET*)dy, \
                      (const ET*)x, main_grad, (int)M, (int)N, (int)K, ntn, ntk, gn, m_per_split, nblocks)
-  const bool m16 = wg_mfma16();
   if (dtype == 2) {
-    if (m16) { if (splits > 1) SMDT_WG(true, f16, 16); else SMDT_WG(false, f16, 16); }
-    else { if (splits > 1) SMDT_WG(true, f16, 32); else SMDT_WG(false, f16, 32); }
+    if (splits > 1) SMDT_WG(true, f16); else SMDT_WG(false, f16);
   } else {
-    if (m16) { if (splits > 1) SMDT_WG(true, bf16, 16); else SMDT_WG(false, bf16, 16); }
-    else { if (splits > 1) SMDT_WG(true, bf16, 32); else SMDT_WG(false, bf16, 32); }
+    if (splits > 1) SMDT_WG(true, bf16); else SMDT_WG(false, bf16);
   }
 #undef SMDT_WG
   return hipGetLastError();
@@ -557,14 +428,10 @@ extern "C" hipError_t smdt_wgrad_grouped_t(int dtype, const SmdtWgradProblem* pr
       g.mps = mps;
     }
     const int nblocks = g.nfull + (tiles - g.nfull) * g.splits;
-    const bool m16 = wg_mfma16();
-    if (dtype == 2) {
-      if (m16) hipLaunchKernelGGL((wg::wgrad_grouped_kernel<f16, 16>), dim3(nblocks), dim3(wg::kThreads), 0, st, g);
-      else hipLaunchKernelGGL((wg::wgrad_grouped_kernel<f16, 32>), dim3(nblocks), dim3(wg::kThreads), 0, st, g);
-    } else {
-      if (m16) hipLaunchKernelGGL((wg::wgrad_grouped_kernel<bf16, 16>), dim3(nblocks), dim3(wg::kThreads), 0, st, g);
-      else hipLaunchKernelGGL((wg::wgrad_grouped_kernel<bf16, 32>), dim3(nblocks), dim3(wg::kThreads), 0, st, g);
-    }
+    if (dtype == 2)
+      hipLaunchKernelGGL((wg::wgrad_grouped_kernel<f16>), dim3(nblocks), dim3(wg::kThreads), 0, st, g);
+    else
+      hipLaunchKernelGGL((wg::wgrad_grouped_kernel<bf16>), dim3(nblocks), dim3(wg::kThreads), 0, st, g);
   }
   return hipGetLastError();
 }

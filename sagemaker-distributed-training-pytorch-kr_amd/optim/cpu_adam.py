@@ -78,7 +78,7 @@ class CPUOffloadAdam(MixedPrecisionAdam):
         ddp.wait_param_gather()
         g = ddp.grad_data
         self.found_inf.zero_()
-        total = torch.zeros(1, dtype=torch.float32, device=self.device)
+        total = torch.zeros(1, dtype=torch.float64, device=self.device)   # order-insensitive sum of pieces
         for s, e, key in self.pieces:
             if e > s and (key[1] or self.scaler is not None):
                 ss = self._sumsq(g[s:e])

@@ -146,7 +146,9 @@ class MixedPrecisionAdam:
         xf = x.float()
         if not torch.isfinite(xf).all():
             self.found_inf.fill_(1)
-        return (xf * xf).sum().view(1)
+        # fp64 accumulation: the norm (hence the clip coefficient) does not depend on how the
+        # gradient is split into pieces (ZeRO shards vs whole buckets) or on the reduction order
+        return xf.double().square().sum().float().view(1)
 
     @torch.no_grad()
     def step(self, lr: Optional[float] = None):
@@ -160,7 +162,7 @@ class MixedPrecisionAdam:
             ddp.wait_param_gather()          # (also the previous step's overlapped updates)
         g = ddp.grad_data
         self.found_inf.zero_()
-        total = torch.zeros(1, dtype=torch.float32, device=self.device)
+        total = torch.zeros(1, dtype=torch.float64, device=self.device)   # order-insensitive sum of pieces
         for s, e, key in self.pieces:
             if key[1] and e > s:                        # counts toward the norm on this rank
                 total += self._sumsq(g[s:e])
@@ -176,7 +178,7 @@ class MixedPrecisionAdam:
             scale_t = self.scaler.scale
         use_k = _ext.use_kernels(g)
         if use_k:
-            mul, norm = _ext.ext().clip_coef(total, float(self.clip_grad), 1.0)
+            mul, norm = _ext.ext().clip_coef(total.float(), float(self.clip_grad), 1.0)
             if scale_t is not None:
                 mul = mul / scale_t
                 norm = norm / scale_t
@@ -185,7 +187,7 @@ class MixedPrecisionAdam:
                     coef = torch.clamp(self.clip_grad / (norm + 1e-6), max=1.0)
                     mul = coef / scale_t
         else:
-            norm = torch.sqrt(total)
+            norm = torch.sqrt(total).float()
             if scale_t is not None:
                 norm = norm / scale_t
             coef = torch.clamp(self.clip_grad / (norm + 1e-6), max=1.0) if self.clip_grad > 0 else torch.ones_like(norm)

@@ -238,9 +238,10 @@ class DistributedDataParallel(nn.Module):
         # fused AdamW of each bucket runs on a side stream in FORWARD order and records an event;
         # a forward pre-hook on every transformer block (and on the root, for the embeddings /
         # head / final norm) makes the compute stream wait only for its own buckets. Each bucket's
-        # gradients are re-zeroed on the side stream right after its update. On LLaMA-7B the
-        # memory-bound update (30 B per parameter, ~36 ms) then runs under the forward GEMMs.
-        # SMDT_OVERLAP_OPTIMIZER=0 keeps the step synchronous.
+        # gradients are re-zeroed on the side stream right after its update. Measured on LLaMA-7B
+        # SFT: +0.9 % only (profiles/r3_optimizer_overlap/) — hipBLASLt's stream-K GEMMs hold every
+        # CU, so the memory-bound update mostly finds free CUs between GEMMs, not under them. It
+        # applies to one DP rank (single-GPU SFT); SMDT_OVERLAP_OPTIMIZER=0 keeps the step synchronous.
         self._opt_events: Dict[int, object] = {}
         self._async_zeroed = False
         self.overlap_optimizer = bool(use_distributed_optimizer and self.dp == 1 and dev.type == "cuda"

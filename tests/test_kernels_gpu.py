@@ -308,8 +308,8 @@ def test_flash_attention_dropout(D, causal, heads, dt):
 @pytest.mark.parametrize("causal", [True, False])
 @pytest.mark.parametrize("p", [0.0, 0.1])
 def test_flash_attention_d64_lengths(S, causal, p):
-    """D = 64 at several lengths: S % 256 == 0 runs the 64-queries-per-wave forward (several
-    256-row blocks, every causal diagonal case), S = 384 the 32-query one."""
+    """D = 64 at several lengths (one and several 128-row query blocks, every causal diagonal
+    case, a length that is not a multiple of 256)."""
     torch.manual_seed(15)
     B, H, D = 2, 4, 64
     q, k, v = (torch.randn(B, S, H, D, device=DEV, dtype=torch.bfloat16, requires_grad=True) for _ in range(3))

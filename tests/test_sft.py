@@ -152,13 +152,11 @@ def test_zero2_world8_matches_world1():
 
 
 def _adam_close(got, ref, steps, what, lr=1e-3):
-    """Parameters after ``steps`` AdamW steps agree elementwise (rtol 2e-4, atol 2e-5) except for
-    a few elements: Adam's first steps move an element by ~lr * sign(g), so where g ~ 0 a
-    different fp32 summation order (shards vs accumulated micro-batches, or the host optimizer's
-    threaded clip-norm reduction) may flip the sign — those may differ by up to steps x 2 lr."""
-    d = (got - ref).abs()
-    off = (d > 2e-5 + 2e-4 * ref.abs()).float().mean().item()
-    assert off < 0.005 and d.max().item() <= steps * 2 * lr + 1e-6, (what, off, d.max().item())
+    """Parameters after ``steps`` AdamW steps agree elementwise at rtol 2e-4 / atol 2e-5. The
+    gradient norm (hence the clip coefficient) is accumulated in fp64 (optim/optimizer._sumsq), so
+    it does not depend on how the gradient is split into ZeRO shards; what remains between a sharded
+    run and single-rank accumulation is the association of the micro-batch gradient sums (1 ulp)."""
+    torch.testing.assert_close(got, ref, rtol=2e-4, atol=2e-5, msg=str(what))
 
 
 @pytest.mark.parametrize("world", [2, 4])
