@@ -59,7 +59,7 @@ from smdt_amd.optim.lr_scheduler import OptimizerParamScheduler  # noqa: E402
 from smdt_amd.parallel import state as ps  # noqa: E402
 from smdt_amd.parallel.distributed import DistributedDataParallel  # noqa: E402
 from smdt_amd.parallel.random import model_parallel_seed  # noqa: E402
-from smdt_amd.train.schedules import configure_p2p, get_forward_backward_func  # noqa: E402
+from smdt_amd.train.schedules import configure_p2p, get_forward_backward_func, set_pipeline_schedule  # noqa: E402
 
 REF_TFLOPS_PER_GPU = 41.0e12  # reference GPT-2-small on A100 (derived)
 
@@ -87,10 +87,17 @@ def parse():
     # per-rank shape emulation on one GPU (benchmarks/predict_scaling.py): a TP rank's heads / FFN
     p.add_argument("--kv-channels", type=int, default=None)
     p.add_argument("--ffn-hidden-size", type=int, default=None)
+    p.add_argument("--emulate-tp", type=int, default=0,
+                   help="(1 process) time one rank of a TP group of this size: sharded shapes, sequence "
+                        "parallelism, ring-chunk GEMMs, collectives as local stand-ins (comm/loopback.py)")
     p.add_argument("--emulate-first-stage", action="store_true",
                    help="(pp = 1 emulation) no LM head: the model outputs hidden states, as pipeline stage 0")
     p.add_argument("--pp-last-layers", type=int, default=None,
                    help="layers on the last pipeline stage (default: balanced against the LM head + CE)")
+    p.add_argument("--pp-schedule", choices=["1f1b", "zb", "zbh1"], default="zbh1",
+                   help="pipeline schedule (train/schedules.py): 1F1B, or its zero-bubble split backward")
+    p.add_argument("--vpp", type=int, default=1,
+                   help="virtual pipeline chunks per rank (interleaved 1F1B; uniform layer split)")
     p.add_argument("--hidden-dropout", type=float, default=0.1)
     p.add_argument("--attention-dropout", type=float, default=0.1)  # Megatron default (reference run)
     p.add_argument("--zero", type=int, default=1, help="ZeRO-1/2 distributed optimizer when DP > 1")
@@ -226,14 +233,23 @@ def main():
     if world != a.gpus and rank == 0:
         print(f"[bench] note: --gpus {a.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
     n = world
-    a.tp, a.pp, sp, a.micro_batch_size, a.grad_accum = choose_layout(a, world)
-    st = ps.initialize_model_parallel(a.tp, a.pp)
+    if a.emulate_tp:
+        if world != 1:
+            raise SystemExit("[bench] --emulate-tp runs in one process")
+        a.tp, a.pp = 1, 1
+        _, _, _, a.micro_batch_size, a.grad_accum = choose_layout(a, world)
+        a.tp, sp = a.emulate_tp, a.sequence_parallel is None or bool(a.sequence_parallel)
+        st = ps.initialize_emulated_tensor_parallel(a.tp)
+    else:
+        a.tp, a.pp, sp, a.micro_batch_size, a.grad_accum = choose_layout(a, world)
+        st = ps.initialize_model_parallel(a.tp, a.pp, a.vpp if (a.vpp > 1 and a.pp > 1) else None)
     model_parallel_seed(1234)
     tuned = enable_gemm_tuning(a, rank)
     dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
     vocab = pad_vocab_size(a.vocab_size, 128, a.tp)
+    vpp = a.vpp if (a.vpp > 1 and a.pp > 1) else 1
     last_layers = a.pp_last_layers
-    if last_layers is None and a.pp > 1:
+    if last_layers is None and a.pp > 1 and vpp == 1:
         last_layers = balanced_last_stage_layers(a.num_layers, a.pp, a.hidden_size, a.seq_length, vocab)
     cfg = TransformerConfig(num_layers=a.num_layers, hidden_size=a.hidden_size,
                             num_attention_heads=a.num_attention_heads, max_position_embeddings=a.seq_length,
@@ -244,8 +260,16 @@ def main():
                             sequence_parallel=sp and a.tp > 1, use_flash_attn=not a.no_flash,
                             recompute_granularity="full" if a.recompute == "full" else None,
                             recompute_method="uniform" if a.recompute == "full" else None)
-    model = GPTModel(cfg, pre_process=st.is_first_stage(),
-                     post_process=st.is_last_stage() and not a.emulate_first_stage, device=dev)
+    if vpp > 1:   # interleaved: vpp chunks per rank in one flat DDP buffer (train/training.get_model)
+        chunks = []
+        for c in range(vpp):
+            st.virtual_pp_rank = c
+            chunks.append(GPTModel(cfg, pre_process=st.is_first_stage(), post_process=st.is_last_stage(), device=dev))
+        st.virtual_pp_rank = 0
+        model = torch.nn.ModuleList(chunks)
+    else:
+        model = GPTModel(cfg, pre_process=st.is_first_stage(),
+                         post_process=st.is_last_stage() and not a.emulate_first_stage, device=dev)
     zero = bool(a.zero) and st.dp > 1
     ddp = DistributedDataParallel(model, bucket_size=a.bucket_size, use_distributed_optimizer=zero,
                                   overlap_param_gather=zero)
@@ -274,6 +298,7 @@ def main():
         return out, loss_func
 
     configure_p2p(overlap=True)   # pipeline receives are waited for at their consumer
+    set_pipeline_schedule(a.pp_schedule)
     fb = get_forward_backward_func()
     shape = (S // a.tp if cfg.sequence_parallel else S, mbs, cfg.hidden_size)
 
@@ -354,10 +379,11 @@ def main():
             "config": {"model": model_label(a, vocab), "global_batch": global_batch,
                        "seq_len": S, "micro_batch": mbs, "grad_accum": a.grad_accum,
                        "parallelism": f"tp{a.tp}pp{a.pp}dp{st.dp}" + ("+sp" if cfg.sequence_parallel else "")
-                       + ("+zero1" if zero else ""),
+                       + ("+zero1" if zero else "") + (" (one emulated TP rank)" if a.emulate_tp else ""),
                        "layout": a.layout, "tp": a.tp, "pp": a.pp, "dp": st.dp,
                        "pp_layers": ([(a.num_layers - last_layers) // (a.pp - 1)] * (a.pp - 1) + [last_layers]
-                                     if a.pp > 1 else [a.num_layers]),
+                                     if (a.pp > 1 and vpp == 1) else [a.num_layers // a.pp] * a.pp),
+                       "pp_schedule": (f"interleaved vpp{vpp}" if vpp > 1 else a.pp_schedule) if a.pp > 1 else None,
                        "ddp_bucket": {"elements": ddp.bucket_size, "count": len(ddp.buckets),
                                       **comm_buckets.TUNED},
                        "scaling_note": f"weak: {a.seqs_per_gpu} seqs x {S} tokens per GPU per step",

@@ -27,6 +27,7 @@ import torch.distributed as dist
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ..comm import loopback as _lb
 from ..comm import relay as _relay
 from ..comm import stats as _cs
 from ..ops import _ext
@@ -297,6 +298,17 @@ class DeferredWgrad:
         self.hold = False
         self.hold_bytes_cap = None      # set at the first push (_hold_cap)
         self.allow_cpu = False          # tests: exercise the queue logic with a torch fallback
+        # Split backward (the zero-bubble pipeline schedules, train/schedules.py): while ``defer``
+        # is on, nothing flushes on size and the opportunistic flushes inside backward (beside an
+        # in-flight TP collective) are skipped, so a stage's whole backward pass is B (the input
+        # gradient chain) and its weight-gradient GEMMs (W) run only when the schedule flushes,
+        # after the input gradient was sent to the previous stage.
+        self.defer = False
+        # Merged items of a held window: concatenate the segments (one GEMM over all tokens, one
+        # main_grad read-modify-write: the SFT engine's small micro-batches) or issue one grouped
+        # launch per segment round (large pipeline micro-batches: no concatenation copy).
+        self.concat_segments = True
+        self.stats = {"flushes": 0, "items": 0, "max_segments": 0}
         self.items = []
         self.by_key = {}
         self.tiles = 0
@@ -352,13 +364,18 @@ class DeferredWgrad:
         self.held_bytes += nbytes
         if self.held_bytes > self.hold_bytes_cap:
             self.flush()
-        elif not self.hold:
+        elif not self.hold and not self.defer:
             # size trigger on what a flush would issue now (the complete items): held items still
             # waiting for this pass's gradient neither count nor flush
             ready = [x for x in self.items if x[4]]
             tiles = sum(-(-x[2][0][0].shape[1] // 256) * -(-x[2][0][1].shape[1] // 256) for x in ready)
             if tiles >= self.flush_tiles or len(ready) >= 32:
                 self.flush(complete_only=True)
+
+    def flush_opportunistic(self):
+        """A flush placed beside an in-flight collective to overlap it; skipped while ``defer``."""
+        if not self.defer:
+            self.flush()
 
     @torch.no_grad()
     def flush(self, complete_only: bool = False):
@@ -388,18 +405,27 @@ class DeferredWgrad:
                     raise RuntimeError("deferred wgrad: a queued dY / X tensor was modified in place before the "
                                        "flush; disable with SMDT_DEFER_WGRAD=0 and report the op that did it")
             if len(segs) == 1:
-                g2, t2 = segs[0][0], segs[0][1]
+                work.append((weight, mg, [(segs[0][0], segs[0][1])], complete))
+            elif self.concat_segments:
+                work.append((weight, mg, [(torch.cat([sg[0] for sg in segs]), torch.cat([sg[1] for sg in segs]))],
+                             complete))
             else:
-                g2 = torch.cat([sg[0] for sg in segs])
-                t2 = torch.cat([sg[1] for sg in segs])
-            work.append((weight, mg, g2, t2, complete))
-        cuda = [it for it in work if it[2].is_cuda]
-        done = False
-        if cuda:
-            done = _ext.ext().wgrad_grouped([it[1] for it in cuda], [it[2] for it in cuda], [it[3] for it in cuda])
-        for weight, mg, g2, t2, complete in work:
-            if not (g2.is_cuda and done):
-                mg.add_(g2.t().matmul(t2).view_as(mg))
+                work.append((weight, mg, [(sg[0], sg[1]) for sg in segs], complete))
+        self.stats["flushes"] += 1
+        self.stats["items"] += len(work)
+        self.stats["max_segments"] = max(self.stats["max_segments"], max(len(w[2]) for w in work))
+        # round i issues the i-th segment of every item: one grouped launch per round, so two
+        # segments of one main_grad never run in the same launch (no write race, no atomics)
+        for i in range(max(len(w[2]) for w in work)):
+            rnd = [(mg, sg[i]) for _, mg, sg, _ in work if len(sg) > i]
+            cuda = [(mg, g2, t2) for mg, (g2, t2) in rnd if g2.is_cuda]
+            done = False
+            if cuda:
+                done = _ext.ext().wgrad_grouped([c[0] for c in cuda], [c[1] for c in cuda], [c[2] for c in cuda])
+            for mg, (g2, t2) in rnd:
+                if not (g2.is_cuda and done):
+                    mg.add_(g2.t().matmul(t2).view_as(mg))
+        for weight, _, _, complete in work:
             cb = getattr(weight, "_smdt_grad_ready", None)
             if cb is not None and complete:
                 cb(weight)
@@ -581,7 +607,7 @@ class LinearWithGradAccumulationAndAsyncCommunication(torch.autograd.Function):
         db = _bias_grad(ctx.bias_p, g2) if ctx.has_bias else None
         if handle is not None:
             # the collective is in flight: run the queued weight-gradient GEMMs beside it
-            DEFERRED_WGRAD.flush()
+            DEFERRED_WGRAD.flush_opportunistic()
             _wait_works([handle], group)
         return gi_out, dw, db, None, None
 
@@ -619,6 +645,9 @@ def _exchange(send, recv, nxt, prv, group):
     issue order, so a 2-rank ring with next == prev cannot deadlock). A 2-rank ring on an
     MI355X node goes over every xGMI link through the relay engine (comm/relay.py) when one was
     built for ``group`` and measured faster than RCCL's single-link p2p."""
+    if _lb.is_loopback(group):          # single-process TP emulation: the transfer as a local copy
+        recv.copy_(send)
+        return []
     if nxt == prv:
         eng = _relay.engine_for(group)
         if eng is not None:
@@ -687,7 +716,7 @@ def rs_ring(partial_fn, group, before_last_wait=None):
 
 
 def _flush_wgrad():
-    DEFERRED_WGRAD.flush()
+    DEFERRED_WGRAD.flush_opportunistic()
 
 
 class _ColumnSPLinear(torch.autograd.Function):

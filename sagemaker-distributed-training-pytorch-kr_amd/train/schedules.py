@@ -253,10 +253,36 @@ def _run_backward(out, gout):
         torch.autograd.backward(out, grad_tensors=gout)
 
 
+# Non-interleaved pipeline schedule (``--pp-schedule``; train/pipeline_sim.py simulates each):
+#   1f1b : Megatron's 1F1B — a stage's weight-gradient GEMMs run inside its backward pass, before
+#          the input gradient is sent to the previous stage;
+#   zb   : the backward split zero-bubble style: B (the input-gradient chain) runs with the
+#          deferred wgrad queue held, the input gradient is SENT, then the stage's W GEMMs run
+#          while it travels — the previous stage waits for B only;
+#   zbh1 : zb, and rank r also keeps the W of its last r + 1 backward passes queued behind its
+#          last B (ZB-H1): the final B chain the earlier stages wait for in the cooldown is not
+#          held up by W work, which then fills their drain instead. Same activation memory as
+#          1F1B; the held W operands (dY, X) of up to pp micro-batches stay in HBM.
+PP_SCHEDULES = ("1f1b", "zb", "zbh1")
+_PP_SCHEDULE = {"name": "zbh1"}
+
+
+def set_pipeline_schedule(name: str):
+    if name not in PP_SCHEDULES:
+        raise ValueError(f"--pp-schedule must be one of {PP_SCHEDULES}, got {name!r}")
+    _PP_SCHEDULE["name"] = name
+
+
+def get_pipeline_schedule() -> str:
+    return _PP_SCHEDULE["name"]
+
+
 def forward_backward_pipelining_without_interleaving(forward_step_func: Callable, data_iterator, model,
                                                      num_microbatches: int, tensor_shape, dtype=torch.bfloat16,
-                                                     forward_only: bool = False, grad_scale=None, **_):
-    """1F1B. ``tensor_shape`` is the [s(/tp), b, h] activation exchanged between stages."""
+                                                     forward_only: bool = False, grad_scale=None, schedule=None, **_):
+    """1F1B, optionally with the split (zero-bubble) backward of ``set_pipeline_schedule``.
+    ``tensor_shape`` is the [s(/tp), b, h] activation exchanged between stages."""
+    from ..parallel.tensor_parallel import DEFERRED_WGRAD
     models = model if isinstance(model, list) else [model]
     m = models[0]
     _enter_schedule(m)
@@ -271,6 +297,11 @@ def forward_backward_pipelining_without_interleaving(forward_step_func: Callable
     outputs: List[torch.Tensor] = []
     losses = []
     n_backward = [0]
+    schedule = schedule or get_pipeline_schedule()
+    split = schedule in ("zb", "zbh1") and not forward_only and DEFERRED_WGRAD.enabled
+    # zbh1: backward passes >= defer_from keep their W queued until after the last B of the step
+    defer_from = num_microbatches - (st.pp_rank + 1) if schedule == "zbh1" else num_microbatches
+    concat0 = DEFERRED_WGRAD.concat_segments
 
     def fwd(inp):
         core = m.module if hasattr(m, "module") else m
@@ -284,13 +315,32 @@ def forward_backward_pipelining_without_interleaving(forward_step_func: Callable
         return out
 
     def bwd(inp, out, gout):
+        k = n_backward[0]
         n_backward[0] += 1
-        gate.set(n_backward[0] == num_microbatches)
+        sync = n_backward[0] == num_microbatches
+        if split:
+            # queued W items of this pass: held (merged with the sync pass's, no readiness of their
+            # own) when they stay queued beyond it; enabling sync must not flush earlier held ones
+            held = k >= defer_from and not sync
+            DEFERRED_WGRAD.defer = True
+            DEFERRED_WGRAD.hold = held or (sync and k > defer_from)
+            gate.set(sync)
+            DEFERRED_WGRAD.hold = held
+        else:
+            gate.set(sync)
         inp, gout = _finish_recv(inp), _finish_recv(gout)
         if inp is not None:
             inp.retain_grad()
         _run_backward(out, gout)
+        if split:
+            DEFERRED_WGRAD.defer = False
         return None if inp is None else inp.grad
+
+    def after_send(k):
+        """W of backward pass k, once its input gradient is on its way (split schedules)."""
+        if split and (k < defer_from or k == num_microbatches - 1):
+            DEFERRED_WGRAD.hold = False
+            DEFERRED_WGRAD.flush()
 
     def recv_fwd():
         return None if first else _p2p(recv_prev_shape=tensor_shape, dtype=dtype, device=dev)[0]
@@ -298,50 +348,62 @@ def forward_backward_pipelining_without_interleaving(forward_step_func: Callable
     def recv_bwd():
         return None if last else _p2p(recv_next_shape=tensor_shape, dtype=dtype, device=dev)[1]
 
-    for _ in range(warm):
-        inp = recv_fwd()
-        out = fwd(inp)
-        if not last:
-            _p2p(send_next=out)
-            _drop_output(out)
-        inputs.append(inp)
-        outputs.append(out)
-    inp = recv_fwd() if steady > 0 else None
-    for i in range(steady):
-        is_last_iter = i == steady - 1
-        out = fwd(inp)
-        if forward_only:
+    if split:
+        DEFERRED_WGRAD.concat_segments = False     # held + sync segments: one launch per round
+    try:
+        for _ in range(warm):
+            inp = recv_fwd()
+            out = fwd(inp)
             if not last:
                 _p2p(send_next=out)
-            if not is_last_iter:
-                inp = recv_fwd()
-            continue
-        if last:
-            gout = None
-        else:
-            gout = _p2p(send_next=out, recv_next_shape=tensor_shape, dtype=dtype, device=dev)[1]
-            _drop_output(out)
-        inputs.append(inp)
-        outputs.append(out)
-        i0, o0 = inputs.pop(0), outputs.pop(0)
-        gin = bwd(i0, o0, gout)
-        if is_last_iter:
-            inp = None
-            if not first:
-                _p2p(send_prev=gin)
-        else:
-            if first:
-                inp = None
-                inp = recv_fwd()
+                _drop_output(out)
+            inputs.append(inp)
+            outputs.append(out)
+        inp = recv_fwd() if steady > 0 else None
+        for i in range(steady):
+            is_last_iter = i == steady - 1
+            out = fwd(inp)
+            if forward_only:
+                if not last:
+                    _p2p(send_next=out)
+                if not is_last_iter:
+                    inp = recv_fwd()
+                continue
+            if last:
+                gout = None
             else:
-                inp = _p2p(send_prev=gin, recv_prev_shape=tensor_shape, dtype=dtype, device=dev)[0]
-    if not forward_only:
-        for _ in range(warm):
+                gout = _p2p(send_next=out, recv_next_shape=tensor_shape, dtype=dtype, device=dev)[1]
+                _drop_output(out)
+            inputs.append(inp)
+            outputs.append(out)
             i0, o0 = inputs.pop(0), outputs.pop(0)
-            gout = recv_bwd()
+            k = n_backward[0]
             gin = bwd(i0, o0, gout)
-            if not first:
-                _p2p(send_prev=gin)
+            if is_last_iter:
+                inp = None
+                if not first:
+                    _p2p(send_prev=gin)
+            else:
+                if first:
+                    inp = None
+                    inp = recv_fwd()
+                else:
+                    inp = _p2p(send_prev=gin, recv_prev_shape=tensor_shape, dtype=dtype, device=dev)[0]
+            after_send(k)
+        if not forward_only:
+            for _ in range(warm):
+                i0, o0 = inputs.pop(0), outputs.pop(0)
+                gout = recv_bwd()
+                k = n_backward[0]
+                gin = bwd(i0, o0, gout)
+                if not first:
+                    _p2p(send_prev=gin)
+                after_send(k)
+    finally:
+        if split:
+            DEFERRED_WGRAD.defer = False
+            DEFERRED_WGRAD.hold = False
+            DEFERRED_WGRAD.concat_segments = concat0
     _retire_sends()
     gate.set(True)
     return losses

@@ -484,7 +484,7 @@ def gpt_cp_worker(rank, world, tp, cp, sp, cfg_over=None, with_ddp=False):
     return loss.detach(), grads, meta
 
 
-def gpt_layout_worker(rank, world, tp, pp, nmb, zero, defer=False, sp=False):
+def gpt_layout_worker(rank, world, tp, pp, nmb, zero, defer=False, sp=False, schedule=None, cfg_over=None):
     """DDP-wrapped tiny GPT under a TP x PP x DP layout with ``nmb`` micro-batches per step (gradient
     accumulation for pp == 1, 1F1B otherwise): returns the reduced fp32 main_grad of every local
     parameter. The global batch (4 sequences) is split over the DP ranks, so the reduced gradients
@@ -496,14 +496,16 @@ def gpt_layout_worker(rank, world, tp, pp, nmb, zero, defer=False, sp=False):
     from smdt_amd.models.transformer import TransformerConfig
     from smdt_amd.parallel import state as ps
     from smdt_amd.parallel.distributed import DistributedDataParallel
-    from smdt_amd.train.schedules import get_forward_backward_func
+    from smdt_amd.train.schedules import get_forward_backward_func, set_pipeline_schedule
     init_distributed("gloo")
     st = ps.initialize_model_parallel(tp, pp)
+    if schedule is not None:
+        set_pipeline_schedule(schedule)
     if defer:
         from smdt_amd.parallel import tensor_parallel as tpm
         tpm.DEFERRED_WGRAD.allow_cpu = True
         tpm.DEFERRED_WGRAD.flush_tiles = 2
-    cfg = TransformerConfig(**{**TINY, "sequence_parallel": sp})
+    cfg = TransformerConfig(**{**TINY, "sequence_parallel": sp, **(cfg_over or {})})
     m = GPTModel(cfg, pre_process=st.is_first_stage(), post_process=st.is_last_stage())
     ddp = DistributedDataParallel(m, bucket_size=6000, use_distributed_optimizer=zero)
     tokens, labels = _batch()
@@ -518,7 +520,7 @@ def gpt_layout_worker(rank, world, tp, pp, nmb, zero, defer=False, sp=False):
     ddp.zero_grad_buffer()
     fb = get_forward_backward_func()
     seq = 32 // tp if (sp and tp > 1) else 32
-    fb(fstep, data, ddp, nmb, tensor_shape=(seq, per // nmb, 64), dtype=torch.float32)
+    losses = fb(fstep, data, ddp, nmb, tensor_shape=(seq, per // nmb, 64), dtype=torch.float32)
     ddp.finish_grad_sync()
     allreduce_word_embedding_grads(m)
     full = ddp.grad_data.clone()
@@ -528,9 +530,12 @@ def gpt_layout_worker(rank, world, tp, pp, nmb, zero, defer=False, sp=False):
             dist.all_gather_into_tensor(full[b.start:b.end], ddp.grad_data[s:e].clone(), group=st.dp_group)
     grads = {n: full[ddp.param_index[id(p)][0]:ddp.param_index[id(p)][0] + p.numel()].view_as(p).clone()
              for n, p in m.named_parameters()}
-    meta = {"tp_rank": st.tp_rank, "pp_rank": st.pp_rank, "layer_offset": m.first_layer}
+    from smdt_amd.parallel import tensor_parallel as tpm
+    meta = {"tp_rank": st.tp_rank, "pp_rank": st.pp_rank, "dp_rank": st.dp_rank, "layer_offset": m.first_layer,
+            "wgrad_stats": dict(tpm.DEFERRED_WGRAD.stats)}
     dist.destroy_process_group()
-    return None, grads, meta
+    loss = torch.cat([d["loss"] for d in losses], dim=0) if losses else None   # [b, s] per micro-batch
+    return loss, grads, meta
 
 
 def tp_overlap_order_worker(rank, world):

@@ -86,3 +86,34 @@ def test_bench_ranks_gloo(n, layout, want, tmp_path):
         assert comm["tp"]["calls"] > 0 and comm["pp"]["calls"] > 0
         assert set(rec["phase_ms_by_pp_stage"]) == {"0", "1"}
         assert rec["phase_ms"]["tp_exchange_wait"] >= 0 and rec["phase_ms"]["pp_p2p_wait_and_bubble"] > 0
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("extra,want", [
+    (["--pp-schedule", "1f1b"], "1f1b"),
+    (["--pp-schedule", "zb"], "zb"),
+    (["--pp-schedule", "zbh1"], "zbh1"),
+    (["--vpp", "2"], "interleaved vpp2"),
+])
+def test_bench_pipeline_schedules_gloo(extra, want, tmp_path):
+    """tp2 pp2 at N = 4 under each pipeline schedule bench.py can select (the zero-bubble split
+    backward, the default zbh1, and the interleaved virtual pipeline): the JSON names it."""
+    rec = _run_bench(4, "tp", tmp_path, extra)
+    assert rec["config"]["pp_schedule"] == want and rec["config"]["parallelism"] == "tp2pp2dp1+sp"
+    assert rec["value"] > 0 and rec["final_loss"] > 0
+    _check_phases(rec)
+
+
+def test_bench_emulated_tp_rank(tmp_path):
+    """--emulate-tp: one process times a TP rank's compute (sharded shapes, SP, ring-chunk GEMMs)
+    with the collectives as local stand-ins (comm/loopback.py)."""
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", OMP_NUM_THREADS="1")
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--emulate-tp", "2", "--micro-batch-size", "2",
+           "--grad-accum", "2"] + TINY
+    r = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert rec["config"]["tp"] == 2 and "emulated" in rec["config"]["parallelism"]
+    assert rec["config"]["model"].endswith("vocab 256, seq 32)")   # padded to 128 x tp and rec["final_loss"] > 0

@@ -268,6 +268,33 @@ def test_ddp_gradient_accumulation_matches_single_process(world, tp, pp, nmb, ze
         _check_tp_grads(ref, grads, meta, tp)
 
 
+@pytest.mark.parametrize("schedule", ["1f1b", "zb", "zbh1"])
+@pytest.mark.parametrize("world,tp,pp,nmb,zero,sp,layers", [
+    (4, 2, 2, 4, False, True, 2),      # tp2 pp2 + SP, 4 micro-batches of 1
+    (4, 1, 4, 4, False, False, 4),     # pp4: three ranks with a cooldown, zbh1 holds up to 4 W
+    (8, 2, 2, 2, True, True, 2),       # the BASELINE layout tp2 pp2 dp2 + SP + ZeRO
+])
+def test_split_backward_schedules_match_single_rank(schedule, world, tp, pp, nmb, zero, sp, layers):
+    """The zero-bubble split backward (train/schedules.py: W GEMMs after the input gradient is
+    sent; zbh1 also holds the last r + 1 passes' W of rank r until its final B) gives the
+    single-process losses and reduced gradients, with the deferred wgrad queue active on CPU."""
+    over = {"num_layers": layers}
+    ref_loss, ref = W.gpt_reference(cfg_over=over)
+    outs = run_workers(W.gpt_layout_worker, world, tp, pp, nmb, zero, True, sp, schedule, over, timeout=600)
+    for _, grads, meta in outs:
+        _check_tp_grads(ref, grads, meta, tp)
+        ws = meta["wgrad_stats"]
+        assert ws["items"] > 0, ws                       # the weight gradients went through the queue
+        # zbh1: rank r (>= 1) held its last r + 1 passes' W and merged them with the sync pass's
+        held = schedule == "zbh1" and meta["pp_rank"] >= 1
+        assert (ws["max_segments"] >= 2) == held, (schedule, meta["pp_rank"], ws)
+    for loss, _, meta in outs:
+        if meta["pp_rank"] == pp - 1:
+            per = 4 // (world // (tp * pp))
+            want = ref_loss[meta["dp_rank"] * per:(meta["dp_rank"] + 1) * per]
+            torch.testing.assert_close(loss.reshape(want.shape), want, atol=2e-4, rtol=2e-4)
+
+
 @pytest.mark.parametrize("world", [2, 4])
 def test_sp_linear_rings_overlap_wgrad_with_comm(world):
     """Collective-matmul SP linears: numerics match plain linears, and in backward each ring's last
