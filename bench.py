@@ -98,6 +98,10 @@ def parse():
                    help="pipeline schedule (train/schedules.py): 1F1B, or its zero-bubble split backward")
     p.add_argument("--vpp", type=int, default=1,
                    help="virtual pipeline chunks per rank (interleaved 1F1B; uniform layer split)")
+    p.add_argument("--phase-probe", type=int, default=0,
+                   help="(pp = 1) after the timed steps, time this many micro-batches as F / B / W: forward, "
+                        "backward with the weight-gradient GEMMs held, then those GEMMs "
+                        "(train/pipeline_sim.py inputs); reported as fbw_ms")
     p.add_argument("--hidden-dropout", type=float, default=0.1)
     p.add_argument("--attention-dropout", type=float, default=0.1)  # Megatron default (reference run)
     p.add_argument("--zero", type=int, default=1, help="ZeRO-1/2 distributed optimizer when DP > 1")
@@ -348,6 +352,7 @@ def main():
     if explain is not None and dist.is_initialized() and world > 1:
         phases_all = [None] * world
         dist.all_gather_object(phases_all, (st.pp_rank, explain["phase_ms"]))
+    fbw = probe_fbw(a, ddp, forward_step, it, dev) if (a.phase_probe and st.pp == 1) else None
     from smdt_amd.comm import xgmi
     relay.check_all()            # (after the timed region) no TP-pair exchange timed out
     global_batch = mbs * a.grad_accum * st.dp
@@ -397,6 +402,8 @@ def main():
         comm = {**relay.TUNED, **xgmi.TUNED}
         if comm:  # run-time RCCL-vs-kernel decisions on this node (comm/relay.py, comm/xgmi.py)
             rec["comm_tuning"] = comm
+        if fbw is not None:
+            rec["fbw_ms"] = fbw
         if explain is not None:
             rec["phase_ms"] = _mean_phases([p for _, p in phases_all]) if phases_all else explain["phase_ms"]
             if phases_all and st.pp > 1:
@@ -406,6 +413,51 @@ def main():
         print(json.dumps(rec), flush=True)
     if dist.is_initialized():
         dist.destroy_process_group()
+
+
+def probe_fbw(a, ddp, forward_step, it, dev):
+    """Untimed diagnostics after the timed steps: per micro-batch, the forward (F), the backward
+    with the deferred weight-gradient queue held (B: the input-gradient chain a pipeline stage must
+    finish before it sends) and the flush of that queue (W), each bracketed by device events
+    (median over ``a.phase_probe`` micro-batches). Gradients accumulate into the buffers and are
+    zeroed at the end; nothing here is part of the measured step."""
+    from smdt_amd.parallel.tensor_parallel import DEFERRED_WGRAD
+    cuda = dev.type == "cuda"
+
+    def stamp():
+        if cuda:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            return e
+        return time.perf_counter()
+
+    def ms(t0, t1):
+        return t0.elapsed_time(t1) if cuda else 1e3 * (t1 - t0)
+    rows = []
+    ddp.set_sync_enabled(False)
+    for _ in range(a.phase_probe):
+        t0 = stamp()
+        out, loss_func = forward_step(it, ddp)
+        loss, _ = loss_func(out)
+        t1 = stamp()
+        DEFERRED_WGRAD.defer = True
+        try:
+            loss.backward()
+        finally:
+            DEFERRED_WGRAD.defer = False
+        t2 = stamp()
+        DEFERRED_WGRAD.flush()
+        t3 = stamp()
+        if cuda:
+            torch.cuda.synchronize()
+        rows.append((ms(t0, t1), ms(t1, t2), ms(t2, t3)))
+    ddp.set_sync_enabled(True)
+    ddp.zero_grad_buffer()
+
+    def med(i):
+        v = sorted(r[i] for r in rows)
+        return round(v[len(v) // 2], 3)
+    return {"F": med(0), "B": med(1), "W": med(2), "micro_batches": len(rows)}
 
 
 def _mean_phases(ps_):

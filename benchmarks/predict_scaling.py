@@ -2,29 +2,35 @@
 """Predicted bench.py step time at N = 2 / 4 / 8 GPUs from ONE MI355X plus the xGMI link budget.
 
 The pool this repo is developed on has one GPU per box, so the multi-GPU points of the headline
-(BASELINE.json: tokens/s of GPT-2 345M at 1/2/4/8 GPUs) are predicted before the driver measures
-them. Two inputs:
+(BASELINE.json: tokens/s of GPT-2 345M at 1/2/4/8 GPUs) and the GPT-3 6.7B TP4 PP2 + SP layout
+(BASELINE config #5) are predicted before the driver measures them. Inputs:
 
-(a) per-rank compute, MEASURED on one GPU by running bench.py on the shape one rank of each layout
-    executes:
-      * DP-N (N = 2 / 4, the default): every rank runs the whole model on its 64 sequences — the
-        1-GPU step itself;
-      * tp2 pp2 dp2 (N = 8, BASELINE): a rank holds 12 of the 24 layers with half the heads (8 x 64)
-        and half the FFN (2048), and the last stage half of the (tied) LM head (vocab 50304 / 2);
-        the replica's 4 GPUs process 4 x 64 = 256 sequences per step, as 8 micro-batches of 32.
-        Emulated as a 12-layer model of that width on 256 sequences (micro-batch 32, 8
-        micro-batches). Sequence parallelism would halve LayerNorm / dropout / residual work and
-        the ring-chunked GEMMs run at M = 8192 instead of 16384: both are noted, not modelled;
-      * tp2 (N = 2, the old default, ``--layout tp``): 24 layers at half width, 128 sequences.
-(b) the link budget: ``LINK_GBPS`` per direction per xGMI link (MI355X: 7 links per GPU, every
-    GPU pair directly connected), which of the step's bytes can hide behind compute (bucketed
-    reduce-scatter during backward, parameter all-gather during the next forward, ring TP exchanges
-    beside their chunk GEMMs, async pipeline p2p) and which cannot (the last gradient bucket, the
-    tied-embedding all-reduce, the 1F1B bubble (pp - 1) / m, a link-bound TP exchange).
+(a) per-rank compute, MEASURED on one GPU by running bench.py on exactly what one rank executes:
+      * DP-N (N = 2 / 4, the default): the 1-GPU step itself (every rank runs the whole model);
+      * tp2 pp2 dp2 + SP (N = 8, BASELINE): ``bench.py --emulate-tp 2`` — ONE process as TP rank 0
+        (parallel/state.initialize_emulated_tensor_parallel, comm/loopback.py): the sharded heads /
+        FFN / vocab, sequence-parallel LayerNorm / dropout on s/2 rows, the ring collective-matmul's
+        per-chunk GEMMs at their real M = s/2 x mbs, the vocab-parallel head + CE; every collective
+        is a local stand-in with the receiving side's memory traffic. One run
+        per pipeline stage at bench.py's 13 | 11 split (first stage without the head, last stage
+        with it), plus the even 12 | 12 split the interleaved schedule needs;
+      * GPT-3 6.7B tp4 pp2 + SP: the same with ``--emulate-tp 4``, 16 layers per stage, seq 2048,
+        8 micro-batches of 4 (32 sequences per replica per step).
+    Each emulated run also reports ``fbw_ms``: per micro-batch forward (F), input-gradient backward
+    with the weight-gradient GEMMs held (B) and those GEMMs (W).
+(b) the pipeline bubble of each schedule from train/pipeline_sim.simulate(F, B, W per stage, the
+    p2p hop of one [s/tp, mbs, h] activation over one link) — 1F1B, the zero-bubble split zb and
+    zbh1 (the bench default) — and the interleaved vpp = 2 schedule as 1F1B's bubble / 2 on the
+    even split;
+(c) the link budget: ``LINK_GBPS`` per direction per xGMI link (7 links per GPU, every pair directly
+    connected): which of the step's bytes hide behind compute (bucketed reduce-scatter during
+    backward, parameter all-gather during the next forward, TP exchanges beside their chunk GEMMs)
+    and which cannot (the last gradient bucket, the tied-embedding all-reduce, a link-bound TP
+    exchange).
 
-Usage (GPU box): ``python benchmarks/predict_scaling.py --out profiles/r3_predict`` runs the three
-measurements and writes ``predicted.json`` + ``predicted.md``. ``--from-json`` recomputes the
-table from saved measurements.
+Usage (GPU box): ``python benchmarks/predict_scaling.py --out profiles/r4_predict`` runs the
+measurements and writes ``predicted.json`` + ``predicted.md``; ``--from-json`` recomputes the
+tables from saved measurements (CPU).
 """
 from __future__ import annotations
 
@@ -35,28 +41,37 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from smdt_amd.train.pipeline_sim import simulate  # noqa: E402
+
 LINK_GBPS = 64.0            # per direction per xGMI link, conservative end of 64-77 (docs/XGMI.md)
 H, L, S, V = 1024, 24, 1024, 50304
 PARAMS = 354.9e6            # GPT-2 345M with the padded vocab (tied embedding)
 
-_TP2 = ["--num-attention-heads", "8", "--kv-channels", "64", "--ffn-hidden-size", "2048", "--vocab-size", str(V // 2)]
-_MB16 = ["--seqs-per-gpu", "256", "--micro-batch-size", "32", "--grad-accum", "8"]   # bench.py's N = 8 split
+_N8 = ["--emulate-tp", "2", "--micro-batch-size", "32", "--grad-accum", "8", "--phase-probe", "8"]
+_G3 = ["--emulate-tp", "4", "--hidden-size", "4096", "--num-attention-heads", "32", "--seq-length", "2048",
+       "--micro-batch-size", "4", "--grad-accum", "8", "--phase-probe", "8", "--tunableop", "0"]
 RUNS = {
     "n1_dp": [],
-    # even split: 12 + 12 layers, the last stage also runs the LM head (the heavier stage)
-    "tp2pp2_rank": ["--num-layers", "12"] + _TP2 + _MB16,
-    # bench.py's balanced split (balanced_last_stage_layers): 13 layers | 11 layers + LM head
-    "tp2pp2_stage0_bal": ["--num-layers", "13", "--emulate-first-stage"] + _TP2 + _MB16,
-    "tp2pp2_stage1_bal": ["--num-layers", "11"] + _TP2 + _MB16,
-    "tp2_rank": ["--num-attention-heads", "8", "--kv-channels", "64", "--ffn-hidden-size", "2048",
-                 "--vocab-size", str(V // 2), "--seqs-per-gpu", "128", "--micro-batch-size", "64",
-                 "--grad-accum", "2"],
+    # bench.py's balanced split: 13 layers | 11 layers + LM head
+    "tp2pp2_stage0": ["--num-layers", "13", "--emulate-first-stage"] + _N8,
+    "tp2pp2_stage1": ["--num-layers", "11"] + _N8,
+    # the even split the interleaved schedule is limited to: 12 | 12 + head (the heavier stage)
+    "tp2pp2_stage1_even": ["--num-layers", "12"] + _N8,
+    "gpt3_tp4_stage0": ["--num-layers", "16", "--emulate-first-stage"] + _G3,
+    "gpt3_tp4_stage1": ["--num-layers", "16"] + _G3,
+    # the whole 6.7B model on ONE GPU (288 GB hold weights, fp32 masters, Adam state, activations)
+    "gpt3_n1": ["--hidden-size", "4096", "--num-attention-heads", "32", "--seq-length", "2048", "--num-layers", "32",
+                "--micro-batch-size", "4", "--grad-accum", "1", "--tunableop", "0"],
 }
+SCHEDS = ("1f1b", "zb", "zbh1")
 
 
-def measure(steps: int, warmup: int, logdir: str) -> dict:
+def measure(steps: int, warmup: int, logdir: str, only=None) -> dict:
     out = {}
     for name, extra in RUNS.items():
+        if only and name not in only:
+            continue
         cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", str(steps), "--warmup", str(warmup),
                "--comm-stats", "1"] + extra
         r = subprocess.run(cmd, capture_output=True, text=True, timeout=900, cwd=ROOT)
@@ -65,9 +80,9 @@ def measure(steps: int, warmup: int, logdir: str) -> dict:
         if r.returncode != 0:
             raise SystemExit(f"{name} failed:\n{r.stderr[-2000:]}")
         rec = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
-        out[name] = {"ms_per_step": rec["ms_per_step"], "phase_ms": rec.get("phase_ms"),
+        out[name] = {"ms_per_step": rec["ms_per_step"], "phase_ms": rec.get("phase_ms"), "fbw_ms": rec.get("fbw_ms"),
                      "tokens_per_step": rec["config"]["global_batch"] * rec["config"]["seq_len"], "args": extra}
-        print(f"[predict] {name}: {rec['ms_per_step']:.1f} ms", flush=True)
+        print(f"[predict] {name}: {rec['ms_per_step']:.1f} ms  fbw {rec.get('fbw_ms')}", flush=True)
     return out
 
 
@@ -75,68 +90,107 @@ def link_ms(nbytes: float, links: float = 1.0) -> float:
     return nbytes / (LINK_GBPS * 1e9 * links) * 1e3
 
 
+def _fbw(m, name):
+    d = m[name]["fbw_ms"]
+    return d["F"], d["B"], d["W"]
+
+
+def pipeline_rows(m, st0, st1, mb, pp, act_bytes, exposed, tok, label, even=None):
+    """One row per schedule for a pp = 2 layout from the two measured stages."""
+    rows = []
+    t = [m[st0]["ms_per_step"], m[st1]["ms_per_step"]]
+    f0, b0, w0 = _fbw(m, st0)
+    f1, b1, w1 = _fbw(m, st1)
+    hop = link_ms(act_bytes)
+    for sched in SCHEDS:
+        sim = simulate(sched, pp, mb, [f0, f1], [b0, b1], [w0, w1], p2p=hop)
+        bubble = sim["bubble"]
+        pred = max(t) + bubble + exposed
+        rows.append({"layout": f"{label}, {sched}", "compute_ms": round(max(t), 1),
+                     "stage_ms": [round(x, 1) for x in t], "bubble_ms": round(bubble, 1),
+                     "exposed_comm_ms": round(exposed, 2), "predicted_ms": round(pred, 1),
+                     "tokens_per_step": tok,
+                     "note": f"F/B/W per micro-batch: stage 0 {f0:.2f}/{b0:.2f}/{w0:.2f}, stage 1 {f1:.2f}/{b1:.2f}/{w1:.2f} ms; "
+                             f"p2p hop {hop:.2f} ms"})
+    if even is not None:
+        te = [m[st0]["ms_per_step"] * 12.0 / 13.0, m[even]["ms_per_step"]]   # 12 | 12 + head
+        fe, be, we = _fbw(m, even)
+        sim = simulate("1f1b", pp, mb, [f0 * 12 / 13, fe], [b0 * 12 / 13, be], [w0 * 12 / 13, we], p2p=hop)
+        bubble = sim["bubble"] / 2.0
+        pred = max(te) + bubble + exposed
+        rows.append({"layout": f"{label}, interleaved vpp2 (even 12|12 split)", "compute_ms": round(max(te), 1),
+                     "stage_ms": [round(x, 1) for x in te], "bubble_ms": round(bubble, 1),
+                     "exposed_comm_ms": round(exposed, 2), "predicted_ms": round(pred, 1), "tokens_per_step": tok,
+                     "note": "1F1B bubble / vpp; uniform layer split only (the LM head stage carries 12 layers)"})
+    return rows
+
+
 def predict(m: dict) -> list:
     rows = []
     t1 = m["n1_dp"]["ms_per_step"]
     tok1 = m["n1_dp"]["tokens_per_step"]
-    rows.append({"N": 1, "layout": "tp1pp1dp1", "compute_ms": t1, "exposed_comm_ms": 0.0, "bubble_ms": 0.0,
-                 "predicted_ms": t1, "tokens_per_step": tok1, "note": "measured"})
-    # DP-N + ZeRO-1: fp32 gradient reduce-scatter + bf16 parameter all-gather, bucketed (16 MB).
+    rows.append({"N": 1, "model": "gpt2-345m", "layout": "tp1pp1dp1", "compute_ms": t1, "exposed_comm_ms": 0.0,
+                 "bubble_ms": 0.0, "predicted_ms": t1, "tokens_per_step": tok1, "note": "measured"})
+    # DP-N + ZeRO-1: fp32 gradient reduce-scatter + bf16 parameter all-gather, bucketed (16 MB)
     for n in (2, 4):
         links = n - 1                       # a direct reduce-scatter / all-gather uses every peer link
         rs = 4 * PARAMS * (n - 1) / n       # bytes each rank sends
         ag = 2 * PARAMS * (n - 1) / n
         hidden = link_ms(rs, links) + link_ms(ag, links)
         exposed = link_ms(16e6 * (n - 1) / n, links) + link_ms(2 * 16e6 / 4 * (n - 1) / n, links) + 0.3
-        rows.append({"N": n, "layout": f"tp1pp1dp{n}+zero1", "compute_ms": t1, "exposed_comm_ms": round(exposed, 2),
-                     "bubble_ms": 0.0, "predicted_ms": round(t1 + exposed, 1), "tokens_per_step": tok1 * n,
+        rows.append({"N": n, "model": "gpt2-345m", "layout": f"tp1pp1dp{n}+zero1", "compute_ms": t1,
+                     "exposed_comm_ms": round(exposed, 2), "bubble_ms": 0.0, "predicted_ms": round(t1 + exposed, 1),
+                     "tokens_per_step": tok1 * n,
                      "note": f"{hidden:.1f} ms of RS+AG per step overlapped with backward / next forward"})
-    # tp2 pp2 dp2 + SP (BASELINE at N = 8), with bench.py's balanced 13 | 11 split when measured.
-    tr_even = m["tp2pp2_rank"]["ms_per_step"]
-    bal = "tp2pp2_stage0_bal" in m and "tp2pp2_stage1_bal" in m
-    tr = max(m["tp2pp2_stage0_bal"]["ms_per_step"], m["tp2pp2_stage1_bal"]["ms_per_step"]) if bal else tr_even
-    mb, pp = 8, 2                                           # micro-batches per step, stages
-    bubble = tr * (pp - 1) / mb
-    grads = 4 * PARAMS / 4                                  # fp32 grads of a rank's quarter
-    dp_tail = link_ms(16e6 / 2) + link_ms(8e6 / 2)          # last RS bucket + first AG bucket, dp2 = 1 link
-    embd = link_ms(4 * (V // 2) * H)                        # tied-embedding grad all-reduce, first <-> last stage
-    tp_chunk = S // 2 * 32 * H * 2                          # [s/2, mbs, h] bf16 = 32 MB per ring step
-    relay_links = 4.0                                       # relay on 8 GPUs: ~4x one link (docs/XGMI.md)
-    tp_per_ex = link_ms(tp_chunk, relay_links)
-    tp_total = tp_per_ex * 8 * 12 * mb                      # 8 exchanges / layer / micro-batch, 12 layers
-    exposed = dp_tail + embd + 0.5
-    if bal:
-        rows.append({"N": 8, "layout": "tp2pp2dp2+sp+zero1, even 12|12 split", "compute_ms": tr_even,
-                     "exposed_comm_ms": round(exposed, 2), "bubble_ms": round(tr_even * (pp - 1) / mb, 1),
-                     "predicted_ms": round(tr_even * (1 + (pp - 1) / mb) + exposed, 1), "tokens_per_step": tok1 * 8,
-                     "note": "the last stage carries 12 layers + the LM head (2x the per-GPU head work of N = 1)"})
-    rows.append({"N": 8, "layout": "tp2pp2dp2+sp+zero1" + (", split 13|11" if bal else ""), "compute_ms": tr,
-                 "exposed_comm_ms": round(exposed, 2),
-                 "bubble_ms": round(bubble, 1), "predicted_ms": round(tr + bubble + exposed, 1),
-                 "tokens_per_step": tok1 * 8,
-                 "note": (f"TP: {tp_total:.0f} ms of relayed exchanges ({tp_per_ex * 1e3:.0f} us each) beside "
-                          f"chunk GEMMs; DP: {link_ms(grads / 2) + link_ms(grads / 4):.1f} ms RS+AG overlapped; "
-                          f"SP halves LN/dropout work (not modelled)")})
-    # the old N = 2 default, for the record: tp2 over ONE link
-    t2 = m["tp2_rank"]["ms_per_step"]
-    ex = S // 2 * 64 * H * 2                                # [s/2, 64, h] bf16 = 64 MB
-    tp_total2 = link_ms(ex) * 8 * 24 * 2                    # 24 layers, 2 micro-batches of 64
-    rows.append({"N": 2, "layout": "tp2+sp (--layout tp)", "compute_ms": t2,
-                 "exposed_comm_ms": round(max(0.0, tp_total2 - t2), 1), "bubble_ms": 0.0,
-                 "predicted_ms": round(max(t2, tp_total2), 1), "tokens_per_step": tok1 * 2,
-                 "note": f"{tp_total2:.0f} ms of exchanges over the pair's single link: link-bound"})
+    # N = 8: tp2 pp2 dp2 + SP + ZeRO-1 (BASELINE config #3)
+    if "tp2pp2_stage0" in m and "tp2pp2_stage1" in m:
+        dp_tail = link_ms(16e6 / 2) + link_ms(8e6 / 2)          # last RS bucket + first AG bucket, dp2 = 1 link
+        embd = link_ms(4 * (V // 2) * H)                        # tied-embedding fp32 grad all-reduce, 1 link
+        act = (S // 2) * 32 * H * 2                             # p2p activation [s/2, 32, h] bf16
+        for r in pipeline_rows(m, "tp2pp2_stage0", "tp2pp2_stage1", 8, 2, act, dp_tail + embd + 0.5, tok1 * 8,
+                               "tp2pp2dp2+sp+zero1 13|11", even="tp2pp2_stage1_even" if "tp2pp2_stage1_even" in m else None):
+            rows.append({"N": 8, "model": "gpt2-345m", **r})
     for r in rows:
         r["predicted_tokens_per_s"] = round(r["tokens_per_step"] / r["predicted_ms"] * 1e3)
         r["efficiency_vs_n1"] = round(r["predicted_tokens_per_s"] / (rows[0]["predicted_tokens_per_s"] * r["N"]), 3)
     return rows
 
 
+def predict_gpt3(m: dict) -> list:
+    """GPT-3 6.7B, tp4 pp2 + SP on 8 GPUs (BASELINE config #5): per-rank compute from the emulated
+    stages; the sequence-parallel exchanges per rank and step (10 per layer and micro-batch, each
+    3/4 of a [2048, 4, 4096] bf16 activation) over ONE link per direction (the ring) or over the
+    three links of the TP group (a direct exchange); the part of it that the rank's GEMMs (~60 % of
+    its compute, the TP collectives' overlap partners) cannot hide is exposed."""
+    if not ("gpt3_tp4_stage0" in m and "gpt3_tp4_stage1" in m):
+        return []
+    rows = []
+    sl, mb, h, layers = 2048, 4, 4096, 16
+    xfer_bytes = layers * 8 * 10 * 0.75 * sl * mb * h * 2
+    tok = 32 * sl                                           # tp4 x pp2 = 8 GPUs: ONE replica, 32 sequences
+    act = (sl // 4) * mb * h * 2
+    base = pipeline_rows(m, "gpt3_tp4_stage0", "gpt3_tp4_stage1", 8, 2, act, 0.0, tok, "tp4pp2dp1+sp")
+    zbh1 = [r for r in base if r["layout"].endswith("zbh1")][0]
+    comp = zbh1["compute_ms"]
+    for links, name in ((1, "ring, one link per direction"), (3, "direct, the TP group's 3 links")):
+        t_x = link_ms(xfer_bytes, links)
+        exposed = max(0.0, t_x - 0.6 * comp)
+        pred = zbh1["predicted_ms"] + exposed
+        rows.append({"N": 8, "model": "gpt3-6.7b", "layout": f"tp4pp2+sp, zbh1, TP exchange {name}",
+                     "compute_ms": comp, "stage_ms": zbh1["stage_ms"], "bubble_ms": zbh1["bubble_ms"],
+                     "exposed_comm_ms": round(exposed, 1), "predicted_ms": round(pred, 1), "tokens_per_step": tok,
+                     "note": f"{xfer_bytes / 1e9:.1f} GB of SP exchanges per rank per step = {t_x:.0f} ms on {links} link(s)"})
+    return rows
+
+
 def to_md(rows: list) -> str:
-    lines = ["| N | layout | per-rank compute ms | 1F1B bubble ms | exposed comm ms | predicted ms/step | "
-             "predicted tokens/s | efficiency vs N=1 | notes |", "|---|---|---|---|---|---|---|---|---|"]
+    lines = ["| N | model | layout | per-rank compute ms (stages) | bubble ms | exposed comm ms | predicted ms/step | "
+             "predicted tokens/s | efficiency vs N=1 | notes |", "|---|---|---|---|---|---|---|---|---|---|"]
     for r in rows:
-        lines.append(f"| {r['N']} | {r['layout']} | {r['compute_ms']:.1f} | {r['bubble_ms']} | {r['exposed_comm_ms']} | "
-                     f"{r['predicted_ms']} | {r['predicted_tokens_per_s'] / 1e3:.1f} k | {r['efficiency_vs_n1']:.2f} | "
+        stages = f" ({' / '.join(str(x) for x in r['stage_ms'])})" if r.get("stage_ms") else ""
+        eff = f"{r['efficiency_vs_n1']:.2f}" if "efficiency_vs_n1" in r else "-"
+        lines.append(f"| {r['N']} | {r['model']} | {r['layout']} | {r['compute_ms']:.1f}{stages} | {r['bubble_ms']} | "
+                     f"{r['exposed_comm_ms']} | {r['predicted_ms']} | {r['predicted_tokens_per_s'] / 1e3:.1f} k | {eff} | "
                      f"{r['note']} |")
     return "\n".join(lines) + "\n"
 
@@ -146,6 +200,7 @@ def main():
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "predict"))
     ap.add_argument("--steps", type=int, default=6)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--only", nargs="*", default=None, help="measure only these runs")
     ap.add_argument("--from-json", default=None)
     a = ap.parse_args()
     os.makedirs(a.out, exist_ok=True)
@@ -153,11 +208,17 @@ def main():
         with open(a.from_json) as f:
             m = json.load(f)["measured"]
     else:
-        m = measure(a.steps, a.warmup, a.out)
+        m = measure(a.steps, a.warmup, a.out, a.only)
     rows = predict(m)
+    g3 = predict_gpt3(m)
+    for r in g3:
+        r["predicted_tokens_per_s"] = round(r["tokens_per_step"] / r["predicted_ms"] * 1e3)
+        if "gpt3_n1" in m:   # vs 8 GPUs each running the whole model data-parallel at N = 1's rate
+            n1 = m["gpt3_n1"]["tokens_per_step"] / m["gpt3_n1"]["ms_per_step"] * 1e3
+            r["efficiency_vs_n1"] = round(r["predicted_tokens_per_s"] / (8 * n1), 3)
     with open(os.path.join(a.out, "predicted.json"), "w") as f:
-        json.dump({"measured": m, "link_GBps_per_direction": LINK_GBPS, "rows": rows}, f, indent=1)
-    md = to_md(rows)
+        json.dump({"measured": m, "link_GBps_per_direction": LINK_GBPS, "rows": rows, "gpt3_rows": g3}, f, indent=1)
+    md = to_md(rows) + ("\n" + to_md(g3) if g3 else "")
     with open(os.path.join(a.out, "predicted.md"), "w") as f:
         f.write(md)
     print(md)
