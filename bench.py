@@ -234,6 +234,8 @@ def main():
     # SMDT_BENCH_BACKEND=gloo: rehearsal of the N > 1 code paths with every rank on ONE GPU (RCCL
     # refuses two ranks on one device); the driver's runs use RCCL
     rank, local, world, backend = init_distributed(os.environ.get("SMDT_BENCH_BACKEND", "nccl"))
+    from smdt_amd.utils.debug import collective_log_from_env
+    collective_log_from_env()      # SMDT_COLLECTIVE_LOG=<prefix>: per-rank collective issue order
     if world != a.gpus and rank == 0:
         print(f"[bench] note: --gpus {a.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
     n = world

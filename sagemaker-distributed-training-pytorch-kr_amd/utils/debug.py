@@ -42,8 +42,11 @@ def enable_async_error_handling(blocking_wait: bool = False):
 class CollectiveTracer:
     """Wraps ``torch.distributed`` collectives to fingerprint the per-rank call sequence."""
 
-    def __init__(self, keep: int = 64):
+    def __init__(self, keep: int = 64, log_path: Optional[str] = None):
         self.records: List[Tuple[str, tuple, str, int]] = []
+        # every call as issued, one line each, flushed at once (a hang leaves the per-rank
+        # sequences on disk to compare: SMDT_COLLECTIVE_LOG=<prefix> writes <prefix>.rank<R>)
+        self._log = open(log_path, "w", buffering=1) if log_path else None
         self.digest = hashlib.sha1()
         self.count = 0
         self.keep = keep
@@ -63,6 +66,8 @@ class CollectiveTracer:
             rec = (name, tuple(t.shape) if t is not None else (), str(t.dtype) if t is not None else "", gsz)
             tracer.digest.update(repr(rec).encode())
             tracer.count += 1
+            if tracer._log is not None:
+                tracer._log.write(f"{tracer.count} {time.time():.6f} {rec} async={kwargs.get('async_op', False)}\n")
             tracer.records.append(rec)
             if len(tracer.records) > tracer.keep:
                 tracer.records.pop(0)
@@ -108,6 +113,18 @@ class CollectiveTracer:
 
 
 _TRACER: Optional[CollectiveTracer] = None
+
+
+def collective_log_from_env():
+    """SMDT_COLLECTIVE_LOG=<prefix>: trace every collective of this rank into <prefix>.rank<R>
+    (installed once; returns the tracer or None)."""
+    global _TRACER
+    pre = os.environ.get("SMDT_COLLECTIVE_LOG")
+    if not pre or _TRACER is not None:
+        return _TRACER
+    r = dist.get_rank() if dist.is_initialized() else 0
+    _TRACER = CollectiveTracer(log_path=f"{pre}.rank{r}").install()
+    return _TRACER
 
 
 def collective_check_from_env(step: int, group=None):
