@@ -321,9 +321,13 @@ bool wgrad_mfma(Tensor main_grad, Tensor dy, Tensor x, int64_t max_splits) {
 
 // Grouped form: main_grads[i] += dys[i]^T . xs[i] for every i in ONE launch per 32 problems.
 // Returns false (and does nothing) when any problem is unsupported. The targets must not overlap.
-bool wgrad_grouped(std::vector<Tensor> main_grads, std::vector<Tensor> dys, std::vector<Tensor> xs) {
+// ``biases`` (optional, one per problem; an empty tensor = none): fp32 [N] targets that receive
+// the column sums of dy — the bias gradient — from the same launch.
+bool wgrad_grouped(std::vector<Tensor> main_grads, std::vector<Tensor> dys, std::vector<Tensor> xs,
+                   std::vector<Tensor> biases) {
   const size_t n = main_grads.size();
   TORCH_CHECK(dys.size() == n && xs.size() == n, "wgrad_grouped: list lengths differ");
+  TORCH_CHECK(biases.empty() || biases.size() == n, "wgrad_grouped: biases list length");
   std::vector<SmdtWgradProblem> probs(n);
   for (size_t i = 0; i < n; ++i) {
     const Tensor &mg = main_grads[i], &dy = dys[i], &x = xs[i];
@@ -335,7 +339,15 @@ bool wgrad_grouped(std::vector<Tensor> main_grads, std::vector<Tensor> dys, std:
     if (dy.get_device() != mg.get_device() || x.get_device() != mg.get_device()) return false;
     const int64_t M = dy.size(0), N = dy.size(1), K = x.size(1);
     if (x.size(0) != M || mg.numel() != N * K || !smdt_wgrad_supported(M, N, K)) return false;
-    probs[i] = SmdtWgradProblem{dy.data_ptr(), x.data_ptr(), mg.data_ptr<float>(), M, N, K};
+    float* bg = nullptr;
+    if (!biases.empty() && biases[i].numel() > 0) {
+      const Tensor& bt = biases[i];
+      if (!bt.is_cuda() || bt.scalar_type() != at::kFloat || !bt.is_contiguous() || bt.numel() != N ||
+          bt.get_device() != mg.get_device())
+        return false;
+      bg = bt.data_ptr<float>();
+    }
+    probs[i] = SmdtWgradProblem{dy.data_ptr(), x.data_ptr(), mg.data_ptr<float>(), M, N, K, bg};
   }
   if (n == 0) return true;
   check(smdt_wgrad_grouped_t(dcode(dys[0]), probs.data(), (int)n, cur_stream()), "wgrad_grouped");
@@ -664,7 +676,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("transpose2d", &transpose2d);
   m.def("bias_grad", &bias_grad);
   m.def("wgrad_mfma", &wgrad_mfma, arg("main_grad"), arg("dy"), arg("x"), arg("max_splits") = 0);
-  m.def("wgrad_grouped", &wgrad_grouped, arg("main_grads"), arg("dys"), arg("xs"));
+  m.def("wgrad_grouped", &wgrad_grouped, arg("main_grads"), arg("dys"), arg("xs"),
+        arg("biases") = std::vector<Tensor>{});
   m.def("ce_stats", &ce_stats);
   m.def("ce_bwd", &ce_bwd);
   namespace py = pybind11;

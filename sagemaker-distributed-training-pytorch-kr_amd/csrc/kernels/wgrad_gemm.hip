@@ -90,10 +90,26 @@ struct Glds {
 // tile measured +1.7 % on the grouped microbenchmark and neutral-to-slower in the training step,
 // profiles/r3_wgrad16/: the kernel is bound by its LDS-DMA operand stream, not by the MFMA clock;
 // it was removed.)
+// Sum of the 8 16-bit values of an operand fragment, in fp32.
+template <class V>
+__device__ __forceinline__ float sum8(V x) {
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s += (float)x[j];
+  return s;
+}
+
+// ``bias`` (optional, k0 == 0 tiles only): bias[n0 + r] += sum over this tile's m range of
+// A[m, n0 + r] — the bias gradient of the linear whose weight gradient this is, taken from the A
+// (dY) fragments the MFMAs read anyway. Wave (wn, wk) sums its A fragment i == wk (all four wk
+// waves of a wn read the same A fragments), so every column of the tile is summed by exactly one
+// lane pair: ~2 VALU per MFMA, no extra pass over dY (this replaces the
+// col_sum_rows + col_partials_reduce kernels).
 template <bool ATOMIC, int VAR, class E>
 __device__ __forceinline__ void tile_gemm(const E* __restrict__ A, const E* __restrict__ B,
                                           float* __restrict__ C, int N, int K, int n0, int k0, int64_t mstart,
-                                          int nst, char* L0, char* L1, char* L2, char* L3) {
+                                          int nst, char* L0, char* L1, char* L2, char* L3,
+                                          float* __restrict__ bias = nullptr) {
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), h = lane >> 5;
   const int wn = wave >> 2, wk = wave & 3;  // wave tile: n rows [128 wn, +128), k cols [64 wk, +64)
   using F = Frag<BT, E>;
@@ -114,6 +130,8 @@ __device__ __forceinline__ void tile_gemm(const E* __restrict__ A, const E* __re
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = zero16();
+  const bool do_bias = bias != nullptr && k0 == 0;   // wave-uniform
+  float cs = 0.f;                                     // column sum of A[., n0 + 128 wn + 32 wk + lane & 31]
 
   Glds ga, gb;
   ga.init(wave, lane, N, n0, N);
@@ -159,6 +177,7 @@ __device__ __forceinline__ void tile_gemm(const E* __restrict__ A, const E* __re
         else a = F::trf_at(at, 0, ks, oa[i][0], oa[i][1]);
         acc[i][0] = mfma(a, b0, acc[i][0]);
         acc[i][1] = mfma(a, b1, acc[i][1]);
+        if (do_bias && i == wk) cs += sum8(a);
       }
     }
     // Stages s+2 .. s+kNBuf-1 stay in flight; stage s+1 must have landed.
@@ -177,6 +196,16 @@ __device__ __forceinline__ void tile_gemm(const E* __restrict__ A, const E* __re
   if (s + 1 < nst) stage(s + 1, L1, L0);
   if (s + 2 < nst) stage(s + 2, L2, L1);
   wait_vm<0>();  // drain the trailing re-reads before the workgroup's LDS is released
+
+  if (do_bias) {
+    // lanes l and l ^ 32 summed the two 8-row halves of each 16-row k-step of one column
+    cs = __shfl_xor(cs, 32, 64) + cs;
+    const int n = n0 + 128 * wn + 32 * wk + (lane & 31);
+    if (h == 0 && n < N) {
+      if constexpr (ATOMIC) unsafeAtomicAdd(bias + n, cs);
+      else bias[n] += cs;
+    }
+  }
 
   // Epilogue: register r of acc[i][j] is C[n0 + 128 wn + 32 i + acc_row(r, h)][k0 + 64 wk + 32 j + lane&31];
   // the 32 lanes of a half write 32 consecutive fp32 (128 B) per register. Full 32-row blocks
@@ -256,6 +285,7 @@ struct Problem {
   const void* A;
   const void* B;
   float* C;
+  float* bias;     // column sums of A (bias gradient) or null
   int M, N, K, ntn, ntk, gn, tile0;
 };
 constexpr int kMaxGroup = 32;
@@ -296,13 +326,13 @@ __global__ __launch_bounds__(kThreads, 1) void wgrad_grouped_kernel(const Group 
   const int stages = P.M / BM;
   if (piece < 0) {
     tile_gemm<false, 0, E>((const E*)P.A, (const E*)P.B, P.C, P.N, P.K, tn * BT, tk * BT, 0, stages, L0, L1,
-                               L2, L3);
+                           L2, L3, P.bias);
   } else {
     const int s0 = piece * g.mps;
     const int nst = min(stages, s0 + g.mps) - s0;
     if (nst <= 0) return;  // a smaller-M problem in the tail: nothing left for this piece (whole block exits)
     tile_gemm<true, 0, E>((const E*)P.A, (const E*)P.B, P.C, P.N, P.K, tn * BT, tk * BT, (int64_t)s0 * BM,
-                              nst, L0, L1, L2, L3);
+                          nst, L0, L1, L2, L3, P.bias);
   }
 }
 
@@ -392,6 +422,7 @@ extern "C" hipError_t smdt_wgrad_grouped_t(int dtype, const SmdtWgradProblem* pr
       p.A = q.dy;
       p.B = q.x;
       p.C = q.main_grad;
+      p.bias = q.bias_grad;
       p.M = (int)q.M;
       p.N = (int)q.N;
       p.K = (int)q.K;

@@ -309,7 +309,8 @@ class ParallelMLP(nn.Module):
                                            params_dtype=cfg.params_dtype, device=device,
                                            sequence_parallel=cfg.sequence_parallel, skip_bias_add=True,
                                            chunks=[f, f] if self.gated else None,
-                                           async_tensor_model_parallel_allreduce=cfg.async_tensor_model_parallel_allreduce)
+                                           async_tensor_model_parallel_allreduce=cfg.async_tensor_model_parallel_allreduce,
+                                           bias_grad_from_output=True)   # forward() only ever uses h + b
         self.fc2 = tp.RowParallelLinear(f, cfg.hidden_size, bias=cfg.add_bias_linear, init_std=out_std,
                                         key=f"layers.{layer_number}.fc2", seed=cfg.seed,
                                         params_dtype=cfg.params_dtype, device=device,

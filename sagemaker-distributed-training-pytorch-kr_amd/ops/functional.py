@@ -185,12 +185,15 @@ class _BiasAct(torch.autograd.Function):
     def backward(ctx, dy):
         x, bias = ctx.saved_tensors
         C = _ext.ext()
-        tgt = grad_accumulate_target(ctx.bias_p) if ctx.has_bias else None
-        dx, dbias = C.bias_act_bwd(dy.contiguous(), x, bias, ctx.act, ctx.has_bias, tgt)
+        # a detached bias (ColumnParallelLinear(bias_grad_from_output=True): the linear produces
+        # the bias gradient with its weight gradient) needs no column sums here
+        want_db = ctx.has_bias and ctx.needs_input_grad[1]
+        tgt = grad_accumulate_target(ctx.bias_p) if want_db else None
+        dx, dbias = C.bias_act_bwd(dy.contiguous(), x, bias, ctx.act, want_db, tgt)
         if tgt is not None:
             _mark_ready(ctx.bias_p)
             return dx, None, None
-        return dx, (dbias.to(bias.dtype) if ctx.has_bias else None), None
+        return dx, (dbias.to(bias.dtype) if want_db else None), None
 
 
 def bias_gelu(x, bias=None, approximate: str = "tanh"):

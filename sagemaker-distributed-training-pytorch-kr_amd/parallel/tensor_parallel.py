@@ -339,7 +339,9 @@ class DeferredWgrad:
             return int(0.25 * torch.cuda.mem_get_info(dev)[0])
         return 64 * 2 ** 30
 
-    def push(self, weight, mg, g2, t2):
+    def push(self, weight, mg, g2, t2, bias=None):
+        """Queue mg += g2^T t2; ``bias`` (a bias Parameter with an fp32 main_grad, or None): its
+        gradient, the column sums of g2, comes out of the same grouped launch."""
         if self.hold_bytes_cap is None:
             self.hold_bytes_cap = self._hold_cap(g2.device)
         key = mg.data_ptr()
@@ -356,8 +358,8 @@ class DeferredWgrad:
             if it is not None:          # same main_grad twice outside a window: keep order
                 self.flush()
             # [weight, main_grad, segments, held (created inside a window), has its segment of
-            # the synchronising pass]
-            it = [weight, mg, [seg], self.hold, not self.hold]
+            # the synchronising pass, bias parameter or None]
+            it = [weight, mg, [seg], self.hold, not self.hold, bias]
             self.items.append(it)
             self.by_key[key] = it
             self.tiles += -(-g2.shape[1] // 256) * -(-t2.shape[1] // 256)
@@ -399,39 +401,58 @@ class DeferredWgrad:
         self.held_bytes = sum(sg[0].numel() * sg[0].element_size() + sg[1].numel() * sg[1].element_size()
                               for it in keep for sg in it[2])
         work = []
-        for weight, mg, segs, _held, complete in items:
+        for weight, mg, segs, _held, complete, bias in items:
             for g2, t2, vg, vt in segs:
                 if g2._version != vg or t2._version != vt:
                     raise RuntimeError("deferred wgrad: a queued dY / X tensor was modified in place before the "
                                        "flush; disable with SMDT_DEFER_WGRAD=0 and report the op that did it")
             if len(segs) == 1:
-                work.append((weight, mg, [(segs[0][0], segs[0][1])], complete))
+                work.append((weight, mg, [(segs[0][0], segs[0][1])], complete, bias))
             elif self.concat_segments:
                 work.append((weight, mg, [(torch.cat([sg[0] for sg in segs]), torch.cat([sg[1] for sg in segs]))],
-                             complete))
+                             complete, bias))
             else:
-                work.append((weight, mg, [(sg[0], sg[1]) for sg in segs], complete))
+                work.append((weight, mg, [(sg[0], sg[1]) for sg in segs], complete, bias))
         self.stats["flushes"] += 1
         self.stats["items"] += len(work)
         self.stats["max_segments"] = max(self.stats["max_segments"], max(len(w[2]) for w in work))
         # round i issues the i-th segment of every item: one grouped launch per round, so two
         # segments of one main_grad never run in the same launch (no write race, no atomics)
         for i in range(max(len(w[2]) for w in work)):
-            rnd = [(mg, sg[i]) for _, mg, sg, _ in work if len(sg) > i]
-            cuda = [(mg, g2, t2) for mg, (g2, t2) in rnd if g2.is_cuda]
+            rnd = [(mg, sg[i], b) for _, mg, sg, _, b in work if len(sg) > i]
+            cuda = [(mg, g2, t2, b) for mg, (g2, t2), b in rnd if g2.is_cuda]
             done = False
             if cuda:
-                done = _ext.ext().wgrad_grouped([c[0] for c in cuda], [c[1] for c in cuda], [c[2] for c in cuda])
-            for mg, (g2, t2) in rnd:
+                bts = [b.main_grad if b is not None else _NO_BIAS.get(g2.device) for _, g2, _, b in cuda]
+                done = _ext.ext().wgrad_grouped([c[0] for c in cuda], [c[1] for c in cuda], [c[2] for c in cuda], bts)
+            for mg, (g2, t2), b in rnd:
                 if not (g2.is_cuda and done):
                     mg.add_(g2.t().matmul(t2).view_as(mg))
-        for weight, _, _, complete in work:
-            cb = getattr(weight, "_smdt_grad_ready", None)
-            if cb is not None and complete:
-                cb(weight)
+                    if b is not None:
+                        b.main_grad.add_(g2.float().sum(0))
+        for weight, _, _, complete, b in work:
+            if not complete:
+                continue
+            for p in (weight, b):
+                cb = getattr(p, "_smdt_grad_ready", None) if p is not None else None
+                if cb is not None:
+                    cb(p)
 
 
 DEFERRED_WGRAD = DeferredWgrad()
+
+
+class _NoBias(dict):
+    """Per-device empty fp32 tensor: 'no bias target' in a grouped wgrad launch's bias list."""
+
+    def get(self, dev):
+        t = super().get(dev)
+        if t is None:
+            t = self[dev] = torch.empty(0, dtype=torch.float32, device=dev)
+        return t
+
+
+_NO_BIAS = _NoBias()
 
 
 def flush_deferred_wgrad():
@@ -501,6 +522,25 @@ def _wgrad(weight, g2, t2):
     if cb is not None:
         cb(weight)
     return None
+
+
+# The bias gradient of a column-parallel linear (the column sums of dY) comes out of the grouped
+# wgrad launch that reads dY anyway (csrc/kernels/wgrad_gemm.hip ``bias``) instead of a separate
+# pass over dY; SMDT_WGRAD_BIAS=0 keeps the separate column-sum kernel.
+_WGRAD_BIAS = os.environ.get("SMDT_WGRAD_BIAS", "1") == "1"
+
+
+def _wgrad_and_bias(weight, bias_p, g2, t2):
+    """(dW, db) for autograd: dW = g2^T t2 and db = sum_rows g2, each None when it went straight
+    into the parameter's fp32 main_grad (queued, or by a kernel now)."""
+    if bias_p is not None and _WGRAD_BIAS and g2.is_cuda:
+        mg = getattr(weight, "main_grad", None)
+        tgt = SF.grad_accumulate_target(bias_p)
+        if mg is not None and tgt is not None and tgt.numel() == g2.shape[-1] and DEFERRED_WGRAD.eligible(mg, g2, t2):
+            DEFERRED_WGRAD.push(weight, mg, g2, t2, bias=bias_p)
+            return None, None
+    dw = _wgrad(weight, g2, t2)
+    return dw, (_bias_grad(bias_p, g2) if bias_p is not None else None)
 
 
 # dgrad layout: dX = dY W with W [out, in] row-major is hipBLASLt's "NN" GEMM on this ROCm build,
@@ -577,14 +617,16 @@ class LinearWithGradAccumulationAndAsyncCommunication(torch.autograd.Function):
     """
 
     @staticmethod
-    def forward(ctx, x, weight, bias, sequence_parallel, async_grad_allreduce):
+    def forward(ctx, x, weight, bias, sequence_parallel, async_grad_allreduce, add_bias=True):
         ctx.sp = sequence_parallel
         ctx.async_ar = async_grad_allreduce
         ctx.has_bias = bias is not None
         ctx.bias_p = bias
         ctx.save_for_backward(x, weight)
         total = _gather_dim0(x, _tp_group()) if sequence_parallel else x
-        return F.linear(total, weight, bias)
+        # add_bias False: the caller adds the bias later (skip_bias_add) and this function only
+        # produces its gradient (the column sums of dY) beside the weight gradient
+        return F.linear(total, weight, bias if add_bias else None)
 
     @staticmethod
     def backward(ctx, g):
@@ -603,21 +645,20 @@ class LinearWithGradAccumulationAndAsyncCommunication(torch.autograd.Function):
                 handle = _all_reduce(gi_out, group, async_op=True)
         g2 = g.reshape(-1, g.shape[-1])
         t2 = total.reshape(-1, total.shape[-1])
-        dw = _wgrad(weight, g2, t2)
-        db = _bias_grad(ctx.bias_p, g2) if ctx.has_bias else None
+        dw, db = _wgrad_and_bias(weight, ctx.bias_p if ctx.has_bias else None, g2, t2)
         if handle is not None:
             # the collective is in flight: run the queued weight-gradient GEMMs beside it
             DEFERRED_WGRAD.flush_opportunistic()
             _wait_works([handle], group)
-        return gi_out, dw, db, None, None
+        return gi_out, dw, db, None, None, None
 
 
 def linear_with_grad_accumulation_and_async_allreduce(x, weight, bias, sequence_parallel=False,
-                                                      async_grad_allreduce=False):
+                                                      async_grad_allreduce=False, add_bias=True):
     if sequence_parallel and _TP_OVERLAP and _tp_size() > 1:
-        return _ColumnSPLinear.apply(x, weight, bias)
+        return _ColumnSPLinear.apply(x, weight, bias, add_bias)
     return LinearWithGradAccumulationAndAsyncCommunication.apply(x, weight, bias, sequence_parallel,
-                                                                 async_grad_allreduce)
+                                                                 async_grad_allreduce, add_bias)
 
 
 # --------------------------------------------------------------------------------------------
@@ -726,13 +767,14 @@ class _ColumnSPLinear(torch.autograd.Function):
     weight gradient queued and drained while the last chunk is in flight."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias):
+    def forward(ctx, x, weight, bias, add_bias=True):
         group = _tp_group()
         x = x.contiguous()
         n = x.shape[0]
         ws = dist.get_world_size(group)
         out = x.new_empty((n * ws,) + tuple(x.shape[1:-1]) + (weight.shape[0],))
-        total = ag_ring(x, group, lambda c, ch: _mm_into(out[c * n:(c + 1) * n], ch, weight, bias))
+        fb = bias if add_bias else None
+        total = ag_ring(x, group, lambda c, ch: _mm_into(out[c * n:(c + 1) * n], ch, weight, fb))
         ctx.save_for_backward(total, weight)
         ctx.bias_p = bias
         ctx.n = n
@@ -748,14 +790,13 @@ class _ColumnSPLinear(torch.autograd.Function):
 
         def wgrad():
             g2 = g.reshape(-1, g.shape[-1])
-            res["dw"] = _wgrad(weight, g2, total.reshape(-1, total.shape[-1]))
-            res["db"] = _bias_grad(ctx.bias_p, g2)
+            res["dw"], res["db"] = _wgrad_and_bias(weight, ctx.bias_p, g2, total.reshape(-1, total.shape[-1]))
             _flush_wgrad()
         wt = _dgrad_weight_t(weight)
         gi = rs_ring(lambda c: dgrad(g[c * n:(c + 1) * n], weight, wt), group, wgrad)
         if "dw" not in res:   # world 1 ring: no wait happened
             wgrad()
-        return gi, res["dw"], res["db"]
+        return gi, res["dw"], res["db"], None
 
 
 class _RowSPLinear(torch.autograd.Function):
@@ -845,7 +886,8 @@ class ColumnParallelLinear(nn.Module):
 
     def __init__(self, input_size, output_size, bias=True, gather_output=False, init_std=0.02, key="col",
                  seed=1234, params_dtype=torch.float32, device=None, sequence_parallel=False,
-                 skip_bias_add=False, chunks=None, async_tensor_model_parallel_allreduce=True):
+                 skip_bias_add=False, chunks=None, async_tensor_model_parallel_allreduce=True,
+                 bias_grad_from_output=False):
         super().__init__()
         st = ps.get_state()
         self.tp, self.rank = st.tp, st.tp_rank
@@ -855,6 +897,11 @@ class ColumnParallelLinear(nn.Module):
         self.gather_output = gather_output
         self.sequence_parallel = sequence_parallel and self.tp > 1
         self.skip_bias_add = skip_bias_add
+        # skip_bias_add and the caller only ever adds the returned bias to the output (h + b, e.g.
+        # the fused bias-GeLU): the bias gradient equals the column sums of this linear's output
+        # gradient, so the linear produces it with its weight gradient (one pass over dY) and the
+        # returned bias is detached
+        self.bias_grad_from_output = bool(bias_grad_from_output and skip_bias_add and bias)
         self.async_ar = async_tensor_model_parallel_allreduce and self.tp > 1 and not self.sequence_parallel
         w = init_full_then_shard((output_size, input_size), init_std, key + ".weight", seed, params_dtype, device, 0,
                                  self.rank, self.tp, chunks)
@@ -871,12 +918,18 @@ class ColumnParallelLinear(nn.Module):
     def forward(self, x):
         if not (self.async_ar or self.sequence_parallel):
             x = copy_to_tensor_model_parallel_region(x)
-        b = None if self.skip_bias_add else self.bias
-        y = linear_with_grad_accumulation_and_async_allreduce(x, self.weight, b, self.sequence_parallel,
-                                                              self.async_ar)
+        if self.bias_grad_from_output:
+            y = linear_with_grad_accumulation_and_async_allreduce(x, self.weight, self.bias, self.sequence_parallel,
+                                                                  self.async_ar, add_bias=False)
+        else:
+            b = None if self.skip_bias_add else self.bias
+            y = linear_with_grad_accumulation_and_async_allreduce(x, self.weight, b, self.sequence_parallel,
+                                                                  self.async_ar)
         if self.gather_output:
             y = gather_from_tensor_model_parallel_region(y)
-        return (y, self.bias) if self.skip_bias_add else y
+        if self.skip_bias_add:
+            return y, (self.bias.detach() if self.bias_grad_from_output else self.bias)
+        return y
 
 
 class RowParallelLinear(nn.Module):

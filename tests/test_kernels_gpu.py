@@ -415,6 +415,29 @@ def test_wgrad_mfma_fp16_and_bf16(dt):
 
 
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+def test_wgrad_grouped_bias_column_sums(dt):
+    """The grouped wgrad launch also accumulates each problem's bias gradient (column sums of
+    dY) into an fp32 target: whole tiles (plain read-modify-write), partial tiles (N = 1008, K = 520
+    not multiples of 256), tail-split pieces (fp32 atomics), a problem without a bias in the same
+    launch, and a second launch accumulating on top."""
+    torch.manual_seed(16)
+    C = _ext.ext()
+    # 256 whole tiles of the first problem run the plain epilogue, the other 45 tiles the split tail
+    shapes = [(2048, 4096, 4096), (4096, 1536, 1024), (2048, 1008, 520), (4096, 256, 256), (1024, 512, 1024)]
+    dys = [torch.randn(M, N, device=DEV, dtype=dt) for M, N, _ in shapes]
+    xs = [torch.randn(M, K, device=DEV, dtype=dt) for M, _, K in shapes]
+    mgs = [torch.zeros(N, K, device=DEV) for _, N, K in shapes]
+    bias = [torch.full((N,), 0.5, device=DEV) if i != 3 else torch.empty(0, device=DEV)
+            for i, (_, N, _) in enumerate(shapes)]
+    for rep in range(2):
+        assert C.wgrad_grouped(mgs, dys, xs, bias)
+    for i, (dy, x, mg) in enumerate(zip(dys, xs, mgs)):
+        torch.testing.assert_close(mg, 2 * (dy.float().t() @ x.float()), atol=0.1, rtol=2e-3)
+        if i != 3:
+            torch.testing.assert_close(bias[i], 0.5 + 2 * dy.float().sum(0), atol=0.02, rtol=1e-4)
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("shape", [(1024, 1024), (3072, 1024), (1024, 4096), (50304, 1024), (200, 136), (8, 8)])
 def test_transpose2d(dt, shape):
     x = torch.randn(*shape, device="cuda").to(dt)
