@@ -443,60 +443,9 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void fwd_kernel(const E* __re
 // accumulators (no VALU in their loops):
 //   ndl[b, h, q]   = -keep * sum_d dO[q, d] O[q, d]      (-delta', the dP accumulator's start)
 //   nlse2[b, h, q] = -(lse log2 e - log2 inv)           (the S accumulator's start, log2 domain)
-constexpr int kDeltaRows = 4;  // rows per 8-lane group in delta_kernel
-
-template <int D, class E>
-__global__ __launch_bounds__(256) void delta_kernel(const E* __restrict__ O,
-                                                    const E* __restrict__ dO,
-                                                    float* __restrict__ delta, const float* __restrict__ LSE,
-                                                    float* __restrict__ NLSE2, float dscale, float lsub, int B,
-                                                    int H, int S, Strides os, Strides dos) {
-  // 8 lanes per row, each lane D/8 contiguous elements. Rows are enumerated (b, q, h) with the
-  // head fastest, the order of the [B, S, H, D] activations, so a wave reads one contiguous
-  // span; 32-bit index math (the launcher checks B * H * S < 2^31).
-  // Each 8-lane group handles kDeltaRows consecutive rows with all their loads issued before the
-  // first reduction (memory-level parallelism: the kernel is a pure stream).
-  const int gid = blockIdx.x * 256 + threadIdx.x;
-  const int r0 = (gid >> 3) * kDeltaRows;
-  const int part = gid & 7;
-  const int nrows = B * H * S;
-  if (r0 >= nrows) return;
-  float a[kDeltaRows][D / 8], bb[kDeltaRows][D / 8];
-  int outi[kDeltaRows];
-#pragma unroll
-  for (int k = 0; k < kDeltaRows; ++k) {
-    const int row = r0 + k < nrows ? r0 + k : nrows - 1;   // tail rows re-read the last row, unstored
-    const int hh = row % H;
-    const int t = row / H;
-    const int q = t % S, b = t / S;
-    const E* o = O + b * os.sb + hh * os.sh + (int64_t)q * os.ss + part * (D / 8);
-    const E* g = dO + b * dos.sb + hh * dos.sh + (int64_t)q * dos.ss + part * (D / 8);
-#pragma unroll
-    for (int c = 0; c < D / 64; ++c) {
-      float ta[8], tb[8];
-      load_vec<E, 8, true>(o + 8 * c, ta);   // read once here: stream past the caches
-      load_vec<E, 8, true>(g + 8 * c, tb);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        a[k][8 * c + j] = ta[j];
-        bb[k][8 * c + j] = tb[j];
-      }
-    }
-    outi[k] = (b * H + hh) * S + q;   // lse / delta are [B, H, S]
-  }
-#pragma unroll
-  for (int k = 0; k < kDeltaRows; ++k) {
-    float acc = 0.f;
-#pragma unroll
-    for (int j = 0; j < D / 8; ++j) acc += a[k][j] * bb[k][j];
-#pragma unroll
-    for (int off = 4; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 8);
-    if (r0 + k < nrows) {
-      if (part == 0) delta[outi[k]] = -acc * dscale;
-      if (part == 1) NLSE2[outi[k]] = lsub - LSE[outi[k]] * kLog2e;
-    }
-  }
-}
+// They are made by the dQ kernel, which runs first and holds dO of its query rows in registers
+// anyway (one extra read of O's rows); the dK / dV kernel reads them from memory. (Round 3 had a
+// separate streaming delta kernel: 1.6 ms per GPT-2 345M step)
 
 // ---------------------------------------------------------------------------------------
 // dK / dV. Workgroup = 4 waves = 128 keys of one (b, kv-head); each wave keeps K, V of its 32
@@ -629,7 +578,7 @@ __global__ __launch_bounds__(256, D == 64 ? SMDT_FA_DKDV_OCC : 1) void bwd_dkdv_
     const float* del_l = lse_l + kTile;
     issue(pre);
     // S'[q, key] = Q . K'^T - lse ; dP'[q, key] = dO . V^T - delta  (key on lane, query rows in
-    // registers): the row constants (prepared by delta_kernel: -(lse log2e - log2 inv) and
+    // registers): the row constants (prepared by the dQ kernel: -(lse log2e - log2 inv) and
     // -delta') are the accumulators' initial values, read straight from LDS.
     auto sd_init = [&](int qs2, bool diag, f32x16& sa, f32x16& pa) {
 #pragma unroll
@@ -778,9 +727,10 @@ __global__ __launch_bounds__(256, D == 64 ? SMDT_FA_DKDV_OCC : 1) void bwd_dkdv_
 template <int D, bool CAUSAL, bool DROP, class E>
 __global__ __launch_bounds__(256, D == 64 ? SMDT_FA_DQ_OCC : 1) void bwd_dq_kernel(
     const E* __restrict__ Q, const E* __restrict__ K, const E* __restrict__ V,
-    const E* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ DELTA,
-    E* __restrict__ dQ, int B, int H, int Hkv, int S, Strides qs, Strides ks_, Strides vs,
-    Strides dos, Strides dqs, float scale, Drop drop) {
+    const E* __restrict__ dO, const E* __restrict__ O, const float* __restrict__ LSE,
+    float* __restrict__ DELTA, float* __restrict__ NLSE2, E* __restrict__ dQ, int B, int H, int Hkv,
+    int S, Strides qs, Strides ks_, Strides vs, Strides dos, Strides os, Strides dqs, float scale,
+    float dscale, float lsub, Drop drop) {
   using G = Geo<D>;
   // D = 64: three [K | V] buffers, two tiles in flight; D = 128 (twice the bytes): two buffers,
   // so two workgroups still fit a CU's 160 KB of LDS.
@@ -823,10 +773,27 @@ __global__ __launch_bounds__(256, D == 64 ? SMDT_FA_DQ_OCC : 1) void bwd_dq_kern
   load_reg_frags<D>(dO + b * dos.sb + hq * dos.sh, dos.ss, qw, lane, dof);
 #pragma unroll
   for (int kk = 0; kk < G::KS; ++kk) qf[kk] = scale8(qf[kk], scale * kLog2e);  // S^T in log2 domain
-  // Row constants (prepared by delta_kernel: -(lse log2e - log2 inv), -delta') as the S / dP MFMAs'
-  // initial accumulators, register-resident for the whole loop (no per-subtile splat).
-  const float nlse2 = LSE[((int64_t)b * H + hq) * S + my_q];
-  const float ndl = DELTA[((int64_t)b * H + hq) * S + my_q];
+  // Row constants -(lse log2e - log2 inv) and -delta' = -keep sum_d dO O, made here from this
+  // lane's dO fragments (lanes l and l ^ 32 hold the two 8-column halves of every 16 columns of
+  // the row) and stored for the dK / dV kernel, which runs next; they are the S / dP MFMAs'
+  // initial accumulators.
+  const int64_t ridx = ((int64_t)b * H + hq) * S + my_q;
+  float ndl;
+  {
+    v8_t<E> of[G::KS];
+    load_reg_frags<D>(O + b * os.sb + hq * os.sh, os.ss, qw, lane, of);
+    float acc = 0.f;
+#pragma unroll
+    for (int kk = 0; kk < G::KS; ++kk)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc = fmaf((float)of[kk][j], (float)dof[kk][j], acc);
+    ndl = -xhalf_sum(acc) * dscale;
+  }
+  const float nlse2 = lsub - LSE[ridx] * kLog2e;
+  if (h == 0) {
+    DELTA[ridx] = ndl;
+    NLSE2[ridx] = nlse2;
+  }
 #if SMDT_FA_DQ_REMAT
   // the two accumulator splats are re-made per sub-tile (opaque: not hoisted), freeing 32 VGPRs
 #define SMDT_DQ_ST0 splat16(opaque(nlse2))
@@ -1026,35 +993,21 @@ extern "C" hipError_t smdt_flash_bwd(int dtype, const void* q, const void* k, co
       vs{strides[6], strides[7], strides[8]}, os{strides[9], strides[10], strides[11]},
       dos{strides[12], strides[13], strides[14]}, dqs{strides[15], strides[16], strides[17]},
       dks{strides[18], strides[19], strides[20]}, dvs{strides[21], strides[22], strides[23]};
-  // delta holds 2 x [B, H, S]: -delta' rows, then -(lse log2e - log2 inv) rows (see delta_kernel)
+  // delta holds 2 x [B, H, S]: -delta' rows, then -(lse log2e - log2 inv) rows, both written by
+  // the dQ kernel (which therefore runs first) and read by the dK / dV kernel
   float* nlse2 = delta + (int64_t)B * H * S;
   const float dscale = drop ? dr.keep : 1.f, lsub = drop ? dr.log2inv : 0.f;
-  {
-    int64_t rows = (int64_t)B * H * S;
-    if (rows * 8 >= (int64_t(1) << 31)) return hipErrorInvalidValue;  // delta_kernel indexes in 32 bits
-    dim3 grid((unsigned)(((rows + kDeltaRows - 1) / kDeltaRows * 8 + 255) / 256));
-    if (dtype == 2) {
-      if (D == 64)
-        hipLaunchKernelGGL((delta_kernel<64, f16>), grid, dim3(256), 0, st, (const f16*)o, (const f16*)dout, delta, lse, nlse2, dscale, lsub, B, H, S, os, dos);
-      else
-        hipLaunchKernelGGL((delta_kernel<128, f16>), grid, dim3(256), 0, st, (const f16*)o, (const f16*)dout, delta, lse, nlse2, dscale, lsub, B, H, S, os, dos);
-    } else {
-      if (D == 64)
-        hipLaunchKernelGGL((delta_kernel<64, bf16>), grid, dim3(256), 0, st, (const bf16*)o, (const bf16*)dout, delta, lse, nlse2, dscale, lsub, B, H, S, os, dos);
-      else
-        hipLaunchKernelGGL((delta_kernel<128, bf16>), grid, dim3(256), 0, st, (const bf16*)o, (const bf16*)dout, delta, lse, nlse2, dscale, lsub, B, H, S, os, dos);
-    }
-  }
   dim3 gkv((unsigned)((int64_t)B * Hkv * (S / kBlockRows)));
   dim3 gq((unsigned)((int64_t)B * H * (S / kBlockRows)));
 #define SMDT_FA_BWD_T(DD, CC, DR, ET)                                                            \
   do {                                                                                           \
+    hipLaunchKernelGGL((bwd_dq_kernel<DD, CC, DR, ET>), gq, dim3(256), 0, st, (const ET*)q,     \
+                       (const ET*)k, (const ET*)v, (const ET*)dout, (const ET*)o, lse, delta,     \
+                       nlse2, (ET*)dq, B, H, Hkv, S, qs, ks, vs, dos, os, dqs, scale, dscale,     \
+                       lsub, dr);                                                                 \
     hipLaunchKernelGGL((bwd_dkdv_kernel<DD, CC, DR, ET>), gkv, dim3(256), 0, st, (const ET*)q,  \
                        (const ET*)k, (const ET*)v, (const ET*)dout, nlse2, delta, (ET*)dk,        \
                        (ET*)dv, B, H, Hkv, S, qs, ks, vs, dos, dks, dvs, scale, dr);              \
-    hipLaunchKernelGGL((bwd_dq_kernel<DD, CC, DR, ET>), gq, dim3(256), 0, st, (const ET*)q,     \
-                       (const ET*)k, (const ET*)v, (const ET*)dout, nlse2, delta, (ET*)dq,        \
-                       B, H, Hkv, S, qs, ks, vs, dos, dqs, scale, dr);                            \
   } while (0)
 #define SMDT_FA_BWD(DD, CC, DR) \
   do { if (dtype == 2) SMDT_FA_BWD_T(DD, CC, DR, f16); else SMDT_FA_BWD_T(DD, CC, DR, bf16); } while (0)
