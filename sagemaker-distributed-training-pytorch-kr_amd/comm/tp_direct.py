@@ -1,0 +1,156 @@
+"""Direct multi-link sequence-parallel exchanges for TP groups of 4 or 8 GPUs.
+
+The sequence-parallel collective-matmul (parallel/tensor_parallel.ag_ring / rs_ring) moves one
+[s/tp, b, h] chunk per ring step from each rank to its ring successor: on the all-to-all xGMI
+mesh of an MI355X node that is ONE link per direction per rank, while the rank has tp - 1 links
+into its TP group (3 at TP4). For GPT-3 6.7B at TP4 PP2 + SP (BASELINE config #5) a rank moves
+~64 GB of SP traffic per step, ~1 s over one link against ~0.38 s of compute
+(BENCHMARKS.md, benchmarks/predict_scaling.py).
+
+``TpDirect`` replaces the ring, for TP groups larger than 2 (TP pairs have the relay engine,
+comm/relay.py), by the single-launch all-gather / reduce-scatter of the xGMI engine
+(comm/xgmi.XgmiAllReduce): every rank reads all of its peers' chunks at once, one per link, so
+the exchange runs at (tp - 1) links per rank:
+
+* all-gather (column-parallel forward, row-parallel backward): the gather starts on the engine's
+  stream while the GEMM of the local chunk runs on the compute stream, then the peers' chunks;
+* reduce-scatter (row-parallel forward, column-parallel backward): the partial products of all
+  chunks, then one engine reduce-scatter, beside which the backward runs its queued weight-gradient
+  GEMMs (the ring's ``before_last_wait``).
+
+It is built at ``initialize_model_parallel`` for TP groups of 4 / 8 on a node whose backend is
+RCCL (collective over the TP group), checked bit-exactly against RCCL by the engine's own
+validation, and KEPT ONLY WHEN a timed all-gather at a representative chunk size beats the ring on
+every rank (``SMDT_TP_DIRECT=1`` / ``0`` forces it on / off). ``TpDirect.for_test(group)`` builds
+it without validation or timing over a Gloo group (multi-process tests sharing one GPU).
+"""
+from __future__ import annotations
+
+import os
+import time
+from typing import Callable, Optional
+
+import torch
+import torch.distributed as dist
+
+TUNED: dict = {}
+
+
+class TpDirect:
+    def __init__(self, engine, group):
+        self.eng = engine
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.calls = 0
+
+    @classmethod
+    def for_test(cls, group, region_bytes: int = 8 << 20) -> "TpDirect":
+        from .xgmi import XgmiAllReduce
+        return cls(XgmiAllReduce(group, region_bytes=region_bytes, blocks=32, validate=False), group)
+
+    @property
+    def active(self) -> bool:
+        return self.eng is not None and self.eng.active
+
+    def fits(self, t: torch.Tensor) -> bool:
+        nb = t.numel() * t.element_size()
+        return self.active and t.is_cuda and t.dtype in (torch.bfloat16, torch.float16, torch.float32) \
+            and nb % 16 == 0 and t.data_ptr() % 16 == 0
+
+    def all_gather(self, x: torch.Tensor, chunk_fn: Optional[Callable] = None,
+                   before_last_wait: Optional[Callable] = None) -> Optional[torch.Tensor]:
+        """``ag_ring`` semantics: returns the gathered [ws * n, ...] tensor after calling
+        ``chunk_fn(c, chunk)`` for every chunk (the local one first, beside the transfer).
+        None: not applicable (the caller runs the ring)."""
+        x = x.contiguous()
+        if not self.fits(x):
+            return None
+        ws, r, n = self.world, self.rank, x.shape[0]
+        total = x.new_empty((n * ws,) + tuple(x.shape[1:]))
+        mine = total[r * n:(r + 1) * n]
+        mine.copy_(x)
+        h = self.eng.all_gather_async(total.view(-1), mine.view(-1))
+        if h is None:
+            return None
+        self.calls += 1
+        if chunk_fn is not None:
+            chunk_fn(r, x)                       # beside the gather
+        if before_last_wait is not None:
+            before_last_wait()
+        h.wait()
+        if chunk_fn is not None:
+            for c in range(ws):
+                if c != r:
+                    chunk_fn(c, total[c * n:(c + 1) * n])
+        return total
+
+    def reduce_scatter(self, partial_fn: Callable, before_last_wait: Optional[Callable] = None) -> torch.Tensor:
+        """``rs_ring`` semantics: chunk c of the tensor being reduced is ``partial_fn(c)``;
+        returns this rank's reduced chunk (RCCL's reduce-scatter if the engine cannot take it)."""
+        ws, r = self.world, self.rank
+        first = partial_fn(r)
+        n = first.shape[0]
+        buf = first.new_empty((n * ws,) + tuple(first.shape[1:]))
+        buf[r * n:(r + 1) * n].copy_(first)
+        del first
+        for c in range(ws):
+            if c != r:
+                buf[c * n:(c + 1) * n].copy_(partial_fn(c))
+        out = buf.new_empty((n,) + tuple(buf.shape[1:]))
+        h = self.eng.reduce_scatter_async(out.view(-1), buf.view(-1)) if self.fits(buf) else None
+        if h is None:
+            w = dist.reduce_scatter_tensor(out, buf, group=self.group, async_op=True)
+            if before_last_wait is not None:
+                before_last_wait()
+            w.wait()
+            return out
+        self.calls += 1
+        if before_last_wait is not None:
+            before_last_wait()
+        h.wait()
+        return out
+
+
+def create(group) -> Optional[TpDirect]:
+    """Collective over the TP ``group`` (4 or 8 ranks on one node): the engine when it is wanted
+    and measured faster than the p2p ring, else None."""
+    env = os.environ.get("SMDT_TP_DIRECT")
+    if env == "0" or not (dist.is_initialized() and torch.cuda.is_available()):
+        return None
+    from . import xgmi
+    ws = dist.get_world_size(group)
+    if ws not in (4, 8) or not xgmi.rccl_backend(group):
+        return None
+    try:
+        eng = xgmi.XgmiAllReduce(group)
+    except (RuntimeError, ValueError) as e:
+        import warnings
+        warnings.warn(f"direct TP exchanges disabled: {e}")
+        return None
+    td = TpDirect(eng, group)
+    if env == "1":
+        return td
+    # time the ring against the engine: one [s/tp, b, h]-sized all-gather (8 MB per rank)
+    from ..parallel.tensor_parallel import ag_ring
+    dev = torch.device("cuda", torch.cuda.current_device())
+    x = torch.randn(4096, 1024, device=dev, dtype=torch.bfloat16)
+    ts = []
+    for fn in (lambda: ag_ring(x, group, _skip_direct=True), lambda: td.all_gather(x)):
+        for _ in range(2):
+            fn()
+        torch.cuda.synchronize()
+        dist.barrier(group=group)
+        t0 = time.perf_counter()
+        for _ in range(5):
+            fn()
+        torch.cuda.synchronize()
+        t = torch.tensor([(time.perf_counter() - t0) / 5], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+        ts.append(float(t.item()))
+    TUNED[f"tp{ws}"] = {"ring_ms": round(ts[0] * 1e3, 3), "direct_ms": round(ts[1] * 1e3, 3),
+                        "direct": ts[1] < ts[0]}
+    if ts[1] < ts[0]:
+        return td
+    eng.close()
+    return None

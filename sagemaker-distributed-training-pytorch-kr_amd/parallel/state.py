@@ -186,6 +186,11 @@ def initialize_model_parallel(tensor_model_parallel_size: int = 1, pipeline_mode
     if tp == 2 and world in (4, 8):
         from ..comm import relay
         st.tp_relay = relay.create_for_pairs(st.tp_group)
+    # TP groups of 4 / 8: sequence-parallel exchanges over all of the group's links (collective over
+    # the TP group; kept only when measured faster than the ring, comm/tp_direct.py)
+    if tp in (4, 8) and world in (4, 8):
+        from ..comm import tp_direct
+        st.tp_direct = tp_direct.create(st.tp_group)
     return st
 
 

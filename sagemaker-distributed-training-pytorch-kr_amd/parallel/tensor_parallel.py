@@ -712,9 +712,24 @@ def _mm_into(dst, a, w, bias=None):
         torch.mm(a2, w.t(), out=d2)
 
 
-def ag_ring(x, group, chunk_fn=None, before_last_wait=None):
+def _direct(group):
+    """The multi-link TP exchange engine (comm/tp_direct.py) bound to ``group``, or None."""
+    st = ps.get_state()
+    td = getattr(st, "tp_direct", None)
+    return td if (td is not None and group is st.tp_group and td.active) else None
+
+
+def ag_ring(x, group, chunk_fn=None, before_last_wait=None, _skip_direct=False):
     """All-gather ``x`` along dim 0 over ``group`` as a ring; ``chunk_fn(c, chunk)`` runs on chunk c
-    as soon as it is resident, while the next chunk is in flight. Returns the gathered tensor."""
+    as soon as it is resident, while the next chunk is in flight. Returns the gathered tensor.
+    TP groups of 4 / 8 with a direct engine (comm/tp_direct.py) gather over all of the group's
+    links at once instead, the local chunk's GEMM beside the transfer."""
+    td = None if _skip_direct else _direct(group)
+    if td is not None:
+        out = td.all_gather(x, chunk_fn, before_last_wait)
+        if out is not None:
+            _cs.collective("all_gather", group, _nbytes(out), transport="xgmi")
+            return out
     ws, r, nxt, prv = _ring(group)
     n = x.shape[0]
     total = x.new_empty((n * ws,) + tuple(x.shape[1:]))
@@ -737,7 +752,13 @@ def ag_ring(x, group, chunk_fn=None, before_last_wait=None):
 def rs_ring(partial_fn, group, before_last_wait=None):
     """Reduce-scatter along dim 0 over ``group`` as a ring, where chunk c of the tensor being
     reduced is produced on demand by ``partial_fn(c)`` (a GEMM on c's rows): step s computes the
-    next partial while the previous one is in flight. Returns this rank's reduced chunk."""
+    next partial while the previous one is in flight. Returns this rank's reduced chunk. TP groups
+    of 4 / 8 with a direct engine reduce all partials over every link of the group at once."""
+    td = _direct(group)
+    if td is not None:
+        out = td.reduce_scatter(partial_fn, before_last_wait)
+        _cs.collective("reduce_scatter", group, _nbytes(out) * td.world, transport="xgmi")
+        return out
     ws, r, nxt, prv = _ring(group)
     works, incoming, keep = None, None, []
     for s in range(ws):

@@ -1018,3 +1018,57 @@ def smddp_torch_ddp_worker(rank, world, port, outdir):
         res["err"] = traceback.format_exc()
     with open(os.path.join(outdir, f"r{rank}.pkl"), "wb") as f:
         pickle.dump(res, f)
+
+
+def tp_direct_worker(rank, world, port, outdir):
+    """One rank of the direct-TP-exchange GPU test: ``world`` processes on cuda:0 with a Gloo
+    world group, the TP group's xGMI engine over same-device IPC (comm/tp_direct.TpDirect.for_test),
+    and the sequence-parallel ring entry points ``ag_ring`` / ``rs_ring`` run through it; results vs
+    the host-side gathered / reduced reference."""
+    import os
+    import pickle
+    import traceback
+
+    import torch
+    os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "RANK": str(rank),
+                       "WORLD_SIZE": str(world), "HSA_ENABLE_IPC_MODE_LEGACY": "0"})
+    res = {"err": None}
+    try:
+        import torch.distributed as dist
+        from smdt_amd.comm import tp_direct
+        from smdt_amd.parallel import state as ps
+        from smdt_amd.parallel import tensor_parallel as T
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        st = ps.initialize_model_parallel(world, 1)
+        st.tp_direct = tp_direct.TpDirect.for_test(st.tp_group)
+        g = st.tp_group
+        torch.manual_seed(100 + rank)
+        n, h, o = 256, 64, 96
+        x = torch.randn(n, 4, h, device="cuda", dtype=torch.bfloat16)
+        w = torch.randn(o, h, device="cuda", dtype=torch.bfloat16)
+        # all-gather with a per-chunk GEMM (the column-parallel forward)
+        out = torch.empty(n * world, 4, o, device="cuda", dtype=torch.bfloat16)
+        seen = []
+        total = T.ag_ring(x, g, lambda c, ch: (seen.append(c), out[c * n:(c + 1) * n].copy_(ch @ w.t())))
+        xs = [torch.empty_like(x.cpu()) for _ in range(world)]
+        dist.all_gather(xs, x.cpu())
+        ref_total = torch.cat(xs)
+        ok_ag = torch.equal(total.cpu(), ref_total) and sorted(seen) == list(range(world)) and seen[0] == rank
+        ok_mm = torch.allclose(out.float().cpu(), (ref_total.float() @ w.float().cpu().t()), atol=0.5, rtol=2e-2)
+        # reduce-scatter of per-chunk partials (the row-parallel forward)
+        full = torch.randn(n * world, 4, o, device="cuda", dtype=torch.float32)
+        part = T.rs_ring(lambda c: full[c * n:(c + 1) * n] * 1.0, g, before_last_wait=lambda: seen.append("wgrad"))
+        red = full.cpu().clone()
+        dist.all_reduce(red)
+        ok_rs = torch.allclose(part.cpu(), red[rank * n:(rank + 1) * n], atol=1e-5, rtol=1e-5)
+        torch.cuda.synchronize()
+        res.update(ok_ag=bool(ok_ag), ok_mm=bool(ok_mm), ok_rs=bool(ok_rs), calls=st.tp_direct.calls,
+                   wgrad_hook="wgrad" in seen, error_word=st.tp_direct.eng.error())
+        dist.barrier()
+        st.tp_direct.eng.close()
+        dist.destroy_process_group()
+    except Exception:  # noqa: BLE001
+        res["err"] = traceback.format_exc()
+    with open(os.path.join(outdir, f"r{rank}.pkl"), "wb") as f:
+        pickle.dump(res, f)

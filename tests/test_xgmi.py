@@ -305,3 +305,42 @@ def test_smddp_backend_name_turns_xgmi_on(monkeypatch):
     assert xgmi.wanted() and xgmi.rccl_backend()
     monkeypatch.setattr(dist, "get_backend", lambda group=None: "gloo")
     assert not xgmi.wanted() and not xgmi.rccl_backend()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [4])
+def test_tp_direct_exchange_through_ring_entry_points(world):
+    """``ag_ring`` / ``rs_ring`` of a TP group of 4 run through the direct
+    multi-link engine (comm/tp_direct.py; 4 processes on one GPU, IPC mappings of the same device):
+    the gather equals RCCL-free host gathering, every chunk's GEMM runs (the local one first, beside
+    the transfer), the reduce-scatter equals the host all-reduce's slice, the backward hook runs."""
+    import os
+    import pickle
+    import tempfile
+
+    import torch.multiprocessing as mp
+
+    import dist_workers as W
+    from _dist import free_port
+
+    port = free_port()
+    with tempfile.TemporaryDirectory() as d:
+        ctx = mp.get_context("spawn")
+        procs = [ctx.Process(target=W.tp_direct_worker, args=(r, world, port, d)) for r in range(world)]
+        for p in procs:
+            p.start()
+        for p in procs:
+            p.join(100)
+        for p in procs:
+            if p.is_alive():
+                p.kill()
+        out = []
+        for r in range(world):
+            path = os.path.join(d, f"r{r}.pkl")
+            assert os.path.exists(path), f"rank {r} wrote no result (exit {procs[r].exitcode})"
+            with open(path, "rb") as f:  # written by this test's own workers
+                out.append(pickle.load(f))
+    for r, res in enumerate(out):
+        assert res["err"] is None, f"rank {r}:\n{res['err']}"
+        assert res["ok_ag"] and res["ok_mm"] and res["ok_rs"], (r, res)
+        assert res["calls"] == 2 and res["wgrad_hook"] and res["error_word"] == 0, (r, res)
