@@ -75,7 +75,11 @@ def auto_bucket_elems(group, total_elems: int, elem_bytes: int) -> int:
     alpha = beta = None
     ws = dist.get_world_size(group) if (dist.is_initialized() and group is not None) else 1
     measured = False
-    if ws > 1 and torch.cuda.is_available() and dist.get_backend(group) in ("nccl", "smddp"):
+    try:
+        rccl = dist.get_backend(group) in ("nccl", "smddp")
+    except (RuntimeError, ValueError):     # a group outside c10d's table (comm/loopback.py)
+        rccl = False
+    if ws > 1 and torch.cuda.is_available() and rccl:
         alpha, beta = latency_bandwidth(group)
         measured = True
     nbytes = choose_bucket_bytes(total_elems * elem_bytes, alpha, beta)

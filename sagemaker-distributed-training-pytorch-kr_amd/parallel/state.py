@@ -194,24 +194,30 @@ def initialize_model_parallel(tensor_model_parallel_size: int = 1, pipeline_mode
     return st
 
 
-def initialize_emulated_tensor_parallel(tensor_model_parallel_size: int) -> ParallelState:
-    """ONE process as rank 0 of a ``tensor_model_parallel_size``-rank TP group whose collectives
-    are local stand-ins (comm/loopback.py): the per-rank compute of a TP layout, timed on one GPU
-    (bench.py --emulate-tp, benchmarks/predict_scaling.py). pp = dp = 1; the model-parallel group
-    (grad-norm all-reduce) is the loopback group too. Timing only: never train with it."""
+def initialize_emulated_tensor_parallel(tensor_model_parallel_size: int = 1,
+                                        data_parallel_size: int = 1) -> ParallelState:
+    """ONE process as rank 0 of a ``tensor_model_parallel_size``-rank TP group and / or of a
+    ``data_parallel_size``-rank DP group whose collectives are local stand-ins
+    (comm/loopback.py): the per-rank work of a multi-GPU layout, timed on one GPU — bench.py
+    --emulate-tp / benchmarks/predict_scaling.py (a TP rank's sharded compute), SMDT_EMULATE_DP
+    for the SFT recipe (a ZeRO rank's 1/dp optimizer shard and its gradient reduce-scatter /
+    parameter all-gather traffic on the receiving side). pp = 1; with tp > 1 the model-parallel
+    group (grad-norm all-reduce) is the loopback group too. Timing only: never train with it."""
     global _STATE
     from ..comm.loopback import LoopbackGroup
-    tp = int(tensor_model_parallel_size)
+    tp, dp = int(tensor_model_parallel_size), int(data_parallel_size)
     if dist.is_initialized() and dist.get_world_size() != 1:
-        raise RuntimeError("TP emulation runs in a single process (world size 1)")
+        raise RuntimeError("TP / DP emulation runs in a single process (world size 1)")
     if not dist.is_initialized():     # a one-rank world: c10d's group calls need a default group
         dist.init_process_group("nccl" if torch.cuda.is_available() else "gloo", store=dist.HashStore(),
                                 rank=0, world_size=1)
-    g = LoopbackGroup(tp)
-    world_group = dist.group.WORLD if dist.is_initialized() else None
-    st = ParallelState(tp=tp, pp=1, dp=1, rank=0, world=1, tp_group=g, mp_group=g,
-                       dp_group=world_group, dp_cp_group=world_group, tp_ranks=list(range(tp)),
-                       pp_ranks=[0], dp_ranks=[0], cp_ranks=[0], dp_cp_ranks=[0], embd_ranks=[0])
+    world_group = dist.group.WORLD
+    tg = LoopbackGroup(tp) if tp > 1 else world_group
+    dg = LoopbackGroup(dp) if dp > 1 else world_group
+    st = ParallelState(tp=tp, pp=1, dp=dp, rank=0, world=1, tp_group=tg, mp_group=tg if tp > 1 else None,
+                       dp_group=dg, dp_cp_group=dg, tp_ranks=list(range(tp)),
+                       pp_ranks=[0], dp_ranks=list(range(dp)), cp_ranks=[0], dp_cp_ranks=list(range(dp)),
+                       embd_ranks=[0])
     st.initialized = True
     st.emulated = True
     _STATE = st

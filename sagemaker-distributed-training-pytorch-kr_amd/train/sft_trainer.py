@@ -55,7 +55,13 @@ def setup_distributed(args=None, backend: str = "nccl"):
         local = int(os.environ.get("LOCAL_RANK", "0"))
     else:  # single process: no process group is created
         rank, local, world, _ = init_distributed(backend)
-    if not ps.model_parallel_is_initialized():
+    emu = int(os.environ.get("SMDT_EMULATE_DP", "0") or 0)
+    if emu > 1 and world == 1:
+        # timing: this process does ONE data-parallel rank's work of an emu-GPU ZeRO job — its own
+        # micro-batches, its 1/emu optimizer shard, its share of the gradient reduce-scatter /
+        # parameter all-gather as local copies (parallel/state.initialize_emulated_tensor_parallel)
+        ps.initialize_emulated_tensor_parallel(1, emu)
+    elif not ps.model_parallel_is_initialized():
         ps.initialize_model_parallel(1, 1)
     dev = torch.device("cuda", local) if torch.cuda.is_available() else torch.device("cpu")
     if args is not None:
@@ -372,6 +378,14 @@ class Trainer:
                             # share of the computed tokens (padded, or padding-free rounded up to
                             # 64) that are real input tokens
                             "train_nonpad_fraction": round(float(in_tokens) / max(1, pad_tokens * max(1, self.world)), 4)})
+        st = ps.get_state()
+        if getattr(st, "emulated", False) and st.dp > 1:
+            # one emulated rank of an st.dp-GPU data-parallel job (SMDT_EMULATE_DP): the job's rate
+            # is st.dp times this rank's, plus whatever of the real collectives would not overlap
+            metrics["emulated_dp_ranks"] = st.dp
+            metrics["predicted_job_train_samples_per_second"] = round(st.dp * metrics["train_samples_per_second"], 3)
+            if "train_input_tokens_per_second" in metrics:
+                metrics["predicted_job_input_tokens_per_second"] = round(st.dp * metrics["train_input_tokens_per_second"], 1)
         self.log(metrics)
         self.train_metrics = metrics
         return metrics

@@ -283,6 +283,26 @@ def test_window_that_does_not_fit_runs_micro_batches(tmp_path, monkeypatch):
         torch.testing.assert_close(runs[1][1][k], v, rtol=0, atol=0)
 
 
+def test_emulated_dp_rank_holds_one_shard(tmp_path, monkeypatch):
+    """SMDT_EMULATE_DP=8: one process runs one ZeRO rank of an 8-GPU job (loopback DP group,
+    comm/loopback.py): its gradient / optimizer storage is 1/8 of the model and the metrics name
+    the emulation and the predicted job rate."""
+    monkeypatch.setenv("SMDT_EMULATE_DP", "8")
+    try:
+        t = _tiny_trainer(tmp_path, _trainer_args(tmp_path, max_steps=2, save_steps=0,
+                                                  deepspeed=os.path.join(REPO, "recipes", "4_training_alpaca_deepspeed", "configs", "zero2_bf16.json"),
+                                                  bf16=False))
+        met = t.train()
+        ddp = t.engine.ddp
+        total = sum(p.numel() for p in t.model.parameters())
+        assert ddp.dp == 8 and ddp.grad_memory_numel() <= total / 8 * 1.05 + 4096
+        assert met["emulated_dp_ranks"] == 8
+        assert met["predicted_job_train_samples_per_second"] == pytest.approx(8 * met["train_samples_per_second"], rel=1e-3)
+    finally:
+        from smdt_amd.parallel import state as ps
+        ps.destroy_model_parallel()
+
+
 def test_save_total_limit_rotates(tmp_path):
     t = _tiny_trainer(tmp_path, _trainer_args(tmp_path, save_total_limit=1, save_steps=2))
     t.train()
