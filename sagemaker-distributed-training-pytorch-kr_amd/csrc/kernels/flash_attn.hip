@@ -142,15 +142,15 @@ __device__ __forceinline__ uint32_t half_masks(uint32_t t) {
 __device__ __forceinline__ uint32_t mask_even_slot(uint32_t t) { return half_masks(t << 8); }
 __device__ __forceinline__ uint32_t mask_odd_slot(uint32_t t) { return half_masks(t); }
 // keep bit b of t ? x : y with x, y fp32: v_bfe_i32 (all-ones / zero; only the bfe is asm, left to
-// itself the compiler turns the sign-extend into test + compare + select) and a compiler-visible
-// (x & m) | (y & ~m), which the backend selects as ONE v_bfi_b32. x comes straight out of an MFMA
-// and must be read by a compiler-emitted instruction (inline asm reading an MFMA result is not
-// covered by the hazard padding).
+// itself the compiler turns the sign-extend into test + compare + select) and ONE gfx950
+// v_bitop3_b32 (LUT 0xCA = m ? x : y, bitwise) through its compiler-visible builtin, so the
+// MFMA-result read of x stays inside the compiler's hazard padding. (The former
+// (x & m) | (y & ~m) form compiled to three and / or instructions per element in these loops.)
 template <int b>
 __device__ __forceinline__ float sel_bit(float x, float y, uint32_t t) {
   int32_t m;
   asm("v_bfe_i32 %0, %1, %2, 1" : "=v"(m) : "v"(t), "n"(b));
-  return __int_as_float((__float_as_int(x) & m) | (__float_as_int(y) & ~m));
+  return __uint_as_float(__builtin_amdgcn_bitop3_b32((uint32_t)m, __float_as_uint(x), __float_as_uint(y), 0xCA));
 }
 // AND the four packed pairs of a 16-bit operand fragment with their masks.
 template <class V>
@@ -162,6 +162,33 @@ __device__ __forceinline__ V and_pairs(V x, uint32_t m0, uint32_t m1, uint32_t m
   w[2] &= m2;
   w[3] &= m3;
   return __builtin_bit_cast(V, w);
+}
+
+// A row constant as an MFMA operand (see bwd_dq_kernel): lanes of half 0 hold x as three 16-bit
+// terms in k-slots 0..2 (x - t0 - t1 - t2 below 2^-24 |x| for bf16), half 1 and the other slots 0;
+// rowconst_ones is the matching all-ones operand.
+template <class E>
+__device__ __forceinline__ v8_t<E> rowconst_terms(float x, int h) {
+  v8_t<E> v;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = (E)0.f;
+  if (h == 0) {
+    const E t0 = (E)x;
+    const float r1 = x - (float)t0;
+    const E t1 = (E)r1;
+    const E t2 = (E)(r1 - (float)t1);
+    v[0] = t0;
+    v[1] = t1;
+    v[2] = t2;
+  }
+  return v;
+}
+template <class E>
+__device__ __forceinline__ v8_t<E> rowconst_ones(int h) {
+  v8_t<E> v;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = (E)((h == 0 && j < 3) ? 1.f : 0.f);
+  return v;
 }
 
 // Operand prescale: x * c rounded back to bf16 (one-time, register-resident fragments).
@@ -460,7 +487,7 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void fwd_kernel(const E* __re
 // them for the whole kernel: 178 -> 140 VGPRs, 2 -> 3 waves per SIMD, no spills; measured bwd
 // 1.014 / 1.041 -> 0.991 / 1.004 ms at B64 (profiles/r2_attn_order/ab_b64_dq_remat.log).
 #ifndef SMDT_FA_DQ_REMAT
-#define SMDT_FA_DQ_REMAT 1
+#define SMDT_FA_DQ_REMAT 2
 #endif
 #ifndef SMDT_FA_DKDV_OCC
 #define SMDT_FA_DKDV_OCC 2
@@ -794,7 +821,17 @@ __global__ __launch_bounds__(256, D == 64 ? SMDT_FA_DQ_OCC : 1) void bwd_dq_kern
     DELTA[ridx] = ndl;
     NLSE2[ridx] = nlse2;
   }
-#if SMDT_FA_DQ_REMAT
+#if SMDT_FA_DQ_REMAT == 2
+  // The row constants enter as one extra MFMA k-step per chain: A = 1 in k-slots 0..2 of every
+  // key row, B = the constant of this lane's query split into three 16-bit terms (t0 + t1 + t2
+  // carries ~24 bits of it), so S' / dP' start at c = 1.t0 + 1.t1 + 1.t2 without the 2 x 16 VALU
+  // moves of a per-sub-tile splat and without pinning 32 VGPRs for a resident one: the loops are
+  // VALU-issue-bound (scripts/isa_loop_stats.py), the matrix pipe has room.
+  const v8_t<E> ones3 = rowconst_ones<E>(h);
+  const v8_t<E> lse3 = rowconst_terms<E>(nlse2, h), dl3 = rowconst_terms<E>(ndl, h);
+#define SMDT_DQ_ST0 mfma(ones3, lse3, zero16())
+#define SMDT_DQ_DP0 mfma(ones3, dl3, zero16())
+#elif SMDT_FA_DQ_REMAT
   // the two accumulator splats are re-made per sub-tile (opaque: not hoisted), freeing 32 VGPRs
 #define SMDT_DQ_ST0 splat16(opaque(nlse2))
 #define SMDT_DQ_DP0 splat16(opaque(ndl))
