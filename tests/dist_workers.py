@@ -978,6 +978,8 @@ def smddp_torch_ddp_worker(rank, world, port, outdir):
         ref_m = torch.nn.Sequential(torch.nn.Linear(64, 256), torch.nn.GELU(), torch.nn.Linear(256, 32)).cuda()
         ref_m.load_state_dict(m.state_dict())
         # small buckets: several all-reduces per backward, launched while backward still runs
+        # (DDP's first bucket has its own 1 MiB limit, which would hold this whole model)
+        dist._DEFAULT_FIRST_BUCKET_BYTES = 40 * 1024
         ddp = torch.nn.parallel.DistributedDataParallel(m, bucket_cap_mb=0.04)
         from smdt_amd.comm import stats as cstats
         ok, placement = [], []
