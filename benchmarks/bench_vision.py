@@ -45,6 +45,8 @@ def main():
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     p.add_argument("--channels-last", type=int, default=1)
+    p.add_argument("--ddp", default="smdt", choices=["smdt", "none"],
+                   help="none: the bare module (MIOpen solver diagnosis at one GPU)")
     p.add_argument("--bucket-mb", type=float, default=0.0,
                    help="DDP gradient bucket size in MB of fp32 gradients (0: auto, comm/buckets.py)")
     a = p.parse_args()
@@ -56,7 +58,9 @@ def main():
     zoo.reset_classifier(model, a.num_classes)
     mf = torch.channels_last if (a.channels_last and dev.type == "cuda") else torch.contiguous_format
     bucket = int(a.bucket_mb * 2 ** 20 / 4) if a.bucket_mb > 0 else "auto"
-    model = DDP(model.to(dev, memory_format=mf), torch_compat=True, bucket_size=bucket)
+    model = model.to(dev, memory_format=mf)
+    if a.ddp == "smdt":
+        model = DDP(model, torch_compat=True, bucket_size=bucket)
     crit = nn.CrossEntropyLoss()
     opt = torch.optim.Adam(model.parameters(), lr=1e-4, fused=dev.type == "cuda")
     aug = GpuAugment((a.size, a.size), train=True, channels_last=mf == torch.channels_last)
@@ -110,7 +114,7 @@ def main():
                        "channels_last": bool(a.channels_last), "parallelism": f"dp{world}",
                        "backend": dist.get_backend() if dist.is_initialized() else None,
                        "ddp_bucket": {"elements": model.bucket_size, "count": len(model.buckets),
-                                      "MB": round(model.bucket_size * 4 / 2 ** 20, 2)}},
+                                      "MB": round(model.bucket_size * 4 / 2 ** 20, 2)} if a.ddp == "smdt" else None},
             "vs_reference_per_gpu": round(ips / world / ref, 2) if ref else None,
             "final_loss": float(loss.item())}), flush=True)
     if dist.is_initialized():

@@ -463,7 +463,8 @@ std::vector<Tensor> flash_bwd(Tensor q, Tensor k, Tensor v, Tensor o, Tensor dou
     return torch::empty({B, S, heads, D}, q.options());
   };
   Tensor dq = mk(dq_out, H, "dq"), dk = mk(dk_out, Hkv, "dk"), dv = mk(dv_out, Hkv, "dv");
-  auto delta = torch::empty({2, B, H, S}, q.options().dtype(at::kFloat));  // -delta' | -lse log2 e rows
+  // -delta' rows | (unused) | 16-byte term rows of -lse log2 e and of -delta' (flash_attn.hip)
+  auto delta = torch::empty({10, B, H, S}, q.options().dtype(at::kFloat));
   int64_t st[24];
   const Tensor* ts[8] = {&q, &k, &v, &o, &dout, &dq, &dk, &dv};
   for (int i = 0; i < 8; ++i)

@@ -231,6 +231,29 @@ __device__ __forceinline__ void wait_vm() {
 }
 using lds_void = __attribute__((address_space(3))) void;
 
+// LDS-DMA of `bytes` per lane from a wave-uniform global base + a 32-bit per-lane byte offset,
+// as buffer_load ... lds: the base lives in an SGPR buffer resource, the lane part in ONE VGPR
+// (global_load_lds needs a 64-bit VGPR address per piece, kept live across the loop).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t dma_rsrc(const void* uniform_base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(uniform_base), (short)0, 0x7FFFFFFF, 0x00020000);
+}
+__device__ __forceinline__ void dma_lds16(const void* uniform_base, uint32_t voff, char* lds) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(dma_rsrc(uniform_base), (lds_void*)lds, 16, voff, 0, 0, 0);
+}
+__device__ __forceinline__ void dma_lds4(const void* uniform_base, uint32_t voff, char* lds) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(dma_rsrc(uniform_base), (lds_void*)lds, 4, voff, 0, 0, 0);
+}
+
+// This lane's index, re-made where it is used (2 VALU): asm volatile is never hoisted out of the
+// tile loop, so a lane-derived DMA offset built from it holds no VGPR across the loop (the
+// compiler spilled such loop-invariant offsets of the dK / dV kernel, and each scratch reload in
+// the loop came with an s_waitcnt vmcnt(0) that drained the stage prefetch).
+__device__ __forceinline__ uint32_t lane_now() {
+  uint32_t l;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+  return l;
+}
+
 // LDS-DMA of one 64-row x D bf16 tile into its swizzled Geo<D> image: wave-instruction i writes
 // 1 KB of LDS lane-linearly (rows 1024 / RB * i ..), so lane l lands at (row, slot l % CH) and
 // loads the global chunk whose swizzled position that is: chunk slot ^ f(row).
@@ -238,22 +261,24 @@ template <int D>
 struct GldsTile {
   static constexpr int kRowsPerInst = 1024 / Geo<D>::RB;             // 8 (D = 64) / 4 (D = 128)
   static constexpr int kPerWave = kTile * Geo<D>::RB / 1024 / 4;      // 2 / 4 per wave (4 waves)
-  int off[kPerWave];  // element offset of this lane's chunk from the tile's first row
+  // BYTE offset of this lane's chunk from the tile's first row, unsigned 32-bit: with a
+  // wave-uniform tile base the DMA then uses the SGPR-base + 32-bit VGPR-offset form (a signed /
+  // 64-bit offset kept a VGPR pair per piece alive across the loop, and those were the values the
+  // dK / dV kernel spilled and reloaded — each reload a vmcnt(0) that drained its own prefetch)
+  uint32_t off[kPerWave];
   __device__ __forceinline__ void init(int w, int lane, int64_t row_stride) {
 #pragma unroll
     for (int j = 0; j < kPerWave; ++j) {
       const int i = w * kPerWave + j;
       const int r = i * kRowsPerInst + lane / Geo<D>::CH;
       const int c = (lane % Geo<D>::CH) ^ Geo<D>::f(r);
-      off[j] = (int)(r * row_stride) + 8 * c;
+      off[j] = (uint32_t)(r * row_stride + 8 * c) * 2u;
     }
   }
   template <class E>
   __device__ __forceinline__ void issue(const E* tile_base, char* img, int w) const {
 #pragma unroll
-    for (int j = 0; j < kPerWave; ++j)
-      __builtin_amdgcn_global_load_lds((const void*)(tile_base + off[j]),
-                                       (lds_void*)(img + (w * kPerWave + j) * 1024), 16, 0, 0);
+    for (int j = 0; j < kPerWave; ++j) dma_lds16(tile_base, off[j], img + (w * kPerWave + j) * 1024);
   }
 };
 
@@ -492,17 +517,33 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void fwd_kernel(const E* __re
 #ifndef SMDT_FA_DKDV_OCC
 #define SMDT_FA_DKDV_OCC 2
 #endif
+#ifndef SMDT_FA_DKDV_STRAIGHT
+#define SMDT_FA_DKDV_STRAIGHT 0
+#endif
 template <int D, bool CAUSAL, bool DROP, class E>
 __global__ __launch_bounds__(256, D == 64 ? SMDT_FA_DKDV_OCC : 1) void bwd_dkdv_kernel(
     const E* __restrict__ Q, const E* __restrict__ K, const E* __restrict__ V,
-    const E* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ DELTA,
-    E* __restrict__ dK, E* __restrict__ dV, int B, int H, int Hkv, int S, Strides qs,
-    Strides ks_, Strides vs, Strides dos, Strides dks, Strides dvs, float scale, Drop drop) {
+    const E* __restrict__ dO, const E* __restrict__ LSE3, const E* __restrict__ DL3,
+    const float* __restrict__ DELTA, E* __restrict__ dK, E* __restrict__ dV, int B, int H, int Hkv, int S,
+    Strides qs, Strides ks_, Strides vs, Strides dos, Strides dks, Strides dvs, float scale, Drop drop) {
   using G = Geo<D>;
-  constexpr int BUF = 2 * G::TB + 2 * kTile * 4;  // Q | dO | lse | delta (raw rows)
-  // D = 64: three stage buffers, two work items in flight; D = 128: two (LDS budget).
+  using VF = v8_t<E>;
+  // Q | dO | the tile's 64 query rows of the row constants as 16-bit term rows (16 B each, written
+  // by the dQ kernel: -(lse log2e - log2 inv), then -delta') | -delta' fp32 (dropout only)
+  constexpr int kRC = kTile * 16;
+  constexpr int RCB = 2 * kRC + kTile * 4;
+  // D = 64: three stage slots, two work items in flight; D = 128: two (LDS budget). Q, dO and the
+  // row constants of a slot are SEPARATE __shared__ objects: with one object per slot the compiler
+  // drained the DMA queue (s_waitcnt vmcnt(0)) between the Q and the dO pieces of every item,
+  // i.e. it waited for the prefetch it had just issued (round-3 listing); the forward kernel's
+  // K | V slots had no such drain.
   constexpr int kBuf = D == 64 ? 3 : 2;
-  __shared__ __attribute__((aligned(16))) char L0[BUF], L1[BUF], L2[kBuf == 3 ? BUF : 16];
+  __shared__ __attribute__((aligned(16))) char Q0[G::TB], Q1[G::TB], Q2[kBuf == 3 ? G::TB : 16];
+  __shared__ __attribute__((aligned(16))) char O0[G::TB], O1[G::TB], O2[kBuf == 3 ? G::TB : 16];
+  __shared__ __attribute__((aligned(16))) char R0[RCB], R1[RCB], R2[kBuf == 3 ? RCB : 16];
+  auto qbuf = [&](int sl) -> char* { return sl == 0 ? Q0 : sl == 1 ? Q1 : Q2; };
+  auto obuf = [&](int sl) -> char* { return sl == 0 ? O0 : sl == 1 ? O1 : O2; };
+  auto rbuf = [&](int sl) -> char* { return sl == 0 ? R0 : sl == 1 ? R1 : R2; };
 
   const int lane = threadIdx.x & 63, h = lane >> 5;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: diagonal tests branch on SCC
@@ -537,6 +578,7 @@ __global__ __launch_bounds__(256, D == 64 ? SMDT_FA_DKDV_OCC : 1) void bwd_dkdv_
   v8_t<E> kf[G::KS], vf[G::KS];
   load_reg_frags<D>(K + b * ks_.sb + hk * ks_.sh, ks_.ss, kw, lane, kf);
   load_reg_frags<D>(V + b * vs.sb + hk * vs.sh, vs.ss, kw, lane, vf);
+  const VF ones3 = rowconst_ones<E>(h);
 #pragma unroll
   for (int kk = 0; kk < G::KS; ++kk) kf[kk] = scale8(kf[kk], scale * kLog2e);  // S in log2 domain
 
@@ -557,17 +599,19 @@ __global__ __launch_bounds__(256, D == 64 ? SMDT_FA_DKDV_OCC : 1) void bwd_dkdv_
   gdo.init(w, lane, dos.ss);
   constexpr int kPer = 2 * GldsTile<D>::kPerWave;
   int ih_n = 0, iq_n = 0, issued = 0;  // next work item to stream in
-  auto issue = [&](char* buf) {
-    // every call issues one item's DMA (past the end: the last item again, into a buffer nobody
+  auto issue = [&](int sl) {
+    // every call issues one item's DMA (past the end: the last item again, into a slot nobody
     // reads), so the counted waits stay uniform
     const int ih = issued < total ? ih_n : group - 1, iq = issued < total ? iq_n : ntiles - 1;
     const int hq = hk * group + ih;
     const int qb = qstart + iq * kTile;
-    gq.issue(Q + b * qs.sb + hq * qs.sh + (int64_t)qb * qs.ss, buf, w);
-    gdo.issue(dO + b * dos.sb + hq * dos.sh + (int64_t)qb * dos.ss, buf + G::TB, w);
+    gq.issue(Q + b * qs.sb + hq * qs.sh + (int64_t)qb * qs.ss, qbuf(sl), w);
+    gdo.issue(dO + b * dos.sb + hq * dos.sh + (int64_t)qb * dos.ss, obuf(sl), w);
+    const int64_t r0 = ((int64_t)b * H + hq) * S + qb;
     if (w < 2) {
-      const float* row = (w == 0 ? LSE : DELTA) + ((int64_t)b * H + hq) * S + qb;
-      __builtin_amdgcn_global_load_lds((const void*)(row + lane), (lds_void*)(buf + 2 * G::TB + w * kTile * 4), 4, 0, 0);
+      dma_lds16((w == 0 ? LSE3 : DL3) + r0 * 8, lane_now() << 4, rbuf(sl) + w * kRC);
+    } else if (DROP && w == 2) {
+      dma_lds4(DELTA + r0, lane_now() << 2, rbuf(sl) + 2 * kRC);
     }
     ++issued;
     if (++iq_n == ntiles) {
@@ -576,13 +620,13 @@ __global__ __launch_bounds__(256, D == 64 ? SMDT_FA_DKDV_OCC : 1) void bwd_dkdv_
     }
   };
   auto wait_next = [&]() {  // the next item's DMA has landed (a later one may still be in flight)
-    if (w < 2) wait_vm<(kBuf - 2) * (kPer + 1)>();
+    if (w < 2 || (DROP && w == 2)) wait_vm<(kBuf - 2) * (kPer + 1)>();
     else wait_vm<(kBuf - 2) * kPer>();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
   };
-  issue(L0);
-  if constexpr (kBuf == 3) issue(L1);
+  issue(0);
+  if constexpr (kBuf == 3) issue(1);
   wait_next();
 
   const uint32_t shalf = (uint32_t)S >> 1;
@@ -595,31 +639,31 @@ __global__ __launch_bounds__(256, D == 64 ? SMDT_FA_DKDV_OCC : 1) void bwd_dkdv_
   // exponential (exp2(-1e30) = 0). Only the diagonal items build that pattern (sd_init), so it
   // holds no registers in the main loop.
   int ch = 0, cq = 0;  // current work item
-  auto item = [&](const char* buf, char* pre) {
+  auto item = [&](int cur, int pre) {
     const int qb = qstart + cq * kTile;
     const uint32_t dkey = DROP ? drop_key(drop, b * H + hk * group + ch) : 0u;
     const uint32_t dblk = ((uint32_t)((qb + 4 * h) >> 1) + (uint32_t)(my_key & 1)) * shalf + (uint32_t)(my_key >> 1);
-    const char* q_l = buf;
-    const char* do_l = buf + G::TB;
-    const float* lse_l = reinterpret_cast<const float*>(buf + 2 * G::TB);
-    const float* del_l = lse_l + kTile;
+    const char* q_l = qbuf(cur);
+    const char* do_l = obuf(cur);
+    const char* lse3_l = rbuf(cur);
+    const char* dl3_l = lse3_l + kRC;
+    const float* del_l = reinterpret_cast<const float*>(dl3_l + kRC);
     issue(pre);
     // S'[q, key] = Q . K'^T - lse ; dP'[q, key] = dO . V^T - delta  (key on lane, query rows in
-    // registers): the row constants (prepared by the dQ kernel: -(lse log2e - log2 inv) and
-    // -delta') are the accumulators' initial values, read straight from LDS.
-    auto sd_init = [&](int qs2, bool diag, f32x16& sa, f32x16& pa) {
+    // registers). The row constants enter as one MFMA k-step ahead of each chain (A = the query
+    // row's three 16-bit terms from LDS, B = ones in k-slots 0..2; half 1's A values meet B's
+    // zeros): no accumulator moves. The causal diagonal block masks key > query after the chain.
+    auto sd_init = [&](int qs2, f32x16& sa, f32x16& pa) {
+      const int r = 32 * qs2 + (lane & 31);
+      sa = mfma(*reinterpret_cast<const VF*>(lse3_l + 16 * r), ones3, zero16());
+      pa = mfma(*reinterpret_cast<const VF*>(dl3_l + 16 * r), ones3, zero16());
+    };
+    auto diag_mask = [&](f32x16& sa) {
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int r0 = 32 * qs2 + 8 * g + 4 * h;  // 4 consecutive query rows of this group
-        const f32x4 lv = *reinterpret_cast<const f32x4*>(lse_l + r0);
-        const f32x4 dl = *reinterpret_cast<const f32x4*>(del_l + r0);
+      for (int g = 0; g < 4; ++g)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          sa[4 * g + j] = lv[j];
-          if (CAUSAL && diag && (lane & 31) > 8 * g + 4 * h + j) sa[4 * g + j] = -1e30f;
-          pa[4 * g + j] = dl[j];  // dP' = dP - delta' (dropped entries select -delta' below)
-        }
-      }
+        for (int j = 0; j < 4; ++j)
+          if ((lane & 31) > 8 * g + 4 * h + j) sa[4 * g + j] = -1e30f;
     };
     auto sd_mma = [&](int qs2, f32x16& sa, f32x16& pa) {
 #pragma unroll
@@ -682,19 +726,34 @@ __global__ __launch_bounds__(256, D == 64 ? SMDT_FA_DKDV_OCC : 1) void bwd_dkdv_
         }
     };
     if (!CAUSAL || qb >= kw + 32) {
+#if SMDT_FA_DKDV_STRAIGHT
       // Both 32-query halves fully visible (every item but the causal diagonal ones): one block
       // of straight-line code whose two halves are independent, so the scheduler overlaps the
       // softmax VALU of one half with the other half's MFMAs.
       f32x16 s0, p0, s1, p1;
       v8_t<E> pb0[2], db0[2], pb1[2], db1[2];
-      sd_init(0, false, s0, p0);
-      sd_init(1, false, s1, p1);
+      sd_init(0, s0, p0);
+      sd_init(1, s1, p1);
       sd_mma(0, s0, p0);
       sd_mma(1, s1, p1);
       softmax_ds(0, s0, p0, pb0, db0);
       acc_mma(0, pb0, db0);
       softmax_ds(1, s1, p1, pb1, db1);
       acc_mma(1, pb1, db1);
+#else
+      // the two 32-query halves one after the other: 48 fewer live VGPRs than straight-line code
+      // (which spilled at 256 VGPRs once the row constants entered as MFMA operands); the
+      // partner wave on the SIMD supplies the overlap of softmax VALU and MFMAs
+#pragma unroll
+      for (int qs2 = 0; qs2 < 2; ++qs2) {
+        f32x16 sa, pa;
+        v8_t<E> pb[2], db[2];
+        sd_init(qs2, sa, pa);
+        sd_mma(qs2, sa, pa);
+        softmax_ds(qs2, sa, pa, pb, db);
+        acc_mma(qs2, pb, db);
+      }
+#endif
     } else {
 #pragma unroll
       for (int qs2 = 0; qs2 < 2; ++qs2) {
@@ -702,8 +761,9 @@ __global__ __launch_bounds__(256, D == 64 ? SMDT_FA_DKDV_OCC : 1) void bwd_dkdv_
         if (qsub + 31 < kw) continue;  // all queries precede all of this wave's keys
         f32x16 sa, pa;
         v8_t<E> pb[2], db[2];
-        sd_init(qs2, qsub == kw, sa, pa);   // the diagonal block folds its mask in
+        sd_init(qs2, sa, pa);
         sd_mma(qs2, sa, pa);
+        if (qsub == kw) diag_mask(sa);      // the diagonal block: key > query is masked
         softmax_ds(qs2, sa, pa, pb, db);
         acc_mma(qs2, pb, db);
       }
@@ -716,14 +776,14 @@ __global__ __launch_bounds__(256, D == 64 ? SMDT_FA_DKDV_OCC : 1) void bwd_dkdv_
   };
   if constexpr (kBuf == 3) {
     for (int it = 0; it < total; it += 3) {
-      item(L0, L2);
-      if (it + 1 < total) item(L1, L0);
-      if (it + 2 < total) item(L2, L1);
+      item(0, 2);
+      if (it + 1 < total) item(1, 0);
+      if (it + 2 < total) item(2, 1);
     }
   } else {
     for (int it = 0; it < total; it += 2) {
-      item(L0, L1);
-      if (it + 1 < total) item(L1, L0);
+      item(0, 1);
+      if (it + 1 < total) item(1, 0);
     }
   }
   wait_vm<0>();  // drain the trailing re-reads before the workgroup's LDS is released
@@ -755,7 +815,7 @@ template <int D, bool CAUSAL, bool DROP, class E>
 __global__ __launch_bounds__(256, D == 64 ? SMDT_FA_DQ_OCC : 1) void bwd_dq_kernel(
     const E* __restrict__ Q, const E* __restrict__ K, const E* __restrict__ V,
     const E* __restrict__ dO, const E* __restrict__ O, const float* __restrict__ LSE,
-    float* __restrict__ DELTA, float* __restrict__ NLSE2, E* __restrict__ dQ, int B, int H, int Hkv,
+    float* __restrict__ DELTA, E* __restrict__ LSE3, E* __restrict__ DL3, E* __restrict__ dQ, int B, int H, int Hkv,
     int S, Strides qs, Strides ks_, Strides vs, Strides dos, Strides os, Strides dqs, float scale,
     float dscale, float lsub, Drop drop) {
   using G = Geo<D>;
@@ -817,9 +877,10 @@ __global__ __launch_bounds__(256, D == 64 ? SMDT_FA_DQ_OCC : 1) void bwd_dq_kern
     ndl = -xhalf_sum(acc) * dscale;
   }
   const float nlse2 = lsub - LSE[ridx] * kLog2e;
-  if (h == 0) {
+  if (h == 0) {   // for the dK / dV kernel: fp32 -delta' (dropout path) and both as term rows
     DELTA[ridx] = ndl;
-    NLSE2[ridx] = nlse2;
+    *reinterpret_cast<v8_t<E>*>(LSE3 + ridx * 8) = rowconst_terms<E>(nlse2, 0);
+    *reinterpret_cast<v8_t<E>*>(DL3 + ridx * 8) = rowconst_terms<E>(ndl, 0);
   }
 #if SMDT_FA_DQ_REMAT == 2
   // The row constants enter as one extra MFMA k-step per chain: A = 1 in k-slots 0..2 of every
@@ -1030,9 +1091,12 @@ extern "C" hipError_t smdt_flash_bwd(int dtype, const void* q, const void* k, co
       vs{strides[6], strides[7], strides[8]}, os{strides[9], strides[10], strides[11]},
       dos{strides[12], strides[13], strides[14]}, dqs{strides[15], strides[16], strides[17]},
       dks{strides[18], strides[19], strides[20]}, dvs{strides[21], strides[22], strides[23]};
-  // delta holds 2 x [B, H, S]: -delta' rows, then -(lse log2e - log2 inv) rows, both written by
-  // the dQ kernel (which therefore runs first) and read by the dK / dV kernel
-  float* nlse2 = delta + (int64_t)B * H * S;
+  // delta holds 10 x [B, H, S] fp32 words, written by the dQ kernel (which therefore runs first)
+  // and read by the dK / dV kernel: -delta' rows, then (after one unused [B, H, S] slot) the
+  // 16-byte term rows of -(lse log2e - log2 inv) and of -delta' (see rowconst_terms)
+  const int64_t bhs = (int64_t)B * H * S;
+  void* lse3 = delta + 2 * bhs;
+  void* dl3 = delta + 6 * bhs;
   const float dscale = drop ? dr.keep : 1.f, lsub = drop ? dr.log2inv : 0.f;
   dim3 gkv((unsigned)((int64_t)B * Hkv * (S / kBlockRows)));
   dim3 gq((unsigned)((int64_t)B * H * (S / kBlockRows)));
@@ -1040,11 +1104,12 @@ extern "C" hipError_t smdt_flash_bwd(int dtype, const void* q, const void* k, co
   do {                                                                                           \
     hipLaunchKernelGGL((bwd_dq_kernel<DD, CC, DR, ET>), gq, dim3(256), 0, st, (const ET*)q,     \
                        (const ET*)k, (const ET*)v, (const ET*)dout, (const ET*)o, lse, delta,     \
-                       nlse2, (ET*)dq, B, H, Hkv, S, qs, ks, vs, dos, os, dqs, scale, dscale,     \
-                       lsub, dr);                                                                 \
+                       (ET*)lse3, (ET*)dl3, (ET*)dq, B, H, Hkv, S, qs, ks, vs, dos, os, dqs,      \
+                       scale, dscale, lsub, dr);                                                  \
     hipLaunchKernelGGL((bwd_dkdv_kernel<DD, CC, DR, ET>), gkv, dim3(256), 0, st, (const ET*)q,  \
-                       (const ET*)k, (const ET*)v, (const ET*)dout, nlse2, delta, (ET*)dk,        \
-                       (ET*)dv, B, H, Hkv, S, qs, ks, vs, dos, dks, dvs, scale, dr);              \
+                       (const ET*)k, (const ET*)v, (const ET*)dout, (const ET*)lse3,              \
+                       (const ET*)dl3, delta, (ET*)dk, (ET*)dv, B, H, Hkv, S, qs, ks, vs, dos,    \
+                       dks, dvs, scale, dr);                                                      \
   } while (0)
 #define SMDT_FA_BWD(DD, CC, DR) \
   do { if (dtype == 2) SMDT_FA_BWD_T(DD, CC, DR, f16); else SMDT_FA_BWD_T(DD, CC, DR, bf16); } while (0)

@@ -90,22 +90,17 @@ struct Glds {
 // tile measured +1.7 % on the grouped microbenchmark and neutral-to-slower in the training step,
 // profiles/r3_wgrad16/: the kernel is bound by its LDS-DMA operand stream, not by the MFMA clock;
 // it was removed.)
-// Sum of the 8 16-bit values of an operand fragment, in fp32.
-template <class V>
-__device__ __forceinline__ float sum8(V x) {
-  float s = 0.f;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) s += (float)x[j];
-  return s;
-}
 
-// ``bias`` (optional, k0 == 0 tiles only): bias[n0 + r] += sum over this tile's m range of
-// A[m, n0 + r] — the bias gradient of the linear whose weight gradient this is, taken from the A
-// (dY) fragments the MFMAs read anyway. Wave (wn, wk) sums its A fragment i == wk (all four wk
-// waves of a wn read the same A fragments), so every column of the tile is summed by exactly one
-// lane pair: ~2 VALU per MFMA, no extra pass over dY (this replaces the
-// col_sum_rows + col_partials_reduce kernels).
-template <bool ATOMIC, int VAR, class E>
+// BIAS (the k0 == 0 tiles of a problem with a bias): bias[n0 + r] += sum over this tile's m range
+// of A[m, n0 + r] — the bias gradient of the linear whose weight gradient this is, taken from the
+// A (dY) fragments the MFMAs read anyway. Wave (wn, wk) multiplies its fragment i == wk (all four
+// wk waves of a wn read the same A fragments) by an all-ones B operand: ONE extra MFMA per 8 on
+// these tiles and no VALU (replaces the col_sum_rows + col_partials_reduce
+// kernels). A fp32 VALU sum of the fragment instead (round-4 first form) was if-converted by the
+// compiler into sums of all four fragments on every tile: 13.6 -> 22.9 VALU per MFMA in the loop
+// and 35.8 -> 45.0 ms of grouped wgrad per GPT-2 345M step (profiles/r4_wgrad_bias/). Tiles
+// without a bias run the BIAS = false instantiation, i.e. the round-3 loop.
+template <bool ATOMIC, int VAR, bool BIAS, class E>
 __device__ __forceinline__ void tile_gemm(const E* __restrict__ A, const E* __restrict__ B,
                                           float* __restrict__ C, int N, int K, int n0, int k0, int64_t mstart,
                                           int nst, char* L0, char* L1, char* L2, char* L3,
@@ -130,8 +125,11 @@ __device__ __forceinline__ void tile_gemm(const E* __restrict__ A, const E* __re
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = zero16();
-  const bool do_bias = bias != nullptr && k0 == 0;   // wave-uniform
-  float cs = 0.f;                                     // column sum of A[., n0 + 128 wn + 32 wk + lane & 31]
+  // BIAS: column sums of A over the fragment i == wk, replicated in every column of accb
+  f32x16 accb = zero16();
+  V ones;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ones[j] = (E)1.f;
 
   Glds ga, gb;
   ga.init(wave, lane, N, n0, N);
@@ -177,7 +175,9 @@ __device__ __forceinline__ void tile_gemm(const E* __restrict__ A, const E* __re
         else a = F::trf_at(at, 0, ks, oa[i][0], oa[i][1]);
         acc[i][0] = mfma(a, b0, acc[i][0]);
         acc[i][1] = mfma(a, b1, acc[i][1]);
-        if (do_bias && i == wk) cs += sum8(a);
+        if constexpr (BIAS) {
+          if (i == wk) accb = mfma(a, ones, accb);  // wk is wave-uniform: a scalar branch
+        }
       }
     }
     // Stages s+2 .. s+kNBuf-1 stay in flight; stage s+1 must have landed.
@@ -197,13 +197,17 @@ __device__ __forceinline__ void tile_gemm(const E* __restrict__ A, const E* __re
   if (s + 2 < nst) stage(s + 2, L2, L1);
   wait_vm<0>();  // drain the trailing re-reads before the workgroup's LDS is released
 
-  if (do_bias) {
-    // lanes l and l ^ 32 summed the two 8-row halves of each 16-row k-step of one column
-    cs = __shfl_xor(cs, 32, 64) + cs;
-    const int n = n0 + 128 * wn + 32 * wk + (lane & 31);
-    if (h == 0 && n < N) {
-      if constexpr (ATOMIC) unsafeAtomicAdd(bias + n, cs);
-      else bias[n] += cs;
+  if constexpr (BIAS) {
+    // register r holds the sum of fragment row acc_row(r, h) (every column alike): lane c < 16 of
+    // each half stores row acc_row(c, h)
+    const int c = lane & 31;
+    float v = accb[0];
+#pragma unroll
+    for (int r = 1; r < 16; ++r) v = c == r ? accb[r] : v;
+    const int n = n0 + 128 * wn + 32 * wk + acc_row(c & 15, h);
+    if (c < 16 && n < N) {
+      if constexpr (ATOMIC) unsafeAtomicAdd(bias + n, v);
+      else bias[n] += v;
     }
   }
 
@@ -278,7 +282,7 @@ __global__ __launch_bounds__(kThreads, 1) void wgrad_kernel(const E* __restrict_
   tile_coords(w - split * tiles, ntn, ntk, gn, tn, tk);
   const int mstart = split * m_per_split;
   const int nst = (min(M, mstart + m_per_split) - mstart) / BM;
-  tile_gemm<ATOMIC, VAR, E>(A, B, C, N, K, tn * BT, tk * BT, mstart, nst, L0, L1, L2, L3);
+  tile_gemm<ATOMIC, VAR, false, E>(A, B, C, N, K, tn * BT, tk * BT, mstart, nst, L0, L1, L2, L3);
 }
 
 struct Problem {
@@ -324,15 +328,22 @@ __global__ __launch_bounds__(kThreads, 1) void wgrad_grouped_kernel(const Group 
   int tn, tk;
   tile_coords(w - P.tile0, P.ntn, P.ntk, P.gn, tn, tk);
   const int stages = P.M / BM;
+  const bool bias_tile = P.bias != nullptr && tk == 0;
+  const E* A = (const E*)P.A;
+  const E* B = (const E*)P.B;
   if (piece < 0) {
-    tile_gemm<false, 0, E>((const E*)P.A, (const E*)P.B, P.C, P.N, P.K, tn * BT, tk * BT, 0, stages, L0, L1,
-                           L2, L3, P.bias);
+    if (bias_tile)
+      tile_gemm<false, 0, true, E>(A, B, P.C, P.N, P.K, tn * BT, 0, 0, stages, L0, L1, L2, L3, P.bias);
+    else
+      tile_gemm<false, 0, false, E>(A, B, P.C, P.N, P.K, tn * BT, tk * BT, 0, stages, L0, L1, L2, L3);
   } else {
     const int s0 = piece * g.mps;
     const int nst = min(stages, s0 + g.mps) - s0;
     if (nst <= 0) return;  // a smaller-M problem in the tail: nothing left for this piece (whole block exits)
-    tile_gemm<true, 0, E>((const E*)P.A, (const E*)P.B, P.C, P.N, P.K, tn * BT, tk * BT, (int64_t)s0 * BM,
-                          nst, L0, L1, L2, L3, P.bias);
+    if (bias_tile)
+      tile_gemm<true, 0, true, E>(A, B, P.C, P.N, P.K, tn * BT, 0, (int64_t)s0 * BM, nst, L0, L1, L2, L3, P.bias);
+    else
+      tile_gemm<true, 0, false, E>(A, B, P.C, P.N, P.K, tn * BT, tk * BT, (int64_t)s0 * BM, nst, L0, L1, L2, L3);
   }
 }
 

@@ -200,7 +200,11 @@ def zero_sft_worker(rank, world, stage, ga, steps, offload=False, offload_param=
     init_stats = {"peak_bytes": ctx.peak_bytes, "shard_bytes": ctx.shard_bytes, "params": ctx.params,
                   "largest_param_bytes": ctx.largest_param_bytes,
                   "resident_bytes_after_build": sum(p.numel() * p.element_size() for p in m.parameters())}
-    cfg = {"optimizer": {"type": "AdamW", "params": {"lr": 1e-3, "betas": [0.9, 0.99], "eps": 1e-8,
+    # eps 1e-6 (DeepSpeed's default is 1e-8): with ga > 1 the sharded run sums a rank's micro-batch
+    # gradients before the reduce-scatter, single-rank accumulation sums them in sequence — 1 ulp
+    # apart, which flips the sign of a gradient element within ~1e-9 of zero; at eps 1e-8 that flip
+    # moved Adam's update by up to ~0.2 lr (a rare full-suite flake), at 1e-6 by < 1e-3 lr
+    cfg = {"optimizer": {"type": "AdamW", "params": {"lr": 1e-3, "betas": [0.9, 0.99], "eps": 1e-6,
                                                      "weight_decay": 0.1}},
            "gradient_accumulation_steps": ga, "gradient_clipping": 1.0,
            "zero_optimization": {"stage": stage, **({"offload_optimizer": {"device": "cpu"}} if offload else {}),
@@ -974,27 +978,40 @@ def smddp_torch_ddp_worker(rank, world, port, outdir):
         torch.cuda.set_device(0)
         dist.init_process_group("smddp", rank=rank, world_size=world)
         torch.manual_seed(0)
-        m = torch.nn.Sequential(torch.nn.Linear(64, 256), torch.nn.GELU(), torch.nn.Linear(256, 32)).cuda()
-        ref_m = torch.nn.Sequential(torch.nn.Linear(64, 256), torch.nn.GELU(), torch.nn.Linear(256, 32)).cuda()
+        def mlp():
+            return torch.nn.Sequential(torch.nn.Linear(64, 256), torch.nn.GELU(), torch.nn.Linear(256, 256),
+                                       torch.nn.GELU(), torch.nn.Linear(256, 256), torch.nn.GELU(),
+                                       torch.nn.Linear(256, 32)).cuda()
+        m = mlp()
+        m_one = mlp()
+        ref_m = mlp()
         ref_m.load_state_dict(m.state_dict())
-        # small buckets: several all-reduces per backward, launched while backward still runs
-        # (DDP's first bucket has its own 1 MiB limit, which would hold this whole model)
-        dist._DEFAULT_FIRST_BUCKET_BYTES = 40 * 1024
-        ddp = torch.nn.parallel.DistributedDataParallel(m, bucket_cap_mb=0.04)
+        m_one.load_state_dict(m.state_dict())
+        # Two torch DDP wrappers of the same module: (a) small buckets, several all-reduces per
+        # backward launched while backward still runs — torch 2.10's DDP splits by bucket_cap_mb
+        # only with find_unused_parameters, whose unused-parameter scan itself syncs the host, so
+        # (b) a default wrapper (one bucket) runs the steps under torch.cuda.set_sync_debug_mode
+        # ("error"): any host sync in the smddp hook path raises there.
+        ddp_multi = torch.nn.parallel.DistributedDataParallel(m, bucket_cap_mb=0.04, find_unused_parameters=True)
+        ddp_one = torch.nn.parallel.DistributedDataParallel(m_one)
         from smdt_amd.comm import stats as cstats
         ok, placement = [], []
-        for step in range(4):
+        for step in range(6):
+            ddp, mod, strict = (ddp_multi, m, False) if step < 4 else (ddp_one, m_one, True)
             x = torch.randn(16, 64, generator=torch.Generator().manual_seed(10 * step + rank)).cuda()
-            m.zero_grad()
-            if step >= 2:            # steady state (bucket rebuild and the engine build are over)
+            mod.zero_grad()
+            measured = step in (2, 3, 5)      # steady state (bucket rebuild and the engine build are over)
+            if measured:
+                torch.cuda.synchronize()
                 cstats.enable(True)
                 S._TIMINGS.clear()
-                torch.cuda.set_sync_debug_mode("error")   # any host sync in the hook path raises
+                if strict:
+                    torch.cuda.set_sync_debug_mode("error")
                 b0 = torch.cuda.Event(enable_timing=True)
                 b1 = torch.cuda.Event(enable_timing=True)
                 b0.record()
             ddp(x).square().mean().backward()
-            if step >= 2:
+            if measured:
                 b1.record()
                 torch.cuda.set_sync_debug_mode(0)
                 cstats.enable(False)
@@ -1003,10 +1020,10 @@ def smddp_torch_ddp_worker(rank, world, port, outdir):
                 starts = [b0.elapsed_time(a) for a, _ in S._TIMINGS]
                 placement.append({"n": len(S._TIMINGS), "engine_stream": pg._engine._stream != torch.cuda.current_stream(),
                                   "first_start_ms": min(starts) if starts else None,
-                                  "backward_ms": b0.elapsed_time(b1)})
+                                  "backward_ms": b0.elapsed_time(b1), "sync_checked": strict})
             ref_m.zero_grad()
             ref_m(x).square().mean().backward()
-            for p, q in zip(m.parameters(), ref_m.parameters()):
+            for p, q in zip(mod.parameters(), ref_m.parameters()):
                 mean = q.grad.cpu()
                 dist.all_reduce(mean)            # a CPU tensor: the Gloo path of the smddp group
                 ok.append(bool(torch.allclose(p.grad.cpu(), mean / world, atol=1e-5, rtol=1e-4)))

@@ -155,7 +155,8 @@ def _adam_close(got, ref, steps, what, lr=1e-3):
     """Parameters after ``steps`` AdamW steps agree elementwise at rtol 2e-4 / atol 2e-5. The
     gradient norm (hence the clip coefficient) is accumulated in fp64 (optim/optimizer._sumsq), so
     it does not depend on how the gradient is split into ZeRO shards; what remains between a sharded
-    run and single-rank accumulation is the association of the micro-batch gradient sums (1 ulp)."""
+    run and single-rank accumulation is the association of the micro-batch gradient sums (1 ulp),
+    which the workers' Adam eps keeps from flipping near-zero updates (dist_workers.zero_sft_worker)."""
     torch.testing.assert_close(got, ref, rtol=2e-4, atol=2e-5, msg=str(what))
 
 

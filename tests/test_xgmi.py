@@ -238,12 +238,13 @@ def test_smddp_backend_torch_ddp_takes_xgmi_path():
                 out.append(pickle.load(f))
     for r, res in enumerate(out):
         assert res["err"] is None, f"rank {r}:\n{res['err']}"
-        assert res["backend"] == "smddp" and all(res["ok"]) and len(res["ok"]) == 16, (r, res)
-        assert res["stats"]["xgmi_calls"] >= 8 and res["error_word"] == 0, (r, res)
+        assert res["backend"] == "smddp" and all(res["ok"]) and len(res["ok"]) == 48, (r, res)
+        assert res["stats"]["xgmi_calls"] >= 10 and res["error_word"] == 0, (r, res)
+        assert [pl["sync_checked"] for pl in res["placement"]] == [False, False, True], (r, res)
         for pl in res["placement"]:
-            # several buckets per backward, all on the engine's own stream, the first one issued
-            # before backward returned (overlap), no host sync in the hook path (sync debug mode)
-            assert pl["n"] >= 2 and pl["engine_stream"], (r, pl)
+            # every bucket all-reduce on the engine's own stream, the first one issued before
+            # backward returned; several buckets per backward with the small-bucket wrapper
+            assert pl["engine_stream"] and pl["n"] >= (1 if pl["sync_checked"] else 2), (r, pl)
             assert pl["first_start_ms"] is not None and pl["first_start_ms"] < pl["backward_ms"], (r, pl)
 
 
