@@ -15,8 +15,10 @@ ranks. The reference published ~1,429 img/s for swin_b fp32 128x128 on 16x V100 
 NB2:3333 corrected for its log_interval division).
 """
 import argparse
+import itertools
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -28,7 +30,7 @@ import torch.distributed as dist  # noqa: E402
 import torch.nn as nn  # noqa: E402
 
 from smdt_amd.comm import init_distributed  # noqa: E402
-from smdt_amd.data.image_folder import GpuAugment  # noqa: E402
+from smdt_amd.data.image_folder import AugmentPrefetcher, GpuAugment  # noqa: E402
 from smdt_amd.models import zoo  # noqa: E402
 from smdt_amd.parallel.distributed import DistributedDataParallel as DDP  # noqa: E402
 
@@ -49,7 +51,29 @@ def main():
                    help="none: the bare module (MIOpen solver diagnosis at one GPU)")
     p.add_argument("--bucket-mb", type=float, default=0.0,
                    help="DDP gradient bucket size in MB of fp32 gradients (0: auto, comm/buckets.py)")
+    p.add_argument("--prefetch", type=int, default=1,
+                   help="augment the next batches on a side stream in a background thread "
+                        "(data/image_folder.AugmentPrefetcher); 0: in line with the step")
+    p.add_argument("--miopen-prewarm", type=int, default=1,
+                   help="before timing, run 13 steps in a child process so MIOpen's find database and "
+                        "kernel cache exist: on a fresh box the first process of a model ran 418-540 ms "
+                        "per ResNet-50 step for its whole life and the next ones 31-48 ms (a 2-step child "
+                        "was not enough: the process after it was still slow), profiles/r4_vision/")
     a = p.parse_args()
+    # (device_count() does not initialise the GPU in this process)
+    if (a.miopen_prewarm and torch.cuda.device_count() > 0 and os.environ.get("LOCAL_RANK", "0") == "0"
+            and not os.environ.get("SMDT_VISION_PREWARM")):
+        # a child process, started before this one touches the GPU
+        cmd = [sys.executable, os.path.abspath(__file__), "--model", a.model, "--size", str(a.size),
+               "--batch", str(a.batch), "--steps", "10", "--warmup", "3", "--dtype", a.dtype,
+               "--channels-last", str(a.channels_last), "--ddp", "none", "--prefetch", "0", "--miopen-prewarm", "0"]
+        env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE",
+                                                                 "MASTER_ADDR", "MASTER_PORT")}
+        env["SMDT_VISION_PREWARM"] = "1"
+        t = time.perf_counter()
+        r = subprocess.run(cmd, env=env, capture_output=True, text=True)
+        print(f"[bench_vision] MIOpen prewarm process: rc {r.returncode}, {time.perf_counter() - t:.1f}s",
+              file=sys.stderr, flush=True)
     rank, local, world, _ = init_distributed("nccl")
     dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
     torch.manual_seed(0)
@@ -72,8 +96,10 @@ def main():
     tgt = torch.randint(0, a.num_classes, (a.batch,), device=dev)
     bf16 = a.dtype == "bf16"
 
+    batches = iter(AugmentPrefetcher(itertools.repeat((src, tgt)), aug, dev, gen)) if a.prefetch else None
+
     def step():
-        x = aug(src, gen)
+        x = next(batches)[0] if batches is not None else aug(src, gen)
         opt.zero_grad(set_to_none=True)
         with torch.autocast(device_type=dev.type, dtype=torch.bfloat16, enabled=bf16):
             out = model(x)
@@ -112,6 +138,7 @@ def main():
             "dtype": a.dtype, "data": "synthetic uint8 images + GPU augmentation; random-init weights",
             "config": {"model": a.model, "image": a.size, "batch_per_gpu": a.batch,
                        "channels_last": bool(a.channels_last), "parallelism": f"dp{world}",
+                       "augment": "prefetched (side stream)" if a.prefetch else "in line",
                        "backend": dist.get_backend() if dist.is_initialized() else None,
                        "ddp_bucket": {"elements": model.bucket_size, "count": len(model.buckets),
                                       "MB": round(model.bucket_size * 4 / 2 ** 20, 2)} if a.ddp == "smdt" else None},

@@ -36,7 +36,7 @@ import torch.optim as optim  # noqa: E402
 
 import util  # noqa: E402
 from smdt_amd.comm import init_distributed  # noqa: E402
-from smdt_amd.data.image_folder import GpuAugment, ImageFolderDataset  # noqa: E402
+from smdt_amd.data.image_folder import AugmentPrefetcher, GpuAugment, ImageFolderDataset  # noqa: E402
 from smdt_amd.parallel.distributed import DistributedDataParallel as DDP  # noqa: E402
 
 logger = logging.getLogger(__name__)
@@ -146,11 +146,11 @@ def train(args):
         model.train()
         train_sampler.set_epoch(epoch)
         end = time.time()
-        for batch_idx, (data, target) in enumerate(train_loader):
+        # batches are moved and augmented ahead of the step on a side stream (GpuAugment's per-sample
+        # transform picks round-trip to the host; in line they stalled the step's launches)
+        for batch_idx, (data, target) in enumerate(AugmentPrefetcher(train_loader, aug_train, dev, gen)):
             if args.max_steps and batch_idx >= args.max_steps:
                 break
-            data = aug_train(data.to(dev, non_blocking=True), gen)
-            target = target.to(dev, non_blocking=True)
             optimizer.zero_grad()
             with torch.autocast(device_type=dev.type, dtype=torch.bfloat16, enabled=use_bf16):
                 output = model(data)

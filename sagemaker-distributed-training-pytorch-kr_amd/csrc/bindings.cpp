@@ -274,6 +274,32 @@ void cast_(Tensor x, Tensor y, bool accumulate) {
         "cast");
 }
 
+// ------------------------------------------------------------------ augmentation filters (fp32)
+// y [N, C, H, W] = x (*) k[n] per sample (reflect padding); k [N, KS, KS], KS in {3, 5, 7}.
+Tensor aug_depthwise(Tensor x, Tensor k) {
+  TORCH_CHECK(x.is_cuda() && k.is_cuda() && x.scalar_type() == at::kFloat && k.scalar_type() == at::kFloat,
+              "aug_depthwise: fp32 GPU tensors");
+  TORCH_CHECK(x.dim() == 4 && k.dim() == 3 && k.size(0) == x.size(0) && k.size(1) == k.size(2), "aug_depthwise: shapes");
+  x = x.contiguous();
+  k = k.contiguous();
+  auto y = torch::empty_like(x);
+  check(smdt_aug_depthwise(x.data_ptr<float>(), k.data_ptr<float>(), y.data_ptr<float>(), (int)x.size(0),
+                           (int)x.size(1), (int)x.size(2), (int)x.size(3), (int)k.size(1), cur_stream()),
+        "aug_depthwise");
+  return y;
+}
+
+// y = 3 x 3 median of every channel of x [N, C, H, W] (reflect padding).
+Tensor aug_median3(Tensor x) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kFloat && x.dim() == 4, "aug_median3: fp32 [N, C, H, W] GPU tensor");
+  x = x.contiguous();
+  auto y = torch::empty_like(x);
+  check(smdt_aug_median3(x.data_ptr<float>(), y.data_ptr<float>(), (int)(x.size(0) * x.size(1)), (int)x.size(2),
+                         (int)x.size(3), cur_stream()),
+        "aug_median3");
+  return y;
+}
+
 // ------------------------------------------------------------------ 2-D transpose (16-bit)
 // out [C, R] = x [R, C]^T, contiguous (feeds the dgrad GEMMs in the TN layout).
 Tensor transpose2d(Tensor x) {
@@ -675,6 +701,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("cast_", &cast_);
   m.def("rope_", &rope_);
   m.def("transpose2d", &transpose2d);
+  m.def("aug_depthwise", &aug_depthwise);
+  m.def("aug_median3", &aug_median3);
   m.def("bias_grad", &bias_grad);
   m.def("wgrad_mfma", &wgrad_mfma, arg("main_grad"), arg("dy"), arg("x"), arg("max_splits") = 0);
   m.def("wgrad_grouped", &wgrad_grouped, arg("main_grads"), arg("dys"), arg("xs"),

@@ -78,6 +78,11 @@ hipError_t smdt_ce_bwd(int dtype, const void* logits, const int64_t* target, con
                        const float* gsum, const float* dloss, void* dlogits, int64_t rows, int V,
                        int Vvalid, int64_t vstart, int64_t ignore_index, hipStream_t st);
 
+// augment.hip: per-sample depthwise filter (KS in {3, 5, 7}) and 3 x 3 median, fp32 NCHW
+hipError_t smdt_aug_depthwise(const float* x, const float* k, float* y, int N, int C, int H, int W, int ks,
+                              hipStream_t st);
+hipError_t smdt_aug_median3(const float* x, float* y, int planes, int H, int W, hipStream_t st);
+
 // flash_attn.hip
 hipError_t smdt_flash_fwd(int dtype, const void* q, const void* k, const void* v, void* o,
                           float* lse, int B, int H, int Hkv, int S, int D, int64_t q_sb,

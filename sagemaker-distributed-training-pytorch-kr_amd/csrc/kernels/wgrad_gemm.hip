@@ -92,14 +92,28 @@ struct Glds {
 // it was removed.)
 
 // BIAS (the k0 == 0 tiles of a problem with a bias): bias[n0 + r] += sum over this tile's m range
-// of A[m, n0 + r] — the bias gradient of the linear whose weight gradient this is, taken from the
-// A (dY) fragments the MFMAs read anyway. Wave (wn, wk) multiplies its fragment i == wk (all four
-// wk waves of a wn read the same A fragments) by an all-ones B operand: ONE extra MFMA per 8 on
-// these tiles and no VALU (replaces the col_sum_rows + col_partials_reduce
-// kernels). A fp32 VALU sum of the fragment instead (round-4 first form) was if-converted by the
-// compiler into sums of all four fragments on every tile: 13.6 -> 22.9 VALU per MFMA in the loop
-// and 35.8 -> 45.0 ms of grouped wgrad per GPT-2 345M step (profiles/r4_wgrad_bias/). Tiles
-// without a bias run the BIAS = false instantiation, i.e. the round-3 loop.
+// of A[m, n0 + r] — the bias gradient of the linear whose weight gradient this is, from the A (dY)
+// fragments the MFMAs read anyway. All four wk waves of a wn read the same A fragments; wave wk
+// sums fragment wk, which it processes first (its accumulators are rotated by wk, so the choice is
+// a compile-time index): ~16 VALU per 8 MFMAs on these tiles, on the vector pipe the MFMA-bound
+// loop leaves idle, no extra LDS reads (replaces the col_sum_rows +
+// col_partials_reduce kernels). Tiles without a bias run the BIAS = false instantiation, i.e. the
+// round-3 loop. Earlier forms, measured on the GPT-2 345M step (profiles/r4_wgrad_bias/): a fp32
+// VALU sum of the fragment was if-converted by the compiler into sums of all four fragments on
+// every tile (35.8 -> 45.0 ms of grouped wgrad); picking fragment wk inside the i loop made it
+// branch around an MFMA per fragment (bias tiles ~2.5x slower: 37.0 -> 43.8 ms); the re-read
+// fragment times an all-ones B operand (one extra MFMA per 8), or the re-read fragment summed by
+// VALU, both cost ~2.7 ms (39.7 / 40.4 ms): the tiles of a launch run in rounds of 256, so a slower
+// k = 0 tile in every round stretches every round.
+// Sum of the 8 16-bit values of an operand fragment, in fp32.
+template <class V>
+__device__ __forceinline__ float sum8(V x) {
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s += (float)x[j];
+  return s;
+}
+
 template <bool ATOMIC, int VAR, bool BIAS, class E>
 __device__ __forceinline__ void tile_gemm(const E* __restrict__ A, const E* __restrict__ B,
                                           float* __restrict__ C, int N, int K, int n0, int k0, int64_t mstart,
@@ -112,8 +126,10 @@ __device__ __forceinline__ void tile_gemm(const E* __restrict__ A, const E* __re
   int oa[4][2], ob[2][2];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    oa[i][0] = F::tr_off(lane, 4 * wn + i, 0);
-    oa[i][1] = F::tr_off(lane, 4 * wn + i, 1);
+    // accumulator i holds the wave's A fragment (i + wk) & 3: every wave meets ITS bias fragment
+    // (wk) first, at compile-time index 0 (the output rows follow in the epilogue)
+    oa[i][0] = F::tr_off(lane, 4 * wn + ((i + wk) & 3), 0);
+    oa[i][1] = F::tr_off(lane, 4 * wn + ((i + wk) & 3), 1);
   }
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
@@ -125,11 +141,10 @@ __device__ __forceinline__ void tile_gemm(const E* __restrict__ A, const E* __re
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = zero16();
-  // BIAS: column sums of A over the fragment i == wk, replicated in every column of accb
-  f32x16 accb = zero16();
-  V ones;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) ones[j] = (E)1.f;
+  // BIAS: column sums of A over the fragment i == wk, replicated in every column of accb. That
+  // fragment is read a second time by its own offsets (wk is only known at run time; selecting it
+  // from the four fragments of the i loop made the compiler branch around an MFMA per fragment)
+  float cs = 0.f;  // fp32 sum of this lane's 8 rows of column (lane & 31) of fragment wk
 
   Glds ga, gb;
   ga.init(wave, lane, N, n0, N);
@@ -176,7 +191,7 @@ __device__ __forceinline__ void tile_gemm(const E* __restrict__ A, const E* __re
         acc[i][0] = mfma(a, b0, acc[i][0]);
         acc[i][1] = mfma(a, b1, acc[i][1]);
         if constexpr (BIAS) {
-          if (i == wk) accb = mfma(a, ones, accb);  // wk is wave-uniform: a scalar branch
+          if (i == 0) cs += sum8(a);   // fragment wk (see oa)
         }
       }
     }
@@ -198,16 +213,12 @@ __device__ __forceinline__ void tile_gemm(const E* __restrict__ A, const E* __re
   wait_vm<0>();  // drain the trailing re-reads before the workgroup's LDS is released
 
   if constexpr (BIAS) {
-    // register r holds the sum of fragment row acc_row(r, h) (every column alike): lane c < 16 of
-    // each half stores row acc_row(c, h)
-    const int c = lane & 31;
-    float v = accb[0];
-#pragma unroll
-    for (int r = 1; r < 16; ++r) v = c == r ? accb[r] : v;
-    const int n = n0 + 128 * wn + 32 * wk + acc_row(c & 15, h);
-    if (c < 16 && n < N) {
-      if constexpr (ATOMIC) unsafeAtomicAdd(bias + n, v);
-      else bias[n] += v;
+    // lanes l and l ^ 32 summed the two 8-row halves of each 16-row k-step of one column
+    cs = __shfl_xor(cs, 32, 64) + cs;
+    const int n = n0 + 128 * wn + 32 * wk + (lane & 31);
+    if (h == 0 && n < N) {
+      if constexpr (ATOMIC) unsafeAtomicAdd(bias + n, cs);
+      else bias[n] += cs;
     }
   }
 
@@ -220,7 +231,7 @@ __device__ __forceinline__ void tile_gemm(const E* __restrict__ A, const E* __re
     const bool kok = k < K;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int nb = n0 + 128 * wn + 32 * i;
+      const int nb = n0 + 128 * wn + 32 * ((i + wk) & 3);
       float* cp = C + (int64_t)nb * K + k;
       if (nb + 32 <= N && kok) {
         if constexpr (ATOMIC) {

@@ -30,6 +30,6 @@ done
 echo "=== rehearse_n4"
 SMDT_BENCH_BACKEND=gloo SMDT_COLLECTIVE_LOG=$R/$O/clog SMDT_BENCH_DUMP_AFTER=100 timeout -k 10 160 \
   python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 --master-port 29611 \
-  bench.py --gpus 4 --steps 2 --warmup 1 > $O/rehearse_n4.log 2>&1
+  bench.py --gpus 4 --steps 2 --warmup 1 --tunableop 0 --seqs-per-gpu 8 > $O/rehearse_n4.log 2>&1
 echo "rc=$?"; grep '^{' $O/rehearse_n4.log | cut -c1-300; wc -l $O/clog.rank* 2>/dev/null
 echo DONE

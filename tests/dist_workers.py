@@ -983,30 +983,25 @@ def smddp_torch_ddp_worker(rank, world, port, outdir):
                                        torch.nn.GELU(), torch.nn.Linear(256, 256), torch.nn.GELU(),
                                        torch.nn.Linear(256, 32)).cuda()
         m = mlp()
-        m_one = mlp()
         ref_m = mlp()
         ref_m.load_state_dict(m.state_dict())
-        m_one.load_state_dict(m.state_dict())
-        # Two torch DDP wrappers of the same module: (a) small buckets, several all-reduces per
-        # backward launched while backward still runs — torch 2.10's DDP splits by bucket_cap_mb
-        # only with find_unused_parameters, whose unused-parameter scan itself syncs the host, so
-        # (b) a default wrapper (one bucket) runs the steps under torch.cuda.set_sync_debug_mode
-        # ("error"): any host sync in the smddp hook path raises there.
-        ddp_multi = torch.nn.parallel.DistributedDataParallel(m, bucket_cap_mb=0.04, find_unused_parameters=True)
-        ddp_one = torch.nn.parallel.DistributedDataParallel(m_one)
+        # torch 2.10's DDP keeps ONE bucket for a model this size (bucket_cap_mb splits only with
+        # find_unused_parameters, whose unused-parameter scan syncs the host itself): one bucket
+        # all-reduce per backward, launched from the autograd hook before backward returns
+        ddp = torch.nn.parallel.DistributedDataParallel(m)
+        mod = m
         from smdt_amd.comm import stats as cstats
         ok, placement = [], []
-        for step in range(6):
-            ddp, mod, strict = (ddp_multi, m, False) if step < 4 else (ddp_one, m_one, True)
+        for step in range(5):
             x = torch.randn(16, 64, generator=torch.Generator().manual_seed(10 * step + rank)).cuda()
             mod.zero_grad()
-            measured = step in (2, 3, 5)      # steady state (bucket rebuild and the engine build are over)
+            measured = step >= 3      # steady state (bucket rebuild and the engine build are over)
             if measured:
                 torch.cuda.synchronize()
                 cstats.enable(True)
+                cstats.begin_step()      # engine calls record start events inside a stats step
                 S._TIMINGS.clear()
-                if strict:
-                    torch.cuda.set_sync_debug_mode("error")
+                torch.cuda.set_sync_debug_mode("error")   # any host sync in the hook path raises
                 b0 = torch.cuda.Event(enable_timing=True)
                 b1 = torch.cuda.Event(enable_timing=True)
                 b0.record()
@@ -1014,13 +1009,14 @@ def smddp_torch_ddp_worker(rank, world, port, outdir):
             if measured:
                 b1.record()
                 torch.cuda.set_sync_debug_mode(0)
+                cstats.end_step()
                 cstats.enable(False)
                 torch.cuda.synchronize()
                 pg = dist.distributed_c10d._get_default_group()
                 starts = [b0.elapsed_time(a) for a, _ in S._TIMINGS]
                 placement.append({"n": len(S._TIMINGS), "engine_stream": pg._engine._stream != torch.cuda.current_stream(),
                                   "first_start_ms": min(starts) if starts else None,
-                                  "backward_ms": b0.elapsed_time(b1), "sync_checked": strict})
+                                  "backward_ms": b0.elapsed_time(b1)})
             ref_m.zero_grad()
             ref_m(x).square().mean().backward()
             for p, q in zip(mod.parameters(), ref_m.parameters()):

@@ -117,3 +117,29 @@ def test_bench_emulated_tp_rank(tmp_path):
     rec = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
     assert rec["config"]["tp"] == 2 and "emulated" in rec["config"]["parallelism"]
     assert rec["config"]["model"].endswith("vocab 256, seq 32)")   # padded to 128 x tp and rec["final_loss"] > 0
+
+
+@pytest.mark.slow
+def test_bench_n4_many_buckets_same_collective_order(tmp_path):
+    """The round-3 one-GPU N = 4 rehearsal stalled in a bucket wait with ~75 buckets. The same
+    many-bucket layout on CPU Gloo (buckets of 256 gradients: one per parameter tensor of the small model,
+    as with the 16 MB buckets of the real one) completes, and the per-rank collective issue order
+    (SMDT_COLLECTIVE_LOG) is identical on all four ranks."""
+    env_extra = {"SMDT_COLLECTIVE_LOG": str(tmp_path / "clog")}
+    old = {k: os.environ.get(k) for k in env_extra}
+    os.environ.update(env_extra)
+    try:
+        rec = _run_bench(4, "baseline", tmp_path, ["--bucket-size", "256"])
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    assert rec["config"]["ddp_bucket"]["count"] >= 30, rec["config"]["ddp_bucket"]
+    orders = []
+    for r in range(4):
+        lines = open(tmp_path / f"clog.rank{r}").read().splitlines()
+        orders.append([ln.split(" ", 2)[2] for ln in lines])      # drop the index and timestamp
+    assert len(orders[0]) > 2 * 30
+    assert all(o == orders[0] for o in orders[1:])

@@ -238,13 +238,12 @@ def test_smddp_backend_torch_ddp_takes_xgmi_path():
                 out.append(pickle.load(f))
     for r, res in enumerate(out):
         assert res["err"] is None, f"rank {r}:\n{res['err']}"
-        assert res["backend"] == "smddp" and all(res["ok"]) and len(res["ok"]) == 48, (r, res)
-        assert res["stats"]["xgmi_calls"] >= 10 and res["error_word"] == 0, (r, res)
-        assert [pl["sync_checked"] for pl in res["placement"]] == [False, False, True], (r, res)
+        assert res["backend"] == "smddp" and all(res["ok"]) and len(res["ok"]) == 40, (r, res)
+        assert res["stats"]["xgmi_calls"] >= 5 and res["error_word"] == 0, (r, res)
         for pl in res["placement"]:
-            # every bucket all-reduce on the engine's own stream, the first one issued before
-            # backward returned; several buckets per backward with the small-bucket wrapper
-            assert pl["engine_stream"] and pl["n"] >= (1 if pl["sync_checked"] else 2), (r, pl)
+            # the bucket all-reduce on the engine's own stream, issued before backward returned,
+            # with no host sync in the hook path (the steps ran under sync debug mode "error")
+            assert pl["engine_stream"] and pl["n"] >= 1, (r, pl)
             assert pl["first_start_ms"] is not None and pl["first_start_ms"] < pl["backward_ms"], (r, pl)
 
 
