@@ -312,7 +312,9 @@ def main():
         if stats:
             comm_stats.begin_step()
         ddp.zero_grad_buffer()
-        losses = fb(forward_step, it, ddp, a.grad_accum, tensor_shape=shape, dtype=torch.bfloat16)
+        # an emulated pipeline stage issues each micro-batch's W GEMMs as its schedule would
+        losses = fb(forward_step, it, ddp, a.grad_accum, tensor_shape=shape, dtype=torch.bfloat16,
+                    split_backward=bool(a.emulate_tp) and a.pp_schedule in ("zb", "zbh1"))
         comm_stats.mark("fwd_bwd")
         ddp.finish_grad_sync()
         allreduce_word_embedding_grads(model)   # tied embedding: first + last pipeline stage

@@ -46,12 +46,19 @@ def _scaled(loss, num_microbatches, grad_scale):
 
 
 def forward_backward_no_pipelining(forward_step_func: Callable, data_iterator, model, num_microbatches: int,
-                                   forward_only: bool = False, grad_scale=None, **_):
+                                   forward_only: bool = False, grad_scale=None, split_backward: bool = False, **_):
     """Gradient accumulation over ``num_microbatches``; returns the list of loss dicts.
 
     ``forward_step_func(data_iterator, model) -> (output_tensor, loss_func)`` with
     ``loss_func(output_tensor) -> (loss, {name: reduced})`` (Megatron's contract,
     `pretrain_gpt.py:92-117`).
+
+    ``split_backward``: each micro-batch's weight-gradient GEMMs are held for the whole backward
+    (``DEFERRED_WGRAD.defer``) and issued as one grouped launch after it — the W work of one
+    micro-batch exactly as a stage of the zero-bubble pipeline schedules issues it. bench.py's
+    per-rank emulation of a pipeline stage (``--emulate-tp``) runs this way, so the measured
+    stage time has the schedule's W grouping instead of the opportunistic per-collective flushes
+    of a plain backward.
     """
     from ..parallel.tensor_parallel import DEFERRED_WGRAD, accumulation_window_ok
     models = model if isinstance(model, list) else [model]
@@ -71,7 +78,15 @@ def forward_backward_no_pipelining(forward_step_func: Callable, data_iterator, m
         loss, info = loss_func(out)
         losses.append(info)
         if not forward_only:
-            _scaled(loss, num_microbatches, grad_scale).backward()
+            if split_backward:
+                DEFERRED_WGRAD.defer = True
+            try:
+                _scaled(loss, num_microbatches, grad_scale).backward()
+            finally:
+                if split_backward:
+                    DEFERRED_WGRAD.defer = False
+            if split_backward:
+                DEFERRED_WGRAD.flush()
     gate.set(True)
     return losses
 
