@@ -54,6 +54,11 @@ def main():
     p.add_argument("--prefetch", type=int, default=1,
                    help="augment the next batches on a side stream in a background thread "
                         "(data/image_folder.AugmentPrefetcher); 0: in line with the step")
+    p.add_argument("--graph", type=int, default=0,
+                   help="1 GPU: capture forward + backward + Adam of one step in a HIP graph after the "
+                        "warm-up and replay it (the step's ~1.5-3.7 k kernel launches leave the device "
+                        "idle 5-42 ms per step in eager mode, profiles/r4_vision/); the augmented batch "
+                        "is copied into the graph's static input")
     p.add_argument("--miopen-prewarm", type=int, default=1,
                    help="before timing, run 13 steps in a child process so MIOpen's find database and "
                         "kernel cache exist: on a fresh box the first process of a model ran 418-540 ms "
@@ -86,7 +91,8 @@ def main():
     if a.ddp == "smdt":
         model = DDP(model, torch_compat=True, bucket_size=bucket)
     crit = nn.CrossEntropyLoss()
-    opt = torch.optim.Adam(model.parameters(), lr=1e-4, fused=dev.type == "cuda")
+    use_graph = bool(a.graph) and dev.type == "cuda" and world == 1
+    opt = torch.optim.Adam(model.parameters(), lr=1e-4, fused=dev.type == "cuda", capturable=use_graph)
     aug = GpuAugment((a.size, a.size), train=True, channels_last=mf == torch.channels_last)
     gen = torch.Generator(device=dev)
     gen.manual_seed(rank)
@@ -98,15 +104,45 @@ def main():
 
     batches = iter(AugmentPrefetcher(itertools.repeat((src, tgt)), aug, dev, gen)) if a.prefetch else None
 
-    def step():
-        x = next(batches)[0] if batches is not None else aug(src, gen)
-        opt.zero_grad(set_to_none=True)
-        with torch.autocast(device_type=dev.type, dtype=torch.bfloat16, enabled=bf16):
+    def train(x):
+        with torch.autocast(device_type=dev.type, dtype=torch.bfloat16, enabled=bf16, cache_enabled=not use_graph):
             out = model(x)
             loss = crit(out.float(), tgt)
         loss.backward()
         opt.step()
         return loss
+
+    def step():
+        x = next(batches)[0] if batches is not None else aug(src, gen)
+        opt.zero_grad(set_to_none=True)
+        return train(x)
+
+    graph = None
+
+    def capture():
+        # whole-step capture: warm-up replays on a side stream, then one captured step; the
+        # gradients live in the graph's pool and every replay rewrites them
+        nonlocal graph
+        static_x = next(batches)[0].clone() if batches is not None else aug(src, gen)
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(3):
+                opt.zero_grad(set_to_none=True)
+                train(static_x)
+        torch.cuda.current_stream().wait_stream(side)
+        g = torch.cuda.CUDAGraph()
+        opt.zero_grad(set_to_none=True)
+        with torch.cuda.graph(g):
+            static_loss = train(static_x)
+        graph = (g, static_x, static_loss)
+
+    def graph_step():
+        g, static_x, static_loss = graph
+        x = next(batches)[0] if batches is not None else aug(src, gen)
+        static_x.copy_(x)
+        g.replay()
+        return static_loss
 
     tw = time.perf_counter()
     for i in range(a.warmup):
@@ -114,13 +150,26 @@ def main():
         if rank == 0:
             print(f"[bench_vision] warmup {i + 1}/{a.warmup} at {time.perf_counter() - tw:.1f}s", file=sys.stderr,
                   flush=True)
+    graph_note = None
+    if use_graph:
+        try:
+            capture()
+            for _ in range(2):
+                graph_step()
+            graph_note = "captured"
+        except Exception as e:  # noqa: BLE001 - report and run eager
+            graph_note = f"capture failed, eager: {type(e).__name__}: {str(e)[:120]}"
+            print(f"[bench_vision] {graph_note}", file=sys.stderr, flush=True)
+            graph = None
+            torch.cuda.synchronize()
+    run = graph_step if graph is not None else step
     if dist.is_initialized():
         dist.barrier()
     if dev.type == "cuda":
         torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(a.steps):
-        loss = step()
+        loss = run()
     if dev.type == "cuda":
         torch.cuda.synchronize()
     if dist.is_initialized():
@@ -139,6 +188,7 @@ def main():
             "config": {"model": a.model, "image": a.size, "batch_per_gpu": a.batch,
                        "channels_last": bool(a.channels_last), "parallelism": f"dp{world}",
                        "augment": "prefetched (side stream)" if a.prefetch else "in line",
+                       "hip_graph": graph_note,
                        "backend": dist.get_backend() if dist.is_initialized() else None,
                        "ddp_bucket": {"elements": model.bucket_size, "count": len(model.buckets),
                                       "MB": round(model.bucket_size * 4 / 2 ** 20, 2)} if a.ddp == "smdt" else None},
