@@ -49,6 +49,7 @@ H, L, S, V = 1024, 24, 1024, 50304
 PARAMS = 354.9e6            # GPT-2 345M with the padded vocab (tied embedding)
 
 _N8 = ["--emulate-tp", "2", "--micro-batch-size", "32", "--grad-accum", "8", "--phase-probe", "8"]
+_N8_64 = ["--emulate-tp", "2", "--micro-batch-size", "64", "--grad-accum", "4", "--phase-probe", "4"]
 _G3 = ["--emulate-tp", "4", "--hidden-size", "4096", "--num-attention-heads", "32", "--seq-length", "2048",
        "--micro-batch-size", "4", "--grad-accum", "8", "--phase-probe", "8", "--tunableop", "0"]
 RUNS = {
@@ -58,6 +59,10 @@ RUNS = {
     "tp2pp2_stage1": ["--num-layers", "11"] + _N8,
     # the even split the interleaved schedule is limited to: 12 | 12 + head (the heavier stage)
     "tp2pp2_stage1_even": ["--num-layers", "12"] + _N8,
+    # the same replica batch as 4 micro-batches of 64: ring chunks of 32768 rows (the N = 1 GEMM
+    # shapes, half the launches) against twice the bubble per micro-batch
+    "tp2pp2_mb64_stage0": ["--num-layers", "13", "--emulate-first-stage"] + _N8_64,
+    "tp2pp2_mb64_stage1": ["--num-layers", "11"] + _N8_64,
     "gpt3_tp4_stage0": ["--num-layers", "16", "--emulate-first-stage"] + _G3,
     "gpt3_tp4_stage1": ["--num-layers", "16"] + _G3,
     # the whole 6.7B model on ONE GPU (288 GB hold weights, fp32 masters, Adam state, activations)
@@ -149,6 +154,11 @@ def predict(m: dict) -> list:
         act = (S // 2) * 32 * H * 2                             # p2p activation [s/2, 32, h] bf16
         for r in pipeline_rows(m, "tp2pp2_stage0", "tp2pp2_stage1", 8, 2, act, dp_tail + embd + 0.5, tok1 * 8,
                                "tp2pp2dp2+sp+zero1 13|11", even="tp2pp2_stage1_even" if "tp2pp2_stage1_even" in m else None):
+            rows.append({"N": 8, "model": "gpt2-345m", **r})
+    if "tp2pp2_mb64_stage0" in m and "tp2pp2_mb64_stage1" in m:
+        act64 = (S // 2) * 64 * H * 2
+        for r in pipeline_rows(m, "tp2pp2_mb64_stage0", "tp2pp2_mb64_stage1", 4, 2, act64, dp_tail + embd + 0.5,
+                               tok1 * 8, "tp2pp2dp2+sp+zero1 13|11, 4 x 64"):
             rows.append({"N": 8, "model": "gpt2-345m", **r})
     for r in rows:
         r["predicted_tokens_per_s"] = round(r["tokens_per_step"] / r["predicted_ms"] * 1e3)
