@@ -54,8 +54,8 @@ def main():
     p.add_argument("--prefetch", type=int, default=1,
                    help="augment the next batches on a side stream in a background thread "
                         "(data/image_folder.AugmentPrefetcher); 0: in line with the step")
-    p.add_argument("--graph", type=int, default=0,
-                   help="1 GPU: capture forward + backward + Adam of one step in a HIP graph after the "
+    p.add_argument("--graph", type=int, default=1,
+                   help="1 GPU (default on): capture forward + backward + Adam of one step in a HIP graph after the "
                         "warm-up and replay it (the step's ~1.5-3.7 k kernel launches leave the device "
                         "idle 5-42 ms per step in eager mode, profiles/r4_vision/); the augmented batch "
                         "is copied into the graph's static input")

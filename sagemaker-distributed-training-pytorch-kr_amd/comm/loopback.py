@@ -7,7 +7,7 @@ every collective replaced by a local stand-in of the same memory traffic on the 
 
 * all-gather: the local shard is copied into every slot of the output;
 * reduce-scatter: this rank's slice of the input is added to the output slot by slot (W - 1
-  adds, the reduction a real rank does);
+  adds, the reduction a real rank does; AVG scales the slice, as RCCL's AVG does);
 * all-reduce / broadcast / barrier: nothing (the values stay this rank's own);
 * a ring exchange (``parallel/tensor_parallel._exchange``): ``recv.copy_(send)``.
 
@@ -73,6 +73,8 @@ class LoopbackGroup(dist.ProcessGroup):
         out.view(-1).copy_(flat[:n])
         for r in range(1, self.world):
             out.view(-1).add_(flat[r * n:(r + 1) * n])
+        if opts is not None and opts.reduceOp == dist.ReduceOp.AVG:
+            out.div_(self.world)         # RCCL's AVG: the scale applies to this rank's slice only
         return _done([out])
 
     def reduce_scatter(self, outs, inps, opts=None):

@@ -114,7 +114,9 @@ class DistributedDataParallel(nn.Module):
         from ..comm import xgmi as _xgmi
         # "smddp" is RCCL underneath (comm/smddp.py): AVG reductions and the xGMI path apply to it
         rccl = self.dp > 1 and _xgmi.rccl_backend(self.dp_group)
-        self.use_avg = average_in_collective and rccl
+        # (the loopback group of a single-GPU rank emulation averages like RCCL: comm/loopback.py)
+        from ..comm import loopback as _loopback
+        self.use_avg = average_in_collective and (rccl or (self.dp > 1 and _loopback.is_loopback(self.dp_group)))
         # Bucket all-reduces, ZeRO reduce-scatters and parameter all-gathers run on the xGMI IPC
         # kernel on its own stream (comm/xgmi.py) when SMDT_XGMI_ALLREDUCE=1 / the "smddp"
         # backend asks for it, or — by default — for each op a run-time timing on this node shows
