@@ -811,7 +811,7 @@ __global__ __launch_bounds__(256, D == 64 ? SMDT_FA_DKDV_OCC : 1) void bwd_dkdv_
 // ---------------------------------------------------------------------------------------
 // dQ. Workgroup = 4 waves = 128 query rows of one (b, h); K/V streamed in 64-key tiles,
 // double-buffered.
-template <int D, bool CAUSAL, bool DROP, class E>
+template <int D, bool CAUSAL, bool DROP, class E, bool STRAIGHT = false>
 __global__ __launch_bounds__(256, D == 64 ? SMDT_FA_DQ_OCC : 1) void bwd_dq_kernel(
     const E* __restrict__ Q, const E* __restrict__ K, const E* __restrict__ V,
     const E* __restrict__ dO, const E* __restrict__ O, const float* __restrict__ LSE,
@@ -933,19 +933,19 @@ __global__ __launch_bounds__(256, D == 64 ? SMDT_FA_DQ_OCC : 1) void bwd_dq_kern
     const int kb = t * kTile;
     const char* vt = kt + G::TB;
     issue(t + kBuf - 1 < ntiles ? t + kBuf - 1 : ntiles - 1, pre);
-#pragma unroll
-    for (int tt = 0; tt < 2; ++tt) {
-      const int ksub = kb + 32 * tt;
-      if (CAUSAL && ksub > qw + 31) continue;
-      // row constants as the initial accumulators: S' = S log2(e) scale - lse, dP' = dP - delta
-      f32x16 st = mfma(fr.rowf(kt, 32 * tt, 0), qf[0], SMDT_DQ_ST0);
-      f32x16 dpt = mfma(fr.rowf(vt, 32 * tt, 0), dof[0], SMDT_DQ_DP0);
+    // row constants as the initial accumulators: S' = S log2(e) scale - lse, dP' = dP - delta
+    auto sd = [&](int tt, f32x16& st, f32x16& dpt) {
+      st = mfma(fr.rowf(kt, 32 * tt, 0), qf[0], SMDT_DQ_ST0);
+      dpt = mfma(fr.rowf(vt, 32 * tt, 0), dof[0], SMDT_DQ_DP0);
 #pragma unroll
       for (int kk = 1; kk < G::KS; ++kk) {
         st = mfma(fr.rowf(kt, 32 * tt, kk), qf[kk], st);
         dpt = mfma(fr.rowf(vt, 32 * tt, kk), dof[kk], dpt);
       }
-      const bool diag = CAUSAL && ksub + 31 > qw;
+    };
+    // dS^T into dpt (P' = exp2(S'); dropout: kept dP - delta', dropped -delta'; causal diagonal)
+    auto soft = [&](int tt, const f32x16& st, f32x16& dpt, bool diag) {
+      const int ksub = kb + 32 * tt;
       uint32_t tb[4];  // keep bits of slots 2u (bits 7 / 23) and 2u + 1 (bits 15 / 31)
       if constexpr (DROP) {
 #pragma unroll
@@ -959,25 +959,48 @@ __global__ __launch_bounds__(256, D == 64 ? SMDT_FA_DQ_OCC : 1) void bwd_dq_kern
           if (ksub + acc_row(i + 1, h) > my_q) p1 = 0.f;
         }
         float d0 = dpt[i], d1 = dpt[i + 1];
-        if constexpr (DROP) {  // kept: dP - delta'; dropped: dS = p' (0 - delta')
-          const uint32_t t = tb[i >> 2];
+        if constexpr (DROP) {
+          const uint32_t tw = tb[i >> 2];
           if ((i & 2) == 0) {
-            d0 = sel_bit<7>(d0, ndl, t);
-            d1 = sel_bit<23>(d1, ndl, t);
+            d0 = sel_bit<7>(d0, ndl, tw);
+            d1 = sel_bit<23>(d1, ndl, tw);
           } else {
-            d0 = sel_bit<15>(d0, ndl, t);
-            d1 = sel_bit<31>(d1, ndl, t);
+            d0 = sel_bit<15>(d0, ndl, tw);
+            d1 = sel_bit<31>(d1, ndl, tw);
           }
         }
-        dpt[i] = p0 * d0;  // dS^T
+        dpt[i] = p0 * d0;
         dpt[i + 1] = p1 * d1;
       }
-      // dQ^T[d, q] += K^T[d, keys] . dS^T[keys, q]
+    };
+    // dQ^T[d, q] += K^T[d, keys] . dS^T[keys, q]
+    auto acc = [&](int tt, const f32x16& dpt) {
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         const v8_t<E> db = pack8<E>(dpt, s);
 #pragma unroll
         for (int dt = 0; dt < G::DT; ++dt) dq[dt] = mfma(fr.trf(kt, 32 * tt, s, dt), db, dq[dt]);
+      }
+    };
+    if (STRAIGHT && (!CAUSAL || kb + 63 <= qw)) {
+      // both sub-tiles visible and off the diagonal: one straight-line block, so the scheduler
+      // can run sub-tile 1's S / dP MFMA chains beside sub-tile 0's softmax VALU
+      f32x16 st0, dp0, st1, dp1;
+      sd(0, st0, dp0);
+      sd(1, st1, dp1);
+      soft(0, st0, dp0, false);
+      acc(0, dp0);
+      soft(1, st1, dp1, false);
+      acc(1, dp1);
+    } else {
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt) {
+        const int ksub = kb + 32 * tt;
+        if (CAUSAL && ksub > qw + 31) continue;
+        f32x16 st, dpt;
+        sd(tt, st, dpt);
+        soft(tt, st, dpt, CAUSAL && ksub + 31 > qw);
+        acc(tt, dpt);
       }
     }
     wait_vm<(kBuf - 2) * kPer>();  // tile t + 1 landed (t + 2 may still be in flight)
@@ -1077,6 +1100,15 @@ extern "C" hipError_t smdt_flash_fwd(int dtype, const void* q, const void* k, co
   return hipGetLastError();
 }
 
+// SMDT_FA_DQ_STRAIGHT=1: the dQ kernel's straight-line sub-tile pair (A/B knob, read once).
+static bool dq_straight() {
+  static const bool on = [] {
+    const char* v = getenv("SMDT_FA_DQ_STRAIGHT");
+    return v != nullptr && v[0] == '1';
+  }();
+  return on;
+}
+
 extern "C" hipError_t smdt_flash_bwd(int dtype, const void* q, const void* k, const void* v,
                                      const void* o, const void* dout, const float* lse,
                                      float* delta, void* dq, void* dk, void* dv, int B, int H,
@@ -1102,10 +1134,16 @@ extern "C" hipError_t smdt_flash_bwd(int dtype, const void* q, const void* k, co
   dim3 gq((unsigned)((int64_t)B * H * (S / kBlockRows)));
 #define SMDT_FA_BWD_T(DD, CC, DR, ET)                                                            \
   do {                                                                                           \
-    hipLaunchKernelGGL((bwd_dq_kernel<DD, CC, DR, ET>), gq, dim3(256), 0, st, (const ET*)q,     \
-                       (const ET*)k, (const ET*)v, (const ET*)dout, (const ET*)o, lse, delta,     \
-                       (ET*)lse3, (ET*)dl3, (ET*)dq, B, H, Hkv, S, qs, ks, vs, dos, os, dqs,      \
-                       scale, dscale, lsub, dr);                                                  \
+    if (dq_straight())                                                                           \
+      hipLaunchKernelGGL((bwd_dq_kernel<DD, CC, DR, ET, true>), gq, dim3(256), 0, st, (const ET*)q, \
+                         (const ET*)k, (const ET*)v, (const ET*)dout, (const ET*)o, lse, delta,   \
+                         (ET*)lse3, (ET*)dl3, (ET*)dq, B, H, Hkv, S, qs, ks, vs, dos, os, dqs,    \
+                         scale, dscale, lsub, dr);                                                \
+    else                                                                                         \
+      hipLaunchKernelGGL((bwd_dq_kernel<DD, CC, DR, ET, false>), gq, dim3(256), 0, st, (const ET*)q, \
+                         (const ET*)k, (const ET*)v, (const ET*)dout, (const ET*)o, lse, delta,   \
+                         (ET*)lse3, (ET*)dl3, (ET*)dq, B, H, Hkv, S, qs, ks, vs, dos, os, dqs,    \
+                         scale, dscale, lsub, dr);                                                \
     hipLaunchKernelGGL((bwd_dkdv_kernel<DD, CC, DR, ET>), gkv, dim3(256), 0, st, (const ET*)q,  \
                        (const ET*)k, (const ET*)v, (const ET*)dout, (const ET*)lse3,              \
                        (const ET*)dl3, delta, (ET*)dk, (ET*)dv, B, H, Hkv, S, qs, ks, vs, dos,    \
