@@ -148,9 +148,9 @@ def predict(m: dict) -> list:
                      "tokens_per_step": tok1 * n,
                      "note": f"{hidden:.1f} ms of RS+AG per step overlapped with backward / next forward"})
     # N = 8: tp2 pp2 dp2 + SP + ZeRO-1 (BASELINE config #3)
+    dp_tail = link_ms(16e6 / 2) + link_ms(8e6 / 2)              # last RS bucket + first AG bucket, dp2 = 1 link
+    embd = link_ms(4 * (V // 2) * H)                            # tied-embedding fp32 grad all-reduce, 1 link
     if "tp2pp2_stage0" in m and "tp2pp2_stage1" in m:
-        dp_tail = link_ms(16e6 / 2) + link_ms(8e6 / 2)          # last RS bucket + first AG bucket, dp2 = 1 link
-        embd = link_ms(4 * (V // 2) * H)                        # tied-embedding fp32 grad all-reduce, 1 link
         act = (S // 2) * 32 * H * 2                             # p2p activation [s/2, 32, h] bf16
         for r in pipeline_rows(m, "tp2pp2_stage0", "tp2pp2_stage1", 8, 2, act, dp_tail + embd + 0.5, tok1 * 8,
                                "tp2pp2dp2+sp+zero1 13|11", even="tp2pp2_stage1_even" if "tp2pp2_stage1_even" in m else None):
