@@ -92,10 +92,14 @@ def parse():
                         "parallelism, ring-chunk GEMMs, collectives as local stand-ins (comm/loopback.py)")
     p.add_argument("--emulate-first-stage", action="store_true",
                    help="(pp = 1 emulation) no LM head: the model outputs hidden states, as pipeline stage 0")
+    p.add_argument("--emulate-last-stage", action="store_true",
+                   help="(pp = 1 emulation) no embedding: the model takes a received [s/tp, mbs, h] "
+                        "activation (random, requires grad) as its input, as the last pipeline stage")
     p.add_argument("--pp-last-layers", type=int, default=None,
                    help="layers on the last pipeline stage (default: balanced against the LM head + CE)")
-    p.add_argument("--pp-schedule", choices=["1f1b", "zb", "zbh1"], default="zbh1",
-                   help="pipeline schedule (train/schedules.py): 1F1B, or its zero-bubble split backward")
+    p.add_argument("--pp-schedule", choices=["1f1b", "zb", "zbh1", "zbh2"], default="zbh2",
+                   help="pipeline schedule (train/schedules.py): 1F1B, or its zero-bubble split backward "
+                        "(zbh2: twice the in-flight micro-batches, the lowest simulated bubble at N = 8)")
     p.add_argument("--vpp", type=int, default=1,
                    help="virtual pipeline chunks per rank (interleaved 1F1B; uniform layer split)")
     p.add_argument("--phase-probe", type=int, default=0,
@@ -274,7 +278,9 @@ def main():
         st.virtual_pp_rank = 0
         model = torch.nn.ModuleList(chunks)
     else:
-        model = GPTModel(cfg, pre_process=st.is_first_stage(),
+        if a.emulate_first_stage and a.emulate_last_stage:
+            raise SystemExit("[bench] --emulate-first-stage and --emulate-last-stage exclude each other")
+        model = GPTModel(cfg, pre_process=st.is_first_stage() and not a.emulate_last_stage,
                          post_process=st.is_last_stage() and not a.emulate_first_stage, device=dev)
     zero = bool(a.zero) and st.dp > 1
     ddp = DistributedDataParallel(model, bucket_size=a.bucket_size, use_distributed_optimizer=zero,
@@ -296,6 +302,9 @@ def main():
     def forward_step(data_iter, m):
         toks = next(data_iter)
         tokens, labels = toks[:, :-1], toks[:, 1:]
+        if a.emulate_last_stage:   # the activation a last stage receives from its predecessor
+            model.set_input_tensor(torch.randn(shape, device=dev, dtype=torch.bfloat16, generator=gen)
+                                   .requires_grad_())
         out = m(tokens, pos, None, labels=labels)
 
         def loss_func(o):
@@ -314,7 +323,7 @@ def main():
         ddp.zero_grad_buffer()
         # an emulated pipeline stage issues each micro-batch's W GEMMs as its schedule would
         losses = fb(forward_step, it, ddp, a.grad_accum, tensor_shape=shape, dtype=torch.bfloat16,
-                    split_backward=bool(a.emulate_tp) and a.pp_schedule in ("zb", "zbh1"))
+                    split_backward=bool(a.emulate_tp) and a.pp_schedule in ("zb", "zbh1", "zbh2"))
         comm_stats.mark("fwd_bwd")
         ddp.finish_grad_sync()
         allreduce_word_embedding_grads(model)   # tied embedding: first + last pipeline stage

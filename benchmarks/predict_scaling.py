@@ -13,14 +13,15 @@ The pool this repo is developed on has one GPU per box, so the multi-GPU points 
         per-chunk GEMMs at their real M = s/2 x mbs, the vocab-parallel head + CE; every collective
         is a local stand-in with the receiving side's memory traffic. One run
         per pipeline stage at bench.py's 13 | 11 split (first stage without the head, last stage
-        with it), plus the even 12 | 12 split the interleaved schedule needs;
+        with it and without the embedding: its input is a received activation), plus the even
+        12 | 12 split the interleaved schedule needs;
       * GPT-3 6.7B tp4 pp2 + SP: the same with ``--emulate-tp 4``, 16 layers per stage, seq 2048,
         8 micro-batches of 4 (32 sequences per replica per step).
     Each emulated run also reports ``fbw_ms``: per micro-batch forward (F), input-gradient backward
     with the weight-gradient GEMMs held (B) and those GEMMs (W).
 (b) the pipeline bubble of each schedule from train/pipeline_sim.simulate(F, B, W per stage, the
     p2p hop of one [s/tp, mbs, h] activation over one link) — 1F1B, the zero-bubble split zb and
-    zbh1 (the bench default) — and the interleaved vpp = 2 schedule as 1F1B's bubble / 2 on the
+    zbh1 and zbh2 (the bench default) — and the interleaved vpp = 2 schedule as 1F1B's bubble / 2 on the
     even split;
 (c) the link budget: ``LINK_GBPS`` per direction per xGMI link (7 links per GPU, every pair directly
     connected): which of the step's bytes hide behind compute (bucketed reduce-scatter during
@@ -56,20 +57,20 @@ RUNS = {
     "n1_dp": [],
     # bench.py's balanced split: 13 layers | 11 layers + LM head
     "tp2pp2_stage0": ["--num-layers", "13", "--emulate-first-stage"] + _N8,
-    "tp2pp2_stage1": ["--num-layers", "11"] + _N8,
+    "tp2pp2_stage1": ["--num-layers", "11", "--emulate-last-stage"] + _N8,
     # the even split the interleaved schedule is limited to: 12 | 12 + head (the heavier stage)
-    "tp2pp2_stage1_even": ["--num-layers", "12"] + _N8,
+    "tp2pp2_stage1_even": ["--num-layers", "12", "--emulate-last-stage"] + _N8,
     # the same replica batch as 4 micro-batches of 64: ring chunks of 32768 rows (the N = 1 GEMM
     # shapes, half the launches) against twice the bubble per micro-batch
     "tp2pp2_mb64_stage0": ["--num-layers", "13", "--emulate-first-stage"] + _N8_64,
-    "tp2pp2_mb64_stage1": ["--num-layers", "11"] + _N8_64,
+    "tp2pp2_mb64_stage1": ["--num-layers", "11", "--emulate-last-stage"] + _N8_64,
     "gpt3_tp4_stage0": ["--num-layers", "16", "--emulate-first-stage"] + _G3,
-    "gpt3_tp4_stage1": ["--num-layers", "16"] + _G3,
+    "gpt3_tp4_stage1": ["--num-layers", "16", "--emulate-last-stage"] + _G3,
     # the whole 6.7B model on ONE GPU (288 GB hold weights, fp32 masters, Adam state, activations)
     "gpt3_n1": ["--hidden-size", "4096", "--num-attention-heads", "32", "--seq-length", "2048", "--num-layers", "32",
                 "--micro-batch-size", "4", "--grad-accum", "1", "--tunableop", "0"],
 }
-SCHEDS = ("1f1b", "zb", "zbh1")
+SCHEDS = ("1f1b", "zb", "zbh1", "zbh2")
 
 
 def measure(steps: int, warmup: int, logdir: str, only=None) -> dict:
@@ -180,13 +181,15 @@ def predict_gpt3(m: dict) -> list:
     tok = 32 * sl                                           # tp4 x pp2 = 8 GPUs: ONE replica, 32 sequences
     act = (sl // 4) * mb * h * 2
     base = pipeline_rows(m, "gpt3_tp4_stage0", "gpt3_tp4_stage1", 8, 2, act, 0.0, tok, "tp4pp2dp1+sp")
-    zbh1 = [r for r in base if r["layout"].endswith("zbh1")][0]
+    # the split-backward schedule with the lowest predicted step (zbh2 at these micro-batch counts)
+    zbh1 = min((r for r in base if r["layout"].split(", ")[-1] in ("zbh1", "zbh2")), key=lambda r: r["predicted_ms"])
+    sched = zbh1["layout"].split(", ")[-1]
     comp = zbh1["compute_ms"]
     for links, name in ((1, "ring, one link per direction"), (3, "direct, the TP group's 3 links")):
         t_x = link_ms(xfer_bytes, links)
         exposed = max(0.0, t_x - 0.6 * comp)
         pred = zbh1["predicted_ms"] + exposed
-        rows.append({"N": 8, "model": "gpt3-6.7b", "layout": f"tp4pp2+sp, zbh1, TP exchange {name}",
+        rows.append({"N": 8, "model": "gpt3-6.7b", "layout": f"tp4pp2+sp, {sched}, TP exchange {name}",
                      "compute_ms": comp, "stage_ms": zbh1["stage_ms"], "bubble_ms": zbh1["bubble_ms"],
                      "exposed_comm_ms": round(exposed, 1), "predicted_ms": round(pred, 1), "tokens_per_step": tok,
                      "note": f"{xfer_bytes / 1e9:.1f} GB of SP exchanges per rank per step = {t_x:.0f} ms on {links} link(s)"})
@@ -212,13 +215,19 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--only", nargs="*", default=None, help="measure only these runs")
     ap.add_argument("--from-json", default=None)
+    ap.add_argument("--merge-json", default=None,
+                    help="start from these saved measurements; --only re-measures and replaces runs")
     a = ap.parse_args()
     os.makedirs(a.out, exist_ok=True)
     if a.from_json:
         with open(a.from_json) as f:
             m = json.load(f)["measured"]
     else:
-        m = measure(a.steps, a.warmup, a.out, a.only)
+        m = {}
+        if a.merge_json:
+            with open(a.merge_json) as f:
+                m = json.load(f)["measured"]
+        m.update(measure(a.steps, a.warmup, a.out, a.only))
     rows = predict(m)
     g3 = predict_gpt3(m)
     for r in g3:

@@ -20,25 +20,40 @@ Schedules (``train/schedules.py`` names):
                  in its cooldown, are not held up by W work, and that W work then runs while the
                  earlier stages finish (ZB-H1's idea, Qi et al., "Zero Bubble Pipeline
                  Parallelism", 2023: same activation memory as 1F1B, bubble ~ (pp-1)(F+B-W)).
+* ``zbh2``     — ZB-H2-style: rank r runs 2 (pp - r - 1) forwards ahead (twice 1F1B's in-flight
+                 micro-batches: the later stages never wait for an input after the first) and
+                 defers the W of its last 2 (r + 1) passes. Activation memory on stage r grows to
+                 2 (pp - r) - 1 micro-batches — free on a 288 GB MI355X (GPT-2 345M at tp2: ~1.6 GB
+                 per in-flight micro-batch). At the BASELINE tp2pp2 point the bubble drops to the
+                 first forward + hop that the last stage cannot avoid (16.2 -> 9.6 ms); with
+                 m <= pp micro-batches it loses to zbh1.
 """
 from __future__ import annotations
 
 from typing import Dict, List, Sequence, Tuple
 
-SCHEDULES = ("1f1b", "zb", "zbh1")
+SCHEDULES = ("1f1b", "zb", "zbh1", "zbh2")
+
+
+def warmup_and_defer(schedule: str, pp: int, r: int, m: int) -> Tuple[int, int]:
+    """(forwards rank r runs before its first backward, first backward pass whose W is deferred
+    behind the rank's last B) — shared with train/schedules.py so the simulation and the real
+    schedule issue the same order."""
+    if schedule == "zbh2":
+        return min(2 * (pp - r - 1), m), max(0, m - 2 * (r + 1))
+    warm = min(pp - r - 1, m)
+    return warm, (max(0, m - (r + 1)) if schedule == "zbh1" else m)
 
 
 def rank_ops(schedule: str, pp: int, r: int, m: int) -> List[Tuple[str, int]]:
     """The op sequence rank ``r`` issues: ("F", k), ("B", k), ("W", k) or ("BW", k) (1f1b)."""
     if schedule not in SCHEDULES:
         raise ValueError(f"unknown schedule {schedule!r}")
-    warm = min(pp - r - 1, m)
+    warm, defer_from = warmup_and_defer(schedule, pp, r, m)
     steady = m - warm
     ops: List[Tuple[str, int]] = [("F", k) for k in range(warm)]
     fk, bk = warm, 0
     deferred: List[int] = []
-
-    defer_from = m - (r + 1) if schedule == "zbh1" else m
 
     def backward(k):
         if schedule == "1f1b":

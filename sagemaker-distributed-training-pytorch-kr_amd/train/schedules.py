@@ -18,6 +18,7 @@ import torch.distributed as dist
 
 from ..comm import stats as _cs
 from ..parallel import state as ps
+from .pipeline_sim import warmup_and_defer
 
 
 def _ddp_list(models):
@@ -278,7 +279,11 @@ def _run_backward(out, gout):
 #          last B (ZB-H1): the final B chain the earlier stages wait for in the cooldown is not
 #          held up by W work, which then fills their drain instead. Same activation memory as
 #          1F1B; the held W operands (dY, X) of up to pp micro-batches stay in HBM.
-PP_SCHEDULES = ("1f1b", "zb", "zbh1")
+#   zbh2 : ZB-H2-style: rank r runs 2 (pp - r - 1) forwards ahead and defers the W of its last
+#          2 (r + 1) passes. Up to 2 (pp - r) - 1 micro-batches of activations in flight on stage
+#          r — HBM the 288 GB part has to spare — for a bubble of just the last stage's first wait
+#          (train/pipeline_sim.py: 16.2 -> 9.6 ms at the tp2pp2 BASELINE point).
+PP_SCHEDULES = ("1f1b", "zb", "zbh1", "zbh2")
 _PP_SCHEDULE = {"name": "zbh1"}
 
 
@@ -306,16 +311,16 @@ def forward_backward_pipelining_without_interleaving(forward_step_func: Callable
     first, last = st.is_first_stage(), st.is_last_stage()
     gate = _SyncGate(models)
     gate.set(False)
-    warm = min(st.pp - st.pp_rank - 1, num_microbatches)
+    schedule = schedule or get_pipeline_schedule()
+    warm, defer_from = warmup_and_defer(schedule if not forward_only else "1f1b", st.pp, st.pp_rank,
+                                        num_microbatches)
     steady = num_microbatches - warm
     inputs: List[Optional[torch.Tensor]] = []
     outputs: List[torch.Tensor] = []
     losses = []
     n_backward = [0]
-    schedule = schedule or get_pipeline_schedule()
-    split = schedule in ("zb", "zbh1") and not forward_only and DEFERRED_WGRAD.enabled
-    # zbh1: backward passes >= defer_from keep their W queued until after the last B of the step
-    defer_from = num_microbatches - (st.pp_rank + 1) if schedule == "zbh1" else num_microbatches
+    split = schedule in ("zb", "zbh1", "zbh2") and not forward_only and DEFERRED_WGRAD.enabled
+    # zbh1 / zbh2: backward passes >= defer_from keep their W queued until after the last B
     concat0 = DEFERRED_WGRAD.concat_segments
 
     def fwd(inp):

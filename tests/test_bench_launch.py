@@ -93,11 +93,12 @@ def test_bench_ranks_gloo(n, layout, want, tmp_path):
     (["--pp-schedule", "1f1b"], "1f1b"),
     (["--pp-schedule", "zb"], "zb"),
     (["--pp-schedule", "zbh1"], "zbh1"),
+    ([], "zbh2"),
     (["--vpp", "2"], "interleaved vpp2"),
 ])
 def test_bench_pipeline_schedules_gloo(extra, want, tmp_path):
     """tp2 pp2 at N = 4 under each pipeline schedule bench.py can select (the zero-bubble split
-    backward, the default zbh1, and the interleaved virtual pipeline): the JSON names it."""
+    backward, zbh1, the default zbh2, and the interleaved virtual pipeline): the JSON names it."""
     rec = _run_bench(4, "tp", tmp_path, extra)
     assert rec["config"]["pp_schedule"] == want and rec["config"]["parallelism"] == "tp2pp2dp1+sp"
     assert rec["value"] > 0 and rec["final_loss"] > 0
@@ -117,6 +118,21 @@ def test_bench_emulated_tp_rank(tmp_path):
     rec = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
     assert rec["config"]["tp"] == 2 and "emulated" in rec["config"]["parallelism"]
     assert rec["config"]["model"].endswith("vocab 256, seq 32)")   # padded to 128 x tp and rec["final_loss"] > 0
+
+
+@pytest.mark.parametrize("stage", ["--emulate-first-stage", "--emulate-last-stage"])
+def test_bench_emulated_pipeline_stage(tmp_path, stage):
+    """The per-stage emulations predict_scaling.py times: the first stage without the LM head, the
+    last without the embedding (its input a received activation), each with the F / B / W probe."""
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", OMP_NUM_THREADS="1")
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--emulate-tp", "2", "--micro-batch-size", "2",
+           "--grad-accum", "2", "--phase-probe", "2", stage] + TINY
+    r = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert rec["value"] > 0 and set(rec["fbw_ms"]) >= {"F", "B", "W"}
 
 
 @pytest.mark.slow

@@ -268,7 +268,7 @@ def test_ddp_gradient_accumulation_matches_single_process(world, tp, pp, nmb, ze
         _check_tp_grads(ref, grads, meta, tp)
 
 
-@pytest.mark.parametrize("schedule", ["1f1b", "zb", "zbh1"])
+@pytest.mark.parametrize("schedule", ["1f1b", "zb", "zbh1", "zbh2"])
 @pytest.mark.parametrize("world,tp,pp,nmb,zero,sp,layers", [
     (4, 2, 2, 4, False, True, 2),      # tp2 pp2 + SP, 4 micro-batches of 1
     (4, 1, 4, 4, False, False, 4),     # pp4: three ranks with a cooldown, zbh1 holds up to 4 W
@@ -276,7 +276,8 @@ def test_ddp_gradient_accumulation_matches_single_process(world, tp, pp, nmb, ze
 ])
 def test_split_backward_schedules_match_single_rank(schedule, world, tp, pp, nmb, zero, sp, layers):
     """The zero-bubble split backward (train/schedules.py: W GEMMs after the input gradient is
-    sent; zbh1 also holds the last r + 1 passes' W of rank r until its final B) gives the
+    sent; zbh1 also holds the last r + 1 passes' W of rank r until its final B; zbh2 runs
+    2 (pp - r - 1) forwards ahead and holds the last 2 (r + 1) passes' W) gives the
     single-process losses and reduced gradients, with the deferred wgrad queue active on CPU."""
     over = {"num_layers": layers}
     ref_loss, ref = W.gpt_reference(cfg_over=over)
@@ -286,7 +287,8 @@ def test_split_backward_schedules_match_single_rank(schedule, world, tp, pp, nmb
         ws = meta["wgrad_stats"]
         assert ws["items"] > 0, ws                       # the weight gradients went through the queue
         # zbh1: rank r (>= 1) held its last r + 1 passes' W and merged them with the sync pass's
-        held = schedule == "zbh1" and meta["pp_rank"] >= 1
+        # zbh2: every rank holds >= 2 passes' W (2 (r + 1) of them) and merges them
+        held = (schedule == "zbh1" and meta["pp_rank"] >= 1) or schedule == "zbh2"
         assert (ws["max_segments"] >= 2) == held, (schedule, meta["pp_rank"], ws)
     for loss, _, meta in outs:
         if meta["pp_rank"] == pp - 1:

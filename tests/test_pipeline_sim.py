@@ -48,6 +48,24 @@ def test_bubble_ordering_and_closed_forms():
     assert b4["zbh1"] < b4["zb"] < b4["1f1b"]
 
 
+def test_zbh2_runs_ahead_and_reaches_the_startup_bound():
+    """zbh2: rank r issues 2 (pp - r - 1) forwards before its first B and defers 2 (r + 1) W; at
+    the measured BASELINE tp2pp2 per-micro-batch costs its bubble is the last stage's unavoidable
+    first wait (stage 0's F + the hop), below zbh1's."""
+    pp, m = 4, 8
+    for r in range(pp):
+        ops = rank_ops("zbh2", pp, r, m)
+        first_b = min(i for i, (kind, _) in enumerate(ops) if kind == "B")
+        assert first_b == 2 * (pp - r - 1) + 1          # the warm-up forwards, then the steady F
+        n_def = min(m, 2 * (r + 1))
+        assert ops[-n_def:] == [("W", k) for k in range(m - n_def, m)]
+    F, B, W, hop = [9.10, 9.24], [11.68, 10.97], [4.77, 5.58], 0.52
+    h1 = simulate("zbh1", 2, 8, F, B, W, p2p=hop)
+    h2 = simulate("zbh2", 2, 8, F, B, W, p2p=hop)
+    assert h2["bubble"] < h1["bubble"]
+    assert h2["makespan"] == pytest.approx(F[0] + hop + 8 * (F[1] + B[1] + W[1]), abs=0.05)
+
+
 def test_p2p_latency_and_uneven_stages():
     pp, m = 2, 8
     F, B, W = [1.0, 1.2], [1.0, 1.3], [0.8, 0.9]

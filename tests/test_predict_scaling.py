@@ -26,7 +26,7 @@ def test_prediction_tables(tmp_path):
     assert r.returncode == 0, r.stderr[-2000:]
     out = json.loads((tmp_path / "predicted.json").read_text())
     n8 = {row["layout"].split(", ")[-1]: row for row in out["rows"] if row["N"] == 8}
-    assert n8["zbh1"]["bubble_ms"] <= n8["zb"]["bubble_ms"] <= n8["1f1b"]["bubble_ms"]
+    assert n8["zbh2"]["bubble_ms"] <= n8["zbh1"]["bubble_ms"] <= n8["zb"]["bubble_ms"] <= n8["1f1b"]["bubble_ms"]
     assert n8["zbh1"]["efficiency_vs_n1"] > n8["1f1b"]["efficiency_vs_n1"]
     assert "interleaved vpp2 (even 12|12 split)" in n8
     g3 = out["gpt3_rows"]
