@@ -169,15 +169,18 @@ def predict(m: dict) -> list:
 
 def predict_gpt3(m: dict) -> list:
     """GPT-3 6.7B, tp4 pp2 + SP on 8 GPUs (BASELINE config #5): per-rank compute from the emulated
-    stages; the sequence-parallel exchanges per rank and step (10 per layer and micro-batch, each
-    3/4 of a [2048, 4, 4096] bf16 activation) over ONE link per direction (the ring) or over the
+    stages; the sequence-parallel exchanges per rank and step (8 per layer and micro-batch — the
+    all-gathers before QKV and fc1 and the reduce-scatters after proj and fc2, forward, and their
+    mirror images in backward (the gathered inputs are kept for the weight gradients, no re-gather)
+    — plus the embedding's / LM head's 2 per micro-batch, each 3/4 of a [2048, 4, 4096] bf16
+    activation; round 4 corrected an earlier count of 10 per layer) over ONE link per direction (the ring) or over the
     three links of the TP group (a direct exchange); the part of it that the rank's GEMMs (~60 % of
     its compute, the TP collectives' overlap partners) cannot hide is exposed."""
     if not ("gpt3_tp4_stage0" in m and "gpt3_tp4_stage1" in m):
         return []
     rows = []
     sl, mb, h, layers = 2048, 4, 4096, 16
-    xfer_bytes = layers * 8 * 10 * 0.75 * sl * mb * h * 2
+    xfer_bytes = 8 * (8 * layers + 2) * 0.75 * sl * mb * h * 2   # 8 micro-batches per step
     tok = 32 * sl                                           # tp4 x pp2 = 8 GPUs: ONE replica, 32 sequences
     act = (sl // 4) * mb * h * 2
     base = pipeline_rows(m, "gpt3_tp4_stage0", "gpt3_tp4_stage1", 8, 2, act, 0.0, tok, "tp4pp2dp1+sp")
