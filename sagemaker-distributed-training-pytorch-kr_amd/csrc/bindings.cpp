@@ -44,9 +44,19 @@ void need_contig(const Tensor& t, const char* name) {
 const void* optr(const OptT& t) { return t.has_value() ? t->data_ptr() : nullptr; }
 
 // ------------------------------------------------------------------ LayerNorm / RMSNorm
+// out_y (optional): a contiguous tensor of x's size and dtype the normalised output is written
+// into — a slice of a sequence-parallel all-gather buffer, so the gather needs no local copy.
+static Tensor out_or_new(const OptT& out, const Tensor& like, const char* n) {
+  if (!out) return torch::empty_like(like);
+  TORCH_CHECK(out->is_contiguous() && out->numel() == like.numel() && out->dtype() == like.dtype() &&
+                  out->device() == like.device(),
+              n, ": output buffer must be contiguous with the input's size, dtype and device");
+  return out->view(like.sizes());
+}
+
 std::vector<Tensor> layernorm_fwd(Tensor x, OptT res, OptT bias, Tensor gamma, OptT beta,
                                   double eps, double p_drop, int64_t seed, int64_t offset,
-                                  bool rms, bool want_s) {
+                                  bool rms, bool want_s, OptT out_y) {
   need_contig(x, "x");
   need_contig(gamma, "gamma");
   const int64_t H = x.size(-1);
@@ -55,7 +65,7 @@ std::vector<Tensor> layernorm_fwd(Tensor x, OptT res, OptT bias, Tensor gamma, O
   if (res) { need_contig(*res, "residual"); TORCH_CHECK(res->sizes() == x.sizes() && res->dtype() == x.dtype(), "layernorm: residual mismatch"); }
   if (bias) { need_contig(*bias, "bias"); TORCH_CHECK(bias->numel() == H && bias->dtype() == gamma.dtype(), "layernorm: bias mismatch"); }
   if (beta) { need_contig(*beta, "beta"); TORCH_CHECK(beta->numel() == H && beta->dtype() == gamma.dtype(), "layernorm: beta mismatch"); }
-  auto y = torch::empty_like(x);
+  auto y = out_or_new(out_y, x, "layernorm_fwd");
   Tensor s;
   const bool make_s = want_s || res.has_value() || bias.has_value() || p_drop > 0.0;
   if (make_s) s = torch::empty_like(x);
@@ -83,7 +93,7 @@ static Tensor acc_target(const OptT& t, int64_t H, const char* n) {
 std::vector<Tensor> layernorm_bwd(Tensor dy, OptT ds_in, Tensor s, Tensor gamma, Tensor mean,
                                   Tensor rstd, double p_drop, int64_t seed, int64_t offset,
                                   bool rms, bool want_dx, bool want_dbias, OptT dgamma_acc,
-                                  OptT dbeta_acc, OptT dbias_acc) {
+                                  OptT dbeta_acc, OptT dbias_acc, OptT out_dx) {
   need_contig(dy, "dy");
   need_contig(s, "s");
   need_contig(gamma, "gamma");
@@ -91,9 +101,11 @@ std::vector<Tensor> layernorm_bwd(Tensor dy, OptT ds_in, Tensor s, Tensor gamma,
   const int64_t rows = s.numel() / H;
   TORCH_CHECK(dy.sizes() == s.sizes() && dy.dtype() == s.dtype(), "layernorm_bwd: dy mismatch");
   if (ds_in) { need_contig(*ds_in, "ds_in"); TORCH_CHECK(ds_in->sizes() == s.sizes() && ds_in->dtype() == s.dtype(), "layernorm_bwd: ds_in mismatch"); }
-  auto ds = torch::empty_like(s);
+  // out_dx (optional): where dx goes (a slice of an all-gather buffer, see layernorm_fwd); without
+  // dropout dx IS ds, so ds lands there too
   const bool sep = want_dx && p_drop > 0.0;
-  Tensor dx = sep ? torch::empty_like(s) : ds;
+  auto ds = (out_dx && !sep) ? out_or_new(out_dx, s, "layernorm_bwd") : torch::empty_like(s);
+  Tensor dx = sep ? out_or_new(out_dx, s, "layernorm_bwd") : ds;
   const int nb = smdt_ln_bwd_nblocks(rows, (int)H);
   auto f32 = s.options().dtype(at::kFloat);
   auto partials = torch::empty({nb, 3, H}, f32);
@@ -681,12 +693,14 @@ void register_blaslt(pybind11::module_& m);
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "smdt_amd gfx950 (MI355X) HIP kernel library";
   register_blaslt(m);
-  m.def("layernorm_fwd", &layernorm_fwd);
   using pybind11::arg;
+  m.def("layernorm_fwd", &layernorm_fwd, arg("x"), arg("res"), arg("bias"), arg("gamma"), arg("beta"),
+        arg("eps"), arg("p_drop"), arg("seed"), arg("offset"), arg("rms"), arg("want_s"),
+        arg("out_y") = pybind11::none());
   m.def("layernorm_bwd", &layernorm_bwd, arg("dy"), arg("ds_in"), arg("s"), arg("gamma"), arg("mean"),
         arg("rstd"), arg("p_drop"), arg("seed"), arg("offset"), arg("rms"), arg("want_dx"), arg("want_dbias"),
         arg("dgamma_acc") = pybind11::none(), arg("dbeta_acc") = pybind11::none(),
-        arg("dbias_acc") = pybind11::none());
+        arg("dbias_acc") = pybind11::none(), arg("out_dx") = pybind11::none());
   m.def("bias_act_fwd", &bias_act_fwd);
   m.def("bias_act_bwd", &bias_act_bwd, arg("dy"), arg("x"), arg("bias"), arg("act"), arg("want_dbias"),
         arg("dbias_acc") = pybind11::none());

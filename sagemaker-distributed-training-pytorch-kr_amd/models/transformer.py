@@ -107,9 +107,9 @@ class Norm(nn.Module):
         else:
             self.register_parameter("bias", None)
 
-    def fused(self, x, xbias, residual, p, training):
+    def fused(self, x, xbias, residual, p, training, gather=None):
         return SF.bias_dropout_add_norm(x, xbias, residual, self.weight, self.bias, p, training, self.eps, self.rms,
-                                        rng=get_rng(self.rng_kind))
+                                        rng=get_rng(self.rng_kind), gather=gather)
 
     def forward(self, x):
         return self.fused(x, None, None, 0.0, False)[0]
@@ -337,6 +337,13 @@ class ParallelMLP(nn.Module):
         return self.fc2(h)
 
 
+def _sp_gather(cfg):
+    """(tp, tp_rank) when sequence-parallel norms should write into all-gather slots."""
+    if not cfg.sequence_parallel or _PACK["idx"] is not None:
+        return None
+    return tp.sp_gather_spec()
+
+
 class ParallelTransformerLayer(nn.Module):
     def __init__(self, cfg: TransformerConfig, layer_number: int, device=None):
         super().__init__()
@@ -350,9 +357,15 @@ class ParallelTransformerLayer(nn.Module):
     def forward(self, x, xbias, residual):
         training = self.training
         p = self.cfg.hidden_dropout
-        ln1, residual = self.input_norm.fused(x, xbias, residual, p, training)
+        # sequence parallelism: each norm's output is all-gathered by the next column-parallel
+        # linear and (after a layer) its input gradient by the row-parallel linear that produced
+        # x — both are written straight into their slot of the gather buffer (no local copy)
+        g = _sp_gather(self.cfg)
+        ln1, residual = self.input_norm.fused(x, xbias, residual, p, training,
+                                              gather=None if g is None else g + (True, residual is not None))
         a, ab = self.attention(ln1, training)
-        ln2, residual = self.post_attention_norm.fused(a, ab, residual, p, training)
+        ln2, residual = self.post_attention_norm.fused(a, ab, residual, p, training,
+                                                       gather=None if g is None else g + (True, True))
         m, mb = self.mlp(ln2)
         return m, mb, residual
 
@@ -389,6 +402,8 @@ class ParallelTransformer(nn.Module):
         for i in range(len(self.layers)):
             x, xbias, residual = self._run(i, x, xbias, residual)
         if self.final_norm is not None:
-            y, _ = self.final_norm.fused(x, xbias, residual, self.cfg.hidden_dropout, self.training)
+            g = _sp_gather(self.cfg)          # y feeds the LM head's column-parallel all-gather
+            y, _ = self.final_norm.fused(x, xbias, residual, self.cfg.hidden_dropout, self.training,
+                                         gather=None if g is None else g + (True, residual is not None))
             return y
         return x, xbias, residual

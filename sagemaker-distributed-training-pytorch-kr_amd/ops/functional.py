@@ -88,16 +88,41 @@ def _mark_ready(*params):
             t._smdt_grad_ready(t)
 
 
+def gather_slot(t, world: int, rank: int):
+    """A [world * n, ...] buffer (uninitialised) and its rank-th row block, the slot ``t``'s
+    producer writes into so that a sequence-parallel all-gather of it needs no local copy
+    (``tensor_parallel.ag_ring`` takes the buffer, marked on the slot as ``_smdt_gather``)."""
+    n = t.shape[0]
+    buf = t.new_empty((world * n,) + tuple(t.shape[1:]))
+    return buf, buf[rank * n:(rank + 1) * n]
+
+
+def _mark_gather(t, buf, rank):
+    t._smdt_gather = (buf, rank)
+    return t
+
+
 class _BDALayerNorm(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, bias, residual, gamma, beta, p, eps, rms, seed, offset):
+    def forward(ctx, x, bias, residual, gamma, beta, p, eps, rms, seed, offset, gather=None):
+        """``gather`` = (world, rank, y_into_gather, dx_into_gather) under sequence parallelism:
+        the normalised output (consumed by a column-parallel ring all-gather) and / or the input
+        gradient (consumed by a row-parallel linear's backward all-gather) are written into their
+        rank's slot of a gather buffer."""
         C = _ext.ext()
-        y, s, mean, rstd = C.layernorm_fwd(x.contiguous(), None if residual is None else residual.contiguous(),
-                                           bias, gamma, beta, eps, p, seed, offset, rms, True)
+        x = x.contiguous()
+        buf = out_y = None
+        if gather is not None and gather[2]:
+            buf, out_y = gather_slot(x, gather[0], gather[1])
+        y, s, mean, rstd = C.layernorm_fwd(x, None if residual is None else residual.contiguous(),
+                                           bias, gamma, beta, eps, p, seed, offset, rms, True, out_y)
+        if buf is not None:
+            _mark_gather(y, buf, gather[1])
         ctx.save_for_backward(s, gamma, mean, rstd)
         ctx.pref = (bias, gamma, beta)  # parameter objects: their main_grad / readiness hooks
         ctx.cfg = (p, seed, offset, rms, bias is not None, residual is not None, beta is not None,
                    gamma.dtype, None if bias is None else bias.dtype)
+        ctx.gather = gather
         return y, s
 
     @staticmethod
@@ -112,28 +137,34 @@ class _BDALayerNorm(torch.autograd.Function):
         ta = grad_accumulate_target(gamma_p)
         tb = grad_accumulate_target(beta_p) if has_beta else None
         tc = grad_accumulate_target(bias_p) if has_bias else None
+        gbuf = out_dx = None
+        if ctx.gather is not None and ctx.gather[3]:
+            gbuf, out_dx = gather_slot(s, ctx.gather[0], ctx.gather[1])
         d_s, dx, dgamma, dbeta, dbias = C.layernorm_bwd(dy, ds, s, gamma, mean, rstd, p, seed, offset, rms,
-                                                        True, has_bias, ta, tb, tc)
+                                                        True, has_bias, ta, tb, tc, out_dx)
+        if gbuf is not None:
+            _mark_gather(dx, gbuf, ctx.gather[1])
         _mark_ready(gamma_p if ta is not None else None, beta_p if tb is not None else None,
                     bias_p if tc is not None else None)
         g_gamma = None if ta is not None else dgamma.to(gdt)
         g_beta = None if (not has_beta or tb is not None) else dbeta.to(gdt)
         g_bias = None if (not has_bias or tc is not None) else dbias.to(bdt)
-        return (dx, g_bias, d_s if has_res else None, g_gamma, g_beta, None, None, None, None, None)
+        return (dx, g_bias, d_s if has_res else None, g_gamma, g_beta, None, None, None, None, None, None)
 
 
 def bias_dropout_add_norm(x, bias, residual, gamma, beta, p: float, training: bool, eps: float = 1e-5,
-                          rms: bool = False, rng: Optional[PhiloxState] = None):
+                          rms: bool = False, rng: Optional[PhiloxState] = None, gather=None):
     """Returns ``(norm(s), s)`` with ``s = residual + dropout(x + bias)``.
 
     ``bias``, ``residual`` may be None; ``beta`` is ignored for RMSNorm. This is the
     residual-stream step of a pre-LN transformer fused with the following LayerNorm.
+    ``gather`` (world, rank, y, dx): see ``_BDALayerNorm.forward`` (kernel path only).
     """
     p = float(p) if training else 0.0
     if _ext.use_kernels(x):
         seed, offset = _rng(rng).next() if p > 0 else (0, 0)
         return _BDALayerNorm.apply(x, bias, residual, gamma, None if rms else beta, p, float(eps), bool(rms),
-                                   int(seed), int(offset))
+                                   int(seed), int(offset), gather)
     h = x if bias is None else x + bias
     if p > 0:
         h = F.dropout(h, p=p, training=True)

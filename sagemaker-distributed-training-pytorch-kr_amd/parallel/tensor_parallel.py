@@ -719,6 +719,11 @@ def _direct(group):
     return td if (td is not None and group is st.tp_group and td.active) else None
 
 
+_SP_GATHER_SLOTS = os.environ.get("SMDT_SP_GATHER_SLOTS", "1") == "1"   # A/B switch
+# ring all-gathers whose local block was already in place (written by its producer) vs copied
+AG_RING_STATS = {"in_place": 0, "copied": 0}
+
+
 def ag_ring(x, group, chunk_fn=None, before_last_wait=None, _skip_direct=False):
     """All-gather ``x`` along dim 0 over ``group`` as a ring; ``chunk_fn(c, chunk)`` runs on chunk c
     as soon as it is resident, while the next chunk is in flight. Returns the gathered tensor.
@@ -732,8 +737,15 @@ def ag_ring(x, group, chunk_fn=None, before_last_wait=None, _skip_direct=False):
             return out
     ws, r, nxt, prv = _ring(group)
     n = x.shape[0]
-    total = x.new_empty((n * ws,) + tuple(x.shape[1:]))
-    total[r * n:(r + 1) * n].copy_(x)
+    mark = getattr(x, "_smdt_gather", None)
+    if (mark is not None and mark[1] == r and mark[0].shape[0] == n * ws and mark[0].shape[1:] == x.shape[1:]
+            and mark[0].is_contiguous() and x.is_contiguous() and x.data_ptr() == mark[0][r * n].data_ptr()):
+        total = mark[0]        # x's producer wrote it into its slot of the gather buffer: no copy
+        AG_RING_STATS["in_place"] += 1
+    else:
+        total = x.new_empty((n * ws,) + tuple(x.shape[1:]))
+        total[r * n:(r + 1) * n].copy_(x)
+        AG_RING_STATS["copied"] += 1
     for s in range(ws):
         c = (r - s) % ws
         works = None
@@ -775,6 +787,19 @@ def rs_ring(partial_fn, group, before_last_wait=None):
         keep.append(part)
         works = _exchange(part, incoming, nxt, prv, group)
     return None  # unreachable
+
+
+def sp_gather_spec():
+    """(world, rank) of the TP group when sequence-parallel linears run the ring collective-matmul
+    (``ag_ring`` can take a producer-filled gather buffer), else None. The multi-link direct
+    engine allocates its own buffers."""
+    st = ps.get_state()
+    if not _TP_OVERLAP or not _SP_GATHER_SLOTS or st.tp <= 1 or st.tp_group is None:
+        return None
+    td = getattr(st, "tp_direct", None)
+    if td is not None and td.active:
+        return None
+    return st.tp, st.tp_rank
 
 
 def _flush_wgrad():

@@ -1087,3 +1087,45 @@ def tp_direct_worker(rank, world, port, outdir):
         res["err"] = traceback.format_exc()
     with open(os.path.join(outdir, f"r{rank}.pkl"), "wb") as f:
         pickle.dump(res, f)
+
+
+def sp_gather_slots_worker():
+    """(one GPU process) A TP2 + SP GPT rank emulated on a loopback group: forward + backward with
+    the sequence-parallel norms writing into their all-gather slots (no local copy in ag_ring),
+    then again with the slots off. Prints one JSON line: max |diff| of the loss and of every
+    gradient, and the ag_ring in-place / copied counts of each pass."""
+    import json
+    from smdt_amd.models.gpt import GPTModel
+    from smdt_amd.models.transformer import TransformerConfig
+    from smdt_amd.parallel import state as ps
+    from smdt_amd.parallel import tensor_parallel as tp
+    from smdt_amd.parallel.random import model_parallel_seed
+    ps.initialize_emulated_tensor_parallel(2)
+    model_parallel_seed(1234)
+    cfg = TransformerConfig(num_layers=2, hidden_size=256, num_attention_heads=4, max_position_embeddings=128,
+                            padded_vocab_size=512, hidden_dropout=0.0, attention_dropout=0.0,
+                            params_dtype=torch.bfloat16, sequence_parallel=True, use_flash_attn=True)
+    model = GPTModel(cfg, device="cuda")
+    g = torch.Generator(device="cuda")
+    g.manual_seed(7)
+    toks = torch.randint(0, 500, (4, 129), device="cuda", generator=g)
+
+    def run():
+        for p in model.parameters():
+            p.grad = None
+        tp.AG_RING_STATS.update(in_place=0, copied=0)
+        loss = model(toks[:, :-1], None, None, labels=toks[:, 1:]).float().mean()
+        loss.backward()
+        torch.cuda.synchronize()
+        return loss.detach(), {n: p.grad.float().clone() for n, p in model.named_parameters() if p.grad is not None}, \
+            dict(tp.AG_RING_STATS)
+    l1, g1, s1 = run()
+    orig = tp.sp_gather_spec
+    tp.sp_gather_spec = lambda: None
+    try:
+        l0, g0, s0 = run()
+    finally:
+        tp.sp_gather_spec = orig
+    diff = max(float((g1[k] - g0[k]).abs().max()) for k in g0)
+    print(json.dumps({"loss_diff": float((l1 - l0).abs()), "grad_max_diff": diff, "n_grads": len(g0),
+                      "same_keys": sorted(g0) == sorted(g1), "stats_slots": s1, "stats_copy": s0}), flush=True)

@@ -251,3 +251,26 @@ def test_merged_accumulation_window_wgrad_matches_per_microbatch():
     for n in p2:
         far = ((p1[n] - p2[n]).abs() > 2e-3 + 1e-2 * p2[n].abs()).float().mean().item()
         assert far < 0.01, (n, far)
+
+
+def test_sp_norms_write_into_all_gather_slots():
+    """Sequence parallelism at TP2 (one process, loopback group): the fused norms write their
+    output (forward) and input gradient (backward) into their rank's slot of the ring all-gather
+    buffer, so ``ag_ring`` copies nothing; loss and every gradient equal the copying path's."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = "import sys; sys.path[:0] = [%r, %r]; import dist_workers as W; W.sp_gather_slots_worker()" % (
+        os.path.join(root, "tests"), root)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300, cwd=root)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    # 2 layers: QKV / fc1 forward gathers + proj / fc2 backward gathers + the LM head's = 9 per pass,
+    # all in place except the first layer's fc2-less input (none) -> every gather is in place
+    assert rec["stats_slots"]["copied"] == 0 and rec["stats_slots"]["in_place"] >= 8, rec
+    assert rec["stats_copy"]["in_place"] == 0 and rec["stats_copy"]["copied"] == rec["stats_slots"]["in_place"], rec
+    assert rec["same_keys"] and rec["n_grads"] > 10
+    assert rec["loss_diff"] == 0.0
+    assert rec["grad_max_diff"] < 1e-3, rec
