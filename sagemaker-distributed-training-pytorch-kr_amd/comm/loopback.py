@@ -18,19 +18,38 @@ per-rank emulation with SP on and the real ring-chunk GEMM shapes, with a local-
 the exchange, so compute is timed honestly". The link time of the real exchange is charged
 separately by ``benchmarks/predict_scaling.py``.
 
+Streams: as RCCL runs a collective on its own stream (the caller's stream waits for it only at
+``Work.wait()``), the all-gather / reduce-scatter stand-ins on CUDA tensors run on a side stream
+and return a Work whose CUDA future completes there — an ``async_op=True`` collective (DDP /
+ZeRO buckets during backward) overlaps the rank's compute as the real one would, a synchronous one
+is waited for at once. ``SMDT_LOOPBACK_ASYNC=0`` runs them in line on the caller's stream.
+
 Values are not those of a real TP run (a reduction sees only this rank's partial), so this is for
 timing, never for training.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.distributed as dist
+
+_ASYNC = os.environ.get("SMDT_LOOPBACK_ASYNC", "1") == "1"
 
 
 def _done(result):
     from torch._C._distributed_c10d import _create_work_from_future
     fut = torch.futures.Future()
     fut.set_result(result)
+    return _create_work_from_future(fut)
+
+
+def _stream_work(result, stream, dev):
+    """A Work whose CUDA future completes on ``stream`` (wait() = a device-side dependency)."""
+    from torch._C._distributed_c10d import _create_work_from_future
+    fut = torch.futures.Future(devices=[dev])
+    with torch.cuda.stream(stream):
+        fut.set_result(result)
     return _create_work_from_future(fut)
 
 
@@ -42,6 +61,25 @@ class LoopbackGroup(dist.ProcessGroup):
         self.world = int(size)
         # c10d's group table: get_rank(group) / get_process_group_ranks(group) work on it
         dist.distributed_c10d._world.pg_group_ranks[self] = {i: i for i in range(self.world)}
+        self._streams = {}
+
+    def _issue(self, tensors, fn, result):
+        """Run ``fn`` (the stand-in's copies / adds) on this group's side stream after the
+        caller's pending work, like a comm kernel; CPU tensors (or SMDT_LOOPBACK_ASYNC=0): in line."""
+        t0 = tensors[0]
+        if not (_ASYNC and t0.is_cuda):
+            fn()
+            return _done(result)
+        dev = t0.device
+        side = self._streams.get(dev)
+        if side is None:
+            side = self._streams[dev] = torch.cuda.Stream(device=dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            fn()
+        for t in tensors:
+            t.record_stream(side)     # the caller may free them before the side stream is done
+        return _stream_work(result, side, dev)
 
     def getBackendName(self) -> str:
         return "loopback"
@@ -56,33 +94,37 @@ class LoopbackGroup(dist.ProcessGroup):
         return _done([])
 
     def _allgather_base(self, out, inp, opts=None):
-        n = inp.numel()
-        flat = out.view(-1)
-        for r in range(self.world):
-            flat[r * n:(r + 1) * n].copy_(inp.view(-1))
-        return _done([out])
+        def fn():
+            n = inp.numel()
+            flat = out.view(-1)
+            for r in range(self.world):
+                flat[r * n:(r + 1) * n].copy_(inp.view(-1))
+        return self._issue([out, inp], fn, [out])
 
     def allgather(self, outs, inps, opts=None):
-        for o in outs[0]:
-            o.copy_(inps[0])
-        return _done(outs)
+        def fn():
+            for o in outs[0]:
+                o.copy_(inps[0])
+        return self._issue(list(outs[0]) + [inps[0]], fn, outs)
 
     def _reduce_scatter_base(self, out, inp, opts=None):
-        n = out.numel()
-        flat = inp.reshape(-1)
-        out.view(-1).copy_(flat[:n])
-        for r in range(1, self.world):
-            out.view(-1).add_(flat[r * n:(r + 1) * n])
-        if opts is not None and opts.reduceOp == dist.ReduceOp.AVG:
-            out.div_(self.world)         # RCCL's AVG: the scale applies to this rank's slice only
-        return _done([out])
+        def fn():
+            n = out.numel()
+            flat = inp.reshape(-1)
+            out.view(-1).copy_(flat[:n])
+            for r in range(1, self.world):
+                out.view(-1).add_(flat[r * n:(r + 1) * n])
+            if opts is not None and opts.reduceOp == dist.ReduceOp.AVG:
+                out.div_(self.world)         # RCCL's AVG: the scale applies to this rank's slice only
+        return self._issue([out, inp], fn, [out])
 
     def reduce_scatter(self, outs, inps, opts=None):
-        out = outs[0]
-        out.copy_(inps[0][0])
-        for t in inps[0][1:]:
-            out.add_(t)
-        return _done(outs)
+        def fn():
+            out = outs[0]
+            out.copy_(inps[0][0])
+            for t in inps[0][1:]:
+                out.add_(t)
+        return self._issue([outs[0]] + list(inps[0]), fn, outs)
 
 
 def is_loopback(group) -> bool:

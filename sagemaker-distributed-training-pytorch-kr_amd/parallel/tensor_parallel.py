@@ -593,11 +593,51 @@ def _dgrad_weight_t(weight):
     return None
 
 
+# Row-split GEMMs. hipBLASLt's heuristic picks poor kernels for token counts just above a multiple
+# of 4096 (the SFT recipe's packed windows: M ~ 4.3 k varies every step, so no per-shape tuning
+# applies): LLaMA-7B layer GEMMs at M = 4300 run at 845 TF/s whole and 1207 TF/s as 4096 rows +
+# the remainder (4608: 927 -> 1206, 8600: 1087 -> 1309; at 5000 / 6100 the whole GEMM is as fast
+# or faster; benchmarks/bench_sft_gemm_split.py, profiles/r4_sft_gemm_split/). So a GEMM whose
+# M exceeds a multiple of SMDT_GEMM_ROW_SPLIT (4096; 0 = off) by at most a sixth of it is issued
+# as two row blocks into one output.
+_ROW_SPLIT = int(os.environ.get("SMDT_GEMM_ROW_SPLIT", "4096"))
+
+
+def _row_blocks(M: int):
+    q = _ROW_SPLIT
+    if q <= 0 or M <= q:
+        return None
+    r = M % q
+    if r == 0 or r > q // 6:
+        return None
+    return ((0, M - r), (M - r, M))
+
+
+def linear_rows(x, w, bias=None):
+    """F.linear(x, w, bias), split into row blocks when ``_row_blocks`` says the whole GEMM would
+    take a slow hipBLASLt kernel (CUDA only; identical results: each row's dot products are the
+    same)."""
+    if x.is_cuda and x.dim() >= 2:
+        M = x.numel() // x.shape[-1]
+        bl = _row_blocks(M)
+        if bl is not None:
+            x2 = x.reshape(M, x.shape[-1])
+            out = x.new_empty(tuple(x.shape[:-1]) + (w.shape[0],))
+            o2 = out.view(M, w.shape[0])
+            for a, b in bl:
+                if bias is not None:
+                    torch.addmm(bias, x2[a:b], w.t(), out=o2[a:b])
+                else:
+                    torch.mm(x2[a:b], w.t(), out=o2[a:b])
+            return out
+    return F.linear(x, w, bias)
+
+
 def dgrad(g, weight, wt=None):
     """dX = g @ weight (g [..., out], weight [out, in]); ``wt`` = weight^T from _dgrad_weight_t."""
     if wt is None:
         return g.matmul(weight)
-    return F.linear(g, wt)
+    return linear_rows(g, wt)
 
 
 def dgrad_into(dst, g, weight, wt=None):
@@ -626,7 +666,7 @@ class LinearWithGradAccumulationAndAsyncCommunication(torch.autograd.Function):
         total = _gather_dim0(x, _tp_group()) if sequence_parallel else x
         # add_bias False: the caller adds the bias later (skip_bias_add) and this function only
         # produces its gradient (the column sums of dY) beside the weight gradient
-        return F.linear(total, weight, bias if add_bias else None)
+        return linear_rows(total, weight, bias if add_bias else None)
 
     @staticmethod
     def backward(ctx, g):

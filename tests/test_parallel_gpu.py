@@ -274,3 +274,22 @@ def test_sp_norms_write_into_all_gather_slots():
     assert rec["same_keys"] and rec["n_grads"] > 10
     assert rec["loss_diff"] == 0.0
     assert rec["grad_max_diff"] < 1e-3, rec
+
+
+@pytest.mark.parametrize("M", [4300, 4608, 8600, 5000, 4096])
+def test_row_split_linear_matches_whole(M):
+    """tensor_parallel.linear_rows: token counts just above a multiple of 4096 run as two row
+    blocks (hipBLASLt's whole-GEMM kernel for them is slow); the result equals F.linear's."""
+    torch.manual_seed(0)
+    x = torch.randn(M, 512, device="cuda", dtype=torch.bfloat16)
+    w = torch.randn(768, 512, device="cuda", dtype=torch.bfloat16) * 0.05
+    b = torch.randn(768, device="cuda", dtype=torch.bfloat16)
+    split = tp._row_blocks(M) is not None
+    assert split == (M in (4300, 4608, 8600))
+    for bias in (None, b):
+        ref = x.float() @ w.float().t() + (0 if bias is None else bias.float())
+        out = tp.linear_rows(x, w, bias)
+        assert out.shape == (M, 768)
+        torch.testing.assert_close(out.float(), ref, atol=0.06, rtol=0.02)
+    x3 = x.view(M // 4 if M % 4 == 0 else 1, -1, 512) if M % 4 == 0 else x.view(1, M, 512)
+    torch.testing.assert_close(tp.linear_rows(x3, w).reshape(M, 768), tp.linear_rows(x, w))
