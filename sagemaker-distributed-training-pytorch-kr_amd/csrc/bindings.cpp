@@ -361,11 +361,14 @@ bool wgrad_mfma(Tensor main_grad, Tensor dy, Tensor x, int64_t max_splits) {
 // Returns false (and does nothing) when any problem is unsupported. The targets must not overlap.
 // ``biases`` (optional, one per problem; an empty tensor = none): fp32 [N] targets that receive
 // the column sums of dy — the bias gradient — from the same launch.
+// overwrite (optional, per problem): the main_grad holds no data yet (a lazily zeroed gradient
+// buffer): the kernel stores dy^T x instead of adding it (no read of the target).
 bool wgrad_grouped(std::vector<Tensor> main_grads, std::vector<Tensor> dys, std::vector<Tensor> xs,
-                   std::vector<Tensor> biases) {
+                   std::vector<Tensor> biases, std::vector<bool> overwrite) {
   const size_t n = main_grads.size();
   TORCH_CHECK(dys.size() == n && xs.size() == n, "wgrad_grouped: list lengths differ");
   TORCH_CHECK(biases.empty() || biases.size() == n, "wgrad_grouped: biases list length");
+  TORCH_CHECK(overwrite.empty() || overwrite.size() == n, "wgrad_grouped: overwrite list length");
   std::vector<SmdtWgradProblem> probs(n);
   for (size_t i = 0; i < n; ++i) {
     const Tensor &mg = main_grads[i], &dy = dys[i], &x = xs[i];
@@ -385,7 +388,8 @@ bool wgrad_grouped(std::vector<Tensor> main_grads, std::vector<Tensor> dys, std:
         return false;
       bg = bt.data_ptr<float>();
     }
-    probs[i] = SmdtWgradProblem{dy.data_ptr(), x.data_ptr(), mg.data_ptr<float>(), M, N, K, bg};
+    probs[i] = SmdtWgradProblem{dy.data_ptr(), x.data_ptr(), mg.data_ptr<float>(), M, N, K, bg,
+                                (!overwrite.empty() && overwrite[i]) ? 1 : 0};
   }
   if (n == 0) return true;
   check(smdt_wgrad_grouped_t(dcode(dys[0]), probs.data(), (int)n, cur_stream()), "wgrad_grouped");
@@ -720,7 +724,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bias_grad", &bias_grad);
   m.def("wgrad_mfma", &wgrad_mfma, arg("main_grad"), arg("dy"), arg("x"), arg("max_splits") = 0);
   m.def("wgrad_grouped", &wgrad_grouped, arg("main_grads"), arg("dys"), arg("xs"),
-        arg("biases") = std::vector<Tensor>{});
+        arg("biases") = std::vector<Tensor>{}, arg("overwrite") = std::vector<bool>{});
   m.def("ce_stats", &ce_stats);
   m.def("ce_bwd", &ce_bwd);
   namespace py = pybind11;

@@ -109,6 +109,7 @@ struct SmdtWgradProblem {
   float* main_grad;    // [N, K] fp32, += dy^T x
   int64_t M, N, K;
   float* bias_grad;    // [N] fp32, += column sums of dy (the linear's bias gradient), or null
+  int overwrite;       // 1: main_grad holds no data yet — write dy^T x instead of adding (no read)
 };
 // Many independent wgrad accumulations in one launch per 32 (no split-K, no atomics). The
 // main_grad targets of one call must not overlap.

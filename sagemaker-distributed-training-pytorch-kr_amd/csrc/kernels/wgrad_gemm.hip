@@ -118,7 +118,7 @@ template <bool ATOMIC, int VAR, bool BIAS, class E>
 __device__ __forceinline__ void tile_gemm(const E* __restrict__ A, const E* __restrict__ B,
                                           float* __restrict__ C, int N, int K, int n0, int k0, int64_t mstart,
                                           int nst, char* L0, char* L1, char* L2, char* L3,
-                                          float* __restrict__ bias = nullptr) {
+                                          float* __restrict__ bias = nullptr, bool ovw = false) {
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), h = lane >> 5;
   const int wn = wave >> 2, wk = wave & 3;  // wave tile: n rows [128 wn, +128), k cols [64 wk, +64)
   using F = Frag<BT, E>;
@@ -237,6 +237,9 @@ __device__ __forceinline__ void tile_gemm(const E* __restrict__ A, const E* __re
         if constexpr (ATOMIC) {
 #pragma unroll
           for (int r2 = 0; r2 < 16; ++r2) unsafeAtomicAdd(cp + (int64_t)acc_row(r2, h) * K, acc[i][j][r2]);
+        } else if (ovw) {   // first gradient of the step into an unzeroed buffer: store only
+#pragma unroll
+          for (int r2 = 0; r2 < 16; ++r2) cp[(int64_t)acc_row(r2, h) * K] = acc[i][j][r2];
         } else {
           float old[16];
 #pragma unroll
@@ -252,7 +255,7 @@ __device__ __forceinline__ void tile_gemm(const E* __restrict__ A, const E* __re
           if constexpr (ATOMIC)
             unsafeAtomicAdd(p, acc[i][j][r2]);
           else
-            *p += acc[i][j][r2];
+            *p = ovw ? acc[i][j][r2] : *p + acc[i][j][r2];
         }
       }
     }
@@ -302,6 +305,7 @@ struct Problem {
   float* C;
   float* bias;     // column sums of A (bias gradient) or null
   int M, N, K, ntn, ntk, gn, tile0;
+  int ovw;         // C holds no data yet: the epilogue stores instead of read-add-store
 };
 constexpr int kMaxGroup = 32;
 struct Group {
@@ -344,9 +348,10 @@ __global__ __launch_bounds__(kThreads, 1) void wgrad_grouped_kernel(const Group 
   const E* B = (const E*)P.B;
   if (piece < 0) {
     if (bias_tile)
-      tile_gemm<false, 0, true, E>(A, B, P.C, P.N, P.K, tn * BT, 0, 0, stages, L0, L1, L2, L3, P.bias);
+      tile_gemm<false, 0, true, E>(A, B, P.C, P.N, P.K, tn * BT, 0, 0, stages, L0, L1, L2, L3, P.bias, P.ovw != 0);
     else
-      tile_gemm<false, 0, false, E>(A, B, P.C, P.N, P.K, tn * BT, tk * BT, 0, stages, L0, L1, L2, L3);
+      tile_gemm<false, 0, false, E>(A, B, P.C, P.N, P.K, tn * BT, tk * BT, 0, stages, L0, L1, L2, L3, nullptr,
+                                    P.ovw != 0);
   } else {
     const int s0 = piece * g.mps;
     const int nst = min(stages, s0 + g.mps) - s0;
@@ -452,6 +457,7 @@ extern "C" hipError_t smdt_wgrad_grouped_t(int dtype, const SmdtWgradProblem* pr
       p.ntk = (int)((q.K + wg::BT - 1) / wg::BT);
       p.gn = wg::group_width(p.ntk);
       p.tile0 = tiles;
+      p.ovw = q.overwrite ? 1 : 0;
       tiles += p.ntn * p.ntk;
     }
     for (int i = cnt; i < wg::kMaxGroup; ++i) g.p[i] = g.p[cnt - 1];
@@ -479,6 +485,16 @@ extern "C" hipError_t smdt_wgrad_grouped_t(int dtype, const SmdtWgradProblem* pr
       g.nfull = tiles - r;
       g.splits = splits;
       g.mps = mps;
+      // the split tail adds partial sums with atomics: an overwrite problem with tail tiles is
+      // zeroed first and accumulates like the rest
+      for (int i = 0; i < cnt; ++i) {
+        wg::Problem& p = g.p[i];
+        if (p.ovw && p.tile0 + p.ntn * p.ntk > g.nfull) {
+          hipError_t e = hipMemsetAsync(p.C, 0, (size_t)p.N * (size_t)p.K * sizeof(float), st);
+          if (e != hipSuccess) return e;
+          p.ovw = 0;
+        }
+      }
     }
     const int nblocks = g.nfull + (tiles - g.nfull) * g.splits;
     if (dtype == 2)

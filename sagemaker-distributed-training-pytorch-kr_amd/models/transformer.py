@@ -108,6 +108,12 @@ class Norm(nn.Module):
             self.register_parameter("bias", None)
 
     def fused(self, x, xbias, residual, p, training, gather=None):
+        # called instead of forward() by the layers: run the overlapped ZeRO parameter all-gather's
+        # wait for this module's bucket (a forward pre-hook, parallel/distributed.py) — without it
+        # the norm could read its weights while their all-gather is still in flight
+        for hook in tuple(self._forward_pre_hooks.values()):
+            if getattr(hook, "_smdt_gather_wait", False):
+                hook(self, (x,))
         return SF.bias_dropout_add_norm(x, xbias, residual, self.weight, self.bias, p, training, self.eps, self.rms,
                                         rng=get_rng(self.rng_kind), gather=gather)
 

@@ -308,7 +308,7 @@ class DeferredWgrad:
         # main_grad read-modify-write: the SFT engine's small micro-batches) or issue one grouped
         # launch per segment round (large pipeline micro-batches: no concatenation copy).
         self.concat_segments = True
-        self.stats = {"flushes": 0, "items": 0, "max_segments": 0}
+        self.stats = {"flushes": 0, "items": 0, "max_segments": 0, "stores": 0}
         self.items = []
         self.by_key = {}
         self.tiles = 0
@@ -339,9 +339,11 @@ class DeferredWgrad:
             return int(0.25 * torch.cuda.mem_get_info(dev)[0])
         return 64 * 2 ** 30
 
-    def push(self, weight, mg, g2, t2, bias=None):
+    def push(self, weight, mg, g2, t2, bias=None, fresh=False):
         """Queue mg += g2^T t2; ``bias`` (a bias Parameter with an fp32 main_grad, or None): its
-        gradient, the column sums of g2, comes out of the same grouped launch."""
+        gradient, the column sums of g2, comes out of the same grouped launch. ``fresh``: mg holds
+        no data yet (a lazily zeroed ZeRO-2 gradient buffer) — the first GEMM into it stores
+        instead of adding."""
         if self.hold_bytes_cap is None:
             self.hold_bytes_cap = self._hold_cap(g2.device)
         key = mg.data_ptr()
@@ -358,8 +360,8 @@ class DeferredWgrad:
             if it is not None:          # same main_grad twice outside a window: keep order
                 self.flush()
             # [weight, main_grad, segments, held (created inside a window), has its segment of
-            # the synchronising pass, bias parameter or None]
-            it = [weight, mg, [seg], self.hold, not self.hold, bias]
+            # the synchronising pass, bias parameter or None, main_grad unwritten (store)]
+            it = [weight, mg, [seg], self.hold, not self.hold, bias, bool(fresh)]
             self.items.append(it)
             self.by_key[key] = it
             self.tiles += -(-g2.shape[1] // 256) * -(-t2.shape[1] // 256)
@@ -401,36 +403,43 @@ class DeferredWgrad:
         self.held_bytes = sum(sg[0].numel() * sg[0].element_size() + sg[1].numel() * sg[1].element_size()
                               for it in keep for sg in it[2])
         work = []
-        for weight, mg, segs, _held, complete, bias in items:
+        for weight, mg, segs, _held, complete, bias, fresh in items:
             for g2, t2, vg, vt in segs:
                 if g2._version != vg or t2._version != vt:
                     raise RuntimeError("deferred wgrad: a queued dY / X tensor was modified in place before the "
                                        "flush; disable with SMDT_DEFER_WGRAD=0 and report the op that did it")
             if len(segs) == 1:
-                work.append((weight, mg, [(segs[0][0], segs[0][1])], complete, bias))
+                work.append((weight, mg, [(segs[0][0], segs[0][1])], complete, bias, fresh))
             elif self.concat_segments:
                 work.append((weight, mg, [(torch.cat([sg[0] for sg in segs]), torch.cat([sg[1] for sg in segs]))],
-                             complete, bias))
+                             complete, bias, fresh))
             else:
-                work.append((weight, mg, [(sg[0], sg[1]) for sg in segs], complete, bias))
+                work.append((weight, mg, [(sg[0], sg[1]) for sg in segs], complete, bias, fresh))
         self.stats["flushes"] += 1
         self.stats["items"] += len(work)
         self.stats["max_segments"] = max(self.stats["max_segments"], max(len(w[2]) for w in work))
         # round i issues the i-th segment of every item: one grouped launch per round, so two
         # segments of one main_grad never run in the same launch (no write race, no atomics)
         for i in range(max(len(w[2]) for w in work)):
-            rnd = [(mg, sg[i], b) for _, mg, sg, _, b in work if len(sg) > i]
-            cuda = [(mg, g2, t2, b) for mg, (g2, t2), b in rnd if g2.is_cuda]
+            # round 0 of an unwritten main_grad stores (overwrite), later rounds add
+            rnd = [(mg, sg[i], b, fr and i == 0) for _, mg, sg, _, b, fr in work if len(sg) > i]
+            self.stats["stores"] += sum(1 for r in rnd if r[3])
+            cuda = [(mg, g2, t2, b, ow) for mg, (g2, t2), b, ow in rnd if g2.is_cuda]
             done = False
             if cuda:
-                bts = [b.main_grad if b is not None else _NO_BIAS.get(g2.device) for _, g2, _, b in cuda]
-                done = _ext.ext().wgrad_grouped([c[0] for c in cuda], [c[1] for c in cuda], [c[2] for c in cuda], bts)
-            for mg, (g2, t2), b in rnd:
+                bts = [b.main_grad if b is not None else _NO_BIAS.get(g2.device) for _, g2, _, b, _ in cuda]
+                done = _ext.ext().wgrad_grouped([c[0] for c in cuda], [c[1] for c in cuda], [c[2] for c in cuda], bts,
+                                                [c[4] for c in cuda])
+            for mg, (g2, t2), b, ow in rnd:
                 if not (g2.is_cuda and done):
-                    mg.add_(g2.t().matmul(t2).view_as(mg))
+                    prod = g2.t().matmul(t2).view_as(mg)
+                    if ow:
+                        mg.copy_(prod)
+                    else:
+                        mg.add_(prod)
                     if b is not None:
                         b.main_grad.add_(g2.float().sum(0))
-        for weight, _, _, complete, b in work:
+        for weight, _, _, complete, b, _ in work:
             if not complete:
                 continue
             for p in (weight, b):
@@ -511,12 +520,15 @@ def _wgrad(weight, g2, t2):
     (``DeferredWgrad``), or ONE GEMM now (the MFMA kernel or hipBLASLt with beta = 1) instead of a
     bf16 GEMM + a separate fp32 add pass. Returns the gradient to hand back to autograd (None
     when it goes to ``main_grad``)."""
-    mg = getattr(weight, "main_grad", None)
+    raw = getattr(weight, "_smdt_mg_raw", None)     # lazily zeroed ZeRO-2 buffer (distributed.py)
+    mg = raw() if raw is not None else getattr(weight, "main_grad", None)
     if mg is None:
         return g2.t().matmul(t2)
     if DEFERRED_WGRAD.eligible(mg, g2, t2):
-        DEFERRED_WGRAD.push(weight, mg, g2, t2)
+        DEFERRED_WGRAD.push(weight, mg, g2, t2, fresh=raw is not None and weight._smdt_mg_claim())
         return None
+    if raw is not None:
+        mg = weight.main_grad                          # zeroes the slice if it is still unwritten
     accumulate_wgrad(mg, g2, t2)
     cb = getattr(weight, "_smdt_grad_ready", None)
     if cb is not None:
@@ -534,10 +546,12 @@ def _wgrad_and_bias(weight, bias_p, g2, t2):
     """(dW, db) for autograd: dW = g2^T t2 and db = sum_rows g2, each None when it went straight
     into the parameter's fp32 main_grad (queued, or by a kernel now)."""
     if bias_p is not None and _WGRAD_BIAS and g2.is_cuda:
-        mg = getattr(weight, "main_grad", None)
+        raw = getattr(weight, "_smdt_mg_raw", None)
+        mg = raw() if raw is not None else getattr(weight, "main_grad", None)
         tgt = SF.grad_accumulate_target(bias_p)
         if mg is not None and tgt is not None and tgt.numel() == g2.shape[-1] and DEFERRED_WGRAD.eligible(mg, g2, t2):
-            DEFERRED_WGRAD.push(weight, mg, g2, t2, bias=bias_p)
+            DEFERRED_WGRAD.push(weight, mg, g2, t2, bias=bias_p,
+                                fresh=raw is not None and weight._smdt_mg_claim())
             return None, None
     dw = _wgrad(weight, g2, t2)
     return dw, (_bias_grad(bias_p, g2) if bias_p is not None else None)

@@ -105,7 +105,9 @@ def ddp_worker(rank, world, zero, steps=3, overlap_pg=False, defer=False):
     m = GPTModel(cfg)
     ddp = DistributedDataParallel(m, bucket_size=20000, use_distributed_optimizer=zero,
                                   overlap_param_gather=overlap_pg)
-    opt = MixedPrecisionAdam(ddp, lr=1e-2, weight_decay=0.1, clip_grad=1.0)
+    # eps 1e-6 (not 1e-8): a gradient within ~1e-9 of zero whose fp32 sum order differs between
+    # the reduced and single-process runs would flip its Adam step sign (lr-sized param delta)
+    opt = MixedPrecisionAdam(ddp, lr=1e-2, weight_decay=0.1, clip_grad=1.0, eps=1e-6)
     tokens, labels = _batch(b=4)
     shard = slice(rank * (4 // world), (rank + 1) * (4 // world))
     first_grads = None
@@ -141,7 +143,9 @@ def single_train(steps=3):
     cfg = TransformerConfig(**TINY)
     m = GPTModel(cfg)
     ddp = DistributedDataParallel(m, bucket_size=20000)
-    opt = MixedPrecisionAdam(ddp, lr=1e-2, weight_decay=0.1, clip_grad=1.0)
+    # eps 1e-6 (not 1e-8): a gradient within ~1e-9 of zero whose fp32 sum order differs between
+    # the reduced and single-process runs would flip its Adam step sign (lr-sized param delta)
+    opt = MixedPrecisionAdam(ddp, lr=1e-2, weight_decay=0.1, clip_grad=1.0, eps=1e-6)
     tokens, labels = _batch(b=4)
     first_grads = None
     for _ in range(steps):
@@ -194,6 +198,11 @@ def zero_sft_worker(rank, world, stage, ga, steps, offload=False, offload_param=
     ps.destroy_model_parallel()
     init_distributed("gloo")
     ps.initialize_model_parallel(1, 1)
+    from smdt_amd.parallel import tensor_parallel as _tpq
+    if os.environ.get("SMDT_TEST_CPU_DEFER") == "1":
+        # the weight gradients go through the deferred grouped-wgrad queue (CPU fallback): with
+        # ZeRO-2's lazily zeroed staging buffers the first gradient of a weight is STORED
+        _tpq.DEFERRED_WGRAD.allow_cpu = True
     torch.manual_seed(0)
     with zi.Init(enabled=zero_init) as ctx:
         m = HFCausalLM(SFT_LLAMA, params_dtype=torch.float32)
@@ -241,7 +250,7 @@ def zero_sft_worker(rank, world, stage, ga, steps, offload=False, offload_param=
     mem = {"total": total, "grad": eng.ddp.grad_memory_numel(),
            "param": (eng.partitioner.param_memory_numel() if eng.partitioner is not None else None),
            "param_numel_now": sum(p.numel() for p in m.parameters()), "init": init_stats,
-           "wt_cache_left": wt_left}
+           "wt_cache_left": wt_left, "wgrad_stats": dict(_tpq.DEFERRED_WGRAD.stats)}
     with eng.gathered_params():
         out = {n: p.detach().clone() for n, p in m.named_parameters()}
     return (out, mem) if with_mem else out

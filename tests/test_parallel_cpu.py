@@ -372,3 +372,27 @@ def test_rampup_batch_size_calculator():
     assert c.num_micro_batches == 32 // 4
     with pytest.raises(ValueError):
         MicroBatchCalculator(32, 2, 2, rampup=[6, 8, 96])  # not a multiple of mbs x dp
+
+
+def test_fused_norms_wait_for_their_parameter_gather():
+    """The layers call ``Norm.fused`` instead of the norm's forward(), so nn.Module never runs its
+    forward pre-hooks: the overlapped ZeRO parameter all-gather's wait (a pre-hook flagged
+    ``_smdt_gather_wait``) must still run there, or the norm reads weights whose all-gather is in
+    flight (the source of an intermittent ZeRO + overlap-param-gather mismatch on CPU)."""
+    from smdt_amd.models.transformer import ParallelTransformerLayer, TransformerConfig
+    cfg = TransformerConfig(num_layers=1, hidden_size=32, num_attention_heads=4, max_position_embeddings=16,
+                            padded_vocab_size=64, hidden_dropout=0.0, attention_dropout=0.0, use_flash_attn=False)
+    layer = ParallelTransformerLayer(cfg, 0)
+    calls = []
+
+    def wait(mod, inp):
+        calls.append(mod)
+    wait._smdt_gather_wait = True
+    other = []
+    layer.input_norm.register_forward_pre_hook(wait)
+    layer.post_attention_norm.register_forward_pre_hook(wait)
+    layer.post_attention_norm.register_forward_pre_hook(lambda m, i: other.append(m))   # unflagged: not run
+    x = torch.randn(8, 2, 32, dtype=layer.input_norm.weight.dtype)
+    layer(x, None, None)
+    assert calls == [layer.input_norm, layer.post_attention_norm]
+    assert other == []

@@ -140,6 +140,22 @@ def test_zero_world2_matches_world1(stage, ga, offload, offload_param):
             _adam_close(outs[r][k], v, steps=3, what=(r, k))
 
 
+@pytest.mark.parametrize("ga", [1, 2])
+def test_zero2_lazy_grad_buffers_match_world1(ga, monkeypatch):
+    """ZeRO-2 with dp 2 allocates each bucket's fp32 accumulation buffer uninitialised: the
+    deferred wgrad launch stores the first gradient of a weight (no zero fill, no read), other
+    writers zero their slice on first access, unwritten slices and alignment padding are zeroed
+    before the reduce-scatter. Training equals single-rank training (CPU path of the queue)."""
+    monkeypatch.setenv("SMDT_TEST_CPU_DEFER", "1")
+    ref = run_workers(W.zero_sft_worker, 1, 0, 2 * ga, 3, False)[0]
+    outs = run_workers(W.zero_sft_worker, 2, 2, ga, 3, False, False, True)
+    for r in range(2):
+        params, mem = outs[r]
+        assert mem["wgrad_stats"]["stores"] > 0, mem["wgrad_stats"]    # the store path ran
+        for k, v in ref.items():
+            _adam_close(params[k], v, steps=3, what=(r, k))
+
+
 @pytest.mark.slow
 def test_zero2_world8_matches_world1():
     """ZeRO-2 over 8 gloo ranks (gradient shards of 1/8, one micro-batch each) == one rank
