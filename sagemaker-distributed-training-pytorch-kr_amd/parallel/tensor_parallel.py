@@ -750,6 +750,18 @@ def _exchange(send, recv, nxt, prv, group):
             if h is not None:
                 _cs.collective("p2p", group, _nbytes(send), transport="relay", events=h.timing())
                 return [h]
+    if send.is_cuda and dist.get_backend(group) == "gloo":
+        # Gloo rehearsals with CUDA tensors (several ranks on one GPU, SMDT_BENCH_BACKEND=gloo):
+        # a rank that sends to and receives from the same peer at once never completes its
+        # receive (both ranks of a tp2 ring stalled in the first wait, profiles/r4_rehearse_tp2/);
+        # the exchange goes through host buffers, synchronously. RCCL runs never take this path.
+        s_cpu = send.detach().cpu()
+        r_cpu = torch.empty(recv.shape, dtype=recv.dtype)
+        for w in dist.batch_isend_irecv([dist.P2POp(dist.isend, s_cpu, nxt, group),
+                                         dist.P2POp(dist.irecv, r_cpu, prv, group)]):
+            w.wait()
+        recv.copy_(r_cpu)
+        return []
     works = dist.batch_isend_irecv([dist.P2POp(dist.isend, send, nxt, group),
                                     dist.P2POp(dist.irecv, recv, prv, group)])
     _cs.collective("p2p", group, _nbytes(send), work=works[0] if len(works) == 1 else None)
