@@ -589,8 +589,24 @@ def drop_cached_weight_t(params):
         _WT_CACHE.pop(id(p), None)
 
 
+def mm_rows(g, w):
+    """g @ w (NN), row-split like ``linear_rows`` (the dgrad form when no W^T is made)."""
+    M = g.numel() // g.shape[-1]
+    bl = _row_blocks(M) if g.is_cuda else None
+    if bl is None:
+        return g.matmul(w)
+    g2 = g.reshape(M, g.shape[-1])
+    out = g.new_empty(tuple(g.shape[:-1]) + (w.shape[1],))
+    o2 = out.view(M, w.shape[1])
+    for a, b in bl:
+        torch.mm(g2[a:b], w, out=o2[a:b])
+    return out
+
+
 def _dgrad_weight_t(weight):
-    """W^T [in, out] contiguous for the TN dgrad, or None to use dY @ W directly."""
+    """W^T [in, out] contiguous for the TN dgrad, or None to use dY @ W directly. (A per-shape
+    timed NN-vs-TN pick for few-token backward passes measured neutral on the SFT recipe,
+    profiles/r4_sft_dgrad_tn/: TN stays.)"""
     if (_DGRAD_TN and weight.is_cuda and weight.dim() == 2 and weight.is_contiguous()
             and weight.dtype in (torch.bfloat16, torch.float16)
             and weight.shape[0] % 8 == 0 and weight.shape[1] % 8 == 0
@@ -650,7 +666,7 @@ def linear_rows(x, w, bias=None):
 def dgrad(g, weight, wt=None):
     """dX = g @ weight (g [..., out], weight [out, in]); ``wt`` = weight^T from _dgrad_weight_t."""
     if wt is None:
-        return g.matmul(weight)
+        return mm_rows(g, weight)
     return linear_rows(g, wt)
 
 

@@ -293,3 +293,11 @@ def test_row_split_linear_matches_whole(M):
         torch.testing.assert_close(out.float(), ref, atol=0.06, rtol=0.02)
     x3 = x.view(M // 4 if M % 4 == 0 else 1, -1, 512) if M % 4 == 0 else x.view(1, M, 512)
     torch.testing.assert_close(tp.linear_rows(x3, w).reshape(M, 768), tp.linear_rows(x, w))
+
+
+def test_mm_rows_matches_matmul():
+    """The NN dgrad form (no W^T) row-splits like linear_rows and equals dY @ W."""
+    torch.manual_seed(0)
+    w = torch.randn(1024, 2048, device="cuda", dtype=torch.bfloat16) * 0.05
+    g = torch.randn(4300, 1024, device="cuda", dtype=torch.bfloat16)
+    torch.testing.assert_close(tp.mm_rows(g, w).float(), g.float() @ w.float(), atol=0.08, rtol=0.02)
