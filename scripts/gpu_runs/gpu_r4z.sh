@@ -27,6 +27,6 @@ SMDT_EMULATE_DP=8 step llama_dp8_lazy 420 python -u $SF/train.py $COMMON --max_s
 SMDT_LAZY_GRAD_ZERO=0 SMDT_EMULATE_DP=8 step llama_dp8_zeroed 420 python -u $SF/train.py $COMMON --max_steps 24 --output_dir /tmp/m3
 SMDT_EMULATE_DP=8 step llama_dp8_lazy2 420 python -u $SF/train.py $COMMON --max_steps 24 --output_dir /tmp/m4
 step bench 300 python bench.py --steps 20 --warmup 5
-bash scripts/gpu_r4y.sh > "$O/r4y.out" 2>&1 || echo "r4y rc=$?"
+bash scripts/gpu_runs/gpu_r4y.sh > "$O/r4y.out" 2>&1 || echo "r4y rc=$?"
 cp -r gpurun_out/r4y "$O/" 2>/dev/null
 echo DONE
