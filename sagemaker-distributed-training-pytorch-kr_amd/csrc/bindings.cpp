@@ -312,6 +312,25 @@ Tensor aug_median3(Tensor x) {
   return y;
 }
 
+// ------------------------------------------------------------------ row gather with zero fill
+// out[r] = map[r] >= 0 ? src[map[r]] : 0; src [Ns, ...] contiguous, map int64 [Nd] on the device
+Tensor gather_rows(Tensor src, Tensor map) {
+  need_contig(src, "src");
+  need_contig(map, "map");
+  TORCH_CHECK(map.scalar_type() == at::kLong && map.dim() == 1 && map.device() == src.device(),
+              "gather_rows: map must be a 1-D int64 tensor on src's device");
+  TORCH_CHECK(src.dim() >= 1, "gather_rows: src must have a row dimension");
+  const int64_t rb = src.numel() / std::max<int64_t>(src.size(0), 1) * src.element_size();
+  TORCH_CHECK(rb % 16 == 0, "gather_rows: row bytes must be a multiple of 16");
+  auto sizes = src.sizes().vec();
+  sizes[0] = map.size(0);
+  auto out = torch::empty(sizes, src.options());
+  check(smdt_gather_rows(src.data_ptr(), map.data_ptr<int64_t>(), out.data_ptr(), map.size(0), src.size(0), rb,
+                         cur_stream()),
+        "gather_rows");
+  return out;
+}
+
 // ------------------------------------------------------------------ 2-D transpose (16-bit)
 // out [C, R] = x [R, C]^T, contiguous (feeds the dgrad GEMMs in the TN layout).
 Tensor transpose2d(Tensor x) {
@@ -719,6 +738,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("cast_", &cast_);
   m.def("rope_", &rope_);
   m.def("transpose2d", &transpose2d);
+  m.def("gather_rows", &gather_rows);
   m.def("aug_depthwise", &aug_depthwise);
   m.def("aug_median3", &aug_median3);
   m.def("bias_grad", &bias_grad);

@@ -69,6 +69,9 @@ hipError_t smdt_rope(int dtype, void* x, int64_t ntok, int nh, int64_t tok_strid
 
 // transpose.hip
 hipError_t smdt_transpose16(const void* in, void* out, int64_t R, int64_t C, hipStream_t st);
+// dst[r] = map[r] >= 0 ? src[map[r]] : 0 (rows of row_bytes, a multiple of 16)
+hipError_t smdt_gather_rows(const void* src, const int64_t* map, void* dst, int64_t nrows, int64_t nsrc,
+                            int64_t row_bytes, hipStream_t st);
 
 // cross_entropy.hip
 hipError_t smdt_ce_stats(int dtype, const void* logits, const int64_t* target, int64_t rows,

@@ -51,9 +51,43 @@ __global__ __launch_bounds__(256) void transpose16_kernel(const uint16_t* __rest
   }
 }
 
+// Row gather with zero fill: dst[r, :] = map[r] >= 0 ? src[map[r], :] : 0, rows of `rb` bytes
+// (a multiple of 16). The padding-free SFT micro-batches move attention's inputs between the
+// packed [T, W] token rows and the padded [L * b, W] layout with it (models/transformer.py):
+// every destination row is written exactly once, so neither a zero fill of the whole padded
+// buffer nor a scatter (index_copy / index_add, ~0.6-0.9 TB/s) is needed. One wave per row
+// chunk of up to 1 KiB (64 lanes x 16 B), 8 waves per block.
+__global__ __launch_bounds__(512) void gather_rows_kernel(const uint8_t* __restrict__ src,
+                                                          const int64_t* __restrict__ map,
+                                                          uint8_t* __restrict__ dst, int64_t nrows,
+                                                          int64_t nsrc, int64_t rb) {
+  const int64_t chunks = (rb + 1023) / 1024;
+  const int64_t item = (int64_t)blockIdx.x * 8 + (threadIdx.x >> 6);
+  if (item >= nrows * chunks) return;
+  const int64_t r = item / chunks;
+  const int64_t off = (item - r * chunks) * 1024 + (int64_t)(threadIdx.x & 63) * 16;
+  if (off >= rb) return;
+  const int64_t s = map[r];
+  u16x8 v = {};
+  if (s >= 0 && s < nsrc) v = __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(src + s * rb + off));
+  *reinterpret_cast<u16x8*>(dst + r * rb + off) = v;
+}
+
 }  // namespace smdt
 
 using namespace smdt;
+
+extern "C" hipError_t smdt_gather_rows(const void* src, const int64_t* map, void* dst, int64_t nrows,
+                                       int64_t nsrc, int64_t row_bytes, hipStream_t st) {
+  if (nrows <= 0) return hipSuccess;
+  if (row_bytes <= 0 || row_bytes % 16 != 0) return hipErrorInvalidValue;
+  const int64_t items = nrows * ((row_bytes + 1023) / 1024);
+  const int64_t blocks = (items + 7) / 8;
+  if (blocks > 0x7FFFFFFF) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(gather_rows_kernel, dim3((unsigned)blocks), dim3(512), 0, st, (const uint8_t*)src, map,
+                     (uint8_t*)dst, nrows, nsrc, row_bytes);
+  return hipGetLastError();
+}
 
 extern "C" hipError_t smdt_transpose16(const void* in, void* out, int64_t R, int64_t C, hipStream_t st) {
   if (R <= 0 || C <= 0 || R % 8 != 0 || C % 8 != 0 || R > (1 << 30) || C > (1 << 30))

@@ -16,6 +16,7 @@ read once per sub-block. Layer 0 folds the embedding dropout into the same kerne
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field
 from typing import Optional
 
@@ -23,6 +24,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ..ops import _ext
 from ..ops import functional as SF
 from ..parallel import state as ps
 from ..parallel import tensor_parallel as tp
@@ -129,7 +131,7 @@ class Norm(nn.Module):
 # padded [L, b] layout (zeros in the pad rows), runs RoPE + the causal flash kernels there and
 # gathers the T context rows back. Real-token outputs and all gradients equal the padded
 # computation's (models/hf.py ``HFCausalLM.forward`` sets it up from the attention mask).
-_PACK = {"idx": None, "b": 0, "L": 0}
+_PACK = {"idx": None, "b": 0, "L": 0, "inv": None}
 
 
 class packed_sequences:
@@ -137,7 +139,7 @@ class packed_sequences:
     tokens of a right-padded [b, L] batch."""
 
     def __init__(self, idx, b: int, L: int):
-        self.state = {"idx": idx, "b": int(b), "L": int(L)}
+        self.state = {"idx": idx, "b": int(b), "L": int(L), "inv": None}
 
     def __enter__(self):
         self.prev = dict(_PACK)
@@ -149,16 +151,50 @@ class packed_sequences:
         return False
 
 
+_PACK_GATHER = os.environ.get("SMDT_PACK_GATHER", "1") == "1"     # A/B: 0 = torch index ops
+
+
+def _inv_map():
+    """[L * b] int64: the packed row of each padded position, -1 for pads (cached per context)."""
+    inv = _PACK.get("inv")
+    if inv is None:
+        idx, b, L = _PACK["idx"], _PACK["b"], _PACK["L"]
+        inv = torch.full((L * b,), -1, dtype=torch.int64, device=idx.device)
+        inv[idx] = torch.arange(idx.numel(), device=idx.device)
+        _PACK["inv"] = inv
+    return inv
+
+
+class _GatherRows(torch.autograd.Function):
+    """out[r] = x[fwd_map[r]] (0 where fwd_map[r] < 0); the gradient is the gather with
+    ``bwd_map``, the inverse row map (ops: gather_rows in transpose.hip — every output row
+    written once: no zero fill of the padded buffer, no index_copy / index_add scatter)."""
+
+    @staticmethod
+    def forward(ctx, x, fwd_map, bwd_map):
+        ctx.bwd_map = bwd_map
+        ctx.nin = x.shape[0]
+        return _ext.ext().gather_rows(x.contiguous(), fwd_map)
+
+    @staticmethod
+    def backward(ctx, g):
+        return _ext.ext().gather_rows(g.contiguous(), ctx.bwd_map), None, None
+
+
 def _unpack_rows(x):
     """[T, 1, W] -> [L, b, W] with zero pad rows (differentiable)."""
     idx, b, L = _PACK["idx"], _PACK["b"], _PACK["L"]
     W = x.shape[-1]
+    if _PACK_GATHER and _ext.use_kernels(x) and (W * x.element_size()) % 16 == 0:
+        return _GatherRows.apply(x.reshape(-1, W), _inv_map(), idx).view(L, b, W)
     return x.new_zeros(L * b, W).index_copy(0, idx, x.reshape(-1, W)).view(L, b, W)
 
 
 def _pack_rows(x):
     """[L, b, C] -> [T, 1, C] (the real-token rows)."""
     C = x.shape[-1]
+    if _PACK_GATHER and _ext.use_kernels(x) and (C * x.element_size()) % 16 == 0:
+        return _GatherRows.apply(x.reshape(-1, C), _PACK["idx"], _inv_map()).unsqueeze(1)
     return x.reshape(-1, C).index_select(0, _PACK["idx"]).unsqueeze(1)
 
 

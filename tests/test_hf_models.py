@@ -87,3 +87,30 @@ def test_flash_dropout_mask_twin_properties():
     assert abs((1 - m1.float().mean().item()) - 0.1) < 0.01
     # heads and batches draw independent masks
     assert not torch.equal(m1[0, 0], m1[0, 1]) and not torch.equal(m1[0, 0], m1[1, 0])
+
+
+@pytest.mark.gpu
+def test_packed_rows_gather_kernel_matches_index_ops():
+    """Padding-free micro-batches: attention's unpack ([T, 1, W] -> [L, b, W], zero pad rows) and
+    pack ([L, b, C] -> [T, 1, C]) run as one row-gather kernel each way (gather_rows) — values and
+    gradients equal torch's index_copy / index_select formulation."""
+    import torch
+    from smdt_amd.models import transformer as T
+    torch.manual_seed(0)
+    L, b = 37, 5
+    lens = torch.tensor([37, 20, 5, 33, 1])
+    pos = [s * b + bi for s in range(L) for bi in range(b) if s < lens[bi]]
+    idx = torch.tensor(pos, dtype=torch.int64, device="cuda")
+    W, C = 96, 64
+    x = torch.randn(idx.numel(), 1, W, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    with T.packed_sequences(idx, b, L):
+        u = T._unpack_rows(x)
+        y = T._pack_rows(u[..., :C].contiguous() * 2)
+    ref_u = x.new_zeros(L * b, W).index_copy(0, idx, x.detach().reshape(-1, W)).view(L, b, W)
+    assert torch.equal(u.detach(), ref_u)
+    torch.testing.assert_close(y.detach(), 2 * ref_u.reshape(-1, W)[idx][:, :C].unsqueeze(1))
+    g = torch.randn_like(y)
+    y.backward(g)
+    gx = torch.zeros(idx.numel(), W, device="cuda", dtype=torch.bfloat16)
+    gx[:, :C] = 2 * g.squeeze(1)
+    torch.testing.assert_close(x.grad.squeeze(1), gx)
