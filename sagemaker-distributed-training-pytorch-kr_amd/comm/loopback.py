@@ -9,7 +9,7 @@ every collective replaced by a local stand-in of the same memory traffic on the 
 * reduce-scatter: this rank's slice of the input is added to the output slot by slot (W - 1
   adds, the reduction a real rank does; AVG scales the slice, as RCCL's AVG does);
 * all-reduce / broadcast / barrier: nothing (the values stay this rank's own);
-* a ring exchange (``parallel/tensor_parallel._exchange``): ``recv.copy_(send)``.
+* a ring exchange (``parallel/tensor_parallel._exchange``): ``recv.copy_(send)``, in line.
 
 It is a real ``torch.distributed.ProcessGroup`` (registered in c10d's group table), so every
 ``dist.all_reduce(..., group=tp_group)`` / ``all_gather_into_tensor`` / ``reduce_scatter_tensor``

@@ -756,7 +756,11 @@ def _exchange(send, recv, nxt, prv, group):
     issue order, so a 2-rank ring with next == prev cannot deadlock). A 2-rank ring on an
     MI355X node goes over every xGMI link through the relay engine (comm/relay.py) when one was
     built for ``group`` and measured faster than RCCL's single-link p2p."""
-    if _lb.is_loopback(group):          # single-process TP emulation: the transfer as a local copy
+    if _lb.is_loopback(group):
+        # single-process TP emulation: the transfer as a local copy on the compute stream (issuing
+        # it on the loopback side stream, as the real exchange runs beside the chunk GEMM, measured
+        # SLOWER: 202.4 -> 219.7 ms per stage-1 rank, the per-exchange stream hand-offs cost more
+        # than the overlap gains; profiles/r4_loopback_ring_async_neg/)
         recv.copy_(send)
         return []
     if nxt == prv:
