@@ -209,6 +209,10 @@ class DistributedDataParallel(nn.Module):
         self._lazy_zero = (self.zero_stage >= 2 and not self._direct
                            and os.environ.get("SMDT_LAZY_GRAD_ZERO", "1") == "1")
         self._fresh: Dict[int, set] = {}               # bucket index -> ids of unwritten slices
+        # ids whose slice a queued wgrad GEMM will STORE into (claimed, not yet issued): another
+        # writer of such a slice (e.g. the tied embedding's lookup gradient next to the LM head's
+        # wgrad) first flushes the queue, so the store lands before its accumulation
+        self._claimed: set = set()
         self._gaps: Dict[int, list] = {}               # bucket index -> (lo, hi) padding ranges
         if self.zero_stage >= 2:
             off = 0
@@ -405,6 +409,10 @@ class DistributedDataParallel(nn.Module):
             if fr is not None and id(p) in fr:
                 fr.discard(id(p))
                 v.zero_()
+            elif id(p) in self._claimed:
+                from .tensor_parallel import flush_deferred_wgrad
+                flush_deferred_wgrad()
+                self._claimed.clear()          # everything queued has been issued
         return v
 
     def _mg_raw(self, p) -> torch.Tensor:
@@ -432,6 +440,7 @@ class DistributedDataParallel(nn.Module):
         if fr is None or id(p) not in fr:
             return False
         fr.discard(id(p))
+        self._claimed.add(id(p))
         return True
 
     def _new_staging(self, b: Bucket) -> torch.Tensor:
@@ -606,6 +615,7 @@ class DistributedDataParallel(nn.Module):
                 self._retire_rs(b)
             self._staging.clear()
             self._fresh.clear()
+            self._claimed.clear()
             self._store_fresh = set(range(len(self.buckets)))   # the next reduce-scatter writes
         else:
             self.grad_data.zero_()

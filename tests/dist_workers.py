@@ -204,8 +204,11 @@ def zero_sft_worker(rank, world, stage, ga, steps, offload=False, offload_param=
         # ZeRO-2's lazily zeroed staging buffers the first gradient of a weight is STORED
         _tpq.DEFERRED_WGRAD.allow_cpu = True
     torch.manual_seed(0)
+    cfg_hf = SFT_LLAMA
+    if os.environ.get("SMDT_TEST_TIED") == "1":     # tied LM head / word embedding (OPT, GPT-2 style)
+        cfg_hf = dict(SFT_LLAMA, tie_word_embeddings=True)
     with zi.Init(enabled=zero_init) as ctx:
-        m = HFCausalLM(SFT_LLAMA, params_dtype=torch.float32)
+        m = HFCausalLM(cfg_hf, params_dtype=torch.float32)
     init_stats = {"peak_bytes": ctx.peak_bytes, "shard_bytes": ctx.shard_bytes, "params": ctx.params,
                   "largest_param_bytes": ctx.largest_param_bytes,
                   "resident_bytes_after_build": sum(p.numel() * p.element_size() for p in m.parameters())}

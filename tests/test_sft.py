@@ -140,13 +140,17 @@ def test_zero_world2_matches_world1(stage, ga, offload, offload_param):
             _adam_close(outs[r][k], v, steps=3, what=(r, k))
 
 
-@pytest.mark.parametrize("ga", [1, 2])
-def test_zero2_lazy_grad_buffers_match_world1(ga, monkeypatch):
+@pytest.mark.parametrize("ga,tied", [(1, False), (2, False), (1, True), (2, True)])
+def test_zero2_lazy_grad_buffers_match_world1(ga, tied, monkeypatch):
     """ZeRO-2 with dp 2 allocates each bucket's fp32 accumulation buffer uninitialised: the
     deferred wgrad launch stores the first gradient of a weight (no zero fill, no read), other
     writers zero their slice on first access, unwritten slices and alignment padding are zeroed
-    before the reduce-scatter. Training equals single-rank training (CPU path of the queue)."""
+    before the reduce-scatter. Training equals single-rank training (CPU path of the queue). Tied:
+    the word embedding's lookup gradient and the LM head's queued wgrad STORE share one slice —
+    the lookup's write flushes the queue first."""
     monkeypatch.setenv("SMDT_TEST_CPU_DEFER", "1")
+    if tied:
+        monkeypatch.setenv("SMDT_TEST_TIED", "1")
     ref = run_workers(W.zero_sft_worker, 1, 0, 2 * ga, 3, False)[0]
     outs = run_workers(W.zero_sft_worker, 2, 2, ga, 3, False, False, True)
     for r in range(2):
