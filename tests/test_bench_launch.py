@@ -85,6 +85,7 @@ def test_bench_ranks_gloo(n, layout, want, tmp_path):
     if "tp2" in want:
         assert comm["tp"]["calls"] > 0 and comm["pp"]["calls"] > 0
         assert set(rec["phase_ms_by_pp_stage"]) == {"0", "1"}
+        assert rec["config"]["pp_schedule"] == "zbh2"       # the N = 8 default schedule
         assert rec["phase_ms"]["tp_exchange_wait"] >= 0 and rec["phase_ms"]["pp_p2p_wait_and_bubble"] > 0
 
 
