@@ -301,3 +301,42 @@ def test_mm_rows_matches_matmul():
     w = torch.randn(1024, 2048, device="cuda", dtype=torch.bfloat16) * 0.05
     g = torch.randn(4300, 1024, device="cuda", dtype=torch.bfloat16)
     torch.testing.assert_close(tp.mm_rows(g, w).float(), g.float() @ w.float(), atol=0.08, rtol=0.02)
+
+
+def test_wgrad_grouped_overwrite_ignores_stale_targets():
+    """Grouped wgrad with ``overwrite``: the targets hold garbage (NaN) — the launch STORES
+    dy^T x for overwrite problems (no read) and accumulates for the others; a problem whose tiles
+    fall into the launch's split tail (atomics) is zeroed first. Bias sums still accumulate."""
+    from smdt_amd.ops import _ext
+    C = _ext.ext()
+    torch.manual_seed(0)
+    M = 2048
+    shapes = [(768, 512), (1024, 256), (256, 1280)]   # 6 + 4 + 5 = 15 tiles: all in the split tail
+    mgs, dys, xs, refs, bias, bref, ow = [], [], [], [], [], [], []
+    for i, (n, k) in enumerate(shapes):
+        dy = torch.randn(M, n, device="cuda", dtype=torch.bfloat16)
+        x = torch.randn(M, k, device="cuda", dtype=torch.bfloat16)
+        prod = dy.float().t() @ x.float()
+        overwrite = i != 1
+        mg = torch.full((n, k), float("nan"), device="cuda") if overwrite else torch.randn(n, k, device="cuda")
+        refs.append(prod if overwrite else mg.clone() + prod)
+        b = torch.zeros(n, device="cuda")
+        bias.append(b)
+        bref.append(dy.float().sum(0))
+        mgs.append(mg)
+        dys.append(dy)
+        xs.append(x)
+        ow.append(overwrite)
+    assert C.wgrad_grouped(mgs, dys, xs, bias, ow)
+    for mg, ref in zip(mgs, refs):
+        assert torch.isfinite(mg).all()
+        torch.testing.assert_close(mg, ref, atol=0.05, rtol=1e-3)
+    for b, r in zip(bias, bref):
+        torch.testing.assert_close(b, r, atol=0.05, rtol=1e-3)
+    # a launch with whole rounds (256 tiles: no tail): the overwrite path proper
+    n, k = 4096, 4096                                 # 16 x 16 = 256 tiles
+    dy = torch.randn(M, n, device="cuda", dtype=torch.bfloat16)
+    x = torch.randn(M, k, device="cuda", dtype=torch.bfloat16)
+    mg = torch.full((n, k), float("nan"), device="cuda")
+    assert C.wgrad_grouped([mg], [dy], [x], [], [True])
+    torch.testing.assert_close(mg, dy.float().t() @ x.float(), atol=0.05, rtol=1e-3)
