@@ -122,8 +122,8 @@ def parse():
     return p.parse_args()
 
 
-TUNED_GEMMS = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "tunableop",
-                           "gfx950_gpt345m_results.csv")
+TUNED_GEMMS = os.environ.get("SMDT_TUNED_GEMMS") or os.path.join(
+    os.path.dirname(os.path.abspath(__file__)), "profiles", "tunableop", "gfx950_gpt345m_results.csv")
 # hipBLASLt algorithm indices of the fused fp32-accumulate wgrad GEMMs, tuned over every algorithm
 # hipBLASLt ships for the problem type (SMDT_WGRAD_TUNE=full) on MI355X; reused as-is so the
 # selection does not vary run to run.
