@@ -51,6 +51,47 @@ __global__ __launch_bounds__(256) void rope_kernel(T* __restrict__ x, int64_t nt
   }
 }
 
+// Token-per-block form: one block per token, so the token's position (and its cos / sin rows) is
+// block-uniform scalar work and the per-thread (head, group) index is 32-bit arithmetic. The
+// grid-stride form above spends five 64-bit divisions / modulos per 16 elements, which made it
+// VALU-bound at ~3.1 TB/s on the LLaMA-7B SFT shapes (64 q + k heads of 128,
+// profiles/r4_sft_gemm_split/sft_dp8_rank_step_breakdown.txt). Measured on the NB4 SFT emulated
+// DP8 rank: 20,614 / 20,617 vs 20,580 input tokens/s with the grid-stride form (same box,
+// profiles/r4_rope_tok/) — the RoPE share of that step is ~1.5 %, so the gain is within noise;
+// kept for its simpler index math.
+template <typename T>
+__global__ __launch_bounds__(256) void rope_tok_kernel(T* __restrict__ x, int nh, int64_t tok_stride,
+                                                       int64_t head_stride, int rot,
+                                                       const float* __restrict__ cos_t,
+                                                       const float* __restrict__ sin_t, int pos_div,
+                                                       int pos_mod, float sign) {
+  const int half = rot / 2;
+  const int groups = half / 8;
+  const int64_t t = blockIdx.x;
+  const int pos = (int)((t / pos_div) % pos_mod);
+  const float* ct = cos_t + (int64_t)pos * half;
+  const float* stb = sin_t + (int64_t)pos * half;
+  T* xt = x + t * tok_stride;
+  for (int i = threadIdx.x; i < nh * groups; i += 256) {
+    const int h = i / groups, gidx = i - h * groups;
+    T* base = xt + (int64_t)h * head_stride + gidx * 8;
+    float a[8], b[8], c[8], s[8];
+    load_vec<T, 8>(base, a);
+    load_vec<T, 8>(base + half, b);
+    load_vec<float, 8>(ct + gidx * 8, c);
+    load_vec<float, 8>(stb + gidx * 8, s);
+    float oa[8], ob[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float sn = sign * s[j];
+      oa[j] = a[j] * c[j] - b[j] * sn;
+      ob[j] = b[j] * c[j] + a[j] * sn;
+    }
+    store_vec<T, 8>(base, oa);
+    store_vec<T, 8>(base + half, ob);
+  }
+}
+
 }  // namespace smdt
 
 using namespace smdt;
@@ -60,8 +101,15 @@ extern "C" hipError_t smdt_rope(int dtype, void* x, int64_t ntok, int nh, int64_
                                 const float* sin_t, int pos_div, int pos_mod, int backward,
                                 hipStream_t st) {
   if (rot % 16 != 0) return hipErrorInvalidValue;
-  int grid = stream_grid(ntok * nh * (rot / 16), 256);
   float sign = backward ? -1.f : 1.f;
+  if (ntok <= 0x7FFFFFFF && (int64_t)nh * (rot / 16) >= 64) {   // one block per token
+    const dim3 g((unsigned)ntok);
+    if (dtype == 1) hipLaunchKernelGGL(rope_tok_kernel<bf16>, g, dim3(256), 0, st, (bf16*)x, nh, tok_stride, head_stride, rot, cos_t, sin_t, pos_div, pos_mod, sign);
+    else if (dtype == 2) hipLaunchKernelGGL(rope_tok_kernel<f16>, g, dim3(256), 0, st, (f16*)x, nh, tok_stride, head_stride, rot, cos_t, sin_t, pos_div, pos_mod, sign);
+    else hipLaunchKernelGGL(rope_tok_kernel<float>, g, dim3(256), 0, st, (float*)x, nh, tok_stride, head_stride, rot, cos_t, sin_t, pos_div, pos_mod, sign);
+    return hipGetLastError();
+  }
+  int grid = stream_grid(ntok * nh * (rot / 16), 256);
   if (dtype == 1) hipLaunchKernelGGL(rope_kernel<bf16>, dim3(grid), dim3(256), 0, st, (bf16*)x, ntok, nh, tok_stride, head_stride, rot, cos_t, sin_t, pos_div, pos_mod, sign);
   else if (dtype == 2) hipLaunchKernelGGL(rope_kernel<f16>, dim3(grid), dim3(256), 0, st, (f16*)x, ntok, nh, tok_stride, head_stride, rot, cos_t, sin_t, pos_div, pos_mod, sign);
   else hipLaunchKernelGGL(rope_kernel<float>, dim3(grid), dim3(256), 0, st, (float*)x, ntok, nh, tok_stride, head_stride, rot, cos_t, sin_t, pos_div, pos_mod, sign);

@@ -198,9 +198,12 @@ def test_sumsq_and_inf_detection():
     torch.testing.assert_close(sb, (xb.double() ** 2).sum().float().view(1), rtol=1e-3, atol=1e-2)
 
 
-def test_rope_inplace_and_inverse():
+@pytest.mark.parametrize("nh", [4, 16])
+def test_rope_inplace_and_inverse(nh):
+    """nh 4: the grid-stride kernel; nh 16 (>= 64 8-pair groups per token): the token-per-block
+    kernel; both also on a strided [tokens, heads, d] view of a wider fused-QKV row."""
     torch.manual_seed(8)
-    s, b, nh, d = 64, 3, 4, 128
+    s, b, d = 64, 3, 128
     x = torch.randn(s * b, nh, d, device=DEV, dtype=torch.bfloat16)
     cos, sin = SF.rope_tables(s, d, device=DEV)
     y = x.clone()
@@ -210,6 +213,13 @@ def test_rope_inplace_and_inverse():
     torch.testing.assert_close(y.float(), yr.float(), atol=2e-2, rtol=2e-2)
     _C().rope_(y, cos, sin, d, b, s, True)
     torch.testing.assert_close(y.float(), x.float(), atol=3e-2, rtol=3e-2)
+    wide = torch.randn(s * b, (nh + 2) * d, device=DEV, dtype=torch.bfloat16)   # [q | k | v]-like row
+    keep = wide.clone()
+    view = wide[:, : nh * d].view(s * b, nh, d)
+    _C().rope_(view, cos, sin, d, b, s, False)
+    ref = SF._rope_ref(keep[:, : nh * d].view(s * b, nh, d), cos, sin, d, pos)
+    torch.testing.assert_close(view.float(), ref.float(), atol=2e-2, rtol=2e-2)
+    assert torch.equal(wide[:, nh * d:], keep[:, nh * d:])                 # the rest of the row untouched
 
 
 @pytest.mark.parametrize("V", [50304, 1000])
