@@ -517,9 +517,6 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void fwd_kernel(const E* __re
 #ifndef SMDT_FA_DKDV_OCC
 #define SMDT_FA_DKDV_OCC 2
 #endif
-#ifndef SMDT_FA_DKDV_STRAIGHT
-#define SMDT_FA_DKDV_STRAIGHT 0
-#endif
 template <int D, bool CAUSAL, bool DROP, class E>
 __global__ __launch_bounds__(256, D == 64 ? SMDT_FA_DKDV_OCC : 1) void bwd_dkdv_kernel(
     const E* __restrict__ Q, const E* __restrict__ K, const E* __restrict__ V,
@@ -726,21 +723,6 @@ __global__ __launch_bounds__(256, D == 64 ? SMDT_FA_DKDV_OCC : 1) void bwd_dkdv_
         }
     };
     if (!CAUSAL || qb >= kw + 32) {
-#if SMDT_FA_DKDV_STRAIGHT
-      // Both 32-query halves fully visible (every item but the causal diagonal ones): one block
-      // of straight-line code whose two halves are independent, so the scheduler overlaps the
-      // softmax VALU of one half with the other half's MFMAs.
-      f32x16 s0, p0, s1, p1;
-      v8_t<E> pb0[2], db0[2], pb1[2], db1[2];
-      sd_init(0, s0, p0);
-      sd_init(1, s1, p1);
-      sd_mma(0, s0, p0);
-      sd_mma(1, s1, p1);
-      softmax_ds(0, s0, p0, pb0, db0);
-      acc_mma(0, pb0, db0);
-      softmax_ds(1, s1, p1, pb1, db1);
-      acc_mma(1, pb1, db1);
-#else
       // the two 32-query halves one after the other: 48 fewer live VGPRs than straight-line code
       // (which spilled at 256 VGPRs once the row constants entered as MFMA operands); the
       // partner wave on the SIMD supplies the overlap of softmax VALU and MFMAs
@@ -753,7 +735,6 @@ __global__ __launch_bounds__(256, D == 64 ? SMDT_FA_DKDV_OCC : 1) void bwd_dkdv_
         softmax_ds(qs2, sa, pa, pb, db);
         acc_mma(qs2, pb, db);
       }
-#endif
     } else {
 #pragma unroll
       for (int qs2 = 0; qs2 < 2; ++qs2) {
@@ -811,7 +792,7 @@ __global__ __launch_bounds__(256, D == 64 ? SMDT_FA_DKDV_OCC : 1) void bwd_dkdv_
 // ---------------------------------------------------------------------------------------
 // dQ. Workgroup = 4 waves = 128 query rows of one (b, h); K/V streamed in 64-key tiles,
 // double-buffered.
-template <int D, bool CAUSAL, bool DROP, class E, bool STRAIGHT = false>
+template <int D, bool CAUSAL, bool DROP, class E>
 __global__ __launch_bounds__(256, D == 64 ? SMDT_FA_DQ_OCC : 1) void bwd_dq_kernel(
     const E* __restrict__ Q, const E* __restrict__ K, const E* __restrict__ V,
     const E* __restrict__ dO, const E* __restrict__ O, const float* __restrict__ LSE,
@@ -982,26 +963,15 @@ __global__ __launch_bounds__(256, D == 64 ? SMDT_FA_DQ_OCC : 1) void bwd_dq_kern
         for (int dt = 0; dt < G::DT; ++dt) dq[dt] = mfma(fr.trf(kt, 32 * tt, s, dt), db, dq[dt]);
       }
     };
-    if (STRAIGHT && (!CAUSAL || kb + 63 <= qw)) {
-      // both sub-tiles visible and off the diagonal: one straight-line block, so the scheduler
-      // can run sub-tile 1's S / dP MFMA chains beside sub-tile 0's softmax VALU
-      f32x16 st0, dp0, st1, dp1;
-      sd(0, st0, dp0);
-      sd(1, st1, dp1);
-      soft(0, st0, dp0, false);
-      acc(0, dp0);
-      soft(1, st1, dp1, false);
-      acc(1, dp1);
-    } else {
+    // (a straight-line pair of the two sub-tiles measured neutral, profiles/r4_attn_dq_straight_neutral/)
 #pragma unroll
-      for (int tt = 0; tt < 2; ++tt) {
-        const int ksub = kb + 32 * tt;
-        if (CAUSAL && ksub > qw + 31) continue;
-        f32x16 st, dpt;
-        sd(tt, st, dpt);
-        soft(tt, st, dpt, CAUSAL && ksub + 31 > qw);
-        acc(tt, dpt);
-      }
+    for (int tt = 0; tt < 2; ++tt) {
+      const int ksub = kb + 32 * tt;
+      if (CAUSAL && ksub > qw + 31) continue;
+      f32x16 st, dpt;
+      sd(tt, st, dpt);
+      soft(tt, st, dpt, CAUSAL && ksub + 31 > qw);
+      acc(tt, dpt);
     }
     wait_vm<(kBuf - 2) * kPer>();  // tile t + 1 landed (t + 2 may still be in flight)
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1100,15 +1070,6 @@ extern "C" hipError_t smdt_flash_fwd(int dtype, const void* q, const void* k, co
   return hipGetLastError();
 }
 
-// SMDT_FA_DQ_STRAIGHT=1: the dQ kernel's straight-line sub-tile pair (A/B knob, read once).
-static bool dq_straight() {
-  static const bool on = [] {
-    const char* v = getenv("SMDT_FA_DQ_STRAIGHT");
-    return v != nullptr && v[0] == '1';
-  }();
-  return on;
-}
-
 extern "C" hipError_t smdt_flash_bwd(int dtype, const void* q, const void* k, const void* v,
                                      const void* o, const void* dout, const float* lse,
                                      float* delta, void* dq, void* dk, void* dv, int B, int H,
@@ -1134,16 +1095,10 @@ extern "C" hipError_t smdt_flash_bwd(int dtype, const void* q, const void* k, co
   dim3 gq((unsigned)((int64_t)B * H * (S / kBlockRows)));
 #define SMDT_FA_BWD_T(DD, CC, DR, ET)                                                            \
   do {                                                                                           \
-    if (dq_straight())                                                                           \
-      hipLaunchKernelGGL((bwd_dq_kernel<DD, CC, DR, ET, true>), gq, dim3(256), 0, st, (const ET*)q, \
-                         (const ET*)k, (const ET*)v, (const ET*)dout, (const ET*)o, lse, delta,   \
-                         (ET*)lse3, (ET*)dl3, (ET*)dq, B, H, Hkv, S, qs, ks, vs, dos, os, dqs,    \
-                         scale, dscale, lsub, dr);                                                \
-    else                                                                                         \
-      hipLaunchKernelGGL((bwd_dq_kernel<DD, CC, DR, ET, false>), gq, dim3(256), 0, st, (const ET*)q, \
-                         (const ET*)k, (const ET*)v, (const ET*)dout, (const ET*)o, lse, delta,   \
-                         (ET*)lse3, (ET*)dl3, (ET*)dq, B, H, Hkv, S, qs, ks, vs, dos, os, dqs,    \
-                         scale, dscale, lsub, dr);                                                \
+    hipLaunchKernelGGL((bwd_dq_kernel<DD, CC, DR, ET>), gq, dim3(256), 0, st, (const ET*)q,      \
+                       (const ET*)k, (const ET*)v, (const ET*)dout, (const ET*)o, lse, delta,     \
+                       (ET*)lse3, (ET*)dl3, (ET*)dq, B, H, Hkv, S, qs, ks, vs, dos, os, dqs,      \
+                       scale, dscale, lsub, dr);                                                  \
     hipLaunchKernelGGL((bwd_dkdv_kernel<DD, CC, DR, ET>), gkv, dim3(256), 0, st, (const ET*)q,  \
                        (const ET*)k, (const ET*)v, (const ET*)dout, (const ET*)lse3,              \
                        (const ET*)dl3, delta, (ET*)dk, (ET*)dv, B, H, Hkv, S, qs, ks, vs, dos,    \
