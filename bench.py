@@ -30,7 +30,8 @@ from CUDA events on the compute stream into forward/backward compute, TP-exchang
 p2p wait + bubble, ZeRO parameter-gather wait, DP gradient sync, optimizer and the device idle gap
 between steps (comm/stats.py; the pieces sum to the step) — and ``comm``: per axis (tp / pp / dp /
 embd / mp) and op the calls, MB, ms and bus GB/s per step, keyed by the transport that carried them
-(rccl / xgmi / relay). No host-device synchronisation is added to the timed loop.
+(rccl / xgmi / relay). They are recorded on two extra steps after the timed ones; nothing is
+added to the timed loop.
 
 Scaling is WEAK: every GPU processes ``--seqs-per-gpu`` (64) sequences of 1024 tokens per step
 at every N, so global batch = 64 N. A DP replica (tp x pp GPUs) therefore runs 64 tp pp sequences
@@ -349,8 +350,11 @@ def main():
         torch.cuda.synchronize()
     t0 = time.perf_counter()
     last = None
+    # on GPUs the stats are recorded on two extra steps after the timed ones (below); the host-clock
+    # stats of a CPU (Gloo) run cost nothing measurable and are recorded on the timed steps
+    cpu_stats = bool(a.comm_stats) and not torch.cuda.is_available()
     for _ in range(a.steps):
-        last = train_step(stats=bool(a.comm_stats))
+        last = train_step(stats=cpu_stats)
     if torch.cuda.is_available():
         torch.cuda.synchronize()
     if dist.is_initialized():
@@ -360,6 +364,13 @@ def main():
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     elapsed = float(el.item())
     ms_step = 1000 * elapsed / a.steps
+    # phase_ms / comm come from two extra steps after the timed ones: the per-collective events
+    # and phase marks cost ~3 % of a step at the N = 8 rank's ~4 k launches per step (207.6 vs
+    # 201.8 ms, profiles/r4_comm_stats_cost/), so the timed steps run without them
+    if a.comm_stats and not cpu_stats:
+        for _ in range(2):
+            train_step(stats=True)
+        torch.cuda.synchronize()
     explain = comm_stats.summary(ms_step) if a.comm_stats else None
     phases_all = None
     if explain is not None and dist.is_initialized() and world > 1:

@@ -57,7 +57,8 @@ def _check_phases(rec):
     parts = [v for k, v in ph.items() if k not in ("sum", "ms_per_step")]
     assert all(v >= 0 for v in parts), ph
     assert abs(sum(parts) - ph["sum"]) < 0.01 * max(1.0, ph["sum"])
-    # the phases (CUDA events on GPU, host clocks on CPU) account for the whole measured step
+    # the phases (CUDA events on GPU — recorded on two extra steps after the timed ones —, host
+    # clocks on the timed steps of a CPU run) account for the whole measured step
     assert abs(ph["sum"] - rec["ms_per_step"]) <= 0.10 * rec["ms_per_step"], (ph, rec["ms_per_step"])
 
 
