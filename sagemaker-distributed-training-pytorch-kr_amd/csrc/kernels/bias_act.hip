@@ -8,7 +8,6 @@
 // 16-byte chunk per thread) and a slice of rows (grid.y); a thread keeps the same columns for
 // every row of its slice, so d(bias) partial sums accumulate in registers and are written once
 // per block as an fp32 [grid.y, N] slab, reduced by `col_partials_reduce_kernel`.
-#include <cstdlib>
 
 #include "activations.h"
 #include "common.h"
@@ -190,28 +189,25 @@ __global__ __launch_bounds__(256) void col_sum_rows_kernel(const T* __restrict__
   for (int j = 0; j < 8; ++j) o[j] = acc[j];
 }
 
-// Rows per slice so that (column blocks) x (row slices) ~ 1024 blocks (x mul). Launches that
-// write d(bias) partials keep ~1024 blocks (the [slices, N] fp32 slab is re-read by the reduce);
-// the partial-free ones (forward, backward when the grouped wgrad makes d(bias)) run 4x the
-// blocks with 8 rows of loads in flight per thread: +2.5 % HBM rate on [65536, 4096] bf16
-// (fwd 5.08 -> 5.20 TB/s, bwd 5.46 -> 5.59, profiles/r4_elementwise_ab). A/B knobs, read once:
-// SMDT_BA_SLICE_MUL (default 4), SMDT_BA_KROWS (8 or 4, default 8).
-static int env_int(const char* name, int dflt) {
-  const char* v = getenv(name);
-  return v ? atoi(v) : dflt;
-}
-static int ba_slice_mul() {
-  static const int m = env_int("SMDT_BA_SLICE_MUL", 4);
-  return m < 1 ? 1 : m;
-}
-static bool ba_krows8() {
-  static const bool on = env_int("SMDT_BA_KROWS", 8) == 8;
-  return on;
+// Launch shapes. Launches that write d(bias) partials keep ~1024 blocks (the [slices, N] fp32
+// slab is re-read by the reduce). The partial-free ones (forward, and backward when the grouped
+// wgrad makes d(bias)) give every thread exactly one batch of kPF rows (all loads in flight at
+// once, no loop): on [65536, 4096] bf16 fwd 5.18 -> 6.16 TB/s, bwd 5.57 -> 6.2 TB/s vs the round-4
+// interim form (4x the blocks, 8-row batches), which had itself beaten the ~1024-block form by
+// 2.5 % (profiles/r4_elementwise_ab/, profiles/r4_elementwise_ab/sweep2.log).
+constexpr int kPF = 4;
+
+static int pf_slices(int64_t rows, int* rows_per_slice) {
+  // kPF rows per slice; more only past grid.y's 65535 slices (the kernel loops over its rows)
+  int64_t rps = (rows + 65534) / 65535;
+  if (rps < kPF) rps = kPF;
+  *rows_per_slice = (int)rps;
+  return (int)((rows + rps - 1) / rps);
 }
 
-static int act_slices(int64_t rows, int N, int* rows_per_slice, int mul = 1) {
+static int act_slices(int64_t rows, int N, int* rows_per_slice) {
   int colblocks = (N / 8 + 255) / 256;
-  int64_t want = (int64_t)1024 * mul / colblocks;
+  int64_t want = (int64_t)1024 / colblocks;
   if (want < 1) want = 1;
   if (want > rows) want = rows;
   int64_t rps = (rows + want - 1) / want;
@@ -232,17 +228,11 @@ extern "C" hipError_t smdt_bias_act_fwd(int dtype, int act, const void* x, const
                                         void* y, int64_t rows, int N, hipStream_t st) {
   if (N % 8 != 0 || rows <= 0) return hipErrorInvalidValue;
   int rps;
-  int slices = act_slices(rows, N, &rps, ba_slice_mul());
+  int slices = pf_slices(rows, &rps);
   dim3 grid((N / 8 + 255) / 256, slices);
 #define SMDT_BA_FWD(T, A)                                                                   \
-  do {                                                                                      \
-    if (ba_krows8())                                                                        \
-      hipLaunchKernelGGL((bias_act_fwd_kernel<T, A, 8>), grid, dim3(256), 0, st, (const T*)x, \
-                         (const T*)bias, (T*)y, rows, N, rps);                              \
-    else                                                                                    \
-      hipLaunchKernelGGL((bias_act_fwd_kernel<T, A, 4>), grid, dim3(256), 0, st, (const T*)x, \
-                         (const T*)bias, (T*)y, rows, N, rps);                              \
-  } while (0)
+  hipLaunchKernelGGL((bias_act_fwd_kernel<T, A, kPF>), grid, dim3(256), 0, st, (const T*)x,  \
+                     (const T*)bias, (T*)y, rows, N, rps)
   if (dtype == 1) { if (act == 0) SMDT_BA_FWD(bf16, 0); else SMDT_BA_FWD(bf16, 1); }
   else if (dtype == 2) { if (act == 0) SMDT_BA_FWD(f16, 0); else SMDT_BA_FWD(f16, 1); }
   else { if (act == 0) SMDT_BA_FWD(float, 0); else SMDT_BA_FWD(float, 1); }
@@ -256,19 +246,13 @@ extern "C" hipError_t smdt_bias_act_bwd(int dtype, int act, const void* dy, cons
                                         hipStream_t st) {
   if (N % 8 != 0 || rows <= 0) return hipErrorInvalidValue;
   int rps;
-  // with d(bias): the partials slab was sized by smdt_bias_act_slices (mul 1)
-  int slices = act_slices(rows, N, &rps, dbias ? 1 : ba_slice_mul());
+  // with d(bias): the partials slab was sized by smdt_bias_act_slices (~1024 blocks)
+  int slices = dbias ? act_slices(rows, N, &rps) : pf_slices(rows, &rps);
   dim3 grid((N / 8 + 255) / 256, slices);
   float* part = dbias ? partials : nullptr;
 #define SMDT_BA_BWD(T, A)                                                                   \
-  do {                                                                                      \
-    if (ba_krows8())                                                                        \
-      hipLaunchKernelGGL((bias_act_bwd_kernel<T, A, 8>), grid, dim3(256), 0, st, (const T*)dy, \
-                         (const T*)x, (const T*)bias, (T*)dx, part, rows, N, rps);          \
-    else                                                                                    \
-      hipLaunchKernelGGL((bias_act_bwd_kernel<T, A, 4>), grid, dim3(256), 0, st, (const T*)dy, \
-                         (const T*)x, (const T*)bias, (T*)dx, part, rows, N, rps);          \
-  } while (0)
+  hipLaunchKernelGGL((bias_act_bwd_kernel<T, A, 4>), grid, dim3(256), 0, st, (const T*)dy,   \
+                     (const T*)x, (const T*)bias, (T*)dx, part, rows, N, rps)
   if (dtype == 1) { if (act == 0) SMDT_BA_BWD(bf16, 0); else SMDT_BA_BWD(bf16, 1); }
   else if (dtype == 2) { if (act == 0) SMDT_BA_BWD(f16, 0); else SMDT_BA_BWD(f16, 1); }
   else { if (act == 0) SMDT_BA_BWD(float, 0); else SMDT_BA_BWD(float, 1); }

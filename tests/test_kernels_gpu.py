@@ -115,6 +115,24 @@ def test_bias_gelu(approx):
     torch.testing.assert_close(b.grad.float(), br.grad, atol=1.0, rtol=2e-2)
 
 
+@pytest.mark.parametrize("rows,N", [(1001, 4096), (300_001, 64), (4, 2048)])
+def test_bias_gelu_partial_free_launch_shapes(rows, N):
+    """The partial-free launches (forward, and backward without d(bias)) give each thread one
+    4-row batch; row counts not a multiple of 4 and past grid.y's 65535 slices (the slice then
+    loops over more rows) still cover every row exactly once."""
+    torch.manual_seed(5)
+    x = torch.randn(rows, N, device=DEV, dtype=torch.bfloat16)
+    b = torch.randn(N, device=DEV, dtype=torch.bfloat16)
+    dy = torch.randn_like(x)
+    z = x.float() + b.float()
+    y = _C().bias_act_fwd(x, b, 0)
+    torch.testing.assert_close(y.float(), F.gelu(z, approximate="tanh"), atol=2e-2, rtol=2e-2)
+    dx, _ = _C().bias_act_bwd(dy, x, b, 0, False, None)
+    zr = z.clone().requires_grad_()
+    F.gelu(zr, approximate="tanh").backward(dy.float())
+    torch.testing.assert_close(dx.float(), zr.grad, atol=3e-2, rtol=3e-2)
+
+
 def test_swiglu():
     torch.manual_seed(4)
     x = torch.randn(777, 2 * 1024, device=DEV, dtype=torch.bfloat16, requires_grad=True)
