@@ -32,70 +32,6 @@ struct AdamArgs {
   const int* found_inf;   // device flag; when nonzero the step is skipped; may be null
 };
 
-template <typename TO>
-__global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
-  if (a.found_inf && *a.found_inf) return;
-  const float gm = a.grad_mul ? *a.grad_mul : 1.f;
-  const int64_t nvec = a.n / 4;
-  const float step_size = a.lr / a.bc1;
-  const float rbc2 = rsqrtf(a.bc2);
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nvec;
-       i += (int64_t)gridDim.x * 256) {
-    // every state word is touched once per step: nontemporal loads
-    f32x4 p = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(a.master) + i);
-    f32x4 g = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(a.grad) + i);
-    f32x4 m = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(a.exp_avg) + i);
-    f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(a.exp_avg_sq) + i);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      float gj = g[j] * gm;
-      if (!a.adamw) gj += a.weight_decay * p[j];
-      m[j] = a.beta1 * m[j] + (1.f - a.beta1) * gj;
-      v[j] = a.beta2 * v[j] + (1.f - a.beta2) * gj * gj;
-      float denom = sqrtf(v[j]) * rbc2 + a.eps;
-      float upd = m[j] / denom;
-      if (a.adamw) p[j] -= a.lr * a.weight_decay * p[j];
-      p[j] -= step_size * upd;
-    }
-    // ... and written once: nontemporal stores (the 10.7 GB per-step state stream of GPT-2 345M
-    // does not fit any cache level, so there is nothing to keep resident)
-    __builtin_nontemporal_store(p, reinterpret_cast<f32x4*>(a.master) + i);
-    __builtin_nontemporal_store(m, reinterpret_cast<f32x4*>(a.exp_avg) + i);
-    __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(a.exp_avg_sq) + i);
-    if constexpr (!std::is_same<TO, float>::value) {
-      if (a.model_out) {
-        TO* o = reinterpret_cast<TO*>(a.model_out) + i * 4;
-        using v4 = __attribute__((ext_vector_type(4))) unsigned short;
-        v4 w;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          TO t = (TO)p[j];
-          unsigned short bits;
-          __builtin_memcpy(&bits, &t, 2);
-          w[j] = bits;
-        }
-        __builtin_nontemporal_store(w, reinterpret_cast<v4*>(o));
-      }
-    }
-  }
-  // Scalar tail (n not a multiple of 4).
-  if (blockIdx.x == 0 && threadIdx.x < (a.n & 3)) {
-    int64_t k = nvec * 4 + threadIdx.x;
-    float p = a.master[k], gj = a.grad[k] * gm, m = a.exp_avg[k], v = a.exp_avg_sq[k];
-    if (!a.adamw) gj += a.weight_decay * p;
-    m = a.beta1 * m + (1.f - a.beta1) * gj;
-    v = a.beta2 * v + (1.f - a.beta2) * gj * gj;
-    float denom = sqrtf(v) * rbc2 + a.eps;
-    if (a.adamw) p -= a.lr * a.weight_decay * p;
-    p -= step_size * (m / denom);
-    a.master[k] = p;
-    a.exp_avg[k] = m;
-    a.exp_avg_sq[k] = v;
-    if constexpr (!std::is_same<TO, float>::value) {
-      if (a.model_out) reinterpret_cast<TO*>(a.model_out)[k] = (TO)p;
-    }
-  }
-}
 
 // Stage 1 of the global L2 norm: per-block sum of squares (fp32 or 16-bit input) and an
 // inf/nan flag. Stage 2 (`l2norm_finalize_kernel`) sums the block partials in a fixed order.
@@ -200,6 +136,83 @@ __global__ __launch_bounds__(256) void cast_kernel(const TI* __restrict__ x, TO*
   }
 }
 
+// Fused Adam / AdamW, one batch per thread: thread t of block b updates the U float4 vectors
+// b*256*U + u*256 + t (u < U; coalesced per u) of every state stream, all loads in flight at
+// once, no grid-stride loop; the grid covers the whole buffer. On the GPT-2 345M buffer (355 M
+// params: fp32 master / grad / m / v + bf16 copy) U = 1 runs at 5.7 TB/s (1.87 ms) against
+// 4.5 TB/s (2.37 ms) for the former grid-stride form capped at 2048 blocks; U = 2 / 4: 5.5-5.6
+// (benchmarks/bench_adam.py, profiles/r4_adam_batch/).
+template <typename TO, int U>
+__global__ __launch_bounds__(256) void adam_batch_kernel(AdamArgs a) {
+  if (a.found_inf && *a.found_inf) return;
+  const float gm = a.grad_mul ? *a.grad_mul : 1.f;
+  const int64_t nvec = a.n / 4;
+  const float step_size = a.lr / a.bc1;
+  const float rbc2 = rsqrtf(a.bc2);
+  const int64_t base = (int64_t)blockIdx.x * 256 * U + threadIdx.x;
+  f32x4 p[U], g[U], m[U], v[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t i = base + u * 256;
+    if (i < nvec) {
+      p[u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(a.master) + i);
+      g[u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(a.grad) + i);
+      m[u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(a.exp_avg) + i);
+      v[u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(a.exp_avg_sq) + i);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t i = base + u * 256;
+    if (i >= nvec) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float gj = g[u][j] * gm;
+      if (!a.adamw) gj += a.weight_decay * p[u][j];
+      m[u][j] = a.beta1 * m[u][j] + (1.f - a.beta1) * gj;
+      v[u][j] = a.beta2 * v[u][j] + (1.f - a.beta2) * gj * gj;
+      float denom = sqrtf(v[u][j]) * rbc2 + a.eps;
+      float upd = m[u][j] / denom;
+      if (a.adamw) p[u][j] -= a.lr * a.weight_decay * p[u][j];
+      p[u][j] -= step_size * upd;
+    }
+    __builtin_nontemporal_store(p[u], reinterpret_cast<f32x4*>(a.master) + i);
+    __builtin_nontemporal_store(m[u], reinterpret_cast<f32x4*>(a.exp_avg) + i);
+    __builtin_nontemporal_store(v[u], reinterpret_cast<f32x4*>(a.exp_avg_sq) + i);
+    if constexpr (!std::is_same<TO, float>::value) {
+      if (a.model_out) {
+        TO* o = reinterpret_cast<TO*>(a.model_out) + i * 4;
+        using v4 = __attribute__((ext_vector_type(4))) unsigned short;
+        v4 w;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          TO t = (TO)p[u][j];
+          unsigned short bits;
+          __builtin_memcpy(&bits, &t, 2);
+          w[j] = bits;
+        }
+        __builtin_nontemporal_store(w, reinterpret_cast<v4*>(o));
+      }
+    }
+  }
+  if (blockIdx.x == 0 && threadIdx.x < (a.n & 3)) {   // scalar tail (n not a multiple of 4)
+    int64_t k = nvec * 4 + threadIdx.x;
+    float pp = a.master[k], gj = a.grad[k] * gm, mm = a.exp_avg[k], vv = a.exp_avg_sq[k];
+    if (!a.adamw) gj += a.weight_decay * pp;
+    mm = a.beta1 * mm + (1.f - a.beta1) * gj;
+    vv = a.beta2 * vv + (1.f - a.beta2) * gj * gj;
+    float denom = sqrtf(vv) * rbc2 + a.eps;
+    if (a.adamw) pp -= a.lr * a.weight_decay * pp;
+    pp -= step_size * (mm / denom);
+    a.master[k] = pp;
+    a.exp_avg[k] = mm;
+    a.exp_avg_sq[k] = vv;
+    if constexpr (!std::is_same<TO, float>::value) {
+      if (a.model_out) reinterpret_cast<TO*>(a.model_out)[k] = (TO)pp;
+    }
+  }
+}
+
 }  // namespace smdt
 
 using namespace smdt;
@@ -211,10 +224,12 @@ extern "C" hipError_t smdt_adam(float* master, const float* grad, float* m, floa
                                 const int* found_inf, hipStream_t st) {
   AdamArgs a{master, grad, m, v, model_out, model_dtype, n, lr, beta1, beta2, eps, wd, bc1, bc2,
              adamw, grad_mul, found_inf};
-  int grid = stream_grid(n / 4 + 1, 256);
-  if (model_dtype == 1) hipLaunchKernelGGL(adam_kernel<bf16>, dim3(grid), dim3(256), 0, st, a);
-  else if (model_dtype == 2) hipLaunchKernelGGL(adam_kernel<f16>, dim3(grid), dim3(256), 0, st, a);
-  else hipLaunchKernelGGL(adam_kernel<float>, dim3(grid), dim3(256), 0, st, a);
+  const int64_t blocks = (n / 4 + 255) / 256;
+  if (blocks > 0x7FFFFFFF) return hipErrorInvalidValue;
+  const dim3 gb((unsigned)(blocks > 0 ? blocks : 1));
+  if (model_dtype == 1) hipLaunchKernelGGL((adam_batch_kernel<bf16, 1>), gb, dim3(256), 0, st, a);
+  else if (model_dtype == 2) hipLaunchKernelGGL((adam_batch_kernel<f16, 1>), gb, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((adam_batch_kernel<float, 1>), gb, dim3(256), 0, st, a);
   return hipGetLastError();
 }
 
