@@ -68,6 +68,14 @@ def main():
         res["ln_bwd_incl_autograd"] = {"ms": round(ms, 4)}
     except Exception as e:  # noqa: BLE001
         res["ln_error"] = repr(e)[:200]
+    # SwiGLU at the LLaMA-7B SFT shape (packed window ~4.3 k tokens, ffn 11008)
+    xs = torch.randn(4300, 2 * 11008, device=dev, dtype=torch.bfloat16)
+    ds = torch.randn(4300, 11008, device=dev, dtype=torch.bfloat16)
+    ns = ds.numel() * 2
+    ms = timeit(lambda: C.swiglu_fwd(xs))
+    res["swiglu_fwd"] = {"ms": round(ms, 4), "TBps": round(3 * ns / ms / 1e9, 2)}
+    ms = timeit(lambda: C.swiglu_bwd(ds, xs))
+    res["swiglu_bwd"] = {"ms": round(ms, 4), "TBps": round(5 * ns / ms / 1e9, 2)}
     print(json.dumps(res), flush=True)
 
 

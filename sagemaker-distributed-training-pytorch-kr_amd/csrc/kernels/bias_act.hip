@@ -109,14 +109,17 @@ __global__ __launch_bounds__(256) void bias_act_bwd_kernel(const T* __restrict__
 }
 
 // SwiGLU on a fused [rows, 2F] input laid out as [gate | up]: y = silu(gate) * up.
+
+// SwiGLU on a [rows, 2F] input: grid.x = 8-column chunk blocks of a row, grid.y = rows (a row
+// stride past 65535) — no 64-bit division / modulo per chunk as in the former grid-stride form:
+// at the LLaMA-7B SFT shape (4300 x 11008) fwd 6.26 -> 6.67 TB/s, bwd 5.18 -> 5.38 TB/s
+// (benchmarks/bench_elementwise.py, profiles/r4_swiglu_2d/).
 template <typename T>
-__global__ __launch_bounds__(256) void swiglu_fwd_kernel(const T* __restrict__ x,
-                                                         T* __restrict__ y, int64_t rows, int F) {
-  const int64_t nchunks = rows * (F / 8);
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nchunks;
-       i += (int64_t)gridDim.x * 256) {
-    int64_t r = i / (F / 8);
-    int c = (int)(i % (F / 8)) * 8;
+__global__ __launch_bounds__(256) void swiglu_fwd_kernel(const T* __restrict__ x, T* __restrict__ y,
+                                                          int64_t rows, int F) {
+  const int c = (blockIdx.x * 256 + threadIdx.x) * 8;
+  if (c >= F) return;
+  for (int64_t r = blockIdx.y; r < rows; r += gridDim.y) {
     float g[8], u[8];
     load_vec<T, 8>(x + r * 2 * F + c, g);
     load_vec<T, 8>(x + r * 2 * F + F + c, u);
@@ -127,29 +130,28 @@ __global__ __launch_bounds__(256) void swiglu_fwd_kernel(const T* __restrict__ x
 }
 
 template <typename T>
-__global__ __launch_bounds__(256) void swiglu_bwd_kernel(const T* __restrict__ dy,
-                                                         const T* __restrict__ x,
-                                                         T* __restrict__ dx, int64_t rows, int F) {
-  const int64_t nchunks = rows * (F / 8);
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nchunks;
-       i += (int64_t)gridDim.x * 256) {
-    int64_t r = i / (F / 8);
-    int c = (int)(i % (F / 8)) * 8;
+__global__ __launch_bounds__(256) void swiglu_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+                                                          T* __restrict__ dx, int64_t rows, int F) {
+  const int c = (blockIdx.x * 256 + threadIdx.x) * 8;
+  if (c >= F) return;
+  for (int64_t r = blockIdx.y; r < rows; r += gridDim.y) {
     float g[8], u[8], d[8], dg[8], du[8];
     load_vec<T, 8>(x + r * 2 * F + c, g);
     load_vec<T, 8>(x + r * 2 * F + F + c, u);
     load_vec<T, 8>(dy + r * F + c, d);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      float s = 1.f / (1.f + __expf(-g[j]));
-      float sl = g[j] * s;
+      float sg = 1.f / (1.f + __expf(-g[j]));
+      float sl = g[j] * sg;
       du[j] = d[j] * sl;
-      dg[j] = d[j] * u[j] * (s * (1.f + g[j] * (1.f - s)));
+      dg[j] = d[j] * u[j] * (sg * (1.f + g[j] * (1.f - sg)));
     }
     store_vec<T, 8>(dx + r * 2 * F + c, dg);
     store_vec<T, 8>(dx + r * 2 * F + F + c, du);
   }
 }
+
+
 
 __global__ __launch_bounds__(256) void col_partials_reduce_kernel(const float* __restrict__ part,
                                                                  int nslices, int N,
@@ -288,19 +290,21 @@ extern "C" hipError_t smdt_bias_grad(int dtype, const void* dy, int64_t rows, in
 extern "C" hipError_t smdt_swiglu_fwd(int dtype, const void* x, void* y, int64_t rows, int F,
                                       hipStream_t st) {
   if (F % 8 != 0) return hipErrorInvalidValue;
-  int grid = stream_grid(rows * (F / 8), 256);
-  if (dtype == 1) hipLaunchKernelGGL(swiglu_fwd_kernel<bf16>, dim3(grid), dim3(256), 0, st, (const bf16*)x, (bf16*)y, rows, F);
-  else if (dtype == 2) hipLaunchKernelGGL(swiglu_fwd_kernel<f16>, dim3(grid), dim3(256), 0, st, (const f16*)x, (f16*)y, rows, F);
-  else hipLaunchKernelGGL(swiglu_fwd_kernel<float>, dim3(grid), dim3(256), 0, st, (const float*)x, (float*)y, rows, F);
+  if (rows <= 0) return hipSuccess;
+  const dim3 g2((unsigned)((F / 8 + 255) / 256), (unsigned)(rows < 65535 ? rows : 65535));
+  if (dtype == 1) hipLaunchKernelGGL(swiglu_fwd_kernel<bf16>, g2, dim3(256), 0, st, (const bf16*)x, (bf16*)y, rows, F);
+  else if (dtype == 2) hipLaunchKernelGGL(swiglu_fwd_kernel<f16>, g2, dim3(256), 0, st, (const f16*)x, (f16*)y, rows, F);
+  else hipLaunchKernelGGL(swiglu_fwd_kernel<float>, g2, dim3(256), 0, st, (const float*)x, (float*)y, rows, F);
   return hipGetLastError();
 }
 
 extern "C" hipError_t smdt_swiglu_bwd(int dtype, const void* dy, const void* x, void* dx,
                                       int64_t rows, int F, hipStream_t st) {
   if (F % 8 != 0) return hipErrorInvalidValue;
-  int grid = stream_grid(rows * (F / 8), 256);
-  if (dtype == 1) hipLaunchKernelGGL(swiglu_bwd_kernel<bf16>, dim3(grid), dim3(256), 0, st, (const bf16*)dy, (const bf16*)x, (bf16*)dx, rows, F);
-  else if (dtype == 2) hipLaunchKernelGGL(swiglu_bwd_kernel<f16>, dim3(grid), dim3(256), 0, st, (const f16*)dy, (const f16*)x, (f16*)dx, rows, F);
-  else hipLaunchKernelGGL(swiglu_bwd_kernel<float>, dim3(grid), dim3(256), 0, st, (const float*)dy, (const float*)x, (float*)dx, rows, F);
+  if (rows <= 0) return hipSuccess;
+  const dim3 g2((unsigned)((F / 8 + 255) / 256), (unsigned)(rows < 65535 ? rows : 65535));
+  if (dtype == 1) hipLaunchKernelGGL(swiglu_bwd_kernel<bf16>, g2, dim3(256), 0, st, (const bf16*)dy, (const bf16*)x, (bf16*)dx, rows, F);
+  else if (dtype == 2) hipLaunchKernelGGL(swiglu_bwd_kernel<f16>, g2, dim3(256), 0, st, (const f16*)dy, (const f16*)x, (f16*)dx, rows, F);
+  else hipLaunchKernelGGL(swiglu_bwd_kernel<float>, g2, dim3(256), 0, st, (const float*)dy, (const float*)x, (float*)dx, rows, F);
   return hipGetLastError();
 }

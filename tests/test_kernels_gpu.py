@@ -133,9 +133,11 @@ def test_bias_gelu_partial_free_launch_shapes(rows, N):
     torch.testing.assert_close(dx.float(), zr.grad, atol=3e-2, rtol=3e-2)
 
 
-def test_swiglu():
+@pytest.mark.parametrize("rows,ffn", [(777, 1024), (70_001, 64)])
+def test_swiglu(rows, ffn):
+    """[rows, 2F] -> [rows, F]; 70,001 rows exercise the row stride past grid.y's 65,535."""
     torch.manual_seed(4)
-    x = torch.randn(777, 2 * 1024, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    x = torch.randn(rows, 2 * ffn, device=DEV, dtype=torch.bfloat16, requires_grad=True)
     y = SF.swiglu(x)
     xr = x.detach().float().requires_grad_()
     g, u = xr.chunk(2, -1)
