@@ -1,4 +1,6 @@
-"""HBM rate of the step's elementwise kernels at the GPT-2 345M bench shapes (one GPU).
+"""HBM rate of the step's elementwise kernels at the GPT-2 345M bench shapes (one GPU), plus the
+SFT recipe's SwiGLU and the LM-head cross-entropy. (A 4-vectors-in-flight CE backward measured
+no faster, 2.51 vs 2.47 ms at [65536, 50304], and was not kept: profiles/r4_swiglu_2d/ce_unroll.log.)
 
 bias-GeLU forward / backward on [65536, 4096] bf16 (fc1 output; backward without d(bias): the
 grouped wgrad makes it), the fused bias-dropout-residual LayerNorm forward and its backward on
@@ -76,6 +78,18 @@ def main():
     res["swiglu_fwd"] = {"ms": round(ms, 4), "TBps": round(3 * ns / ms / 1e9, 2)}
     ms = timeit(lambda: C.swiglu_bwd(ds, xs))
     res["swiglu_bwd"] = {"ms": round(ms, 4), "TBps": round(5 * ns / ms / 1e9, 2)}
+    del xs, ds
+    # vocab-parallel CE backward at the bench's LM head: [65536, 50304] bf16 logits -> dlogits
+    lg = torch.randn(T, 50304, device=dev, dtype=torch.bfloat16)
+    tg = torch.randint(0, 50257, (T,), device=dev)
+    mx, se, _ = C.ce_stats(lg, tg, 0, 50257)
+    dl = torch.ones(T, device=dev)
+    out = torch.empty_like(lg)
+    nl = lg.numel() * 2
+    ms = timeit(lambda: C.ce_bwd(lg, tg, mx, se, dl, out, 0, -100, 50257))
+    res["ce_bwd"] = {"ms": round(ms, 4), "TBps": round(2 * nl / ms / 1e9, 2)}
+    ms = timeit(lambda: C.ce_stats(lg, tg, 0, 50257))
+    res["ce_stats"] = {"ms": round(ms, 4), "TBps": round(nl / ms / 1e9, 2)}
     print(json.dumps(res), flush=True)
 
 
