@@ -429,6 +429,20 @@ void bias_grad(Tensor dy, Tensor out, bool accumulate) {
 }
 
 // ------------------------------------------------------------------ cross entropy
+// loss[rows] fp32; logits (16-bit, [rows, V]) are overwritten with softmax - onehot
+Tensor ce_fused(Tensor logits, Tensor target, int64_t ignore_index, int64_t vvalid) {
+  need_contig(logits, "logits");
+  need_contig(target, "target");
+  TORCH_CHECK(target.scalar_type() == at::kLong, "ce_fused: int64 targets");
+  const int64_t V = logits.size(-1), rows = logits.numel() / V;
+  TORCH_CHECK(target.numel() == rows, "ce_fused: target size mismatch");
+  auto loss = torch::empty({rows}, logits.options().dtype(at::kFloat));
+  check(smdt_ce_fused(dcode(logits), logits.data_ptr(), target.data_ptr<int64_t>(), loss.data_ptr<float>(),
+                      rows, (int)V, (int)(vvalid > 0 ? vvalid : V), ignore_index, cur_stream()),
+        "ce_fused");
+  return loss;
+}
+
 std::vector<Tensor> ce_stats(Tensor logits, Tensor target, int64_t vstart, int64_t vvalid) {
   need_contig(logits, "logits");
   need_contig(target, "target");
@@ -747,6 +761,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         arg("biases") = std::vector<Tensor>{}, arg("overwrite") = std::vector<bool>{});
   m.def("ce_stats", &ce_stats);
   m.def("ce_bwd", &ce_bwd);
+  m.def("ce_fused", &ce_fused);
   namespace py = pybind11;
   m.def("flash_fwd", &flash_fwd, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("scale"), py::arg("causal"),
         py::arg("out") = py::none(), py::arg("dropout_p") = 0.0, py::arg("seed") = 0, py::arg("offset") = 0);

@@ -175,10 +175,18 @@ class GPTModel(nn.Module):
         if not self.post_process:
             px, pb, res = out
             return SF.bias_dropout_add(px, pb, res, self.cfg.hidden_dropout, self.training)
+        st = ps.get_state()
+        if labels is not None:
+            w = self.output_weight if self.output_weight is not None else self.embedding.weight
+            if tp.lm_head_ce_ok(out, w, st.tp):
+                # LM-head GEMM + CE as one op: no backward pass over the [tokens, vocab] logits
+                vs = int(self.loss_vocab_size or 0)
+                vvalid = vs if 0 < vs < w.shape[0] else 0
+                loss = tp.LMHeadCrossEntropy.apply(out, w, labels.transpose(0, 1), -100, vvalid)
+                return loss.transpose(0, 1).contiguous()             # [b, s]
         logits = self.lm_logits(out)
         if labels is None:
             return logits.transpose(0, 1).contiguous()
-        st = ps.get_state()
         vstart = st.tp_rank * (self.cfg.padded_vocab_size // st.tp) if self.parallel_output else 0
         group = st.tp_group if (st.tp > 1 and self.parallel_output) else None
         loss = SF.cross_entropy(logits, labels.transpose(0, 1), vstart, group, inplace_grad=True,

@@ -723,6 +723,53 @@ class LinearWithGradAccumulationAndAsyncCommunication(torch.autograd.Function):
         return gi_out, dw, db, None, None, None
 
 
+class LMHeadCrossEntropy(torch.autograd.Function):
+    """Per-token CE of ``h W^T`` for an unsplit vocab (TP = 1), the LM head and the loss as ONE op.
+
+    The forward runs the logits GEMM, then ``ce_fused`` reads each logits row once and overwrites
+    it with softmax - onehot (cross_entropy.hip). The backward applies the per-row dloss on the
+    [tokens, hidden] side instead of the [tokens, vocab] side: dX = diag(dloss) (D W) and
+    dW = D^T (diag(dloss) X), so no pass over the logits remains in the backward. Against the
+    separate ce_stats / ce_bwd kernels this removes one full read of the logits per step. Same
+    math as Megatron's LM head + vocab-parallel CE at TP = 1 (SURVEY K12 / K13;
+    /root/reference/3_training_megatron-lm/pretrain_gpt.py:51-57).
+    """
+
+    @staticmethod
+    def forward(ctx, h, weight, target, ignore_index, vvalid):
+        logits = linear_rows(h, weight)
+        loss = _ext_mod().ce_fused(logits.view(-1, logits.shape[-1]), target.contiguous().view(-1),
+                                   int(ignore_index), int(vvalid))
+        ctx.save_for_backward(h, weight, logits)
+        return loss.view(target.shape)
+
+    @staticmethod
+    def backward(ctx, dloss):
+        h, weight, d = ctx.saved_tensors
+        dl = dloss.contiguous().view(-1, 1).float()
+        gi = dgrad(d, weight, _dgrad_weight_t(weight))
+        gi.view(-1, gi.shape[-1]).mul_(dl)
+        hs = torch.mul(h.reshape(-1, h.shape[-1]), dl).to(h.dtype)
+        dw = _wgrad(weight, d.view(-1, d.shape[-1]), hs)
+        return gi, dw, None, None, None
+
+
+def _ext_mod():
+    from ..ops import _ext
+    return _ext.ext()
+
+
+def lm_head_ce_ok(h, weight, tp: int) -> bool:
+    """Whether ``LMHeadCrossEntropy`` applies: HIP kernels on, TP = 1, 16-bit operands, a vocab
+    whose row fits one block's registers (V % 8 == 0, V <= 65536). SMDT_LM_HEAD_CE=0 disables."""
+    from ..ops import _ext
+    return (_LM_HEAD_CE and tp == 1 and _ext.use_kernels(h) and h.dtype in (torch.bfloat16, torch.float16)
+            and weight.dtype == h.dtype and weight.shape[0] % 8 == 0 and weight.shape[0] <= 65536)
+
+
+_LM_HEAD_CE = os.environ.get("SMDT_LM_HEAD_CE", "1") == "1"
+
+
 def linear_with_grad_accumulation_and_async_allreduce(x, weight, bias, sequence_parallel=False,
                                                       async_grad_allreduce=False, add_bias=True):
     if sequence_parallel and _TP_OVERLAP and _tp_size() > 1:

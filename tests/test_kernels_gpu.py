@@ -276,6 +276,36 @@ def test_cross_entropy_padded_vocab(vocab):
     assert logits.grad[:, vocab:].abs().max().item() == 0
 
 
+@pytest.mark.parametrize("V,vocab", [(50304, 50257), (1000, 0), (33792, 0), (60000, 0)])
+def test_lm_head_cross_entropy(V, vocab):
+    """LM-head GEMM + ce_fused (row overwritten in place, dloss applied on the hidden side)
+    against an fp32 linear + F.cross_entropy with per-token dloss, ignored rows and vocab padding."""
+    from smdt_amd.parallel import tensor_parallel as tp
+    torch.manual_seed(12)
+    s, b, H = 96, 3, 256
+    h = (0.5 * torch.randn(s, b, H, device=DEV)).bfloat16().requires_grad_()
+    w = (0.05 * torch.randn(V, H, device=DEV)).bfloat16().requires_grad_()
+    nv = vocab or V
+    tgt = torch.randint(0, nv, (s, b), device=DEV)
+    tgt[3, 1] = -100
+    tgt[7, 0] = nv - 1
+    assert tp.lm_head_ce_ok(h, w, 1)
+    loss = tp.LMHeadCrossEntropy.apply(h, w, tgt, -100, vocab if 0 < vocab < V else 0)
+    hr = h.detach().float().requires_grad_()
+    wr = w.detach().float().requires_grad_()
+    lg = (hr @ wr.t())[..., :nv]
+    ref = F.cross_entropy(lg.reshape(-1, nv), tgt.view(-1), reduction="none", ignore_index=-100).view(s, b)
+    torch.testing.assert_close(loss, ref, atol=2e-2, rtol=1e-2)
+    assert loss[3, 1].item() == 0
+    dl = torch.rand(s, b, device=DEV) / (s * b)
+    (loss * dl).sum().backward()
+    (ref * dl).sum().backward()
+    torch.testing.assert_close(h.grad.float(), hr.grad, atol=1e-4, rtol=5e-2)
+    torch.testing.assert_close(w.grad.float(), wr.grad, atol=1e-4, rtol=5e-2)
+    if vocab:
+        assert w.grad[vocab:].abs().max().item() == 0
+
+
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("D", [64, 128])
 @pytest.mark.parametrize("causal", [True, False])
