@@ -132,6 +132,9 @@ __global__ __launch_bounds__(256) void ce_bwd_kernel(const T* __restrict__ logit
 // thread, V <= NV * 8192), so the logits are read from HBM once and the row is overwritten IN PLACE
 // with softmax - onehot (zero for ignored rows and padding columns); loss[row] = log(S) + M - x_t.
 // Against ce_stats + ce_bwd this drops one full read of the logits (6.6 GB per GPT-2 345M step).
+// amdgpu_waves_per_eu(8) caps the kernel at 64 VGPRs (62 used at NV = 7, no scratch) so TWO blocks
+// share a CU and one block's reductions overlap the other's loads / stores: 3.31 -> 2.40 ms per step
+// at [65536, 50304] (with 68 VGPRs only one block fit; profiles/r4_lm_head_ce/).
 template <typename T, int NV>
 __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void ce_fused_kernel(T* __restrict__ logits,
                                                         const int64_t* __restrict__ target,
