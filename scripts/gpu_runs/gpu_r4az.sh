@@ -4,7 +4,7 @@
 set -u
 R="${GRAFT_REPO_ROOT:-$(pwd)}"
 cd "$R"
-O=gpurun_out/r4az
+O=gpurun_out/${R4AZ_OUT:-r4az}
 mkdir -p $O
 export TMPDIR=/tmp HSA_ENABLE_IPC_MODE_LEGACY=0
 step() {  # name timeout cmd...
