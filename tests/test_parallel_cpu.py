@@ -396,3 +396,22 @@ def test_fused_norms_wait_for_their_parameter_gather():
     layer(x, None, None)
     assert calls == [layer.input_norm, layer.post_attention_norm]
     assert other == []
+
+
+def test_lm_head_ce_gate_and_cpu_loss_path():
+    """The fused LM-head CE is a HIP-only path: on CPU tensors (and with TP > 1) the GPT loss goes
+    through the separate linear + cross_entropy, whose per-token loss matches F.cross_entropy."""
+    import torch.nn.functional as F
+    from smdt_amd.ops import functional as SF
+    from smdt_amd.parallel import tensor_parallel as tp
+    torch.manual_seed(0)
+    h = torch.randn(8, 2, 16, dtype=torch.bfloat16)
+    w = torch.randn(64, 16, dtype=torch.bfloat16)
+    assert not tp.lm_head_ce_ok(h, w, 1)
+    assert not tp.lm_head_ce_ok(h, w, 2)
+    tgt = torch.randint(0, 64, (8, 2))
+    tgt[1, 1] = -100
+    logits = (h.float() @ w.float().t())
+    loss = SF.cross_entropy(logits, tgt)
+    ref = F.cross_entropy(logits.view(-1, 64), tgt.view(-1), reduction="none", ignore_index=-100).view(8, 2)
+    torch.testing.assert_close(loss, ref, atol=1e-5, rtol=1e-5)
