@@ -760,10 +760,14 @@ def _ext_mod():
 
 
 def lm_head_ce_ok(h, weight, tp: int) -> bool:
-    """Whether ``LMHeadCrossEntropy`` applies: HIP kernels on, TP = 1, 16-bit operands, a vocab
-    whose row fits one block's registers (V % 8 == 0, V <= 65536). SMDT_LM_HEAD_CE=0 disables."""
+    """Whether ``LMHeadCrossEntropy`` applies: HIP kernels on, TP = 1, bf16 operands, a vocab
+    whose row fits one block's registers (V % 8 == 0, V <= 65536). SMDT_LM_HEAD_CE=0 disables.
+
+    bf16 only: the backward scales the hidden rows by the per-token dloss (``h * dl`` stored in
+    the 16-bit type). Under an fp16 loss scale dl ~ scale / tokens, and |h| > 1 would overflow
+    fp16 at loss scales the separate CE path (dl times softmax - onehot, |.| <= 1) still takes."""
     from ..ops import _ext
-    return (_LM_HEAD_CE and tp == 1 and _ext.use_kernels(h) and h.dtype in (torch.bfloat16, torch.float16)
+    return (_LM_HEAD_CE and tp == 1 and _ext.use_kernels(h) and h.dtype == torch.bfloat16
             and weight.dtype == h.dtype and weight.shape[0] % 8 == 0 and weight.shape[0] <= 65536)
 
 

@@ -12,6 +12,8 @@ import torch.nn.functional as F
 from smdt_amd.ops import _ext
 from smdt_amd.ops import functional as SF
 
+import _numerics as N
+
 pytestmark = pytest.mark.gpu
 
 DEV = "cuda"
@@ -152,29 +154,32 @@ def test_swiglu(rows, ffn):
 @pytest.mark.parametrize("sk", [128, 1024, 2048])
 @pytest.mark.parametrize("causal", [True, False])
 def test_scaled_masked_softmax(sk, causal):
-    torch.manual_seed(5)
-    x = torch.randn(2, 4, sk, sk, device=DEV, dtype=torch.bfloat16, requires_grad=True)
-    scale = 0.125
-    y = SF.scaled_masked_softmax(x, None, scale, causal)
-    xr = x.detach().float().requires_grad_()
-    s = xr * scale
-    if causal:
-        s = s.masked_fill(torch.ones(sk, sk, device=DEV, dtype=torch.bool).triu(1), float("-inf"))
-    yr = torch.softmax(s, -1)
-    torch.testing.assert_close(y.float(), yr, atol=1e-2, rtol=2e-2)
-    dy = torch.randn_like(y)
+    """Sharp scores (scaled std 1), judged per row relative to the row's max (tests/_numerics.py).
+    Mutation check (tests/test_numerics_sensitivity.py): an all-zero y or dx, dx x1.1, or dx zero
+    past row 64 fail this criterion (row-relative errors 1.0 / 1.0 / 0.10 / 1.0 vs tol 0.03); a bf16
+    emulation of the kernel passes at <= 0.01."""
+    x, dy = N.softmax_case(sk, causal, device=DEV)
+    x.requires_grad_()
+    y = SF.scaled_masked_softmax(x, None, 0.125, causal)
+    yr, dxr = N.softmax_ref(x, dy, 0.125, causal)
+    N.assert_rows_close(y, yr, N.SOFTMAX_TOL, "y")
     y.backward(dy)
-    yr.backward(dy.float())
-    torch.testing.assert_close(x.grad.float(), xr.grad, atol=1e-2, rtol=5e-2)
+    N.assert_rows_close(x.grad, dxr, N.SOFTMAX_TOL, "dx", row_floor=N.softmax_grad_floor(yr, dy, 0.125))
 
 
 def test_softmax_explicit_mask():
-    torch.manual_seed(6)
-    x = torch.randn(2, 3, 64, 256, device=DEV, dtype=torch.bfloat16)
-    mask = torch.rand(2, 1, 64, 256, device=DEV) < 0.3
-    y = SF.scaled_masked_softmax(x, mask, 1.0, False)
-    yr = torch.softmax(x.float().masked_fill(mask, float("-inf")), -1)
-    torch.testing.assert_close(y.float(), yr, atol=1e-2, rtol=2e-2)
+    """Arbitrary [b, 1, sq, sk] mask, forward and backward, row-relative (an unmasked softmax or
+    dx x1.1 fails the criterion: tests/test_numerics_sensitivity.py)."""
+    g = torch.Generator().manual_seed(6)
+    x = (8 * torch.randn(2, 3, 64, 256, generator=g)).bfloat16().to(DEV).requires_grad_()
+    mask = (torch.rand(2, 1, 64, 256, generator=g) < 0.3).to(DEV)
+    dy = torch.randn(2, 3, 64, 256, generator=g).bfloat16().to(DEV)
+    y = SF.scaled_masked_softmax(x, mask, 0.125, False)
+    yr, dxr = N.softmax_ref(x, dy, 0.125, False, mask)
+    N.assert_rows_close(y, yr, N.SOFTMAX_TOL, "y")
+    assert torch.all(y[mask.expand_as(y)] == 0)
+    y.backward(dy)
+    N.assert_rows_close(x.grad, dxr, N.SOFTMAX_TOL, "dx", row_floor=N.softmax_grad_floor(yr, dy, 0.125))
 
 
 def test_fused_adam_matches_reference():
@@ -244,64 +249,57 @@ def test_rope_inplace_and_inverse(nh):
 
 @pytest.mark.parametrize("V", [50304, 1000])
 def test_cross_entropy(V):
-    torch.manual_seed(9)
-    N = 300
-    logits = torch.randn(N, V, device=DEV, dtype=torch.bfloat16, requires_grad=True)
-    tgt = torch.randint(0, V, (N,), device=DEV)
-    tgt[5] = -100
+    """Peaked logits (std 8), half the targets the row's argmax and half random, O(1) signed
+    dloss; gradient judged per row relative to the row max. Mutation check
+    (tests/test_numerics_sensitivity.py): dropping the softmax term or scaling it by 1.1 / 0.9
+    gives row-relative errors >= 300 vs tol 0.03; a bf16 emulation of the kernel gives 0.004."""
+    logits, tgt, dl = N.ce_case(300, V, device=DEV)
+    logits.requires_grad_()
     loss = SF.cross_entropy(logits, tgt)
-    lr = logits.detach().float().requires_grad_()
-    ref = F.cross_entropy(lr, tgt, reduction="none", ignore_index=-100)
-    torch.testing.assert_close(loss, ref, atol=2e-2, rtol=1e-2)
-    w = torch.randn(N, device=DEV)
-    (loss * w).sum().backward()
-    (ref * w).sum().backward()
-    torch.testing.assert_close(logits.grad.float(), lr.grad, atol=2e-3, rtol=5e-2)
+    ref, gref = N.ce_ref(logits, tgt, dl)
+    torch.testing.assert_close(loss, ref, atol=5e-3, rtol=1e-3)
+    (loss * dl).sum().backward()
+    N.assert_rows_close(logits.grad, gref, N.CE_TOL, "dlogits")
 
 
 @pytest.mark.parametrize("vocab", [1000, 1017, 1024 - 8])
 def test_cross_entropy_padded_vocab(vocab):
-    """Columns >= vocab are padding: excluded from the softmax and given zero gradient."""
-    torch.manual_seed(11)
-    N, V = 200, 1024
-    logits = torch.randn(N, V, device=DEV, dtype=torch.bfloat16, requires_grad=True)
-    tgt = torch.randint(0, vocab, (N,), device=DEV)
+    """Columns >= vocab are padding: excluded from the softmax and given zero gradient (same
+    peaked inputs and row-relative criterion as test_cross_entropy)."""
+    logits, tgt, dl = N.ce_case(200, 1024, vocab, device=DEV, seed=11)
+    logits.requires_grad_()
     loss = SF.cross_entropy(logits, tgt, vocab_size=vocab)
-    lr = logits.detach()[:, :vocab].float().requires_grad_()
-    ref = F.cross_entropy(lr, tgt, reduction="none")
-    torch.testing.assert_close(loss, ref, atol=2e-2, rtol=1e-2)
-    loss.sum().backward()
-    ref.sum().backward()
-    torch.testing.assert_close(logits.grad[:, :vocab].float(), lr.grad, atol=2e-3, rtol=5e-2)
+    ref, gref = N.ce_ref(logits, tgt, dl, vocab)
+    torch.testing.assert_close(loss, ref, atol=5e-3, rtol=1e-3)
+    (loss * dl).sum().backward()
+    N.assert_rows_close(logits.grad, gref, N.CE_TOL, "dlogits")
     assert logits.grad[:, vocab:].abs().max().item() == 0
 
 
 @pytest.mark.parametrize("V,vocab", [(50304, 50257), (1000, 0), (33792, 0), (60000, 0)])
 def test_lm_head_cross_entropy(V, vocab):
     """LM-head GEMM + ce_fused (row overwritten in place, dloss applied on the hidden side)
-    against an fp32 linear + F.cross_entropy with per-token dloss, ignored rows and vocab padding."""
+    against fp32 math on the same 16-bit logits, with peaked logits (std ~4), half the targets
+    the argmax, an ignored row, vocab padding and O(1) signed dloss; dh and dW judged per row
+    relative to the row max. Mutation check (tests/test_numerics_sensitivity.py): the softmax
+    term dropped gives row-relative errors ~9-10, scaled x1.1 ~0.87-1.0, vs tol 0.03; a bf16
+    emulation of this op's rounding points gives <= 0.009."""
     from smdt_amd.parallel import tensor_parallel as tp
-    torch.manual_seed(12)
-    s, b, H = 96, 3, 256
-    h = (0.5 * torch.randn(s, b, H, device=DEV)).bfloat16().requires_grad_()
-    w = (0.05 * torch.randn(V, H, device=DEV)).bfloat16().requires_grad_()
-    nv = vocab or V
-    tgt = torch.randint(0, nv, (s, b), device=DEV)
-    tgt[3, 1] = -100
-    tgt[7, 0] = nv - 1
+    h, w, tgt, dl = N.lmce_case(96, 3, 256, V, vocab, device=DEV)
+    h.requires_grad_()
+    w.requires_grad_()
     assert tp.lm_head_ce_ok(h, w, 1)
+    assert not tp.lm_head_ce_ok(h.detach().half(), w.detach().half(), 1)   # fp16: separate CE path
+    lg16 = tp.linear_rows(h.detach(), w.detach())                # the GEMM the op runs, same kernel
+    lgf = h.detach().float() @ w.detach().float().t()
+    assert ((lg16.float() - lgf).abs() <= lgf.abs() * 2 ** -7 + 1e-3).all()
     loss = tp.LMHeadCrossEntropy.apply(h, w, tgt, -100, vocab if 0 < vocab < V else 0)
-    hr = h.detach().float().requires_grad_()
-    wr = w.detach().float().requires_grad_()
-    lg = (hr @ wr.t())[..., :nv]
-    ref = F.cross_entropy(lg.reshape(-1, nv), tgt.view(-1), reduction="none", ignore_index=-100).view(s, b)
-    torch.testing.assert_close(loss, ref, atol=2e-2, rtol=1e-2)
+    ref, dhr, dwr = N.lmce_ref(h, w, lg16, tgt, dl, vocab)
+    torch.testing.assert_close(loss, ref, atol=5e-3, rtol=1e-3)
     assert loss[3, 1].item() == 0
-    dl = torch.rand(s, b, device=DEV) / (s * b)
     (loss * dl).sum().backward()
-    (ref * dl).sum().backward()
-    torch.testing.assert_close(h.grad.float(), hr.grad, atol=1e-4, rtol=5e-2)
-    torch.testing.assert_close(w.grad.float(), wr.grad, atol=1e-4, rtol=5e-2)
+    N.assert_rows_close(h.grad, dhr, N.CE_TOL, "dh")
+    N.assert_rows_close(w.grad, dwr, N.CE_TOL, "dW")
     if vocab:
         assert w.grad[vocab:].abs().max().item() == 0
 
