@@ -162,6 +162,22 @@ class Trainer:
     # fraction of the free device memory a fused accumulation window may take for its activations
     FUSE_MEM_FRACTION = 0.6
 
+    def _fuse_decision(self, window) -> bool:
+        """``_window_fits`` agreed across the data-parallel group (MIN of one int per window).
+        ZeRO-2 reduce-scatters its buckets on every micro-batch and ZeRO-3 all-gathers parameters
+        on every forward, so a rank that ran a window unfused would issue GA times the
+        collectives of a rank that fused it: each rank's own token count and free memory must
+        not decide alone. One 4-byte all-reduce per accumulation window."""
+        ok = self._window_fits(window)
+        ddp = getattr(getattr(self, "engine", None), "ddp", None)
+        if ddp is not None and ddp.dp > 1:
+            dev = self.device if self.device.type == "cuda" and dist.get_backend(ddp.dp_group) != "gloo" \
+                else torch.device("cpu")
+            t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MIN, group=ddp.dp_group)
+            ok = bool(t.item())
+        return ok
+
     def _window_fits(self, window) -> bool:
         """Whether GA micro-batches fused into one batch fit in free device memory: an upper
         estimate of the activations autograd keeps for the fused batch (bf16 per token and layer:
@@ -280,7 +296,7 @@ class Trainer:
                         window.append(batch)
                         if len(window) < ga:
                             continue
-                        if self._window_fits(window):
+                        if self._fuse_decision(window):
                             fused, row_groups = _fuse_window(window)
                             if fused_windows == 0:
                                 self._log0(f"[sft] fused accumulation window: {ga} micro-batches as one batch of "

@@ -1,5 +1,6 @@
 """Worker bodies for the multi-process (gloo, CPU) tests. Importable by spawned children."""
 import os
+import time
 import sys
 
 import torch
@@ -1141,3 +1142,43 @@ def sp_gather_slots_worker():
     diff = max(float((g1[k] - g0[k]).abs().max()) for k in g0)
     print(json.dumps({"loss_diff": float((l1 - l0).abs()), "grad_max_diff": diff, "n_grads": len(g0),
                       "same_keys": sorted(g0) == sorted(g1), "stats_slots": s1, "stats_copy": s0}), flush=True)
+
+
+def sft_window_agreement_worker(rank, world, tmpdir, ds_cfg, nofit_rank, fuse_ga):
+    """The SFT Trainer on ``world`` Gloo ranks for 2 optimizer steps (GA 2) where only rank
+    ``nofit_rank`` finds its fused accumulation window too large (``Trainer._window_fits``
+    False there, True elsewhere). The decision must be agreed across the data-parallel group:
+    otherwise the ranks issue different numbers of ZeRO collectives and hang or mis-reduce.
+    Returns (full parameters, (fused, unfused) window counts logged by the trainer)."""
+    from smdt_amd.models.hf import HFCausalLM
+    from smdt_amd.data import sft
+    from smdt_amd.parallel import state as ps
+    from smdt_amd.train import hf_args
+    from smdt_amd.train.sft_trainer import Trainer
+    os.environ["SMDT_SFT_FUSE_GA"] = "1" if fuse_ga else "0"
+    Trainer._window_fits = lambda self, window: self.rank != nofit_rank
+    ps.destroy_model_parallel()
+    torch.manual_seed(0)
+    model = HFCausalLM(SFT_LLAMA, params_dtype=torch.float32)
+    tok = sft.HashWordTokenizer(120, 48, pad_token="<pad>", special_ids={"<pad>": 0, "</s>": 1, "<s>": 2, "<unk>": 3})
+    path = os.path.join(tmpdir, "alpaca.json")
+    if rank == 0 and not os.path.exists(path):
+        sft.write_synthetic_alpaca(path + ".tmp", 40, seed=1)
+        os.replace(path + ".tmp", path)
+    while not os.path.exists(path):
+        time.sleep(0.05)
+    ds = sft.SupervisedDataset(path, tok)
+    p = hf_args.ArgumentParser((hf_args.ModelArguments, hf_args.DataArguments, hf_args.TrainingArguments))
+    argv = ["--output_dir", os.path.join(tmpdir, f"out{int(fuse_ga)}{nofit_rank}"), "--per_device_train_batch_size", "2",
+            "--gradient_accumulation_steps", "2", "--learning_rate", "1e-3", "--logging_steps", "1",
+            "--save_steps", "0", "--max_steps", "2", "--deepspeed", ds_cfg, "--pad_to_multiple_of", "8",
+            "--warmup_steps", "1", "--seed", "5"]
+    args = p.parse_args_into_dataclasses(argv)[2]
+    logs = []
+    t = Trainer(model=model, tokenizer=tok, args=args, train_dataset=ds,
+                data_collator=sft.DataCollatorForSupervisedDataset(tok, 8))
+    t._log0 = lambda msg: logs.append(msg)
+    t.train()
+    with t.engine.gathered_params():
+        full = {k: v.detach().clone() for k, v in t.model.named_parameters()}
+    return full, [m for m in logs if "[sft]" in m]

@@ -425,3 +425,18 @@ def test_fused_accumulation_window_matches_micro_batches():
     assert abs(l0[0] - l1[0]) < 1e-5 and abs(l0[1] - l1[1]) < 1e-4, (l0, l1)
     for n in p0:
         torch.testing.assert_close(p1[n], p0[n], atol=1e-5, rtol=1e-4, msg=n)
+
+
+@pytest.mark.parametrize("cfg", ["zero2_bf16.json", "default_offload_opt_param.json"])
+def test_fused_window_decision_agreed_across_ranks(tmp_path, cfg):
+    """Only rank 1 finds its fused accumulation window too large: both ranks must run the window
+    micro-batch by micro-batch (ZeRO-2 reduce-scatters per micro-batch, ZeRO-3 gathers per
+    forward, so a split decision hangs or mis-reduces). Result equals SMDT_SFT_FUSE_GA=0."""
+    ds = os.path.join(REPO, "recipes", "4_training_alpaca_deepspeed", "configs", cfg)
+    split = run_workers(W.sft_window_agreement_worker, 2, str(tmp_path), ds, 1, True, timeout=400)
+    off = run_workers(W.sft_window_agreement_worker, 2, str(tmp_path), ds, -1, False, timeout=400)
+    assert not any("fused accumulation window:" in m for _, logs in split for m in logs)
+    assert any("would not fit" in m for m in split[0][1])          # rank 0 fits alone, yet agrees
+    for k, v in off[0][0].items():
+        torch.testing.assert_close(split[0][0][k], v, rtol=0, atol=0)
+        torch.testing.assert_close(split[1][0][k], v, rtol=0, atol=0)
