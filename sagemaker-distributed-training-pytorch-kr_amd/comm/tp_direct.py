@@ -54,9 +54,14 @@ class TpDirect:
         return self.eng is not None and self.eng.active
 
     def fits(self, t: torch.Tensor) -> bool:
+        """Whether the engine takes a tensor shaped like ``t``. World-uniform facts only (TP ranks
+        exchange equal shapes and dtypes; ``active`` changes only by a world-agreed fallback):
+        a rank that ran the ring while a peer ran the engine would deadlock the group. Address
+        alignment is not asked here: the engine only ever sees the freshly allocated (512-byte
+        aligned) gather / staging buffers below, never the caller's views."""
         nb = t.numel() * t.element_size()
         return self.active and t.is_cuda and t.dtype in (torch.bfloat16, torch.float16, torch.float32) \
-            and nb % 16 == 0 and t.data_ptr() % 16 == 0
+            and nb > 0 and nb % 16 == 0
 
     def all_gather(self, x: torch.Tensor, chunk_fn: Optional[Callable] = None,
                    before_last_wait: Optional[Callable] = None) -> Optional[torch.Tensor]:
@@ -64,15 +69,15 @@ class TpDirect:
         ``chunk_fn(c, chunk)`` for every chunk (the local one first, beside the transfer).
         None: not applicable (the caller runs the ring)."""
         x = x.contiguous()
-        if not self.fits(x):
+        if not (self.fits(x) and self.eng.use["all_gather"]):
             return None
         ws, r, n = self.world, self.rank, x.shape[0]
         total = x.new_empty((n * ws,) + tuple(x.shape[1:]))
         mine = total[r * n:(r + 1) * n]
         mine.copy_(x)
         h = self.eng.all_gather_async(total.view(-1), mine.view(-1))
-        if h is None:
-            return None
+        if h is None:     # cannot happen for a tensor fits() took: refuse loudly instead of mixing paths
+            raise RuntimeError("TpDirect.all_gather: the xGMI engine refused an exchange fits() accepted")
         self.calls += 1
         if chunk_fn is not None:
             chunk_fn(r, x)                       # beside the gather
@@ -98,8 +103,12 @@ class TpDirect:
             if c != r:
                 buf[c * n:(c + 1) * n].copy_(partial_fn(c))
         out = buf.new_empty((n,) + tuple(buf.shape[1:]))
-        h = self.eng.reduce_scatter_async(out.view(-1), buf.view(-1)) if self.fits(buf) else None
-        if h is None:
+        h = None
+        if self.fits(buf) and self.eng.use["reduce_scatter"]:
+            h = self.eng.reduce_scatter_async(out.view(-1), buf.view(-1))
+            if h is None:
+                raise RuntimeError("TpDirect.reduce_scatter: the xGMI engine refused an exchange fits() accepted")
+        else:
             w = dist.reduce_scatter_tensor(out, buf, group=self.group, async_op=True)
             if before_last_wait is not None:
                 before_last_wait()

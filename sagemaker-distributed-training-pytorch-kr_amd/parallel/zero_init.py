@@ -87,7 +87,13 @@ class Init:
         for cls in _module_classes():
             self._wrap_init(cls)
 
+        # chain to (and on exit restore) whatever __init_subclass__ nn.Module had: an outer Init
+        # context's hook, or another library's
+        self._prev_init_subclass = prev = nn.Module.__dict__.get("__init_subclass__")
+
         def init_subclass(cls, **kw):     # classes defined inside the context
+            if prev is not None:
+                prev.__get__(None, cls)(**kw)
             me._wrap_init(cls)
         nn.Module.__init_subclass__ = classmethod(init_subclass)
         return self
@@ -99,7 +105,11 @@ class Init:
             for cls, init in self._wrapped.items():
                 cls.__init__ = init
             self._wrapped = {}
-            del nn.Module.__init_subclass__
+            if self._prev_init_subclass is not None:
+                nn.Module.__init_subclass__ = self._prev_init_subclass
+            else:
+                del nn.Module.__init_subclass__
+            self._prev_init_subclass = None
         return False
 
     def _wrap_init(self, cls):

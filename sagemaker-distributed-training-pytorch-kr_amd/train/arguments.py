@@ -180,6 +180,9 @@ _GROUPS = {
         ("--model-parallel-size", dict(type=int, default=None)),
         ("--num-layers-per-virtual-pipeline-stage", dict(type=int, default=None)),
         ("--overlap-p2p-communication", dict(action="store_true")),
+        # non-interleaved pipeline schedule (train/schedules.py): Megatron's 1F1B by default; the
+        # zero-bubble split backward forms hold up to pp micro-batches of W operands in HBM
+        ("--pp-schedule", dict(default="1f1b", choices=["1f1b", "zb", "zbh1", "zbh2"])),
         ("--overlap-param-gather", dict(action="store_true")),
         ("--distributed-backend", dict(default="nccl", choices=["nccl", "gloo", "smddp", "rccl"])),
         ("--distributed-timeout-minutes", dict(type=int, default=10)),

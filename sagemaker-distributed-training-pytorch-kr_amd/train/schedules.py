@@ -284,7 +284,9 @@ def _run_backward(out, gout):
 #          r — HBM the 288 GB part has to spare — for a bubble of just the last stage's first wait
 #          (train/pipeline_sim.py: 16.2 -> 9.6 ms at the tp2pp2 BASELINE point).
 PP_SCHEDULES = ("1f1b", "zb", "zbh1", "zbh2")
-_PP_SCHEDULE = {"name": "zbh1"}
+# library default: Megatron's 1F1B (the reference's schedule, no extra held W operands); the
+# zero-bubble forms are opt-in (``--pp-schedule`` here and in bench.py, which selects zbh2)
+_PP_SCHEDULE = {"name": "1f1b"}
 
 
 def set_pipeline_schedule(name: str):

@@ -70,6 +70,11 @@ def initialize_megatron(extra_args_provider=None, args_defaults=None, ignore_unk
     ps.initialize_model_parallel(args.tensor_model_parallel_size, args.pipeline_model_parallel_size,
                                  args.virtual_pipeline_model_parallel_size, args.context_parallel_size)
     model_parallel_seed(args.seed, args.data_parallel_random_init)
+    from .schedules import set_pipeline_schedule
+    set_pipeline_schedule(getattr(args, "pp_schedule", "1f1b"))
+    if args.pipeline_model_parallel_size > 1:
+        print_rank_0(f"> pipeline schedule: "
+                     f"{'interleaved' if args.virtual_pipeline_model_parallel_size else args.pp_schedule}")
     args.mb_calculator = A.MicroBatchCalculator(args.global_batch_size, args.micro_batch_size,
                                                 args.data_parallel_size, args.rampup_batch_size)
     print_rank_0(args.mb_calculator.describe())

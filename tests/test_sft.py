@@ -440,3 +440,29 @@ def test_fused_window_decision_agreed_across_ranks(tmp_path, cfg):
     for k, v in off[0][0].items():
         torch.testing.assert_close(split[0][0][k], v, rtol=0, atol=0)
         torch.testing.assert_close(split[1][0][k], v, rtol=0, atol=0)
+
+
+def test_zero_init_contexts_nest_and_restore_init_subclass():
+    """Nested Init contexts: the inner exit must not drop the outer hook, the outer
+    exit must not raise, and an __init_subclass__ another library put on nn.Module survives."""
+    from torch import nn
+    from smdt_amd.parallel import zero_init as zi
+    seen = []
+
+    def lib_hook(cls, **kw):
+        seen.append(cls.__name__)
+    nn.Module.__init_subclass__ = classmethod(lib_hook)
+    try:
+        with zi.Init(enabled=True):
+            with zi.Init(enabled=True):
+                class A(nn.Module):
+                    pass
+            class B(nn.Module):          # outer context still hooks new classes
+                pass
+        class C(nn.Module):
+            pass
+        assert seen == ["A", "B", "C"]
+        assert nn.Module.__dict__["__init_subclass__"].__func__ is lib_hook
+    finally:
+        del nn.Module.__init_subclass__
+    assert "__init_subclass__" not in nn.Module.__dict__
