@@ -392,20 +392,26 @@ def main():
         dist.all_reduce(lv, op=dist.ReduceOp.MAX)
     loss_val = float(lv.item())
     if rank == 0:
+        emulated = bool(a.emulate_tp or a.emulate_first_stage or a.emulate_last_stage)
+        label = model_label(a, vocab)
+        if emulated:
+            # ONE rank of a larger job on one GPU, collectives as local copies: its time is an
+            # input to benchmarks/predict_scaling.py, never a job throughput (no value / vs_baseline
+            # / model TFLOP/s from the whole-model formula)
+            head = {"metric": "emulated rank ms/step", "value": round(ms_step, 3), "unit": "ms",
+                    "n_gpus": n, "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms_step, 3),
+                    "higher_is_better": False, "scaling": None, "vs_baseline": None}
+        else:
+            head = {"metric": ("tokens/sec (whole node) GPT-2 345M pretrain" if label.startswith("gpt2-345m")
+                               else f"tokens/sec (whole node) {label.split(' (')[0]} pretrain"),
+                    "value": round(tps, 1), "unit": "tokens/s", "n_gpus": n, "steps": a.steps,
+                    "warmup": a.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True,
+                    "scaling": "weak", "vs_baseline": round(tps / ref_tps, 3)}
         rec = {
-            "metric": "tokens/sec (whole node) GPT-2 345M pretrain",
-            "value": round(tps, 1),
-            "unit": "tokens/s",
-            "n_gpus": n,
-            "steps": a.steps,
-            "warmup": a.warmup,
-            "ms_per_step": round(ms_step, 3),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": round(tps / ref_tps, 3),
+            **head,
             "dtype": "bf16",
             "data": "synthetic (random tokens, CodeParrot-shaped [mbs, 1025] int64; random-init weights)",
-            "config": {"model": model_label(a, vocab), "global_batch": global_batch,
+            "config": {"model": label, "global_batch": global_batch,
                        "seq_len": S, "micro_batch": mbs, "grad_accum": a.grad_accum,
                        "parallelism": f"tp{a.tp}pp{a.pp}dp{st.dp}" + ("+sp" if cfg.sequence_parallel else "")
                        + ("+zero1" if zero else "") + (" (one emulated TP rank)" if a.emulate_tp else ""),
@@ -419,8 +425,9 @@ def main():
                        "flash_attn": not a.no_flash, "hidden_dropout": a.hidden_dropout,
                        "attention_dropout": a.attention_dropout, "recompute": a.recompute,
                        "gemm_autotune": tuned},
-            "model_tflops_per_gpu": round(tps * fpt / n / 1e12, 2),
-            "baseline": "41 model-TFLOP/s/GPU (reference GPT-2-small, 16xA100, BASELINE.md) at equal model FLOPs",
+            **({} if emulated else {
+                "model_tflops_per_gpu": round(tps * fpt / n / 1e12, 2),
+                "baseline": "41 model-TFLOP/s/GPU (reference GPT-2-small, 16xA100, BASELINE.md) at equal model FLOPs"}),
             "final_loss": loss_val,
         }
         comm = {**relay.TUNED, **xgmi.TUNED}

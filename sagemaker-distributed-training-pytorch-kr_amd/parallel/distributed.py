@@ -82,7 +82,7 @@ class DistributedDataParallel(nn.Module):
     def __init__(self, module: nn.Module, dp_group=None, grad_dtype=torch.float32, bucket_size="auto",
                  overlap_grad_reduce: bool = True, use_distributed_optimizer: bool = False,
                  average_in_collective: bool = True, torch_compat: bool = False,
-                 overlap_param_gather: bool = False, zero_stage: int = 1):
+                 overlap_param_gather: bool = False, zero_stage: int = 1, deterministic_reduce: bool = None):
         """``torch_compat=True`` gives drop-in ``torch.nn.parallel.DistributedDataParallel``
         semantics for scripts that drive a stock ``torch.optim`` optimizer: gradient sync is
         finalised automatically at the end of ``backward()`` (autograd-engine callback),
@@ -122,6 +122,17 @@ class DistributedDataParallel(nn.Module):
         # backend asks for it, or — by default — for each op a run-time timing on this node shows
         # faster than RCCL (SMDT_XGMI_ALLREDUCE=0: never); larger messages are chunked.
         self.xgmi = _xgmi.create_for_group(self.dp_group, auto=True) if rccl else None
+        # Fixed-order combine (``deterministic_reduce`` / SMDT_DETERMINISTIC_REDUCE=1): every
+        # gradient reduction all-gathers the ranks' buckets and sums them locally in rank order,
+        # (g_0 + g_1) + g_2 + ..., then divides by dp — independent of the backend's ring / tree
+        # association, so a run is bit-reproducible and a single-process reference that folds
+        # the same micro-batch gradients in the same order matches it exactly. Costs dp x the
+        # bucket bytes of an all-gather and runs synchronously: a debugging / testing mode.
+        if deterministic_reduce is None:
+            deterministic_reduce = os.environ.get("SMDT_DETERMINISTIC_REDUCE", "0") == "1"
+        self.deterministic = bool(deterministic_reduce) and self.dp > 1
+        if self.deterministic:
+            self.xgmi = None
         self._syncs = 0
 
         params = [p for p in module.parameters() if p.requires_grad]
@@ -364,6 +375,15 @@ class DistributedDataParallel(nn.Module):
             return
         view = self.grad_data[b.start:b.end]
         nb = view.numel() * view.element_size()
+        if self.deterministic:
+            folded = self._fold(view)
+            if self.zero:
+                s, e = self.shard_range(b)
+                self.grad_data[s:e].copy_(folded[s - b.start:e - b.start])
+            else:
+                view.copy_(folded)
+            b.handle = None
+            return
         if self.zero:
             s, e = self.shard_range(b)
             out = self.grad_data[s:e]
@@ -507,7 +527,10 @@ class DistributedDataParallel(nn.Module):
         out = sh if fresh else torch.empty_like(sh)
         h = self.xgmi.reduce_scatter_async(out, buf, op="avg") if (self.xgmi is not None and self.dp > 1) else None
         nb = buf.numel() * buf.element_size()
-        if self.dp == 1:
+        if self.deterministic:
+            out.copy_(self._fold(buf)[self.dp_rank * n:(self.dp_rank + 1) * n])
+            handle = None
+        elif self.dp == 1:
             out.copy_(buf)
             handle = None
         elif h is not None:
@@ -522,6 +545,17 @@ class DistributedDataParallel(nn.Module):
                 handle = dist.reduce_scatter_tensor(out, buf, group=self.dp_group, async_op=True)
             _cs.collective("reduce_scatter", self.dp_group, nb, work=handle)
         self._rs_inflight[b.index] = (handle, None if fresh else out)
+
+    def _fold(self, x: torch.Tensor) -> torch.Tensor:
+        """Fixed-order combine (``deterministic_reduce``): all-gather ``x`` from every rank of
+        the DP group, sum the copies in rank order and divide by dp."""
+        parts = x.new_empty((self.dp,) + tuple(x.shape))
+        dist.all_gather_into_tensor(parts.view(-1), x.contiguous().view(-1), group=self.dp_group)
+        _cs.collective("all_gather", self.dp_group, x.numel() * x.element_size())
+        acc = parts[0].clone()
+        for r in range(1, self.dp):
+            acc.add_(parts[r])
+        return acc.div_(self.dp)
 
     def bucket_shard_grad(self, b: Bucket) -> torch.Tensor:
         """This rank's reduced gradient shard of bucket b (any stage, after finish_grad_sync)."""

@@ -106,9 +106,7 @@ def ddp_worker(rank, world, zero, steps=3, overlap_pg=False, defer=False):
     m = GPTModel(cfg)
     ddp = DistributedDataParallel(m, bucket_size=20000, use_distributed_optimizer=zero,
                                   overlap_param_gather=overlap_pg)
-    # eps 1e-6 (not 1e-8): a gradient within ~1e-9 of zero whose fp32 sum order differs between
-    # the reduced and single-process runs would flip its Adam step sign (lr-sized param delta)
-    opt = MixedPrecisionAdam(ddp, lr=1e-2, weight_decay=0.1, clip_grad=1.0, eps=1e-6)
+    opt = MixedPrecisionAdam(ddp, lr=1e-2, weight_decay=0.1, clip_grad=1.0, eps=1e-8)
     tokens, labels = _batch(b=4)
     shard = slice(rank * (4 // world), (rank + 1) * (4 // world))
     first_grads = None
@@ -134,7 +132,13 @@ def ddp_worker(rank, world, zero, steps=3, overlap_pg=False, defer=False):
     return out, first_grads
 
 
-def single_train(steps=3):
+def single_train(steps=3, split=2):
+    """Single-process reference for ``ddp_worker``: the global batch of 4 sequences as ``split``
+    (the DP world size) micro-batches whose gradients land in separate buffers and are then
+    combined in rank order and divided by ``split`` — the association the reduced run uses
+    ((g_0 + g_1) / 2 over two ranks, exact up to that fixed order), so the reduced gradients are
+    bit-identical and Adam runs at its real eps 1e-8 (a near-zero gradient summed in another
+    order would flip its step-1 update sign, an lr-sized parameter difference)."""
     from smdt_amd.models.gpt import GPTModel
     from smdt_amd.models.transformer import TransformerConfig
     from smdt_amd.optim.optimizer import MixedPrecisionAdam
@@ -144,16 +148,23 @@ def single_train(steps=3):
     cfg = TransformerConfig(**TINY)
     m = GPTModel(cfg)
     ddp = DistributedDataParallel(m, bucket_size=20000)
-    # eps 1e-6 (not 1e-8): a gradient within ~1e-9 of zero whose fp32 sum order differs between
-    # the reduced and single-process runs would flip its Adam step sign (lr-sized param delta)
-    opt = MixedPrecisionAdam(ddp, lr=1e-2, weight_decay=0.1, clip_grad=1.0, eps=1e-6)
+    opt = MixedPrecisionAdam(ddp, lr=1e-2, weight_decay=0.1, clip_grad=1.0, eps=1e-8)
     tokens, labels = _batch(b=4)
     first_grads = None
+    per = 4 // split
     for _ in range(steps):
-        ddp.zero_grad_buffer()
-        loss = ddp(tokens, None, None, labels=labels).mean()
-        loss.backward()
-        ddp.finish_grad_sync()
+        parts = []
+        for k in range(split):
+            ddp.zero_grad_buffer()
+            sl = slice(k * per, (k + 1) * per)
+            loss = ddp(tokens[sl], None, None, labels=labels[sl]).mean()
+            loss.backward()
+            ddp.finish_grad_sync()
+            parts.append(ddp.grad_data.clone())
+        tot = parts[0]
+        for p_ in parts[1:]:
+            tot = tot + p_
+        ddp.grad_data.copy_(tot * (1.0 / split))
         if first_grads is None:
             first_grads = {n: p.main_grad.detach().clone() for n, p in m.named_parameters()}
         opt.step()
@@ -187,10 +198,18 @@ def sft_batches(n=8, b=2, s=16, v=120, seed=3):
 
 
 def zero_sft_worker(rank, world, stage, ga, steps, offload=False, offload_param=False, with_mem=False,
-                    zero_init=False):
+                    zero_init=False, emulate=0, emulate_stage=0):
     """Data-parallel SFT steps with the ZeroEngine; global batch = world * 2 * ga rows of
     ``sft_batches``. Returns full params after ``steps`` optimizer steps. ``zero_init``: build the
-    model under parallel/zero_init.Init (stage 3)."""
+    model under parallel/zero_init.Init (stage 3).
+
+    Multi-rank runs use the fixed-order combine (DistributedDataParallel ``deterministic_reduce``:
+    rank-order sum, then / dp). ``emulate`` = W (world 1, ``ga`` = W x the emulated per-rank GA):
+    the single-process reference reproduces that association exactly — each emulated rank's
+    micro-batch gradients land in their own buffer and are folded in rank order, per
+    accumulation window for gradient stages <= 1 (``emulate_stage``; each rank sums its window
+    locally, then one reduction) or per micro-batch for stages >= 2 (reduced every micro-batch,
+    accumulated into the shard) — so the runs agree bit for bit and Adam runs at its real eps."""
     from smdt_amd.comm import init_distributed
     from smdt_amd.models.hf import HFCausalLM
     from smdt_amd.parallel import state as ps
@@ -213,11 +232,9 @@ def zero_sft_worker(rank, world, stage, ga, steps, offload=False, offload_param=
     init_stats = {"peak_bytes": ctx.peak_bytes, "shard_bytes": ctx.shard_bytes, "params": ctx.params,
                   "largest_param_bytes": ctx.largest_param_bytes,
                   "resident_bytes_after_build": sum(p.numel() * p.element_size() for p in m.parameters())}
-    # eps 1e-6 (DeepSpeed's default is 1e-8): with ga > 1 the sharded run sums a rank's micro-batch
-    # gradients before the reduce-scatter, single-rank accumulation sums them in sequence — 1 ulp
-    # apart, which flips the sign of a gradient element within ~1e-9 of zero; at eps 1e-8 that flip
-    # moved Adam's update by up to ~0.2 lr (a rare full-suite flake), at 1e-6 by < 1e-3 lr
-    cfg = {"optimizer": {"type": "AdamW", "params": {"lr": 1e-3, "betas": [0.9, 0.99], "eps": 1e-6,
+    if world > 1:
+        os.environ["SMDT_DETERMINISTIC_REDUCE"] = "1"
+    cfg = {"optimizer": {"type": "AdamW", "params": {"lr": 1e-3, "betas": [0.9, 0.99], "eps": 1e-8,
                                                      "weight_decay": 0.1}},
            "gradient_accumulation_steps": ga, "gradient_clipping": 1.0,
            "zero_optimization": {"stage": stage, **({"offload_optimizer": {"device": "cpu"}} if offload else {}),
@@ -225,8 +242,10 @@ def zero_sft_worker(rank, world, stage, ga, steps, offload=False, offload_param=
                                  "stage3_param_persistence_threshold": 200, "stage3_prefetch_bucket_size": 4000}}
     eng = ZeroEngine(m, cfg, log=lambda *_: None)
     data = sft_batches(n=steps * ga * world + 8)
+    if emulate > 1:
+        _emulated_reference_steps(eng, m, data, emulate, ga // emulate, steps, emulate_stage)
     k = 0
-    for _ in range(steps):
+    for _ in range(steps if emulate <= 1 else 0):
         for _ in range(ga):
             # each optimizer step consumes world*ga micro-batches in order; rank r takes every world-th
             ids = torch.cat([data[k + j * world + rank][0] for j in range(1)])
@@ -258,6 +277,52 @@ def zero_sft_worker(rank, world, stage, ga, steps, offload=False, offload_param=
     with eng.gathered_params():
         out = {n: p.detach().clone() for n, p in m.named_parameters()}
     return (out, mem) if with_mem else out
+
+
+def _emulated_reference_steps(eng, m, data, W, ga_r, steps, stage):
+    """zero_sft_worker's ``emulate`` path: one process, W emulated ranks of ``ga_r`` micro-batches
+    each per optimizer step (micro-batch j of rank r = data[base + j W + r], as in the W-rank run),
+    gradients combined in the fixed order DistributedDataParallel.deterministic_reduce uses. The
+    engine's GA is W ga_r, so each micro-batch loss carries 1 / (W ga_r) — the W-rank run's
+    1 / ga_r and its / W after the rank-order sum, equal up to exact powers of two."""
+    ddp = eng.ddp
+    eng._hold_wgrad = lambda: False          # every micro-batch's gradient must land in the buffer
+
+    def grad_of(idx):
+        ddp.zero_grad_buffer()
+        loss, _ = m(data[idx][0], labels=data[idx][1])
+        eng.backward(loss)
+        return ddp.grad_data.clone()
+
+    base = 0
+    for _ in range(steps):
+        order = [(j, r) for r in range(W) for j in range(ga_r)] if stage <= 1 else \
+            [(j, r) for j in range(ga_r) for r in range(W)]
+        grads = {}
+        for n_done, (j, r) in enumerate(order):
+            grads[(j, r)] = grad_of(base + j * W + r)
+            if n_done < len(order) - 1:
+                eng.step()                    # not a boundary: counts the micro-batch
+        if stage <= 1:                        # each rank sums its window, then the rank fold
+            per_rank = []
+            for r in range(W):
+                acc = grads[(0, r)]
+                for j in range(1, ga_r):
+                    acc = acc + grads[(j, r)]
+                per_rank.append(acc)
+            tot = per_rank[0]
+            for r in range(1, W):
+                tot = tot + per_rank[r]
+        else:                                 # reduced per micro-batch, accumulated into the shard
+            tot = None
+            for j in range(ga_r):
+                f = grads[(j, 0)]
+                for r in range(1, W):
+                    f = f + grads[(j, r)]
+                tot = f if tot is None else tot + f
+        ddp.grad_data.copy_(tot)
+        eng.step()                            # the boundary: optimizer step on the folded gradient
+        base += W * ga_r
 
 
 def zero_init_torch_modules_worker(rank, world):
@@ -1182,3 +1247,26 @@ def sft_window_agreement_worker(rank, world, tmpdir, ds_cfg, nofit_rank, fuse_ga
     with t.engine.gathered_params():
         full = {k: v.detach().clone() for k, v in t.model.named_parameters()}
     return full, [m for m in logs if "[sft]" in m]
+
+
+def deterministic_fold_worker(rank, world, zero):
+    """DistributedDataParallel(deterministic_reduce=True): each rank's gradient buffer holds
+    rank-seeded values; returns the reduced buffer (this rank's shard region for ZeRO-1)."""
+    import torch.distributed as dist
+    from smdt_amd.comm import init_distributed
+    from smdt_amd.parallel import state as ps
+    from smdt_amd.parallel.distributed import DistributedDataParallel
+    init_distributed("gloo")
+    ps.initialize_model_parallel(1, 1)
+    m = torch.nn.Sequential(torch.nn.Linear(64, 96), torch.nn.Linear(96, 48))
+    ddp = DistributedDataParallel(m, bucket_size=3000, use_distributed_optimizer=zero, deterministic_reduce=True)
+    ddp.zero_grad_buffer()
+    g = torch.Generator().manual_seed(100 + rank)
+    ddp.grad_data.copy_(torch.randn(ddp.grad_data.numel(), generator=g) * torch.logspace(-6, 3, ddp.grad_data.numel()))
+    for b in ddp.buckets:
+        ddp._launch(b)
+    ddp.finish_grad_sync()
+    ranges = [ddp.shard_range(b) for b in ddp.buckets] if zero else [(0, ddp.grad_data.numel())]
+    out = (ddp.grad_data.clone(), ranges)
+    dist.destroy_process_group()
+    return out

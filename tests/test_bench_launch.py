@@ -119,6 +119,7 @@ def test_bench_emulated_tp_rank(tmp_path):
     assert r.returncode == 0, r.stderr[-3000:]
     rec = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
     assert rec["config"]["tp"] == 2 and "emulated" in rec["config"]["parallelism"]
+    assert rec["metric"] == "emulated rank ms/step" and rec["unit"] == "ms" and not rec["higher_is_better"]
     assert rec["config"]["model"].endswith("vocab 256, seq 32)")   # padded to 128 x tp and rec["final_loss"] > 0
 
 
@@ -134,7 +135,10 @@ def test_bench_emulated_pipeline_stage(tmp_path, stage):
     r = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     rec = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
-    assert rec["value"] > 0 and set(rec["fbw_ms"]) >= {"F", "B", "W"}
+    assert set(rec["fbw_ms"]) >= {"F", "B", "W"}
+    # an emulated rank is not a job throughput: its own metric, no headline fields
+    assert rec["metric"] == "emulated rank ms/step" and rec["value"] == rec["ms_per_step"] > 0
+    assert rec["vs_baseline"] is None and "model_tflops_per_gpu" not in rec
 
 
 @pytest.mark.slow

@@ -133,7 +133,8 @@ def test_cpu_adam_matches_torch_adamw():
 def test_zero_world2_matches_world1(stage, ga, offload, offload_param):
     """Every ZeRO stage (2: partitioned gradients; 3: + partitioned parameters gathered per layer,
     optionally offloaded to pinned host memory, with CPU Adam) reproduces single-rank training."""
-    ref = run_workers(W.zero_sft_worker, 1, 0, 2 * ga, 3, False)[0]      # GA 2*ga on one rank
+    # GA 2*ga on one rank, folded like two ranks (dist_workers._emulated_reference_steps)
+    ref = run_workers(W.zero_sft_worker, 1, 0, 2 * ga, 3, False, False, False, False, 2, stage)[0]
     outs = run_workers(W.zero_sft_worker, 2, stage, ga, 3, offload, offload_param)   # GA ga on two ranks
     for r in range(2):
         for k, v in ref.items():
@@ -151,7 +152,7 @@ def test_zero2_lazy_grad_buffers_match_world1(ga, tied, monkeypatch):
     monkeypatch.setenv("SMDT_TEST_CPU_DEFER", "1")
     if tied:
         monkeypatch.setenv("SMDT_TEST_TIED", "1")
-    ref = run_workers(W.zero_sft_worker, 1, 0, 2 * ga, 3, False)[0]
+    ref = run_workers(W.zero_sft_worker, 1, 0, 2 * ga, 3, False, False, False, False, 2, 2)[0]
     outs = run_workers(W.zero_sft_worker, 2, 2, ga, 3, False, False, True)
     for r in range(2):
         params, mem = outs[r]
@@ -164,7 +165,7 @@ def test_zero2_lazy_grad_buffers_match_world1(ga, tied, monkeypatch):
 def test_zero2_world8_matches_world1():
     """ZeRO-2 over 8 gloo ranks (gradient shards of 1/8, one micro-batch each) == one rank
     accumulating the same 8 micro-batches."""
-    ref = run_workers(W.zero_sft_worker, 1, 0, 8, 2, False)[0]
+    ref = run_workers(W.zero_sft_worker, 1, 0, 8, 2, False, False, False, False, 8, 2)[0]
     outs = run_workers(W.zero_sft_worker, 8, 2, 1, 2, False, False, timeout=600)
     for r in range(8):
         for k, v in ref.items():
@@ -172,11 +173,12 @@ def test_zero2_world8_matches_world1():
 
 
 def _adam_close(got, ref, steps, what, lr=1e-3):
-    """Parameters after ``steps`` AdamW steps agree elementwise at rtol 2e-4 / atol 2e-5. The
-    gradient norm (hence the clip coefficient) is accumulated in fp64 (optim/optimizer._sumsq), so
-    it does not depend on how the gradient is split into ZeRO shards; what remains between a sharded
-    run and single-rank accumulation is the association of the micro-batch gradient sums (1 ulp),
-    which the workers' Adam eps keeps from flipping near-zero updates (dist_workers.zero_sft_worker)."""
+    """Parameters after ``steps`` AdamW steps (eps 1e-8) agree elementwise at rtol 2e-4 / atol
+    2e-5. The reference folds the micro-batch gradients in the sharded run's fixed order
+    (dist_workers._emulated_reference_steps, DistributedDataParallel.deterministic_reduce), so the
+    reduced gradients are equal; the gradient norm is accumulated in fp64 (optim/optimizer._sumsq)
+    and does not depend on the shard split. What remains is the CPU-Adam / torch-Adam arithmetic
+    of the offload configurations."""
     torch.testing.assert_close(got, ref, rtol=2e-4, atol=2e-5, msg=str(what))
 
 
