@@ -53,6 +53,7 @@ import torch.distributed as dist
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 from smdt_amd.comm import init_distributed, relay  # noqa: E402
+from smdt_amd.comm import streams as comm_streams  # noqa: E402
 from smdt_amd.models.gpt import GPTModel, allreduce_word_embedding_grads, gpt_flops_per_token, pad_vocab_size  # noqa: E402
 from smdt_amd.models.transformer import TransformerConfig  # noqa: E402
 from smdt_amd.optim.optimizer import MixedPrecisionAdam  # noqa: E402
@@ -424,7 +425,8 @@ def main():
                        "scaling_note": f"weak: {a.seqs_per_gpu} seqs x {S} tokens per GPU per step",
                        "flash_attn": not a.no_flash, "hidden_dropout": a.hidden_dropout,
                        "attention_dropout": a.attention_dropout, "recompute": a.recompute,
-                       "gemm_autotune": tuned},
+                       "gemm_autotune": tuned,
+                       "comm_stream_priority": comm_streams.describe()["comm_stream_priority"]},
             **({} if emulated else {
                 "model_tflops_per_gpu": round(tps * fpt / n / 1e12, 2),
                 "baseline": "41 model-TFLOP/s/GPU (reference GPT-2-small, 16xA100, BASELINE.md) at equal model FLOPs"}),

@@ -73,7 +73,8 @@ class LoopbackGroup(dist.ProcessGroup):
         dev = t0.device
         side = self._streams.get(dev)
         if side is None:
-            side = self._streams[dev] = torch.cuda.Stream(device=dev)
+            from .streams import comm_stream
+            side = self._streams[dev] = comm_stream(dev)
         side.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(side):
             fn()

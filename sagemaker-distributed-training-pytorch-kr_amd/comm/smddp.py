@@ -181,7 +181,8 @@ class SMDDPProcessGroup(dist.ProcessGroup):
             return
         work = self._inner.allreduce([flag], mx)
         if self._side is None:
-            self._side = torch.cuda.Stream(device=dev)
+            from .streams import comm_stream
+            self._side = comm_stream(dev)
         pinned = torch.zeros(1, dtype=torch.int32, pin_memory=True)
         with torch.cuda.stream(self._side):
             work.wait()                  # the side stream waits for RCCL, not the compute stream

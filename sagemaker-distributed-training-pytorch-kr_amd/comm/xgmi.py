@@ -409,7 +409,8 @@ class XgmiAllReduce(IpcEngine):
     def _async(self, fn, tensors, *args) -> Optional[_EventHandle]:
         dev = tensors[0].device
         if self._stream is None:
-            self._stream = torch.cuda.Stream(device=dev)
+            from .streams import comm_stream
+            self._stream = comm_stream(dev)
         cur = torch.cuda.current_stream(dev)
         self._stream.wait_stream(cur)
         with torch.cuda.stream(self._stream):

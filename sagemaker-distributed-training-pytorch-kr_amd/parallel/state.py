@@ -97,10 +97,16 @@ _STATE: Optional[ParallelState] = None
 
 
 def _new_group(ranks, backend=None):
-    if len(ranks) == 1 and dist.get_world_size() > 1:
-        # Single-rank groups are still created so every rank calls new_group identically.
-        return dist.new_group(ranks, backend=backend)
-    return dist.new_group(ranks, backend=backend)
+    """Every rank calls this identically (single-rank groups are created too). RCCL groups get a
+    high-priority internal stream (comm/streams.nccl_pg_options; SMDT_COMM_PRIORITY=normal: off):
+    TP / SP exchanges, pipeline p2p and DP buckets overlap GEMMs and must not queue behind them."""
+    kw = {}
+    if (backend or dist.get_backend()) == "nccl":
+        from ..comm.streams import nccl_pg_options
+        opts = nccl_pg_options()
+        if opts is not None:
+            kw["pg_options"] = opts
+    return dist.new_group(ranks, backend=backend, **kw)
 
 
 def initialize_model_parallel(tensor_model_parallel_size: int = 1, pipeline_model_parallel_size: int = 1,

@@ -71,7 +71,8 @@ class ZeroParamPartitioner:
         self._traced = {"fwd": False, "bwd": False}
         # H2D copies of offloaded shards and the parameter gathers run on a side stream, ordered by
         # events, so they overlap the compute of the previous block
-        self.side = torch.cuda.Stream(device=self.dev) if self.dev.type == "cuda" else None
+        from ..comm.streams import comm_stream
+        self.side = comm_stream(self.dev) if self.dev.type == "cuda" else None
         old = ddp.param_data
         with torch.no_grad():
             if ddp._zero_init:
