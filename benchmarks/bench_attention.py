@@ -13,6 +13,16 @@ import torch.nn.functional as F
 
 import os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+if "--ext" in sys.argv:
+    # A/B builds: load an alternate kernel library (e.g. benchmarks/bin/ab_ref_C.so, the same
+    # sources before a change) as smdt_amd._C before anything imports the in-tree one
+    import importlib.util
+    _p = sys.argv[sys.argv.index("--ext") + 1]
+    _spec = importlib.util.spec_from_file_location("smdt_amd._C", _p)
+    _m = importlib.util.module_from_spec(_spec)
+    import smdt_amd  # noqa: E402,F401
+    sys.modules["smdt_amd._C"] = _m
+    _spec.loader.exec_module(_m)
 from smdt_amd.ops import functional as SF  # noqa: E402
 
 
@@ -42,6 +52,7 @@ def main():
     p.add_argument("--causal", type=int, default=1)
     p.add_argument("--sdpa", type=int, default=1)
     p.add_argument("--dropout", type=float, default=0.0)
+    p.add_argument("--ext", default=None, help="alternate _C.so for A/B runs")
     a = p.parse_args()
     B, H, S, D = a.b, a.h, a.s, a.d
     Hkv = a.hkv or H

@@ -438,9 +438,24 @@ Tensor ce_fused(Tensor logits, Tensor target, int64_t ignore_index, int64_t vval
   TORCH_CHECK(target.numel() == rows, "ce_fused: target size mismatch");
   auto loss = torch::empty({rows}, logits.options().dtype(at::kFloat));
   check(smdt_ce_fused(dcode(logits), logits.data_ptr(), target.data_ptr<int64_t>(), loss.data_ptr<float>(),
-                      rows, (int)V, (int)(vvalid > 0 ? vvalid : V), ignore_index, cur_stream()),
+                      rows, (int)V, (int)(vvalid > 0 ? vvalid : V), ignore_index, 0, 0, cur_stream()),
         "ce_fused");
   return loss;
+}
+
+// Vocab-parallel form: logits [rows, V] = this rank's vocab slice starting at vstart, overwritten
+// with exp(x - m_local); returns stats [3, rows] fp32 = (m_local, sum, target logit or 0).
+Tensor ce_fused_local(Tensor logits, Tensor target, int64_t vstart, int64_t vvalid) {
+  need_contig(logits, "logits");
+  need_contig(target, "target");
+  TORCH_CHECK(target.scalar_type() == at::kLong, "ce_fused_local: int64 targets");
+  const int64_t V = logits.size(-1), rows = logits.numel() / V;
+  TORCH_CHECK(target.numel() == rows, "ce_fused_local: target size mismatch");
+  auto stats = torch::empty({3, rows}, logits.options().dtype(at::kFloat));
+  check(smdt_ce_fused(dcode(logits), logits.data_ptr(), target.data_ptr<int64_t>(), stats.data_ptr<float>(),
+                      rows, (int)V, (int)(vvalid > 0 ? vvalid : V), -100, 1, vstart, cur_stream()),
+        "ce_fused_local");
+  return stats;
 }
 
 std::vector<Tensor> ce_stats(Tensor logits, Tensor target, int64_t vstart, int64_t vvalid) {
@@ -760,6 +775,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("wgrad_grouped", &wgrad_grouped, arg("main_grads"), arg("dys"), arg("xs"),
         arg("biases") = std::vector<Tensor>{}, arg("overwrite") = std::vector<bool>{});
   m.def("ce_stats", &ce_stats);
+  m.def("ce_fused_local", &ce_fused_local);
   m.def("ce_bwd", &ce_bwd);
   m.def("ce_fused", &ce_fused);
   namespace py = pybind11;

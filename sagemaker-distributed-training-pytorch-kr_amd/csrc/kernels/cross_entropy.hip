@@ -135,18 +135,26 @@ __global__ __launch_bounds__(256) void ce_bwd_kernel(const T* __restrict__ logit
 // amdgpu_waves_per_eu(8) caps the kernel at 64 VGPRs (62 used at NV = 7, no scratch) so TWO blocks
 // share a CU and one block's reductions overlap the other's loads / stores: 3.31 -> 2.40 ms per step
 // at [65536, 50304] (with 68 VGPRs only one block fit; profiles/r4_lm_head_ce/).
-template <typename T, int NV>
+//
+// LOCAL (the vocab-parallel form, TP > 1: parallel/tensor_parallel.VocabParallelLMHeadCE): the
+// row is this rank's vocab slice [vstart, vstart + V); the kernel writes e = exp(x - m_local) in
+// place (0 on padding) and the row's local statistics (m_local, sum e, the target logit if the
+// target falls in this slice, else 0) to stats[0 / 1 / 2][row]. After the ranks combine their
+// statistics the row scale c = exp(m_local - M) / S turns e into the softmax, and the one-hot is
+// subtracted at ONE element per row — still a single pass over the logits.
+template <typename T, int NV, bool LOCAL>
 __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void ce_fused_kernel(T* __restrict__ logits,
                                                         const int64_t* __restrict__ target,
                                                         float* __restrict__ loss, int64_t rows,
-                                                        int V, int Vvalid, int64_t ignore_index) {
+                                                        int V, int Vvalid, int64_t ignore_index,
+                                                        int64_t vstart) {
   __shared__ float red[16];
   __shared__ float xt_s;
   const int64_t row = blockIdx.x;
   if (row >= rows) return;
   T* lr = logits + row * V;
-  const int64_t tg = target[row];
-  const bool ign = tg == ignore_index;
+  const int64_t tg = LOCAL ? target[row] - vstart : target[row];
+  const bool ign = LOCAL ? false : tg == ignore_index;
   if (threadIdx.x == 0) xt_s = (!ign && tg >= 0 && tg < Vvalid) ? to_f32(lr[tg]) : 0.f;
   const int nvec = V / 8;
   u16x8 raw[NV];
@@ -195,7 +203,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
   float S = 0.f;
 #pragma unroll
   for (int w = 0; w < 16; ++w) S += red[w];
-  const float inv = ign ? 0.f : 1.f / S;
+  const float inv = LOCAL ? 1.f : (ign ? 0.f : 1.f / S);
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
     const int i = threadIdx.x + k * 1024;
@@ -205,13 +213,21 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
       for (int j = 0; j < 8; ++j) {
         const int c = i * 8 + j;
         float p = c < Vvalid ? __expf(val(k, j) - M) * inv : 0.f;
-        if (!ign && c == tg) p -= 1.f;
+        if (!LOCAL && !ign && c == tg) p -= 1.f;
         o[j] = p;
       }
       store_vec8_nt<T>(lr + i * 8, o);
     }
   }
-  if (threadIdx.x == 0) loss[row] = ign ? 0.f : __logf(S) + M - xt_s;
+  if (threadIdx.x == 0) {
+    if constexpr (LOCAL) {   // stats = [3, rows]: local max, local sum, target logit (or 0)
+      loss[row] = M;
+      loss[rows + row] = S;
+      loss[2 * rows + row] = xt_s;
+    } else {
+      loss[row] = ign ? 0.f : __logf(S) + M - xt_s;
+    }
+  }
 }
 
 }  // namespace smdt
@@ -240,16 +256,24 @@ extern "C" hipError_t smdt_ce_bwd(int dtype, const void* logits, const int64_t* 
   return hipGetLastError();
 }
 
+// local != 0: the vocab-parallel form (``loss`` = stats [3, rows], target offset by vstart)
 extern "C" hipError_t smdt_ce_fused(int dtype, void* logits, const int64_t* target, float* loss,
                                     int64_t rows, int V, int Vvalid, int64_t ignore_index,
-                                    hipStream_t st) {
+                                    int local, int64_t vstart, hipStream_t st) {
   // 16-bit logits only; V % 8 == 0 and the row must fit the registers of one block
   if (dtype != 1 && dtype != 2) return hipErrorInvalidValue;
   if (V % 8 != 0 || V > 8 * 8192 || Vvalid < 1 || Vvalid > V) return hipErrorInvalidValue;
   if (rows <= 0) return hipSuccess;
   const int nv = (V / 8 + 1023) / 1024;
-#define SMDT_CE_FUSED(TT, NVV) \
-  hipLaunchKernelGGL((ce_fused_kernel<TT, NVV>), dim3(rows), dim3(1024), 0, st, (TT*)logits, target, loss, rows, V, Vvalid, ignore_index)
+#define SMDT_CE_FUSED(TT, NVV)                                                                                 \
+  do {                                                                                                         \
+    if (local)                                                                                                 \
+      hipLaunchKernelGGL((ce_fused_kernel<TT, NVV, true>), dim3(rows), dim3(1024), 0, st, (TT*)logits, target, \
+                         loss, rows, V, Vvalid, ignore_index, vstart);                                         \
+    else                                                                                                       \
+      hipLaunchKernelGGL((ce_fused_kernel<TT, NVV, false>), dim3(rows), dim3(1024), 0, st, (TT*)logits, target,\
+                         loss, rows, V, Vvalid, ignore_index, vstart);                                         \
+  } while (0)
   if (dtype == 1) {
     if (nv <= 4) SMDT_CE_FUSED(bf16, 4);
     else if (nv <= 7) SMDT_CE_FUSED(bf16, 7);

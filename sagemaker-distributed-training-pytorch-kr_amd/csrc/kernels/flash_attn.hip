@@ -384,31 +384,55 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void fwd_kernel(const E* __re
     if (!CAUSAL || kb <= qw + 31) {
       // S^T tiles (log2 domain, minus m): rows = keys (registers), column = this lane's query.
       f32x16 st[2];
+      auto scores = [&]() {
 #pragma unroll
-      for (int tt = 0; tt < 2; ++tt) {
-        st[tt] = mfma(fr.rowf(kt, 32 * tt, 0), qf[0], negm);  // starts at -m: no per-tile splat
+        for (int tt = 0; tt < 2; ++tt) {
+          st[tt] = mfma(fr.rowf(kt, 32 * tt, 0), qf[0], negm);  // starts at -m: no per-tile splat
 #pragma unroll
-        for (int kk = 1; kk < G::KS; ++kk) st[tt] = mfma(fr.rowf(kt, 32 * tt, kk), qf[kk], st[tt]);
-      }
-      if (CAUSAL && kb + kTile - 1 > qw) {  // diagonal tile for this wave: mask key > query
+          for (int kk = 1; kk < G::KS; ++kk) st[tt] = mfma(fr.rowf(kt, 32 * tt, kk), qf[kk], st[tt]);
+        }
+        if (CAUSAL && kb + kTile - 1 > qw) {  // diagonal tile for this wave: mask key > query
+#pragma unroll
+          for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+            for (int i = 0; i < 16; ++i)
+              if (kb + 32 * tt + acc_row(i, h) > my_q) st[tt][i] = -INFINITY;
+        }
+      };
+      float rs0 = 0.f, rs1 = 0.f;  // two chains: the denominator uses the un-dropped p
+      auto expsum = [&]() {
+        rs0 = rs1 = 0.f;
 #pragma unroll
         for (int tt = 0; tt < 2; ++tt)
 #pragma unroll
-          for (int i = 0; i < 16; ++i)
-            if (kb + 32 * tt + acc_row(i, h) > my_q) st[tt][i] = -INFINITY;
-      }
-      float tmax = st[0][0];
+          for (int i = 0; i < 16; i += 2) {
+            const float p0 = fexp2(st[tt][i]), p1 = fexp2(st[tt][i + 1]);
+            rs0 += p0;
+            rs1 += p1;
+            st[tt][i] = p0;
+            st[tt][i + 1] = p1;
+          }
+        return xhalf_sum(rs0 + rs1);
+      };
+      scores();
+      // Lazy reference max without a per-tile row max: p = exp2(S - m) is taken straight away and
+      // m only moves when the row's tile sum leaves [2^-64, 2^64] (p that large or small is still
+      // exact in fp32 / bf16, l and O have range to spare) — too large (or not finite), or, before
+      // anything was accumulated, so small that the row could underflow. Wave-uniform branch
+      // (ballot); rare: it recomputes the tile's scores (the K tile is still in LDS), takes the
+      // exact row max, rescales and redoes the exponentials. Saves the ~21 max instructions per
+      // tile of a per-tile max (the loop is VALU-issue-bound).
+      float rsum = expsum();
+      const bool bad = !(rsum <= 0x1p64f) || (l == 0.f && rsum < 0x1p-64f);
+      if (__builtin_amdgcn_ballot_w64(bad) != 0) {
+        scores();
+        float tmax = st[0][0];
 #pragma unroll
-      for (int tt = 0; tt < 2; ++tt)
+        for (int tt = 0; tt < 2; ++tt)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) tmax = fmaxf(tmax, st[tt][i]);
-      tmax = xhalf_max(tmax);  // this tile's row max relative to m
-      // Lazy rescale: m only moves when the tile max exceeds it by more than 8 (p <= 2^8 stays
-      // exact enough in fp32 / bf16), or — before anything was accumulated — when the scores sit
-      // far below it (so they cannot all underflow). Wave-uniform branch (ballot); rare.
-      const bool up = tmax > 8.f, down = l == 0.f && tmax < -64.f && tmax != -INFINITY;
-      if (__builtin_amdgcn_ballot_w64(up || down) != 0) {
-        const float d = (up || down) ? tmax : 0.f;
+          for (int i = 0; i < 16; ++i) tmax = fmaxf(tmax, st[tt][i]);
+        tmax = xhalf_max(tmax);
+        const float d = bad ? tmax : 0.f;
         const float alpha = fexp2(-d);
         l *= alpha;
 #pragma unroll
@@ -417,18 +441,8 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void fwd_kernel(const E* __re
         for (int tt = 0; tt < 2; ++tt) st[tt] -= d;
         m += d;
         negm = splat16(-m);
+        rsum = expsum();
       }
-      float rs0 = 0.f, rs1 = 0.f;  // two chains: the denominator uses the un-dropped p
-#pragma unroll
-      for (int tt = 0; tt < 2; ++tt)
-#pragma unroll
-        for (int i = 0; i < 16; i += 2) {
-          const float p0 = fexp2(st[tt][i]), p1 = fexp2(st[tt][i + 1]);
-          rs0 += p0;
-          rs1 += p1;
-          st[tt][i] = p0;
-          st[tt][i + 1] = p1;
-        }
       // dropout: packed-pair masks of the 8 key-pair slots of each 32-key sub-tile (slot m =
       // registers 2m, 2m + 1); dropped entries leave P.V only (l sums the un-dropped p) and the
       // 1/(1-p) scale is applied in the epilogue
@@ -443,7 +457,7 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void fwd_kernel(const E* __re
             dm[tt][2 * u + 1] = mask_odd_slot(t);
           }
       }
-      l += xhalf_sum(rs0 + rs1);
+      l += rsum;
       // O^T[d, q] += V^T[d, keys] . P^T[keys, q]
 #pragma unroll
       for (int tt = 0; tt < 2; ++tt) {
@@ -516,6 +530,9 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void fwd_kernel(const E* __re
 #endif
 #ifndef SMDT_FA_DKDV_OCC
 #define SMDT_FA_DKDV_OCC 2
+#endif
+#ifndef SMDT_FA_DKDV_ROLLED
+#define SMDT_FA_DKDV_ROLLED 0
 #endif
 template <int D, bool CAUSAL, bool DROP, class E>
 __global__ __launch_bounds__(256, D == 64 ? SMDT_FA_DKDV_OCC : 1) void bwd_dkdv_kernel(
@@ -722,32 +739,24 @@ __global__ __launch_bounds__(256, D == 64 ? SMDT_FA_DKDV_OCC : 1) void bwd_dkdv_
           dk[dt] = mfma(fr.trf(q_l, 32 * qs2, st, dt), db[st], dk[dt]);
         }
     };
-    if (!CAUSAL || qb >= kw + 32) {
-      // the two 32-query halves one after the other: 48 fewer live VGPRs than straight-line code
-      // (which spilled at 256 VGPRs once the row constants entered as MFMA operands); the
-      // partner wave on the SIMD supplies the overlap of softmax VALU and MFMAs
+    // ONE code path for every item: the two 32-query halves one after the other (48 fewer live
+    // VGPRs than straight-line code, which spilled at 256 VGPRs once the row constants entered as
+    // MFMA operands; the partner wave on the SIMD supplies the overlap of softmax VALU and MFMAs).
+    // Causal items only add wave-uniform tests: a half whose queries all precede this wave's keys
+    // is skipped, the diagonal half masks key > query. (A separate straight path for the
+    // non-diagonal items made the compiler keep dK / dV in two register sets and copy all 64
+    // accumulator VGPRs, 64 v_mov_b64, on every item's loop back-edge.)
 #pragma unroll
-      for (int qs2 = 0; qs2 < 2; ++qs2) {
-        f32x16 sa, pa;
-        v8_t<E> pb[2], db[2];
-        sd_init(qs2, sa, pa);
-        sd_mma(qs2, sa, pa);
-        softmax_ds(qs2, sa, pa, pb, db);
-        acc_mma(qs2, pb, db);
-      }
-    } else {
-#pragma unroll
-      for (int qs2 = 0; qs2 < 2; ++qs2) {
-        const int qsub = qb + 32 * qs2;
-        if (qsub + 31 < kw) continue;  // all queries precede all of this wave's keys
-        f32x16 sa, pa;
-        v8_t<E> pb[2], db[2];
-        sd_init(qs2, sa, pa);
-        sd_mma(qs2, sa, pa);
-        if (qsub == kw) diag_mask(sa);      // the diagonal block: key > query is masked
-        softmax_ds(qs2, sa, pa, pb, db);
-        acc_mma(qs2, pb, db);
-      }
+    for (int qs2 = 0; qs2 < 2; ++qs2) {
+      const int qsub = qb + 32 * qs2;
+      if (CAUSAL && qsub + 31 < kw) continue;  // all queries precede all of this wave's keys
+      f32x16 sa, pa;
+      v8_t<E> pb[2], db[2];
+      sd_init(qs2, sa, pa);
+      sd_mma(qs2, sa, pa);
+      if (CAUSAL && qsub == kw) diag_mask(sa);  // the diagonal block: key > query is masked
+      softmax_ds(qs2, sa, pa, pb, db);
+      acc_mma(qs2, pb, db);
     }
     if (++cq == ntiles) {
       cq = 0;
@@ -755,6 +764,20 @@ __global__ __launch_bounds__(256, D == 64 ? SMDT_FA_DKDV_OCC : 1) void bwd_dkdv_
     }
     wait_next();
   };
+#if SMDT_FA_DKDV_ROLLED
+  // One work item per iteration, the stage slots rotating as wave-uniform counters (their LDS
+  // bases are selected per item, SALU): the unrolled kBuf-item body with a conditional call per
+  // item made the compiler copy the dK / dV accumulators (32 v_mov_b64) on the joins.
+  {
+    int cur = 0, pre = kBuf - 1;
+#pragma nounroll
+    for (int it = 0; it < total; ++it) {
+      item(cur, pre);
+      cur = cur + 1 == kBuf ? 0 : cur + 1;
+      pre = pre + 1 == kBuf ? 0 : pre + 1;
+    }
+  }
+#else
   if constexpr (kBuf == 3) {
     for (int it = 0; it < total; it += 3) {
       item(0, 2);
@@ -767,6 +790,7 @@ __global__ __launch_bounds__(256, D == 64 ? SMDT_FA_DKDV_OCC : 1) void bwd_dkdv_
       if (it + 1 < total) item(1, 0);
     }
   }
+#endif
   wait_vm<0>();  // drain the trailing re-reads before the workgroup's LDS is released
 
 
@@ -924,8 +948,17 @@ __global__ __launch_bounds__(256, D == 64 ? SMDT_FA_DQ_OCC : 1) void bwd_dq_kern
         dpt = mfma(fr.rowf(vt, 32 * tt, kk), dof[kk], dpt);
       }
     };
-    // dS^T into dpt (P' = exp2(S'); dropout: kept dP - delta', dropped -delta'; causal diagonal)
-    auto soft = [&](int tt, const f32x16& st, f32x16& dpt, bool diag) {
+    // causal diagonal sub-tile: key > query gets S' = -1e30 (exp2 -> 0), ONE uniform block before
+    // the softmax. (Testing it per element pair inside the softmax made the compiler branch on the
+    // flag around every pair: 16 basic blocks per sub-tile, no MFMA / VALU interleave across them.)
+    auto diag_mask = [&](int tt, f32x16& st) {
+      const int ksub = kb + 32 * tt;
+#pragma unroll
+      for (int i = 0; i < 16; ++i)
+        if (ksub + acc_row(i, h) > my_q) st[i] = -1e30f;
+    };
+    // dS^T into dpt (P' = exp2(S'); dropout: kept dP - delta', dropped -delta')
+    auto soft = [&](int tt, const f32x16& st, f32x16& dpt) {
       const int ksub = kb + 32 * tt;
       uint32_t tb[4];  // keep bits of slots 2u (bits 7 / 23) and 2u + 1 (bits 15 / 31)
       if constexpr (DROP) {
@@ -934,11 +967,7 @@ __global__ __launch_bounds__(256, D == 64 ? SMDT_FA_DQ_OCC : 1) void bwd_dq_kern
       }
 #pragma unroll
       for (int i = 0; i < 16; i += 2) {
-        float p0 = fexp2(st[i]), p1 = fexp2(st[i + 1]);  // with dropout: p / (1 - p_drop)
-        if (diag) {
-          if (ksub + acc_row(i, h) > my_q) p0 = 0.f;
-          if (ksub + acc_row(i + 1, h) > my_q) p1 = 0.f;
-        }
+        const float p0 = fexp2(st[i]), p1 = fexp2(st[i + 1]);  // with dropout: p / (1 - p_drop)
         float d0 = dpt[i], d1 = dpt[i + 1];
         if constexpr (DROP) {
           const uint32_t tw = tb[i >> 2];
@@ -970,7 +999,8 @@ __global__ __launch_bounds__(256, D == 64 ? SMDT_FA_DQ_OCC : 1) void bwd_dq_kern
       if (CAUSAL && ksub > qw + 31) continue;
       f32x16 st, dpt;
       sd(tt, st, dpt);
-      soft(tt, st, dpt, CAUSAL && ksub + 31 > qw);
+      if (CAUSAL && ksub + 31 > qw) diag_mask(tt, st);
+      soft(tt, st, dpt);
       acc(tt, dpt);
     }
     wait_vm<(kBuf - 2) * kPer>();  // tile t + 1 landed (t + 2 may still be in flight)

@@ -81,7 +81,7 @@ hipError_t smdt_ce_bwd(int dtype, const void* logits, const int64_t* target, con
                        const float* gsum, const float* dloss, void* dlogits, int64_t rows, int V,
                        int Vvalid, int64_t vstart, int64_t ignore_index, hipStream_t st);
 hipError_t smdt_ce_fused(int dtype, void* logits, const int64_t* target, float* loss, int64_t rows,
-                         int V, int Vvalid, int64_t ignore_index, hipStream_t st);
+                         int V, int Vvalid, int64_t ignore_index, int local, int64_t vstart, hipStream_t st);
 
 // augment.hip: per-sample depthwise filter (KS in {3, 5, 7}) and 3 x 3 median, fp32 NCHW
 hipError_t smdt_aug_depthwise(const float* x, const float* k, float* y, int N, int C, int H, int W, int ks,

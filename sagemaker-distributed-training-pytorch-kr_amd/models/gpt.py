@@ -184,6 +184,16 @@ class GPTModel(nn.Module):
                 vvalid = vs if 0 < vs < w.shape[0] else 0
                 loss = tp.LMHeadCrossEntropy.apply(out, w, labels.transpose(0, 1), -100, vvalid)
                 return loss.transpose(0, 1).contiguous()             # [b, s]
+            if self.parallel_output and tp.vp_lm_head_ce_ok(out, w, st.tp):
+                # vocab-parallel LM head + CE as one op: one pass over this rank's logit slice
+                vl = w.shape[0]
+                vstart = st.tp_rank * vl
+                vs = int(self.loss_vocab_size or 0)
+                vvalid = min(max(vs - vstart, 0), vl) if vs > 0 else 0
+                assert vs <= 0 or vvalid > 0, "a vocab shard holds only padding; use a smaller padding multiple"
+                loss = tp.VocabParallelLMHeadCE.apply(out, w, labels.transpose(0, 1), -100, vstart,
+                                                      0 if vvalid == vl else vvalid, bool(self.sp))
+                return loss.transpose(0, 1).contiguous()             # [b, s]
         logits = self.lm_logits(out)
         if labels is None:
             return logits.transpose(0, 1).contiguous()

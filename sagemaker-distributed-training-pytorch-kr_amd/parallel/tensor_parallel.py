@@ -754,6 +754,151 @@ class LMHeadCrossEntropy(torch.autograd.Function):
         return gi, dw, None, None, None
 
 
+def ce_local_pass(logits2d, target, vstart: int, vvalid: int):
+    """One pass over this rank's vocab slice of the logits: overwrite them with e = exp(x - m_local)
+    (0 on padding columns >= vvalid) and return the row statistics [3, rows] fp32 = (m_local,
+    sum e, target logit if the target is in [vstart, vstart + vvalid) else 0). HIP kernel
+    (cross_entropy.hip ce_fused_kernel<LOCAL>) on the GPU, the same math in PyTorch on the CPU."""
+    if logits2d.is_cuda:
+        return _ext_mod().ce_fused_local(logits2d, target, int(vstart), int(vvalid))
+    V = logits2d.shape[-1]
+    nv = vvalid or V
+    z = logits2d.float()[:, :nv]
+    m = z.max(-1).values
+    e = torch.exp(z - m[:, None])
+    loc = target - vstart
+    inr = (loc >= 0) & (loc < nv)
+    t = torch.where(inr, z.gather(1, loc.clamp(0, nv - 1)[:, None])[:, 0], torch.zeros_like(m))
+    out = torch.zeros(logits2d.shape, dtype=torch.float32, device=logits2d.device)
+    out[:, :nv] = e
+    logits2d.copy_(out.to(logits2d.dtype))
+    return torch.stack([m, e.sum(-1), t])
+
+
+def combine_ce_stats(allst, st, t, ignore_index):
+    """Per-row loss and softmax scale c from every rank's ``ce_local_pass`` statistics
+    ``allst`` [ranks, 3, rows] (this rank's: ``st``): M = max m_r, S = sum s_r exp(m_r - M),
+    loss = log S + M - x_t, c = exp(m_mine - M) / S (0 for ignored rows)."""
+    M = allst[:, 0].max(0).values
+    S = (allst[:, 1] * torch.exp(allst[:, 0] - M)).sum(0)
+    ign = t == ignore_index
+    loss = torch.where(ign, torch.zeros_like(S), torch.log(S) + M - allst[:, 2].sum(0))
+    c = torch.where(ign, torch.zeros_like(S), torch.exp(st[0] - M) / S)
+    return loss, c
+
+
+def subtract_onehot_(l2, t, c, vstart, vvalid, ignore_index):
+    """The one-hot at ONE element per row whose target lies in this slice: e[t] -= 1 / c, so that
+    c e = softmax - onehot. No host sync (every row writes its clamped position; rows without an
+    in-slice target write their own value back)."""
+    V = l2.shape[-1]
+    loc = t - vstart
+    inr = (loc >= 0) & (loc < (vvalid or V)) & (t != ignore_index)
+    lin = torch.arange(l2.shape[0], device=l2.device) * V + loc.clamp(0, V - 1)
+    flat = l2.view(-1)
+    cur = flat[lin].float()
+    flat[lin] = torch.where(inr, cur - 1.0 / c, cur).to(flat.dtype)
+
+
+class VocabParallelLMHeadCE(torch.autograd.Function):
+    """LM head + CE for a vocabulary split over the TP group (TP > 1), the LM-head GEMM and the loss
+    as ONE op with a single pass over this rank's [tokens, V / tp] logits (the
+    TP = 1 form is ``LMHeadCrossEntropy``). Same math as Megatron's parallel_lm_logits +
+    vocab-parallel CE (/root/reference/3_training_megatron-lm/pretrain_gpt.py:51-57;
+    megatron/arguments.py:992-994):
+
+    * logits = X W_r^T — with sequence parallelism through the ring all-gather collective-matmul
+      (``_ColumnSPLinear``'s forward);
+    * ``ce_local_pass`` overwrites them with e = exp(x - m_r) and returns (m_r, s_r, x_t) per row;
+    * ONE all-gather of those [3, tokens] statistics replaces the three all-reduces (MAX, SUM,
+      SUM): M = max m_r, S = sum s_r exp(m_r - M), loss = log S + M - x_t;
+    * with the row scale c = exp(m_r - M) / S, softmax = c e, so the one-hot is subtracted at ONE
+      element per row: e[t] -= 1 / c (no second pass);
+    * backward: D = c e - onehot never exists — the per-row c dloss goes on the [tokens, hidden]
+      side: dX = diag(c dl) (E W) (reduce-scattered along the sequence by the ring, or all-reduced
+      without SP) and dW = E^T diag(c dl) X.
+
+    Against logits -> separate stats kernel -> 3 all-reduces -> backward kernel over the logits,
+    this drops one full read of the logits per micro-batch on the last pipeline stage.
+    bf16 only (the hidden-side scaling, see ``lm_head_ce_ok``)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, target, ignore_index, vstart, vvalid, sp):
+        group = _tp_group()
+        ws = dist.get_world_size(group)
+        x = x.contiguous()
+        if sp:
+            n = x.shape[0]
+            logits = x.new_empty((n * ws,) + tuple(x.shape[1:-1]) + (weight.shape[0],))
+            total = ag_ring(x, group, lambda c, ch: _mm_into(logits[c * n:(c + 1) * n], ch, weight))
+        else:
+            n = x.shape[0] // ws
+            total = x
+            logits = linear_rows(x, weight)
+        V = logits.shape[-1]
+        l2 = logits.view(-1, V)
+        t = target.contiguous().view(-1)
+        st = ce_local_pass(l2, t, vstart, vvalid).contiguous()
+        allst = st.new_empty((ws,) + tuple(st.shape))
+        if ws > 1:
+            from ..comm import stats as _cs
+            with _cs.blocking("all_gather", group, allst.numel() * allst.element_size()):
+                dist.all_gather_into_tensor(allst.view(-1), st.view(-1), group=group)
+        else:
+            allst[0].copy_(st)
+        loss, c = combine_ce_stats(allst, st, t, ignore_index)
+        subtract_onehot_(l2, t, c, vstart, vvalid, ignore_index)
+        ctx.save_for_backward(total, weight, logits, c)
+        ctx.sp, ctx.n = sp, n
+        return loss.view(target.shape)
+
+    @staticmethod
+    def backward(ctx, dloss):
+        total, weight, e, c = ctx.saved_tensors
+        group = _tp_group()
+        n = ctx.n
+        r = dloss.contiguous().view(-1).float() * c          # per-row scale of E = c dl
+        r3 = r.view(e.shape[:-1] + (1,))
+        wt = _dgrad_weight_t(weight)
+        res = {}
+
+        def wgrad():
+            H = total.shape[-1]
+            hs = torch.mul(total.reshape(-1, H), r.view(-1, 1)).to(total.dtype)
+            res["dw"] = _wgrad(weight, e.view(-1, e.shape[-1]), hs)
+            _flush_wgrad()
+
+        def part(ci):
+            g = dgrad(e[ci * n:(ci + 1) * n], weight, wt)
+            g.mul_(r3[ci * n:(ci + 1) * n])
+            return g
+        if ctx.sp:
+            gi = rs_ring(part, group, wgrad)
+        else:
+            gi = dgrad(e, weight, wt)
+            gi.mul_(r3)
+            h = dist.all_reduce(gi, group=group, async_op=True) if dist.get_world_size(group) > 1 else None
+            wgrad()
+            if h is not None:
+                h.wait()
+        if "dw" not in res:
+            wgrad()
+        return gi, res["dw"], None, None, None, None, None
+
+
+def vp_lm_head_ce_ok(h, weight, tp: int) -> bool:
+    """Whether ``VocabParallelLMHeadCE`` applies: TP > 1, HIP kernels on and bf16 operands (or the
+    CPU reference with SMDT_LM_HEAD_CE_CPU=1, for the Gloo equivalence tests), a vocab slice whose
+    row fits one block's registers (V / tp % 8 == 0, <= 65536). SMDT_LM_HEAD_CE=0 disables."""
+    from ..ops import _ext
+    if not (_LM_HEAD_CE and tp > 1 and weight.shape[0] % 8 == 0 and weight.shape[0] <= 65536
+            and weight.dtype == h.dtype):
+        return False
+    if h.is_cuda:
+        return _ext.use_kernels(h) and h.dtype == torch.bfloat16
+    return os.environ.get("SMDT_LM_HEAD_CE_CPU", "0") == "1"
+
+
 def _ext_mod():
     from ..ops import _ext
     return _ext.ext()

@@ -143,3 +143,40 @@ def softmax_ref(x, dy, scale, causal, mask=None):
     y = torch.softmax(s, -1)
     y.backward(dy.float())
     return y.detach(), xr.grad
+
+
+def vp_lmce_two_shards(h, w, tgt, dl, vocab=0, ranks=2, local_pass=None):
+    """The vocab-parallel LM-head CE math of ``VocabParallelLMHeadCE`` run for ``ranks`` vocab
+    shards in one process: per shard the logits GEMM and ``local_pass`` (the HIP kernel or its CPU
+    reference), the statistics combined, the one-hot subtracted at one element per row, and the
+    backward products with the per-row scale c dl on the hidden side. Returns (loss, dh, dW,
+    16-bit logits of all shards) for comparison with ``lmce_ref`` on the same logits."""
+    from smdt_amd.parallel import tensor_parallel as tp
+    local_pass = local_pass or tp.ce_local_pass
+    H = h.shape[-1]
+    V = w.shape[0]
+    vl = V // ranks
+    x = h.reshape(-1, H)
+    t = tgt.reshape(-1)
+    shards, stats, lgs = [], [], []
+    for r in range(ranks):
+        ws_ = w[r * vl:(r + 1) * vl]
+        lg = x @ ws_.t() if not x.is_cuda else tp.linear_rows(x, ws_)
+        lg = lg.to(h.dtype)
+        lgs.append(lg.clone())
+        vv = min(max(vocab - r * vl, 0), vl) if vocab else 0
+        vv = 0 if vv == vl else vv
+        st = local_pass(lg, t, r * vl, vv)
+        shards.append((lg, vv))
+        stats.append(st)
+    allst = torch.stack(stats)
+    d = dl.reshape(-1).float()
+    dh = torch.zeros(x.shape, dtype=torch.float32, device=x.device)
+    dws = []
+    for r, (e, vv) in enumerate(shards):
+        loss, c = tp.combine_ce_stats(allst, stats[r], t, -100)
+        tp.subtract_onehot_(e, t, c, r * vl, vv, -100)
+        rr = (d * c)[:, None]
+        dh += (e.float() @ w[r * vl:(r + 1) * vl].float()) * rr
+        dws.append(e.float().t() @ (x.float() * rr).to(h.dtype).float())
+    return loss.view(tgt.shape), dh.view(h.shape), torch.cat(dws), torch.cat(lgs, -1)

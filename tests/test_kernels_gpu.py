@@ -304,6 +304,29 @@ def test_lm_head_cross_entropy(V, vocab):
         assert w.grad[vocab:].abs().max().item() == 0
 
 
+@pytest.mark.parametrize("V,vocab,ranks", [(50304, 50257, 2), (50432, 50257, 2), (4096, 0, 4)])
+def test_vocab_parallel_lm_head_ce_two_shards(V, vocab, ranks):
+    """VocabParallelLMHeadCE's math for ``ranks`` vocab shards in one process on the HIP kernel
+    (ce_fused_kernel<LOCAL>: exp(x - m_local) in place + row statistics): combined loss, dh and dW
+    against fp32 math on the same 16-bit logits, peaked logits, row-relative criterion (its
+    mutation check: tests/test_numerics_sensitivity.py, vocab-parallel CPU twin included)."""
+    from smdt_amd.parallel import tensor_parallel as tp
+    h, w, tgt, dl = N.lmce_case(64, 3, 256, V, vocab, device=DEV)
+    loss, dh, dw, lg = N.vp_lmce_two_shards(h, w, tgt, dl, vocab, ranks)
+    rl, rdh, rdw = N.lmce_ref(h, w, lg, tgt, dl, vocab)
+    torch.testing.assert_close(loss, rl, atol=5e-3, rtol=1e-3)
+    N.assert_rows_close(dh, rdh, N.CE_TOL, "dh")
+    N.assert_rows_close(dw, rdw, N.CE_TOL, "dW")
+    # the kernel against its CPU reference on one shard (statistics and the in-place e)
+    x = h.reshape(-1, h.shape[-1])
+    lg0 = tp.linear_rows(x, w[: V // ranks])
+    cpu = lg0.cpu().clone()
+    st = tp.ce_local_pass(lg0, tgt.reshape(-1), 0, 0)
+    stc = tp.ce_local_pass(cpu, tgt.reshape(-1).cpu(), 0, 0)
+    torch.testing.assert_close(st.cpu(), stc, atol=1e-3, rtol=1e-3)
+    torch.testing.assert_close(lg0.float().cpu(), cpu.float(), atol=1e-2, rtol=1e-2)
+
+
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("D", [64, 128])
 @pytest.mark.parametrize("causal", [True, False])

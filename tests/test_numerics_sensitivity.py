@@ -69,3 +69,20 @@ def test_masked_softmax_criterion_rejects_mutations():
     unmasked = torch.softmax(x.float() * 0.125, -1)
     assert row_rel_err(unmasked, y) > 2 * SOFTMAX_TOL
     assert row_rel_err(1.1 * dx, dx, row_floor=softmax_grad_floor(y, dy, 0.125)) > 2 * SOFTMAX_TOL
+
+
+@pytest.mark.parametrize("V,vocab", [(50304, 50257), (1024, 0)])
+def test_vocab_parallel_lm_head_ce_math_cpu(V, vocab):
+    """CPU twin of test_kernels_gpu.test_vocab_parallel_lm_head_ce_two_shards: the two-shard math
+    (local pass, combined statistics, one-hot at one element, hidden-side scale) equals the fp32
+    reference on the same 16-bit logits within the criterion, and the same math with the
+    softmax term mutated would not."""
+    h, w, tgt, dl = lmce_case(s=32, b=3, V=V, vocab=vocab)
+    from _numerics import vp_lmce_two_shards
+    loss, dh, dw, lg = vp_lmce_two_shards(h, w, tgt, dl, vocab)
+    rl, rdh, rdw = lmce_ref(h, w, lg, tgt, dl, vocab)
+    assert (loss - rl).abs().max().item() < 1e-3
+    assert row_rel_err(dh, rdh) <= CE_TOL / 3, row_rel_err(dh, rdh)
+    assert row_rel_err(dw, rdw) <= CE_TOL / 3, row_rel_err(dw, rdw)
+    _, bdh, bdw = lmce_ref(h, w, lg, tgt, dl, vocab, soft=1.1)
+    assert row_rel_err(bdh, rdh) > 2 * CE_TOL and row_rel_err(bdw, rdw) > 2 * CE_TOL

@@ -434,3 +434,32 @@ def test_deterministic_reduce_is_rank_order_fold(zero):
     for got, ranges in outs:
         for s, e in ranges:
             assert _t.equal(got[s:e], want[s:e])
+
+
+@pytest.mark.parametrize("tp,sp,pp", [(2, True, 1), (2, False, 1), (4, True, 1), (2, True, 2)])
+def test_vocab_parallel_fused_lm_head_ce_matches_single_rank(tp, sp, pp, monkeypatch):
+    """The vocab-parallel LM head + CE as one op (tensor_parallel.VocabParallelLMHeadCE: one pass
+    over the logit slice, one all-gather of the [3, tokens] row statistics, the one-hot subtracted
+    at one element per row, the row scale applied on the hidden side in the backward) on its CPU
+    reference path: losses and every gradient equal single-rank training, with and without SP,
+    at TP 4 and at the tp2 pp2 + SP layout of the N = 8 BASELINE point."""
+    monkeypatch.setenv("SMDT_LM_HEAD_CE_CPU", "1")
+    ref_loss, ref = W.gpt_reference()
+    outs = run_workers(W.gpt_tp_worker, tp * pp, tp, pp, sp)
+    for loss, grads, meta in outs:
+        if pp == 1:
+            _close(loss, ref_loss)
+        _check_tp_grads(ref, grads, meta, tp)
+    if pp > 1:
+        last = [o for o in outs if o[2]["pp_rank"] == 1][0]
+        torch.testing.assert_close(last[0].view(-1), ref_loss.view(-1), atol=2e-4, rtol=2e-4)
+
+
+def test_vocab_parallel_fused_ce_path_is_taken(monkeypatch):
+    """The gate: off for fp32 CPU tensors unless SMDT_LM_HEAD_CE_CPU=1, never at TP 1."""
+    from smdt_amd.parallel import tensor_parallel as tp
+    h = torch.zeros(4, 2, 16)
+    w = torch.zeros(64, 16)
+    assert not tp.vp_lm_head_ce_ok(h, w, 2)
+    monkeypatch.setenv("SMDT_LM_HEAD_CE_CPU", "1")
+    assert tp.vp_lm_head_ce_ok(h, w, 2) and not tp.vp_lm_head_ce_ok(h, w, 1)
