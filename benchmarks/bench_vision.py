@@ -55,10 +55,19 @@ def main():
                    help="augment the next batches on a side stream in a background thread "
                         "(data/image_folder.AugmentPrefetcher); 0: in line with the step")
     p.add_argument("--graph", type=int, default=1,
-                   help="1 GPU (default on): capture forward + backward + Adam of one step in a HIP graph after the "
-                        "warm-up and replay it (the step's ~1.5-3.7 k kernel launches leave the device "
-                        "idle 5-42 ms per step in eager mode, profiles/r4_vision/); the augmented batch "
-                        "is copied into the graph's static input")
+                   help="(default on, any world size) capture forward + backward (DDP bucket reductions "
+                        "included: RCCL / loopback collectives are captured, the xGMI engine sits out "
+                        "the capture) + Adam of one step in a HIP graph after the warm-up and replay it "
+                        "(the step's ~1.5-3.7 k kernel launches leave the device idle 5-42 ms per step "
+                        "in eager mode, profiles/r4_vision/); the augmented batch is copied into the "
+                        "graph's static input")
+    p.add_argument("--optim", default="smdt", choices=["smdt", "torch"],
+                   help="smdt: the hand-written fused Adam (optim.hip, device-side step count: "
+                        "capturable) over the DDP's flat buffers; torch: torch.optim.Adam(fused)")
+    p.add_argument("--emulate-dp", type=int, default=0,
+                   help="one process = rank 0 of an N-GPU DDP job (loopback DP group, comm/loopback.py): "
+                        "the rank's exact per-step work with the collectives as local stand-ins; the JSON "
+                        "line then reports the rank's ms/step, not a job throughput")
     p.add_argument("--miopen-prewarm", type=int, default=1,
                    help="before timing, run 13 steps in a child process so MIOpen's find database and "
                         "kernel cache exist: on a fresh box the first process of a model ran 418-540 ms "
@@ -79,7 +88,14 @@ def main():
         r = subprocess.run(cmd, env=env, capture_output=True, text=True)
         print(f"[bench_vision] MIOpen prewarm process: rc {r.returncode}, {time.perf_counter() - t:.1f}s",
               file=sys.stderr, flush=True)
-    rank, local, world, _ = init_distributed("nccl")
+    if a.emulate_dp > 1:
+        from smdt_amd.parallel import state as ps
+        if torch.cuda.is_available():
+            torch.cuda.set_device(0)
+        ps.initialize_emulated_tensor_parallel(1, a.emulate_dp)
+        rank, world = 0, 1
+    else:
+        rank, local, world, _ = init_distributed("nccl")
     dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
     torch.manual_seed(0)
     torch.backends.cudnn.benchmark = True
@@ -91,8 +107,14 @@ def main():
     if a.ddp == "smdt":
         model = DDP(model, torch_compat=True, bucket_size=bucket)
     crit = nn.CrossEntropyLoss()
-    use_graph = bool(a.graph) and dev.type == "cuda" and world == 1
-    opt = torch.optim.Adam(model.parameters(), lr=1e-4, fused=dev.type == "cuda", capturable=use_graph)
+    use_graph = bool(a.graph) and dev.type == "cuda"
+    if a.optim == "smdt" and a.ddp == "smdt":
+        from smdt_amd.optim.optimizer import MixedPrecisionAdam
+        # torch.optim.Adam's defaults (L2 weight decay 0), the reference's optimizer (pytorch_oxford_ddp.py:258)
+        opt = MixedPrecisionAdam(model, lr=1e-4, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, adamw=False,
+                                 capturable=use_graph)
+    else:
+        opt = torch.optim.Adam(model.parameters(), lr=1e-4, fused=dev.type == "cuda", capturable=use_graph)
     aug = GpuAugment((a.size, a.size), train=True, channels_last=mf == torch.channels_last)
     gen = torch.Generator(device=dev)
     gen.manual_seed(rank)
@@ -181,18 +203,26 @@ def main():
     ips = a.batch * world * a.steps / el
     if rank == 0:
         ref = REF_IMG_S_PER_GPU.get(a.model)
+        ms = round(1000 * el / a.steps, 3)
+        if a.emulate_dp > 1:   # one rank of a larger job: its time, never a job throughput
+            head = {"metric": "emulated rank ms/step", "value": ms, "unit": "ms", "n_gpus": 1,
+                    "emulated_dp": a.emulate_dp, "rank_images_per_s": round(ips, 1)}
+        else:
+            head = {"metric": "Oxford-Pet DDP train images/sec (whole job)", "value": round(ips, 1),
+                    "unit": "images/s", "n_gpus": world}
         print(json.dumps({
-            "metric": "Oxford-Pet DDP train images/sec (whole job)", "value": round(ips, 1), "unit": "images/s",
-            "n_gpus": world, "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(1000 * el / a.steps, 3),
+            **head, "steps": a.steps, "warmup": a.warmup, "ms_per_step": ms,
             "dtype": a.dtype, "data": "synthetic uint8 images + GPU augmentation; random-init weights",
             "config": {"model": a.model, "image": a.size, "batch_per_gpu": a.batch,
-                       "channels_last": bool(a.channels_last), "parallelism": f"dp{world}",
+                       "channels_last": bool(a.channels_last),
+                       "parallelism": f"dp{a.emulate_dp} (one emulated rank)" if a.emulate_dp > 1 else f"dp{world}",
+                       "optimizer": "smdt fused Adam (optim.hip)" if a.optim == "smdt" and a.ddp == "smdt" else "torch Adam (fused)",
                        "augment": "prefetched (side stream)" if a.prefetch else "in line",
                        "hip_graph": graph_note,
                        "backend": dist.get_backend() if dist.is_initialized() else None,
                        "ddp_bucket": {"elements": model.bucket_size, "count": len(model.buckets),
                                       "MB": round(model.bucket_size * 4 / 2 ** 20, 2)} if a.ddp == "smdt" else None},
-            "vs_reference_per_gpu": round(ips / world / ref, 2) if ref else None,
+            "vs_reference_per_gpu": round(ips / world / ref, 2) if (ref and a.emulate_dp <= 1) else None,
             "final_loss": float(loss.item())}), flush=True)
     if dist.is_initialized():
         dist.destroy_process_group()

@@ -37,6 +37,8 @@ import torch.optim as optim  # noqa: E402
 import util  # noqa: E402
 from smdt_amd.comm import init_distributed  # noqa: E402
 from smdt_amd.data.image_folder import AugmentPrefetcher, GpuAugment, ImageFolderDataset  # noqa: E402
+from smdt_amd.optim.optimizer import MixedPrecisionAdam  # noqa: E402
+from smdt_amd.train.graphs import CapturedStep  # noqa: E402
 from smdt_amd.parallel.distributed import DistributedDataParallel as DDP  # noqa: E402
 
 logger = logging.getLogger(__name__)
@@ -69,6 +71,9 @@ def args_fn(argv=None):
     parser.add_argument("--data-dir", type=str, default=None)
     parser.add_argument("--model-dir", type=str, default=None)
     parser.add_argument("--max-steps", type=int, default=0, help="stop each epoch after N steps (smoke tests)")
+    parser.add_argument("--graph", type=str2bool, default=False,
+                        help="capture the training step (forward, backward with the DDP bucket reductions, the "
+                             "hand-written fused Adam) in a HIP graph and replay it (smdt_amd/train/graphs.py)")
     return parser.parse_args(argv)
 
 
@@ -122,7 +127,12 @@ def train(args):
     model = model.to(dev, memory_format=mf)
     model = DDP(model, torch_compat=True)
     criterion = nn.CrossEntropyLoss().to(dev)
-    optimizer = optim.Adam(model.parameters(), lr=args.lr)
+    use_graph = bool(args.graph) and dev.type == "cuda"
+    if use_graph:   # the same Adam (torch.optim defaults), device-side step count: capturable
+        optimizer = MixedPrecisionAdam(model, lr=args.lr, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0,
+                                       adamw=False, capturable=True)
+    else:
+        optimizer = optim.Adam(model.parameters(), lr=args.lr)
     train_loader, train_sampler = _get_train_data_loader(args)
     logger.info("Processes {}/{} ({:.0f}%) of train data".format(
         len(train_loader.sampler), len(train_loader.dataset),
@@ -138,6 +148,17 @@ def train(args):
     gen = torch.Generator(device=dev)
     gen.manual_seed(args.seed + args.rank)
 
+    def train_step(data, target):
+        optimizer.zero_grad()
+        with torch.autocast(device_type=dev.type, dtype=torch.bfloat16, enabled=use_bf16,
+                            cache_enabled=not use_graph):
+            output = model(data)
+            loss = criterion(output.float(), target)
+        loss.backward()
+        optimizer.step()
+        return output, loss
+    step = CapturedStep(train_step, enabled=use_graph)
+
     for epoch in range(1, args.num_epochs + 1):
         batch_time = util.AverageMeter("Time", ":6.3f")
         losses = util.AverageMeter("Loss", ":.4e")
@@ -151,12 +172,7 @@ def train(args):
         for batch_idx, (data, target) in enumerate(AugmentPrefetcher(train_loader, aug_train, dev, gen)):
             if args.max_steps and batch_idx >= args.max_steps:
                 break
-            optimizer.zero_grad()
-            with torch.autocast(device_type=dev.type, dtype=torch.bfloat16, enabled=use_bf16):
-                output = model(data)
-                loss = criterion(output.float(), target)
-            loss.backward()
-            optimizer.step()
+            output, loss = step(data, target)
             if args.rank == 0:
                 prec1, prec5 = util.accuracy(output, target, topk=(1, min(5, args.num_classes)))
                 losses.update(util.to_python_float(loss), data.size(0))
@@ -183,6 +199,8 @@ def train(args):
                 model_history["losses"].append(losses.val)
                 model_history["top1"].append(top1.val)
                 model_history["top5"].append(top5.val)
+        if epoch == 1 and use_graph and args.rank == 0:
+            logger.info("training step HIP graph: {}".format(step.note))
         acc1 = validate(test_loader, model, criterion, epoch, model_history, args, aug_eval, use_bf16)
         if args.rank == 0:
             is_best = acc1 > best_acc1

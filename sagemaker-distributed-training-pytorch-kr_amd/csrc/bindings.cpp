@@ -242,8 +242,38 @@ void adam(Tensor master, Tensor grad, Tensor m, Tensor v, OptT model_out, double
                   master.numel(), (float)lr, (float)beta1, (float)beta2, (float)eps, (float)wd,
                   (float)bc1, (float)bc2, adamw ? 1 : 0,
                   grad_mul ? grad_mul->data_ptr<float>() : nullptr,
-                  found_inf ? found_inf->data_ptr<int>() : nullptr, cur_stream()),
+                  found_inf ? found_inf->data_ptr<int>() : nullptr, nullptr, cur_stream()),
         "adam");
+}
+
+// HIP-graph capturable form: lr and the bias corrections come from the device tensor
+// hyper = [lr, 1 - beta1^t, 1 - beta2^t] (fp32, updated on the device each step), so a captured
+// step replays with the current step count and learning rate.
+void adam_capturable(Tensor master, Tensor grad, Tensor m, Tensor v, OptT model_out, Tensor hyper,
+                     double beta1, double beta2, double eps, double wd, bool adamw, OptT grad_mul,
+                     OptT found_inf) {
+  for (auto* t : {&master, &grad, &m, &v}) {
+    need_contig(*t, "adam buffer");
+    TORCH_CHECK(t->scalar_type() == at::kFloat, "adam: fp32 buffers expected");
+    TORCH_CHECK(t->numel() == master.numel(), "adam: buffer size mismatch");
+  }
+  TORCH_CHECK(hyper.scalar_type() == at::kFloat && hyper.is_cuda() && hyper.numel() == 3 && hyper.is_contiguous(),
+              "adam_capturable: hyper = device fp32 [lr, bc1, bc2]");
+  int mdt = 0;
+  if (model_out) {
+    need_contig(*model_out, "model_out");
+    TORCH_CHECK(model_out->numel() == master.numel(), "adam: model_out size mismatch");
+    mdt = dcode(*model_out);
+    TORCH_CHECK(mdt != 0, "adam: model_out must be bf16/fp16 (fp32 masters ARE the model)");
+  }
+  if (grad_mul) TORCH_CHECK(grad_mul->scalar_type() == at::kFloat && grad_mul->is_cuda(), "adam: grad_mul fp32 scalar");
+  if (found_inf) TORCH_CHECK(found_inf->scalar_type() == at::kInt && found_inf->is_cuda(), "adam: found_inf int32 scalar");
+  check(smdt_adam(master.data_ptr<float>(), grad.data_ptr<float>(), m.data_ptr<float>(),
+                  v.data_ptr<float>(), model_out ? model_out->data_ptr() : nullptr, mdt,
+                  master.numel(), 0.f, (float)beta1, (float)beta2, (float)eps, (float)wd, 1.f, 1.f,
+                  adamw ? 1 : 0, grad_mul ? grad_mul->data_ptr<float>() : nullptr,
+                  found_inf ? found_inf->data_ptr<int>() : nullptr, hyper.data_ptr<float>(), cur_stream()),
+        "adam_capturable");
 }
 
 Tensor sumsq(Tensor x, OptT found_inf) {
@@ -775,6 +805,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("wgrad_grouped", &wgrad_grouped, arg("main_grads"), arg("dys"), arg("xs"),
         arg("biases") = std::vector<Tensor>{}, arg("overwrite") = std::vector<bool>{});
   m.def("ce_stats", &ce_stats);
+  m.def("adam_capturable", &adam_capturable);
   m.def("ce_fused_local", &ce_fused_local);
   m.def("ce_bwd", &ce_bwd);
   m.def("ce_fused", &ce_fused);

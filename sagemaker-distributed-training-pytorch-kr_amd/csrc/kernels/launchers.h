@@ -51,7 +51,7 @@ hipError_t smdt_softmax_bwd(int dtype, int mode, const void* dy, const void* y, 
 hipError_t smdt_adam(float* master, const float* grad, float* m, float* v, void* model_out,
                      int model_dtype, int64_t n, float lr, float beta1, float beta2, float eps,
                      float wd, float bc1, float bc2, int adamw, const float* grad_mul,
-                     const int* found_inf, hipStream_t st);
+                     const int* found_inf, const float* hyper, hipStream_t st);
 int smdt_sumsq_nblocks(int64_t n);
 hipError_t smdt_sumsq(int dtype, const void* x, int64_t n, float* partial, int nblocks,
                       float* out, int* found_inf, hipStream_t st);

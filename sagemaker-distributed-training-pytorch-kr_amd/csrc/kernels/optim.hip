@@ -30,6 +30,8 @@ struct AdamArgs {
   int adamw;              // 1: decoupled weight decay; 0: L2 added to grad
   const float* grad_mul;  // device scalar multiplier applied to grads (clip * 1/loss_scale); may be null
   const int* found_inf;   // device flag; when nonzero the step is skipped; may be null
+  const float* hyper;     // capturable form: device [lr, bc1, bc2] read at run time (HIP-graph
+                          // replays see the current step / lr); null: the scalars above
 };
 
 
@@ -147,8 +149,9 @@ __global__ __launch_bounds__(256) void adam_batch_kernel(AdamArgs a) {
   if (a.found_inf && *a.found_inf) return;
   const float gm = a.grad_mul ? *a.grad_mul : 1.f;
   const int64_t nvec = a.n / 4;
-  const float step_size = a.lr / a.bc1;
-  const float rbc2 = rsqrtf(a.bc2);
+  const float lr = a.hyper ? a.hyper[0] : a.lr;
+  const float step_size = lr / (a.hyper ? a.hyper[1] : a.bc1);
+  const float rbc2 = rsqrtf(a.hyper ? a.hyper[2] : a.bc2);
   const int64_t base = (int64_t)blockIdx.x * 256 * U + threadIdx.x;
   f32x4 p[U], g[U], m[U], v[U];
 #pragma unroll
@@ -173,7 +176,7 @@ __global__ __launch_bounds__(256) void adam_batch_kernel(AdamArgs a) {
       v[u][j] = a.beta2 * v[u][j] + (1.f - a.beta2) * gj * gj;
       float denom = sqrtf(v[u][j]) * rbc2 + a.eps;
       float upd = m[u][j] / denom;
-      if (a.adamw) p[u][j] -= a.lr * a.weight_decay * p[u][j];
+      if (a.adamw) p[u][j] -= lr * a.weight_decay * p[u][j];
       p[u][j] -= step_size * upd;
     }
     __builtin_nontemporal_store(p[u], reinterpret_cast<f32x4*>(a.master) + i);
@@ -202,7 +205,7 @@ __global__ __launch_bounds__(256) void adam_batch_kernel(AdamArgs a) {
     mm = a.beta1 * mm + (1.f - a.beta1) * gj;
     vv = a.beta2 * vv + (1.f - a.beta2) * gj * gj;
     float denom = sqrtf(vv) * rbc2 + a.eps;
-    if (a.adamw) pp -= a.lr * a.weight_decay * pp;
+    if (a.adamw) pp -= lr * a.weight_decay * pp;
     pp -= step_size * (mm / denom);
     a.master[k] = pp;
     a.exp_avg[k] = mm;
@@ -221,9 +224,9 @@ extern "C" hipError_t smdt_adam(float* master, const float* grad, float* m, floa
                                 void* model_out, int model_dtype, int64_t n, float lr,
                                 float beta1, float beta2, float eps, float wd, float bc1,
                                 float bc2, int adamw, const float* grad_mul,
-                                const int* found_inf, hipStream_t st) {
+                                const int* found_inf, const float* hyper, hipStream_t st) {
   AdamArgs a{master, grad, m, v, model_out, model_dtype, n, lr, beta1, beta2, eps, wd, bc1, bc2,
-             adamw, grad_mul, found_inf};
+             adamw, grad_mul, found_inf, hyper};
   const int64_t blocks = (n / 4 + 255) / 256;
   if (blocks > 0x7FFFFFFF) return hipErrorInvalidValue;
   const dim3 gb((unsigned)(blocks > 0 ? blocks : 1));

@@ -87,7 +87,13 @@ class ConstantLossScaler:
 class MixedPrecisionAdam:
     def __init__(self, ddp: DistributedDataParallel, lr: float = 1e-4, betas=(0.9, 0.999), eps: float = 1e-8,
                  weight_decay: float = 0.0, adamw: bool = True, clip_grad: float = 0.0,
-                 loss_scaler=None, use_distributed_optimizer: Optional[bool] = None):
+                 loss_scaler=None, use_distributed_optimizer: Optional[bool] = None,
+                 capturable: bool = False):
+        """``capturable``: the step count, bias corrections and lr live on the device
+        (``adam_capturable`` reads [lr, 1 - beta1^t, 1 - beta2^t] at run time), so the whole
+        training step, optimizer included, can be captured in a HIP graph and replayed. Inside
+        a capture the lr is not re-written (it would be baked in): change it between replays
+        with ``set_lr``."""
         self.ddp = ddp
         self.lr = lr
         self.beta1, self.beta2 = betas
@@ -125,6 +131,10 @@ class MixedPrecisionAdam:
         self.param_is_fp32 = ddp.param_data.dtype == torch.float32
         self.found_inf = torch.zeros(1, dtype=torch.int32, device=dev)
         self.grad_norm = torch.zeros(1, dtype=torch.float32, device=dev)
+        self.capturable = bool(capturable) and dev.type == "cuda"
+        if self.capturable:
+            self._step_t = torch.zeros(1, dtype=torch.float32, device=dev)
+            self._hyp = torch.tensor([lr, 1.0, 1.0], dtype=torch.float32, device=dev)
         self.param_groups = [{"lr": lr, "weight_decay": weight_decay}]
         # an xGMI engine that timed out NaN-filled gathered parameters: rewrite them from the
         # masters and re-gather over RCCL (comm/health.py)
@@ -150,12 +160,31 @@ class MixedPrecisionAdam:
         # gradient is split into pieces (ZeRO shards vs whole buckets) or on the reduction order
         return xf.double().square().sum().float().view(1)
 
+    def zero_grad(self, set_to_none: bool = True):
+        """torch.optim-style: a torch_compat DDP re-zeroes its flat gradient buffer on the next
+        forward by itself; the explicit-step API zeroes it here."""
+        if not getattr(self.ddp, "torch_compat", False):
+            self.ddp.zero_grad_buffer()
+
+    def set_lr(self, lr: float):
+        """The learning rate of the next steps (outside a capture for a capturable optimizer)."""
+        self.lr = float(lr)
+        self.param_groups[0]["lr"] = self.lr
+        if self.capturable:
+            self._hyp[0:1].fill_(self.lr)
+
     @torch.no_grad()
     def step(self, lr: Optional[float] = None):
         """One optimizer step over the reduced gradients. Returns the device grad-norm tensor."""
         if lr is not None:
             self.lr = lr
         self.param_groups[0]["lr"] = self.lr
+        if self.capturable:
+            if not torch.cuda.is_current_stream_capturing():
+                self._hyp[0:1].fill_(self.lr)
+            self._step_t += 1                            # device step count: replays advance it
+            self._hyp[1:2].copy_(1.0 - torch.pow(self.beta1, self._step_t))
+            self._hyp[2:3].copy_(1.0 - torch.pow(self.beta2, self._step_t))
         _tp.params_changed()
         ddp = self.ddp
         if hasattr(ddp, "wait_param_gather"):
@@ -198,7 +227,7 @@ class MixedPrecisionAdam:
         bc1 = 1 - self.beta1 ** t
         bc2 = 1 - self.beta2 ** t
         if (use_k and self.zero and getattr(ddp, "overlap_optimizer", False) and ddp.zero3 is None
-                and not self.param_is_fp32 and len(self.pieces) == len(ddp.buckets)):
+                and not self.param_is_fp32 and len(self.pieces) == len(ddp.buckets) and not self.capturable):
             self._step_overlapped(g, mul, t)
             if self.scaler is not None:
                 self.scaler.update(self.found_inf)
@@ -217,8 +246,12 @@ class MixedPrecisionAdam:
                 host_out = None
                 if model_out is not None and not model_out.is_cuda:   # offloaded ZeRO-3 param shard
                     host_out, model_out = model_out, torch.empty(n, dtype=model_out.dtype, device=mst.device)
-                _ext.ext().adam(mst, gr, m, v, model_out, self.lr, self.beta1, self.beta2, self.eps, wd, t,
-                                self.adamw, mul, self.found_inf)
+                if self.capturable:
+                    _ext.ext().adam_capturable(mst, gr, m, v, model_out, self._hyp, self.beta1, self.beta2,
+                                               self.eps, wd, self.adamw, mul, self.found_inf)
+                else:
+                    _ext.ext().adam(mst, gr, m, v, model_out, self.lr, self.beta1, self.beta2, self.eps, wd, t,
+                                    self.adamw, mul, self.found_inf)
                 if host_out is not None:
                     host_out.copy_(model_out)
                 if self.param_is_fp32:
@@ -306,6 +339,8 @@ class MixedPrecisionAdam:
     # ------------------------------------------------------------------ checkpoint
     def state_dict(self):
         self.ddp.wait_param_gather()         # an overlapped update may still be writing the state
+        if self.capturable:                  # graph replays advance the device count only
+            self.step_count = int(self._step_t.item())
         d = {"step": self.step_count, "master": self.master, "exp_avg": self.exp_avg,
              "exp_avg_sq": self.exp_avg_sq, "lr": self.lr, "zero": self.zero,
              "pieces": [(s, e) for s, e, _ in self.pieces]}
@@ -317,6 +352,8 @@ class MixedPrecisionAdam:
         self.ddp.wait_param_gather()
         _tp.params_changed()
         self.step_count = int(d["step"])
+        if self.capturable:
+            self._step_t.fill_(self.step_count)
         self.master.copy_(d["master"])
         self.exp_avg.copy_(d["exp_avg"])
         self.exp_avg_sq.copy_(d["exp_avg_sq"])

@@ -387,7 +387,7 @@ class DistributedDataParallel(nn.Module):
         if self.zero:
             s, e = self.shard_range(b)
             out = self.grad_data[s:e]
-            h = self.xgmi.reduce_scatter_async(out, view, op="avg") if self.xgmi is not None else None
+            h = self._xg().reduce_scatter_async(out, view, op="avg") if self._xg() is not None else None
             if h is not None:
                 b.handle = h
                 _cs.collective("reduce_scatter", self.dp_group, nb, transport="xgmi", events=h.timing())
@@ -400,7 +400,7 @@ class DistributedDataParallel(nn.Module):
                 b.handle = dist.reduce_scatter_tensor(out, view, group=self.dp_group, async_op=True)
             _cs.collective("reduce_scatter", self.dp_group, nb, work=b.handle)
         else:
-            h = self.xgmi.all_reduce_async(view, op="avg") if self.xgmi is not None else None
+            h = self._xg().all_reduce_async(view, op="avg") if self._xg() is not None else None
             if h is not None:
                 b.handle = h
                 _cs.collective("all_reduce", self.dp_group, nb, transport="xgmi", events=h.timing())
@@ -525,7 +525,7 @@ class DistributedDataParallel(nn.Module):
         fresh = b.index in self._store_fresh
         self._store_fresh.discard(b.index)
         out = sh if fresh else torch.empty_like(sh)
-        h = self.xgmi.reduce_scatter_async(out, buf, op="avg") if (self.xgmi is not None and self.dp > 1) else None
+        h = self._xg().reduce_scatter_async(out, buf, op="avg") if (self._xg() is not None and self.dp > 1) else None
         nb = buf.numel() * buf.element_size()
         if self.deterministic:
             out.copy_(self._fold(buf)[self.dp_rank * n:(self.dp_rank + 1) * n])
@@ -545,6 +545,14 @@ class DistributedDataParallel(nn.Module):
                 handle = dist.reduce_scatter_tensor(out, buf, group=self.dp_group, async_op=True)
             _cs.collective("reduce_scatter", self.dp_group, nb, work=handle)
         self._rs_inflight[b.index] = (handle, None if fresh else out)
+
+    def _xg(self):
+        """The xGMI engine for the next collective, or None: none while a HIP graph is being
+        captured (its host-side banding / fallback bookkeeping is not replay-safe; the RCCL and
+        loopback collectives are captured into the graph instead)."""
+        if self.xgmi is None or (torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()):
+            return None
+        return self.xgmi
 
     def _fold(self, x: torch.Tensor) -> torch.Tensor:
         """Fixed-order combine (``deterministic_reduce``): all-gather ``x`` from every rank of
@@ -634,6 +642,8 @@ class DistributedDataParallel(nn.Module):
         sync (comm/health.py): a peer that never arrived (its outputs were NaN-filled, so that step
         is skipped by found-inf) switches every xGMI engine off and the run continues on RCCL."""
         self._syncs += 1
+        if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+            return                       # (no engine runs inside a captured step: DDP._xg)
         _health.monitor().launch()
 
     def zero_grad_buffer(self):
@@ -680,7 +690,7 @@ class DistributedDataParallel(nn.Module):
         for b in reversed(self.buckets):
             s, e = self.shard_range(b)
             full, mine = self.param_data[b.start:b.end], self.param_data[s:e]
-            h = self.xgmi.all_gather_async(full, mine) if self.xgmi is not None else None
+            h = self._xg().all_gather_async(full, mine) if self._xg() is not None else None
             nb = full.numel() * full.element_size()
             if h is not None:
                 b.ag_handle = h
