@@ -392,11 +392,17 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void fwd_kernel(const E* __re
           for (int kk = 1; kk < G::KS; ++kk) st[tt] = mfma(fr.rowf(kt, 32 * tt, kk), qf[kk], st[tt]);
         }
         if (CAUSAL && kb + kTile - 1 > qw) {  // diagonal tile for this wave: mask key > query
+          // kb is qw or qw - 32 (64-key tiles, 32-query waves): two lane-only patterns, so the
+          // compares are loop-invariant and only the selects run, on diagonal tiles
+          auto diag = [&](int off) {
 #pragma unroll
-          for (int tt = 0; tt < 2; ++tt)
+            for (int tt = 0; tt < 2; ++tt)
 #pragma unroll
-            for (int i = 0; i < 16; ++i)
-              if (kb + 32 * tt + acc_row(i, h) > my_q) st[tt][i] = -INFINITY;
+              for (int i = 0; i < 16; ++i)
+                if (off + 32 * tt + acc_row(i, h) > (lane & 31)) st[tt][i] = -INFINITY;
+          };
+          if (kb == qw) diag(0);
+          else diag(-32);
         }
       };
       float rs0 = 0.f, rs1 = 0.f;  // two chains: the denominator uses the un-dropped p
