@@ -111,6 +111,9 @@ def parse():
     p.add_argument("--hidden-dropout", type=float, default=0.1)
     p.add_argument("--attention-dropout", type=float, default=0.1)  # Megatron default (reference run)
     p.add_argument("--zero", type=int, default=1, help="ZeRO-1/2 distributed optimizer when DP > 1")
+    p.add_argument("--overlap-optimizer", type=int, default=0,
+                   help="one DP rank: the fused Adam of each gradient bucket on a side stream, overlapped "
+                        "with the next step's forward (DistributedDataParallel.overlap_optimizer)")
     p.add_argument("--bucket-size", type=int, default=None,
                    help="DDP bucket elements (default: auto, 8-32 MB from a start-up link timing)")
     p.add_argument("--comm-stats", type=int, default=1, help="phase_ms / per-collective stats in the JSON")
@@ -284,9 +287,9 @@ def main():
             raise SystemExit("[bench] --emulate-first-stage and --emulate-last-stage exclude each other")
         model = GPTModel(cfg, pre_process=st.is_first_stage() and not a.emulate_last_stage,
                          post_process=st.is_last_stage() and not a.emulate_first_stage, device=dev)
-    zero = bool(a.zero) and st.dp > 1
+    zero = bool(a.zero) and (st.dp > 1 or (bool(a.overlap_optimizer) and st.pp == 1))
     ddp = DistributedDataParallel(model, bucket_size=a.bucket_size, use_distributed_optimizer=zero,
-                                  overlap_param_gather=zero)
+                                  overlap_param_gather=zero and st.dp > 1)
     opt = MixedPrecisionAdam(ddp, lr=1.5e-4, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.01, clip_grad=1.0)
     sched = OptimizerParamScheduler(opt, max_lr=1.5e-4, min_lr=1e-5, lr_warmup_steps=10, lr_decay_steps=10000,
                                     lr_decay_style="cosine")
@@ -426,7 +429,8 @@ def main():
                        "flash_attn": not a.no_flash, "hidden_dropout": a.hidden_dropout,
                        "attention_dropout": a.attention_dropout, "recompute": a.recompute,
                        "gemm_autotune": tuned,
-                       "comm_stream_priority": comm_streams.describe()["comm_stream_priority"]},
+                       "comm_stream_priority": comm_streams.describe()["comm_stream_priority"],
+                       "optimizer_overlap": bool(getattr(ddp, "overlap_optimizer", False))},
             **({} if emulated else {
                 "model_tflops_per_gpu": round(tps * fpt / n / 1e12, 2),
                 "baseline": "41 model-TFLOP/s/GPU (reference GPT-2-small, 16xA100, BASELINE.md) at equal model FLOPs"}),
