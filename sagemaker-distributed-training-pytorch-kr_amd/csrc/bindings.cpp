@@ -217,6 +217,23 @@ Tensor softmax_bwd(Tensor dy, Tensor y, int64_t mode, double scale) {
   return dx;
 }
 
+// ------------------------------------------------------------------ graph-safe dropout RNG
+// counter: a persistent device int32 [1] (None: off). While set, every dropout kernel (flash
+// attention, fused LayerNorm) mixes *counter into its keys at run time; the training step
+// advances it on the device, so HIP-graph replays of a captured step draw fresh masks.
+static Tensor g_rng_counter;
+void set_rng_step(OptT counter) {
+  if (counter) {
+    TORCH_CHECK(counter->is_cuda() && counter->scalar_type() == at::kInt && counter->numel() == 1,
+                "set_rng_step: device int32 [1] counter");
+    g_rng_counter = *counter;
+    smdt_set_rng_step(reinterpret_cast<uint32_t*>(counter->data_ptr<int>()));
+  } else {
+    g_rng_counter = Tensor();
+    smdt_set_rng_step(nullptr);
+  }
+}
+
 // ------------------------------------------------------------------ optimizer
 void adam(Tensor master, Tensor grad, Tensor m, Tensor v, OptT model_out, double lr, double beta1,
           double beta2, double eps, double wd, int64_t step, bool adamw, OptT grad_mul,
@@ -805,6 +822,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("wgrad_grouped", &wgrad_grouped, arg("main_grads"), arg("dys"), arg("xs"),
         arg("biases") = std::vector<Tensor>{}, arg("overwrite") = std::vector<bool>{});
   m.def("ce_stats", &ce_stats);
+  m.def("set_rng_step", &set_rng_step);
   m.def("adam_capturable", &adam_capturable);
   m.def("ce_fused_local", &ce_fused_local);
   m.def("ce_bwd", &ce_bwd);

@@ -96,6 +96,9 @@ struct Strides {
 // VALU than the MFMA work of an attention tile on CDNA4.
 struct Drop {
   uint32_t thr, key0, key1;
+  // graph-safe RNG (smdt_set_rng_step): a device step counter mixed into every key at run time,
+  // so a HIP graph replay draws new masks while the per-call (seed, offset) stays baked in
+  const uint32_t* step;
   uint32_t k4;    // (128 - T) in every byte: the SWAR threshold addend
   float inv;      // 1 / (1 - p_realised)
   float keep;     // 1 - p_realised  (= 1 / inv)
@@ -111,7 +114,8 @@ __device__ __forceinline__ uint32_t fmix32(uint32_t x) {
   return x;
 }
 __device__ __forceinline__ uint32_t drop_key(const Drop& d, int bh) {
-  return fmix32(d.key0 + (uint32_t)bh * 0x632BE5ABu) ^ d.key1;
+  const uint32_t k = fmix32(d.key0 + (uint32_t)bh * 0x632BE5ABu) ^ d.key1;
+  return d.step ? k ^ fmix32(*d.step * 0x9E3779B1u + 0x85EBCA77u) : k;
 }
 __device__ __forceinline__ uint32_t drop_hash(uint32_t blk, uint32_t key) {
   // full-rate ops only (v_mul_u32_u24, xor, shift): v_mul_lo_u32 is a quarter-rate instruction
@@ -1060,6 +1064,10 @@ static uint32_t host_fmix32(uint32_t x) {
   return x;
 }
 
+static uint32_t* g_rng_step = nullptr;
+extern "C" void smdt_set_rng_step(uint32_t* counter) { g_rng_step = counter; }
+extern "C" uint32_t* smdt_rng_step() { return g_rng_step; }
+
 // keys: key0 from the seed, key1 from the per-call offset (see drop_key / drop_hash).
 static Drop make_drop(float p, uint64_t seed, uint64_t offset) {
   Drop d;
@@ -1071,6 +1079,7 @@ static Drop make_drop(float p, uint64_t seed, uint64_t offset) {
   d.log2inv = (float)std::log2(128.0 / (128.0 - (double)d.thr));
   d.key0 = host_fmix32((uint32_t)seed ^ host_fmix32((uint32_t)(seed >> 32) + 0x9E3779B9u));
   d.key1 = host_fmix32((uint32_t)offset * 0x27D4EB2Fu ^ host_fmix32((uint32_t)(offset >> 32) + 0x165667B1u));
+  d.step = smdt_rng_step();
   return d;
 }
 

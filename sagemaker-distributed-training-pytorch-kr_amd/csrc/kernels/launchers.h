@@ -47,6 +47,11 @@ hipError_t smdt_softmax_fwd(int dtype, int mode, const void* x, const uint8_t* m
 hipError_t smdt_softmax_bwd(int dtype, int mode, const void* dy, const void* y, void* dx,
                             int64_t rows, int sq, int sk, float scale, hipStream_t st);
 
+// graph-safe dropout RNG (flash_attn.hip): the device step counter every dropout kernel mixes into
+// its key at run time (null: none). Set by the bindings (set_rng_step), read by the launchers.
+extern "C" void smdt_set_rng_step(uint32_t* counter);
+extern "C" uint32_t* smdt_rng_step();
+
 // optim.hip
 hipError_t smdt_adam(float* master, const float* grad, float* m, float* v, void* model_out,
                      int model_dtype, int64_t n, float lr, float beta1, float beta2, float eps,

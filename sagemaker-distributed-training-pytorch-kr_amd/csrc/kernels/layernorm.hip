@@ -36,6 +36,7 @@ struct LnFwdArgs {
   float p_drop;
   uint64_t seed, offset;
   int rms;
+  const uint32_t* step;  // graph-safe RNG step counter (smdt_set_rng_step), may be null
 };
 
 struct LnBwdArgs {
@@ -55,6 +56,7 @@ struct LnBwdArgs {
   int rms;
   int want_dbias;
   int nblocks;
+  const uint32_t* step;
 };
 
 template <int G>
@@ -79,9 +81,10 @@ __device__ __forceinline__ uint32_t fmix32(uint32_t x) {
 }
 __device__ __forceinline__ uint32_t drop_thr16(float p) { return (uint32_t)(p * 65536.f + 0.5f); }
 __device__ __forceinline__ float drop_scale16(uint32_t thr) { return 65536.f / (65536.f - (float)thr); }
-__device__ __forceinline__ uint32_t ln_drop_key(uint64_t seed, uint64_t offset) {
-  return fmix32((uint32_t)seed ^ fmix32((uint32_t)(seed >> 32) + 0x9E3779B9u * ((uint32_t)offset + 1u)) ^
-                fmix32((uint32_t)(offset >> 32) + 0x27D4EB2Fu));
+__device__ __forceinline__ uint32_t ln_drop_key(uint64_t seed, uint64_t offset, const uint32_t* step) {
+  const uint32_t k = fmix32((uint32_t)seed ^ fmix32((uint32_t)(seed >> 32) + 0x9E3779B9u * ((uint32_t)offset + 1u)) ^
+                            fmix32((uint32_t)(offset >> 32) + 0x27D4EB2Fu));
+  return step ? k ^ fmix32(*step * 0x9E3779B1u + 0x85EBCA77u) : k;
 }
 // keep[j] (1 / 0) for the 8 elements starting at (row, col), col % 8 == 0.
 __device__ __forceinline__ void dropout_mask8(uint32_t key, int64_t row, int H, int col, uint32_t thr,
@@ -109,7 +112,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(LnFwdArgs a) {
   const bool drop = a.p_drop > 0.f;
   const bool write_s = a.s_out != nullptr;
   const uint32_t dthr = drop ? drop_thr16(a.p_drop) : 0u;
-  const uint32_t dkey = drop ? ln_drop_key(a.seed, a.offset) : 0u;
+  const uint32_t dkey = drop ? ln_drop_key(a.seed, a.offset, a.step) : 0u;
   const float keep_scale = drop ? drop_scale16(dthr) : 1.f;
 
   // gamma / beta / bias are row-invariant: load once.
@@ -211,7 +214,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(LnBwdArgs a) {
   const int nchunk = H / 8;
   const bool drop = a.p_drop > 0.f;
   const uint32_t dthr = drop ? drop_thr16(a.p_drop) : 0u;
-  const uint32_t dkey = drop ? ln_drop_key(a.seed, a.offset) : 0u;
+  const uint32_t dkey = drop ? ln_drop_key(a.seed, a.offset, a.step) : 0u;
   const float keep_scale = drop ? drop_scale16(dthr) : 1.f;
   const bool has_dsin = a.ds_in != nullptr;
   const bool separate_dx = a.dx_out != nullptr && a.dx_out != a.ds_out;
@@ -444,7 +447,8 @@ extern "C" hipError_t smdt_layernorm_fwd(int dtype, int wdtype, const void* x, c
                                          uint64_t seed, uint64_t offset, int rms,
                                          hipStream_t st) {
   if (H % 8 != 0 || H > 16384) return hipErrorInvalidValue;
-  LnFwdArgs a{x, res, bias, gamma, beta, y, s_out, mean, rstd, rows, H, eps, p_drop, seed, offset, rms};
+  LnFwdArgs a{x, res, bias, gamma, beta, y, s_out, mean, rstd, rows, H, eps, p_drop, seed, offset, rms,
+              smdt_rng_step()};
   if (dtype == 1 && wdtype == 1) return ln_fwd_typed<bf16, bf16>(a, st);
   if (dtype == 1 && wdtype == 0) return ln_fwd_typed<bf16, float>(a, st);
   if (dtype == 2 && wdtype == 2) return ln_fwd_typed<f16, f16>(a, st);
@@ -462,7 +466,7 @@ extern "C" hipError_t smdt_layernorm_bwd(int dtype, int wdtype, const void* dy, 
                                          int acc_mask, hipStream_t st) {
   if (H % 8 != 0 || H > 16384) return hipErrorInvalidValue;
   LnBwdArgs a{dy, ds_in, s, gamma, mean, rstd, ds_out, dx_out, partials, rows, H, p_drop, seed,
-              offset, rms, dbias != nullptr, nblocks};
+              offset, rms, dbias != nullptr, nblocks, smdt_rng_step()};
   hipError_t e;
   if (dtype == 1 && wdtype == 1) e = ln_bwd_typed<bf16, bf16>(a, st);
   else if (dtype == 1 && wdtype == 0) e = ln_bwd_typed<bf16, float>(a, st);

@@ -398,13 +398,48 @@ def flash_dropout_thr(p: float):
     return thr, 128.0 / (128.0 - thr)
 
 
-def flash_dropout_keep_mask(B: int, H: int, S: int, p: float, seed: int, offset: int, device=None):
+# Graph-safe dropout RNG. The fused dropout kernels take a (seed, offset) pair per call from the
+# host (``_Rng``); inside a captured HIP graph those values are baked into the kernel arguments
+# and every replay would redraw the same masks. With a device step counter registered, every
+# dropout kernel mixes the counter's value into its key at run time (flash_attn.hip drop_key,
+# layernorm.hip ln_drop_key); ``advance_graph_rng`` (a device add, captured with the step)
+# moves it once per training step — after the backward, so forward and backward of a step see
+# the same masks.
+_GRAPH_RNG = {"counter": None}
+
+
+def enable_graph_rng(device=None) -> torch.Tensor:
+    c = _GRAPH_RNG["counter"]
+    if c is None:
+        c = torch.zeros(1, dtype=torch.int32, device=device or torch.device("cuda", torch.cuda.current_device()))
+        _ext.ext().set_rng_step(c)
+        _GRAPH_RNG["counter"] = c
+    return c
+
+
+def disable_graph_rng():
+    if _GRAPH_RNG["counter"] is not None:
+        _ext.ext().set_rng_step(None)
+        _GRAPH_RNG["counter"] = None
+
+
+def advance_graph_rng():
+    c = _GRAPH_RNG["counter"]
+    if c is not None:
+        c.add_(1)
+
+
+def flash_dropout_keep_mask(B: int, H: int, S: int, p: float, seed: int, offset: int, device=None,
+                            step: Optional[int] = None):
     """Bit-exact twin of the flash kernels' dropout mask: bool [B, H, S(q), S(k)], True = kept
     (see ``drop_hash`` in flash_attn.hip): each 2x2 (query, key) block shares one hash, byte
-    2 (q & 1) + (k & 1) decides the element (kept iff its low 7 bits >= the threshold)."""
+    2 (q & 1) + (k & 1) decides the element (kept iff its low 7 bits >= the threshold).
+    ``step``: the graph-safe RNG counter value the kernels read (``enable_graph_rng``)."""
     thr, _ = flash_dropout_thr(p)
     key0 = _fmix32_i((seed & _M32) ^ _fmix32_i(((seed >> 32) + 0x9E3779B9) & _M32))
     key1 = _fmix32_i((((offset & _M32) * 0x27D4EB2F) & _M32) ^ _fmix32_i(((offset >> 32) + 0x165667B1) & _M32))
+    if step is not None:
+        key1 ^= _fmix32_i(((step & _M32) * 0x9E3779B1 + 0x85EBCA77) & _M32)
     bh = torch.arange(B * H, dtype=torch.int64, device=device)
     kbh = _fmix32_t((key0 + bh * 0x632BE5AB) & _M32) ^ key1                          # [BH]
     half = S // 2

@@ -6,7 +6,7 @@ cd "$R"
 O=$R/gpurun_out/${OUT:-r5_check}; mkdir -p $O
 export TMPDIR=/tmp HSA_ENABLE_IPC_MODE_LEGACY=0
 run() { local n=$1 t=$2; shift 2; echo "=== $n $(date +%T)"; timeout -k 10 $t "$@" > $O/$n.log 2>&1; local rc=$?; echo "=== $n rc=$rc"; tail -n 1 $O/$n.log | cut -c1-700; [ $rc -eq 0 ] || exit $rc; }
-run tests 600 python -u -m pytest -q -x --timeout 120 --timeout-method thread -m gpu tests/test_graph_gpu.py tests/test_kernels_gpu.py -k "graph or vocab_parallel or lm_head or cross_entropy"
+run tests 600 python -u -m pytest -q -x --timeout 120 --timeout-method thread -m gpu tests/test_graph_gpu.py tests/test_kernels_gpu.py tests/test_model_gpu.py
 for i in 1 2; do
   run bench_$i 400 python bench.py --steps 20 --warmup 5
   run bench_ovl_$i 400 python bench.py --steps 20 --warmup 5 --overlap-optimizer 1

@@ -567,3 +567,66 @@ def test_dgrad_weight_t_cache_invalidation():
     tp.params_changed()
     c = tp._dgrad_weight_t(w)
     assert c is not b and torch.equal(c, w.detach().t().contiguous())
+
+
+def test_graph_safe_dropout_rng():
+    """With the device step counter registered (SF.enable_graph_rng) the flash and fused-LayerNorm
+    dropout kernels mix its value into their keys at run time: the flash mask equals its bit-exact
+    twin at that step (forward and all three gradients), a new step gives a new mask, and a
+    captured HIP graph that advances the counter draws a fresh mask on every replay."""
+    torch.manual_seed(21)
+    B, S, H, D, p, seed, off = 2, 256, 4, 64, 0.1, 77, 5
+    q, k, v = (torch.randn(B, S, H, D, device=DEV, dtype=torch.bfloat16, requires_grad=True) for _ in range(3))
+    scale = 1 / math.sqrt(D)
+    c = SF.enable_graph_rng()
+    try:
+        c.fill_(5)
+        o = SF._FlashAttn.apply(q, k, v, scale, True, p, seed, off)
+        keep = SF.flash_dropout_keep_mask(B, H, S, p, seed, off, DEV, step=5)
+        assert not torch.equal(keep, SF.flash_dropout_keep_mask(B, H, S, p, seed, off, DEV))
+        qr, kr, vr = (t.detach().float().requires_grad_() for t in (q, k, v))
+        orf = SF.attention_ref(qr, kr, vr, scale, True, p, keep)
+        torch.testing.assert_close(o.float(), orf, atol=2e-2, rtol=2e-2)
+        do = torch.randn_like(o)
+        o.backward(do)
+        orf.backward(do.float())
+        for a, r in ((q, qr), (k, kr), (v, vr)):
+            err = (a.grad.float() - r.grad).abs().max().item()
+            assert err < 0.05 * max(1.0, r.grad.abs().max().item()), err
+        qd, kd, vd = q.detach(), k.detach(), v.detach()
+        c.fill_(6)
+        assert not torch.equal(SF._FlashAttn.apply(qd, kd, vd, scale, True, p, seed, off), o.detach())
+        # captured: the replays see counter values 7, 8 (advanced inside the graph)
+        c.fill_(6)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            SF.advance_graph_rng()
+            og = SF._FlashAttn.apply(qd, kd, vd, scale, True, p, seed, off)
+        outs = []
+        for _ in range(2):
+            g.replay()
+            outs.append(og.clone())
+        for st, got in zip((7, 8), outs):
+            kp = SF.flash_dropout_keep_mask(B, H, S, p, seed, off, DEV, step=st)
+            want = SF.attention_ref(qd.float(), kd.float(), vd.float(), scale, True, p, kp)
+            torch.testing.assert_close(got.float(), want, atol=2e-2, rtol=2e-2)
+        assert not torch.equal(outs[0], outs[1])
+        # fused LayerNorm dropout: forward and backward agree at a step, differ across steps
+        x = torch.randn(128, 1024, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+        res = torch.zeros(128, 1024, device=DEV, dtype=torch.bfloat16)
+        gam = torch.ones(1024, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+        bet = torch.zeros(1024, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+        masks = []
+        for st in (3, 4):
+            c.fill_(st)
+            # the same host (seed, offset) both times: only the device counter differs
+            _, s_ = SF.bias_dropout_add_norm(x, None, res, gam, bet, 0.25, True, 1e-5, False, rng=SF.PhiloxState(9))
+            x.grad = None
+            s_.backward(torch.ones_like(s_))
+            kept = s_ != 0
+            assert torch.all(x.grad[~kept] == 0) and torch.all(x.grad[kept] != 0)
+            masks.append(kept)
+        assert not torch.equal(masks[0], masks[1])
+    finally:
+        SF.disable_graph_rng()
