@@ -120,6 +120,12 @@ def parse():
     p.add_argument("--no-flash", action="store_true")
     p.add_argument("--recompute", choices=["none", "full"], default="none")
     p.add_argument("--profile-steps", type=int, default=0)
+    p.add_argument("--graph", type=int, default=0,
+                   help="capture one whole training step (every micro-batch's forward / backward, the "
+                        "gradient sync, the fused Adam with a device-side step count) in a HIP graph after "
+                        "the warm-up and replay it: fresh tokens are copied into static buffers and the lr "
+                        "set before each replay; dropout masks advance through the device RNG counter "
+                        "(ops/functional.enable_graph_rng). pp = 1 (one process per stage emulation too)")
     p.add_argument("--tunableop", type=int, default=1,
                    help="autotune torch's hipBLASLt GEMMs per shape during the (untimed) warmup")
     p.add_argument("--tune-ms", type=int, default=40)
@@ -290,7 +296,12 @@ def main():
     zero = bool(a.zero) and (st.dp > 1 or (bool(a.overlap_optimizer) and st.pp == 1))
     ddp = DistributedDataParallel(model, bucket_size=a.bucket_size, use_distributed_optimizer=zero,
                                   overlap_param_gather=zero and st.dp > 1)
-    opt = MixedPrecisionAdam(ddp, lr=1.5e-4, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.01, clip_grad=1.0)
+    use_graph = bool(a.graph) and dev.type == "cuda" and st.pp == 1
+    opt = MixedPrecisionAdam(ddp, lr=1.5e-4, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.01, clip_grad=1.0,
+                             capturable=use_graph)
+    if use_graph:
+        from smdt_amd.ops import functional as _SF
+        _SF.enable_graph_rng(dev)
     sched = OptimizerParamScheduler(opt, max_lr=1.5e-4, min_lr=1e-5, lr_warmup_steps=10, lr_decay_steps=10000,
                                     lr_decay_style="cosine")
     mbs, S = a.micro_batch_size, a.seq_length
@@ -303,13 +314,28 @@ def main():
 
     it = batches()
     pos = None   # positions 0 .. S-1 in every sequence (the model's broadcast position-table slice)
+    # graph mode: the step reads its micro-batches from static buffers refilled before each replay
+    static_tok = [torch.empty((mbs, S + 1), dtype=torch.long, device=dev) for _ in range(a.grad_accum)] \
+        if use_graph else None
+    static_act = None
+
+    def refill():
+        for t in static_tok:
+            t.copy_(next(it))
+        if static_act is not None:
+            static_act.normal_(generator=gen)
+
+    def static_batches():
+        while True:
+            yield from static_tok
 
     def forward_step(data_iter, m):
         toks = next(data_iter)
         tokens, labels = toks[:, :-1], toks[:, 1:]
         if a.emulate_last_stage:   # the activation a last stage receives from its predecessor
-            model.set_input_tensor(torch.randn(shape, device=dev, dtype=torch.bfloat16, generator=gen)
-                                   .requires_grad_())
+            act = static_act if static_act is not None else \
+                torch.randn(shape, device=dev, dtype=torch.bfloat16, generator=gen)
+            model.set_input_tensor(act.detach().requires_grad_())
         out = m(tokens, pos, None, labels=labels)
 
         def loss_func(o):
@@ -322,22 +348,34 @@ def main():
     fb = get_forward_backward_func()
     shape = (S // a.tp if cfg.sequence_parallel else S, mbs, cfg.hidden_size)
 
-    def train_step(stats=False):
+    def train_step(stats=False, data=None, lr=None):
         if stats:
             comm_stats.begin_step()
         ddp.zero_grad_buffer()
         # an emulated pipeline stage issues each micro-batch's W GEMMs as its schedule would
-        losses = fb(forward_step, it, ddp, a.grad_accum, tensor_shape=shape, dtype=torch.bfloat16,
+        losses = fb(forward_step, data if data is not None else it, ddp, a.grad_accum, tensor_shape=shape,
+                    dtype=torch.bfloat16,
                     split_backward=bool(a.emulate_tp) and a.pp_schedule in ("zb", "zbh1", "zbh2"))
         comm_stats.mark("fwd_bwd")
         ddp.finish_grad_sync()
         allreduce_word_embedding_grads(model)   # tied embedding: first + last pipeline stage
         comm_stats.mark("grad_sync")
-        lr = sched.step(1)
-        opt.step(lr)
+        opt.step(sched.step(1) if lr is None else None)
         comm_stats.mark("optimizer")
         comm_stats.end_step()
+        if use_graph:
+            _SF.advance_graph_rng()
         return losses
+
+    graph = None
+
+    def graph_step():
+        """Refill the static inputs, set this step's lr (the captured Adam reads it from the
+        device), replay."""
+        refill()
+        opt.set_lr(sched.step(1))
+        graph[0].replay()
+        return graph[1]
 
     tw = time.perf_counter()
     for i in range(a.warmup):
@@ -348,6 +386,26 @@ def main():
     if rank == 0:
         print(f"[bench] warmup ({a.warmup} steps, incl. GEMM autotune) took {time.perf_counter() - tw:.1f}s",
               file=sys.stderr, flush=True)
+    graph_note = None
+    if use_graph:
+        if a.emulate_last_stage:
+            static_act = torch.empty(shape, device=dev, dtype=torch.bfloat16)
+        refill()
+        torch.cuda.synchronize()
+        try:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                glosses = train_step(data=static_batches(), lr=False)
+            graph = (g, glosses)
+            for _ in range(2):
+                graph_step()
+            graph_note = "captured"
+        except Exception as e:  # noqa: BLE001 - report and run eager
+            graph_note = f"capture failed, eager: {type(e).__name__}: {str(e)[:160]}"
+            print(f"[bench] {graph_note}", file=sys.stderr, flush=True)
+            graph = None
+        torch.cuda.synchronize()
+    run_step = (lambda stats=False: graph_step()) if graph is not None else train_step
     if dist.is_initialized():
         dist.barrier()
     if torch.cuda.is_available():
@@ -358,7 +416,7 @@ def main():
     # stats of a CPU (Gloo) run cost nothing measurable and are recorded on the timed steps
     cpu_stats = bool(a.comm_stats) and not torch.cuda.is_available()
     for _ in range(a.steps):
-        last = train_step(stats=cpu_stats)
+        last = run_step(stats=cpu_stats)
     if torch.cuda.is_available():
         torch.cuda.synchronize()
     if dist.is_initialized():
@@ -430,7 +488,8 @@ def main():
                        "attention_dropout": a.attention_dropout, "recompute": a.recompute,
                        "gemm_autotune": tuned,
                        "comm_stream_priority": comm_streams.describe()["comm_stream_priority"],
-                       "optimizer_overlap": bool(getattr(ddp, "overlap_optimizer", False))},
+                       "optimizer_overlap": bool(getattr(ddp, "overlap_optimizer", False)),
+                       "hip_graph": graph_note},
             **({} if emulated else {
                 "model_tflops_per_gpu": round(tps * fpt / n / 1e12, 2),
                 "baseline": "41 model-TFLOP/s/GPU (reference GPT-2-small, 16xA100, BASELINE.md) at equal model FLOPs"}),
