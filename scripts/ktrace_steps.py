@@ -26,7 +26,7 @@ def main():
         for r in csv.DictReader(f):
             rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
     rows.sort()
-    adam = [i for i, r in enumerate(rows) if "adam_kernel" in r[2]]
+    adam = [i for i, r in enumerate(rows) if "adam_kernel" in r[2] or "adam_batch_kernel" in r[2]]
     ends = []
     for j, i in enumerate(adam):
         if j + 1 == len(adam) or adam[j + 1] - i > 50:
