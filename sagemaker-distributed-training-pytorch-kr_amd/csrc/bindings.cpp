@@ -408,6 +408,46 @@ void rope_(Tensor x, Tensor cos_t, Tensor sin_t, int64_t rot, int64_t pos_div, i
         "rope");
 }
 
+// ------------------------------------------------------------------ forward / dgrad GEMM (MFMA)
+// out[M, N] = a[M, K] . b[N, K]^T with the epilogue `epi` (0 none, 1 + bias, 2 bias + GeLU-tanh:
+// out = pre-activation, out2 = activation). Returns false (and does nothing) for an unsupported
+// shape / layout so the caller can take the library GEMM; out / out2 may be given (e.g. a slice of
+// a larger buffer), else they are allocated.
+bool gemm_tn_supported(Tensor a, Tensor b) {
+  if (!a.is_cuda() || !b.is_cuda() || a.dim() != 2 || b.dim() != 2 || !a.is_contiguous() || !b.is_contiguous()) return false;
+  if ((a.scalar_type() != at::kBFloat16 && a.scalar_type() != at::kHalf) || b.scalar_type() != a.scalar_type()) return false;
+  if (a.size(1) != b.size(1)) return false;
+  if (reinterpret_cast<uintptr_t>(a.data_ptr()) % 16 || reinterpret_cast<uintptr_t>(b.data_ptr()) % 16) return false;
+  return smdt_gemm_tn_supported(a.size(0), b.size(0), a.size(1)) != 0;
+}
+
+std::vector<Tensor> gemm_tn(Tensor a, Tensor b, int64_t epi, OptT bias, OptT out, OptT out2, int64_t max_blocks,
+                            int64_t var) {
+  TORCH_CHECK(gemm_tn_supported(a, b), "gemm_tn: unsupported operands");
+  TORCH_CHECK(epi >= 0 && epi <= 2, "gemm_tn: epilogue");
+  const int64_t M = a.size(0), N = b.size(0), K = a.size(1);
+  if (epi >= 1) {
+    TORCH_CHECK(bias.has_value(), "gemm_tn: the epilogue needs a bias");
+    need_contig(*bias, "bias");
+    TORCH_CHECK(bias->numel() == N && bias->scalar_type() == a.scalar_type(), "gemm_tn: bias mismatch");
+  }
+  auto mk = [&](const OptT& o, const char* n) {
+    if (!o) return torch::empty({M, N}, a.options());
+    need_contig(*o, n);
+    TORCH_CHECK(o->numel() == M * N && o->scalar_type() == a.scalar_type() && o->device() == a.device(),
+                "gemm_tn: output buffer mismatch");
+    return *o;
+  };
+  Tensor c = mk(out, "out");
+  Tensor c2 = epi == 2 ? mk(out2, "out2") : Tensor();
+  check(smdt_gemm_tn_var(dcode(a), (int)epi, a.data_ptr(), b.data_ptr(), c.data_ptr(),
+                         epi == 2 ? c2.data_ptr() : nullptr, optr(bias), M, N, K, (int)max_blocks, (int)var,
+                         cur_stream()),
+        "gemm_tn");
+  if (epi == 2) return {c, c2};
+  return {c};
+}
+
 // ------------------------------------------------------------------ weight gradient (MFMA)
 // main_grad[N, K] (fp32) += dy[M, N]^T . x[M, K]; returns false when the shape is unsupported.
 bool wgrad_mfma(Tensor main_grad, Tensor dy, Tensor x, int64_t max_splits) {
@@ -818,6 +858,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("aug_depthwise", &aug_depthwise);
   m.def("aug_median3", &aug_median3);
   m.def("bias_grad", &bias_grad);
+  m.def("gemm_tn_supported", &gemm_tn_supported, arg("a"), arg("b"));
+  m.def("gemm_tn", &gemm_tn, arg("a"), arg("b"), arg("epi") = 0, arg("bias") = pybind11::none(),
+        arg("out") = pybind11::none(), arg("out2") = pybind11::none(), arg("max_blocks") = 0,
+        arg("var") = 0);
   m.def("wgrad_mfma", &wgrad_mfma, arg("main_grad"), arg("dy"), arg("x"), arg("max_splits") = 0);
   m.def("wgrad_grouped", &wgrad_grouped, arg("main_grads"), arg("dys"), arg("xs"),
         arg("biases") = std::vector<Tensor>{}, arg("overwrite") = std::vector<bool>{});

@@ -359,8 +359,11 @@ class ParallelMLP(nn.Module):
                                         sequence_parallel=cfg.sequence_parallel, skip_bias_add=True)
 
     def forward(self, x):
-        h, b = self.fc1(x)
         act = self.cfg.activation
+        if act == "gelu" and self.cfg.bias_gelu_fusion and tp.linear_bias_gelu_ok(x, self.fc1):
+            # fc1 GEMM + bias + GeLU in one launch (gemm_tn.hip's bias-GeLU epilogue)
+            return self.fc2(tp.linear_bias_gelu(x, self.fc1))
+        h, b = self.fc1(x)
         if act in ("gelu", "gelu_erf"):
             if self.cfg.bias_gelu_fusion:
                 h = SF.bias_gelu(h, b, "tanh" if act == "gelu" else "none")

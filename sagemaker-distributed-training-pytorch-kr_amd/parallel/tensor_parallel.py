@@ -643,12 +643,48 @@ def _row_blocks(M: int):
     return ((0, M - r), (M - r, M))
 
 
+# Hand-written MFMA GEMM (csrc/kernels/gemm_tn.hip: persistent 256 x 256 tiles, LDS-DMA stage
+# ring, trickled epilogue stores) for out = x W^T where it beats hipBLASLt. SMDT_GEMM_TN: "0" off,
+# "1" every supported shape, a comma list of "N:K" pairs (e.g. "4096:1024,1024:4096") for those
+# shapes only. The fused fc1 + bias-GeLU op (``linear_bias_gelu``) is governed separately by
+# SMDT_FUSED_BIAS_GELU.
+_GEMM_TN = os.environ.get("SMDT_GEMM_TN", "0")
+
+
+def _gemm_tn_shapes():
+    if _GEMM_TN in ("0", "", "1"):
+        return None
+    out = set()
+    for item in _GEMM_TN.split(","):
+        n, k = item.split(":")
+        out.add((int(n), int(k)))
+    return out
+
+
+_GEMM_TN_SHAPES = _gemm_tn_shapes()
+
+
+def _gemm_tn_ok(x2, w, bias):
+    if _GEMM_TN == "0" or not x2.is_cuda or w.dim() != 2:
+        return False
+    if bias is not None and (bias.dtype != x2.dtype or not bias.is_contiguous()):
+        return False
+    if _GEMM_TN_SHAPES is not None and (w.shape[0], w.shape[1]) not in _GEMM_TN_SHAPES:
+        return False
+    return _ext.ext().gemm_tn_supported(x2, w)
+
+
 def linear_rows(x, w, bias=None):
     """F.linear(x, w, bias), split into row blocks when ``_row_blocks`` says the whole GEMM would
     take a slow hipBLASLt kernel (CUDA only; identical results: each row's dot products are the
-    same)."""
+    same); the hand-written gemm_tn where SMDT_GEMM_TN selects it."""
     if x.is_cuda and x.dim() >= 2:
         M = x.numel() // x.shape[-1]
+        if x.is_contiguous():
+            x2 = x.view(M, x.shape[-1])
+            if _gemm_tn_ok(x2, w, bias):
+                y = _ext.ext().gemm_tn(x2, w, 1 if bias is not None else 0, bias)[0]
+                return y.view(tuple(x.shape[:-1]) + (w.shape[0],))
         bl = _row_blocks(M)
         if bl is not None:
             x2 = x.reshape(M, x.shape[-1])
@@ -701,26 +737,85 @@ class LinearWithGradAccumulationAndAsyncCommunication(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         x, weight = ctx.saved_tensors
-        group = _tp_group()
-        tp = dist.get_world_size(group) if group is not None else 1
-        total = _gather_dim0(x, group) if (ctx.sp and tp > 1) else x
-        g = g.contiguous()
-        gi = dgrad(g, weight, _dgrad_weight_t(weight))
-        handle = None
-        if ctx.sp and tp > 1:
-            gi_out, handle = _reduce_scatter_dim0(gi, group, async_op=True)
-        else:
-            gi_out = gi
-            if ctx.async_ar and tp > 1:
-                handle = _all_reduce(gi_out, group, async_op=True)
-        g2 = g.reshape(-1, g.shape[-1])
-        t2 = total.reshape(-1, total.shape[-1])
-        dw, db = _wgrad_and_bias(weight, ctx.bias_p if ctx.has_bias else None, g2, t2)
-        if handle is not None:
-            # the collective is in flight: run the queued weight-gradient GEMMs beside it
-            DEFERRED_WGRAD.flush_opportunistic()
-            _wait_works([handle], group)
+        gi_out, dw, db = _linear_backward(ctx, g, x, weight)
         return gi_out, dw, db, None, None, None
+
+
+def _linear_backward(ctx, g, x, weight):
+    """dgrad -> async TP all-reduce / SP reduce-scatter of it -> wgrad (+ bias grad) into the fp32
+    main_grad -> wait: the backward of ``LinearWithGradAccumulationAndAsyncCommunication`` (ctx
+    carries sp, async_ar, has_bias, bias_p)."""
+    group = _tp_group()
+    tp = dist.get_world_size(group) if group is not None else 1
+    total = _gather_dim0(x, group) if (ctx.sp and tp > 1) else x
+    g = g.contiguous()
+    gi = dgrad(g, weight, _dgrad_weight_t(weight))
+    handle = None
+    if ctx.sp and tp > 1:
+        gi_out, handle = _reduce_scatter_dim0(gi, group, async_op=True)
+    else:
+        gi_out = gi
+        if ctx.async_ar and tp > 1:
+            handle = _all_reduce(gi_out, group, async_op=True)
+    g2 = g.reshape(-1, g.shape[-1])
+    t2 = total.reshape(-1, total.shape[-1])
+    dw, db = _wgrad_and_bias(weight, ctx.bias_p if ctx.has_bias else None, g2, t2)
+    if handle is not None:
+        # the collective is in flight: run the queued weight-gradient GEMMs beside it
+        DEFERRED_WGRAD.flush_opportunistic()
+        _wait_works([handle], group)
+    return gi_out, dw, db
+
+
+# fc1 + bias + GeLU(tanh) as ONE GEMM launch (gemm_tn.hip EPI_BIAS_GELU): the epilogue writes the
+# pre-activation (kept for the backward) and the activation; the separate bias_act_fwd pass over
+# the [tokens, 4h] tensor is gone (SURVEY K5; Megatron's bias_gelu_fusion,
+# /root/reference/3_training_megatron-lm/megatron/arguments.py:819-821). SMDT_FUSED_BIAS_GELU=0 off.
+_FUSED_BIAS_GELU = os.environ.get("SMDT_FUSED_BIAS_GELU", "0") == "1"
+
+
+class LinearBiasGeLU(torch.autograd.Function):
+    """act = gelu_tanh(x W^T + b) for a column-parallel fc1 without sequence parallelism. Backward:
+    d(pre) = bias_act_bwd(d(act), pre) (the bias gradient comes from the wgrad launch, as for
+    ``ColumnParallelLinear(bias_grad_from_output=True)``), then the linear's own backward."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, async_grad_allreduce):
+        ctx.sp = False
+        ctx.async_ar = async_grad_allreduce
+        ctx.has_bias = True
+        ctx.bias_p = bias
+        x2 = x.reshape(-1, x.shape[-1])
+        pre, act = _ext.ext().gemm_tn(x2, weight, 2, bias)
+        ctx.save_for_backward(x, weight, pre)
+        shape = tuple(x.shape[:-1]) + (weight.shape[0],)
+        return act.view(shape)
+
+    @staticmethod
+    def backward(ctx, dact):
+        x, weight, pre = ctx.saved_tensors
+        d2 = dact.reshape(-1, dact.shape[-1]).contiguous()
+        dpre = _ext.ext().bias_act_bwd(d2, pre, ctx.bias_p.detach(), 0, False, None)[0]
+        gi, dw, db = _linear_backward(ctx, dpre.view(tuple(x.shape[:-1]) + (weight.shape[0],)), x, weight)
+        return gi, dw, db, None
+
+
+def linear_bias_gelu_ok(x, layer) -> bool:
+    """The fused fc1 + bias + GeLU path applies: CUDA, 16-bit, no sequence parallelism, a bias, and
+    a shape gemm_tn supports."""
+    if not (_FUSED_BIAS_GELU and x.is_cuda and layer.bias is not None and not layer.sequence_parallel
+            and x.dtype in (torch.bfloat16, torch.float16) and layer.weight.dtype == x.dtype
+            and layer.bias.dtype == x.dtype and x.is_contiguous() and not layer.gather_output):
+        return False
+    x2 = x.view(-1, x.shape[-1])
+    return bool(_ext.ext().gemm_tn_supported(x2, layer.weight))
+
+
+def linear_bias_gelu(x, layer):
+    """gelu_tanh(fc1(x) + b) through ``LinearBiasGeLU`` (call only when ``linear_bias_gelu_ok``)."""
+    if not layer.async_ar:
+        x = copy_to_tensor_model_parallel_region(x)
+    return LinearBiasGeLU.apply(x, layer.weight, layer.bias, layer.async_ar)
 
 
 class LMHeadCrossEntropy(torch.autograd.Function):
