@@ -91,6 +91,16 @@ def main():
         ract = C.bias_act_fwd(h, b, 0)
         eact = ((act.float() - ract.float()).abs().max()).item()
         res["fc1_bias_gelu"] = {"N": N, "K": K, "max_abs_err_vs_unfused": eact, "ours_ms": [], "lib_ms": []}
+    if "fc2_dgrad" in names:
+        # fc2 dgrad with the GeLU backward in the epilogue vs the library GEMM + bias_act_bwd
+        N, K = SHAPES["fc2_dgrad"]
+        dy, w2t, dout = data["fc2_dgrad"]
+        b1 = torch.randn(N, device=dev, dtype=torch.bfloat16) * 0.1
+        pre1 = torch.randn(M, N, device=dev, dtype=torch.bfloat16)
+        got = C.gemm_tn(dy, w2t, 3, b1, dout, None, a.max_blocks, 0, pre1)[0].clone()
+        ref = C.bias_act_bwd(torch.mm(dy, w2t.t()), pre1, b1, 0, False, None)[0]
+        ed = ((got.float() - ref.float()).abs().max() / ref.float().abs().max()).item()
+        res["fc2_dgrad_dgelu"] = {"N": N, "K": K, "max_rel_err_vs_unfused": ed, "ours_ms": [], "lib_ms": []}
     if a.ablate:
         out_ab = {}
         for n in names:
@@ -116,6 +126,11 @@ def main():
                 timeit(lambda: C.gemm_tn(x, w, 2, b, out, o2, a.max_blocks), a.reps))
             res["fc1_bias_gelu"]["lib_ms"].append(
                 timeit(lambda: C.bias_act_fwd(torch.mm(x, w.t(), out=out), b, 0), a.reps))
+        if "fc2_dgrad" in names:
+            res["fc2_dgrad_dgelu"]["ours_ms"].append(
+                timeit(lambda: C.gemm_tn(dy, w2t, 3, b1, dout, None, a.max_blocks, 0, pre1), a.reps))
+            res["fc2_dgrad_dgelu"]["lib_ms"].append(
+                timeit(lambda: C.bias_act_bwd(torch.mm(dy, w2t.t(), out=dout), pre1, b1, 0, False, None), a.reps))
     tot_o = tot_l = 0.0
     for n, r in res.items():
         o = sorted(r["ours_ms"])[len(r["ours_ms"]) // 2]
@@ -123,7 +138,7 @@ def main():
         fl = 2.0 * M * r["N"] * r["K"]
         r.update(ours_med_ms=round(o, 4), lib_med_ms=round(lb, 4), ours_tflops=round(fl / o / 1e9, 1),
                  lib_tflops=round(fl / lb / 1e9, 1), speedup=round(lb / o, 3))
-        if n != "fc1_bias_gelu":
+        if n not in ("fc1_bias_gelu", "fc2_dgrad_dgelu"):
             tot_o += o
             tot_l += lb
         print(f"{n:14s} N {r['N']:5d} K {r['K']:5d}  ours {o:.4f} ms ({r['ours_tflops']:.0f} TF/s)  "

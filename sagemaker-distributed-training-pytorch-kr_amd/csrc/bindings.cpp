@@ -422,14 +422,20 @@ bool gemm_tn_supported(Tensor a, Tensor b) {
 }
 
 std::vector<Tensor> gemm_tn(Tensor a, Tensor b, int64_t epi, OptT bias, OptT out, OptT out2, int64_t max_blocks,
-                            int64_t var) {
+                            int64_t var, OptT aux) {
   TORCH_CHECK(gemm_tn_supported(a, b), "gemm_tn: unsupported operands");
-  TORCH_CHECK(epi >= 0 && epi <= 2, "gemm_tn: epilogue");
+  TORCH_CHECK(epi >= 0 && epi <= 3, "gemm_tn: epilogue");
   const int64_t M = a.size(0), N = b.size(0), K = a.size(1);
   if (epi >= 1) {
     TORCH_CHECK(bias.has_value(), "gemm_tn: the epilogue needs a bias");
     need_contig(*bias, "bias");
     TORCH_CHECK(bias->numel() == N && bias->scalar_type() == a.scalar_type(), "gemm_tn: bias mismatch");
+  }
+  if (epi == 3) {
+    TORCH_CHECK(aux.has_value(), "gemm_tn: the GeLU-backward epilogue needs the pre-activation");
+    need_contig(*aux, "aux");
+    TORCH_CHECK(aux->numel() == M * N && aux->scalar_type() == a.scalar_type() && aux->device() == a.device(),
+                "gemm_tn: pre-activation mismatch");
   }
   auto mk = [&](const OptT& o, const char* n) {
     if (!o) return torch::empty({M, N}, a.options());
@@ -441,8 +447,8 @@ std::vector<Tensor> gemm_tn(Tensor a, Tensor b, int64_t epi, OptT bias, OptT out
   Tensor c = mk(out, "out");
   Tensor c2 = epi == 2 ? mk(out2, "out2") : Tensor();
   check(smdt_gemm_tn_var(dcode(a), (int)epi, a.data_ptr(), b.data_ptr(), c.data_ptr(),
-                         epi == 2 ? c2.data_ptr() : nullptr, optr(bias), M, N, K, (int)max_blocks, (int)var,
-                         cur_stream()),
+                         epi == 2 ? c2.data_ptr() : nullptr, optr(bias), epi == 3 ? aux->data_ptr() : nullptr, M,
+                         N, K, (int)max_blocks, (int)var, cur_stream()),
         "gemm_tn");
   if (epi == 2) return {c, c2};
   return {c};
@@ -861,7 +867,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_tn_supported", &gemm_tn_supported, arg("a"), arg("b"));
   m.def("gemm_tn", &gemm_tn, arg("a"), arg("b"), arg("epi") = 0, arg("bias") = pybind11::none(),
         arg("out") = pybind11::none(), arg("out2") = pybind11::none(), arg("max_blocks") = 0,
-        arg("var") = 0);
+        arg("var") = 0, arg("aux") = pybind11::none());
   m.def("wgrad_mfma", &wgrad_mfma, arg("main_grad"), arg("dy"), arg("x"), arg("max_splits") = 0);
   m.def("wgrad_grouped", &wgrad_grouped, arg("main_grads"), arg("dys"), arg("xs"),
         arg("biases") = std::vector<Tensor>{}, arg("overwrite") = std::vector<bool>{});

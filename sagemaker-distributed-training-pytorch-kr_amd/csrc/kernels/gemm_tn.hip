@@ -5,6 +5,8 @@
 //   EPI_NONE       C = acc
 //   EPI_BIAS       C = acc + bias[n]
 //   EPI_BIAS_GELU  C = acc (the pre-activation the backward needs) and C2 = gelu_tanh(acc + bias[n])
+//   EPI_DGELU      C = acc * gelu_tanh'(pre[m, n] + bias[n]) — the fc2 dgrad with the GeLU backward
+//                  of the fc1 activation applied in its epilogue (bias_act_bwd's pass, fused)
 //                  — Megatron's bias_gelu fusion (/root/reference/3_training_megatron-lm/megatron/
 //                  arguments.py:819-821, bias_gelu_fusion=True in 3_training_megatron-lm.ipynb)
 //                  moved into the fc1 GEMM: the [tokens, 4h] pre-activation is never re-read.
@@ -45,16 +47,16 @@ namespace smdt {
 namespace gt {
 
 constexpr int kT = 256;                  // output tile edge
-constexpr int kBK = 32;                  // K per stage
+constexpr int kBK = 64;                  // K per stage
 constexpr int kThreads = 512;
-constexpr int kRowB = kBK * 2;           // 64-B LDS rows
-constexpr int kOp = kT * kRowB;          // 16 KB: one operand of a stage
+constexpr int kRowB = kBK * 2;           // 128-B LDS rows: every DMA request is a whole line
+constexpr int kOp = kT * kRowB;          // 32 KB: one operand of a stage
 constexpr int kSlot = 2 * kOp;           // A + B
-constexpr int kNSlot = 4;
-constexpr int kGl = kOp / 1024 / 8;      // 1-KB DMA wave-instructions per wave per operand (2)
+constexpr int kNSlot = 2;
+constexpr int kGl = kOp / 2 / 1024 / 8;  // 1-KB DMA wave-instructions per wave per 128-row half (2)
 constexpr int kEpiB = 32 * 128;          // per-wave epilogue staging: 2 x 16 rows x 64 columns of 16-bit
 
-enum { EPI_NONE = 0, EPI_BIAS = 1, EPI_BIAS_GELU = 2 };
+enum { EPI_NONE = 0, EPI_BIAS = 1, EPI_BIAS_GELU = 2, EPI_DGELU = 3 };
 
 using lds_void = __attribute__((address_space(3))) void;
 using f16x8 = __attribute__((ext_vector_type(8))) _Float16;
@@ -113,10 +115,13 @@ struct Args {
   void* C;
   void* C2;
   const void* bias;
+  const void* aux;   // EPI_DGELU: the GeLU pre-activation [M, N] (without the bias)
   int M, N, K;
   int ntn;      // N / 256
+  int ntm;      // M / 256
+  int gm;       // tile order: groups of gm row blocks x all column blocks, rows fastest inside
   int tiles;    // (M / 256) * ntn
-  int nt;       // K / 32 (a multiple of 4)
+  int nt;       // K / 64 (even)
 };
 
 // Stream cursor: K-step `pos` of this workgroup's tile sequence (wave-uniform).
@@ -154,15 +159,21 @@ __device__ __forceinline__ void dma2(i32x4 rsrc, uint32_t soff, uint32_t v0, uin
       : "memory");
 }
 
-// Loads hidden from hipcc's wait bookkeeping (retired by our own counted wait + a "+v" statement
-// naming the destination, so the compiler cannot touch the register before the data lands).
-__device__ __forceinline__ void load16_hidden(u32x4& d, const void* p) {
-  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(d) : "v"(p) : "memory");
+// One 1-KB LDS-DMA wave-instruction (same form as dma2).
+__device__ __forceinline__ void dma1(i32x4 rsrc, uint32_t soff, uint32_t v0, uint32_t lds) {
+  uint32_t keep;
+  asm volatile(
+      "s_nop 4\n\t"
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %4\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %1, %2, %3 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(v0), "s"(rsrc), "s"(soff), "s"(lds)
+      : "memory");
 }
-// retires a hidden load that is older than the 2 youngest DMA halves (4 wave-instructions)
-__device__ __forceinline__ void wait_reg4(u32x4& a) {
-  asm volatile("s_waitcnt vmcnt(4)" : "+v"(a) :: "memory");
-}
+
 
 // This lane's index, re-made where it is used: asm volatile is never hoisted out of the tile loop,
 // so the epilogue's lane-derived addresses hold no VGPRs across the main loop (the compiler kept
@@ -187,11 +198,13 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
 
 // VAR: diagnostic ablations for benchmarks/bench_gemm_tn.py only (the library runs VAR = 0):
 // bit 0 no in-loop DMA, bit 1 no in-loop fragment reads, bit 2 no wave stagger, bit 3 no stores,
-// bit 5 plain (L2-allocating) output stores instead of sc1.
-template <class E, int EPI, bool TRICKLE, int VAR = 0>
+// bit 5 sc1 (L2-bypassing) output stores instead of plain ones; (host) bit 7 / 8 tile groups of 1 / 4
+// row blocks instead of 8.
+template <class E, int EPI, int VAR = 0>
 __global__ __launch_bounds__(kThreads, 1) void gemm_tn_kernel(const Args g) {
   using V = typename V8<E>::t;
-  // [slot][A 16 KB | B 16 KB] x 4, then 4 KB of epilogue staging per wave (160 KB: the whole LDS)
+  // [A slot 0 | A slot 1 | B slot 0 | B slot 1] 32 KB each, then 4 KB of epilogue staging per
+  // wave (160 KB: the whole LDS)
   __shared__ __attribute__((aligned(1024))) char L[kNSlot * kSlot + kThreads / 64 * kEpiB];
 
   const int lane = threadIdx.x & 63;
@@ -205,33 +218,48 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_tn_kernel(const Args g) {
   const uint32_t rowb = (uint32_t)g.K * 2;   // bytes per operand row
   const uint64_t Ab = (uint64_t)g.A, Bb = (uint64_t)g.B;
 
-  // ---- fragment read bases: row (lane & 15) of a 16-row block, chunk lane >> 4 swizzled by
-  // f(row) = -(row >> 2) & 3; the wave's A rows are 128 wr .., its B rows 64 wc ..
+  // ---- fragment reads: row (lane & 15) of a 16-row block, 16-byte chunk 4 ks + (lane >> 4),
+  // XOR-swizzled by row bits 1..3 (every ds_read_b128 lane group hits 16 distinct bank slots);
+  // the wave's A rows are 128 wr .., its B rows 64 wc ..; LDS = [A slot 0 | A slot 1 | B slot 0 |
+  // B slot 1], 32 KB each, so one base register per (operand, ks) reaches both slots within the
+  // 16-bit ds_read offset
   const uint32_t l0 = lds_addr(L);
-  const uint32_t lo = (lane & 15) * kRowB + 16 * ((lane >> 4) ^ ((4 - ((lane >> 2) & 3)) & 3));
-  const uint32_t ra = l0 + 128 * wr * kRowB + lo;
-  const uint32_t rbq = l0 + kOp + 64 * wc * kRowB + lo;
-  // slots 2, 3 lie beyond the 16-bit ds_read offset field: their own base registers (opaque, so
-  // the compiler does not re-derive one address register per fragment from the slot 0 base)
-  uint32_t ra_hi = ra + 2 * kSlot, rb_hi = rbq + 2 * kSlot;
-  asm volatile("" : "+v"(ra_hi), "+v"(rb_hi));
+  uint32_t ra[2], rbq[2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    const uint32_t lo = (lane & 15) * kRowB + 16 * ((4 * ks + (lane >> 4)) ^ ((lane >> 1) & 7));
+    ra[ks] = l0 + 128 * wr * kRowB + lo;
+    rbq[ks] = l0 + 2 * kOp + 64 * wc * kRowB + lo;
+  }
   auto rd = [&](uint32_t addr) -> V {
     return *(const V*)(__attribute__((address_space(3))) const char*)(uintptr_t)addr;
   };
 
-  // ---- per-lane DMA byte offsets: wave-instruction j writes rows 16 (2 wave + j) + lane / 4,
-  // slot lane % 4, which holds chunk slot ^ f(row)
+  // ---- per-lane DMA byte offsets: wave-instruction j of a 128-row half writes rows
+  // 8 (2 wave + j) + lane / 8, 16-byte slot lane % 8, which holds chunk slot ^ f(row)
   uint32_t voff[kGl];
 #pragma unroll
   for (int j = 0; j < kGl; ++j) {
-    const int r = 16 * (kGl * wave + j) + (lane >> 2);
-    const int c = (lane & 3) ^ ((4 - ((r >> 2) & 3)) & 3);
+    const int r = 8 * (kGl * wave + j) + (lane >> 3);
+    const int c = (lane & 7) ^ ((r >> 1) & 7);
     voff[j] = (uint32_t)r * rowb + 16 * c;
   }
   const uint32_t my_lds = (uint32_t)(kGl * wave) * 1024;
+  const uint32_t half_b = 128 * rowb;
 
+  // tile t -> (row block, column block): groups of gm row blocks, row fastest inside a group, so
+  // the 32 consecutive tiles an XCD runs together share few A and B panels in its L2
+  auto coords = [&](int t, int& tm, int& tn) {
+    const int per = g.gm * g.ntn;
+    const int grp = t / per, first = grp * g.gm;
+    const int gsz = min(g.ntm - first, g.gm);
+    const int r = t - grp * per;
+    tm = first + r % gsz;
+    tn = r / gsz;
+  };
   auto tile_base = [&](Cur& c) {
-    const int tm = c.tile / g.ntn, tn = c.tile - tm * g.ntn;
+    int tm, tn;
+    coords(c.tile, tm, tn);
     c.a = Ab + (uint64_t)tm * kT * rowb;
     c.b = Bb + (uint64_t)tn * kT * rowb;
     c.k = 0;
@@ -247,50 +275,38 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_tn_kernel(const Args g) {
       c.k += kBK * 2;
     }
   };
-  // DMA of operand op (0 A, 1 B) of cursor c's stage into its ring slot (c.pos % 4)
-  auto issue = [&](const Cur& c, int op) {
-    dma2(srd(op ? c.b : c.a), c.k, voff[0], voff[1],
-         l0 + (uint32_t)(c.pos & (kNSlot - 1)) * kSlot + op * kOp + my_lds);
+  // DMA of half h (0 A rows 0..127, 1 A rows 128..255, 2 / 3 the same of B) of cursor c's stage
+  // into its slot (c.pos & 1)
+  auto issue = [&](const Cur& c, int h) {
+    dma2(srd(h < 2 ? c.a : c.b), c.k + ((h & 1) ? half_b : 0u), voff[0], voff[1],
+         l0 + (uint32_t)(h >> 1) * 2 * kOp + (uint32_t)(c.pos & 1) * kOp + (h & 1) * (kOp / 2) + my_lds);
   };
 
   f32x4 acc[8][4];
-  V fa[4], fb[4];
-  if constexpr ((VAR & 2) != 0) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) { fa[i] = rd(ra + i * 1024); fb[i] = rd(rbq + i * 1024); }
-  }
+  V fa[8][2], fb[4][2];
 
-  // ---- prologue: A / B of stages 0, 1 and A of stage 2 in flight; wait for stage 0
-  Cur cb, ca;  // cursors of the next B issue (stage u + 2) and the next A issue (stage u + 3)
+  // ---- prologue: stages 0 and 1 in flight, wait for stage 0
+  Cur cd;   // cursor of the next DMA (stage u + 2 while stage u runs)
+  Cur cb;   // the stage whose B halves the next p0 issues (u + 1)
   {
     Cur c0;
     c0.pos = 0; c0.kt = 0; c0.tile = rb;
     tile_base(c0);
     Cur c1 = c0; advance(c1);
-    Cur c2 = c1; advance(c2);
-    issue(c0, 0); issue(c0, 1); issue(c1, 0); issue(c1, 1); issue(c2, 0);
-    cb = c2;
-    ca = c2; advance(ca);
+    issue(c0, 0); issue(c0, 1); issue(c0, 2); issue(c0, 3);
+    issue(c1, 0); issue(c1, 1);   // (stage 1's B: stage 0's p0)
+    cd = c1; advance(cd);
+    cb = c1;
   }
-  wait_vm<3 * kGl>();   // the 3 youngest halves may stay in flight
+  wait_vm<2 * kGl>();   // stage 1's A halves may stay in flight
   __builtin_amdgcn_s_barrier();
   if (wr && !(VAR & 4)) __builtin_amdgcn_s_barrier();   // stagger: waves 4-7 one interval behind
 
   int otile = rb;
   constexpr int NOUT = EPI == EPI_BIAS_GELU ? 2 : 1;
-  // Epilogue, half trickled: rows 0..63 of the wave's finished tile are stored at once, rows
-  // 64..127 wait as packed 16-bit values (pend, 32 VGPRs: all 128 rows would spill) and are
-  // stored over the NEXT tile's first 4 stages, one 16-row block per stage: each lane writes its
-  // 4 x 8-byte pieces (4 consecutive n of one row) into the wave's LDS staging, reads back 16-byte
-  // row chunks, and every global store instruction writes 8 whole 128-byte lines. (Stored at the
-  // tile's end instead, the 256 workgroups — which finish their tiles together — put a 32 MB
-  // burst on HBM and the next tile's operand DMA queued behind it: +25 % on a K = 1024 GEMM.)
-  // The bias is added, and the activation computed, from the rounded 16-bit pre-activation at
-  // store time — the same arithmetic as the separate bias_act_fwd pass it replaces.
-  u32x2 pend[4][4];   // blocks 4..7 of the finished tile
-  u32x4 bias_w;              // 8 bias values of this lane's 16-byte column chunk
-  bool has_pend = false;
-  int ptile = 0;             // tile of the pending values
+  constexpr int kStores = 16 * NOUT;   // 16-byte stores per wave of one epilogue
+  u32x4 bias_w;                        // 8 bias values of this lane's 16-byte column chunk
+  (void)bias_w;
   const uint32_t epi_l = l0 + kNSlot * kSlot + wave * kEpiB;
 
   auto sync = [&]() {
@@ -298,19 +314,112 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_tn_kernel(const Args g) {
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
   };
+  auto mfma_q = [&](int mh, int ks) {   // 64 x 64 quadrant rows 64 mh .., one 32-deep k-step
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[4 * mh + i][j] = mma(fb[j][ks], fa[4 * mh + i][ks], acc[4 * mh + i][j]);
+  };
+  // One 64-deep stage in slot SL, four phases of 16 MFMAs each:
+  //   p0 reads A rows 0..63 and all 64 B rows of the wave (16 ds_read_b128), DMA of B of stage
+  //      u + 1 (the other slot), MFMAs rows 0..63 x k 0..31;
+  //   p1 reads A rows 64..127 (8 ds_read_b128), rows 0..63 x k 32..63;
+  //   p2 rows 64..127 x k 0..31;
+  //   p3 DMA of A of stage u + 2 into this slot (its reads retired two barriers back), wait for
+  //      stage u + 1 (stage u + 2's A halves stay in flight, plus the epilogue's stores when this
+  //      is a tile's first stage), rows 64..127 x k 32..63.
+  // A tile's last stage also issues B of stage u + 2 in p3 (ahead of the epilogue's stores, so the
+  // next tile's first waits never cover them), and its first stage then skips the p0 DMA.
+  auto stage = [&](auto slc, auto lastc, bool first) {
+    constexpr int SL = decltype(slc)::value;
+    constexpr bool LAST = decltype(lastc)::value;
+    if constexpr (EPI != EPI_NONE && LAST) {
+      // this tile's 64 bias values of the wave, by LDS-DMA into the second half of the wave's
+      // staging area (lanes 8.. re-load the same 128 bytes): no register held through the stage
+      int otm, otn;
+      coords(otile, otm, otn);
+      dma1(srd((uint64_t)((const E*)g.bias + otn * kT + 64 * wc)), 0u, (uint32_t)(lane_now() & 7) * 16,
+           epi_l + 2048);
+    }
+    // ---------------- p0
+    if (!(VAR & 2)) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) fa[i][ks] = rd(ra[ks] + SL * kOp + i * 16 * kRowB);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) fb[j][ks] = rd(rbq[ks] + SL * kOp + j * 16 * kRowB);
+    }
+    if (!(VAR & 1) && !first) { issue(cb, 2); issue(cb, 3); }
+    sync();
+    __builtin_amdgcn_s_setprio(1);
+    mfma_q(0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    sync();
+    // ---------------- p1
+    if (!(VAR & 2)) {
+#pragma unroll
+      for (int i = 4; i < 8; ++i)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) fa[i][ks] = rd(ra[ks] + SL * kOp + i * 16 * kRowB);
+    }
+    sync();
+    __builtin_amdgcn_s_setprio(1);
+    mfma_q(0, 1);
+    __builtin_amdgcn_s_setprio(0);
+    sync();
+    // ---------------- p2
+    sync();
+    __builtin_amdgcn_s_setprio(1);
+    mfma_q(1, 0);
+    __builtin_amdgcn_s_setprio(0);
+    sync();
+    // ---------------- p3
+    if (!(VAR & 1)) { issue(cd, 0); issue(cd, 1); }
+    cb = cd;
+    if (LAST && !(VAR & 1)) { issue(cb, 2); issue(cb, 3); }
+    advance(cd);
+    // younger than stage u + 1's last half: stage u + 2's halves issued here
+    constexpr int kW = (LAST ? 4 : 2) * kGl;
+    if (first) wait_vm<kW + kStores>();
+    else wait_vm<kW>();
+    sync();
+    __builtin_amdgcn_s_setprio(1);
+    mfma_q(1, 1);
+    __builtin_amdgcn_s_setprio(0);
+    sync();
+  };
+
   auto lds_w8 = [&](uint32_t addr, u32x2 v) {
     *(__attribute__((address_space(3))) u32x2*)(uintptr_t)addr = v;
   };
   auto lds_r16 = [&](uint32_t addr) -> u32x4 {
     return *(__attribute__((address_space(3))) const u32x4*)(uintptr_t)addr;
   };
-  // bias / activation on 8 consecutive values of one row (chunk rc)
-  auto finish8 = [&](u32x4 v, int o) -> u32x4 {
+  // bias / activation on 8 consecutive values of one row (chunk rc), o = 0 the first output
+  auto finish8 = [&](u32x4 v, int o, u32x4 pv) -> u32x4 {
     if constexpr (EPI == EPI_NONE) {
       return v;
     } else {
-      if (EPI == EPI_BIAS_GELU && o == 0) return v;
+      if (EPI == EPI_BIAS_GELU && o == 0) return v;   // the pre-activation
       u32x2 lo = {v[0], v[1]}, hi = {v[2], v[3]};
+      if constexpr (EPI == EPI_DGELU) {   // v = d(activation), pv = pre-activation
+        u32x2 plo = {pv[0], pv[1]}, phi = {pv[2], pv[3]};
+        float x[8], z[8], b[8];
+        u32x2 blo = {bias_w[0], bias_w[1]}, bhi = {bias_w[2], bias_w[3]};
+        unpack4<E>(lo, *reinterpret_cast<float(*)[4]>(x));
+        unpack4<E>(hi, *reinterpret_cast<float(*)[4]>(x + 4));
+        unpack4<E>(plo, *reinterpret_cast<float(*)[4]>(z));
+        unpack4<E>(phi, *reinterpret_cast<float(*)[4]>(z + 4));
+        unpack4<E>(blo, *reinterpret_cast<float(*)[4]>(b));
+        unpack4<E>(bhi, *reinterpret_cast<float(*)[4]>(b + 4));
+#pragma unroll
+        for (int e = 0; e < 8; ++e) x[e] = x[e] * gelu_tanh_grad(z[e] + b[e]);
+        const u32x2 ol = pack4<E>(x[0], x[1], x[2], x[3]), oh = pack4<E>(x[4], x[5], x[6], x[7]);
+        return u32x4{ol[0], ol[1], oh[0], oh[1]};
+      }
       u32x2 blo = {bias_w[0], bias_w[1]}, bhi = {bias_w[2], bias_w[3]};
       float x[8], b[8];
       unpack4<E>(lo, *reinterpret_cast<float(*)[4]>(x));
@@ -323,204 +432,83 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_tn_kernel(const Args g) {
       return u32x4{ol[0], ol[1], oh[0], oh[1]};
     }
   };
-  // Store 8 rows (half h of pending block k) from the staging area: NOUT store instructions.
-  auto block_rows = [&](int k, int h, u32x4 v) {
-    const int ln = lane_now(), rr = ln >> 3, rc = ln & 7;   // read side: row (+ 8 h), 16-byte chunk
-    const int ptm = ptile / g.ntn, ptn = ptile - ptm * g.ntn;
+  // Epilogue through the wave's 4 KB of LDS, one 16-row block at a time: each lane writes its
+  // 4 x 8-byte pieces (4 consecutive n of one row), then reads back 16-byte row chunks, so every
+  // global store instruction writes 8 whole 128-byte lines (the accumulator layout alone gives
+  // 16 rows x 32 bytes per instruction). The bias is added, and the activation computed, from the
+  // rounded 16-bit pre-activation — the arithmetic of the separate bias_act_fwd pass it replaces.
+  auto epilogue = [&]() {
+    if constexpr (EPI != EPI_NONE) {
+      wait_vm<4 * kGl>();   // the bias DMA: older than stage u + 2's 4 halves (and retired already)
+      bias_w = lds_r16(epi_l + 2048 + (lane_now() & 7) * 16);
+    }
+    int otm, otn;
+    coords(otile, otm, otn);
     const int64_t N = g.N;
-    const int64_t off = (int64_t)(ptm * kT + 128 * wr + 16 * k + 8 * h + rr) * N + ptn * kT + 64 * wc + 8 * rc;
+    // EPI_DGELU: the pre-activation rows of the whole wave tile (16 x 16 B per lane, in the
+    // read-side layout), issued before any block so their latency overlaps the first blocks
+    u32x4 pre_v[8][2];
+    if constexpr (EPI == EPI_DGELU) {
+      const int ln = lane_now(), rr = ln >> 3, rc = ln & 7;
+      const E* pre = (const E*)g.aux + (int64_t)(otm * kT + 128 * wr + rr) * N + otn * kT + 64 * wc + 8 * rc;
 #pragma unroll
-    for (int o = 0; o < NOUT; ++o) {
-      E* dst = (E*)(o == 0 ? g.C : g.C2) + off;
-      const u32x4 w = finish8(v, o + (EPI == EPI_BIAS ? 1 : 0));
-      if constexpr ((VAR & 8) != 0) asm volatile("" ::"v"(w));
-      else if constexpr ((VAR & 32) != 0) *(u32x4*)dst = w;
-      else store16_sc1(dst, w);
+      for (int k = 0; k < 8; ++k)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) pre_v[k][h] = *(const u32x4*)(pre + (int64_t)(16 * k + 8 * h) * N);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) pre_v[k][0] = pre_v[k][1] = u32x4{0, 0, 0, 0};
     }
-  };
-  // 16-row block k (4 packed pieces per lane) -> the wave's staging area (half k & 1), read back
-  // as two 8-row halves
-  auto stage_block = [&](int k, const u32x2 (&pc)[4], u32x4& r0, u32x4& r1) {
-    // write side: row r16 of the block, columns 16 j + 4 qq; read side: row rr (+ 8), chunk rc
-    const int ln = lane_now(), r16 = ln & 15, qq = ln >> 4, rr = ln >> 3, rc = ln & 7;
-    const uint32_t area = epi_l + (k & 1) * 2048;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int chunk = (2 * j + (qq >> 1)) ^ (r16 & 7);
-      lds_w8(area + r16 * 128 + chunk * 16 + (qq & 1) * 8, pc[j]);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // other lanes' pieces are in place
-    __builtin_amdgcn_sched_barrier(0);
-    r0 = lds_r16(area + rr * 128 + ((rc ^ (rr & 7)) * 16));
-    r1 = lds_r16(area + (rr + 8) * 128 + ((rc ^ ((rr + 8) & 7)) * 16));
-  };
-  u32x4 held;   // second half of the block staged in phase (a), stored in phase (b)
-
-  // One stage. SK: trickle window stage (0..3: store pending block 4 + SK; 4: the stage after
-  // the window; -1: none). LAST: the tile's last stage (bias load). The phase (b) wait leaves the 3
-  // younger DMA halves in flight plus every store / bias load issued after the awaited half.
-  auto stage = [&](auto slotc, auto skc, auto lastc) {
-    constexpr int slot = decltype(slotc)::value;
-    constexpr int SK = decltype(skc)::value;
-    constexpr bool LAST = decltype(lastc)::value;
-    constexpr uint32_t so = (slot & 1) * kSlot;
-    const uint32_t ra_s = slot < 2 ? ra : ra_hi;
-    const uint32_t rb_s = slot < 2 ? rbq : rb_hi;
-    if constexpr (EPI != EPI_NONE && LAST) {   // this tile's bias for the read-side chunk
-      const int otn = otile - (otile / g.ntn) * g.ntn;
-      load16_hidden(bias_w, (const E*)g.bias + otn * kT + 64 * wc + 8 * (lane_now() & 7));
-    }
-    // ---------------- phase (a): A rows 0..63 x B rows 0..63 of the wave
-#pragma unroll
-    for (int i = 0; i < 4; ++i) if (!(VAR & 2)) fa[i] = rd(ra_s + so + i * 16 * kRowB);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) if (!(VAR & 2)) fb[j] = rd(rb_s + so + j * 16 * kRowB);
-    if constexpr (SK >= 0 && SK < 4) {
-      if (has_pend) {
-        u32x4 r0;
-        stage_block(4 + SK, pend[SK], r0, held);
-        block_rows(4 + SK, 0, r0);
-      }
-    }
-    if (!(VAR & 1)) issue(cb, 1);
-    advance(cb);
-    sync();
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = mma(fb[j], fa[i], acc[i][j]);
-    __builtin_amdgcn_s_setprio(0);
-    sync();
-    // ---------------- phase (b): A rows 64..127
-#pragma unroll
-    for (int i = 0; i < 4; ++i) if (!(VAR & 2)) fa[i] = rd(ra_s + so + (64 + i * 16) * kRowB);
-    if constexpr (SK >= 0 && SK < 4) {
-      if (has_pend) block_rows(4 + SK, 1, held);
-    }
-    if (!(VAR & 1)) issue(ca, 0);
-    advance(ca);
-    // stores younger than the awaited half (B of the next stage, issued in phase (a) of the
-    // previous stage, after that phase's stores): phase (b) of the previous stage, (a) and (b) of
-    // this one — and, at the first stage, the 8 direct stores of the tile's retirement
-    // (SK 9: first stage after a retirement that stored all 8 blocks at once)
-    constexpr int kSt = NOUT * (SK == 0 ? 10 : (SK > 0 && SK < 4) ? 3 : SK == 4 ? 1 : SK == 9 ? 16 : 0);
-    constexpr int kW = 3 * kGl + ((EPI != EPI_NONE && LAST) ? 1 : 0);
-    if (kSt > 0 && has_pend) wait_vm<kW + kSt>();
-    else wait_vm<kW>();
-    sync();
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[4 + i][j] = mma(fb[j], fa[i], acc[4 + i][j]);
-    __builtin_amdgcn_s_setprio(0);
-    sync();
-  };
-
-  // finished tile: blocks 0..3 stored now, blocks 4..7 -> pend (16-bit pre-activation / product);
-  // without TRICKLE (fewer than 12 stages per tile) all 8 blocks are stored now
-  auto retire_tile = [&]() {
-    if constexpr (EPI != EPI_NONE) wait_reg4(bias_w);   // older than the last stage's 2 DMA halves
-    ptile = otile;
-#pragma unroll
-    for (int k = 0; k < (TRICKLE ? 4 : 8); ++k) {
-      u32x2 pc[4];
+    for (int k = 0; k < 8; ++k) {
+      const int ln = lane_now(), r16 = ln & 15, qq = ln >> 4, rr = ln >> 3, rc = ln & 7;
+      const uint32_t area = epi_l + (k & 1) * 2048;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const f32x4 v = acc[k][j];
-        pc[j] = pack4<E>(v[0], v[1], v[2], v[3]);
-        acc[k][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        const int chunk = (2 * j + (qq >> 1)) ^ (r16 & 7);
+        lds_w8(area + r16 * 128 + chunk * 16 + (qq & 1) * 8, pack4<E>(v[0], v[1], v[2], v[3]));
       }
-      u32x4 r0, r1;
-      stage_block(k, pc, r0, r1);
-      block_rows(k, 0, r0);
-      block_rows(k, 1, r1);
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // other lanes' pieces are in place
+      __builtin_amdgcn_sched_barrier(0);
+      u32x4 rv[2];
+      rv[0] = lds_r16(area + rr * 128 + ((rc ^ (rr & 7)) * 16));
+      rv[1] = lds_r16(area + (rr + 8) * 128 + ((rc ^ ((rr + 8) & 7)) * 16));
+      const int64_t off = (int64_t)(otm * kT + 128 * wr + 16 * k + rr) * N + otn * kT + 64 * wc + 8 * rc;
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int o = 0; o < NOUT; ++o) {
+          E* dst = (E*)(o == 0 ? g.C : g.C2) + off + (int64_t)(8 * h) * N;
+          const u32x4 w = finish8(rv[h], o + (EPI == EPI_BIAS ? 1 : 0), pre_v[k][h]);
+          if constexpr ((VAR & 8) != 0) asm volatile("" ::"v"(w));
+          else if constexpr ((VAR & 32) != 0) store16_sc1(dst, w);
+          else *(u32x4*)dst = w;
+        }
       __builtin_amdgcn_sched_barrier(0);
     }
-    if constexpr (TRICKLE) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const f32x4 v = acc[4 + i][j];
-          pend[i][j] = pack4<E>(v[0], v[1], v[2], v[3]);
-          acc[4 + i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-        }
-    }
-    has_pend = true;
   };
-  using I0 = std::integral_constant<int, 0>;
-  using I1 = std::integral_constant<int, 1>;
-  using I2 = std::integral_constant<int, 2>;
-  using I3 = std::integral_constant<int, 3>;
-  using NO = std::integral_constant<int, -1>;
+  using S0 = std::integral_constant<int, 0>;
+  using S1 = std::integral_constant<int, 1>;
   using F_ = std::false_type;
   using T_ = std::true_type;
 
+  // tile loop outside, stage pairs inside (nt even: every tile starts in slot 0; the last pair is
+  // peeled for the bias load); the DMA cursor runs ahead across the tile boundary on its own
+  for (int it = 0; it < ntile; ++it) {
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < 8; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // tile loop outside, stages inside (nt % 4 == 0 and nt >= 12: every tile starts on slot 0; the
-  // first 8 stages are peeled for the store window, the last 4 for the bias load); the DMA
-  // cursors run ahead across the tile boundary on their own
-  for (int it = 0; it < ntile && TRICKLE; ++it) {
-    stage(I0{}, std::integral_constant<int, 0>{}, F_{});
-    stage(I1{}, std::integral_constant<int, 1>{}, F_{});
-    stage(I2{}, std::integral_constant<int, 2>{}, F_{});
-    stage(I3{}, std::integral_constant<int, 3>{}, F_{});
-    stage(I0{}, std::integral_constant<int, 4>{}, F_{});
-    stage(I1{}, NO{}, F_{});
-    stage(I2{}, NO{}, F_{});
-    stage(I3{}, NO{}, F_{});
-    for (int kt = 8; kt < g.nt - 4; kt += 4) {
-      stage(I0{}, NO{}, F_{});
-      stage(I1{}, NO{}, F_{});
-      stage(I2{}, NO{}, F_{});
-      stage(I3{}, NO{}, F_{});
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int kt = 0; kt < g.nt - 2; kt += 2) {
+      stage(S0{}, F_{}, kt == 0 && it > 0);
+      stage(S1{}, F_{}, false);
     }
-    stage(I0{}, NO{}, F_{});
-    stage(I1{}, NO{}, F_{});
-    stage(I2{}, NO{}, F_{});
-    stage(I3{}, NO{}, T_{});
-    retire_tile();
+    stage(S0{}, F_{}, g.nt == 2 && it > 0);
+    stage(S1{}, T_{}, false);
+    epilogue();
     otile += G;
-  }
-  using S9 = std::integral_constant<int, 9>;
-  for (int it = 0; it < ntile && !TRICKLE; ++it) {
-    if (g.nt == 4) {
-      stage(I0{}, S9{}, F_{});
-      stage(I1{}, NO{}, F_{});
-      stage(I2{}, NO{}, F_{});
-      stage(I3{}, NO{}, T_{});
-    } else {
-      stage(I0{}, S9{}, F_{});
-      stage(I1{}, NO{}, F_{});
-      stage(I2{}, NO{}, F_{});
-      stage(I3{}, NO{}, F_{});
-      for (int kt = 4; kt < g.nt - 4; kt += 4) {
-        stage(I0{}, NO{}, F_{});
-        stage(I1{}, NO{}, F_{});
-        stage(I2{}, NO{}, F_{});
-        stage(I3{}, NO{}, F_{});
-      }
-      stage(I0{}, NO{}, F_{});
-      stage(I1{}, NO{}, F_{});
-      stage(I2{}, NO{}, F_{});
-      stage(I3{}, NO{}, T_{});
-    }
-    retire_tile();
-    otile += G;
-  }
-  // the last tile's pending half: nothing left to hide it behind
-#pragma unroll
-  for (int k = 0; k < (TRICKLE ? 4 : 0); ++k) {
-    u32x4 r0, r1;
-    stage_block(4 + k, pend[k], r0, r1);
-    block_rows(4 + k, 0, r0);
-    block_rows(4 + k, 1, r1);
   }
   if (!wr && !(VAR & 4)) __builtin_amdgcn_s_barrier();  // matching barrier count for the unstaggered half
   wait_vm<0>();   // trailing re-read DMAs land before the workgroup's LDS is released
@@ -532,7 +520,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_tn_kernel(const Args g) {
 using namespace smdt;
 
 extern "C" int smdt_gemm_tn_supported(int64_t M, int64_t N, int64_t K) {
-  return M > 0 && N > 0 && M % gt::kT == 0 && N % gt::kT == 0 && K % (4 * gt::kBK) == 0 &&
+  return M > 0 && N > 0 && M % gt::kT == 0 && N % gt::kT == 0 && K % (2 * gt::kBK) == 0 &&
          M * K < (1ll << 31) && N * K < (1ll << 31) && (M / gt::kT) * (N / gt::kT) < (1ll << 30);
 }
 
@@ -547,38 +535,33 @@ static int gt_num_cus() {
 }
 
 extern "C" hipError_t smdt_gemm_tn(int dtype, int epi, const void* a, const void* b, void* c, void* c2,
-                                   const void* bias, int64_t M, int64_t N, int64_t K, int max_blocks,
-                                   hipStream_t st) {
-  return smdt_gemm_tn_var(dtype, epi, a, b, c, c2, bias, M, N, K, max_blocks, 0, st);
+                                   const void* bias, const void* aux, int64_t M, int64_t N, int64_t K,
+                                   int max_blocks, hipStream_t st) {
+  return smdt_gemm_tn_var(dtype, epi, a, b, c, c2, bias, aux, M, N, K, max_blocks, 0, st);
 }
 
 extern "C" hipError_t smdt_gemm_tn_var(int dtype, int epi, const void* a, const void* b, void* c, void* c2,
-                                       const void* bias, int64_t M, int64_t N, int64_t K, int max_blocks,
-                                       int var, hipStream_t st) {
+                                       const void* bias, const void* aux, int64_t M, int64_t N, int64_t K,
+                                       int max_blocks, int var, hipStream_t st) {
   if (dtype != 1 && dtype != 2) return hipErrorInvalidValue;
   if (!smdt_gemm_tn_supported(M, N, K)) return hipErrorInvalidValue;
-  if (epi < 0 || epi > 2 || (epi >= 1 && !bias) || (epi == 2 && !c2)) return hipErrorInvalidValue;
+  if (epi < 0 || epi > 3 || (epi >= 1 && !bias) || (epi == 2 && !c2) || (epi == 3 && !aux)) return hipErrorInvalidValue;
   gt::Args g;
-  g.A = a; g.B = b; g.C = c; g.C2 = c2; g.bias = bias;
+  g.A = a; g.B = b; g.C = c; g.C2 = c2; g.bias = bias; g.aux = aux;
   g.M = (int)M; g.N = (int)N; g.K = (int)K;
   g.ntn = (int)(N / gt::kT);
+  g.ntm = (int)(M / gt::kT);
+  g.gm = (var & 128) ? 1 : (var & 256) ? 4 : 8;   // 8 measured best (fc1 / fc2 / qkv shapes)
   g.tiles = (int)(M / gt::kT) * g.ntn;
-  g.nt = (int)(K / gt::kBK);   // stages of 32, a multiple of 4
+  g.nt = (int)(K / gt::kBK);   // stages of 64, even
   int grid = gt_num_cus();
   if (max_blocks > 0 && max_blocks < grid) grid = max_blocks;
   if (grid > g.tiles) grid = g.tiles;
-  // half-trickled epilogue from 12 stages per tile (its 4-stage store window + peeled groups)
-  const bool tr = g.nt >= 12 && !(var & 16);
-#define SMDT_GT(E, P)                                                                                      \
-  do {                                                                                                     \
-    if (tr) hipLaunchKernelGGL((gt::gemm_tn_kernel<E, P, true>), dim3(grid), dim3(gt::kThreads), 0, st, g); \
-    else hipLaunchKernelGGL((gt::gemm_tn_kernel<E, P, false>), dim3(grid), dim3(gt::kThreads), 0, st, g);   \
-  } while (0)
-#define SMDT_GTV(V) hipLaunchKernelGGL((gt::gemm_tn_kernel<bf16, 0, true, V>), dim3(grid), dim3(gt::kThreads), 0, st, g)
+#define SMDT_GT(E, P) hipLaunchKernelGGL((gt::gemm_tn_kernel<E, P>), dim3(grid), dim3(gt::kThreads), 0, st, g)
+#define SMDT_GTV(V) hipLaunchKernelGGL((gt::gemm_tn_kernel<bf16, 0, V>), dim3(grid), dim3(gt::kThreads), 0, st, g)
   if (var != 0) {   // diagnostic ablations: bf16, no epilogue
     if (dtype != 1 || epi != 0) return hipErrorInvalidValue;
     switch (var) {
-      case 16: SMDT_GT(bf16, 0); break;   // every block stored at the tile's end (no trickle)
       case 1: SMDT_GTV(1); break;
       case 2: SMDT_GTV(2); break;
       case 3: SMDT_GTV(3); break;
@@ -586,15 +569,17 @@ extern "C" hipError_t smdt_gemm_tn_var(int dtype, int epi, const void* a, const 
       case 8: SMDT_GTV(8); break;
       case 11: SMDT_GTV(11); break;
       case 32: SMDT_GTV(32); break;
+      case 128: SMDT_GTV(0); break;    // (tile order only: g.gm)
+      case 256: SMDT_GTV(0); break;
       default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
   }
 #undef SMDT_GTV
   if (dtype == 1) {
-    if (epi == 0) SMDT_GT(bf16, 0); else if (epi == 1) SMDT_GT(bf16, 1); else SMDT_GT(bf16, 2);
+    if (epi == 0) SMDT_GT(bf16, 0); else if (epi == 1) SMDT_GT(bf16, 1); else if (epi == 2) SMDT_GT(bf16, 2); else SMDT_GT(bf16, 3);
   } else {
-    if (epi == 0) SMDT_GT(f16, 0); else if (epi == 1) SMDT_GT(f16, 1); else SMDT_GT(f16, 2);
+    if (epi == 0) SMDT_GT(f16, 0); else if (epi == 1) SMDT_GT(f16, 1); else if (epi == 2) SMDT_GT(f16, 2); else SMDT_GT(f16, 3);
   }
 #undef SMDT_GT
   return hipGetLastError();

@@ -108,14 +108,16 @@ hipError_t smdt_flash_bwd(int dtype, const void* q, const void* k, const void* v
                           uint64_t offset, hipStream_t st);
 
 // gemm_tn.hip: C[M, N] = A[M, K] . B[N, K]^T (16-bit in / out, fp32 accumulate) with an epilogue:
-// epi 0 none, 1 + bias[n], 2 C = pre-activation and C2 = gelu_tanh(C + bias[n]) (bias_gelu fusion).
+// epi 0 none, 1 + bias[n], 2 C = pre-activation and C2 = gelu_tanh(C + bias[n]) (bias_gelu fusion),
+// 3 C = product * gelu_tanh'(aux + bias[n]) (fc2 dgrad + GeLU backward; aux = pre-activation [M, N]).
 // max_blocks <= 0: one persistent workgroup per CU.
 int smdt_gemm_tn_supported(int64_t M, int64_t N, int64_t K);
 hipError_t smdt_gemm_tn(int dtype, int epi, const void* a, const void* b, void* c, void* c2, const void* bias,
-                        int64_t M, int64_t N, int64_t K, int max_blocks, hipStream_t st);
+                        const void* aux, int64_t M, int64_t N, int64_t K, int max_blocks, hipStream_t st);
 // diagnostic ablations of the same kernel (benchmarks only): var bits as gemm_tn_kernel's VAR
 hipError_t smdt_gemm_tn_var(int dtype, int epi, const void* a, const void* b, void* c, void* c2, const void* bias,
-                            int64_t M, int64_t N, int64_t K, int max_blocks, int var, hipStream_t st);
+                            const void* aux, int64_t M, int64_t N, int64_t K, int max_blocks, int var,
+                            hipStream_t st);
 
 // wgrad_gemm.hip: main_grad[N, K] (fp32) += dy[M, N]^T . x[M, K] (bf16, or fp16 with dtype 2)
 int smdt_wgrad_supported(int64_t M, int64_t N, int64_t K);

@@ -361,6 +361,11 @@ class ParallelMLP(nn.Module):
     def forward(self, x):
         act = self.cfg.activation
         if act == "gelu" and self.cfg.bias_gelu_fusion and tp.linear_bias_gelu_ok(x, self.fc1):
+            if tp.fused_gelu_mlp_ok(x, self):
+                # both GeLU halves inside the GEMMs: fc1 + bias + GeLU forward, fc2 dgrad + GeLU
+                # backward (gemm_tn.hip epilogues)
+                y = tp.FusedGeLUMLP.apply(x, self.fc1.weight, self.fc1.bias, self.fc2.weight)
+                return y, self.fc2.bias
             # fc1 GEMM + bias + GeLU in one launch (gemm_tn.hip's bias-GeLU epilogue)
             return self.fc2(tp.linear_bias_gelu(x, self.fc1))
         h, b = self.fc1(x)

@@ -800,6 +800,50 @@ class LinearBiasGeLU(torch.autograd.Function):
         return gi, dw, db, None
 
 
+class FusedGeLUMLP(torch.autograd.Function):
+    """fc2(gelu_tanh(fc1(x) + b1)) at TP = 1 with both GeLU halves inside the GEMMs (gemm_tn.hip):
+    forward fc1 + bias + GeLU in one launch (EPI_BIAS_GELU), backward fc2's dgrad with the GeLU
+    backward in its epilogue (EPI_DGELU: d(pre) = (dY W2) * gelu'(pre + b1), the [tokens, 4h]
+    d(activation) is never written). Saves x, pre and act — what the unfused path saves. fc2's bias
+    is added by the caller (skip_bias_add), as in ``ParallelMLP``. Same math as Megatron's
+    ParallelMLP with bias_gelu_fusion (/root/reference/3_training_megatron-lm/megatron/
+    arguments.py:819-821)."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2):
+        C = _ext.ext()
+        x2 = x.reshape(-1, x.shape[-1])
+        pre, act = C.gemm_tn(x2, w1, 2, b1)
+        y = linear_rows(act, w2)
+        ctx.save_for_backward(x, w1, w2, pre, act)
+        ctx.b1 = b1
+        return y.view(tuple(x.shape[:-1]) + (w2.shape[0],))
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w1, w2, pre, act = ctx.saved_tensors
+        C = _ext.ext()
+        b1 = ctx.b1
+        dy2 = dy.reshape(-1, dy.shape[-1]).contiguous()
+        w2t = _dgrad_weight_t(w2)
+        if w2t is not None and C.gemm_tn_supported(dy2, w2t):
+            dz = C.gemm_tn(dy2, w2t, 3, b1.detach(), None, None, 0, 0, pre)[0]
+        else:
+            dz = C.bias_act_bwd(dgrad(dy2, w2, w2t).contiguous(), pre, b1.detach(), 0, False, None)[0]
+        dw2, _ = _wgrad_and_bias(w2, None, dy2, act)
+        x2 = x.reshape(-1, x.shape[-1])
+        dx = dgrad(dz, w1, _dgrad_weight_t(w1))
+        dw1, db1 = _wgrad_and_bias(w1, b1, dz, x2)
+        return dx.view(x.shape), dw1, db1, dw2
+
+
+def fused_gelu_mlp_ok(x, mlp) -> bool:
+    """``FusedGeLUMLP`` applies: the fc1 + bias-GeLU conditions, TP = 1, fc2 without sequence
+    parallelism and with its bias left to the caller."""
+    return (_tp_size() == 1 and linear_bias_gelu_ok(x, mlp.fc1) and mlp.fc2.skip_bias_add
+            and not mlp.fc2.sequence_parallel and mlp.fc2.weight.dtype == x.dtype)
+
+
 def linear_bias_gelu_ok(x, layer) -> bool:
     """The fused fc1 + bias + GeLU path applies: CUDA, 16-bit, no sequence parallelism, a bias, and
     a shape gemm_tn supports."""

@@ -83,24 +83,56 @@ def test_gemm_tn_into_given_buffers_and_unsupported():
     assert not C.gemm_tn_supported(a.float(), b.float())
 
 
-@pytest.mark.parametrize("mode", ["fused_fc1", "all_linears"])
+@pytest.mark.parametrize("blocks", [0, 3])
+def test_gemm_tn_gelu_backward_epilogue(blocks):
+    """EPI_DGELU: out = (a . b^T) * gelu_tanh'(pre + bias), against the unfused path (the product
+    rounded to 16 bits, then bias_act_bwd) and the fp32 reference."""
+    C = _ext.ext()
+    torch.manual_seed(3)
+    M, N, K = 2048, 1024, 512
+    a = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    b = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) * 0.05
+    bias = torch.randn(N, device=DEV, dtype=torch.bfloat16)
+    pre = torch.randn(M, N, device=DEV, dtype=torch.bfloat16) * 2
+    got = C.gemm_tn(a, b, 3, bias, None, None, blocks, 0, pre)[0]
+    prod = a.float() @ b.float().t()
+    z = (pre.float() + bias.float()).requires_grad_()
+    torch.nn.functional.gelu(z, approximate="tanh").backward(torch.ones_like(z))
+    ref = prod * z.grad
+    assert _rel(got, ref) < 2e-2
+    unf = C.bias_act_bwd(prod.to(torch.bfloat16), pre, bias, 0, False, None)[0]
+    assert (got.float() - unf.float()).abs().max().item() <= 1e-2 * ref.abs().max().item()
+
+
+@pytest.mark.parametrize("mode", ["fused_mlp", "fused_fc1", "all_linears"])
 def test_gpt_step_on_gemm_tn_matches_fp32_reference(monkeypatch, mode):
-    """The flagship GPT step with fc1 + bias + GeLU as one gemm_tn launch ("fused_fc1"), and with
-    every supported forward / dgrad linear on gemm_tn as well ("all_linears"), against the fp32
-    PyTorch reference (the peaked-head case of test_model_gpu, whose gradients check every
-    parameter). The fused path must actually run: its calls are counted."""
+    """The flagship GPT step with both GeLU halves in the GEMMs ("fused_mlp": FusedGeLUMLP), with
+    only fc1 + bias + GeLU fused ("fused_fc1"), and with every supported forward / dgrad linear on
+    gemm_tn as well ("all_linears"), against the fp32 PyTorch reference (the peaked-head case of
+    test_model_gpu, whose gradients check every parameter). The fused paths must actually run:
+    their calls are counted."""
     import test_model_gpu as T
     from smdt_amd.parallel import tensor_parallel as tp
     monkeypatch.setattr(tp, "_FUSED_BIAS_GELU", True)
     if mode == "all_linears":
         monkeypatch.setattr(tp, "_GEMM_TN", "1")
         monkeypatch.setattr(tp, "_GEMM_TN_SHAPES", None)
-    calls = {"fused": 0}
-    orig = tp.linear_bias_gelu
+    calls = {"fc1": 0, "mlp": 0}
+    orig_fc1, orig_mlp = tp.linear_bias_gelu, tp.FusedGeLUMLP.forward
 
-    def counted(x, layer):
-        calls["fused"] += 1
-        return orig(x, layer)
-    monkeypatch.setattr(tp, "linear_bias_gelu", counted)
+    def counted_fc1(x, layer):
+        calls["fc1"] += 1
+        return orig_fc1(x, layer)
+
+    def counted_mlp(ctx, *args):
+        calls["mlp"] += 1
+        return orig_mlp(ctx, *args)
+    monkeypatch.setattr(tp, "linear_bias_gelu", counted_fc1)
+    monkeypatch.setattr(tp.FusedGeLUMLP, "forward", staticmethod(counted_mlp))
+    if mode == "fused_fc1":
+        monkeypatch.setattr(tp, "fused_gelu_mlp_ok", lambda x, mlp: False)
     T.test_gpt_step_matches_fp32_reference(torch.bfloat16, True)
-    assert calls["fused"] == 2   # both layers' MLPs
+    if mode == "fused_fc1":
+        assert calls == {"fc1": 2, "mlp": 0}   # both layers' MLPs
+    else:
+        assert calls == {"fc1": 0, "mlp": 2}
