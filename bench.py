@@ -154,6 +154,15 @@ def model_label(a, vocab):
     return f"{known.get((a.num_layers, a.hidden_size, a.num_attention_heads), 'gpt')} ({shape}, seq {a.seq_length})"
 
 
+def _mlp_fusion_desc():
+    """How the MLP's bias + GeLU runs (recorded in the JSON): inside the hand-written GEMMs
+    (gemm_tn.hip epilogues, TP = 1) or as the separate bias_act kernels."""
+    from smdt_amd.parallel import tensor_parallel as tpm
+    if not tpm._FUSED_BIAS_GELU:
+        return "bias_act kernels"
+    return "gemm_tn epilogues (fc1 bias+GeLU fwd, fc2 dgrad+GeLU bwd)"
+
+
 def enable_gemm_tuning(a, rank):
     """PyTorch TunableOp over torch's hipBLASLt / rocBLAS GEMMs.
 
@@ -489,6 +498,7 @@ def main():
                        "gemm_autotune": tuned,
                        "comm_stream_priority": comm_streams.describe()["comm_stream_priority"],
                        "optimizer_overlap": bool(getattr(ddp, "overlap_optimizer", False)),
+                       "mlp_gelu_fusion": _mlp_fusion_desc(),
                        "hip_graph": graph_note},
             **({} if emulated else {
                 "model_tflops_per_gpu": round(tps * fpt / n / 1e12, 2),

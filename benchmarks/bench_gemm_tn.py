@@ -107,7 +107,12 @@ def main():
             x, w, out = data[n]
             N, K = SHAPES[n]
             fl = 2.0 * M * N * K
+            ref = F.linear(x, w).float()
             for v in [0] + list(a.ablate):
+                if not (v & 9):   # variants that compute the product: check it
+                    got = C.gemm_tn(x, w, 0, None, out, None, a.max_blocks, v)[0].float()
+                    err = ((got - ref).abs().max() / ref.abs().max()).item()
+                    assert err < 1e-2, (n, v, err)
                 ts = [timeit(lambda: C.gemm_tn(x, w, 0, None, out, None, a.max_blocks, v), a.reps)
                       for _ in range(a.rounds)]
                 t = sorted(ts)[len(ts) // 2]

@@ -4,39 +4,38 @@
 // the cached W^T). Epilogues:
 //   EPI_NONE       C = acc
 //   EPI_BIAS       C = acc + bias[n]
-//   EPI_BIAS_GELU  C = acc (the pre-activation the backward needs) and C2 = gelu_tanh(acc + bias[n])
-//   EPI_DGELU      C = acc * gelu_tanh'(pre[m, n] + bias[n]) — the fc2 dgrad with the GeLU backward
-//                  of the fc1 activation applied in its epilogue (bias_act_bwd's pass, fused)
-//                  — Megatron's bias_gelu fusion (/root/reference/3_training_megatron-lm/megatron/
-//                  arguments.py:819-821, bias_gelu_fusion=True in 3_training_megatron-lm.ipynb)
-//                  moved into the fc1 GEMM: the [tokens, 4h] pre-activation is never re-read.
+//   EPI_BIAS_GELU  C = acc (the pre-activation the backward needs) and C2 = gelu_tanh(C + bias[n])
+//   EPI_DGELU      C = acc * gelu_tanh'(pre[m, n] + bias[n]): the fc2 dgrad with the GeLU backward
+//                  of the fc1 activation in its epilogue
+// The last two are Megatron's bias_gelu fusion (/root/reference/3_training_megatron-lm/megatron/
+// arguments.py:819-821, bias_gelu_fusion=True in 3_training_megatron-lm.ipynb) moved into the fc1
+// and fc2-dgrad GEMMs: the separate bias_act_fwd / bias_act_bwd passes over the [tokens, 4h]
+// tensors are gone (FusedGeLUMLP, parallel/tensor_parallel.py).
 //
 // Structure (after cdna_hip_programming.md §5's staged-MFMA GEMM rules; written for gfx950):
-//   * persistent: one 512-thread workgroup per CU walks its tiles (blockIdx remapped so the 32
-//     workgroups of an XCD take consecutive tiles, n fastest: they share A rows / B panels in that
-//     XCD's L2). The K-stages of ALL its tiles form one stream: the LDS-DMA prefetch runs across
-//     tile boundaries, so a tile's epilogue (registers -> global stores, no LDS) overlaps the next
-//     tile's operand loads;
-//   * 256 x 256 output tile, 32-deep K-stages in a ring of 4 LDS slots (A 256 x 32 + B 256 x 32,
-//     32 KB each, 128 KB), copied global -> LDS by buffer_load_dwordx4 ... lds. 64-B rows, 16-B
-//     chunks XOR-swizzled by row bits 2..3 (f = -(r >> 2) & 3: every ds_read_b128 lane group hits 16
-//     distinct bank slots); the swizzle is applied to the per-lane SOURCE offset, the LDS image
-//     stays lane-linear;
+//   * persistent: one 512-thread workgroup per CU walks its tiles; blockIdx is remapped so the 32
+//     workgroups of an XCD take consecutive tiles, ordered in groups of 8 row blocks (row fastest)
+//     so they share few A / B panels in that XCD's L2. The K-stages of ALL its tiles form one
+//     stream: the LDS-DMA prefetch runs across tile boundaries;
+//   * 256 x 256 output tile, 64-deep K-stages in 2 LDS slots per operand (128-B rows: every DMA
+//     request is a whole cache line — 32-deep stages doubled the L2 requests, profiles/r5_gemm_tn/),
+//     copied global -> LDS by buffer_load_dwordx4 ... lds with the XOR swizzle (row bits 1..3) on
+//     the per-lane SOURCE offset, so the LDS image stays lane-linear and the fragment reads are
+//     bank-conflict free;
 //   * 8 waves as 2 (m) x 4 (n), each 128 x 64 outputs = 8 x 4 accumulators of
 //     v_mfma_f32_16x16x32 (the bf16 shape gfx950 clocks higher on random data than 32x32x16);
-//   * a stage is two phases: (a) read A rows 0..63 of the wave + all its 64 B rows, 16 MFMAs;
-//     (b) read A rows 64..127, 16 MFMAs with the B fragments still in registers. A phase is a read
-//     interval (ds_reads + one half of a stage's DMA + at most one counted vmcnt) and an MFMA
-//     interval, separated by raw s_barriers; waves 4-7 run one barrier behind waves 0-3, so on
-//     every SIMD one wave's MFMAs run beside its partner's LDS reads and DMA issue;
+//   * a stage is four phases of 16 MFMAs; a phase is a read interval and an MFMA interval between
+//     raw s_barriers, and waves 4-7 run one interval behind waves 0-3, so on every SIMD one wave's
+//     MFMAs run beside its partner's LDS reads and DMA issue (the wave stagger is worth 8 %);
 //   * the operands are swapped in the MFMA (B rows as the A operand): each lane's accumulator
-//     then holds FOUR CONSECUTIVE n of one row m, stored as one 8-byte write per accumulator.
+//     holds four consecutive n of one row m; the epilogue stages 16-row blocks through 4 KB of
+//     LDS per wave and stores whole 128-B lines (16-byte stores).
 //
-// Prefetch schedule (stage u of the stream, slot u % 4): phase (a) issues B of stage u + 2,
-// phase (b) issues A of stage u + 3, and phase (b) waits for stage u + 1 (vmcnt(6): the three
-// younger halves stay in flight; +the epilogue's stores / bias loads where they sit between).
-// A slot is refilled two phases after its last read (b of stage u -> A of u + 4 at b of u + 1),
-// the distance that covers the staggered half's reads (retired by its lgkmcnt one barrier later).
+// Measured on MI355X at the GPT-2 345M step shapes (benchmarks/bench_gemm_tn.py): 0.85-0.92x
+// of hipBLASLt's tuned GEMM (MT256x256x64, 4 waves of 128 x 128 with AGPR accumulators, 1.3-1.5
+// PFLOP/s) alone, 1.02x (fc1 + bias + GeLU) and 1.05x (fc2 dgrad + GeLU backward) against the
+// library GEMM followed by the elementwise pass. A 4-wave 128 x 128-per-wave form of this kernel
+// (plain double buffering) measured 0.69 vs 0.47 ms on fc1 and was removed.
 #include "activations.h"
 #include "common.h"
 #include "launchers.h"

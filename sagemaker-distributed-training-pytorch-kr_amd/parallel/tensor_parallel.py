@@ -770,8 +770,12 @@ def _linear_backward(ctx, g, x, weight):
 # fc1 + bias + GeLU(tanh) as ONE GEMM launch (gemm_tn.hip EPI_BIAS_GELU): the epilogue writes the
 # pre-activation (kept for the backward) and the activation; the separate bias_act_fwd pass over
 # the [tokens, 4h] tensor is gone (Megatron's bias_gelu_fusion,
-# /root/reference/3_training_megatron-lm/megatron/arguments.py:819-821). SMDT_FUSED_BIAS_GELU=0 off.
-_FUSED_BIAS_GELU = os.environ.get("SMDT_FUSED_BIAS_GELU", "0") == "1"
+# /root/reference/3_training_megatron-lm/megatron/arguments.py:819-821); at TP = 1 the backward's
+# GeLU half goes into the fc2 dgrad's epilogue as well (FusedGeLUMLP). On by default: the GPT-2
+# 345M step measured 160.45 / 161.06 / 160.64 ms against 160.67 / 160.68 / 161.01 ms unfused (one
+# box, interleaved; profiles/r5_gemm_tn/) — the fused ops are 1.02x / 1.05x the library GEMM +
+# elementwise pass, the hand-written GEMM itself 0.85-0.92x hipBLASLt. SMDT_FUSED_BIAS_GELU=0 off.
+_FUSED_BIAS_GELU = os.environ.get("SMDT_FUSED_BIAS_GELU", "1") == "1"
 
 
 class LinearBiasGeLU(torch.autograd.Function):
