@@ -360,6 +360,9 @@ class ParallelMLP(nn.Module):
 
     def forward(self, x):
         act = self.cfg.activation
+        if act == "gelu" and self.cfg.bias_gelu_fusion and tp.sp_fused_gelu_mlp_ok(x, self):
+            # TP > 1 + sequence parallelism: the GeLU halves inside the ring-chunk GEMMs
+            return tp.SPFusedGeLUMLP.apply(x, self.fc1.weight, self.fc1.bias, self.fc2.weight), self.fc2.bias
         if act == "gelu" and self.cfg.bias_gelu_fusion and tp.linear_bias_gelu_ok(x, self.fc1):
             if tp.fused_gelu_mlp_ok(x, self):
                 # both GeLU halves inside the GEMMs: fc1 + bias + GeLU forward, fc2 dgrad + GeLU

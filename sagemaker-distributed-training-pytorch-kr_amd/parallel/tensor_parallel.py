@@ -848,6 +848,100 @@ def fused_gelu_mlp_ok(x, mlp) -> bool:
             and not mlp.fc2.sequence_parallel and mlp.fc2.weight.dtype == x.dtype)
 
 
+class SPFusedGeLUMLP(torch.autograd.Function):
+    """The sequence-parallel MLP of a TP > 1 rank with both GeLU halves inside the ring-chunk GEMMs
+    (the TP form of ``FusedGeLUMLP``; BASELINE config 3's tp2 + SP layers):
+
+      forward   fc1: ring all-gather of the SP chunks of x, each chunk's GEMM with the bias-GeLU
+                epilogue (gemm_tn EPI_BIAS_GELU) writing its rows of the pre-activation and the
+                activation; fc2: per-chunk GEMMs fused with the ring reduce-scatter (as
+                ``_RowSPLinear``);
+      backward  fc2: ring all-gather of dY, each chunk's dgrad with the GeLU backward in its
+                epilogue (EPI_DGELU) writing d(pre) directly — the [tokens, 4h / tp] d(activation)
+                and the separate bias_act_bwd pass are gone; fc1: dgrad chunks fused with the ring
+                reduce-scatter, the fc1 weight and bias gradients (one grouped-wgrad pass over
+                d(pre)) drained while the last chunk is in flight (as ``_ColumnSPLinear``).
+
+    The collectives, their order and the saved tensors (gathered x, pre, act) are those of the
+    unfused column / row SP linears, so a TP group whose ranks disagree on the gate could not
+    deadlock on the exchanges either (the gate depends on shapes and dtypes only). Megatron's
+    ParallelMLP with bias_gelu_fusion + sequence_parallel (/root/reference/3_training_megatron-lm/
+    megatron/arguments.py:819-821, 848-849)."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2):
+        C = _ext.ext()
+        group = _tp_group()
+        x = x.contiguous()
+        n = x.shape[0]
+        ws = dist.get_world_size(group)
+        rows = x.numel() // x.shape[-1]           # rows of one SP chunk
+        lead = (n * ws,) + tuple(x.shape[1:-1])
+        f = w1.shape[0]
+        pre = x.new_empty(lead + (f,))
+        act = x.new_empty(lead + (f,))
+        p2, a2 = pre.view(-1, f), act.view(-1, f)
+
+        def fc1_chunk(c, ch):
+            C.gemm_tn(ch.reshape(rows, ch.shape[-1]), w1, 2, b1, p2[c * rows:(c + 1) * rows],
+                      a2[c * rows:(c + 1) * rows])
+        total = ag_ring(x, group, fc1_chunk)
+        y = rs_ring(lambda c: torch.nn.functional.linear(act[c * n:(c + 1) * n], w2), group)
+        ctx.save_for_backward(total, w1, w2, pre, act)
+        ctx.b1 = b1
+        ctx.n = n
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        total, w1, w2, pre, act = ctx.saved_tensors
+        C = _ext.ext()
+        group = _tp_group()
+        b1 = ctx.b1
+        n = ctx.n
+        dy = dy.contiguous()
+        rows = dy.numel() // dy.shape[-1]
+        f = w1.shape[0]
+        dz = pre.new_empty(pre.shape)
+        d2, p2 = dz.view(-1, f), pre.view(-1, f)
+        w2t = _dgrad_weight_t(w2)
+        bd = b1.detach()
+
+        def fc2_dgrad_chunk(c, ch):
+            C.gemm_tn(ch.reshape(rows, ch.shape[-1]), w2t, 3, bd, d2[c * rows:(c + 1) * rows], None, 0, 0,
+                      p2[c * rows:(c + 1) * rows])
+        gfull = ag_ring(dy, group, fc2_dgrad_chunk, before_last_wait=_flush_wgrad)
+        dw2 = _wgrad(w2, gfull.reshape(-1, gfull.shape[-1]), act.reshape(-1, f))
+        res = {}
+
+        def wgrad():
+            res["dw"], res["db"] = _wgrad_and_bias(w1, b1, d2, total.reshape(-1, total.shape[-1]))
+            _flush_wgrad()
+        w1t = _dgrad_weight_t(w1)
+        dx = rs_ring(lambda c: dgrad(dz[c * n:(c + 1) * n], w1, w1t), group, wgrad)
+        if "dw" not in res:
+            wgrad()
+        return dx, res["dw"], res["db"], dw2
+
+
+def sp_fused_gelu_mlp_ok(x, mlp) -> bool:
+    """``SPFusedGeLUMLP`` applies: TP > 1 with the ring collective-matmul sequence-parallel linears,
+    fc1 with a bias and fc2 with its bias left to the caller, 16-bit CUDA operands, and every chunk
+    GEMM on a gemm_tn shape (SP-chunk rows and the local 4h a multiple of 256, h of 128).
+    Depends on shapes / dtypes / flags only, so every rank of the TP group decides alike."""
+    fc1, fc2 = mlp.fc1, mlp.fc2
+    if not (_FUSED_BIAS_GELU and _TP_OVERLAP and _tp_size() > 1 and x.is_cuda and fc1.sequence_parallel
+            and fc2.sequence_parallel and fc1.bias is not None and fc1.bias_grad_from_output
+            and fc2.skip_bias_add and not fc1.gather_output and x.dtype in (torch.bfloat16, torch.float16)
+            and fc1.weight.dtype == x.dtype and fc2.weight.dtype == x.dtype and fc1.bias.dtype == x.dtype
+            and _ext.use_kernels(x)):
+        return False
+    rows = x.numel() // x.shape[-1]
+    f, h = fc1.weight.shape
+    return (rows % 256 == 0 and f % 256 == 0 and h % 128 == 0 and fc2.weight.shape == (h, f)
+            and bool(_ext.ext().gemm_tn_supported(x.reshape(rows, h), fc1.weight)))
+
+
 def linear_bias_gelu_ok(x, layer) -> bool:
     """The fused fc1 + bias + GeLU path applies: CUDA, 16-bit, no sequence parallelism, a bias, and
     a shape gemm_tn supports."""

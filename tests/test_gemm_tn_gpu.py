@@ -136,3 +136,58 @@ def test_gpt_step_on_gemm_tn_matches_fp32_reference(monkeypatch, mode):
         assert calls == {"fc1": 2, "mlp": 0}   # both layers' MLPs
     else:
         assert calls == {"fc1": 0, "mlp": 2}
+
+
+def _emulated_tp2_sp_gpt_grads(fused, monkeypatch):
+    """One process as TP rank 0 of a tp2 + SP GPT (loopback TP group, ring collective-matmul
+    linears): one forward + backward with dropout off; the loss and the fp32 main_grad buffer.
+    SP chunks of 128 x 4 = 512 rows and a local 4h of 512: every chunk GEMM is a gemm_tn shape."""
+    from smdt_amd.models.gpt import GPTModel
+    from smdt_amd.models.transformer import TransformerConfig
+    from smdt_amd.parallel import state as ps
+    from smdt_amd.parallel import tensor_parallel as tp
+    from smdt_amd.parallel.distributed import DistributedDataParallel as DDP
+    monkeypatch.setattr(tp, "_FUSED_BIAS_GELU", fused)
+    calls = {"n": 0}
+    orig = tp.SPFusedGeLUMLP.forward
+
+    def counted(ctx, *args):
+        calls["n"] += 1
+        return orig(ctx, *args)
+    monkeypatch.setattr(tp.SPFusedGeLUMLP, "forward", staticmethod(counted))
+    ps.destroy_model_parallel()
+    ps.initialize_emulated_tensor_parallel(2, 1)
+    try:
+        cfg = TransformerConfig(num_layers=2, hidden_size=256, num_attention_heads=4, padded_vocab_size=1024,
+                                max_position_embeddings=256, hidden_dropout=0.0, attention_dropout=0.0,
+                                params_dtype=torch.bfloat16, sequence_parallel=True, seed=7)
+        model = GPTModel(cfg, device="cuda")
+        ddp = DDP(model, grad_dtype=torch.float32)
+        g = torch.Generator(device="cuda").manual_seed(13)
+        t = torch.randint(0, 1000, (4, 257), device="cuda", generator=g)
+        ddp.zero_grad_buffer()
+        loss = model(t[:, :-1], labels=t[:, 1:]).float().mean()
+        loss.backward()
+        ddp.finish_grad_sync()
+        torch.cuda.synchronize()
+        return loss.item(), ddp.grad_data.clone(), calls["n"]
+    finally:
+        ps.destroy_model_parallel()
+
+
+def test_sp_fused_gelu_mlp_matches_unfused(monkeypatch):
+    """SPFusedGeLUMLP (TP > 1 + SP: fc1 bias-GeLU and fc2-dgrad GeLU-backward epilogues in the
+    ring-chunk GEMMs) against the unfused column / row SP linears + bias_act passes on the same
+    emulated tp2 rank: loss and every parameter's fp32 gradient (fc1 weight and bias, fc2 weight,
+    and everything upstream of the MLP through d(x)). The fused path must run (counted) and the
+    unfused one must not take it. Mutation check: dropping the GeLU derivative from the EPI_DGELU
+    epilogue (d(pre) = dY W2) moves the fc1 gradients by O(1) of their max and fails here."""
+    lf, gf, nf = _emulated_tp2_sp_gpt_grads(True, monkeypatch)
+    lu, gu, nu = _emulated_tp2_sp_gpt_grads(False, monkeypatch)
+    assert nf == 2 and nu == 0
+    assert abs(lf - lu) <= 2e-3 * abs(lu)
+    scale = gu.abs().max().item()
+    assert scale > 0
+    assert (gf - gu).abs().max().item() <= 2e-2 * scale
+    # every parameter, relative to its own magnitude
+    assert torch.linalg.vector_norm(gf - gu).item() <= 2e-2 * torch.linalg.vector_norm(gu).item()
