@@ -169,6 +169,9 @@ def enable_gemm_tuning(a, rank):
     --tunableop 1 (default): load the per-shape winners measured on MI355X and committed under
     profiles/tunableop/ (no tuning at run time); tune on first use only if that file is absent.
     --tunableop 2: re-tune every shape (minutes) and write the results to --tune-out.
+    --tunableop 3: load the committed winners and tune only the shapes missing from them; the
+                   table (loaded + new rows) is written to --tune-out at exit (merge it into
+                   profiles/tunableop/ with scripts/merge_tunableop.py).
     --tunableop 0: library heuristics only.
     """
     if not (a.tunableop and torch.cuda.is_available()):
@@ -186,6 +189,8 @@ def enable_gemm_tuning(a, rank):
         tun.set_max_tuning_duration(a.tune_ms)
         out = a.tune_out or os.path.join(tempfile.gettempdir(), "smdt_tunableop_r%d.csv")
         tun.set_filename(out % rank if "%d" in out else out)
+        if a.tunableop == 3 and os.path.exists(TUNED_GEMMS):
+            tun.read_file(TUNED_GEMMS)
         return "tuning"
     except Exception as e:  # pragma: no cover
         print(f"[bench] TunableOp unavailable: {e!r}", file=sys.stderr)
