@@ -31,6 +31,9 @@ SHAPES = {  # name: (N, K) of out[M, N] = a[M, K] . b[N, K]^T
     "qkv_dgrad": (1024, 3072),
     "fc1_dgrad": (1024, 4096),
     "fc2_dgrad": (4096, 1024),
+    # tp2 stage-rank ring chunks (run with --m 16384)
+    "fc1_chunk": (2048, 1024),
+    "qkv_chunk": (1536, 1024),
 }
 
 
@@ -109,7 +112,7 @@ def main():
             fl = 2.0 * M * N * K
             ref = F.linear(x, w).float()
             for v in [0] + list(a.ablate):
-                if not (v & 9):   # variants that compute the product: check it
+                if not (v & 9) or v in (64, 1024):   # variants that compute the product: check it
                     got = C.gemm_tn(x, w, 0, None, out, None, a.max_blocks, v)[0].float()
                     err = ((got - ref).abs().max() / ref.abs().max()).item()
                     assert err < 1e-2, (n, v, err)
@@ -118,6 +121,14 @@ def main():
                 t = sorted(ts)[len(ts) // 2]
                 out_ab[f"{n}/var{v}"] = round(t, 4)
                 print(f"{n:12s} var {v:2d}: {t:.4f} ms ({fl / t / 1e9:.0f} TF/s)", flush=True)
+                if n in ("fc1_fwd", "fc1_chunk") and v in (0, 64, 1024):   # bias + GeLU epilogue
+                    bb = torch.randn(N, device=dev, dtype=torch.bfloat16) * 0.1
+                    o2 = torch.empty_like(out)
+                    ts = [timeit(lambda: C.gemm_tn(x, w, 2, bb, out, o2, a.max_blocks, v), a.reps)
+                          for _ in range(a.rounds)]
+                    t = sorted(ts)[len(ts) // 2]
+                    out_ab[f"{n}/gelu/var{v}"] = round(t, 4)
+                    print(f"{n:12s} gelu var {v:2d}: {t:.4f} ms ({fl / t / 1e9:.0f} TF/s)", flush=True)
         print(json.dumps({"M": M, "ablate_ms": out_ab}))
         return
     for r in range(a.rounds):

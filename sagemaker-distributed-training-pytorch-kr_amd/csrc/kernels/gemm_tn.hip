@@ -121,6 +121,7 @@ struct Args {
   int gm;       // tile order: groups of gm row blocks x all column blocks, rows fastest inside
   int tiles;    // (M / 256) * ntn
   int nt;       // K / 64 (even)
+  int skew;     // odd workgroups start this many ~8k-cycle sleeps late (de-phased epilogues), 0 none
 };
 
 // Stream cursor: K-step `pos` of this workgroup's tile sequence (wave-uniform).
@@ -212,6 +213,9 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_tn_kernel(const Args g) {
   const int G = gridDim.x;
   const int rb = xcd_remap(blockIdx.x, G);
   if (rb >= g.tiles) return;  // (host sizes G <= tiles; whole workgroup, before any barrier)
+  if (g.skew > 0 && (blockIdx.x & 1)) {
+    for (int i = 0; i < g.skew; ++i) __builtin_amdgcn_s_sleep(127);
+  }
   const int ntile = (g.tiles - rb + G - 1) / G;
   const int total = ntile * g.nt;
   const uint32_t rowb = (uint32_t)g.K * 2;   // bytes per operand row
@@ -553,6 +557,15 @@ extern "C" hipError_t smdt_gemm_tn_var(int dtype, int epi, const void* a, const 
   g.gm = (var & 128) ? 1 : (var & 256) ? 4 : 8;   // 8 measured best (fc1 / fc2 / qkv shapes)
   g.tiles = (int)(M / gt::kT) * g.ntn;
   g.nt = (int)(K / gt::kBK);   // stages of 64, even
+  g.skew = 0;
+  if (var & 64) {   // diagnostic: odd workgroups start about half a tile late (~2k cycles per stage, 8k per sleep)
+    g.skew = g.nt / 8 > 0 ? g.nt / 8 : 1;
+    var &= ~64;
+  }
+  if (var & 1024) {   // diagnostic: odd workgroups start about a quarter tile late
+    g.skew = g.nt / 16 > 0 ? g.nt / 16 : 1;
+    var &= ~1024;
+  }
   int grid = gt_num_cus();
   if (max_blocks > 0 && max_blocks < grid) grid = max_blocks;
   if (grid > g.tiles) grid = g.tiles;
