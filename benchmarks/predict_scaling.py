@@ -167,19 +167,70 @@ def predict(m: dict) -> list:
     return rows
 
 
+def _ag_exposed(g: float, t_x: float, W: int, k: int, wq: float = 0.0) -> float:
+    """Compute-stream time lost to an all-gather collective-matmul beyond its GEMMs (g ms over all
+    W chunks) and the weight-gradient GEMMs drained before the last wait (wq): the transfer runs
+    as k row pieces back to back on the engine stream (t_x ms in all); the local chunk's GEMM runs
+    beside the first piece, the peers' rows of piece j once piece j has landed
+    (comm/tp_direct.TpDirect.all_gather; the ring is k = W - 1 pieces of one chunk each, its
+    local chunk first)."""
+    piece = t_x / k
+    c = g / W
+    per = g * (W - 1) / (W * k)
+    for j in range(k):
+        if j == k - 1:
+            c += wq
+        c = max(c, (j + 1) * piece) + per
+    return c - (g + wq)
+
+
+def _rs_exposed(g: float, t_x: float, k: int, wq: float = 0.0) -> float:
+    """The same for a reduce-scatter collective-matmul: piece j's partial GEMMs (g / k), then its
+    reduce-scatter on the engine stream (t_x / k) beside piece j + 1's GEMMs; the queued
+    weight-gradient GEMMs (wq) run before the last wait (TpDirect.reduce_scatter, ``rs_ring``)."""
+    c = e = 0.0
+    for _ in range(k):
+        c += g / k
+        e = max(e, c) + t_x / k
+    c += wq
+    return max(c, e) - (g + wq)
+
+
+def gpt3_exchange_model(W_ms: float, layers: int, mb: int, t_x: float, tp: int, k: int) -> dict:
+    """Exposed SP-exchange time per step for one tp4 stage: per layer and micro-batch the 8
+    exchanges (forward AG qkv / RS proj / AG fc1 / RS fc2, backward AG fc2 / RS fc1 / AG proj /
+    RS qkv) simulated against their own GEMMs, which are priced from the measured weight-gradient
+    GEMM time of a micro-batch (``W`` of the stage's F/B/W split: the forward and the input-gradient
+    GEMMs have the same FLOPs) split over the four linears by FLOPs (qkv 3, proj 1, fc1 4, fc2 4 of
+    12 h^2); the backward's exchanges get their linear's weight-gradient GEMM as the drained queue.
+    Plus the embedding output's reduce-scatter per micro-batch (no GEMM partner)."""
+    g = W_ms / layers
+    share = {"qkv": 3 / 12, "proj": 1 / 12, "fc1": 4 / 12, "fc2": 4 / 12}
+    gl = {n: g * f for n, f in share.items()}
+    fwd = (_ag_exposed(gl["qkv"], t_x, tp, k) + _rs_exposed(gl["proj"], t_x, k)
+           + _ag_exposed(gl["fc1"], t_x, tp, k) + _rs_exposed(gl["fc2"], t_x, k))
+    bwd = (_ag_exposed(gl["fc2"], t_x, tp, k, wq=gl["fc2"]) + _rs_exposed(gl["fc1"], t_x, k, wq=gl["fc1"])
+           + _ag_exposed(gl["proj"], t_x, tp, k, wq=gl["proj"]) + _rs_exposed(gl["qkv"], t_x, k, wq=gl["qkv"]))
+    per_step = layers * mb * (fwd + bwd) + mb * t_x
+    return {"fwd_per_layer_mb": fwd, "bwd_per_layer_mb": bwd, "exposed_ms": per_step}
+
+
 def predict_gpt3(m: dict) -> list:
     """GPT-3 6.7B, tp4 pp2 + SP on 8 GPUs (BASELINE config #5): per-rank compute from the emulated
     stages; the sequence-parallel exchanges per rank and step (8 per layer and micro-batch — the
     all-gathers before QKV and fc1 and the reduce-scatters after proj and fc2, forward, and their
     mirror images in backward (the gathered inputs are kept for the weight gradients, no re-gather)
     — plus the embedding's / LM head's 2 per micro-batch, each 3/4 of a [2048, 4, 4096] bf16
-    activation; round 4 corrected an earlier count of 10 per layer) over ONE link per direction (the ring) or over the
-    three links of the TP group (a direct exchange); the part of it that the rank's GEMMs (~60 % of
-    its compute, the TP collectives' overlap partners) cannot hide is exposed."""
+    activation) over ONE link per direction (the ring) or over the three links of the TP group (a
+    direct exchange). The exposed part is SIMULATED per exchange against its own GEMMs
+    (``gpt3_exchange_model``): the ring's chunk-by-chunk overlap, and the direct engine gathering /
+    reducing whole chunks (1 piece: only the local chunk's GEMM beside the gather, every partial
+    before the reduce-scatter — the round-4 engine) or in 2 / 4 row pieces (round 5,
+    ``SMDT_TP_DIRECT_PIECES``)."""
     if not ("gpt3_tp4_stage0" in m and "gpt3_tp4_stage1" in m):
         return []
     rows = []
-    sl, mb, h, layers = 2048, 4, 4096, 16
+    sl, mb, h, layers, tp = 2048, 4, 4096, 16, 4
     xfer_bytes = 8 * (8 * layers + 2) * 0.75 * sl * mb * h * 2   # 8 micro-batches per step
     tok = 32 * sl                                           # tp4 x pp2 = 8 GPUs: ONE replica, 32 sequences
     act = (sl // 4) * mb * h * 2
@@ -188,14 +239,24 @@ def predict_gpt3(m: dict) -> list:
     zbh1 = min((r for r in base if r["layout"].split(", ")[-1] in ("zbh1", "zbh2")), key=lambda r: r["predicted_ms"])
     sched = zbh1["layout"].split(", ")[-1]
     comp = zbh1["compute_ms"]
-    for links, name in ((1, "ring, one link per direction"), (3, "direct, the TP group's 3 links")):
-        t_x = link_ms(xfer_bytes, links)
-        exposed = max(0.0, t_x - 0.6 * comp)
+    slow = max(("gpt3_tp4_stage0", "gpt3_tp4_stage1"), key=lambda n: m[n]["ms_per_step"])
+    W_ms = m[slow]["fbw_ms"]["W"]
+    ex_bytes = 0.75 * sl * mb * h * 2                       # one exchange, per rank
+    for links, k, name in ((1, tp - 1, "ring, one link per direction"),
+                           (3, 1, "direct, 3 links, whole chunks (round 4)"),
+                           (3, 2, "direct, 3 links, 2 row pieces"),
+                           (3, 4, "direct, 3 links, 4 row pieces")):
+        t_x = link_ms(ex_bytes, links)
+        mdl = gpt3_exchange_model(W_ms, layers, 8, t_x, tp, k)
+        exposed = mdl["exposed_ms"]
         pred = zbh1["predicted_ms"] + exposed
         rows.append({"N": 8, "model": "gpt3-6.7b", "layout": f"tp4pp2+sp, {sched}, TP exchange {name}",
                      "compute_ms": comp, "stage_ms": zbh1["stage_ms"], "bubble_ms": zbh1["bubble_ms"],
                      "exposed_comm_ms": round(exposed, 1), "predicted_ms": round(pred, 1), "tokens_per_step": tok,
-                     "note": f"{xfer_bytes / 1e9:.1f} GB of SP exchanges per rank per step = {t_x:.0f} ms on {links} link(s)"})
+                     "note": f"{xfer_bytes / 1e9:.1f} GB of SP exchanges per rank per step = "
+                             f"{link_ms(xfer_bytes, links):.0f} ms on {links} link(s); exposed per layer and "
+                             f"micro-batch fwd {mdl['fwd_per_layer_mb']:.3f} / bwd {mdl['bwd_per_layer_mb']:.3f} ms "
+                             f"against {W_ms / layers:.3f} ms of GEMMs per pass"})
     return rows
 
 

@@ -34,6 +34,9 @@ import torch
 import torch.distributed as dist
 
 TUNED: dict = {}
+# Row pieces per direct exchange (SMDT_TP_DIRECT_PIECES): piece j's GEMMs start when piece j has
+# landed (all-gather) / piece j's reduce-scatter runs beside piece j + 1's GEMMs. 1 = whole chunks.
+PIECES = max(1, int(os.environ.get("SMDT_TP_DIRECT_PIECES", "2")))
 
 
 class TpDirect:
@@ -43,6 +46,7 @@ class TpDirect:
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         self.calls = 0
+        self.pieces_issued = 0
 
     @classmethod
     def for_test(cls, group, region_bytes: int = 8 << 20) -> "TpDirect":
@@ -63,61 +67,88 @@ class TpDirect:
         return self.active and t.is_cuda and t.dtype in (torch.bfloat16, torch.float16, torch.float32) \
             and nb > 0 and nb % 16 == 0
 
+    def _pieces(self, n: int, row_bytes: int):
+        """Row pieces [a, b) of an n-row chunk: ``PIECES`` equal ones when n divides and every
+        piece starts on a 16-byte boundary, else one. World-uniform (shapes only)."""
+        k = max(1, min(PIECES, n))
+        while k > 1 and n % k:
+            k -= 1
+        if row_bytes % 16:
+            k = 1
+        p = n // k
+        return [(j * p, (j + 1) * p) for j in range(k)]
+
     def all_gather(self, x: torch.Tensor, chunk_fn: Optional[Callable] = None,
                    before_last_wait: Optional[Callable] = None) -> Optional[torch.Tensor]:
         """``ag_ring`` semantics: returns the gathered [ws * n, ...] tensor after calling
-        ``chunk_fn(c, chunk)`` for every chunk (the local one first, beside the transfer).
+        ``chunk_fn(lo, rows)`` on every gathered row range. The gather runs as row pieces, each
+        piece ONE engine call that reads that piece of every peer's chunk at once (all of the
+        group's links); the local chunk's GEMM runs beside the first piece, and the peers' rows
+        of piece j as soon as piece j has landed (its event), beside piece j + 1's transfer.
         None: not applicable (the caller runs the ring)."""
         x = x.contiguous()
         if not (self.fits(x) and self.eng.use["all_gather"]):
             return None
         ws, r, n = self.world, self.rank, x.shape[0]
         total = x.new_empty((n * ws,) + tuple(x.shape[1:]))
-        mine = total[r * n:(r + 1) * n]
-        mine.copy_(x)
-        h = self.eng.all_gather_async(total.view(-1), mine.view(-1))
-        if h is None:     # cannot happen for a tensor fits() took: refuse loudly instead of mixing paths
+        total[r * n:(r + 1) * n].copy_(x)
+        row = x[0].numel() if n else 0
+        pieces = self._pieces(n, row * x.element_size())
+        hs = self.eng.all_gather_pieces_async(total.view(-1), n * row, [(a * row, b * row) for a, b in pieces])
+        if hs is None:     # cannot happen for a tensor fits() took: refuse loudly instead of mixing paths
             raise RuntimeError("TpDirect.all_gather: the xGMI engine refused an exchange fits() accepted")
         self.calls += 1
+        self.pieces_issued += len(pieces)
         if chunk_fn is not None:
-            chunk_fn(r, x)                       # beside the gather
-        if before_last_wait is not None:
-            before_last_wait()
-        h.wait()
-        if chunk_fn is not None:
-            for c in range(ws):
-                if c != r:
-                    chunk_fn(c, total[c * n:(c + 1) * n])
+            chunk_fn(r * n, x)                   # beside the first piece
+        for j, (a, b) in enumerate(pieces):
+            if j == len(pieces) - 1 and before_last_wait is not None:
+                before_last_wait()
+            hs[j].wait()
+            if chunk_fn is not None:
+                for d in range(1, ws):
+                    c = (r + d) % ws
+                    chunk_fn(c * n + a, total[c * n + a:c * n + b])
         return total
 
-    def reduce_scatter(self, partial_fn: Callable, before_last_wait: Optional[Callable] = None) -> torch.Tensor:
-        """``rs_ring`` semantics: chunk c of the tensor being reduced is ``partial_fn(c)``;
-        returns this rank's reduced chunk (RCCL's reduce-scatter if the engine cannot take it)."""
+    def reduce_scatter(self, partial_fn: Callable, full_shape, ref: torch.Tensor,
+                       before_last_wait: Optional[Callable] = None) -> torch.Tensor:
+        """``rs_ring`` semantics: ``partial_fn(lo, rows, out)`` writes rows [lo, lo + rows) of the
+        [ws * n, ...] tensor being reduced (``full_shape``, ``ref``'s dtype / device) into ``out``;
+        returns this rank's reduced chunk. Push-style in row pieces: piece j's partials of every
+        chunk go straight into the engine's input buffer (no staging copy of whole partials), then
+        ONE engine reduce-scatter of that piece over all links runs on the engine stream while the
+        GEMMs of piece j + 1 run. RCCL's reduce-scatter when the engine cannot take the buffer."""
         ws, r = self.world, self.rank
-        first = partial_fn(r)
-        n = first.shape[0]
-        buf = first.new_empty((n * ws,) + tuple(first.shape[1:]))
-        buf[r * n:(r + 1) * n].copy_(first)
-        del first
-        for c in range(ws):
-            if c != r:
-                buf[c * n:(c + 1) * n].copy_(partial_fn(c))
-        out = buf.new_empty((n,) + tuple(buf.shape[1:]))
-        h = None
-        if self.fits(buf) and self.eng.use["reduce_scatter"]:
-            h = self.eng.reduce_scatter_async(out.view(-1), buf.view(-1))
-            if h is None:
-                raise RuntimeError("TpDirect.reduce_scatter: the xGMI engine refused an exchange fits() accepted")
-        else:
+        full_shape = tuple(full_shape)
+        n = full_shape[0] // ws
+        buf = torch.empty(full_shape, dtype=ref.dtype, device=ref.device)
+        out = buf.new_empty((n,) + full_shape[1:])
+        row = buf[0].numel() if n else 0
+        if not (self.fits(buf) and self.eng.use["reduce_scatter"]):
+            for c in range(ws):
+                partial_fn(c * n, n, buf[c * n:(c + 1) * n])
             w = dist.reduce_scatter_tensor(out, buf, group=self.group, async_op=True)
             if before_last_wait is not None:
                 before_last_wait()
             w.wait()
             return out
+        pieces = self._pieces(n, row * buf.element_size())
+        hs = []
+        for a, b in pieces:
+            for d in range(1, ws + 1):           # the peers' rows first, this rank's own last
+                c = (r + d) % ws
+                partial_fn(c * n + a, b - a, buf[c * n + a:c * n + b])
+            h = self.eng.reduce_scatter_piece_async(out.view(-1), buf.view(-1), a * row, b * row, n * row)
+            if h is None:
+                raise RuntimeError("TpDirect.reduce_scatter: the xGMI engine refused an exchange fits() accepted")
+            hs.append(h)
         self.calls += 1
+        self.pieces_issued += len(pieces)
         if before_last_wait is not None:
             before_last_wait()
-        h.wait()
+        for h in hs:
+            h.wait()
         return out
 
 

@@ -437,6 +437,50 @@ class XgmiAllReduce(IpcEngine):
     def all_gather_async(self, out, inp) -> Optional[_EventHandle]:
         return self._async(self.all_gather, [out, inp], out, inp)
 
+    def _ag_range(self, flat: torch.Tensor, lo: int, hi: int, stride: int) -> bool:
+        """All-gather elements [lo, hi) of every rank's slice of ``flat`` (slice r at r * stride,
+        this rank's already in place), region-sized bands, one engine call each."""
+        es = flat.element_size()
+        mine = self.rank * stride
+        for a, b in _bands(hi - lo, self.region // es, 16 // es):
+            self._call("all_gather", flat[mine + lo + a:mine + lo + b], flat[lo + a:], b - a, stride, 1.0)
+        return True
+
+    def all_gather_pieces_async(self, flat: torch.Tensor, stride: int, ranges) -> Optional[List[_EventHandle]]:
+        """``flat`` = W slices ``stride`` elements apart, this rank's in place; one engine call per
+        element range of the slices (all peers' pieces at once, every link), issued in order on
+        the engine stream; one handle per range (None: not eligible)."""
+        if not (self.use["all_gather"] and self.fits(flat)):
+            return None
+        es = flat.element_size()
+        if (stride * es) % 16 or any((lo * es) % 16 or (hi * es) % 16 for lo, hi in ranges):
+            return None
+        hs = []
+        for lo, hi in ranges:
+            h = self._async(self._ag_range, [flat], flat, lo, hi, stride)
+            if h is None:
+                return None
+            hs.append(h)
+        return hs
+
+    def _rs_range(self, out: torch.Tensor, inp: torch.Tensor, lo: int, hi: int, stride: int) -> bool:
+        es = inp.element_size()
+        for a, b in _bands(hi - lo, self.region // (self.world * es), 16 // es):
+            self._call("reduce_scatter", inp[lo + a:], out[lo + a:lo + b], b - a, stride, 1.0)
+        return True
+
+    def reduce_scatter_piece_async(self, out: torch.Tensor, inp: torch.Tensor, lo: int, hi: int,
+                                   stride: int) -> Optional[_EventHandle]:
+        """out[lo:hi] = sum over ranks of elements [lo, hi) of slice ``rank`` (``inp`` = W slices
+        ``stride`` apart, ``out`` this rank's reduced slice, both flat), on the engine stream."""
+        if not (self.use["reduce_scatter"] and self.fits(inp) and out.is_contiguous() and out.dtype == inp.dtype
+                and out.data_ptr() % 16 == 0 and inp.numel() == self.world * stride):
+            return None
+        es = inp.element_size()
+        if (stride * es) % 16 or (lo * es) % 16 or (hi * es) % 16:
+            return None
+        return self._async(self._rs_range, [out, inp], out, inp, lo, hi, stride)
+
     def error(self) -> int:
         return int(self.C.ar_read_error(self._sig)) if self._sig is not None else 0
 

@@ -875,21 +875,19 @@ class SPFusedGeLUMLP(torch.autograd.Function):
         x = x.contiguous()
         n = x.shape[0]
         ws = dist.get_world_size(group)
-        rows = x.numel() // x.shape[-1]           # rows of one SP chunk
         lead = (n * ws,) + tuple(x.shape[1:-1])
         f = w1.shape[0]
         pre = x.new_empty(lead + (f,))
         act = x.new_empty(lead + (f,))
-        p2, a2 = pre.view(-1, f), act.view(-1, f)
 
-        def fc1_chunk(c, ch):
-            C.gemm_tn(ch.reshape(rows, ch.shape[-1]), w1, 2, b1, p2[c * rows:(c + 1) * rows],
-                      a2[c * rows:(c + 1) * rows])
+        def fc1_chunk(lo, ch):
+            m = ch.shape[0]
+            C.gemm_tn(ch.reshape(-1, ch.shape[-1]), w1, 2, b1, pre[lo:lo + m].view(-1, f),
+                      act[lo:lo + m].view(-1, f))
         total = ag_ring(x, group, fc1_chunk)
-        y = rs_ring(lambda c: torch.nn.functional.linear(act[c * n:(c + 1) * n], w2), group)
+        y = rs_ring(lambda lo, m, o: _linear_into(act[lo:lo + m], w2, o), group, lead + (w2.shape[0],), act)
         ctx.save_for_backward(total, w1, w2, pre, act)
         ctx.b1 = b1
-        ctx.n = n
         return y
 
     @staticmethod
@@ -898,18 +896,17 @@ class SPFusedGeLUMLP(torch.autograd.Function):
         C = _ext.ext()
         group = _tp_group()
         b1 = ctx.b1
-        n = ctx.n
         dy = dy.contiguous()
-        rows = dy.numel() // dy.shape[-1]
         f = w1.shape[0]
         dz = pre.new_empty(pre.shape)
-        d2, p2 = dz.view(-1, f), pre.view(-1, f)
+        d2 = dz.view(-1, f)
         w2t = _dgrad_weight_t(w2)
         bd = b1.detach()
 
-        def fc2_dgrad_chunk(c, ch):
-            C.gemm_tn(ch.reshape(rows, ch.shape[-1]), w2t, 3, bd, d2[c * rows:(c + 1) * rows], None, 0, 0,
-                      p2[c * rows:(c + 1) * rows])
+        def fc2_dgrad_chunk(lo, ch):
+            m = ch.shape[0]
+            C.gemm_tn(ch.reshape(-1, ch.shape[-1]), w2t, 3, bd, dz[lo:lo + m].view(-1, f), None, 0, 0,
+                      pre[lo:lo + m].view(-1, f))
         gfull = ag_ring(dy, group, fc2_dgrad_chunk, before_last_wait=_flush_wgrad)
         dw2 = _wgrad(w2, gfull.reshape(-1, gfull.shape[-1]), act.reshape(-1, f))
         res = {}
@@ -918,7 +915,8 @@ class SPFusedGeLUMLP(torch.autograd.Function):
             res["dw"], res["db"] = _wgrad_and_bias(w1, b1, d2, total.reshape(-1, total.shape[-1]))
             _flush_wgrad()
         w1t = _dgrad_weight_t(w1)
-        dx = rs_ring(lambda c: dgrad(dz[c * n:(c + 1) * n], w1, w1t), group, wgrad)
+        dx = rs_ring(lambda lo, m, o: _dgrad_rows(dz[lo:lo + m], w1, w1t, o), group,
+                     dz.shape[:-1] + (w1.shape[1],), dz, wgrad)
         if "dw" not in res:
             wgrad()
         return dx, res["dw"], res["db"], dw2
@@ -935,6 +933,8 @@ def sp_fused_gelu_mlp_ok(x, mlp) -> bool:
             and fc2.skip_bias_add and not fc1.gather_output and x.dtype in (torch.bfloat16, torch.float16)
             and fc1.weight.dtype == x.dtype and fc2.weight.dtype == x.dtype and fc1.bias.dtype == x.dtype
             and _ext.use_kernels(x)):
+        return False
+    if _direct(_tp_group()) is not None:   # the direct TP4 / TP8 engine hands over row pieces
         return False
     rows = x.numel() // x.shape[-1]
     f, h = fc1.weight.shape
@@ -1067,7 +1067,7 @@ class VocabParallelLMHeadCE(torch.autograd.Function):
         if sp:
             n = x.shape[0]
             logits = x.new_empty((n * ws,) + tuple(x.shape[1:-1]) + (weight.shape[0],))
-            total = ag_ring(x, group, lambda c, ch: _mm_into(logits[c * n:(c + 1) * n], ch, weight))
+            total = ag_ring(x, group, lambda lo, ch: _mm_into(logits[lo:lo + ch.shape[0]], ch, weight))
         else:
             n = x.shape[0] // ws
             total = x
@@ -1105,12 +1105,12 @@ class VocabParallelLMHeadCE(torch.autograd.Function):
             res["dw"] = _wgrad(weight, e.view(-1, e.shape[-1]), hs)
             _flush_wgrad()
 
-        def part(ci):
-            g = dgrad(e[ci * n:(ci + 1) * n], weight, wt)
-            g.mul_(r3[ci * n:(ci + 1) * n])
+        def part(lo, m, o):
+            g = _dgrad_rows(e[lo:lo + m], weight, wt, o)
+            g.mul_(r3[lo:lo + m])
             return g
         if ctx.sp:
-            gi = rs_ring(part, group, wgrad)
+            gi = rs_ring(part, group, e.shape[:-1] + (weight.shape[1],), e, wgrad)
         else:
             gi = dgrad(e, weight, wt)
             gi.mul_(r3)
@@ -1221,6 +1221,22 @@ def _exchange(send, recv, nxt, prv, group):
     return works
 
 
+def _linear_into(x, w, out=None):
+    """x W^T into ``out`` (returned) when given, else a new tensor (``rs_ring`` partials)."""
+    if out is None:
+        return torch.nn.functional.linear(x, w)
+    _mm_into(out, x, w)
+    return out
+
+
+def _dgrad_rows(g, weight, wt, out=None):
+    """dX = g @ weight into ``out`` (returned) when given, else a new tensor."""
+    if out is None:
+        return dgrad(g, weight, wt)
+    dgrad_into(out, g, weight, wt)
+    return out
+
+
 def _mm_into(dst, a, w, bias=None):
     """dst[..., o] = a[..., k] @ w[o, k]^T (+ bias) written in place (hipBLASLt out= GEMM)."""
     a2 = a.reshape(-1, a.shape[-1])
@@ -1244,10 +1260,12 @@ AG_RING_STATS = {"in_place": 0, "copied": 0}
 
 
 def ag_ring(x, group, chunk_fn=None, before_last_wait=None, _skip_direct=False):
-    """All-gather ``x`` along dim 0 over ``group`` as a ring; ``chunk_fn(c, chunk)`` runs on chunk c
-    as soon as it is resident, while the next chunk is in flight. Returns the gathered tensor.
+    """All-gather ``x`` along dim 0 over ``group`` as a ring; ``chunk_fn(lo, rows)`` runs on the
+    gathered rows [lo, lo + rows.shape[0]) (dim 0) as soon as they are resident, while the next
+    chunk is in flight: the ring hands over whole chunks (lo = c * n). Returns the gathered tensor.
     TP groups of 4 / 8 with a direct engine (comm/tp_direct.py) gather over all of the group's
-    links at once instead, the local chunk's GEMM beside the transfer."""
+    links at once instead, in row pieces: the local chunk's GEMM beside the first piece, every
+    peer's rows of piece j as soon as piece j has landed."""
     td = None if _skip_direct else _direct(group)
     if td is not None:
         out = td.all_gather(x, chunk_fn, before_last_wait)
@@ -1272,7 +1290,7 @@ def ag_ring(x, group, chunk_fn=None, before_last_wait=None, _skip_direct=False):
             nc = (c - 1) % ws
             works = _exchange(total[c * n:(c + 1) * n], total[nc * n:(nc + 1) * n], nxt, prv, group)
         if chunk_fn is not None:
-            chunk_fn(c, x if s == 0 else total[c * n:(c + 1) * n])
+            chunk_fn(c * n, x if s == 0 else total[c * n:(c + 1) * n])
         if works is not None:
             if s == ws - 2 and before_last_wait is not None:
                 before_last_wait()
@@ -1280,21 +1298,25 @@ def ag_ring(x, group, chunk_fn=None, before_last_wait=None, _skip_direct=False):
     return total
 
 
-def rs_ring(partial_fn, group, before_last_wait=None):
-    """Reduce-scatter along dim 0 over ``group`` as a ring, where chunk c of the tensor being
-    reduced is produced on demand by ``partial_fn(c)`` (a GEMM on c's rows): step s computes the
-    next partial while the previous one is in flight. Returns this rank's reduced chunk. TP groups
-    of 4 / 8 with a direct engine reduce all partials over every link of the group at once."""
+def rs_ring(partial_fn, group, full_shape, ref, before_last_wait=None):
+    """Reduce-scatter along dim 0 over ``group`` as a ring. The tensor being reduced (``full_shape``,
+    ``ref``'s dtype / device) is produced on demand: ``partial_fn(lo, rows, out)`` computes its rows
+    [lo, lo + rows) — a GEMM on those rows — into ``out`` when given (and returns it), else into a
+    new tensor. Ring step s computes the next chunk's partial while the previous one is in flight.
+    Returns this rank's reduced chunk. TP groups of 4 / 8 with a direct engine write the partials
+    straight into the engine's input buffer in row pieces, each piece reduce-scattered over every
+    link of the group while the next piece's GEMMs run."""
     td = _direct(group)
     if td is not None:
-        out = td.reduce_scatter(partial_fn, before_last_wait)
+        out = td.reduce_scatter(partial_fn, full_shape, ref, before_last_wait)
         _cs.collective("reduce_scatter", group, _nbytes(out) * td.world, transport="xgmi")
         return out
     ws, r, nxt, prv = _ring(group)
+    n = full_shape[0] // ws
     works, incoming, keep = None, None, []
     for s in range(ws):
         c = (r - s - 1) % ws
-        part = partial_fn(c)
+        part = partial_fn(c * n, n, None)
         if works is not None:
             if s == ws - 1 and before_last_wait is not None:
                 before_last_wait()
@@ -1339,7 +1361,7 @@ class _ColumnSPLinear(torch.autograd.Function):
         ws = dist.get_world_size(group)
         out = x.new_empty((n * ws,) + tuple(x.shape[1:-1]) + (weight.shape[0],))
         fb = bias if add_bias else None
-        total = ag_ring(x, group, lambda c, ch: _mm_into(out[c * n:(c + 1) * n], ch, weight, fb))
+        total = ag_ring(x, group, lambda lo, ch: _mm_into(out[lo:lo + ch.shape[0]], ch, weight, fb))
         ctx.save_for_backward(total, weight)
         ctx.bias_p = bias
         ctx.n = n
@@ -1358,7 +1380,8 @@ class _ColumnSPLinear(torch.autograd.Function):
             res["dw"], res["db"] = _wgrad_and_bias(weight, ctx.bias_p, g2, total.reshape(-1, total.shape[-1]))
             _flush_wgrad()
         wt = _dgrad_weight_t(weight)
-        gi = rs_ring(lambda c: dgrad(g[c * n:(c + 1) * n], weight, wt), group, wgrad)
+        gi = rs_ring(lambda lo, m, o: _dgrad_rows(g[lo:lo + m], weight, wt, o), group,
+                     g.shape[:-1] + (weight.shape[1],), g, wgrad)
         if "dw" not in res:   # world 1 ring: no wait happened
             wgrad()
         return gi, res["dw"], res["db"], None
@@ -1376,7 +1399,8 @@ class _RowSPLinear(torch.autograd.Function):
         ws = dist.get_world_size(group)
         assert x.shape[0] % ws == 0, "sequence length must divide the TP size"
         n = x.shape[0] // ws
-        y = rs_ring(lambda c: torch.nn.functional.linear(x[c * n:(c + 1) * n], weight), group)
+        y = rs_ring(lambda lo, m, o: _linear_into(x[lo:lo + m], weight, o), group,
+                    x.shape[:-1] + (weight.shape[0],), x)
         ctx.save_for_backward(x, weight)
         ctx.n = n
         return y
@@ -1389,7 +1413,7 @@ class _RowSPLinear(torch.autograd.Function):
         n = ctx.n
         gi = x.new_empty(x.shape)
         wt = _dgrad_weight_t(weight)
-        gfull = ag_ring(g, group, lambda c, ch: dgrad_into(gi[c * n:(c + 1) * n], ch, weight, wt),
+        gfull = ag_ring(g, group, lambda lo, ch: dgrad_into(gi[lo:lo + ch.shape[0]], ch, weight, wt),
                         before_last_wait=_flush_wgrad)
         dw = _wgrad(weight, gfull.reshape(-1, gfull.shape[-1]), x.reshape(-1, x.shape[-1]))
         return gi, dw

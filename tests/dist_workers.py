@@ -765,7 +765,7 @@ def relay_ipc_worker(rank, world, port, outdir):
             torch.cuda.synchronize()
             res["ok"].append(bool(torch.equal(total, torch.cat(parts))))
             full = lambda r: (torch.arange(16 * 16, device="cuda", dtype=torch.float32).view(16, 16) % 7 * (r + 1)).to(dt)
-            got = tpl.rs_ring(lambda c: full(rank)[c * 8:(c + 1) * 8].clone(), pg)
+            got = tpl.rs_ring(lambda lo, m, o: full(rank)[lo:lo + m].clone(), pg, (16, 16), full(rank))
             exp = (full(rank).float() + full(partner).float())[me * 8:(me + 1) * 8].to(dt)
             torch.cuda.synchronize()
             res["ok"].append(bool(torch.equal(got, exp)))
@@ -1140,24 +1140,55 @@ def tp_direct_worker(rank, world, port, outdir):
         n, h, o = 256, 64, 96
         x = torch.randn(n, 4, h, device="cuda", dtype=torch.bfloat16)
         w = torch.randn(o, h, device="cuda", dtype=torch.bfloat16)
-        # all-gather with a per-chunk GEMM (the column-parallel forward)
-        out = torch.empty(n * world, 4, o, device="cuda", dtype=torch.bfloat16)
-        seen = []
-        total = T.ag_ring(x, g, lambda c, ch: (seen.append(c), out[c * n:(c + 1) * n].copy_(ch @ w.t())))
         xs = [torch.empty_like(x.cpu()) for _ in range(world)]
         dist.all_gather(xs, x.cpu())
         ref_total = torch.cat(xs)
-        ok_ag = torch.equal(total.cpu(), ref_total) and sorted(seen) == list(range(world)) and seen[0] == rank
-        ok_mm = torch.allclose(out.float().cpu(), (ref_total.float() @ w.float().cpu().t()), atol=0.5, rtol=2e-2)
-        # reduce-scatter of per-chunk partials (the row-parallel forward)
         full = torch.randn(n * world, 4, o, device="cuda", dtype=torch.float32)
-        part = T.rs_ring(lambda c: full[c * n:(c + 1) * n] * 1.0, g, before_last_wait=lambda: seen.append("wgrad"))
-        red = full.cpu().clone()
-        dist.all_reduce(red)
-        ok_rs = torch.allclose(part.cpu(), red[rank * n:(rank + 1) * n], atol=1e-5, rtol=1e-5)
+        fulls = [torch.empty_like(full.cpu()) for _ in range(world)]
+        dist.all_gather(fulls, full.cpu())
+        red = fulls[0].clone()
+        for t in fulls[1:]:       # rank order, fp32: the engine's summation order
+            red += t
+        oks = {}
+        for k in (1, 2, 4):   # row pieces per exchange (1 = whole chunks)
+            tp_direct.PIECES = k
+            # all-gather with a per-row-range GEMM (the column-parallel forward)
+            out = torch.empty(n * world, 4, o, device="cuda", dtype=torch.bfloat16)
+            seen = []
+
+            def chunk(lo, ch):
+                seen.append((lo, ch.shape[0]))
+                out[lo:lo + ch.shape[0]].copy_(ch @ w.t())
+            total = T.ag_ring(x, g, chunk)
+            cover = sorted(seen)
+            ok_ag = (torch.equal(total.cpu(), ref_total) and seen[0] == (rank * n, n)
+                     and sum(m for _, m in seen) == n * world
+                     and all(a + m == b for (a, m), (b, _) in zip(cover, cover[1:]))
+                     and len(seen) == 1 + (world - 1) * k)
+            ok_mm = torch.allclose(out.float().cpu(), (ref_total.float() @ w.float().cpu().t()), atol=0.5, rtol=2e-2)
+            # reduce-scatter of per-row-range partials (the row-parallel forward), bit-exact: the
+            # engine sums in rank order in fp32, as the host reference below does
+            calls = []
+
+            def part(lo, m, dst):
+                calls.append((lo, m))
+                src = full[lo:lo + m] * 1.0
+                if dst is None:
+                    return src
+                dst.copy_(src)
+                return dst
+            got = T.rs_ring(part, g, full.shape, full, before_last_wait=lambda: seen.append("wgrad"))
+            ok_rs = torch.equal(got.cpu(), red[rank * n:(rank + 1) * n]) and len(calls) == world * k
+            oks[k] = (bool(ok_ag), bool(ok_mm), bool(ok_rs), "wgrad" in seen)
+        tp_direct.PIECES = 2
+        ok_ag = all(v[0] for v in oks.values())
+        ok_mm = all(v[1] for v in oks.values())
+        ok_rs = all(v[2] for v in oks.values())
+        res["pieces"] = oks
+        res["pieces_issued"] = st.tp_direct.pieces_issued
         torch.cuda.synchronize()
         res.update(ok_ag=bool(ok_ag), ok_mm=bool(ok_mm), ok_rs=bool(ok_rs), calls=st.tp_direct.calls,
-                   wgrad_hook="wgrad" in seen, error_word=st.tp_direct.eng.error())
+                   wgrad_hook=all(v[3] for v in oks.values()), error_word=st.tp_direct.eng.error())
         dist.barrier()
         st.tp_direct.eng.close()
         dist.destroy_process_group()

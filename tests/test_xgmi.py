@@ -310,10 +310,13 @@ def test_smddp_backend_name_turns_xgmi_on(monkeypatch):
 @pytest.mark.gpu
 @pytest.mark.parametrize("world", [4])
 def test_tp_direct_exchange_through_ring_entry_points(world):
-    """``ag_ring`` / ``rs_ring`` of a TP group of 4 run through the direct
-    multi-link engine (comm/tp_direct.py; 4 processes on one GPU, IPC mappings of the same device):
-    the gather equals RCCL-free host gathering, every chunk's GEMM runs (the local one first, beside
-    the transfer), the reduce-scatter equals the host all-reduce's slice, the backward hook runs."""
+    """``ag_ring`` / ``rs_ring`` of a TP group of 4 run through the
+    direct multi-link engine (comm/tp_direct.py; 4 processes on one GPU, IPC mappings of the same
+    device) in 1, 2 and 4 row pieces per exchange: the gather equals host gathering bit for bit,
+    every gathered row range's GEMM runs exactly once (the local chunk first, beside the first
+    piece; then each peer's rows of piece j), the push-style reduce-scatter (partials written
+    straight into the engine's input, one engine call per piece) equals the host all-reduce's slice
+    BIT-EXACTLY (fp32, rank-order sums on both sides), the backward hook runs."""
     import os
     import pickle
     import tempfile
@@ -343,4 +346,5 @@ def test_tp_direct_exchange_through_ring_entry_points(world):
     for r, res in enumerate(out):
         assert res["err"] is None, f"rank {r}:\n{res['err']}"
         assert res["ok_ag"] and res["ok_mm"] and res["ok_rs"], (r, res)
-        assert res["calls"] == 2 and res["wgrad_hook"] and res["error_word"] == 0, (r, res)
+        assert res["calls"] == 6 and res["wgrad_hook"] and res["error_word"] == 0, (r, res)
+        assert res["pieces_issued"] == 2 * (1 + 2 + 4), (r, res)
