@@ -35,7 +35,65 @@ def gpt_reference(steps=1, sp=False, cfg_over=None):
     return loss.detach(), grads
 
 
-def gpt_tp_worker(rank, world, tp, pp, sp, cfg_over=None, p2p=None):
+class _Done:
+    def wait(self):
+        return True
+
+
+class _GlooPieceEngine:
+    """CPU stand-in of the xGMI engine's piece API (comm/xgmi.XgmiAllReduce.all_gather_pieces_async
+    / reduce_scatter_piece_async) over a Gloo group, synchronous: lets the Gloo equivalence tests
+    run ``TpDirect``'s row-piece logic and every ring caller's row-range / write-into-``out``
+    callbacks. Reductions sum in rank order, as the engine does."""
+
+    def __init__(self, group):
+        import torch.distributed as dist
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.active = True
+        self.use = {"all_gather": True, "reduce_scatter": True}
+
+    def all_gather_pieces_async(self, flat, stride, ranges):
+        import torch.distributed as dist
+        hs = []
+        for lo, hi in ranges:
+            mine = flat[self.rank * stride + lo:self.rank * stride + hi].clone()
+            parts = [torch.empty_like(mine) for _ in range(self.world)]
+            dist.all_gather(parts, mine, group=self.group)
+            for r in range(self.world):
+                flat[r * stride + lo:r * stride + hi].copy_(parts[r])
+            hs.append(_Done())
+        return hs
+
+    def reduce_scatter_piece_async(self, out, inp, lo, hi, stride):
+        import torch.distributed as dist
+        mine = torch.cat([inp[d * stride + lo:d * stride + hi] for d in range(self.world)])
+        parts = [torch.empty_like(mine) for _ in range(self.world)]
+        dist.all_gather(parts, mine, group=self.group)
+        n = hi - lo
+        acc = parts[0][self.rank * n:(self.rank + 1) * n].clone()
+        for r in range(1, self.world):
+            acc += parts[r][self.rank * n:(self.rank + 1) * n]
+        out[lo:hi].copy_(acc)
+        return _Done()
+
+
+def _cpu_tp_direct(group, pieces):
+    """A ``TpDirect`` over ``_GlooPieceEngine`` that accepts CPU tensors."""
+    from smdt_amd.comm import tp_direct
+
+    class _CpuTpDirect(tp_direct.TpDirect):
+        def fits(self, t):
+            return self.active and t.numel() > 0 and (t.numel() * t.element_size()) % 16 == 0
+
+    tp_direct.PIECES = pieces
+    return _CpuTpDirect(_GlooPieceEngine(group), group)
+
+
+def gpt_tp_worker(rank, world, tp, pp, sp, cfg_over=None, p2p=None, direct_pieces=0):
+    """``direct_pieces`` > 0: the TP exchanges run through ``TpDirect`` in that many row pieces
+    (over the CPU stand-in engine) instead of the ring."""
     import torch.distributed as dist
     from smdt_amd.comm import init_distributed
     from smdt_amd.models.gpt import GPTModel, allreduce_word_embedding_grads
@@ -44,6 +102,8 @@ def gpt_tp_worker(rank, world, tp, pp, sp, cfg_over=None, p2p=None):
     from smdt_amd.train.schedules import get_forward_backward_func
     init_distributed("gloo")
     st = ps.initialize_model_parallel(tp, pp)
+    if direct_pieces:
+        st.tp_direct = _cpu_tp_direct(st.tp_group, direct_pieces)
     from smdt_amd.train import schedules
     schedules.configure_p2p(**(p2p or {}))
     cfg = TransformerConfig(**{**TINY, **(cfg_over or {}), "sequence_parallel": sp})
@@ -79,7 +139,9 @@ def gpt_tp_worker(rank, world, tp, pp, sp, cfg_over=None, p2p=None):
             if getattr(p, "sequence_parallel", False) and n in grads:
                 dist.all_reduce(grads[n], group=st.tp_group)
     meta = {"tp_rank": st.tp_rank, "pp_rank": st.pp_rank, "first": st.first_layer if hasattr(st, "first_layer") else None,
-            "layer_offset": m.first_layer}
+            "layer_offset": m.first_layer,
+            "direct_calls": st.tp_direct.calls if direct_pieces else 0,
+            "direct_pieces": st.tp_direct.pieces_issued if direct_pieces else 0}
     dist.destroy_process_group()
     return out_loss, grads, meta
 

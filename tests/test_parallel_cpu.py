@@ -49,6 +49,21 @@ def test_tensor_parallel_matches_single_rank(tp, sp):
         _check_tp_grads(ref, grads, meta, tp)
 
 
+@pytest.mark.parametrize("tp,pieces", [(4, 1), (4, 2), (2, 4)])
+def test_direct_tp_exchange_pieces_match_single_rank(tp, pieces):
+    """TP + SP with every sequence-parallel exchange through ``TpDirect`` in row pieces (a CPU
+    stand-in of the xGMI engine's piece calls over Gloo): the all-gather callers get row ranges
+    (lo, rows) piece by piece, the reduce-scatter callers write their partials straight into the
+    engine's input (``partial_fn(lo, rows, out)``) — column / row SP linears, both directions.
+    Loss and every gradient equal the single-rank model's."""
+    ref_loss, ref = W.gpt_reference()
+    outs = run_workers(W.gpt_tp_worker, tp, tp, 1, True, None, None, pieces)
+    for loss, grads, meta in outs:
+        _close(loss, ref_loss)
+        _check_tp_grads(ref, grads, meta, tp)
+        assert meta["direct_calls"] > 0 and meta["direct_pieces"] == pieces * meta["direct_calls"]
+
+
 @pytest.mark.parametrize("over", [None, {"num_layers": 3, "decoder_last_pipeline_num_layers": 1}])
 def test_pipeline_parallel_matches_single_rank(over):
     """pp = 2, uniform split and the uneven split bench.py uses to balance the LM head (first stage
