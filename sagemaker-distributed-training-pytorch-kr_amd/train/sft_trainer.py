@@ -170,7 +170,9 @@ class Trainer:
         not decide alone. One 4-byte all-reduce per accumulation window."""
         ok = self._window_fits(window)
         ddp = getattr(getattr(self, "engine", None), "ddp", None)
-        if ddp is not None and ddp.dp > 1:
+        from ..comm import loopback as _lb
+        if ddp is not None and ddp.dp > 1 and not _lb.is_loopback(ddp.dp_group):
+            # (a loopback group is ONE process emulating a rank, SMDT_EMULATE_DP: its own decision)
             dev = self.device if self.device.type == "cuda" and dist.get_backend(ddp.dp_group) != "gloo" \
                 else torch.device("cpu")
             t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
