@@ -396,14 +396,17 @@ class HFCausalLM(nn.Module):
         shifted[:, :-1] = labels[:, 1:]
         idx = self._pack_index(attention_mask)
         if idx is not None:
+            from . import transformer as _T
             from .transformer import packed_sequences
             b, L = input_ids.shape
+            groups = (_T.length_groups(attention_mask.bool(), idx, input_ids.device)
+                      if _T._LENGTH_GROUPS and input_ids.is_cuda else None)
             idx = idx.to(input_ids.device, non_blocking=True)
             tok = input_ids.t().reshape(-1).index_select(0, idx).unsqueeze(0)          # [1, T]
             pos = torch.div(idx, b, rounding_mode="floor").unsqueeze(0)                # position in its row
             lab = shifted.t().reshape(-1).index_select(0, idx).unsqueeze(0)
             self.last_computed_tokens = int(idx.numel())
-            with packed_sequences(idx, b, L):
+            with packed_sequences(idx, b, L, groups):
                 tl = self.model(tok, pos, None, labels=lab)                            # [1, T]
             valid = (lab != -100).float()
             rows = torch.remainder(idx, b) if row_groups is not None else None

@@ -131,15 +131,16 @@ class Norm(nn.Module):
 # padded [L, b] layout (zeros in the pad rows), runs RoPE + the causal flash kernels there and
 # gathers the T context rows back. Real-token outputs and all gradients equal the padded
 # computation's (models/hf.py ``HFCausalLM.forward`` sets it up from the attention mask).
-_PACK = {"idx": None, "b": 0, "L": 0, "inv": None}
+_PACK = {"idx": None, "b": 0, "L": 0, "inv": None, "groups": None}
 
 
 class packed_sequences:
     """Context: ``idx`` (device int64 [T]) = seq-first flat positions s * b + bi of the real
-    tokens of a right-padded [b, L] batch."""
+    tokens of a right-padded [b, L] batch. ``groups`` (optional, ``length_groups``): the rows
+    bucketed by their own length, for the length-grouped attention layout."""
 
-    def __init__(self, idx, b: int, L: int):
-        self.state = {"idx": idx, "b": int(b), "L": int(L), "inv": None}
+    def __init__(self, idx, b: int, L: int, groups=None):
+        self.state = {"idx": idx, "b": int(b), "L": int(L), "inv": None, "groups": groups}
 
     def __enter__(self):
         self.prev = dict(_PACK)
@@ -179,6 +180,113 @@ class _GatherRows(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         return _ext.ext().gather_rows(g.contiguous(), ctx.bwd_map), None, None
+
+
+# Length-grouped attention layout (SMDT_SFT_LENGTH_GROUPS, default on). The padded [L, b] layout
+# pays attention (and the row gathers) for every row at the window's longest length L: an NB4
+# window of 32 Alpaca rows (~135 tokens each, the longest a few hundred) spends most of its causal
+# attention on pad rows. Rows are instead bucketed by their own length rounded up to 128 (the
+# flash kernels' S granularity) into blocks [L_g, b_g], laid out one after another in ONE
+# [sum_g L_g b_g, W] buffer: ONE row gather in, the causal flash kernels per block on views of
+# it (no copies either way), ONE gather out. Real-token results equal the [L, b] layout's: a real
+# token still sees exactly its own row's earlier tokens.
+_LENGTH_GROUPS = os.environ.get("SMDT_SFT_LENGTH_GROUPS", "1") == "1"
+_GROUP_ALIGN = 128
+
+
+def length_groups(mask_cpu, idx_cpu, device):
+    """Host-side (CPU, no device sync) plan of the length-grouped layout for a right-padded
+    [b, L] CPU ``mask_cpu`` whose packed tokens are the seq-first positions ``idx_cpu``:
+    ``{"blocks": [(row offset, L_g, b_g)], "inv": [P] packed index of each grouped position
+    (-1 = pad), "pack": [T] grouped position of each packed token (-1: a trailing pad token
+    beyond its row's block, whose attention output is then 0)}``, the maps on ``device``."""
+    b, L = mask_cpu.shape
+    lens = mask_cpu.sum(1).clamp(min=1)
+    Lr = ((lens + _GROUP_ALIGN - 1) // _GROUP_ALIGN) * _GROUP_ALIGN          # per-row block length
+    blocks, off = [], 0
+    row_off = torch.empty(b, dtype=torch.int64)      # block offset of each row's block
+    row_j = torch.empty(b, dtype=torch.int64)        # the row's index inside its block
+    row_b = torch.empty(b, dtype=torch.int64)        # rows in the row's block
+    row_L = torch.empty(b, dtype=torch.int64)
+    for Lg in sorted(set(Lr.tolist())):
+        rows = (Lr == Lg).nonzero().squeeze(1)
+        bg = rows.numel()
+        blocks.append((off, int(Lg), int(bg)))
+        row_off[rows] = off
+        row_j[rows] = torch.arange(bg)
+        row_b[rows] = bg
+        row_L[rows] = Lg
+        off += int(Lg) * bg
+    s_t, i_t = idx_cpu // b, idx_cpu % b
+    ok = s_t < row_L[i_t]
+    pos = row_off[i_t] + s_t * row_b[i_t] + row_j[i_t]
+    pack = torch.where(ok, pos, torch.full_like(pos, -1))
+    inv = torch.full((off,), -1, dtype=torch.int64)
+    inv[pos[ok]] = torch.arange(idx_cpu.numel())[ok]
+    return {"blocks": blocks, "inv": inv.to(device, non_blocking=True),
+            "pack": pack.to(device, non_blocking=True), "rows": off}
+
+
+class _RopeQKVGroups(torch.autograd.Function):
+    """RoPE (in place) on the q / k parts of the length-grouped [P, W] buffer: one launch per
+    block, positions (row // b_g) within the block."""
+
+    @staticmethod
+    def forward(ctx, x, cos, sin, rot, nh, nkv, hd, blocks):
+        ctx.mark_dirty(x)
+        for o, Lg, bg in blocks:
+            _ext.ext().rope_(x[o:o + Lg * bg, :(nh + nkv) * hd].view(Lg * bg, nh + nkv, hd), cos, sin, rot,
+                             bg, Lg, False)
+        ctx.save_for_backward(cos, sin)
+        ctx.cfg = (rot, nh, nkv, hd, blocks)
+        return x
+
+    @staticmethod
+    def backward(ctx, g):
+        cos, sin = ctx.saved_tensors
+        rot, nh, nkv, hd, blocks = ctx.cfg
+        d = g if g.is_contiguous() else g.contiguous()
+        for o, Lg, bg in blocks:
+            _ext.ext().rope_(d[o:o + Lg * bg, :(nh + nkv) * hd].view(Lg * bg, nh + nkv, hd), cos, sin, rot,
+                             bg, Lg, True)
+        return d, None, None, None, None, None, None, None
+
+
+class _FlashQKVGroups(torch.autograd.Function):
+    """Causal flash attention of every block [L_g, b_g] of the length-grouped [P, W] fused-QKV
+    buffer, reading q / k / v as strided views of it and writing the context [P, nh hd] and, in
+    backward, d(qkv) [P, W] block by block in place (the kernels take strided views)."""
+
+    @staticmethod
+    def forward(ctx, qkv, nh, nkv, hd, scale, dropout_p, seeds, blocks):
+        C = _ext.ext()
+        P, W = qkv.shape
+        out = qkv.new_empty(P, nh, hd)
+        lses = []
+        for (o, Lg, bg), (seed, off) in zip(blocks, seeds):
+            q, k, v = SF._qkv_views(qkv[o:o + Lg * bg].view(Lg, bg, W), nh, nkv, hd, True)
+            ov = out[o:o + Lg * bg].view(Lg, bg, nh, hd).transpose(0, 1)
+            lses.append(C.flash_fwd(q, k, v, scale, True, ov, dropout_p, seed, off)[1])
+        ctx.save_for_backward(qkv, out, *lses)
+        ctx.cfg = (nh, nkv, hd, scale, dropout_p, seeds, blocks)
+        return out.view(P, nh * hd)
+
+    @staticmethod
+    def backward(ctx, dout):
+        qkv, out, *lses = ctx.saved_tensors
+        nh, nkv, hd, scale, dropout_p, seeds, blocks = ctx.cfg
+        C = _ext.ext()
+        P, W = qkv.shape
+        dqkv = torch.empty_like(qkv)
+        do_all = dout.contiguous().view(P, nh, hd)
+        for (o, Lg, bg), (seed, off), lse in zip(blocks, seeds, lses):
+            sl = slice(o, o + Lg * bg)
+            q, k, v = SF._qkv_views(qkv[sl].view(Lg, bg, W), nh, nkv, hd, True)
+            dq, dk, dv = SF._qkv_views(dqkv[sl].view(Lg, bg, W), nh, nkv, hd, True)
+            o_v = out[sl].view(Lg, bg, nh, hd).transpose(0, 1)
+            do_v = do_all[sl].view(Lg, bg, nh, hd).transpose(0, 1)
+            C.flash_bwd(q, k, v, o_v, do_v, lse, scale, True, dq, dk, dv, dropout_p, seed, off)
+        return dqkv, None, None, None, None, None, None, None
 
 
 def _unpack_rows(x):
@@ -264,8 +372,33 @@ class ParallelAttention(nn.Module):
     def forward(self, x, training=True):
         qkv = self.qkv(x)                                        # [s, b, (nh + 2 nkv) d]
         if _PACK["idx"] is not None:                              # padding-free micro-batch
+            if self._groups_ok(qkv):
+                return self.proj(self._attend_groups(qkv, training))
             return self.proj(_pack_rows(self._attend(_unpack_rows(qkv), training)))
         return self.proj(self._attend(qkv, training))            # (out, bias)
+
+    def _groups_ok(self, qkv) -> bool:
+        g = _PACK.get("groups")
+        W = qkv.shape[-1]
+        return (g is not None and self.cfg.use_flash_attn and ps.get_state().cp == 1 and _ext.use_kernels(qkv)
+                and self.hd in (64, 128) and qkv.dtype in (torch.bfloat16, torch.float16)
+                and (W * qkv.element_size()) % 16 == 0 and W % 8 == 0)
+
+    def _attend_groups(self, qkv, training):
+        """Padding-free attention in the length-grouped layout (``length_groups``): [T, 1, W]
+        packed QKV -> grouped blocks (one row gather) -> RoPE -> causal flash per block -> [T, 1,
+        nh hd] (one row gather)."""
+        g = _PACK["groups"]
+        W = qkv.shape[-1]
+        x = _GatherRows.apply(qkv.reshape(-1, W), g["inv"], g["pack"])           # [P, W]
+        if self.rope is not None:
+            cos, sin, rot = self.rope
+            x = _RopeQKVGroups.apply(x, cos, sin, rot, self.nh, self.nkv, self.hd, g["blocks"])
+        p = self.cfg.attention_dropout if training else 0.0
+        seeds = [SF._rng(get_rng("tp")).next() if p > 0 else (0, 0) for _ in g["blocks"]]
+        ctx = _FlashQKVGroups.apply(x, self.nh, self.nkv, self.hd, 1.0 / math.sqrt(self.hd), float(p), seeds,
+                                    g["blocks"])
+        return _GatherRows.apply(ctx, g["pack"], g["inv"]).unsqueeze(1)         # [T, 1, nh hd]
 
     def _attend(self, qkv, training):
         cp = ps.get_state().cp

@@ -114,3 +114,78 @@ def test_packed_rows_gather_kernel_matches_index_ops():
     gx = torch.zeros(idx.numel(), W, device="cuda", dtype=torch.bfloat16)
     gx[:, :C] = 2 * g.squeeze(1)
     torch.testing.assert_close(x.grad.squeeze(1), gx)
+
+
+def test_length_groups_plan_maps():
+    """The length-grouped attention layout's host plan (models/transformer.length_groups): rows
+    bucketed by their own length rounded up to 128, blocks [L_g, b_g] back to back; every real
+    token sits at block offset + s * b_g + (its row's index in the block), the two maps invert
+    each other, and a packed trailing pad token beyond its row's block maps to -1."""
+    import torch
+    from smdt_amd.models import transformer as T
+    b, L = 5, 384
+    lens = torch.tensor([300, 20, 130, 1, 128])
+    mask = torch.arange(L).unsqueeze(0) < lens.unsqueeze(1)
+    real = [s * b + i for s in range(L) for i in range(b) if s < lens[i]]
+    extra = [200 * b + 1]                       # a pad position of row 1 (len 20, block 128)
+    idx = torch.tensor(sorted(real + extra), dtype=torch.int64)
+    g = T.length_groups(mask, idx, "cpu")
+    assert [(Lg, bg) for _, Lg, bg in g["blocks"]] == [(128, 3), (256, 1), (384, 1)]
+    assert g["rows"] == 128 * 3 + 256 + 384
+    inv, pack = g["inv"], g["pack"]
+    rows_of = {128: [1, 3, 4], 256: [2], 384: [0]}
+    offs = {Lg: o for o, Lg, _ in g["blocks"]}
+    for t, p in enumerate(idx.tolist()):
+        s, i = p // b, p % b
+        if s >= lens[i]:
+            assert pack[t] == -1                 # the trailing pad beyond row 1's 128-block
+            continue
+        Lg = int(((int(lens[i]) + 127) // 128) * 128)
+        j = rows_of[Lg].index(i)
+        assert pack[t] == offs[Lg] + s * len(rows_of[Lg]) + j
+        assert inv[pack[t]] == t
+    assert int((inv >= 0).sum()) == len(real)
+
+
+@pytest.mark.gpu
+def test_length_grouped_attention_matches_padded_layout(monkeypatch):
+    """Padding-free SFT micro-batch with attention in the length-grouped layout (blocks of rows
+    of similar length, causal flash per block on views of one buffer) against the single padded
+    [L, b] layout: the loss, every real token's loss and every parameter gradient agree (bf16,
+    relative to each tensor's max), and the grouped path actually runs."""
+    import torch
+    from smdt_amd.models import transformer as T
+    from smdt_amd.models.hf import HFCausalLM
+    cfg = dict(model_type="llama", hidden_size=256, num_hidden_layers=2, num_attention_heads=4,
+               num_key_value_heads=2, intermediate_size=512, vocab_size=120, max_position_embeddings=512,
+               rms_norm_eps=1e-6, rope_theta=10000.0, tie_word_embeddings=False)
+    torch.manual_seed(0)
+    b, L = 6, 384
+    lens = torch.tensor([300, 20, 130, 256, 5, 129])
+    mask = (torch.arange(L).unsqueeze(0) < lens.unsqueeze(1)).long()
+    ids = torch.randint(0, 120, (b, L))
+    labels = torch.where(mask.bool(), ids, torch.full_like(ids, -100))
+    calls = {"n": 0}
+    orig = T.ParallelAttention._attend_groups
+
+    def counted(self, *a):
+        calls["n"] += 1
+        return orig(self, *a)
+    monkeypatch.setattr(T.ParallelAttention, "_attend_groups", counted)
+    res = []
+    for on in (True, False):
+        monkeypatch.setattr(T, "_LENGTH_GROUPS", on)
+        torch.manual_seed(1)
+        m = HFCausalLM(cfg, params_dtype=torch.bfloat16, device="cuda")
+        loss, tok = m(ids.cuda(), attention_mask=mask, labels=labels.cuda())
+        loss.backward()
+        res.append((loss.detach().float(), tok.detach().float(),
+                    {n: p.grad.detach().float() for n, p in m.named_parameters() if p.grad is not None}))
+    assert calls["n"] == 2                       # both layers, grouped run only
+    (l1, t1, g1), (l0, t0, g0) = res
+    assert abs(l1.item() - l0.item()) <= 1e-2 * abs(l0.item())
+    real = mask.cuda().bool()
+    assert (t1[real] - t0[real]).abs().max().item() <= 2e-2 * t0[real].abs().max().item()
+    assert g1.keys() == g0.keys()
+    for n in g0:
+        assert (g1[n] - g0[n]).abs().max().item() <= 3e-2 * g0[n].abs().max().item() + 1e-6, n
