@@ -68,12 +68,16 @@ def main():
                    help="one process = rank 0 of an N-GPU DDP job (loopback DP group, comm/loopback.py): "
                         "the rank's exact per-step work with the collectives as local stand-ins; the JSON "
                         "line then reports the rank's ms/step, not a job throughput")
-    p.add_argument("--miopen-prewarm", type=int, default=1,
+    p.add_argument("--miopen-prewarm", type=int, default=0,
                    help="before timing, run 13 steps in a child process so MIOpen's find database and "
-                        "kernel cache exist: on a fresh box the first process of a model ran 418-540 ms "
-                        "per ResNet-50 step for its whole life and the next ones 31-48 ms (a 2-step child "
-                        "was not enough: the process after it was still slow), profiles/r4_vision/")
+                        "kernel cache exist. Round 4 needed it (a first process ran 418-540 ms per "
+                        "ResNet-50 step for its whole life, profiles/r4_vision/; the MIOpen grouped-conv "
+                        "augmentation behind that is gone); since round 5 a fresh process runs at the "
+                        "warm rate and the shipped find / perf db (utils/miopen.py) cuts its start-up "
+                        "84 -> 22 s (profiles/r5_miopen/), so it is off by default")
     a = p.parse_args()
+    from smdt_amd.utils.miopen import seed_user_db
+    seed_user_db()
     # (device_count() does not initialise the GPU in this process)
     if (a.miopen_prewarm and torch.cuda.device_count() > 0 and os.environ.get("LOCAL_RANK", "0") == "0"
             and not os.environ.get("SMDT_VISION_PREWARM")):

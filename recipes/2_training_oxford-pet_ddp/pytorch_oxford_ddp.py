@@ -39,6 +39,7 @@ from smdt_amd.comm import init_distributed  # noqa: E402
 from smdt_amd.data.image_folder import AugmentPrefetcher, GpuAugment, ImageFolderDataset  # noqa: E402
 from smdt_amd.optim.optimizer import MixedPrecisionAdam  # noqa: E402
 from smdt_amd.train.graphs import CapturedStep  # noqa: E402
+from smdt_amd.utils.miopen import seed_user_db  # noqa: E402
 from smdt_amd.parallel.distributed import DistributedDataParallel as DDP  # noqa: E402
 
 logger = logging.getLogger(__name__)
@@ -273,6 +274,9 @@ def validate(val_loader, model, criterion, epoch, model_history, args, aug, use_
 
 def main(argv=None):
     print("start main function")
+    # MIOpen's find / perf databases of this recipe's models on gfx950, seeded before the first
+    # convolution: a fresh job skips the per-config solver search (utils/miopen.py)
+    seed_user_db()
     args = args_fn(argv)
     args = check_sagemaker(args)
     args = dist_setting(args)

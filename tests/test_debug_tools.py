@@ -143,3 +143,26 @@ def test_host_runtime_under_asan_ubsan(tmp_path):
                        env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert "runtime OK under ASan+UBSan" in r.stdout
+
+
+def test_miopen_user_db_seeding(tmp_path, monkeypatch):
+    """utils/miopen.seed_user_db: the shipped gfx950 find / perf databases (text) land in
+    MIOPEN_USER_DB_PATH before the first convolution, and whatever MIOpen already wrote there is
+    kept."""
+    from smdt_amd.utils import miopen
+    files = miopen.shipped_files()
+    assert any(f.endswith(".ufdb.txt") for f in files) and any(f.endswith(".udb.txt") for f in files)
+    target = tmp_path / "udb"
+    target.mkdir()
+    keep = target / files[0]
+    keep.write_text("written by MIOpen\n")
+    monkeypatch.setenv("MIOPEN_USER_DB_PATH", str(target))
+    assert miopen.seed_user_db() == str(target)
+    assert keep.read_text() == "written by MIOpen\n"
+    for f in files[1:]:
+        assert (target / f).read_bytes() == open(os.path.join(miopen._SHIPPED, f), "rb").read()
+    # no MIOPEN_USER_DB_PATH: a per-user cache directory becomes it
+    monkeypatch.delenv("MIOPEN_USER_DB_PATH")
+    monkeypatch.setenv("HOME", str(tmp_path / "home"))
+    d = miopen.seed_user_db()
+    assert d == os.environ["MIOPEN_USER_DB_PATH"] and sorted(os.listdir(d)) == files
