@@ -399,7 +399,8 @@ class HFCausalLM(nn.Module):
             from . import transformer as _T
             from .transformer import packed_sequences
             b, L = input_ids.shape
-            groups = (_T.length_groups(attention_mask.bool(), idx, input_ids.device)
+            groups = (_T.length_groups(attention_mask.bool(), idx, input_ids.device,
+                                       hidden=None if _T._LENGTH_GROUPS_FORCE else int(self.cfg.hidden_size))
                       if _T._LENGTH_GROUPS and input_ids.is_cuda else None)
             idx = idx.to(input_ids.device, non_blocking=True)
             tok = input_ids.t().reshape(-1).index_select(0, idx).unsqueeze(0)          # [1, T]

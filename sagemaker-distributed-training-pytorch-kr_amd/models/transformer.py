@@ -190,16 +190,28 @@ class _GatherRows(torch.autograd.Function):
 # [sum_g L_g b_g, W] buffer: ONE row gather in, the causal flash kernels per block on views of
 # it (no copies either way), ONE gather out. Real-token results equal the [L, b] layout's: a real
 # token still sees exactly its own row's earlier tokens.
-_LENGTH_GROUPS = os.environ.get("SMDT_SFT_LENGTH_GROUPS", "1") == "1"
+_LENGTH_GROUPS = os.environ.get("SMDT_SFT_LENGTH_GROUPS", "1") in ("1", "force")   # force: skip the cost gate
+_LENGTH_GROUPS_FORCE = os.environ.get("SMDT_SFT_LENGTH_GROUPS", "1") == "force"
 _GROUP_ALIGN = 128
 
 
-def length_groups(mask_cpu, idx_cpu, device):
+# When the grouping pays: the attention work it saves is ~7 x (b L^2 saved) x hidden FLOPs per
+# layer (forward + backward, at ~150 TFLOP/s for the padded causal kernels at these lengths);
+# each extra block costs per layer its own launches and host work, calibrated at 250 us from the
+# two NB4 models: OPT-125m (hidden 768) ran 11 % slower grouped, LLaMA-7B (4096) 6-7 % faster
+# (profiles/r5_sft_groups/).
+_GROUP_LAUNCH_S = 250e-6
+_GROUP_FLOPS = 1.5e14
+
+
+def length_groups(mask_cpu, idx_cpu, device, hidden: int = None):
     """Host-side (CPU, no device sync) plan of the length-grouped layout for a right-padded
     [b, L] CPU ``mask_cpu`` whose packed tokens are the seq-first positions ``idx_cpu``:
     ``{"blocks": [(row offset, L_g, b_g)], "inv": [P] packed index of each grouped position
     (-1 = pad), "pack": [T] grouped position of each packed token (-1: a trailing pad token
-    beyond its row's block, whose attention output is then 0)}``, the maps on ``device``."""
+    beyond its row's block, whose attention output is then 0)}``, the maps on ``device``. None
+    when, for a model of this ``hidden`` size, the attention work saved would not pay for the
+    extra launches."""
     b, L = mask_cpu.shape
     lens = mask_cpu.sum(1).clamp(min=1)
     Lr = ((lens + _GROUP_ALIGN - 1) // _GROUP_ALIGN) * _GROUP_ALIGN          # per-row block length
@@ -217,6 +229,10 @@ def length_groups(mask_cpu, idx_cpu, device):
         row_b[rows] = bg
         row_L[rows] = Lg
         off += int(Lg) * bg
+    if hidden is not None:
+        saved = b * L * L - sum(bg * Lg * Lg for _, Lg, bg in blocks)
+        if 7.0 * saved * hidden / _GROUP_FLOPS < (len(blocks) - 1) * _GROUP_LAUNCH_S:
+            return None
     s_t, i_t = idx_cpu // b, idx_cpu % b
     ok = s_t < row_L[i_t]
     pos = row_off[i_t] + s_t * row_b[i_t] + row_j[i_t]

@@ -116,6 +116,21 @@ def test_packed_rows_gather_kernel_matches_index_ops():
     torch.testing.assert_close(x.grad.squeeze(1), gx)
 
 
+def test_length_groups_cost_gate():
+    """The grouping is planned only when the attention work it saves pays for its extra launches:
+    a LLaMA-7B-sized hidden groups an Alpaca-like window, an OPT-125m-sized one does not."""
+    import torch
+    from smdt_amd.models import transformer as T
+    b, L = 32, 512
+    g = torch.Generator().manual_seed(0)
+    lens = torch.randint(40, 300, (b,), generator=g)
+    lens[0] = 500
+    mask = torch.arange(L).unsqueeze(0) < lens.unsqueeze(1)
+    idx = torch.tensor(sorted(s * b + i for s in range(L) for i in range(b) if s < lens[i]), dtype=torch.int64)
+    assert T.length_groups(mask, idx, "cpu", hidden=4096) is not None
+    assert T.length_groups(mask, idx, "cpu", hidden=768) is None
+
+
 def test_length_groups_plan_maps():
     """The length-grouped attention layout's host plan (models/transformer.length_groups): rows
     bucketed by their own length rounded up to 128, blocks [L_g, b_g] back to back; every real
@@ -172,6 +187,7 @@ def test_length_grouped_attention_matches_padded_layout(monkeypatch):
         calls["n"] += 1
         return orig(self, *a)
     monkeypatch.setattr(T.ParallelAttention, "_attend_groups", counted)
+    monkeypatch.setattr(T, "_GROUP_LAUNCH_S", 0.0)   # group even this small model (the cost gate)
     res = []
     for on in (True, False):
         monkeypatch.setattr(T, "_LENGTH_GROUPS", on)
