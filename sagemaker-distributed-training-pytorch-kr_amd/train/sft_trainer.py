@@ -54,7 +54,9 @@ def setup_distributed(args=None, backend: str = "nccl"):
         rank, world = dist.get_rank(), dist.get_world_size()
         local = int(os.environ.get("LOCAL_RANK", "0"))
     else:  # single process: no process group is created
-        rank, local, world, _ = init_distributed(backend)
+        # SMDT_DIST_BACKEND=gloo: one-GPU rehearsal of the multi-rank path (RCCL refuses two ranks
+        # on one device)
+        rank, local, world, _ = init_distributed(os.environ.get("SMDT_DIST_BACKEND", backend))
     emu = int(os.environ.get("SMDT_EMULATE_DP", "0") or 0)
     if emu > 1 and world == 1:
         # timing: this process does ONE data-parallel rank's work of an emu-GPU ZeRO job — its own
@@ -63,7 +65,8 @@ def setup_distributed(args=None, backend: str = "nccl"):
         ps.initialize_emulated_tensor_parallel(1, emu)
     elif not ps.model_parallel_is_initialized():
         ps.initialize_model_parallel(1, 1)
-    dev = torch.device("cuda", local) if torch.cuda.is_available() else torch.device("cpu")
+    # the device init_distributed selected (local_rank modulo the visible devices)
+    dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
     if args is not None:
         args.local_rank = local
     return rank, local, world, dev
