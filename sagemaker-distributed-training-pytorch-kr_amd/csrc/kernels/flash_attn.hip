@@ -187,11 +187,22 @@ __device__ __forceinline__ v8_t<E> rowconst_terms(float x, int h) {
   }
   return v;
 }
+// The dK / dV kernel's 16-byte row of BOTH constants: x's terms in k-slots 0..2, y's in 4..6, so
+// one LDS row per query feeds both accumulator starts (rowconst_ones<E>(h, 0) picks x,
+// rowconst_ones<E>(h, 4) picks y).
 template <class E>
-__device__ __forceinline__ v8_t<E> rowconst_ones(int h) {
+__device__ __forceinline__ v8_t<E> rowconst_pair(float x, float y) {
+  const v8_t<E> a = rowconst_terms<E>(x, 0), c = rowconst_terms<E>(y, 0);
+  v8_t<E> v = a;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) v[4 + j] = c[j];
+  return v;
+}
+template <class E>
+__device__ __forceinline__ v8_t<E> rowconst_ones(int h, int first = 0) {
   v8_t<E> v;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) v[j] = (E)((h == 0 && j < 3) ? 1.f : 0.f);
+  for (int j = 0; j < 8; ++j) v[j] = (E)((h == 0 && j >= first && j < first + 3) ? 1.f : 0.f);
   return v;
 }
 
@@ -527,8 +538,7 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void fwd_kernel(const E* __re
 // dK / dV. Workgroup = 4 waves = 128 keys of one (b, kv-head); each wave keeps K, V of its 32
 // keys and dK^T, dV^T in registers while the workgroup sweeps the query heads of the group and
 // their 64-row query tiles (Q, dO, lse*log2e, delta staged in double-buffered LDS).
-// Workgroups per CU requested from the compiler for the D = 64 backward kernels (A/B knobs:
-// 3 caps them at 168 VGPRs, which spills).
+// Workgroups per CU requested from the compiler for the D = 64 backward kernels (A/B knobs).
 #ifndef SMDT_FA_DQ_OCC
 #define SMDT_FA_DQ_OCC 2
 #endif
@@ -538,24 +548,29 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void fwd_kernel(const E* __re
 #ifndef SMDT_FA_DQ_REMAT
 #define SMDT_FA_DQ_REMAT 2
 #endif
-#ifndef SMDT_FA_DKDV_OCC
-#define SMDT_FA_DKDV_OCC 2
-#endif
 #ifndef SMDT_FA_DKDV_ROLLED
 #define SMDT_FA_DKDV_ROLLED 0
+#endif
+// The two row constants share one 16-byte LDS row per query: 52,992 B of LDS per workgroup, so
+// three workgroups would fit a CU (56,064 B before). Asking the compiler for 3 (168 VGPRs) spills
+// 140 B per lane in the dropout variant and measured 605 vs 564 us per call at the bench shape
+// (profiles/r5_dkdv_occ/): the kernel stays at 2 workgroups per CU.
+#ifndef SMDT_FA_DKDV_OCC
+#define SMDT_FA_DKDV_OCC 2
 #endif
 template <int D, bool CAUSAL, bool DROP, class E>
 __global__ __launch_bounds__(256, D == 64 ? SMDT_FA_DKDV_OCC : 1) void bwd_dkdv_kernel(
     const E* __restrict__ Q, const E* __restrict__ K, const E* __restrict__ V,
-    const E* __restrict__ dO, const E* __restrict__ LSE3, const E* __restrict__ DL3,
+    const E* __restrict__ dO, const E* __restrict__ RC3,
     const float* __restrict__ DELTA, E* __restrict__ dK, E* __restrict__ dV, int B, int H, int Hkv, int S,
     Strides qs, Strides ks_, Strides vs, Strides dos, Strides dks, Strides dvs, float scale, Drop drop) {
   using G = Geo<D>;
   using VF = v8_t<E>;
-  // Q | dO | the tile's 64 query rows of the row constants as 16-bit term rows (16 B each, written
-  // by the dQ kernel: -(lse log2e - log2 inv), then -delta') | -delta' fp32 (dropout only)
+  // Q | dO | the tile's 64 query rows of the row constants as ONE 16-bit term row each (16 B,
+  // written by the dQ kernel: -(lse log2e - log2 inv) in k-slots 0..2, -delta' in 4..6) | -delta'
+  // fp32 (dropout only)
   constexpr int kRC = kTile * 16;
-  constexpr int RCB = 2 * kRC + kTile * 4;
+  constexpr int RCB = kRC + kTile * 4;
   // D = 64: three stage slots, two work items in flight; D = 128: two (LDS budget). Q, dO and the
   // row constants of a slot are SEPARATE __shared__ objects: with one object per slot the compiler
   // drained the DMA queue (s_waitcnt vmcnt(0)) between the Q and the dO pieces of every item,
@@ -602,7 +617,7 @@ __global__ __launch_bounds__(256, D == 64 ? SMDT_FA_DKDV_OCC : 1) void bwd_dkdv_
   v8_t<E> kf[G::KS], vf[G::KS];
   load_reg_frags<D>(K + b * ks_.sb + hk * ks_.sh, ks_.ss, kw, lane, kf);
   load_reg_frags<D>(V + b * vs.sb + hk * vs.sh, vs.ss, kw, lane, vf);
-  const VF ones3 = rowconst_ones<E>(h);
+  const VF ones_l = rowconst_ones<E>(h, 0), ones_d = rowconst_ones<E>(h, 4);
 #pragma unroll
   for (int kk = 0; kk < G::KS; ++kk) kf[kk] = scale8(kf[kk], scale * kLog2e);  // S in log2 domain
 
@@ -632,10 +647,10 @@ __global__ __launch_bounds__(256, D == 64 ? SMDT_FA_DKDV_OCC : 1) void bwd_dkdv_
     gq.issue(Q + b * qs.sb + hq * qs.sh + (int64_t)qb * qs.ss, qbuf(sl), w);
     gdo.issue(dO + b * dos.sb + hq * dos.sh + (int64_t)qb * dos.ss, obuf(sl), w);
     const int64_t r0 = ((int64_t)b * H + hq) * S + qb;
-    if (w < 2) {
-      dma_lds16((w == 0 ? LSE3 : DL3) + r0 * 8, lane_now() << 4, rbuf(sl) + w * kRC);
-    } else if (DROP && w == 2) {
-      dma_lds4(DELTA + r0, lane_now() << 2, rbuf(sl) + 2 * kRC);
+    if (w == 0) {
+      dma_lds16(RC3 + r0 * 8, lane_now() << 4, rbuf(sl));
+    } else if (DROP && w == 1) {
+      dma_lds4(DELTA + r0, lane_now() << 2, rbuf(sl) + kRC);
     }
     ++issued;
     if (++iq_n == ntiles) {
@@ -644,7 +659,7 @@ __global__ __launch_bounds__(256, D == 64 ? SMDT_FA_DKDV_OCC : 1) void bwd_dkdv_
     }
   };
   auto wait_next = [&]() {  // the next item's DMA has landed (a later one may still be in flight)
-    if (w < 2 || (DROP && w == 2)) wait_vm<(kBuf - 2) * (kPer + 1)>();
+    if (w == 0 || (DROP && w == 1)) wait_vm<(kBuf - 2) * (kPer + 1)>();
     else wait_vm<(kBuf - 2) * kPer>();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
@@ -669,9 +684,8 @@ __global__ __launch_bounds__(256, D == 64 ? SMDT_FA_DKDV_OCC : 1) void bwd_dkdv_
     const uint32_t dblk = ((uint32_t)((qb + 4 * h) >> 1) + (uint32_t)(my_key & 1)) * shalf + (uint32_t)(my_key >> 1);
     const char* q_l = qbuf(cur);
     const char* do_l = obuf(cur);
-    const char* lse3_l = rbuf(cur);
-    const char* dl3_l = lse3_l + kRC;
-    const float* del_l = reinterpret_cast<const float*>(dl3_l + kRC);
+    const char* rc_l = rbuf(cur);
+    const float* del_l = reinterpret_cast<const float*>(rc_l + kRC);
     issue(pre);
     // S'[q, key] = Q . K'^T - lse ; dP'[q, key] = dO . V^T - delta  (key on lane, query rows in
     // registers). The row constants enter as one MFMA k-step ahead of each chain (A = the query
@@ -679,8 +693,9 @@ __global__ __launch_bounds__(256, D == 64 ? SMDT_FA_DKDV_OCC : 1) void bwd_dkdv_
     // zeros): no accumulator moves. The causal diagonal block masks key > query after the chain.
     auto sd_init = [&](int qs2, f32x16& sa, f32x16& pa) {
       const int r = 32 * qs2 + (lane & 31);
-      sa = mfma(*reinterpret_cast<const VF*>(lse3_l + 16 * r), ones3, zero16());
-      pa = mfma(*reinterpret_cast<const VF*>(dl3_l + 16 * r), ones3, zero16());
+      const VF rc = *reinterpret_cast<const VF*>(rc_l + 16 * r);
+      sa = mfma(rc, ones_l, zero16());
+      pa = mfma(rc, ones_d, zero16());
     };
     auto diag_mask = [&](f32x16& sa) {
 #pragma unroll
@@ -830,7 +845,7 @@ template <int D, bool CAUSAL, bool DROP, class E>
 __global__ __launch_bounds__(256, D == 64 ? SMDT_FA_DQ_OCC : 1) void bwd_dq_kernel(
     const E* __restrict__ Q, const E* __restrict__ K, const E* __restrict__ V,
     const E* __restrict__ dO, const E* __restrict__ O, const float* __restrict__ LSE,
-    float* __restrict__ DELTA, E* __restrict__ LSE3, E* __restrict__ DL3, E* __restrict__ dQ, int B, int H, int Hkv,
+    float* __restrict__ DELTA, E* __restrict__ RC3, E* __restrict__ dQ, int B, int H, int Hkv,
     int S, Strides qs, Strides ks_, Strides vs, Strides dos, Strides os, Strides dqs, float scale,
     float dscale, float lsub, Drop drop) {
   using G = Geo<D>;
@@ -892,10 +907,9 @@ __global__ __launch_bounds__(256, D == 64 ? SMDT_FA_DQ_OCC : 1) void bwd_dq_kern
     ndl = -xhalf_sum(acc) * dscale;
   }
   const float nlse2 = lsub - LSE[ridx] * kLog2e;
-  if (h == 0) {   // for the dK / dV kernel: fp32 -delta' (dropout path) and both as term rows
+  if (h == 0) {   // for the dK / dV kernel: fp32 -delta' (dropout path) and both in one term row
     DELTA[ridx] = ndl;
-    *reinterpret_cast<v8_t<E>*>(LSE3 + ridx * 8) = rowconst_terms<E>(nlse2, 0);
-    *reinterpret_cast<v8_t<E>*>(DL3 + ridx * 8) = rowconst_terms<E>(ndl, 0);
+    *reinterpret_cast<v8_t<E>*>(RC3 + ridx * 8) = rowconst_pair<E>(nlse2, ndl);
   }
 #if SMDT_FA_DQ_REMAT == 2
   // The row constants enter as one extra MFMA k-step per chain: A = 1 in k-slots 0..2 of every
@@ -1131,10 +1145,9 @@ extern "C" hipError_t smdt_flash_bwd(int dtype, const void* q, const void* k, co
       dks{strides[18], strides[19], strides[20]}, dvs{strides[21], strides[22], strides[23]};
   // delta holds 10 x [B, H, S] fp32 words, written by the dQ kernel (which therefore runs first)
   // and read by the dK / dV kernel: -delta' rows, then (after one unused [B, H, S] slot) the
-  // 16-byte term rows of -(lse log2e - log2 inv) and of -delta' (see rowconst_terms)
+  // 16-byte term rows of -(lse log2e - log2 inv) and -delta' (see rowconst_pair)
   const int64_t bhs = (int64_t)B * H * S;
-  void* lse3 = delta + 2 * bhs;
-  void* dl3 = delta + 6 * bhs;
+  void* rc3 = delta + 2 * bhs;
   const float dscale = drop ? dr.keep : 1.f, lsub = drop ? dr.log2inv : 0.f;
   dim3 gkv((unsigned)((int64_t)B * Hkv * (S / kBlockRows)));
   dim3 gq((unsigned)((int64_t)B * H * (S / kBlockRows)));
@@ -1142,12 +1155,11 @@ extern "C" hipError_t smdt_flash_bwd(int dtype, const void* q, const void* k, co
   do {                                                                                           \
     hipLaunchKernelGGL((bwd_dq_kernel<DD, CC, DR, ET>), gq, dim3(256), 0, st, (const ET*)q,      \
                        (const ET*)k, (const ET*)v, (const ET*)dout, (const ET*)o, lse, delta,     \
-                       (ET*)lse3, (ET*)dl3, (ET*)dq, B, H, Hkv, S, qs, ks, vs, dos, os, dqs,      \
+                       (ET*)rc3, (ET*)dq, B, H, Hkv, S, qs, ks, vs, dos, os, dqs,                 \
                        scale, dscale, lsub, dr);                                                  \
     hipLaunchKernelGGL((bwd_dkdv_kernel<DD, CC, DR, ET>), gkv, dim3(256), 0, st, (const ET*)q,  \
-                       (const ET*)k, (const ET*)v, (const ET*)dout, (const ET*)lse3,              \
-                       (const ET*)dl3, delta, (ET*)dk, (ET*)dv, B, H, Hkv, S, qs, ks, vs, dos,    \
-                       dks, dvs, scale, dr);                                                      \
+                       (const ET*)k, (const ET*)v, (const ET*)dout, (const ET*)rc3, delta,        \
+                       (ET*)dk, (ET*)dv, B, H, Hkv, S, qs, ks, vs, dos, dks, dvs, scale, dr);     \
   } while (0)
 #define SMDT_FA_BWD(DD, CC, DR) \
   do { if (dtype == 2) SMDT_FA_BWD_T(DD, CC, DR, f16); else SMDT_FA_BWD_T(DD, CC, DR, bf16); } while (0)

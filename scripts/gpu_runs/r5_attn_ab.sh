@@ -11,6 +11,8 @@ A="--b 64 --sdpa 0 --dropout 0.1"
 for i in $(seq 1 ${ROUNDS:-3}); do
   run ref_$i 150 python benchmarks/bench_attention.py $A --ext benchmarks/bin/ab_ref_C.so
   run new_$i 150 python benchmarks/bench_attention.py $A
+  # optional third arm: the new build under extra environment (e.g. NEW_ENV2=SMDT_FA_DKDV_OCC=2)
+  if [ -n "${NEW_ENV2:-}" ]; then run new2_$i 150 env $NEW_ENV2 python benchmarks/bench_attention.py $A; fi
 done
 cd /tmp
 run prof_new 200 rocprofv3 --kernel-trace --stats -d "$O/prof_new" -o run --output-format csv -- python3 "$R/benchmarks/bench_attention.py" $A
