@@ -542,6 +542,9 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void fwd_kernel(const E* __re
 #ifndef SMDT_FA_DQ_OCC
 #define SMDT_FA_DQ_OCC 2
 #endif
+#ifndef SMDT_FA_DQ_BUF
+#define SMDT_FA_DQ_BUF 3   // K / V stage slots of the D = 64 dQ kernel
+#endif
 // dQ: re-make the two accumulator splats (-lse', -delta') per 32-key sub-tile instead of pinning
 // them for the whole kernel: 178 -> 140 VGPRs, 2 -> 3 waves per SIMD, no spills; measured bwd
 // 1.014 / 1.041 -> 0.991 / 1.004 ms at B64 (profiles/r2_attn_order/ab_b64_dq_remat.log).
@@ -851,7 +854,7 @@ __global__ __launch_bounds__(256, D == 64 ? SMDT_FA_DQ_OCC : 1) void bwd_dq_kern
   using G = Geo<D>;
   // D = 64: three [K | V] buffers, two tiles in flight; D = 128 (twice the bytes): two buffers,
   // so two workgroups still fit a CU's 160 KB of LDS.
-  constexpr int kBuf = D == 64 ? 3 : 2;
+  constexpr int kBuf = D == 64 ? SMDT_FA_DQ_BUF : 2;
   __shared__ __attribute__((aligned(16))) char L0[2 * G::TB], L1[2 * G::TB], L2[kBuf == 3 ? 2 * G::TB : 16];
 
   const int lane = threadIdx.x & 63, h = lane >> 5;
