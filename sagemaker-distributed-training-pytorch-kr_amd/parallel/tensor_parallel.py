@@ -1175,6 +1175,7 @@ def linear_with_grad_accumulation_and_async_allreduce(x, weight, bias, sequence_
 # -> wgrad GEMM -> wait", arguments.py:837-842, with the grouped MFMA wgrad as the overlapped work).
 
 _TP_OVERLAP = os.environ.get("SMDT_TP_OVERLAP", "1") == "1"
+_LB_RING_ASYNC = os.environ.get("SMDT_LOOPBACK_RING_ASYNC", "0") == "1"
 
 
 def _ring(group):
@@ -1193,7 +1194,10 @@ def _exchange(send, recv, nxt, prv, group):
         # single-process TP emulation: the transfer as a local copy on the compute stream (issuing
         # it on the loopback side stream, as the real exchange runs beside the chunk GEMM, measured
         # SLOWER: 202.4 -> 219.7 ms per stage-1 rank, the per-exchange stream hand-offs cost more
-        # than the overlap gains; profiles/r4_loopback_ring_async_neg/)
+        # than the overlap gains; profiles/r4_loopback_ring_async_neg/). SMDT_LOOPBACK_RING_ASYNC=1
+        # re-runs that arm (the side stream is now a high-priority one).
+        if _LB_RING_ASYNC and send.is_cuda:
+            return [group._issue([send, recv], lambda: recv.copy_(send), [recv])]
         recv.copy_(send)
         return []
     if nxt == prv:
