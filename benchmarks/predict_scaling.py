@@ -156,6 +156,7 @@ def predict(m: dict) -> list:
         for r in pipeline_rows(m, "tp2pp2_stage0", "tp2pp2_stage1", 8, 2, act, dp_tail + embd + 0.5, tok1 * 8,
                                "tp2pp2dp2+sp+zero1 13|11", even="tp2pp2_stage1_even" if "tp2pp2_stage1_even" in m else None):
             rows.append({"N": 8, "model": "gpt2-345m", **r})
+        rows += gpt2_tp2_exchange_rows(m, act, dp_tail + embd + 0.5, tok1 * 8)
     if "tp2pp2_mb64_stage0" in m and "tp2pp2_mb64_stage1" in m:
         act64 = (S // 2) * 64 * H * 2
         for r in pipeline_rows(m, "tp2pp2_mb64_stage0", "tp2pp2_mb64_stage1", 4, 2, act64, dp_tail + embd + 0.5,
@@ -194,6 +195,64 @@ def _rs_exposed(g: float, t_x: float, k: int, wq: float = 0.0) -> float:
         e = max(e, c) + t_x / k
     c += wq
     return max(c, e) - (g + wq)
+
+
+SYNC_MS = 0.012   # per-exchange cross-stream hand-off, eager (profiles/r5_lb_async_neg/: 10.5 ms / 869)
+
+
+def _ring2_exposed(g: float, t_x: float, wq: float = 0.0) -> float:
+    """A 2-rank ring collective-matmul (``ag_ring`` / ``rs_ring`` at tp = 2): the transfer (t_x)
+    runs beside ONE of the two chunk GEMMs (g / 2) and, in backward, the weight-gradient GEMMs
+    drained before the wait (wq)."""
+    return max(0.0, t_x - g / 2 - wq)
+
+
+def gpt2_tp2_exchange_model(W_mb_ms: float, layers: int, mb: int, t_x: float, sync_ms: float = SYNC_MS) -> dict:
+    """Exposed SP-exchange time per step of one tp2 stage of the BASELINE N = 8 layout: per layer
+    and micro-batch 8 exchanges (forward AG qkv / RS proj / AG fc1 / RS fc2; backward AG fc2 /
+    RS fc1 / AG proj / RS qkv), each against its own chunk GEMMs priced from the stage's measured
+    weight-gradient time per micro-batch (W / layers, split by FLOPs qkv 3 : proj 1 : fc1 4 :
+    fc2 4), backward ones with their linear's wgrad as the drained queue; plus ``sync_ms`` per
+    exchange for the side-stream hand-off the emulation does not pay (it copies in line)."""
+    g = W_mb_ms / layers
+    gl = {n: g * f for n, f in {"qkv": 3 / 12, "proj": 1 / 12, "fc1": 4 / 12, "fc2": 4 / 12}.items()}
+    fwd = sum(_ring2_exposed(gl[n], t_x) for n in ("qkv", "proj", "fc1", "fc2"))
+    bwd = sum(_ring2_exposed(gl[n], t_x, wq=gl[n]) for n in ("fc2", "fc1", "proj", "qkv"))
+    per_step = layers * mb * (fwd + bwd + 8 * sync_ms)
+    return {"fwd_per_layer_mb": fwd, "bwd_per_layer_mb": bwd, "exposed_ms": per_step}
+
+
+def gpt2_tp2_exchange_rows(m: dict, act_bytes: float, other_exposed: float, tok: float) -> list:
+    """The N = 8 zbh2 row again with the TP-pair exchanges SIMULATED instead of assumed hidden:
+    one [s/2, 32, h] bf16 chunk per exchange, over the relay (every TP pair of the node exchanging
+    at once: each directed link carries 2/8 of a message, W/2 = 4 links' worth, docs/XGMI.md) or,
+    if the relay lost its start-up timing, over RCCL's single link. Each stage pays its own
+    exposure; the slower stage sets the step."""
+    names = ("tp2pp2_stage0", "tp2pp2_stage1")
+    if not all(n in m and m[n].get("fbw_ms") for n in names):
+        return []
+    base = [r for r in pipeline_rows(m, names[0], names[1], 8, 2, act_bytes, other_exposed, tok,
+                                     "tp2pp2dp2+sp+zero1 13|11") if r["layout"].endswith("zbh2")][0]
+    ex_bytes = (S // 2) * 32 * H * 2
+    rows = []
+    for links, name in ((4.0, "relay, all 4 pairs at once"), (1.0, "RCCL p2p, one link")):
+        # (layout keys: "... TP exchange relay" / "... TP exchange RCCL p2p"; the rest goes to the note)
+        t_x = link_ms(ex_bytes, links)
+        exp, notes = [], []
+        for n, layers in zip(names, (13, 11)):
+            mdl = gpt2_tp2_exchange_model(m[n]["fbw_ms"]["W"], layers, 8, t_x)
+            exp.append(mdl["exposed_ms"])
+            notes.append(f"fwd {mdl['fwd_per_layer_mb']:.3f} / bwd {mdl['bwd_per_layer_mb']:.3f}")
+        stage = [m[n]["ms_per_step"] + e for n, e in zip(names, exp)]
+        pred = max(stage) + base["bubble_ms"] + other_exposed
+        rows.append({"N": 8, "model": "gpt2-345m", "layout": f"tp2pp2dp2+sp+zero1 13|11, zbh2, TP exchange {name.split(',')[0]}",
+                     "compute_ms": base["compute_ms"], "stage_ms": base["stage_ms"], "bubble_ms": base["bubble_ms"],
+                     "exposed_comm_ms": round(max(stage) - base["compute_ms"] + other_exposed, 1),
+                     "predicted_ms": round(pred, 1), "tokens_per_step": tok,
+                     "note": f"{name}: {t_x * 1e3:.0f} us per {ex_bytes / 1e6:.1f} MB exchange; exposed per layer and "
+                             f"micro-batch (stage 0 ; stage 1) {' ; '.join(notes)} ms + {SYNC_MS * 1e3:.0f} us "
+                             f"hand-off per exchange; stages with exposure {stage[0]:.1f} / {stage[1]:.1f} ms"})
+    return rows
 
 
 def gpt3_exchange_model(W_ms: float, layers: int, mb: int, t_x: float, tp: int, k: int) -> dict:

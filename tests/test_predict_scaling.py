@@ -1,7 +1,8 @@
 """benchmarks/predict_scaling.py's tables from synthetic per-stage measurements (CPU): the
 schedule rows are ordered as the simulator says (zbh1 <= zb <= 1f1b bubble) and the GPT-3 TP4
 rows charge the one-link ring more than the three-link exchange, and the direct exchange's row
-pieces (simulated per exchange against its own GEMMs) less than whole chunks."""
+pieces (simulated per exchange against its own GEMMs) less than whole chunks; the GPT-2 N = 8
+TP-pair exchanges, simulated the same way, cost more over one link than over the relay."""
 import json
 import os
 import subprocess
@@ -30,6 +31,12 @@ def test_prediction_tables(tmp_path):
     assert n8["zbh2"]["bubble_ms"] <= n8["zbh1"]["bubble_ms"] <= n8["zb"]["bubble_ms"] <= n8["1f1b"]["bubble_ms"]
     assert n8["zbh1"]["efficiency_vs_n1"] > n8["1f1b"]["efficiency_vs_n1"]
     assert "interleaved vpp2 (even 12|12 split)" in n8
+    # the TP-pair exchanges simulated per exchange: the relay (4 links' worth) exposes less than
+    # RCCL's single link, and both more than the assumed-hidden zbh2 row
+    rl = n8["TP exchange relay"]
+    one = n8["TP exchange RCCL p2p"]
+    assert n8["zbh2"]["predicted_ms"] < rl["predicted_ms"] < one["predicted_ms"]
+    assert rl["bubble_ms"] == n8["zbh2"]["bubble_ms"]
     g3 = out["gpt3_rows"]
     assert len(g3) == 4
     ex = [row["exposed_comm_ms"] for row in g3]   # ring, direct whole chunks, 2 pieces, 4 pieces
