@@ -571,6 +571,36 @@ class ParallelTransformerLayer(nn.Module):
         m, mb = self.mlp(ln2)
         return m, mb, residual
 
+    def forward_phases(self, st):
+        """``forward`` cut at its four sequence-parallel exchanges for the sub-batch interleave
+        (``ParallelTransformer._forward_subbatch``): each phase ends right after it STARTS an
+        exchange (the norms' all-gathers by ``tp.ag_start``; the row-parallel linears' reduce-
+        scatters are left in flight by ``rs_ring`` under ``tp.begin_subbatch``) and the next phase
+        of this half begins by completing it. ``st`` holds this half's (x, xbias, residual)."""
+        training = self.training
+        p = self.cfg.hidden_dropout
+        g = _sp_gather(self.cfg)
+        group = ps.get_state().tp_group
+        x, residual = tp.rs_finish(st["x"]), st["residual"]
+        ln1, residual = self.input_norm.fused(x, st["xbias"], residual, p, training,
+                                              gather=None if g is None else g + (True, residual is not None))
+        tp.ag_start(ln1, group)
+        yield
+        a, ab = self.attention(ln1, training)
+        yield
+        ln2, residual = self.post_attention_norm.fused(tp.rs_finish(a), ab, residual, p, training,
+                                                       gather=None if g is None else g + (True, True))
+        tp.ag_start(ln2, group)
+        yield
+        m, mb = self.mlp(ln2)
+        st.update(x=m, xbias=mb, residual=residual)
+        yield
+
+
+# Sub-batch interleave of the sequence-parallel TP-pair exchanges (tp.begin_subbatch). "2": the
+# two batch halves of a micro-batch alternate phase by phase; "0" (default) off.
+_SUBBATCH = int(os.environ.get("SMDT_SP_SUBBATCH", "0") or 0)
+
 
 class ParallelTransformer(nn.Module):
     """A stack of layers [first, first + n) of the full model (pipeline stages own a slice)."""
@@ -598,11 +628,50 @@ class ParallelTransformer(nn.Module):
             return rng_checkpoint(layer, x, xb, res)
         return layer(x, xb, res)
 
+    def _subbatch_ok(self, x) -> bool:
+        cfg = self.cfg
+        st = ps.get_state()
+        return (_SUBBATCH == 2 and self.training and torch.is_grad_enabled() and cfg.sequence_parallel
+                and st.tp == 2 and st.cp == 1 and cfg.recompute_granularity != "full" and _PACK["idx"] is None
+                and tp.sp_gather_spec() is not None and x.dim() == 3 and x.shape[1] % 2 == 0
+                and len(self.layers) > 0)
+
+    def _forward_subbatch(self, x, xbias, residual):
+        """The layer stack on the two batch halves of the micro-batch, phase by phase alternately
+        (see ``ParallelTransformerLayer.forward_phases``): half b's GEMMs / attention run while half
+        a's exchange is in flight and vice versa. The halves meet again (one concat each) before
+        the final norm / the pipeline send. Same math as ``forward`` per half; with dropout, the
+        masks are drawn in the interleaved order."""
+        hb = x.shape[1] // 2
+        halves = []
+        for i in range(2):
+            sl = slice(i * hb, (i + 1) * hb)
+            halves.append({"x": x[:, sl].contiguous(), "xbias": xbias,
+                           "residual": None if residual is None else residual[:, sl].contiguous()})
+        tp.begin_subbatch()
+        try:
+            for layer in self.layers:
+                gens = [layer.forward_phases(h) for h in halves]
+                for _ in range(4):
+                    for gen in gens:
+                        next(gen)
+            for h in halves:
+                tp.rs_finish(h["x"])
+        finally:
+            tp.end_subbatch()
+        x = torch.cat([h["x"] for h in halves], dim=1)
+        xbias = halves[0]["xbias"]
+        residual = torch.cat([h["residual"] for h in halves], dim=1)
+        return x, xbias, residual
+
     def forward(self, x, xbias=None, residual=None):
         """Returns (pending_x, pending_bias, residual) or, with ``final_norm``, the normalised
         output (the pending branch folded into the residual first)."""
-        for i in range(len(self.layers)):
-            x, xbias, residual = self._run(i, x, xbias, residual)
+        if self._subbatch_ok(x):
+            x, xbias, residual = self._forward_subbatch(x, xbias, residual)
+        else:
+            for i in range(len(self.layers)):
+                x, xbias, residual = self._run(i, x, xbias, residual)
         if self.final_norm is not None:
             g = _sp_gather(self.cfg)          # y feeds the LM head's column-parallel all-gather
             y, _ = self.final_norm.fused(x, xbias, residual, self.cfg.hidden_dropout, self.training,

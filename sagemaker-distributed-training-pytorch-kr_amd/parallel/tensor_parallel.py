@@ -308,6 +308,10 @@ class DeferredWgrad:
         # main_grad read-modify-write: the SFT engine's small micro-batches) or issue one grouped
         # launch per segment round (large pipeline micro-batches: no concatenation copy).
         self.concat_segments = True
+        # the sub-batch interleave (models/transformer._forward_subbatch) pushes every weight twice
+        # per pass (once per batch half): merge the second push instead of flushing, the segments
+        # issued as rounds (no concatenation copy)
+        self.merge_repeats = False
         self.stats = {"flushes": 0, "items": 0, "max_segments": 0, "stores": 0}
         self.items = []
         self.by_key = {}
@@ -351,7 +355,7 @@ class DeferredWgrad:
         seg = (g2, t2, g2._version, t2._version)
         nbytes = g2.numel() * g2.element_size() + t2.numel() * t2.element_size()
         it = self.by_key.get(key)
-        if it is not None and (it[3] or self.hold):
+        if it is not None and (it[3] or self.hold or self.merge_repeats):
             # the same main_grad again inside an accumulation window: merge (the sum over the
             # concatenated token range is the same accumulation; one readiness report)
             it[2].append(seg)
@@ -410,7 +414,7 @@ class DeferredWgrad:
                                        "flush; disable with SMDT_DEFER_WGRAD=0 and report the op that did it")
             if len(segs) == 1:
                 work.append((weight, mg, [(segs[0][0], segs[0][1])], complete, bias, fresh))
-            elif self.concat_segments:
+            elif self.concat_segments and _held:
                 work.append((weight, mg, [(torch.cat([sg[0] for sg in segs]), torch.cat([sg[1] for sg in segs]))],
                              complete, bias, fresh))
             else:
@@ -888,6 +892,7 @@ class SPFusedGeLUMLP(torch.autograd.Function):
         y = rs_ring(lambda lo, m, o: _linear_into(act[lo:lo + m], w2, o), group, lead + (w2.shape[0],), act)
         ctx.save_for_backward(total, w1, w2, pre, act)
         ctx.b1 = b1
+        ctx.bulk = _SPLIT["on"]     # a sub-batch half: bulk rings in backward
         return y
 
     @staticmethod
@@ -907,7 +912,7 @@ class SPFusedGeLUMLP(torch.autograd.Function):
             m = ch.shape[0]
             C.gemm_tn(ch.reshape(-1, ch.shape[-1]), w2t, 3, bd, dz[lo:lo + m].view(-1, f), None, 0, 0,
                       pre[lo:lo + m].view(-1, f))
-        gfull = ag_ring(dy, group, fc2_dgrad_chunk, before_last_wait=_flush_wgrad)
+        gfull = ag_ring(dy, group, fc2_dgrad_chunk, before_last_wait=_flush_wgrad, bulk=ctx.bulk)
         dw2 = _wgrad(w2, gfull.reshape(-1, gfull.shape[-1]), act.reshape(-1, f))
         res = {}
 
@@ -916,7 +921,7 @@ class SPFusedGeLUMLP(torch.autograd.Function):
             _flush_wgrad()
         w1t = _dgrad_weight_t(w1)
         dx = rs_ring(lambda lo, m, o: _dgrad_rows(dz[lo:lo + m], w1, w1t, o), group,
-                     dz.shape[:-1] + (w1.shape[1],), dz, wgrad)
+                     dz.shape[:-1] + (w1.shape[1],), dz, wgrad, bulk=ctx.bulk)
         if "dw" not in res:
             wgrad()
         return dx, res["dw"], res["db"], dw2
@@ -1263,13 +1268,112 @@ _SP_GATHER_SLOTS = os.environ.get("SMDT_SP_GATHER_SLOTS", "1") == "1"   # A/B sw
 AG_RING_STATS = {"in_place": 0, "copied": 0}
 
 
-def ag_ring(x, group, chunk_fn=None, before_last_wait=None, _skip_direct=False):
+def _gather_buffer(x, ws, r):
+    """The [n * ws, ...] all-gather buffer of ``x`` with x in slot r: the buffer x's producer wrote
+    it into (the norm's gather slot, no copy) or a new one with x copied in."""
+    n = x.shape[0]
+    mark = getattr(x, "_smdt_gather", None)
+    if (mark is not None and mark[1] == r and mark[0].shape[0] == n * ws and mark[0].shape[1:] == x.shape[1:]
+            and mark[0].is_contiguous() and x.is_contiguous() and x.data_ptr() == mark[0][r * n].data_ptr()):
+        AG_RING_STATS["in_place"] += 1
+        return mark[0]
+    total = x.new_empty((n * ws,) + tuple(x.shape[1:]))
+    total[r * n:(r + 1) * n].copy_(x)
+    AG_RING_STATS["copied"] += 1
+    return total
+
+
+# Sub-batch interleave (``models/transformer.ParallelTransformer``, SMDT_SP_SUBBATCH): the two
+# halves of a micro-batch run each layer phase by phase, alternately, so one half's TP-pair
+# exchange travels beside the other half's GEMMs / attention instead of beside half of its own
+# GEMM only (a 2-rank ring's sole overlap partner in forward: profiles/r5_predict_tp2x/). The
+# issue order of the exchanges stays a pure function of the layer stack on both partners, which
+# the relay's per-call epochs need. Forward only: the backward's exchanges already overlap the
+# drained weight-gradient GEMMs.
+_SPLIT = {"on": False}
+_AG_PENDING = {}      # (data_ptr, shape) of a started all-gather's input -> (total, works, rank, n)
+_RS_PENDING = []      # outputs whose reduce-scatter was started but not yet combined
+SPLIT_STATS = {"ag_started": 0, "rs_deferred": 0}
+
+
+def _pending_key(x):
+    return (x.data_ptr(), tuple(x.shape)) if _AG_PENDING else None
+
+
+def ag_start(x, group):
+    """Issue the 2-rank ring all-gather of ``x`` now; the ``ag_ring`` call of x's consumer then
+    runs its local chunk's GEMM, waits, and runs the peer's chunk."""
+    ws, r, nxt, prv = _ring(group)
+    assert ws == 2, "ag_start: 2-rank rings only"
+    x = x.contiguous()
+    n = x.shape[0]
+    total = _gather_buffer(x, ws, r)
+    peer = 1 - r
+    # the receive goes through ``.data`` (same storage, own version counter): x is usually a view
+    # of ``total`` returned by the fused norm (a multi-output autograd node), and an in-place write
+    # into its base seen by autograd before x's consumer is applied would be refused
+    raw = total.data
+    works = _exchange(raw[r * n:(r + 1) * n], raw[peer * n:(peer + 1) * n], nxt, prv, group)
+    _AG_PENDING[(x.data_ptr(), tuple(x.shape))] = (total, works, r, n)
+    SPLIT_STATS["ag_started"] += 1
+    return x
+
+
+def rs_finish(t):
+    """Complete a reduce-scatter ``rs_ring`` left in flight under the sub-batch interleave: wait for
+    the peer's partial of this rank's chunk and add it into ``t`` (in place, outside autograd: the
+    gradient of the sum is the gradient of t). Returns t; a no-op for any other tensor."""
+    pend = getattr(t, "_smdt_rs_pending", None)
+    if pend is None:
+        return t
+    del t._smdt_rs_pending
+    works, incoming, _keep, group = pend
+    _wait_works(works, group)
+    t.data.add_(incoming)    # outside autograd (t may be a view output of the linear's Function)
+    try:
+        _RS_PENDING.remove(t)
+    except ValueError:
+        pass
+    return t
+
+
+def begin_subbatch():
+    _SPLIT["on"] = True
+    DEFERRED_WGRAD.merge_repeats = True
+
+
+def end_subbatch():
+    """Leave the interleave: any exchange still in flight is completed (a consumer that never came
+    would otherwise leave the relay's epochs of the two partners apart)."""
+    _SPLIT["on"] = False
+    for t in list(_RS_PENDING):
+        rs_finish(t)
+    _RS_PENDING.clear()
+    for total, works, _r, _n in list(_AG_PENDING.values()):
+        for w in works:
+            w.wait()
+    _AG_PENDING.clear()
+
+
+def ag_ring(x, group, chunk_fn=None, before_last_wait=None, _skip_direct=False, bulk=False):
     """All-gather ``x`` along dim 0 over ``group`` as a ring; ``chunk_fn(lo, rows)`` runs on the
     gathered rows [lo, lo + rows.shape[0]) (dim 0) as soon as they are resident, while the next
     chunk is in flight: the ring hands over whole chunks (lo = c * n). Returns the gathered tensor.
     TP groups of 4 / 8 with a direct engine (comm/tp_direct.py) gather over all of the group's
     links at once instead, in row pieces: the local chunk's GEMM beside the first piece, every
     peer's rows of piece j as soon as piece j has landed."""
+    pend = _AG_PENDING.pop(_pending_key(x), None)
+    if pend is not None:
+        # started earlier by ``ag_start`` (sub-batch interleave): the other half's phase ran beside
+        # the transfer, so the consumer waits and runs ONE GEMM over both chunks (16,384 rows at
+        # the BASELINE point instead of two 8,192-row chunk GEMMs)
+        total, works, r, n = pend
+        if before_last_wait is not None:
+            before_last_wait()
+        _wait_works(works, group)
+        if chunk_fn is not None:
+            chunk_fn(0, total)
+        return total
     td = None if _skip_direct else _direct(group)
     if td is not None:
         out = td.all_gather(x, chunk_fn, before_last_wait)
@@ -1278,15 +1382,18 @@ def ag_ring(x, group, chunk_fn=None, before_last_wait=None, _skip_direct=False):
             return out
     ws, r, nxt, prv = _ring(group)
     n = x.shape[0]
-    mark = getattr(x, "_smdt_gather", None)
-    if (mark is not None and mark[1] == r and mark[0].shape[0] == n * ws and mark[0].shape[1:] == x.shape[1:]
-            and mark[0].is_contiguous() and x.is_contiguous() and x.data_ptr() == mark[0][r * n].data_ptr()):
-        total = mark[0]        # x's producer wrote it into its slot of the gather buffer: no copy
-        AG_RING_STATS["in_place"] += 1
-    else:
-        total = x.new_empty((n * ws,) + tuple(x.shape[1:]))
-        total[r * n:(r + 1) * n].copy_(x)
-        AG_RING_STATS["copied"] += 1
+    total = _gather_buffer(x, ws, r)
+    if bulk and ws == 2:
+        # a sub-batch half's backward (``bulk``): the exchange beside the drained weight-gradient
+        # GEMMs, then ONE GEMM over both chunks (half-size chunk GEMMs measured slow)
+        peer = 1 - r
+        works = _exchange(total[r * n:(r + 1) * n], total[peer * n:(peer + 1) * n], nxt, prv, group)
+        if before_last_wait is not None:
+            before_last_wait()
+        _wait_works(works, group)
+        if chunk_fn is not None:
+            chunk_fn(0, total)
+        return total
     for s in range(ws):
         c = (r - s) % ws
         works = None
@@ -1302,7 +1409,7 @@ def ag_ring(x, group, chunk_fn=None, before_last_wait=None, _skip_direct=False):
     return total
 
 
-def rs_ring(partial_fn, group, full_shape, ref, before_last_wait=None):
+def rs_ring(partial_fn, group, full_shape, ref, before_last_wait=None, bulk=False):
     """Reduce-scatter along dim 0 over ``group`` as a ring. The tensor being reduced (``full_shape``,
     ``ref``'s dtype / device) is produced on demand: ``partial_fn(lo, rows, out)`` computes its rows
     [lo, lo + rows) — a GEMM on those rows — into ``out`` when given (and returns it), else into a
@@ -1317,6 +1424,31 @@ def rs_ring(partial_fn, group, full_shape, ref, before_last_wait=None):
         return out
     ws, r, nxt, prv = _ring(group)
     n = full_shape[0] // ws
+    if _SPLIT["on"] and ws == 2 and before_last_wait is None:
+        # sub-batch interleave: the peer's partial, its exchange, this rank's partial; the combine
+        # is left to ``rs_finish`` so the other half's work runs while the partial travels
+        # (one GEMM over both chunks, then the peer's half goes out; ``own`` is a view of it)
+        peer = 1 - r
+        full = partial_fn(0, 2 * n, None)
+        part = full[peer * n:(peer + 1) * n]
+        incoming = torch.empty_like(part)
+        works = _exchange(part, incoming, nxt, prv, group)
+        own = full[r * n:(r + 1) * n]
+        own._smdt_rs_pending = (works, incoming, full, group)
+        _RS_PENDING.append(own)
+        SPLIT_STATS["rs_deferred"] += 1
+        return own
+    if bulk and ws == 2:
+        # a sub-batch half's backward: one GEMM over both chunks, the peer's half out beside the
+        # drained weight-gradient GEMMs, then the combine
+        peer = 1 - r
+        full = partial_fn(0, 2 * n, None)
+        incoming = torch.empty_like(full[:n])
+        works = _exchange(full[peer * n:(peer + 1) * n], incoming, nxt, prv, group)
+        if before_last_wait is not None:
+            before_last_wait()
+        _wait_works(works, group)
+        return full[r * n:(r + 1) * n].add_(incoming)
     works, incoming, keep = None, None, []
     for s in range(ws):
         c = (r - s - 1) % ws
@@ -1369,6 +1501,7 @@ class _ColumnSPLinear(torch.autograd.Function):
         ctx.save_for_backward(total, weight)
         ctx.bias_p = bias
         ctx.n = n
+        ctx.bulk = _SPLIT["on"]
         return out
 
     @staticmethod
@@ -1385,7 +1518,7 @@ class _ColumnSPLinear(torch.autograd.Function):
             _flush_wgrad()
         wt = _dgrad_weight_t(weight)
         gi = rs_ring(lambda lo, m, o: _dgrad_rows(g[lo:lo + m], weight, wt, o), group,
-                     g.shape[:-1] + (weight.shape[1],), g, wgrad)
+                     g.shape[:-1] + (weight.shape[1],), g, wgrad, bulk=ctx.bulk)
         if "dw" not in res:   # world 1 ring: no wait happened
             wgrad()
         return gi, res["dw"], res["db"], None
@@ -1407,6 +1540,7 @@ class _RowSPLinear(torch.autograd.Function):
                     x.shape[:-1] + (weight.shape[0],), x)
         ctx.save_for_backward(x, weight)
         ctx.n = n
+        ctx.bulk = _SPLIT["on"]
         return y
 
     @staticmethod
@@ -1418,7 +1552,7 @@ class _RowSPLinear(torch.autograd.Function):
         gi = x.new_empty(x.shape)
         wt = _dgrad_weight_t(weight)
         gfull = ag_ring(g, group, lambda lo, ch: dgrad_into(gi[lo:lo + ch.shape[0]], ch, weight, wt),
-                        before_last_wait=_flush_wgrad)
+                        before_last_wait=_flush_wgrad, bulk=ctx.bulk)
         dw = _wgrad(weight, gfull.reshape(-1, gfull.shape[-1]), x.reshape(-1, x.shape[-1]))
         return gi, dw
 

@@ -91,9 +91,10 @@ def _cpu_tp_direct(group, pieces):
     return _CpuTpDirect(_GlooPieceEngine(group), group)
 
 
-def gpt_tp_worker(rank, world, tp, pp, sp, cfg_over=None, p2p=None, direct_pieces=0):
+def gpt_tp_worker(rank, world, tp, pp, sp, cfg_over=None, p2p=None, direct_pieces=0, subbatch=0):
     """``direct_pieces`` > 0: the TP exchanges run through ``TpDirect`` in that many row pieces
-    (over the CPU stand-in engine) instead of the ring."""
+    (over the CPU stand-in engine) instead of the ring. ``subbatch`` = 2: the layer stack runs the
+    two batch halves interleaved phase by phase (SMDT_SP_SUBBATCH)."""
     import torch.distributed as dist
     from smdt_amd.comm import init_distributed
     from smdt_amd.models.gpt import GPTModel, allreduce_word_embedding_grads
@@ -102,6 +103,9 @@ def gpt_tp_worker(rank, world, tp, pp, sp, cfg_over=None, p2p=None, direct_piece
     from smdt_amd.train.schedules import get_forward_backward_func
     init_distributed("gloo")
     st = ps.initialize_model_parallel(tp, pp)
+    if subbatch:
+        import smdt_amd.models.transformer as T
+        T._SUBBATCH = subbatch
     if direct_pieces:
         st.tp_direct = _cpu_tp_direct(st.tp_group, direct_pieces)
     from smdt_amd.train import schedules
@@ -142,6 +146,8 @@ def gpt_tp_worker(rank, world, tp, pp, sp, cfg_over=None, p2p=None, direct_piece
             "layer_offset": m.first_layer,
             "direct_calls": st.tp_direct.calls if direct_pieces else 0,
             "direct_pieces": st.tp_direct.pieces_issued if direct_pieces else 0}
+    from smdt_amd.parallel import tensor_parallel as TPm
+    meta["split"] = dict(TPm.SPLIT_STATS)
     dist.destroy_process_group()
     return out_loss, grads, meta
 

@@ -64,6 +64,22 @@ def test_direct_tp_exchange_pieces_match_single_rank(tp, pieces):
         assert meta["direct_calls"] > 0 and meta["direct_pieces"] == pieces * meta["direct_calls"]
 
 
+@pytest.mark.parametrize("pp", [1, 2])
+def test_subbatch_interleave_matches_single_rank(pp):
+    """tp2 + SP with the two batch halves of every micro-batch interleaved phase by phase
+    (SMDT_SP_SUBBATCH=2: one half's all-gather / reduce-scatter in flight while the other half's
+    layer phase runs, ``tp.ag_start`` / ``rs_finish``): loss and every gradient equal the
+    single-rank model's, and the interleave really ran (4 started exchanges per layer, half and
+    micro-batch)."""
+    ref_loss, ref = W.gpt_reference()
+    outs = run_workers(W.gpt_tp_worker, 2 * pp, 2, pp, True, None, None, 0, 2)
+    for loss, grads, meta in outs:
+        _check_tp_grads(ref, grads, meta, 2)
+        assert meta["split"]["ag_started"] > 0 and meta["split"]["ag_started"] == meta["split"]["rs_deferred"]
+    last = [o for o in outs if o[2]["pp_rank"] == pp - 1][0]
+    torch.testing.assert_close(last[0].view(-1), ref_loss.view(-1), atol=2e-4, rtol=2e-4)
+
+
 @pytest.mark.parametrize("over", [None, {"num_layers": 3, "decoder_last_pipeline_num_layers": 1}])
 def test_pipeline_parallel_matches_single_rank(over):
     """pp = 2, uniform split and the uneven split bench.py uses to balance the LM head (first stage
