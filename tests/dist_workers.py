@@ -1369,3 +1369,51 @@ def deterministic_fold_worker(rank, world, zero):
     out = (ddp.grad_data.clone(), ranges)
     dist.destroy_process_group()
     return out
+
+
+def ag_start_view_worker(rank, world, emulate=False):
+    """``tp.ag_start`` on the first output of a multi-output autograd node that is a VIEW of the
+    all-gather buffer (what the fused sequence-parallel norm returns on the GPU), then the column
+    SP linear over it and its backward: the receive into the buffer must stay invisible to
+    autograd (it goes through ``.data``). Returns (out, dx) for comparison with the plain ring."""
+    import torch.distributed as dist
+    from smdt_amd.comm import init_distributed
+    from smdt_amd.parallel import state as ps
+    from smdt_amd.parallel import tensor_parallel as TPm
+    init_distributed("gloo")
+    if emulate:   # one process as TP rank 0 of 2: the exchange is an in-place local copy
+        st = ps.initialize_emulated_tensor_parallel(2, 1)
+    else:
+        st = ps.initialize_model_parallel(2, 1)
+    rank = st.tp_rank
+    torch.manual_seed(0)
+    n, b, h, o = 4, 2, 8, 6
+    full_x = torch.randn(2 * n, b, h)
+    w = torch.randn(o, h, requires_grad=True)
+
+    class _Producer(torch.autograd.Function):
+        """Writes 2x its input into its slot of a fresh gather buffer; returns (view, other)."""
+        @staticmethod
+        def forward(ctx, x):
+            buf = x.new_empty((2 * n, b, h))
+            buf[rank * n:(rank + 1) * n].copy_(2 * x)
+            y = buf[rank * n:(rank + 1) * n]
+            y._smdt_gather = (buf, rank)
+            return y, x * 3
+
+        @staticmethod
+        def backward(ctx, gy, gs):
+            return 2 * gy + 3 * gs
+
+    res = {}
+    for mode in ("ring", "started"):
+        x = full_x[rank * n:(rank + 1) * n].clone().requires_grad_(True)
+        y, s = _Producer.apply(x)
+        if mode == "started":
+            TPm.ag_start(y, st.tp_group)
+        out = TPm._ColumnSPLinear.apply(y, w, None)
+        (out.sum() + s.sum()).backward()
+        res[mode] = (out.detach().clone(), x.grad.detach().clone())
+        w.grad = None
+    dist.destroy_process_group()
+    return res

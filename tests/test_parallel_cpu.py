@@ -80,6 +80,18 @@ def test_subbatch_interleave_matches_single_rank(pp):
     torch.testing.assert_close(last[0].view(-1), ref_loss.view(-1), atol=2e-4, rtol=2e-4)
 
 
+def test_ag_start_on_a_gather_slot_view():
+    """The sub-batch interleave's early all-gather on a norm-style output that is a view of the
+    gather buffer (multi-output autograd node, as the fused norm returns on the GPU): forward and
+    input gradient equal the plain ring's, and autograd does not refuse the buffer write (the
+    loopback rank's exchange is an in-place copy into the buffer: refused without the ``.data``
+    alias, checked by mutation)."""
+    for world, emulate in ((2, False), (1, True)):     # Gloo pair; loopback (in-place copy) rank
+        for res in run_workers(W.ag_start_view_worker, world, emulate):
+            for a, b in zip(res["ring"], res["started"]):
+                torch.testing.assert_close(a, b)
+
+
 @pytest.mark.parametrize("over", [None, {"num_layers": 3, "decoder_last_pipeline_num_layers": 1}])
 def test_pipeline_parallel_matches_single_rank(over):
     """pp = 2, uniform split and the uneven split bench.py uses to balance the LM head (first stage
