@@ -141,6 +141,26 @@ def test_captured_emulated_tp2_gpt_step_equals_eager(sp):
     torch.testing.assert_close(gg, ge, rtol=1e-4, atol=1e-6)
 
 
+def test_subbatch_interleave_emulated_tp2_step_matches_default(monkeypatch):
+    """The sub-batch interleave (SMDT_SP_SUBBATCH=2) on the GPU kernel path of one emulated tp2 +
+    SP rank: the fused norms return views of the all-gather buffers that ``tp.ag_start`` fills
+    early, the halves' reduce-scatters complete in ``tp.rs_finish``. Same losses and fp32
+    main_grad as the default layer loop up to bf16 GEMM-shape rounding (one GEMM over both
+    chunks instead of two)."""
+    import smdt_amd.models.transformer as T
+    from smdt_amd.parallel import tensor_parallel as TPm
+    le, ge = _gpt_emulated_tp_run(False, sp=True)
+    monkeypatch.setattr(T, "_SUBBATCH", 2)
+    before = dict(TPm.SPLIT_STATS)
+    try:
+        ls, gs = _gpt_emulated_tp_run(False, sp=True)
+    finally:
+        TPm.DEFERRED_WGRAD.merge_repeats = False
+    assert TPm.SPLIT_STATS["ag_started"] > before["ag_started"]
+    torch.testing.assert_close(ls, le, rtol=2e-2, atol=2e-2)
+    assert (gs - ge).abs().max() <= 3e-2 * ge.abs().max()
+
+
 def test_bench_graph_mode_captures(tmp_path):
     """bench.py --graph 1 on an emulated tp2 last-stage rank reports a captured HIP graph."""
     import json
