@@ -56,7 +56,7 @@ static Tensor out_or_new(const OptT& out, const Tensor& like, const char* n) {
 
 std::vector<Tensor> layernorm_fwd(Tensor x, OptT res, OptT bias, Tensor gamma, OptT beta,
                                   double eps, double p_drop, int64_t seed, int64_t offset,
-                                  bool rms, bool want_s, OptT out_y) {
+                                  bool rms, bool want_s, OptT out_y, OptT x2) {
   need_contig(x, "x");
   need_contig(gamma, "gamma");
   const int64_t H = x.size(-1);
@@ -65,9 +65,10 @@ std::vector<Tensor> layernorm_fwd(Tensor x, OptT res, OptT bias, Tensor gamma, O
   if (res) { need_contig(*res, "residual"); TORCH_CHECK(res->sizes() == x.sizes() && res->dtype() == x.dtype(), "layernorm: residual mismatch"); }
   if (bias) { need_contig(*bias, "bias"); TORCH_CHECK(bias->numel() == H && bias->dtype() == gamma.dtype(), "layernorm: bias mismatch"); }
   if (beta) { need_contig(*beta, "beta"); TORCH_CHECK(beta->numel() == H && beta->dtype() == gamma.dtype(), "layernorm: beta mismatch"); }
+  if (x2) { need_contig(*x2, "x2"); TORCH_CHECK(x2->sizes() == x.sizes() && x2->dtype() == x.dtype(), "layernorm: x2 mismatch"); }
   auto y = out_or_new(out_y, x, "layernorm_fwd");
   Tensor s;
-  const bool make_s = want_s || res.has_value() || bias.has_value() || p_drop > 0.0;
+  const bool make_s = want_s || res.has_value() || bias.has_value() || p_drop > 0.0 || x2.has_value();
   if (make_s) s = torch::empty_like(x);
   auto f32 = x.options().dtype(at::kFloat);
   auto mean = torch::empty({rows}, f32);
@@ -76,7 +77,7 @@ std::vector<Tensor> layernorm_fwd(Tensor x, OptT res, OptT bias, Tensor gamma, O
                            gamma.data_ptr(), optr(beta), y.data_ptr(),
                            make_s ? s.data_ptr() : nullptr, mean.data_ptr<float>(),
                            rstd.data_ptr<float>(), rows, (int)H, (float)eps, (float)p_drop,
-                           (uint64_t)seed, (uint64_t)offset, rms ? 1 : 0, cur_stream()),
+                           (uint64_t)seed, (uint64_t)offset, rms ? 1 : 0, optr(x2), cur_stream()),
         "layernorm_fwd");
   return {y, make_s ? s : x, mean, rstd};
 }
@@ -841,7 +842,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   using pybind11::arg;
   m.def("layernorm_fwd", &layernorm_fwd, arg("x"), arg("res"), arg("bias"), arg("gamma"), arg("beta"),
         arg("eps"), arg("p_drop"), arg("seed"), arg("offset"), arg("rms"), arg("want_s"),
-        arg("out_y") = pybind11::none());
+        arg("out_y") = pybind11::none(), arg("x2") = pybind11::none());
   m.def("layernorm_bwd", &layernorm_bwd, arg("dy"), arg("ds_in"), arg("s"), arg("gamma"), arg("mean"),
         arg("rstd"), arg("p_drop"), arg("seed"), arg("offset"), arg("rms"), arg("want_dx"), arg("want_dbias"),
         arg("dgamma_acc") = pybind11::none(), arg("dbeta_acc") = pybind11::none(),

@@ -15,7 +15,7 @@ hipError_t smdt_layernorm_fwd(int dtype, int wdtype, const void* x, const void* 
                               const void* bias, const void* gamma, const void* beta, void* y,
                               void* s_out, float* mean, float* rstd, int64_t rows, int H,
                               float eps, float p_drop, uint64_t seed, uint64_t offset, int rms,
-                              hipStream_t st);
+                              const void* x2, hipStream_t st);
 hipError_t smdt_layernorm_bwd(int dtype, int wdtype, const void* dy, const void* ds_in,
                               const void* s, const void* gamma, const float* mean,
                               const float* rstd, void* ds_out, void* dx_out, float* partials,

@@ -37,6 +37,9 @@ struct LnFwdArgs {
   uint64_t seed, offset;
   int rms;
   const uint32_t* step;  // graph-safe RNG step counter (smdt_set_rng_step), may be null
+  const void* x2;        // [rows, H] optional second summand of x (a reduce-scatter's incoming
+                         // partial: x + x2 is the row-parallel output, added here instead of in
+                         // a separate pass)
 };
 
 struct LnBwdArgs {
@@ -141,6 +144,11 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(LnFwdArgs a) {
       int ch = c * G + tid_in_group;
       if (ch < nchunk) {
         load_vec<T, 8, true>(xr + ch * 8, v[c]);  // streamed once: nontemporal
+        if (a.x2 != nullptr) {
+          float u[8];
+          load_vec<T, 8, true>((const T*)a.x2 + row * H + ch * 8, u);
+          for (int j = 0; j < 8; ++j) v[c][j] += u[j];
+        }
         if (has_bias)
           for (int j = 0; j < 8; ++j) v[c][j] += bi[c][j];
         if (drop) {
@@ -445,10 +453,10 @@ extern "C" hipError_t smdt_layernorm_fwd(int dtype, int wdtype, const void* x, c
                                          void* y, void* s_out, float* mean, float* rstd,
                                          int64_t rows, int H, float eps, float p_drop,
                                          uint64_t seed, uint64_t offset, int rms,
-                                         hipStream_t st) {
+                                         const void* x2, hipStream_t st) {
   if (H % 8 != 0 || H > 16384) return hipErrorInvalidValue;
   LnFwdArgs a{x, res, bias, gamma, beta, y, s_out, mean, rstd, rows, H, eps, p_drop, seed, offset, rms,
-              smdt_rng_step()};
+              smdt_rng_step(), x2};
   if (dtype == 1 && wdtype == 1) return ln_fwd_typed<bf16, bf16>(a, st);
   if (dtype == 1 && wdtype == 0) return ln_fwd_typed<bf16, float>(a, st);
   if (dtype == 2 && wdtype == 2) return ln_fwd_typed<f16, f16>(a, st);

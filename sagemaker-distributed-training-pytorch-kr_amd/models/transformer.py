@@ -669,6 +669,12 @@ class ParallelTransformer(nn.Module):
         output (the pending branch folded into the residual first)."""
         if self._subbatch_ok(x):
             x, xbias, residual = self._forward_subbatch(x, xbias, residual)
+        elif self.cfg.recompute_granularity != "full":
+            # every row-parallel output of the stack is consumed by the next fused norm (the
+            # layers' own, or the final one): the ring reduce-scatters leave their combine to it
+            with tp.defer_rs_add():
+                for i in range(len(self.layers)):
+                    x, xbias, residual = self._run(i, x, xbias, residual)
         else:
             for i in range(len(self.layers)):
                 x, xbias, residual = self._run(i, x, xbias, residual)
@@ -677,4 +683,4 @@ class ParallelTransformer(nn.Module):
             y, _ = self.final_norm.fused(x, xbias, residual, self.cfg.hidden_dropout, self.training,
                                          gather=None if g is None else g + (True, residual is not None))
             return y
-        return x, xbias, residual
+        return tp.materialize_add(x), xbias, residual      # leaves the stage: no pending summand

@@ -104,18 +104,21 @@ def _mark_gather(t, buf, rank):
 
 class _BDALayerNorm(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, bias, residual, gamma, beta, p, eps, rms, seed, offset, gather=None):
+    def forward(ctx, x, bias, residual, gamma, beta, p, eps, rms, seed, offset, gather=None, x2=None):
         """``gather`` = (world, rank, y_into_gather, dx_into_gather) under sequence parallelism:
         the normalised output (consumed by a column-parallel ring all-gather) and / or the input
         gradient (consumed by a row-parallel linear's backward all-gather) are written into their
-        rank's slot of a gather buffer."""
+        rank's slot of a gather buffer. ``x2`` (no gradient): a second summand of x, added in the
+        kernel (a reduce-scatter's incoming partial, see ``tensor_parallel.rs_ring``); x's
+        gradient is also x + x2's."""
         C = _ext.ext()
         x = x.contiguous()
         buf = out_y = None
         if gather is not None and gather[2]:
             buf, out_y = gather_slot(x, gather[0], gather[1])
         y, s, mean, rstd = C.layernorm_fwd(x, None if residual is None else residual.contiguous(),
-                                           bias, gamma, beta, eps, p, seed, offset, rms, True, out_y)
+                                           bias, gamma, beta, eps, p, seed, offset, rms, True, out_y,
+                                           None if x2 is None else x2.contiguous())
         if buf is not None:
             _mark_gather(y, buf, gather[1])
         ctx.save_for_backward(s, gamma, mean, rstd)
@@ -149,7 +152,7 @@ class _BDALayerNorm(torch.autograd.Function):
         g_gamma = None if ta is not None else dgamma.to(gdt)
         g_beta = None if (not has_beta or tb is not None) else dbeta.to(gdt)
         g_bias = None if (not has_bias or tc is not None) else dbias.to(bdt)
-        return (dx, g_bias, d_s if has_res else None, g_gamma, g_beta, None, None, None, None, None, None)
+        return (dx, g_bias, d_s if has_res else None, g_gamma, g_beta, None, None, None, None, None, None, None)
 
 
 def bias_dropout_add_norm(x, bias, residual, gamma, beta, p: float, training: bool, eps: float = 1e-5,
@@ -161,10 +164,17 @@ def bias_dropout_add_norm(x, bias, residual, gamma, beta, p: float, training: bo
     ``gather`` (world, rank, y, dx): see ``_BDALayerNorm.forward`` (kernel path only).
     """
     p = float(p) if training else 0.0
+    # a row-parallel output whose reduce-scatter left its peer's partial as a pending summand
+    # (tensor_parallel.rs_ring under defer_rs_add): x + x2 is the value, added in the kernel
+    x2 = getattr(x, "_smdt_add", None)
+    if x2 is not None:
+        del x._smdt_add
     if _ext.use_kernels(x):
         seed, offset = _rng(rng).next() if p > 0 else (0, 0)
         return _BDALayerNorm.apply(x, bias, residual, gamma, None if rms else beta, p, float(eps), bool(rms),
-                                   int(seed), int(offset), gather)
+                                   int(seed), int(offset), gather, x2)
+    if x2 is not None:
+        x = x + x2
     h = x if bias is None else x + bias
     if p > 0:
         h = F.dropout(h, p=p, training=True)

@@ -1291,9 +1291,36 @@ def _gather_buffer(x, ws, r):
 # the relay's per-call epochs need. Forward only: the backward's exchanges already overlap the
 # drained weight-gradient GEMMs.
 _SPLIT = {"on": False}
+# Forward reduce-scatters whose consumer is a fused norm (``defer_rs_add``, set by the layer
+# stack): the 2-rank ring's combine (own partial + the peer's) is left to the norm kernel, which
+# reads both summands (ops/functional.bias_dropout_add_norm, x2) instead of a separate add pass.
+_DEFER_ADD = {"on": False}
+_DEFER_RS_ADD = os.environ.get("SMDT_DEFER_RS_ADD", "1") == "1"
+
+
+class defer_rs_add:
+    """Context: forward ring reduce-scatters leave their combine to the consuming fused norm."""
+
+    def __enter__(self):
+        self.prev = _DEFER_ADD["on"]
+        _DEFER_ADD["on"] = _DEFER_RS_ADD
+        return self
+
+    def __exit__(self, *exc):
+        _DEFER_ADD["on"] = self.prev
+        return False
+
+
+def materialize_add(t):
+    """Apply a pending reduce-scatter summand (``defer_rs_add``) in place; returns t."""
+    x2 = getattr(t, "_smdt_add", None)
+    if x2 is not None:
+        del t._smdt_add
+        t.data.add_(x2)
+    return t
 _AG_PENDING = {}      # (data_ptr, shape) of a started all-gather's input -> (total, works, rank, n)
 _RS_PENDING = []      # outputs whose reduce-scatter was started but not yet combined
-SPLIT_STATS = {"ag_started": 0, "rs_deferred": 0}
+SPLIT_STATS = {"ag_started": 0, "rs_deferred": 0, "rs_add_to_norm": 0}
 
 
 def _pending_key(x):
@@ -1457,6 +1484,10 @@ def rs_ring(partial_fn, group, full_shape, ref, before_last_wait=None, bulk=Fals
             if s == ws - 1 and before_last_wait is not None:
                 before_last_wait()
             _wait_works(works, group)
+            if s == ws - 1 and ws == 2 and _DEFER_ADD["on"] and before_last_wait is None:
+                part._smdt_add = incoming      # the consuming norm adds it (see _DEFER_ADD)
+                SPLIT_STATS["rs_add_to_norm"] += 1
+                return part
             part = part.add_(incoming)
         if s == ws - 1:
             return part

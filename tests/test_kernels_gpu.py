@@ -81,6 +81,39 @@ def test_fused_bias_residual_layernorm():
         torch.testing.assert_close(a.grad.float(), r.grad, atol=0.5, rtol=5e-2)
 
 
+def test_fused_norm_with_pending_summand():
+    """A row-parallel output whose reduce-scatter combine was left to the norm (``x._smdt_add`` =
+    the peer's partial, tensor_parallel.defer_rs_add): the kernel reads both summands, s = res +
+    (x + x2 + bias), and x's gradient is that of x + x2. fp32 reference of the same op."""
+    torch.manual_seed(3)
+    rows, H = 512, 1024
+    dt = torch.bfloat16
+    x = torch.randn(rows, H, device=DEV, dtype=dt, requires_grad=True)
+    x2 = torch.randn(rows, H, device=DEV, dtype=dt)
+    res = torch.randn(rows, H, device=DEV, dtype=dt, requires_grad=True)
+    bias = (0.1 * torch.randn(H, device=DEV, dtype=dt)).requires_grad_()
+    g = (1 + 0.1 * torch.randn(H, device=DEV, dtype=dt)).requires_grad_()
+    be = (0.1 * torch.randn(H, device=DEV, dtype=dt)).requires_grad_()
+    x._smdt_add = x2
+    y, s = SF.bias_dropout_add_norm(x, bias, res, g, be, 0.0, True, 1e-5, False)
+    assert not hasattr(x, "_smdt_add")          # consumed
+    leaves = [x, res, bias, g, be]
+    ref = [t.detach().float().requires_grad_() for t in leaves]
+    sr = ref[1] + (ref[0] + x2.float() + ref[2])
+    yr = F.layer_norm(sr, (H,), ref[3], ref[4], 1e-5)
+    torch.testing.assert_close(s.float(), sr, atol=3e-2, rtol=2e-2)
+    torch.testing.assert_close(y.float(), yr, atol=5e-2, rtol=3e-2)
+    dy, ds = torch.randn_like(y), torch.randn_like(s)
+    torch.autograd.backward([y, s], [dy, ds])
+    torch.autograd.backward([yr, sr], [dy.float(), ds.float()])
+    for a, r in zip(leaves, ref):
+        torch.testing.assert_close(a.grad.float(), r.grad, atol=0.5, rtol=5e-2)
+    # without the summand the output differs by far more than the tolerance (the test can fail)
+    y0, _ = SF.bias_dropout_add_norm(x.detach(), bias.detach(), res.detach(), g.detach(), be.detach(),
+                                     0.0, True, 1e-5, False)
+    assert (y0.float() - yr).abs().max() > 0.5
+
+
 def test_fused_dropout_mask_consistency():
     torch.manual_seed(2)
     rows, H, p = 256, 1024, 0.25

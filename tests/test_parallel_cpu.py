@@ -41,12 +41,15 @@ def _check_tp_grads(ref, grads, meta, tp):
 
 @pytest.mark.parametrize("tp,sp", [(2, False), (2, True), (4, True), (4, False)])
 def test_tensor_parallel_matches_single_rank(tp, sp):
-    """tp 4 + SP exercises the multi-step collective-matmul rings (send next / recv prev)."""
+    """tp 4 + SP exercises the multi-step collective-matmul rings (send next / recv prev); tp 2 + SP
+    the forward reduce-scatters whose combine the consuming fused norm does (x2 summand)."""
     ref_loss, ref = W.gpt_reference()
     outs = run_workers(W.gpt_tp_worker, tp, tp, 1, sp)
     for loss, grads, meta in outs:
         _close(loss, ref_loss)
         _check_tp_grads(ref, grads, meta, tp)
+        # tp2 + SP: the forward reduce-scatters left their combine to the consuming norms
+        assert (meta["split"]["rs_add_to_norm"] > 0) == (sp and tp == 2)
 
 
 @pytest.mark.parametrize("tp,pieces", [(4, 1), (4, 2), (2, 4)])
