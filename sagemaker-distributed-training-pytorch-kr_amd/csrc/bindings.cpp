@@ -94,7 +94,7 @@ static Tensor acc_target(const OptT& t, int64_t H, const char* n) {
 std::vector<Tensor> layernorm_bwd(Tensor dy, OptT ds_in, Tensor s, Tensor gamma, Tensor mean,
                                   Tensor rstd, double p_drop, int64_t seed, int64_t offset,
                                   bool rms, bool want_dx, bool want_dbias, OptT dgamma_acc,
-                                  OptT dbeta_acc, OptT dbias_acc, OptT out_dx) {
+                                  OptT dbeta_acc, OptT dbias_acc, OptT out_dx, OptT dy2) {
   need_contig(dy, "dy");
   need_contig(s, "s");
   need_contig(gamma, "gamma");
@@ -102,6 +102,7 @@ std::vector<Tensor> layernorm_bwd(Tensor dy, OptT ds_in, Tensor s, Tensor gamma,
   const int64_t rows = s.numel() / H;
   TORCH_CHECK(dy.sizes() == s.sizes() && dy.dtype() == s.dtype(), "layernorm_bwd: dy mismatch");
   if (ds_in) { need_contig(*ds_in, "ds_in"); TORCH_CHECK(ds_in->sizes() == s.sizes() && ds_in->dtype() == s.dtype(), "layernorm_bwd: ds_in mismatch"); }
+  if (dy2) { need_contig(*dy2, "dy2"); TORCH_CHECK(dy2->sizes() == s.sizes() && dy2->dtype() == s.dtype(), "layernorm_bwd: dy2 mismatch"); }
   // out_dx (optional): where dx goes (a slice of an all-gather buffer, see layernorm_fwd); without
   // dropout dx IS ds, so ds lands there too
   const bool sep = want_dx && p_drop > 0.0;
@@ -123,7 +124,7 @@ std::vector<Tensor> layernorm_bwd(Tensor dy, OptT ds_in, Tensor s, Tensor gamma,
                            rms ? nullptr : dbeta.data_ptr<float>(),
                            want_dbias ? dbias.data_ptr<float>() : nullptr, rows, (int)H,
                            (float)p_drop, (uint64_t)seed, (uint64_t)offset, rms ? 1 : 0, acc_mask,
-                           cur_stream()),
+                           optr(dy2), cur_stream()),
         "layernorm_bwd");
   return {ds, dx, dgamma, rms ? dgamma.new_empty({0}) : dbeta,
           want_dbias ? dbias : dgamma.new_empty({0})};
@@ -846,7 +847,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("layernorm_bwd", &layernorm_bwd, arg("dy"), arg("ds_in"), arg("s"), arg("gamma"), arg("mean"),
         arg("rstd"), arg("p_drop"), arg("seed"), arg("offset"), arg("rms"), arg("want_dx"), arg("want_dbias"),
         arg("dgamma_acc") = pybind11::none(), arg("dbeta_acc") = pybind11::none(),
-        arg("dbias_acc") = pybind11::none(), arg("out_dx") = pybind11::none());
+        arg("dbias_acc") = pybind11::none(), arg("out_dx") = pybind11::none(), arg("dy2") = pybind11::none());
   m.def("bias_act_fwd", &bias_act_fwd);
   m.def("bias_act_bwd", &bias_act_bwd, arg("dy"), arg("x"), arg("bias"), arg("act"), arg("want_dbias"),
         arg("dbias_acc") = pybind11::none());

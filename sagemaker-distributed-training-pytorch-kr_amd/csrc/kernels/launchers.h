@@ -21,7 +21,7 @@ hipError_t smdt_layernorm_bwd(int dtype, int wdtype, const void* dy, const void*
                               const float* rstd, void* ds_out, void* dx_out, float* partials,
                               int nblocks, float* dgamma, float* dbeta, float* dbias,
                               int64_t rows, int H, float p_drop, uint64_t seed, uint64_t offset,
-                              int rms, int acc_mask, hipStream_t st);
+                              int rms, int acc_mask, const void* dy2, hipStream_t st);
 
 // bias_act.hip
 int smdt_bias_act_slices(int64_t rows, int N);

@@ -60,6 +60,8 @@ struct LnBwdArgs {
   int want_dbias;
   int nblocks;
   const uint32_t* step;
+  const void* dy2;    // [rows, H] optional second summand of dy (a backward reduce-scatter's
+                      // incoming partial, added here instead of in a separate pass)
 };
 
 template <int G>
@@ -243,10 +245,12 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(LnBwdArgs a) {
   const T* __restrict__ sp = (const T*)a.s;
   const T* __restrict__ dyp = (const T*)a.dy;
   const T* __restrict__ dip = (const T*)a.ds_in;
+  const T* __restrict__ dy2p = (const T*)a.dy2;
+  const bool has_dy2 = dy2p != nullptr;
   const int64_t rstep = (int64_t)gridDim.x * groups_per_block;
-  Raw8<T> ns[C], ndy[C], ndi[C];
+  Raw8<T> ns[C], ndy[C], ndi[C], ndy2[C];
 #pragma unroll
-  for (int c = 0; c < C; ++c) ns[c] = ndy[c] = ndi[c] = Raw8<T>{};
+  for (int c = 0; c < C; ++c) ns[c] = ndy[c] = ndi[c] = ndy2[c] = Raw8<T>{};
   float nmu = 0.f, nrs = 0.f;
   auto fetch = [&](int64_t r) {
 #pragma unroll
@@ -256,6 +260,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(LnBwdArgs a) {
         ns[c] = load_raw8_nt(sp + r * H + ch * 8);  // streamed once: nontemporal
         ndy[c] = load_raw8_nt(dyp + r * H + ch * 8);
         if (has_dsin) ndi[c] = load_raw8_nt(dip + r * H + ch * 8);
+        if (has_dy2) ndy2[c] = load_raw8_nt(dy2p + r * H + ch * 8);
       }
     }
     nmu = a.rms ? 0.f : a.mean[r];
@@ -264,12 +269,13 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(LnBwdArgs a) {
   int64_t row = (int64_t)blockIdx.x * groups_per_block + group;
   if (row < a.rows) fetch(row);
   for (; row < a.rows; row += rstep) {
-    Raw8<T> cs[C], cdy[C], cdi[C];
+    Raw8<T> cs[C], cdy[C], cdi[C], cdy2[C];
 #pragma unroll
     for (int c = 0; c < C; ++c) {
       cs[c] = ns[c];
       cdy[c] = ndy[c];
       cdi[c] = ndi[c];
+      cdy2[c] = ndy2[c];
     }
     const float mu = nmu;
     const float rs = nrs;
@@ -283,6 +289,12 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(LnBwdArgs a) {
         float dy[8];
         cvt_raw8<T>(cs[c], xh[c]);
         cvt_raw8<T>(cdy[c], dy);
+        if (has_dy2) {
+          float d2[8];
+          cvt_raw8<T>(cdy2[c], d2);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) dy[j] += d2[j];
+        }
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           xh[c][j] = (xh[c][j] - mu) * rs;
@@ -471,10 +483,10 @@ extern "C" hipError_t smdt_layernorm_bwd(int dtype, int wdtype, const void* dy, 
                                          float* partials, int nblocks, float* dgamma,
                                          float* dbeta, float* dbias, int64_t rows, int H,
                                          float p_drop, uint64_t seed, uint64_t offset, int rms,
-                                         int acc_mask, hipStream_t st) {
+                                         int acc_mask, const void* dy2, hipStream_t st) {
   if (H % 8 != 0 || H > 16384) return hipErrorInvalidValue;
   LnBwdArgs a{dy, ds_in, s, gamma, mean, rstd, ds_out, dx_out, partials, rows, H, p_drop, seed,
-              offset, rms, dbias != nullptr, nblocks, smdt_rng_step()};
+              offset, rms, dbias != nullptr, nblocks, smdt_rng_step(), dy2};
   hipError_t e;
   if (dtype == 1 && wdtype == 1) e = ln_bwd_typed<bf16, bf16>(a, st);
   else if (dtype == 1 && wdtype == 0) e = ln_bwd_typed<bf16, float>(a, st);

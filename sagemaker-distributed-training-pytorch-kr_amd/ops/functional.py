@@ -133,6 +133,11 @@ class _BDALayerNorm(torch.autograd.Function):
         s, gamma, mean, rstd = ctx.saved_tensors
         p, seed, offset, rms, has_bias, has_res, has_beta, gdt, bdt = ctx.cfg
         C = _ext.ext()
+        # the consuming column-parallel linear's backward reduce-scatter may leave its peer's
+        # partial as a pending summand of dy (tensor_parallel.rs_ring, defer_add): added in-kernel
+        dy2 = getattr(dy, "_smdt_add", None)
+        if dy2 is not None:
+            del dy._smdt_add
         dy = dy.contiguous()
         ds = None if ds is None else ds.contiguous()
         bias_p, gamma_p, beta_p = ctx.pref
@@ -144,7 +149,8 @@ class _BDALayerNorm(torch.autograd.Function):
         if ctx.gather is not None and ctx.gather[3]:
             gbuf, out_dx = gather_slot(s, ctx.gather[0], ctx.gather[1])
         d_s, dx, dgamma, dbeta, dbias = C.layernorm_bwd(dy, ds, s, gamma, mean, rstd, p, seed, offset, rms,
-                                                        True, has_bias, ta, tb, tc, out_dx)
+                                                        True, has_bias, ta, tb, tc, out_dx,
+                                                        None if dy2 is None else dy2.contiguous())
         if gbuf is not None:
             _mark_gather(dx, gbuf, ctx.gather[1])
         _mark_ready(gamma_p if ta is not None else None, beta_p if tb is not None else None,

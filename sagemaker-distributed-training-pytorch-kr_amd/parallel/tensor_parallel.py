@@ -893,6 +893,7 @@ class SPFusedGeLUMLP(torch.autograd.Function):
         ctx.save_for_backward(total, w1, w2, pre, act)
         ctx.b1 = b1
         ctx.bulk = _SPLIT["on"]     # a sub-batch half: bulk rings in backward
+        ctx.defer_add = _bwd_add_to_norm(x)
         return y
 
     @staticmethod
@@ -921,7 +922,7 @@ class SPFusedGeLUMLP(torch.autograd.Function):
             _flush_wgrad()
         w1t = _dgrad_weight_t(w1)
         dx = rs_ring(lambda lo, m, o: _dgrad_rows(dz[lo:lo + m], w1, w1t, o), group,
-                     dz.shape[:-1] + (w1.shape[1],), dz, wgrad, bulk=ctx.bulk)
+                     dz.shape[:-1] + (w1.shape[1],), dz, wgrad, bulk=ctx.bulk, defer_add=ctx.defer_add)
         if "dw" not in res:
             wgrad()
         return dx, res["dw"], res["db"], dw2
@@ -1311,6 +1312,15 @@ class defer_rs_add:
         return False
 
 
+def _bwd_add_to_norm(x) -> bool:
+    """Whether a column SP linear's backward reduce-scatter may leave its combine to x's producer:
+    inside the layer stack (``defer_rs_add``), x written by the fused norm kernel into its
+    all-gather slot (``_smdt_gather``: the norm's autograd node receives the gradient as is) and on
+    the kernel path (the norm backward that reads the pending summand)."""
+    return (_DEFER_ADD["on"] and not _SPLIT["on"] and getattr(x, "_smdt_gather", None) is not None
+            and _ext.use_kernels(x))
+
+
 def materialize_add(t):
     """Apply a pending reduce-scatter summand (``defer_rs_add``) in place; returns t."""
     x2 = getattr(t, "_smdt_add", None)
@@ -1320,7 +1330,7 @@ def materialize_add(t):
     return t
 _AG_PENDING = {}      # (data_ptr, shape) of a started all-gather's input -> (total, works, rank, n)
 _RS_PENDING = []      # outputs whose reduce-scatter was started but not yet combined
-SPLIT_STATS = {"ag_started": 0, "rs_deferred": 0, "rs_add_to_norm": 0}
+SPLIT_STATS = {"ag_started": 0, "rs_deferred": 0, "rs_add_to_norm": 0, "bwd_add_to_norm": 0}
 
 
 def _pending_key(x):
@@ -1436,7 +1446,7 @@ def ag_ring(x, group, chunk_fn=None, before_last_wait=None, _skip_direct=False, 
     return total
 
 
-def rs_ring(partial_fn, group, full_shape, ref, before_last_wait=None, bulk=False):
+def rs_ring(partial_fn, group, full_shape, ref, before_last_wait=None, bulk=False, defer_add=False):
     """Reduce-scatter along dim 0 over ``group`` as a ring. The tensor being reduced (``full_shape``,
     ``ref``'s dtype / device) is produced on demand: ``partial_fn(lo, rows, out)`` computes its rows
     [lo, lo + rows) — a GEMM on those rows — into ``out`` when given (and returns it), else into a
@@ -1484,9 +1494,9 @@ def rs_ring(partial_fn, group, full_shape, ref, before_last_wait=None, bulk=Fals
             if s == ws - 1 and before_last_wait is not None:
                 before_last_wait()
             _wait_works(works, group)
-            if s == ws - 1 and ws == 2 and _DEFER_ADD["on"] and before_last_wait is None:
+            if s == ws - 1 and ws == 2 and ((_DEFER_ADD["on"] and before_last_wait is None) or defer_add):
                 part._smdt_add = incoming      # the consuming norm adds it (see _DEFER_ADD)
-                SPLIT_STATS["rs_add_to_norm"] += 1
+                SPLIT_STATS["bwd_add_to_norm" if defer_add else "rs_add_to_norm"] += 1
                 return part
             part = part.add_(incoming)
         if s == ws - 1:
@@ -1533,6 +1543,7 @@ class _ColumnSPLinear(torch.autograd.Function):
         ctx.bias_p = bias
         ctx.n = n
         ctx.bulk = _SPLIT["on"]
+        ctx.defer_add = _bwd_add_to_norm(x)
         return out
 
     @staticmethod
@@ -1549,7 +1560,7 @@ class _ColumnSPLinear(torch.autograd.Function):
             _flush_wgrad()
         wt = _dgrad_weight_t(weight)
         gi = rs_ring(lambda lo, m, o: _dgrad_rows(g[lo:lo + m], weight, wt, o), group,
-                     g.shape[:-1] + (weight.shape[1],), g, wgrad, bulk=ctx.bulk)
+                     g.shape[:-1] + (weight.shape[1],), g, wgrad, bulk=ctx.bulk, defer_add=ctx.defer_add)
         if "dw" not in res:   # world 1 ring: no wait happened
             wgrad()
         return gi, res["dw"], res["db"], None

@@ -161,6 +161,23 @@ def test_subbatch_interleave_emulated_tp2_step_matches_default(monkeypatch):
     assert (gs - ge).abs().max() <= 3e-2 * ge.abs().max()
 
 
+def test_reduce_scatter_combine_in_norms_matches_plain_combine(monkeypatch):
+    """One emulated tp2 + SP rank on the kernel path: with the ring reduce-scatters' combines left
+    to the fused norms (forward: the norm reads x + x2; backward: the norm backward reads dy +
+    dy2) the losses and fp32 main_grad equal the plain separate-add path up to bf16 rounding, and
+    both deferrals really ran."""
+    from smdt_amd.parallel import tensor_parallel as TPm
+    monkeypatch.setattr(TPm, "_DEFER_RS_ADD", False)
+    lo, go = _gpt_emulated_tp_run(False, sp=True)
+    monkeypatch.setattr(TPm, "_DEFER_RS_ADD", True)
+    before = dict(TPm.SPLIT_STATS)
+    ld, gd = _gpt_emulated_tp_run(False, sp=True)
+    assert TPm.SPLIT_STATS["rs_add_to_norm"] > before["rs_add_to_norm"]
+    assert TPm.SPLIT_STATS["bwd_add_to_norm"] > before["bwd_add_to_norm"]
+    torch.testing.assert_close(ld, lo, rtol=1e-2, atol=1e-2)
+    assert (gd - go).abs().max() <= 2e-2 * go.abs().max()
+
+
 def test_bench_graph_mode_captures(tmp_path):
     """bench.py --graph 1 on an emulated tp2 last-stage rank reports a captured HIP graph."""
     import json
