@@ -37,6 +37,12 @@ import torch.distributed as dist
 _ASYNC = os.environ.get("SMDT_LOOPBACK_ASYNC", "1") == "1"
 
 
+def _delay_cycles() -> int:
+    """SMDT_LOOPBACK_DELAY_CYCLES (tests): a GPU spin of that many cycles on the side stream before
+    every stand-in, so a consumer that skips its ``Work.wait()`` reads stale data visibly."""
+    return int(os.environ.get("SMDT_LOOPBACK_DELAY_CYCLES", "0") or 0)
+
+
 def _done(result):
     from torch._C._distributed_c10d import _create_work_from_future
     fut = torch.futures.Future()
@@ -77,6 +83,9 @@ class LoopbackGroup(dist.ProcessGroup):
             side = self._streams[dev] = comm_stream(dev)
         side.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(side):
+            delay = _delay_cycles()
+            if delay > 0:
+                torch.cuda._sleep(delay)
             fn()
         for t in tensors:
             t.record_stream(side)     # the caller may free them before the side stream is done

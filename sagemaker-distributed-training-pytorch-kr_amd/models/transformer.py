@@ -91,6 +91,16 @@ class TransformerConfig:
         return self.normalization.lower() == "rmsnorm"
 
 
+def _gather_wait(mod, x):
+    """Run ``mod``'s overlapped-ZeRO parameter all-gather wait (a forward pre-hook installed by
+    parallel/distributed.py) for a module whose weights are read without calling ``mod(x)``
+    (Norm.fused, the fused MLP paths). Without it the kernel could read weights whose async
+    all-gather is still in flight. The wait is idempotent."""
+    for hook in tuple(mod._forward_pre_hooks.values()):
+        if getattr(hook, "_smdt_gather_wait", False):
+            hook(mod, (x,))
+
+
 class Norm(nn.Module):
     """LayerNorm / RMSNorm parameters; the math runs in the fused BDA+norm kernel."""
 
@@ -110,12 +120,9 @@ class Norm(nn.Module):
             self.register_parameter("bias", None)
 
     def fused(self, x, xbias, residual, p, training, gather=None):
-        # called instead of forward() by the layers: run the overlapped ZeRO parameter all-gather's
-        # wait for this module's bucket (a forward pre-hook, parallel/distributed.py) — without it
-        # the norm could read its weights while their all-gather is still in flight
-        for hook in tuple(self._forward_pre_hooks.values()):
-            if getattr(hook, "_smdt_gather_wait", False):
-                hook(self, (x,))
+        # called instead of forward() by the layers: wait for this module's overlapped ZeRO
+        # parameter all-gather (see _gather_wait) before the kernel reads the weights
+        _gather_wait(self, x)
         return SF.bias_dropout_add_norm(x, xbias, residual, self.weight, self.bias, p, training, self.eps, self.rms,
                                         rng=get_rng(self.rng_kind), gather=gather)
 
@@ -509,6 +516,10 @@ class ParallelMLP(nn.Module):
 
     def forward(self, x):
         act = self.cfg.activation
+        if act == "gelu" and self.cfg.bias_gelu_fusion:
+            # the fused forms read fc1 / fc2 weights without calling fc1(x) / fc2(x)
+            _gather_wait(self.fc1, x)
+            _gather_wait(self.fc2, x)
         if act == "gelu" and self.cfg.bias_gelu_fusion and tp.sp_fused_gelu_mlp_ok(x, self):
             # TP > 1 + sequence parallelism: the GeLU halves inside the ring-chunk GEMMs
             return tp.SPFusedGeLUMLP.apply(x, self.fc1.weight, self.fc1.bias, self.fc2.weight), self.fc2.bias
@@ -643,6 +654,8 @@ class ParallelTransformer(nn.Module):
         the final norm / the pipeline send. Same math as ``forward`` per half; with dropout, the
         masks are drawn in the interleaved order."""
         hb = x.shape[1] // 2
+        if x.requires_grad:
+            x = tp.WgradMergeScope.apply(x, False)
         halves = []
         for i in range(2):
             sl = slice(i * hb, (i + 1) * hb)
@@ -660,6 +673,8 @@ class ParallelTransformer(nn.Module):
         finally:
             tp.end_subbatch()
         x = torch.cat([h["x"] for h in halves], dim=1)
+        if x.requires_grad:
+            x = tp.WgradMergeScope.apply(x, True)
         xbias = halves[0]["xbias"]
         residual = torch.cat([h["residual"] for h in halves], dim=1)
         return x, xbias, residual
@@ -669,9 +684,13 @@ class ParallelTransformer(nn.Module):
         output (the pending branch folded into the residual first)."""
         if self._subbatch_ok(x):
             x, xbias, residual = self._forward_subbatch(x, xbias, residual)
-        elif self.cfg.recompute_granularity != "full":
+        elif self.cfg.recompute_granularity != "full" and not tp.foreign_hooks(self):
             # every row-parallel output of the stack is consumed by the next fused norm (the
-            # layers' own, or the final one): the ring reduce-scatters leave their combine to it
+            # layers' own, or the final one): the ring reduce-scatters leave their combine to it.
+            # Not with user hooks on the stack (they would read a tensor missing the peer's
+            # partial); the ledger (tp.check_pending_adds) catches any other consumer.
+            if x.requires_grad and torch.is_grad_enabled():
+                x = tp.PendingAddCheck.apply(x)
             with tp.defer_rs_add():
                 for i in range(len(self.layers)):
                     x, xbias, residual = self._run(i, x, xbias, residual)
@@ -682,5 +701,8 @@ class ParallelTransformer(nn.Module):
             g = _sp_gather(self.cfg)          # y feeds the LM head's column-parallel all-gather
             y, _ = self.final_norm.fused(x, xbias, residual, self.cfg.hidden_dropout, self.training,
                                          gather=None if g is None else g + (True, residual is not None))
+            tp.check_pending_adds("the end of the layer stack's forward")
             return y
-        return tp.materialize_add(x), xbias, residual      # leaves the stage: no pending summand
+        x = tp.materialize_add(x)      # leaves the stage: no pending summand
+        tp.check_pending_adds("the end of the layer stack's forward")
+        return x, xbias, residual

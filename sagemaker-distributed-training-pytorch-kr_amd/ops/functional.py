@@ -135,9 +135,8 @@ class _BDALayerNorm(torch.autograd.Function):
         C = _ext.ext()
         # the consuming column-parallel linear's backward reduce-scatter may leave its peer's
         # partial as a pending summand of dy (tensor_parallel.rs_ring, defer_add): added in-kernel
-        dy2 = getattr(dy, "_smdt_add", None)
-        if dy2 is not None:
-            del dy._smdt_add
+        from ..parallel.tensor_parallel import take_pending_add
+        dy2 = take_pending_add(dy)
         dy = dy.contiguous()
         ds = None if ds is None else ds.contiguous()
         bias_p, gamma_p, beta_p = ctx.pref
@@ -172,9 +171,8 @@ def bias_dropout_add_norm(x, bias, residual, gamma, beta, p: float, training: bo
     p = float(p) if training else 0.0
     # a row-parallel output whose reduce-scatter left its peer's partial as a pending summand
     # (tensor_parallel.rs_ring under defer_rs_add): x + x2 is the value, added in the kernel
-    x2 = getattr(x, "_smdt_add", None)
-    if x2 is not None:
-        del x._smdt_add
+    from ..parallel.tensor_parallel import take_pending_add
+    x2 = take_pending_add(x)
     if _ext.use_kernels(x):
         seed, offset = _rng(rng).next() if p > 0 else (0, 0)
         return _BDALayerNorm.apply(x, bias, residual, gamma, None if rms else beta, p, float(eps), bool(rms),

@@ -322,9 +322,6 @@ class MixedPrecisionAdam:
             ddp.all_gather_params()
             ddp.wait_param_gather()
 
-    def zero_grad(self, set_to_none=True):
-        self.ddp.zero_grad_buffer()
-
     @torch.no_grad()
     def reload_model_params(self):
         """Refresh the fp32 masters from the model buffer (after loading weights only)."""

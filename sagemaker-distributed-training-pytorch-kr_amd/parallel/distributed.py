@@ -603,6 +603,8 @@ class DistributedDataParallel(nn.Module):
 
     def finish_grad_sync(self):
         """Launch what is left, wait for every bucket, then fix up sequence-parallel grads."""
+        from .tensor_parallel import check_pending_adds
+        check_pending_adds("finish_grad_sync")   # a deferred RS summand no consumer added
         self.wait_param_gather()  # params a forward never touched
         if self.zero_stage >= 2:
             from .tensor_parallel import flush_deferred_wgrad
@@ -744,12 +746,14 @@ class DistributedDataParallel(nn.Module):
         def hook(_mod, _inp):
             if self._opt_events:
                 self.wait_param_update(indices)
+        hook._smdt_internal = True
         return hook
 
     def _make_gather_wait(self, indices):
         def hook(_mod, _inp):
             self.wait_param_gather(indices)
         hook._smdt_gather_wait = True      # also run by modules used without forward() (Norm.fused)
+        hook._smdt_internal = True         # reads no activation (tensor_parallel.foreign_hooks)
         return hook
 
     def state_dict(self, *args, **kwargs):

@@ -953,7 +953,8 @@ def linear_bias_gelu_ok(x, layer) -> bool:
     a shape gemm_tn supports."""
     if not (_FUSED_BIAS_GELU and x.is_cuda and layer.bias is not None and not layer.sequence_parallel
             and x.dtype in (torch.bfloat16, torch.float16) and layer.weight.dtype == x.dtype
-            and layer.bias.dtype == x.dtype and x.is_contiguous() and not layer.gather_output):
+            and layer.bias.dtype == x.dtype and x.is_contiguous() and not layer.gather_output
+            and _ext.use_kernels(x)):
         return False
     x2 = x.view(-1, x.shape[-1])
     return bool(_ext.ext().gemm_tn_supported(x2, layer.weight))
@@ -1321,11 +1322,68 @@ def _bwd_add_to_norm(x) -> bool:
             and _ext.use_kernels(x))
 
 
-def materialize_add(t):
-    """Apply a pending reduce-scatter summand (``defer_rs_add``) in place; returns t."""
+# Ledger of the pending summands: every summand hung on a tensor by
+# ``set_pending_add`` must be taken by ``take_pending_add`` (the fused norm, forward or backward,
+# or ``materialize_add``). A consumer that reads the tensor some other way would silently miss the
+# peer's half, so anything left over at a check point raises instead: the end of the layer
+# stack's forward and the end of its backward (models/transformer.ParallelTransformer), and
+# DistributedDataParallel.finish_grad_sync.
+_ADD_LEDGER = {"issued": 0, "consumed": 0, "live": {}}
+
+
+def set_pending_add(t, x2, where: str):
+    t._smdt_add = x2
+    _ADD_LEDGER["issued"] += 1
+    _ADD_LEDGER["live"][id(t)] = where
+
+
+def take_pending_add(t):
+    """The pending summand of ``t`` (removed from it and from the ledger), or None."""
     x2 = getattr(t, "_smdt_add", None)
     if x2 is not None:
         del t._smdt_add
+        _ADD_LEDGER["consumed"] += 1
+        _ADD_LEDGER["live"].pop(id(t), None)
+    return x2
+
+
+def check_pending_adds(where: str):
+    """Raise if a deferred reduce-scatter summand was issued but never consumed."""
+    live = _ADD_LEDGER["live"]
+    if live:
+        kinds = sorted(set(live.values()))
+        n = len(live)
+        live.clear()
+        raise RuntimeError(
+            f"{n} deferred reduce-scatter summand(s) ({', '.join(kinds)}) were never added by their "
+            f"consumer (checked at {where}): a hook, a second consumer or a non-fused norm read a "
+            "row-parallel output / column-parallel input gradient without the peer's partial. Run "
+            "with SMDT_DEFER_RS_ADD=0 or keep the fused norm as the only consumer.")
+
+
+def foreign_hooks(module) -> bool:
+    """Whether any hook other than the framework's own parameter-wait pre-hooks (marked
+    ``_smdt_internal``) could see the layer stack's activations or gradients: global module hooks,
+    or forward / backward hooks on ``module`` or a submodule. Deferring the reduce-scatter combine
+    is only safe without them (a hook would read a tensor missing the peer's partial)."""
+    from torch.nn.modules import module as _M
+    for name in ("_global_forward_hooks", "_global_forward_pre_hooks", "_global_backward_hooks",
+                 "_global_backward_pre_hooks"):
+        if getattr(_M, name, None):
+            return True
+    for m in module.modules():
+        if m._forward_hooks or m._backward_hooks or getattr(m, "_backward_pre_hooks", None):
+            return True
+        for h in m._forward_pre_hooks.values():
+            if not getattr(h, "_smdt_internal", False):
+                return True
+    return False
+
+
+def materialize_add(t):
+    """Apply a pending reduce-scatter summand (``defer_rs_add``) in place; returns t."""
+    x2 = take_pending_add(t)
+    if x2 is not None:
         t.data.add_(x2)
     return t
 _AG_PENDING = {}      # (data_ptr, shape) of a started all-gather's input -> (total, works, rank, n)
@@ -1376,7 +1434,37 @@ def rs_finish(t):
 
 def begin_subbatch():
     _SPLIT["on"] = True
-    DEFERRED_WGRAD.merge_repeats = True
+
+
+class PendingAddCheck(torch.autograd.Function):
+    """Identity on the layer stack's input whose backward (the last node of the stack's backward)
+    checks that every deferred summand of that backward was consumed (``check_pending_adds``)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        check_pending_adds("the end of the layer stack's backward")
+        return g
+
+
+class WgradMergeScope(torch.autograd.Function):
+    """Identity whose backward sets ``DEFERRED_WGRAD.merge_repeats`` to ``on``. The sub-batch
+    interleave wraps its output with on=True (the first node of the pass's backward) and its
+    input with on=False (the last), so the merge of the two halves' pushes is scoped to that
+    backward and every later pass flushes repeated pushes in order again."""
+
+    @staticmethod
+    def forward(ctx, x, on):
+        ctx.on = bool(on)
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        DEFERRED_WGRAD.merge_repeats = ctx.on
+        return g, None
 
 
 def end_subbatch():
@@ -1495,7 +1583,8 @@ def rs_ring(partial_fn, group, full_shape, ref, before_last_wait=None, bulk=Fals
                 before_last_wait()
             _wait_works(works, group)
             if s == ws - 1 and ws == 2 and ((_DEFER_ADD["on"] and before_last_wait is None) or defer_add):
-                part._smdt_add = incoming      # the consuming norm adds it (see _DEFER_ADD)
+                # the consuming norm adds it (see _DEFER_ADD)
+                set_pending_add(part, incoming, "backward dgrad" if defer_add else "forward output")
                 SPLIT_STATS["bwd_add_to_norm" if defer_add else "rs_add_to_norm"] += 1
                 return part
             part = part.add_(incoming)

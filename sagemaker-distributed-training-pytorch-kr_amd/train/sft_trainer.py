@@ -53,6 +53,9 @@ def setup_distributed(args=None, backend: str = "nccl"):
     if dist.is_initialized():
         rank, world = dist.get_rank(), dist.get_world_size()
         local = int(os.environ.get("LOCAL_RANK", "0"))
+        if torch.cuda.is_available():
+            # a caller-initialised group may not have selected this rank's device
+            torch.cuda.set_device(local % torch.cuda.device_count())
     else:  # single process: no process group is created
         # SMDT_DIST_BACKEND=gloo: one-GPU rehearsal of the multi-rank path (RCCL refuses two ranks
         # on one device)

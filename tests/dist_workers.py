@@ -1417,3 +1417,54 @@ def ag_start_view_worker(rank, world, emulate=False):
         w.grad = None
     dist.destroy_process_group()
     return res
+
+
+def deferred_add_worker(rank, world, case, guard=True, defer=True):
+    """tp2 + SP on Gloo with the ring reduce-scatter's combine deferred to the consuming fused norm
+    (tensor_parallel.defer_rs_add). ``case``:
+      * "hook": a forward hook on layer 0's attention output projection (a row-parallel linear)
+        records its output; ``guard`` False disables the foreign-hook check (mutation arm);
+      * "plain_norm": the layers' norm replaced by a plain one that never takes the pending summand;
+      * "bwd": the column-parallel linears' backward reduce-scatter is made to defer its combine
+        (forced on CPU), and the norm backward on CPU does not take it.
+    Returns (loss or the raised error text, hook capture, split stats)."""
+    import torch.nn.functional as F
+    import torch.distributed as dist
+    from smdt_amd.comm import init_distributed
+    from smdt_amd.models import transformer as T
+    from smdt_amd.models.gpt import GPTModel
+    from smdt_amd.models.transformer import TransformerConfig
+    from smdt_amd.parallel import state as ps
+    from smdt_amd.parallel import tensor_parallel as TPm
+    init_distributed("gloo")
+    ps.initialize_model_parallel(2, 1)
+    TPm._DEFER_RS_ADD = defer
+    for k in TPm.SPLIT_STATS:
+        TPm.SPLIT_STATS[k] = 0
+    if not guard:
+        TPm.foreign_hooks = lambda module: False
+    if case == "plain_norm":
+        def plain(self, x, xbias, residual, p, training, gather=None):
+            h = x if xbias is None else x + xbias
+            s = h if residual is None else residual + h
+            return F.layer_norm(s, s.shape[-1:], self.weight, self.bias, self.eps), s
+        T.Norm.fused = plain
+    if case == "bwd":
+        TPm._bwd_add_to_norm = lambda x: True
+    cfg = TransformerConfig(**{**TINY, "sequence_parallel": True})
+    m = GPTModel(cfg)
+    seen = []
+    if case == "hook":
+        m.decoder.layers[0].attention.proj.register_forward_hook(
+            lambda mod, inp, out: seen.append((out[0] if isinstance(out, tuple) else out).detach().clone()))
+    tokens, labels = _batch()
+    try:
+        loss = m(tokens, None, None, labels=labels)
+        loss.mean().backward()
+        out = loss.detach()
+    except RuntimeError as e:
+        out = str(e)
+    TPm._ADD_LEDGER["live"].clear()
+    stats = dict(TPm.SPLIT_STATS)
+    dist.destroy_process_group()
+    return out, (seen[0] if seen else None), stats

@@ -509,3 +509,48 @@ def test_vocab_parallel_fused_ce_path_is_taken(monkeypatch):
     assert not tp.vp_lm_head_ce_ok(h, w, 2)
     monkeypatch.setenv("SMDT_LM_HEAD_CE_CPU", "1")
     assert tp.vp_lm_head_ce_ok(h, w, 2) and not tp.vp_lm_head_ce_ok(h, w, 1)
+
+
+def test_pending_add_ledger_unit():
+    """A summand hung on a tensor must be taken before a check point (tensor_parallel ledger)."""
+    from smdt_amd.parallel import tensor_parallel as tp
+    t, x2 = torch.ones(4), torch.full((4,), 2.0)
+    tp.set_pending_add(t, x2, "forward output")
+    assert tp.take_pending_add(t) is x2 and not hasattr(t, "_smdt_add")
+    tp.check_pending_adds("after take")            # nothing pending: no error
+    u = torch.ones(4)
+    tp.set_pending_add(u, x2, "forward output")
+    v = u * 3                                        # a consumer that is not the fused norm
+    assert not hasattr(v, "_smdt_add")
+    with pytest.raises(RuntimeError, match="never added"):
+        tp.check_pending_adds("test")
+    tp.set_pending_add(u, x2, "forward output")
+    assert torch.equal(tp.materialize_add(u), torch.full((4,), 3.0))
+    tp.check_pending_adds("after materialize")
+
+
+def test_deferred_rs_add_with_a_forward_hook_materializes():
+    """tp2 + SP (Gloo): a forward hook on a row-parallel linear of the layer stack turns the
+    deferred reduce-scatter combine off, so the hook sees the complete output (equal to the run
+    with SMDT_DEFER_RS_ADD=0) and the loss is unchanged. Mutation arm: with the hook guard
+    disabled the hook sees the output without the peer's partial."""
+    base = run_workers(W.deferred_add_worker, 2, "hook", True, False)
+    hooked = run_workers(W.deferred_add_worker, 2, "hook", True, True)
+    unguarded = run_workers(W.deferred_add_worker, 2, "hook", False, True)
+    for (l0, h0, _), (l1, h1, s1), (_, h2, s2) in zip(base, hooked, unguarded):
+        assert isinstance(l1, torch.Tensor), l1
+        _close(l1, l0)
+        _close(h1, h0)
+        assert s1["rs_add_to_norm"] == 0 and s2["rs_add_to_norm"] > 0
+        assert (h2 - h0).abs().max() > 1e-3
+
+
+@pytest.mark.parametrize("case", ["plain_norm", "bwd"])
+def test_deferred_rs_add_unconsumed_summand_raises(case):
+    """tp2 + SP (Gloo) with the combine deferred, but the summand's consumer is not the fused norm:
+    a model variant whose norm never takes it (forward), or a backward consumer of a deferred
+    input-gradient summand that is not the fused norm kernel (the case of a norm output with a
+    second consumer, whose summed gradient drops the attribute). The ledger raises instead of
+    returning a loss / gradients without the peer's partial."""
+    for out, _, _ in run_workers(W.deferred_add_worker, 2, case):
+        assert isinstance(out, str) and "never added" in out, out

@@ -340,3 +340,63 @@ def test_wgrad_grouped_overwrite_ignores_stale_targets():
     mg = torch.full((n, k), float("nan"), device="cuda")
     assert C.wgrad_grouped([mg], [dy], [x], [], [True])
     torch.testing.assert_close(mg, dy.float().t() @ x.float(), atol=0.05, rtol=1e-3)
+
+
+def test_fused_mlp_waits_for_overlapped_param_gather(monkeypatch):
+    """ZeRO-1 with ``overlap_param_gather`` (one emulated DP=2 rank: the parameter all-gather is a
+    loopback stand-in on a side stream, delayed ~10 ms so a skipped wait reads stale weights). The
+    fused fc1 + bias-GeLU MLP reads fc1 / fc2 weights without calling fc1(x) / fc2(x), so it must
+    run their gather-wait pre-hooks itself (models/transformer._gather_wait): its losses equal the
+    unfused MLP's, which waits through the modules' own forward pre-hooks."""
+    from smdt_amd.models.gpt import GPTModel
+    from smdt_amd.models.transformer import TransformerConfig
+    from smdt_amd.optim.optimizer import MixedPrecisionAdam
+    from smdt_amd.parallel import state as ps
+    from smdt_amd.parallel.distributed import DistributedDataParallel
+    monkeypatch.setenv("SMDT_LOOPBACK_DELAY_CYCLES", "20000000")
+    calls = {"n": 0}
+    orig = tp.FusedGeLUMLP.apply
+
+    def counted(*a):
+        calls["n"] += 1
+        return orig(*a)
+    monkeypatch.setattr(tp.FusedGeLUMLP, "apply", counted)
+    import smdt_amd.models.transformer as T
+    real_wait = T._gather_wait
+    runs = []
+    # third arm, a mutation check of the test itself: the fused MLP WITHOUT its gather waits must
+    # read stale weights and move the losses
+    for fused, wait in ((True, True), (False, True), (True, False)):
+        monkeypatch.setattr(tp, "_FUSED_BIAS_GELU", fused)
+        monkeypatch.setattr(T, "_gather_wait", real_wait if wait else (lambda mod, x: None))
+        ps.destroy_model_parallel()
+        ps.initialize_emulated_tensor_parallel(1, 2)
+        torch.manual_seed(0)
+        cfg = TransformerConfig(num_layers=2, hidden_size=256, num_attention_heads=4, padded_vocab_size=1024,
+                                max_position_embeddings=256, hidden_dropout=0.0, attention_dropout=0.0,
+                                params_dtype=torch.bfloat16)
+        model = GPTModel(cfg, device="cuda")
+        ddp = DistributedDataParallel(model, bucket_size=200_000, use_distributed_optimizer=True,
+                                      overlap_param_gather=True)
+        assert len(ddp.buckets) > 2
+        opt = MixedPrecisionAdam(ddp, lr=1e-2, weight_decay=0.0, clip_grad=1.0)
+        g = torch.Generator(device="cuda").manual_seed(1)
+        tokens = torch.randint(0, 1000, (4, 257), device="cuda", generator=g)
+        losses = []
+        for _ in range(4):
+            ddp.zero_grad_buffer()
+            loss = ddp(tokens[:, :-1], None, None, labels=tokens[:, 1:]).float().mean()
+            loss.backward()
+            ddp.finish_grad_sync()
+            opt.step()
+            losses.append(loss.detach())
+        ddp.wait_param_gather()
+        torch.cuda.synchronize()
+        runs.append(torch.stack(losses).cpu())
+        if fused:
+            assert calls["n"] >= 4 * cfg.num_layers, calls      # the fused MLP really ran
+    ps.destroy_model_parallel()
+    a, b, stale = runs
+    assert (a[1:] - a[:-1]).abs().max() > 1e-2          # steps move the loss: stale weights would show
+    torch.testing.assert_close(a, b, atol=2e-2, rtol=0)
+    assert (stale - b).abs().max() > 5 * (a - b).abs().max(), (a, b, stale)
