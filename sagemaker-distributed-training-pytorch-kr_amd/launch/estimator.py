@@ -327,12 +327,29 @@ class _LocalJob:
             argvs.append(cmd)
             envs.append([f"{k}={v}" for k, v in e.items()])
         log_path = os.path.join(self.root, "logs", "job.log")
+        req_lines, missing = check_requirements(p["code"])
+        if req_lines:
+            txt = "".join(f"[smdt] {ln}\n" for ln in req_lines)
+            if stream:
+                sys.stdout.write(txt)
+        if missing:
+            err = ("[smdt] ERROR: source_dir/requirements.txt names module(s) that are not importable: "
+                   + ", ".join(f"{r} ({m})" for r, m in missing) + "\n")
+            with open(log_path, "w") as f:
+                f.write(txt + err)
+            if stream:
+                sys.stdout.write(err)
+            self._write_status("Failed", exit_status=1, failure_reason=err.strip(), missing_requirements=missing)
+            self.est.status = 1
+            return 1
         scraper = MetricScraper(self.est.metric_definitions)
         self._write_status("InProgress", nprocs=nprocs, command=cmd)
         hdr = (f"[smdt] job {self.job_name}: {nprocs} process(es) on {socket.gethostname()} "
                f"(GPUs visible: {ngpu}); cmd: {' '.join(cmd)}\n")
         rfd, wfd = os.pipe()
         logf = open(log_path, "w")
+        if req_lines:
+            logf.write(txt)
         logf.write(hdr)
         if stream:
             sys.stdout.write(hdr)
@@ -375,6 +392,45 @@ class _LocalJob:
         with tarfile.open(os.path.join(out, "model.tar.gz"), "w:gz") as tar:
             for name in sorted(os.listdir(p["model"])):
                 tar.add(os.path.join(p["model"], name), arcname=name)
+
+
+# Requirements the framework provides in-tree (no package index on the node): the module the
+# recipe would import -> what replaces it. The Oxford recipe's albumentations pipeline runs as the
+# GPU augmentation of data/augment.py (csrc/kernels/augment.hip).
+PROVIDED_IN_TREE = {"albumentations": "smdt_amd.data.augment (GPU augmentation, csrc/kernels/augment.hip)"}
+# distribution name -> import name where they differ
+_IMPORT_NAMES = {"opencv-python": "cv2", "opencv-python-headless": "cv2", "scikit-learn": "sklearn",
+                 "pillow": "PIL", "pyyaml": "yaml", "protobuf": "google.protobuf", "python-dateutil": "dateutil"}
+
+
+def check_requirements(code_dir):
+    """E6: the toolkit pip-installs ``source_dir/requirements.txt`` before the entry point runs
+    (reference 2_training_oxford-pet_ddp/requirements.txt:1, toolkit log at
+    2_training_oxford-pet_ddp.ipynb:622). Offline there is nothing to install from, so each
+    requirement must already be importable or be provided in-tree (PROVIDED_IN_TREE).
+    Returns (log lines, missing [(requirement, module)]); no file -> ([], [])."""
+    import importlib.util
+    import re
+    path = os.path.join(code_dir, "requirements.txt")
+    if not os.path.exists(path):
+        return [], []
+    lines = ["sagemaker-training-toolkit INFO     Installing dependencies from requirements.txt:",
+             f"sagemaker-training-toolkit INFO     (offline: checking importability, no pip) {path}"]
+    missing = []
+    for raw in open(path):
+        req = raw.split("#", 1)[0].strip()
+        if not req or req.startswith("-"):
+            continue
+        name = re.split(r"[\s<>=!~;\[]", req, 1)[0].strip()
+        mod = _IMPORT_NAMES.get(name.lower(), name.replace("-", "_"))
+        if mod in PROVIDED_IN_TREE:
+            lines.append(f"  {req}: provided in-tree by {PROVIDED_IN_TREE[mod]}")
+        elif importlib.util.find_spec(mod.split(".")[0]) is not None:
+            lines.append(f"  {req}: importable ({mod})")
+        else:
+            lines.append(f"  {req}: NOT importable (module {mod!r}) and no package index to install from")
+            missing.append((req, mod))
+    return lines, missing
 
 
 def _run_ranks(argvs, envs, grace, max_run, cwd, out_fd):

@@ -250,7 +250,94 @@ _GROUPS = {
         ("--fp8-amax-history-len", dict(type=int, default=1)),
         ("--fp8-amax-compute-algo", dict(default="most_recent", choices=["most_recent", "max"])),
     ],
+    # Task families of the reference's Megatron tree that this framework does not train (vision
+    # classification / inpainting / DINO, ICT / REALM biencoder retrieval, Retro, text-generation
+    # inference): accepted so a reference hyperparameter dict parses unchanged, and ignored with a
+    # warning when set to a non-default value (validate_args). Reference:
+    # 3_training_megatron-lm/megatron/arguments.py:478-483 (inference), 500-503 (Bert embedder),
+    # 1182-1199 (Retro), 1239-1305 (biencoder, vision).
+    "inference (accepted, ignored)": [
+        ("--inference-batch-times-seqlen-threshold", dict(type=int, default=512)),
+        ("--max-tokens-to-oom", dict(type=int, default=12000)),
+        ("--output-bert-embeddings", dict(action="store_true")),
+        ("--bert-embedder-type", dict(default="megatron", choices=["megatron", "huggingface"])),
+    ],
+    "retro (accepted, ignored)": [
+        ("--retro-workdir", dict(default=None)),
+        ("--retro-add-retriever", dict(action="store_true", default=False)),
+        ("--retro-cyclic-train-iters", dict(type=int, default=None)),
+        ("--retro-encoder-layers", dict(type=int, default=2)),
+        ("--retro-encoder-hidden-dropout", dict(type=float, default=0.1)),
+        ("--retro-encoder-attention-dropout", dict(type=float, default=0.1)),
+        ("--retro-num-neighbors", dict(type=int, default=2)),
+        ("--retro-num-retrieved-chunks", dict(type=int, default=2)),
+        ("--retro-return-doc-ids", dict(action="store_true")),
+    ],
+    "biencoder (accepted, ignored)": [
+        ("--ict-head-size", dict(type=int, default=None)),
+        ("--biencoder-projection-dim", dict(type=int, default=0)),
+        ("--biencoder-shared-query-context-model", dict(action="store_true")),
+        ("--ict-load", dict(type=str, default=None)),
+        ("--bert-load", dict(type=str, default=None)),
+        ("--titles-data-path", dict(type=str, default=None)),
+        ("--query-in-block-prob", dict(type=float, default=0.1)),
+        ("--use-one-sent-docs", dict(action="store_true")),
+        ("--evidence-data-path", dict(type=str, default=None)),
+        ("--retriever-report-topk-accuracies", dict(nargs="+", type=int, default=[])),
+        ("--retriever-score-scaling", dict(action="store_true")),
+        ("--block-data-path", dict(type=str, default=None)),
+        ("--embedding-path", dict(type=str, default=None)),
+        ("--indexer-batch-size", dict(type=int, default=128)),
+        ("--indexer-log-interval", dict(type=int, default=1000)),
+    ],
+    "vision (accepted, ignored)": [
+        ("--num-classes", dict(type=int, default=1000)),
+        ("--img-h", dict(type=int, default=224)),
+        ("--img-w", dict(type=int, default=224)),
+        ("--num-channels", dict(type=int, default=3)),
+        ("--patch-dim", dict(type=int, default=16)),
+        ("--classes-fraction", dict(type=float, default=1.0)),
+        ("--data-per-class-fraction", dict(type=float, default=1.0)),
+        ("--no-data-sharding", dict(action="store_false", dest="data_sharding")),
+        ("--head-lr-mult", dict(type=float, default=1.0)),
+        ("--vision-pretraining", dict(action="store_true")),
+        ("--vision-pretraining-type", dict(type=str, default="classify", choices=["classify", "inpaint", "dino"])),
+        ("--vision-backbone-type", dict(type=str, default="vit", choices=["vit", "mit", "swin"])),
+        ("--swin-backbone-type", dict(type=str, default="tiny", choices=["tiny", "base", "h3"])),
+        ("--mask-type", dict(type=str, default="random", choices=["random", "row"])),
+        ("--mask-factor", dict(type=float, default=1.0)),
+        ("--iter-per-epoch", dict(type=int, default=1250)),
+        ("--dino-local-img-size", dict(type=int, default=96)),
+        ("--dino-local-crops-number", dict(type=int, default=10)),
+        ("--dino-head-hidden-size", dict(type=int, default=2048)),
+        ("--dino-bottleneck-size", dict(type=int, default=256)),
+        ("--dino-freeze-last-layer", dict(type=float, default=1)),
+        ("--dino-norm-last-layer", dict(action="store_true")),
+        ("--dino-warmup-teacher-temp", dict(type=float, default=0.04)),
+        ("--dino-teacher-temp", dict(type=float, default=0.07)),
+        ("--dino-warmup-teacher-temp-epochs", dict(type=int, default=30)),
+    ],
 }
+
+# groups whose flags are parsed but drive nothing here (see the comment above)
+IGNORED_GROUPS = tuple(t for t in _GROUPS if t.endswith("(accepted, ignored)"))
+
+
+def ignored_flags_set(args) -> list:
+    """The accepted-but-ignored flags (IGNORED_GROUPS) whose value differs from the default."""
+    out = []
+    for title in IGNORED_GROUPS:
+        for flag, kw in _GROUPS[title]:
+            dest = kw.get("dest", flag.lstrip("-").replace("-", "_"))
+            if kw.get("action") == "store_true":
+                default = kw.get("default", False)
+            elif kw.get("action") == "store_false":
+                default = True
+            else:
+                default = kw.get("default")
+            if hasattr(args, dest) and getattr(args, dest) != default:
+                out.append(flag)
+    return out
 
 
 def build_parser(extra_args_provider=None) -> argparse.ArgumentParser:
@@ -277,6 +364,11 @@ def parse_args(extra_args_provider=None, ignore_unknown_args=False, argv=None):
 
 def validate_args(args, defaults=None):
     defaults = defaults or {}
+    ignored = ignored_flags_set(args)
+    if ignored and int(getattr(args, "rank", 0) or 0) == 0:
+        import warnings
+        warnings.warn("accepted but ignored (task families this framework does not train: vision, "
+                      "biencoder / ICT, Retro, inference): " + " ".join(ignored), stacklevel=2)
     args.tensor_model_parallel_size = min(args.tensor_model_parallel_size, args.world_size)
     assert args.world_size % args.tensor_model_parallel_size == 0, "world size not divisible by TP"
     args.pipeline_model_parallel_size = min(args.pipeline_model_parallel_size,

@@ -90,6 +90,57 @@ def test_nb3_hyperparameters_parse_and_derive(monkeypatch):
     assert (cfg.num_layers, cfg.hidden_size, cfg.num_attention_heads) == (12, 768, 12)
 
 
+def test_every_reference_megatron_flag_parses(monkeypatch):
+    """All 230 flag names of the reference's arguments.py (fixture tests/fixtures/
+    megatron_reference_flags.json) parse in ONE command line; the task families this framework
+    does not train (vision, biencoder / ICT, Retro, inference) are accepted, reported by
+    ``ignored_flags_set`` and warned about by ``validate_args``."""
+    import json
+    import warnings
+    from smdt_amd.train import arguments as A
+    flags = json.load(open(os.path.join(REPO, "tests", "fixtures", "megatron_reference_flags.json")))["flags"]
+    assert len(flags) == 230
+    p = A.build_parser()
+    by_flag = {o: a for a in p._actions for o in a.option_strings}
+    skip = {"--batch-size", "--warmup", "--model-parallel-size", "--checkpoint-activations"}  # rejected later
+    argv = []
+    for f in flags:
+        a = by_flag[f]                    # KeyError = a reference flag this parser does not know
+        if f in skip:
+            continue
+        if a.nargs == 0:
+            argv.append(f)
+            continue
+        if a.choices:
+            v = str(list(a.choices)[0])
+        elif a.type is int:
+            v = "2"
+        elif a.type is float:
+            v = "0.5"
+        elif a.type is A.str_bool:
+            v = "true"
+        else:
+            v = "x"
+        argv += [f, v]
+    args = p.parse_args(argv)
+    assert args.num_classes == 2 and args.dino_teacher_temp == 0.5 and args.retro_add_retriever is True
+    assert args.data_sharding is False and args.retriever_report_topk_accuracies == [2]
+    ign = A.ignored_flags_set(args)
+    assert "--num-classes" in ign and "--retro-workdir" in ign and "--max-tokens-to-oom" in ign
+    # defaults only: nothing to report; a non-default ignored flag warns in validate_args
+    monkeypatch.setenv("WORLD_SIZE", "1")
+    monkeypatch.setenv("RANK", "0")
+    base = ["--num-layers", "2", "--hidden-size", "64", "--num-attention-heads", "4", "--seq-length", "32",
+            "--max-position-embeddings", "32", "--micro-batch-size", "2"]
+    assert A.ignored_flags_set(A.parse_args(argv=base)) == []
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        A.validate_args(A.parse_args(argv=base + ["--img-h", "128", "--vision-pretraining"]),
+                        {"tokenizer_type": "GPT2BPETokenizer"})
+    msg = " ".join(str(x.message) for x in w)
+    assert "--img-h" in msg and "--vision-pretraining" in msg
+
+
 @pytest.mark.slow
 @pytest.mark.parametrize("async_save", [False, True])
 def test_pretrain_gpt_checkpoint_and_resume(tmp_path, async_save):

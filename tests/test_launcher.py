@@ -74,3 +74,32 @@ def test_mnist_ddp_gloo_world2_through_estimator(tmp_path):
         t.extractall(tmp_path / "model")
     sd = torch.load(next((tmp_path / "model").rglob("mnist_cnn.pt")), weights_only=True)
     assert "module.conv1.weight" in sd
+
+
+@pytest.mark.parametrize("reqs,ok", [("albumentations\nnumpy>=1.20  # comment\n", True),
+                                     ("numpy\ndefinitely-not-a-module-xyz==1.0\n", False)])
+def test_source_dir_requirements_txt(tmp_path, reqs, ok):
+    """E6: a source_dir with requirements.txt logs the toolkit's "Installing dependencies from
+    requirements.txt" line; offline, each requirement must be importable or provided in-tree
+    (albumentations -> the GPU augmentation), else the job fails before the entry point runs,
+    naming the missing module (reference 2_training_oxford-pet_ddp/requirements.txt:1)."""
+    from smdt_amd.launch import LocalSession, PyTorch
+    src = tmp_path / "src"
+    src.mkdir()
+    (src / "requirements.txt").write_text(reqs)
+    (src / "train.py").write_text("print('ENTRY POINT RAN')\n")
+    sess = LocalSession(root=str(tmp_path / "jobs"))
+    est = PyTorch(entry_point="train.py", source_dir=str(src), role="r", framework_version="2.0.0",
+                  py_version="py310", instance_count=1, instance_type="local", sagemaker_session=sess)
+    try:
+        est.fit(job_name="reqs")
+    except Exception as e:          # a failed job may raise from fit(); the log is what counts
+        assert not ok, e
+    log = open(os.path.join(sess.job_dir("reqs"), "logs", "job.log")).read()
+    assert "Installing dependencies from requirements.txt" in log
+    if ok:
+        assert "albumentations: provided in-tree" in log and "ENTRY POINT RAN" in log
+    else:
+        assert "definitely_not_a_module_xyz" in log and "ENTRY POINT RAN" not in log
+        status = json.load(open(os.path.join(sess.job_dir("reqs"), "status.json")))
+        assert status["state"] == "Failed"
