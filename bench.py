@@ -54,6 +54,7 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 from smdt_amd.comm import init_distributed, relay  # noqa: E402
 from smdt_amd.comm import streams as comm_streams  # noqa: E402
+from smdt_amd.comm.loopback import link_standin  # noqa: E402
 from smdt_amd.models.gpt import GPTModel, allreduce_word_embedding_grads, gpt_flops_per_token, pad_vocab_size  # noqa: E402
 from smdt_amd.models.transformer import TransformerConfig  # noqa: E402
 from smdt_amd.optim.optimizer import MixedPrecisionAdam  # noqa: E402
@@ -504,7 +505,11 @@ def main():
                        "comm_stream_priority": comm_streams.describe()["comm_stream_priority"],
                        "optimizer_overlap": bool(getattr(ddp, "overlap_optimizer", False)),
                        "mlp_gelu_fusion": _mlp_fusion_desc(),
-                       "hip_graph": graph_note},
+                       "hip_graph": graph_note,
+                       **({"link_standin": {"GBps": link_standin()[0], "workgroups": link_standin()[1],
+                                            "exchanges_per_step": _split_stats().get("standin_exchanges", 0)}}
+                          if emulated and link_standin() else {}),
+                       **({"sp_subbatch": 2} if _subbatch_on() else {})},
             **({} if emulated else {
                 "model_tflops_per_gpu": round(tps * fpt / n / 1e12, 2),
                 "baseline": "41 model-TFLOP/s/GPU (reference GPT-2-small, 16xA100, BASELINE.md) at equal model FLOPs"}),
@@ -524,6 +529,16 @@ def main():
         print(json.dumps(rec), flush=True)
     if dist.is_initialized():
         dist.destroy_process_group()
+
+
+def _split_stats():
+    from smdt_amd.parallel import tensor_parallel as _tp
+    return _tp.SPLIT_STATS
+
+
+def _subbatch_on():
+    from smdt_amd.models import transformer as _T
+    return _T._SUBBATCH == 2
 
 
 def probe_fbw(a, ddp, forward_step, it, dev):

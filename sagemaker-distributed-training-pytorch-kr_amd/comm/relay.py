@@ -181,11 +181,17 @@ class XgmiRelay(IpcEngine):
         fs, fr = send.view(-1), recv.view(-1)
         n = fs.numel()
         step = max(16 // es, per // (16 // es) * (16 // es))
+        # device epochs: call i of this exchange runs at (this rank's device call counter) + i, and
+        # one bump after the calls advances the counter — identical on both partners, and correct
+        # when a HIP graph replays a captured exchange (no host value is baked into the launches)
+        i = 0
         for lo in range(0, n, step):
             hi = min(n, lo + step)
-            self.epoch += 1
+            i += 1
             self.C.xgmi_relay(fs[lo:hi], fr[lo:hi], self.stage_ptrs, self.sig_ptrs, self.partners, self.rank, 1,
-                              self.slot, self.sub, self.epoch)
+                              self.slot, self.sub, i, True)
+        self.C.relay_epoch_bump(self.sig_ptrs, self.rank, 1, i)
+        self.epoch += i
         self.calls += 1
         return True
 
@@ -281,9 +287,17 @@ class XgmiRelayLoopback:
         self.stage_ptrs = [self.C.ipc_malloc(world * 2 * self.slot, False) for _ in range(world)]
         self.sig_ptrs = [self.C.ipc_malloc(self.C.relay_signal_bytes(), True) for _ in range(world)]
 
-    def exchange(self, x: torch.Tensor, out: Optional[torch.Tensor] = None, epoch: Optional[int] = None):
-        """x: [world, n] (row r = virtual rank r's message). Returns [world, n]: row r = row r^1 of x."""
+    def exchange(self, x: torch.Tensor, out: Optional[torch.Tensor] = None, epoch: Optional[int] = None,
+                 device_epoch: bool = False):
+        """x: [world, n] (row r = virtual rank r's message). Returns [world, n]: row r = row r^1 of x.
+        ``device_epoch``: the engine's mode — the epoch comes from each virtual rank's device call
+        counter, advanced by one bump after the call (graph-replayable)."""
         out = torch.empty_like(x) if out is None else out
+        if device_epoch:
+            self.C.xgmi_relay(x, out, self.stage_ptrs, self.sig_ptrs, self.partners, 0, self.world, self.slot,
+                              self.sub, 1, True)
+            self.C.relay_epoch_bump(self.sig_ptrs, 0, self.world, 1)
+            return out
         self.epoch = self.epoch + 1 if epoch is None else epoch
         self.C.xgmi_relay(x, out, self.stage_ptrs, self.sig_ptrs, self.partners, 0, self.world, self.slot, self.sub,
                           self.epoch)

@@ -392,6 +392,18 @@ Tensor transpose2d(Tensor x) {
   return out;
 }
 
+// ------------------------------------------------------------------ paced link stand-in
+// recv <- send on `blocks` workgroups, held until `ns` have passed (comm/loopback.py)
+void paced_copy(Tensor recv, Tensor send, int64_t blocks, int64_t ns) {
+  need_contig(recv, "recv");
+  need_contig(send, "send");
+  TORCH_CHECK(recv.is_cuda() && send.is_cuda(), "paced_copy: CUDA tensors");
+  const int64_t nb = send.numel() * send.element_size();
+  TORCH_CHECK(nb == recv.numel() * recv.element_size() && nb % 16 == 0, "paced_copy: equal sizes, multiple of 16 B");
+  TORCH_CHECK((uintptr_t)send.data_ptr() % 16 == 0 && (uintptr_t)recv.data_ptr() % 16 == 0, "paced_copy: 16-B aligned");
+  check(smdt_paced_copy(send.data_ptr(), recv.data_ptr(), nb, (int)blocks, ns, cur_stream()), "paced_copy");
+}
+
 // ------------------------------------------------------------------ RoPE
 // x: [ntok, nh, d] strided view (last dim contiguous), rotary applied in place to the first
 // `rot` elements of each head.
@@ -797,7 +809,7 @@ int64_t relay_read_error(int64_t sig) {
 // partner. Loopback (nranks_local > 1): in / out are [nranks_local, m] rows, one per virtual rank.
 void xgmi_relay(Tensor in, Tensor out, std::vector<int64_t> stage_ptrs, std::vector<int64_t> sig_ptrs,
                 std::vector<int64_t> partners, int64_t rank, int64_t nranks_local, int64_t slot_bytes, int64_t sub,
-                int64_t epoch) {
+                int64_t epoch, bool dev_epoch) {
   TORCH_CHECK(in.dtype() == out.dtype() && in.device() == out.device(), "xgmi_relay: in / out mismatch");
   TORCH_CHECK(in.is_cuda() && in.device().index() == c10::hip::current_device(),
               "xgmi_relay: tensors must live on the current device");
@@ -829,8 +841,18 @@ void xgmi_relay(Tensor in, Tensor out, std::vector<int64_t> stage_ptrs, std::vec
     p[r] = (int)partners[r];
   }
   check(smdt_xgmi_relay(dcode(in), in.data_ptr(), out.data_ptr(), in_rs, out_rs, n, d.data(), s.data(), p.data(), world,
-                        (int)rank, (int)nranks_local, slot_bytes, (int)sub, (uint32_t)epoch, cur_stream()),
+                        (int)rank, (int)nranks_local, slot_bytes, (int)sub, (uint32_t)epoch, dev_epoch ? 1 : 0,
+                        cur_stream()),
         "xgmi_relay");
+}
+
+// Device epochs (xgmi_relay.hip): advance the local ranks' call counters by n on the current stream.
+void relay_epoch_bump(std::vector<int64_t> sig_ptrs, int64_t rank, int64_t nranks_local, int64_t n) {
+  std::vector<void*> s(sig_ptrs.size());
+  for (size_t r = 0; r < sig_ptrs.size(); ++r) s[r] = vp(sig_ptrs[r]);
+  TORCH_CHECK(n >= 1 && n <= 0xffffll, "relay_epoch_bump: n out of range");
+  check(smdt_relay_epoch_bump(s.data(), (int)s.size(), (int)rank, (int)nranks_local, (uint32_t)n, cur_stream()),
+        "relay_epoch_bump");
 }
 
 }  // namespace
@@ -862,6 +884,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("cast_", &cast_);
   m.def("rope_", &rope_);
   m.def("transpose2d", &transpose2d);
+  m.def("paced_copy", &paced_copy);
   m.def("gather_rows", &gather_rows);
   m.def("aug_depthwise", &aug_depthwise);
   m.def("aug_median3", &aug_median3);
@@ -901,7 +924,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("n"), py::arg("slice_stride"), py::arg("scale") = 1.0);
   m.def("xgmi_relay", &xgmi_relay, py::arg("input"), py::arg("out"), py::arg("stage_ptrs"), py::arg("sig_ptrs"),
         py::arg("partners"), py::arg("rank"), py::arg("nranks_local"), py::arg("slot_bytes"), py::arg("sub"),
-        py::arg("epoch"));
+        py::arg("epoch"), py::arg("dev_epoch") = false);
+  m.def("relay_epoch_bump", &relay_epoch_bump, py::arg("sig_ptrs"), py::arg("rank"), py::arg("nranks_local"),
+        py::arg("n"));
   m.def("relay_signal_bytes", &smdt_relay_signal_bytes);
   m.def("relay_read_error", &relay_read_error);
   m.def("flash_bwd", &flash_bwd, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("o"), py::arg("dout"),

@@ -74,6 +74,8 @@ hipError_t smdt_rope(int dtype, void* x, int64_t ntok, int nh, int64_t tok_strid
 
 // transpose.hip
 hipError_t smdt_transpose16(const void* in, void* out, int64_t R, int64_t C, hipStream_t st);
+// link_standin.hip: paced copy standing in for a TP-pair exchange in single-GPU rank emulation
+hipError_t smdt_paced_copy(const void* src, void* dst, int64_t nbytes, int blocks, int64_t ns, hipStream_t st);
 // dst[r] = map[r] >= 0 ? src[map[r]] : 0 (rows of row_bytes, a multiple of 16)
 hipError_t smdt_gather_rows(const void* src, const int64_t* map, void* dst, int64_t nrows, int64_t nsrc,
                             int64_t row_bytes, hipStream_t st);
@@ -175,6 +177,10 @@ hipError_t smdt_relay_read_error(void* sig, int* err);
 int64_t smdt_relay_word_offset(int which);
 hipError_t smdt_xgmi_relay(int dtype, const void* in, void* out, int64_t in_rank_stride, int64_t out_rank_stride,
                            int64_t n, void* const* stage_ptrs, void* const* sig_ptrs, const int* partners, int world,
-                           int rank, int nranks_local, int64_t slot_bytes, int sub, uint32_t epoch, hipStream_t st);
+                           int rank, int nranks_local, int64_t slot_bytes, int sub, uint32_t epoch, int dev_epoch,
+                           hipStream_t st);
+// device epochs: advance the call counter of local ranks [rank, rank + nranks_local) by n
+hipError_t smdt_relay_epoch_bump(void* const* sig_ptrs, int world, int rank, int nranks_local, uint32_t n,
+                                 hipStream_t st);
 
 }  // extern "C"

@@ -12,7 +12,11 @@
 // a message: ~4x the one-link rate (7x for a lone pair). The reference has nothing like it: its TP
 // collectives are stock NCCL rings.
 //
-// Protocol (per call, epoch e = host call counter, identical on both partners; parity = e & 1):
+// Protocol (per call, epoch e identical on both partners; parity = e & 1). e is either a host call
+// counter passed by value, or (device epochs, the engine's mode) this rank's device-side call
+// counter `epoch` of its signal buffer plus the call's index inside the exchange: the counter is
+// advanced by smdt_relay_epoch_bump after the exchange's calls, so a HIP graph that captured an
+// exchange replays it with fresh epochs instead of the epochs frozen at capture.
 //   send block (part j, sub-block q): wait until the partner freed this (j, q, parity) slot two
 //     calls ago (freed >= e - 2), copy its sub-range into host(j)'s slot with sc0|sc1 stores, drain
 //     (vmcnt 0), barrier, publish ready[j][q] = e in the PARTNER's signal buffer.
@@ -47,7 +51,8 @@ struct SignalBuf {
   uint32_t freed[kMaxRanks][kMaxSub];  // written by my partner's recv blocks
   uint32_t error;                        // != 0: a spin timed out (sticky)
   uint32_t spin_limit;                   // polls before giving up (0: kSpinLimit); set by the host
-  uint32_t pad[2];
+  uint32_t epoch;                        // device epochs: calls completed (smdt_relay_epoch_bump)
+  uint32_t pad;
 };
 
 struct Peers {
@@ -63,7 +68,8 @@ struct Args {
   int64_t nvec;                             // 16-byte vectors of this call's message
   int64_t part;                             // vectors per part
   int64_t slot;                             // vectors per (flow, parity) slot (>= 2 * part)
-  uint32_t epoch;
+  uint32_t epoch;   // host mode: the call's epoch; device mode: its index (>= 1) within the exchange
+  int dev_epoch;    // 1: e = own signal buffer's counter + epoch
   int sub;
 };
 
@@ -110,7 +116,7 @@ __global__ __launch_bounds__(kThreads) void relay_kernel(Peers P, int rank0, Arg
   const int64_t p0 = min((int64_t)j * a.part, a.nvec), p1 = min(p0 + a.part, a.nvec);
   const int64_t chunk = (a.part + nsub - 1) / nsub;
   const int64_t v0 = min(p0 + (int64_t)q * chunk, p1), v1 = min(v0 + chunk, p1);
-  const uint32_t e = a.epoch;
+  const uint32_t e = (a.dev_epoch ? load_sys(&me->epoch) : 0u) + a.epoch;
   const int64_t par = e & 1u;
   if (threadIdx.x == 0) s_ok = load_sys(&me->error) == 0u;
   __syncthreads();
@@ -175,6 +181,13 @@ __global__ __launch_bounds__(kThreads) void relay_kernel(Peers P, int rank0, Arg
   if (threadIdx.x == 0) store_sys(&P.sig[src]->freed[j][q], e);
 }
 
+// Device epochs: advance the call counter of each local rank's signal buffer by n (the calls of the
+// exchange just issued). One vector atomic per rank: never a scalar-memory write.
+__global__ void epoch_bump_kernel(Peers P, int rank0, int nlocal, uint32_t n) {
+  const int t = (int)threadIdx.x;
+  if (t < nlocal) __hip_atomic_fetch_add(&P.sig[rank0 + t]->epoch, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 template <typename T>
 hipError_t launch_t(int world, const Peers& P, int rank0, int nranks_local, const Args& a, hipStream_t st) {
   const dim3 grid(2 * world * a.sub, nranks_local);
@@ -196,7 +209,22 @@ extern "C" {
 
 int64_t smdt_relay_signal_bytes() { return (int64_t)sizeof(relay::SignalBuf); }
 int64_t smdt_relay_word_offset(int which) {
-  return which == 0 ? (int64_t)offsetof(relay::SignalBuf, error) : (int64_t)offsetof(relay::SignalBuf, spin_limit);
+  return which == 0   ? (int64_t)offsetof(relay::SignalBuf, error)
+         : which == 1 ? (int64_t)offsetof(relay::SignalBuf, spin_limit)
+                      : (int64_t)offsetof(relay::SignalBuf, epoch);
+}
+
+hipError_t smdt_relay_epoch_bump(void* const* sig_ptrs, int world, int rank, int nranks_local, uint32_t n,
+                                 hipStream_t st) {
+  if (world < 1 || world > relay::kMaxRanks || rank < 0 || nranks_local < 1 || rank + nranks_local > world)
+    return hipErrorInvalidValue;
+  relay::Peers P{};
+  for (int r = 0; r < world; ++r) {
+    if (!sig_ptrs[r]) return hipErrorInvalidValue;
+    P.sig[r] = (relay::SignalBuf*)sig_ptrs[r];
+  }
+  hipLaunchKernelGGL(relay::epoch_bump_kernel, dim3(1), dim3(64), 0, st, P, rank, nranks_local, n);
+  return hipGetLastError();
 }
 int smdt_relay_max_sub() { return relay::kMaxSub; }
 
@@ -209,7 +237,8 @@ hipError_t smdt_relay_read_error(void* sig, int* err) {
 
 hipError_t smdt_xgmi_relay(int dtype, const void* in, void* out, int64_t in_rank_stride, int64_t out_rank_stride,
                            int64_t n, void* const* stage_ptrs, void* const* sig_ptrs, const int* partners, int world,
-                           int rank, int nranks_local, int64_t slot_bytes, int sub, uint32_t epoch, hipStream_t st) {
+                           int rank, int nranks_local, int64_t slot_bytes, int sub, uint32_t epoch, int dev_epoch,
+                           hipStream_t st) {
   if (world != 2 && world != 4 && world != 8) return hipErrorInvalidValue;
   if (rank < 0 || nranks_local < 1 || rank + nranks_local > world || sub < 1 || sub > relay::kMaxSub || epoch == 0)
     return hipErrorInvalidValue;
@@ -237,6 +266,7 @@ hipError_t smdt_xgmi_relay(int dtype, const void* in, void* out, int64_t in_rank
   a.in_rank_stride = in_rank_stride * esz / 16;
   a.out_rank_stride = out_rank_stride * esz / 16;
   a.epoch = epoch;
+  a.dev_epoch = dev_epoch ? 1 : 0;
   a.sub = sub;
   switch (dtype) {
     case 0: return relay::launch_t<float>(world, P, rank, nranks_local, a, st);

@@ -1203,6 +1203,15 @@ def _exchange(send, recv, nxt, prv, group):
         # SLOWER: 202.4 -> 219.7 ms per stage-1 rank, the per-exchange stream hand-offs cost more
         # than the overlap gains; profiles/r4_loopback_ring_async_neg/). SMDT_LOOPBACK_RING_ASYNC=1
         # re-runs that arm (the side stream is now a high-priority one).
+        standin = _lb.link_standin() if send.is_cuda else None
+        if standin is not None:
+            # paced link stand-in (SMDT_LINK_STANDIN): the modelled link time and the relay's CU
+            # footprint, on the side stream beside the rank's compute, waited for like the relay
+            gbps, blocks = standin
+            ns = int(_nbytes(send) / gbps)          # bytes / (GB/s) = ns
+            C = _ext.ext()
+            SPLIT_STATS["standin_exchanges"] = SPLIT_STATS.get("standin_exchanges", 0) + 1
+            return [group._issue([send, recv], lambda: C.paced_copy(recv, send, blocks, ns), [recv])]
         if _LB_RING_ASYNC and send.is_cuda:
             return [group._issue([send, recv], lambda: recv.copy_(send), [recv])]
         recv.copy_(send)

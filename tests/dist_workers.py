@@ -1468,3 +1468,62 @@ def deferred_add_worker(rank, world, case, guard=True, defer=True):
     stats = dict(TPm.SPLIT_STATS)
     dist.destroy_process_group()
     return out, (seen[0] if seen else None), stats
+
+
+def relay_graph_worker(rank, world, port, outdir):
+    """One rank of the graph-captured relay test: 2 processes on cuda:0 (one TP pair), the relay's
+    exchange captured in a HIP graph and replayed 20 times with fresh inputs, interleaved with
+    eager exchanges: every result must equal the partner's input bit for bit (device epochs,
+    csrc/kernels/xgmi_relay.hip)."""
+    import os
+    import pickle
+    import traceback
+
+    import torch
+
+    os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "RANK": str(rank),
+                       "WORLD_SIZE": str(world)})
+    res = {"ok": [], "err": None, "error_word": None, "replays": 0}
+    try:
+        import torch.distributed as dist
+        from smdt_amd.comm import relay
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        torch.cuda.set_device(0)
+        pg = dist.new_group(list(range(world)))
+        partner = rank ^ 1
+        eng = relay.XgmiRelay(pg, slot_bytes=1 << 20, sub=2, validate=True)
+        n = 3 * world * (1 << 20) // 2 // 2 + 800            # bf16: 3 relay calls per exchange
+        base = torch.arange(n, device="cuda", dtype=torch.float32) % 251
+
+        def val(r, it):
+            return ((base + 7.0 * r + 3.0 * it) % 509).to(torch.bfloat16)
+        x = torch.empty(n, device="cuda", dtype=torch.bfloat16)
+        y = torch.empty_like(x)
+        for it in range(3):                                # eager: the counter advances
+            x.copy_(val(rank, it))
+            assert eng.exchange(x, y)
+            torch.cuda.synchronize()
+            res["ok"].append(bool(torch.equal(y, val(partner, it))))
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            eng.exchange(x, y)
+        dist.barrier()
+        for it in range(20):
+            x.copy_(val(rank, 100 + it))
+            g.replay()
+            torch.cuda.synchronize()
+            res["ok"].append(bool(torch.equal(y, val(partner, 100 + it))))
+            res["replays"] += 1
+            if it % 5 == 4:                                # eager calls between replays
+                x.copy_(val(rank, 200 + it))
+                eng.exchange(x, y)
+                torch.cuda.synchronize()
+                res["ok"].append(bool(torch.equal(y, val(partner, 200 + it))))
+        res["error_word"] = eng.error()
+        del g
+        eng.close()
+        dist.destroy_process_group()
+    except Exception:
+        res["err"] = traceback.format_exc()
+    with open(os.path.join(outdir, f"r{rank}.pkl"), "wb") as f:
+        pickle.dump(res, f)

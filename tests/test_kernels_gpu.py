@@ -663,3 +663,23 @@ def test_graph_safe_dropout_rng():
         assert not torch.equal(masks[0], masks[1])
     finally:
         SF.disable_graph_rng()
+
+
+def test_paced_copy_copies_and_holds_for_its_link_time():
+    """Link stand-in of the single-GPU rank emulation (csrc/kernels/link_standin.hip): an exact
+    copy that does not finish before its modelled transfer time (and not grossly after it)."""
+    from smdt_amd.ops import _ext
+    C = _ext.ext()
+    send = torch.randn(16 << 20, device="cuda", dtype=torch.bfloat16)      # 32 MB
+    recv = torch.empty_like(send)
+    C.paced_copy(recv, send, 64, 1000)
+    torch.cuda.synchronize()
+    assert torch.equal(recv, send)
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for ns in (200_000, 1_000_000):
+        s.record()
+        C.paced_copy(recv, send, 64, ns)
+        e.record()
+        torch.cuda.synchronize()
+        ms = s.elapsed_time(e)
+        assert ns / 1e6 * 0.98 <= ms <= ns / 1e6 + 0.5, (ns, ms)

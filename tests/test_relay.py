@@ -131,3 +131,37 @@ def test_tensor_parallel_mlp_over_relay_matches_fp32_reference():
         assert res["error_word"] == 0 and res["calls"] >= 8, (r, res)
         bad = {k: v for k, v in res["rel"].items() if not v < 2e-2}
         assert not bad, (r, bad)
+
+
+@pytest.mark.gpu
+def test_relay_exchange_replays_from_a_hip_graph():
+    """2 processes on cuda:0 (one TP pair) capture the relay exchange in a HIP
+    graph and replay it 20x with fresh inputs, eager exchanges in between; every replay equals the
+    partner's input bit for bit. Possible because the relay's epochs are device counters, bumped
+    in-stream, not host values baked into the captured launches."""
+    import torch.multiprocessing as mp
+
+    import dist_workers as W
+    from _dist import free_port
+
+    world = 2
+    port = free_port()
+    with tempfile.TemporaryDirectory() as d:
+        ctx = mp.get_context("spawn")
+        procs = [ctx.Process(target=W.relay_graph_worker, args=(r, world, port, d)) for r in range(world)]
+        for p in procs:
+            p.start()
+        for p in procs:
+            p.join(120)
+        for p in procs:
+            if p.is_alive():
+                p.kill()
+        out = []
+        for r in range(world):
+            path = os.path.join(d, f"r{r}.pkl")
+            assert os.path.exists(path), f"rank {r} wrote no result (exit {procs[r].exitcode})"
+            with open(path, "rb") as f:  # written by this test's own workers
+                out.append(pickle.load(f))
+    for r, res in enumerate(out):
+        assert res["err"] is None, f"rank {r}:\n{res['err']}"
+        assert res["error_word"] == 0 and res["replays"] == 20 and all(res["ok"]) and len(res["ok"]) == 27, (r, res)
