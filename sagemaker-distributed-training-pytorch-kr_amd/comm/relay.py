@@ -167,6 +167,10 @@ class XgmiRelay(IpcEngine):
         return res
 
     # ------------------------------------------------------------------ API
+    def cu_blocks(self) -> int:
+        """Workgroups the relay kernel keeps resident during an exchange (one CU each)."""
+        return 2 * self.world * self.sub
+
     def fits(self, send, recv) -> bool:
         return (self.active and eligible(send, recv)
                 and send.numel() * send.element_size() >= (self.min_bytes or 0))

@@ -92,8 +92,39 @@ def _reduce_scatter_dim0(x, group, async_op=False):
     return out, h
 
 
+# CUs held by in-flight exchanges (id(work) -> workgroups): the relay engine's kernel (and its
+# paced single-GPU stand-in) keeps 2 x world x sub workgroups resident for the whole transfer, one
+# per CU (a GEMM workgroup fills a CU's register file, so neither can share a CU). A persistent
+# GEMM launched beside it with one workgroup per CU (gemm_tn) would leave that many of its
+# workgroups waiting for the transfer to end — or, launched first, keep the transfer from starting
+# until the GEMM's tail: measured with the paced stand-in as ~every exchange fully exposed
+# (profiles/r6_standin/). Chunk GEMMs issued while an exchange is in flight size their grid to
+# the CUs left over (``gemm_tn_blocks``). SMDT_EXCHANGE_CU_RESERVE=0 turns this off.
+_CU_HELD = {}
+_CU_RESERVE_ON = os.environ.get("SMDT_EXCHANGE_CU_RESERVE", "1") == "1"
+_NUM_CUS = []
+
+
+def _hold_cus(works, blocks):
+    if _CU_RESERVE_ON and blocks > 0:
+        for w in works:
+            _CU_HELD[id(w)] = int(blocks)
+
+
+def gemm_tn_blocks() -> int:
+    """max_blocks for a persistent gemm_tn launch now: 0 (every CU) unless exchanges in flight hold
+    CUs, then the CUs they leave."""
+    if not _CU_HELD:
+        return 0
+    if not _NUM_CUS:
+        _NUM_CUS.append(torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count)
+    return max(_NUM_CUS[0] - sum(_CU_HELD.values()), _NUM_CUS[0] // 2)
+
+
 def _wait_works(works, group):
     """Wait (on the current stream) for in-flight works of ``group``'s collectives."""
+    for w in works:
+        _CU_HELD.pop(id(w), None)
     if not _cs._ON:
         for w in works:
             w.wait()
@@ -887,7 +918,7 @@ class SPFusedGeLUMLP(torch.autograd.Function):
         def fc1_chunk(lo, ch):
             m = ch.shape[0]
             C.gemm_tn(ch.reshape(-1, ch.shape[-1]), w1, 2, b1, pre[lo:lo + m].view(-1, f),
-                      act[lo:lo + m].view(-1, f))
+                      act[lo:lo + m].view(-1, f), gemm_tn_blocks())
         total = ag_ring(x, group, fc1_chunk)
         y = rs_ring(lambda lo, m, o: _linear_into(act[lo:lo + m], w2, o), group, lead + (w2.shape[0],), act)
         ctx.save_for_backward(total, w1, w2, pre, act)
@@ -911,8 +942,8 @@ class SPFusedGeLUMLP(torch.autograd.Function):
 
         def fc2_dgrad_chunk(lo, ch):
             m = ch.shape[0]
-            C.gemm_tn(ch.reshape(-1, ch.shape[-1]), w2t, 3, bd, dz[lo:lo + m].view(-1, f), None, 0, 0,
-                      pre[lo:lo + m].view(-1, f))
+            C.gemm_tn(ch.reshape(-1, ch.shape[-1]), w2t, 3, bd, dz[lo:lo + m].view(-1, f), None,
+                      gemm_tn_blocks(), 0, pre[lo:lo + m].view(-1, f))
         gfull = ag_ring(dy, group, fc2_dgrad_chunk, before_last_wait=_flush_wgrad, bulk=ctx.bulk)
         dw2 = _wgrad(w2, gfull.reshape(-1, gfull.shape[-1]), act.reshape(-1, f))
         res = {}
@@ -1211,7 +1242,9 @@ def _exchange(send, recv, nxt, prv, group):
             ns = int(_nbytes(send) / gbps)          # bytes / (GB/s) = ns
             C = _ext.ext()
             SPLIT_STATS["standin_exchanges"] = SPLIT_STATS.get("standin_exchanges", 0) + 1
-            return [group._issue([send, recv], lambda: C.paced_copy(recv, send, blocks, ns), [recv])]
+            works = [group._issue([send, recv], lambda: C.paced_copy(recv, send, blocks, ns), [recv])]
+            _hold_cus(works, blocks)
+            return works
         if _LB_RING_ASYNC and send.is_cuda:
             return [group._issue([send, recv], lambda: recv.copy_(send), [recv])]
         recv.copy_(send)
@@ -1222,6 +1255,7 @@ def _exchange(send, recv, nxt, prv, group):
             h = eng.exchange_async(send, recv)
             if h is not None:
                 _cs.collective("p2p", group, _nbytes(send), transport="relay", events=h.timing())
+                _hold_cus([h], eng.cu_blocks())
                 return [h]
     if send.is_cuda and dist.get_backend(group) == "gloo":
         # Gloo rehearsals with CUDA tensors (several ranks on one GPU, SMDT_BENCH_BACKEND=gloo):
@@ -1243,6 +1277,8 @@ def _exchange(send, recv, nxt, prv, group):
 
 def _linear_into(x, w, out=None):
     """x W^T into ``out`` (returned) when given, else a new tensor (``rs_ring`` partials)."""
+    if out is None and _RING_GEMM_TN and _CU_HELD and x.is_cuda:
+        out = x.new_empty(tuple(x.shape[:-1]) + (w.shape[0],))
     if out is None:
         return torch.nn.functional.linear(x, w)
     _mm_into(out, x, w)
@@ -1257,10 +1293,20 @@ def _dgrad_rows(g, weight, wt, out=None):
     return out
 
 
+# SMDT_RING_GEMM_TN=1: ring-chunk GEMMs issued while an exchange holds CUs run on gemm_tn with
+# the leftover grid (gemm_tn_blocks) instead of hipBLASLt, whose full-chip grid races the exchange
+_RING_GEMM_TN = os.environ.get("SMDT_RING_GEMM_TN", "0") == "1"
+
+
 def _mm_into(dst, a, w, bias=None):
     """dst[..., o] = a[..., k] @ w[o, k]^T (+ bias) written in place (hipBLASLt out= GEMM)."""
     a2 = a.reshape(-1, a.shape[-1])
     d2 = dst.view(-1, dst.shape[-1])
+    if _RING_GEMM_TN and _CU_HELD and a2.is_cuda and a2.is_contiguous() and d2.is_contiguous() \
+            and a2.dtype in (torch.bfloat16, torch.float16) and w.dtype == a2.dtype \
+            and (bias is None or bias.dtype == a2.dtype) and _ext.ext().gemm_tn_supported(a2, w):
+        _ext.ext().gemm_tn(a2, w, 1 if bias is not None else 0, bias, d2, None, gemm_tn_blocks())
+        return
     if bias is not None:
         torch.addmm(bias, a2, w.t(), out=d2)
     else:
@@ -1487,6 +1533,7 @@ def end_subbatch():
         for w in works:
             w.wait()
     _AG_PENDING.clear()
+    _CU_HELD.clear()
 
 
 def ag_ring(x, group, chunk_fn=None, before_last_wait=None, _skip_direct=False, bulk=False):
