@@ -490,7 +490,7 @@ bool wgrad_mfma(Tensor main_grad, Tensor dy, Tensor x, int64_t max_splits) {
 // overwrite (optional, per problem): the main_grad holds no data yet (a lazily zeroed gradient
 // buffer): the kernel stores dy^T x instead of adding it (no read of the target).
 bool wgrad_grouped(std::vector<Tensor> main_grads, std::vector<Tensor> dys, std::vector<Tensor> xs,
-                   std::vector<Tensor> biases, std::vector<bool> overwrite) {
+                   std::vector<Tensor> biases, std::vector<bool> overwrite, int64_t cus) {
   const size_t n = main_grads.size();
   TORCH_CHECK(dys.size() == n && xs.size() == n, "wgrad_grouped: list lengths differ");
   TORCH_CHECK(biases.empty() || biases.size() == n, "wgrad_grouped: biases list length");
@@ -518,7 +518,7 @@ bool wgrad_grouped(std::vector<Tensor> main_grads, std::vector<Tensor> dys, std:
                                 (!overwrite.empty() && overwrite[i]) ? 1 : 0};
   }
   if (n == 0) return true;
-  check(smdt_wgrad_grouped_t(dcode(dys[0]), probs.data(), (int)n, cur_stream()), "wgrad_grouped");
+  check(smdt_wgrad_grouped_cus(dcode(dys[0]), probs.data(), (int)n, (int)cus, cur_stream()), "wgrad_grouped");
   return true;
 }
 
@@ -895,7 +895,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         arg("var") = 0, arg("aux") = pybind11::none());
   m.def("wgrad_mfma", &wgrad_mfma, arg("main_grad"), arg("dy"), arg("x"), arg("max_splits") = 0);
   m.def("wgrad_grouped", &wgrad_grouped, arg("main_grads"), arg("dys"), arg("xs"),
-        arg("biases") = std::vector<Tensor>{}, arg("overwrite") = std::vector<bool>{});
+        arg("biases") = std::vector<Tensor>{}, arg("overwrite") = std::vector<bool>{}, arg("cus") = 0);
   m.def("ce_stats", &ce_stats);
   m.def("set_rng_step", &set_rng_step);
   m.def("adam_capturable", &adam_capturable);

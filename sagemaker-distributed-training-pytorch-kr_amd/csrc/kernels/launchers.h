@@ -139,6 +139,8 @@ struct SmdtWgradProblem {
 // main_grad targets of one call must not overlap.
 hipError_t smdt_wgrad_grouped(const SmdtWgradProblem* probs, int n, hipStream_t st);
 hipError_t smdt_wgrad_grouped_t(int dtype, const SmdtWgradProblem* probs, int n, hipStream_t st);
+// the same with the tail split sized for `cus` concurrently usable CUs (0: 256, the whole chip)
+hipError_t smdt_wgrad_grouped_cus(int dtype, const SmdtWgradProblem* probs, int n, int cus, hipStream_t st);
 
 // xgmi_allreduce.hip: single-node all-reduce over HIP-IPC-mapped peer buffers.
 int smdt_ar_max_ranks();

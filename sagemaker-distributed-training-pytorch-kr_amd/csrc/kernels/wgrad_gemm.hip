@@ -436,7 +436,16 @@ extern "C" hipError_t smdt_wgrad_grouped(const SmdtWgradProblem* probs, int n, h
 }
 
 extern "C" hipError_t smdt_wgrad_grouped_t(int dtype, const SmdtWgradProblem* probs, int n, hipStream_t st) {
+  return smdt_wgrad_grouped_cus(dtype, probs, n, 0, st);
+}
+
+// `cus`: the CUs this launch can use at once (0 = 256). A launch beside a transfer that holds CUs
+// (a filler in a TP exchange wait, parallel/tensor_parallel.DeferredWgrad.fill_one) sizes its
+// rounds and its tail split to what is left, so no tail piece waits for the transfer to end.
+extern "C" hipError_t smdt_wgrad_grouped_cus(int dtype, const SmdtWgradProblem* probs, int n, int cus,
+                                             hipStream_t st) {
   if (dtype != 1 && dtype != 2) return hipErrorInvalidValue;
+  const int R = (cus > 0 && cus < 256) ? cus : 256;
   for (int i = 0; i < n; ++i)
     if (!smdt_wgrad_supported(probs[i].M, probs[i].N, probs[i].K)) return hipErrorInvalidValue;
   for (int base = 0; base < n; base += wg::kMaxGroup) {
@@ -464,12 +473,12 @@ extern "C" hipError_t smdt_wgrad_grouped_t(int dtype, const SmdtWgradProblem* pr
     g.nprob = cnt;
     // Tail split (see wgrad_grouped_kernel): r = tiles mod 256 tail tiles, ~256 / r pieces each
     // of at least 8 stages; off with SMDT_WGRAD_TAIL_SPLIT=0.
-    const int r = tiles % 256;
+    const int r = tiles % R;
     int splits = 1, mps = 0;
     if (r > 0 && wg_tail_split_enabled()) {
       int max_stages = 0;
       for (int i = 0; i < cnt; ++i) max_stages = max_stages > g.p[i].M / wg::BM ? max_stages : g.p[i].M / wg::BM;
-      splits = 256 / r;
+      splits = R / r;
       if (splits > 16) splits = 16;
       if (splits > max_stages / 8) splits = max_stages / 8;
       if (splits > 1) {

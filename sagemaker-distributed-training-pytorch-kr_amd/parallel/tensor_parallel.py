@@ -483,7 +483,92 @@ class DeferredWgrad:
                     cb(p)
 
 
+    @torch.no_grad()
+    def fill_one(self, cus: int = 0) -> bool:
+        """Exchange-wait filler (``fill``): issue the oldest queued, complete and not held item —
+        ONE weight's gradient GEMM — as its own grouped launch sized for ``cus`` CUs (the ones an
+        in-flight TP exchange leaves; its tail split into pieces that fill them), and report its
+        readiness. Returns False when there was nothing to issue."""
+        pick = next((it for it in self.items if it[4] and not it[3]), None)
+        if pick is None:
+            return False
+        self.items = [it for it in self.items if it is not pick]
+        self.by_key.pop(pick[1].data_ptr(), None)
+        weight, mg, segs, _held, _complete, bias, fresh = pick
+        self.tiles -= -(-segs[0][0].shape[1] // 256) * -(-segs[0][1].shape[1] // 256)
+        self.held_bytes -= sum(sg[0].numel() * sg[0].element_size() + sg[1].numel() * sg[1].element_size()
+                               for sg in segs)
+        for g2, t2, vg, vt in segs:
+            if g2._version != vg or t2._version != vt:
+                raise RuntimeError("deferred wgrad: a queued dY / X tensor was modified in place before the "
+                                   "flush; disable with SMDT_DEFER_WGRAD=0 and report the op that did it")
+        bt = bias.main_grad if bias is not None else _NO_BIAS.get(mg.device)
+        for i, (g2, t2, _, _) in enumerate(segs):      # segments in order: round 0 may store
+            ow = bool(fresh) and i == 0
+            if g2.is_cuda:
+                if not _ext.ext().wgrad_grouped([mg], [g2], [t2], [bt], [ow], int(cus)):
+                    raise RuntimeError("deferred wgrad filler: grouped launch refused")
+                continue
+            prod = g2.t().matmul(t2).view_as(mg)       # CPU (tests: allow_cpu)
+            if ow:
+                mg.copy_(prod)
+            else:
+                mg.add_(prod)
+            if bias is not None:
+                bias.main_grad.add_(g2.float().sum(0))
+        self.stats["fills"] = self.stats.get("fills", 0) + 1
+        for p in (weight, bias):
+            cb = getattr(p, "_smdt_grad_ready", None) if p is not None else None
+            if cb is not None:
+                cb(p)
+        return True
+
+    def flush_unheld(self):
+        """Issue every queued item that is not held for a later synchronising pass."""
+        if not any(not it[3] for it in self.items):
+            return
+        held = [it for it in self.items if it[3]]
+        if not held:
+            self.flush()
+            return
+        self.items = [it for it in self.items if not it[3]]
+        self.flush()
+        self.items = held + self.items
+        self.by_key = {it[1].data_ptr(): it for it in self.items}
+        self.tiles = sum(-(-it[2][0][0].shape[1] // 256) * -(-it[2][0][1].shape[1] // 256) for it in self.items)
+        self.held_bytes = sum(sg[0].numel() * sg[0].element_size() + sg[1].numel() * sg[1].element_size()
+                              for it in self.items for sg in it[2])
+
+
 DEFERRED_WGRAD = DeferredWgrad()
+# Exchange-wait fillers (SMDT_W_FILL=1, split-backward pipeline schedules): the W GEMMs of the last
+# backward pass stay queued into the next forward, whose TP-exchange waits each issue one of them
+# (``fill_exchange_wait``) beside the in-flight transfer, on the CUs the transfer leaves; the rest
+# is flushed when that forward ends (train/schedules.py). VERDICT r5 item 1, "split-K W fillers".
+W_FILL = os.environ.get("SMDT_W_FILL", "0") == "1"
+_FILL = {"on": False}
+
+
+def fill_exchange_wait():
+    """Before a forward ring exchange's wait: issue one queued W GEMM beside the transfer."""
+    if _FILL["on"] and not DEFERRED_WGRAD.defer and DEFERRED_WGRAD.items:
+        DEFERRED_WGRAD.fill_one(gemm_tn_blocks())
+
+
+class forward_fill:
+    """Context for one forward pass of a split-backward schedule: exchange waits take W fillers;
+    whatever is left unheld is flushed at the end."""
+
+    def __enter__(self):
+        self.prev = _FILL["on"]
+        _FILL["on"] = W_FILL
+        return self
+
+    def __exit__(self, *exc):
+        _FILL["on"] = self.prev
+        if W_FILL:
+            DEFERRED_WGRAD.flush_unheld()
+        return False
 
 
 class _NoBias(dict):
@@ -1586,6 +1671,7 @@ def ag_ring(x, group, chunk_fn=None, before_last_wait=None, _skip_direct=False, 
         if works is not None:
             if s == ws - 2 and before_last_wait is not None:
                 before_last_wait()
+            fill_exchange_wait()
             _wait_works(works, group)
     return total
 
@@ -1637,6 +1723,7 @@ def rs_ring(partial_fn, group, full_shape, ref, before_last_wait=None, bulk=Fals
         if works is not None:
             if s == ws - 1 and before_last_wait is not None:
                 before_last_wait()
+            fill_exchange_wait()
             _wait_works(works, group)
             if s == ws - 1 and ws == 2 and ((_DEFER_ADD["on"] and before_last_wait is None) or defer_add):
                 # the consuming norm adds it (see _DEFER_ADD)

@@ -61,10 +61,13 @@ def forward_backward_no_pipelining(forward_step_func: Callable, data_iterator, m
     stage time has the schedule's W grouping instead of the opportunistic per-collective flushes
     of a plain backward.
     """
-    from ..parallel.tensor_parallel import DEFERRED_WGRAD, accumulation_window_ok
+    from ..parallel.tensor_parallel import DEFERRED_WGRAD, W_FILL, accumulation_window_ok, forward_fill
     models = model if isinstance(model, list) else [model]
     m = models[0]
     gate = _SyncGate(models)
+    # SMDT_W_FILL: a micro-batch's W stays queued into the next forward, whose TP-exchange waits
+    # issue it piece by piece (parallel/tensor_parallel.fill_exchange_wait)
+    fill = split_backward and W_FILL and not forward_only
     # opt-in (SMDT_WGRAD_MERGE_ACCUM=1): the micro-batches' weight-gradient GEMMs merge per weight
     # and run once, in the last backward (DeferredWgrad.hold): one fp32 main_grad update per
     # iteration; it loses at Megatron's usual micro-batch sizes (profiles/r3_l4l/)
@@ -75,7 +78,11 @@ def forward_backward_no_pipelining(forward_step_func: Callable, data_iterator, m
         gate.set(last)                   # (re-enabling sync does not drain a held window)
         if hold:
             DEFERRED_WGRAD.hold = not last
-        out, loss_func = forward_step_func(data_iterator, m)
+        if fill:
+            with forward_fill():
+                out, loss_func = forward_step_func(data_iterator, m)
+        else:
+            out, loss_func = forward_step_func(data_iterator, m)
         loss, info = loss_func(out)
         losses.append(info)
         if not forward_only:
@@ -86,7 +93,7 @@ def forward_backward_no_pipelining(forward_step_func: Callable, data_iterator, m
             finally:
                 if split_backward:
                     DEFERRED_WGRAD.defer = False
-            if split_backward:
+            if split_backward and (last or not fill):
                 DEFERRED_WGRAD.flush()
     gate.set(True)
     return losses
@@ -304,7 +311,7 @@ def forward_backward_pipelining_without_interleaving(forward_step_func: Callable
                                                      forward_only: bool = False, grad_scale=None, schedule=None, **_):
     """1F1B, optionally with the split (zero-bubble) backward of ``set_pipeline_schedule``.
     ``tensor_shape`` is the [s(/tp), b, h] activation exchanged between stages."""
-    from ..parallel.tensor_parallel import DEFERRED_WGRAD
+    from ..parallel.tensor_parallel import DEFERRED_WGRAD, W_FILL, forward_fill
     models = model if isinstance(model, list) else [model]
     m = models[0]
     _enter_schedule(m)
@@ -325,11 +332,17 @@ def forward_backward_pipelining_without_interleaving(forward_step_func: Callable
     # zbh1 / zbh2: backward passes >= defer_from keep their W queued until after the last B
     concat0 = DEFERRED_WGRAD.concat_segments
 
+    fill = split and W_FILL
+
     def fwd(inp):
         core = m.module if hasattr(m, "module") else m
         inp = _finish_recv(inp)
         core.set_input_tensor(inp)
-        out, loss_func = forward_step_func(data_iterator, m)
+        if fill:
+            with forward_fill():     # the exchange waits issue the queued W of the last pass
+                out, loss_func = forward_step_func(data_iterator, m)
+        else:
+            out, loss_func = forward_step_func(data_iterator, m)
         if last:
             loss, info = loss_func(out)
             losses.append(info)
@@ -358,11 +371,13 @@ def forward_backward_pipelining_without_interleaving(forward_step_func: Callable
             DEFERRED_WGRAD.defer = False
         return None if inp is None else inp.grad
 
-    def after_send(k):
-        """W of backward pass k, once its input gradient is on its way (split schedules)."""
+    def after_send(k, forward_follows=False):
+        """W of backward pass k, once its input gradient is on its way (split schedules). With
+        SMDT_W_FILL and a forward next, it stays queued for that forward's exchange waits."""
         if split and (k < defer_from or k == num_microbatches - 1):
             DEFERRED_WGRAD.hold = False
-            DEFERRED_WGRAD.flush()
+            if not (fill and forward_follows):
+                DEFERRED_WGRAD.flush()
 
     def recv_fwd():
         return None if first else _p2p(recv_prev_shape=tensor_shape, dtype=dtype, device=dev)[0]
@@ -411,7 +426,7 @@ def forward_backward_pipelining_without_interleaving(forward_step_func: Callable
                     inp = recv_fwd()
                 else:
                     inp = _p2p(send_prev=gin, recv_prev_shape=tensor_shape, dtype=dtype, device=dev)[0]
-            after_send(k)
+            after_send(k, forward_follows=not is_last_iter)
         if not forward_only:
             for _ in range(warm):
                 i0, o0 = inputs.pop(0), outputs.pop(0)

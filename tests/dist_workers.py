@@ -634,7 +634,8 @@ def gpt_cp_worker(rank, world, tp, cp, sp, cfg_over=None, with_ddp=False):
     return loss.detach(), grads, meta
 
 
-def gpt_layout_worker(rank, world, tp, pp, nmb, zero, defer=False, sp=False, schedule=None, cfg_over=None):
+def gpt_layout_worker(rank, world, tp, pp, nmb, zero, defer=False, sp=False, schedule=None, cfg_over=None,
+                      w_fill=False):
     """DDP-wrapped tiny GPT under a TP x PP x DP layout with ``nmb`` micro-batches per step (gradient
     accumulation for pp == 1, 1F1B otherwise): returns the reduced fp32 main_grad of every local
     parameter. The global batch (4 sequences) is split over the DP ranks, so the reduced gradients
@@ -651,6 +652,9 @@ def gpt_layout_worker(rank, world, tp, pp, nmb, zero, defer=False, sp=False, sch
     st = ps.initialize_model_parallel(tp, pp)
     if schedule is not None:
         set_pipeline_schedule(schedule)
+    if w_fill:
+        from smdt_amd.parallel import tensor_parallel as tpm
+        tpm.W_FILL = True
     if defer:
         from smdt_amd.parallel import tensor_parallel as tpm
         tpm.DEFERRED_WGRAD.allow_cpu = True

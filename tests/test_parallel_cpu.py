@@ -314,6 +314,29 @@ def test_ddp_gradient_accumulation_matches_single_process(world, tp, pp, nmb, ze
         _check_tp_grads(ref, grads, meta, tp)
 
 
+@pytest.mark.parametrize("schedule", ["zb", "zbh2"])
+@pytest.mark.parametrize("world,tp,pp,nmb,zero", [(4, 2, 2, 4, False), (8, 2, 2, 2, True)])
+def test_w_fillers_in_exchange_waits_match_single_rank(schedule, world, tp, pp, nmb, zero):
+    """SMDT_W_FILL: a pass's W GEMMs stay queued into the next forward and are issued one per
+    TP-exchange wait (tensor_parallel.fill_exchange_wait), the rest flushed at its end; the split
+    schedules still give the single-process losses and reduced gradients, and fillers ran."""
+    over = {"num_layers": 2}
+    ref_loss, ref = W.gpt_reference(cfg_over=over)
+    outs = run_workers(W.gpt_layout_worker, world, tp, pp, nmb, zero, True, True, schedule, over, True,
+                       timeout=600)
+    fills = 0
+    for _, grads, meta in outs:
+        _check_tp_grads(ref, grads, meta, tp)
+        fills += meta["wgrad_stats"].get("fills", 0)
+    # zbh2 on pp2 with 2 micro-batches runs every forward ahead of every backward: nothing to fill
+    assert (fills > 0) == (nmb > 2 or schedule == "zb"), fills
+    for loss, _, meta in outs:
+        if meta["pp_rank"] == pp - 1:
+            per = 4 // (world // (tp * pp))
+            want = ref_loss[meta["dp_rank"] * per:(meta["dp_rank"] + 1) * per]
+            torch.testing.assert_close(loss.reshape(want.shape), want, atol=2e-4, rtol=2e-4)
+
+
 @pytest.mark.parametrize("schedule", ["1f1b", "zb", "zbh1", "zbh2"])
 @pytest.mark.parametrize("world,tp,pp,nmb,zero,sp,layers", [
     (4, 2, 2, 4, False, True, 2),      # tp2 pp2 + SP, 4 micro-batches of 1
