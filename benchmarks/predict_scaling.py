@@ -70,6 +70,15 @@ RUNS = {
     "gpt3_n1": ["--hidden-size", "4096", "--num-attention-heads", "32", "--seq-length", "2048", "--num-layers", "32",
                 "--micro-batch-size", "4", "--grad-accum", "1", "--tunableop", "0"],
 }
+# the N = 8 stage ranks with the TP exchanges MEASURED: the paced link stand-in (comm/loopback.py,
+# SMDT_LINK_STANDIN=relay: the relay's modelled 131 us per 33.6 MB chunk and its 64 workgroups on a
+# side stream beside the rank's compute) instead of an in-line copy; the stage times and F / B / W
+# then include whatever of the exchanges the compute does not hide (profiles/r6_standin/).
+# STANDIN_ENV holds the exchange-overlap settings the bench's N = 8 run uses.
+STANDIN_ENV = {"SMDT_LINK_STANDIN": "relay", "SMDT_RING_GEMM_TN": "1", "SMDT_W_FILL": "1"}
+RUNS["tp2pp2_stage0_standin"] = RUNS["tp2pp2_stage0"]
+RUNS["tp2pp2_stage1_standin"] = RUNS["tp2pp2_stage1"]
+RUN_ENV = {"tp2pp2_stage0_standin": STANDIN_ENV, "tp2pp2_stage1_standin": STANDIN_ENV}
 SCHEDS = ("1f1b", "zb", "zbh1", "zbh2")
 
 
@@ -80,7 +89,8 @@ def measure(steps: int, warmup: int, logdir: str, only=None) -> dict:
             continue
         cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", str(steps), "--warmup", str(warmup),
                "--comm-stats", "1"] + extra
-        r = subprocess.run(cmd, capture_output=True, text=True, timeout=900, cwd=ROOT)
+        env = dict(os.environ, **RUN_ENV.get(name, {}))
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=900, cwd=ROOT, env=env)
         with open(os.path.join(logdir, f"{name}.log"), "w") as f:
             f.write(r.stdout + "\n" + r.stderr)
         if r.returncode != 0:
@@ -157,6 +167,14 @@ def predict(m: dict) -> list:
                                "tp2pp2dp2+sp+zero1 13|11", even="tp2pp2_stage1_even" if "tp2pp2_stage1_even" in m else None):
             rows.append({"N": 8, "model": "gpt2-345m", **r})
         rows += gpt2_tp2_exchange_rows(m, act, dp_tail + embd + 0.5, tok1 * 8)
+    if "tp2pp2_stage0_standin" in m and "tp2pp2_stage1_standin" in m:
+        act = (S // 2) * 32 * H * 2
+        flags = " ".join(f"{k}={v}" for k, v in STANDIN_ENV.items() if k != "SMDT_LINK_STANDIN")
+        for r in pipeline_rows(m, "tp2pp2_stage0_standin", "tp2pp2_stage1_standin", 8, 2, act,
+                               dp_tail + embd + 0.5, tok1 * 8,
+                               f"tp2pp2dp2+sp+zero1 13|11, TP exchanges MEASURED (paced relay stand-in; {flags})"):
+            if r["layout"].endswith("zbh2"):
+                rows.append({"N": 8, "model": "gpt2-345m", **r})
     if "tp2pp2_mb64_stage0" in m and "tp2pp2_mb64_stage1" in m:
         act64 = (S // 2) * 64 * H * 2
         for r in pipeline_rows(m, "tp2pp2_mb64_stage0", "tp2pp2_mb64_stage1", 4, 2, act64, dp_tail + embd + 0.5,

@@ -546,18 +546,41 @@ DEFERRED_WGRAD = DeferredWgrad()
 # (``fill_exchange_wait``) beside the in-flight transfer, on the CUs the transfer leaves; the rest
 # is flushed when that forward ends (train/schedules.py). VERDICT r5 item 1, "split-K W fillers".
 W_FILL = os.environ.get("SMDT_W_FILL", "0") == "1"
+# W GEMM time offered to one exchange wait (us): ~ the relay's 131 us per 33.6 MB chunk less the
+# chunk GEMM beside it; fillers are priced at _FILL_PFLOPS over the CUs the exchange leaves
+_FILL_US = float(os.environ.get("SMDT_W_FILL_US", "110"))
+_FILL_PFLOPS = 1.0
 _FILL = {"on": False}
 
 
+def _item_us(it, cus):
+    g2, t2 = it[2][0][0], it[2][0][1]
+    fl = 2.0 * g2.shape[0] * g2.shape[1] * t2.shape[1] * len(it[2])
+    return fl / (_FILL_PFLOPS * 1e9 * max(cus or 256, 1) / 256.0)
+
+
 def fill_exchange_wait():
-    """Before a forward ring exchange's wait: issue one queued W GEMM beside the transfer."""
-    if _FILL["on"] and not DEFERRED_WGRAD.defer and DEFERRED_WGRAD.items:
-        DEFERRED_WGRAD.fill_one(gemm_tn_blocks())
+    """Before a ring exchange's wait (forward or backward): issue queued W GEMMs beside the
+    transfer, oldest first, up to ~_FILL_US of estimated GEMM time."""
+    if not (_FILL["on"] and DEFERRED_WGRAD.items):
+        return
+    cus = gemm_tn_blocks()
+    spent = 0.0
+    while spent < _FILL_US:
+        it = next((x for x in DEFERRED_WGRAD.items if x[4] and not x[3]), None)
+        if it is None:
+            return
+        spent += _item_us(it, cus)
+        DEFERRED_WGRAD.fill_one(cus)
 
 
 class forward_fill:
-    """Context for one forward pass of a split-backward schedule: exchange waits take W fillers;
-    whatever is left unheld is flushed at the end."""
+    """Context for one pass (``flush_end``: a forward) of a split-backward schedule under
+    SMDT_W_FILL: exchange waits take W fillers; after a forward, whatever is left unheld is
+    flushed (a backward leaves its own W queued for the next forward)."""
+
+    def __init__(self, flush_end: bool = True):
+        self.flush_end = flush_end
 
     def __enter__(self):
         self.prev = _FILL["on"]
@@ -566,7 +589,7 @@ class forward_fill:
 
     def __exit__(self, *exc):
         _FILL["on"] = self.prev
-        if W_FILL:
+        if W_FILL and self.flush_end:
             DEFERRED_WGRAD.flush_unheld()
         return False
 

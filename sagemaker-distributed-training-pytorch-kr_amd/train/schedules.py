@@ -89,7 +89,11 @@ def forward_backward_no_pipelining(forward_step_func: Callable, data_iterator, m
             if split_backward:
                 DEFERRED_WGRAD.defer = True
             try:
-                _scaled(loss, num_microbatches, grad_scale).backward()
+                if fill:
+                    with forward_fill(flush_end=False):   # B's exchange waits take queued W too
+                        _scaled(loss, num_microbatches, grad_scale).backward()
+                else:
+                    _scaled(loss, num_microbatches, grad_scale).backward()
             finally:
                 if split_backward:
                     DEFERRED_WGRAD.defer = False
@@ -366,7 +370,11 @@ def forward_backward_pipelining_without_interleaving(forward_step_func: Callable
         inp, gout = _finish_recv(inp), _finish_recv(gout)
         if inp is not None:
             inp.retain_grad()
-        _run_backward(out, gout)
+        if fill:
+            with forward_fill(flush_end=False):   # B's exchange waits take queued W too
+                _run_backward(out, gout)
+        else:
+            _run_backward(out, gout)
         if split:
             DEFERRED_WGRAD.defer = False
         return None if inp is None else inp.grad
