@@ -279,6 +279,14 @@ def main():
     else:
         a.tp, a.pp, sp, a.micro_batch_size, a.grad_accum = choose_layout(a, world)
         st = ps.initialize_model_parallel(a.tp, a.pp, a.vpp if (a.vpp > 1 and a.pp > 1) else None)
+    if a.tp > 1:
+        # TP exchange overlap of the N = 8 layouts (profiles/r6_fill2/: measured under the paced
+        # link stand-in): queued W GEMMs fill the ring-exchange waits, and ring-chunk GEMMs issued
+        # beside an in-flight transfer run on gemm_tn with the CUs the transfer leaves.
+        # SMDT_W_FILL=0 / SMDT_RING_GEMM_TN=0 turn them off.
+        from smdt_amd.parallel import tensor_parallel as _tpm
+        _tpm.W_FILL = os.environ.get("SMDT_W_FILL", "1") == "1"
+        _tpm._RING_GEMM_TN = os.environ.get("SMDT_RING_GEMM_TN", "1") == "1"
     model_parallel_seed(1234)
     tuned = enable_gemm_tuning(a, rank)
     dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
@@ -506,6 +514,8 @@ def main():
                        "optimizer_overlap": bool(getattr(ddp, "overlap_optimizer", False)),
                        "mlp_gelu_fusion": _mlp_fusion_desc(),
                        "hip_graph": graph_note,
+                       **({"tp_overlap": {"w_fill": _tp_flag("W_FILL"), "ring_gemm_tn": _tp_flag("_RING_GEMM_TN"),
+                                          "exchange_cu_reserve": _tp_flag("_CU_RESERVE_ON")}} if a.tp > 1 else {}),
                        **({"link_standin": {"GBps": link_standin()[0], "workgroups": link_standin()[1],
                                             "exchanges_per_step": _split_stats().get("standin_exchanges", 0)}}
                           if emulated and link_standin() else {}),
@@ -529,6 +539,11 @@ def main():
         print(json.dumps(rec), flush=True)
     if dist.is_initialized():
         dist.destroy_process_group()
+
+
+def _tp_flag(name):
+    from smdt_amd.parallel import tensor_parallel as _tp
+    return bool(getattr(_tp, name))
 
 
 def _split_stats():

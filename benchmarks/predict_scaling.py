@@ -78,7 +78,10 @@ RUNS = {
 STANDIN_ENV = {"SMDT_LINK_STANDIN": "relay", "SMDT_RING_GEMM_TN": "1", "SMDT_W_FILL": "1"}
 RUNS["tp2pp2_stage0_standin"] = RUNS["tp2pp2_stage0"]
 RUNS["tp2pp2_stage1_standin"] = RUNS["tp2pp2_stage1"]
-RUN_ENV = {"tp2pp2_stage0_standin": STANDIN_ENV, "tp2pp2_stage1_standin": STANDIN_ENV}
+_COPY_ENV = {"SMDT_W_FILL": "0", "SMDT_RING_GEMM_TN": "0"}   # compute-only runs: no overlap machinery
+RUN_ENV = {"tp2pp2_stage0_standin": STANDIN_ENV, "tp2pp2_stage1_standin": STANDIN_ENV,
+           **{k: _COPY_ENV for k in ("tp2pp2_stage0", "tp2pp2_stage1", "tp2pp2_stage1_even",
+                                     "tp2pp2_mb64_stage0", "tp2pp2_mb64_stage1")}}
 SCHEDS = ("1f1b", "zb", "zbh1", "zbh2")
 
 
