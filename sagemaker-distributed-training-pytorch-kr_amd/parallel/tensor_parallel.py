@@ -505,6 +505,17 @@ class DeferredWgrad:
         bt = bias.main_grad if bias is not None else _NO_BIAS.get(mg.device)
         for i, (g2, t2, _, _) in enumerate(segs):      # segments in order: round 0 may store
             ow = bool(fresh) and i == 0
+            if g2.is_cuda and _FILL_IMPL == "blaslt":
+                # hipBLASLt beta = 1 into main_grad (its own non-persistent tiling shares the CUs
+                # with the transfer without a tail split) + the bias column sums
+                C = _ext.ext()
+                if ow:
+                    mg.zero_()
+                if not C.wgrad_accumulate(mg, g2, t2):
+                    raise RuntimeError("deferred wgrad filler: hipBLASLt wgrad refused")
+                if bias is not None:
+                    C.bias_grad(g2, bias.main_grad, True)
+                continue
             if g2.is_cuda:
                 if not _ext.ext().wgrad_grouped([mg], [g2], [t2], [bt], [ow], int(cus)):
                     raise RuntimeError("deferred wgrad filler: grouped launch refused")
@@ -550,6 +561,7 @@ W_FILL = os.environ.get("SMDT_W_FILL", "0") == "1"
 # chunk GEMM beside it; fillers are priced at _FILL_PFLOPS over the CUs the exchange leaves
 _FILL_US = float(os.environ.get("SMDT_W_FILL_US", "110"))
 _FILL_PFLOPS = 1.0
+_FILL_IMPL = os.environ.get("SMDT_W_FILL_IMPL", "grouped")     # "grouped" (MFMA, split tail) / "blaslt"
 _FILL = {"on": False}
 
 
