@@ -1096,7 +1096,17 @@ def sp_fused_gelu_mlp_ok(x, mlp) -> bool:
     rows = x.numel() // x.shape[-1]
     f, h = fc1.weight.shape
     return (rows % 256 == 0 and f % 256 == 0 and h % 128 == 0 and fc2.weight.shape == (h, f)
-            and bool(_ext.ext().gemm_tn_supported(x.reshape(rows, h), fc1.weight)))
+            and _fills_chip(rows, f) and bool(_ext.ext().gemm_tn_supported(x.reshape(rows, h), fc1.weight)))
+
+
+def _fills_chip(rows: int, n: int) -> bool:
+    """A chunk GEMM of rows x n has at least one 256 x 256 output tile per CU: gemm_tn's
+    persistent grid is one workgroup per tile up to the CU count, so fewer tiles leave CUs idle
+    (GPT-3 6.7B tp4 + SP: 2048-row chunks x 4096 = 128 tiles -> the stage rank 426 ms with the
+    fused MLP vs 394 ms on hipBLASLt, profiles/r6_ab/)."""
+    if not _NUM_CUS:
+        _NUM_CUS.append(torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count)
+    return (rows // 256) * (n // 256) >= _NUM_CUS[0]
 
 
 def linear_bias_gelu_ok(x, layer) -> bool:
@@ -1108,7 +1118,7 @@ def linear_bias_gelu_ok(x, layer) -> bool:
             and _ext.use_kernels(x)):
         return False
     x2 = x.view(-1, x.shape[-1])
-    return bool(_ext.ext().gemm_tn_supported(x2, layer.weight))
+    return _fills_chip(x2.shape[0], layer.weight.shape[0]) and bool(_ext.ext().gemm_tn_supported(x2, layer.weight))
 
 
 def linear_bias_gelu(x, layer):

@@ -114,6 +114,7 @@ def test_gpt_step_on_gemm_tn_matches_fp32_reference(monkeypatch, mode):
     import test_model_gpu as T
     from smdt_amd.parallel import tensor_parallel as tp
     monkeypatch.setattr(tp, "_FUSED_BIAS_GELU", True)
+    monkeypatch.setattr(tp, "_fills_chip", lambda rows, n: True)   # test shapes: a few tiles only
     if mode == "all_linears":
         monkeypatch.setattr(tp, "_GEMM_TN", "1")
         monkeypatch.setattr(tp, "_GEMM_TN_SHAPES", None)
@@ -148,6 +149,7 @@ def _emulated_tp2_sp_gpt_grads(fused, monkeypatch):
     from smdt_amd.parallel import tensor_parallel as tp
     from smdt_amd.parallel.distributed import DistributedDataParallel as DDP
     monkeypatch.setattr(tp, "_FUSED_BIAS_GELU", fused)
+    monkeypatch.setattr(tp, "_fills_chip", lambda rows, n: True)   # test shapes: a few tiles only
     calls = {"n": 0}
     orig = tp.SPFusedGeLUMLP.forward
 
