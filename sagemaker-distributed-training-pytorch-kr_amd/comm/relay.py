@@ -166,6 +166,48 @@ class XgmiRelay(IpcEngine):
             self.active = False
         return res
 
+    def tune_sub(self, candidates=(1, 2, 4), nbytes: int = 16 << 20, iters: int = 10, tol: float = 1.05) -> dict:
+        """Pick the blocks per part and direction (``sub``): the kernel keeps 2 x world x sub
+        workgroups resident for a whole exchange, one CU each, which the rank's chunk GEMMs then do
+        without (tensor_parallel.gemm_tn_blocks; 16 vs 64 held CUs, profiles/r6_mix/). Times every
+        candidate with all pairs exchanging at once (max over ranks, so every rank decides alike)
+        and keeps the smallest within ``tol`` of the fastest. Returns {sub: ms}."""
+        dev = torch.device("cuda", torch.cuda.current_device())
+        x = torch.randn(nbytes // 2, device=dev, dtype=torch.bfloat16)
+        y = torch.empty_like(x)
+        keep = self.sub
+        res = {}
+        host = dist.get_backend() == "gloo"
+        for sub in candidates:
+            self._set_sub(int(sub))
+            for _ in range(3):
+                self.exchange(x, y)
+            torch.cuda.synchronize()
+            dist.barrier()
+            t0 = time.perf_counter()
+            for _ in range(iters):
+                self.exchange(x, y)
+            torch.cuda.synchronize()
+            t = torch.tensor([(time.perf_counter() - t0) / iters * 1e3], device="cpu" if host else dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            res[int(sub)] = float(t.item())
+        best = min(res.values())
+        self._set_sub(min(sb for sb, t in res.items() if t <= tol * best) if res else keep)
+        return res
+
+    def _set_sub(self, sub: int):
+        """Change the blocks per part between exchanges: the (part, block) -> sub-range map
+        changes, so every rank drains, the flags and device epochs are zeroed (partners stay
+        equal: both restart at epoch 1) and every rank resumes together. Collective over WORLD."""
+        if sub == self.sub:
+            return
+        torch.cuda.synchronize()
+        dist.barrier()
+        self.C.relay_reset(self.sig_ptrs[self.rank])
+        torch.cuda.synchronize()
+        dist.barrier()
+        self.sub = int(sub)
+
     # ------------------------------------------------------------------ API
     def cu_blocks(self) -> int:
         """Workgroups the relay kernel keeps resident during an exchange (one CU each)."""
@@ -265,6 +307,11 @@ def create_for_pairs(pair_group, log=print) -> Optional[XgmiRelay]:
         TUNED["tp_pair"] = {f"{nb >> 20}MB": {"rccl_ms": round(a, 3), "relay_ms": round(b, 3)}
                             for nb, (a, b) in res.items()}
         TUNED["tp_pair"]["relay_min_bytes"] = eng.min_bytes if eng.active else None
+        if eng.active:
+            subs = eng.tune_sub()
+            TUNED["tp_pair"]["relay_sub_ms"] = {str(k): round(v, 3) for k, v in subs.items()}
+            TUNED["tp_pair"]["relay_sub"] = eng.sub
+            TUNED["tp_pair"]["relay_cu_blocks"] = eng.cu_blocks()
         if dist.get_rank() == 0 and log is not None:
             pretty = ", ".join(f"{nb >> 20} MB: rccl {a:.3f} ms / relay {b:.3f} ms" for nb, (a, b) in res.items())
             log(f"[smdt] TP-pair exchange over all xGMI links: {pretty} -> "

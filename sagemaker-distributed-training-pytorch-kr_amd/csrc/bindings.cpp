@@ -846,6 +846,8 @@ void xgmi_relay(Tensor in, Tensor out, std::vector<int64_t> stage_ptrs, std::vec
         "xgmi_relay");
 }
 
+void relay_reset(int64_t sig) { check(smdt_relay_reset(vp(sig), cur_stream()), "relay_reset"); }
+
 // Device epochs (xgmi_relay.hip): advance the local ranks' call counters by n on the current stream.
 void relay_epoch_bump(std::vector<int64_t> sig_ptrs, int64_t rank, int64_t nranks_local, int64_t n) {
   std::vector<void*> s(sig_ptrs.size());
@@ -925,6 +927,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("xgmi_relay", &xgmi_relay, py::arg("input"), py::arg("out"), py::arg("stage_ptrs"), py::arg("sig_ptrs"),
         py::arg("partners"), py::arg("rank"), py::arg("nranks_local"), py::arg("slot_bytes"), py::arg("sub"),
         py::arg("epoch"), py::arg("dev_epoch") = false);
+  m.def("relay_reset", &relay_reset, py::arg("sig"));
   m.def("relay_epoch_bump", &relay_epoch_bump, py::arg("sig_ptrs"), py::arg("rank"), py::arg("nranks_local"),
         py::arg("n"));
   m.def("relay_signal_bytes", &smdt_relay_signal_bytes);

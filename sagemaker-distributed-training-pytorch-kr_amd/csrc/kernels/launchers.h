@@ -181,6 +181,8 @@ hipError_t smdt_xgmi_relay(int dtype, const void* in, void* out, int64_t in_rank
                            int64_t n, void* const* stage_ptrs, void* const* sig_ptrs, const int* partners, int world,
                            int rank, int nranks_local, int64_t slot_bytes, int sub, uint32_t epoch, int dev_epoch,
                            hipStream_t st);
+// zero one signal buffer's flags and device epoch (all ranks synchronised, no call in flight)
+hipError_t smdt_relay_reset(void* sig, hipStream_t st);
 // device epochs: advance the call counter of local ranks [rank, rank + nranks_local) by n
 hipError_t smdt_relay_epoch_bump(void* const* sig_ptrs, int world, int rank, int nranks_local, uint32_t n,
                                  hipStream_t st);

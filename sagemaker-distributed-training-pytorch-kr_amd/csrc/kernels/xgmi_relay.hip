@@ -214,6 +214,17 @@ int64_t smdt_relay_word_offset(int which) {
                       : (int64_t)offsetof(relay::SignalBuf, epoch);
 }
 
+// Protocol reset (host, between exchanges, after every rank synchronised): zero this rank's ready /
+// freed flags and its device epoch, so the next call is epoch 1 with no slot waits. Used when
+// the engine changes its blocks per part (XgmiRelay.tune_sub): the (part, block) -> sub-range map
+// changes, so flags of the old map must not satisfy waits of the new one.
+hipError_t smdt_relay_reset(void* sig, hipStream_t st) {
+  if (!sig) return hipErrorInvalidValue;
+  hipError_t e = hipMemsetAsync(sig, 0, offsetof(relay::SignalBuf, error), st);
+  if (e != hipSuccess) return e;
+  return hipMemsetAsync((char*)sig + offsetof(relay::SignalBuf, epoch), 0, sizeof(uint32_t), st);
+}
+
 hipError_t smdt_relay_epoch_bump(void* const* sig_ptrs, int world, int rank, int nranks_local, uint32_t n,
                                  hipStream_t st) {
   if (world < 1 || world > relay::kMaxRanks || rank < 0 || nranks_local < 1 || rank + nranks_local > world)

@@ -1434,7 +1434,10 @@ def _mm_into(dst, a, w, bias=None):
     d2 = dst.view(-1, dst.shape[-1])
     if _RING_GEMM_TN and _CU_HELD and a2.is_cuda and a2.is_contiguous() and d2.is_contiguous() \
             and a2.dtype in (torch.bfloat16, torch.float16) and w.dtype == a2.dtype \
-            and (bias is None or bias.dtype == a2.dtype) and _ext.ext().gemm_tn_supported(a2, w):
+            and (bias is None or bias.dtype == a2.dtype) and _ext.ext().gemm_tn_supported(a2, w) \
+            and (a2.shape[0] // 256) * (w.shape[0] // 256) >= gemm_tn_blocks():
+        # (only when the GEMM has a tile for every CU it may use: GPT-3 tp4's 2,048-row chunks have
+        # 128 and stay on hipBLASLt, profiles/r6_mix/)
         _ext.ext().gemm_tn(a2, w, 1 if bias is not None else 0, bias, d2, None, gemm_tn_blocks())
         return
     if bias is not None:

@@ -813,6 +813,8 @@ def relay_ipc_worker(rank, world, port, outdir):
         t = eng.tune(sizes=(64 << 10, 256 << 10), iters=2)
         res["ok"].append(sorted(t) == [64 << 10, 256 << 10] and eng.active == (eng.min_bytes is not None))
         eng.active, eng.min_bytes = True, 0
+        subs = eng.tune_sub(nbytes=1 << 20, iters=2)     # one decision on every rank
+        res["ok"].append(sorted(subs) == [1, 2, 4] and eng.sub in (1, 2, 4) and eng.cu_blocks() == 2 * world * eng.sub)
         # a message of 3 calls (fp32) and a short bf16 one
         for n, dt in ((3 * world * (1 << 20) // 2 // 4 + 400, torch.float32), (777 * 8, torch.bfloat16)):
             base = torch.arange(n, device="cuda", dtype=torch.float32) % 113

@@ -95,7 +95,7 @@ def test_cross_process_relay_and_tp_ring():
                 out.append(pickle.load(f))
     for r, res in enumerate(out):
         assert res["err"] is None, f"rank {r}:\n{res['err']}"
-        assert res["error_word"] == 0 and all(res["ok"]) and len(res["ok"]) == 9, (r, res)
+        assert res["error_word"] == 0 and all(res["ok"]) and len(res["ok"]) == 10, (r, res)
 
 
 @pytest.mark.gpu
