@@ -112,6 +112,9 @@ def parse():
     p.add_argument("--hidden-dropout", type=float, default=0.1)
     p.add_argument("--attention-dropout", type=float, default=0.1)  # Megatron default (reference run)
     p.add_argument("--zero", type=int, default=1, help="ZeRO-1/2 distributed optimizer when DP > 1")
+    p.add_argument("--overlap-grad-reduce", type=int, default=1,
+                   help="DP bucket reductions during backward and ZeRO parameter all-gathers during the next "
+                        "forward (0: both synchronous; one-GPU Gloo rehearsals)")
     p.add_argument("--overlap-optimizer", type=int, default=0,
                    help="one DP rank: the fused Adam of each gradient bucket on a side stream, overlapped "
                         "with the next step's forward (DistributedDataParallel.overlap_optimizer)")
@@ -318,7 +321,8 @@ def main():
                          post_process=st.is_last_stage() and not a.emulate_first_stage, device=dev)
     zero = bool(a.zero) and (st.dp > 1 or (bool(a.overlap_optimizer) and st.pp == 1))
     ddp = DistributedDataParallel(model, bucket_size=a.bucket_size, use_distributed_optimizer=zero,
-                                  overlap_param_gather=zero and st.dp > 1)
+                                  overlap_param_gather=zero and st.dp > 1 and bool(a.overlap_grad_reduce),
+                                  overlap_grad_reduce=bool(a.overlap_grad_reduce))
     use_graph = bool(a.graph) and dev.type == "cuda" and st.pp == 1
     opt = MixedPrecisionAdam(ddp, lr=1.5e-4, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.01, clip_grad=1.0,
                              capturable=use_graph)
