@@ -401,3 +401,50 @@ def test_fused_mlp_waits_for_overlapped_param_gather(monkeypatch):
     assert (a[1:] - a[:-1]).abs().max() > 1e-2          # steps move the loss: stale weights would show
     torch.testing.assert_close(a, b, atol=2e-2, rtol=0)
     assert (stale - b).abs().max() > 5 * (a - b).abs().max(), (a, b, stale)
+
+
+def test_w_fillers_match_grouped_flush_on_gpu(monkeypatch):
+    """One emulated tp2 + SP rank, split backward over 3 micro-batches (the zero-bubble stage's W
+    grouping), TP exchanges on the paced link stand-in so they hold CUs: with SMDT_W_FILL the W
+    GEMMs run as fillers inside the exchange waits (single items, tail split sized to the free
+    CUs, fp32 atomics) instead of one grouped flush per pass. The fp32 main_grad buffer and the
+    losses match the flush run, and fillers really ran."""
+    from smdt_amd.models.gpt import GPTModel
+    from smdt_amd.models.transformer import TransformerConfig
+    from smdt_amd.parallel import state as ps
+    from smdt_amd.parallel.distributed import DistributedDataParallel as DDP
+    from smdt_amd.train.schedules import forward_backward_no_pipelining
+    monkeypatch.setenv("SMDT_LINK_STANDIN", "256:32")
+    out = []
+    for fill in (False, True):
+        monkeypatch.setattr(tp, "W_FILL", fill)
+        tp.DEFERRED_WGRAD.stats.pop("fills", None)
+        ps.destroy_model_parallel()
+        ps.initialize_emulated_tensor_parallel(2, 1)
+        try:
+            cfg = TransformerConfig(num_layers=2, hidden_size=256, num_attention_heads=4, padded_vocab_size=1024,
+                                    max_position_embeddings=256, hidden_dropout=0.0, attention_dropout=0.0,
+                                    params_dtype=torch.bfloat16, sequence_parallel=True, seed=7)
+            model = GPTModel(cfg, device="cuda")
+            ddp = DDP(model, grad_dtype=torch.float32)
+            g = torch.Generator(device="cuda").manual_seed(13)
+            t = torch.randint(0, 1000, (6, 257), device="cuda", generator=g)
+            data = iter([(t[2 * i:2 * i + 2, :-1], t[2 * i:2 * i + 2, 1:]) for i in range(3)])
+
+            def fstep(di, m):
+                x, y = next(di)
+                o = m(x, None, None, labels=y)
+                return o, (lambda z: (z.float().mean(), {"loss": z.detach().float().mean()}))
+            ddp.zero_grad_buffer()
+            losses = forward_backward_no_pipelining(fstep, data, ddp, 3, split_backward=True)
+            ddp.finish_grad_sync()
+            torch.cuda.synchronize()
+            out.append((torch.stack([d["loss"] for d in losses]).cpu(), ddp.grad_data.clone(),
+                        tp.DEFERRED_WGRAD.stats.get("fills", 0)))
+        finally:
+            ps.destroy_model_parallel()
+    (l0, g0, f0), (l1, g1, f1) = out
+    assert f0 == 0 and f1 > 0
+    torch.testing.assert_close(l1, l0, atol=1e-4, rtol=0)
+    scale = g0.abs().max().item()
+    assert scale > 0 and (g1 - g0).abs().max().item() <= 1e-3 * scale
