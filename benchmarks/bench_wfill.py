@@ -7,7 +7,7 @@ Times, on one GPU, the W work of one micro-batch of a 13-layer stage:
   * ``fill<cus>``: 52 single-item launches, each with its tail split sized for ``cus`` CUs (the
     filler form; 192 = the CUs a relay transfer leaves);
   * ``fill<cus>_x<k>``: k items per launch;
-  * the same fillers beside a paced copy holding 64 CUs for the whole run (``--standin``).
+  * the fillers beside a paced copy holding 64 CUs for the whole run (the relay stand-in).
 Prints one JSON line: microseconds and effective PFLOP/s per form.
 
     python benchmarks/bench_wfill.py [--layers 13] [--reps 5]
