@@ -343,6 +343,7 @@ class DeferredWgrad:
         # per pass (once per batch half): merge the second push instead of flushing, the segments
         # issued as rounds (no concatenation copy)
         self.merge_repeats = False
+        self.ready_after_join = []      # filler-stream items waiting for their readiness report
         self.stats = {"flushes": 0, "items": 0, "max_segments": 0, "stores": 0}
         self.items = []
         self.by_key = {}
@@ -534,6 +535,65 @@ class DeferredWgrad:
                 cb(p)
         return True
 
+    @torch.no_grad()
+    def fill_many(self, budget_us: float, cus: int = 0, stream=None) -> int:
+        """Exchange-wait filler, grouped form: the oldest queued, complete, not held, single-segment
+        CUDA items up to ~``budget_us`` of estimated GEMM time (at least one) as ONE grouped launch
+        sized for ``cus`` CUs. ``stream``: issue it there (the filler stream: it then never delays
+        the next exchange, which waits only for the compute stream) — the caller joins that stream
+        and ``fire_ready`` reports the items' readiness afterwards. Returns the items issued."""
+        picks, spent = [], 0.0
+        for it in self.items:
+            if not (it[4] and not it[3] and len(it[2]) == 1 and it[1].is_cuda):
+                continue
+            if picks and spent + _item_us(it, cus) > budget_us:
+                break
+            picks.append(it)
+            spent += _item_us(it, cus)
+            if spent >= budget_us:
+                break
+        if not picks:
+            return 0
+        ids = {id(it) for it in picks}
+        self.items = [it for it in self.items if id(it) not in ids]
+        for it in picks:
+            self.by_key.pop(it[1].data_ptr(), None)
+            g2, t2, vg, vt = it[2][0]
+            if g2._version != vg or t2._version != vt:
+                raise RuntimeError("deferred wgrad: a queued dY / X tensor was modified in place before the "
+                                   "flush; disable with SMDT_DEFER_WGRAD=0 and report the op that did it")
+            self.tiles -= -(-g2.shape[1] // 256) * -(-t2.shape[1] // 256)
+            self.held_bytes -= g2.numel() * g2.element_size() + t2.numel() * t2.element_size()
+        mgs = [it[1] for it in picks]
+        g2s = [it[2][0][0] for it in picks]
+        t2s = [it[2][0][1] for it in picks]
+        bts = [it[5].main_grad if it[5] is not None else _NO_BIAS.get(it[1].device) for it in picks]
+        ows = [bool(it[6]) for it in picks]
+        if stream is not None:
+            for t in g2s + t2s:
+                t.record_stream(stream)      # the queue drops them before the filler stream ran
+        if not _ext.ext().wgrad_grouped(mgs, g2s, t2s, bts, ows, int(cus)):
+            raise RuntimeError("deferred wgrad filler: grouped launch refused")
+        self.stats["fills"] = self.stats.get("fills", 0) + len(picks)
+        ready = [p for it in picks for p in (it[0], it[5]) if p is not None]
+        if stream is None:
+            self._fire(ready)
+        else:
+            self.ready_after_join.extend(ready)
+        return len(picks)
+
+    def fire_ready(self):
+        """Readiness of the items issued on the filler stream (after the caller joined it)."""
+        ready, self.ready_after_join = self.ready_after_join, []
+        self._fire(ready)
+
+    @staticmethod
+    def _fire(params):
+        for p in params:
+            cb = getattr(p, "_smdt_grad_ready", None)
+            if cb is not None:
+                cb(p)
+
     def flush_unheld(self):
         """Issue every queued item that is not held for a later synchronising pass."""
         if not any(not it[3] for it in self.items):
@@ -571,12 +631,36 @@ def _item_us(it, cus):
     return fl / (_FILL_PFLOPS * 1e9 * max(cus or 256, 1) / 256.0)
 
 
+# SMDT_W_FILL_STREAM=1: the fillers go to a stream of their own (joined at the end of each pass),
+# so a filler that outlasts its exchange no longer holds up the next exchange's start
+_FILL_STREAM_ON = os.environ.get("SMDT_W_FILL_STREAM", "0") == "1"
+_FILL_STREAMS = {}
+
+
+def _fill_stream(dev):
+    s = _FILL_STREAMS.get(dev)
+    if s is None:
+        s = _FILL_STREAMS[dev] = torch.cuda.Stream(dev)
+    return s
+
+
 def fill_exchange_wait():
     """Before a ring exchange's wait (forward or backward): issue queued W GEMMs beside the
     transfer, oldest first, up to ~_FILL_US of estimated GEMM time."""
     if not (_FILL["on"] and DEFERRED_WGRAD.items):
         return
     cus = gemm_tn_blocks()
+    it0 = next((x for x in DEFERRED_WGRAD.items if x[4] and not x[3]), None)
+    if it0 is not None and it0[1].is_cuda and len(it0[2]) == 1:
+        if _FILL_STREAM_ON:
+            dev = it0[1].device
+            fs = _fill_stream(dev)
+            fs.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(fs):
+                DEFERRED_WGRAD.fill_many(_FILL_US, cus, stream=fs)
+        else:
+            DEFERRED_WGRAD.fill_many(_FILL_US, cus)
+        return
     spent = 0.0
     while spent < _FILL_US:
         it = next((x for x in DEFERRED_WGRAD.items if x[4] and not x[3]), None)
@@ -584,6 +668,15 @@ def fill_exchange_wait():
             return
         spent += _item_us(it, cus)
         DEFERRED_WGRAD.fill_one(cus)
+
+
+def join_fill_stream():
+    """The compute stream waits for the filler stream; then the filled items report readiness."""
+    if _FILL_STREAMS:
+        for dev, fs in _FILL_STREAMS.items():
+            torch.cuda.current_stream(dev).wait_stream(fs)
+    if DEFERRED_WGRAD.ready_after_join:
+        DEFERRED_WGRAD.fire_ready()
 
 
 class forward_fill:
@@ -601,8 +694,10 @@ class forward_fill:
 
     def __exit__(self, *exc):
         _FILL["on"] = self.prev
-        if W_FILL and self.flush_end:
-            DEFERRED_WGRAD.flush_unheld()
+        if W_FILL:
+            join_fill_stream()
+            if self.flush_end:
+                DEFERRED_WGRAD.flush_unheld()
         return False
 
 

@@ -403,18 +403,21 @@ def test_fused_mlp_waits_for_overlapped_param_gather(monkeypatch):
     assert (stale - b).abs().max() > 5 * (a - b).abs().max(), (a, b, stale)
 
 
-def test_w_fillers_match_grouped_flush_on_gpu(monkeypatch):
+@pytest.mark.parametrize("stream", [False, True])
+def test_w_fillers_match_grouped_flush_on_gpu(monkeypatch, stream):
     """One emulated tp2 + SP rank, split backward over 3 micro-batches (the zero-bubble stage's W
     grouping), TP exchanges on the paced link stand-in so they hold CUs: with SMDT_W_FILL the W
     GEMMs run as fillers inside the exchange waits (single items, tail split sized to the free
-    CUs, fp32 atomics) instead of one grouped flush per pass. The fp32 main_grad buffer and the
-    losses match the flush run, and fillers really ran."""
+    CUs, fp32 atomics) instead of one grouped flush per pass — on the compute stream, or on a
+    filler stream of their own (``stream``: joined at each pass end, readiness reported after the
+    join). The fp32 main_grad buffer and the losses match the flush run, and fillers really ran."""
     from smdt_amd.models.gpt import GPTModel
     from smdt_amd.models.transformer import TransformerConfig
     from smdt_amd.parallel import state as ps
     from smdt_amd.parallel.distributed import DistributedDataParallel as DDP
     from smdt_amd.train.schedules import forward_backward_no_pipelining
     monkeypatch.setenv("SMDT_LINK_STANDIN", "256:32")
+    monkeypatch.setattr(tp, "_FILL_STREAM_ON", stream)
     out = []
     for fill in (False, True):
         monkeypatch.setattr(tp, "W_FILL", fill)
