@@ -619,7 +619,10 @@ DEFERRED_WGRAD = DeferredWgrad()
 W_FILL = os.environ.get("SMDT_W_FILL", "0") == "1"
 # W GEMM time offered to one exchange wait (us): ~ the relay's 131 us per 33.6 MB chunk less the
 # chunk GEMM beside it; fillers are priced at _FILL_PFLOPS over the CUs the exchange leaves
-_FILL_US = float(os.environ.get("SMDT_W_FILL_US", "110"))
+_FILL_STREAM_ON = os.environ.get("SMDT_W_FILL_STREAM", "1") == "1"
+# on the filler stream a filler may outlast its exchange without delaying the next one: 250 us
+# measured best there (profiles/r6_fill3/: 110 / 250 / 500 us), 110 us on the compute stream
+_FILL_US = float(os.environ.get("SMDT_W_FILL_US", "250" if _FILL_STREAM_ON else "110"))
 _FILL_PFLOPS = 1.0
 _FILL_IMPL = os.environ.get("SMDT_W_FILL_IMPL", "grouped")     # "grouped" (MFMA, split tail) / "blaslt"
 _FILL = {"on": False}
@@ -631,9 +634,8 @@ def _item_us(it, cus):
     return fl / (_FILL_PFLOPS * 1e9 * max(cus or 256, 1) / 256.0)
 
 
-# SMDT_W_FILL_STREAM=1: the fillers go to a stream of their own (joined at the end of each pass),
-# so a filler that outlasts its exchange no longer holds up the next exchange's start
-_FILL_STREAM_ON = os.environ.get("SMDT_W_FILL_STREAM", "0") == "1"
+# SMDT_W_FILL_STREAM (default 1, above): the fillers go to a stream of their own (joined at the end
+# of each pass), so a filler that outlasts its exchange no longer holds up the next exchange's start
 _FILL_STREAMS = {}
 
 
