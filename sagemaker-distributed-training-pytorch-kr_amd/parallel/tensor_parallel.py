@@ -1633,7 +1633,10 @@ def take_pending_add(t):
 
 
 def check_pending_adds(where: str):
-    """Raise if a deferred reduce-scatter summand was issued but never consumed."""
+    """Raise if a deferred reduce-scatter summand was issued but never consumed. (Also drops any CU
+    hold left by an exchange no ring waited for: every TP exchange of a layer-stack pass is
+    complete at these check points.)"""
+    _CU_HELD.clear()
     live = _ADD_LEDGER["live"]
     if live:
         kinds = sorted(set(live.values()))
