@@ -118,7 +118,8 @@ def gemm_tn_blocks() -> int:
         return 0
     if not _NUM_CUS:
         _NUM_CUS.append(torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count)
-    return max(_NUM_CUS[0] - sum(_CU_HELD.values()), _NUM_CUS[0] // 2)
+    # max, not sum: the exchanges in flight run one after another on their engine's stream
+    return max(_NUM_CUS[0] - max(_CU_HELD.values()), _NUM_CUS[0] // 2)
 
 
 def _wait_works(works, group):
@@ -1769,6 +1770,23 @@ def end_subbatch():
     _CU_HELD.clear()
 
 
+# SMDT_RING_PIECES=k (2-rank rings): each exchange goes out in k row pieces, so the peer chunk's
+# GEMM starts on the first piece (all-gather) and the first partial piece leaves before the whole
+# partial exists (reduce-scatter); pieces keep whole 256-row GEMM blocks (else one piece)
+_RING_PIECES = int(os.environ.get("SMDT_RING_PIECES", "1") or 1)
+
+
+def _row_pieces(n: int, rows_per: int, k: int, align: int = 256):
+    """[(a, b)) bounds of k row pieces of an n-row chunk (dim 0) whose GEMM rows (x rows_per) stay
+    multiples of ``align`` (256 on the GPU: gemm_tn's row blocks); [(0, n)] when impossible."""
+    if k <= 1 or n % k:
+        return [(0, n)]
+    step = n // k
+    if (step * rows_per) % align:
+        return [(0, n)]
+    return [(i * step, (i + 1) * step) for i in range(k)]
+
+
 def ag_ring(x, group, chunk_fn=None, before_last_wait=None, _skip_direct=False, bulk=False):
     """All-gather ``x`` along dim 0 over ``group`` as a ring; ``chunk_fn(lo, rows)`` runs on the
     gathered rows [lo, lo + rows.shape[0]) (dim 0) as soon as they are resident, while the next
@@ -1807,6 +1825,26 @@ def ag_ring(x, group, chunk_fn=None, before_last_wait=None, _skip_direct=False, 
         _wait_works(works, group)
         if chunk_fn is not None:
             chunk_fn(0, total)
+        return total
+    rows_per = x.numel() // max(x.shape[0], 1) // max(x.shape[-1], 1)
+    bounds = _row_pieces(n, rows_per, _RING_PIECES, 256 if x.is_cuda else 1) if ws == 2 else [(0, n)]
+    if len(bounds) > 1:
+        # 2-rank ring in row pieces: every piece of this rank's chunk goes out at once (the
+        # engine's stream runs them in order), the local chunk's GEMM runs beside them, then each
+        # peer piece's GEMM as soon as that piece has landed
+        peer = 1 - r
+        works_j = [_exchange(total[r * n + a:r * n + b], total[peer * n + a:peer * n + b], nxt, prv, group)
+                   for a, b in bounds]
+        SPLIT_STATS["ring_pieces"] = SPLIT_STATS.get("ring_pieces", 0) + len(bounds)
+        if chunk_fn is not None:
+            chunk_fn(r * n, x)
+        for j, (a, b) in enumerate(bounds):
+            if j == len(bounds) - 1 and before_last_wait is not None:
+                before_last_wait()
+            fill_exchange_wait()
+            _wait_works(works_j[j], group)
+            if chunk_fn is not None:
+                chunk_fn(peer * n + a, total[peer * n + a:peer * n + b])
         return total
     for s in range(ws):
         c = (r - s) % ws
@@ -1864,6 +1902,34 @@ def rs_ring(partial_fn, group, full_shape, ref, before_last_wait=None, bulk=Fals
             before_last_wait()
         _wait_works(works, group)
         return full[r * n:(r + 1) * n].add_(incoming)
+    rows_per = 1
+    for d in full_shape[1:-1]:
+        rows_per *= d
+    bounds = _row_pieces(n, rows_per, _RING_PIECES, 256 if ref.is_cuda else 1) if ws == 2 else [(0, n)]
+    if len(bounds) > 1:
+        # 2-rank ring in row pieces: the peer's partial piece by piece, each piece out as soon as
+        # it exists, then this rank's own partial beside the transfers, then the combine
+        peer = 1 - r
+        incoming = None
+        works_j, keep = [], []
+        for a, b in bounds:
+            part = partial_fn(peer * n + a, b - a, None)
+            if incoming is None:
+                incoming = torch.empty((n,) + tuple(part.shape[1:]), dtype=part.dtype, device=part.device)
+            keep.append(part)
+            works_j.append(_exchange(part, incoming[a:b], nxt, prv, group))
+        SPLIT_STATS["ring_pieces"] = SPLIT_STATS.get("ring_pieces", 0) + len(bounds)
+        own = partial_fn(r * n, n, None)
+        for j in range(len(bounds)):
+            if j == len(bounds) - 1 and before_last_wait is not None:
+                before_last_wait()
+            fill_exchange_wait()
+            _wait_works(works_j[j], group)
+        if (_DEFER_ADD["on"] and before_last_wait is None) or defer_add:
+            set_pending_add(own, incoming, "backward dgrad" if defer_add else "forward output")
+            SPLIT_STATS["bwd_add_to_norm" if defer_add else "rs_add_to_norm"] += 1
+            return own
+        return own.add_(incoming)
     works, incoming, keep = None, None, []
     for s in range(ws):
         c = (r - s - 1) % ws

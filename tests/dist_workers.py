@@ -91,7 +91,7 @@ def _cpu_tp_direct(group, pieces):
     return _CpuTpDirect(_GlooPieceEngine(group), group)
 
 
-def gpt_tp_worker(rank, world, tp, pp, sp, cfg_over=None, p2p=None, direct_pieces=0, subbatch=0):
+def gpt_tp_worker(rank, world, tp, pp, sp, cfg_over=None, p2p=None, direct_pieces=0, subbatch=0, ring_pieces=1):
     """``direct_pieces`` > 0: the TP exchanges run through ``TpDirect`` in that many row pieces
     (over the CPU stand-in engine) instead of the ring. ``subbatch`` = 2: the layer stack runs the
     two batch halves interleaved phase by phase (SMDT_SP_SUBBATCH)."""
@@ -103,6 +103,9 @@ def gpt_tp_worker(rank, world, tp, pp, sp, cfg_over=None, p2p=None, direct_piece
     from smdt_amd.train.schedules import get_forward_backward_func
     init_distributed("gloo")
     st = ps.initialize_model_parallel(tp, pp)
+    if ring_pieces > 1:
+        from smdt_amd.parallel import tensor_parallel as _TPr
+        _TPr._RING_PIECES = ring_pieces
     if subbatch:
         import smdt_amd.models.transformer as T
         T._SUBBATCH = subbatch

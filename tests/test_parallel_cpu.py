@@ -68,6 +68,20 @@ def test_direct_tp_exchange_pieces_match_single_rank(tp, pieces):
 
 
 @pytest.mark.parametrize("pp", [1, 2])
+def test_ring_pieces_match_single_rank(pp):
+    """tp2 + SP with every 2-rank ring exchange in 2 row pieces (SMDT_RING_PIECES=2: the peer
+    chunk's GEMM per landed piece, the reduce-scatter's partial sent piece by piece): loss and
+    every gradient equal the single-rank model's, and the pieces really ran."""
+    ref_loss, ref = W.gpt_reference()
+    outs = run_workers(W.gpt_tp_worker, 2 * pp, 2, pp, True, None, None, 0, 0, 2)
+    for loss, grads, meta in outs:
+        _check_tp_grads(ref, grads, meta, 2)
+        assert meta["split"].get("ring_pieces", 0) > 0
+    last = [o for o in outs if o[2]["pp_rank"] == pp - 1][0]
+    torch.testing.assert_close(last[0].view(-1), ref_loss.view(-1), atol=2e-4, rtol=2e-4)
+
+
+@pytest.mark.parametrize("pp", [1, 2])
 def test_subbatch_interleave_matches_single_rank(pp):
     """tp2 + SP with the two batch halves of every micro-batch interleaved phase by phase
     (SMDT_SP_SUBBATCH=2: one half's all-gather / reduce-scatter in flight while the other half's
