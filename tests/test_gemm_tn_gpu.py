@@ -193,3 +193,18 @@ def test_sp_fused_gelu_mlp_matches_unfused(monkeypatch):
     assert (gf - gu).abs().max().item() <= 2e-2 * scale
     # every parameter, relative to its own magnitude
     assert torch.linalg.vector_norm(gf - gu).item() <= 2e-2 * torch.linalg.vector_norm(gu).item()
+
+
+def test_sp_ring_pieces_match_whole_chunks(monkeypatch):
+    """The emulated tp2 + SP rank with every ring exchange in 2 row pieces (SMDT_RING_PIECES=2:
+    the fused MLP's gemm_tn chunk GEMMs and the other ring GEMMs run per piece, at row offsets)
+    gives the whole-chunk run's loss and fp32 gradients."""
+    from smdt_amd.parallel import tensor_parallel as tp
+    lw, gw, _ = _emulated_tp2_sp_gpt_grads(True, monkeypatch)
+    monkeypatch.setattr(tp, "_RING_PIECES", 2)
+    tp.SPLIT_STATS.pop("ring_pieces", None)
+    lp, gp, _ = _emulated_tp2_sp_gpt_grads(True, monkeypatch)
+    assert tp.SPLIT_STATS.get("ring_pieces", 0) > 0
+    assert abs(lp - lw) <= 1e-3 * abs(lw)
+    scale = gw.abs().max().item()
+    assert (gp - gw).abs().max().item() <= 1e-2 * scale
