@@ -101,9 +101,11 @@ class TpDirect:
         self.pieces_issued += len(pieces)
         if chunk_fn is not None:
             chunk_fn(r * n, x)                   # beside the first piece
+        from ..parallel.tensor_parallel import fill_exchange_wait
         for j, (a, b) in enumerate(pieces):
             if j == len(pieces) - 1 and before_last_wait is not None:
                 before_last_wait()
+            fill_exchange_wait()      # queued W GEMMs beside the piece in flight (SMDT_W_FILL)
             hs[j].wait()
             if chunk_fn is not None:
                 for d in range(1, ws):
@@ -147,6 +149,8 @@ class TpDirect:
         self.pieces_issued += len(pieces)
         if before_last_wait is not None:
             before_last_wait()
+        from ..parallel.tensor_parallel import fill_exchange_wait
+        fill_exchange_wait()          # queued W GEMMs beside the last pieces in flight (SMDT_W_FILL)
         for h in hs:
             h.wait()
         return out
