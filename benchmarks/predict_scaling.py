@@ -78,8 +78,14 @@ RUNS = {
 STANDIN_ENV = {"SMDT_LINK_STANDIN": "relay", "SMDT_RING_GEMM_TN": "1", "SMDT_W_FILL": "1"}
 RUNS["tp2pp2_stage0_standin"] = RUNS["tp2pp2_stage0"]
 RUNS["tp2pp2_stage1_standin"] = RUNS["tp2pp2_stage1"]
+# GPT-3 tp4 stages with the SP exchanges MEASURED: TpDirect's row pieces over a paced stand-in of
+# the direct engine (comm/loopback.PacedDirectEngine: 3 links at LINK_GBPS, 32 workgroups)
+DIRECT_ENV = {"SMDT_LINK_STANDIN": f"direct:{LINK_GBPS:g}:32", "SMDT_RING_GEMM_TN": "1", "SMDT_W_FILL": "1"}
+RUNS["gpt3_tp4_stage0_direct"] = RUNS["gpt3_tp4_stage0"]
+RUNS["gpt3_tp4_stage1_direct"] = RUNS["gpt3_tp4_stage1"]
 _COPY_ENV = {"SMDT_W_FILL": "0", "SMDT_RING_GEMM_TN": "0"}   # compute-only runs: no overlap machinery
 RUN_ENV = {"tp2pp2_stage0_standin": STANDIN_ENV, "tp2pp2_stage1_standin": STANDIN_ENV,
+           "gpt3_tp4_stage0_direct": DIRECT_ENV, "gpt3_tp4_stage1_direct": DIRECT_ENV,
            **{k: _COPY_ENV for k in ("tp2pp2_stage0", "tp2pp2_stage1", "tp2pp2_stage1_even",
                                      "tp2pp2_mb64_stage0", "tp2pp2_mb64_stage1")}}
 SCHEDS = ("1f1b", "zb", "zbh1", "zbh2")
@@ -337,6 +343,13 @@ def predict_gpt3(m: dict) -> list:
                              f"{link_ms(xfer_bytes, links):.0f} ms on {links} link(s); exposed per layer and "
                              f"micro-batch fwd {mdl['fwd_per_layer_mb']:.3f} / bwd {mdl['bwd_per_layer_mb']:.3f} ms "
                              f"against {W_ms / layers:.3f} ms of GEMMs per pass"})
+    if "gpt3_tp4_stage0_direct" in m and "gpt3_tp4_stage1_direct" in m:
+        # the same layout with the exchanges MEASURED inside the emulated stages (no model term)
+        flags = " ".join(f"{k}={v}" for k, v in DIRECT_ENV.items())
+        for r in pipeline_rows(m, "gpt3_tp4_stage0_direct", "gpt3_tp4_stage1_direct", 8, 2, act, 0.0, tok,
+                               f"tp4pp2+sp, TP exchanges MEASURED (paced direct-engine stand-in; {flags})"):
+            if r["layout"].endswith(sched):
+                rows.append({"N": 8, "model": "gpt3-6.7b", **r})
     return rows
 
 

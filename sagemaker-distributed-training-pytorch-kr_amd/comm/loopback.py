@@ -44,12 +44,88 @@ def link_standin():
     (256 GB/s per direction: 4 links' worth at 64 GB/s, docs/XGMI.md; 64 workgroups), or
     ``<GB/s>:<workgroups>``. Returns (GB/s, workgroups) or None (off, the default)."""
     v = os.environ.get("SMDT_LINK_STANDIN", "").strip().lower()
-    if not v or v in ("0", "off"):
+    if not v or v in ("0", "off") or v.startswith("direct"):
         return None
     if v == "relay":
         return 256.0, 64
     gbps, _, blocks = v.partition(":")
     return float(gbps), int(blocks or 64)
+
+
+def direct_standin():
+    """SMDT_LINK_STANDIN=direct[:<GB/s per link>[:<workgroups>]]: the emulated TP4 / TP8 group's
+    exchanges through a paced stand-in of the direct multi-link engine (comm/tp_direct.py) instead
+    of the ring: each piece of an all-gather / reduce-scatter takes piece bytes / (GB/s per link)
+    (every peer over its own link, all at once) on ``workgroups`` CUs. Returns (GB/s, workgroups)
+    or None."""
+    v = os.environ.get("SMDT_LINK_STANDIN", "").strip().lower()
+    if not v.startswith("direct"):
+        return None
+    parts = v.split(":")
+    gbps = float(parts[1]) if len(parts) > 1 and parts[1] else 64.0
+    blocks = int(parts[2]) if len(parts) > 2 and parts[2] else 32
+    return gbps, blocks
+
+
+class PacedDirectEngine:
+    """Single-GPU stand-in of the xGMI engine's piece API (``all_gather_pieces_async`` /
+    ``reduce_scatter_piece_async``, what ``TpDirect`` drives) for an emulated TP rank: the
+    receiving side's copies / adds, held on the engine's CUs for the modelled link time of the
+    piece, on a side stream; the handles are waited for like the engine's events. Timing only."""
+
+    def __init__(self, world: int, gbps: float, blocks: int):
+        self.world, self.rank = int(world), 0
+        self.gbps, self.blocks = float(gbps), int(blocks)
+        self.active = True
+        self.use = {"all_gather": True, "reduce_scatter": True}
+        self._stream = None
+
+    def _side(self, dev):
+        if self._stream is None:
+            from .streams import comm_stream
+            self._stream = comm_stream(dev)
+        self._stream.wait_stream(torch.cuda.current_stream(dev))
+        return self._stream
+
+    def _handle(self, side):
+        from .xgmi import _EventHandle
+        ev = torch.cuda.Event()
+        ev.record(side)
+        return _EventHandle(ev)
+
+    def _hold(self, nbytes, tmp_src, tmp_dst):
+        # one paced copy of this piece's bytes on the engine's CUs for the piece's link time
+        from ..ops import _ext
+        _ext.ext().paced_copy(tmp_dst, tmp_src, self.blocks, int(nbytes / self.gbps))
+
+    def all_gather_pieces_async(self, flat, stride, ranges):
+        side = self._side(flat.device)
+        hs = []
+        with torch.cuda.stream(side):
+            for lo, hi in ranges:
+                own = flat[self.rank * stride + lo:self.rank * stride + hi]
+                for d in range(1, self.world):
+                    dst = flat[d * stride + lo:d * stride + hi]
+                    if d == 1:
+                        self._hold(own.numel() * own.element_size(), own, dst)
+                    else:
+                        dst.copy_(own)
+                hs.append(self._handle(side))
+        flat.record_stream(side)
+        return hs
+
+    def reduce_scatter_piece_async(self, out, inp, lo, hi, stride):
+        side = self._side(out.device)
+        with torch.cuda.stream(side):
+            o = out[lo:hi]
+            first = inp[lo:hi]
+            self._hold(o.numel() * o.element_size(), first, o)       # o = this rank's own partial
+            for d in range(1, self.world):
+                o.add_(inp[d * stride + lo:d * stride + hi])
+            h = self._handle(side)
+        out.record_stream(side)
+        inp.record_stream(side)
+        return h
 
 
 def _delay_cycles() -> int:

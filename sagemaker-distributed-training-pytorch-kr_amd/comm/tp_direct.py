@@ -40,11 +40,11 @@ PIECES = max(1, int(os.environ.get("SMDT_TP_DIRECT_PIECES", "2")))
 
 
 class TpDirect:
-    def __init__(self, engine, group):
+    def __init__(self, engine, group, world: Optional[int] = None, rank: Optional[int] = None):
         self.eng = engine
         self.group = group
-        self.world = dist.get_world_size(group)
-        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group) if world is None else int(world)
+        self.rank = dist.get_rank(group) if rank is None else int(rank)
         self.calls = 0
         self.pieces_issued = 0
 
@@ -107,11 +107,53 @@ class TpDirect:
                 before_last_wait()
             fill_exchange_wait()      # queued W GEMMs beside the piece in flight (SMDT_W_FILL)
             hs[j].wait()
-            if chunk_fn is not None:
-                for d in range(1, ws):
-                    c = (r + d) % ws
-                    chunk_fn(c * n + a, total[c * n + a:c * n + b])
+            if chunk_fn is None:
+                continue
+            if len(pieces) == 1:
+                # whole chunks: the peers' rows are (at most) two contiguous runs, one GEMM each
+                for c0, c1 in ((r + 1, ws), (0, r)):
+                    if c1 > c0:
+                        chunk_fn(c0 * n, total[c0 * n:c1 * n])
+                continue
+            for d in range(1, ws):
+                c = (r + d) % ws
+                chunk_fn(c * n + a, total[c * n + a:c * n + b])
         return total
+
+    def start_all_gather(self, x: torch.Tensor):
+        """Issue the whole-chunk gather of ``x`` now and return (gathered buffer, handles) without
+        waiting (the sub-batch interleave, ``tensor_parallel.ag_start``: the other batch half's
+        phase runs beside the transfer); None when the engine does not take ``x``."""
+        x = x.contiguous()
+        if not (self.fits(x) and self.eng.use["all_gather"]):
+            return None
+        ws, r, n = self.world, self.rank, x.shape[0]
+        total = x.new_empty((n * ws,) + tuple(x.shape[1:]))
+        total[r * n:(r + 1) * n].copy_(x)
+        row = x[0].numel() if n else 0
+        hs = self.eng.all_gather_pieces_async(total.view(-1), n * row, [(0, n * row)])
+        if hs is None:
+            raise RuntimeError("TpDirect.start_all_gather: the xGMI engine refused an exchange fits() accepted")
+        self.calls += 1
+        self.pieces_issued += 1
+        return total, hs
+
+    def start_reduce_scatter(self, full: torch.Tensor):
+        """Issue the reduce-scatter of the complete [ws * n, ...] partials ``full`` now and return
+        (this rank's output chunk, handles) without waiting (sub-batch interleave); None when the
+        engine does not take ``full``."""
+        full = full.contiguous()
+        if not (self.fits(full) and self.eng.use["reduce_scatter"]):
+            return None
+        n = full.shape[0] // self.world
+        row = full[0].numel() if n else 0
+        out = full.new_empty((n,) + tuple(full.shape[1:]))
+        h = self.eng.reduce_scatter_piece_async(out.view(-1), full.view(-1), 0, n * row, n * row)
+        if h is None:
+            raise RuntimeError("TpDirect.start_reduce_scatter: the xGMI engine refused an exchange fits() accepted")
+        self.calls += 1
+        self.pieces_issued += 1
+        return out, [h]
 
     def reduce_scatter(self, partial_fn: Callable, full_shape, ref: torch.Tensor,
                        before_last_wait: Optional[Callable] = None) -> torch.Tensor:
@@ -138,6 +180,12 @@ class TpDirect:
         pieces = self._pieces(n, row * buf.element_size())
         hs = []
         for a, b in pieces:
+            if len(pieces) == 1:                 # whole chunks: every chunk's partial in ONE GEMM
+                partial_fn(0, ws * n, buf)
+                hs.append(self.eng.reduce_scatter_piece_async(out.view(-1), buf.view(-1), 0, n * row, n * row))
+                if hs[-1] is None:
+                    raise RuntimeError("TpDirect.reduce_scatter: the xGMI engine refused an exchange fits() accepted")
+                continue
             for d in range(1, ws + 1):           # the peers' rows first, this rank's own last
                 c = (r + d) % ws
                 partial_fn(c * n + a, b - a, buf[c * n + a:c * n + b])

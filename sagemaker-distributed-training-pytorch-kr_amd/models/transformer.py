@@ -643,8 +643,8 @@ class ParallelTransformer(nn.Module):
         cfg = self.cfg
         st = ps.get_state()
         return (_SUBBATCH == 2 and self.training and torch.is_grad_enabled() and cfg.sequence_parallel
-                and st.tp == 2 and st.cp == 1 and cfg.recompute_granularity != "full" and _PACK["idx"] is None
-                and tp.sp_gather_spec() is not None and x.dim() == 3 and x.shape[1] % 2 == 0
+                and st.cp == 1 and cfg.recompute_granularity != "full" and _PACK["idx"] is None
+                and tp.subbatch_capable(st) and x.dim() == 3 and x.shape[1] % 2 == 0
                 and len(self.layers) > 0)
 
     def _forward_subbatch(self, x, xbias, residual):

@@ -226,6 +226,12 @@ def initialize_emulated_tensor_parallel(tensor_model_parallel_size: int = 1,
                        embd_ranks=[0])
     st.initialized = True
     st.emulated = True
+    from ..comm.loopback import PacedDirectEngine, direct_standin
+    ds = direct_standin()
+    if ds is not None and tp in (4, 8):
+        # the TP4 / TP8 exchanges through a paced stand-in of the direct multi-link engine
+        from ..comm.tp_direct import TpDirect
+        st.tp_direct = TpDirect(PacedDirectEngine(tp, *ds), tg, world=tp, rank=0)
     _STATE = st
     return st
 

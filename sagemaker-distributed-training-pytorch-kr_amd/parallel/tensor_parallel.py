@@ -1684,9 +1684,26 @@ def _pending_key(x):
     return (x.data_ptr(), tuple(x.shape)) if _AG_PENDING else None
 
 
+def subbatch_capable(st) -> bool:
+    """Whether the TP exchanges can be started / left in flight for the sub-batch interleave: a
+    2-rank ring writing into producer-filled gather slots, or a TP4 / TP8 direct engine."""
+    if st.tp == 2:
+        return sp_gather_spec() is not None
+    return st.tp in (4, 8) and _direct(st.tp_group) is not None
+
+
 def ag_start(x, group):
-    """Issue the 2-rank ring all-gather of ``x`` now; the ``ag_ring`` call of x's consumer then
-    runs its local chunk's GEMM, waits, and runs the peer's chunk."""
+    """Issue the 2-rank ring all-gather of ``x`` now (TP4 / TP8: the direct engine's whole-chunk
+    gather); the ``ag_ring`` call of x's consumer then waits and runs ONE GEMM over all chunks
+    (the ring: its local chunk's GEMM, the wait, the peer's chunk)."""
+    td = _direct(group)
+    if td is not None:
+        started = td.start_all_gather(x)
+        if started is not None:     # (world-uniform: else the consumer's ag_ring gathers as usual)
+            total, hs = started
+            _AG_PENDING[(x.data_ptr(), tuple(x.shape))] = (total, hs, td.rank, x.shape[0])
+            SPLIT_STATS["ag_started"] += 1
+        return x
     ws, r, nxt, prv = _ring(group)
     assert ws == 2, "ag_start: 2-rank rings only"
     x = x.contiguous()
@@ -1713,7 +1730,8 @@ def rs_finish(t):
     del t._smdt_rs_pending
     works, incoming, _keep, group = pend
     _wait_works(works, group)
-    t.data.add_(incoming)    # outside autograd (t may be a view output of the linear's Function)
+    if incoming is not None:     # the ring's combine (the direct engine's output is the sum)
+        t.data.add_(incoming)    # outside autograd (t may be a view output of the linear's Function)
     try:
         _RS_PENDING.remove(t)
     except ValueError:
@@ -1871,6 +1889,22 @@ def rs_ring(partial_fn, group, full_shape, ref, before_last_wait=None, bulk=Fals
     straight into the engine's input buffer in row pieces, each piece reduce-scattered over every
     link of the group while the next piece's GEMMs run."""
     td = _direct(group)
+    if td is not None and _SPLIT["on"] and before_last_wait is None:
+        # sub-batch interleave: every chunk's partial in ONE GEMM, the reduce-scatter left in
+        # flight (``rs_finish`` waits) while the other half's phase runs
+        n = full_shape[0] // td.world
+        full = partial_fn(0, td.world * n, None)
+        started = td.start_reduce_scatter(full)
+        if started is None:
+            out = full.new_empty((n,) + tuple(full.shape[1:]))
+            dist.reduce_scatter_tensor(out, full.contiguous(), group=group)
+            return out
+        out, hs = started
+        out._smdt_rs_pending = (hs, None, full, group)
+        _RS_PENDING.append(out)
+        SPLIT_STATS["rs_deferred"] += 1
+        _cs.collective("reduce_scatter", group, _nbytes(out) * td.world, transport="xgmi")
+        return out
     if td is not None:
         out = td.reduce_scatter(partial_fn, full_shape, ref, before_last_wait)
         _cs.collective("reduce_scatter", group, _nbytes(out) * td.world, transport="xgmi")

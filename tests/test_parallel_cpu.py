@@ -68,6 +68,23 @@ def test_direct_tp_exchange_pieces_match_single_rank(tp, pieces):
 
 
 @pytest.mark.parametrize("pp", [1, 2])
+def test_direct_tp4_subbatch_interleave_matches_single_rank(pp):
+    """tp4 + SP over ``TpDirect`` (CPU stand-in engine) with the sub-batch interleave
+    (SMDT_SP_SUBBATCH=2): each half's whole-chunk gathers are started by ``ag_start`` and its
+    reduce-scatters left in flight (``TpDirect.start_all_gather`` / ``start_reduce_scatter``)
+    while the other half's phase runs. Loss and every gradient equal the single-rank model's, and
+    the interleave really ran over the engine."""
+    ref_loss, ref = W.gpt_reference()
+    outs = run_workers(W.gpt_tp_worker, 4 * pp, 4, pp, True, None, None, 2, 2)
+    for loss, grads, meta in outs:
+        _check_tp_grads(ref, grads, meta, 4)
+        assert meta["split"]["ag_started"] > 0 and meta["split"]["rs_deferred"] > 0
+        assert meta["direct_calls"] > 0
+    last = [o for o in outs if o[2]["pp_rank"] == pp - 1][0]
+    torch.testing.assert_close(last[0].view(-1), ref_loss.view(-1), atol=2e-4, rtol=2e-4)
+
+
+@pytest.mark.parametrize("pp", [1, 2])
 def test_ring_pieces_match_single_rank(pp):
     """tp2 + SP with every 2-rank ring exchange in 2 row pieces (SMDT_RING_PIECES=2: the peer
     chunk's GEMM per landed piece, the reduce-scatter's partial sent piece by piece): loss and

@@ -451,3 +451,53 @@ def test_w_fillers_match_grouped_flush_on_gpu(monkeypatch, stream):
     torch.testing.assert_close(l1, l0, atol=1e-4, rtol=0)
     scale = g0.abs().max().item()
     assert scale > 0 and (g1 - g0).abs().max().item() <= 1e-3 * scale
+
+
+def test_direct_engine_standin_matches_ring_emulation(monkeypatch):
+    """One emulated tp4 + SP rank with SMDT_LINK_STANDIN=direct: the SP exchanges go through
+    ``TpDirect`` (row pieces, per-piece handles) over the paced stand-in of the direct engine
+    (comm/loopback.PacedDirectEngine) instead of the loopback ring. The stand-in's values are the
+    loopback ring's (gather = own shard in every slot, reduce-scatter = sum of this rank's
+    partials), so losses and the fp32 gradient buffer agree with the ring run to bf16 add-order
+    rounding; with W fillers on, fillers ran inside the direct waits."""
+    from smdt_amd.models.gpt import GPTModel
+    from smdt_amd.models.transformer import TransformerConfig
+    from smdt_amd.parallel import state as ps
+    from smdt_amd.parallel.distributed import DistributedDataParallel as DDP
+    from smdt_amd.train.schedules import forward_backward_no_pipelining
+    out = []
+    for standin in ("", "direct:64:32"):
+        monkeypatch.setenv("SMDT_LINK_STANDIN", standin)
+        monkeypatch.setattr(tp, "W_FILL", bool(standin))
+        tp.DEFERRED_WGRAD.stats.pop("fills", None)
+        ps.destroy_model_parallel()
+        st = ps.initialize_emulated_tensor_parallel(4, 1)
+        try:
+            td = getattr(st, "tp_direct", None)
+            assert (td is not None) == bool(standin)
+            cfg = TransformerConfig(num_layers=2, hidden_size=256, num_attention_heads=4, padded_vocab_size=1024,
+                                    max_position_embeddings=256, hidden_dropout=0.0, attention_dropout=0.0,
+                                    params_dtype=torch.bfloat16, sequence_parallel=True, seed=7)
+            model = GPTModel(cfg, device="cuda")
+            ddp = DDP(model, grad_dtype=torch.float32)
+            g = torch.Generator(device="cuda").manual_seed(13)
+            t = torch.randint(0, 1000, (6, 257), device="cuda", generator=g)
+            data = iter([(t[2 * i:2 * i + 2, :-1], t[2 * i:2 * i + 2, 1:]) for i in range(3)])
+
+            def fstep(di, m):
+                x, y = next(di)
+                o = m(x, None, None, labels=y)
+                return o, (lambda z: (z.float().mean(), {"loss": z.detach().float().mean()}))
+            ddp.zero_grad_buffer()
+            losses = forward_backward_no_pipelining(fstep, data, ddp, 3, split_backward=True)
+            ddp.finish_grad_sync()
+            torch.cuda.synchronize()
+            out.append((torch.stack([d["loss"] for d in losses]).cpu(), ddp.grad_data.clone(),
+                        tp.DEFERRED_WGRAD.stats.get("fills", 0), td.pieces_issued if td else 0))
+        finally:
+            ps.destroy_model_parallel()
+    (l0, g0, _, p0), (l1, g1, f1, p1) = out
+    assert p0 == 0 and p1 > 0 and f1 > 0
+    torch.testing.assert_close(l1, l0, atol=2e-2, rtol=0)
+    scale = g0.abs().max().item()
+    assert scale > 0 and (g1 - g0).abs().max().item() <= 3e-2 * scale
