@@ -35,8 +35,11 @@ import torch.distributed as dist
 
 TUNED: dict = {}
 # Row pieces per direct exchange (SMDT_TP_DIRECT_PIECES): piece j's GEMMs start when piece j has
-# landed (all-gather) / piece j's reduce-scatter runs beside piece j + 1's GEMMs. 1 = whole chunks.
-PIECES = max(1, int(os.environ.get("SMDT_TP_DIRECT_PIECES", "2")))
+# landed (all-gather) / piece j's reduce-scatter runs beside piece j + 1's GEMMs. 1 = whole chunks,
+# the peers' rows in one GEMM per contiguous run and every partial in one GEMM: measured fastest on
+# the emulated GPT-3 tp4 stage under the paced engine stand-in (532 vs 590 ms at 2 pieces, 694 at
+# 4: the per-piece GEMMs of M = 1,024 rows fill a quarter of the chip; profiles/r6_direct/).
+PIECES = max(1, int(os.environ.get("SMDT_TP_DIRECT_PIECES", "1")))
 
 
 class TpDirect:
@@ -101,12 +104,12 @@ class TpDirect:
         self.pieces_issued += len(pieces)
         if chunk_fn is not None:
             chunk_fn(r * n, x)                   # beside the first piece
-        from ..parallel.tensor_parallel import fill_exchange_wait
+        from ..parallel.tensor_parallel import _wait_works, fill_exchange_wait
         for j, (a, b) in enumerate(pieces):
             if j == len(pieces) - 1 and before_last_wait is not None:
                 before_last_wait()
             fill_exchange_wait()      # queued W GEMMs beside the piece in flight (SMDT_W_FILL)
-            hs[j].wait()
+            _wait_works([hs[j]], self.group)       # (counted as TP exchange wait by comm/stats)
             if chunk_fn is None:
                 continue
             if len(pieces) == 1:
@@ -197,10 +200,9 @@ class TpDirect:
         self.pieces_issued += len(pieces)
         if before_last_wait is not None:
             before_last_wait()
-        from ..parallel.tensor_parallel import fill_exchange_wait
+        from ..parallel.tensor_parallel import _wait_works, fill_exchange_wait
         fill_exchange_wait()          # queued W GEMMs beside the last pieces in flight (SMDT_W_FILL)
-        for h in hs:
-            h.wait()
+        _wait_works(hs, self.group)
         return out
 
 

@@ -13,6 +13,15 @@ SMDT_LINK_STANDIN=192:32 run g0_ring_overlap 500 python bench.py $G
 SMDT_LINK_STANDIN=direct:64:32 run g0_direct_overlap 500 python bench.py $G
 SMDT_LINK_STANDIN=direct:64:32 SMDT_W_FILL=0 SMDT_RING_GEMM_TN=0 run g0_direct_nofill 500 python bench.py $G
 SMDT_LINK_STANDIN=direct:64:32 SMDT_TP_DIRECT_PIECES=4 run g0_direct_p4 500 python bench.py $G
+elif [ "${PASS:-1}" = 4 ]; then
+# pass 4: the interleave's short phases on a chain stream per half (SMDT_SP_SUBBATCH_CHAIN=1)
+run test4 400 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_parallel_gpu.py tests/test_graph_gpu.py -k "direct_engine_standin or subbatch"
+SMDT_LINK_STANDIN=direct:64:32 SMDT_TP_DIRECT_PIECES=1 SMDT_SP_SUBBATCH=2 run g0_direct_p1_chain 500 python bench.py $G
+SMDT_LINK_STANDIN=direct:64:32 SMDT_TP_DIRECT_PIECES=1 run g0_direct_p1_c 500 python bench.py $G
+N8="--emulate-tp 2 --micro-batch-size 32 --grad-accum 8 --num-layers 13 --emulate-first-stage --steps 6 --warmup 3"
+SMDT_LINK_STANDIN=relay run s0_relay 300 python bench.py $N8
+SMDT_LINK_STANDIN=relay SMDT_SP_SUBBATCH=2 run s0_relay_chain 300 python bench.py $N8
+SMDT_LINK_STANDIN=relay SMDT_SP_SUBBATCH=2 SMDT_SP_SUBBATCH_CHAIN=0 run s0_relay_sub_inline 300 python bench.py $N8
 elif [ "${PASS:-1}" = 3 ]; then
 # pass 3: whole chunks (merged peer GEMMs) with and without the sub-batch interleave over the engine
 SMDT_LINK_STANDIN=direct:64:32 SMDT_TP_DIRECT_PIECES=1 run g0_direct_p1_b 500 python bench.py $G

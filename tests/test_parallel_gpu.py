@@ -453,13 +453,17 @@ def test_w_fillers_match_grouped_flush_on_gpu(monkeypatch, stream):
     assert scale > 0 and (g1 - g0).abs().max().item() <= 1e-3 * scale
 
 
-def test_direct_engine_standin_matches_ring_emulation(monkeypatch):
+@pytest.mark.parametrize("sub", [0, 2])
+def test_direct_engine_standin_matches_ring_emulation(monkeypatch, sub):
     """One emulated tp4 + SP rank with SMDT_LINK_STANDIN=direct: the SP exchanges go through
     ``TpDirect`` (row pieces, per-piece handles) over the paced stand-in of the direct engine
     (comm/loopback.PacedDirectEngine) instead of the loopback ring. The stand-in's values are the
     loopback ring's (gather = own shard in every slot, reduce-scatter = sum of this rank's
     partials), so losses and the fp32 gradient buffer agree with the ring run to bf16 add-order
-    rounding; with W fillers on, fillers ran inside the direct waits."""
+    rounding; with W fillers on, fillers ran inside the direct waits. ``sub`` = 2: the direct run
+    with the sub-batch interleave (whole-chunk exchanges started early, the short phases on a
+    chain stream per half)."""
+    import smdt_amd.models.transformer as T
     from smdt_amd.models.gpt import GPTModel
     from smdt_amd.models.transformer import TransformerConfig
     from smdt_amd.parallel import state as ps
@@ -469,7 +473,9 @@ def test_direct_engine_standin_matches_ring_emulation(monkeypatch):
     for standin in ("", "direct:64:32"):
         monkeypatch.setenv("SMDT_LINK_STANDIN", standin)
         monkeypatch.setattr(tp, "W_FILL", bool(standin))
+        monkeypatch.setattr(T, "_SUBBATCH", sub if standin else 0)
         tp.DEFERRED_WGRAD.stats.pop("fills", None)
+        started = tp.SPLIT_STATS["ag_started"]
         ps.destroy_model_parallel()
         st = ps.initialize_emulated_tensor_parallel(4, 1)
         try:
@@ -494,7 +500,9 @@ def test_direct_engine_standin_matches_ring_emulation(monkeypatch):
             torch.cuda.synchronize()
             out.append((torch.stack([d["loss"] for d in losses]).cpu(), ddp.grad_data.clone(),
                         tp.DEFERRED_WGRAD.stats.get("fills", 0), td.pieces_issued if td else 0))
+            assert (tp.SPLIT_STATS["ag_started"] > started) == bool(standin and sub)
         finally:
+            tp.DEFERRED_WGRAD.merge_repeats = False
             ps.destroy_model_parallel()
     (l0, g0, _, p0), (l1, g1, f1, p1) = out
     assert p0 == 0 and p1 > 0 and f1 > 0
