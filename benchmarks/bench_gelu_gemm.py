@@ -1,10 +1,10 @@
 """The GeLU-MLP GEMMs of the GPT-2 345M N = 1 step (fc1 forward with bias + GeLU, fc2 dgrad with the
-GeLU backward), three ways, at the bench shape (mbs 64 x seq 1024 = 65,536 tokens, h 1024, ffn 4096):
+GeLU backward), two ways, at the bench shape (mbs 64 x seq 1024 = 65,536 tokens, h 1024, ffn 4096):
 
   * ``gemm_tn``: the hand-written MFMA kernel with its epilogues (csrc/kernels/gemm_tn.hip, the
     default K5 path);
-  * ``blaslt``: hipBLASLt with its own fused epilogues, GELU_AUX_BIAS / DGELU (csrc/blaslt.cpp
-    ``gemm_gelu``);
+  (hipBLASLt's own GELU_AUX_BIAS / DGELU epilogues were measured at commit 69dd621 and removed:
+    no gfx950 solution for GELU_AUX*, DGELU 3.5x slower and wrong; profiles/r6_gelu_neg/);
   * ``lib+ew``: the library GEMM (torch / hipBLASLt) and a separate elementwise pass.
 
 Also checks each against an fp32 reference (tanh and erf GeLU) and prints one JSON line.
@@ -88,24 +88,6 @@ def main():
     torch.cuda.synchronize()
     res["gemm_tn_dgelu"] = {"us": round(timed(bwd_tn, a.reps), 1), "err_tanh": rel(dz[:R], dz_tanh),
                             "err_erf": rel(dz[:R], dz_erf)}
-    # ---- hipBLASLt epilogues
-    ok0 = C.gemm_gelu(x, w1, b1, act, pre, 0)
-    pre_bl = pre_keep + b1    # hipBLASLt's DGELU aux: the pre-activation WITH the bias
-    ok1 = C.gemm_gelu(dy, w2, nob, dz, pre_bl, 1)
-    torch.cuda.synchronize()
-    res["blaslt_supported"] = [bool(ok0), bool(ok1)]
-    if ok0:
-        C.gemm_gelu(x, w1, b1, act, pre, 0)
-        torch.cuda.synchronize()
-        e = {"err_tanh": rel(act[:R], act_tanh), "err_erf": rel(act[:R], act_erf), "err_pre": rel(pre[:R], pre_ref)}
-        e["us"] = round(timed(lambda: C.gemm_gelu(x, w1, b1, act, pre, 0), a.reps), 1)
-        res["blaslt_fwd"] = e
-    if ok1:
-        C.gemm_gelu(dy, w2, nob, dz, pre_bl, 1)
-        torch.cuda.synchronize()
-        e = {"err_tanh": rel(dz[:R], dz_tanh), "err_erf": rel(dz[:R], dz_erf)}
-        e["us"] = round(timed(lambda: C.gemm_gelu(dy, w2, nob, dz, pre_bl, 1), a.reps), 1)
-        res["blaslt_dgelu"] = e
     # ---- library GEMM + elementwise
     res["lib_fwd_gemm_us"] = round(timed(lambda: torch.matmul(x, w1.t(), out=pre), a.reps), 1)
     res["lib_dgrad_gemm_us"] = round(timed(lambda: torch.matmul(dy, w2, out=dz), a.reps), 1)

@@ -216,192 +216,9 @@ bool wgrad_accumulate(torch::Tensor main_grad, torch::Tensor dy, torch::Tensor x
 }
 
 
-// ---- GEMM + GeLU epilogues (the fc1 forward / fc2 dgrad of a GeLU MLP, K5) -------------------
-// epi 0: out[M,N] = gelu(x[M,K] . w[N,K]^T + bias[N]), aux[M,N] = the pre-activation (GELU_AUX_BIAS)
-// epi 1: out[M,N] = (x[M,K] . w[K,N]) * gelu'(aux[M,N])                               (DGELU)
-// The library's own fused epilogues, as the A/B partner of the hand-written gemm_tn epilogues
-// (csrc/kernels/gemm_tn.hip): SMDT_GELU_GEMM=blaslt.
-struct ActPlan {
-  hipblasLtMatmulDesc_t desc = nullptr;
-  hipblasLtMatrixLayout_t la = nullptr, lb = nullptr, lc = nullptr;
-  hipblasLtMatmulAlgo_t algo;
-  size_t ws = 0;
-  bool ok = false;
-};
-std::map<std::tuple<int, int64_t, int64_t, int64_t, int, int>, ActPlan> g_act_plans;
-
-void act_set_ptrs(ActPlan& p, int epi, const void* bias, const void* aux, int64_t ld) {
-  const hipblasLtEpilogue_t e = epi == 0 ? HIPBLASLT_EPILOGUE_GELU_AUX_BIAS : HIPBLASLT_EPILOGUE_DGELU;
-  hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_EPILOGUE, &e, sizeof(e));
-  if (epi == 0) hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &bias, sizeof(bias));
-  hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_EPILOGUE_AUX_POINTER, &aux, sizeof(aux));
-  hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_EPILOGUE_AUX_LD, &ld, sizeof(ld));
-}
-
-ActPlan make_act_plan(DevState& st, int64_t M, int64_t N, int64_t K, hipDataType t, int epi,
-                      const torch::TensorOptions& opts) {
-  // Column-major view: D^T[N x M] (ld N) = op(A) . B, B = x^T [K x M] (ld K);
-  // epi 0: A = w as [K x N] (ld K), op T; epi 1: A = w as [N x K] (ld N), op N.
-  ActPlan p;
-  if (!chk(hipblasLtMatmulDescCreate(&p.desc, HIPBLAS_COMPUTE_32F, HIP_R_32F))) return p;
-  hipblasOperation_t ta = epi == 0 ? HIPBLAS_OP_T : HIPBLAS_OP_N, tb = HIPBLAS_OP_N;
-  hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_TRANSA, &ta, sizeof(ta));
-  hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_TRANSB, &tb, sizeof(tb));
-  if (epi == 0) {
-    hipDataType bt = t;
-    hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_BIAS_DATA_TYPE, &bt, sizeof(bt));
-  }
-  hipDataType at_ = t;
-  hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_EPILOGUE_AUX_DATA_TYPE, &at_, sizeof(at_));
-  if (!chk(epi == 0 ? hipblasLtMatrixLayoutCreate(&p.la, t, K, N, K) : hipblasLtMatrixLayoutCreate(&p.la, t, N, K, N)))
-    return p;
-  if (!chk(hipblasLtMatrixLayoutCreate(&p.lb, t, K, M, K))) return p;
-  if (!chk(hipblasLtMatrixLayoutCreate(&p.lc, t, N, M, N))) return p;
-  // scratch operands for the heuristic's support checks and the timing below
-  torch::Tensor x = torch::randn({M, K}, opts), w = torch::randn({N * K}, opts), bias = torch::randn({N}, opts);
-  torch::Tensor out = torch::empty({M, N}, opts), aux = torch::randn({M, N}, opts);
-  act_set_ptrs(p, epi, bias.data_ptr(), aux.data_ptr(), N);
-  hipblasLtMatmulPreference_t pref;
-  if (!chk(hipblasLtMatmulPreferenceCreate(&pref))) return p;
-  size_t wsb = kWorkspace;
-  hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &wsb, sizeof(wsb));
-  constexpr int kCand = 16;
-  hipblasLtMatmulHeuristicResult_t res[kCand];
-  int n = 0;
-  bool got = chk(hipblasLtMatmulAlgoGetHeuristic(st.handle, p.desc, p.la, p.lb, p.lc, p.lc, pref, kCand, res, &n));
-  hipblasLtMatmulPreferenceDestroy(pref);
-  if (!got || n == 0) return p;
-  const float alpha = 1.f, beta = 0.f;
-  hipStream_t stream = c10::hip::getCurrentHIPStream().stream();
-  hipEvent_t e0, e1;
-  hipEventCreate(&e0);
-  hipEventCreate(&e1);
-  int best = -1;
-  float best_ms = 1e30f;
-  for (int i = 0; i < n; ++i) {
-    if (res[i].state != HIPBLAS_STATUS_SUCCESS || res[i].workspaceSize > kWorkspace) continue;
-    bool okc = true;
-    for (int r = 0; r < 2 && okc; ++r)
-      okc = chk(hipblasLtMatmul(st.handle, p.desc, &alpha, w.data_ptr(), p.la, x.data_ptr(), p.lb, &beta,
-                                out.data_ptr(), p.lc, out.data_ptr(), p.lc, &res[i].algo, st.workspace.data_ptr(),
-                                res[i].workspaceSize, stream));
-    if (!okc) continue;
-    hipEventRecord(e0, stream);
-    for (int r = 0; r < 3; ++r)
-      hipblasLtMatmul(st.handle, p.desc, &alpha, w.data_ptr(), p.la, x.data_ptr(), p.lb, &beta, out.data_ptr(), p.lc,
-                      out.data_ptr(), p.lc, &res[i].algo, st.workspace.data_ptr(), res[i].workspaceSize, stream);
-    hipEventRecord(e1, stream);
-    hipEventSynchronize(e1);
-    float ms = 0.f;
-    hipEventElapsedTime(&ms, e0, e1);
-    if (ms < best_ms) {
-      best_ms = ms;
-      best = i;
-    }
-  }
-  hipEventDestroy(e0);
-  hipEventDestroy(e1);
-  if (best >= 0) {
-    p.algo = res[best].algo;
-    p.ws = res[best].workspaceSize;
-    p.ok = true;
-  }
-  return p;
-}
-
-// Returns false (and does nothing) when hipBLASLt has no algorithm for the shape / epilogue.
-bool gemm_gelu(torch::Tensor x, torch::Tensor w, torch::Tensor bias, torch::Tensor out, torch::Tensor aux, int64_t epi) {
-  TORCH_CHECK(epi == 0 || epi == 1, "gemm_gelu: epi must be 0 (GELU_AUX_BIAS) or 1 (DGELU)");
-  if (!x.is_cuda() || x.dim() != 2 || w.dim() != 2 || out.dim() != 2 || aux.dim() != 2) return false;
-  const auto dt = x.scalar_type();
-  if (dt != at::kBFloat16 && dt != at::kHalf) return false;
-  for (auto* t : {&w, &out, &aux})
-    if (t->scalar_type() != dt || !t->is_contiguous()) return false;
-  if (!x.is_contiguous()) return false;
-  const int64_t M = x.size(0), K = x.size(1);
-  const int64_t N = epi == 0 ? w.size(0) : w.size(1);
-  if ((epi == 0 ? w.size(1) : w.size(0)) != K) return false;
-  if (out.size(0) != M || out.size(1) != N || aux.size(0) != M || aux.size(1) != N) return false;
-  if (epi == 0 && (!bias.defined() || bias.numel() != N || bias.scalar_type() != dt || !bias.is_contiguous()))
-    return false;
-  const hipDataType t = dt == at::kBFloat16 ? HIP_R_16BF : HIP_R_16F;
-  std::lock_guard<std::mutex> lk(g_mu);
-  const int dev = x.get_device();
-  DevState& st = state_for(dev, x.options());
-  auto key = std::make_tuple(dev, M, N, K, (int)t, (int)epi);
-  auto it = g_act_plans.find(key);
-  if (it == g_act_plans.end()) it = g_act_plans.emplace(key, make_act_plan(st, M, N, K, t, (int)epi, x.options())).first;
-  ActPlan& p = it->second;
-  if (!p.ok) return false;
-  act_set_ptrs(p, (int)epi, epi == 0 ? bias.data_ptr() : nullptr, aux.data_ptr(), N);
-  const float alpha = 1.f, beta = 0.f;
-  hipStream_t stream = c10::hip::getCurrentHIPStream().stream();
-  hipblasStatus_t s = hipblasLtMatmul(st.handle, p.desc, &alpha, w.data_ptr(), p.la, x.data_ptr(), p.lb, &beta,
-                                      out.data_ptr(), p.lc, out.data_ptr(), p.lc, &p.algo, st.workspace.data_ptr(),
-                                      p.ws, stream);
-  TORCH_CHECK(chk(s), "hipblasLtMatmul (gemm_gelu) failed: status ", (int)s);
-  return true;
-}
-
-// Diagnostics: how many heuristic candidates hipBLASLt returns for an (M, N, K) bf16 GEMM with the
-// epilogue ``epi`` (hipblasLtEpilogue_t value), aux type code (0 unset, 1 bf16, 2 fp32), bias on /
-// off, and the D type (1 bf16, 2 fp32). -1: descriptor / layout error.
-int64_t gelu_probe(int64_t M, int64_t N, int64_t K, int64_t epi, int64_t aux_code, bool with_bias, int64_t trans_a,
-                   int64_t d_code) {
-  std::lock_guard<std::mutex> lk(g_mu);
-  DevState& st = state_for(0, torch::TensorOptions().device(torch::kCUDA, 0));
-  const hipDataType t = HIP_R_16BF, dt = d_code == 2 ? HIP_R_32F : HIP_R_16BF;
-  hipblasLtMatmulDesc_t desc;
-  if (!chk(hipblasLtMatmulDescCreate(&desc, HIPBLAS_COMPUTE_32F, HIP_R_32F))) return -1;
-  hipblasOperation_t ta = trans_a ? HIPBLAS_OP_T : HIPBLAS_OP_N, tb = HIPBLAS_OP_N;
-  hipblasLtMatmulDescSetAttribute(desc, HIPBLASLT_MATMUL_DESC_TRANSA, &ta, sizeof(ta));
-  hipblasLtMatmulDescSetAttribute(desc, HIPBLASLT_MATMUL_DESC_TRANSB, &tb, sizeof(tb));
-  hipblasLtEpilogue_t e = (hipblasLtEpilogue_t)epi;
-  hipblasLtMatmulDescSetAttribute(desc, HIPBLASLT_MATMUL_DESC_EPILOGUE, &e, sizeof(e));
-  torch::Tensor buf = torch::empty({M * N * 4 + N * 4}, torch::TensorOptions().device(torch::kCUDA, 0).dtype(at::kByte));
-  void* bp = buf.data_ptr();
-  if (with_bias) {
-    hipDataType bt = t;
-    hipblasLtMatmulDescSetAttribute(desc, HIPBLASLT_MATMUL_DESC_BIAS_DATA_TYPE, &bt, sizeof(bt));
-    hipblasLtMatmulDescSetAttribute(desc, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &bp, sizeof(bp));
-  }
-  if (aux_code) {
-    hipDataType at_ = aux_code == 2 ? HIP_R_32F : HIP_R_16BF;
-    hipblasLtMatmulDescSetAttribute(desc, HIPBLASLT_MATMUL_DESC_EPILOGUE_AUX_DATA_TYPE, &at_, sizeof(at_));
-  }
-  if (epi >= 128) {
-    int64_t ld = N;
-    hipblasLtMatmulDescSetAttribute(desc, HIPBLASLT_MATMUL_DESC_EPILOGUE_AUX_POINTER, &bp, sizeof(bp));
-    hipblasLtMatmulDescSetAttribute(desc, HIPBLASLT_MATMUL_DESC_EPILOGUE_AUX_LD, &ld, sizeof(ld));
-  }
-  hipblasLtMatrixLayout_t la, lb, lc;
-  hipblasLtMatrixLayoutCreate(&la, t, trans_a ? K : N, trans_a ? N : K, trans_a ? K : N);
-  hipblasLtMatrixLayoutCreate(&lb, t, K, M, K);
-  hipblasLtMatrixLayoutCreate(&lc, dt, N, M, N);
-  hipblasLtMatmulPreference_t pref;
-  hipblasLtMatmulPreferenceCreate(&pref);
-  size_t wsb = kWorkspace;
-  hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &wsb, sizeof(wsb));
-  hipblasLtMatmulHeuristicResult_t res[16];
-  int n = 0;
-  hipblasStatus_t s = hipblasLtMatmulAlgoGetHeuristic(st.handle, desc, la, lb, lc, lc, pref, 16, res, &n);
-  hipblasLtMatmulPreferenceDestroy(pref);
-  hipblasLtMatrixLayoutDestroy(la);
-  hipblasLtMatrixLayoutDestroy(lb);
-  hipblasLtMatrixLayoutDestroy(lc);
-  hipblasLtMatmulDescDestroy(desc);
-  return chk(s) ? n : -100 - (int64_t)s;
-}
-
 }  // namespace
 
 void register_blaslt(pybind11::module_& m) {
-  m.def("gelu_probe", &gelu_probe, "hipBLASLt heuristic candidate count for a GeLU-epilogue GEMM (diagnostics)");
-  m.def("gemm_gelu", &gemm_gelu,
-        "hipBLASLt GEMM with a GeLU epilogue: epi 0 out = gelu(x @ w^T + bias), aux = pre-activation; "
-        "epi 1 out = (x @ w) * gelu'(aux). Returns False if unsupported",
-        pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("bias"), pybind11::arg("out"), pybind11::arg("aux"),
-        pybind11::arg("epi"));
   m.def("wgrad_accumulate", &wgrad_accumulate,
         "main_grad(fp32 [N,K]) += dy([M,N])^T @ x([M,K]) in one hipBLASLt GEMM (beta = 1); "
         "returns False if unsupported");
