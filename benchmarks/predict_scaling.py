@@ -78,6 +78,13 @@ RUNS = {
 STANDIN_ENV = {"SMDT_LINK_STANDIN": "relay", "SMDT_RING_GEMM_TN": "1", "SMDT_W_FILL": "1"}
 RUNS["tp2pp2_stage0_standin"] = RUNS["tp2pp2_stage0"]
 RUNS["tp2pp2_stage1_standin"] = RUNS["tp2pp2_stage1"]
+# the same replica batch split differently, exchanges measured: 4 x 64 (bigger chunk GEMMs and
+# exchanges, twice the bubble per micro-batch) and 16 x 16 (smaller ones, half the bubble)
+_N8_16 = ["--emulate-tp", "2", "--micro-batch-size", "16", "--grad-accum", "16", "--phase-probe", "16"]
+RUNS["tp2pp2_mb64_stage0_standin"] = RUNS["tp2pp2_mb64_stage0"]
+RUNS["tp2pp2_mb64_stage1_standin"] = RUNS["tp2pp2_mb64_stage1"]
+RUNS["tp2pp2_mb16_stage0_standin"] = ["--num-layers", "13", "--emulate-first-stage"] + _N8_16
+RUNS["tp2pp2_mb16_stage1_standin"] = ["--num-layers", "11", "--emulate-last-stage"] + _N8_16
 # GPT-3 tp4 stages with the SP exchanges MEASURED: TpDirect's row pieces over a paced stand-in of
 # the direct engine (comm/loopback.PacedDirectEngine: 3 links at LINK_GBPS, 32 workgroups)
 DIRECT_ENV = {"SMDT_LINK_STANDIN": f"direct:{LINK_GBPS:g}:32", "SMDT_RING_GEMM_TN": "1", "SMDT_W_FILL": "1"}
@@ -85,6 +92,7 @@ RUNS["gpt3_tp4_stage0_direct"] = RUNS["gpt3_tp4_stage0"]
 RUNS["gpt3_tp4_stage1_direct"] = RUNS["gpt3_tp4_stage1"]
 _COPY_ENV = {"SMDT_W_FILL": "0", "SMDT_RING_GEMM_TN": "0"}   # compute-only runs: no overlap machinery
 RUN_ENV = {"tp2pp2_stage0_standin": STANDIN_ENV, "tp2pp2_stage1_standin": STANDIN_ENV,
+           **{f"tp2pp2_mb{m}_stage{i}_standin": STANDIN_ENV for m in (16, 64) for i in (0, 1)},
            "gpt3_tp4_stage0_direct": DIRECT_ENV, "gpt3_tp4_stage1_direct": DIRECT_ENV,
            **{k: _COPY_ENV for k in ("tp2pp2_stage0", "tp2pp2_stage1", "tp2pp2_stage1_even",
                                      "tp2pp2_mb64_stage0", "tp2pp2_mb64_stage1")}}
@@ -184,6 +192,14 @@ def predict(m: dict) -> list:
                                f"tp2pp2dp2+sp+zero1 13|11, TP exchanges MEASURED (paced relay stand-in; {flags})"):
             if r["layout"].endswith("zbh2"):
                 rows.append({"N": 8, "model": "gpt2-345m", **r})
+    for mbs, nmb in ((64, 4), (16, 16)):
+        k0, k1 = f"tp2pp2_mb{mbs}_stage0_standin", f"tp2pp2_mb{mbs}_stage1_standin"
+        if k0 in m and k1 in m:
+            actm = (S // 2) * mbs * H * 2
+            for r in pipeline_rows(m, k0, k1, nmb, 2, actm, dp_tail + embd + 0.5, tok1 * 8,
+                                   f"tp2pp2dp2+sp+zero1 13|11, {nmb} x {mbs}, TP exchanges MEASURED (paced relay stand-in)"):
+                if r["layout"].endswith("zbh2"):
+                    rows.append({"N": 8, "model": "gpt2-345m", **r})
     if "tp2pp2_mb64_stage0" in m and "tp2pp2_mb64_stage1" in m:
         act64 = (S // 2) * 64 * H * 2
         for r in pipeline_rows(m, "tp2pp2_mb64_stage0", "tp2pp2_mb64_stage1", 4, 2, act64, dp_tail + embd + 0.5,
