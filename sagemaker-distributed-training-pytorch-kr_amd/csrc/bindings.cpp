@@ -610,19 +610,8 @@ void fa_check(const Tensor& t, const char* n) {
 
 // `out` (optional) is a preallocated [B, S, H, D] view with any strides (e.g. the [s, b, h]
 // activation layout used by the transformer trunk).
-// keep (optional): int32 buffer of keep_words(B, H, S) words for the dropout keep words the
-// backward's dQ kernel then reads (flash_bwd's `keep`) instead of re-deriving them.
-int64_t keep_words(int64_t B, int64_t H, int64_t S) { return B * H * (S / 64) * S * 2; }
-
-void keep_check(const OptT& keep, int64_t B, int64_t H, int64_t S) {
-  if (!keep) return;
-  need_cuda(*keep, "keep");
-  TORCH_CHECK(keep->scalar_type() == at::kInt && keep->is_contiguous() && keep->numel() == keep_words(B, H, S),
-              "flash: keep must be a contiguous int32 buffer of keep_words(B, H, S) words");
-}
-
 std::vector<Tensor> flash_fwd(Tensor q, Tensor k, Tensor v, double scale, bool causal, OptT out,
-                              double dropout_p, int64_t seed, int64_t offset, OptT keep) {
+                              double dropout_p, int64_t seed, int64_t offset) {
   fa_check(q, "q"); fa_check(k, "k"); fa_check(v, "v");
   TORCH_CHECK(k.scalar_type() == q.scalar_type() && v.scalar_type() == q.scalar_type(), "flash: q/k/v dtypes differ");
   const int64_t B = q.size(0), S = q.size(1), H = q.size(2), D = q.size(3), Hkv = k.size(2);
@@ -638,13 +627,11 @@ std::vector<Tensor> flash_fwd(Tensor q, Tensor k, Tensor v, double scale, bool c
   }
   auto lse = torch::empty({B, H, S}, q.options().dtype(at::kFloat));
   TORCH_CHECK(o.scalar_type() == q.scalar_type(), "flash: out dtype mismatch");
-  keep_check(keep, B, H, S);
   check(smdt_flash_fwd(dcode(q), q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr<float>(),
                        (int)B, (int)H, (int)Hkv, (int)S, (int)D, q.stride(0), q.stride(1), q.stride(2),
                        k.stride(0), k.stride(1), k.stride(2), v.stride(0), v.stride(1), v.stride(2),
                        o.stride(0), o.stride(1), o.stride(2), (float)scale, causal ? 1 : 0, (float)dropout_p,
-                       (uint64_t)seed, (uint64_t)offset,
-                       keep ? reinterpret_cast<uint32_t*>(keep->data_ptr<int>()) : nullptr, cur_stream()),
+                       (uint64_t)seed, (uint64_t)offset, cur_stream()),
         "flash_fwd");
   return {o, lse};
 }
@@ -653,7 +640,7 @@ std::vector<Tensor> flash_fwd(Tensor q, Tensor k, Tensor v, double scale, bool c
 // views into one fused d(QKV) buffer so the QKV projection backward needs no concatenation.
 std::vector<Tensor> flash_bwd(Tensor q, Tensor k, Tensor v, Tensor o, Tensor dout, Tensor lse,
                               double scale, bool causal, OptT dq_out, OptT dk_out, OptT dv_out,
-                              double dropout_p, int64_t seed, int64_t offset, OptT keep) {
+                              double dropout_p, int64_t seed, int64_t offset) {
   fa_check(q, "q"); fa_check(k, "k"); fa_check(v, "v"); fa_check(o, "o");
   TORCH_CHECK(k.scalar_type() == q.scalar_type() && v.scalar_type() == q.scalar_type() &&
               o.scalar_type() == q.scalar_type() && dout.scalar_type() == q.scalar_type(), "flash_bwd: dtypes differ");
@@ -673,7 +660,6 @@ std::vector<Tensor> flash_bwd(Tensor q, Tensor k, Tensor v, Tensor o, Tensor dou
     return torch::empty({B, S, heads, D}, q.options());
   };
   Tensor dq = mk(dq_out, H, "dq"), dk = mk(dk_out, Hkv, "dk"), dv = mk(dv_out, Hkv, "dv");
-  keep_check(keep, B, H, S);
   // -delta' rows | (unused) | 16-byte term rows of -lse log2 e and of -delta' (flash_attn.hip)
   auto delta = torch::empty({10, B, H, S}, q.options().dtype(at::kFloat));
   int64_t st[24];
@@ -683,8 +669,7 @@ std::vector<Tensor> flash_bwd(Tensor q, Tensor k, Tensor v, Tensor o, Tensor dou
   check(smdt_flash_bwd(dcode(q), q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), dout.data_ptr(),
                        lse.data_ptr<float>(), delta.data_ptr<float>(), dq.data_ptr(), dk.data_ptr(),
                        dv.data_ptr(), (int)B, (int)H, (int)Hkv, (int)S, (int)D, st, (float)scale,
-                       causal ? 1 : 0, (float)dropout_p, (uint64_t)seed, (uint64_t)offset,
-                       keep ? reinterpret_cast<const uint32_t*>(keep->data_ptr<int>()) : nullptr, cur_stream()),
+                       causal ? 1 : 0, (float)dropout_p, (uint64_t)seed, (uint64_t)offset, cur_stream()),
         "flash_bwd");
   return {dq, dk, dv};
 }
@@ -921,9 +906,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("ce_fused", &ce_fused);
   namespace py = pybind11;
   m.def("flash_fwd", &flash_fwd, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("scale"), py::arg("causal"),
-        py::arg("out") = py::none(), py::arg("dropout_p") = 0.0, py::arg("seed") = 0, py::arg("offset") = 0,
-        py::arg("keep") = py::none());
-  m.def("flash_keep_words", &keep_words, "int32 words of flash_fwd's optional dropout keep buffer");
+        py::arg("out") = py::none(), py::arg("dropout_p") = 0.0, py::arg("seed") = 0, py::arg("offset") = 0);
   m.def("ipc_malloc", &ipc_malloc, py::arg("bytes"), py::arg("uncached"));
   m.def("ipc_free", &ipc_free);
   m.def("ipc_get_handle", &ipc_get_handle);
@@ -951,6 +934,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("relay_read_error", &relay_read_error);
   m.def("flash_bwd", &flash_bwd, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("o"), py::arg("dout"),
         py::arg("lse"), py::arg("scale"), py::arg("causal"), py::arg("dq") = py::none(), py::arg("dk") = py::none(),
-        py::arg("dv") = py::none(), py::arg("dropout_p") = 0.0, py::arg("seed") = 0, py::arg("offset") = 0,
-        py::arg("keep") = py::none());
+        py::arg("dv") = py::none(), py::arg("dropout_p") = 0.0, py::arg("seed") = 0, py::arg("offset") = 0);
 }

@@ -297,19 +297,6 @@ struct GldsTile {
   }
 };
 
-// Stored keep words (the forward writes them, the dQ kernel reads them instead of re-hashing;
-// the dK / dV kernel, whose lanes run over keys, keeps hashing). Word j = 4 tt + u of a tile
-// (sub-tile tt, slot pair u) carries its 4 decisions at bits 7 / 15 / 23 / 31; packed, decision
-// (j, byte c) sits at bit 8 c + 7 - j, so (pk << j) puts word j's decisions back at 7 / 15 / 23 /
-// 31 for sel_bit. One word per (b, h, key tile, query row, lane half): [B H][S / 64][S][2].
-__device__ __forceinline__ uint32_t pack_keep(uint32_t pk, uint32_t t, int j) {
-  // v_lshrrev + ONE v_bitop3 ((a & b) | c, LUT 0xEA) per word
-  return __builtin_amdgcn_bitop3_b32(t >> j, 0x80808080u >> j, pk, 0xEA);
-}
-__device__ __forceinline__ int64_t keep_index(int bh, int tile, int S, int q, int h) {
-  return (((int64_t)bh * (S / kTile) + tile) * S + q) * 2 + h;
-}
-
 // ---------------------------------------------------------------------------------------
 // Forward. Workgroup = 4 waves = 128 query rows of one (b, h); K/V streamed in 64-key tiles,
 // double-buffered.
@@ -320,7 +307,7 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void fwd_kernel(const E* __re
                                                      E* __restrict__ O, float* __restrict__ LSE,
                                                      int B, int H, int Hkv, int S, Strides qs,
                                                      Strides ks_, Strides vs, Strides os,
-                                                     float scale, Drop drop, uint32_t* __restrict__ KEEP) {
+                                                     float scale, Drop drop) {
   using G = Geo<D>;
   // Three [K | V] tile buffers (separate objects: the compiler sees that the LDS-DMA into one does
   // not alias the fragment reads of another, so it leaves the DMA queue alone).
@@ -403,23 +390,11 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void fwd_kernel(const E* __re
   wait_vm<(kBuf - 2) * kPer>();
   __builtin_amdgcn_s_barrier();
 
-  // Dropout keep words for the dQ kernel (KEEP, optional): the 32 decisions of this lane's row in
-  // a tile, packed (see keep_index / pack_keep), stored at the START of the next tile, before its
-  // DMA issue, so the store never sits behind the newest DMA in the counted vmcnt waits.
-  uint32_t kp_word = 0u;
-  int kp_tile = -1;
-  auto flush_keep = [&]() {
-    if (DROP && KEEP != nullptr && kp_tile >= 0) {
-      KEEP[keep_index(bh, kp_tile, S, my_q, h)] = kp_word;
-      kp_tile = -1;
-    }
-  };
   // Every call issues exactly one tile's DMA (past the end it re-reads the last tile into a
   // buffer nobody reads again), so the counted waits stay uniform.
   auto tile = [&](int t, const char* kt, char* pre) {
     const int kb = t * kTile;
     const char* vt = kt + G::TB;
-    flush_keep();
     issue(t + kBuf - 1 < ntiles ? t + kBuf - 1 : ntiles - 1, pre);
     if (!CAUSAL || kb <= qw + 31) {
       // S^T tiles (log2 domain, minus m): rows = keys (registers), column = this lane's query.
@@ -494,7 +469,6 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void fwd_kernel(const E* __re
       // 1/(1-p) scale is applied in the epilogue
       uint32_t dm[2][8];
       if constexpr (DROP) {
-        uint32_t pk = 0u;
 #pragma unroll
         for (int tt = 0; tt < 2; ++tt)
 #pragma unroll
@@ -502,12 +476,7 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void fwd_kernel(const E* __re
             const uint32_t t = keep_bits(drop_hash(dblk + ((kb + 32 * tt) >> 1) + 4 * u, dkey), dsel, drop.k4);
             dm[tt][2 * u] = mask_even_slot(t);
             dm[tt][2 * u + 1] = mask_odd_slot(t);
-            pk = pack_keep(pk, t, 4 * tt + u);
           }
-        if (KEEP != nullptr) {
-          kp_word = pk;
-          kp_tile = kb / kTile;
-        }
       }
       l += rsum;
       // O^T[d, q] += V^T[d, keys] . P^T[keys, q]
@@ -538,7 +507,6 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void fwd_kernel(const E* __re
       if (t + 1 < ntiles) tile(t + 1, L1, L0);
     }
   }
-  flush_keep();
   wait_vm<0>();  // drain the trailing re-read before the workgroup's LDS is released
 
   // Epilogue: O[q, d] = O^T / l (x 1/(1-p) with dropout) ; lse = (m + log2 l) * ln 2.
@@ -882,7 +850,7 @@ __global__ __launch_bounds__(256, D == 64 ? SMDT_FA_DQ_OCC : 1) void bwd_dq_kern
     const E* __restrict__ dO, const E* __restrict__ O, const float* __restrict__ LSE,
     float* __restrict__ DELTA, E* __restrict__ RC3, E* __restrict__ dQ, int B, int H, int Hkv,
     int S, Strides qs, Strides ks_, Strides vs, Strides dos, Strides os, Strides dqs, float scale,
-    float dscale, float lsub, Drop drop, const uint32_t* __restrict__ KEEP) {
+    float dscale, float lsub, Drop drop) {
   using G = Geo<D>;
   // D = 64: three [K | V] buffers, two tiles in flight; D = 128 (twice the bytes): two buffers,
   // so two workgroups still fit a CU's 160 KB of LDS.
@@ -993,17 +961,9 @@ __global__ __launch_bounds__(256, D == 64 ? SMDT_FA_DQ_OCC : 1) void bwd_dq_kern
   wait_vm<(kBuf - 2) * kPer>();
   __builtin_amdgcn_s_barrier();
 
-  auto keep_word = [&](int t) -> uint32_t {
-    return (t < ntiles && (!CAUSAL || t * kTile <= qw + 31)) ? KEEP[keep_index(bh, t, S, my_q, h)] : 0u;
-  };
-  uint32_t kp_next = (DROP && KEEP != nullptr) ? keep_word(0) : 0u;
   auto tile = [&](int t, const char* kt, char* pre) {
     const int kb = t * kTile;
     const char* vt = kt + G::TB;
-    // the forward's keep word of this tile, loaded one tile ahead (an HBM round trip is longer
-    // than the MFMA chain before its first use), before the DMA issue
-    const uint32_t kpw = kp_next;
-    if (DROP && KEEP != nullptr) kp_next = keep_word(t + 1);
     issue(t + kBuf - 1 < ntiles ? t + kBuf - 1 : ntiles - 1, pre);
     // row constants as the initial accumulators: S' = S log2(e) scale - lse, dP' = dP - delta
     auto sd = [&](int tt, f32x16& st, f32x16& dpt) {
@@ -1029,13 +989,8 @@ __global__ __launch_bounds__(256, D == 64 ? SMDT_FA_DQ_OCC : 1) void bwd_dq_kern
       const int ksub = kb + 32 * tt;
       uint32_t tb[4];  // keep bits of slots 2u (bits 7 / 23) and 2u + 1 (bits 15 / 31)
       if constexpr (DROP) {
-        if (KEEP != nullptr) {
 #pragma unroll
-          for (int u = 0; u < 4; ++u) tb[u] = kpw << (4 * tt + u);
-        } else {
-#pragma unroll
-          for (int u = 0; u < 4; ++u) tb[u] = keep_bits(drop_hash(dblk + (ksub >> 1) + 4 * u, dkey), dsel, drop.k4);
-        }
+        for (int u = 0; u < 4; ++u) tb[u] = keep_bits(drop_hash(dblk + (ksub >> 1) + 4 * u, dkey), dsel, drop.k4);
       }
 #pragma unroll
       for (int i = 0; i < 16; i += 2) {
@@ -1151,7 +1106,7 @@ extern "C" hipError_t smdt_flash_fwd(int dtype, const void* q, const void* k, co
                                      int64_t k_ss, int64_t k_sh, int64_t v_sb, int64_t v_ss,
                                      int64_t v_sh, int64_t o_sb, int64_t o_ss, int64_t o_sh,
                                      float scale, int causal, float dropout_p, uint64_t seed,
-                                     uint64_t offset, uint32_t* keep, hipStream_t st) {
+                                     uint64_t offset, hipStream_t st) {
   if (!fa_shape_ok(dtype, H, Hkv, S, D) || dropout_p < 0.f || dropout_p >= 1.f) return hipErrorInvalidValue;
   Strides qs{q_sb, q_ss, q_sh}, ks{k_sb, k_ss, k_sh}, vs{v_sb, v_ss, v_sh}, os{o_sb, o_ss, o_sh};
   dim3 grid((unsigned)((int64_t)B * H * (S / kBlockRows)));
@@ -1162,11 +1117,11 @@ extern "C" hipError_t smdt_flash_fwd(int dtype, const void* q, const void* k, co
     if (dtype == 2)                                                                             \
       hipLaunchKernelGGL((fwd_kernel<DD, CC, DR, f16>), grid, dim3(256), 0, st, (const f16*)q,  \
                          (const f16*)k, (const f16*)v, (f16*)o, lse, B, H, Hkv, S, qs, ks, vs, os, \
-                         scale, dr, keep);                                                          \
+                         scale, dr);                                                            \
     else                                                                                        \
       hipLaunchKernelGGL((fwd_kernel<DD, CC, DR, bf16>), grid, dim3(256), 0, st, (const bf16*)q, \
                          (const bf16*)k, (const bf16*)v, (bf16*)o, lse, B, H, Hkv, S, qs, ks, vs, os, \
-                         scale, dr, keep);                                                          \
+                         scale, dr);                                                            \
   } while (0)
 #define SMDT_FA_FWD2(DD, CC) \
   do { if (drop) SMDT_FA_FWD(DD, CC, true); else SMDT_FA_FWD(DD, CC, false); } while (0)
@@ -1182,7 +1137,7 @@ extern "C" hipError_t smdt_flash_bwd(int dtype, const void* q, const void* k, co
                                      float* delta, void* dq, void* dk, void* dv, int B, int H,
                                      int Hkv, int S, int D, const int64_t* strides, float scale,
                                      int causal, float dropout_p, uint64_t seed, uint64_t offset,
-                                     const uint32_t* keep, hipStream_t st) {
+                                     hipStream_t st) {
   if (!fa_shape_ok(dtype, H, Hkv, S, D) || dropout_p < 0.f || dropout_p >= 1.f) return hipErrorInvalidValue;
   const Drop dr = make_drop(dropout_p, seed, offset);
   const bool drop = dropout_p > 0.f;
@@ -1204,10 +1159,10 @@ extern "C" hipError_t smdt_flash_bwd(int dtype, const void* q, const void* k, co
     hipLaunchKernelGGL((bwd_dq_kernel<DD, CC, DR, ET>), gq, dim3(256), 0, st, (const ET*)q,      \
                        (const ET*)k, (const ET*)v, (const ET*)dout, (const ET*)o, lse, delta,     \
                        (ET*)rc3, (ET*)dq, B, H, Hkv, S, qs, ks, vs, dos, os, dqs,                 \
-                       scale, dscale, lsub, dr, keep);                                                  \
+                       scale, dscale, lsub, dr);                                                  \
     hipLaunchKernelGGL((bwd_dkdv_kernel<DD, CC, DR, ET>), gkv, dim3(256), 0, st, (const ET*)q,  \
                        (const ET*)k, (const ET*)v, (const ET*)dout, (const ET*)rc3, delta,        \
-                       (ET*)dk, (ET*)dv, B, H, Hkv, S, qs, ks, vs, dos, dks, dvs, scale, dr);         \
+                       (ET*)dk, (ET*)dv, B, H, Hkv, S, qs, ks, vs, dos, dks, dvs, scale, dr);     \
   } while (0)
 #define SMDT_FA_BWD(DD, CC, DR) \
   do { if (dtype == 2) SMDT_FA_BWD_T(DD, CC, DR, f16); else SMDT_FA_BWD_T(DD, CC, DR, bf16); } while (0)

@@ -101,15 +101,13 @@ hipError_t smdt_flash_fwd(int dtype, const void* q, const void* k, const void* v
                           int64_t q_ss, int64_t q_sh, int64_t k_sb, int64_t k_ss, int64_t k_sh,
                           int64_t v_sb, int64_t v_ss, int64_t v_sh, int64_t o_sb, int64_t o_ss,
                           int64_t o_sh, float scale, int causal, float dropout_p, uint64_t seed,
-                          uint64_t offset, uint32_t* keep, hipStream_t st);
-// keep (optional, dropout): int32 [B H, S / 64, S, 2] dropout keep words the forward writes and
-// the backward's dQ kernel reads instead of re-hashing (flash_attn.hip keep_index); null: hashed.
+                          uint64_t offset, hipStream_t st);
 // delta: fp32 scratch of 2 x B x H x S (the backward's prepared per-query row constants).
 hipError_t smdt_flash_bwd(int dtype, const void* q, const void* k, const void* v, const void* o,
                           const void* dout, const float* lse, float* delta, void* dq, void* dk,
                           void* dv, int B, int H, int Hkv, int S, int D, const int64_t* strides,
                           float scale, int causal, float dropout_p, uint64_t seed,
-                          uint64_t offset, const uint32_t* keep, hipStream_t st);
+                          uint64_t offset, hipStream_t st);
 
 // gemm_tn.hip: C[M, N] = A[M, K] . B[N, K]^T (16-bit in / out, fp32 accumulate) with an epilogue:
 // epi 0 none, 1 + bias[n], 2 C = pre-activation and C2 = gelu_tanh(C + bias[n]) (bias_gelu fusion),

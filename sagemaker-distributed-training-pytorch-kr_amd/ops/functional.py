@@ -332,18 +332,6 @@ def _qkv_views(qkv, nh, nkv, hd, seq_first):
     return q, k, v
 
 
-# Dropout keep words stored by the flash forward and read by the dQ kernel instead of re-hashing
-# them (csrc/kernels/flash_attn.hip keep_index): int32 [B H, S / 64, S, 2], 4 bytes per 32
-# attention elements. SMDT_FA_KEEP_MASK=0: every backward kernel re-derives the mask.
-_FA_KEEP = os.environ.get("SMDT_FA_KEEP_MASK", "1") == "1"
-
-
-def _keep_buffer(C, ref, B, H, S, dropout_p, needs_grad):
-    if not (_FA_KEEP and dropout_p > 0.0 and needs_grad):
-        return None
-    return torch.empty(C.flash_keep_words(B, H, S), dtype=torch.int32, device=ref.device)
-
-
 class _FlashAttnQKV(torch.autograd.Function):
     @staticmethod
     def forward(ctx, qkv, nh, nkv, hd, seq_first, scale, causal, dropout_p=0.0, seed=0, offset=0):
@@ -357,10 +345,8 @@ class _FlashAttnQKV(torch.autograd.Function):
             B, S = qkv.shape[0], qkv.shape[1]
             out = qkv.new_empty(B, S, nh, hd)
             ov = out
-        keep = _keep_buffer(C, qkv, B, nh, S, dropout_p, ctx.needs_input_grad[0])
-        _, lse = C.flash_fwd(q, k, v, scale, causal, ov, dropout_p, seed, offset, keep)
+        _, lse = C.flash_fwd(q, k, v, scale, causal, ov, dropout_p, seed, offset)
         ctx.save_for_backward(qkv, out, lse)
-        ctx.keep = keep
         ctx.cfg = (nh, nkv, hd, seq_first, scale, causal, dropout_p, seed, offset)
         return out.flatten(-2)
 
@@ -377,8 +363,7 @@ class _FlashAttnQKV(torch.autograd.Function):
         if seq_first:
             do = do.transpose(0, 1)
             o = o.transpose(0, 1)
-        C.flash_bwd(q, k, v, o, do, lse, scale, causal, dq, dk, dv, dropout_p, seed, offset, ctx.keep)
-        ctx.keep = None
+        C.flash_bwd(q, k, v, o, do, lse, scale, causal, dq, dk, dv, dropout_p, seed, offset)
         return dqkv, None, None, None, None, None, None, None, None, None
 
 
@@ -386,11 +371,8 @@ class _FlashAttn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, q, k, v, scale, causal, dropout_p=0.0, seed=0, offset=0):
         C = _ext.ext()
-        keep = _keep_buffer(C, q, q.shape[0], q.shape[2], q.shape[1], dropout_p,
-                            any(ctx.needs_input_grad[:3]))
-        o, lse = C.flash_fwd(q, k, v, scale, causal, None, dropout_p, seed, offset, keep)
+        o, lse = C.flash_fwd(q, k, v, scale, causal, None, dropout_p, seed, offset)
         ctx.save_for_backward(q, k, v, o, lse)
-        ctx.keep = keep
         ctx.cfg = (scale, causal, dropout_p, seed, offset)
         return o
 
@@ -398,9 +380,7 @@ class _FlashAttn(torch.autograd.Function):
     def backward(ctx, do):
         q, k, v, o, lse = ctx.saved_tensors
         scale, causal, p, seed, offset = ctx.cfg
-        dq, dk, dv = _ext.ext().flash_bwd(q, k, v, o, do, lse, scale, causal, None, None, None, p, seed, offset,
-                                          ctx.keep)
-        ctx.keep = None
+        dq, dk, dv = _ext.ext().flash_bwd(q, k, v, o, do, lse, scale, causal, None, None, None, p, seed, offset)
         return dq, dk, dv, None, None, None, None, None
 
 

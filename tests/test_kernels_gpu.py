@@ -418,44 +418,6 @@ def test_flash_attention_dropout(D, causal, heads, dt):
     assert torch.equal(o2, o.detach()) and not torch.equal(o3, o2)
 
 
-@pytest.mark.parametrize("D", [64, 128])
-@pytest.mark.parametrize("causal", [True, False])
-def test_flash_dropout_stored_keep_words_match_rehashing(monkeypatch, D, causal):
-    """The forward's stored dropout keep words (SMDT_FA_KEEP_MASK, read by the dQ kernel instead
-    of re-hashing): dQ / dK / dV are bit-identical to the re-hashing backward, the words really
-    were written (their set bits are the kept fraction of the computed tiles), and the dQ kernel
-    really reads them (a corrupted buffer changes dQ only)."""
-    torch.manual_seed(21)
-    B, H, S = 2, 4, 384
-    p, seed, off = 0.1, 4321, 9
-    q0, k0, v0 = (torch.randn(B, S, H, D, device=DEV, dtype=torch.bfloat16) for _ in range(3))
-    do = torch.randn(B, S, H, D, device=DEV, dtype=torch.bfloat16)
-    scale = 1 / math.sqrt(D)
-    C = SF._ext.ext()
-
-    def run(keep_on, corrupt=False):
-        monkeypatch.setattr(SF, "_FA_KEEP", keep_on)
-        q, k, v = (t.clone().requires_grad_() for t in (q0, k0, v0))
-        o = SF._FlashAttn.apply(q, k, v, scale, causal, p, seed, off)
-        keep = o.grad_fn.keep if hasattr(o.grad_fn, "keep") else None
-        if corrupt and keep is not None:
-            keep.bitwise_not_()
-        o.backward(do)
-        return o.detach(), q.grad, k.grad, v.grad, keep
-    oh, qh, kh, vh, kh_buf = run(False)
-    assert kh_buf is None
-    os_, qs, ks, vs, kbuf = run(True)
-    assert kbuf is not None and kbuf.numel() == C.flash_keep_words(B, H, S)
-    assert torch.equal(os_, oh) and torch.equal(qs, qh) and torch.equal(ks, kh) and torch.equal(vs, vh)
-    # key tile 0 of (b, h) = (0, 0) is computed for every query row: its 2 S words hold ~(1 - p)
-    # of their 32 decisions set
-    bits = torch.tensor([bin(int(w) & 0xFFFFFFFF).count("1") for w in kbuf[:2 * S].tolist()], dtype=torch.float)
-    assert abs(bits.mean().item() / 32 - (1 - p)) < 0.03, bits.mean().item()
-    # the dQ kernel reads them: flipping every word changes dQ, not dK / dV
-    _, qc, kc, vc, _ = run(True, corrupt=True)
-    assert not torch.equal(qc, qh) and torch.equal(kc, kh) and torch.equal(vc, vh)
-
-
 @pytest.mark.parametrize("S", [384, 512, 1024])
 @pytest.mark.parametrize("causal", [True, False])
 @pytest.mark.parametrize("p", [0.0, 0.1])
