@@ -1,6 +1,7 @@
 """HBM rate of the step's elementwise kernels at the GPT-2 345M bench shapes (one GPU), plus the
 SFT recipe's SwiGLU and the LM-head cross-entropy. (A 4-vectors-in-flight CE backward measured
-no faster, 2.51 vs 2.47 ms at [65536, 50304], and was not kept: profiles/r4_swiglu_2d/ce_unroll.log.)
+no faster, 2.51 vs 2.47 ms at [65536, 50304], and was not kept: profiles/r4_swiglu_2d/ce_unroll.log,
+in git history.)
 
 bias-GeLU forward / backward on [65536, 4096] bf16 (fc1 output; backward without d(bias): the
 grouped wgrad makes it), the fused bias-dropout-residual LayerNorm forward and its backward on
