@@ -1329,6 +1329,9 @@ def sft_window_agreement_worker(rank, world, tmpdir, ds_cfg, nofit_rank, fuse_ga
     from smdt_amd.train import hf_args
     from smdt_amd.train.sft_trainer import Trainer
     os.environ["SMDT_SFT_FUSE_GA"] = "1" if fuse_ga else "0"
+    # the two runs are compared bit-exactly: one intra-op thread, so the CPU GEMMs' reduction
+    # split cannot follow the machine's load (a parallel test run flipped bf16 ulps otherwise)
+    torch.set_num_threads(1)
     Trainer._window_fits = lambda self, window: self.rank != nofit_rank
     ps.destroy_model_parallel()
     torch.manual_seed(0)

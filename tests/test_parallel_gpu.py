@@ -453,17 +453,20 @@ def test_w_fillers_match_grouped_flush_on_gpu(monkeypatch, stream):
     assert scale > 0 and (g1 - g0).abs().max().item() <= 1e-3 * scale
 
 
-@pytest.mark.parametrize("sub", [0, 2])
-def test_direct_engine_standin_matches_ring_emulation(monkeypatch, sub):
+@pytest.mark.parametrize("sub,pieces", [(0, 1), (2, 1), (0, 2)])
+def test_direct_engine_standin_matches_ring_emulation(monkeypatch, sub, pieces):
     """One emulated tp4 + SP rank with SMDT_LINK_STANDIN=direct: the SP exchanges go through
-    ``TpDirect`` (row pieces, per-piece handles) over the paced stand-in of the direct engine
+    ``TpDirect`` (per-piece handles) over the paced stand-in of the direct engine
     (comm/loopback.PacedDirectEngine) instead of the loopback ring. The stand-in's values are the
     loopback ring's (gather = own shard in every slot, reduce-scatter = sum of this rank's
     partials), so losses and the fp32 gradient buffer agree with the ring run to bf16 add-order
     rounding; with W fillers on, fillers ran inside the direct waits. ``sub`` = 2: the direct run
-    with the sub-batch interleave (whole-chunk exchanges started early, the short phases on a
-    chain stream per half)."""
+    with the sub-batch interleave (whole-chunk exchanges started by ``ag_start`` / left in flight
+    by ``rs_ring``). ``pieces`` = 1: whole chunks (the default); 2: row pieces (per-piece handles,
+    per-peer GEMMs as each piece lands)."""
     import smdt_amd.models.transformer as T
+    from smdt_amd.comm import tp_direct
+    monkeypatch.setattr(tp_direct, "PIECES", pieces)
     from smdt_amd.models.gpt import GPTModel
     from smdt_amd.models.transformer import TransformerConfig
     from smdt_amd.parallel import state as ps
