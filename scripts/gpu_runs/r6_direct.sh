@@ -13,6 +13,24 @@ SMDT_LINK_STANDIN=192:32 run g0_ring_overlap 500 python bench.py $G
 SMDT_LINK_STANDIN=direct:64:32 run g0_direct_overlap 500 python bench.py $G
 SMDT_LINK_STANDIN=direct:64:32 SMDT_W_FILL=0 SMDT_RING_GEMM_TN=0 run g0_direct_nofill 500 python bench.py $G
 SMDT_LINK_STANDIN=direct:64:32 SMDT_TP_DIRECT_PIECES=4 run g0_direct_p4 500 python bench.py $G
+elif [ "${PASS:-1}" = 5 ]; then
+# pass 5: row pieces with the per-peer GEMMs concurrent on side streams (SMDT_TP_DIRECT_CONCURRENT)
+run test5 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_parallel_gpu.py -k "direct_engine_standin"
+SMDT_LINK_STANDIN=direct:64:32 SMDT_TP_DIRECT_PIECES=1 run g0_p1_d 500 python bench.py $G
+SMDT_LINK_STANDIN=direct:64:32 SMDT_TP_DIRECT_PIECES=2 run g0_p2_conc 500 python bench.py $G
+SMDT_LINK_STANDIN=direct:64:32 SMDT_TP_DIRECT_PIECES=4 run g0_p4_conc 500 python bench.py $G
+SMDT_LINK_STANDIN=direct:64:32 SMDT_TP_DIRECT_PIECES=2 SMDT_TP_DIRECT_CONCURRENT=0 run g0_p2_seq 500 python bench.py $G
+SMDT_TP_DIRECT_PIECES=2 run g0_p2_conc_nolink 500 python bench.py $G
+elif [ "${PASS:-1}" = 6 ]; then
+# pass 6: the same with 16 hardware queues per process (HIP's default is 4: streams beyond share
+# queues, so a side stream can queue behind a paced copy that spins for its link time)
+N8="--emulate-tp 2 --micro-batch-size 32 --grad-accum 8 --num-layers 13 --emulate-first-stage --steps 6 --warmup 3"
+GPU_MAX_HW_QUEUES=16 SMDT_LINK_STANDIN=direct:64:32 SMDT_TP_DIRECT_PIECES=2 run q16_g0_p2_conc 500 python bench.py $G
+GPU_MAX_HW_QUEUES=16 SMDT_LINK_STANDIN=direct:64:32 SMDT_TP_DIRECT_PIECES=1 run q16_g0_p1 500 python bench.py $G
+GPU_MAX_HW_QUEUES=16 SMDT_LINK_STANDIN=relay run q16_s0_relay 300 python bench.py $N8
+SMDT_LINK_STANDIN=relay run q4_s0_relay 300 python bench.py $N8
+GPU_MAX_HW_QUEUES=16 run q16_n1 300 python bench.py --steps 20 --warmup 5
+run q4_n1 300 python bench.py --steps 20 --warmup 5
 elif [ "${PASS:-1}" = 4 ]; then
 # pass 4: the interleave's short phases on a chain stream per half (SMDT_SP_SUBBATCH_CHAIN=1)
 run test4 400 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_parallel_gpu.py tests/test_graph_gpu.py -k "direct_engine_standin or subbatch"
