@@ -324,6 +324,8 @@ def main():
                                   overlap_param_gather=zero and st.dp > 1 and bool(a.overlap_grad_reduce),
                                   overlap_grad_reduce=bool(a.overlap_grad_reduce))
     use_graph = bool(a.graph) and dev.type == "cuda" and st.pp == 1
+    # the xGMI DP engine stays in the captured step (replay-safe; health checked between replays)
+    ddp.xgmi_in_graph = use_graph and ddp.xgmi is not None
     opt = MixedPrecisionAdam(ddp, lr=1.5e-4, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.01, clip_grad=1.0,
                              capturable=use_graph)
     if use_graph:
@@ -398,7 +400,12 @@ def main():
 
     def graph_step():
         """Refill the static inputs, set this step's lr (the captured Adam reads it from the
-        device), replay."""
+        device), replay. With the xGMI engine inside the graph, its health check runs between
+        replays; after a fallback to RCCL the step runs eager from then on."""
+        nonlocal graph
+        if ddp.xgmi_in_graph and not ddp.health_between_replays():
+            graph = None
+            return train_step()
         refill()
         opt.set_lr(sched.step(1))
         graph[0].replay()

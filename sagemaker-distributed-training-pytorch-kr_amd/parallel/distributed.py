@@ -122,6 +122,7 @@ class DistributedDataParallel(nn.Module):
         # backend asks for it, or — by default — for each op a run-time timing on this node shows
         # faster than RCCL (SMDT_XGMI_ALLREDUCE=0: never); larger messages are chunked.
         self.xgmi = _xgmi.create_for_group(self.dp_group, auto=True) if rccl else None
+        self.xgmi_in_graph = False     # see _xg: set by a caller that checks health between replays
         # Fixed-order combine (``deterministic_reduce`` / SMDT_DETERMINISTIC_REDUCE=1): every
         # gradient reduction all-gathers the ranks' buckets and sums them locally in rank order,
         # (g_0 + g_1) + g_2 + ..., then divides by dp — independent of the backend's ring / tree
@@ -547,12 +548,29 @@ class DistributedDataParallel(nn.Module):
         self._rs_inflight[b.index] = (handle, None if fresh else out)
 
     def _xg(self):
-        """The xGMI engine for the next collective, or None: none while a HIP graph is being
-        captured (its host-side banding / fallback bookkeeping is not replay-safe; the RCCL and
-        loopback collectives are captured into the graph instead)."""
-        if self.xgmi is None or (torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()):
+        """The xGMI engine for the next collective, or None. While a HIP graph is being captured:
+        only with ``xgmi_in_graph`` — the engine's calls are replay-safe (per-block device call
+        counters; `tests/test_xgmi.py::test_xgmi_engine_replays_from_a_hip_graph`), but its
+        per-step health check (comm/health.py, launched in ``finish_grad_sync``) does not run inside
+        a replay, so the replaying caller must run it between replays (``health_between_replays``,
+        as bench.py's graph step does). Otherwise RCCL's collectives are captured instead."""
+        if self.xgmi is None:
+            return None
+        if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing() and not self.xgmi_in_graph:
             return None
         return self.xgmi
+
+    def health_between_replays(self) -> bool:
+        """For a caller that replays a captured step with the xGMI engine in it: read the previous
+        check, then launch this step's (eager, outside the graph). False once the engines fell back
+        to RCCL (a peer timed out): the graph holds engine kernels and must not be replayed again."""
+        mon = _health.monitor()
+        mon.consume()
+        if self.xgmi is not None and not self.xgmi.active:
+            self.xgmi = None
+            return False
+        mon.launch()
+        return True
 
     def _fold(self, x: torch.Tensor) -> torch.Tensor:
         """Fixed-order combine (``deterministic_reduce``): all-gather ``x`` from every rank of

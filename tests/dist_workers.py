@@ -1539,3 +1539,160 @@ def relay_graph_worker(rank, world, port, outdir):
         res["err"] = traceback.format_exc()
     with open(os.path.join(outdir, f"r{rank}.pkl"), "wb") as f:
         pickle.dump(res, f)
+
+
+def xgmi_graph_worker(rank, world, port, outdir):
+    """One rank of the graph-captured xGMI-engine test: ``world`` processes on cuda:0 (real IPC
+    mappings), the engine's chunked all-reduce, reduce-scatter and all-gather — the async forms
+    DDP / ZeRO use, on the engine's side stream with event handles — captured ONCE in a HIP graph
+    and replayed 20 times with fresh inputs, eager calls interleaved; every result exact against
+    the host-computed sum (per-block device call counters, csrc/kernels/xgmi_allreduce.hip)."""
+    import os
+    import pickle
+    import traceback
+
+    import torch
+
+    os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "RANK": str(rank),
+                       "WORLD_SIZE": str(world)})
+    res = {"ok": [], "err": None, "error_word": None, "replays": 0}
+    try:
+        import torch.distributed as dist
+        from smdt_amd.comm import xgmi
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        torch.cuda.set_device(0)
+        eng = xgmi.XgmiAllReduce(None, region_bytes=4 << 20, blocks=16, validate=False)
+        n_ar = 2 * (4 << 20) // 4 + 1024            # fp32: 3 region bands
+        ns = 3 * (4 << 20) // (4 * world) + 256     # reduce-scatter / all-gather slice: 4 bands
+        ar = torch.empty(n_ar, device="cuda")
+        full = torch.empty(world * ns, device="cuda")
+        gat = torch.empty(world * ns, device="cuda")
+
+        def fill(it):
+            ar.copy_(torch.arange(n_ar, device="cuda", dtype=torch.float32) % 89 + 7.0 * rank + it)
+            full.copy_(torch.arange(world * ns, device="cuda", dtype=torch.float32) % 53 + 3.0 * rank + it)
+            gat.fill_(-1.0)
+            gat.view(world, ns)[rank].copy_(torch.arange(ns, device="cuda", dtype=torch.float32) + 100.0 * rank + it)
+
+        def want(it):
+            a = sum(torch.arange(n_ar, device="cuda", dtype=torch.float32) % 89 + 7.0 * r + it for r in range(world))
+            f = sum(torch.arange(world * ns, device="cuda", dtype=torch.float32) % 53 + 3.0 * r + it
+                    for r in range(world)).view(world, ns)[rank]
+            g = torch.cat([torch.arange(ns, device="cuda", dtype=torch.float32) + 100.0 * r + it for r in range(world)])
+            return a, f, g
+
+        def step():
+            h1 = eng.all_reduce_async(ar)
+            h2 = eng.reduce_scatter_async(full.view(world, ns)[rank], full)
+            h3 = eng.all_gather_async(gat, gat.view(world, ns)[rank])
+            assert h1 is not None and h2 is not None and h3 is not None
+            for h in (h1, h2, h3):
+                h.wait()
+
+        def check(it):
+            torch.cuda.synchronize()
+            a, f, g = want(it)
+            res["ok"].append(bool(torch.equal(ar, a) and torch.equal(full.view(world, ns)[rank], f)
+                                  and torch.equal(gat, g)))
+        for it in range(3):                        # eager: the device call counters advance
+            fill(it)
+            step()
+            check(it)
+        fill(0)
+        torch.cuda.synchronize()
+        dist.barrier()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            step()
+        torch.cuda.synchronize()
+        dist.barrier()
+        for it in range(20):
+            fill(10 + it)
+            g.replay()
+            check(10 + it)
+            res["replays"] += 1
+            if it % 5 == 4:                        # eager calls between replays
+                fill(100 + it)
+                step()
+                check(100 + it)
+        res["error_word"] = eng.error()
+        del g
+        eng.close()
+        dist.destroy_process_group()
+    except Exception:
+        res["err"] = traceback.format_exc()
+    with open(os.path.join(outdir, f"r{rank}.pkl"), "wb") as f:
+        pickle.dump(res, f)
+
+
+def ddp_xgmi_graph_worker(rank, world, port, outdir, zero):
+    """One rank of the DDP-level graph test: ``world`` processes on cuda:0, the framework's DDP
+    over a Gloo world with an xGMI engine on real IPC mappings put in as its DP engine and
+    ``xgmi_in_graph`` on: the gradient sync (``finish_grad_sync``: every bucket's all-reduce, or
+    with ``zero`` its reduce-scatter) captured once and replayed with fresh gradients, the health
+    check run between replays (``health_between_replays``). Every reduced value exact."""
+    import os
+    import pickle
+    import traceback
+
+    import torch
+
+    os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "RANK": str(rank),
+                       "WORLD_SIZE": str(world)})
+    res = {"ok": [], "err": None, "error_word": None, "replays": 0, "engine_calls": 0}
+    try:
+        import torch.distributed as dist
+        from smdt_amd.comm import xgmi
+        from smdt_amd.parallel import state as ps
+        from smdt_amd.parallel.distributed import DistributedDataParallel as DDP
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        torch.cuda.set_device(0)
+        ps.initialize_model_parallel(1, 1)
+        torch.manual_seed(0)
+        model = torch.nn.Sequential(torch.nn.Linear(256, 512), torch.nn.Linear(512, 256)).cuda()
+        ddp = DDP(model, grad_dtype=torch.float32, bucket_size=40000, use_distributed_optimizer=zero)
+        assert ddp.xgmi is None                        # a Gloo group: no engine of its own
+        ddp.xgmi = xgmi.XgmiAllReduce(None, region_bytes=1 << 20, blocks=16, validate=False)
+        ddp.xgmi_in_graph = True
+        n = ddp.grad_data.numel()
+        base = torch.arange(n, device="cuda", dtype=torch.float32) % 97
+
+        def fill(it):
+            ddp.grad_data.copy_(base + 4.0 * rank + it)
+
+        def check(it):
+            torch.cuda.synchronize()
+            want = base + 2.0 * (world - 1) + it      # the average of the ranks' fills
+            ok = True
+            for b in ddp.buckets:
+                s, e = ddp.shard_range(b) if zero else (b.start, b.end)
+                ok = ok and torch.equal(ddp.grad_data[s:e], want[s:e])
+            res["ok"].append(bool(ok))
+        for it in range(2):
+            fill(it)
+            ddp.finish_grad_sync()
+            check(it)
+        calls0 = ddp.xgmi.calls
+        fill(0)
+        torch.cuda.synchronize()
+        dist.barrier()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            ddp.finish_grad_sync()
+        res["engine_calls"] = ddp.xgmi.calls - calls0   # issued into the graph
+        torch.cuda.synchronize()
+        dist.barrier()
+        for it in range(10):
+            assert ddp.health_between_replays()
+            fill(10 + it)
+            g.replay()
+            check(10 + it)
+            res["replays"] += 1
+        res["error_word"] = ddp.xgmi.error()
+        del g
+        ddp.xgmi.close()
+        dist.destroy_process_group()
+    except Exception:
+        res["err"] = traceback.format_exc()
+    with open(os.path.join(outdir, f"r{rank}.pkl"), "wb") as f:
+        pickle.dump(res, f)

@@ -167,6 +167,83 @@ def test_cross_process_ipc_allreduce_world2():
 
 
 @pytest.mark.gpu
+def test_xgmi_engine_replays_from_a_hip_graph():
+    """The xGMI engine's async all-reduce / reduce-scatter / all-gather (the DDP / ZeRO bucket
+    forms), captured once in a HIP graph by 2 processes on one GPU and replayed 20 times with
+    fresh inputs, eager calls in between: exact every time, no error word."""
+    import os
+    import pickle
+    import tempfile
+
+    import torch.multiprocessing as mp
+
+    import dist_workers as W
+    from _dist import free_port
+
+    world = 2
+    port = free_port()
+    with tempfile.TemporaryDirectory() as d:
+        ctx = mp.get_context("spawn")
+        procs = [ctx.Process(target=W.xgmi_graph_worker, args=(r, world, port, d)) for r in range(world)]
+        for p in procs:
+            p.start()
+        for p in procs:
+            p.join(120)
+        for p in procs:
+            if p.is_alive():
+                p.kill()
+        out = []
+        for r in range(world):
+            path = os.path.join(d, f"r{r}.pkl")
+            assert os.path.exists(path), f"rank {r} wrote no result (exit {procs[r].exitcode})"
+            with open(path, "rb") as f:  # written by this test's own workers
+                out.append(pickle.load(f))
+    for r, res in enumerate(out):
+        assert res["err"] is None, f"rank {r}:\n{res['err']}"
+        assert res["error_word"] == 0 and res["replays"] == 20 and all(res["ok"]) and len(res["ok"]) == 27, (r, res)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("zero", [False, True])
+def test_ddp_xgmi_gradient_sync_replays_from_a_hip_graph(zero):
+    """DDP's gradient sync over the xGMI engine inside a captured HIP graph (``xgmi_in_graph``,
+    the engine's health check between replays): 2 processes on one GPU, the sync captured once
+    (engine calls really issued into the graph) and replayed 10 times with fresh gradients,
+    every bucket (ZeRO: every shard) exact."""
+    import os
+    import pickle
+    import tempfile
+
+    import torch.multiprocessing as mp
+
+    import dist_workers as W
+    from _dist import free_port
+
+    world = 2
+    port = free_port()
+    with tempfile.TemporaryDirectory() as d:
+        ctx = mp.get_context("spawn")
+        procs = [ctx.Process(target=W.ddp_xgmi_graph_worker, args=(r, world, port, d, zero)) for r in range(world)]
+        for p in procs:
+            p.start()
+        for p in procs:
+            p.join(120)
+        for p in procs:
+            if p.is_alive():
+                p.kill()
+        out = []
+        for r in range(world):
+            path = os.path.join(d, f"r{r}.pkl")
+            assert os.path.exists(path), f"rank {r} wrote no result (exit {procs[r].exitcode})"
+            with open(path, "rb") as f:  # written by this test's own workers
+                out.append(pickle.load(f))
+    for r, res in enumerate(out):
+        assert res["err"] is None, f"rank {r}:\n{res['err']}"
+        assert res["engine_calls"] > 0, res
+        assert res["error_word"] == 0 and res["replays"] == 10 and all(res["ok"]) and len(res["ok"]) == 12, (r, res)
+
+
+@pytest.mark.gpu
 def test_smddp_backend_rccl_world1_torch_ddp():
     """backend="smddp" on its production inner group (ProcessGroupNCCL = RCCL) in a fresh
     process: torch DDP construction (broadcast), bucket all-reduce, barrier and all-gather all
