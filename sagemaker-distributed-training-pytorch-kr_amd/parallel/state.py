@@ -228,6 +228,10 @@ def initialize_emulated_tensor_parallel(tensor_model_parallel_size: int = 1,
     st.emulated = True
     from ..comm.loopback import PacedDirectEngine, direct_standin
     ds = direct_standin()
+    if ds is not None and tp not in (4, 8):
+        import warnings
+        warnings.warn(f"SMDT_LINK_STANDIN=direct models the TP4 / TP8 direct engine; at tp {tp} the "
+                      "emulated exchanges stay in-line copies (use 'relay' or '<GB/s>:<workgroups>')")
     if ds is not None and tp in (4, 8):
         # the TP4 / TP8 exchanges through a paced stand-in of the direct multi-link engine
         from ..comm.tp_direct import TpDirect
