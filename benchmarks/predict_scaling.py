@@ -51,8 +51,10 @@ PARAMS = 354.9e6            # GPT-2 345M with the padded vocab (tied embedding)
 
 _N8 = ["--emulate-tp", "2", "--micro-batch-size", "32", "--grad-accum", "8", "--phase-probe", "8"]
 _N8_64 = ["--emulate-tp", "2", "--micro-batch-size", "64", "--grad-accum", "4", "--phase-probe", "4"]
+# GPT-3 stage shapes: the committed TunableOp table has their winners (profiles/r6_g3tune/: 397.1 /
+# 397.8 ms against 399.7 / 400.3 with the library heuristics)
 _G3 = ["--emulate-tp", "4", "--hidden-size", "4096", "--num-attention-heads", "32", "--seq-length", "2048",
-       "--micro-batch-size", "4", "--grad-accum", "8", "--phase-probe", "8", "--tunableop", "0"]
+       "--micro-batch-size", "4", "--grad-accum", "8", "--phase-probe", "8"]
 RUNS = {
     "n1_dp": [],
     # bench.py's balanced split: 13 layers | 11 layers + LM head
