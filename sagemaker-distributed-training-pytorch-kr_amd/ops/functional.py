@@ -171,8 +171,9 @@ def bias_dropout_add_norm(x, bias, residual, gamma, beta, p: float, training: bo
     p = float(p) if training else 0.0
     # a row-parallel output whose reduce-scatter left its peer's partial as a pending summand
     # (tensor_parallel.rs_ring under defer_rs_add): x + x2 is the value, added in the kernel
-    from ..parallel.tensor_parallel import take_pending_add
+    from ..parallel.tensor_parallel import plain, take_pending_add
     x2 = take_pending_add(x)
+    x = plain(x)
     if _ext.use_kernels(x):
         seed, offset = _rng(rng).next() if p > 0 else (0, 0)
         return _BDALayerNorm.apply(x, bias, residual, gamma, None if rms else beta, p, float(eps), bool(rms),

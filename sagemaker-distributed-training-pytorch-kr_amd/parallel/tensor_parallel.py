@@ -1617,14 +1617,68 @@ def _bwd_add_to_norm(x) -> bool:
 _ADD_LEDGER = {"issued": 0, "consumed": 0, "live": {}}
 
 
+# Forward guard (SMDT_DEFER_RS_GUARD, default on): a row-parallel output whose combine is deferred
+# becomes a ``PendingPartial`` — its class is swapped in place (0.5 us; an ``as_subclass`` alias
+# cost 6 us, +1.5 ms per emulated N = 8 stage step, profiles/r6_guard/) to a tensor subclass
+# whose every torch operation raises, apart from metadata reads — until its fused norm takes the
+# summand (``take_pending_add``) and turns it back into a plain tensor (``plain``). A consumer
+# that reads it before that (a forward hook, a model variant reading the output twice or through
+# a non-fused norm) fails at its first read instead of seeing a partial sum.
+_GUARD = os.environ.get("SMDT_DEFER_RS_GUARD", "1") == "1"
+
+
+def _meta_funcs():
+    T = torch.Tensor
+    out = {T.as_subclass, T.data_ptr, T.dim, T.size, T.numel, T.element_size, T.stride, T.is_contiguous,
+           T.__len__, T.__hash__}
+    for name in ("shape", "dtype", "device", "is_cuda", "requires_grad", "grad_fn", "ndim", "layout",
+                 "is_leaf", "_version", "names"):
+        prop = getattr(T, name, None)
+        if prop is not None and hasattr(prop, "__get__"):
+            out.add(prop.__get__)
+    return out
+
+
+class PendingPartial(torch.Tensor):
+    """See _GUARD. Only metadata reads and ``as_subclass`` pass."""
+
+    _META = None
+
+    @classmethod
+    def __torch_function__(cls, func, types, args=(), kwargs=None):
+        if cls._META is None:
+            cls._META = _meta_funcs()
+        if func in cls._META:
+            with torch._C.DisableTorchFunctionSubclass():
+                return func(*args, **(kwargs or {}))
+        name = getattr(func, "__name__", str(func))
+        raise RuntimeError(
+            f"a row-parallel output whose reduce-scatter combine was deferred to its fused norm was "
+            f"read by another consumer ({name}) — it holds only this rank's partial sum. Run with "
+            "SMDT_DEFER_RS_ADD=0, or keep the fused norm as the only consumer.")
+
+
+def plain(t):
+    """``t`` as a plain tensor again (a ``PendingPartial``'s class is swapped back in place)."""
+    if type(t) is PendingPartial:
+        t.__class__ = torch.Tensor
+    return t
+
+
 def set_pending_add(t, x2, where: str):
+    """Hang ``x2`` on ``t`` for its consumer; returns t (forward outputs: turned into a
+    ``PendingPartial`` in place under the guard)."""
+    if _GUARD and where == "forward output" and type(t) is torch.Tensor:
+        t.__class__ = PendingPartial
     t._smdt_add = x2
     _ADD_LEDGER["issued"] += 1
     _ADD_LEDGER["live"][id(t)] = where
+    return t
 
 
 def take_pending_add(t):
-    """The pending summand of ``t`` (removed from it and from the ledger), or None."""
+    """The pending summand of ``t`` (removed from it and from the ledger), or None. The caller
+    then reads ``plain(t)``."""
     x2 = getattr(t, "_smdt_add", None)
     if x2 is not None:
         del t._smdt_add
@@ -1670,8 +1724,9 @@ def foreign_hooks(module) -> bool:
 
 
 def materialize_add(t):
-    """Apply a pending reduce-scatter summand (``defer_rs_add``) in place; returns t."""
+    """Apply a pending reduce-scatter summand (``defer_rs_add``) in place; returns the plain t."""
     x2 = take_pending_add(t)
+    t = plain(t)
     if x2 is not None:
         t.data.add_(x2)
     return t
@@ -1960,7 +2015,7 @@ def rs_ring(partial_fn, group, full_shape, ref, before_last_wait=None, bulk=Fals
             fill_exchange_wait()
             _wait_works(works_j[j], group)
         if (_DEFER_ADD["on"] and before_last_wait is None) or defer_add:
-            set_pending_add(own, incoming, "backward dgrad" if defer_add else "forward output")
+            own = set_pending_add(own, incoming, "backward dgrad" if defer_add else "forward output")
             SPLIT_STATS["bwd_add_to_norm" if defer_add else "rs_add_to_norm"] += 1
             return own
         return own.add_(incoming)
@@ -1975,7 +2030,7 @@ def rs_ring(partial_fn, group, full_shape, ref, before_last_wait=None, bulk=Fals
             _wait_works(works, group)
             if s == ws - 1 and ws == 2 and ((_DEFER_ADD["on"] and before_last_wait is None) or defer_add):
                 # the consuming norm adds it (see _DEFER_ADD)
-                set_pending_add(part, incoming, "backward dgrad" if defer_add else "forward output")
+                part = set_pending_add(part, incoming, "backward dgrad" if defer_add else "forward output")
                 SPLIT_STATS["bwd_add_to_norm" if defer_add else "rs_add_to_norm"] += 1
                 return part
             part = part.add_(incoming)

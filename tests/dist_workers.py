@@ -1431,7 +1431,7 @@ def ag_start_view_worker(rank, world, emulate=False):
     return res
 
 
-def deferred_add_worker(rank, world, case, guard=True, defer=True):
+def deferred_add_worker(rank, world, case, guard=True, defer=True, pending_guard=True):
     """tp2 + SP on Gloo with the ring reduce-scatter's combine deferred to the consuming fused norm
     (tensor_parallel.defer_rs_add). ``case``:
       * "hook": a forward hook on layer 0's attention output projection (a row-parallel linear)
@@ -1439,6 +1439,8 @@ def deferred_add_worker(rank, world, case, guard=True, defer=True):
       * "plain_norm": the layers' norm replaced by a plain one that never takes the pending summand;
       * "bwd": the column-parallel linears' backward reduce-scatter is made to defer its combine
         (forced on CPU), and the norm backward on CPU does not take it.
+    ``pending_guard`` False turns the forward guard off (``PendingPartial``: any read of a pending
+    row-parallel output other than its fused norm's raises).
     Returns (loss or the raised error text, hook capture, split stats)."""
     import torch.nn.functional as F
     import torch.distributed as dist
@@ -1451,6 +1453,7 @@ def deferred_add_worker(rank, world, case, guard=True, defer=True):
     init_distributed("gloo")
     ps.initialize_model_parallel(2, 1)
     TPm._DEFER_RS_ADD = defer
+    TPm._GUARD = pending_guard
     for k in TPm.SPLIT_STATS:
         TPm.SPLIT_STATS[k] = 0
     if not guard:
@@ -1463,6 +1466,13 @@ def deferred_add_worker(rank, world, case, guard=True, defer=True):
         T.Norm.fused = plain
     if case == "bwd":
         TPm._bwd_add_to_norm = lambda x: True
+    if case == "second_consumer":
+        fused = T.Norm.fused
+
+        def twice(self, x, *a, **k):
+            _ = x.float().abs().max()          # a second reader of the row-parallel output
+            return fused(self, x, *a, **k)
+        T.Norm.fused = twice
     cfg = TransformerConfig(**{**TINY, "sequence_parallel": True})
     m = GPTModel(cfg)
     seen = []

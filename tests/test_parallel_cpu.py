@@ -569,34 +569,60 @@ def test_pending_add_ledger_unit():
     """A summand hung on a tensor must be taken before a check point (tensor_parallel ledger)."""
     from smdt_amd.parallel import tensor_parallel as tp
     t, x2 = torch.ones(4), torch.full((4,), 2.0)
-    tp.set_pending_add(t, x2, "forward output")
+    t = tp.set_pending_add(t, x2, "forward output")
+    assert isinstance(t, tp.PendingPartial) and t.shape == (4,) and t.dtype == torch.float32
     assert tp.take_pending_add(t) is x2 and not hasattr(t, "_smdt_add")
+    assert type(tp.plain(t)) is torch.Tensor and torch.equal(t, torch.ones(4))
     tp.check_pending_adds("after take")            # nothing pending: no error
-    u = torch.ones(4)
-    tp.set_pending_add(u, x2, "forward output")
-    v = u * 3                                        # a consumer that is not the fused norm
-    assert not hasattr(v, "_smdt_add")
-    with pytest.raises(RuntimeError, match="never added"):
-        tp.check_pending_adds("test")
-    tp.set_pending_add(u, x2, "forward output")
-    assert torch.equal(tp.materialize_add(u), torch.full((4,), 3.0))
-    tp.check_pending_adds("after materialize")
+    # the forward guard: any read of a pending output other than the fused norm's raises ...
+    u = tp.set_pending_add(torch.ones(4), x2, "forward output")
+    with pytest.raises(RuntimeError, match="another consumer"):
+        u * 3
+    # ... and without it (SMDT_DEFER_RS_GUARD=0) the ledger still catches the untaken summand
+    prev = tp._GUARD
+    tp._GUARD = False
+    try:
+        w = tp.set_pending_add(torch.ones(4), x2, "forward output")
+        v = w * 3                                    # a consumer that is not the fused norm
+        assert not hasattr(v, "_smdt_add")
+        with pytest.raises(RuntimeError, match="never added"):
+            tp.check_pending_adds("test")
+        w = tp.set_pending_add(torch.ones(4), x2, "forward output")
+        assert torch.equal(tp.materialize_add(w), torch.full((4,), 3.0))
+        tp.check_pending_adds("after materialize")
+    finally:
+        tp._GUARD = prev
+    u2 = tp.set_pending_add(torch.ones(4), x2, "forward output")
+    m = tp.materialize_add(u2)
+    assert type(m) is torch.Tensor and torch.equal(m, torch.full((4,), 3.0))
+    tp.check_pending_adds("after guarded materialize")
 
 
 def test_deferred_rs_add_with_a_forward_hook_materializes():
     """tp2 + SP (Gloo): a forward hook on a row-parallel linear of the layer stack turns the
     deferred reduce-scatter combine off, so the hook sees the complete output (equal to the run
-    with SMDT_DEFER_RS_ADD=0) and the loss is unchanged. Mutation arm: with the hook guard
-    disabled the hook sees the output without the peer's partial."""
+    with SMDT_DEFER_RS_ADD=0) and the loss is unchanged. With the hook check disabled, the hook's
+    read of the pending output raises (the forward guard, ``PendingPartial``); mutation arm: with
+    that guard off too, the hook silently sees the output without the peer's partial."""
     base = run_workers(W.deferred_add_worker, 2, "hook", True, False)
     hooked = run_workers(W.deferred_add_worker, 2, "hook", True, True)
-    unguarded = run_workers(W.deferred_add_worker, 2, "hook", False, True)
-    for (l0, h0, _), (l1, h1, s1), (_, h2, s2) in zip(base, hooked, unguarded):
+    caught = run_workers(W.deferred_add_worker, 2, "hook", False, True)
+    unguarded = run_workers(W.deferred_add_worker, 2, "hook", False, True, False)
+    for (l0, h0, _), (l1, h1, s1), (l2, _, s2), (_, h3, s3) in zip(base, hooked, caught, unguarded):
         assert isinstance(l1, torch.Tensor), l1
         _close(l1, l0)
         _close(h1, h0)
-        assert s1["rs_add_to_norm"] == 0 and s2["rs_add_to_norm"] > 0
-        assert (h2 - h0).abs().max() > 1e-3
+        assert s1["rs_add_to_norm"] == 0 and s2["rs_add_to_norm"] > 0 and s3["rs_add_to_norm"] > 0
+        assert isinstance(l2, str) and "another consumer" in l2, l2
+        assert (h3 - h0).abs().max() > 1e-3
+
+
+def test_deferred_rs_add_second_consumer_raises():
+    """tp2 + SP (Gloo) with the combine deferred: a model variant that reads the attention output
+    (a pending row-parallel output) before handing it to the fused norm raises at that read (the
+    forward guard) instead of computing with this rank's partial sum."""
+    for out, _, _ in run_workers(W.deferred_add_worker, 2, "second_consumer"):
+        assert isinstance(out, str) and "another consumer" in out, out
 
 
 @pytest.mark.parametrize("case", ["plain_norm", "bwd"])
@@ -604,7 +630,12 @@ def test_deferred_rs_add_unconsumed_summand_raises(case):
     """tp2 + SP (Gloo) with the combine deferred, but the summand's consumer is not the fused norm:
     a model variant whose norm never takes it (forward), or a backward consumer of a deferred
     input-gradient summand that is not the fused norm kernel (the case of a norm output with a
-    second consumer, whose summed gradient drops the attribute). The ledger raises instead of
-    returning a loss / gradients without the peer's partial."""
+    second consumer, whose summed gradient drops the attribute). It raises instead of returning a
+    loss / gradients without the peer's partial: the forward guard at the plain norm's first read,
+    the ledger for the backward (and for the forward with the guard off)."""
     for out, _, _ in run_workers(W.deferred_add_worker, 2, case):
-        assert isinstance(out, str) and "never added" in out, out
+        want = "another consumer" if case == "plain_norm" else "never added"
+        assert isinstance(out, str) and want in out, out
+    if case == "plain_norm":
+        for out, _, _ in run_workers(W.deferred_add_worker, 2, case, True, True, False):
+            assert isinstance(out, str) and "never added" in out, out
