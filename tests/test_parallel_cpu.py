@@ -639,3 +639,34 @@ def test_deferred_rs_add_unconsumed_summand_raises(case):
     if case == "plain_norm":
         for out, _, _ in run_workers(W.deferred_add_worker, 2, case, True, True, False):
             assert isinstance(out, str) and "never added" in out, out
+
+
+def test_link_standin_env_parsing(monkeypatch):
+    """SMDT_LINK_STANDIN: ``relay`` / ``<GB/s>:<workgroups>`` select the paced ring stand-in,
+    ``direct[:<GB/s per link>[:<workgroups>]]`` the paced direct-engine stand-in (TP4 / TP8 only:
+    at tp 2 it warns and the exchanges stay in-line copies); unset / 0 / off: neither."""
+    import warnings
+
+    from smdt_amd.comm import loopback as lb
+    from smdt_amd.parallel import state as ps
+    cases = {"": (None, None), "0": (None, None), "off": (None, None), "relay": ((256.0, 64), None),
+             "192:32": ((192.0, 32), None), "300": ((300.0, 64), None), "direct": (None, (64.0, 32)),
+             "direct:80": (None, (80.0, 32)), "direct:80:16": (None, (80.0, 16))}
+    for v, (ring, direct) in cases.items():
+        monkeypatch.setenv("SMDT_LINK_STANDIN", v)
+        assert lb.link_standin() == ring and lb.direct_standin() == direct, v
+    monkeypatch.setenv("SMDT_LINK_STANDIN", "direct")
+    ps.destroy_model_parallel()
+    try:
+        with warnings.catch_warnings(record=True) as w:
+            warnings.simplefilter("always")
+            st = ps.initialize_emulated_tensor_parallel(2)
+        assert getattr(st, "tp_direct", None) is None
+        assert any("TP4 / TP8 direct engine" in str(x.message) for x in w)
+        ps.destroy_model_parallel()
+        st = ps.initialize_emulated_tensor_parallel(4)
+        td = st.tp_direct
+        assert td is not None and td.world == 4 and td.rank == 0 and isinstance(td.eng, lb.PacedDirectEngine)
+        assert (td.eng.gbps, td.eng.blocks) == (64.0, 32)
+    finally:
+        ps.destroy_model_parallel()
