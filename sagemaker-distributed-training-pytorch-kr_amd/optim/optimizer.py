@@ -160,6 +160,32 @@ class MixedPrecisionAdam:
         # gradient is split into pieces (ZeRO shards vs whole buckets) or on the reduction order
         return xf.double().square().sum().float().view(1)
 
+    def _counted_sum(self, fn) -> torch.Tensor:
+        """sum over this rank's counted pieces (regions whose params count toward the norm on this
+        rank: TP-replicated params on TP rank 0, the shared embedding on the first stage) of
+        fn(piece index, start, end), reduced over the grad-norm groups (ZeRO's DP group, TP x PP)."""
+        tot = torch.zeros(1, dtype=torch.float64, device=self.device)
+        for i, (s, e, key) in enumerate(self.pieces):
+            if key[1] and e > s:
+                tot += fn(i, s, e)
+        for g in self._norm_groups():
+            dist.all_reduce(tot, group=g)
+        return tot
+
+    def params_norm(self) -> float:
+        """L2 norm of the model's parameters (``--log-params-norm``; Megatron's
+        calc_params_l2_norm), from the fp32 masters; collective over the grad-norm groups."""
+        def sq(i, s, e):
+            o = self.master_off[i]
+            return self.master[o:o + (e - s)].double().square().sum()
+        return float(self._counted_sum(sq).sqrt().item())
+
+    def num_zeros_in_grad(self) -> int:
+        """Zero entries of the reduced gradients (``--log-num-zeros-in-grad``), over the same
+        pieces and groups; call after the gradient sync."""
+        g = self.ddp.grad_data
+        return int(self._counted_sum(lambda i, s, e: (g[s:e] == 0).sum().double()).item())
+
     def zero_grad(self, set_to_none: bool = True):
         """torch.optim-style: a torch_compat DDP re-zeroes its flat gradient buffer on the next
         forward by itself; the explicit-step API zeroes it here."""

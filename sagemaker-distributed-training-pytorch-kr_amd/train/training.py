@@ -261,7 +261,7 @@ def _tensorboard_log(writer, loss_dict, lr, iteration, loss_scale, grad_norm, ar
 
 
 def training_log(loss_dict, total_loss_dict, lr, iteration, loss_scale, report_memory_flag, skipped, grad_norm,
-                 args, elapsed_per_iter, model_cfg=None):
+                 args, elapsed_per_iter, model_cfg=None, num_zeros_in_grad=None, params_norm=None):
     timers = A.get_timers()
     if iteration % args.log_interval == 0:
         _relay.check_all()          # no TP-pair exchange timed out (outputs would be NaN)
@@ -287,6 +287,10 @@ def training_log(loss_dict, total_loss_dict, lr, iteration, loss_scale, report_m
         s += f" loss scale: {loss_scale:.1f} |"
     if grad_norm is not None:
         s += f" grad norm: {grad_norm:.3f} |"
+    if num_zeros_in_grad is not None:
+        s += f" num zeros: {float(num_zeros_in_grad):.1f} |"
+    if params_norm is not None:
+        s += f" params norm: {params_norm:.3f} |"
     s += f" number of skipped iterations: {total_loss_dict['skipped']:3d} |"
     s += f" number of nan iterations: {total_loss_dict.get('nan', 0):3d} |"
     tps = _tokens_per_iter(args) / max(elapsed_per_iter, 1e-9)
@@ -330,6 +334,11 @@ def train_step(forward_step_func, data_iterator, model, optimizer, scheduler, ar
     timers("optimizer", log_level=1).start(barrier=args.barrier_with_L1_time)
     samples = getattr(args, "lr_step_unit", "iterations") == "samples"
     lr = scheduler.step(getattr(args, "current_global_batch_size", args.global_batch_size) if samples else 1)
+    # --log-num-zeros-in-grad: counted on the reduced gradients before the update (an overlapped
+    # optimizer re-zeroes them as it goes), on the iterations that log
+    if getattr(args, "log_num_zeros_in_grad", False) and hasattr(optimizer, "num_zeros_in_grad") \
+            and (getattr(args, "iteration", 0) + 1) % args.log_interval == 0:
+        optimizer.last_num_zeros = optimizer.num_zeros_in_grad()
     grad_norm = optimizer.step(lr)
     timers("optimizer").stop()
     out = {}
@@ -434,8 +443,13 @@ def train(forward_step_func, model, optimizer, scheduler, train_iter, valid_iter
             gn = float(grad_norm.item()) if grad_norm is not None else None
             if gn is not None and not math.isfinite(gn):
                 total["nan"] = total.get("nan", 0) + 1
+            # --log-num-zeros-in-grad / --log-params-norm (collective over the grad-norm groups:
+            # every rank reaches this log point)
+            nz = getattr(optimizer, "last_num_zeros", None) if getattr(args, "log_num_zeros_in_grad", False) else None
+            pn = optimizer.params_norm() if (getattr(args, "log_params_norm", False)
+                                             and hasattr(optimizer, "params_norm")) else None
             report_mem = training_log({k: float(v) for k, v in loss_dict.items()}, total, lr, iteration, ls,
-                                      report_mem, fi, gn, args, elapsed, model_cfg)
+                                      report_mem, fi, gn, args, elapsed, model_cfg, nz, pn)
             if getattr(args, "async_save", False):
                 finalize_async_save(blocking=False)   # tracker once every rank's writer is done
         # (TP ranks > 0 hold no iterator: get_batch broadcasts from TP rank 0, so all ranks evaluate)

@@ -378,3 +378,28 @@ def test_async_save_snapshots_state_at_save_time(tmp_path):
     for k, v in want.items():
         assert torch.equal(sd["model"][k], v), k
     assert ck.finalize_async_save(blocking=False)   # nothing pending any more
+
+
+@pytest.mark.slow
+def test_pretrain_gpt_logs_params_norm_and_num_zeros(tmp_path):
+    """--log-params-norm / --log-num-zeros-in-grad: every training-log line carries Megatron's
+    ``num zeros: N |`` and ``params norm: X |`` fields (after the grad norm); the norm is finite,
+    positive and moves with the updates, the zero count is a non-negative count."""
+    import re
+    script = os.path.join(REPO, "recipes", "3_training_megatron-lm", "pretrain_gpt.py")
+    args = ["--num-layers", "2", "--hidden-size", "64", "--num-attention-heads", "4", "--seq-length", "64",
+            "--max-position-embeddings", "64", "--micro-batch-size", "2", "--global-batch-size", "4",
+            "--lr", "0.01", "--lr-warmup-iters", "1", "--mock-data", "--log-interval", "1", "--eval-interval",
+            "100", "--eval-iters", "1", "--vocab-size", "512", "--tokenizer-type", "NullTokenizer",
+            "--train-iters", "3", "--log-params-norm", "--log-num-zeros-in-grad"]
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT="29541")
+    r = subprocess.run([sys.executable, script] + args, env=env, capture_output=True, text=True, timeout=600,
+                       cwd=str(tmp_path))
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if "lm loss:" in ln and "iteration" in ln]
+    assert len(lines) == 3, r.stdout[-2000:]
+    pn = [float(re.search(r"params norm: (\S+) \|", ln).group(1)) for ln in lines]
+    nz = [float(re.search(r"num zeros: (\S+) \|", ln).group(1)) for ln in lines]
+    assert all(math.isfinite(x) and x > 0 for x in pn) and len(set(pn)) > 1, pn
+    assert all(x >= 0 and x == int(x) for x in nz), nz
+    assert all(ln.index("grad norm:") < ln.index("num zeros:") < ln.index("params norm:") for ln in lines)
