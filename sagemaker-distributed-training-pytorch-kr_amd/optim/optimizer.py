@@ -253,7 +253,8 @@ class MixedPrecisionAdam:
         bc1 = 1 - self.beta1 ** t
         bc2 = 1 - self.beta2 ** t
         if (use_k and self.zero and getattr(ddp, "overlap_optimizer", False) and ddp.zero3 is None
-                and not self.param_is_fp32 and len(self.pieces) == len(ddp.buckets) and not self.capturable):
+                and not self.param_is_fp32 and len(self.pieces) == len(ddp.buckets) and not self.capturable
+                and self._overlappable):
             self._step_overlapped(g, mul, t)
             if self.scaler is not None:
                 self.scaler.update(self.found_inf)
@@ -261,46 +262,54 @@ class MixedPrecisionAdam:
         for (s, e, key), mo in zip(self.pieces, self.master_off):
             if e <= s:
                 continue
-            n = e - s
-            wd = self.weight_decay if key[0] else 0.0
-            mst, m, v = self.master[mo:mo + n], self.exp_avg[mo:mo + n], self.exp_avg_sq[mo:mo + n]
-            gr = g[s:e]
-            if gr.dtype != torch.float32:
-                gr = gr.float()
-            if use_k:
-                model_out = None if self.param_is_fp32 else ddp.param_data[s:e]
-                host_out = None
-                if model_out is not None and not model_out.is_cuda:   # offloaded ZeRO-3 param shard
-                    host_out, model_out = model_out, torch.empty(n, dtype=model_out.dtype, device=mst.device)
-                if self.capturable:
-                    _ext.ext().adam_capturable(mst, gr, m, v, model_out, self._hyp, self.beta1, self.beta2,
-                                               self.eps, wd, self.adamw, mul, self.found_inf)
-                else:
-                    _ext.ext().adam(mst, gr, m, v, model_out, self.lr, self.beta1, self.beta2, self.eps, wd, t,
-                                    self.adamw, mul, self.found_inf)
-                if host_out is not None:
-                    host_out.copy_(model_out)
-                if self.param_is_fp32:
-                    ddp.param_data[s:e].copy_(mst)
-            else:
-                ok = (self.found_inf == 0).float()
-                # an overflow step must leave every state untouched: inf * 0 would be NaN
-                gg = torch.where(self.found_inf == 0, gr * mul, torch.zeros_like(gr))
-                if not self.adamw and wd:
-                    gg = gg + wd * mst
-                m.mul_(1 - (1 - self.beta1) * ok).add_(gg * ((1 - self.beta1) * ok))
-                v.mul_(1 - (1 - self.beta2) * ok).add_(gg * gg * ((1 - self.beta2) * ok))
-                denom = v.sqrt() / math.sqrt(bc2) + self.eps
-                upd = (m / bc1) / denom
-                if self.adamw and wd:
-                    upd = upd + wd * mst
-                mst.sub_(self.lr * upd * ok)
-                ddp.param_data[s:e].copy_(mst.to(ddp.param_data.dtype))
+            self._update_piece(g, s, e, key, mo, mul, use_k, t, bc1, bc2)
         if self.scaler is not None:
             self.scaler.update(self.found_inf)
         if self.zero:
             ddp.all_gather_params()
         return self.grad_norm
+
+    _overlappable = True     # the per-bucket update may run on the overlapped side stream
+
+    def _update_piece(self, g, s, e, key, mo, mul, use_k, t, bc1, bc2):
+        """The fused (Adam / AdamW) update of one piece [s, e) of the flat buffers: fp32 master,
+        moments, the model-dtype parameter copy; skipped (state untouched) on found_inf."""
+        ddp = self.ddp
+        n = e - s
+        wd = self.weight_decay if key[0] else 0.0
+        mst, m, v = self.master[mo:mo + n], self.exp_avg[mo:mo + n], self.exp_avg_sq[mo:mo + n]
+        gr = g[s:e]
+        if gr.dtype != torch.float32:
+            gr = gr.float()
+        if use_k:
+            model_out = None if self.param_is_fp32 else ddp.param_data[s:e]
+            host_out = None
+            if model_out is not None and not model_out.is_cuda:   # offloaded ZeRO-3 param shard
+                host_out, model_out = model_out, torch.empty(n, dtype=model_out.dtype, device=mst.device)
+            if self.capturable:
+                _ext.ext().adam_capturable(mst, gr, m, v, model_out, self._hyp, self.beta1, self.beta2,
+                                           self.eps, wd, self.adamw, mul, self.found_inf)
+            else:
+                _ext.ext().adam(mst, gr, m, v, model_out, self.lr, self.beta1, self.beta2, self.eps, wd, t,
+                                self.adamw, mul, self.found_inf)
+            if host_out is not None:
+                host_out.copy_(model_out)
+            if self.param_is_fp32:
+                ddp.param_data[s:e].copy_(mst)
+        else:
+            ok = (self.found_inf == 0).float()
+            # an overflow step must leave every state untouched: inf * 0 would be NaN
+            gg = torch.where(self.found_inf == 0, gr * mul, torch.zeros_like(gr))
+            if not self.adamw and wd:
+                gg = gg + wd * mst
+            m.mul_(1 - (1 - self.beta1) * ok).add_(gg * ((1 - self.beta1) * ok))
+            v.mul_(1 - (1 - self.beta2) * ok).add_(gg * gg * ((1 - self.beta2) * ok))
+            denom = v.sqrt() / math.sqrt(bc2) + self.eps
+            upd = (m / bc1) / denom
+            if self.adamw and wd:
+                upd = upd + wd * mst
+            mst.sub_(self.lr * upd * ok)
+            ddp.param_data[s:e].copy_(mst.to(ddp.param_data.dtype))
 
     def _step_overlapped(self, g, mul, t):
         """The fused AdamW of every bucket on a side stream, in the forward order DDP computed
@@ -379,7 +388,8 @@ class MixedPrecisionAdam:
             self._step_t.fill_(self.step_count)
         self.master.copy_(d["master"])
         self.exp_avg.copy_(d["exp_avg"])
-        self.exp_avg_sq.copy_(d["exp_avg_sq"])
+        if self.exp_avg_sq.numel():          # (SGD keeps no second moment)
+            self.exp_avg_sq.copy_(d["exp_avg_sq"])
         self.lr = d.get("lr", self.lr)
         if self.scaler is not None and "scaler" in d:
             self.scaler.load_state_dict(d["scaler"])
@@ -388,3 +398,37 @@ class MixedPrecisionAdam:
                 self.ddp.param_data[s:e].copy_(self.master[mo:mo + (e - s)].to(self.ddp.param_data.dtype))
         if self.zero:
             self.ddp.all_gather_params()
+
+
+class MixedPrecisionSGD(MixedPrecisionAdam):
+    """``--optimizer sgd`` (Megatron's SGD path, /root/reference/3_training_megatron-lm/megatron/
+    arguments.py ``--optimizer`` / ``--sgd-momentum``): momentum SGD, torch.optim.SGD semantics
+    (buf = momentum * buf + g + wd * p; p -= lr * buf), over the same flat fp32 masters, gradient
+    reduction, clipping, loss scaling and found-inf skip as the Adam path. The momentum buffer is
+    ``exp_avg``; no second moment is kept. Elementwise torch ops (not a fused kernel): SGD is off
+    the measured path."""
+
+    _overlappable = False
+
+    def __init__(self, ddp: DistributedDataParallel, lr: float = 1e-2, momentum: float = 0.9,
+                 weight_decay: float = 0.0, clip_grad: float = 0.0, loss_scaler=None,
+                 use_distributed_optimizer: Optional[bool] = None):
+        super().__init__(ddp, lr=lr, weight_decay=weight_decay, adamw=False, clip_grad=clip_grad,
+                         loss_scaler=loss_scaler, use_distributed_optimizer=use_distributed_optimizer)
+        self.momentum = float(momentum)
+        self.exp_avg_sq = torch.empty(0, dtype=torch.float32, device=self.device)
+
+    def _update_piece(self, g, s, e, key, mo, mul, use_k, t, bc1, bc2):
+        ddp = self.ddp
+        n = e - s
+        wd = self.weight_decay if key[0] else 0.0
+        mst, buf = self.master[mo:mo + n], self.exp_avg[mo:mo + n]
+        gr = g[s:e].float()
+        ok = self.found_inf == 0
+        gg = torch.where(ok, gr * mul, torch.zeros_like(gr))
+        if wd:
+            gg = gg + wd * mst
+        buf.copy_(torch.where(ok, buf * self.momentum + gg, buf))
+        mst.sub_(self.lr * buf * ok.float())
+        out = ddp.param_data[s:e]
+        out.copy_(mst.to(out.dtype) if out.device == mst.device else mst.to(out.device, out.dtype))

@@ -323,6 +323,24 @@ _GROUPS = {
 IGNORED_GROUPS = tuple(t for t in _GROUPS if t.endswith("(accepted, ignored)"))
 
 
+# Model-form / NVIDIA-stack flags that parse but change nothing here: (flag, (dest, default)).
+# validate_args warns when one is set to a non-default value, so a run never silently differs.
+_NO_EFFECT = [
+    ("--apply-layernorm-1p", ("apply_layernorm_1p", False)),
+    ("--apply-residual-connection-post-layernorm", ("apply_residual_connection_post_layernorm", False)),
+    ("--fp32-residual-connection", ("fp32_residual_connection", False)),
+    ("--init-method-xavier-uniform", ("init_method_xavier_uniform", False)),
+    ("--num-experts", ("num_experts", None)),
+    ("--embedding-weights-in-fp32", ("embedding_weights_in_fp32", False)),
+    ("--fp16-lm-cross-entropy", ("fp16_lm_cross_entropy", False)),
+    ("--use-checkpoint-args", ("use_checkpoint_args", False)),
+    ("--no-initialization", ("perform_initialization", True)),
+    ("--transformer-impl", ("transformer_impl", "local")),
+    ("--fp8-e4m3", ("fp8_e4m3", False)),
+    ("--fp8-hybrid", ("fp8_hybrid", False)),
+]
+
+
 def ignored_flags_set(args) -> list:
     """The accepted-but-ignored flags (IGNORED_GROUPS) whose value differs from the default."""
     out = []
@@ -452,6 +470,13 @@ def validate_args(args, defaults=None):
         args.num_query_groups = args.num_attention_heads
     if args.use_rotary_position_embeddings:
         args.position_embedding_type = "rope"
+    if not args.add_position_embedding and args.position_embedding_type == "learned_absolute":
+        args.position_embedding_type = "none"          # --no-position-embedding: no positional table
+    no_effect = [f for f, d in _NO_EFFECT if getattr(args, d[0], d[1]) != d[1]]
+    if no_effect and args.rank == 0:
+        import warnings
+        warnings.warn("accepted but without effect here (the model keeps its standard form): "
+                      + " ".join(no_effect), stacklevel=2)
     if args.tensor_model_parallel_size == 1 and args.sequence_parallel:
         if args.rank == 0:
             print("Disabling sequence parallelism because tensor model parallel size is 1", flush=True)

@@ -37,7 +37,7 @@ from ..data.gpt_dataset import SyntheticGPTDataset, build_pretraining_data_loade
 from ..data.tokenizer import build_tokenizer, vocab_size_with_padding
 from ..models.gpt import allreduce_word_embedding_grads, gpt_flops_per_token
 from ..optim.lr_scheduler import OptimizerParamScheduler
-from ..optim.optimizer import ConstantLossScaler, DynamicLossScaler, MixedPrecisionAdam
+from ..optim.optimizer import ConstantLossScaler, DynamicLossScaler, MixedPrecisionAdam, MixedPrecisionSGD
 from ..parallel import state as ps
 from ..parallel.distributed import DistributedDataParallel
 from ..parallel.random import model_parallel_seed
@@ -143,9 +143,15 @@ def setup_model_and_optimizer(model_provider_func, args):
         scaler = ConstantLossScaler(args.loss_scale, dev) if args.loss_scale else DynamicLossScaler(
             args.initial_loss_scale, args.min_loss_scale, growth_interval=int(args.loss_scale_window),
             hysteresis=args.hysteresis, device=dev)
-    opt = MixedPrecisionAdam(ddp, lr=args.lr, betas=(args.adam_beta1, args.adam_beta2), eps=args.adam_eps,
-                             weight_decay=args.weight_decay, adamw=True, clip_grad=args.clip_grad,
-                             loss_scaler=scaler)
+    if getattr(args, "optimizer", "adam") == "sgd":
+        opt = MixedPrecisionSGD(ddp, lr=args.lr, momentum=args.sgd_momentum,
+                                weight_decay=args.weight_decay, clip_grad=args.clip_grad,
+                                loss_scaler=scaler)
+    else:
+        opt = MixedPrecisionAdam(ddp, lr=args.lr, betas=(args.adam_beta1, args.adam_beta2),
+                                 eps=args.adam_eps, weight_decay=args.weight_decay, adamw=True,
+                                 clip_grad=args.clip_grad, loss_scaler=scaler)
+    print_rank_0(f"> optimizer: {type(opt).__name__}")
     if args.train_samples:
         # Sample-based training (Megatron's rule, also under --rampup-batch-size, where
         # initialize_megatron derived train_iters): warmup / decay are counted in SAMPLES and the

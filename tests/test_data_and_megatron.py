@@ -139,6 +139,25 @@ def test_every_reference_megatron_flag_parses(monkeypatch):
                         {"tokenizer_type": "GPT2BPETokenizer"})
     msg = " ".join(str(x.message) for x in w)
     assert "--img-h" in msg and "--vision-pretraining" in msg
+    # model-form flags without effect here warn too; --no-position-embedding drops the table
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        A.validate_args(A.parse_args(argv=base), {"tokenizer_type": "GPT2BPETokenizer"})
+    assert not any("without effect" in str(x.message) for x in w)
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        a = A.validate_args(A.parse_args(argv=base + ["--apply-layernorm-1p", "--num-experts", "8",
+                                                      "--no-position-embedding"]),
+                            {"tokenizer_type": "GPT2BPETokenizer"})
+    msg = " ".join(str(x.message) for x in w)
+    assert "--apply-layernorm-1p" in msg and "--num-experts" in msg and "--no-position-embedding" not in msg
+    assert a.position_embedding_type == "none"
+    from smdt_amd.models.gpt import GPTModel
+    from smdt_amd.parallel import state as ps
+    ps.destroy_model_parallel()
+    a.padded_vocab_size = 64
+    cfg = A.core_transformer_config_from_args(a)
+    assert GPTModel(cfg).position_embeddings is None
 
 
 @pytest.mark.slow
@@ -403,3 +422,57 @@ def test_pretrain_gpt_logs_params_norm_and_num_zeros(tmp_path):
     assert all(math.isfinite(x) and x > 0 for x in pn) and len(set(pn)) > 1, pn
     assert all(x >= 0 and x == int(x) for x in nz), nz
     assert all(ln.index("grad norm:") < ln.index("num zeros:") < ln.index("params norm:") for ln in lines)
+
+
+def test_sgd_optimizer_matches_torch_sgd():
+    """``--optimizer sgd``: MixedPrecisionSGD over the flat fp32 masters equals torch.optim.SGD
+    (momentum, no dampening) on an identical copy of the model, step for step."""
+    import copy
+    from smdt_amd.models.gpt import GPTModel
+    from smdt_amd.models.transformer import TransformerConfig
+    from smdt_amd.optim.optimizer import MixedPrecisionSGD
+    from smdt_amd.parallel import state as ps
+    from smdt_amd.parallel.distributed import DistributedDataParallel
+    ps.destroy_model_parallel()
+    cfg = TransformerConfig(num_layers=1, hidden_size=32, num_attention_heads=2, max_position_embeddings=16,
+                            padded_vocab_size=64, params_dtype=torch.float32, hidden_dropout=0.0,
+                            attention_dropout=0.0, seed=3)
+    model = GPTModel(cfg)
+    ref = copy.deepcopy(model)
+    ddp = DistributedDataParallel(model)
+    opt = MixedPrecisionSGD(ddp, lr=0.05, momentum=0.9)
+    ropt = torch.optim.SGD(ref.parameters(), lr=0.05, momentum=0.9)
+    g = torch.Generator().manual_seed(0)
+    for _ in range(3):
+        tok = torch.randint(0, 64, (2, 17), generator=g)
+        ddp.zero_grad_buffer()
+        ddp(tok[:, :-1], None, None, labels=tok[:, 1:]).float().mean().backward()
+        ddp.finish_grad_sync()
+        opt.step()
+        ropt.zero_grad()
+        ref(tok[:, :-1], None, None, labels=tok[:, 1:]).float().mean().backward()
+        ropt.step()
+    got = dict(model.named_parameters())
+    for k, p in ref.named_parameters():
+        torch.testing.assert_close(got[k], p, rtol=1e-5, atol=1e-6, msg=k)
+    assert opt.exp_avg.abs().sum() > 0 and opt.exp_avg_sq.numel() == 0
+
+
+def test_pretrain_gpt_optimizer_sgd_trains(tmp_path):
+    """``--optimizer sgd --sgd-momentum 0.9`` reaches the SGD update (not Adam's): the run logs the
+    optimizer it built and every logged loss is finite."""
+    import re
+    script = os.path.join(REPO, "recipes", "3_training_megatron-lm", "pretrain_gpt.py")
+    args = ["--num-layers", "2", "--hidden-size", "64", "--num-attention-heads", "4", "--seq-length", "64",
+            "--max-position-embeddings", "64", "--micro-batch-size", "2", "--global-batch-size", "4",
+            "--lr", "0.05", "--lr-warmup-iters", "0", "--mock-data", "--log-interval", "1", "--eval-interval",
+            "100", "--eval-iters", "1", "--vocab-size", "512", "--tokenizer-type", "NullTokenizer",
+            "--train-iters", "4", "--optimizer", "sgd", "--sgd-momentum", "0.9"]
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT="29543")
+    r = subprocess.run([sys.executable, script] + args, env=env, capture_output=True, text=True, timeout=600,
+                       cwd=str(tmp_path))
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    assert "optimizer: MixedPrecisionSGD" in r.stdout + r.stderr
+    losses = [float(re.search(r"lm loss: (\S+) \|", ln).group(1)) for ln in r.stdout.splitlines()
+              if "lm loss:" in ln and "iteration" in ln]
+    assert len(losses) == 4 and all(math.isfinite(x) for x in losses), losses
