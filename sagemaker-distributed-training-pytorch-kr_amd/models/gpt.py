@@ -60,6 +60,10 @@ class GPTModel(nn.Module):
     def __init__(self, cfg: TransformerConfig, pre_process: bool = True, post_process: bool = True,
                  parallel_output: bool = True, device=None, layer_range=None):
         super().__init__()
+        with tp.weight_init(cfg.init_method, cfg.perform_initialization):
+            self._build(cfg, pre_process, post_process, parallel_output, device, layer_range)
+
+    def _build(self, cfg, pre_process, post_process, parallel_output, device, layer_range):
         st = ps.get_state()
         self.cfg = cfg
         self.pre_process, self.post_process = pre_process, post_process

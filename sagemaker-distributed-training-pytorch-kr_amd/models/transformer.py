@@ -46,6 +46,8 @@ class TransformerConfig:
     hidden_dropout: float = 0.1
     attention_dropout: float = 0.1
     layernorm_epsilon: float = 1e-5
+    layernorm_zero_centered_gamma: bool = False  # --apply-layernorm-1p: gamma stored as (gamma - 1)
+    apply_residual_connection_post_layernorm: bool = False   # residual taken after the norm
     normalization: str = "LayerNorm"            # or "RMSNorm"
     activation: str = "gelu"                     # gelu | swiglu | squared_relu | gelu_erf
     add_bias_linear: bool = True
@@ -57,6 +59,8 @@ class TransformerConfig:
     padded_vocab_size: int = 50304
     untie_embeddings_and_output_weights: bool = False
     init_method_std: float = 0.02
+    init_method: str = "normal"                  # or "xavier_uniform" (--init-method-xavier-uniform)
+    perform_initialization: bool = True         # False: --no-initialization (weights left unset)
     params_dtype: torch.dtype = torch.bfloat16
     seed: int = 1234
     # parallelism
@@ -111,7 +115,11 @@ class Norm(nn.Module):
         # Sequence-parallel activations are sharded across TP: draw their dropout masks from the
         # per-TP-rank stream; replicated activations use the TP-identical default stream.
         self.rng_kind = "tp" if cfg.sequence_parallel and ps.get_state().tp > 1 else "default"
-        self.weight = nn.Parameter(torch.ones(h, dtype=cfg.params_dtype, device=device))
+        # --apply-layernorm-1p: the stored gamma is centred on zero (so weight decay pulls the
+        # scale toward 1) and the kernel reads 1 + weight
+        self.one_p = bool(cfg.layernorm_zero_centered_gamma)
+        init = torch.zeros if self.one_p else torch.ones
+        self.weight = nn.Parameter(init(h, dtype=cfg.params_dtype, device=device))
         self.weight.sequence_parallel = cfg.sequence_parallel
         if not self.rms:
             self.bias = nn.Parameter(torch.zeros(h, dtype=cfg.params_dtype, device=device))
@@ -123,7 +131,8 @@ class Norm(nn.Module):
         # called instead of forward() by the layers: wait for this module's overlapped ZeRO
         # parameter all-gather (see _gather_wait) before the kernel reads the weights
         _gather_wait(self, x)
-        return SF.bias_dropout_add_norm(x, xbias, residual, self.weight, self.bias, p, training, self.eps, self.rms,
+        w = self.weight + 1 if self.one_p else self.weight
+        return SF.bias_dropout_add_norm(x, xbias, residual, w, self.bias, p, training, self.eps, self.rms,
                                         rng=get_rng(self.rng_kind), gather=gather)
 
     def forward(self, x):
@@ -566,6 +575,10 @@ class ParallelTransformerLayer(nn.Module):
         self.attention = ParallelAttention(cfg, layer_number, device)
         self.post_attention_norm = Norm(cfg.hidden_size, cfg, device)
         self.mlp = ParallelMLP(cfg, layer_number, device)
+        self.post_ln_residual = bool(cfg.apply_residual_connection_post_layernorm)
+        if self.post_ln_residual and cfg.sequence_parallel and ps.get_state().tp > 1:
+            # the SP norms hand their output to the all-gather, not back as a local residual
+            raise NotImplementedError("--apply-residual-connection-post-layernorm with --sequence-parallel")
 
     def forward(self, x, xbias, residual):
         training = self.training
@@ -576,9 +589,13 @@ class ParallelTransformerLayer(nn.Module):
         g = _sp_gather(self.cfg)
         ln1, residual = self.input_norm.fused(x, xbias, residual, p, training,
                                               gather=None if g is None else g + (True, residual is not None))
+        if self.post_ln_residual:           # Megatron's --apply-residual-connection-post-layernorm
+            residual = ln1
         a, ab = self.attention(ln1, training)
         ln2, residual = self.post_attention_norm.fused(a, ab, residual, p, training,
                                                        gather=None if g is None else g + (True, True))
+        if self.post_ln_residual:
+            residual = ln2
         m, mb = self.mlp(ln2)
         return m, mb, residual
 

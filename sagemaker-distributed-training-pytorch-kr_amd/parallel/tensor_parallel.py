@@ -17,6 +17,7 @@ Design notes (MI355X-first):
 """
 from __future__ import annotations
 
+import contextlib
 import hashlib
 import math
 import os
@@ -2163,18 +2164,47 @@ def _key_seed(base_seed: int, key: str) -> int:
     return int.from_bytes(h[:8], "little") & ((1 << 62) - 1)
 
 
+_INIT = {"method": "normal", "perform": True}
+
+
+@contextlib.contextmanager
+def weight_init(method: str = "normal", perform: bool = True):
+    """The init rule of the weights built inside (Megatron's ``--init-method-xavier-uniform`` /
+    ``--no-initialization``, /root/reference/3_training_megatron-lm/megatron/arguments.py):
+    ``"normal"`` draws N(0, std); ``"xavier_uniform"`` draws U(-a, a), a = sqrt(6 / (fan_in +
+    fan_out)) of the FULL 2-D weight (so the values do not depend on the TP degree), for every
+    weight, the scaled output layers included; ``perform=False`` leaves weights unset (they are
+    about to be loaded from a checkpoint) and skips the full-tensor draw."""
+    assert method in ("normal", "xavier_uniform"), method
+    old = dict(_INIT)
+    _INIT.update(method=method, perform=bool(perform))
+    try:
+        yield
+    finally:
+        _INIT.update(old)
+
+
 @torch.no_grad()
 def init_full_then_shard(shape, std: float, key: str, base_seed: int, dtype, device, shard_dim: Optional[int],
                          rank: int, world: int, chunks=None):
     """Normal(0, std) init of the FULL tensor from a deterministic generator, then return this
     rank's shard along ``shard_dim``. ``chunks`` (a list of sizes along shard_dim) shards each
-    chunk separately (fused QKV / gate-up weights keep per-rank [q|k|v] groups)."""
+    chunk separately (fused QKV / gate-up weights keep per-rank [q|k|v] groups). ``weight_init``
+    switches the rule (Xavier-uniform, or no initialization)."""
     dev = torch.device(device) if device is not None else torch.device("cpu")
+    if not _INIT["perform"]:
+        sh = list(shape)
+        if shard_dim is not None and world > 1:
+            sh[shard_dim] //= world
+        return torch.empty(sh, dtype=dtype, device=dev)
     gen = torch.Generator(device=dev)
     gen.manual_seed(_key_seed(base_seed, key))
     full = torch.empty(shape, dtype=torch.float32, device=dev)
     if std == 0:
         full.zero_()
+    elif _INIT["method"] == "xavier_uniform" and len(shape) == 2:
+        a = math.sqrt(6.0 / (shape[0] + shape[1]))
+        full.uniform_(-a, a, generator=gen)
     else:
         full.normal_(0.0, std, generator=gen)
     if shard_dim is None or world == 1:

@@ -326,15 +326,10 @@ IGNORED_GROUPS = tuple(t for t in _GROUPS if t.endswith("(accepted, ignored)"))
 # Model-form / NVIDIA-stack flags that parse but change nothing here: (flag, (dest, default)).
 # validate_args warns when one is set to a non-default value, so a run never silently differs.
 _NO_EFFECT = [
-    ("--apply-layernorm-1p", ("apply_layernorm_1p", False)),
-    ("--apply-residual-connection-post-layernorm", ("apply_residual_connection_post_layernorm", False)),
     ("--fp32-residual-connection", ("fp32_residual_connection", False)),
-    ("--init-method-xavier-uniform", ("init_method_xavier_uniform", False)),
     ("--num-experts", ("num_experts", None)),
     ("--embedding-weights-in-fp32", ("embedding_weights_in_fp32", False)),
     ("--fp16-lm-cross-entropy", ("fp16_lm_cross_entropy", False)),
-    ("--use-checkpoint-args", ("use_checkpoint_args", False)),
-    ("--no-initialization", ("perform_initialization", True)),
     ("--transformer-impl", ("transformer_impl", "local")),
     ("--fp8-e4m3", ("fp8_e4m3", False)),
     ("--fp8-hybrid", ("fp8_hybrid", False)),
@@ -530,6 +525,10 @@ def core_transformer_config_from_args(args) -> TransformerConfig:
         padded_vocab_size=args.padded_vocab_size,
         untie_embeddings_and_output_weights=args.untie_embeddings_and_output_weights,
         init_method_std=args.init_method_std, params_dtype=args.params_dtype, seed=args.seed,
+        init_method="xavier_uniform" if args.init_method_xavier_uniform else "normal",
+        layernorm_zero_centered_gamma=args.apply_layernorm_1p,
+        apply_residual_connection_post_layernorm=args.apply_residual_connection_post_layernorm,
+        perform_initialization=args.perform_initialization,
         sequence_parallel=args.sequence_parallel,
         async_tensor_model_parallel_allreduce=args.async_tensor_model_parallel_allreduce,
         masked_softmax_fusion=args.masked_softmax_fusion, bias_gelu_fusion=args.bias_gelu_fusion,

@@ -232,6 +232,43 @@ def read_tracker(load_dir: str):
     return int(s), False
 
 
+# The model-shape arguments ``--use-checkpoint-args`` takes from the checkpoint (Megatron's
+# load_args_from_checkpoint, /root/reference/3_training_megatron-lm/megatron/checkpointing.py).
+CHECKPOINT_ARGS = ("num_layers", "hidden_size", "ffn_hidden_size", "seq_length", "num_attention_heads",
+                   "num_query_groups", "group_query_attention", "kv_channels", "max_position_embeddings",
+                   "position_embedding_type", "add_position_embedding", "use_rotary_position_embeddings",
+                   "rotary_percent", "add_bias_linear", "swiglu", "untie_embeddings_and_output_weights",
+                   "normalization", "layernorm_epsilon", "tokenizer_type", "vocab_size", "padded_vocab_size",
+                   "make_vocab_size_divisible_by", "tensor_model_parallel_size",
+                   "pipeline_model_parallel_size")
+
+
+def load_args_from_checkpoint(args, load_dir: Optional[str] = None) -> bool:
+    """``--use-checkpoint-args``: overwrite the model-shape arguments with the ones the checkpoint
+    under ``--load`` was saved with (before ``validate_args``). Reads the tensor/pipeline rank-0
+    file only, with ``weights_only=True``. Returns False (args untouched) when there is none."""
+    load_dir = load_dir or getattr(args, "load", None)
+    if not load_dir:
+        raise SystemExit("--use-checkpoint-args needs --load")
+    it, release = read_tracker(load_dir)
+    if it is None:
+        print(f"WARNING: --use-checkpoint-args: no checkpoint under {load_dir}; using the command line",
+              flush=True)
+        return False
+    d = os.path.join(load_dir, "release" if release else f"iter_{it:07d}")
+    for sub in ("mp_rank_00", "mp_rank_00_000"):
+        f = os.path.join(d, sub, "model_optim_rng.pt")
+        if os.path.isfile(f):
+            break
+    else:
+        raise SystemExit(f"--use-checkpoint-args: no rank-0 checkpoint file under {d}")
+    saved = torch.load(f, map_location="cpu", weights_only=True).get("args", {})
+    for k in CHECKPOINT_ARGS:
+        if k in saved and hasattr(args, k):
+            setattr(args, k, saved[k])
+    return True
+
+
 def load_checkpoint(model, optimizer=None, scheduler=None, args=None, load_dir: Optional[str] = None,
                     strict: bool = True) -> int:
     """Returns the iteration to resume from (0 when nothing was loaded)."""

@@ -66,6 +66,9 @@ def initialize_megatron(extra_args_provider=None, args_defaults=None, ignore_unk
     args = A.parse_args(extra_args_provider, ignore_unknown_args, argv)
     rank, local, world, backend = init_distributed(args.distributed_backend, args.distributed_timeout_minutes)
     args.rank, args.world_size, args.local_rank = rank, world, local
+    if args.use_checkpoint_args or (args_defaults or {}).get("use_checkpoint_args", False):
+        from .checkpointing import load_args_from_checkpoint
+        load_args_from_checkpoint(args)
     A.validate_args(args, args_defaults or {})
     ps.initialize_model_parallel(args.tensor_model_parallel_size, args.pipeline_model_parallel_size,
                                  args.virtual_pipeline_model_parallel_size, args.context_parallel_size)

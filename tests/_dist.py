@@ -8,7 +8,25 @@ import traceback
 import torch.multiprocessing as mp
 
 
+_NEXT = [0]
+
+
 def free_port():
+    """A free port BELOW the kernel's ephemeral range (32768+), in a block of its own per xdist
+    worker: an ephemeral port probed free here could be taken by another test's Gloo connection
+    before rank 0's store binds it (a parallel run then hung in rendezvous)."""
+    w = os.environ.get("PYTEST_XDIST_WORKER", "gw0")
+    wid = int(w[2:]) if w[2:].isdigit() else 0
+    base = 10000 + (wid % 16) * 1000
+    for _ in range(1000):
+        port = base + (os.getpid() * 7 + _NEXT[0]) % 1000
+        _NEXT[0] += 1
+        with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+            try:
+                s.bind(("127.0.0.1", port))
+            except OSError:
+                continue
+            return port
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
         s.bind(("127.0.0.1", 0))
         return s.getsockname()[1]

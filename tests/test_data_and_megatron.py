@@ -146,11 +146,12 @@ def test_every_reference_megatron_flag_parses(monkeypatch):
     assert not any("without effect" in str(x.message) for x in w)
     with warnings.catch_warnings(record=True) as w:
         warnings.simplefilter("always")
-        a = A.validate_args(A.parse_args(argv=base + ["--apply-layernorm-1p", "--num-experts", "8",
-                                                      "--no-position-embedding"]),
+        a = A.validate_args(A.parse_args(argv=base + ["--fp32-residual-connection", "--num-experts", "8",
+                                                      "--no-position-embedding", "--apply-layernorm-1p"]),
                             {"tokenizer_type": "GPT2BPETokenizer"})
     msg = " ".join(str(x.message) for x in w)
-    assert "--apply-layernorm-1p" in msg and "--num-experts" in msg and "--no-position-embedding" not in msg
+    assert "--fp32-residual-connection" in msg and "--num-experts" in msg
+    assert "--no-position-embedding" not in msg and "--apply-layernorm-1p" not in msg
     assert a.position_embedding_type == "none"
     from smdt_amd.models.gpt import GPTModel
     from smdt_amd.parallel import state as ps
@@ -476,3 +477,114 @@ def test_pretrain_gpt_optimizer_sgd_trains(tmp_path):
     losses = [float(re.search(r"lm loss: (\S+) \|", ln).group(1)) for ln in r.stdout.splitlines()
               if "lm loss:" in ln and "iteration" in ln]
     assert len(losses) == 4 and all(math.isfinite(x) for x in losses), losses
+
+
+def test_pretrain_gpt_use_checkpoint_args(tmp_path):
+    """``--use-checkpoint-args``: a resumed run given a different model shape on its command line
+    takes the checkpoint's (num layers, hidden size, heads) and loads it strictly; without the flag
+    the same command line cannot load that checkpoint."""
+    script = os.path.join(REPO, "recipes", "3_training_megatron-lm", "pretrain_gpt.py")
+    common = ["--seq-length", "32", "--max-position-embeddings", "32", "--micro-batch-size", "2",
+              "--global-batch-size", "2", "--lr", "0.01", "--mock-data", "--log-interval", "1",
+              "--eval-interval", "100", "--eval-iters", "1", "--vocab-size", "256", "--tokenizer-type",
+              "NullTokenizer", "--save-interval", "2"]
+    first = ["--num-layers", "2", "--hidden-size", "64", "--num-attention-heads", "4", "--train-iters", "2",
+             "--save", str(tmp_path / "ck")]
+    other = ["--num-layers", "3", "--hidden-size", "32", "--num-attention-heads", "2", "--train-iters", "3",
+             "--load", str(tmp_path / "ck")]
+
+    def run(extra, port):
+        env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port))
+        return subprocess.run([sys.executable, script] + common + extra, env=env, capture_output=True,
+                              text=True, timeout=600, cwd=str(tmp_path))
+    r = run(first, 29545)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    r = run(other + ["--use-checkpoint-args"], 29546)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    assert "successfully loaded checkpoint" in r.stdout and "iteration        3/" in r.stdout, r.stdout[-2000:]
+    r = run(other, 29547)
+    assert r.returncode != 0
+
+
+def test_xavier_init_and_no_initialization():
+    """``--init-method-xavier-uniform`` draws every 2-D weight from U(-a, a), a = sqrt(6 / (fan_in +
+    fan_out)) of the full weight; ``--no-initialization`` builds the model without drawing (the
+    checkpoint load fills it); the default stays N(0, init_method_std)."""
+    import math as _m
+    from smdt_amd.models.gpt import GPTModel
+    from smdt_amd.models.transformer import TransformerConfig
+    from smdt_amd.parallel import state as ps
+    from smdt_amd.train import arguments as A
+    ps.destroy_model_parallel()
+    base = dict(num_layers=1, hidden_size=64, num_attention_heads=4, max_position_embeddings=32,
+                padded_vocab_size=128, params_dtype=torch.float32, ffn_hidden_size=256)
+    xa = GPTModel(TransformerConfig(init_method="xavier_uniform", **base))
+    nm = GPTModel(TransformerConfig(**base))
+    for (k, p), (_, q) in zip(xa.named_parameters(), nm.named_parameters()):
+        if p.dim() != 2:
+            continue
+        a = _m.sqrt(6.0 / (p.shape[0] + p.shape[1]))
+        assert p.abs().max() <= a and p.abs().max() > 0.9 * a, k      # bounded by, and fills, [-a, a]
+        assert abs(p.std().item() - a / _m.sqrt(3)) < 0.1 * a, k
+        assert 0 < q.std().item() < 0.022, k                         # N(0, std) (scaled on outputs)
+    un = GPTModel(TransformerConfig(perform_initialization=False, **base))
+    assert [p.shape for p in un.parameters()] == [p.shape for p in nm.parameters()]
+    argv = ["--num-layers", "1", "--hidden-size", "64", "--num-attention-heads", "4", "--seq-length", "32",
+            "--max-position-embeddings", "32", "--micro-batch-size", "2", "--init-method-xavier-uniform",
+            "--no-initialization"]
+    old = {k: os.environ.get(k) for k in ("WORLD_SIZE", "RANK")}
+    os.environ.update(WORLD_SIZE="1", RANK="0")
+    try:
+        a = A.validate_args(A.parse_args(argv=argv), {"tokenizer_type": "GPT2BPETokenizer"})
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    a.padded_vocab_size = 128
+    cfg = A.core_transformer_config_from_args(a)
+    assert cfg.init_method == "xavier_uniform" and cfg.perform_initialization is False
+
+
+def test_layernorm_1p_and_post_layernorm_residual():
+    """``--apply-layernorm-1p``: gamma is stored centred on zero and the norm scales by 1 + gamma
+    (same output as the standard norm at init, gradient lands on the stored tensor).
+    ``--apply-residual-connection-post-layernorm``: each sub-block's residual is the norm's OUTPUT,
+    checked against the layer's own modules composed by hand (eval mode, no dropout)."""
+    from smdt_amd.models.gpt import GPTModel
+    from smdt_amd.models.transformer import ParallelTransformerLayer, TransformerConfig
+    from smdt_amd.parallel import state as ps
+    ps.destroy_model_parallel()
+    base = dict(num_layers=1, hidden_size=64, num_attention_heads=4, max_position_embeddings=32,
+                padded_vocab_size=128, params_dtype=torch.float32, hidden_dropout=0.0, attention_dropout=0.0)
+    tok = torch.randint(0, 128, (2, 17), generator=torch.Generator().manual_seed(0))
+    std = GPTModel(TransformerConfig(seed=5, **base)).eval()
+    onep = GPTModel(TransformerConfig(seed=5, layernorm_zero_centered_gamma=True, **base)).eval()
+    w = onep.decoder.layers[0].input_norm.weight
+    assert torch.equal(w, torch.zeros_like(w))
+    l0 = std(tok[:, :-1], None, None, labels=tok[:, 1:]).float().mean()
+    l1 = onep(tok[:, :-1], None, None, labels=tok[:, 1:]).float().mean()
+    torch.testing.assert_close(l1, l0)
+    l1.backward()
+    assert w.grad is not None and w.grad.abs().sum() > 0
+    with torch.no_grad():
+        w.add_(0.5)                                   # scale 1.5: the output changes
+    assert not torch.allclose(onep(tok[:, :-1], None, None, labels=tok[:, 1:]).float().mean(), l0)
+
+    cfg = TransformerConfig(seed=7, apply_residual_connection_post_layernorm=True, **base)
+    layer = ParallelTransformerLayer(cfg, 1).eval()
+    x = torch.randn(16, 2, 64, generator=torch.Generator().manual_seed(1))
+    with torch.no_grad():
+        m, mb, res = layer(x, None, None)
+        ln1 = layer.input_norm(x)
+        a, ab = layer.attention(ln1, False)
+        ln2 = layer.post_attention_norm(ln1 + a + (ab if ab is not None else 0))
+        m2, mb2 = layer.mlp(ln2)
+    torch.testing.assert_close(res, ln2)
+    torch.testing.assert_close(m, m2)
+    model = GPTModel(TransformerConfig(seed=7, apply_residual_connection_post_layernorm=True, **base))
+    loss = model(tok[:, :-1], None, None, labels=tok[:, 1:]).float().mean()
+    loss.backward()
+    assert torch.isfinite(loss) and all(p.grad is not None for p in model.parameters() if p.requires_grad)

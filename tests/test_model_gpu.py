@@ -79,3 +79,40 @@ def test_pretrain_gpt_nb3_fp16_flags_on_kernels(tmp_path):
     assert math.isfinite(loss), last[:400]
 
 
+
+
+@pytest.mark.parametrize("one_p,post_ln", [(True, False), (False, True)])
+def test_gpt_model_form_variants_match_fp32_reference(one_p, post_ln):
+    """``--apply-layernorm-1p`` (the fused norm kernel reads 1 + stored gamma) and
+    ``--apply-residual-connection-post-layernorm`` (residual = norm output) through the bf16
+    kernels: loss and every gradient against the same weights on the fp32 PyTorch path."""
+    from smdt_amd.models.gpt import GPTModel
+    from smdt_amd.models.transformer import TransformerConfig
+    from smdt_amd.parallel import state as ps
+    from smdt_amd.parallel.distributed import DistributedDataParallel
+    ps.destroy_model_parallel()
+    kw = dict(num_layers=2, hidden_size=256, num_attention_heads=4, max_position_embeddings=256,
+              padded_vocab_size=1024, hidden_dropout=0.0, attention_dropout=0.0, seed=3,
+              layernorm_zero_centered_gamma=one_p, apply_residual_connection_post_layernorm=post_ln)
+    ref = GPTModel(TransformerConfig(**kw, params_dtype=torch.float32))
+    gpu = GPTModel(TransformerConfig(**kw, params_dtype=torch.bfloat16), device="cuda")
+    g = torch.Generator().manual_seed(5)
+    with torch.no_grad():
+        for n, pr in ref.named_parameters():
+            if "norm.weight" in n:                     # gamma away from its init value
+                pr.add_(0.2 * torch.randn(pr.shape, generator=g))
+        for pr, pg in zip(ref.parameters(), gpu.parameters()):
+            pg.copy_(pr.to(torch.bfloat16))
+            pr.copy_(pg.float().cpu())
+    ddp = DistributedDataParallel(gpu)
+    toks = torch.randint(0, 1000, (4, 257), generator=g)
+    loss_ref = ref(toks[:, :-1], labels=toks[:, 1:])
+    loss_ref.mean().backward()
+    ddp.zero_grad_buffer()
+    loss = gpu(toks[:, :-1].cuda(), labels=toks[:, 1:].cuda())
+    loss.float().mean().backward()
+    ddp.finish_grad_sync()
+    torch.testing.assert_close(loss.float().cpu(), loss_ref.detach(), atol=3e-2, rtol=1e-2)
+    for (n, pr), pg in zip(ref.named_parameters(), gpu.parameters()):
+        err = (pg.main_grad.float().cpu() - pr.grad).norm() / pr.grad.norm().clamp_min(1e-12)
+        assert err < 3e-2, (n, err.item())
