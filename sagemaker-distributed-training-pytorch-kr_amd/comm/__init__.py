@@ -68,7 +68,21 @@ def init_distributed(backend: str | None = None, timeout_minutes: int = 10, set_
         if be == "nccl":
             kw["device_id"] = torch.device("cuda", torch.cuda.current_device())
         dist.init_process_group(**kw)
+        if be == "gloo":
+            # tear the Gloo group down before the interpreter does: left to the shutdown order, a
+            # 2-rank CPU job sometimes aborted at exit ("terminate called without an active
+            # exception") after finishing its work
+            import atexit
+            atexit.register(_destroy_at_exit)
     return rank, local, world, be
+
+
+def _destroy_at_exit():
+    if dist.is_initialized():
+        try:
+            dist.destroy_process_group()
+        except Exception:       # exiting anyway; the group may already be torn down
+            pass
 
 
 def is_rank_0() -> bool:

@@ -50,6 +50,7 @@ class TransformerConfig:
     apply_residual_connection_post_layernorm: bool = False   # residual taken after the norm
     normalization: str = "LayerNorm"            # or "RMSNorm"
     activation: str = "gelu"                     # gelu | swiglu | squared_relu | gelu_erf
+    num_experts: Optional[int] = None            # --num-experts: Switch MLP (top-1 routed experts)
     add_bias_linear: bool = True
     position_embedding_type: str = "learned_absolute"   # or "rope"
     rotary_percent: float = 1.0
@@ -503,23 +504,24 @@ def _apply_rope_parts(flat, cos, sin, rot, nh, nkv, hd, b, s, inverse):
 
 
 class ParallelMLP(nn.Module):
-    def __init__(self, cfg: TransformerConfig, layer_number: int, device=None):
+    def __init__(self, cfg: TransformerConfig, layer_number: int, device=None, key: Optional[str] = None):
         super().__init__()
         self.cfg = cfg
+        key = key or f"layers.{layer_number}"
         f = cfg.ffn_hidden_size
         std = cfg.init_method_std
         out_std = std / math.sqrt(2.0 * cfg.num_layers)
         self.gated = cfg.activation == "swiglu"
         fc1_out = 2 * f if self.gated else f
         self.fc1 = tp.ColumnParallelLinear(cfg.hidden_size, fc1_out, bias=cfg.add_bias_linear, init_std=std,
-                                           key=f"layers.{layer_number}.fc1", seed=cfg.seed,
+                                           key=f"{key}.fc1", seed=cfg.seed,
                                            params_dtype=cfg.params_dtype, device=device,
                                            sequence_parallel=cfg.sequence_parallel, skip_bias_add=True,
                                            chunks=[f, f] if self.gated else None,
                                            async_tensor_model_parallel_allreduce=cfg.async_tensor_model_parallel_allreduce,
                                            bias_grad_from_output=True)   # forward() only ever uses h + b
         self.fc2 = tp.RowParallelLinear(f, cfg.hidden_size, bias=cfg.add_bias_linear, init_std=out_std,
-                                        key=f"layers.{layer_number}.fc2", seed=cfg.seed,
+                                        key=f"{key}.fc2", seed=cfg.seed,
                                         params_dtype=cfg.params_dtype, device=device,
                                         sequence_parallel=cfg.sequence_parallel, skip_bias_add=True)
 
@@ -559,6 +561,57 @@ class ParallelMLP(nn.Module):
         return self.fc2(h)
 
 
+class SwitchMLP(nn.Module):
+    """``--num-experts E``: Megatron's Switch MLP (top-1 routing; the flag at
+    /root/reference/3_training_megatron-lm/megatron/arguments.py:610-611, no expert-parallel group
+    there either). A router (h -> E, softmax in fp32) picks one expert per token; each expert is a
+    full ``ParallelMLP`` (tensor-parallel like the dense MLP); the token's output is the expert's
+    (output + bias) scaled by the router probability. Tokens are sorted by expert once, so each
+    expert runs ONE contiguous GEMM chain on its slice (no per-expert masks or scatters), and one
+    gather puts the rows back. The per-expert token counts are read on the host (one sync per layer),
+    so an MoE step is not graph-captured."""
+
+    def __init__(self, cfg: TransformerConfig, layer_number: int, device=None):
+        super().__init__()
+        if cfg.sequence_parallel and ps.get_state().tp > 1:
+            # each TP rank would route a different sequence shard, so the experts' TP collectives
+            # would not line up across the group
+            raise NotImplementedError("--num-experts with --sequence-parallel")
+        self.cfg = cfg
+        e = int(cfg.num_experts)
+        self.router = nn.Parameter(tp.init_full_then_shard(
+            (e, cfg.hidden_size), cfg.init_method_std, f"layers.{layer_number}.router", cfg.seed,
+            cfg.params_dtype, device, None, 0, 1))
+        self.router_bias = nn.Parameter(torch.zeros(e, dtype=cfg.params_dtype, device=device))
+        self.experts = nn.ModuleList(ParallelMLP(cfg, layer_number, device, key=f"layers.{layer_number}.experts.{i}")
+                                     for i in range(e))
+
+    def route(self, flat):
+        """(top-1 probability [n] fp32, expert index [n]) of each token row."""
+        prob = torch.softmax(F.linear(flat, self.router, self.router_bias).float(), dim=-1)
+        return prob.max(dim=-1)
+
+    def forward(self, x):
+        s, b, h = x.shape
+        flat = x.reshape(s * b, h)
+        top_p, top_e = self.route(flat)
+        order = torch.argsort(top_e, stable=True)
+        counts = torch.bincount(top_e, minlength=len(self.experts)).tolist()
+        xs = flat.index_select(0, order)
+        outs, o = [], 0
+        for i, n in enumerate(counts):
+            if n == 0:
+                continue          # an expert with no tokens gets no gradient this step
+            y, yb = self.experts[i](xs[o:o + n].unsqueeze(1))
+            y = y.squeeze(1)
+            outs.append(y + yb if yb is not None else y)
+            o += n
+        inv = torch.empty_like(order)
+        inv[order] = torch.arange(order.numel(), device=order.device)
+        out = torch.cat(outs).index_select(0, inv) * top_p.unsqueeze(-1).to(x.dtype)
+        return out.view(s, b, h), None
+
+
 def _sp_gather(cfg):
     """(tp, tp_rank) when sequence-parallel norms should write into all-gather slots."""
     if not cfg.sequence_parallel or _PACK["idx"] is not None:
@@ -574,7 +627,7 @@ class ParallelTransformerLayer(nn.Module):
         self.input_norm = Norm(cfg.hidden_size, cfg, device)
         self.attention = ParallelAttention(cfg, layer_number, device)
         self.post_attention_norm = Norm(cfg.hidden_size, cfg, device)
-        self.mlp = ParallelMLP(cfg, layer_number, device)
+        self.mlp = SwitchMLP(cfg, layer_number, device) if cfg.num_experts else ParallelMLP(cfg, layer_number, device)
         self.post_ln_residual = bool(cfg.apply_residual_connection_post_layernorm)
         if self.post_ln_residual and cfg.sequence_parallel and ps.get_state().tp > 1:
             # the SP norms hand their output to the all-gather, not back as a local residual

@@ -327,7 +327,6 @@ IGNORED_GROUPS = tuple(t for t in _GROUPS if t.endswith("(accepted, ignored)"))
 # validate_args warns when one is set to a non-default value, so a run never silently differs.
 _NO_EFFECT = [
     ("--fp32-residual-connection", ("fp32_residual_connection", False)),
-    ("--num-experts", ("num_experts", None)),
     ("--embedding-weights-in-fp32", ("embedding_weights_in_fp32", False)),
     ("--fp16-lm-cross-entropy", ("fp16_lm_cross_entropy", False)),
     ("--transformer-impl", ("transformer_impl", "local")),
@@ -526,7 +525,7 @@ def core_transformer_config_from_args(args) -> TransformerConfig:
         untie_embeddings_and_output_weights=args.untie_embeddings_and_output_weights,
         init_method_std=args.init_method_std, params_dtype=args.params_dtype, seed=args.seed,
         init_method="xavier_uniform" if args.init_method_xavier_uniform else "normal",
-        layernorm_zero_centered_gamma=args.apply_layernorm_1p,
+        layernorm_zero_centered_gamma=args.apply_layernorm_1p, num_experts=args.num_experts,
         apply_residual_connection_post_layernorm=args.apply_residual_connection_post_layernorm,
         perform_initialization=args.perform_initialization,
         sequence_parallel=args.sequence_parallel,

@@ -146,11 +146,11 @@ def test_every_reference_megatron_flag_parses(monkeypatch):
     assert not any("without effect" in str(x.message) for x in w)
     with warnings.catch_warnings(record=True) as w:
         warnings.simplefilter("always")
-        a = A.validate_args(A.parse_args(argv=base + ["--fp32-residual-connection", "--num-experts", "8",
+        a = A.validate_args(A.parse_args(argv=base + ["--fp32-residual-connection", "--embedding-weights-in-fp32",
                                                       "--no-position-embedding", "--apply-layernorm-1p"]),
                             {"tokenizer_type": "GPT2BPETokenizer"})
     msg = " ".join(str(x.message) for x in w)
-    assert "--fp32-residual-connection" in msg and "--num-experts" in msg
+    assert "--fp32-residual-connection" in msg and "--embedding-weights-in-fp32" in msg
     assert "--no-position-embedding" not in msg and "--apply-layernorm-1p" not in msg
     assert a.position_embedding_type == "none"
     from smdt_amd.models.gpt import GPTModel
@@ -588,3 +588,62 @@ def test_layernorm_1p_and_post_layernorm_residual():
     loss = model(tok[:, :-1], None, None, labels=tok[:, 1:]).float().mean()
     loss.backward()
     assert torch.isfinite(loss) and all(p.grad is not None for p in model.parameters() if p.requires_grad)
+
+
+def test_switch_mlp_routes_each_token_to_one_expert():
+    """``--num-experts``: every token's MLP output is (its top-1 expert's output + bias) x the
+    router probability, checked token by token; gradients reach the router and every expert that
+    received tokens; a GPT with experts trains a step through DDP + the optimizer."""
+    from smdt_amd.models.gpt import GPTModel
+    from smdt_amd.models.transformer import SwitchMLP, TransformerConfig
+    from smdt_amd.optim.optimizer import MixedPrecisionAdam
+    from smdt_amd.parallel import state as ps
+    from smdt_amd.parallel.distributed import DistributedDataParallel
+    from smdt_amd.train import arguments as A
+    ps.destroy_model_parallel()
+    base = dict(num_layers=2, hidden_size=32, num_attention_heads=2, max_position_embeddings=32,
+                padded_vocab_size=64, params_dtype=torch.float32, hidden_dropout=0.0, attention_dropout=0.0,
+                num_experts=4, seed=2)
+    cfg = TransformerConfig(**base)
+    mlp = SwitchMLP(cfg, 1)
+    with torch.no_grad():
+        mlp.router.mul_(50)                              # spread the routing over the experts
+    x = torch.randn(8, 3, 32, generator=torch.Generator().manual_seed(0), requires_grad=True)
+    out, bias = mlp(x)
+    assert bias is None and out.shape == x.shape
+    p, e = mlp.route(x.detach().reshape(-1, 32))
+    assert len(set(e.tolist())) > 1
+    for t in range(24):
+        y, yb = mlp.experts[int(e[t])](x.detach().reshape(-1, 32)[t].view(1, 1, 32))
+        want = (y + yb).view(32) * p[t]
+        torch.testing.assert_close(out.reshape(-1, 32)[t], want, rtol=1e-5, atol=1e-6)
+    out.square().sum().backward()
+    assert mlp.router.grad is not None and mlp.router.grad.abs().sum() > 0
+    for i, ex in enumerate(mlp.experts):
+        if (e == i).any():
+            assert ex.fc1.weight.grad is not None or getattr(ex.fc1.weight, "main_grad", None) is not None
+    model = GPTModel(TransformerConfig(**base))
+    assert sum(1 for n, _ in model.named_parameters() if ".experts." in n) > 0
+    ddp = DistributedDataParallel(model)
+    opt = MixedPrecisionAdam(ddp, lr=1e-2)
+    tok = torch.randint(0, 64, (2, 17), generator=torch.Generator().manual_seed(1))
+    before = ddp.param_data.clone()
+    ddp.zero_grad_buffer()
+    ddp(tok[:, :-1], None, None, labels=tok[:, 1:]).float().mean().backward()
+    ddp.finish_grad_sync()
+    opt.step()
+    assert not torch.equal(before, ddp.param_data)
+    argv = ["--num-layers", "1", "--hidden-size", "64", "--num-attention-heads", "4", "--seq-length", "32",
+            "--max-position-embeddings", "32", "--micro-batch-size", "2", "--num-experts", "8"]
+    old = {k: os.environ.get(k) for k in ("WORLD_SIZE", "RANK")}
+    os.environ.update(WORLD_SIZE="1", RANK="0")
+    try:
+        a = A.validate_args(A.parse_args(argv=argv), {"tokenizer_type": "GPT2BPETokenizer"})
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    a.padded_vocab_size = 128
+    assert A.core_transformer_config_from_args(a).num_experts == 8

@@ -116,3 +116,32 @@ def test_gpt_model_form_variants_match_fp32_reference(one_p, post_ln):
     for (n, pr), pg in zip(ref.named_parameters(), gpu.parameters()):
         err = (pg.main_grad.float().cpu() - pr.grad).norm() / pr.grad.norm().clamp_min(1e-12)
         assert err < 3e-2, (n, err.item())
+
+
+def test_switch_mlp_on_kernels_matches_per_expert_composition():
+    """``--num-experts`` on the GPU: the sorted-slice Switch MLP (bf16 expert MLPs on the fused
+    kernels) equals each token's expert run by itself on the same device, and backward runs."""
+    from smdt_amd.models.transformer import SwitchMLP, TransformerConfig
+    from smdt_amd.parallel import state as ps
+    ps.destroy_model_parallel()
+    cfg = TransformerConfig(num_layers=2, hidden_size=256, num_attention_heads=4, max_position_embeddings=256,
+                            padded_vocab_size=1024, hidden_dropout=0.0, attention_dropout=0.0, seed=3,
+                            num_experts=4, params_dtype=torch.bfloat16)
+    mlp = SwitchMLP(cfg, 1, device="cuda")
+    with torch.no_grad():
+        mlp.router.mul_(20)
+    x = torch.randn(128, 4, 256, device="cuda", generator=torch.Generator(device="cuda").manual_seed(0))
+    x = x.to(torch.bfloat16).requires_grad_(True)
+    out, _ = mlp(x)
+    flat = x.detach().reshape(-1, 256)
+    p, e = mlp.route(flat)
+    assert len(set(e.tolist())) == 4
+    want = torch.empty_like(flat)
+    with torch.no_grad():
+        for i in range(4):
+            idx = (e == i).nonzero().view(-1)
+            y, yb = mlp.experts[i](flat[idx].unsqueeze(1))
+            want[idx] = ((y.squeeze(1) + yb) * p[idx].unsqueeze(-1).to(y.dtype))
+    torch.testing.assert_close(out.reshape(-1, 256).float(), want.float(), atol=2e-2, rtol=2e-2)
+    out.float().square().sum().backward()
+    assert torch.isfinite(x.grad.float()).all() and mlp.router.grad.abs().sum() > 0
