@@ -670,3 +670,16 @@ def test_link_standin_env_parsing(monkeypatch):
         assert (td.eng.gbps, td.eng.blocks) == (64.0, 32)
     finally:
         ps.destroy_model_parallel()
+
+
+def test_switch_mlp_tensor_parallel_matches_single_rank():
+    """``--num-experts`` under TP 2 (no SP): each expert is a tensor-parallel MLP, the router is
+    replicated and routes identically on both ranks; loss and every (sharded) gradient equal the
+    single-rank model's."""
+    over = {"num_experts": 3}
+    ref_loss, ref = W.gpt_reference(cfg_over=over)
+    assert any(".experts.2." in n for n in ref)
+    outs = run_workers(W.gpt_tp_worker, 2, 2, 1, False, over)
+    for loss, grads, meta in outs:
+        _close(loss, ref_loss)
+        _check_tp_grads(ref, grads, meta, 2)
