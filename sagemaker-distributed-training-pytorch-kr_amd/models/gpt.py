@@ -60,7 +60,7 @@ class GPTModel(nn.Module):
     def __init__(self, cfg: TransformerConfig, pre_process: bool = True, post_process: bool = True,
                  parallel_output: bool = True, device=None, layer_range=None):
         super().__init__()
-        with tp.weight_init(cfg.init_method, cfg.perform_initialization):
+        with tp.weight_init(cfg.init_method, cfg.perform_initialization, cfg.use_cpu_initialization):
             self._build(cfg, pre_process, post_process, parallel_output, device, layer_range)
 
     def _build(self, cfg, pre_process, post_process, parallel_output, device, layer_range):

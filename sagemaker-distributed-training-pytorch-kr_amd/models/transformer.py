@@ -62,6 +62,7 @@ class TransformerConfig:
     init_method_std: float = 0.02
     init_method: str = "normal"                  # or "xavier_uniform" (--init-method-xavier-uniform)
     perform_initialization: bool = True         # False: --no-initialization (weights left unset)
+    use_cpu_initialization: bool = False        # --use-cpu-initialization: draw on the host
     params_dtype: torch.dtype = torch.bfloat16
     seed: int = 1234
     # parallelism

@@ -2164,20 +2164,22 @@ def _key_seed(base_seed: int, key: str) -> int:
     return int.from_bytes(h[:8], "little") & ((1 << 62) - 1)
 
 
-_INIT = {"method": "normal", "perform": True}
+_INIT = {"method": "normal", "perform": True, "cpu": False}
 
 
 @contextlib.contextmanager
-def weight_init(method: str = "normal", perform: bool = True):
+def weight_init(method: str = "normal", perform: bool = True, cpu: bool = False):
     """The init rule of the weights built inside (Megatron's ``--init-method-xavier-uniform`` /
     ``--no-initialization``, /root/reference/3_training_megatron-lm/megatron/arguments.py):
     ``"normal"`` draws N(0, std); ``"xavier_uniform"`` draws U(-a, a), a = sqrt(6 / (fan_in +
     fan_out)) of the FULL 2-D weight (so the values do not depend on the TP degree), for every
     weight, the scaled output layers included; ``perform=False`` leaves weights unset (they are
-    about to be loaded from a checkpoint) and skips the full-tensor draw."""
+    about to be loaded from a checkpoint) and skips the full-tensor draw; ``cpu=True``
+    (``--use-cpu-initialization``) draws on the host generator and moves the shard to the device,
+    so a GPU model starts from exactly the CPU model's weights."""
     assert method in ("normal", "xavier_uniform"), method
     old = dict(_INIT)
-    _INIT.update(method=method, perform=bool(perform))
+    _INIT.update(method=method, perform=bool(perform), cpu=bool(cpu))
     try:
         yield
     finally:
@@ -2197,6 +2199,10 @@ def init_full_then_shard(shape, std: float, key: str, base_seed: int, dtype, dev
         if shard_dim is not None and world > 1:
             sh[shard_dim] //= world
         return torch.empty(sh, dtype=dtype, device=dev)
+    if _INIT["cpu"] and dev.type != "cpu":
+        with weight_init(_INIT["method"], True, False):
+            return init_full_then_shard(shape, std, key, base_seed, dtype, None, shard_dim, rank, world,
+                                        chunks).to(dev)
     gen = torch.Generator(device=dev)
     gen.manual_seed(_key_seed(base_seed, key))
     full = torch.empty(shape, dtype=torch.float32, device=dev)

@@ -528,6 +528,7 @@ def core_transformer_config_from_args(args) -> TransformerConfig:
         layernorm_zero_centered_gamma=args.apply_layernorm_1p, num_experts=args.num_experts,
         apply_residual_connection_post_layernorm=args.apply_residual_connection_post_layernorm,
         perform_initialization=args.perform_initialization,
+        use_cpu_initialization=bool(args.use_cpu_initialization),
         sequence_parallel=args.sequence_parallel,
         async_tensor_model_parallel_allreduce=args.async_tensor_model_parallel_allreduce,
         masked_softmax_fusion=args.masked_softmax_fusion, bias_gelu_fusion=args.bias_gelu_fusion,

@@ -39,6 +39,7 @@ from ..models.gpt import allreduce_word_embedding_grads, gpt_flops_per_token
 from ..optim.lr_scheduler import OptimizerParamScheduler
 from ..optim.optimizer import ConstantLossScaler, DynamicLossScaler, MixedPrecisionAdam, MixedPrecisionSGD
 from ..parallel import state as ps
+from ..parallel import tensor_parallel as tp
 from ..parallel.distributed import DistributedDataParallel
 from ..parallel.random import model_parallel_seed
 from . import arguments as A
@@ -139,6 +140,9 @@ def get_model(model_provider_func, args):
 
 
 def setup_model_and_optimizer(model_provider_func, args):
+    # --no-gradient-accumulation-fusion: weight gradients are computed, then added to main_grad
+    # (instead of the MFMA wgrad kernels accumulating straight into the fp32 buffer)
+    tp._FUSED_WGRAD = bool(getattr(args, "gradient_accumulation_fusion", True)) and tp._FUSED_WGRAD
     ddp = get_model(model_provider_func, args)
     scaler = None
     if args.fp16:
@@ -325,6 +329,14 @@ def training_log(loss_dict, total_loss_dict, lr, iteration, loss_scale, report_m
     return report_memory_flag
 
 
+def empty_unused_memory(args, level: int):
+    """Megatron's ``--empty-unused-memory-level``: 1 returns the caching allocator's free blocks to
+    the device after each forward-backward (and each eval iteration), 2 also after the optimizer
+    step. Costs allocator re-warm-up; for runs that share the GPU or sit at the HBM limit."""
+    if int(getattr(args, "empty_unused_memory_level", 0) or 0) >= level and torch.cuda.is_available():
+        torch.cuda.empty_cache()
+
+
 def train_step(forward_step_func, data_iterator, model, optimizer, scheduler, args):
     timers = A.get_timers()
     model.zero_grad_buffer()
@@ -339,6 +351,7 @@ def train_step(forward_step_func, data_iterator, model, optimizer, scheduler, ar
                 grad_scale=scaler.scale if scaler is not None else None)
     model.finish_grad_sync()
     allreduce_word_embedding_grads(unwrap_model(model))
+    empty_unused_memory(args, 1)
     timers("forward-backward").stop()
     timers("optimizer", log_level=1).start(barrier=args.barrier_with_L1_time)
     samples = getattr(args, "lr_step_unit", "iterations") == "samples"
@@ -349,6 +362,7 @@ def train_step(forward_step_func, data_iterator, model, optimizer, scheduler, ar
             and (getattr(args, "iteration", 0) + 1) % args.log_interval == 0:
         optimizer.last_num_zeros = optimizer.num_zeros_in_grad()
     grad_norm = optimizer.step(lr)
+    empty_unused_memory(args, 2)
     timers("optimizer").stop()
     out = {}
     if st.is_last_stage(ignore_virtual=True) and losses:
@@ -371,6 +385,7 @@ def evaluate(forward_step_func, data_iterator, model, args, verbose=False):
                 for k, v in l.items():
                     totals[k] = totals.get(k, 0.0) + float(v)
             args.consumed_valid_samples += args.global_batch_size
+            empty_unused_memory(args, 1)
     model.train()
     n = max(args.eval_iters * args.num_micro_batches, 1)
     return {k: v / n for k, v in totals.items()}

@@ -647,3 +647,41 @@ def test_switch_mlp_routes_each_token_to_one_expert():
                 os.environ[k] = v
     a.padded_vocab_size = 128
     assert A.core_transformer_config_from_args(a).num_experts == 8
+
+
+def test_empty_unused_memory_level_and_grad_accum_fusion_flags(monkeypatch):
+    """``--empty-unused-memory-level`` 1 empties the allocator cache after forward-backward (and
+    eval iterations), 2 also after the optimizer step; ``--no-gradient-accumulation-fusion`` turns
+    the MFMA wgrad-into-main_grad path off; ``--use-cpu-initialization`` reaches the config."""
+    import argparse
+    from smdt_amd.parallel import tensor_parallel as tp
+    from smdt_amd.train import arguments as A
+    from smdt_amd.train import training as T
+    calls = []
+    with monkeypatch.context() as m:
+        m.setattr(torch.cuda, "is_available", lambda: True)
+        m.setattr(torch.cuda, "empty_cache", lambda: calls.append(1))
+        for level, want in ((0, 0), (1, 1), (2, 2)):
+            calls.clear()
+            a = argparse.Namespace(empty_unused_memory_level=level)
+            T.empty_unused_memory(a, 1)
+            T.empty_unused_memory(a, 2)
+            assert len(calls) == want, (level, calls)
+    monkeypatch.setenv("WORLD_SIZE", "1")
+    monkeypatch.setenv("RANK", "0")
+    argv = ["--num-layers", "1", "--hidden-size", "64", "--num-attention-heads", "4", "--seq-length", "32",
+            "--max-position-embeddings", "32", "--micro-batch-size", "2", "--no-gradient-accumulation-fusion",
+            "--use-cpu-initialization", "--empty-unused-memory-level", "2"]
+    a = A.validate_args(A.parse_args(argv=argv), {"tokenizer_type": "GPT2BPETokenizer"})
+    assert a.gradient_accumulation_fusion is False and a.empty_unused_memory_level == 2
+    a.padded_vocab_size = 128
+    assert A.core_transformer_config_from_args(a).use_cpu_initialization is True
+    monkeypatch.setattr(tp, "_FUSED_WGRAD", True)
+    class _Stop(Exception):
+        pass
+
+    def provider(**kw):
+        raise _Stop                 # only the flag handling before the model build is under test
+    with pytest.raises(_Stop):
+        T.setup_model_and_optimizer(provider, a)
+    assert tp._FUSED_WGRAD is False

@@ -145,3 +145,20 @@ def test_switch_mlp_on_kernels_matches_per_expert_composition():
     torch.testing.assert_close(out.reshape(-1, 256).float(), want.float(), atol=2e-2, rtol=2e-2)
     out.float().square().sum().backward()
     assert torch.isfinite(x.grad.float()).all() and mlp.router.grad.abs().sum() > 0
+
+
+def test_use_cpu_initialization_gives_the_cpu_weights_on_the_gpu():
+    """``--use-cpu-initialization``: the weights are drawn by the host generator and moved, so a
+    GPU model starts from exactly the CPU model's weights (the device generator's draws differ)."""
+    from smdt_amd.models.gpt import GPTModel
+    from smdt_amd.models.transformer import TransformerConfig
+    from smdt_amd.parallel import state as ps
+    ps.destroy_model_parallel()
+    kw = dict(num_layers=2, hidden_size=256, num_attention_heads=4, max_position_embeddings=256,
+              padded_vocab_size=1024, seed=3, params_dtype=torch.bfloat16)
+    cpu = GPTModel(TransformerConfig(**kw))
+    gpu = GPTModel(TransformerConfig(**kw, use_cpu_initialization=True), device="cuda")
+    dev = GPTModel(TransformerConfig(**kw), device="cuda")
+    for (n, pc), pg, pd in zip(cpu.named_parameters(), gpu.parameters(), dev.parameters()):
+        assert pg.is_cuda and torch.equal(pg.cpu(), pc), n
+    assert not all(torch.equal(pd.cpu(), pc) for pc, pd in zip(cpu.parameters(), dev.parameters()))
